@@ -1,0 +1,600 @@
+// engine.hip — the C ABI of include/gossip.h over the HIP round kernels.
+//
+// Replaces the reference's per-process NodeState/MessageKeeper (main.go:22-63)
+// and the recursive flood of (*NodeState).Gossip (main.go:65-89) with one
+// engine object that holds every node's rumor words in HBM and advances all of
+// them one synchronous round per gossip_step iteration.  HIP only: there is no
+// CPU fallback; without a gfx950 device gossip_create fails with ENODEV.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/gossip.h"
+#include "kernels.h"
+#include "philox.h"
+
+using namespace gossip;
+
+namespace {
+
+thread_local std::string g_create_error;
+
+constexpr int kTimers = 2;  // 0 = round kernel, 1 = stats kernel
+
+}  // namespace
+
+struct gossip_engine {
+  gossip_config_t cfg{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  std::string err;
+
+  uint64_t N = 0, Nl = 0, lo = 0, hi = 0, nown = 0;
+  uint32_t R = 0, W = 0, k = 0, mode = 0, G = 1, rank = 0;
+  uint32_t t = 0;
+  uint32_t key0 = 0, key1 = 0;
+
+  // Random modes: two gathered images [G][W][Nl]; S_t is this rank's slice of
+  // img[cur], S_{t+1} its slice of img[cur^1], so the all-gather runs in place.
+  // FLOOD: S/Snext/Sprev/skip are shard-sized and the frontier F is the slice of imgF.
+  uint64_t* img[2] = {nullptr, nullptr};
+  int cur = 0;
+  uint64_t* imgF = nullptr;
+  uint64_t* S = nullptr;      // S_t, own shard [W][Nl]
+  uint64_t* Snext = nullptr;  // S_{t+1}
+  uint64_t* Sprev = nullptr;  // FLOOD S_{t-1}
+  uint64_t* skip = nullptr;   // FLOOD sender-skip masks
+  uint64_t* F = nullptr;      // FLOOD frontier (exchange send slice)
+  uint64_t* partial_d = nullptr;
+  uint64_t* partial_h = nullptr;  // pinned
+  uint64_t* scratch_d = nullptr;  // 8 B
+  uint32_t *orow = nullptr, *ocol = nullptr, *irow = nullptr, *icol = nullptr;
+  bool has_topo = false;
+
+  hipEvent_t ev[kTimers][2] = {};
+  double time_ms[kTimers] = {0, 0};
+  uint64_t launches[kTimers] = {0, 0};
+  bool timing = false;
+  bool ev_pending[kTimers] = {false, false};
+
+  int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    err = buf;
+    return code;
+  }
+};
+
+#define HIP_OK(eng, expr)                                                                          \
+  do {                                                                                             \
+    hipError_t e_ = (expr);                                                                        \
+    if (e_ != hipSuccess) return (eng)->fail(GOSSIP_EHIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+namespace {
+
+int set_dev(gossip_engine* e) {
+  HIP_OK(e, hipSetDevice(e->device));
+  return GOSSIP_OK;
+}
+
+void free_all(gossip_engine* e) {
+  uint64_t* bufs[] = {e->img[0], e->img[1], e->imgF, e->partial_d, e->scratch_d};
+  if (e->mode == GOSSIP_MODE_FLOOD) {
+    uint64_t* fb[] = {e->S, e->Snext, e->Sprev, e->skip};
+    for (uint64_t* b : fb)
+      if (b) (void)hipFree(b);
+  }
+  for (uint64_t* b : bufs)
+    if (b) (void)hipFree(b);
+  uint32_t* tb[] = {e->orow, e->ocol, e->irow, e->icol};
+  for (uint32_t* b : tb)
+    if (b) (void)hipFree(b);
+  if (e->partial_h) (void)hipHostFree(e->partial_h);
+  for (auto& p : e->ev)
+    for (auto& x : p)
+      if (x) (void)hipEventDestroy(x);
+  if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
+}
+
+RoundArgs make_args(gossip_engine* e, const uint64_t* gathered) {
+  RoundArgs a{};
+  a.S = e->S;
+  a.G = gathered;
+  a.Snext = e->Snext;
+  a.partial = e->partial_d;
+  a.N = e->N;
+  a.Nl = e->Nl;
+  a.lo = e->lo;
+  a.nown = e->nown;
+  a.W = e->W;
+  a.R = e->R;
+  a.k = e->k;
+  a.t = e->t;
+  a.key0 = e->key0;
+  a.key1 = e->key1;
+  a.flags = e->cfg.flags;
+  a.mode = e->mode;
+  a.Sprev = e->Sprev;
+  a.skip = e->skip;
+  a.orow = e->orow;
+  a.ocol = e->ocol;
+  a.irow = e->irow;
+  a.icol = e->icol;
+  return a;
+}
+
+int timer_begin(gossip_engine* e, int which) {
+  if (!e->timing) return GOSSIP_OK;
+  HIP_OK(e, hipEventRecord(e->ev[which][0], e->stream));
+  return GOSSIP_OK;
+}
+
+int timer_end(gossip_engine* e, int which) {
+  if (!e->timing) return GOSSIP_OK;
+  HIP_OK(e, hipEventRecord(e->ev[which][1], e->stream));
+  e->ev_pending[which] = true;
+  return GOSSIP_OK;
+}
+
+// called after a stream sync: fold finished event pairs into the totals
+int timer_collect(gossip_engine* e) {
+  if (!e->timing) return GOSSIP_OK;
+  for (int w = 0; w < kTimers; ++w) {
+    if (!e->ev_pending[w]) continue;
+    float ms = 0.f;
+    HIP_OK(e, hipEventElapsedTime(&ms, e->ev[w][0], e->ev[w][1]));
+    e->time_ms[w] += ms;
+    e->launches[w] += 1;
+    e->ev_pending[w] = false;
+  }
+  return GOSSIP_OK;
+}
+
+// exchange payload for this round: S_t (random modes) or F_t (FLOOD); the
+// send slice lies inside the gathered image, so the all-gather is in place.
+int prepare_send(gossip_engine* e, uint64_t** send, uint64_t** image) {
+  if (e->mode == GOSSIP_MODE_FLOOD) {
+    HIP_OK(e, launch_frontier(e->S, e->Sprev, e->F, (uint64_t)e->W * e->Nl, e->stream));
+    *send = e->F;
+    *image = e->imgF;
+  } else {
+    *send = e->S;
+    *image = e->img[e->cur];
+  }
+  return GOSSIP_OK;
+}
+
+uint64_t* current_image(gossip_engine* e) { return e->mode == GOSSIP_MODE_FLOOD ? e->imgF : e->img[e->cur]; }
+
+void bind_slices(gossip_engine* e) {
+  const size_t off = (size_t)e->rank * e->W * e->Nl;
+  if (e->mode == GOSSIP_MODE_FLOOD) {
+    e->F = e->imgF + off;
+  } else {
+    e->S = e->img[e->cur] + off;
+    e->Snext = e->img[e->cur ^ 1] + off;
+  }
+}
+
+// compute S_{t+1} of the owned shard from the gathered image + partial stats (device)
+int compute_round(gossip_engine* e, const uint64_t* gathered) {
+  const size_t bytes = (size_t)e->W * e->Nl * 8;
+  HIP_OK(e, hipMemsetAsync(e->partial_d, 0, (4 + e->R) * 8, e->stream));
+  RoundArgs a = make_args(e, gathered);
+  int rc;
+  if (e->mode == GOSSIP_MODE_FLOOD) {
+    if ((rc = timer_begin(e, 0))) return rc;
+    HIP_OK(e, launch_round_flood(a, e->stream));
+    if ((rc = timer_end(e, 0))) return rc;
+  } else {
+    HIP_OK(e, hipMemcpyAsync(e->Snext, e->S, bytes, hipMemcpyDeviceToDevice, e->stream));
+    if ((rc = timer_begin(e, 0))) return rc;
+    HIP_OK(e, launch_round_random(a, e->stream));
+    if ((rc = timer_end(e, 0))) return rc;
+  }
+  if ((rc = timer_begin(e, 1))) return rc;
+  HIP_OK(e, launch_stats(a, e->stream));
+  if ((rc = timer_end(e, 1))) return rc;
+  return GOSSIP_OK;
+}
+
+void rotate(gossip_engine* e) {
+  if (e->mode == GOSSIP_MODE_FLOOD) {
+    uint64_t* tmp = e->Sprev;
+    e->Sprev = e->S;
+    e->S = e->Snext;
+    e->Snext = tmp;
+  } else {
+    e->cur ^= 1;
+    bind_slices(e);
+  }
+}
+
+void fill_stats(gossip_engine* e, const uint64_t* total, gossip_round_stats_t* st) {
+  st->round = e->t;
+  st->full_nodes = total[0];
+  st->alive_nodes = total[1];
+  st->converged = total[0] == total[1] ? 1u : 0u;
+  st->messages = total[2];
+  st->state_hash = (e->cfg.flags & GOSSIP_FLAG_HASH) ? total[3] : 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t gossip_abi_version(void) { return GOSSIP_ABI_VERSION; }
+
+const char* gossip_last_error(const gossip_engine_t* eng) {
+  return eng ? eng->err.c_str() : g_create_error.c_str();
+}
+
+int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
+  g_create_error.clear();
+  if (!cfg || !out) {
+    g_create_error = "null argument";
+    return GOSSIP_EINVAL;
+  }
+  *out = nullptr;
+  if (cfg->n_nodes < 2 || cfg->n_nodes >= (1ull << 32)) {
+    g_create_error = "n_nodes must be in [2, 2^32)";
+    return GOSSIP_EINVAL;
+  }
+  if (cfg->n_rumors == 0 || cfg->n_rumors > 4096) {
+    g_create_error = "n_rumors must be in [1, 4096]";
+    return GOSSIP_EINVAL;
+  }
+  if (cfg->mode > GOSSIP_MODE_PUSHPULL) {
+    g_create_error = "mode not built";
+    return GOSSIP_ENOTSUP;
+  }
+  if (cfg->mode != GOSSIP_MODE_FLOOD && (cfg->fanout == 0 || cfg->fanout > 64)) {
+    g_create_error = "fanout must be in [1, 64]";
+    return GOSSIP_EINVAL;
+  }
+  const uint32_t G = cfg->shard_count ? cfg->shard_count : 1;
+  if (cfg->shard_rank >= G) {
+    g_create_error = "shard_rank >= shard_count";
+    return GOSSIP_EINVAL;
+  }
+  for (uint32_t r : cfg->reserved)
+    if (r) {
+      g_create_error = "reserved fields must be zero";
+      return GOSSIP_EINVAL;
+    }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    g_create_error = "no HIP device (libgossip_hip has no CPU fallback)";
+    return GOSSIP_ENODEV;
+  }
+  int dev = cfg->device;
+  if (dev < 0 && hipGetDevice(&dev) != hipSuccess) dev = 0;
+  if (dev >= ndev) {
+    g_create_error = "device ordinal out of range";
+    return GOSSIP_ENODEV;
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess || std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    g_create_error = std::string("device is not gfx950 (MI355X): ") + prop.gcnArchName;
+    return GOSSIP_ENODEV;
+  }
+
+  gossip_engine* e = new gossip_engine();
+  e->cfg = *cfg;
+  e->device = dev;
+  e->N = cfg->n_nodes;
+  e->R = cfg->n_rumors;
+  e->W = (e->R + 63) / 64;
+  e->k = cfg->fanout;
+  e->mode = cfg->mode;
+  e->G = G;
+  e->rank = cfg->shard_rank;
+  e->Nl = (e->N + G - 1) / G;
+  e->lo = std::min<uint64_t>((uint64_t)e->rank * e->Nl, e->N);
+  e->hi = std::min<uint64_t>(e->lo + e->Nl, e->N);
+  e->nown = e->hi - e->lo;
+  e->key0 = (uint32_t)cfg->seed;
+  e->key1 = (uint32_t)(cfg->seed >> 32);
+  e->timing = (cfg->flags & GOSSIP_FLAG_TIMING) != 0;
+
+  auto bail = [&](int rc) {
+    g_create_error = e->err;
+    free_all(e);
+    delete e;
+    return rc;
+  };
+  if (hipSetDevice(dev) != hipSuccess) {
+    e->err = "hipSetDevice failed";
+    return bail(GOSSIP_EHIP);
+  }
+  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+    e->err = "hipStreamCreate failed";
+    return bail(GOSSIP_EHIP);
+  }
+  e->own_stream = true;
+  const size_t shard = (size_t)e->W * e->Nl * 8;
+  const size_t image = shard * G;
+  auto alloc = [&](uint64_t** p, size_t bytes) {
+    if (hipMalloc((void**)p, bytes) != hipSuccess) {
+      e->err = "hipMalloc of " + std::to_string(bytes) + " bytes failed";
+      return false;
+    }
+    return hipMemset(*p, 0, bytes) == hipSuccess;
+  };
+  if (!alloc(&e->partial_d, (4 + e->R) * 8) || !alloc(&e->scratch_d, 8)) return bail(GOSSIP_ENOMEM);
+  if (e->mode == GOSSIP_MODE_FLOOD) {
+    if (!alloc(&e->S, shard) || !alloc(&e->Snext, shard) || !alloc(&e->Sprev, shard) || !alloc(&e->skip, shard) ||
+        !alloc(&e->imgF, image))
+      return bail(GOSSIP_ENOMEM);
+  } else if (!alloc(&e->img[0], image) || !alloc(&e->img[1], image)) {
+    return bail(GOSSIP_ENOMEM);
+  }
+  bind_slices(e);
+  if (hipHostMalloc((void**)&e->partial_h, (4 + e->R) * 8, hipHostMallocDefault) != hipSuccess) {
+    e->err = "hipHostMalloc failed";
+    return bail(GOSSIP_ENOMEM);
+  }
+  if (e->timing)
+    for (auto& p : e->ev)
+      for (auto& x : p)
+        if (hipEventCreate(&x) != hipSuccess) {
+          e->err = "hipEventCreate failed";
+          return bail(GOSSIP_EHIP);
+        }
+  *out = e;
+  return GOSSIP_OK;
+}
+
+void gossip_destroy(gossip_engine_t* eng) {
+  if (!eng) return;
+  (void)hipSetDevice(eng->device);
+  if (eng->stream) (void)hipStreamSynchronize(eng->stream);
+  free_all(eng);
+  delete eng;
+}
+
+int gossip_set_stream(gossip_engine_t* e, void* hip_stream) {
+  if (!e) return GOSSIP_EINVAL;
+  if (int rc = set_dev(e)) return rc;
+  HIP_OK(e, hipStreamSynchronize(e->stream));
+  if (hip_stream) {
+    if (e->own_stream) HIP_OK(e, hipStreamDestroy(e->stream));
+    e->stream = (hipStream_t)hip_stream;
+    e->own_stream = false;
+  }
+  return GOSSIP_OK;
+}
+
+// "topology" handler (main.go:132-149).  Rows become sorted sets; the in-adjacency
+// is built here once so the flood kernel can run as a race-free pull.
+int gossip_set_topology_csr(gossip_engine_t* e, const uint32_t* row_ptr, const uint32_t* col, uint64_t n,
+                            uint64_t n_edges) {
+  if (!e || !row_ptr || (n_edges && !col)) return GOSSIP_EINVAL;
+  if (n != e->N) return e->fail(GOSSIP_EINVAL, "topology has %llu nodes, engine has %llu",
+                                (unsigned long long)n, (unsigned long long)e->N);
+  if (row_ptr[0] != 0 || row_ptr[n] != n_edges) return e->fail(GOSSIP_EINVAL, "row_ptr does not span col");
+  for (uint64_t u = 0; u < n; ++u)
+    if (row_ptr[u + 1] < row_ptr[u]) return e->fail(GOSSIP_EINVAL, "row_ptr not monotone at %llu", (unsigned long long)u);
+  for (uint64_t i = 0; i < n_edges; ++i)
+    if (col[i] >= n) return e->fail(GOSSIP_EINVAL, "col[%llu] out of range", (unsigned long long)i);
+  std::vector<uint32_t> orow(n + 1, 0), ocol;
+  ocol.reserve(n_edges);
+  for (uint64_t u = 0; u < n; ++u) {
+    const size_t b = ocol.size();
+    ocol.insert(ocol.end(), col + row_ptr[u], col + row_ptr[u + 1]);
+    std::sort(ocol.begin() + b, ocol.end());
+    ocol.erase(std::unique(ocol.begin() + b, ocol.end()), ocol.end());
+    orow[u + 1] = (uint32_t)ocol.size();
+  }
+  std::vector<uint32_t> irow(n + 1, 0), icol(ocol.size());
+  for (uint32_t v : ocol) irow[v + 1]++;
+  for (uint64_t v = 0; v < n; ++v) irow[v + 1] += irow[v];
+  std::vector<uint32_t> fill(irow.begin(), irow.end() - 1);
+  for (uint64_t u = 0; u < n; ++u)
+    for (uint32_t q = orow[u]; q < orow[u + 1]; ++q) icol[fill[ocol[q]]++] = (uint32_t)u;
+  if (int rc = set_dev(e)) return rc;
+  HIP_OK(e, hipStreamSynchronize(e->stream));
+  uint32_t** bufs[] = {&e->orow, &e->ocol, &e->irow, &e->icol};
+  for (uint32_t** b : bufs)
+    if (*b) {
+      HIP_OK(e, hipFree(*b));
+      *b = nullptr;
+    }
+  const size_t eb = std::max<size_t>(ocol.size(), 1) * 4, rb = (n + 1) * 4;
+  if (hipMalloc((void**)&e->orow, rb) != hipSuccess || hipMalloc((void**)&e->ocol, eb) != hipSuccess ||
+      hipMalloc((void**)&e->irow, rb) != hipSuccess || hipMalloc((void**)&e->icol, eb) != hipSuccess)
+    return e->fail(GOSSIP_ENOMEM, "topology allocation failed");
+  HIP_OK(e, hipMemcpy(e->orow, orow.data(), rb, hipMemcpyHostToDevice));
+  HIP_OK(e, hipMemcpy(e->irow, irow.data(), rb, hipMemcpyHostToDevice));
+  if (!ocol.empty()) {
+    HIP_OK(e, hipMemcpy(e->ocol, ocol.data(), ocol.size() * 4, hipMemcpyHostToDevice));
+    HIP_OK(e, hipMemcpy(e->icol, icol.data(), icol.size() * 4, hipMemcpyHostToDevice));
+  }
+  e->has_topo = true;
+  return GOSSIP_OK;
+}
+
+int gossip_reset(gossip_engine_t* e) {
+  if (!e) return GOSSIP_EINVAL;
+  if (int rc = set_dev(e)) return rc;
+  const size_t shard = (size_t)e->W * e->Nl * 8;
+  if (e->mode == GOSSIP_MODE_FLOOD) {
+    HIP_OK(e, hipMemsetAsync(e->S, 0, shard, e->stream));
+    HIP_OK(e, hipMemsetAsync(e->Snext, 0, shard, e->stream));
+    HIP_OK(e, hipMemsetAsync(e->Sprev, 0, shard, e->stream));
+    HIP_OK(e, hipMemsetAsync(e->skip, 0, shard, e->stream));
+    HIP_OK(e, hipMemsetAsync(e->imgF, 0, shard * e->G, e->stream));
+  } else {
+    HIP_OK(e, hipMemsetAsync(e->img[0], 0, shard * e->G, e->stream));
+    HIP_OK(e, hipMemsetAsync(e->img[1], 0, shard * e->G, e->stream));
+  }
+  e->t = 0;
+  return GOSSIP_OK;
+}
+
+int gossip_inject(gossip_engine_t* e, uint64_t node, uint32_t rumor) {
+  if (!e) return GOSSIP_EINVAL;
+  if (node >= e->N || rumor >= e->R) return e->fail(GOSSIP_EINVAL, "inject(%llu, %u) out of range",
+                                                    (unsigned long long)node, rumor);
+  if (int rc = set_dev(e)) return rc;
+  HIP_OK(e, launch_inject(e->S, e->Nl, e->lo, e->hi, e->N, e->R, e->key0, e->key1, (int64_t)node, rumor, e->stream));
+  return GOSSIP_OK;
+}
+
+int gossip_inject_random(gossip_engine_t* e) {
+  if (!e) return GOSSIP_EINVAL;
+  if (int rc = set_dev(e)) return rc;
+  HIP_OK(e, launch_inject(e->S, e->Nl, e->lo, e->hi, e->N, e->R, e->key0, e->key1, -1, 0, e->stream));
+  return GOSSIP_OK;
+}
+
+uint64_t gossip_partial_len(const gossip_engine_t* e) { return e ? 4 + e->R : 0; }
+
+int gossip_exchange_buffers(gossip_engine_t* e, void** send, void** recv, uint64_t* send_bytes) {
+  if (!e) return GOSSIP_EINVAL;
+  if (e->mode == GOSSIP_MODE_FLOOD && !e->has_topo) return e->fail(GOSSIP_ESTATE, "FLOOD needs a topology");
+  if (int rc = set_dev(e)) return rc;
+  uint64_t *s = nullptr, *img = nullptr;
+  if (int rc = prepare_send(e, &s, &img)) return rc;
+  // the caller's collective runs on another stream: publish the slice first
+  HIP_OK(e, hipStreamSynchronize(e->stream));
+  if (send) *send = s;
+  if (recv) *recv = img;
+  if (send_bytes) *send_bytes = (uint64_t)e->W * e->Nl * 8;
+  return GOSSIP_OK;
+}
+
+int gossip_round_compute(gossip_engine_t* e, uint64_t* partial) {
+  if (!e || !partial) return GOSSIP_EINVAL;
+  if (e->mode == GOSSIP_MODE_FLOOD && !e->has_topo) return e->fail(GOSSIP_ESTATE, "FLOOD needs a topology");
+  if (int rc = set_dev(e)) return rc;
+  if (int rc = compute_round(e, current_image(e))) return rc;
+  HIP_OK(e, hipMemcpyAsync(e->partial_h, e->partial_d, (4 + e->R) * 8, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(e, hipStreamSynchronize(e->stream));
+  if (int rc = timer_collect(e)) return rc;
+  std::memcpy(partial, e->partial_h, (4 + e->R) * 8);
+  partial[1] = e->nown;
+  return GOSSIP_OK;
+}
+
+int gossip_round_commit(gossip_engine_t* e, const uint64_t* total, gossip_round_stats_t* st) {
+  if (!e || !total) return GOSSIP_EINVAL;
+  rotate(e);
+  if (st) fill_stats(e, total, st);
+  e->t++;
+  return GOSSIP_OK;
+}
+
+int gossip_step(gossip_engine_t* e, uint32_t max_rounds, gossip_round_stats_t* stats, uint64_t* infected,
+                uint32_t* rounds_done) {
+  if (!e) return GOSSIP_EINVAL;
+  if (rounds_done) *rounds_done = 0;
+  if (e->G != 1) return e->fail(GOSSIP_ESTATE, "gossip_step drives one shard; use the round_* calls for G > 1");
+  if (e->mode == GOSSIP_MODE_FLOOD && !e->has_topo) return e->fail(GOSSIP_ESTATE, "FLOOD needs a topology");
+  if (int rc = set_dev(e)) return rc;
+  std::vector<uint64_t> part(4 + e->R);
+  uint32_t r = 0;
+  while (r < max_rounds) {
+    uint64_t *send = nullptr, *img = nullptr;
+    if (int rc = prepare_send(e, &send, &img)) return rc;
+    if (int rc = gossip_round_compute(e, part.data())) return rc;
+    gossip_round_stats_t st;
+    gossip_round_commit(e, part.data(), &st);
+    if (stats) stats[r] = st;
+    if (infected) std::memcpy(infected + (size_t)r * e->R, part.data() + 4, (size_t)e->R * 8);
+    ++r;
+    if (rounds_done) *rounds_done = r;
+    // converged, or FLOOD quiescence: no message sent means S_{t+1} == S_t forever
+    if (st.converged || (e->mode == GOSSIP_MODE_FLOOD && st.messages == 0)) break;
+  }
+  return GOSSIP_OK;
+}
+
+int gossip_read_bitset(gossip_engine_t* e, uint64_t node, uint64_t* out, uint32_t nwords) {
+  if (!e || !out) return GOSSIP_EINVAL;
+  if (node < e->lo || node >= e->hi) return e->fail(GOSSIP_EINVAL, "node %llu not in this shard", (unsigned long long)node);
+  if (nwords < e->W) return e->fail(GOSSIP_EINVAL, "need %u words", e->W);
+  if (int rc = set_dev(e)) return rc;
+  HIP_OK(e, hipStreamSynchronize(e->stream));
+  for (uint32_t w = 0; w < e->W; ++w)
+    HIP_OK(e, hipMemcpy(out + w, e->S + (size_t)w * e->Nl + (node - e->lo), 8, hipMemcpyDeviceToHost));
+  return GOSSIP_OK;
+}
+
+int gossip_read_shard(gossip_engine_t* e, uint64_t* out, uint64_t n_words) {
+  if (!e || !out) return GOSSIP_EINVAL;
+  if (n_words < (uint64_t)e->W * e->nown) return e->fail(GOSSIP_EINVAL, "output too small");
+  if (int rc = set_dev(e)) return rc;
+  HIP_OK(e, hipStreamSynchronize(e->stream));
+  for (uint32_t w = 0; w < e->W; ++w)
+    HIP_OK(e, hipMemcpy(out + (size_t)w * e->nown, e->S + (size_t)w * e->Nl, e->nown * 8, hipMemcpyDeviceToHost));
+  return GOSSIP_OK;
+}
+
+int gossip_shard_range(const gossip_engine_t* e, uint64_t* lo, uint64_t* hi) {
+  if (!e) return GOSSIP_EINVAL;
+  if (lo) *lo = e->lo;
+  if (hi) *hi = e->hi;
+  return GOSSIP_OK;
+}
+
+int gossip_state_hash(gossip_engine_t* e, uint64_t* out) {
+  if (!e || !out) return GOSSIP_EINVAL;
+  if (int rc = set_dev(e)) return rc;
+  HIP_OK(e, hipMemsetAsync(e->scratch_d, 0, 8, e->stream));
+  HIP_OK(e, launch_hash(e->S, e->Nl, e->nown, e->W, e->N, e->lo, e->scratch_d, e->stream));
+  HIP_OK(e, hipMemcpyAsync(e->partial_h, e->scratch_d, 8, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(e, hipStreamSynchronize(e->stream));
+  *out = e->partial_h[0];
+  return GOSSIP_OK;
+}
+
+uint32_t gossip_round_index(const gossip_engine_t* e) { return e ? e->t : 0; }
+
+uint32_t gossip_peer(uint64_t seed, uint64_t n_nodes, uint32_t node, uint32_t round, uint32_t j) {
+  const u32x4 x = philox4x32_10(u32x4{node, round, 0u, j >> 2}, (uint32_t)seed, (uint32_t)(seed >> 32));
+  return peer_from_word(lane_of(x, j & 3u), n_nodes - 1, node);
+}
+
+int gossip_philox_device(gossip_engine_t* e, const uint32_t* ctr4, const uint32_t* key2, uint32_t* out4, uint32_t n) {
+  if (!e || !ctr4 || !key2 || !out4) return GOSSIP_EINVAL;
+  if (int rc = set_dev(e)) return rc;
+  uint32_t *dc = nullptr, *dout = nullptr;
+  HIP_OK(e, hipMalloc((void**)&dc, (size_t)n * 16 + 16));
+  HIP_OK(e, hipMalloc((void**)&dout, (size_t)n * 16 + 16));
+  HIP_OK(e, hipMemcpy(dc, ctr4, (size_t)n * 16, hipMemcpyHostToDevice));
+  HIP_OK(e, launch_philox(dc, key2[0], key2[1], dout, n, e->stream));
+  HIP_OK(e, hipStreamSynchronize(e->stream));
+  HIP_OK(e, hipMemcpy(out4, dout, (size_t)n * 16, hipMemcpyDeviceToHost));
+  HIP_OK(e, hipFree(dc));
+  HIP_OK(e, hipFree(dout));
+  return GOSSIP_OK;
+}
+
+int gossip_kernel_time(const gossip_engine_t* e, uint32_t which, double* total_ms, uint64_t* launches) {
+  if (!e || which >= (uint32_t)kTimers) return GOSSIP_EINVAL;
+  if (total_ms) *total_ms = e->time_ms[which];
+  if (launches) *launches = e->launches[which];
+  return GOSSIP_OK;
+}
+
+int gossip_reset_timing(gossip_engine_t* e) {
+  if (!e) return GOSSIP_EINVAL;
+  for (int w = 0; w < kTimers; ++w) {
+    e->time_ms[w] = 0;
+    e->launches[w] = 0;
+  }
+  return GOSSIP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,38 @@
+// kernels.h — HIP round kernels for gfx950 (declarations + launch helpers).
+//
+// Device layout: rumor words are structure-of-arrays,
+// word w of local node i at S[w * Nl + i]; the gathered image of all shards is
+// [G][W][Nl], which for W == 1 is simply the global node order.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gossip {
+
+struct RoundArgs {
+  const uint64_t* S;      // own shard S_t            [W][Nl]
+  const uint64_t* G;      // gathered exchange image  [G][W][Nl] (S_t, or F_t for FLOOD)
+  uint64_t* Snext;        // own shard S_{t+1}        [W][Nl]
+  uint64_t* partial;      // stats partial vector (device, zeroed per round)
+  uint64_t N, Nl, lo, nown;
+  uint32_t W, R, k, t;
+  uint32_t key0, key1;
+  uint32_t flags;
+  uint32_t mode;
+  // FLOOD only
+  const uint64_t* Sprev;  // own shard S_{t-1}
+  uint64_t* skip;         // own shard sender-skip masks
+  const uint32_t *orow, *ocol, *irow, *icol;
+};
+
+hipError_t launch_round_random(const RoundArgs& a, hipStream_t st);
+hipError_t launch_round_flood(const RoundArgs& a, hipStream_t st);
+hipError_t launch_stats(const RoundArgs& a, hipStream_t st);
+hipError_t launch_frontier(const uint64_t* S, const uint64_t* Sprev, uint64_t* F, uint64_t n, hipStream_t st);
+hipError_t launch_inject(uint64_t* S, uint64_t Nl, uint64_t lo, uint64_t hi, uint64_t N, uint32_t R, uint32_t key0,
+                         uint32_t key1, int64_t node, uint32_t rumor, hipStream_t st);
+hipError_t launch_hash(const uint64_t* S, uint64_t Nl, uint64_t nown, uint32_t W, uint64_t N, uint64_t lo,
+                       uint64_t* out, hipStream_t st);
+hipError_t launch_philox(const uint32_t* ctr, uint32_t k0, uint32_t k1, uint32_t* out, uint32_t n, hipStream_t st);
+
+}  // namespace gossip

@@ -1,0 +1,86 @@
+"""ctypes description of include/gossip.h, shared by every binding of that ABI.
+
+`bind(lib, prefix)` declares argument/return types for the entry points of a
+library exporting the gossip ABI under `prefix` ("gossip_" for the HIP engine).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+MODE_FLOOD, MODE_PUSH, MODE_PULL, MODE_PUSHPULL, MODE_ANTIENTROPY = range(5)
+MODES = {"flood": MODE_FLOOD, "push": MODE_PUSH, "pull": MODE_PULL,
+         "pushpull": MODE_PUSHPULL, "antientropy": MODE_ANTIENTROPY}
+FLAG_HASH = 1 << 0
+FLAG_TIMING = 1 << 1
+
+STATUS = {0: "OK", -1: "EINVAL", -2: "EHIP", -3: "ENOMEM", -4: "ESTATE", -5: "ENODEV", -6: "ENOTSUP"}
+
+
+class Config(C.Structure):
+    _fields_ = [
+        ("n_nodes", C.c_uint64),
+        ("n_rumors", C.c_uint32),
+        ("mode", C.c_uint32),
+        ("fanout", C.c_uint32),
+        ("flags", C.c_uint32),
+        ("seed", C.c_uint64),
+        ("device", C.c_int32),
+        ("shard_rank", C.c_uint32),
+        ("shard_count", C.c_uint32),
+        ("reserved", C.c_uint32 * 5),
+    ]
+
+
+class RoundStats(C.Structure):
+    _fields_ = [
+        ("round", C.c_uint32),
+        ("converged", C.c_uint32),
+        ("full_nodes", C.c_uint64),
+        ("alive_nodes", C.c_uint64),
+        ("messages", C.c_uint64),
+        ("state_hash", C.c_uint64),
+    ]
+
+    def as_dict(self) -> dict:
+        return {f: int(getattr(self, f)) for f, _ in self._fields_}
+
+
+# (name, restype, argtypes) of every entry point declared in include/gossip.h
+P = C.c_void_p
+U64P = C.POINTER(C.c_uint64)
+U32P = C.POINTER(C.c_uint32)
+SIGNATURES = [
+    ("abi_version", C.c_uint32, []),
+    ("create", C.c_int, [C.POINTER(Config), C.POINTER(P)]),
+    ("destroy", None, [P]),
+    ("last_error", C.c_char_p, [P]),
+    ("set_stream", C.c_int, [P, P]),
+    ("set_topology_csr", C.c_int, [P, U32P, U32P, C.c_uint64, C.c_uint64]),
+    ("reset", C.c_int, [P]),
+    ("inject", C.c_int, [P, C.c_uint64, C.c_uint32]),
+    ("inject_random", C.c_int, [P]),
+    ("step", C.c_int, [P, C.c_uint32, C.POINTER(RoundStats), U64P, U32P]),
+    ("partial_len", C.c_uint64, [P]),
+    ("exchange_buffers", C.c_int, [P, C.POINTER(P), C.POINTER(P), U64P]),
+    ("round_compute", C.c_int, [P, U64P]),
+    ("round_commit", C.c_int, [P, U64P, C.POINTER(RoundStats)]),
+    ("read_bitset", C.c_int, [P, C.c_uint64, U64P, C.c_uint32]),
+    ("read_shard", C.c_int, [P, U64P, C.c_uint64]),
+    ("shard_range", C.c_int, [P, U64P, U64P]),
+    ("state_hash", C.c_int, [P, U64P]),
+    ("round_index", C.c_uint32, [P]),
+    ("peer", C.c_uint32, [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32]),
+    ("philox_device", C.c_int, [P, U32P, U32P, U32P, C.c_uint32]),
+    ("kernel_time", C.c_int, [P, C.c_uint32, C.POINTER(C.c_double), U64P]),
+    ("reset_timing", C.c_int, [P]),
+]
+
+
+def bind(lib: C.CDLL, prefix: str, names=None) -> C.CDLL:
+    for name, res, args in SIGNATURES:
+        if names is not None and name not in names:
+            continue
+        fn = getattr(lib, prefix + name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib

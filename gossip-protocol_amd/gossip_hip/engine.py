@@ -1,0 +1,232 @@
+"""Python mirror of the engine ABI (include/gossip.h).
+
+`Engine` drives libgossip_hip.so (HIP, gfx950).  `AbiEngine` is the same
+wrapper over any library exporting the ABI under another prefix; tests use it
+to drive the CPU oracle with identical calls.  There is no fallback: if the
+HIP library is missing or no gfx950 device exists, `Engine(...)` raises.
+
+Reference interface mirrored (0xSherlokMo/gossip-protocol main.go):
+  Engine.set_topology  ≙ topology handler, main.go:132-149
+  Engine.inject        ≙ broadcast handler from a client, main.go:102-117
+  Engine.step          ≙ (*NodeState).Gossip, main.go:65-89, as synchronous rounds
+  Engine.read_bitset   ≙ read handler, main.go:123-130
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _abi
+from ._abi import Config, RoundStats
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgossip_hip.so")
+_LIB = None
+
+
+class GossipError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{_abi.STATUS.get(code, code)}: {msg}")
+        self.code = code
+
+
+def load_library(path: str = LIB_PATH) -> C.CDLL:
+    """Loads libgossip_hip.so; raises if it has not been built (make -C gossip-protocol_amd)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path} missing: build it with `make -C gossip-protocol_amd` "
+                                    "(the engine has no CPU fallback)")
+        _LIB = _abi.bind(C.CDLL(path), "gossip_")
+    return _LIB
+
+
+@dataclass
+class StepResult:
+    rounds: int
+    stats: list          # list[dict] per round
+    infected: np.ndarray  # [rounds, R] uint64
+
+    @property
+    def converged(self) -> bool:
+        return bool(self.stats and self.stats[-1]["converged"])
+
+
+def make_config(n_nodes: int, n_rumors: int = 1, mode="push", fanout: int = 1, seed: int = 0,
+                flags: int = 0, device: int = -1, shard_rank: int = 0, shard_count: int = 1) -> Config:
+    cfg = Config()
+    cfg.n_nodes = n_nodes
+    cfg.n_rumors = n_rumors
+    cfg.mode = _abi.MODES[mode] if isinstance(mode, str) else int(mode)
+    cfg.fanout = fanout
+    cfg.flags = flags
+    cfg.seed = seed
+    cfg.device = device
+    cfg.shard_rank = shard_rank
+    cfg.shard_count = shard_count
+    return cfg
+
+
+class AbiEngine:
+    """Generic wrapper over a library exporting the gossip ABI under `prefix`."""
+
+    on_device = False
+
+    def __init__(self, lib: C.CDLL, prefix: str, cfg: Config, create_extra=()):
+        self._lib, self._p = lib, prefix
+        self.cfg = cfg
+        h = C.c_void_p()
+        rc = self._fn("create")(C.byref(cfg), *create_extra, C.byref(h))
+        if rc != 0:
+            raise GossipError(rc, self._fn("last_error")(None).decode(errors="replace"))
+        self._h = h
+        self.n_nodes = cfg.n_nodes
+        self.n_rumors = cfg.n_rumors
+        self.n_words = (cfg.n_rumors + 63) // 64
+        lo, hi = C.c_uint64(), C.c_uint64()
+        self._check(self._fn("shard_range")(self._h, C.byref(lo), C.byref(hi)))
+        self.lo, self.hi = lo.value, hi.value
+
+    # -- plumbing ---------------------------------------------------------
+    def _fn(self, name):
+        return getattr(self._lib, self._p + name)
+
+    def _check(self, rc: int):
+        if rc != 0:
+            raise GossipError(rc, self._fn("last_error")(self._h).decode(errors="replace"))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._fn("destroy")(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # -- reference-shaped API ---------------------------------------------
+    def set_topology(self, adjacency) -> None:
+        """adjacency: list (index = node) of neighbour lists, or (row_ptr, col) arrays."""
+        if isinstance(adjacency, tuple):
+            row_ptr, col = (np.ascontiguousarray(a, dtype=np.uint32) for a in adjacency)
+        else:
+            lens = [len(r) for r in adjacency]
+            row_ptr = np.zeros(len(adjacency) + 1, dtype=np.uint32)
+            row_ptr[1:] = np.cumsum(lens)
+            col = np.array([v for r in adjacency for v in r], dtype=np.uint32)
+        colp = col if col.size else np.zeros(1, dtype=np.uint32)
+        self._check(self._fn("set_topology_csr")(
+            self._h, row_ptr.ctypes.data_as(_abi.U32P), colp.ctypes.data_as(_abi.U32P),
+            C.c_uint64(row_ptr.size - 1), C.c_uint64(col.size)))
+
+    def reset(self):
+        self._check(self._fn("reset")(self._h))
+
+    def inject(self, node: int, rumor: int = 0):
+        self._check(self._fn("inject")(self._h, C.c_uint64(node), C.c_uint32(rumor)))
+
+    def inject_random(self):
+        self._check(self._fn("inject_random")(self._h))
+
+    def step(self, max_rounds: int, with_infected: bool = True) -> StepResult:
+        stats = (RoundStats * max(max_rounds, 1))()
+        inf = np.zeros((max(max_rounds, 1), self.n_rumors), dtype=np.uint64) if with_infected else None
+        done = C.c_uint32()
+        self._check(self._fn("step")(
+            self._h, C.c_uint32(max_rounds), stats,
+            inf.ctypes.data_as(_abi.U64P) if inf is not None else None, C.byref(done)))
+        r = done.value
+        return StepResult(r, [stats[i].as_dict() for i in range(r)],
+                          inf[:r] if inf is not None else np.zeros((r, 0), np.uint64))
+
+    def read_bitset(self, node: int) -> np.ndarray:
+        out = np.zeros(self.n_words, dtype=np.uint64)
+        self._check(self._fn("read_bitset")(self._h, C.c_uint64(node), out.ctypes.data_as(_abi.U64P),
+                                            C.c_uint32(self.n_words)))
+        return out
+
+    def read(self, node: int) -> list:
+        """Rumor slots held by `node` (the read handler's view, main.go:123-130)."""
+        words = self.read_bitset(node)
+        return [w * 64 + b for w in range(self.n_words) for b in range(64) if (int(words[w]) >> b) & 1]
+
+    def read_shard(self) -> np.ndarray:
+        n = self.hi - self.lo
+        out = np.zeros(self.n_words * n, dtype=np.uint64)
+        self._check(self._fn("read_shard")(self._h, out.ctypes.data_as(_abi.U64P), C.c_uint64(out.size)))
+        return out.reshape(self.n_words, n)
+
+    def state_hash(self) -> int:
+        h = C.c_uint64()
+        self._check(self._fn("state_hash")(self._h, C.byref(h)))
+        return h.value
+
+    @property
+    def round_index(self) -> int:
+        return int(self._fn("round_index")(self._h))
+
+    # -- sharded rounds --------------------------------------
+    def partial_len(self) -> int:
+        return int(self._fn("partial_len")(self._h))
+
+    def exchange_buffers(self):
+        send, recv, nbytes = C.c_void_p(), C.c_void_p(), C.c_uint64()
+        self._check(self._fn("exchange_buffers")(self._h, C.byref(send), C.byref(recv), C.byref(nbytes)))
+        return send.value, recv.value, nbytes.value
+
+    def round_compute(self) -> np.ndarray:
+        out = np.zeros(self.partial_len(), dtype=np.uint64)
+        self._check(self._fn("round_compute")(self._h, out.ctypes.data_as(_abi.U64P)))
+        return out
+
+    def round_commit(self, total: np.ndarray) -> dict:
+        total = np.ascontiguousarray(total, dtype=np.uint64)
+        st = RoundStats()
+        self._check(self._fn("round_commit")(self._h, total.ctypes.data_as(_abi.U64P), C.byref(st)))
+        return st.as_dict()
+
+
+class Engine(AbiEngine):
+    """The HIP engine (libgossip_hip.so) on one gfx950 device."""
+
+    on_device = True
+
+    def __init__(self, n_nodes: int, n_rumors: int = 1, mode="push", fanout: int = 1, seed: int = 0,
+                 flags: int = 0, device: int = -1, shard_rank: int = 0, shard_count: int = 1):
+        cfg = make_config(n_nodes, n_rumors, mode, fanout, seed, flags, device, shard_rank, shard_count)
+        super().__init__(load_library(), "gossip_", cfg)
+
+    def set_stream(self, hip_stream: int):
+        self._check(self._fn("set_stream")(self._h, C.c_void_p(hip_stream)))
+
+    def kernel_time(self, which: int):
+        ms, n = C.c_double(), C.c_uint64()
+        self._check(self._fn("kernel_time")(self._h, C.c_uint32(which), C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+    def reset_timing(self):
+        self._check(self._fn("reset_timing")(self._h))
+
+    def philox_device(self, ctr: np.ndarray, key) -> np.ndarray:
+        ctr = np.ascontiguousarray(ctr, dtype=np.uint32).reshape(-1, 4)
+        key = np.ascontiguousarray(key, dtype=np.uint32)
+        out = np.zeros_like(ctr)
+        self._check(self._fn("philox_device")(self._h, ctr.ctypes.data_as(_abi.U32P), key.ctypes.data_as(_abi.U32P),
+                                              out.ctypes.data_as(_abi.U32P), C.c_uint32(ctr.shape[0])))
+        return out
+
+
+def peer(seed: int, n_nodes: int, node: int, round_: int, j: int) -> int:
+    """p_j(node, round) as the kernels draw it (host copy of the device function)."""
+    return int(load_library().gossip_peer(seed, n_nodes, node, round_, j))

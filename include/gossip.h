@@ -1,0 +1,165 @@
+/*
+ * gossip.h — C ABI of the MI355X gossip-round engine (libgossip_hip.so).
+ *
+ * This is the drop-in boundary for the dissemination hot path of
+ * 0xSherlokMo/gossip-protocol.  Each entry point names the reference
+ * interface it replaces (paths are relative to the reference repo root):
+ *
+ *   gossip_create / gossip_destroy    NodeState + MessageKeeper construction,
+ *                                     main.go:22-33 (NewMessageKeeper),
+ *                                     main.go:60-63,91-97 (NodeState, NewState, var State)
+ *   gossip_set_topology_csr           "topology" handler, main.go:132-149
+ *                                     (State.Topology = body.Topology, :142)
+ *   gossip_inject / _inject_random    "broadcast" handler from a client,
+ *                                     main.go:102-117 (Broadcasted :113, Append :117)
+ *   gossip_step                       (*NodeState).Gossip, main.go:65-89, run as
+ *                                     synchronous rounds over every node at once
+ *   gossip_read_bitset                "read" handler, main.go:123-130 (Messages.All :126)
+ *
+ * Semantics of a round are pinned in DESIGN.md §2 ("round model").  The
+ * reference has no error returns on this path (Gossip retries until acked,
+ * main.go:79-87); here every call returns 0 (GOSSIP_OK) or a negative
+ * gossip_status and never aborts.  gossip_last_error() has the message.
+ *
+ * Ownership: the engine owns every device buffer.  Host pointers passed in
+ * are read during the call only and never retained (cgo pointer rule).
+ * Threading: one engine is not thread-safe; serialize calls per engine
+ * (the reference serializes MessageKeeper with sync.RWMutex, main.go:25).
+ *
+ * Plain C: fixed-width integers and pointers only, no C++ or torch types.
+ */
+#ifndef GOSSIP_H_
+#define GOSSIP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GOSSIP_ABI_VERSION 1u
+
+/* Dissemination modes. */
+enum gossip_mode {
+  GOSSIP_MODE_FLOOD = 0,      /* reference-faithful: forward once to topology neighbours, main.go:65-89 */
+  GOSSIP_MODE_PUSH = 1,       /* S'[p_j(n)] |= S[n]                                         */
+  GOSSIP_MODE_PULL = 2,       /* S'[n] |= S[p_j(n)]                                         */
+  GOSSIP_MODE_PUSHPULL = 3,   /* both, over the same Philox peers                           */
+  GOSSIP_MODE_ANTIENTROPY = 4 /* version-vector max-merge with churn (reserved, not yet built) */
+};
+
+enum gossip_status {
+  GOSSIP_OK = 0,
+  GOSSIP_EINVAL = -1, /* bad argument                                  */
+  GOSSIP_EHIP = -2,   /* HIP runtime error                             */
+  GOSSIP_ENOMEM = -3, /* device allocation failed                      */
+  GOSSIP_ESTATE = -4, /* call out of order (e.g. FLOOD without topology) */
+  GOSSIP_ENODEV = -5, /* no usable gfx950 device                        */
+  GOSSIP_ENOTSUP = -6 /* mode/feature not built                         */
+};
+
+enum gossip_flags {
+  GOSSIP_FLAG_HASH = 1u << 0,   /* compute the per-round state hash */
+  GOSSIP_FLAG_TIMING = 1u << 1  /* bracket hot kernels with hipEvents (gossip_kernel_time) */
+};
+
+typedef struct gossip_config {
+  uint64_t n_nodes;     /* N: global node count, 2 <= N < 2^32                       */
+  uint32_t n_rumors;    /* R: rumor slots, bit r of word r/64 (W = ceil(R/64) words)  */
+  uint32_t mode;        /* enum gossip_mode                                           */
+  uint32_t fanout;      /* k: Philox peers per node per round (random modes)          */
+  uint32_t flags;       /* enum gossip_flags                                          */
+  uint64_t seed;        /* Philox key = {seed lo32, seed hi32}                        */
+  int32_t device;       /* HIP device ordinal, -1 = current device                    */
+  uint32_t shard_rank;  /* this engine owns nodes [rank*Nl, min(N,(rank+1)*Nl))        */
+  uint32_t shard_count; /* G >= 1, Nl = ceil(N/G)                                     */
+  uint32_t reserved[5]; /* must be zero                                               */
+} gossip_config_t;
+
+/* Stats of one round t: they describe S_{t+1}, the state the round produced. */
+typedef struct gossip_round_stats {
+  uint32_t round;       /* t                                                     */
+  uint32_t converged;   /* full_nodes == alive_nodes                             */
+  uint64_t full_nodes;  /* nodes holding all R rumors                            */
+  uint64_t alive_nodes; /* N (churn not enabled in these modes)                   */
+  uint64_t messages;    /* FLOOD: broadcast RPCs sent in round t */
+  uint64_t state_hash;  /* GOSSIP_FLAG_HASH: Σ mix64 over nonzero words, else 0   */
+} gossip_round_stats_t;
+
+typedef struct gossip_engine gossip_engine_t;
+
+uint32_t gossip_abi_version(void);
+
+/* Creates an engine on cfg->device.  Fails with GOSSIP_ENODEV when no HIP
+ * device is present: there is no CPU fallback in this library. */
+int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out);
+void gossip_destroy(gossip_engine_t* eng);
+
+/* Last error message of eng, or of the last failed gossip_create when eng is NULL. */
+const char* gossip_last_error(const gossip_engine_t* eng);
+
+/* Launch all work on this hipStream_t (NULL = the engine's own stream). */
+int gossip_set_stream(gossip_engine_t* eng, void* hip_stream);
+
+/* FLOOD peer source: directed adjacency Topology[u] = col[row_ptr[u]..row_ptr[u+1]),
+ * global node ids, n == N.  Copied; never retained. */
+int gossip_set_topology_csr(gossip_engine_t* eng, const uint32_t* row_ptr, const uint32_t* col,
+                            uint64_t n, uint64_t n_edges);
+
+/* Clears every rumor bit and sets t = 0. */
+int gossip_reset(gossip_engine_t* eng);
+
+/* Client broadcast of rumor slot `rumor` to `node` (no-op when the node is
+ * outside this shard or already holds it — the dedupe of main.go:113). */
+int gossip_inject(gossip_engine_t* eng, uint64_t node, uint32_t rumor);
+
+/* Injects every rumor r < R at origin(r) = Philox tag-2 draw. */
+int gossip_inject_random(gossip_engine_t* eng);
+
+/* Runs rounds until converged or max_rounds rounds have run (single shard only,
+ * G == 1).  stats: max_rounds entries or NULL; infected: max_rounds * R counters
+ * (row t = per-rumor infected counts after round t) or NULL. */
+int gossip_step(gossip_engine_t* eng, uint32_t max_rounds, gossip_round_stats_t* stats,
+                uint64_t* infected, uint32_t* rounds_done);
+
+/* --- sharded rounds (G > 1, one engine per GPU) -------------
+ * Per round:  gossip_exchange_buffers → all-gather(send → recv) over RCCL
+ *             → gossip_round_compute → all-reduce(SUM) of the partial vector
+ *             → gossip_round_commit.
+ * partial layout (uint64): [0]=full_nodes [1]=alive_nodes [2]=messages
+ *                          [3]=state_hash [4..4+R)=infected per rumor.      */
+uint64_t gossip_partial_len(const gossip_engine_t* eng);
+int gossip_exchange_buffers(gossip_engine_t* eng, void** send, void** recv, uint64_t* send_bytes);
+int gossip_round_compute(gossip_engine_t* eng, uint64_t* partial);
+int gossip_round_commit(gossip_engine_t* eng, const uint64_t* total, gossip_round_stats_t* stats);
+
+/* Readout ("read" handler, main.go:123-130).  Bitset of one node (nwords >= W),
+ * or the whole owned shard in logical order out[w * Nl_owned + i]. */
+int gossip_read_bitset(gossip_engine_t* eng, uint64_t node, uint64_t* out, uint32_t nwords);
+int gossip_read_shard(gossip_engine_t* eng, uint64_t* out, uint64_t n_words);
+/* Owned node range [lo, hi). */
+int gossip_shard_range(const gossip_engine_t* eng, uint64_t* lo, uint64_t* hi);
+
+/* Hash of the current state (same definition as the per-round hash). */
+int gossip_state_hash(gossip_engine_t* eng, uint64_t* out);
+
+/* Current round index t (rounds executed since reset). */
+uint32_t gossip_round_index(const gossip_engine_t* eng);
+
+/* Philox peer draw p_j(n, t) exactly as the kernels compute it (parity probe). */
+uint32_t gossip_peer(uint64_t seed, uint64_t n_nodes, uint32_t node, uint32_t round, uint32_t j);
+
+/* Device-side Philox4x32-10 of n counters (known-answer tests): ctr4/out4 hold
+ * 4*n words, key2 = 2 words. Runs on the engine's device. */
+int gossip_philox_device(gossip_engine_t* eng, const uint32_t* ctr4, const uint32_t* key2,
+                         uint32_t* out4, uint32_t n);
+
+/* GOSSIP_FLAG_TIMING: accumulated device time (ms) and launch count of kernel
+ * `which` (0 = round kernel, 1 = stats/apply kernel), since the last reset_timing. */
+int gossip_kernel_time(const gossip_engine_t* eng, uint32_t which, double* total_ms, uint64_t* launches);
+int gossip_reset_timing(gossip_engine_t* eng);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GOSSIP_H_ */

@@ -1,0 +1,453 @@
+/*
+ * gossip_oracle.c — TEST INFRASTRUCTURE ONLY (see gossip_oracle.h).
+ *
+ * Plain-C restatement of the round model in DESIGN.md §2.  Every function
+ * names the reference code it restates.  Reference = 0xSherlokMo/gossip-protocol
+ * main.go (Go; not buildable here: no Go toolchain).  Parity is pinned by
+ * Philox KATs, FLOOD BFS properties and the independent numpy restatement
+ * (oracle/numpy_ref.py → tests/golden/); see DESIGN.md §4.
+ *
+ * threads == 1: scalar reference loops.  threads > 1: the same loops under
+ * OpenMP with atomic ORs for pushes (used only as bench.py's cpu_baseline).
+ */
+#include "gossip_oracle.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define GOLD64 0x9E3779B97F4A7C15ull
+
+struct oracle_sim {
+  gossip_config_t cfg;
+  int threads;
+  uint64_t N, Nl, lo, hi, nown;
+  uint32_t R, W, k, mode, G, rank;
+  uint64_t* S;     /* own shard S_t, [W][Nl]                  */
+  uint64_t* Snext; /* own shard S_{t+1}, [W][Nl]              */
+  uint64_t* Sprev; /* FLOOD: own shard S_{t-1}                */
+  uint64_t* skip;  /* FLOOD: first-sender-in-Adj mask per bit */
+  uint64_t* send;  /* exchange send buffer [W][Nl]            */
+  uint64_t* recv;  /* gathered [G][W][Nl]                     */
+  uint64_t* fullm; /* W valid-bit masks                        */
+  uint32_t *orow, *ocol, *irow, *icol;
+  uint64_t E;
+  int has_topo;
+  uint32_t t;
+};
+
+/* ---------------- Philox4x32-10 (Random123; rocRAND philox4x32_10.h:270-302) ---- */
+void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+  uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
+  uint32_t k0 = key[0], k1 = key[1];
+  for (int i = 0; i < 10; ++i) {
+    uint64_t m0 = (uint64_t)0xD2511F53u * c0;
+    uint64_t m1 = (uint64_t)0xCD9E8D57u * c2;
+    uint32_t n0 = (uint32_t)(m1 >> 32) ^ c1 ^ k0;
+    uint32_t n1 = (uint32_t)m1;
+    uint32_t n2 = (uint32_t)(m0 >> 32) ^ c3 ^ k1;
+    uint32_t n3 = (uint32_t)m0;
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+/* Peer draw p_j(n,t) — replaces Topology[node.ID()] (main.go:72). */
+static inline uint32_t peer_from_word(uint32_t x, uint64_t N, uint32_t n) {
+  uint32_t p = (uint32_t)(((uint64_t)x * (N - 1)) >> 32);
+  return p + (p >= n);
+}
+
+uint32_t oracle_peer(uint64_t seed, uint64_t N, uint32_t n, uint32_t t, uint32_t j) {
+  uint32_t ctr[4] = {n, t, 0u, j >> 2};
+  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  uint32_t x[4];
+  oracle_philox4x32_10(ctr, key, x);
+  return peer_from_word(x[j & 3], N, n);
+}
+
+/* Rumor origin, Philox stream tag 2. */
+uint32_t oracle_origin(uint64_t seed, uint64_t N, uint32_t r) {
+  uint32_t ctr[4] = {r, 0u, 2u, 0u};
+  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  uint32_t x[4];
+  oracle_philox4x32_10(ctr, key, x);
+  return (uint32_t)(((uint64_t)x[0] * N) >> 32);
+}
+
+uint64_t oracle_mix64(uint64_t z) {
+  z ^= z >> 30; z *= 0xBF58476D1CE4E5B9ull;
+  z ^= z >> 27; z *= 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return z;
+}
+
+static inline int popc64(uint64_t x) { return __builtin_popcountll(x); }
+
+/* ---------------- construction (NewState/NewMessageKeeper, main.go:28-33,91-97) -- */
+int oracle_create(const gossip_config_t* cfg, int threads, oracle_sim_t** out) {
+  if (!cfg || !out) return GOSSIP_EINVAL;
+  *out = NULL;
+  if (cfg->n_nodes < 2 || cfg->n_nodes >= (1ull << 32)) return GOSSIP_EINVAL;
+  if (cfg->n_rumors == 0 || cfg->n_rumors > 4096) return GOSSIP_EINVAL;
+  if (cfg->mode > GOSSIP_MODE_PUSHPULL) return GOSSIP_ENOTSUP;
+  if (cfg->mode != GOSSIP_MODE_FLOOD && (cfg->fanout == 0 || cfg->fanout > 64)) return GOSSIP_EINVAL;
+  uint32_t G = cfg->shard_count ? cfg->shard_count : 1;
+  if (cfg->shard_rank >= G) return GOSSIP_EINVAL;
+  oracle_sim_t* s = (oracle_sim_t*)calloc(1, sizeof(*s));
+  if (!s) return GOSSIP_ENOMEM;
+  s->cfg = *cfg;
+  s->threads = threads < 1 ? 1 : threads;
+  s->N = cfg->n_nodes;
+  s->R = cfg->n_rumors;
+  s->W = (s->R + 63) / 64;
+  s->k = cfg->fanout;
+  s->mode = cfg->mode;
+  s->G = G;
+  s->rank = cfg->shard_rank;
+  s->Nl = (s->N + G - 1) / G;
+  s->lo = (uint64_t)s->rank * s->Nl;
+  s->hi = s->lo + s->Nl < s->N ? s->lo + s->Nl : s->N;
+  if (s->lo > s->hi) s->lo = s->hi;
+  s->nown = s->hi - s->lo;
+  size_t shard = (size_t)s->W * s->Nl;
+  s->S = (uint64_t*)calloc(shard, 8);
+  s->Snext = (uint64_t*)calloc(shard, 8);
+  s->send = (uint64_t*)calloc(shard, 8);
+  s->recv = G > 1 ? (uint64_t*)calloc(shard * G, 8) : NULL;
+  s->fullm = (uint64_t*)calloc(s->W, 8);
+  if (s->mode == GOSSIP_MODE_FLOOD) {
+    s->Sprev = (uint64_t*)calloc(shard, 8);
+    s->skip = (uint64_t*)calloc(shard, 8);
+  }
+  if (!s->S || !s->Snext || !s->send || (G > 1 && !s->recv) || !s->fullm ||
+      (s->mode == GOSSIP_MODE_FLOOD && (!s->Sprev || !s->skip))) {
+    oracle_destroy(s);
+    return GOSSIP_ENOMEM;
+  }
+  for (uint32_t w = 0; w < s->W; ++w) {
+    uint32_t bits = s->R - 64 * w;
+    s->fullm[w] = bits >= 64 ? ~0ull : ((1ull << bits) - 1);
+  }
+  *out = s;
+  return GOSSIP_OK;
+}
+
+void oracle_destroy(oracle_sim_t* s) {
+  if (!s) return;
+  free(s->S); free(s->Snext); free(s->Sprev); free(s->skip); free(s->send); free(s->recv);
+  free(s->fullm); free(s->orow); free(s->ocol); free(s->irow); free(s->icol);
+  free(s);
+}
+
+/* "topology" handler, main.go:132-149: State.Topology = body.Topology (:142).
+ * Rows are treated as sets (sorted, duplicates dropped); the in-adjacency
+ * (transpose) is built for the pull form of the flood. */
+static int cmp_u32(const void* a, const void* b) {
+  uint32_t x = *(const uint32_t*)a, y = *(const uint32_t*)b;
+  return x < y ? -1 : x > y;
+}
+
+int oracle_set_topology_csr(oracle_sim_t* s, const uint32_t* row_ptr, const uint32_t* col,
+                            uint64_t n, uint64_t n_edges) {
+  if (!s || !row_ptr || (n_edges && !col) || n != s->N) return GOSSIP_EINVAL;
+  if (row_ptr[0] != 0 || row_ptr[n] != n_edges) return GOSSIP_EINVAL;
+  for (uint64_t u = 0; u < n; ++u)
+    if (row_ptr[u + 1] < row_ptr[u]) return GOSSIP_EINVAL;
+  for (uint64_t e = 0; e < n_edges; ++e)
+    if (col[e] >= n) return GOSSIP_EINVAL;
+  uint32_t* orow = (uint32_t*)calloc(n + 1, 4);
+  uint32_t* ocol = (uint32_t*)malloc((n_edges ? n_edges : 1) * 4);
+  uint32_t* irow = (uint32_t*)calloc(n + 1, 4);
+  uint32_t* icol = (uint32_t*)malloc((n_edges ? n_edges : 1) * 4);
+  if (!orow || !ocol || !irow || !icol) {
+    free(orow); free(ocol); free(irow); free(icol);
+    return GOSSIP_ENOMEM;
+  }
+  uint64_t E = 0;
+  for (uint64_t u = 0; u < n; ++u) {
+    uint64_t b = row_ptr[u], e = row_ptr[u + 1];
+    uint64_t start = E;
+    memcpy(ocol + E, col + b, (e - b) * 4);
+    qsort(ocol + E, e - b, 4, cmp_u32);
+    uint64_t m = 0;
+    for (uint64_t i = 0; i < e - b; ++i)
+      if (m == 0 || ocol[start + m - 1] != ocol[start + i]) ocol[start + m++] = ocol[start + i];
+    E += m;
+    orow[u + 1] = (uint32_t)E;
+  }
+  for (uint64_t e = 0; e < E; ++e) irow[ocol[e] + 1]++;
+  for (uint64_t v = 0; v < n; ++v) irow[v + 1] += irow[v];
+  uint32_t* fill = (uint32_t*)malloc((n + 1) * 4);
+  if (!fill) {
+    free(orow); free(ocol); free(irow); free(icol);
+    return GOSSIP_ENOMEM;
+  }
+  memcpy(fill, irow, (n + 1) * 4);
+  for (uint64_t u = 0; u < n; ++u) /* ascending u => each in-row sorted */
+    for (uint32_t e = orow[u]; e < orow[u + 1]; ++e) icol[fill[ocol[e]]++] = (uint32_t)u;
+  free(fill);
+  free(s->orow); free(s->ocol); free(s->irow); free(s->icol);
+  s->orow = orow; s->ocol = ocol; s->irow = irow; s->icol = icol;
+  s->E = E;
+  s->has_topo = 1;
+  return GOSSIP_OK;
+}
+
+int oracle_reset(oracle_sim_t* s) {
+  if (!s) return GOSSIP_EINVAL;
+  size_t shard = (size_t)s->W * s->Nl * 8;
+  memset(s->S, 0, shard);
+  memset(s->Snext, 0, shard);
+  if (s->Sprev) memset(s->Sprev, 0, shard);
+  if (s->skip) memset(s->skip, 0, shard);
+  s->t = 0;
+  return GOSSIP_OK;
+}
+
+/* Client "broadcast" (main.go:102-117): dedupe (:113) is the bit test, Append (:117)
+ * the bit set.  Injected bits carry no sender in Adj, so skip stays 0 for them. */
+int oracle_inject(oracle_sim_t* s, uint64_t node, uint32_t rumor) {
+  if (!s || node >= s->N || rumor >= s->R) return GOSSIP_EINVAL;
+  if (node < s->lo || node >= s->hi) return GOSSIP_OK;
+  s->S[(size_t)(rumor >> 6) * s->Nl + (node - s->lo)] |= 1ull << (rumor & 63);
+  return GOSSIP_OK;
+}
+
+int oracle_inject_random(oracle_sim_t* s) {
+  if (!s) return GOSSIP_EINVAL;
+  for (uint32_t r = 0; r < s->R; ++r) oracle_inject(s, oracle_origin(s->cfg.seed, s->N, r), r);
+  return GOSSIP_OK;
+}
+
+uint64_t oracle_partial_len(const oracle_sim_t* s) { return 4 + (s ? s->R : 0); }
+
+/* Exchange payload: S_t for random modes, the frontier F_t = S_t & ~S_{t-1} for FLOOD. */
+int oracle_exchange_buffers(oracle_sim_t* s, void** send, void** recv, uint64_t* send_bytes) {
+  if (!s) return GOSSIP_EINVAL;
+  size_t shard = (size_t)s->W * s->Nl;
+  if (s->mode == GOSSIP_MODE_FLOOD)
+    for (size_t i = 0; i < shard; ++i) s->send[i] = s->S[i] & ~s->Sprev[i];
+  else
+    memcpy(s->send, s->S, shard * 8);
+  if (send) *send = s->send;
+  if (recv) *recv = s->G > 1 ? s->recv : s->send;
+  if (send_bytes) *send_bytes = shard * 8;
+  return GOSSIP_OK;
+}
+
+/* word w of global node n inside the gathered [G][W][Nl] image */
+static inline uint64_t gword(const oracle_sim_t* s, const uint64_t* g, uint64_t n, uint32_t w) {
+  uint64_t r = n / s->Nl, i = n - r * s->Nl;
+  return g[(r * s->W + w) * s->Nl + i];
+}
+
+static int in_sorted(const uint32_t* a, uint32_t len, uint32_t x) {
+  uint32_t lo = 0, hi = len;
+  while (lo < hi) {
+    uint32_t mid = (lo + hi) / 2;
+    if (a[mid] < x) lo = mid + 1; else hi = mid;
+  }
+  return lo < len && a[lo] == x;
+}
+
+/* One round S_t -> S_{t+1} for the owned nodes (Gossip, main.go:65-89, as a
+ * synchronous round).  g = gathered exchange image (S_t or F_t). */
+int oracle_round_compute(oracle_sim_t* s, uint64_t* partial) {
+  if (!s || !partial) return GOSSIP_EINVAL;
+  const uint64_t* g = s->G > 1 ? s->recv : s->send;
+  const uint64_t N = s->N, Nl = s->Nl, lo = s->lo, nown = s->nown;
+  const uint32_t W = s->W, k = s->k, t = s->t;
+  const uint32_t key[2] = {(uint32_t)s->cfg.seed, (uint32_t)(s->cfg.seed >> 32)};
+  const int nt = s->threads;
+  uint64_t* Sn = s->Snext;
+  memcpy(Sn, s->S, (size_t)W * Nl * 8); /* S_{t+1} starts as S_t (OR is monotone) */
+  uint64_t msgs = 0;
+
+  if (s->mode == GOSSIP_MODE_FLOOD) {
+    if (!s->has_topo) return GOSSIP_ESTATE;
+    /* main.go:72-75: every node that learned a value last round (frontier F)
+     * sends it to each topology neighbour except the one it came from. */
+#pragma omp parallel for num_threads(nt) if (nt > 1) schedule(static) reduction(+ : msgs)
+    for (uint64_t i = 0; i < nown; ++i) {
+      uint64_t v = lo + i;
+      uint32_t ob = s->orow[v], oe = s->orow[v + 1], deg = oe - ob;
+      for (uint32_t w = 0; w < W; ++w) {
+        uint64_t Fv = s->S[(size_t)w * Nl + i] & ~s->Sprev[(size_t)w * Nl + i];
+        msgs += (uint64_t)popc64(Fv) * deg - popc64(Fv & s->skip[(size_t)w * Nl + i]);
+        uint64_t acc = s->S[(size_t)w * Nl + i];
+        for (uint32_t e = s->irow[v]; e < s->irow[v + 1]; ++e) acc |= gword(s, g, s->icol[e], w);
+        uint64_t nw = acc & ~s->S[(size_t)w * Nl + i];
+        uint64_t seen = 0, sk = 0;
+        for (uint32_t e = s->irow[v]; e < s->irow[v + 1] && seen != nw; ++e) {
+          uint32_t u = s->icol[e];
+          uint64_t c = gword(s, g, u, w) & nw & ~seen;
+          if (c && in_sorted(s->ocol + ob, deg, u)) sk |= c; /* sender skip, main.go:73 */
+          seen |= c;
+        }
+        Sn[(size_t)w * Nl + i] = acc;
+        s->skip[(size_t)w * Nl + i] = sk;
+      }
+    }
+  } else {
+    const int do_pull = s->mode == GOSSIP_MODE_PULL || s->mode == GOSSIP_MODE_PUSHPULL;
+    const int do_push = s->mode == GOSSIP_MODE_PUSH || s->mode == GOSSIP_MODE_PUSHPULL;
+    if (do_pull) {
+#pragma omp parallel for num_threads(nt) if (nt > 1) schedule(static)
+      for (uint64_t i = 0; i < nown; ++i) {
+        uint32_t n = (uint32_t)(lo + i), x[4] = {0, 0, 0, 0};
+        for (uint32_t j = 0; j < k; ++j) {
+          if ((j & 3) == 0) {
+            uint32_t ctr[4] = {n, t, 0u, j >> 2};
+            oracle_philox4x32_10(ctr, key, x);
+          }
+          uint32_t p = peer_from_word(x[j & 3], N, n);
+          for (uint32_t w = 0; w < W; ++w) Sn[(size_t)w * Nl + i] |= gword(s, g, p, w);
+        }
+      }
+    }
+    if (do_push) {
+      /* every sender s in [0,N): contributions that land in the owned range */
+#pragma omp parallel for num_threads(nt) if (nt > 1) schedule(static)
+      for (uint64_t sn = 0; sn < N; ++sn) {
+        uint32_t n = (uint32_t)sn, x[4] = {0, 0, 0, 0};
+        for (uint32_t j = 0; j < k; ++j) {
+          if ((j & 3) == 0) {
+            uint32_t ctr[4] = {n, t, 0u, j >> 2};
+            oracle_philox4x32_10(ctr, key, x);
+          }
+          uint32_t p = peer_from_word(x[j & 3], N, n);
+          if (p < lo || p >= lo + nown) continue;
+          for (uint32_t w = 0; w < W; ++w) {
+            uint64_t v = gword(s, g, n, w);
+            if (!v) continue;
+            uint64_t* dst = &Sn[(size_t)w * Nl + (p - lo)];
+            if (nt > 1) __atomic_fetch_or(dst, v, __ATOMIC_RELAXED);
+            else *dst |= v;
+          }
+        }
+      }
+    }
+  }
+
+  /* stats partials over S_{t+1} */
+  uint64_t full = 0, hash = 0;
+  uint64_t* inf = partial + 4;
+  memset(inf, 0, (size_t)s->R * 8);
+  const int do_hash = (s->cfg.flags & GOSSIP_FLAG_HASH) != 0;
+#pragma omp parallel num_threads(nt) if (nt > 1)
+  {
+    uint64_t* li = (uint64_t*)calloc(s->R, 8);
+    uint64_t lf = 0, lh = 0;
+#pragma omp for schedule(static)
+    for (uint64_t i = 0; i < nown; ++i) {
+      int isfull = 1;
+      for (uint32_t w = 0; w < W; ++w) {
+        uint64_t x = Sn[(size_t)w * Nl + i];
+        if ((x & s->fullm[w]) != s->fullm[w]) isfull = 0;
+        if (x && do_hash) lh += oracle_mix64(x + ((uint64_t)w * N + lo + i) * GOLD64);
+        while (x) {
+          int b = __builtin_ctzll(x);
+          li[w * 64 + b]++;
+          x &= x - 1;
+        }
+      }
+      lf += isfull;
+    }
+#pragma omp critical
+    {
+      full += lf;
+      hash += lh;
+      for (uint32_t r = 0; r < s->R; ++r) inf[r] += li[r];
+    }
+    free(li);
+  }
+  partial[0] = full;
+  partial[1] = nown;
+  partial[2] = msgs;
+  partial[3] = hash;
+  return GOSSIP_OK;
+}
+
+int oracle_round_commit(oracle_sim_t* s, const uint64_t* total, gossip_round_stats_t* st) {
+  if (!s || !total) return GOSSIP_EINVAL;
+  uint64_t* tmp;
+  if (s->mode == GOSSIP_MODE_FLOOD) { /* S_{t-1} <- S_t <- S_{t+1} */
+    tmp = s->Sprev; s->Sprev = s->S; s->S = s->Snext; s->Snext = tmp;
+  } else {
+    tmp = s->S; s->S = s->Snext; s->Snext = tmp;
+  }
+  if (st) {
+    st->round = s->t;
+    st->full_nodes = total[0];
+    st->alive_nodes = total[1];
+    st->converged = total[0] == total[1];
+    st->messages = total[2];
+    st->state_hash = (s->cfg.flags & GOSSIP_FLAG_HASH) ? total[3] : 0;
+  }
+  s->t++;
+  return GOSSIP_OK;
+}
+
+int oracle_step(oracle_sim_t* s, uint32_t max_rounds, gossip_round_stats_t* stats,
+                uint64_t* infected, uint32_t* rounds_done) {
+  if (!s) return GOSSIP_EINVAL;
+  if (s->G != 1) return GOSSIP_ESTATE;
+  if (s->mode == GOSSIP_MODE_FLOOD && !s->has_topo) return GOSSIP_ESTATE;
+  uint64_t* partial = (uint64_t*)malloc(oracle_partial_len(s) * 8);
+  if (!partial) return GOSSIP_ENOMEM;
+  uint32_t r = 0;
+  int rc = GOSSIP_OK;
+  while (r < max_rounds) {
+    gossip_round_stats_t st;
+    oracle_exchange_buffers(s, NULL, NULL, NULL);
+    if ((rc = oracle_round_compute(s, partial)) != GOSSIP_OK) break;
+    oracle_round_commit(s, partial, &st);
+    if (stats) stats[r] = st;
+    if (infected) memcpy(infected + (size_t)r * s->R, partial + 4, (size_t)s->R * 8);
+    ++r;
+    if (st.converged || (s->mode == GOSSIP_MODE_FLOOD && st.messages == 0)) break;
+  }
+  free(partial);
+  if (rounds_done) *rounds_done = r;
+  return rc;
+}
+
+int oracle_read_bitset(oracle_sim_t* s, uint64_t node, uint64_t* out, uint32_t nwords) {
+  if (!s || !out || node < s->lo || node >= s->hi || nwords < s->W) return GOSSIP_EINVAL;
+  for (uint32_t w = 0; w < s->W; ++w) out[w] = s->S[(size_t)w * s->Nl + (node - s->lo)];
+  return GOSSIP_OK;
+}
+
+int oracle_read_shard(oracle_sim_t* s, uint64_t* out, uint64_t n_words) {
+  if (!s || !out || n_words < (uint64_t)s->W * s->nown) return GOSSIP_EINVAL;
+  for (uint32_t w = 0; w < s->W; ++w)
+    memcpy(out + (size_t)w * s->nown, s->S + (size_t)w * s->Nl, s->nown * 8);
+  return GOSSIP_OK;
+}
+
+int oracle_shard_range(const oracle_sim_t* s, uint64_t* lo, uint64_t* hi) {
+  if (!s) return GOSSIP_EINVAL;
+  if (lo) *lo = s->lo;
+  if (hi) *hi = s->hi;
+  return GOSSIP_OK;
+}
+
+int oracle_state_hash(oracle_sim_t* s, uint64_t* out) {
+  if (!s || !out) return GOSSIP_EINVAL;
+  uint64_t h = 0;
+  for (uint32_t w = 0; w < s->W; ++w)
+    for (uint64_t i = 0; i < s->nown; ++i) {
+      uint64_t x = s->S[(size_t)w * s->Nl + i];
+      if (x) h += oracle_mix64(x + ((uint64_t)w * s->N + s->lo + i) * GOLD64);
+    }
+  *out = h;
+  return GOSSIP_OK;
+}
+
+uint32_t oracle_round_index(const oracle_sim_t* s) { return s ? s->t : 0; }

@@ -1,0 +1,192 @@
+"""numpy_ref.py — TEST INFRASTRUCTURE ONLY.
+
+An independent, vectorised numpy restatement of the round model,
+written separately from the C oracle (oracle/gossip_oracle.c) so the two can be
+cross-checked.  It generates the committed golden fixtures in tests/golden/
+(tests/golden/make_golden.py).  Never imported by the product path.
+
+Reference anchors (0xSherlokMo/gossip-protocol, main.go):
+  flood      — (*NodeState).Gossip main.go:65-89: once-only forward to
+               Topology[self] (:72) minus the sender (:73-75); dedupe :113.
+  inject     — broadcast handler main.go:102-117.
+  readout    — read handler main.go:123-130.
+Random modes, Philox peers, multi-rumor words and the state hash are
+build-defined (SURVEY.md §8 round model), not present in the reference.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+M0 = np.uint64(0xD2511F53)
+M1 = np.uint64(0xCD9E8D57)
+W0 = np.uint32(0x9E3779B9)
+W1 = np.uint32(0xBB67AE85)
+GOLD = 0x9E3779B97F4A7C15
+MASK64 = (1 << 64) - 1
+
+
+def philox4x32_10(c0, c1, c2, c3, k0, k1):
+    """Philox4x32-10 over arrays (Random123 / rocRAND philox4x32_10.h:270-302)."""
+    c0, c1, c2, c3 = (np.asarray(c, dtype=np.uint32) for c in (c0, c1, c2, c3))
+    c0, c1, c2, c3 = np.broadcast_arrays(c0, c1, c2, c3)
+    c0, c1, c2, c3 = (c.copy() for c in (c0, c1, c2, c3))
+    k0 = np.uint32(k0)
+    k1 = np.uint32(k1)
+    with np.errstate(over="ignore"):
+        for _ in range(10):
+            p0 = c0.astype(np.uint64) * M0
+            p1 = c2.astype(np.uint64) * M1
+            n0 = (p1 >> np.uint64(32)).astype(np.uint32) ^ c1 ^ k0
+            n1 = p1.astype(np.uint32)
+            n2 = (p0 >> np.uint64(32)).astype(np.uint32) ^ c3 ^ k1
+            n3 = p0.astype(np.uint32)
+            c0, c1, c2, c3 = n0, n1, n2, n3
+            k0 = np.uint32((int(k0) + int(W0)) & 0xFFFFFFFF)
+            k1 = np.uint32((int(k1) + int(W1)) & 0xFFFFFFFF)
+    return c0, c1, c2, c3
+
+
+def peers(seed: int, n_nodes: int, t: int, k: int, nodes=None) -> np.ndarray:
+    """p_j(n, t) for all n (rows) and j < k (cols); DESIGN.md §2.2."""
+    n = np.arange(n_nodes, dtype=np.uint64) if nodes is None else np.asarray(nodes, dtype=np.uint64)
+    out = np.empty((n.size, k), dtype=np.uint64)
+    k0, k1 = seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF
+    for blk in range((k + 3) // 4):
+        x = philox4x32_10(n.astype(np.uint32), np.uint32(t), np.uint32(0), np.uint32(blk), k0, k1)
+        for q in range(4):
+            j = blk * 4 + q
+            if j >= k:
+                break
+            p = (x[q].astype(np.uint64) * np.uint64(n_nodes - 1)) >> np.uint64(32)
+            p = p + (p >= n).astype(np.uint64)
+            out[:, j] = p
+    return out
+
+
+def origins(seed: int, n_nodes: int, n_rumors: int) -> np.ndarray:
+    """origin(r): Philox stream tag 2."""
+    r = np.arange(n_rumors, dtype=np.uint32)
+    x = philox4x32_10(r, 0, 2, 0, seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
+    return ((x[0].astype(np.uint64) * np.uint64(n_nodes)) >> np.uint64(32)).astype(np.int64)
+
+
+def mix64(z: np.ndarray) -> np.ndarray:
+    z = z.astype(np.uint64)
+    with np.errstate(over="ignore"):
+        z = z ^ (z >> np.uint64(30))
+        z = z * np.uint64(0xBF58476D1CE4E5B9)
+        z = z ^ (z >> np.uint64(27))
+        z = z * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return z
+
+
+def state_hash(S: np.ndarray) -> int:
+    """Σ over nonzero words of mix64(word + (w*N+n)*GOLD) mod 2^64; S is [W, N]."""
+    W, N = S.shape
+    idx = np.arange(W * N, dtype=np.uint64).reshape(W, N)
+    with np.errstate(over="ignore"):
+        v = mix64(S + idx * np.uint64(GOLD))
+    v = np.where(S != 0, v, np.uint64(0))
+    return int(sum(int(x) for x in v.ravel().tolist()) & MASK64) if v.size < 4096 else \
+        int(np.sum(v, dtype=np.uint64))
+
+
+def full_masks(R: int) -> np.ndarray:
+    W = (R + 63) // 64
+    m = []
+    for w in range(W):
+        bits = R - 64 * w
+        m.append((1 << 64) - 1 if bits >= 64 else (1 << bits) - 1)
+    return np.array(m, dtype=np.uint64)
+
+
+def stats_of(S: np.ndarray, R: int):
+    W, N = S.shape
+    fm = full_masks(R)
+    full = int(np.all((S & fm[:, None]) == fm[:, None], axis=0).sum())
+    bits = np.unpackbits(S.view(np.uint8).reshape(W, N, 8), axis=2, bitorder="little")  # [W,N,64]
+    inf = bits.sum(axis=1, dtype=np.int64).reshape(W * 64)[:R]
+    return full, [int(x) for x in inf]
+
+
+class Sim:
+    """Unsharded reference loop.  mode: 'flood' | 'push' | 'pull' | 'pushpull'."""
+
+    def __init__(self, n_nodes, n_rumors, mode, fanout=0, seed=0, topology=None):
+        self.N, self.R, self.mode, self.k, self.seed = n_nodes, n_rumors, mode, fanout, seed
+        self.W = (n_rumors + 63) // 64
+        self.S = np.zeros((self.W, n_nodes), dtype=np.uint64)
+        self.Sprev = np.zeros_like(self.S)
+        self.t = 0
+        self.adj = None
+        if topology is not None:
+            # rows as sets
+            self.adj = [sorted(set(int(v) for v in topology[u])) for u in range(n_nodes)]
+            src, dst = [], []
+            for u, row in enumerate(self.adj):
+                for v in row:
+                    src.append(u)
+                    dst.append(v)
+            self.src = np.array(src, dtype=np.int64)
+            self.dst = np.array(dst, dtype=np.int64)
+            self.deg = np.array([len(r) for r in self.adj], dtype=np.int64)
+            self.skip = np.zeros_like(self.S)
+
+    def inject(self, node, rumor):
+        self.S[rumor // 64, node] |= np.uint64(1 << (rumor % 64))
+
+    def inject_random(self):
+        for r, o in enumerate(origins(self.seed, self.N, self.R)):
+            self.inject(int(o), r)
+
+    def round(self):
+        S = self.S
+        Sn = S.copy()
+        msgs = 0
+        if self.mode == "flood":
+            F = S & ~self.Sprev
+            for w in range(self.W):
+                # messages sent this round: |F[v]|*deg(v) - skipped senders (main.go:72-75)
+                pc = np.array([bin(int(x)).count("1") for x in F[w]], dtype=np.int64)
+                pk = np.array([bin(int(x)).count("1") for x in (F[w] & self.skip[w])], dtype=np.int64)
+                msgs += int((pc * self.deg).sum() - pk.sum())
+                np.bitwise_or.at(Sn[w], self.dst, F[w][self.src])
+                new = Sn[w] & ~S[w]
+                # first (lowest-id) sender per (v, bit); skip if it is in Adj(v)
+                sk = np.zeros(self.N, dtype=np.uint64)
+                seen = np.zeros(self.N, dtype=np.uint64)
+                order = np.lexsort((self.src, self.dst))  # by dst, then src ascending
+                for e in order:
+                    u, v = self.src[e], self.dst[e]
+                    c = F[w][u] & new[v] & ~seen[v]
+                    if c:
+                        if u in self.adj[v]:
+                            sk[v] |= c
+                        seen[v] |= c
+                self.skip[w] = sk
+            self.Sprev = S
+        else:
+            P = peers(self.seed, self.N, self.t, self.k).astype(np.int64)
+            for w in range(self.W):
+                if self.mode in ("pull", "pushpull"):
+                    for j in range(self.k):
+                        Sn[w] |= S[w][P[:, j]]
+                if self.mode in ("push", "pushpull"):
+                    for j in range(self.k):
+                        np.bitwise_or.at(Sn[w], P[:, j], S[w])
+        self.S = Sn
+        full, inf = stats_of(Sn, self.R)
+        st = dict(round=self.t, full=full, converged=int(full == self.N), messages=msgs,
+                  hash=state_hash(Sn), infected=inf)
+        self.t += 1
+        return st
+
+    def run(self, max_rounds):
+        out = []
+        for _ in range(max_rounds):
+            st = self.round()
+            out.append(st)
+            if st["converged"] or (self.mode == "flood" and st["messages"] == 0):
+                break
+        return out

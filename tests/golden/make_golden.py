@@ -1,0 +1,94 @@
+"""Generates tests/golden/golden.json from the independent numpy restatement
+(oracle/numpy_ref.py).  TEST INFRASTRUCTURE: the reference (Go) has no tests,
+fixtures or runnable toolchain here, so these vectors pin the C oracle and the
+HIP engine to a second, separately written restatement of DESIGN.md §2.
+
+Run:  python tests/golden/make_golden.py
+"""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "gossip-protocol_amd"))
+
+import numpy_ref as nr  # noqa: E402
+from gossip_hip.maelstrom import grid_topology, line_topology, total_topology, tree_topology  # noqa: E402
+
+KAT = [  # Random123 kat_vectors for philox4x32_10 (also checked against rocRAND's ten_rounds)
+    {"ctr": [0, 0, 0, 0], "key": [0, 0], "out": [0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8]},
+    {"ctr": [0xffffffff] * 4, "key": [0xffffffff] * 2, "out": [0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd]},
+    {"ctr": [0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344], "key": [0xa4093822, 0x299f31d0],
+     "out": [0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1]},
+]
+
+RANDOM_CASES = [
+    # name, N, R, mode, k, seed, injection ("random" or [(node, rumor), ...])
+    ("push_k3_r1", 4096, 1, "push", 3, 0x5EED0001, [(0, 0)]),
+    ("push_k1_r1", 2048, 1, "push", 1, 0x5EED0001, [(0, 0)]),
+    ("pull_k2_r1", 4096, 1, "pull", 2, 0x5EED0002, [(7, 0)]),
+    ("pushpull_k2_r64", 4096, 64, "pushpull", 2, 0x5EED0003, "random"),
+    ("pushpull_k2_r1_small", 2, 1, "pushpull", 2, 1, [(1, 0)]),
+    ("pushpull_k3_r130", 1500, 130, "pushpull", 3, 0xABCDEF0123456789, "random"),
+    ("push_k5_r70", 777, 70, "push", 5, 42, "random"),
+    ("pull_k6_r64_ragged", 1023, 64, "pull", 6, 0xFFFFFFFF00000001, "random"),
+]
+
+
+def adj(topo, n):
+    return [[int(v[1:]) for v in topo[f"n{i}"]] for i in range(n)]
+
+
+FLOOD_CASES = [
+    ("grid25_n0", 25, 1, adj(grid_topology(25), 25), [(0, 0)]),
+    ("grid25_all_origins", 25, 25, adj(grid_topology(25), 25), [(i, i) for i in range(25)]),
+    ("grid5_n0", 5, 1, adj(grid_topology(5), 5), [(0, 0)]),
+    ("line16_mid", 16, 1, adj(line_topology(16), 16), [(7, 0)]),
+    ("tree3_40", 40, 2, adj(tree_topology(40, 3), 40), [(0, 0), (39, 1)]),
+    ("total8", 8, 1, adj(total_topology(8), 8), [(3, 0)]),
+    # directed, asymmetric, with a duplicate edge and a self loop; disconnected node 5
+    ("directed_ring", 6, 2, [[1, 1], [2], [3, 0], [4], [0, 4], [5]], [(0, 0), (2, 1)]),
+]
+
+
+def run_case(sim, inj, max_rounds=256):
+    if inj == "random":
+        sim.inject_random()
+    else:
+        for n, r in inj:
+            sim.inject(n, r)
+    rounds = sim.run(max_rounds)
+    return [{k: (int(v) if not isinstance(v, list) else v) for k, v in st.items()} for st in rounds]
+
+
+def main():
+    out = {"philox_kat": KAT, "peers": [], "origins": [], "random": [], "flood": []}
+    for seed, N, t in [(0x5EED0001, 1 << 20, 0), (0x5EED0003, 1 << 24, 5), (7, 1000, 3), (0, 2, 0)]:
+        nodes = sorted(set([i for i in range(16) if i < N] + [N - 1]))
+        p = nr.peers(seed, N, t, 6, nodes=nodes)
+        out["peers"].append({"seed": seed, "N": N, "t": t, "nodes": nodes,
+                             "peers": [[int(x) for x in row] for row in p]})
+    for seed, N, R in [(0x5EED0003, 1 << 24, 64), (1, 1000, 10)]:
+        out["origins"].append({"seed": seed, "N": N, "R": R,
+                               "origins": [int(x) for x in nr.origins(seed, N, R)]})
+    for name, N, R, mode, k, seed, inj in RANDOM_CASES:
+        sim = nr.Sim(N, R, mode, k, seed)
+        rounds = run_case(sim, inj)
+        out["random"].append({"name": name, "N": N, "R": R, "mode": mode, "k": k, "seed": seed,
+                              "inject": inj, "rounds": rounds, "final_hash": nr.state_hash(sim.S)})
+    for name, N, R, A, inj in FLOOD_CASES:
+        sim = nr.Sim(N, R, "flood", topology=A)
+        rounds = run_case(sim, inj)
+        reads = {i: [r for r in range(R) if (int(sim.S[r // 64, i]) >> (r % 64)) & 1] for i in range(N)}
+        out["flood"].append({"name": name, "N": N, "R": R, "adj": A, "inject": inj, "rounds": rounds,
+                             "reads": reads})
+    path = os.path.join(HERE, "golden.json")
+    with open(path, "w") as f:
+        json.dump(out, f, separators=(",", ":"))
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,66 @@
+"""CPU: the C-ABI library loads, exports exactly what include/gossip.h
+declares, and refuses to run without a GPU (no CPU fallback)."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+import oracle_py as op
+from conftest import ROOT
+from gossip_hip import engine as eng_mod
+from gossip_hip import _abi
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "gossip.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(gossip_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = C.CDLL(eng_mod.LIB_PATH)
+    names = header_functions()
+    assert len(names) >= 20
+    for n in names:
+        assert hasattr(lib, n), n
+    # and the Python binding covers them all
+    assert {"gossip_" + n for n, _, _ in _abi.SIGNATURES} == set(names)
+
+
+def test_abi_version():
+    assert eng_mod.load_library().gossip_abi_version() == 1
+
+
+def test_struct_layout():
+    assert C.sizeof(_abi.Config) == 64
+    assert C.sizeof(_abi.RoundStats) == 40
+
+
+def test_host_peer_matches_oracle():
+    for seed, N in [(0x5EED0001, 1 << 20), (0x5EED0003, 1 << 24), (5, 3)]:
+        for n in [0, 1, N - 1, N // 2]:
+            for t in range(3):
+                for j in range(7):
+                    assert eng_mod.peer(seed, N, n, t, j) == op.peer(seed, N, n, t, j)
+
+
+def test_no_cpu_fallback():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(eng_mod.GossipError) as ei:
+        eng_mod.Engine(1000, 1, "push", 3, 1)
+    assert ei.value.code in (-5, -2)
+
+
+def test_bad_config_rejected():
+    lib = eng_mod.load_library()
+    cfg = eng_mod.make_config(1, 1, "push", 3, 1)  # N < 2
+    h = C.c_void_p()
+    assert lib.gossip_create(C.byref(cfg), C.byref(h)) == -1
+    assert b"n_nodes" in lib.gossip_last_error(None)
+    cfg = eng_mod.make_config(100, 1, "push", 0, 1)  # fanout 0
+    assert lib.gossip_create(C.byref(cfg), C.byref(h)) == -1
+    cfg = eng_mod.make_config(100, 1, "antientropy", 1, 1)
+    assert lib.gossip_create(C.byref(cfg), C.byref(h)) == -6

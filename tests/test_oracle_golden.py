@@ -1,0 +1,66 @@
+"""CPU: the C oracle (oracle/gossip_oracle.c) against the committed golden
+vectors of the independent numpy restatement and the Philox KATs."""
+import numpy as np
+import pytest
+
+import numpy_ref as nr
+import oracle_py as op
+from conftest import inject_case
+
+
+def test_philox_kat(golden):
+    for v in golden["philox_kat"]:
+        assert op.philox(v["ctr"], v["key"]) == v["out"]
+        x = nr.philox4x32_10(*v["ctr"], *v["key"])
+        assert [int(a) for a in x] == v["out"]
+
+
+def test_peers_and_origins(golden):
+    for c in golden["peers"]:
+        for i, n in enumerate(c["nodes"]):
+            for j in range(6):
+                p = op.peer(c["seed"], c["N"], n, c["t"], j)
+                assert p == c["peers"][i][j]
+                assert p != n and 0 <= p < c["N"]
+    for c in golden["origins"]:
+        assert [op.origin(c["seed"], c["N"], r) for r in range(c["R"])] == c["origins"]
+
+
+@pytest.mark.parametrize("idx", range(8))
+def test_random_modes_golden(golden, idx):
+    c = golden["random"][idx]
+    e = op.OracleEngine(c["N"], c["R"], c["mode"], c["k"], c["seed"], flags=1)
+    inject_case(e, c["inject"])
+    res = e.step(256)
+    assert res.rounds == len(c["rounds"])
+    for got, inf, want in zip(res.stats, res.infected, c["rounds"]):
+        assert got["round"] == want["round"]
+        assert got["full_nodes"] == want["full"]
+        assert got["converged"] == want["converged"]
+        assert got["state_hash"] == want["hash"]
+        assert [int(x) for x in inf] == want["infected"]
+    assert e.state_hash() == c["final_hash"]
+
+
+@pytest.mark.parametrize("idx", range(7))
+def test_flood_golden(golden, idx):
+    c = golden["flood"][idx]
+    e = op.OracleEngine(c["N"], c["R"], "flood", 0, flags=1)
+    e.set_topology(c["adj"])
+    inject_case(e, c["inject"])
+    res = e.step(256)
+    assert [s["messages"] for s in res.stats] == [r["messages"] for r in c["rounds"]]
+    assert [s["full_nodes"] for s in res.stats] == [r["full"] for r in c["rounds"]]
+    assert [s["state_hash"] for s in res.stats] == [r["hash"] for r in c["rounds"]]
+    for node, want in c["reads"].items():
+        assert e.read(int(node)) == want
+
+
+def test_openmp_matches_scalar():
+    for mode, k, R in [("push", 3, 1), ("pushpull", 2, 64), ("pull", 2, 70)]:
+        a = op.OracleEngine(20000, R, mode, k, 99, flags=1)
+        b = op.OracleEngine(20000, R, mode, k, 99, flags=1, threads=4)
+        a.inject_random(); b.inject_random()
+        ra, rb = a.step(100), b.step(100)
+        assert ra.stats == rb.stats
+        assert np.array_equal(ra.infected, rb.infected)
