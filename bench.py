@@ -1,0 +1,175 @@
+#!/usr/bin/env python3
+"""bench.py — gossip node-updates/sec on MI355X (BASELINE.json metric).
+
+A step is one full dissemination run of the hot path: reset, inject the 64
+rumors at their Philox origins, then push-pull rounds (fanout 2) until every
+node holds every rumor.  node-updates = nodes x rounds.  Workload per GPU is
+2^24 nodes (configs[2]; at 8 GPUs this is configs[3], 2^27 nodes sharded
+2^24/GPU, weak scaling).  State is resident in HBM; nothing crosses PCIe in
+the timed region except the per-round 8-byte-per-rumor stats readback.
+
+Single GPU:  python bench.py [--steps K --warmup W]
+N GPUs:      python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "gossip-protocol_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+NODES_PER_GPU = 1 << 24
+RUMORS = 64
+FANOUT = 2
+MODE = "pushpull"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def alg_bytes_per_node_round(mode: str, k: int, words: int) -> int:
+    """PULL 8W(2+k), PUSH 8W(2+2k), PUSH-PULL 8W(2+3k)."""
+    return {"pull": 8 * words * (2 + k), "push": 8 * words * (2 + 2 * k),
+            "pushpull": 8 * words * (2 + 3 * k)}[mode]
+
+
+def load_pmc(workload: str):
+    """HBM traffic per round-kernel launch from the committed PMC passes (profiles/)."""
+    path = os.path.join(ROOT, "profiles", "pmc_round_kernel.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("workload") == workload:
+            return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def cpu_baseline(n_nodes: int, seed: int, budget_s: float = 12.0):
+    """Oracle (C restatement, OpenMP) on the host cores, same workload, bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_py as op
+    threads = min(16, os.cpu_count() or 1)
+    o = op.OracleEngine(n_nodes, RUMORS, MODE, FANOUT, seed, threads=threads)
+    o.inject_random()
+    rounds, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        res = o.step(1, with_infected=False)
+        rounds += res.rounds
+        if res.converged:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": n_nodes * rounds / dt, "unit": "node-updates/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/gossip_oracle.c OpenMP x{threads}, first {rounds} rounds of the same "
+                      f"{n_nodes}-node push-pull k=2 R=64 run ({dt:.1f}s)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--nodes-per-gpu", type=int, default=NODES_PER_GPU)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+
+    from gossip_hip import FLAG_TIMING, Engine
+    from gossip_hip.sharded import sharded_run
+
+    n_total = args.nodes_per_gpu * world
+    seed = 0x5EED0003 if world == 1 else 0x5EED0004
+    eng = Engine(n_total, RUMORS, MODE, FANOUT, seed, flags=FLAG_TIMING, device=local,
+                 shard_rank=rank, shard_count=world)
+    if world > 1:
+        eng.set_stream(torch.cuda.current_stream().cuda_stream)
+
+    def one_step():
+        eng.reset()
+        eng.inject_random()
+        if world == 1:
+            res = eng.step(64, with_infected=False)
+            return res.rounds, res.converged
+        st = sharded_run(eng, 64)
+        return len(st), bool(st[-1]["converged"])
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        one_step()
+    eng.reset_timing()
+    barrier()
+    t0 = time.perf_counter()
+    rounds = []
+    for _ in range(args.steps):
+        r, conv = one_step()
+        assert conv, "run did not converge within 64 rounds"
+        rounds.append(r)
+    barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    round_ms, round_launches = eng.kernel_time(0)
+    stats_ms, stats_launches = eng.kernel_time(1)
+    total_rounds = sum(rounds)
+    value = n_total * total_rounds / dt
+    nown = eng.hi - eng.lo
+    bpn = alg_bytes_per_node_round(MODE, FANOUT, 1)
+    avg_launch_s = round_ms / 1e3 / max(round_launches, 1)
+    achieved = bpn * nown / avg_launch_s / 1e9
+    workload = f"pushpull k=2 R=64, 2^{int(np.log2(args.nodes_per_gpu))} nodes/GPU x {world}"
+
+    if rank == 0:
+        out = {
+            "metric": "gossip node-updates/sec (nodes x rounds)",
+            "value": value,
+            "unit": "node-updates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (64 rumors injected at Philox tag-2 origins)",
+            "config": {"workload": workload, "nodes": n_total, "rumors": RUMORS, "fanout": FANOUT,
+                       "mode": MODE, "seed": hex(seed), "rounds_to_converge": rounds[0],
+                       "parallelism": f"shard{world}" if world > 1 else "single"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": load_pmc(workload),
+                         "kernel": "round_random_kernel<W=1,pull,push>",
+                         "bytes_per_node_round": bpn, "avg_launch_us": avg_launch_s * 1e6,
+                         "stats_kernel_avg_us": stats_ms * 1e3 / max(stats_launches, 1)},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(n_total, seed)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

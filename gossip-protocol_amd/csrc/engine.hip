@@ -197,8 +197,9 @@ int compute_round(gossip_engine* e, const uint64_t* gathered) {
     HIP_OK(e, launch_round_flood(a, e->stream));
     if ((rc = timer_end(e, 0))) return rc;
   } else {
-    HIP_OK(e, hipMemcpyAsync(e->Snext, e->S, bytes, hipMemcpyDeviceToDevice, e->stream));
+    // timer 0 covers the whole S_t -> S_{t+1} transform (seed copy + round kernel)
     if ((rc = timer_begin(e, 0))) return rc;
+    HIP_OK(e, hipMemcpyAsync(e->Snext, e->S, bytes, hipMemcpyDeviceToDevice, e->stream));
     HIP_OK(e, launch_round_random(a, e->stream));
     if ((rc = timer_end(e, 0))) return rc;
   }

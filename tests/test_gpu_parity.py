@@ -1,0 +1,182 @@
+"""GPU parity: the HIP engine (libgossip_hip.so, through the C ABI) against
+the CPU oracle and the committed golden vectors — bit-exact per round."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle_py as op
+from conftest import inject_case
+from gossip_hip import Cluster, Engine, grid_topology
+from gossip_hip.engine import GossipError
+
+pytestmark = pytest.mark.gpu
+THREADS = min(16, os.cpu_count() or 1)
+
+
+def test_device_philox_kat(golden):
+    e = Engine(16, 1, "push", 1, 0)
+    ctr = np.array([v["ctr"] for v in golden["philox_kat"]], dtype=np.uint32)
+    for i, v in enumerate(golden["philox_kat"]):
+        out = e.philox_device(ctr[i:i + 1], v["key"])
+        assert [int(x) for x in out[0]] == v["out"]
+    # a bulk batch against the oracle
+    rng = np.random.default_rng(1)
+    c = rng.integers(0, 2**32, size=(4096, 4), dtype=np.uint64).astype(np.uint32)
+    out = e.philox_device(c, [0x5EED0003, 0])
+    for i in range(0, 4096, 257):
+        assert [int(x) for x in out[i]] == op.philox([int(x) for x in c[i]], [0x5EED0003, 0])
+
+
+@pytest.mark.parametrize("idx", range(8))
+def test_random_golden(golden, idx):
+    c = golden["random"][idx]
+    e = Engine(c["N"], c["R"], c["mode"], c["k"], c["seed"], flags=1)
+    inject_case(e, c["inject"])
+    res = e.step(256)
+    assert res.rounds == len(c["rounds"])
+    for got, inf, want in zip(res.stats, res.infected, c["rounds"]):
+        assert (got["full_nodes"], got["converged"], got["state_hash"]) == (want["full"], want["converged"], want["hash"])
+        assert [int(x) for x in inf] == want["infected"]
+    assert e.state_hash() == c["final_hash"]
+
+
+@pytest.mark.parametrize("idx", range(7))
+def test_flood_golden(golden, idx):
+    c = golden["flood"][idx]
+    e = Engine(c["N"], c["R"], "flood", 0, 0, flags=1)
+    e.set_topology(c["adj"])
+    inject_case(e, c["inject"])
+    res = e.step(256)
+    assert [s["messages"] for s in res.stats] == [r["messages"] for r in c["rounds"]]
+    assert [s["state_hash"] for s in res.stats] == [r["hash"] for r in c["rounds"]]
+    for node, want in c["reads"].items():
+        assert e.read(int(node)) == want
+
+
+def _compare(cfg, inj="random", rounds=256, threads=THREADS):
+    N, R, mode, k, seed = cfg
+    e = Engine(N, R, mode, k, seed, flags=1)
+    o = op.OracleEngine(N, R, mode, k, seed, flags=1, threads=threads)
+    inject_case(e, inj)
+    inject_case(o, inj)
+    re_, ro = e.step(rounds), o.step(rounds)
+    assert re_.stats == ro.stats
+    assert np.array_equal(re_.infected, ro.infected)
+    assert np.array_equal(e.read_shard(), o.read_shard())
+    return re_
+
+
+def test_cfg2_push_1M_k3():
+    """configs[1]: 1M nodes, push fanout 3, one rumor, seed 0x5EED0001."""
+    res = _compare((1 << 20, 1, "push", 3, 0x5EED0001), [(0, 0)])
+    assert res.converged and 12 <= res.rounds <= 20
+
+
+def test_pull_and_multiword():
+    _compare((1 << 18, 1, "pull", 2, 0x5EED0002), [(123, 0)])
+    _compare((100003, 130, "pushpull", 3, 77))
+    _compare((65536, 64, "push", 1, 5))
+
+
+def test_cfg3_pushpull_16M_r64():
+    """configs[2]: 16M nodes, push-pull fanout 2, 64 rumors at Philox origins."""
+    res = _compare((1 << 24, 64, "pushpull", 2, 0x5EED0003))
+    assert res.converged
+    inf = res.infected.astype(np.int64)
+    assert (np.diff(inf, axis=0) >= 0).all() and (inf[-1] == 1 << 24).all()
+
+
+def test_tiny_and_edge_sizes():
+    _compare((2, 1, "pushpull", 2, 1), [(1, 0)])
+    _compare((3, 64, "push", 4, 9))
+    _compare((1000, 1, "pull", 1, 3), [(999, 0)])
+    # no injection: nothing ever spreads, never converges
+    e = Engine(5000, 1, "pushpull", 2, 1)
+    res = e.step(5)
+    assert res.rounds == 5 and not res.converged and res.infected.sum() == 0
+
+
+def test_reset_and_rerun_identical():
+    e = Engine(1 << 16, 64, "pushpull", 2, 21, flags=1)
+    e.inject_random()
+    a = e.step(100)
+    e.reset()
+    e.inject_random()
+    b = e.step(100)
+    assert a.stats == b.stats
+
+
+def test_maelstrom_cluster_grid25():
+    c = Cluster(25, max_values=3)
+    c.topology(grid_topology(25))
+    c.broadcast("n0", 1000)
+    c.broadcast("n24", -7)
+    c.broadcast("n0", 1000)  # dedupe, main.go:113
+    res = c.gossip()
+    # both values are everywhere after 8 rounds; the last learners still forward
+    # once (round 8) and round 9 sends nothing (quiescence stop)
+    assert res.rounds == 10 and res.stats[-1]["messages"] == 0
+    assert [int(x) for x in res.infected[7][:2]] == [25, 25]
+    for i in range(25):
+        assert sorted(c.read(f"n{i}")) == [-7, 1000]
+
+
+def test_errors():
+    e = Engine(100, 2, "flood", 0, 0)
+    with pytest.raises(GossipError) as ei:
+        e.step(3)
+    assert ei.value.code == -4  # ESTATE: FLOOD without topology
+    with pytest.raises(GossipError):
+        e.inject(100, 0)
+    with pytest.raises(GossipError):
+        e.inject(0, 2)
+    with pytest.raises(GossipError):
+        e.set_topology(([0, 1], [0]))  # wrong node count
+
+
+def _dev_tensor(ptr, nbytes):
+    from gossip_hip.sharded import _as_tensor
+    return _as_tensor(ptr, nbytes, True)
+
+
+@pytest.mark.parametrize("mode,k,R,N", [("pushpull", 2, 64, 300001), ("push", 3, 1, 1 << 18),
+                                         ("pull", 2, 130, 50000), ("flood", 0, 2, 400)])
+def test_two_shards_on_one_gpu(mode, k, R, N):
+    """The sharded round protocol with both shards on one device: the all-gather
+    is done with device copies; results equal the unsharded engine bit for bit."""
+    seed = 0x5EED0004
+    shards = [Engine(N, R, mode, k, seed, flags=1, shard_rank=r, shard_count=2) for r in range(2)]
+    ref = Engine(N, R, mode, k, seed, flags=1)
+    engines = shards + [ref]
+    if mode == "flood":
+        adj = [[int(v[1:]) for v in grid_topology(N)[f"n{i}"]] for i in range(N)]
+        for e in engines:
+            e.set_topology(adj)
+            e.inject(0, 0)
+            e.inject(N - 1, 1)
+    else:
+        for e in engines:
+            e.inject_random()
+    want = ref.step(200)
+    got = []
+    for _ in range(200):
+        bufs = [s.exchange_buffers() for s in shards]
+        nbytes = bufs[0][2]
+        for r, s in enumerate(shards):  # all-gather: every shard's slice into every image
+            dst = _dev_tensor(bufs[r][1], nbytes * 2)
+            for q in range(2):
+                dst[q * (nbytes // 8):(q + 1) * (nbytes // 8)].copy_(_dev_tensor(bufs[q][0], nbytes))
+        torch.cuda.synchronize()
+        parts = [s.round_compute() for s in shards]
+        total = parts[0] + parts[1]
+        st = [s.round_commit(total) for s in shards]
+        assert st[0] == st[1]
+        got.append(st[0])
+        if st[0]["converged"] or (mode == "flood" and st[0]["messages"] == 0):
+            break
+    assert got == want.stats
+    full = ref.read_shard()
+    for s in shards:
+        assert np.array_equal(s.read_shard(), full[:, s.lo:s.hi])
