@@ -1,0 +1,47 @@
+// binned.h — propagation-blocked round pipeline (W == 1, one shard).
+//
+// Every random access of a round is moved into LDS: edges are binned by
+// destination tile in a sender-tile pass, pull requests are served from an LDS
+// copy of the peer tile, and pushes plus pull responses are OR-ed into an LDS
+// copy of the receiving tile.  Global traffic is streaming or short runs.
+// DESIGN.md §3.2 has the data layout and the byte accounting.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gossip {
+
+constexpr uint32_t kTileD = 16384;   // destination tile (nodes): one 128 KiB LDS image of u64 words
+constexpr uint32_t kTileDLog = 14;
+constexpr uint32_t kRecPerRegion = 16384;  // records staged per sender tile (LDS, 4 B each)
+constexpr uint32_t kMaxSenders = 8192;     // senders per sender tile (their values staged once, 8 B each)
+constexpr uint32_t kMaxTilesD = 4096;     // N <= 2^26 on this path (and <= 4096 sender regions)
+
+struct BinGeom {
+  uint64_t N;
+  uint32_t k;
+  uint32_t ts, ts_log;   // sender tile size (power of two <= kMaxSenders, ts * k <= kRecPerRegion)
+  uint32_t rp;           // records per sender region = ts * k
+  uint32_t nt_s, nt_d;   // sender tiles, destination tiles
+};
+
+BinGeom make_bin_geom(uint64_t N, uint32_t k);
+bool bin_path_ok(uint64_t N, uint32_t k, uint32_t W, uint32_t G);
+
+struct BinBufs {
+  uint32_t* ids;    // [nt_s][rp]   p_local | n_local << 14
+  uint64_t* vals;   // [nt_s][rp]   S_t[sender]
+  uint64_t* resp;   // [nt_s][rp]   pull response S_t[p] & ~S_t[n]
+  uint16_t* off;    // [nt_s][nt_d + 1] run starts inside each sender region
+  uint16_t* offT;   // [nt_d + 1][nt_s]
+};
+
+size_t bin_bytes(const BinGeom& g);
+void bin_carve(const BinGeom& g, void* base, BinBufs* b);
+
+// One round S -> Snext with stats partials (same layout as stats_kernel's).
+hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, const uint64_t* S, uint64_t* Snext,
+                               uint64_t* partial, uint32_t R, uint32_t t, uint32_t key0, uint32_t key1,
+                               uint32_t mode, uint32_t flags, hipStream_t st, hipEvent_t* marks);
+
+}  // namespace gossip

@@ -1,0 +1,462 @@
+// binned.hip — propagation-blocked push / pull / push-pull round for gfx950.
+//
+// Reference hot path: (*NodeState).Gossip, main.go:65-89 — each informed node
+// sends its value to its peers (:72-81).  A synchronous round over N nodes is
+// N*k random 8-byte reads (pull) and N*k random 8-byte OR-updates (push) —
+// ~55 G/s and ~27 G/s on MI355X (profiles/r01_v0/microbench.jsonl) — so the
+// round is restructured so that every random access lands in LDS:
+//
+//   K1 bin_emit   (one block per sender tile of ts nodes)
+//        reads S_t[sender] (streaming), draws Philox peers, counting-sorts the
+//        edge records {p_local | n_local<<14, S_t[n]} by destination tile in
+//        LDS and writes them out as one contiguous region per sender tile.
+//   K1b transpose the per-region run offsets so a destination tile finds its
+//        runs with two contiguous row reads.
+//   K2 bin_serve  (one block per destination tile, pull modes)
+//        LDS image of S_t[tile]; for every record aimed at the tile writes the
+//        pull response S_t[p] & ~S_t[n] next to the record.
+//   K3 bin_apply  (one block per destination tile)
+//        LDS image acc = S_t[tile]; ORs in the pushes aimed at the tile and the
+//        responses owed to the tile's own senders (ds_or_b64), writes
+//        S_{t+1}[tile] and folds the convergence stats (ballot + 64x64 bit
+//        transpose popcounts).
+//
+// OR is commutative and idempotent and every read is of S_t, so the record
+// order inside a run (decided by LDS atomics) never changes a result bit.
+#include "binned.h"
+#include "philox.h"
+
+namespace gossip {
+
+namespace {
+
+constexpr int kEmitThreads = 1024;
+constexpr int kTileThreads = 1024;
+constexpr int kUnroll = 4;     // records in flight per lane in the response walker
+
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {
+  // blocks are dealt round-robin over the 8 XCDs: give each XCD a contiguous
+  // range of tiles so neighbouring runs share its L2 (speed only)
+  if (n & 7u) return b;
+  return (b & 7u) * (n >> 3) + (b >> 3);
+}
+
+__device__ __forceinline__ uint64_t full_mask1(uint32_t R) { return R >= 64 ? ~0ull : ((1ull << R) - 1ull); }
+
+// which edges of a sender carry information: a push needs S_t[n] != 0, a pull
+// request is pointless once the sender already holds every rumor
+__device__ __forceinline__ bool edge_needed(uint32_t mode, uint64_t v, uint64_t fm) {
+  const bool push = (mode == 1 || mode == 3) && v != 0;
+  const bool pull = (mode == 2 || mode == 3) && v != fm;
+  return push || pull;
+}
+
+__global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const uint64_t* __restrict__ S, BinBufs b,
+                                                                  uint32_t R, uint32_t t, uint32_t key0,
+                                                                  uint32_t key1, uint32_t mode) {
+  __shared__ uint32_t cur[kMaxTilesD];
+  __shared__ uint32_t st_ids[kRecPerRegion];  // p_local | n_local << 14, sorted by destination tile
+  __shared__ uint64_t sval[kMaxSenders];      // S_t of each sender, once (not once per record)
+  __shared__ uint32_t wsum[kEmitThreads / 64];
+  __shared__ uint32_t wpre[kEmitThreads / 64 + 1];
+
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t s = blockIdx.x;
+  const uint64_t base = (uint64_t)s << g.ts_log;
+  const uint32_t nsend = (uint32_t)min<uint64_t>(g.ts, g.N - base);
+  const uint64_t nm1 = g.N - 1, fm = full_mask1(R);
+  constexpr uint32_t kQ = kMaxSenders / kEmitThreads;  // senders per thread upper bound
+
+  for (uint32_t d = tid; d < g.nt_d; d += kEmitThreads) cur[d] = 0;
+  // all sender values of this thread first: independent loads in flight together
+  uint64_t v[kQ];
+#pragma unroll
+  for (uint32_t q = 0; q < kQ; ++q) {
+    const uint32_t i = tid + q * kEmitThreads;
+    // clamp, never branch around a load: a guarded load is waited on alone
+    const uint64_t x = S[base + min(i, nsend - 1)];
+    v[q] = i < nsend ? x : 0ull;
+    if (i < g.ts) sval[i] = v[q];
+  }
+  __syncthreads();
+
+  // pass A: per-destination-tile counts
+#pragma unroll
+  for (uint32_t q = 0; q < kQ; ++q) {
+    const uint32_t i = tid + q * kEmitThreads;
+    if (i >= nsend) break;
+    if (!edge_needed(mode, v[q], fm)) continue;
+    const uint32_t n = (uint32_t)(base + i);
+    u32x4 x{0, 0, 0, 0};
+    for (uint32_t j = 0; j < g.k; ++j) {
+      if ((j & 3u) == 0) x = philox4x32_10(u32x4{n, t, 0u, j >> 2}, key0, key1);
+      atomicAdd(&cur[peer_from_word(lane_of(x, j & 3u), nm1, n) >> kTileDLog], 1u);
+    }
+  }
+  __syncthreads();
+
+  // exclusive scan of cur[0, nt_d)
+  const uint32_t per = (g.nt_d + kEmitThreads - 1) / kEmitThreads;
+  const uint32_t lo = min(tid * per, g.nt_d), hi = min(lo + per, g.nt_d);
+  uint32_t mine = 0;
+  for (uint32_t d = lo; d < hi; ++d) mine += cur[d];
+  uint32_t inc = mine;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if (lane >= (uint32_t)o) inc += y;
+  }
+  if (lane == 63) wsum[wave] = inc;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t a = 0;
+    for (int w = 0; w < kEmitThreads / 64; ++w) {
+      wpre[w] = a;
+      a += wsum[w];
+    }
+    wpre[kEmitThreads / 64] = a;
+  }
+  __syncthreads();
+  uint32_t run = wpre[wave] + inc - mine;
+  uint16_t* off = b.off + (size_t)s * (g.nt_d + 1);
+  for (uint32_t d = lo; d < hi; ++d) {
+    const uint32_t c = cur[d];
+    cur[d] = run;
+    off[d] = (uint16_t)run;
+    run += c;
+  }
+  const uint32_t total = wpre[kEmitThreads / 64];
+  if (tid == 0) off[g.nt_d] = (uint16_t)total;
+  __syncthreads();
+
+  // pass B: the same draws again, each record to its slot
+#pragma unroll
+  for (uint32_t q = 0; q < kQ; ++q) {
+    const uint32_t i = tid + q * kEmitThreads;
+    if (i >= nsend) break;
+    if (!edge_needed(mode, v[q], fm)) continue;
+    const uint32_t n = (uint32_t)(base + i);
+    u32x4 x{0, 0, 0, 0};
+    for (uint32_t j = 0; j < g.k; ++j) {
+      if ((j & 3u) == 0) x = philox4x32_10(u32x4{n, t, 0u, j >> 2}, key0, key1);
+      const uint32_t p = peer_from_word(lane_of(x, j & 3u), nm1, n);
+      const uint32_t pos = atomicAdd(&cur[p >> kTileDLog], 1u);
+      st_ids[pos] = (p & (kTileD - 1)) | (i << kTileDLog);
+    }
+  }
+  __syncthreads();
+
+  uint32_t* gids = b.ids + (size_t)s * g.rp;
+  uint64_t* gvals = b.vals + (size_t)s * g.rp;
+  for (uint32_t e = tid; e < total; e += kEmitThreads) {
+    const uint32_t id = st_ids[e];
+    gids[e] = id;
+    gvals[e] = sval[id >> kTileDLog];
+  }
+}
+
+__global__ __launch_bounds__(256) void transpose_u16_kernel(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
+                                                             uint32_t rows, uint32_t cols) {
+  // in [rows][cols] -> out [cols][rows]
+  __shared__ uint16_t tile[32][33];
+  const uint32_t c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+  for (uint32_t y = threadIdx.y; y < 32; y += 8) {
+    const uint32_t r = r0 + y, c = c0 + threadIdx.x;
+    if (r < rows && c < cols) tile[y][threadIdx.x] = in[(size_t)r * cols + c];
+  }
+  __syncthreads();
+  for (uint32_t y = threadIdx.y; y < 32; y += 8) {
+    const uint32_t c = c0 + y, r = r0 + threadIdx.x;
+    if (r < rows && c < cols) out[(size_t)c * rows + r] = tile[threadIdx.x][y];
+  }
+}
+
+
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// 64x64 bit-matrix transpose across a wave64: on entry lane i holds row i, on
+// exit lane j holds column j (bit i = bit j of lane i's input word).
+__device__ __forceinline__ uint64_t transpose64(uint64_t x, uint32_t lane) {
+  constexpr uint64_t kMask[6] = {0x00000000FFFFFFFFull, 0x0000FFFF0000FFFFull, 0x00FF00FF00FF00FFull,
+                                 0x0F0F0F0F0F0F0F0Full, 0x3333333333333333ull, 0x5555555555555555ull};
+#pragma unroll
+  for (int st = 0; st < 6; ++st) {
+    const uint32_t d = 32u >> st;
+    const uint64_t y = __shfl_xor(x, d, 64);
+    const uint64_t m = kMask[st];
+    x = (lane & d) ? ((x & ~m) | ((y & ~m) >> d)) : ((x & m) | ((y & m) << d));
+  }
+  return x;
+}
+
+// Writes the finished tile (LDS) to S_{t+1} and folds the round stats
+// (definitions as in stats_kernel): fully-informed count by ballot, per-rumor
+// counts as column popcounts of each wave's 64x64 bit matrix, optional hash.
+__device__ __forceinline__ void tile_epilogue(const unsigned long long* acc, uint64_t node0, uint64_t N,
+                                              uint64_t* __restrict__ Snext, uint64_t* __restrict__ partial,
+                                              uint32_t R, uint32_t flags, uint32_t* cnt, uint64_t* red_hash,
+                                              uint32_t* red_full) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint64_t fm = full_mask1(R);
+  const bool do_hash = (flags & 1u) != 0;
+  uint64_t hash = 0;
+  uint32_t full = 0, c_lane = 0;
+  for (uint32_t q = 0; q < kTileD / kTileThreads; ++q) {
+    const uint32_t i = q * kTileThreads + tid;
+    const uint64_t n = node0 + i;
+    const bool valid = n < N;
+    const uint64_t x = valid ? (uint64_t)acc[i] : 0ull;
+    if (valid) Snext[n] = x;
+    if (do_hash && x) hash += mix64(x + n * kGold64);
+    full += (uint32_t)__popcll(__ballot(valid && x == fm));
+    const uint64_t nz = __ballot(x != 0);
+    if (nz == 0) continue;
+    const uint64_t fl = __ballot(x == fm);
+    if (fl == nz) {
+      c_lane += (uint32_t)__popcll(nz);
+    } else {
+      c_lane += (uint32_t)__popcll(transpose64(x, lane));
+    }
+  }
+  if (lane < R && c_lane) atomicAdd(&cnt[lane], c_lane);  // bits >= R are never set
+  hash = wave_sum64(hash);
+  if (lane == 0) {
+    red_hash[wave] = hash;
+    red_full[wave] = full;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint64_t h = 0, f = 0;
+    for (int w = 0; w < kTileThreads / 64; ++w) {
+      h += red_hash[w];
+      f += red_full[w];
+    }
+    if (f) atomicAdd((unsigned long long*)&partial[0], (unsigned long long)f);
+    if (h) atomicAdd((unsigned long long*)&partial[3], (unsigned long long)h);
+  }
+  if (tid < R && cnt[tid]) atomicAdd((unsigned long long*)&partial[4 + tid], (unsigned long long)cnt[tid]);
+}
+
+// Visits every record of the runs (s, T) for s in [0, nt_s): a wave takes 64
+// consecutive runs at a time (lane = run), scans their lengths, and its lanes
+// then walk the concatenated records in order, kUnroll records per lane with
+// all loads issued before any is consumed.  fn(rec) receives the global record
+// index s * rp + pos, or -1 past the end.
+template <int U, typename F>
+__device__ __forceinline__ void for_each_run_record(const BinGeom& g, const uint16_t* rowb, const uint16_t* rowe,
+                                                    F&& fn) {
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+  for (uint32_t s0 = wave * 64; s0 < g.nt_s; s0 += nwaves * 64) {
+    const uint32_t s = s0 + lane;
+    const uint32_t sc = min(s, g.nt_s - 1);
+    const uint32_t be0 = rowb[sc], en0 = rowe[sc];
+    const uint32_t be = s < g.nt_s ? be0 : 0u, en = s < g.nt_s ? en0 : 0u;
+    const uint32_t len = en - be;
+    uint32_t inc = len;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o, 64);
+      if (lane >= (uint32_t)o) inc += y;
+    }
+    const uint32_t exc = inc - len;
+    const uint32_t total = __shfl(inc, 63, 64);
+    const int64_t basep = (int64_t)s * g.rp + be - exc;  // record = basep(owner) + f
+    for (uint32_t f0 = 0; f0 < total; f0 += 64 * U) {
+      int64_t rec[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t f = f0 + u * 64 + lane;
+        uint32_t r = 0;  // owner run: largest r with exc[r] <= f
+#pragma unroll
+        for (uint32_t step = 32; step > 0; step >>= 1) {
+          const uint32_t c = r + step;
+          if (__shfl(exc, c, 64) <= f) r = c;
+        }
+        // every lane takes part in the shuffle: a bpermute from a lane that is
+        // masked off returns garbage, so no conditional around it
+        const int64_t bp = __shfl(basep, r, 64);
+        rec[u] = f < total ? bp + f : -1;
+      }
+      fn(rec);
+    }
+  }
+}
+
+// K2 — one block per destination tile T (pull modes): LDS image of S_t[T];
+// every record aimed at T gets its pull response S_t[p] & ~S_t[n] written
+// next to it.
+__global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, const uint64_t* __restrict__ S, BinBufs b) {
+  __shared__ unsigned long long img[kTileD];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t T = xcd_remap(blockIdx.x, g.nt_d);
+  const uint64_t node0 = (uint64_t)T << kTileDLog;
+  for (uint32_t q0 = 0; q0 < kTileD / kTileThreads; q0 += 4) {
+    uint64_t x[4];
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) x[q] = S[min<uint64_t>(node0 + (q0 + q) * kTileThreads + tid, g.N - 1)];
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q)
+      img[(q0 + q) * kTileThreads + tid] = node0 + (q0 + q) * kTileThreads + tid < g.N ? x[q] : 0ull;
+  }
+  __syncthreads();
+  const uint32_t* __restrict__ gids = b.ids;
+  const uint64_t* __restrict__ gvals = b.vals;
+  uint64_t* __restrict__ gresp = b.resp;
+  const uint16_t* rowb = b.offT + (size_t)T * g.nt_s;
+  for_each_run_record<kUnroll>(g, rowb, rowb + g.nt_s, [&](const int64_t* rec) {
+    uint32_t id[kUnroll];
+    uint64_t v[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int64_t r = rec[u] >= 0 ? rec[u] : 0;
+      id[u] = gids[r];
+      v[u] = gvals[r];
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u)
+      if (rec[u] >= 0) gresp[rec[u]] = img[id[u] & (kTileD - 1)] & ~v[u];
+  });
+}
+
+// K3 — one block per tile X: acc = S_t[X]; OR in the pushes aimed at X (its
+// runs) and the pull responses owed to X's own senders (their regions, read
+// sequentially); write S_{t+1}[X] and fold the stats.
+__global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, const uint64_t* __restrict__ S,
+                                                                  uint64_t* __restrict__ Snext, BinBufs b,
+                                                                  uint64_t* __restrict__ partial, uint32_t R,
+                                                                  uint32_t mode, uint32_t flags) {
+  __shared__ unsigned long long acc[kTileD];
+  __shared__ uint32_t cnt[64];
+  __shared__ uint64_t red_hash[kTileThreads / 64];
+  __shared__ uint32_t red_full[kTileThreads / 64];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t X = xcd_remap(blockIdx.x, g.nt_d);
+  const uint64_t node0 = (uint64_t)X << kTileDLog;
+  for (uint32_t q0 = 0; q0 < kTileD / kTileThreads; q0 += 4) {
+    uint64_t x[4];
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) x[q] = S[min<uint64_t>(node0 + (q0 + q) * kTileThreads + tid, g.N - 1)];
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q)
+      acc[(q0 + q) * kTileThreads + tid] = node0 + (q0 + q) * kTileThreads + tid < g.N ? x[q] : 0ull;
+  }
+  if (tid < 64) cnt[tid] = 0;
+  __syncthreads();
+  const uint32_t* __restrict__ gids = b.ids;
+  const uint64_t* __restrict__ gvals = b.vals;
+  const uint64_t* __restrict__ gresp = b.resp;
+  if (mode == 1 || mode == 3) {  // pushes aimed at this tile
+    const uint16_t* rowb = b.offT + (size_t)X * g.nt_s;
+    for_each_run_record<kUnroll>(g, rowb, rowb + g.nt_s, [&](const int64_t* rec) {
+      uint32_t id[kUnroll];
+      uint64_t v[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const int64_t r = rec[u] >= 0 ? rec[u] : 0;
+        const uint64_t x = gvals[r];
+        id[u] = gids[r];
+        v[u] = rec[u] >= 0 ? x : 0ull;
+      }
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const uint32_t p = id[u] & (kTileD - 1);
+        if (v[u] && (v[u] & ~acc[p])) atomicOr(&acc[p], (unsigned long long)v[u]);
+      }
+    });
+  }
+  if (mode == 2 || mode == 3) {  // responses owed to this tile's own senders
+    const uint32_t per = kTileD >> g.ts_log;
+    const uint32_t s0 = X * per, s1 = min(s0 + per, g.nt_s);
+    for (uint32_t s = s0; s < s1; ++s) {
+      const uint32_t total = b.off[(size_t)s * (g.nt_d + 1) + g.nt_d];
+      const size_t reg = (size_t)s * g.rp;
+      const uint32_t nb = (s - s0) << g.ts_log;
+      for (uint32_t p0 = 0; p0 < total; p0 += kTileThreads * kUnroll) {
+        uint64_t r[kUnroll];
+        uint32_t id[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+          const uint32_t pos = p0 + u * kTileThreads + tid;
+          const size_t at = reg + (pos < total ? pos : 0u);
+          const uint64_t x = gresp[at];
+          id[u] = gids[at];
+          r[u] = pos < total ? x : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+          if (!r[u]) continue;
+          const uint32_t node = nb + (id[u] >> kTileDLog);
+          if (r[u] & ~acc[node]) atomicOr(&acc[node], (unsigned long long)r[u]);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  tile_epilogue(acc, node0, g.N, Snext, partial, R, flags, cnt, red_hash, red_full);
+}
+
+}  // namespace
+
+BinGeom make_bin_geom(uint64_t N, uint32_t k) {
+  BinGeom g{};
+  g.N = N;
+  g.k = k;
+  uint32_t ts = kMaxSenders, lg = 13;
+  while (ts * k > kRecPerRegion) {
+    ts >>= 1;
+    --lg;
+  }
+  g.ts = ts;
+  g.ts_log = lg;
+  g.rp = ts * k;
+  g.nt_s = (uint32_t)((N + ts - 1) / ts);
+  g.nt_d = (uint32_t)((N + kTileD - 1) / kTileD);
+  return g;
+}
+
+bool bin_path_ok(uint64_t N, uint32_t k, uint32_t W, uint32_t G) {
+  if (W != 1 || G != 1 || k == 0 || k > 64 || N < 2) return false;
+  const BinGeom g = make_bin_geom(N, k);
+  return g.nt_d <= kMaxTilesD;
+}
+
+size_t bin_bytes(const BinGeom& g) {
+  const size_t recs = (size_t)g.nt_s * g.rp;
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  return al(recs * 4) + al(recs * 8) + al(recs * 8) + 2 * al((size_t)g.nt_s * (g.nt_d + 1) * 2);
+}
+
+void bin_carve(const BinGeom& g, void* base, BinBufs* b) {
+  const size_t recs = (size_t)g.nt_s * g.rp;
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  char* p = (char*)base;
+  b->ids = (uint32_t*)p;
+  p += al(recs * 4);
+  b->vals = (uint64_t*)p;
+  p += al(recs * 8);
+  b->resp = (uint64_t*)p;
+  p += al(recs * 8);
+  b->off = (uint16_t*)p;
+  p += al((size_t)g.nt_s * (g.nt_d + 1) * 2);
+  b->offT = (uint16_t*)p;
+}
+
+hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, const uint64_t* S, uint64_t* Snext,
+                               uint64_t* partial, uint32_t R, uint32_t t, uint32_t key0, uint32_t key1,
+                               uint32_t mode, uint32_t flags, hipStream_t st, hipEvent_t* marks) {
+  (void)marks;
+  bin_emit_kernel<<<g.nt_s, kEmitThreads, 0, st>>>(g, S, b, R, t, key0, key1, mode);
+  const dim3 tg((g.nt_d + 1 + 31) / 32, (g.nt_s + 31) / 32);
+  transpose_u16_kernel<<<tg, dim3(32, 8), 0, st>>>(b.off, b.offT, g.nt_s, g.nt_d + 1);
+  const bool pull = mode == 2 || mode == 3;
+  // expected records per tile = k * kTileD: keep them in registers when they fit
+  if (pull) bin_serve_kernel<<<g.nt_d, kTileThreads, 0, st>>>(g, S, b);
+  bin_apply_kernel<<<g.nt_d, kTileThreads, 0, st>>>(g, S, Snext, b, partial, R, mode, flags);
+  return hipGetLastError();
+}
+
+}  // namespace gossip

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../../include/gossip.h"
+#include "binned.h"
 #include "kernels.h"
 #include "philox.h"
 
@@ -56,6 +57,11 @@ struct gossip_engine {
   uint64_t* scratch_d = nullptr;  // 8 B
   uint32_t *orow = nullptr, *ocol = nullptr, *irow = nullptr, *icol = nullptr;
   bool has_topo = false;
+  // binned (LDS) pipeline for W == 1 random modes on one shard
+  bool binned = false;
+  BinGeom bg{};
+  BinBufs bb{};
+  void* bin_mem = nullptr;
 
   hipEvent_t ev[kTimers][2] = {};
   double time_ms[kTimers] = {0, 0};
@@ -99,6 +105,7 @@ void free_all(gossip_engine* e) {
   uint32_t* tb[] = {e->orow, e->ocol, e->irow, e->icol};
   for (uint32_t* b : tb)
     if (b) (void)hipFree(b);
+  if (e->bin_mem) (void)hipFree(e->bin_mem);
   if (e->partial_h) (void)hipHostFree(e->partial_h);
   for (auto& p : e->ev)
     for (auto& x : p)
@@ -196,6 +203,12 @@ int compute_round(gossip_engine* e, const uint64_t* gathered) {
     if ((rc = timer_begin(e, 0))) return rc;
     HIP_OK(e, launch_round_flood(a, e->stream));
     if ((rc = timer_end(e, 0))) return rc;
+  } else if (e->binned) {
+    if ((rc = timer_begin(e, 0))) return rc;
+    HIP_OK(e, launch_binned_round(e->bg, e->bb, gathered, e->Snext, e->partial_d, e->R, e->t, e->key0, e->key1,
+                                  e->mode, e->cfg.flags, e->stream, nullptr));
+    if ((rc = timer_end(e, 0))) return rc;
+    return GOSSIP_OK;  // stats are fused into the apply kernel
   } else {
     // timer 0 covers the whole S_t -> S_{t+1} transform (seed copy + round kernel)
     if ((rc = timer_begin(e, 0))) return rc;
@@ -341,6 +354,16 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
     return bail(GOSSIP_ENOMEM);
   }
   bind_slices(e);
+  if (e->mode != GOSSIP_MODE_FLOOD && !(cfg->flags & GOSSIP_FLAG_DIRECT) && bin_path_ok(e->N, e->k, e->W, G)) {
+    e->bg = make_bin_geom(e->N, e->k);
+    const size_t bytes = bin_bytes(e->bg);
+    if (hipMalloc(&e->bin_mem, bytes) != hipSuccess) {
+      e->err = "hipMalloc of " + std::to_string(bytes) + " bytes (bins) failed";
+      return bail(GOSSIP_ENOMEM);
+    }
+    bin_carve(e->bg, e->bin_mem, &e->bb);
+    e->binned = true;
+  }
   if (hipHostMalloc((void**)&e->partial_h, (4 + e->R) * 8, hipHostMallocDefault) != hipSuccess) {
     e->err = "hipHostMalloc failed";
     return bail(GOSSIP_ENOMEM);

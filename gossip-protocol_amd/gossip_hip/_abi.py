@@ -12,6 +12,7 @@ MODES = {"flood": MODE_FLOOD, "push": MODE_PUSH, "pull": MODE_PULL,
          "pushpull": MODE_PUSHPULL, "antientropy": MODE_ANTIENTROPY}
 FLAG_HASH = 1 << 0
 FLAG_TIMING = 1 << 1
+FLAG_DIRECT = 1 << 2
 
 STATUS = {0: "OK", -1: "EINVAL", -2: "EHIP", -3: "ENOMEM", -4: "ESTATE", -5: "ENODEV", -6: "ENOTSUP"}
 

@@ -60,7 +60,9 @@ enum gossip_status {
 
 enum gossip_flags {
   GOSSIP_FLAG_HASH = 1u << 0,   /* compute the per-round state hash */
-  GOSSIP_FLAG_TIMING = 1u << 1  /* bracket hot kernels with hipEvents (gossip_kernel_time) */
+  GOSSIP_FLAG_TIMING = 1u << 1, /* bracket hot kernels with hipEvents (gossip_kernel_time) */
+  GOSSIP_FLAG_DIRECT = 1u << 2  /* random modes: direct random-access kernels instead of the
+                                   binned (LDS) pipeline — same results, for A/B checks */
 };
 
 typedef struct gossip_config {
@@ -154,8 +156,9 @@ uint32_t gossip_peer(uint64_t seed, uint64_t n_nodes, uint32_t node, uint32_t ro
 int gossip_philox_device(gossip_engine_t* eng, const uint32_t* ctr4, const uint32_t* key2,
                          uint32_t* out4, uint32_t n);
 
-/* GOSSIP_FLAG_TIMING: accumulated device time (ms) and launch count of kernel
- * `which` (0 = round kernel, 1 = stats/apply kernel), since the last reset_timing. */
+/* GOSSIP_FLAG_TIMING: accumulated device time (ms) and count of `which`:
+ * 0 = the whole S_t -> S_{t+1} transform of a round (all its kernels),
+ * 1 = the separate stats kernel (direct path only; fused in the binned path). */
 int gossip_kernel_time(const gossip_engine_t* eng, uint32_t which, double* total_ms, uint64_t* launches);
 int gossip_reset_timing(gossip_engine_t* eng);
 

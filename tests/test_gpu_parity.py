@@ -8,7 +8,7 @@ import torch
 
 import oracle_py as op
 from conftest import inject_case
-from gossip_hip import Cluster, Engine, grid_topology
+from gossip_hip import FLAG_DIRECT, Cluster, Engine, grid_topology
 from gossip_hip.engine import GossipError
 
 pytestmark = pytest.mark.gpu
@@ -29,10 +29,14 @@ def test_device_philox_kat(golden):
         assert [int(x) for x in out[i]] == op.philox([int(x) for x in c[i]], [0x5EED0003, 0])
 
 
+PATHS = [0, FLAG_DIRECT]  # binned LDS pipeline (default) and the direct random-access kernels
+
+
+@pytest.mark.parametrize("path", PATHS, ids=["binned", "direct"])
 @pytest.mark.parametrize("idx", range(8))
-def test_random_golden(golden, idx):
+def test_random_golden(golden, idx, path):
     c = golden["random"][idx]
-    e = Engine(c["N"], c["R"], c["mode"], c["k"], c["seed"], flags=1)
+    e = Engine(c["N"], c["R"], c["mode"], c["k"], c["seed"], flags=1 | path)
     inject_case(e, c["inject"])
     res = e.step(256)
     assert res.rounds == len(c["rounds"])
@@ -55,9 +59,9 @@ def test_flood_golden(golden, idx):
         assert e.read(int(node)) == want
 
 
-def _compare(cfg, inj="random", rounds=256, threads=THREADS):
+def _compare(cfg, inj="random", rounds=256, threads=THREADS, path=0):
     N, R, mode, k, seed = cfg
-    e = Engine(N, R, mode, k, seed, flags=1)
+    e = Engine(N, R, mode, k, seed, flags=1 | path)
     o = op.OracleEngine(N, R, mode, k, seed, flags=1, threads=threads)
     inject_case(e, inj)
     inject_case(o, inj)
@@ -68,30 +72,37 @@ def _compare(cfg, inj="random", rounds=256, threads=THREADS):
     return re_
 
 
-def test_cfg2_push_1M_k3():
+@pytest.mark.parametrize("path", PATHS, ids=["binned", "direct"])
+def test_cfg2_push_1M_k3(path):
     """configs[1]: 1M nodes, push fanout 3, one rumor, seed 0x5EED0001."""
-    res = _compare((1 << 20, 1, "push", 3, 0x5EED0001), [(0, 0)])
+    res = _compare((1 << 20, 1, "push", 3, 0x5EED0001), [(0, 0)], path=path)
     assert res.converged and 12 <= res.rounds <= 20
 
 
-def test_pull_and_multiword():
-    _compare((1 << 18, 1, "pull", 2, 0x5EED0002), [(123, 0)])
-    _compare((100003, 130, "pushpull", 3, 77))
-    _compare((65536, 64, "push", 1, 5))
+@pytest.mark.parametrize("path", PATHS, ids=["binned", "direct"])
+def test_pull_and_multiword(path):
+    _compare((1 << 18, 1, "pull", 2, 0x5EED0002), [(123, 0)], path=path)
+    _compare((100003, 130, "pushpull", 3, 77), path=path)
+    _compare((65536, 64, "push", 1, 5), path=path)
+    _compare((300007, 17, "pushpull", 5, 0xFEED), path=path)   # ragged tiles, fanout 5
+    _compare((40000, 64, "pull", 9, 0xC0FFEE), path=path)      # fanout > 8: small sender tiles
 
 
-def test_cfg3_pushpull_16M_r64():
+@pytest.mark.parametrize("path", PATHS, ids=["binned", "direct"])
+def test_cfg3_pushpull_16M_r64(path):
     """configs[2]: 16M nodes, push-pull fanout 2, 64 rumors at Philox origins."""
-    res = _compare((1 << 24, 64, "pushpull", 2, 0x5EED0003))
+    res = _compare((1 << 24, 64, "pushpull", 2, 0x5EED0003), path=path)
     assert res.converged
     inf = res.infected.astype(np.int64)
     assert (np.diff(inf, axis=0) >= 0).all() and (inf[-1] == 1 << 24).all()
 
 
-def test_tiny_and_edge_sizes():
-    _compare((2, 1, "pushpull", 2, 1), [(1, 0)])
-    _compare((3, 64, "push", 4, 9))
-    _compare((1000, 1, "pull", 1, 3), [(999, 0)])
+@pytest.mark.parametrize("path", PATHS, ids=["binned", "direct"])
+def test_tiny_and_edge_sizes(path):
+    _compare((2, 1, "pushpull", 2, 1), [(1, 0)], path=path)
+    _compare((3, 64, "push", 4, 9), path=path)
+    _compare((1000, 1, "pull", 1, 3), [(999, 0)], path=path)
+    _compare((16385, 64, "pushpull", 64, 3), path=path)  # maximum fanout, one-node last tile
     # no injection: nothing ever spreads, never converges
     e = Engine(5000, 1, "pushpull", 2, 1)
     res = e.step(5)
