@@ -14,7 +14,7 @@
 //        runs with two contiguous row reads.
 //   K2 bin_serve  (one block per destination tile, pull modes)
 //        LDS image of S_t[tile]; for every record aimed at the tile writes the
-//        pull response S_t[p] & ~S_t[n] next to the record.
+//        pull response S_t[p] next to the record (nonzero ones only, flagged).
 //   K3 bin_apply  (one block per destination tile)
 //        LDS image acc = S_t[tile]; ORs in the pushes aimed at the tile and the
 //        responses owed to the tile's own senders (ds_or_b64), writes
@@ -32,7 +32,14 @@ namespace {
 
 constexpr int kEmitThreads = 1024;
 constexpr int kTileThreads = 1024;
-constexpr int kUnroll = 4;     // records in flight per lane in the response walker
+constexpr int kUnroll = 16;    // records in flight per lane in the run walkers
+constexpr int kUnrollSeq = 8;  // records in flight per lane in the sequential response walker
+// record id word: p_local [0,14) | n_local [14,27) | flags.  K1 rewrites every
+// id each round, so a flag never outlives its round.
+constexpr uint32_t kIdVZ = 1u << 27;  // sender value is 0: no value stored
+constexpr uint32_t kIdVF = 1u << 28;  // sender value is the full mask: no value stored
+constexpr uint32_t kIdRV = 1u << 29;  // K2 stored a nonzero pull response
+constexpr uint32_t kIdNMask = (1u << 13) - 1u;
 
 __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {
   // blocks are dealt round-robin over the 8 XCDs: give each XCD a contiguous
@@ -51,6 +58,7 @@ __device__ __forceinline__ bool edge_needed(uint32_t mode, uint64_t v, uint64_t 
   return push || pull;
 }
 
+template <int KREG>  // KREG > 0: the k (<= KREG) peers of each sender stay in registers between passes
 __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const uint64_t* __restrict__ S, BinBufs b,
                                                                   uint32_t R, uint32_t t, uint32_t key0,
                                                                   uint32_t key1, uint32_t mode) {
@@ -81,16 +89,26 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
   __syncthreads();
 
   // pass A: per-destination-tile counts
+  uint32_t pr[KREG > 0 ? kQ * KREG : 1];
 #pragma unroll
   for (uint32_t q = 0; q < kQ; ++q) {
     const uint32_t i = tid + q * kEmitThreads;
     if (i >= nsend) break;
     if (!edge_needed(mode, v[q], fm)) continue;
     const uint32_t n = (uint32_t)(base + i);
-    u32x4 x{0, 0, 0, 0};
-    for (uint32_t j = 0; j < g.k; ++j) {
-      if ((j & 3u) == 0) x = philox4x32_10(u32x4{n, t, 0u, j >> 2}, key0, key1);
-      atomicAdd(&cur[peer_from_word(lane_of(x, j & 3u), nm1, n) >> kTileDLog], 1u);
+    if (KREG > 0) {
+      const u32x4 x = philox4x32_10(u32x4{n, t, 0u, 0u}, key0, key1);
+#pragma unroll
+      for (int j = 0; j < KREG; ++j) {
+        pr[q * KREG + j] = peer_from_word(lane_of(x, j), nm1, n);
+        if ((uint32_t)j < g.k) atomicAdd(&cur[pr[q * KREG + j] >> kTileDLog], 1u);
+      }
+    } else {
+      u32x4 x{0, 0, 0, 0};
+      for (uint32_t j = 0; j < g.k; ++j) {
+        if ((j & 3u) == 0) x = philox4x32_10(u32x4{n, t, 0u, j >> 2}, key0, key1);
+        atomicAdd(&cur[peer_from_word(lane_of(x, j & 3u), nm1, n) >> kTileDLog], 1u);
+      }
     }
   }
   __syncthreads();
@@ -136,12 +154,22 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
     if (i >= nsend) break;
     if (!edge_needed(mode, v[q], fm)) continue;
     const uint32_t n = (uint32_t)(base + i);
-    u32x4 x{0, 0, 0, 0};
-    for (uint32_t j = 0; j < g.k; ++j) {
-      if ((j & 3u) == 0) x = philox4x32_10(u32x4{n, t, 0u, j >> 2}, key0, key1);
-      const uint32_t p = peer_from_word(lane_of(x, j & 3u), nm1, n);
-      const uint32_t pos = atomicAdd(&cur[p >> kTileDLog], 1u);
-      st_ids[pos] = (p & (kTileD - 1)) | (i << kTileDLog);
+    if (KREG > 0) {
+#pragma unroll
+      for (int j = 0; j < KREG; ++j) {
+        if ((uint32_t)j >= g.k) break;
+        const uint32_t p = pr[q * KREG + j];
+        const uint32_t pos = atomicAdd(&cur[p >> kTileDLog], 1u);
+        st_ids[pos] = (p & (kTileD - 1)) | (i << kTileDLog);
+      }
+    } else {
+      u32x4 x{0, 0, 0, 0};
+      for (uint32_t j = 0; j < g.k; ++j) {
+        if ((j & 3u) == 0) x = philox4x32_10(u32x4{n, t, 0u, j >> 2}, key0, key1);
+        const uint32_t p = peer_from_word(lane_of(x, j & 3u), nm1, n);
+        const uint32_t pos = atomicAdd(&cur[p >> kTileDLog], 1u);
+        st_ids[pos] = (p & (kTileD - 1)) | (i << kTileDLog);
+      }
     }
   }
   __syncthreads();
@@ -150,8 +178,11 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
   uint64_t* gvals = b.vals + (size_t)s * g.rp;
   for (uint32_t e = tid; e < total; e += kEmitThreads) {
     const uint32_t id = st_ids[e];
-    gids[e] = id;
-    gvals[e] = sval[id >> kTileDLog];
+    const uint64_t x = sval[id >> kTileDLog];
+    // zero and full values are implied by a flag: light rounds move ids only
+    const uint32_t fl = x == 0 ? kIdVZ : (x == fm ? kIdVF : 0u);
+    gids[e] = id | fl;
+    if (!fl) gvals[e] = x;
   }
 }
 
@@ -241,6 +272,15 @@ __device__ __forceinline__ void tile_epilogue(const unsigned long long* acc, uin
   if (tid < R && cnt[tid]) atomicAdd((unsigned long long*)&partial[4 + tid], (unsigned long long)cnt[tid]);
 }
 
+// value of a record: implied by its flag, else loaded (from a clamped index so
+// that no load sits behind a branch)
+__device__ __forceinline__ uint64_t record_value(uint32_t id, const uint64_t* __restrict__ vals, int32_t rec,
+                                                 uint64_t fm) {
+  const bool stored = rec >= 0 && !(id & (kIdVZ | kIdVF));
+  const uint64_t x = vals[stored ? rec : 0];
+  return stored ? x : ((id & kIdVF) ? fm : 0ull);
+}
+
 // Visits every record of the runs (s, T) for s in [0, nt_s): a wave takes 64
 // consecutive runs at a time (lane = run), scans their lengths, and its lanes
 // then walk the concatenated records in order, kUnroll records per lane with
@@ -264,9 +304,9 @@ __device__ __forceinline__ void for_each_run_record(const BinGeom& g, const uint
     }
     const uint32_t exc = inc - len;
     const uint32_t total = __shfl(inc, 63, 64);
-    const int64_t basep = (int64_t)s * g.rp + be - exc;  // record = basep(owner) + f
+    const int32_t basep = (int32_t)(s * g.rp + be - exc);  // record = basep(owner) + f (< 2^31)
     for (uint32_t f0 = 0; f0 < total; f0 += 64 * U) {
-      int64_t rec[U];
+      int32_t rec[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint32_t f = f0 + u * 64 + lane;
@@ -278,8 +318,8 @@ __device__ __forceinline__ void for_each_run_record(const BinGeom& g, const uint
         }
         // every lane takes part in the shuffle: a bpermute from a lane that is
         // masked off returns garbage, so no conditional around it
-        const int64_t bp = __shfl(basep, r, 64);
-        rec[u] = f < total ? bp + f : -1;
+        const int32_t bp = __shfl(basep, r, 64);
+        rec[u] = f < total ? bp + (int32_t)f : -1;
       }
       fn(rec);
     }
@@ -287,9 +327,10 @@ __device__ __forceinline__ void for_each_run_record(const BinGeom& g, const uint
 }
 
 // K2 — one block per destination tile T (pull modes): LDS image of S_t[T];
-// every record aimed at T gets its pull response S_t[p] & ~S_t[n] written
-// next to it.
-__global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, const uint64_t* __restrict__ S, BinBufs b) {
+// every record aimed at T from a sender that is not yet fully informed gets
+// its pull response S_t[p] written next to it when nonzero (id flag kIdRV).
+__global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, const uint64_t* __restrict__ S, BinBufs b,
+                                                                  uint32_t R) {
   __shared__ unsigned long long img[kTileD];
   const uint32_t tid = threadIdx.x;
   const uint32_t T = xcd_remap(blockIdx.x, g.nt_d);
@@ -303,22 +344,25 @@ __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, cons
       img[(q0 + q) * kTileThreads + tid] = node0 + (q0 + q) * kTileThreads + tid < g.N ? x[q] : 0ull;
   }
   __syncthreads();
-  const uint32_t* __restrict__ gids = b.ids;
-  const uint64_t* __restrict__ gvals = b.vals;
+  const uint32_t* gids = b.ids;
+  uint32_t* gidsw = b.ids;
   uint64_t* __restrict__ gresp = b.resp;
   const uint16_t* rowb = b.offT + (size_t)T * g.nt_s;
-  for_each_run_record<kUnroll>(g, rowb, rowb + g.nt_s, [&](const int64_t* rec) {
+  for_each_run_record<kUnroll>(g, rowb, rowb + g.nt_s, [&](const int32_t* rec) {
     uint32_t id[kUnroll];
-    uint64_t v[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) id[u] = gids[rec[u] >= 0 ? rec[u] : 0];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
-      const int64_t r = rec[u] >= 0 ? rec[u] : 0;
-      id[u] = gids[r];
-      v[u] = gvals[r];
+      // a fully informed sender needs nothing; otherwise the whole S_t[p] goes
+      // back (bits n already holds are harmless to OR), so no value is read
+      if (rec[u] < 0 || (id[u] & kIdVF)) continue;
+      const uint64_t r = img[id[u] & (kTileD - 1)];
+      if (r) {  // only nonzero responses move: the flag tells K3 to read it
+        gresp[rec[u]] = r;
+        gidsw[rec[u]] = id[u] | kIdRV;
+      }
     }
-#pragma unroll
-    for (int u = 0; u < kUnroll; ++u)
-      if (rec[u] >= 0) gresp[rec[u]] = img[id[u] & (kTileD - 1)] & ~v[u];
   });
 }
 
@@ -349,18 +393,16 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, cons
   const uint32_t* __restrict__ gids = b.ids;
   const uint64_t* __restrict__ gvals = b.vals;
   const uint64_t* __restrict__ gresp = b.resp;
+  const uint64_t fm = full_mask1(R);
   if (mode == 1 || mode == 3) {  // pushes aimed at this tile
     const uint16_t* rowb = b.offT + (size_t)X * g.nt_s;
-    for_each_run_record<kUnroll>(g, rowb, rowb + g.nt_s, [&](const int64_t* rec) {
+    for_each_run_record<kUnroll>(g, rowb, rowb + g.nt_s, [&](const int32_t* rec) {
       uint32_t id[kUnroll];
       uint64_t v[kUnroll];
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        const int64_t r = rec[u] >= 0 ? rec[u] : 0;
-        const uint64_t x = gvals[r];
-        id[u] = gids[r];
-        v[u] = rec[u] >= 0 ? x : 0ull;
-      }
+      for (int u = 0; u < kUnroll; ++u) id[u] = gids[rec[u] >= 0 ? rec[u] : 0];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) v[u] = rec[u] >= 0 ? record_value(id[u], gvals, rec[u], fm) : 0ull;
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         const uint32_t p = id[u] & (kTileD - 1);
@@ -375,21 +417,26 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, cons
       const uint32_t total = b.off[(size_t)s * (g.nt_d + 1) + g.nt_d];
       const size_t reg = (size_t)s * g.rp;
       const uint32_t nb = (s - s0) << g.ts_log;
-      for (uint32_t p0 = 0; p0 < total; p0 += kTileThreads * kUnroll) {
-        uint64_t r[kUnroll];
-        uint32_t id[kUnroll];
+      for (uint32_t p0 = 0; p0 < total; p0 += kTileThreads * kUnrollSeq) {
+        uint64_t r[kUnrollSeq];
+        uint32_t id[kUnrollSeq];
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
+        for (int u = 0; u < kUnrollSeq; ++u) {
           const uint32_t pos = p0 + u * kTileThreads + tid;
-          const size_t at = reg + (pos < total ? pos : 0u);
-          const uint64_t x = gresp[at];
-          id[u] = gids[at];
-          r[u] = pos < total ? x : 0ull;
+          id[u] = gids[reg + (pos < total ? pos : 0u)];
+          if (pos >= total) id[u] = 0;
         }
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
+        for (int u = 0; u < kUnrollSeq; ++u) {
+          const uint32_t pos = p0 + u * kTileThreads + tid;
+          const bool rv = (id[u] & kIdRV) != 0;
+          const uint64_t x = gresp[rv ? reg + pos : 0];
+          r[u] = rv ? x : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < kUnrollSeq; ++u) {
           if (!r[u]) continue;
-          const uint32_t node = nb + (id[u] >> kTileDLog);
+          const uint32_t node = nb + ((id[u] >> kTileDLog) & kIdNMask);
           if (r[u] & ~acc[node]) atomicOr(&acc[node], (unsigned long long)r[u]);
         }
       }
@@ -449,12 +496,15 @@ hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, const uint64_
                                uint64_t* partial, uint32_t R, uint32_t t, uint32_t key0, uint32_t key1,
                                uint32_t mode, uint32_t flags, hipStream_t st, hipEvent_t* marks) {
   (void)marks;
-  bin_emit_kernel<<<g.nt_s, kEmitThreads, 0, st>>>(g, S, b, R, t, key0, key1, mode);
+  if (g.k <= 2)
+    bin_emit_kernel<2><<<g.nt_s, kEmitThreads, 0, st>>>(g, S, b, R, t, key0, key1, mode);
+  else
+    bin_emit_kernel<0><<<g.nt_s, kEmitThreads, 0, st>>>(g, S, b, R, t, key0, key1, mode);
   const dim3 tg((g.nt_d + 1 + 31) / 32, (g.nt_s + 31) / 32);
   transpose_u16_kernel<<<tg, dim3(32, 8), 0, st>>>(b.off, b.offT, g.nt_s, g.nt_d + 1);
   const bool pull = mode == 2 || mode == 3;
   // expected records per tile = k * kTileD: keep them in registers when they fit
-  if (pull) bin_serve_kernel<<<g.nt_d, kTileThreads, 0, st>>>(g, S, b);
+  if (pull) bin_serve_kernel<<<g.nt_d, kTileThreads, 0, st>>>(g, S, b, R);
   bin_apply_kernel<<<g.nt_d, kTileThreads, 0, st>>>(g, S, Snext, b, partial, R, mode, flags);
   return hipGetLastError();
 }
