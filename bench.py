@@ -132,7 +132,6 @@ def main():
         dt = float(t.item())
 
     round_ms, round_launches = eng.kernel_time(0)
-    stats_ms, stats_launches = eng.kernel_time(1)
     total_rounds = sum(rounds)
     value = n_total * total_rounds / dt
     nown = eng.hi - eng.lo
@@ -160,9 +159,10 @@ def main():
                        "parallelism": f"shard{world}" if world > 1 else "single"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": load_pmc(workload),
-                         "kernel": "round_random_kernel<W=1,pull,push>",
+                         "kernel": ("round pipeline bin_emit+transpose_u16+bin_serve+bin_apply" if world == 1 else
+                                    "sharded round: seed copy + round_random_kernel") + " (hipEvent-timed per round)",
                          "bytes_per_node_round": bpn, "avg_launch_us": avg_launch_s * 1e6,
-                         "stats_kernel_avg_us": stats_ms * 1e3 / max(stats_launches, 1)},
+                         "rounds_timed": round_launches},
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(n_total, seed)

@@ -33,20 +33,32 @@ def _as_tensor(ptr: int, nbytes: int, on_device: bool) -> torch.Tensor:
     return torch.from_numpy(arr)
 
 
+def _device_collectives(group) -> bool:
+    return dist.get_backend(group) == "nccl"
+
+
 def sharded_round(engine, group=None) -> dict:
     """Runs one round of a sharded engine; every rank must call it."""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     send_p, recv_p, nbytes = engine.exchange_buffers()
+    on_dev = engine.on_device and world > 1 and _device_collectives(group)
     if world > 1:
         recv = _as_tensor(recv_p, nbytes * world, engine.on_device)
         send = _as_tensor(send_p, nbytes, engine.on_device)
-        if not engine.on_device:
-            send = send.clone()  # gloo: keep source and destination disjoint
-        dist.all_gather_into_tensor(recv, send, group=group)
+        if on_dev:
+            # RCCL all-gather in place: the send slice lies inside the image
+            dist.all_gather_into_tensor(recv, send, group=group)
+        else:
+            # gloo (CPU): disjoint host buffers; device engines stage through host
+            host = torch.empty(nbytes // 8 * world, dtype=torch.int64)
+            dist.all_gather_into_tensor(host, send.cpu() if engine.on_device else send.clone(), group=group)
+            recv.copy_(host)
+            if engine.on_device:
+                torch.cuda.synchronize()
     partial = engine.round_compute()
     if world > 1:
         t = torch.from_numpy(partial.view(np.int64).copy())
-        if engine.on_device:
+        if on_dev:
             t = t.cuda()
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
         partial = t.cpu().numpy().view(np.uint64)
