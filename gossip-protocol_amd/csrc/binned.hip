@@ -31,6 +31,7 @@ namespace gossip {
 namespace {
 
 constexpr int kEmitThreads = 1024;
+constexpr uint32_t kEmitGrid = 256;  // one persistent emit block per CU
 constexpr int kTileThreads = 1024;
 constexpr int kUnroll = 16;    // records in flight per lane in the run walkers
 constexpr int kUnrollSeq = 8;  // records in flight per lane in the sequential response walker
@@ -69,25 +70,37 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
   __shared__ uint32_t wpre[kEmitThreads / 64 + 1];
 
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t s = blockIdx.x;
-  const uint64_t base = (uint64_t)s << g.ts_log;
-  const uint32_t nsend = (uint32_t)min<uint64_t>(g.ts, g.N - base);
   const uint64_t nm1 = g.N - 1, fm = full_mask1(R);
   constexpr uint32_t kQ = kMaxSenders / kEmitThreads;  // senders per thread upper bound
 
+  // persistent over sender regions s = blockIdx.x, +gridDim.x, ...: the next
+  // region's sender values are loaded while this one is sorted and written
+  auto load_values = [&](uint32_t s, uint64_t* v) {
+    const uint64_t base = (uint64_t)s << g.ts_log;
+    const uint32_t nsend = (uint32_t)min<uint64_t>(g.ts, g.N - base);
+#pragma unroll
+    for (uint32_t q = 0; q < kQ; ++q) {
+      const uint32_t i = tid + q * kEmitThreads;
+      // clamp, never branch around a load: a guarded load is waited on alone
+      const uint64_t x = S[base + min(i, nsend - 1)];
+      v[q] = i < nsend ? x : 0ull;
+    }
+  };
+  uint64_t v[kQ], vn[kQ];
+  if (blockIdx.x < g.nt_s) load_values(blockIdx.x, v);
+  for (uint32_t s = blockIdx.x; s < g.nt_s; s += gridDim.x) {
+  const uint64_t base = (uint64_t)s << g.ts_log;
+  const uint32_t nsend = (uint32_t)min<uint64_t>(g.ts, g.N - base);
+  __syncthreads();  // the previous region's write-out has read cur/st_ids/sval
+
   for (uint32_t d = tid; d < g.nt_d; d += kEmitThreads) cur[d] = 0;
-  // all sender values of this thread first: independent loads in flight together
-  uint64_t v[kQ];
 #pragma unroll
   for (uint32_t q = 0; q < kQ; ++q) {
     const uint32_t i = tid + q * kEmitThreads;
-    // clamp, never branch around a load: a guarded load is waited on alone
-    const uint64_t x = S[base + min(i, nsend - 1)];
-    v[q] = i < nsend ? x : 0ull;
     if (i < g.ts) sval[i] = v[q];
   }
+  if (s + gridDim.x < g.nt_s) load_values(s + gridDim.x, vn);
   __syncthreads();
-
   // pass A: per-destination-tile counts
   uint32_t pr[KREG > 0 ? kQ * KREG : 1];
 #pragma unroll
@@ -183,6 +196,9 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
     const uint32_t fl = x == 0 ? kIdVZ : (x == fm ? kIdVF : 0u);
     gids[e] = id | fl;
     if (!fl) gvals[e] = x;
+  }
+#pragma unroll
+  for (uint32_t q = 0; q < kQ; ++q) v[q] = vn[q];
   }
 }
 
@@ -496,10 +512,11 @@ hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, const uint64_
                                uint64_t* partial, uint32_t R, uint32_t t, uint32_t key0, uint32_t key1,
                                uint32_t mode, uint32_t flags, hipStream_t st, hipEvent_t* marks) {
   (void)marks;
+  const uint32_t eg = g.nt_s < kEmitGrid ? g.nt_s : kEmitGrid;  // persistent: one block per CU
   if (g.k <= 2)
-    bin_emit_kernel<2><<<g.nt_s, kEmitThreads, 0, st>>>(g, S, b, R, t, key0, key1, mode);
+    bin_emit_kernel<2><<<eg, kEmitThreads, 0, st>>>(g, S, b, R, t, key0, key1, mode);
   else
-    bin_emit_kernel<0><<<g.nt_s, kEmitThreads, 0, st>>>(g, S, b, R, t, key0, key1, mode);
+    bin_emit_kernel<0><<<eg, kEmitThreads, 0, st>>>(g, S, b, R, t, key0, key1, mode);
   const dim3 tg((g.nt_d + 1 + 31) / 32, (g.nt_s + 31) / 32);
   transpose_u16_kernel<<<tg, dim3(32, 8), 0, st>>>(b.off, b.offT, g.nt_s, g.nt_d + 1);
   const bool pull = mode == 2 || mode == 3;

@@ -19,14 +19,10 @@ struct u32x4 {
 __host__ __device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
-    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
-#else
+    // one 32x32->64 product each (v_mad_u64_u32 on gfx950) gives both halves
     const uint64_t m0 = (uint64_t)0xD2511F53u * c.x, m1 = (uint64_t)0xCD9E8D57u * c.z;
     const uint32_t hi0 = (uint32_t)(m0 >> 32), lo0 = (uint32_t)m0;
     const uint32_t hi1 = (uint32_t)(m1 >> 32), lo1 = (uint32_t)m1;
-#endif
     c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
@@ -39,8 +35,9 @@ __host__ __device__ __forceinline__ uint32_t lane_of(const u32x4& x, uint32_t q)
 }
 
 // Uniform over [0, N) \ {n} by integer arithmetic only.
+// N < 2^32, so N-1 fits 32 bits and the scaling is one high-half product.
 __host__ __device__ __forceinline__ uint32_t peer_from_word(uint32_t x, uint64_t nm1, uint32_t n) {
-  const uint32_t p = (uint32_t)(((uint64_t)x * nm1) >> 32);
+  const uint32_t p = (uint32_t)(((uint64_t)x * (uint32_t)nm1) >> 32);
   return p + (p >= n ? 1u : 0u);
 }
 
