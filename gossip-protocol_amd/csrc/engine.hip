@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../../include/gossip.h"
+#include "antientropy.h"
 #include "binned.h"
 #include "kernels.h"
 #include "philox.h"
@@ -57,6 +58,9 @@ struct gossip_engine {
   uint64_t* scratch_d = nullptr;  // 8 B
   uint32_t *orow = nullptr, *ocol = nullptr, *irow = nullptr, *icol = nullptr;
   bool has_topo = false;
+  // ANTIENTROPY: rows V[n*K + c], alive bytes, global max vector
+  uint32_t *V = nullptr, *Vn = nullptr, *target = nullptr;
+  uint8_t *alive = nullptr, *alive_n = nullptr;
   // binned (LDS) pipeline for W == 1 random modes on one shard
   bool binned = false;
   BinGeom bg{};
@@ -106,6 +110,9 @@ void free_all(gossip_engine* e) {
   for (uint32_t* b : tb)
     if (b) (void)hipFree(b);
   if (e->bin_mem) (void)hipFree(e->bin_mem);
+  void* ae[] = {e->V, e->Vn, e->target, e->alive, e->alive_n};
+  for (void* b : ae)
+    if (b) (void)hipFree(b);
   if (e->partial_h) (void)hipHostFree(e->partial_h);
   for (auto& p : e->ev)
     for (auto& x : p)
@@ -170,6 +177,10 @@ int timer_collect(gossip_engine* e) {
 // exchange payload for this round: S_t (random modes) or F_t (FLOOD); the
 // send slice lies inside the gathered image, so the all-gather is in place.
 int prepare_send(gossip_engine* e, uint64_t** send, uint64_t** image) {
+  if (e->mode == GOSSIP_MODE_ANTIENTROPY) {  // single shard: nothing to exchange
+    *send = *image = nullptr;
+    return GOSSIP_OK;
+  }
   if (e->mode == GOSSIP_MODE_FLOOD) {
     HIP_OK(e, launch_frontier(e->S, e->Sprev, e->F, (uint64_t)e->W * e->Nl, e->stream));
     *send = e->F;
@@ -185,6 +196,7 @@ uint64_t* current_image(gossip_engine* e) { return e->mode == GOSSIP_MODE_FLOOD 
 
 void bind_slices(gossip_engine* e) {
   const size_t off = (size_t)e->rank * e->W * e->Nl;
+  if (e->mode == GOSSIP_MODE_ANTIENTROPY) return;
   if (e->mode == GOSSIP_MODE_FLOOD) {
     e->F = e->imgF + off;
   } else {
@@ -193,10 +205,42 @@ void bind_slices(gossip_engine* e) {
   }
 }
 
+AeArgs make_ae_args(gossip_engine* e) {
+  AeArgs a{};
+  a.V = e->V;
+  a.Vn = e->Vn;
+  a.alive = e->alive;
+  a.alive_n = e->alive_n;
+  a.target = e->target;
+  a.partial = e->partial_d;
+  a.N = e->N;
+  a.K = e->R;
+  a.L = ae_lanes(e->R);
+  a.k = e->k;
+  a.t = e->t;
+  a.key0 = e->key0;
+  a.key1 = e->key1;
+  a.fail = e->cfg.churn_fail;
+  a.rec = e->cfg.churn_recover;
+  a.flags = e->cfg.flags;
+  return a;
+}
+
 // compute S_{t+1} of the owned shard from the gathered image + partial stats (device)
 int compute_round(gossip_engine* e, const uint64_t* gathered) {
   const size_t bytes = (size_t)e->W * e->Nl * 8;
   HIP_OK(e, hipMemsetAsync(e->partial_d, 0, (4 + e->R) * 8, e->stream));
+  if (e->mode == GOSSIP_MODE_ANTIENTROPY) {
+    int rc;
+    const AeArgs a = make_ae_args(e);
+    if ((rc = timer_begin(e, 0))) return rc;
+    HIP_OK(e, hipMemcpyAsync(e->Vn, e->V, e->N * e->R * 4, hipMemcpyDeviceToDevice, e->stream));
+    HIP_OK(e, launch_ae_round(a, e->stream));
+    if ((rc = timer_end(e, 0))) return rc;
+    if ((rc = timer_begin(e, 1))) return rc;
+    HIP_OK(e, launch_ae_stats(a, e->Vn, e->alive_n, e->stream));
+    return timer_end(e, 1);
+  }
   RoundArgs a = make_args(e, gathered);
   int rc;
   if (e->mode == GOSSIP_MODE_FLOOD) {
@@ -223,7 +267,10 @@ int compute_round(gossip_engine* e, const uint64_t* gathered) {
 }
 
 void rotate(gossip_engine* e) {
-  if (e->mode == GOSSIP_MODE_FLOOD) {
+  if (e->mode == GOSSIP_MODE_ANTIENTROPY) {
+    std::swap(e->V, e->Vn);
+    std::swap(e->alive, e->alive_n);
+  } else if (e->mode == GOSSIP_MODE_FLOOD) {
     uint64_t* tmp = e->Sprev;
     e->Sprev = e->S;
     e->S = e->Snext;
@@ -268,8 +315,13 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
     g_create_error = "n_rumors must be in [1, 4096]";
     return GOSSIP_EINVAL;
   }
-  if (cfg->mode > GOSSIP_MODE_PUSHPULL) {
-    g_create_error = "mode not built";
+  if (cfg->mode > GOSSIP_MODE_ANTIENTROPY) {
+    g_create_error = "unknown mode";
+    return GOSSIP_ENOTSUP;
+  }
+  if (cfg->mode == GOSSIP_MODE_ANTIENTROPY &&
+      ((cfg->shard_count ? cfg->shard_count : 1) != 1 || cfg->n_rumors > 64)) {
+    g_create_error = "ANTIENTROPY runs on one shard with at most 64 components";
     return GOSSIP_ENOTSUP;
   }
   if (cfg->mode != GOSSIP_MODE_FLOOD && (cfg->fanout == 0 || cfg->fanout > 64)) {
@@ -346,7 +398,20 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
     return hipMemset(*p, 0, bytes) == hipSuccess;
   };
   if (!alloc(&e->partial_d, (4 + e->R) * 8) || !alloc(&e->scratch_d, 8)) return bail(GOSSIP_ENOMEM);
-  if (e->mode == GOSSIP_MODE_FLOOD) {
+  auto alloc_raw = [&](void** p, size_t bytes) {
+    if (hipMalloc(p, bytes) != hipSuccess) {
+      e->err = "hipMalloc of " + std::to_string(bytes) + " bytes failed";
+      return false;
+    }
+    return hipMemset(*p, 0, bytes) == hipSuccess;
+  };
+  if (e->mode == GOSSIP_MODE_ANTIENTROPY) {
+    const size_t vb = (size_t)e->N * e->R * 4;
+    if (!alloc_raw((void**)&e->V, vb) || !alloc_raw((void**)&e->Vn, vb) || !alloc_raw((void**)&e->target, 256) ||
+        !alloc_raw((void**)&e->alive, e->N) || !alloc_raw((void**)&e->alive_n, e->N))
+      return bail(GOSSIP_ENOMEM);
+    if (hipMemset(e->alive, 1, e->N) != hipSuccess) return bail(GOSSIP_EHIP);
+  } else if (e->mode == GOSSIP_MODE_FLOOD) {
     if (!alloc(&e->S, shard) || !alloc(&e->Snext, shard) || !alloc(&e->Sprev, shard) || !alloc(&e->skip, shard) ||
         !alloc(&e->imgF, image))
       return bail(GOSSIP_ENOMEM);
@@ -354,7 +419,8 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
     return bail(GOSSIP_ENOMEM);
   }
   bind_slices(e);
-  if (e->mode != GOSSIP_MODE_FLOOD && !(cfg->flags & GOSSIP_FLAG_DIRECT) && bin_path_ok(e->N, e->k, e->W, G)) {
+  if (e->mode != GOSSIP_MODE_FLOOD && e->mode != GOSSIP_MODE_ANTIENTROPY && !(cfg->flags & GOSSIP_FLAG_DIRECT) &&
+      bin_path_ok(e->N, e->k, e->W, G)) {
     e->bg = make_bin_geom(e->N, e->k);
     const size_t bytes = bin_bytes(e->bg);
     if (hipMalloc(&e->bin_mem, bytes) != hipSuccess) {
@@ -452,7 +518,11 @@ int gossip_reset(gossip_engine_t* e) {
   if (!e) return GOSSIP_EINVAL;
   if (int rc = set_dev(e)) return rc;
   const size_t shard = (size_t)e->W * e->Nl * 8;
-  if (e->mode == GOSSIP_MODE_FLOOD) {
+  if (e->mode == GOSSIP_MODE_ANTIENTROPY) {
+    HIP_OK(e, hipMemsetAsync(e->V, 0, e->N * e->R * 4, e->stream));
+    HIP_OK(e, hipMemsetAsync(e->target, 0, 256, e->stream));
+    HIP_OK(e, hipMemsetAsync(e->alive, 1, e->N, e->stream));
+  } else if (e->mode == GOSSIP_MODE_FLOOD) {
     HIP_OK(e, hipMemsetAsync(e->S, 0, shard, e->stream));
     HIP_OK(e, hipMemsetAsync(e->Snext, 0, shard, e->stream));
     HIP_OK(e, hipMemsetAsync(e->Sprev, 0, shard, e->stream));
@@ -471,6 +541,10 @@ int gossip_inject(gossip_engine_t* e, uint64_t node, uint32_t rumor) {
   if (node >= e->N || rumor >= e->R) return e->fail(GOSSIP_EINVAL, "inject(%llu, %u) out of range",
                                                     (unsigned long long)node, rumor);
   if (int rc = set_dev(e)) return rc;
+  if (e->mode == GOSSIP_MODE_ANTIENTROPY) {
+    HIP_OK(e, launch_ae_inject(e->V, e->target, node, e->R, rumor, e->stream));
+    return GOSSIP_OK;
+  }
   HIP_OK(e, launch_inject(e->S, e->Nl, e->lo, e->hi, e->N, e->R, e->key0, e->key1, (int64_t)node, rumor, e->stream));
   return GOSSIP_OK;
 }
@@ -478,6 +552,10 @@ int gossip_inject(gossip_engine_t* e, uint64_t node, uint32_t rumor) {
 int gossip_inject_random(gossip_engine_t* e) {
   if (!e) return GOSSIP_EINVAL;
   if (int rc = set_dev(e)) return rc;
+  if (e->mode == GOSSIP_MODE_ANTIENTROPY) {
+    HIP_OK(e, launch_ae_init(e->V, e->target, e->N, e->R, e->key0, e->key1, e->stream));
+    return GOSSIP_OK;
+  }
   HIP_OK(e, launch_inject(e->S, e->Nl, e->lo, e->hi, e->N, e->R, e->key0, e->key1, -1, 0, e->stream));
   return GOSSIP_OK;
 }
@@ -507,7 +585,7 @@ int gossip_round_compute(gossip_engine_t* e, uint64_t* partial) {
   HIP_OK(e, hipStreamSynchronize(e->stream));
   if (int rc = timer_collect(e)) return rc;
   std::memcpy(partial, e->partial_h, (4 + e->R) * 8);
-  partial[1] = e->nown;
+  if (e->mode != GOSSIP_MODE_ANTIENTROPY) partial[1] = e->nown;
   return GOSSIP_OK;
 }
 
@@ -546,6 +624,7 @@ int gossip_step(gossip_engine_t* e, uint32_t max_rounds, gossip_round_stats_t* s
 
 int gossip_read_bitset(gossip_engine_t* e, uint64_t node, uint64_t* out, uint32_t nwords) {
   if (!e || !out) return GOSSIP_EINVAL;
+  if (e->mode == GOSSIP_MODE_ANTIENTROPY) return e->fail(GOSSIP_ESTATE, "ANTIENTROPY: use gossip_read_versions");
   if (node < e->lo || node >= e->hi) return e->fail(GOSSIP_EINVAL, "node %llu not in this shard", (unsigned long long)node);
   if (nwords < e->W) return e->fail(GOSSIP_EINVAL, "need %u words", e->W);
   if (int rc = set_dev(e)) return rc;
@@ -557,11 +636,27 @@ int gossip_read_bitset(gossip_engine_t* e, uint64_t node, uint64_t* out, uint32_
 
 int gossip_read_shard(gossip_engine_t* e, uint64_t* out, uint64_t n_words) {
   if (!e || !out) return GOSSIP_EINVAL;
+  if (e->mode == GOSSIP_MODE_ANTIENTROPY) return e->fail(GOSSIP_ESTATE, "ANTIENTROPY: use gossip_read_versions");
   if (n_words < (uint64_t)e->W * e->nown) return e->fail(GOSSIP_EINVAL, "output too small");
   if (int rc = set_dev(e)) return rc;
   HIP_OK(e, hipStreamSynchronize(e->stream));
   for (uint32_t w = 0; w < e->W; ++w)
     HIP_OK(e, hipMemcpy(out + (size_t)w * e->nown, e->S + (size_t)w * e->Nl, e->nown * 8, hipMemcpyDeviceToHost));
+  return GOSSIP_OK;
+}
+
+int gossip_read_versions(gossip_engine_t* e, uint64_t node, uint32_t* out, uint32_t ncomp, uint32_t* alive) {
+  if (!e || !out) return GOSSIP_EINVAL;
+  if (e->mode != GOSSIP_MODE_ANTIENTROPY) return e->fail(GOSSIP_ESTATE, "read_versions needs ANTIENTROPY mode");
+  if (node >= e->N || ncomp < e->R) return e->fail(GOSSIP_EINVAL, "bad node or component count");
+  if (int rc = set_dev(e)) return rc;
+  HIP_OK(e, hipStreamSynchronize(e->stream));
+  HIP_OK(e, hipMemcpy(out, e->V + node * e->R, e->R * 4, hipMemcpyDeviceToHost));
+  if (alive) {
+    uint8_t a = 0;
+    HIP_OK(e, hipMemcpy(&a, e->alive + node, 1, hipMemcpyDeviceToHost));
+    *alive = a;
+  }
   return GOSSIP_OK;
 }
 
@@ -575,6 +670,16 @@ int gossip_shard_range(const gossip_engine_t* e, uint64_t* lo, uint64_t* hi) {
 int gossip_state_hash(gossip_engine_t* e, uint64_t* out) {
   if (!e || !out) return GOSSIP_EINVAL;
   if (int rc = set_dev(e)) return rc;
+  if (e->mode == GOSSIP_MODE_ANTIENTROPY) {  // the stats kernel's hash of the current rows
+    AeArgs a = make_ae_args(e);
+    a.flags |= GOSSIP_FLAG_HASH;
+    HIP_OK(e, hipMemsetAsync(e->partial_d, 0, (4 + e->R) * 8, e->stream));
+    HIP_OK(e, launch_ae_stats(a, e->V, e->alive, e->stream));
+    HIP_OK(e, hipMemcpyAsync(e->partial_h, e->partial_d, (4 + e->R) * 8, hipMemcpyDeviceToHost, e->stream));
+    HIP_OK(e, hipStreamSynchronize(e->stream));
+    *out = e->partial_h[3];
+    return GOSSIP_OK;
+  }
   HIP_OK(e, hipMemsetAsync(e->scratch_d, 0, 8, e->stream));
   HIP_OK(e, launch_hash(e->S, e->Nl, e->nown, e->W, e->N, e->lo, e->scratch_d, e->stream));
   HIP_OK(e, hipMemcpyAsync(e->partial_h, e->scratch_d, 8, hipMemcpyDeviceToHost, e->stream));

@@ -28,7 +28,9 @@ class Config(C.Structure):
         ("device", C.c_int32),
         ("shard_rank", C.c_uint32),
         ("shard_count", C.c_uint32),
-        ("reserved", C.c_uint32 * 5),
+        ("churn_fail", C.c_uint32),
+        ("churn_recover", C.c_uint32),
+        ("reserved", C.c_uint32 * 3),
     ]
 
 
@@ -67,6 +69,7 @@ SIGNATURES = [
     ("round_commit", C.c_int, [P, U64P, C.POINTER(RoundStats)]),
     ("read_bitset", C.c_int, [P, C.c_uint64, U64P, C.c_uint32]),
     ("read_shard", C.c_int, [P, U64P, C.c_uint64]),
+    ("read_versions", C.c_int, [P, C.c_uint64, U32P, C.c_uint32, U32P]),
     ("shard_range", C.c_int, [P, U64P, U64P]),
     ("state_hash", C.c_int, [P, U64P]),
     ("round_index", C.c_uint32, [P]),

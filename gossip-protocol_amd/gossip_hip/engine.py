@@ -55,8 +55,14 @@ class StepResult:
         return bool(self.stats and self.stats[-1]["converged"])
 
 
+def churn_threshold(p: float) -> int:
+    """Probability -> the u32 threshold x of DESIGN.md §2.7 (event iff Philox word < x)."""
+    return max(0, min(0xFFFFFFFF, int(round(p * 2.0 ** 32))))
+
+
 def make_config(n_nodes: int, n_rumors: int = 1, mode="push", fanout: int = 1, seed: int = 0,
-                flags: int = 0, device: int = -1, shard_rank: int = 0, shard_count: int = 1) -> Config:
+                flags: int = 0, device: int = -1, shard_rank: int = 0, shard_count: int = 1,
+                churn_fail: int = 0, churn_recover: int = 0) -> Config:
     cfg = Config()
     cfg.n_nodes = n_nodes
     cfg.n_rumors = n_rumors
@@ -67,6 +73,8 @@ def make_config(n_nodes: int, n_rumors: int = 1, mode="push", fanout: int = 1, s
     cfg.device = device
     cfg.shard_rank = shard_rank
     cfg.shard_count = shard_count
+    cfg.churn_fail = churn_fail
+    cfg.churn_recover = churn_recover
     return cfg
 
 
@@ -161,6 +169,14 @@ class AbiEngine:
         words = self.read_bitset(node)
         return [w * 64 + b for w in range(self.n_words) for b in range(64) if (int(words[w]) >> b) & 1]
 
+    def read_versions(self, node: int):
+        """ANTIENTROPY: (versions[K], alive) of one node."""
+        out = np.zeros(self.n_rumors, dtype=np.uint32)
+        alive = C.c_uint32()
+        self._check(self._fn("read_versions")(self._h, C.c_uint64(node), out.ctypes.data_as(_abi.U32P),
+                                              C.c_uint32(self.n_rumors), C.byref(alive)))
+        return out, bool(alive.value)
+
     def read_shard(self) -> np.ndarray:
         n = self.hi - self.lo
         out = np.zeros(self.n_words * n, dtype=np.uint64)
@@ -203,8 +219,10 @@ class Engine(AbiEngine):
     on_device = True
 
     def __init__(self, n_nodes: int, n_rumors: int = 1, mode="push", fanout: int = 1, seed: int = 0,
-                 flags: int = 0, device: int = -1, shard_rank: int = 0, shard_count: int = 1):
-        cfg = make_config(n_nodes, n_rumors, mode, fanout, seed, flags, device, shard_rank, shard_count)
+                 flags: int = 0, device: int = -1, shard_rank: int = 0, shard_count: int = 1,
+                 churn_fail: int = 0, churn_recover: int = 0):
+        cfg = make_config(n_nodes, n_rumors, mode, fanout, seed, flags, device, shard_rank, shard_count,
+                          churn_fail, churn_recover)
         super().__init__(load_library(), "gossip_", cfg)
 
     def set_stream(self, hip_stream: int):

@@ -45,7 +45,7 @@ enum gossip_mode {
   GOSSIP_MODE_PUSH = 1,       /* S'[p_j(n)] |= S[n]                                         */
   GOSSIP_MODE_PULL = 2,       /* S'[n] |= S[p_j(n)]                                         */
   GOSSIP_MODE_PUSHPULL = 3,   /* both, over the same Philox peers                           */
-  GOSSIP_MODE_ANTIENTROPY = 4 /* version-vector max-merge with churn (reserved, not yet built) */
+  GOSSIP_MODE_ANTIENTROPY = 4 /* version vectors, push-pull max-merge with churn */
 };
 
 enum gossip_status {
@@ -67,7 +67,8 @@ enum gossip_flags {
 
 typedef struct gossip_config {
   uint64_t n_nodes;     /* N: global node count, 2 <= N < 2^32                       */
-  uint32_t n_rumors;    /* R: rumor slots, bit r of word r/64 (W = ceil(R/64) words)  */
+  uint32_t n_rumors;    /* R: rumor slots, bit r of word r/64 (W = ceil(R/64) words);
+                           ANTIENTROPY: K version components per node (1..64)        */
   uint32_t mode;        /* enum gossip_mode                                           */
   uint32_t fanout;      /* k: Philox peers per node per round (random modes)          */
   uint32_t flags;       /* enum gossip_flags                                          */
@@ -75,7 +76,9 @@ typedef struct gossip_config {
   int32_t device;       /* HIP device ordinal, -1 = current device                    */
   uint32_t shard_rank;  /* this engine owns nodes [rank*Nl, min(N,(rank+1)*Nl))        */
   uint32_t shard_count; /* G >= 1, Nl = ceil(N/G)                                     */
-  uint32_t reserved[5]; /* must be zero                                               */
+  uint32_t churn_fail;    /* ANTIENTROPY: P(alive -> dead) per round, as x / 2^32      */
+  uint32_t churn_recover; /* ANTIENTROPY: P(dead -> alive) per round, as x / 2^32      */
+  uint32_t reserved[3]; /* must be zero                                               */
 } gossip_config_t;
 
 /* Stats of one round t: they describe S_{t+1}, the state the round produced. */
@@ -83,8 +86,9 @@ typedef struct gossip_round_stats {
   uint32_t round;       /* t                                                     */
   uint32_t converged;   /* full_nodes == alive_nodes                             */
   uint64_t full_nodes;  /* nodes holding all R rumors                            */
-  uint64_t alive_nodes; /* N (churn not enabled in these modes)                   */
-  uint64_t messages;    /* FLOOD: broadcast RPCs sent in round t */
+  uint64_t alive_nodes; /* N, or the alive count after round t's churn (ANTIENTROPY) */
+  uint64_t messages;    /* FLOOD: broadcast RPCs sent in round t;
+                           ANTIENTROPY: exchanges between two alive nodes           */
   uint64_t state_hash;  /* GOSSIP_FLAG_HASH: Σ mix64 over nonzero words, else 0   */
 } gossip_round_stats_t;
 
@@ -112,10 +116,12 @@ int gossip_set_topology_csr(gossip_engine_t* eng, const uint32_t* row_ptr, const
 int gossip_reset(gossip_engine_t* eng);
 
 /* Client broadcast of rumor slot `rumor` to `node` (no-op when the node is
- * outside this shard or already holds it — the dedupe of main.go:113). */
+ * outside this shard or already holds it — the dedupe of main.go:113).
+ * ANTIENTROPY: a local write of key `rumor` at `node` (its version + 1). */
 int gossip_inject(gossip_engine_t* eng, uint64_t node, uint32_t rumor);
 
-/* Injects every rumor r < R at origin(r) = Philox tag-2 draw. */
+/* Injects every rumor r < R at origin(r) = Philox tag-2 draw.
+ * ANTIENTROPY: initial versions V[n][c] = Philox tag-3 draw & 0xFFFF. */
 int gossip_inject_random(gossip_engine_t* eng);
 
 /* Runs rounds until converged or max_rounds rounds have run (single shard only,
@@ -139,6 +145,8 @@ int gossip_round_commit(gossip_engine_t* eng, const uint64_t* total, gossip_roun
  * or the whole owned shard in logical order out[w * Nl_owned + i]. */
 int gossip_read_bitset(gossip_engine_t* eng, uint64_t node, uint64_t* out, uint32_t nwords);
 int gossip_read_shard(gossip_engine_t* eng, uint64_t* out, uint64_t n_words);
+/* ANTIENTROPY readout: the K versions of one node, and its alive flag. */
+int gossip_read_versions(gossip_engine_t* eng, uint64_t node, uint32_t* out, uint32_t ncomp, uint32_t* alive);
 /* Owned node range [lo, hi). */
 int gossip_shard_range(const gossip_engine_t* eng, uint64_t* lo, uint64_t* hi);
 

@@ -37,6 +37,9 @@ struct oracle_sim {
   uint64_t E;
   int has_topo;
   uint32_t t;
+  /* ANTIENTROPY: V[n*K + c], alive bytes, global max vector */
+  uint32_t *V, *Vn, *target;
+  uint8_t *alive, *alive_n;
 };
 
 /* ---------------- Philox4x32-10 (Random123; rocRAND philox4x32_10.h:270-302) ---- */
@@ -95,10 +98,11 @@ int oracle_create(const gossip_config_t* cfg, int threads, oracle_sim_t** out) {
   *out = NULL;
   if (cfg->n_nodes < 2 || cfg->n_nodes >= (1ull << 32)) return GOSSIP_EINVAL;
   if (cfg->n_rumors == 0 || cfg->n_rumors > 4096) return GOSSIP_EINVAL;
-  if (cfg->mode > GOSSIP_MODE_PUSHPULL) return GOSSIP_ENOTSUP;
+  if (cfg->mode > GOSSIP_MODE_ANTIENTROPY) return GOSSIP_ENOTSUP;
   if (cfg->mode != GOSSIP_MODE_FLOOD && (cfg->fanout == 0 || cfg->fanout > 64)) return GOSSIP_EINVAL;
   uint32_t G = cfg->shard_count ? cfg->shard_count : 1;
   if (cfg->shard_rank >= G) return GOSSIP_EINVAL;
+  if (cfg->mode == GOSSIP_MODE_ANTIENTROPY && (G != 1 || cfg->n_rumors > 64)) return GOSSIP_ENOTSUP;
   oracle_sim_t* s = (oracle_sim_t*)calloc(1, sizeof(*s));
   if (!s) return GOSSIP_ENOMEM;
   s->cfg = *cfg;
@@ -125,6 +129,18 @@ int oracle_create(const gossip_config_t* cfg, int threads, oracle_sim_t** out) {
     s->Sprev = (uint64_t*)calloc(shard, 8);
     s->skip = (uint64_t*)calloc(shard, 8);
   }
+  if (s->mode == GOSSIP_MODE_ANTIENTROPY) {
+    s->V = (uint32_t*)calloc((size_t)s->N * s->R, 4);
+    s->Vn = (uint32_t*)calloc((size_t)s->N * s->R, 4);
+    s->target = (uint32_t*)calloc(s->R, 4);
+    s->alive = (uint8_t*)malloc(s->N);
+    s->alive_n = (uint8_t*)malloc(s->N);
+    if (!s->V || !s->Vn || !s->target || !s->alive || !s->alive_n) {
+      oracle_destroy(s);
+      return GOSSIP_ENOMEM;
+    }
+    memset(s->alive, 1, s->N);
+  }
   if (!s->S || !s->Snext || !s->send || (G > 1 && !s->recv) || !s->fullm ||
       (s->mode == GOSSIP_MODE_FLOOD && (!s->Sprev || !s->skip))) {
     oracle_destroy(s);
@@ -142,6 +158,7 @@ void oracle_destroy(oracle_sim_t* s) {
   if (!s) return;
   free(s->S); free(s->Snext); free(s->Sprev); free(s->skip); free(s->send); free(s->recv);
   free(s->fullm); free(s->orow); free(s->ocol); free(s->irow); free(s->icol);
+  free(s->V); free(s->Vn); free(s->target); free(s->alive); free(s->alive_n);
   free(s);
 }
 
@@ -206,6 +223,11 @@ int oracle_reset(oracle_sim_t* s) {
   memset(s->Snext, 0, shard);
   if (s->Sprev) memset(s->Sprev, 0, shard);
   if (s->skip) memset(s->skip, 0, shard);
+  if (s->V) {
+    memset(s->V, 0, (size_t)s->N * s->R * 4);
+    memset(s->target, 0, (size_t)s->R * 4);
+    memset(s->alive, 1, s->N);
+  }
   s->t = 0;
   return GOSSIP_OK;
 }
@@ -214,6 +236,12 @@ int oracle_reset(oracle_sim_t* s) {
  * the bit set.  Injected bits carry no sender in Adj, so skip stays 0 for them. */
 int oracle_inject(oracle_sim_t* s, uint64_t node, uint32_t rumor) {
   if (!s || node >= s->N || rumor >= s->R) return GOSSIP_EINVAL;
+  if (s->mode == GOSSIP_MODE_ANTIENTROPY) { /* a local write of key `rumor` */
+    uint32_t* x = &s->V[node * s->R + rumor];
+    *x += 1;
+    if (*x > s->target[rumor]) s->target[rumor] = *x;
+    return GOSSIP_OK;
+  }
   if (node < s->lo || node >= s->hi) return GOSSIP_OK;
   s->S[(size_t)(rumor >> 6) * s->Nl + (node - s->lo)] |= 1ull << (rumor & 63);
   return GOSSIP_OK;
@@ -221,6 +249,21 @@ int oracle_inject(oracle_sim_t* s, uint64_t node, uint32_t rumor) {
 
 int oracle_inject_random(oracle_sim_t* s) {
   if (!s) return GOSSIP_EINVAL;
+  if (s->mode == GOSSIP_MODE_ANTIENTROPY) { /* V[n][c] = Philox({n, c/4, 3, 0})[c%4] & 0xFFFF */
+    const uint32_t key[2] = {(uint32_t)s->cfg.seed, (uint32_t)(s->cfg.seed >> 32)};
+    memset(s->target, 0, (size_t)s->R * 4);
+    for (uint64_t n = 0; n < s->N; ++n)
+      for (uint32_t c = 0; c < s->R; c += 4) {
+        uint32_t ctr[4] = {(uint32_t)n, c >> 2, 3u, 0u}, x[4];
+        oracle_philox4x32_10(ctr, key, x);
+        for (uint32_t q = 0; q < 4 && c + q < s->R; ++q) {
+          uint32_t v = x[q] & 0xFFFFu;
+          s->V[n * s->R + c + q] = v;
+          if (v > s->target[c + q]) s->target[c + q] = v;
+        }
+      }
+    return GOSSIP_OK;
+  }
   for (uint32_t r = 0; r < s->R; ++r) oracle_inject(s, oracle_origin(s->cfg.seed, s->N, r), r);
   return GOSSIP_OK;
 }
@@ -230,6 +273,7 @@ uint64_t oracle_partial_len(const oracle_sim_t* s) { return 4 + (s ? s->R : 0); 
 /* Exchange payload: S_t for random modes, the frontier F_t = S_t & ~S_{t-1} for FLOOD. */
 int oracle_exchange_buffers(oracle_sim_t* s, void** send, void** recv, uint64_t* send_bytes) {
   if (!s) return GOSSIP_EINVAL;
+  if (s->mode == GOSSIP_MODE_ANTIENTROPY) return GOSSIP_OK; /* single shard: nothing to exchange */
   size_t shard = (size_t)s->W * s->Nl;
   if (s->mode == GOSSIP_MODE_FLOOD)
     for (size_t i = 0; i < shard; ++i) s->send[i] = s->S[i] & ~s->Sprev[i];
@@ -258,8 +302,66 @@ static int in_sorted(const uint32_t* a, uint32_t len, uint32_t x) {
 
 /* One round S_t -> S_{t+1} for the owned nodes (Gossip, main.go:65-89, as a
  * synchronous round).  g = gathered exchange image (S_t or F_t). */
+/* Churn (Philox tag 1): the alive flag of node n after round t's churn. */
+static inline int churned(int alive, uint32_t n, uint32_t t, const uint32_t key[2], uint32_t fail, uint32_t rec) {
+  uint32_t ctr[4] = {n, t, 1u, 0u}, x[4];
+  oracle_philox4x32_10(ctr, key, x);
+  return alive ? !(x[0] < fail) : (x[0] < rec);
+}
+
+/* Anti-entropy round: push-pull max-merge over alive-alive edges. */
+static int ae_round(oracle_sim_t* s, uint64_t* partial) {
+  const uint64_t N = s->N;
+  const uint32_t K = s->R, k = s->k, t = s->t;
+  const uint32_t key[2] = {(uint32_t)s->cfg.seed, (uint32_t)(s->cfg.seed >> 32)};
+  const uint32_t fail = s->cfg.churn_fail, rec = s->cfg.churn_recover;
+  for (uint64_t n = 0; n < N; ++n) s->alive_n[n] = (uint8_t)churned(s->alive[n], (uint32_t)n, t, key, fail, rec);
+  memcpy(s->Vn, s->V, (size_t)N * K * 4);
+  uint64_t msgs = 0;
+  for (uint64_t n = 0; n < N; ++n) {
+    if (!s->alive_n[n]) continue;
+    uint32_t x[4] = {0, 0, 0, 0};
+    for (uint32_t j = 0; j < k; ++j) {
+      if ((j & 3) == 0) {
+        uint32_t ctr[4] = {(uint32_t)n, t, 0u, j >> 2};
+        oracle_philox4x32_10(ctr, key, x);
+      }
+      uint32_t p = peer_from_word(x[j & 3], N, (uint32_t)n);
+      if (!s->alive_n[p]) continue;
+      ++msgs;
+      for (uint32_t c = 0; c < K; ++c) {
+        uint32_t a = s->V[n * K + c], b = s->V[(uint64_t)p * K + c];
+        if (b > s->Vn[n * K + c]) s->Vn[n * K + c] = b;                    /* pull */
+        if (a > s->Vn[(uint64_t)p * K + c]) s->Vn[(uint64_t)p * K + c] = a; /* push */
+      }
+    }
+  }
+  uint64_t full = 0, alive = 0, hash = 0;
+  uint64_t* inf = partial + 4;
+  memset(inf, 0, (size_t)K * 8);
+  for (uint64_t n = 0; n < N; ++n) {
+    int isfull = 1;
+    for (uint32_t c = 0; c < K; ++c) {
+      uint32_t v = s->Vn[n * K + c];
+      if (v && (s->cfg.flags & GOSSIP_FLAG_HASH)) hash += oracle_mix64((uint64_t)v + ((uint64_t)c * N + n) * GOLD64);
+      if (v != s->target[c]) isfull = 0;
+      else if (s->alive_n[n]) inf[c]++;
+    }
+    if (s->alive_n[n]) {
+      alive++;
+      full += isfull;
+    }
+  }
+  partial[0] = full;
+  partial[1] = alive;
+  partial[2] = msgs;
+  partial[3] = hash;
+  return GOSSIP_OK;
+}
+
 int oracle_round_compute(oracle_sim_t* s, uint64_t* partial) {
   if (!s || !partial) return GOSSIP_EINVAL;
+  if (s->mode == GOSSIP_MODE_ANTIENTROPY) return ae_round(s, partial);
   const uint64_t* g = s->G > 1 ? s->recv : s->send;
   const uint64_t N = s->N, Nl = s->Nl, lo = s->lo, nown = s->nown;
   const uint32_t W = s->W, k = s->k, t = s->t;
@@ -377,7 +479,10 @@ int oracle_round_compute(oracle_sim_t* s, uint64_t* partial) {
 int oracle_round_commit(oracle_sim_t* s, const uint64_t* total, gossip_round_stats_t* st) {
   if (!s || !total) return GOSSIP_EINVAL;
   uint64_t* tmp;
-  if (s->mode == GOSSIP_MODE_FLOOD) { /* S_{t-1} <- S_t <- S_{t+1} */
+  if (s->mode == GOSSIP_MODE_ANTIENTROPY) {
+    uint32_t* tv = s->V; s->V = s->Vn; s->Vn = tv;
+    uint8_t* ta = s->alive; s->alive = s->alive_n; s->alive_n = ta;
+  } else if (s->mode == GOSSIP_MODE_FLOOD) { /* S_{t-1} <- S_t <- S_{t+1} */
     tmp = s->Sprev; s->Sprev = s->S; s->S = s->Snext; s->Snext = tmp;
   } else {
     tmp = s->S; s->S = s->Snext; s->Snext = tmp;
@@ -441,12 +546,28 @@ int oracle_shard_range(const oracle_sim_t* s, uint64_t* lo, uint64_t* hi) {
 int oracle_state_hash(oracle_sim_t* s, uint64_t* out) {
   if (!s || !out) return GOSSIP_EINVAL;
   uint64_t h = 0;
+  if (s->mode == GOSSIP_MODE_ANTIENTROPY) {
+    for (uint64_t n = 0; n < s->N; ++n)
+      for (uint32_t c = 0; c < s->R; ++c) {
+        uint32_t v = s->V[n * s->R + c];
+        if (v) h += oracle_mix64((uint64_t)v + ((uint64_t)c * s->N + n) * GOLD64);
+      }
+    *out = h;
+    return GOSSIP_OK;
+  }
   for (uint32_t w = 0; w < s->W; ++w)
     for (uint64_t i = 0; i < s->nown; ++i) {
       uint64_t x = s->S[(size_t)w * s->Nl + i];
       if (x) h += oracle_mix64(x + ((uint64_t)w * s->N + s->lo + i) * GOLD64);
     }
   *out = h;
+  return GOSSIP_OK;
+}
+
+int oracle_read_versions(oracle_sim_t* s, uint64_t node, uint32_t* out, uint32_t ncomp, uint32_t* alive) {
+  if (!s || !out || !s->V || node >= s->N || ncomp < s->R) return GOSSIP_EINVAL;
+  memcpy(out, s->V + node * s->R, (size_t)s->R * 4);
+  if (alive) *alive = s->alive[node];
   return GOSSIP_OK;
 }
 

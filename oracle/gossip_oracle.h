@@ -54,6 +54,7 @@ int oracle_round_commit(oracle_sim_t* s, const uint64_t* total, gossip_round_sta
 
 int oracle_read_bitset(oracle_sim_t* s, uint64_t node, uint64_t* out, uint32_t nwords);
 int oracle_read_shard(oracle_sim_t* s, uint64_t* out, uint64_t n_words);
+int oracle_read_versions(oracle_sim_t* s, uint64_t node, uint32_t* out, uint32_t ncomp, uint32_t* alive);
 int oracle_shard_range(const oracle_sim_t* s, uint64_t* lo, uint64_t* hi);
 int oracle_state_hash(oracle_sim_t* s, uint64_t* out);
 uint32_t oracle_round_index(const oracle_sim_t* s);

@@ -190,3 +190,73 @@ class Sim:
             if st["converged"] or (self.mode == "flood" and st["messages"] == 0):
                 break
         return out
+
+
+class AntiEntropySim:
+    """Version-vector anti-entropy with churn, unsharded, vectorised.
+
+    V[n, c] uint32; alive[n] bool.  Round t: churn by Philox tag 1 (x0 < fail
+    kills an alive node, x0 < recover revives a dead one), then over every edge
+    (n, p_j(n, t)) with both ends alive, both ends take the elementwise max of
+    the two S_t vectors.  Stats: alive count, alive nodes equal to the global
+    max vector (constant between injections), per-component counts, hash.
+    """
+
+    def __init__(self, n_nodes, k_comp, fanout, seed, fail, recover):
+        self.N, self.K, self.k, self.seed, self.fail, self.rec = n_nodes, k_comp, fanout, seed, fail, recover
+        self.V = np.zeros((n_nodes, k_comp), dtype=np.uint32)
+        self.alive = np.ones(n_nodes, dtype=bool)
+        self.t = 0
+
+    def inject_random(self):
+        n = np.arange(self.N, dtype=np.uint32)
+        k0, k1 = self.seed & 0xFFFFFFFF, (self.seed >> 32) & 0xFFFFFFFF
+        for c0 in range(0, self.K, 4):
+            x = philox4x32_10(n, np.uint32(c0 // 4), np.uint32(3), np.uint32(0), k0, k1)
+            for q in range(4):
+                if c0 + q < self.K:
+                    self.V[:, c0 + q] = x[q] & np.uint32(0xFFFF)
+
+    def inject(self, node, comp):
+        self.V[node, comp] += np.uint32(1)
+
+    def round(self):
+        N = self.N
+        k0, k1 = self.seed & 0xFFFFFFFF, (self.seed >> 32) & 0xFFFFFFFF
+        n = np.arange(N, dtype=np.uint32)
+        x0 = philox4x32_10(n, np.uint32(self.t), np.uint32(1), np.uint32(0), k0, k1)[0]
+        alive = np.where(self.alive, ~(x0 < np.uint32(self.fail)), x0 < np.uint32(self.rec))
+        P = peers(self.seed, N, self.t, self.k).astype(np.int64)
+        V = self.V
+        Vn = V.copy()
+        msgs = 0
+        for j in range(self.k):
+            p = P[:, j]
+            e = alive & alive[p]
+            src = np.nonzero(e)[0]
+            dst = p[e]
+            msgs += int(src.size)
+            np.maximum.at(Vn, src, V[dst])  # pull
+            np.maximum.at(Vn, dst, V[src])  # push
+        self.V, self.alive = Vn, alive
+        target = V.max(axis=0) if N else V[0]
+        eq = Vn == target[None, :]
+        full = int((eq.all(axis=1) & alive).sum())
+        inf = [int(x) for x in (eq & alive[:, None]).sum(axis=0)]
+        idx = (np.arange(self.K, dtype=np.uint64)[None, :] * np.uint64(N) + np.arange(N, dtype=np.uint64)[:, None])
+        with np.errstate(over="ignore"):
+            h = mix64(Vn.astype(np.uint64) + idx * np.uint64(GOLD))
+        h = int(np.sum(np.where(Vn != 0, h, np.uint64(0)), dtype=np.uint64))
+        st = dict(round=self.t, full=full, alive=int(alive.sum()), converged=int(full == int(alive.sum())),
+                  messages=msgs, hash=h, infected=inf)
+        self.t += 1
+        return st
+
+    def run(self, max_rounds):
+        out = []
+        for _ in range(max_rounds):
+            st = self.round()
+            out.append(st)
+            if st["converged"]:
+                break
+        return out

@@ -53,6 +53,14 @@ FLOOD_CASES = [
 ]
 
 
+AE_CASES = [
+    # name, N, K, fanout, seed, fail, recover  (thresholds = probability * 2^32)
+    ("ae_cfg5_small", 4096, 16, 1, 0x5EED0005, int(0.01 * 2**32), int(0.1 * 2**32)),
+    ("ae_heavy_churn", 1000, 5, 2, 7, int(0.2 * 2**32), int(0.3 * 2**32)),
+    ("ae_no_churn_k64", 513, 64, 1, 3, 0, 0),
+]
+
+
 def run_case(sim, inj, max_rounds=256):
     if inj == "random":
         sim.inject_random()
@@ -64,7 +72,7 @@ def run_case(sim, inj, max_rounds=256):
 
 
 def main():
-    out = {"philox_kat": KAT, "peers": [], "origins": [], "random": [], "flood": []}
+    out = {"philox_kat": KAT, "peers": [], "origins": [], "random": [], "flood": [], "antientropy": []}
     for seed, N, t in [(0x5EED0001, 1 << 20, 0), (0x5EED0003, 1 << 24, 5), (7, 1000, 3), (0, 2, 0)]:
         nodes = sorted(set([i for i in range(16) if i < N] + [N - 1]))
         p = nr.peers(seed, N, t, 6, nodes=nodes)
@@ -84,6 +92,14 @@ def main():
         reads = {i: [r for r in range(R) if (int(sim.S[r // 64, i]) >> (r % 64)) & 1] for i in range(N)}
         out["flood"].append({"name": name, "N": N, "R": R, "adj": A, "inject": inj, "rounds": rounds,
                              "reads": reads})
+    for name, N, K, k, seed, fail, rec in AE_CASES:
+        sim = nr.AntiEntropySim(N, K, k, seed, fail, rec)
+        sim.inject_random()
+        sim.inject(N - 1, 0)  # a client write after the initial versions
+        rounds = sim.run(300)
+        out["antientropy"].append({"name": name, "N": N, "K": K, "k": k, "seed": seed, "fail": fail,
+                                   "recover": rec, "rounds": rounds,
+                                   "node0": [int(x) for x in sim.V[0]], "node0_alive": bool(sim.alive[0])})
     path = os.path.join(HERE, "golden.json")
     with open(path, "w") as f:
         json.dump(out, f, separators=(",", ":"))

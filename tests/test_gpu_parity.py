@@ -191,3 +191,51 @@ def test_two_shards_on_one_gpu(mode, k, R, N):
     full = ref.read_shard()
     for s in shards:
         assert np.array_equal(s.read_shard(), full[:, s.lo:s.hi])
+
+
+@pytest.mark.parametrize("idx", range(3))
+def test_antientropy_golden_gpu(golden, idx):
+    c = golden["antientropy"][idx]
+    e = Engine(c["N"], c["K"], "antientropy", c["k"], c["seed"], flags=1,
+               churn_fail=c["fail"], churn_recover=c["recover"])
+    e.inject_random()
+    e.inject(c["N"] - 1, 0)
+    res = e.step(300)
+    assert res.rounds == len(c["rounds"])
+    for got, inf, want in zip(res.stats, res.infected, c["rounds"]):
+        assert (got["full_nodes"], got["alive_nodes"], got["messages"], got["state_hash"], got["converged"]) == \
+            (want["full"], want["alive"], want["messages"], want["hash"], want["converged"])
+        assert [int(x) for x in inf] == want["infected"]
+    v, alive = e.read_versions(0)
+    assert [int(x) for x in v] == c["node0"] and alive == c["node0_alive"]
+
+
+def test_antientropy_vs_oracle_1M():
+    from gossip_hip.engine import churn_threshold as ct
+    N, K, k, seed = 1 << 20, 16, 1, 0x5EED0005
+    e = Engine(N, K, "antientropy", k, seed, flags=1, churn_fail=ct(0.01), churn_recover=ct(0.1))
+    o = op.OracleEngine(N, K, "antientropy", k, seed, flags=1, churn_fail=ct(0.01), churn_recover=ct(0.1))
+    for x in (e, o):
+        x.inject_random()
+    a, b = e.step(200), o.step(200)
+    assert a.stats == b.stats and np.array_equal(a.infected, b.infected)
+    assert a.converged
+    for node in (0, 1, N // 3, N - 1):
+        assert [int(x) for x in e.read_versions(node)[0]] == [int(x) for x in o.read_versions(node)[0]]
+
+
+def test_antientropy_cfg5_64M_properties():
+    """configs[4] at full size: 2^26 nodes, K=16, fanout 1, churn 1% / 10%."""
+    from gossip_hip.engine import churn_threshold as ct
+    N = 1 << 26
+    e = Engine(N, 16, "antientropy", 1, 0x5EED0005, churn_fail=ct(0.01), churn_recover=ct(0.1))
+    e.inject_random()
+    res = e.step(400)
+    # convergence waits for the stale nodes that died before the versions reached
+    # them: they revive at 10% per round, so ~log(0.6M)/log(1/0.9) ~ 126 rounds
+    assert res.converged and res.rounds < 300
+    inf = res.infected.astype(np.int64)
+    alive = np.array([s["alive_nodes"] for s in res.stats])
+    assert (inf <= alive[:, None]).all()
+    # steady-state alive fraction of the churn chain is 0.1 / 0.11
+    assert 0.85 * N < alive[-1] <= N

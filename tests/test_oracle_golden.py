@@ -64,3 +64,20 @@ def test_openmp_matches_scalar():
         ra, rb = a.step(100), b.step(100)
         assert ra.stats == rb.stats
         assert np.array_equal(ra.infected, rb.infected)
+
+
+@pytest.mark.parametrize("idx", range(3))
+def test_antientropy_golden(golden, idx):
+    c = golden["antientropy"][idx]
+    e = op.OracleEngine(c["N"], c["K"], "antientropy", c["k"], c["seed"], flags=1,
+                        churn_fail=c["fail"], churn_recover=c["recover"])
+    e.inject_random()
+    e.inject(c["N"] - 1, 0)
+    res = e.step(300)
+    assert res.rounds == len(c["rounds"])
+    for got, inf, want in zip(res.stats, res.infected, c["rounds"]):
+        assert (got["full_nodes"], got["alive_nodes"], got["messages"], got["state_hash"], got["converged"]) == \
+            (want["full"], want["alive"], want["messages"], want["hash"], want["converged"])
+        assert [int(x) for x in inf] == want["infected"]
+    v, alive = e.read_versions(0)
+    assert [int(x) for x in v] == c["node0"] and alive == c["node0_alive"]
