@@ -34,6 +34,8 @@ struct BinBufs {
   uint64_t* resp;   // [nt_s][rp]   pull response S_t[p] & ~S_t[n]
   uint16_t* off;    // [nt_s][nt_d + 1] run starts inside each sender region
   uint16_t* offT;   // [nt_d + 1][nt_s]
+  uint64_t* nzb;    // occupancy bitmaps of S_{t+1} written by K3 (frontier.h), or null
+  uint64_t* fullb;
 };
 
 size_t bin_bytes(const BinGeom& g);

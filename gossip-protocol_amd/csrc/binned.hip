@@ -246,12 +246,13 @@ __device__ __forceinline__ uint64_t transpose64(uint64_t x, uint32_t lane) {
 __device__ __forceinline__ void tile_epilogue(const unsigned long long* acc, uint64_t node0, uint64_t N,
                                               uint64_t* __restrict__ Snext, uint64_t* __restrict__ partial,
                                               uint32_t R, uint32_t flags, uint32_t* cnt, uint64_t* red_hash,
-                                              uint32_t* red_full) {
+                                              uint32_t* red_full, uint32_t* red_nz, uint64_t* __restrict__ nzb,
+                                              uint64_t* __restrict__ fullb) {
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint64_t fm = full_mask1(R);
   const bool do_hash = (flags & 1u) != 0;
   uint64_t hash = 0;
-  uint32_t full = 0, c_lane = 0;
+  uint32_t full = 0, nzc = 0, c_lane = 0;
   for (uint32_t q = 0; q < kTileD / kTileThreads; ++q) {
     const uint32_t i = q * kTileThreads + tid;
     const uint64_t n = node0 + i;
@@ -259,8 +260,15 @@ __device__ __forceinline__ void tile_epilogue(const unsigned long long* acc, uin
     const uint64_t x = valid ? (uint64_t)acc[i] : 0ull;
     if (valid) Snext[n] = x;
     if (do_hash && x) hash += mix64(x + n * kGold64);
-    full += (uint32_t)__popcll(__ballot(valid && x == fm));
+    const uint64_t fw = __ballot(valid && x == fm);
     const uint64_t nz = __ballot(x != 0);
+    full += (uint32_t)__popcll(fw);
+    nzc += (uint32_t)__popcll(nz);
+    // a wave holds 64 consecutive nodes: one word of each occupancy bitmap
+    if (nzb && lane == 0 && (n - lane) < N) {
+      nzb[n >> 6] = nz;
+      fullb[n >> 6] = fw;
+    }
     if (nz == 0) continue;
     const uint64_t fl = __ballot(x == fm);
     if (fl == nz) {
@@ -274,16 +282,19 @@ __device__ __forceinline__ void tile_epilogue(const unsigned long long* acc, uin
   if (lane == 0) {
     red_hash[wave] = hash;
     red_full[wave] = full;
+    red_nz[wave] = nzc;
   }
   __syncthreads();
   if (tid == 0) {
-    uint64_t h = 0, f = 0;
+    uint64_t h = 0, f = 0, z = 0;
     for (int w = 0; w < kTileThreads / 64; ++w) {
       h += red_hash[w];
       f += red_full[w];
+      z += red_nz[w];
     }
     if (f) atomicAdd((unsigned long long*)&partial[0], (unsigned long long)f);
     if (h) atomicAdd((unsigned long long*)&partial[3], (unsigned long long)h);
+    if (z) atomicAdd((unsigned long long*)&partial[4 + R], (unsigned long long)z);  // nonzero nodes
   }
   if (tid < R && cnt[tid]) atomicAdd((unsigned long long*)&partial[4 + tid], (unsigned long long)cnt[tid]);
 }
@@ -393,6 +404,7 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, cons
   __shared__ uint32_t cnt[64];
   __shared__ uint64_t red_hash[kTileThreads / 64];
   __shared__ uint32_t red_full[kTileThreads / 64];
+  __shared__ uint32_t red_nz[kTileThreads / 64];
   const uint32_t tid = threadIdx.x;
   const uint32_t X = xcd_remap(blockIdx.x, g.nt_d);
   const uint64_t node0 = (uint64_t)X << kTileDLog;
@@ -459,7 +471,7 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, cons
     }
   }
   __syncthreads();
-  tile_epilogue(acc, node0, g.N, Snext, partial, R, flags, cnt, red_hash, red_full);
+  tile_epilogue(acc, node0, g.N, Snext, partial, R, flags, cnt, red_hash, red_full, red_nz, b.nzb, b.fullb);
 }
 
 }  // namespace

@@ -17,6 +17,7 @@
 #include "../../include/gossip.h"
 #include "antientropy.h"
 #include "binned.h"
+#include "frontier.h"
 #include "kernels.h"
 #include "philox.h"
 
@@ -66,6 +67,15 @@ struct gossip_engine {
   BinGeom bg{};
   BinBufs bb{};
   void* bin_mem = nullptr;
+  // frontier (sparse-round) path, on top of the binned one
+  bool frontier = false;
+  FrontierBufs fb{};
+  void* fr_mem = nullptr;
+  bool fr_valid = false;          // partial_d holds the totals of S and the bitmaps are exact
+  bool inplace = false;           // the last computed round updated S in place (no buffer flip)
+  double sparse_frac = 1.0 / 16;  // rare fraction at or below which a round runs sparse
+  std::vector<uint64_t> tot;      // host copy of the totals of S [5 + R]
+  uint64_t sparse_rounds = 0;
 
   hipEvent_t ev[kTimers][2] = {};
   double time_ms[kTimers] = {0, 0};
@@ -97,6 +107,9 @@ int set_dev(gossip_engine* e) {
   return GOSSIP_OK;
 }
 
+// stats vector: [0] full [1] alive [2] messages [3] hash [4, 4+R) infected, [4+R] nonzero nodes (internal)
+size_t part_len(const gossip_engine* e) { return 5 + (size_t)e->R; }
+
 void free_all(gossip_engine* e) {
   uint64_t* bufs[] = {e->img[0], e->img[1], e->imgF, e->partial_d, e->scratch_d};
   if (e->mode == GOSSIP_MODE_FLOOD) {
@@ -110,6 +123,7 @@ void free_all(gossip_engine* e) {
   for (uint32_t* b : tb)
     if (b) (void)hipFree(b);
   if (e->bin_mem) (void)hipFree(e->bin_mem);
+  if (e->fr_mem) (void)hipFree(e->fr_mem);
   void* ae[] = {e->V, e->Vn, e->target, e->alive, e->alive_n};
   for (void* b : ae)
     if (b) (void)hipFree(b);
@@ -229,7 +243,7 @@ AeArgs make_ae_args(gossip_engine* e) {
 // compute S_{t+1} of the owned shard from the gathered image + partial stats (device)
 int compute_round(gossip_engine* e, const uint64_t* gathered) {
   const size_t bytes = (size_t)e->W * e->Nl * 8;
-  HIP_OK(e, hipMemsetAsync(e->partial_d, 0, (4 + e->R) * 8, e->stream));
+  if (!e->binned) HIP_OK(e, hipMemsetAsync(e->partial_d, 0, part_len(e) * 8, e->stream));
   if (e->mode == GOSSIP_MODE_ANTIENTROPY) {
     int rc;
     const AeArgs a = make_ae_args(e);
@@ -249,6 +263,28 @@ int compute_round(gossip_engine* e, const uint64_t* gathered) {
     if ((rc = timer_end(e, 0))) return rc;
   } else if (e->binned) {
     if ((rc = timer_begin(e, 0))) return rc;
+    e->inplace = false;
+    if (e->frontier) {
+      if (!e->fr_valid) {  // after reset/inject: totals and bitmaps of S from scratch
+        HIP_OK(e, hipMemsetAsync(e->partial_d, 0, part_len(e) * 8, e->stream));
+        HIP_OK(e, launch_frontier_rebuild(e->fb, e->S, e->N, e->partial_d, e->R, e->cfg.flags, e->stream));
+        HIP_OK(e, hipMemcpyAsync(e->partial_h, e->partial_d, part_len(e) * 8, hipMemcpyDeviceToHost, e->stream));
+        HIP_OK(e, hipStreamSynchronize(e->stream));
+        e->tot.assign(e->partial_h, e->partial_h + part_len(e));
+        e->fr_valid = true;
+      }
+      const uint64_t nz = e->tot[4 + e->R], full = e->tot[0];
+      const uint64_t rare_lo = nz, rare_hi = e->N - full, lim = (uint64_t)(e->sparse_frac * (double)e->N);
+      if (std::min(rare_lo, rare_hi) <= lim) {
+        // partial_d already holds the totals of S_t: the round adds its deltas
+        HIP_OK(e, launch_frontier_round(e->fb, e->S, e->N, e->partial_d, e->R, e->k, e->t, e->key0, e->key1, e->mode,
+                                        rare_hi < rare_lo ? 1u : 0u, e->cfg.flags, e->stream));
+        e->inplace = true;
+        e->sparse_rounds++;
+        return timer_end(e, 0);
+      }
+    }
+    HIP_OK(e, hipMemsetAsync(e->partial_d, 0, part_len(e) * 8, e->stream));
     HIP_OK(e, launch_binned_round(e->bg, e->bb, gathered, e->Snext, e->partial_d, e->R, e->t, e->key0, e->key1,
                                   e->mode, e->cfg.flags, e->stream, nullptr));
     if ((rc = timer_end(e, 0))) return rc;
@@ -275,7 +311,7 @@ void rotate(gossip_engine* e) {
     e->Sprev = e->S;
     e->S = e->Snext;
     e->Snext = tmp;
-  } else {
+  } else if (!e->inplace) {
     e->cur ^= 1;
     bind_slices(e);
   }
@@ -397,7 +433,7 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
     }
     return hipMemset(*p, 0, bytes) == hipSuccess;
   };
-  if (!alloc(&e->partial_d, (4 + e->R) * 8) || !alloc(&e->scratch_d, 8)) return bail(GOSSIP_ENOMEM);
+  if (!alloc(&e->partial_d, part_len(e) * 8) || !alloc(&e->scratch_d, 8)) return bail(GOSSIP_ENOMEM);
   auto alloc_raw = [&](void** p, size_t bytes) {
     if (hipMalloc(p, bytes) != hipSuccess) {
       e->err = "hipMalloc of " + std::to_string(bytes) + " bytes failed";
@@ -429,8 +465,17 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
     }
     bin_carve(e->bg, e->bin_mem, &e->bb);
     e->binned = true;
+    if (!(cfg->flags & GOSSIP_FLAG_DENSE)) {
+      const size_t fbytes = frontier_bytes(e->N);
+      if (!alloc_raw(&e->fr_mem, fbytes)) return bail(GOSSIP_ENOMEM);
+      frontier_carve(e->N, e->fr_mem, &e->fb);
+      e->bb.nzb = e->fb.nzb;
+      e->bb.fullb = e->fb.fullb;
+      e->frontier = true;
+      if (const char* f = getenv("GOSSIP_SPARSE_FRAC")) e->sparse_frac = atof(f);
+    }
   }
-  if (hipHostMalloc((void**)&e->partial_h, (4 + e->R) * 8, hipHostMallocDefault) != hipSuccess) {
+  if (hipHostMalloc((void**)&e->partial_h, part_len(e) * 8, hipHostMallocDefault) != hipSuccess) {
     e->err = "hipHostMalloc failed";
     return bail(GOSSIP_ENOMEM);
   }
@@ -532,6 +577,7 @@ int gossip_reset(gossip_engine_t* e) {
     HIP_OK(e, hipMemsetAsync(e->img[0], 0, shard * e->G, e->stream));
     HIP_OK(e, hipMemsetAsync(e->img[1], 0, shard * e->G, e->stream));
   }
+  e->fr_valid = false;
   e->t = 0;
   return GOSSIP_OK;
 }
@@ -546,6 +592,7 @@ int gossip_inject(gossip_engine_t* e, uint64_t node, uint32_t rumor) {
     return GOSSIP_OK;
   }
   HIP_OK(e, launch_inject(e->S, e->Nl, e->lo, e->hi, e->N, e->R, e->key0, e->key1, (int64_t)node, rumor, e->stream));
+  e->fr_valid = false;
   return GOSSIP_OK;
 }
 
@@ -557,6 +604,7 @@ int gossip_inject_random(gossip_engine_t* e) {
     return GOSSIP_OK;
   }
   HIP_OK(e, launch_inject(e->S, e->Nl, e->lo, e->hi, e->N, e->R, e->key0, e->key1, -1, 0, e->stream));
+  e->fr_valid = false;
   return GOSSIP_OK;
 }
 
@@ -581,9 +629,10 @@ int gossip_round_compute(gossip_engine_t* e, uint64_t* partial) {
   if (e->mode == GOSSIP_MODE_FLOOD && !e->has_topo) return e->fail(GOSSIP_ESTATE, "FLOOD needs a topology");
   if (int rc = set_dev(e)) return rc;
   if (int rc = compute_round(e, current_image(e))) return rc;
-  HIP_OK(e, hipMemcpyAsync(e->partial_h, e->partial_d, (4 + e->R) * 8, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(e, hipMemcpyAsync(e->partial_h, e->partial_d, part_len(e) * 8, hipMemcpyDeviceToHost, e->stream));
   HIP_OK(e, hipStreamSynchronize(e->stream));
   if (int rc = timer_collect(e)) return rc;
+  if (e->frontier) e->tot.assign(e->partial_h, e->partial_h + part_len(e));
   std::memcpy(partial, e->partial_h, (4 + e->R) * 8);
   if (e->mode != GOSSIP_MODE_ANTIENTROPY) partial[1] = e->nown;
   return GOSSIP_OK;
@@ -673,9 +722,9 @@ int gossip_state_hash(gossip_engine_t* e, uint64_t* out) {
   if (e->mode == GOSSIP_MODE_ANTIENTROPY) {  // the stats kernel's hash of the current rows
     AeArgs a = make_ae_args(e);
     a.flags |= GOSSIP_FLAG_HASH;
-    HIP_OK(e, hipMemsetAsync(e->partial_d, 0, (4 + e->R) * 8, e->stream));
+    HIP_OK(e, hipMemsetAsync(e->partial_d, 0, part_len(e) * 8, e->stream));
     HIP_OK(e, launch_ae_stats(a, e->V, e->alive, e->stream));
-    HIP_OK(e, hipMemcpyAsync(e->partial_h, e->partial_d, (4 + e->R) * 8, hipMemcpyDeviceToHost, e->stream));
+    HIP_OK(e, hipMemcpyAsync(e->partial_h, e->partial_d, part_len(e) * 8, hipMemcpyDeviceToHost, e->stream));
     HIP_OK(e, hipStreamSynchronize(e->stream));
     *out = e->partial_h[3];
     return GOSSIP_OK;

@@ -1,0 +1,42 @@
+// frontier.h — sparse rounds of the random modes (W == 1, one shard).
+//
+// When almost every node is in one class — all-zero early in a run, all-full
+// late in it — an edge between two majority nodes moves nothing, so a round
+// only has to find the edges that touch a "rare" node.  Two occupancy bitmaps
+// (nonzero, full) are kept exact by every round; a coarse summary of the rare
+// set sits in LDS so that the peer test of an edge almost never leaves the CU.
+// Deltas are OR-ed into D (zero between rounds) and committed in place.
+// DESIGN.md §3.3 has the rules and the byte accounting.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gossip {
+
+constexpr uint32_t kSummBits = 1u << 20;  // LDS summary: at most 2^20 bits (128 KiB)
+
+struct FrontierBufs {
+  uint64_t* nzb;    // [ceil(N/64)] bit n: S[n] != 0
+  uint64_t* fullb;  // [ceil(N/64)] bit n: S[n] == full mask
+  uint32_t* summ;   // [summ_words] bit b: some rare node in [b*g, (b+1)*g)
+  uint64_t* D;      // [N] pending deltas, zero outside a sparse round
+  uint32_t glog;    // g = 1 << glog nodes per summary bit
+  uint32_t summ_words;
+};
+
+uint32_t frontier_glog(uint64_t N);
+size_t frontier_bytes(uint64_t N);
+void frontier_carve(uint64_t N, void* base, FrontierBufs* f);
+
+// Absolute stats of S into partial (zeroed by the caller) + both bitmaps.
+hipError_t launch_frontier_rebuild(const FrontierBufs& f, const uint64_t* S, uint64_t N, uint64_t* partial,
+                                   uint32_t R, uint32_t flags, hipStream_t st);
+
+// One sparse round, in place on S.  maj = 0: rare = nonzero nodes; maj = 1:
+// rare = nodes not yet full.  partial holds the totals of S_t on entry and
+// those of S_{t+1} on exit.
+hipError_t launch_frontier_round(const FrontierBufs& f, uint64_t* S, uint64_t N, uint64_t* partial, uint32_t R,
+                                 uint32_t k, uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t maj,
+                                 uint32_t flags, hipStream_t st);
+
+}  // namespace gossip

@@ -4,13 +4,13 @@ The compute path is libgossip_hip.so (hand-written HIP kernels for gfx950);
 this package only binds it (ctypes) and orchestrates sharded rounds over
 torch.distributed.  See DESIGN.md.
 """
-from ._abi import (FLAG_DIRECT, FLAG_HASH, FLAG_TIMING, MODE_FLOOD, MODE_PULL, MODE_PUSH, MODE_PUSHPULL, MODES,
+from ._abi import (FLAG_DENSE, FLAG_DIRECT, FLAG_HASH, FLAG_TIMING, MODE_FLOOD, MODE_PULL, MODE_PUSH, MODE_PUSHPULL, MODES,
                    Config, RoundStats)
 from .engine import AbiEngine, Engine, GossipError, LIB_PATH, StepResult, load_library, make_config, peer
 from .maelstrom import Cluster, grid_topology, line_topology, total_topology, tree_topology
 
 __all__ = [
     "AbiEngine", "Engine", "GossipError", "StepResult", "Config", "RoundStats", "MODES", "MODE_FLOOD",
-    "MODE_PUSH", "MODE_PULL", "MODE_PUSHPULL", "FLAG_DIRECT", "FLAG_HASH", "FLAG_TIMING", "LIB_PATH", "load_library",
+    "MODE_PUSH", "MODE_PULL", "MODE_PUSHPULL", "FLAG_DENSE", "FLAG_DIRECT", "FLAG_HASH", "FLAG_TIMING", "LIB_PATH", "load_library",
     "make_config", "peer", "Cluster", "grid_topology", "line_topology", "total_topology", "tree_topology",
 ]

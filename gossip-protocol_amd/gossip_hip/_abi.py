@@ -13,6 +13,7 @@ MODES = {"flood": MODE_FLOOD, "push": MODE_PUSH, "pull": MODE_PULL,
 FLAG_HASH = 1 << 0
 FLAG_TIMING = 1 << 1
 FLAG_DIRECT = 1 << 2
+FLAG_DENSE = 1 << 3
 
 STATUS = {0: "OK", -1: "EINVAL", -2: "EHIP", -3: "ENOMEM", -4: "ESTATE", -5: "ENODEV", -6: "ENOTSUP"}
 

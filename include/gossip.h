@@ -61,8 +61,10 @@ enum gossip_status {
 enum gossip_flags {
   GOSSIP_FLAG_HASH = 1u << 0,   /* compute the per-round state hash */
   GOSSIP_FLAG_TIMING = 1u << 1, /* bracket hot kernels with hipEvents (gossip_kernel_time) */
-  GOSSIP_FLAG_DIRECT = 1u << 2  /* random modes: direct random-access kernels instead of the
+  GOSSIP_FLAG_DIRECT = 1u << 2, /* random modes: direct random-access kernels instead of the
                                    binned (LDS) pipeline — same results, for A/B checks */
+  GOSSIP_FLAG_DENSE = 1u << 3   /* random modes: every round on the dense binned pipeline, no
+                                   sparse (frontier) rounds — same results, for A/B checks */
 };
 
 typedef struct gossip_config {

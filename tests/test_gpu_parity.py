@@ -8,7 +8,7 @@ import torch
 
 import oracle_py as op
 from conftest import inject_case
-from gossip_hip import FLAG_DIRECT, Cluster, Engine, grid_topology
+from gossip_hip import FLAG_DENSE, FLAG_DIRECT, Cluster, Engine, grid_topology
 from gossip_hip.engine import GossipError
 
 pytestmark = pytest.mark.gpu
@@ -29,10 +29,26 @@ def test_device_philox_kat(golden):
         assert [int(x) for x in out[i]] == op.philox([int(x) for x in c[i]], [0x5EED0003, 0])
 
 
-PATHS = [0, FLAG_DIRECT]  # binned LDS pipeline (default) and the direct random-access kernels
+# round paths of the random modes, all bit-identical:
+#   auto   — default: sparse frontier rounds while one class dominates, dense binned rounds otherwise
+#   dense  — every round on the binned LDS pipeline
+#   sparse — every round on the frontier kernels (GOSSIP_SPARSE_FRAC=1 lifts the sparsity test)
+#   direct — the random-access kernels
+PATHS = ["auto", "dense", "sparse", "direct"]
+_PATH_FLAGS = {"auto": 0, "dense": FLAG_DENSE, "sparse": 0, "direct": FLAG_DIRECT}
 
 
-@pytest.mark.parametrize("path", PATHS, ids=["binned", "direct"])
+@pytest.fixture
+def path(request, monkeypatch):
+    name = request.param
+    if name == "sparse":
+        monkeypatch.setenv("GOSSIP_SPARSE_FRAC", "1.0")
+    else:
+        monkeypatch.delenv("GOSSIP_SPARSE_FRAC", raising=False)
+    return _PATH_FLAGS[name]
+
+
+@pytest.mark.parametrize("path", PATHS, indirect=True)
 @pytest.mark.parametrize("idx", range(8))
 def test_random_golden(golden, idx, path):
     c = golden["random"][idx]
@@ -59,27 +75,42 @@ def test_flood_golden(golden, idx):
         assert e.read(int(node)) == want
 
 
+_ORACLE_CACHE = {}
+
+
+def _oracle_run(cfg, inj, rounds, threads):
+    """Oracle result for cfg, computed once per session and shared by every path."""
+    key = (cfg, str(inj), rounds)
+    if key not in _ORACLE_CACHE:
+        N, R, mode, k, seed = cfg
+        o = op.OracleEngine(N, R, mode, k, seed, flags=1, threads=threads)
+        inject_case(o, inj)
+        ro = o.step(rounds)
+        _ORACLE_CACHE.clear()  # keep one state image alive at a time
+        _ORACLE_CACHE[key] = (ro, o.read_shard())
+    return _ORACLE_CACHE[key]
+
+
 def _compare(cfg, inj="random", rounds=256, threads=THREADS, path=0):
     N, R, mode, k, seed = cfg
     e = Engine(N, R, mode, k, seed, flags=1 | path)
-    o = op.OracleEngine(N, R, mode, k, seed, flags=1, threads=threads)
     inject_case(e, inj)
-    inject_case(o, inj)
-    re_, ro = e.step(rounds), o.step(rounds)
+    re_ = e.step(rounds)
+    ro, oshard = _oracle_run(cfg, inj, rounds, threads)
     assert re_.stats == ro.stats
     assert np.array_equal(re_.infected, ro.infected)
-    assert np.array_equal(e.read_shard(), o.read_shard())
+    assert np.array_equal(e.read_shard(), oshard)
     return re_
 
 
-@pytest.mark.parametrize("path", PATHS, ids=["binned", "direct"])
+@pytest.mark.parametrize("path", PATHS, indirect=True)
 def test_cfg2_push_1M_k3(path):
     """configs[1]: 1M nodes, push fanout 3, one rumor, seed 0x5EED0001."""
     res = _compare((1 << 20, 1, "push", 3, 0x5EED0001), [(0, 0)], path=path)
     assert res.converged and 12 <= res.rounds <= 20
 
 
-@pytest.mark.parametrize("path", PATHS, ids=["binned", "direct"])
+@pytest.mark.parametrize("path", PATHS, indirect=True)
 def test_pull_and_multiword(path):
     _compare((1 << 18, 1, "pull", 2, 0x5EED0002), [(123, 0)], path=path)
     _compare((100003, 130, "pushpull", 3, 77), path=path)
@@ -88,7 +119,7 @@ def test_pull_and_multiword(path):
     _compare((40000, 64, "pull", 9, 0xC0FFEE), path=path)      # fanout > 8: small sender tiles
 
 
-@pytest.mark.parametrize("path", PATHS, ids=["binned", "direct"])
+@pytest.mark.parametrize("path", PATHS, indirect=True)
 def test_cfg3_pushpull_16M_r64(path):
     """configs[2]: 16M nodes, push-pull fanout 2, 64 rumors at Philox origins."""
     res = _compare((1 << 24, 64, "pushpull", 2, 0x5EED0003), path=path)
@@ -97,7 +128,7 @@ def test_cfg3_pushpull_16M_r64(path):
     assert (np.diff(inf, axis=0) >= 0).all() and (inf[-1] == 1 << 24).all()
 
 
-@pytest.mark.parametrize("path", PATHS, ids=["binned", "direct"])
+@pytest.mark.parametrize("path", PATHS, indirect=True)
 def test_tiny_and_edge_sizes(path):
     _compare((2, 1, "pushpull", 2, 1), [(1, 0)], path=path)
     _compare((3, 64, "push", 4, 9), path=path)
@@ -107,6 +138,27 @@ def test_tiny_and_edge_sizes(path):
     e = Engine(5000, 1, "pushpull", 2, 1)
     res = e.step(5)
     assert res.rounds == 5 and not res.converged and res.infected.sum() == 0
+
+
+@pytest.mark.parametrize("path", PATHS, indirect=True)
+def test_inject_between_steps(path):
+    """A client broadcast between rounds (main.go:102-117) invalidates the
+    engine's running totals and occupancy bitmaps; the next round rebuilds them."""
+    cfg = (200003, 11, "pushpull", 2, 0x5EED0007)
+    e = Engine(*cfg, flags=1 | path)
+    o = op.OracleEngine(*cfg, flags=1, threads=THREADS)
+    for x in (e, o):
+        x.inject(5, 0)
+        x.inject(77777, 10)
+    for burst in ([(123, 1), (5, 2)], [(200002, 3), (9, 4)], [(0, 5), (1, 6), (2, 7), (3, 8), (4, 9)]):
+        a, b = e.step(3), o.step(3)
+        assert a.stats == b.stats and np.array_equal(a.infected, b.infected)
+        for x in (e, o):
+            for n, r in burst:
+                x.inject(n, r)
+    a, b = e.step(200), o.step(200)
+    assert a.stats == b.stats and a.converged
+    assert np.array_equal(e.read_shard(), o.read_shard())
 
 
 def test_reset_and_rerun_identical():

@@ -1,22 +1,48 @@
-"""Per-round kernel durations of the last dissemination step in a rocprofv3 kernel trace."""
+"""Per-round kernel durations of the last dissemination step in a rocprofv3 kernel trace.
+
+A round starts at bin_emit (dense binned round) or frontier_summary (sparse
+frontier round); a frontier rebuild (after inject) is counted with the round
+that follows it.
+"""
 import csv
 import sys
 
 path = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof/run_kernel_trace.csv"
-names = ("bin_emit_kernel", "transpose_u16_kernel", "bin_serve_kernel", "bin_apply_kernel")
+SHORT = {"bin_emit_kernel": "emit", "transpose_u16_kernel": "u16", "bin_serve_kernel": "serve",
+         "bin_apply_kernel": "apply", "frontier_summary_kernel": "summ", "frontier_scan_kernel": "scan",
+         "frontier_commit_kernel<true>": "rebuild", "frontier_commit_kernel<false>": "commit"}
+STARTS = ("emit", "summ", "rebuild")
+
+
+def short(name):
+    base = name.replace("(anonymous namespace)::", "").split("(")[0]
+    base = base.split("::")[-1]
+    if base.startswith("frontier_commit_kernel"):
+        return SHORT["frontier_commit_kernel<true>" if "<true>" in base else "frontier_commit_kernel<false>"]
+    return SHORT.get(base.split("<")[0])
+
+
 rows = list(csv.DictReader(open(path)))
-seq = sorted((int(r["Start_Timestamp"]),
-              r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].split("::")[-1].split("<")[0],
+seq = sorted((int(r["Start_Timestamp"]), short(r["Kernel_Name"]),
               (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000) for r in rows)
-ks = [x for x in seq if x[1] in names]
-starts = [i for i, x in enumerate(ks) if x[1] == names[0]]
-rounds = [ks[a:b] for a, b in zip(starts, starts[1:] + [len(ks)])]
-# last step = trailing rounds after the largest gap between consecutive emits
-gaps = [(rounds[i + 1][0][0] - rounds[i][-1][0], i) for i in range(len(rounds) - 1)]
-cut = max(gaps)[1] + 1 if gaps else 0
+ks = [x for x in seq if x[1]]
+rounds, cur = [], []
+for x in ks:
+    if x[1] in STARTS and cur and not (cur[-1][1] == "rebuild"):
+        rounds.append(cur)
+        cur = []
+    cur.append(x)
+if cur:
+    rounds.append(cur)
+# last step = trailing rounds after the last rebuild (one per step, after inject)
+cut = max((i for i, r in enumerate(rounds) if r[0][1] == "rebuild"), default=0)
+if cut == 0 and len(rounds) > 1:
+    gaps = [(rounds[i + 1][0][0] - rounds[i][-1][0], i) for i in range(len(rounds) - 1)]
+    cut = max(gaps)[1] + 1
 tot = 0
 for r in rounds[cut:]:
     t = sum(d for _, _, d in r)
     tot += t
-    print(" ".join(f"{n.split('_')[1][:6]}:{d:6.1f}" for _, n, d in r), f" round {t:6.1f} us")
+    kind = "sparse" if any(n == "scan" for _, n, _ in r) else "dense "
+    print(kind, " ".join(f"{n}:{d:6.1f}" for _, n, d in r), f" round {t:6.1f} us")
 print(f"rounds {len(rounds) - cut}, kernel time {tot / 1000:.2f} ms")
