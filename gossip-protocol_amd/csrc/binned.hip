@@ -26,6 +26,8 @@
 #include "binned.h"
 #include "philox.h"
 
+#include <cstdlib>
+
 namespace gossip {
 
 namespace {
@@ -39,7 +41,6 @@ constexpr int kUnrollSeq = 8;  // records in flight per lane in the sequential r
 // id each round, so a flag never outlives its round.
 constexpr uint32_t kIdVZ = 1u << 27;  // sender value is 0: no value stored
 constexpr uint32_t kIdVF = 1u << 28;  // sender value is the full mask: no value stored
-constexpr uint32_t kIdRV = 1u << 29;  // K2 stored a nonzero pull response
 constexpr uint32_t kIdNMask = (1u << 13) - 1u;
 
 __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {
@@ -299,24 +300,31 @@ __device__ __forceinline__ void tile_epilogue(const unsigned long long* acc, uin
   if (tid < R && cnt[tid]) atomicAdd((unsigned long long*)&partial[4 + tid], (unsigned long long)cnt[tid]);
 }
 
-// value of a record: implied by its flag, else loaded (from a clamped index so
-// that no load sits behind a branch)
-__device__ __forceinline__ uint64_t record_value(uint32_t id, const uint64_t* __restrict__ vals, int32_t rec,
-                                                 uint64_t fm) {
-  const bool stored = rec >= 0 && !(id & (kIdVZ | kIdVF));
-  const uint64_t x = vals[stored ? rec : 0];
-  return stored ? x : ((id & kIdVF) ? fm : 0ull);
+// Orders this wave's LDS accesses (a wave's LDS operations complete in order;
+// the fences keep the compiler from moving them across).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // Visits every record of the runs (s, T) for s in [0, nt_s): a wave takes 64
-// consecutive runs at a time (lane = run), scans their lengths, and its lanes
-// then walk the concatenated records in order, kUnroll records per lane with
-// all loads issued before any is consumed.  fn(rec) receives the global record
-// index s * rp + pos, or -1 past the end.
+// consecutive runs at a time (lane = run) and scans their lengths; the
+// concatenated records are then walked in windows of 64*U, lane-strided (so
+// each load instruction reads consecutive records of a run).  The owner of a
+// record comes from a per-wave LDS bitmap of run starts in the window and a
+// list of the window's runs: rank = (run starts at or before it) - 1, one
+// popcount and one LDS read per record, no search.  fn(rec) receives the
+// global record index s * rp + pos, or -1 past the end.
+// LDS per wave: wmask[U] u64, wlist[64] i32.
 template <int U, typename F>
 __device__ __forceinline__ void for_each_run_record(const BinGeom& g, const uint16_t* rowb, const uint16_t* rowe,
-                                                    F&& fn) {
+                                                    uint64_t* wmask_all, int32_t* wlist_all, F&& fn) {
+  constexpr uint32_t kWin = 64 * U;
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+  uint64_t* wm = wmask_all + wave * U;
+  int32_t* wl = wlist_all + wave * 64;
+  const uint64_t below = (1ull << lane) - 1ull, upto = (2ull << lane) - 1ull;  // lane 63: 2 << 63 wraps to all ones
   for (uint32_t s0 = wave * 64; s0 < g.nt_s; s0 += nwaves * 64) {
     const uint32_t s = s0 + lane;
     const uint32_t sc = min(s, g.nt_s - 1);
@@ -332,50 +340,73 @@ __device__ __forceinline__ void for_each_run_record(const BinGeom& g, const uint
     const uint32_t exc = inc - len;
     const uint32_t total = __shfl(inc, 63, 64);
     const int32_t basep = (int32_t)(s * g.rp + be - exc);  // record = basep(owner) + f (< 2^31)
-    for (uint32_t f0 = 0; f0 < total; f0 += 64 * U) {
+    for (uint32_t f0 = 0; f0 < total; f0 += kWin) {
+      if (lane < (uint32_t)U) wm[lane] = 0;
+      wave_sync();
+      // runs meeting this window, in order; a run begun in an earlier window marks position 0
+      const bool in = len != 0 && exc < f0 + kWin && exc + len > f0;
+      const uint64_t inm = __ballot(in);
+      if (in) {
+        const uint32_t pos = exc > f0 ? exc - f0 : 0u;
+        atomicOr((unsigned long long*)&wm[pos >> 6], 1ull << (pos & 63u));
+        wl[__popcll(inm & below)] = basep;
+      }
+      wave_sync();
       int32_t rec[U];
+      uint32_t pre = 0;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
+        const uint64_t w = wm[u];
+        const uint32_t rank = pre + (uint32_t)__popcll(w & upto) - 1u;
+        pre += (uint32_t)__popcll(w);
         const uint32_t f = f0 + u * 64 + lane;
-        uint32_t r = 0;  // owner run: largest r with exc[r] <= f
-#pragma unroll
-        for (uint32_t step = 32; step > 0; step >>= 1) {
-          const uint32_t c = r + step;
-          if (__shfl(exc, c, 64) <= f) r = c;
-        }
-        // every lane takes part in the shuffle: a bpermute from a lane that is
-        // masked off returns garbage, so no conditional around it
-        const int32_t bp = __shfl(basep, r, 64);
-        rec[u] = f < total ? bp + (int32_t)f : -1;
+        rec[u] = f < total ? wl[rank & 63u] + (int32_t)f : -1;
       }
+      wave_sync();  // the next window rewrites wm/wl
       fn(rec);
     }
   }
 }
 
+// LDS image of S_t[node0, node0 + kTileD): every load of the tile in flight at
+// once (8 x 16 B per lane), then the LDS stores.
+__device__ __forceinline__ void load_tile(unsigned long long* img, const uint64_t* __restrict__ S, uint64_t node0,
+                                          uint64_t N) {
+  constexpr uint32_t kQ = kTileD / kTileThreads / 2;
+  const uint32_t tid = threadIdx.x;
+  uint4 x[kQ];
+  if (node0 + kTileD <= N) {
+    const uint4* src = (const uint4*)(S + node0);
+#pragma unroll
+    for (uint32_t q = 0; q < kQ; ++q) x[q] = src[q * kTileThreads + tid];
+  } else {  // last, ragged tile
+#pragma unroll
+    for (uint32_t q = 0; q < kQ; ++q) {
+      const uint64_t n = node0 + 2ull * (q * kTileThreads + tid);
+      const uint64_t a = n < N ? S[n] : 0ull, b = n + 1 < N ? S[n + 1] : 0ull;
+      x[q] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+    }
+  }
+#pragma unroll
+  for (uint32_t q = 0; q < kQ; ++q) ((uint4*)img)[q * kTileThreads + tid] = x[q];
+}
+
 // K2 — one block per destination tile T (pull modes): LDS image of S_t[T];
 // every record aimed at T from a sender that is not yet fully informed gets
-// its pull response S_t[p] written next to it when nonzero (id flag kIdRV).
+// its pull response S_t[p] written next to it when nonzero (every one, in dense rounds).
 __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, const uint64_t* __restrict__ S, BinBufs b,
                                                                   uint32_t R) {
   __shared__ unsigned long long img[kTileD];
-  const uint32_t tid = threadIdx.x;
+  __shared__ uint64_t wmask[(kTileThreads / 64) * kUnroll];
+  __shared__ int32_t wlist[(kTileThreads / 64) * 64];
   const uint32_t T = xcd_remap(blockIdx.x, g.nt_d);
   const uint64_t node0 = (uint64_t)T << kTileDLog;
-  for (uint32_t q0 = 0; q0 < kTileD / kTileThreads; q0 += 4) {
-    uint64_t x[4];
-#pragma unroll
-    for (uint32_t q = 0; q < 4; ++q) x[q] = S[min<uint64_t>(node0 + (q0 + q) * kTileThreads + tid, g.N - 1)];
-#pragma unroll
-    for (uint32_t q = 0; q < 4; ++q)
-      img[(q0 + q) * kTileThreads + tid] = node0 + (q0 + q) * kTileThreads + tid < g.N ? x[q] : 0ull;
-  }
+  load_tile(img, S, node0, g.N);
   __syncthreads();
   const uint32_t* gids = b.ids;
-  uint32_t* gidsw = b.ids;
   uint64_t* __restrict__ gresp = b.resp;
   const uint16_t* rowb = b.offT + (size_t)T * g.nt_s;
-  for_each_run_record<kUnroll>(g, rowb, rowb + g.nt_s, [&](const int32_t* rec) {
+  for_each_run_record<kUnroll>(g, rowb, rowb + g.nt_s, wmask, wlist, [&](const int32_t* rec) {
     uint32_t id[kUnroll];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) id[u] = gids[rec[u] >= 0 ? rec[u] : 0];
@@ -383,12 +414,9 @@ __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, cons
     for (int u = 0; u < kUnroll; ++u) {
       // a fully informed sender needs nothing; otherwise the whole S_t[p] goes
       // back (bits n already holds are harmless to OR), so no value is read
+      // dense rounds: every response is written (K3 tells stale slots by kIdVF)
       if (rec[u] < 0 || (id[u] & kIdVF)) continue;
-      const uint64_t r = img[id[u] & (kTileD - 1)];
-      if (r) {  // only nonzero responses move: the flag tells K3 to read it
-        gresp[rec[u]] = r;
-        gidsw[rec[u]] = id[u] | kIdRV;
-      }
+      gresp[rec[u]] = img[id[u] & (kTileD - 1)];
     }
   });
 }
@@ -399,38 +427,36 @@ __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, cons
 __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, const uint64_t* __restrict__ S,
                                                                   uint64_t* __restrict__ Snext, BinBufs b,
                                                                   uint64_t* __restrict__ partial, uint32_t R,
-                                                                  uint32_t mode, uint32_t flags) {
+                                                                  uint32_t mode, uint32_t flags, uint32_t exp) {
   __shared__ unsigned long long acc[kTileD];
   __shared__ uint32_t cnt[64];
   __shared__ uint64_t red_hash[kTileThreads / 64];
   __shared__ uint32_t red_full[kTileThreads / 64];
   __shared__ uint32_t red_nz[kTileThreads / 64];
+  __shared__ uint64_t wmask[(kTileThreads / 64) * kUnroll];
+  __shared__ int32_t wlist[(kTileThreads / 64) * 64];
   const uint32_t tid = threadIdx.x;
   const uint32_t X = xcd_remap(blockIdx.x, g.nt_d);
   const uint64_t node0 = (uint64_t)X << kTileDLog;
-  for (uint32_t q0 = 0; q0 < kTileD / kTileThreads; q0 += 4) {
-    uint64_t x[4];
-#pragma unroll
-    for (uint32_t q = 0; q < 4; ++q) x[q] = S[min<uint64_t>(node0 + (q0 + q) * kTileThreads + tid, g.N - 1)];
-#pragma unroll
-    for (uint32_t q = 0; q < 4; ++q)
-      acc[(q0 + q) * kTileThreads + tid] = node0 + (q0 + q) * kTileThreads + tid < g.N ? x[q] : 0ull;
-  }
+  if (!(exp & 32u)) load_tile(acc, S, node0, g.N);
   if (tid < 64) cnt[tid] = 0;
   __syncthreads();
   const uint32_t* __restrict__ gids = b.ids;
   const uint64_t* __restrict__ gvals = b.vals;
   const uint64_t* __restrict__ gresp = b.resp;
   const uint64_t fm = full_mask1(R);
-  if (mode == 1 || mode == 3) {  // pushes aimed at this tile
+  if ((mode == 1 || mode == 3) && !(exp & 4u)) {  // pushes aimed at this tile
     const uint16_t* rowb = b.offT + (size_t)X * g.nt_s;
-    for_each_run_record<kUnroll>(g, rowb, rowb + g.nt_s, [&](const int32_t* rec) {
+    for_each_run_record<kUnroll>(g, rowb, rowb + g.nt_s, wmask, wlist, [&](const int32_t* rec) {
       uint32_t id[kUnroll];
       uint64_t v[kUnroll];
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) id[u] = gids[rec[u] >= 0 ? rec[u] : 0];
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) v[u] = rec[u] >= 0 ? record_value(id[u], gvals, rec[u], fm) : 0ull;
+      for (int u = 0; u < kUnroll; ++u) v[u] = gvals[rec[u] >= 0 ? rec[u] : 0];  // not behind the id: both loads fly together
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u)
+        v[u] = rec[u] < 0 || (id[u] & kIdVZ) ? 0ull : ((id[u] & kIdVF) ? fm : v[u]);
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         const uint32_t p = id[u] & (kTileD - 1);
@@ -438,7 +464,7 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, cons
       }
     });
   }
-  if (mode == 2 || mode == 3) {  // responses owed to this tile's own senders
+  if ((mode == 2 || mode == 3) && !(exp & 8u)) {  // responses owed to this tile's own senders
     const uint32_t per = kTileD >> g.ts_log;
     const uint32_t s0 = X * per, s1 = min(s0 + per, g.nt_s);
     for (uint32_t s = s0; s < s1; ++s) {
@@ -448,22 +474,17 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, cons
       for (uint32_t p0 = 0; p0 < total; p0 += kTileThreads * kUnrollSeq) {
         uint64_t r[kUnrollSeq];
         uint32_t id[kUnrollSeq];
+        // id and response loads are independent: both fly together
 #pragma unroll
         for (int u = 0; u < kUnrollSeq; ++u) {
-          const uint32_t pos = p0 + u * kTileThreads + tid;
-          id[u] = gids[reg + (pos < total ? pos : 0u)];
-          if (pos >= total) id[u] = 0;
+          const uint32_t pos = min(p0 + u * kTileThreads + tid, total - 1);
+          id[u] = gids[reg + pos];
+          r[u] = gresp[reg + pos];
         }
 #pragma unroll
         for (int u = 0; u < kUnrollSeq; ++u) {
-          const uint32_t pos = p0 + u * kTileThreads + tid;
-          const bool rv = (id[u] & kIdRV) != 0;
-          const uint64_t x = gresp[rv ? reg + pos : 0];
-          r[u] = rv ? x : 0ull;
-        }
-#pragma unroll
-        for (int u = 0; u < kUnrollSeq; ++u) {
-          if (!r[u]) continue;
+          // a full sender's slot was never written this round (K2 skips it)
+          if (p0 + u * kTileThreads + tid >= total || (id[u] & kIdVF)) continue;
           const uint32_t node = nb + ((id[u] >> kTileDLog) & kIdNMask);
           if (r[u] & ~acc[node]) atomicOr(&acc[node], (unsigned long long)r[u]);
         }
@@ -471,6 +492,10 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, cons
     }
   }
   __syncthreads();
+  if (exp & 16u) {  // timing experiment: store only
+    for (uint32_t q = 0; q < kTileD / kTileThreads; ++q) Snext[node0 + q * kTileThreads + tid] = acc[q * kTileThreads + tid];
+    return;
+  }
   tile_epilogue(acc, node0, g.N, Snext, partial, R, flags, cnt, red_hash, red_full, red_nz, b.nzb, b.fullb);
 }
 
@@ -534,7 +559,9 @@ hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, const uint64_
   const bool pull = mode == 2 || mode == 3;
   // expected records per tile = k * kTileD: keep them in registers when they fit
   if (pull) bin_serve_kernel<<<g.nt_d, kTileThreads, 0, st>>>(g, S, b, R);
-  bin_apply_kernel<<<g.nt_d, kTileThreads, 0, st>>>(g, S, Snext, b, partial, R, mode, flags);
+  const char* xs = getenv("GOSSIP_EXPERIMENT");  // timing experiments only: results are wrong when set
+  const uint32_t exp = xs ? (uint32_t)atoi(xs) : 0u;
+  bin_apply_kernel<<<g.nt_d, kTileThreads, 0, st>>>(g, S, Snext, b, partial, R, mode, flags, exp);
   return hipGetLastError();
 }
 

@@ -72,6 +72,7 @@ struct gossip_engine {
   FrontierBufs fb{};
   void* fr_mem = nullptr;
   bool fr_valid = false;          // partial_d holds the totals of S and the bitmaps are exact
+  bool tot_stale = false;         // partial_d moved on the device (inject) since tot was read
   bool inplace = false;           // the last computed round updated S in place (no buffer flip)
   double sparse_frac = 1.0 / 16;  // rare fraction at or below which a round runs sparse
   std::vector<uint64_t> tot;      // host copy of the totals of S [5 + R]
@@ -272,6 +273,12 @@ int compute_round(gossip_engine* e, const uint64_t* gathered) {
         HIP_OK(e, hipStreamSynchronize(e->stream));
         e->tot.assign(e->partial_h, e->partial_h + part_len(e));
         e->fr_valid = true;
+        e->tot_stale = false;
+      } else if (e->tot_stale) {  // after inject: the device totals are exact, the host copy is not
+        HIP_OK(e, hipMemcpyAsync(e->partial_h, e->partial_d, part_len(e) * 8, hipMemcpyDeviceToHost, e->stream));
+        HIP_OK(e, hipStreamSynchronize(e->stream));
+        e->tot.assign(e->partial_h, e->partial_h + part_len(e));
+        e->tot_stale = false;
       }
       const uint64_t nz = e->tot[4 + e->R], full = e->tot[0];
       const uint64_t rare_lo = nz, rare_hi = e->N - full, lim = (uint64_t)(e->sparse_frac * (double)e->N);
@@ -578,6 +585,15 @@ int gossip_reset(gossip_engine_t* e) {
     HIP_OK(e, hipMemsetAsync(e->img[1], 0, shard * e->G, e->stream));
   }
   e->fr_valid = false;
+  if (e->frontier) {  // all-zero state: zero totals, empty bitmaps (D, P and dirty flags are zero between rounds)
+    const size_t nwb = (e->N + 63) / 64 * 8;
+    HIP_OK(e, hipMemsetAsync(e->fb.nzb, 0, nwb, e->stream));
+    HIP_OK(e, hipMemsetAsync(e->fb.fullb, 0, nwb, e->stream));
+    HIP_OK(e, hipMemsetAsync(e->partial_d, 0, part_len(e) * 8, e->stream));
+    e->tot.assign(part_len(e), 0);
+    e->fr_valid = true;
+    e->tot_stale = false;
+  }
   e->t = 0;
   return GOSSIP_OK;
 }
@@ -591,6 +607,12 @@ int gossip_inject(gossip_engine_t* e, uint64_t node, uint32_t rumor) {
     HIP_OK(e, launch_ae_inject(e->V, e->target, node, e->R, rumor, e->stream));
     return GOSSIP_OK;
   }
+  if (e->frontier && e->fr_valid) {
+    HIP_OK(e, launch_frontier_inject(e->fb, e->S, e->N, e->partial_d, e->R, e->key0, e->key1, (int64_t)node, rumor,
+                                     e->cfg.flags, e->stream));
+    e->tot_stale = true;
+    return GOSSIP_OK;
+  }
   HIP_OK(e, launch_inject(e->S, e->Nl, e->lo, e->hi, e->N, e->R, e->key0, e->key1, (int64_t)node, rumor, e->stream));
   e->fr_valid = false;
   return GOSSIP_OK;
@@ -601,6 +623,12 @@ int gossip_inject_random(gossip_engine_t* e) {
   if (int rc = set_dev(e)) return rc;
   if (e->mode == GOSSIP_MODE_ANTIENTROPY) {
     HIP_OK(e, launch_ae_init(e->V, e->target, e->N, e->R, e->key0, e->key1, e->stream));
+    return GOSSIP_OK;
+  }
+  if (e->frontier && e->fr_valid) {
+    HIP_OK(e, launch_frontier_inject(e->fb, e->S, e->N, e->partial_d, e->R, e->key0, e->key1, -1, 0, e->cfg.flags,
+                                     e->stream));
+    e->tot_stale = true;
     return GOSSIP_OK;
   }
   HIP_OK(e, launch_inject(e->S, e->Nl, e->lo, e->hi, e->N, e->R, e->key0, e->key1, -1, 0, e->stream));

@@ -16,11 +16,14 @@ namespace gossip {
 constexpr uint32_t kSummBits = 1u << 20;  // LDS summary: at most 2^20 bits (128 KiB)
 
 struct FrontierBufs {
-  uint64_t* nzb;    // [ceil(N/64)] bit n: S[n] != 0
-  uint64_t* fullb;  // [ceil(N/64)] bit n: S[n] == full mask
-  uint32_t* summ;   // [summ_words] bit b: some rare node in [b*g, (b+1)*g)
-  uint64_t* D;      // [N] pending deltas, zero outside a sparse round
-  uint32_t glog;    // g = 1 << glog nodes per summary bit
+  uint64_t* nzb;      // [ceil(N/64)] bit n: S[n] != 0
+  uint64_t* fullb;    // [ceil(N/64)] bit n: S[n] == full mask
+  uint32_t* summ;     // [summ_words] bit b: some rare node in [b*g, (b+1)*g)
+  uint64_t* D;        // [N] pending push deltas (atomic OR), zero outside a sparse round
+  uint64_t* P;        // [N] pending pull deltas (plain store by the node's own lane), zero outside
+  uint8_t* dirtyD;    // [ceil(N/64)] group g has a push delta
+  uint8_t* dirtyP;    // [ceil(N/64)] group g has a pull delta
+  uint32_t glog;      // g = 1 << glog nodes per summary bit
   uint32_t summ_words;
 };
 
@@ -31,6 +34,12 @@ void frontier_carve(uint64_t N, void* base, FrontierBufs* f);
 // Absolute stats of S into partial (zeroed by the caller) + both bitmaps.
 hipError_t launch_frontier_rebuild(const FrontierBufs& f, const uint64_t* S, uint64_t N, uint64_t* partial,
                                    uint32_t R, uint32_t flags, hipStream_t st);
+
+// Client broadcast that keeps the running totals (partial) and both bitmaps
+// exact: node >= 0 sets one bit, node < 0 injects every rumor at its origin.
+hipError_t launch_frontier_inject(const FrontierBufs& f, uint64_t* S, uint64_t N, uint64_t* partial, uint32_t R,
+                                  uint32_t key0, uint32_t key1, int64_t node, uint32_t rumor, uint32_t flags,
+                                  hipStream_t st);
 
 // One sparse round, in place on S.  maj = 0: rare = nonzero nodes; maj = 1:
 // rare = nodes not yet full.  partial holds the totals of S_t on entry and

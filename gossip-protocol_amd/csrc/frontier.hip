@@ -27,6 +27,7 @@
 // both bitmaps from S (after inject/reset or a direct-path round).
 #include "frontier.h"
 #include "philox.h"
+#include "wave.h"
 
 namespace gossip {
 
@@ -35,8 +36,9 @@ namespace {
 constexpr int kScanThreads = 1024;
 constexpr uint32_t kScanGrid = 256;  // one block per CU: the summary takes 128 KiB of LDS
 constexpr int kCommitThreads = 256;
-
-__device__ __forceinline__ uint64_t full_mask(uint32_t R) { return R >= 64 ? ~0ull : ((1ull << R) - 1ull); }
+constexpr uint32_t kRwWords = 1024;  // rare-bitmap words staged per scan chunk (64K nodes)
+constexpr int kScanUnroll = 2;       // nodes per lane per scan step
+constexpr int kCommitUnroll = 4;     // dirty groups per wave per commit step
 
 // valid-node mask of bitmap word w (bits past N are zero in both bitmaps)
 __device__ __forceinline__ uint64_t word_valid(uint64_t w, uint64_t N) {
@@ -83,102 +85,126 @@ __global__ __launch_bounds__(256) void frontier_summary_kernel(FrontierBufs f, u
 }
 
 // K1.  MODE: 1 push, 2 pull, 3 push-pull.  MAJ: majority value 0 (0) or full (1).
+// Each block owns a contiguous node range; the rare-bitmap words of the next
+// 64K nodes are staged in LDS so the per-node test never waits on memory.
+// A summary hit is confirmed in the exact rare bitmap before S_t[p] is read
+// (the bitmap is L2-resident; S is not).  Pull deltas belong to the node's own
+// lane and are plain stores to P; push deltas are atomic ORs into D.
 template <int MAJ, int MODE>
 __global__ __launch_bounds__(kScanThreads) void frontier_scan_kernel(FrontierBufs f, const uint64_t* __restrict__ S,
                                                                       uint64_t N, uint32_t R, uint32_t k, uint32_t t,
-                                                                      uint32_t key0, uint32_t key1) {
+                                                                      uint32_t key0, uint32_t key1,
+                                                                      uint64_t per_block) {
   __shared__ uint4 summ4[kSummBits / 128];
+  __shared__ uint64_t rws[kRwWords];
   const uint32_t* summ = (const uint32_t*)summ4;
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t n4 = (f.summ_words + 3) / 4;
   for (uint32_t i = tid; i < n4; i += kScanThreads) summ4[i] = ((const uint4*)f.summ)[i];
-  __syncthreads();
 
   constexpr bool kPush = (MODE & 1) != 0, kPull = (MODE & 2) != 0;
-  const uint64_t fm = full_mask(R), maj = MAJ ? fm : 0ull, nm1 = N - 1;
+  const uint64_t fm = full_mask1(R), maj = MAJ ? fm : 0ull, nm1 = N - 1;
   const uint32_t glog = f.glog;
-  for (uint64_t base = (uint64_t)blockIdx.x * kScanThreads; base < N; base += (uint64_t)gridDim.x * kScanThreads) {
-    const uint64_t n = base + tid;
-    const bool valid = n < N;
-    const uint64_t rw = rare_word<MAJ>(f, (valid ? n : N - 1) >> 6, N);  // one address per wave
-    const bool rn = valid && ((rw >> lane) & 1ull);
-    // a majority node only acts through a rare peer; push from an empty node and
-    // pull into a full one are no-ops, so those nodes skip the draws entirely
-    if (!valid || (!rn && ((!kPull && MAJ == 0) || (!kPush && MAJ == 1)))) continue;
-    const uint64_t x = rn ? S[n] : maj;
-    uint64_t acc = 0;
-    u32x4 r4{0, 0, 0, 0};
-    for (uint32_t j = 0; j < k; ++j) {
-      if ((j & 3u) == 0) r4 = philox4x32_10(u32x4{(uint32_t)n, t, 0u, j >> 2}, key0, key1);
-      const uint32_t p = peer_from_word(lane_of(r4, j & 3u), nm1, (uint32_t)n);
-      bool rp = (summ[p >> (glog + 5)] >> ((p >> glog) & 31u)) & 1u;
-      if (rp && glog) rp = (rare_word<MAJ>(f, p >> 6, N) >> (p & 63u)) & 1ull;
-      if (!rn && !rp) continue;  // both ends majority: nothing moves
-      const uint64_t vp = rp ? S[p] : maj;
-      if (kPull) acc |= vp;
-      if (kPush) {
-        const uint64_t d = x & ~vp;
-        if (d) atomicOr((unsigned long long*)&f.D[p], (unsigned long long)d);
+  auto summ_bit = [&](uint32_t p) -> bool { return (summ[p >> (glog + 5)] >> ((p >> glog) & 31u)) & 1u; };
+  const uint64_t b0 = (uint64_t)blockIdx.x * per_block, b1 = min(b0 + per_block, N);
+  for (uint64_t c0 = b0; c0 < b1; c0 += (uint64_t)kRwWords * 64) {
+    const uint64_t c1 = min(c0 + (uint64_t)kRwWords * 64, b1);
+    __syncthreads();  // previous chunk done with rws
+    for (uint32_t i = tid; i < (uint32_t)((c1 - c0 + 63) >> 6); i += kScanThreads)
+      rws[i] = rare_word<MAJ>(f, (c0 >> 6) + i, N);
+    __syncthreads();
+    for (uint64_t base = c0; base < c1; base += kScanThreads * kScanUnroll) {
+      uint64_t x[kScanUnroll], vp[kScanUnroll][4];
+      uint32_t pp[kScanUnroll][4], hit[kScanUnroll];
+      bool act[kScanUnroll], rn[kScanUnroll];
+      // 1. draws and LDS summary tests (no global memory)
+#pragma unroll
+      for (int u = 0; u < kScanUnroll; ++u) {
+        const uint64_t n = base + (uint64_t)u * kScanThreads + tid;
+        const bool valid = n < c1;
+        rn[u] = valid && ((rws[valid ? (n - c0) >> 6 : 0] >> lane) & 1ull);
+        // a majority node only acts through a rare peer; push from an empty node and
+        // pull into a full one are no-ops, so those nodes skip the draws entirely
+        act[u] = valid && (rn[u] || !((!kPull && MAJ == 0) || (!kPush && MAJ == 1)));
+        hit[u] = 0;
+        if (act[u] && k <= 4) {
+          const u32x4 r4 = philox4x32_10(u32x4{(uint32_t)n, t, 0u, 0u}, key0, key1);
+#pragma unroll
+          for (uint32_t j = 0; j < 4; ++j) {
+            if (j >= k) break;
+            pp[u][j] = peer_from_word(lane_of(r4, j), nm1, (uint32_t)n);
+            if (summ_bit(pp[u][j])) hit[u] |= 1u << j;
+          }
+        }
+      }
+      // 2. summary hits: exact test in the rare bitmap (2 MiB at 2^24 nodes, L2-resident)
+      if (glog) {
+#pragma unroll
+        for (int u = 0; u < kScanUnroll; ++u)
+#pragma unroll
+          for (uint32_t j = 0; j < 4; ++j)
+            if ((hit[u] >> j) & 1u)
+              if (!((rare_word<MAJ>(f, pp[u][j] >> 6, N) >> (pp[u][j] & 63u)) & 1ull)) hit[u] &= ~(1u << j);
+      }
+      // 3. S_t of the rare ends only (a majority node's value is known)
+#pragma unroll
+      for (int u = 0; u < kScanUnroll; ++u) {
+        const uint64_t n = base + (uint64_t)u * kScanThreads + tid;
+        x[u] = rn[u] ? S[n] : maj;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) vp[u][j] = ((hit[u] >> j) & 1u) ? S[pp[u][j]] : maj;
+      }
+      // 4. deltas
+#pragma unroll
+      for (int u = 0; u < kScanUnroll; ++u) {
+        if (!act[u]) continue;
+        const uint64_t n = base + (uint64_t)u * kScanThreads + tid;
+        uint64_t acc = 0;
+        auto edge = [&](uint32_t p, uint64_t v) {
+          if (kPull) acc |= v;
+          if (kPush) {
+            const uint64_t d = x[u] & ~v;
+            if (d) {
+              atomicOr((unsigned long long*)&f.D[p], (unsigned long long)d);
+              f.dirtyD[p >> 6] = 1;
+            }
+          }
+        };
+        if (k <= 4) {
+#pragma unroll
+          for (uint32_t j = 0; j < 4; ++j) {
+            if (j >= k) break;
+            if (rn[u] || ((hit[u] >> j) & 1u)) edge(pp[u][j], vp[u][j]);  // else both ends majority
+          }
+        } else {
+          u32x4 r4{0, 0, 0, 0};
+          for (uint32_t j = 0; j < k; ++j) {
+            if ((j & 3u) == 0) r4 = philox4x32_10(u32x4{(uint32_t)n, t, 0u, j >> 2}, key0, key1);
+            const uint32_t p = peer_from_word(lane_of(r4, j & 3u), nm1, (uint32_t)n);
+            bool rp = summ_bit(p);
+            if (rp && glog) rp = (rare_word<MAJ>(f, p >> 6, N) >> (p & 63u)) & 1ull;
+            if (!rn[u] && !rp) continue;  // both ends majority: nothing moves
+            edge(p, rp ? S[p] : maj);
+          }
+        }
+        acc &= ~x[u];
+        if (acc) {
+          f.P[n] = acc;
+          f.dirtyP[n >> 6] = 1;
+        }
       }
     }
-    acc &= ~x;
-    if (acc) atomicOr((unsigned long long*)&f.D[n], (unsigned long long)acc);
   }
 }
 
-__device__ __forceinline__ uint64_t transpose64(uint64_t x, uint32_t lane) {
-  constexpr uint64_t kMask[6] = {0x00000000FFFFFFFFull, 0x0000FFFF0000FFFFull, 0x00FF00FF00FF00FFull,
-                                 0x0F0F0F0F0F0F0F0Full, 0x3333333333333333ull, 0x5555555555555555ull};
-#pragma unroll
-  for (int st = 0; st < 6; ++st) {
-    const uint32_t d = 32u >> st;
-    const uint64_t y = __shfl_xor(x, d, 64);
-    const uint64_t m = kMask[st];
-    x = (lane & d) ? ((x & ~m) | ((y & ~m) >> d)) : ((x & m) | ((y & m) << d));
-  }
-  return x;
-}
-
-__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
-
-// K2.  REBUILD: absolute stats + bitmaps of S (partial zeroed by the caller);
-// else: apply D in place and add the deltas to the totals already in partial.
-template <bool REBUILD>
-__global__ __launch_bounds__(kCommitThreads) void frontier_commit_kernel(FrontierBufs f, uint64_t* __restrict__ S,
-                                                                          uint64_t N, uint64_t* __restrict__ partial,
-                                                                          uint32_t R, uint32_t flags) {
-  __shared__ uint32_t cnt[64];
-  __shared__ uint64_t red[3][kCommitThreads / 64];  // full, nonzero, hash
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint64_t fm = full_mask(R);
-  const bool do_hash = (flags & 1u) != 0;
-  if (tid < 64) cnt[tid] = 0;
-  __syncthreads();
-  const uint64_t ngroups = (N + 63) >> 6;
+// Stats of one 64-node group whose words went from old to nw (old == 0 in a
+// rebuild), and its two bitmap words (wave-exclusive plain stores).
+struct GroupStats {
   uint64_t hash = 0;
   uint32_t full = 0, nz = 0, c_lane = 0;
-  for (uint64_t g = (uint64_t)blockIdx.x * (kCommitThreads / 64) + wave; g < ngroups;
-       g += (uint64_t)gridDim.x * (kCommitThreads / 64)) {
-    const uint64_t n = (g << 6) + lane;
-    const bool valid = n < N;
-    uint64_t old, nw;
-    if (REBUILD) {
-      old = 0;
-      nw = valid ? S[n] : 0ull;
-    } else {
-      const uint64_t d = valid ? f.D[n] : 0ull;
-      if (__ballot(d != 0) == 0) continue;
-      old = valid ? S[n] : 0ull;
-      nw = old | d;
-      if (d) {
-        f.D[n] = 0;
-        if (nw != old) S[n] = nw;
-      }
-    }
+
+  __device__ __forceinline__ void add(const FrontierBufs& f, uint64_t g, uint64_t n, bool valid, uint64_t old,
+                                      uint64_t nw, uint64_t fm, bool do_hash, uint32_t lane) {
     const uint64_t nzw = __ballot(valid && nw != 0), fw = __ballot(valid && nw == fm);
     if (lane == 0) {
       f.nzb[g] = nzw;
@@ -193,26 +219,139 @@ __global__ __launch_bounds__(kCommitThreads) void frontier_commit_kernel(Frontie
     }
     if (__ballot(nb != 0)) c_lane += (uint32_t)__popcll(transpose64(nb, lane));
   }
-  if (lane < R && c_lane) atomicAdd(&cnt[lane], c_lane);
-  hash = wave_sum64(hash);
-  if (lane == 0) {
-    red[0][wave] = full;
-    red[1][wave] = nz;
-    red[2][wave] = hash;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    uint64_t a = 0, b = 0, h = 0;
-    for (int w = 0; w < kCommitThreads / 64; ++w) {
-      a += red[0][w];
-      b += red[1][w];
-      h += red[2][w];
+
+  // block-level fold into the running totals
+  __device__ __forceinline__ void flush(uint64_t* __restrict__ partial, uint32_t R, uint32_t* cnt,
+                                        uint64_t (*red)[kCommitThreads / 64]) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (lane < R && c_lane) atomicAdd(&cnt[lane], c_lane);
+    const uint64_t h = wave_sum64(hash);
+    if (lane == 0) {
+      red[0][wave] = full;
+      red[1][wave] = nz;
+      red[2][wave] = h;
     }
-    if (a) atomicAdd((unsigned long long*)&partial[0], (unsigned long long)a);
-    if (h) atomicAdd((unsigned long long*)&partial[3], (unsigned long long)h);
-    if (b) atomicAdd((unsigned long long*)&partial[4 + R], (unsigned long long)b);
+    __syncthreads();
+    if (tid == 0) {
+      uint64_t a = 0, b = 0, hh = 0;
+      for (int w = 0; w < kCommitThreads / 64; ++w) {
+        a += red[0][w];
+        b += red[1][w];
+        hh += red[2][w];
+      }
+      if (a) atomicAdd((unsigned long long*)&partial[0], (unsigned long long)a);
+      if (hh) atomicAdd((unsigned long long*)&partial[3], (unsigned long long)hh);
+      if (b) atomicAdd((unsigned long long*)&partial[4 + R], (unsigned long long)b);
+    }
+    if (tid < R && cnt[tid]) atomicAdd((unsigned long long*)&partial[4 + tid], (unsigned long long)cnt[tid]);
   }
-  if (tid < R && cnt[tid]) atomicAdd((unsigned long long*)&partial[4 + tid], (unsigned long long)cnt[tid]);
+};
+
+// Absolute stats + bitmaps of S (partial zeroed by the caller).
+__global__ __launch_bounds__(kCommitThreads) void frontier_rebuild_kernel(FrontierBufs f, const uint64_t* __restrict__ S,
+                                                                           uint64_t N, uint64_t* __restrict__ partial,
+                                                                           uint32_t R, uint32_t flags) {
+  __shared__ uint32_t cnt[64];
+  __shared__ uint64_t red[3][kCommitThreads / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid < 64) cnt[tid] = 0;
+  __syncthreads();
+  const uint64_t fm = full_mask1(R), ngroups = (N + 63) >> 6;
+  GroupStats gs;
+  for (uint64_t g = (uint64_t)blockIdx.x * (kCommitThreads / 64) + wave; g < ngroups;
+       g += (uint64_t)gridDim.x * (kCommitThreads / 64)) {
+    const uint64_t n = (g << 6) + lane;
+    const bool valid = n < N;
+    gs.add(f, g, n, valid, 0ull, valid ? S[n] : 0ull, fm, (flags & 1u) != 0, lane);
+  }
+  gs.flush(partial, R, cnt, red);
+}
+
+// K2: a wave takes 64 groups, finds the dirty ones by one coalesced load of
+// their flags, and commits kCommitUnroll of them per step: S |= D | P in
+// place, D, P and the flags back to zero, bitmaps and stats deltas.
+__global__ __launch_bounds__(kCommitThreads) void frontier_commit_kernel(FrontierBufs f, uint64_t* __restrict__ S,
+                                                                          uint64_t N, uint64_t* __restrict__ partial,
+                                                                          uint32_t R, uint32_t flags) {
+  __shared__ uint32_t cnt[64];
+  __shared__ uint64_t red[3][kCommitThreads / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid < 64) cnt[tid] = 0;
+  __syncthreads();
+  const uint64_t fm = full_mask1(R), ngroups = (N + 63) >> 6;
+  const bool do_hash = (flags & 1u) != 0;
+  GroupStats gs;
+  for (uint64_t c = (uint64_t)blockIdx.x * (kCommitThreads / 64) + wave; (c << 6) < ngroups;
+       c += (uint64_t)gridDim.x * (kCommitThreads / 64)) {
+    const uint64_t gl = (c << 6) + lane;
+    const bool gv = gl < ngroups;
+    const uint8_t fd = gv ? f.dirtyD[gl] : 0, fp = gv ? f.dirtyP[gl] : 0;
+    if (fd) f.dirtyD[gl] = 0;
+    if (fp) f.dirtyP[gl] = 0;
+    const uint64_t mD = __ballot(fd != 0), mP = __ballot(fp != 0);
+    uint64_t mask = mD | mP;
+    while (mask) {
+      uint32_t gi[kCommitUnroll];
+      uint32_t cntg = 0;
+#pragma unroll
+      for (int u = 0; u < kCommitUnroll; ++u) {
+        gi[u] = mask ? (uint32_t)__builtin_ctzll(mask) : 64u;
+        if (mask) {
+          mask &= mask - 1;
+          ++cntg;
+        }
+      }
+      uint64_t d[kCommitUnroll], pv[kCommitUnroll], old[kCommitUnroll];
+#pragma unroll
+      for (int u = 0; u < kCommitUnroll; ++u) {
+        const uint64_t n = (((c << 6) + (gi[u] & 63u)) << 6) + lane;
+        const bool valid = gi[u] < 64 && n < N;
+        const bool hd = gi[u] < 64 && ((mD >> gi[u]) & 1ull), hp = gi[u] < 64 && ((mP >> gi[u]) & 1ull);
+        d[u] = valid && hd ? f.D[n] : 0ull;
+        pv[u] = valid && hp ? f.P[n] : 0ull;
+        old[u] = valid ? S[n] : 0ull;
+      }
+#pragma unroll
+      for (int u = 0; u < kCommitUnroll; ++u) {
+        if ((uint32_t)u >= cntg) break;
+        const uint64_t g = (c << 6) + gi[u];
+        const uint64_t n = (g << 6) + lane;
+        const bool valid = n < N;
+        const uint64_t nw = old[u] | d[u] | pv[u];
+        if (nw != old[u]) S[n] = nw;
+        if (d[u]) f.D[n] = 0;
+        if (pv[u]) f.P[n] = 0;
+        gs.add(f, g, n, valid, old[u], nw, fm, do_hash, lane);
+      }
+    }
+  }
+  gs.flush(partial, R, cnt, red);
+}
+
+// Client broadcast with exact running totals and bitmaps (atomics: two rumors
+// may share an origin; each atomic's own old value makes every delta exact).
+__global__ void frontier_inject_kernel(FrontierBufs f, uint64_t* S, uint64_t N, uint64_t* partial, uint32_t R,
+                                       uint32_t key0, uint32_t key1, int64_t node, uint32_t rumor, uint32_t flags) {
+  const uint32_t r = node >= 0 ? rumor : blockIdx.x * blockDim.x + threadIdx.x;
+  if (node >= 0 && (blockIdx.x | threadIdx.x)) return;
+  if (r >= R) return;
+  const uint64_t n = node >= 0 ? (uint64_t)node : origin_of(r, N, key0, key1);
+  const uint64_t bit = 1ull << r, fm = full_mask1(R);
+  const uint64_t old = atomicOr((unsigned long long*)&S[n], (unsigned long long)bit);
+  if (old & bit) return;
+  const uint64_t nw = old | bit;
+  atomicAdd((unsigned long long*)&partial[4 + r], 1ull);
+  if (old == 0) {
+    atomicAdd((unsigned long long*)&partial[4 + R], 1ull);
+    atomicOr((unsigned long long*)&f.nzb[n >> 6], 1ull << (n & 63));
+  }
+  if (nw == fm) {
+    atomicAdd((unsigned long long*)&partial[0], 1ull);
+    atomicOr((unsigned long long*)&f.fullb[n >> 6], 1ull << (n & 63));
+  }
+  if (flags & 1u)
+    atomicAdd((unsigned long long*)&partial[3],
+              (unsigned long long)(mix64(nw + n * kGold64) - (old ? mix64(old + n * kGold64) : 0ull)));
 }
 
 uint32_t commit_grid(uint64_t N) {
@@ -229,33 +368,48 @@ uint32_t frontier_glog(uint64_t N) {
   return glog;
 }
 
+namespace {
+size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+}  // namespace
+
 size_t frontier_bytes(uint64_t N) {
   const size_t nwords = (N + 63) / 64;
   const uint32_t glog = frontier_glog(N);
   const size_t sw = ((((N + (1ull << glog) - 1) >> glog) + 127) / 128) * 4;  // u32 words, uint4-padded
-  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-  return 2 * al(nwords * 8) + al(sw * 4) + al(N * 8);
+  return 2 * al256(nwords * 8) + al256(sw * 4) + 2 * al256(N * 8) + 2 * al256(nwords);
 }
 
 void frontier_carve(uint64_t N, void* base, FrontierBufs* f) {
   const size_t nwords = (N + 63) / 64;
-  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   f->glog = frontier_glog(N);
   f->summ_words = (uint32_t)((((N + (1ull << f->glog) - 1) >> f->glog) + 127) / 128) * 4;
   char* p = (char*)base;
   f->nzb = (uint64_t*)p;
-  p += al(nwords * 8);
+  p += al256(nwords * 8);
   f->fullb = (uint64_t*)p;
-  p += al(nwords * 8);
+  p += al256(nwords * 8);
   f->summ = (uint32_t*)p;
-  p += al((size_t)f->summ_words * 4);
+  p += al256((size_t)f->summ_words * 4);
   f->D = (uint64_t*)p;
+  p += al256(N * 8);
+  f->P = (uint64_t*)p;
+  p += al256(N * 8);
+  f->dirtyD = (uint8_t*)p;
+  p += al256(nwords);
+  f->dirtyP = (uint8_t*)p;
 }
 
 hipError_t launch_frontier_rebuild(const FrontierBufs& f, const uint64_t* S, uint64_t N, uint64_t* partial,
                                    uint32_t R, uint32_t flags, hipStream_t st) {
-  frontier_commit_kernel<true><<<commit_grid(N), kCommitThreads, 0, st>>>(f, const_cast<uint64_t*>(S), N, partial,
-                                                                          R, flags);
+  frontier_rebuild_kernel<<<commit_grid(N), kCommitThreads, 0, st>>>(f, S, N, partial, R, flags);
+  return hipGetLastError();
+}
+
+hipError_t launch_frontier_inject(const FrontierBufs& f, uint64_t* S, uint64_t N, uint64_t* partial, uint32_t R,
+                                  uint32_t key0, uint32_t key1, int64_t node, uint32_t rumor, uint32_t flags,
+                                  hipStream_t st) {
+  const uint32_t grid = node >= 0 ? 1 : (R + 255) / 256;
+  frontier_inject_kernel<<<grid, 256, 0, st>>>(f, S, N, partial, R, key0, key1, node, rumor, flags);
   return hipGetLastError();
 }
 
@@ -269,7 +423,10 @@ hipError_t launch_frontier_round(const FrontierBufs& f, uint64_t* S, uint64_t N,
     frontier_summary_kernel<0><<<sg, 256, 0, st>>>(f, N);
   const uint64_t chunks = (N + kScanThreads - 1) / kScanThreads;
   const uint32_t grid = (uint32_t)(chunks < kScanGrid ? chunks : kScanGrid);
-#define GOSSIP_SCAN(MJ, MD) frontier_scan_kernel<MJ, MD><<<grid, kScanThreads, 0, st>>>(f, S, N, R, k, t, key0, key1)
+  // contiguous node range per block, a multiple of the block width (so lanes map to bitmap bits)
+  const uint64_t per = ((N + grid - 1) / grid + kScanThreads - 1) / kScanThreads * kScanThreads;
+#define GOSSIP_SCAN(MJ, MD) \
+  frontier_scan_kernel<MJ, MD><<<grid, kScanThreads, 0, st>>>(f, S, N, R, k, t, key0, key1, per)
   switch (maj * 4 + mode) {
     case 1: GOSSIP_SCAN(0, 1); break;
     case 2: GOSSIP_SCAN(0, 2); break;
@@ -280,7 +437,10 @@ hipError_t launch_frontier_round(const FrontierBufs& f, uint64_t* S, uint64_t N,
     default: return hipErrorInvalidValue;
   }
 #undef GOSSIP_SCAN
-  frontier_commit_kernel<false><<<commit_grid(N), kCommitThreads, 0, st>>>(f, S, N, partial, R, flags);
+  const uint64_t wchunks = (((N + 63) >> 6) + 63) >> 6;  // 64-group chunks, one per wave
+  const uint64_t cblocks = (wchunks + kCommitThreads / 64 - 1) / (kCommitThreads / 64);
+  frontier_commit_kernel<<<(uint32_t)(cblocks < 4096 ? cblocks : 4096), kCommitThreads, 0, st>>>(f, S, N, partial,
+                                                                                                 R, flags);
   return hipGetLastError();
 }
 

@@ -8,17 +8,15 @@ import csv
 import sys
 
 path = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof/run_kernel_trace.csv"
-SHORT = {"bin_emit_kernel": "emit", "transpose_u16_kernel": "u16", "bin_serve_kernel": "serve",
+SHORT = {"bin_count_kernel": "count", "bin_emit_kernel": "emit", "transpose_u16_kernel": "u16", "bin_serve_kernel": "serve",
          "bin_apply_kernel": "apply", "frontier_summary_kernel": "summ", "frontier_scan_kernel": "scan",
-         "frontier_commit_kernel<true>": "rebuild", "frontier_commit_kernel<false>": "commit"}
+         "frontier_rebuild_kernel": "rebuild", "frontier_commit_kernel": "commit", "frontier_inject_kernel": "inject"}
 STARTS = ("emit", "summ", "rebuild")
 
 
 def short(name):
     base = name.replace("(anonymous namespace)::", "").split("(")[0]
     base = base.split("::")[-1]
-    if base.startswith("frontier_commit_kernel"):
-        return SHORT["frontier_commit_kernel<true>" if "<true>" in base else "frontier_commit_kernel<false>"]
     return SHORT.get(base.split("<")[0])
 
 
@@ -34,9 +32,9 @@ for x in ks:
     cur.append(x)
 if cur:
     rounds.append(cur)
-# last step = trailing rounds after the last rebuild (one per step, after inject)
-cut = max((i for i, r in enumerate(rounds) if r[0][1] == "rebuild"), default=0)
-if cut == 0 and len(rounds) > 1:
+# last step = trailing rounds after the largest gap (the host-side reset/inject between steps)
+cut = 0
+if len(rounds) > 1:
     gaps = [(rounds[i + 1][0][0] - rounds[i][-1][0], i) for i in range(len(rounds) - 1)]
     cut = max(gaps)[1] + 1
 tot = 0
