@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "round.h"
+
 namespace gossip {
 
 constexpr uint32_t kTileD = 16384;   // destination tile (nodes): one 128 KiB LDS image of u64 words
@@ -41,9 +43,11 @@ struct BinBufs {
 size_t bin_bytes(const BinGeom& g);
 void bin_carve(const BinGeom& g, void* base, BinBufs* b);
 
-// One round S -> Snext with stats partials (same layout as stats_kernel's).
-hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, const uint64_t* S, uint64_t* Snext,
-                               uint64_t* partial, uint32_t R, uint32_t t, uint32_t key0, uint32_t key1,
-                               uint32_t mode, uint32_t flags, hipStream_t st, hipEvent_t* marks);
+// One dense round, in place on S.  The totals in partial are cleared and
+// recomputed (layout as stats_kernel's plus [4+R] = nonzero nodes); the last
+// apply block hands them to the host through rs.
+hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, uint64_t* partial, uint32_t R,
+                               uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t flags,
+                               const RoundSync& rs, hipStream_t st);
 
 }  // namespace gossip

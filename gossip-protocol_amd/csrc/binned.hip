@@ -25,8 +25,7 @@
 // order inside a run (decided by LDS atomics) never changes a result bit.
 #include "binned.h"
 #include "philox.h"
-
-#include <cstdlib>
+#include "round.h"
 
 namespace gossip {
 
@@ -204,7 +203,11 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
 }
 
 __global__ __launch_bounds__(256) void transpose_u16_kernel(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
-                                                             uint32_t rows, uint32_t cols) {
+                                                             uint32_t rows, uint32_t cols,
+                                                             uint64_t* __restrict__ partial, uint32_t plen) {
+  // the dense round's stats are absolute: clear the totals before K3 adds to them
+  if (blockIdx.x == 0 && blockIdx.y == 0)
+    for (uint32_t i = threadIdx.y * 32 + threadIdx.x; i < plen; i += 256) partial[i] = 0;
   // in [rows][cols] -> out [cols][rows]
   __shared__ uint16_t tile[32][33];
   const uint32_t c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
@@ -424,10 +427,10 @@ __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, cons
 // K3 — one block per tile X: acc = S_t[X]; OR in the pushes aimed at X (its
 // runs) and the pull responses owed to X's own senders (their regions, read
 // sequentially); write S_{t+1}[X] and fold the stats.
-__global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, const uint64_t* __restrict__ S,
-                                                                  uint64_t* __restrict__ Snext, BinBufs b,
+__global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, const uint64_t* S,
+                                                                  uint64_t* Snext, BinBufs b,  // may alias S
                                                                   uint64_t* __restrict__ partial, uint32_t R,
-                                                                  uint32_t mode, uint32_t flags, uint32_t exp) {
+                                                                  uint32_t mode, uint32_t flags) {
   __shared__ unsigned long long acc[kTileD];
   __shared__ uint32_t cnt[64];
   __shared__ uint64_t red_hash[kTileThreads / 64];
@@ -438,14 +441,14 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, cons
   const uint32_t tid = threadIdx.x;
   const uint32_t X = xcd_remap(blockIdx.x, g.nt_d);
   const uint64_t node0 = (uint64_t)X << kTileDLog;
-  if (!(exp & 32u)) load_tile(acc, S, node0, g.N);
+  load_tile(acc, S, node0, g.N);
   if (tid < 64) cnt[tid] = 0;
   __syncthreads();
   const uint32_t* __restrict__ gids = b.ids;
   const uint64_t* __restrict__ gvals = b.vals;
   const uint64_t* __restrict__ gresp = b.resp;
   const uint64_t fm = full_mask1(R);
-  if ((mode == 1 || mode == 3) && !(exp & 4u)) {  // pushes aimed at this tile
+  if (mode == 1 || mode == 3) {  // pushes aimed at this tile
     const uint16_t* rowb = b.offT + (size_t)X * g.nt_s;
     for_each_run_record<kUnroll>(g, rowb, rowb + g.nt_s, wmask, wlist, [&](const int32_t* rec) {
       uint32_t id[kUnroll];
@@ -464,7 +467,7 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, cons
       }
     });
   }
-  if ((mode == 2 || mode == 3) && !(exp & 8u)) {  // responses owed to this tile's own senders
+  if (mode == 2 || mode == 3) {  // responses owed to this tile's own senders
     const uint32_t per = kTileD >> g.ts_log;
     const uint32_t s0 = X * per, s1 = min(s0 + per, g.nt_s);
     for (uint32_t s = s0; s < s1; ++s) {
@@ -492,10 +495,6 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, cons
     }
   }
   __syncthreads();
-  if (exp & 16u) {  // timing experiment: store only
-    for (uint32_t q = 0; q < kTileD / kTileThreads; ++q) Snext[node0 + q * kTileThreads + tid] = acc[q * kTileThreads + tid];
-    return;
-  }
   tile_epilogue(acc, node0, g.N, Snext, partial, R, flags, cnt, red_hash, red_full, red_nz, b.nzb, b.fullb);
 }
 
@@ -545,23 +544,21 @@ void bin_carve(const BinGeom& g, void* base, BinBufs* b) {
   b->offT = (uint16_t*)p;
 }
 
-hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, const uint64_t* S, uint64_t* Snext,
-                               uint64_t* partial, uint32_t R, uint32_t t, uint32_t key0, uint32_t key1,
-                               uint32_t mode, uint32_t flags, hipStream_t st, hipEvent_t* marks) {
-  (void)marks;
+hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, uint64_t* partial, uint32_t R,
+                               uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t flags,
+                               const RoundSync& rs, hipStream_t st) {
   const uint32_t eg = g.nt_s < kEmitGrid ? g.nt_s : kEmitGrid;  // persistent: one block per CU
   if (g.k <= 2)
     bin_emit_kernel<2><<<eg, kEmitThreads, 0, st>>>(g, S, b, R, t, key0, key1, mode);
   else
     bin_emit_kernel<0><<<eg, kEmitThreads, 0, st>>>(g, S, b, R, t, key0, key1, mode);
   const dim3 tg((g.nt_d + 1 + 31) / 32, (g.nt_s + 31) / 32);
-  transpose_u16_kernel<<<tg, dim3(32, 8), 0, st>>>(b.off, b.offT, g.nt_s, g.nt_d + 1);
-  const bool pull = mode == 2 || mode == 3;
-  // expected records per tile = k * kTileD: keep them in registers when they fit
-  if (pull) bin_serve_kernel<<<g.nt_d, kTileThreads, 0, st>>>(g, S, b, R);
-  const char* xs = getenv("GOSSIP_EXPERIMENT");  // timing experiments only: results are wrong when set
-  const uint32_t exp = xs ? (uint32_t)atoi(xs) : 0u;
-  bin_apply_kernel<<<g.nt_d, kTileThreads, 0, st>>>(g, S, Snext, b, partial, R, mode, flags, exp);
+  transpose_u16_kernel<<<tg, dim3(32, 8), 0, st>>>(b.off, b.offT, g.nt_s, g.nt_d + 1, partial, rs.plen);
+  if (mode == 2 || mode == 3) bin_serve_kernel<<<g.nt_d, kTileThreads, 0, st>>>(g, S, b, R);
+  // in place: K3 of tile X reads and writes only S[X] (push values and pull
+  // responses come from the record buffers), and K1/K2 have finished reading S_t
+  bin_apply_kernel<<<g.nt_d, kTileThreads, 0, st>>>(g, S, S, b, partial, R, mode, flags);
+  return launch_round_snapshot(partial, rs, st);
   return hipGetLastError();
 }
 

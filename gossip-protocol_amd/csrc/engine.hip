@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstring>
 #include <algorithm>
+#include <atomic>
 #include <string>
 #include <vector>
 
@@ -18,6 +19,10 @@
 #include "antientropy.h"
 #include "binned.h"
 #include "frontier.h"
+#include "round.h"
+
+#include <cmath>
+#include <immintrin.h>
 #include "kernels.h"
 #include "philox.h"
 
@@ -72,11 +77,14 @@ struct gossip_engine {
   FrontierBufs fb{};
   void* fr_mem = nullptr;
   bool fr_valid = false;          // partial_d holds the totals of S and the bitmaps are exact
-  bool tot_stale = false;         // partial_d moved on the device (inject) since tot was read
-  bool inplace = false;           // the last computed round updated S in place (no buffer flip)
   double sparse_frac = 1.0 / 16;  // rare fraction at or below which a round runs sparse
-  std::vector<uint64_t> tot;      // host copy of the totals of S [5 + R]
-  uint64_t sparse_rounds = 0;
+  // pipelined rounds (binned engines): the host picks each round's path from the
+  // totals it has read, predicted forward over the rounds still in flight, and
+  // stays up to `ahead` rounds in front
+  uint64_t* ring_h = nullptr;  // [kRing][part_len + 1] host-mapped totals + sequence word per round
+  uint64_t* ring_d = nullptr;
+  uint64_t seq = 0;
+  uint32_t ahead = 2;
 
   hipEvent_t ev[kTimers][2] = {};
   double time_ms[kTimers] = {0, 0};
@@ -129,6 +137,7 @@ void free_all(gossip_engine* e) {
   for (void* b : ae)
     if (b) (void)hipFree(b);
   if (e->partial_h) (void)hipHostFree(e->partial_h);
+  if (e->ring_h) (void)hipHostFree(e->ring_h);
   for (auto& p : e->ev)
     for (auto& x : p)
       if (x) (void)hipEventDestroy(x);
@@ -241,6 +250,168 @@ AeArgs make_ae_args(gossip_engine* e) {
   return a;
 }
 
+constexpr uint32_t kRing = 8;
+
+// Binned engines: make partial_d hold the exact totals of S (and the bitmaps
+// exact) when an untracked write (plain inject) left them stale.
+int prepare_planned(gossip_engine* e) {
+  if (!e->frontier || e->fr_valid) return GOSSIP_OK;
+  HIP_OK(e, hipMemsetAsync(e->partial_d, 0, part_len(e) * 8, e->stream));
+  HIP_OK(e, launch_frontier_rebuild(e->fb, e->S, e->N, e->partial_d, e->R, e->cfg.flags, e->stream));
+  e->fr_valid = true;
+  return GOSSIP_OK;
+}
+
+// Totals the path choice needs: full and nonzero counts, per-rumor infected.
+struct Est {
+  double full = 0, nz = 0;
+  std::vector<double> inf;
+};
+
+Est est_of(const gossip_engine* e, const uint64_t* tot) {
+  Est x;
+  x.full = (double)tot[0];
+  x.nz = (double)tot[4 + e->R];
+  x.inf.assign(tot + 4, tot + 4 + e->R);
+  return x;
+}
+
+// One round of the mean-field model of the random modes, per rumor: a node
+// misses rumor r after the round iff it held no copy, none of its k pulls hit a
+// holder (u^k) and no holder pushed to it (e^{-k(1-u)}).  Only steers the path
+// choice, never a result.
+Est predict(const gossip_engine* e, const Est& x) {
+  Est y;
+  const double N = (double)e->N, k = (double)e->k;
+  const bool push = e->mode == GOSSIP_MODE_PUSH || e->mode == GOSSIP_MODE_PUSHPULL;
+  const bool pull = e->mode == GOSSIP_MODE_PULL || e->mode == GOSSIP_MODE_PUSHPULL;
+  double all_miss = 1.0, all_hit = 1.0;
+  y.inf.resize(x.inf.size());
+  for (size_t r = 0; r < x.inf.size(); ++r) {
+    const double u = 1.0 - x.inf[r] / N;
+    double v = u;
+    if (pull) v *= std::pow(u, k);
+    if (push) v *= std::exp(-k * (1.0 - u));
+    y.inf[r] = (1.0 - v) * N;
+    all_miss *= v;
+    all_hit *= 1.0 - v;
+  }
+  y.nz = N * (1.0 - all_miss);
+  y.full = N * all_hit;
+  return y;
+}
+
+// sparse when the smaller rare class is at most sparse_frac * N; maj = which class is rare
+bool choose_sparse(const gossip_engine* e, const Est& x, uint32_t* maj) {
+  if (!e->frontier) return false;
+  const double lo = x.nz, hi = (double)e->N - x.full;
+  *maj = hi < lo ? 1u : 0u;
+  return std::min(lo, hi) <= e->sparse_frac * (double)e->N;
+}
+
+RoundSync ring_sync(gossip_engine* e, uint32_t slot) {
+  RoundSync rs;
+  rs.ring = e->ring_d + (size_t)slot * (part_len(e) + 1);
+  rs.plen = (uint32_t)part_len(e);
+  rs.seq = (uint32_t)++e->seq;
+  return rs;
+}
+
+int launch_round_path(gossip_engine* e, uint32_t t, bool sparse, uint32_t maj, const RoundSync& rs) {
+  if (sparse)
+    HIP_OK(e, launch_frontier_round(e->fb, e->S, e->N, e->partial_d, e->R, e->k, t, e->key0, e->key1, e->mode, maj,
+                                    e->cfg.flags, rs, e->stream));
+  else
+    HIP_OK(e, launch_binned_round(e->bg, e->bb, e->S, e->partial_d, e->R, t, e->key0, e->key1, e->mode,
+                                  e->cfg.flags, rs, e->stream));
+  return GOSSIP_OK;
+}
+
+// Waits until ring slot `slot` carries sequence `want` (the round's last block
+// wrote it), polling host memory; a stream error ends the wait.
+int wait_slot(gossip_engine* e, uint32_t slot, uint64_t want) {
+  volatile uint64_t* sq = e->ring_h + (size_t)slot * (part_len(e) + 1) + part_len(e);
+  for (uint64_t spin = 0; *sq != want; ++spin) {
+    _mm_pause();
+    if ((spin & 4095) == 4095) {
+      const hipError_t q = hipStreamQuery(e->stream);
+      if (q != hipSuccess && q != hipErrorNotReady)
+        return e->fail(GOSSIP_EHIP, "round kernels failed: %s", hipGetErrorString(q));
+      if (q == hipSuccess && *sq != want) return e->fail(GOSSIP_EHIP, "round %llu never reported",
+                                                        (unsigned long long)want);
+    }
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  return GOSSIP_OK;
+}
+
+int read_totals(gossip_engine* e, std::vector<uint64_t>* out) {
+  HIP_OK(e, hipMemcpyAsync(e->partial_h, e->partial_d, part_len(e) * 8, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(e, hipStreamSynchronize(e->stream));
+  out->assign(e->partial_h, e->partial_h + part_len(e));
+  return GOSSIP_OK;
+}
+
+// gossip_step for binned engines.  Round r's path is chosen from the last totals
+// read (S after round done-1) predicted forward over the rounds still in
+// flight; rounds past convergence find nothing rare and return at once, and are
+// not counted.  Timer 0 brackets the whole step (per-round device time
+// including the gaps between rounds).
+int step_planned(gossip_engine* e, uint32_t max_rounds, gossip_round_stats_t* stats, uint64_t* infected,
+                 uint32_t* rounds_done) {
+  if (int rc = prepare_planned(e)) return rc;
+  std::vector<uint64_t> t0tot;
+  if (int rc = read_totals(e, &t0tot)) return rc;
+  Est base = est_of(e, t0tot.data());
+  const size_t pl = part_len(e);
+  const uint32_t t0 = e->t;
+  std::vector<uint64_t> want(kRing, 0);
+  uint32_t launched = 0, done = 0;
+  bool stop = false;
+  if (e->timing) HIP_OK(e, hipEventRecord(e->ev[0][0], e->stream));
+  while (done < max_rounds) {
+    while (!stop && launched < max_rounds && launched - done < e->ahead) {
+      Est x = base;
+      for (uint32_t i = done; i < launched; ++i) x = predict(e, x);
+      uint32_t maj = 0;
+      const bool sparse = choose_sparse(e, x, &maj);
+      const uint32_t slot = launched % kRing;
+      const RoundSync rs = ring_sync(e, slot);
+      want[slot] = rs.seq;
+      if (int rc = launch_round_path(e, t0 + launched, sparse, maj, rs)) return rc;
+      ++launched;
+    }
+    if (done == launched) break;
+    const uint32_t slot = done % kRing;
+    if (int rc = wait_slot(e, slot, want[slot])) return rc;
+    const uint64_t* tot = e->ring_h + (size_t)slot * (pl + 1);
+    gossip_round_stats_t st;
+    st.round = t0 + done;
+    st.full_nodes = tot[0];
+    st.alive_nodes = e->N;
+    st.converged = tot[0] == e->N ? 1u : 0u;
+    st.messages = 0;
+    st.state_hash = (e->cfg.flags & GOSSIP_FLAG_HASH) ? tot[3] : 0;
+    if (stats) stats[done] = st;
+    if (infected) std::memcpy(infected + (size_t)done * e->R, tot + 4, (size_t)e->R * 8);
+    base = est_of(e, tot);
+    ++done;
+    if (st.converged) stop = true;
+    if (stop) break;
+  }
+  if (e->timing) HIP_OK(e, hipEventRecord(e->ev[0][1], e->stream));
+  HIP_OK(e, hipStreamSynchronize(e->stream));
+  if (e->timing) {
+    float ms = 0.f;
+    HIP_OK(e, hipEventElapsedTime(&ms, e->ev[0][0], e->ev[0][1]));
+    e->time_ms[0] += ms;
+    e->launches[0] += done;
+  }
+  e->t = t0 + done;
+  if (rounds_done) *rounds_done = done;
+  return GOSSIP_OK;
+}
+
 // compute S_{t+1} of the owned shard from the gathered image + partial stats (device)
 int compute_round(gossip_engine* e, const uint64_t* gathered) {
   const size_t bytes = (size_t)e->W * e->Nl * 8;
@@ -262,40 +433,15 @@ int compute_round(gossip_engine* e, const uint64_t* gathered) {
     if ((rc = timer_begin(e, 0))) return rc;
     HIP_OK(e, launch_round_flood(a, e->stream));
     if ((rc = timer_end(e, 0))) return rc;
-  } else if (e->binned) {
+  } else if (e->binned) {  // one round, path chosen from the exact totals of S_t
+    if ((rc = prepare_planned(e))) return rc;
+    std::vector<uint64_t> tot;
+    if ((rc = read_totals(e, &tot))) return rc;
+    uint32_t maj = 0;
+    const bool sparse = choose_sparse(e, est_of(e, tot.data()), &maj);
     if ((rc = timer_begin(e, 0))) return rc;
-    e->inplace = false;
-    if (e->frontier) {
-      if (!e->fr_valid) {  // after reset/inject: totals and bitmaps of S from scratch
-        HIP_OK(e, hipMemsetAsync(e->partial_d, 0, part_len(e) * 8, e->stream));
-        HIP_OK(e, launch_frontier_rebuild(e->fb, e->S, e->N, e->partial_d, e->R, e->cfg.flags, e->stream));
-        HIP_OK(e, hipMemcpyAsync(e->partial_h, e->partial_d, part_len(e) * 8, hipMemcpyDeviceToHost, e->stream));
-        HIP_OK(e, hipStreamSynchronize(e->stream));
-        e->tot.assign(e->partial_h, e->partial_h + part_len(e));
-        e->fr_valid = true;
-        e->tot_stale = false;
-      } else if (e->tot_stale) {  // after inject: the device totals are exact, the host copy is not
-        HIP_OK(e, hipMemcpyAsync(e->partial_h, e->partial_d, part_len(e) * 8, hipMemcpyDeviceToHost, e->stream));
-        HIP_OK(e, hipStreamSynchronize(e->stream));
-        e->tot.assign(e->partial_h, e->partial_h + part_len(e));
-        e->tot_stale = false;
-      }
-      const uint64_t nz = e->tot[4 + e->R], full = e->tot[0];
-      const uint64_t rare_lo = nz, rare_hi = e->N - full, lim = (uint64_t)(e->sparse_frac * (double)e->N);
-      if (std::min(rare_lo, rare_hi) <= lim) {
-        // partial_d already holds the totals of S_t: the round adds its deltas
-        HIP_OK(e, launch_frontier_round(e->fb, e->S, e->N, e->partial_d, e->R, e->k, e->t, e->key0, e->key1, e->mode,
-                                        rare_hi < rare_lo ? 1u : 0u, e->cfg.flags, e->stream));
-        e->inplace = true;
-        e->sparse_rounds++;
-        return timer_end(e, 0);
-      }
-    }
-    HIP_OK(e, hipMemsetAsync(e->partial_d, 0, part_len(e) * 8, e->stream));
-    HIP_OK(e, launch_binned_round(e->bg, e->bb, gathered, e->Snext, e->partial_d, e->R, e->t, e->key0, e->key1,
-                                  e->mode, e->cfg.flags, e->stream, nullptr));
-    if ((rc = timer_end(e, 0))) return rc;
-    return GOSSIP_OK;  // stats are fused into the apply kernel
+    if ((rc = launch_round_path(e, e->t, sparse, maj, ring_sync(e, 0)))) return rc;
+    return timer_end(e, 0);  // stats are fused into the round kernels
   } else {
     // timer 0 covers the whole S_t -> S_{t+1} transform (seed copy + round kernel)
     if ((rc = timer_begin(e, 0))) return rc;
@@ -318,7 +464,7 @@ void rotate(gossip_engine* e) {
     e->Sprev = e->S;
     e->S = e->Snext;
     e->Snext = tmp;
-  } else if (!e->inplace) {
+  } else if (!e->binned) {  // binned rounds run in place
     e->cur ^= 1;
     bind_slices(e);
   }
@@ -481,6 +627,13 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
       e->frontier = true;
       if (const char* f = getenv("GOSSIP_SPARSE_FRAC")) e->sparse_frac = atof(f);
     }
+    if (const char* a = getenv("GOSSIP_AHEAD")) e->ahead = std::max(1, std::min((int)kRing - 1, atoi(a)));
+    if (hipHostMalloc((void**)&e->ring_h, kRing * (part_len(e) + 1) * 8, hipHostMallocMapped) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&e->ring_d, e->ring_h, 0) != hipSuccess) {
+      e->err = "round ring allocation failed";
+      return bail(GOSSIP_ENOMEM);
+    }
+    std::memset(e->ring_h, 0, kRing * (part_len(e) + 1) * 8);
   }
   if (hipHostMalloc((void**)&e->partial_h, part_len(e) * 8, hipHostMallocDefault) != hipSuccess) {
     e->err = "hipHostMalloc failed";
@@ -590,9 +743,7 @@ int gossip_reset(gossip_engine_t* e) {
     HIP_OK(e, hipMemsetAsync(e->fb.nzb, 0, nwb, e->stream));
     HIP_OK(e, hipMemsetAsync(e->fb.fullb, 0, nwb, e->stream));
     HIP_OK(e, hipMemsetAsync(e->partial_d, 0, part_len(e) * 8, e->stream));
-    e->tot.assign(part_len(e), 0);
     e->fr_valid = true;
-    e->tot_stale = false;
   }
   e->t = 0;
   return GOSSIP_OK;
@@ -610,7 +761,6 @@ int gossip_inject(gossip_engine_t* e, uint64_t node, uint32_t rumor) {
   if (e->frontier && e->fr_valid) {
     HIP_OK(e, launch_frontier_inject(e->fb, e->S, e->N, e->partial_d, e->R, e->key0, e->key1, (int64_t)node, rumor,
                                      e->cfg.flags, e->stream));
-    e->tot_stale = true;
     return GOSSIP_OK;
   }
   HIP_OK(e, launch_inject(e->S, e->Nl, e->lo, e->hi, e->N, e->R, e->key0, e->key1, (int64_t)node, rumor, e->stream));
@@ -628,7 +778,6 @@ int gossip_inject_random(gossip_engine_t* e) {
   if (e->frontier && e->fr_valid) {
     HIP_OK(e, launch_frontier_inject(e->fb, e->S, e->N, e->partial_d, e->R, e->key0, e->key1, -1, 0, e->cfg.flags,
                                      e->stream));
-    e->tot_stale = true;
     return GOSSIP_OK;
   }
   HIP_OK(e, launch_inject(e->S, e->Nl, e->lo, e->hi, e->N, e->R, e->key0, e->key1, -1, 0, e->stream));
@@ -660,7 +809,6 @@ int gossip_round_compute(gossip_engine_t* e, uint64_t* partial) {
   HIP_OK(e, hipMemcpyAsync(e->partial_h, e->partial_d, part_len(e) * 8, hipMemcpyDeviceToHost, e->stream));
   HIP_OK(e, hipStreamSynchronize(e->stream));
   if (int rc = timer_collect(e)) return rc;
-  if (e->frontier) e->tot.assign(e->partial_h, e->partial_h + part_len(e));
   std::memcpy(partial, e->partial_h, (4 + e->R) * 8);
   if (e->mode != GOSSIP_MODE_ANTIENTROPY) partial[1] = e->nown;
   return GOSSIP_OK;
@@ -681,6 +829,7 @@ int gossip_step(gossip_engine_t* e, uint32_t max_rounds, gossip_round_stats_t* s
   if (e->G != 1) return e->fail(GOSSIP_ESTATE, "gossip_step drives one shard; use the round_* calls for G > 1");
   if (e->mode == GOSSIP_MODE_FLOOD && !e->has_topo) return e->fail(GOSSIP_ESTATE, "FLOOD needs a topology");
   if (int rc = set_dev(e)) return rc;
+  if (e->binned) return step_planned(e, max_rounds, stats, infected, rounds_done);
   std::vector<uint64_t> part(4 + e->R);
   uint32_t r = 0;
   while (r < max_rounds) {

@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "round.h"
+
 namespace gossip {
 
 constexpr uint32_t kSummBits = 1u << 20;  // LDS summary: at most 2^20 bits (128 KiB)
@@ -42,10 +44,12 @@ hipError_t launch_frontier_inject(const FrontierBufs& f, uint64_t* S, uint64_t N
                                   hipStream_t st);
 
 // One sparse round, in place on S.  maj = 0: rare = nonzero nodes; maj = 1:
-// rare = nodes not yet full.  partial holds the totals of S_t on entry and
-// those of S_{t+1} on exit.
+// rare = nodes not yet full (either choice is exact; it only moves time).
+// partial holds the totals of S_t on entry and those of S_{t+1} on exit; the
+// last commit block hands them to the host through rs.  With no rare node the
+// round is a no-op (every kernel returns at once).
 hipError_t launch_frontier_round(const FrontierBufs& f, uint64_t* S, uint64_t N, uint64_t* partial, uint32_t R,
                                  uint32_t k, uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t maj,
-                                 uint32_t flags, hipStream_t st);
+                                 uint32_t flags, const RoundSync& rs, hipStream_t st);
 
 }  // namespace gossip

@@ -27,6 +27,7 @@
 // both bitmaps from S (after inject/reset or a direct-path round).
 #include "frontier.h"
 #include "philox.h"
+#include "round.h"
 #include "wave.h"
 
 namespace gossip {
@@ -52,7 +53,7 @@ __device__ __forceinline__ uint64_t rare_word(const FrontierBufs& f, uint64_t w,
 }
 
 template <int MAJ>
-__global__ __launch_bounds__(256) void frontier_summary_kernel(FrontierBufs f, uint64_t N) {
+__device__ __forceinline__ void summary_body(const FrontierBufs& f, uint64_t N) {
   const uint32_t s = blockIdx.x * 256 + threadIdx.x;
   if (s >= f.summ_words) return;
   const uint64_t nwords = (N + 63) >> 6;
@@ -84,6 +85,20 @@ __global__ __launch_bounds__(256) void frontier_summary_kernel(FrontierBufs f, u
   f.summ[s] = out;
 }
 
+// number of rare nodes of S_t from the running totals (0: the round is a no-op)
+__device__ __forceinline__ uint64_t rare_count(const uint64_t* partial, uint64_t N, uint32_t R, uint32_t maj) {
+  return maj ? N - partial[0] : partial[4 + R];
+}
+
+__global__ __launch_bounds__(256) void frontier_summary_kernel(FrontierBufs f, uint64_t N, const uint64_t* partial,
+                                                                uint32_t R, uint32_t maj) {
+  if (rare_count(partial, N, R, maj) == 0) return;
+  if (maj)
+    summary_body<1>(f, N);
+  else
+    summary_body<0>(f, N);
+}
+
 // K1.  MODE: 1 push, 2 pull, 3 push-pull.  MAJ: majority value 0 (0) or full (1).
 // Each block owns a contiguous node range; the rare-bitmap words of the next
 // 64K nodes are staged in LDS so the per-node test never waits on memory.
@@ -91,12 +106,9 @@ __global__ __launch_bounds__(256) void frontier_summary_kernel(FrontierBufs f, u
 // (the bitmap is L2-resident; S is not).  Pull deltas belong to the node's own
 // lane and are plain stores to P; push deltas are atomic ORs into D.
 template <int MAJ, int MODE>
-__global__ __launch_bounds__(kScanThreads) void frontier_scan_kernel(FrontierBufs f, const uint64_t* __restrict__ S,
-                                                                      uint64_t N, uint32_t R, uint32_t k, uint32_t t,
-                                                                      uint32_t key0, uint32_t key1,
-                                                                      uint64_t per_block) {
-  __shared__ uint4 summ4[kSummBits / 128];
-  __shared__ uint64_t rws[kRwWords];
+__device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const FrontierBufs& f,
+                                          const uint64_t* __restrict__ S, uint64_t N, uint32_t R, uint32_t k,
+                                          uint32_t t, uint32_t key0, uint32_t key1, uint64_t per_block) {
   const uint32_t* summ = (const uint32_t*)summ4;
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t n4 = (f.summ_words + 3) / 4;
@@ -195,6 +207,20 @@ __global__ __launch_bounds__(kScanThreads) void frontier_scan_kernel(FrontierBuf
       }
     }
   }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kScanThreads) void frontier_scan_kernel(FrontierBufs f, const uint64_t* __restrict__ S,
+                                                                      uint64_t N, uint32_t R, uint32_t k, uint32_t t,
+                                                                      uint32_t key0, uint32_t key1, uint64_t per_block,
+                                                                      const uint64_t* partial, uint32_t maj) {
+  __shared__ uint4 summ4[kSummBits / 128];
+  __shared__ uint64_t rws[kRwWords];
+  if (rare_count(partial, N, R, maj) == 0) return;  // converged (or nothing injected): nothing moves
+  if (maj)
+    scan_body<1, MODE>(summ4, rws, f, S, N, R, k, t, key0, key1, per_block);
+  else
+    scan_body<0, MODE>(summ4, rws, f, S, N, R, k, t, key0, key1, per_block);
 }
 
 // Stats of one 64-node group whose words went from old to nw (old == 0 in a
@@ -415,33 +441,23 @@ hipError_t launch_frontier_inject(const FrontierBufs& f, uint64_t* S, uint64_t N
 
 hipError_t launch_frontier_round(const FrontierBufs& f, uint64_t* S, uint64_t N, uint64_t* partial, uint32_t R,
                                  uint32_t k, uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t maj,
-                                 uint32_t flags, hipStream_t st) {
-  const uint32_t sg = (f.summ_words + 255) / 256;
-  if (maj)
-    frontier_summary_kernel<1><<<sg, 256, 0, st>>>(f, N);
-  else
-    frontier_summary_kernel<0><<<sg, 256, 0, st>>>(f, N);
+                                 uint32_t flags, const RoundSync& rs, hipStream_t st) {
+  frontier_summary_kernel<<<(f.summ_words + 255) / 256, 256, 0, st>>>(f, N, partial, R, maj);
   const uint64_t chunks = (N + kScanThreads - 1) / kScanThreads;
   const uint32_t grid = (uint32_t)(chunks < kScanGrid ? chunks : kScanGrid);
   // contiguous node range per block, a multiple of the block width (so lanes map to bitmap bits)
   const uint64_t per = ((N + grid - 1) / grid + kScanThreads - 1) / kScanThreads * kScanThreads;
-#define GOSSIP_SCAN(MJ, MD) \
-  frontier_scan_kernel<MJ, MD><<<grid, kScanThreads, 0, st>>>(f, S, N, R, k, t, key0, key1, per)
-  switch (maj * 4 + mode) {
-    case 1: GOSSIP_SCAN(0, 1); break;
-    case 2: GOSSIP_SCAN(0, 2); break;
-    case 3: GOSSIP_SCAN(0, 3); break;
-    case 5: GOSSIP_SCAN(1, 1); break;
-    case 6: GOSSIP_SCAN(1, 2); break;
-    case 7: GOSSIP_SCAN(1, 3); break;
+  switch (mode) {
+    case 1: frontier_scan_kernel<1><<<grid, kScanThreads, 0, st>>>(f, S, N, R, k, t, key0, key1, per, partial, maj); break;
+    case 2: frontier_scan_kernel<2><<<grid, kScanThreads, 0, st>>>(f, S, N, R, k, t, key0, key1, per, partial, maj); break;
+    case 3: frontier_scan_kernel<3><<<grid, kScanThreads, 0, st>>>(f, S, N, R, k, t, key0, key1, per, partial, maj); break;
     default: return hipErrorInvalidValue;
   }
-#undef GOSSIP_SCAN
   const uint64_t wchunks = (((N + 63) >> 6) + 63) >> 6;  // 64-group chunks, one per wave
   const uint64_t cblocks = (wchunks + kCommitThreads / 64 - 1) / (kCommitThreads / 64);
   frontier_commit_kernel<<<(uint32_t)(cblocks < 4096 ? cblocks : 4096), kCommitThreads, 0, st>>>(f, S, N, partial,
                                                                                                  R, flags);
-  return hipGetLastError();
+  return launch_round_snapshot(partial, rs, st);
 }
 
 }  // namespace gossip

@@ -7,6 +7,7 @@
 // OR is commutative, associative and idempotent, so the atomics below give a
 // schedule-independent, bit-exact result.
 #include "kernels.h"
+#include "round.h"
 #include "philox.h"
 
 namespace gossip {
@@ -294,6 +295,24 @@ hipError_t launch_hash(const uint64_t* S, uint64_t Nl, uint64_t nown, uint32_t W
 hipError_t launch_philox(const uint32_t* ctr, uint32_t k0, uint32_t k1, uint32_t* out, uint32_t n, hipStream_t st) {
   if (n == 0) return hipSuccess;
   philox_kernel<<<(n + 255) / 256, 256, 0, st>>>(ctr, k0, k1, out, n);
+  return hipGetLastError();
+}
+
+namespace {
+
+__global__ __launch_bounds__(64) void round_snapshot_kernel(const uint64_t* __restrict__ partial, RoundSync rs) {
+  for (uint32_t i = threadIdx.x; i < rs.plen; i += 64) rs.ring[i] = partial[i];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();  // totals visible to the host before the sequence word
+    __atomic_store_n(&rs.ring[rs.plen], (uint64_t)rs.seq, __ATOMIC_RELEASE);
+  }
+}
+
+}  // namespace
+
+hipError_t launch_round_snapshot(const uint64_t* partial, const RoundSync& rs, hipStream_t st) {
+  round_snapshot_kernel<<<1, 64, 0, st>>>(partial, rs);
   return hipGetLastError();
 }
 

@@ -10,8 +10,8 @@ import sys
 path = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof/run_kernel_trace.csv"
 SHORT = {"bin_count_kernel": "count", "bin_emit_kernel": "emit", "transpose_u16_kernel": "u16", "bin_serve_kernel": "serve",
          "bin_apply_kernel": "apply", "frontier_summary_kernel": "summ", "frontier_scan_kernel": "scan",
-         "frontier_rebuild_kernel": "rebuild", "frontier_commit_kernel": "commit", "frontier_inject_kernel": "inject"}
-STARTS = ("emit", "summ", "rebuild")
+         "frontier_rebuild_kernel": "rebuild", "frontier_commit_kernel": "commit", "frontier_inject_kernel": "inject", "round_snapshot_kernel": "snap"}
+STARTS = ("summ", "rebuild")
 
 
 def short(name):
@@ -41,6 +41,7 @@ tot = 0
 for r in rounds[cut:]:
     t = sum(d for _, _, d in r)
     tot += t
-    kind = "sparse" if any(n == "scan" for _, n, _ in r) else "dense "
-    print(kind, " ".join(f"{n}:{d:6.1f}" for _, n, d in r), f" round {t:6.1f} us")
+    # both paths are enqueued every round; the unplanned one's kernels exit at once
+    kind = "sparse" if sum(d for _, n, d in r if n == "scan") > 10 else "dense "
+    print(kind, " ".join(f"{n}:{d:6.1f}" for _, n, d in r if d > 3.0), f" round {t:6.1f} us")
 print(f"rounds {len(rounds) - cut}, kernel time {tot / 1000:.2f} ms")
