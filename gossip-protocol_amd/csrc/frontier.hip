@@ -118,33 +118,33 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
   const uint64_t fm = full_mask1(R), maj = MAJ ? fm : 0ull, nm1 = N - 1;
   const uint32_t glog = f.glog;
   auto summ_bit = [&](uint32_t p) -> bool { return (summ[p >> (glog + 5)] >> ((p >> glog) & 31u)) & 1u; };
-  const uint64_t b0 = (uint64_t)blockIdx.x * per_block, b1 = min(b0 + per_block, N);
-  for (uint64_t c0 = b0; c0 < b1; c0 += (uint64_t)kRwWords * 64) {
-    const uint64_t c1 = min(c0 + (uint64_t)kRwWords * 64, b1);
+  // node ids are < 2^32 (gossip_create checks N), so all index math is 32-bit
+  const uint32_t b0 = blockIdx.x * (uint32_t)per_block, b1 = (uint32_t)min<uint64_t>((uint64_t)b0 + per_block, N);
+  for (uint32_t c0 = b0; c0 < b1; c0 += kRwWords * 64) {
+    const uint32_t c1 = min(c0 + kRwWords * 64, b1);
     __syncthreads();  // previous chunk done with rws
-    for (uint32_t i = tid; i < (uint32_t)((c1 - c0 + 63) >> 6); i += kScanThreads)
-      rws[i] = rare_word<MAJ>(f, (c0 >> 6) + i, N);
+    for (uint32_t i = tid; i < ((c1 - c0 + 63) >> 6); i += kScanThreads) rws[i] = rare_word<MAJ>(f, (c0 >> 6) + i, N);
     __syncthreads();
-    for (uint64_t base = c0; base < c1; base += kScanThreads * kScanUnroll) {
+    for (uint32_t base = c0; base < c1; base += kScanThreads * kScanUnroll) {
       uint64_t x[kScanUnroll], vp[kScanUnroll][4];
       uint32_t pp[kScanUnroll][4], hit[kScanUnroll];
       bool act[kScanUnroll], rn[kScanUnroll];
       // 1. draws and LDS summary tests (no global memory)
 #pragma unroll
       for (int u = 0; u < kScanUnroll; ++u) {
-        const uint64_t n = base + (uint64_t)u * kScanThreads + tid;
+        const uint32_t n = base + u * kScanThreads + tid;
         const bool valid = n < c1;
-        rn[u] = valid && ((rws[valid ? (n - c0) >> 6 : 0] >> lane) & 1ull);
+        rn[u] = valid && ((rws[(n - c0) >> 6] >> lane) & 1ull);
         // a majority node only acts through a rare peer; push from an empty node and
         // pull into a full one are no-ops, so those nodes skip the draws entirely
         act[u] = valid && (rn[u] || !((!kPull && MAJ == 0) || (!kPush && MAJ == 1)));
         hit[u] = 0;
         if (act[u] && k <= 4) {
-          const u32x4 r4 = philox4x32_10(u32x4{(uint32_t)n, t, 0u, 0u}, key0, key1);
+          const u32x4 r4 = philox4x32_10(u32x4{n, t, 0u, 0u}, key0, key1);
 #pragma unroll
           for (uint32_t j = 0; j < 4; ++j) {
             if (j >= k) break;
-            pp[u][j] = peer_from_word(lane_of(r4, j), nm1, (uint32_t)n);
+            pp[u][j] = peer_from_word(lane_of(r4, j), nm1, n);
             if (summ_bit(pp[u][j])) hit[u] |= 1u << j;
           }
         }
@@ -161,7 +161,7 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
       // 3. S_t of the rare ends only (a majority node's value is known)
 #pragma unroll
       for (int u = 0; u < kScanUnroll; ++u) {
-        const uint64_t n = base + (uint64_t)u * kScanThreads + tid;
+        const uint32_t n = base + u * kScanThreads + tid;
         x[u] = rn[u] ? S[n] : maj;
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) vp[u][j] = ((hit[u] >> j) & 1u) ? S[pp[u][j]] : maj;
@@ -170,7 +170,7 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
 #pragma unroll
       for (int u = 0; u < kScanUnroll; ++u) {
         if (!act[u]) continue;
-        const uint64_t n = base + (uint64_t)u * kScanThreads + tid;
+        const uint32_t n = base + u * kScanThreads + tid;
         uint64_t acc = 0;
         auto edge = [&](uint32_t p, uint64_t v) {
           if (kPull) acc |= v;
@@ -191,8 +191,8 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
         } else {
           u32x4 r4{0, 0, 0, 0};
           for (uint32_t j = 0; j < k; ++j) {
-            if ((j & 3u) == 0) r4 = philox4x32_10(u32x4{(uint32_t)n, t, 0u, j >> 2}, key0, key1);
-            const uint32_t p = peer_from_word(lane_of(r4, j & 3u), nm1, (uint32_t)n);
+            if ((j & 3u) == 0) r4 = philox4x32_10(u32x4{n, t, 0u, j >> 2}, key0, key1);
+            const uint32_t p = peer_from_word(lane_of(r4, j & 3u), nm1, n);
             bool rp = summ_bit(p);
             if (rp && glog) rp = (rare_word<MAJ>(f, p >> 6, N) >> (p & 63u)) & 1ull;
             if (!rn[u] && !rp) continue;  // both ends majority: nothing moves

@@ -16,6 +16,15 @@ struct u32x4 {
   uint32_t x, y, z, w;
 };
 
+// a ^ b ^ c: one v_bitop3_b32 (truth table 0x96) on gfx950, which has no v_xor3
+__host__ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+  return a ^ b ^ c;
+#endif
+}
+
 __host__ __device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
@@ -23,7 +32,7 @@ __host__ __device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, ui
     const uint64_t m0 = (uint64_t)0xD2511F53u * c.x, m1 = (uint64_t)0xCD9E8D57u * c.z;
     const uint32_t hi0 = (uint32_t)(m0 >> 32), lo0 = (uint32_t)m0;
     const uint32_t hi1 = (uint32_t)(m1 >> 32), lo1 = (uint32_t)m1;
-    c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    c = u32x4{xor3(hi1, c.y, k0), lo1, xor3(hi0, c.w, k1), lo0};
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
   }
