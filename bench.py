@@ -159,8 +159,10 @@ def main():
                        "parallelism": f"shard{world}" if world > 1 else "single"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": load_pmc(workload),
-                         "kernel": ("round pipeline bin_emit+transpose_u16+bin_serve+bin_apply" if world == 1 else
-                                    "sharded round: seed copy + round_random_kernel") + " (hipEvent-timed per round)",
+                         "kernel": ("round pipeline: sparse rounds frontier_summary+scan+commit, dense rounds "
+                                    "bin_emit+transpose_u16+bin_serve+bin_apply, + round_snapshot; hipEvents around "
+                                    "each step, gaps between rounds included" if world == 1 else
+                                    "sharded round: seed copy + round_random_kernel (hipEvent-timed per round)"),
                          "bytes_per_node_round": bpn, "avg_launch_us": avg_launch_s * 1e6,
                          "rounds_timed": round_launches},
         }

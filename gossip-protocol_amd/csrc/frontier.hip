@@ -167,8 +167,10 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
         for (uint32_t j = 0; j < 4; ++j) vp[u][j] = ((hit[u] >> j) & 1u) ? S[pp[u][j]] : maj;
       }
       // 4. deltas
+      uint64_t accs[kScanUnroll];
 #pragma unroll
       for (int u = 0; u < kScanUnroll; ++u) {
+        accs[u] = 0;
         if (!act[u]) continue;
         const uint32_t n = base + u * kScanThreads + tid;
         uint64_t acc = 0;
@@ -199,11 +201,17 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
             edge(p, rp ? S[p] : maj);
           }
         }
-        acc &= ~x[u];
-        if (acc) {
-          f.P[n] = acc;
-          f.dirtyP[n >> 6] = 1;
-        }
+        accs[u] = acc & ~x[u];
+      }
+      // pull deltas: whole 8-word chunks (P is zero where there is no delta), so
+      // no store is a partial 64-B chunk
+#pragma unroll
+      for (int u = 0; u < kScanUnroll; ++u) {
+        const uint32_t n = base + u * kScanThreads + tid;
+        const uint64_t pz = __ballot(accs[u] != 0);
+        if (!pz) continue;
+        if (n < c1 && ((pz >> (lane & ~7u)) & 0xFFull)) f.P[n] = accs[u];
+        if (accs[u]) f.dirtyP[n >> 6] = 1;
       }
     }
   }
@@ -344,9 +352,12 @@ __global__ __launch_bounds__(kCommitThreads) void frontier_commit_kernel(Frontie
         const uint64_t n = (g << 6) + lane;
         const bool valid = n < N;
         const uint64_t nw = old[u] | d[u] | pv[u];
-        if (nw != old[u]) S[n] = nw;
-        if (d[u]) f.D[n] = 0;
-        if (pv[u]) f.P[n] = 0;
+        // write whole 8-word (64 B) chunks: a partial chunk costs the HBM a read-modify-write
+        const uint32_t sh = lane & ~7u;
+        const uint64_t chg = __ballot(valid && nw != old[u]), dz = __ballot(d[u] != 0), pz = __ballot(pv[u] != 0);
+        if (valid && ((chg >> sh) & 0xFFull)) S[n] = nw;
+        if (valid && ((dz >> sh) & 0xFFull)) f.D[n] = 0;
+        if (valid && ((pz >> sh) & 0xFFull)) f.P[n] = 0;
         gs.add(f, g, n, valid, old[u], nw, fm, do_hash, lane);
       }
     }

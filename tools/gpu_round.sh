@@ -1,0 +1,22 @@
+#!/bin/bash
+# Round evidence: GPU tests, smoke, bench (+cpu_baseline), rocprof kernel trace/stats,
+# PMC traffic passes; everything under gpurun_out/round/.
+set -u
+O=gpurun_out/round
+mkdir -p $O
+export TMPDIR=/tmp
+ok() { local rc=$1; if [ "$rc" -ne 0 ]; then echo "STOP: step exited $rc"; exit "$rc"; fi; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $O/pytest_gpu.txt 2>&1; ok $?
+tail -1 $O/pytest_gpu.txt
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1; ok $?
+tail -1 $O/smoke.txt
+timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err; ok $?
+cat $O/bench.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/prof.out 2>&1; ok $?
+python tools/rounds.py $O/prof/run_kernel_trace.csv > $O/rounds.txt; python tools/idle.py $O/prof/run_kernel_trace.csv > $O/idle.txt
+B="python bench.py --steps 1 --warmup 0 --no-cpu-baseline"
+timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc -o fetch -- $B > $O/pmc_fetch.out 2>&1; ok $?
+timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/pmc -o write -- $B > $O/pmc_write.out 2>&1; ok $?
+timeout -k 10 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace --output-format csv -d $O/pmc -o hit -- $B > $O/pmc_hit.out 2>&1; ok $?
+python tools/pmc_round.py $O/pmc "pushpull k=2 R=64, 2^24 nodes/GPU x 1" $O/pmc_round_kernel.json
+echo done

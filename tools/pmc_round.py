@@ -15,6 +15,8 @@ import os
 import sys
 
 ROUND_KERNELS = ("bin_emit_kernel", "transpose_u16_kernel", "bin_serve_kernel", "bin_apply_kernel",
+                 "frontier_summary_kernel", "frontier_scan_kernel", "frontier_commit_kernel",
+                 "frontier_rebuild_kernel", "frontier_inject_kernel", "round_snapshot_kernel",
                  "round_random_kernel", "stats_kernel", "round_flood_kernel", "frontier_kernel")
 
 
@@ -38,7 +40,8 @@ def main():
             per_kernel[k][c] += v
             if c == "FETCH_SIZE":
                 launches[k] += 1
-    rounds = launches.get("bin_emit_kernel") or launches.get("round_random_kernel") or 1
+    # one snapshot per round (binned engines); the direct path has one round kernel per round
+    rounds = launches.get("round_snapshot_kernel") or launches.get("round_random_kernel") or 1
     fetch = tot["FETCH_SIZE"] * 1024 / rounds
     write = tot["WRITE_SIZE"] * 1024 / rounds
     res = {

@@ -1,8 +1,8 @@
 """Per-round kernel durations of the last dissemination step in a rocprofv3 kernel trace.
 
 A round starts at bin_emit (dense binned round) or frontier_summary (sparse
-frontier round); a frontier rebuild (after inject) is counted with the round
-that follows it.
+frontier round) and ends with round_snapshot; a rebuild or inject before it is
+counted with it.
 """
 import csv
 import sys
@@ -11,7 +11,7 @@ path = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof/run_kernel_trace.c
 SHORT = {"bin_count_kernel": "count", "bin_emit_kernel": "emit", "transpose_u16_kernel": "u16", "bin_serve_kernel": "serve",
          "bin_apply_kernel": "apply", "frontier_summary_kernel": "summ", "frontier_scan_kernel": "scan",
          "frontier_rebuild_kernel": "rebuild", "frontier_commit_kernel": "commit", "frontier_inject_kernel": "inject", "round_snapshot_kernel": "snap"}
-STARTS = ("summ", "rebuild")
+STARTS = ("summ", "emit", "rebuild")
 
 
 def short(name):
@@ -26,7 +26,7 @@ seq = sorted((int(r["Start_Timestamp"]), short(r["Kernel_Name"]),
 ks = [x for x in seq if x[1]]
 rounds, cur = [], []
 for x in ks:
-    if x[1] in STARTS and cur and not (cur[-1][1] == "rebuild"):
+    if x[1] in STARTS and cur and cur[-1][1] not in ("rebuild", "inject"):
         rounds.append(cur)
         cur = []
     cur.append(x)
@@ -41,7 +41,6 @@ tot = 0
 for r in rounds[cut:]:
     t = sum(d for _, _, d in r)
     tot += t
-    # both paths are enqueued every round; the unplanned one's kernels exit at once
-    kind = "sparse" if sum(d for _, n, d in r if n == "scan") > 10 else "dense "
-    print(kind, " ".join(f"{n}:{d:6.1f}" for _, n, d in r if d > 3.0), f" round {t:6.1f} us")
+    kind = "sparse" if any(n == "scan" for _, n, _ in r) else "dense "
+    print(kind, " ".join(f"{n}:{d:6.1f}" for _, n, d in r), f" round {t:6.1f} us")
 print(f"rounds {len(rounds) - cut}, kernel time {tot / 1000:.2f} ms")
