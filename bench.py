@@ -71,6 +71,32 @@ def cpu_baseline(n_nodes: int, seed: int, budget_s: float = 12.0):
                       f"{n_nodes}-node push-pull k=2 R=64 run ({dt:.1f}s)"}
 
 
+def dense_only(n_nodes: int, seed: int, device: int, steps: int = 2):
+    """Every round on the binned (dense) pipeline, same workload: the per-round cost the sparse
+    frontier rounds avoid, reported beside the headline so that saving never hides in `frac`."""
+    from gossip_hip import FLAG_DENSE, FLAG_TIMING, Engine
+    prev = os.environ.get("GOSSIP_AHEAD")
+    os.environ["GOSSIP_AHEAD"] = "1"  # no round enqueued past convergence inside the timed region
+    try:
+        e = Engine(n_nodes, RUMORS, MODE, FANOUT, seed, flags=FLAG_TIMING | FLAG_DENSE, device=device)
+    finally:
+        if prev is None:
+            os.environ.pop("GOSSIP_AHEAD")
+        else:
+            os.environ["GOSSIP_AHEAD"] = prev
+    e.reset(); e.inject_random(); e.step(64, with_infected=False)
+    e.reset_timing()
+    for _ in range(steps):
+        e.reset(); e.inject_random(); e.step(64, with_infected=False)
+    ms, n = e.kernel_time(0)
+    e.close()
+    us = ms * 1e3 / max(n, 1)
+    bpn = alg_bytes_per_node_round(MODE, FANOUT, 1)
+    return {"avg_round_us": us, "achieved_GBps": bpn * n_nodes / us / 1e3,
+            "frac": bpn * n_nodes / us / 1e3 / HBM_PEAK_GBS, "rounds_timed": n,
+            "note": "GOSSIP_FLAG_DENSE: every round on bin_emit+transpose+serve+apply, same workload"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -78,6 +104,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--nodes-per-gpu", type=int, default=NODES_PER_GPU)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-dense-only", action="store_true", help="skip the all-dense comparison run (profiling)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -166,6 +193,11 @@ def main():
                          "bytes_per_node_round": bpn, "avg_launch_us": avg_launch_s * 1e6,
                          "rounds_timed": round_launches},
         }
+        traffic = out["roofline"]["traffic"]
+        if traffic:
+            out["roofline"]["traffic_GBps"] = traffic / avg_launch_s / 1e9  # PMC bytes per round / round time
+        if world == 1 and not args.no_dense_only:
+            out["roofline"]["dense_only"] = dense_only(n_total, seed, local)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(n_total, seed)
         print(json.dumps(out), flush=True)

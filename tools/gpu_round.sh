@@ -12,9 +12,9 @@ timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 tail -1 $O/smoke.txt
 timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err; ok $?
 cat $O/bench.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/prof.out 2>&1; ok $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-dense-only > $O/prof.out 2>&1; ok $?
 python tools/rounds.py $O/prof/run_kernel_trace.csv > $O/rounds.txt; python tools/idle.py $O/prof/run_kernel_trace.csv > $O/idle.txt
-B="python bench.py --steps 1 --warmup 0 --no-cpu-baseline"
+B="python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-dense-only"
 timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc -o fetch -- $B > $O/pmc_fetch.out 2>&1; ok $?
 timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/pmc -o write -- $B > $O/pmc_write.out 2>&1; ok $?
 timeout -k 10 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace --output-format csv -d $O/pmc -o hit -- $B > $O/pmc_hit.out 2>&1; ok $?
