@@ -646,6 +646,12 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
           e->err = "hipEventCreate failed";
           return bail(GOSSIP_EHIP);
         }
+  // the zeroing above ran on the null stream, which the engine's non-blocking
+  // stream does not wait for: finish it before any engine work is enqueued
+  if (hipDeviceSynchronize() != hipSuccess) {
+    e->err = "hipDeviceSynchronize after allocation failed";
+    return bail(GOSSIP_EHIP);
+  }
   *out = e;
   return GOSSIP_OK;
 }
