@@ -26,6 +26,7 @@
 #include "binned.h"
 #include "philox.h"
 #include "round.h"
+#include "wave.h"
 
 namespace gossip {
 
@@ -34,7 +35,8 @@ namespace {
 constexpr int kEmitThreads = 1024;
 constexpr uint32_t kEmitGrid = 256;  // one persistent emit block per CU
 constexpr int kTileThreads = 1024;
-constexpr int kUnroll = 16;    // records in flight per lane in the run walkers
+constexpr int kUnroll = 16;       // records in flight per lane in the run walkers (32 spills in K3)
+constexpr int kUnrollServe = 16;
 constexpr int kUnrollSeq = 8;  // records in flight per lane in the sequential response walker
 // record id word: p_local [0,14) | n_local [14,27) | flags.  K1 rewrites every
 // id each round, so a flag never outlives its round.
@@ -48,8 +50,6 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {
   if (n & 7u) return b;
   return (b & 7u) * (n >> 3) + (b >> 3);
 }
-
-__device__ __forceinline__ uint64_t full_mask1(uint32_t R) { return R >= 64 ? ~0ull : ((1ull << R) - 1ull); }
 
 // which edges of a sender carry information: a push needs S_t[n] != 0, a pull
 // request is pointless once the sender already holds every rumor
@@ -192,10 +192,12 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
   for (uint32_t e = tid; e < total; e += kEmitThreads) {
     const uint32_t id = st_ids[e];
     const uint64_t x = sval[id >> kTileDLog];
-    // zero and full values are implied by a flag: light rounds move ids only
+    // the flags let K2/K3 skip work; the value is stored all the same, so the
+    // region is written without holes (a partly written 64-B chunk costs HBM
+    // a read-modify-write: profiles/r01_experiments/microbench5.jsonl)
     const uint32_t fl = x == 0 ? kIdVZ : (x == fm ? kIdVF : 0u);
     gids[e] = id | fl;
-    if (!fl) gvals[e] = x;
+    gvals[e] = x;
   }
 #pragma unroll
   for (uint32_t q = 0; q < kQ; ++q) v[q] = vn[q];
@@ -222,27 +224,6 @@ __global__ __launch_bounds__(256) void transpose_u16_kernel(const uint16_t* __re
   }
 }
 
-
-__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
-
-// 64x64 bit-matrix transpose across a wave64: on entry lane i holds row i, on
-// exit lane j holds column j (bit i = bit j of lane i's input word).
-__device__ __forceinline__ uint64_t transpose64(uint64_t x, uint32_t lane) {
-  constexpr uint64_t kMask[6] = {0x00000000FFFFFFFFull, 0x0000FFFF0000FFFFull, 0x00FF00FF00FF00FFull,
-                                 0x0F0F0F0F0F0F0F0Full, 0x3333333333333333ull, 0x5555555555555555ull};
-#pragma unroll
-  for (int st = 0; st < 6; ++st) {
-    const uint32_t d = 32u >> st;
-    const uint64_t y = __shfl_xor(x, d, 64);
-    const uint64_t m = kMask[st];
-    x = (lane & d) ? ((x & ~m) | ((y & ~m) >> d)) : ((x & m) | ((y & m) << d));
-  }
-  return x;
-}
 
 // Writes the finished tile (LDS) to S_{t+1} and folds the round stats
 // (definitions as in stats_kernel): fully-informed count by ballot, per-rumor
@@ -400,7 +381,7 @@ __device__ __forceinline__ void load_tile(unsigned long long* img, const uint64_
 __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, const uint64_t* __restrict__ S, BinBufs b,
                                                                   uint32_t R) {
   __shared__ unsigned long long img[kTileD];
-  __shared__ uint64_t wmask[(kTileThreads / 64) * kUnroll];
+  __shared__ uint64_t wmask[(kTileThreads / 64) * kUnrollServe];
   __shared__ int32_t wlist[(kTileThreads / 64) * 64];
   const uint32_t T = xcd_remap(blockIdx.x, g.nt_d);
   const uint64_t node0 = (uint64_t)T << kTileDLog;
@@ -409,12 +390,12 @@ __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, cons
   const uint32_t* gids = b.ids;
   uint64_t* __restrict__ gresp = b.resp;
   const uint16_t* rowb = b.offT + (size_t)T * g.nt_s;
-  for_each_run_record<kUnroll>(g, rowb, rowb + g.nt_s, wmask, wlist, [&](const int32_t* rec) {
-    uint32_t id[kUnroll];
+  for_each_run_record<kUnrollServe>(g, rowb, rowb + g.nt_s, wmask, wlist, [&](const int32_t* rec) {
+    uint32_t id[kUnrollServe];
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) id[u] = gids[rec[u] >= 0 ? rec[u] : 0];
+    for (int u = 0; u < kUnrollServe; ++u) id[u] = gids[rec[u] >= 0 ? rec[u] : 0];
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
+    for (int u = 0; u < kUnrollServe; ++u) {
       // a fully informed sender needs nothing; otherwise the whole S_t[p] goes
       // back (bits n already holds are harmless to OR), so no value is read
       // dense rounds: every response is written (K3 tells stale slots by kIdVF)
@@ -447,7 +428,6 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, cons
   const uint32_t* __restrict__ gids = b.ids;
   const uint64_t* __restrict__ gvals = b.vals;
   const uint64_t* __restrict__ gresp = b.resp;
-  const uint64_t fm = full_mask1(R);
   if (mode == 1 || mode == 3) {  // pushes aimed at this tile
     const uint16_t* rowb = b.offT + (size_t)X * g.nt_s;
     for_each_run_record<kUnroll>(g, rowb, rowb + g.nt_s, wmask, wlist, [&](const int32_t* rec) {
@@ -459,7 +439,7 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, cons
       for (int u = 0; u < kUnroll; ++u) v[u] = gvals[rec[u] >= 0 ? rec[u] : 0];  // not behind the id: both loads fly together
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u)
-        v[u] = rec[u] < 0 || (id[u] & kIdVZ) ? 0ull : ((id[u] & kIdVF) ? fm : v[u]);
+        v[u] = rec[u] < 0 || (id[u] & kIdVZ) ? 0ull : v[u];  // every value is stored (K1)
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         const uint32_t p = id[u] & (kTileD - 1);
@@ -520,7 +500,7 @@ BinGeom make_bin_geom(uint64_t N, uint32_t k) {
 bool bin_path_ok(uint64_t N, uint32_t k, uint32_t W, uint32_t G) {
   if (W != 1 || G != 1 || k == 0 || k > 64 || N < 2) return false;
   const BinGeom g = make_bin_geom(N, k);
-  return g.nt_d <= kMaxTilesD;
+  return g.nt_d <= kMaxTilesD && (uint64_t)g.nt_s * g.rp < (1ull << 31);  // record indices are int32
 }
 
 size_t bin_bytes(const BinGeom& g) {
@@ -559,7 +539,6 @@ hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, 
   // responses come from the record buffers), and K1/K2 have finished reading S_t
   bin_apply_kernel<<<g.nt_d, kTileThreads, 0, st>>>(g, S, S, b, partial, R, mode, flags);
   return launch_round_snapshot(partial, rs, st);
-  return hipGetLastError();
 }
 
 }  // namespace gossip
