@@ -78,6 +78,7 @@ struct gossip_engine {
   void* fr_mem = nullptr;
   bool fr_valid = false;          // partial_d holds the totals of S and the bitmaps are exact
   double sparse_frac = 1.0 / 16;  // rare fraction at or below which a round runs sparse
+  double alld_frac = 1.0 / 64;    // sparse rounds with k * rare >= alld_frac * N commit every group's D (bench sweep)
   // pipelined rounds (binned engines): the host picks each round's path from the
   // totals it has read, predicted forward over the rounds still in flight, and
   // stays up to `ahead` rounds in front
@@ -301,12 +302,15 @@ Est predict(const gossip_engine* e, const Est& x) {
   return y;
 }
 
-// sparse when the smaller rare class is at most sparse_frac * N; maj = which class is rare
-bool choose_sparse(const gossip_engine* e, const Est& x, uint32_t* maj) {
+// sparse when the smaller rare class is at most sparse_frac * N; maj = which
+// class is rare; all_d once the rare ends' pushes (~k per rare node) reach
+// alld_frac * N (launch_frontier_round)
+bool choose_sparse(const gossip_engine* e, const Est& x, uint32_t* maj, bool* all_d) {
   if (!e->frontier) return false;
-  const double lo = x.nz, hi = (double)e->N - x.full;
+  const double lo = x.nz, hi = (double)e->N - x.full, rare = std::min(lo, hi);
   *maj = hi < lo ? 1u : 0u;
-  return std::min(lo, hi) <= e->sparse_frac * (double)e->N;
+  *all_d = rare * (double)e->k >= e->alld_frac * (double)e->N;
+  return rare <= e->sparse_frac * (double)e->N;
 }
 
 RoundSync ring_sync(gossip_engine* e, uint32_t slot) {
@@ -317,10 +321,10 @@ RoundSync ring_sync(gossip_engine* e, uint32_t slot) {
   return rs;
 }
 
-int launch_round_path(gossip_engine* e, uint32_t t, bool sparse, uint32_t maj, const RoundSync& rs) {
+int launch_round_path(gossip_engine* e, uint32_t t, bool sparse, uint32_t maj, bool all_d, const RoundSync& rs) {
   if (sparse)
     HIP_OK(e, launch_frontier_round(e->fb, e->S, e->N, e->partial_d, e->R, e->k, t, e->key0, e->key1, e->mode, maj,
-                                    e->cfg.flags, rs, e->stream));
+                                    all_d, e->cfg.flags, rs, e->stream));
   else
     HIP_OK(e, launch_binned_round(e->bg, e->bb, e->S, e->partial_d, e->R, t, e->key0, e->key1, e->mode,
                                   e->cfg.flags, rs, e->stream));
@@ -374,11 +378,12 @@ int step_planned(gossip_engine* e, uint32_t max_rounds, gossip_round_stats_t* st
       Est x = base;
       for (uint32_t i = done; i < launched; ++i) x = predict(e, x);
       uint32_t maj = 0;
-      const bool sparse = choose_sparse(e, x, &maj);
+      bool all_d = false;
+      const bool sparse = choose_sparse(e, x, &maj, &all_d);
       const uint32_t slot = launched % kRing;
       const RoundSync rs = ring_sync(e, slot);
       want[slot] = rs.seq;
-      if (int rc = launch_round_path(e, t0 + launched, sparse, maj, rs)) return rc;
+      if (int rc = launch_round_path(e, t0 + launched, sparse, maj, all_d, rs)) return rc;
       ++launched;
     }
     if (done == launched) break;
@@ -438,9 +443,10 @@ int compute_round(gossip_engine* e, const uint64_t* gathered) {
     std::vector<uint64_t> tot;
     if ((rc = read_totals(e, &tot))) return rc;
     uint32_t maj = 0;
-    const bool sparse = choose_sparse(e, est_of(e, tot.data()), &maj);
+    bool all_d = false;
+    const bool sparse = choose_sparse(e, est_of(e, tot.data()), &maj, &all_d);
     if ((rc = timer_begin(e, 0))) return rc;
-    if ((rc = launch_round_path(e, e->t, sparse, maj, ring_sync(e, 0)))) return rc;
+    if ((rc = launch_round_path(e, e->t, sparse, maj, all_d, ring_sync(e, 0)))) return rc;
     return timer_end(e, 0);  // stats are fused into the round kernels
   } else {
     // timer 0 covers the whole S_t -> S_{t+1} transform (seed copy + round kernel)
@@ -626,6 +632,7 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
       e->bb.fullb = e->fb.fullb;
       e->frontier = true;
       if (const char* f = getenv("GOSSIP_SPARSE_FRAC")) e->sparse_frac = atof(f);
+      if (const char* f = getenv("GOSSIP_ALLD_FRAC")) e->alld_frac = atof(f);
     }
     if (const char* a = getenv("GOSSIP_AHEAD")) e->ahead = std::max(1, std::min((int)kRing - 1, atoi(a)));
     if (hipHostMalloc((void**)&e->ring_h, kRing * (part_len(e) + 1) * 8, hipHostMallocMapped) != hipSuccess ||

@@ -23,7 +23,7 @@ struct FrontierBufs {
   uint32_t* summ;     // [summ_words] bit b: some rare node in [b*g, (b+1)*g)
   uint64_t* D;        // [N] pending push deltas (atomic OR), zero outside a sparse round
   uint64_t* P;        // [N] pending pull deltas (plain store by the node's own lane), zero outside
-  uint8_t* dirtyD;    // [ceil(N/64)] group g has a push delta
+  uint8_t* dirtyD;    // [ceil(N/64)] group g has a push delta (not kept in all_d rounds)
   uint8_t* dirtyP;    // [ceil(N/64)] group g has a pull delta
   uint32_t glog;      // g = 1 << glog nodes per summary bit
   uint32_t summ_words;
@@ -48,8 +48,11 @@ hipError_t launch_frontier_inject(const FrontierBufs& f, uint64_t* S, uint64_t N
 // partial holds the totals of S_t on entry and those of S_{t+1} on exit; the
 // last commit block hands them to the host through rs.  With no rare node the
 // round is a no-op (every kernel returns at once).
+// all_d: the scan does not flag push-dirty groups and the commit reads D of
+// every group instead — cheaper once pushes touch most groups (a random byte
+// store per push costs about as much as the push atomic itself).  Exact either way.
 hipError_t launch_frontier_round(const FrontierBufs& f, uint64_t* S, uint64_t N, uint64_t* partial, uint32_t R,
                                  uint32_t k, uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t maj,
-                                 uint32_t flags, const RoundSync& rs, hipStream_t st);
+                                 bool all_d, uint32_t flags, const RoundSync& rs, hipStream_t st);
 
 }  // namespace gossip

@@ -108,7 +108,8 @@ __global__ __launch_bounds__(256) void frontier_summary_kernel(FrontierBufs f, u
 template <int MAJ, int MODE>
 __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const FrontierBufs& f,
                                           const uint64_t* __restrict__ S, uint64_t N, uint32_t R, uint32_t k,
-                                          uint32_t t, uint32_t key0, uint32_t key1, uint64_t per_block) {
+                                          uint32_t t, uint32_t key0, uint32_t key1, uint64_t per_block,
+                                          bool mark_d) {
   const uint32_t* summ = (const uint32_t*)summ4;
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t n4 = (f.summ_words + 3) / 4;
@@ -150,13 +151,21 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
         }
       }
       // 2. summary hits: exact test in the rare bitmap (2 MiB at 2^24 nodes, L2-resident)
+      // (all probes issued before any is consumed: one wait for the lot)
       if (glog) {
+        uint64_t rw[kScanUnroll][4];
 #pragma unroll
         for (int u = 0; u < kScanUnroll; ++u)
 #pragma unroll
-          for (uint32_t j = 0; j < 4; ++j)
-            if ((hit[u] >> j) & 1u)
-              if (!((rare_word<MAJ>(f, pp[u][j] >> 6, N) >> (pp[u][j] & 63u)) & 1ull)) hit[u] &= ~(1u << j);
+          for (uint32_t j = 0; j < 4; ++j)  // raw bitmap words: nothing computed on them inside the branch
+            rw[u][j] = ((hit[u] >> j) & 1u) ? (MAJ ? f.fullb[pp[u][j] >> 6] : f.nzb[pp[u][j] >> 6]) : 0ull;
+#pragma unroll
+        for (int u = 0; u < kScanUnroll; ++u)
+#pragma unroll
+          for (uint32_t j = 0; j < 4; ++j) {
+            const bool bit = (rw[u][j] >> (pp[u][j] & 63u)) & 1ull;  // p < N: always a valid bit
+            if (bit == (MAJ != 0)) hit[u] &= ~(1u << j);  // rare = nonzero (MAJ 0) / not full (MAJ 1)
+          }
       }
       // 3. S_t of the rare ends only (a majority node's value is known)
 #pragma unroll
@@ -166,31 +175,43 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) vp[u][j] = ((hit[u] >> j) & 1u) ? S[pp[u][j]] : maj;
       }
-      // 4. deltas
-      uint64_t accs[kScanUnroll];
+      // 4. deltas, in registers: every gather above is consumed here, before
+      // the first atomic or store below.  (A load consumed after a store was
+      // issued waits for that store too: vmcnt retires in order, so each edge
+      // would wait out the previous edge's atomic round trip.)
+      uint64_t accs[kScanUnroll], dpush[kScanUnroll][4];
 #pragma unroll
       for (int u = 0; u < kScanUnroll; ++u) {
         accs[u] = 0;
-        if (!act[u]) continue;
-        const uint32_t n = base + u * kScanThreads + tid;
-        uint64_t acc = 0;
-        auto edge = [&](uint32_t p, uint64_t v) {
-          if (kPull) acc |= v;
-          if (kPush) {
-            const uint64_t d = x[u] & ~v;
-            if (d) {
-              atomicOr((unsigned long long*)&f.D[p], (unsigned long long)d);
-              f.dirtyD[p >> 6] = 1;
-            }
-          }
-        };
-        if (k <= 4) {
 #pragma unroll
-          for (uint32_t j = 0; j < 4; ++j) {
-            if (j >= k) break;
-            if (rn[u] || ((hit[u] >> j) & 1u)) edge(pp[u][j], vp[u][j]);  // else both ends majority
+        for (uint32_t j = 0; j < 4; ++j) dpush[u][j] = 0;
+        if (!act[u] || k > 4) continue;
+        uint64_t acc = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+          if (j >= k) break;
+          if (!rn[u] && !((hit[u] >> j) & 1u)) continue;  // both ends majority: nothing moves
+          if (kPull) acc |= vp[u][j];
+          if (kPush) dpush[u][j] = x[u] & ~vp[u][j];
+        }
+        accs[u] = acc & ~x[u];
+      }
+      // 5. push deltas: atomics into D and the group's dirty byte
+#pragma unroll
+      for (int u = 0; u < kScanUnroll; ++u)
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j)
+          if (dpush[u][j]) {
+            atomicOr((unsigned long long*)&f.D[pp[u][j]], (unsigned long long)dpush[u][j]);
+            if (mark_d) f.dirtyD[pp[u][j] >> 6] = 1;
           }
-        } else {
+      // k > 4: the draws are redone edge by edge (no registers for them)
+      if (k > 4) {
+#pragma unroll
+        for (int u = 0; u < kScanUnroll; ++u) {
+          if (!act[u]) continue;
+          const uint32_t n = base + u * kScanThreads + tid;
+          uint64_t acc = 0;
           u32x4 r4{0, 0, 0, 0};
           for (uint32_t j = 0; j < k; ++j) {
             if ((j & 3u) == 0) r4 = philox4x32_10(u32x4{n, t, 0u, j >> 2}, key0, key1);
@@ -198,10 +219,18 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
             bool rp = summ_bit(p);
             if (rp && glog) rp = (rare_word<MAJ>(f, p >> 6, N) >> (p & 63u)) & 1ull;
             if (!rn[u] && !rp) continue;  // both ends majority: nothing moves
-            edge(p, rp ? S[p] : maj);
+            const uint64_t v = rp ? S[p] : maj;
+            if (kPull) acc |= v;
+            if (kPush) {
+              const uint64_t d = x[u] & ~v;
+              if (d) {
+                atomicOr((unsigned long long*)&f.D[p], (unsigned long long)d);
+                if (mark_d) f.dirtyD[p >> 6] = 1;
+              }
+            }
           }
+          accs[u] = acc & ~x[u];
         }
-        accs[u] = acc & ~x[u];
       }
       // pull deltas: whole 8-word chunks (P is zero where there is no delta), so
       // no store is a partial 64-B chunk
@@ -221,14 +250,15 @@ template <int MODE>
 __global__ __launch_bounds__(kScanThreads) void frontier_scan_kernel(FrontierBufs f, const uint64_t* __restrict__ S,
                                                                       uint64_t N, uint32_t R, uint32_t k, uint32_t t,
                                                                       uint32_t key0, uint32_t key1, uint64_t per_block,
-                                                                      const uint64_t* partial, uint32_t maj) {
+                                                                      const uint64_t* partial, uint32_t maj,
+                                                                      uint32_t mark_d) {
   __shared__ uint4 summ4[kSummBits / 128];
   __shared__ uint64_t rws[kRwWords];
   if (rare_count(partial, N, R, maj) == 0) return;  // converged (or nothing injected): nothing moves
   if (maj)
-    scan_body<1, MODE>(summ4, rws, f, S, N, R, k, t, key0, key1, per_block);
+    scan_body<1, MODE>(summ4, rws, f, S, N, R, k, t, key0, key1, per_block, mark_d != 0);
   else
-    scan_body<0, MODE>(summ4, rws, f, S, N, R, k, t, key0, key1, per_block);
+    scan_body<0, MODE>(summ4, rws, f, S, N, R, k, t, key0, key1, per_block, mark_d != 0);
 }
 
 // Stats of one 64-node group whose words went from old to nw (old == 0 in a
@@ -303,10 +333,11 @@ __global__ __launch_bounds__(kCommitThreads) void frontier_rebuild_kernel(Fronti
 
 // K2: a wave takes 64 groups, finds the dirty ones by one coalesced load of
 // their flags, and commits kCommitUnroll of them per step: S |= D | P in
-// place, D, P and the flags back to zero, bitmaps and stats deltas.
+// place, D, P and the flags back to zero, bitmaps and stats deltas.  all_d:
+// every group's D is read (the scan kept no push flags).
 __global__ __launch_bounds__(kCommitThreads) void frontier_commit_kernel(FrontierBufs f, uint64_t* __restrict__ S,
                                                                           uint64_t N, uint64_t* __restrict__ partial,
-                                                                          uint32_t R, uint32_t flags) {
+                                                                          uint32_t R, uint32_t flags, uint32_t all_d) {
   __shared__ uint32_t cnt[64];
   __shared__ uint64_t red[3][kCommitThreads / 64];
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -319,8 +350,8 @@ __global__ __launch_bounds__(kCommitThreads) void frontier_commit_kernel(Frontie
        c += (uint64_t)gridDim.x * (kCommitThreads / 64)) {
     const uint64_t gl = (c << 6) + lane;
     const bool gv = gl < ngroups;
-    const uint8_t fd = gv ? f.dirtyD[gl] : 0, fp = gv ? f.dirtyP[gl] : 0;
-    if (fd) f.dirtyD[gl] = 0;
+    const uint8_t fd = gv ? (all_d ? 1 : f.dirtyD[gl]) : 0, fp = gv ? f.dirtyP[gl] : 0;
+    if (fd && !all_d) f.dirtyD[gl] = 0;
     if (fp) f.dirtyP[gl] = 0;
     const uint64_t mD = __ballot(fd != 0), mP = __ballot(fp != 0);
     uint64_t mask = mD | mP;
@@ -452,22 +483,22 @@ hipError_t launch_frontier_inject(const FrontierBufs& f, uint64_t* S, uint64_t N
 
 hipError_t launch_frontier_round(const FrontierBufs& f, uint64_t* S, uint64_t N, uint64_t* partial, uint32_t R,
                                  uint32_t k, uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t maj,
-                                 uint32_t flags, const RoundSync& rs, hipStream_t st) {
+                                 bool all_d, uint32_t flags, const RoundSync& rs, hipStream_t st) {
   frontier_summary_kernel<<<(f.summ_words + 255) / 256, 256, 0, st>>>(f, N, partial, R, maj);
   const uint64_t chunks = (N + kScanThreads - 1) / kScanThreads;
   const uint32_t grid = (uint32_t)(chunks < kScanGrid ? chunks : kScanGrid);
   // contiguous node range per block, a multiple of the block width (so lanes map to bitmap bits)
   const uint64_t per = ((N + grid - 1) / grid + kScanThreads - 1) / kScanThreads * kScanThreads;
   switch (mode) {
-    case 1: frontier_scan_kernel<1><<<grid, kScanThreads, 0, st>>>(f, S, N, R, k, t, key0, key1, per, partial, maj); break;
-    case 2: frontier_scan_kernel<2><<<grid, kScanThreads, 0, st>>>(f, S, N, R, k, t, key0, key1, per, partial, maj); break;
-    case 3: frontier_scan_kernel<3><<<grid, kScanThreads, 0, st>>>(f, S, N, R, k, t, key0, key1, per, partial, maj); break;
+    case 1: frontier_scan_kernel<1><<<grid, kScanThreads, 0, st>>>(f, S, N, R, k, t, key0, key1, per, partial, maj, !all_d); break;
+    case 2: frontier_scan_kernel<2><<<grid, kScanThreads, 0, st>>>(f, S, N, R, k, t, key0, key1, per, partial, maj, !all_d); break;
+    case 3: frontier_scan_kernel<3><<<grid, kScanThreads, 0, st>>>(f, S, N, R, k, t, key0, key1, per, partial, maj, !all_d); break;
     default: return hipErrorInvalidValue;
   }
   const uint64_t wchunks = (((N + 63) >> 6) + 63) >> 6;  // 64-group chunks, one per wave
   const uint64_t cblocks = (wchunks + kCommitThreads / 64 - 1) / (kCommitThreads / 64);
   frontier_commit_kernel<<<(uint32_t)(cblocks < 4096 ? cblocks : 4096), kCommitThreads, 0, st>>>(f, S, N, partial,
-                                                                                                 R, flags);
+                                                                                                 R, flags, all_d);
   return launch_round_snapshot(partial, rs, st);
 }
 

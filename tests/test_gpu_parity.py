@@ -32,19 +32,24 @@ def test_device_philox_kat(golden):
 # round paths of the random modes, all bit-identical:
 #   auto   — default: sparse frontier rounds while one class dominates, dense binned rounds otherwise
 #   dense  — every round on the binned LDS pipeline
-#   sparse — every round on the frontier kernels (GOSSIP_SPARSE_FRAC=1 lifts the sparsity test)
+#   sparse — every round on the frontier kernels (GOSSIP_SPARSE_FRAC=1 lifts the sparsity test),
+#            pushes tracked by per-group dirty flags
+#   sparse_alld — the same, but every round's commit reads D of every group (no push flags)
 #   direct — the random-access kernels
-PATHS = ["auto", "dense", "sparse", "direct"]
-_PATH_FLAGS = {"auto": 0, "dense": FLAG_DENSE, "sparse": 0, "direct": FLAG_DIRECT}
+PATHS = ["auto", "dense", "sparse", "sparse_alld", "direct"]
+_PATH_FLAGS = {"auto": 0, "dense": FLAG_DENSE, "sparse": 0, "sparse_alld": 0, "direct": FLAG_DIRECT}
+# GOSSIP_ALLD_FRAC: 0 = every sparse round commits every group's D, huge = none does
+_PATH_ENV = {"sparse": {"GOSSIP_SPARSE_FRAC": "1.0", "GOSSIP_ALLD_FRAC": "1e30"},
+             "sparse_alld": {"GOSSIP_SPARSE_FRAC": "1.0", "GOSSIP_ALLD_FRAC": "0"}}
 
 
 @pytest.fixture
 def path(request, monkeypatch):
     name = request.param
-    if name == "sparse":
-        monkeypatch.setenv("GOSSIP_SPARSE_FRAC", "1.0")
-    else:
-        monkeypatch.delenv("GOSSIP_SPARSE_FRAC", raising=False)
+    for var in ("GOSSIP_SPARSE_FRAC", "GOSSIP_ALLD_FRAC"):
+        monkeypatch.delenv(var, raising=False)
+    for var, val in _PATH_ENV.get(name, {}).items():
+        monkeypatch.setenv(var, val)
     return _PATH_FLAGS[name]
 
 

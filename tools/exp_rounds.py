@@ -17,6 +17,6 @@ e = Engine(1 << 24, 64, "pushpull", 2, 0x5EED0003, flags=FLAG_TIMING | (0 if aut
 for rep in range(3 if auto else 1):
     e.reset()
     e.inject_random()
-    e.step(7 if auto else 10)
+    e.step(int(os.environ.get("EXP_BEFORE", "7")) if auto else 10)
     for _ in range(1 if auto else 3):
         e.step(1)
