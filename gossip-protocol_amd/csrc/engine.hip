@@ -19,6 +19,7 @@
 #include "antientropy.h"
 #include "binned.h"
 #include "frontier.h"
+#include "sharded.h"
 #include "round.h"
 
 #include <cmath>
@@ -86,6 +87,22 @@ struct gossip_engine {
   uint64_t* ring_d = nullptr;
   uint64_t seq = 0;
   uint32_t ahead = 2;
+  // sharded sparse rounds (G > 1, W == 1 random modes; sharded.h):
+  // lf = frontier buffers over the owned nodes, sb = rare lists, global index, messages
+  bool sx = false;
+  bool sx_valid = false;    // partial_d holds the owned nodes' totals and lf's bitmaps are exact
+  bool gtot_valid = false;  // gtot = global totals of S_t (from the driver's all-reduce)
+  bool sx_planned = false, sx_alld = false, last_sparse = false;
+  uint32_t sx_maj = 0;
+  std::vector<uint64_t> gtot;
+  SxGeom sg{};
+  SxBufs sb{};
+  FrontierBufs lf{};
+  void *lf_mem = nullptr, *sx_mem = nullptr;
+  SxItem* rare_recv = nullptr;
+  SxItem* msg_recv = nullptr;
+  uint64_t rare_recv_cap = 0, msg_recv_cap = 0, sx_stride = 0;
+  uint64_t* sx_host = nullptr;  // pinned: [G + 2] counts / list bases
 
   hipEvent_t ev[kTimers][2] = {};
   double time_ms[kTimers] = {0, 0};
@@ -134,6 +151,10 @@ void free_all(gossip_engine* e) {
     if (b) (void)hipFree(b);
   if (e->bin_mem) (void)hipFree(e->bin_mem);
   if (e->fr_mem) (void)hipFree(e->fr_mem);
+  void* sx[] = {e->lf_mem, e->sx_mem, e->rare_recv, e->msg_recv};
+  for (void* b : sx)
+    if (b) (void)hipFree(b);
+  if (e->sx_host) (void)hipHostFree(e->sx_host);
   void* ae[] = {e->V, e->Vn, e->target, e->alive, e->alive_n};
   for (void* b : ae)
     if (b) (void)hipFree(b);
@@ -306,7 +327,7 @@ Est predict(const gossip_engine* e, const Est& x) {
 // class is rare; all_d once the rare ends' pushes (~k per rare node) reach
 // alld_frac * N (launch_frontier_round)
 bool choose_sparse(const gossip_engine* e, const Est& x, uint32_t* maj, bool* all_d) {
-  if (!e->frontier) return false;
+  if (!e->frontier && !e->sx) return false;
   const double lo = x.nz, hi = (double)e->N - x.full, rare = std::min(lo, hi);
   *maj = hi < lo ? 1u : 0u;
   *all_d = rare * (double)e->k >= e->alld_frac * (double)e->N;
@@ -456,7 +477,12 @@ int compute_round(gossip_engine* e, const uint64_t* gathered) {
     if ((rc = timer_end(e, 0))) return rc;
   }
   if ((rc = timer_begin(e, 1))) return rc;
-  HIP_OK(e, launch_stats(a, e->stream));
+  if (e->sx) {  // totals incl. nonzero nodes and exact bitmaps of S_{t+1}, for the next round's plan
+    HIP_OK(e, launch_frontier_rebuild(e->lf, e->Snext, e->nown, e->partial_d, e->R, e->cfg.flags, e->stream));
+    e->sx_valid = true;
+  } else {
+    HIP_OK(e, launch_stats(a, e->stream));
+  }
   if ((rc = timer_end(e, 1))) return rc;
   return GOSSIP_OK;
 }
@@ -642,6 +668,22 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
     }
     std::memset(e->ring_h, 0, kRing * (part_len(e) + 1) * 8);
   }
+  if (G > 1 && G <= 1024 && e->W == 1 && e->mode >= GOSSIP_MODE_PUSH && e->mode <= GOSSIP_MODE_PUSHPULL &&
+      !(cfg->flags & (GOSSIP_FLAG_DIRECT | GOSSIP_FLAG_DENSE))) {
+    e->sg = SxGeom{e->N, e->Nl, e->lo, e->nown, G, e->rank, e->k, e->R};
+    if (!alloc_raw(&e->lf_mem, frontier_bytes(e->nown)) || !alloc_raw(&e->sx_mem, sx_bytes(e->sg)))
+      return bail(GOSSIP_ENOMEM);
+    frontier_carve(e->nown, e->lf_mem, &e->lf);
+    e->lf.id0 = e->lo;
+    sx_carve(e->sg, e->sx_mem, &e->sb);
+    if (hipHostMalloc((void**)&e->sx_host, (G + 2) * 8, hipHostMallocDefault) != hipSuccess) {
+      e->err = "hipHostMalloc failed";
+      return bail(GOSSIP_ENOMEM);
+    }
+    e->sx = true;
+    if (const char* f = getenv("GOSSIP_SPARSE_FRAC")) e->sparse_frac = atof(f);
+    if (const char* f = getenv("GOSSIP_ALLD_FRAC")) e->alld_frac = atof(f);
+  }
   if (hipHostMalloc((void**)&e->partial_h, part_len(e) * 8, hipHostMallocDefault) != hipSuccess) {
     e->err = "hipHostMalloc failed";
     return bail(GOSSIP_ENOMEM);
@@ -751,6 +793,7 @@ int gossip_reset(gossip_engine_t* e) {
     HIP_OK(e, hipMemsetAsync(e->img[1], 0, shard * e->G, e->stream));
   }
   e->fr_valid = false;
+  e->sx_valid = e->gtot_valid = e->last_sparse = false;
   if (e->frontier) {  // all-zero state: zero totals, empty bitmaps (D, P and dirty flags are zero between rounds)
     const size_t nwb = (e->N + 63) / 64 * 8;
     HIP_OK(e, hipMemsetAsync(e->fb.nzb, 0, nwb, e->stream));
@@ -777,7 +820,7 @@ int gossip_inject(gossip_engine_t* e, uint64_t node, uint32_t rumor) {
     return GOSSIP_OK;
   }
   HIP_OK(e, launch_inject(e->S, e->Nl, e->lo, e->hi, e->N, e->R, e->key0, e->key1, (int64_t)node, rumor, e->stream));
-  e->fr_valid = false;
+  e->fr_valid = e->sx_valid = e->gtot_valid = false;
   return GOSSIP_OK;
 }
 
@@ -794,11 +837,11 @@ int gossip_inject_random(gossip_engine_t* e) {
     return GOSSIP_OK;
   }
   HIP_OK(e, launch_inject(e->S, e->Nl, e->lo, e->hi, e->N, e->R, e->key0, e->key1, -1, 0, e->stream));
-  e->fr_valid = false;
+  e->fr_valid = e->sx_valid = e->gtot_valid = false;
   return GOSSIP_OK;
 }
 
-uint64_t gossip_partial_len(const gossip_engine_t* e) { return e ? 4 + e->R : 0; }
+uint64_t gossip_partial_len(const gossip_engine_t* e) { return e ? part_len(e) : 0; }
 
 int gossip_exchange_buffers(gossip_engine_t* e, void** send, void** recv, uint64_t* send_bytes) {
   if (!e) return GOSSIP_EINVAL;
@@ -822,16 +865,166 @@ int gossip_round_compute(gossip_engine_t* e, uint64_t* partial) {
   HIP_OK(e, hipMemcpyAsync(e->partial_h, e->partial_d, part_len(e) * 8, hipMemcpyDeviceToHost, e->stream));
   HIP_OK(e, hipStreamSynchronize(e->stream));
   if (int rc = timer_collect(e)) return rc;
-  std::memcpy(partial, e->partial_h, (4 + e->R) * 8);
+  std::memcpy(partial, e->partial_h, part_len(e) * 8);
   if (e->mode != GOSSIP_MODE_ANTIENTROPY) partial[1] = e->nown;
+  e->last_sparse = false;
   return GOSSIP_OK;
 }
 
 int gossip_round_commit(gossip_engine_t* e, const uint64_t* total, gossip_round_stats_t* st) {
   if (!e || !total) return GOSSIP_EINVAL;
-  rotate(e);
+  if (!e->last_sparse) rotate(e);  // sparse sharded rounds update S in place
+  e->last_sparse = false;
+  if (e->sx) {  // global totals of S_{t+1}: the next round's plan
+    e->gtot.assign(total, total + part_len(e));
+    e->gtot_valid = true;
+  }
   if (st) fill_stats(e, total, st);
   e->t++;
+  return GOSSIP_OK;
+}
+
+// --- sharded sparse rounds (sharded.h) ---------------------------------------
+
+namespace {
+
+// exact totals of the owned nodes in partial_d and exact bitmaps in lf
+int sx_prepare(gossip_engine* e) {
+  if (e->sx_valid) return GOSSIP_OK;
+  HIP_OK(e, hipMemsetAsync(e->partial_d, 0, part_len(e) * 8, e->stream));
+  HIP_OK(e, launch_frontier_rebuild(e->lf, e->S, e->nown, e->partial_d, e->R, e->cfg.flags, e->stream));
+  e->sx_valid = true;
+  return GOSSIP_OK;
+}
+
+int sx_check(gossip_engine* e, bool planned) {
+  if (!e) return GOSSIP_EINVAL;
+  if (!e->sx) return e->fail(GOSSIP_ENOTSUP, "sparse sharded rounds need G > 1, W == 1 and a random mode");
+  if (planned && !e->sx_planned) return e->fail(GOSSIP_ESTATE, "gossip_sharded_plan did not plan a sparse round");
+  return set_dev(e);
+}
+
+int grow(gossip_engine* e, SxItem** buf, uint64_t* cap, uint64_t items) {
+  if (items <= *cap && *buf) return GOSSIP_OK;
+  const uint64_t want = std::max<uint64_t>(items + items / 4, 1024);
+  if (*buf) HIP_OK(e, hipFree(*buf));
+  *buf = nullptr;
+  *cap = 0;
+  HIP_OK(e, hipMalloc((void**)buf, want * sizeof(SxItem)));
+  *cap = want;
+  return GOSSIP_OK;
+}
+
+int copy_partial_out(gossip_engine* e, uint64_t* partial) {
+  HIP_OK(e, hipMemcpyAsync(e->partial_h, e->partial_d, part_len(e) * 8, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(e, hipStreamSynchronize(e->stream));
+  std::memcpy(partial, e->partial_h, part_len(e) * 8);
+  partial[1] = e->nown;
+  return GOSSIP_OK;
+}
+
+}  // namespace
+
+int gossip_local_totals(gossip_engine_t* e, uint64_t* partial) {
+  if (!partial) return GOSSIP_EINVAL;
+  if (int rc = sx_check(e, false)) return rc;
+  if (int rc = sx_prepare(e)) return rc;
+  return copy_partial_out(e, partial);
+}
+
+int gossip_sharded_plan(gossip_engine_t* e, const uint64_t* total, int32_t* kind) {
+  if (!e || !kind) return GOSSIP_EINVAL;
+  e->sx_planned = false;
+  if (!e->sx) {
+    *kind = 0;
+    return GOSSIP_OK;
+  }
+  if (total) {
+    e->gtot.assign(total, total + part_len(e));
+    e->gtot_valid = true;
+  }
+  if (!e->gtot_valid) {
+    *kind = -1;
+    return GOSSIP_OK;
+  }
+  uint32_t maj = 0;
+  bool all_d = false;
+  e->sx_planned = choose_sparse(e, est_of(e, e->gtot.data()), &maj, &all_d);
+  e->sx_maj = maj;
+  e->sx_alld = all_d;
+  *kind = e->sx_planned ? 1 : 0;
+  return GOSSIP_OK;
+}
+
+int gossip_sparse_rare(gossip_engine_t* e, void** send, uint64_t* count) {
+  if (!send || !count) return GOSSIP_EINVAL;
+  if (int rc = sx_check(e, true)) return rc;
+  if (int rc = sx_prepare(e)) return rc;
+  HIP_OK(e, sx_compact(e->sg, e->sb, e->lf, e->S, e->sx_maj, e->stream));
+  const uint64_t nwl = (e->nown + 63) / 64;
+  e->sx_host[0] = 0;
+  HIP_OK(e, hipMemcpyAsync(e->sx_host, e->sb.wpos + nwl, 4, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(e, hipStreamSynchronize(e->stream));
+  *count = e->sx_host[0] & 0xFFFFFFFFull;
+  *send = e->sb.rare_send;
+  return GOSSIP_OK;
+}
+
+int gossip_sparse_rare_recv(gossip_engine_t* e, uint64_t stride, void** recv) {
+  if (!recv) return GOSSIP_EINVAL;
+  if (int rc = sx_check(e, true)) return rc;
+  if (stride > e->Nl) return e->fail(GOSSIP_EINVAL, "rare list stride %llu > nodes per shard", (unsigned long long)stride);
+  if (int rc = grow(e, &e->rare_recv, &e->rare_recv_cap, stride * e->G)) return rc;
+  e->sx_stride = stride;
+  *recv = e->rare_recv;
+  return GOSSIP_OK;
+}
+
+int gossip_sparse_scan(gossip_engine_t* e, const uint64_t* counts, void** send, uint64_t* send_counts) {
+  if (!counts || !send || !send_counts) return GOSSIP_EINVAL;
+  if (int rc = sx_check(e, true)) return rc;
+  if (!e->rare_recv) return e->fail(GOSSIP_ESTATE, "gossip_sparse_rare_recv first");
+  uint64_t* cb = e->sx_host;
+  cb[0] = 0;
+  for (uint32_t q = 0; q < e->G; ++q) {
+    if (counts[q] > e->sx_stride) return e->fail(GOSSIP_EINVAL, "rare list %u longer than the stride", q);
+    cb[q + 1] = cb[q] + counts[q];
+  }
+  HIP_OK(e, hipMemcpyAsync(e->sb.cbase, cb, (e->G + 1) * 8, hipMemcpyHostToDevice, e->stream));
+  if (int rc = timer_begin(e, 0)) return rc;
+  HIP_OK(e, sx_index(e->sg, e->sb, e->rare_recv, e->sx_stride, e->stream));
+  HIP_OK(e, sx_scan(e->sg, e->sb, e->lf, e->S, e->rare_recv, e->sx_stride, e->t, e->key0, e->key1, e->mode,
+                    e->sx_maj, e->sx_alld, e->stream));
+  if (int rc = timer_end(e, 0)) return rc;
+  HIP_OK(e, hipStreamSynchronize(e->stream));  // cb is read by the copy above
+  HIP_OK(e, hipMemcpyAsync(e->sx_host, e->sb.msg_cnt, (e->G + 1) * 4, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(e, hipStreamSynchronize(e->stream));
+  const uint32_t* c = (const uint32_t*)e->sx_host;
+  for (uint32_t q = 0; q < e->G; ++q) send_counts[q] = c[q];
+  *send = e->sb.msg_out;
+  return GOSSIP_OK;
+}
+
+int gossip_sparse_msg_recv(gossip_engine_t* e, uint64_t items, void** recv) {
+  if (!recv) return GOSSIP_EINVAL;
+  if (int rc = sx_check(e, true)) return rc;
+  if (int rc = grow(e, &e->msg_recv, &e->msg_recv_cap, items)) return rc;
+  *recv = e->msg_recv;
+  return GOSSIP_OK;
+}
+
+int gossip_sparse_commit(gossip_engine_t* e, uint64_t items, uint64_t* partial) {
+  if (!partial) return GOSSIP_EINVAL;
+  if (int rc = sx_check(e, true)) return rc;
+  if (items > e->msg_recv_cap) return e->fail(GOSSIP_EINVAL, "more messages than the receive buffer holds");
+  if (int rc = timer_begin(e, 1)) return rc;
+  HIP_OK(e, sx_apply(e->lf, e->msg_recv, items, e->sx_alld, e->stream));
+  HIP_OK(e, launch_frontier_commit(e->lf, e->S, e->nown, e->partial_d, e->R, e->sx_alld, e->cfg.flags, e->stream));
+  if (int rc = timer_end(e, 1)) return rc;
+  if (int rc = copy_partial_out(e, partial)) return rc;
+  if (int rc = timer_collect(e)) return rc;
+  e->sx_planned = false;
+  e->last_sparse = true;
   return GOSSIP_OK;
 }
 

@@ -27,11 +27,21 @@ struct FrontierBufs {
   uint8_t* dirtyP;    // [ceil(N/64)] group g has a pull delta
   uint32_t glog;      // g = 1 << glog nodes per summary bit
   uint32_t summ_words;
+  uint64_t id0;       // global id of node 0 of these arrays (a shard's first node; 0 on one GPU): the hash uses global ids
 };
 
 uint32_t frontier_glog(uint64_t N);
 size_t frontier_bytes(uint64_t N);
 void frontier_carve(uint64_t N, void* base, FrontierBufs* f);
+
+// Coarse summary (f.summ, 1 bit per 2^f.glog nodes) of the rare set of an
+// N-node bitmap pair: maj 0 -> f.nzb, maj 1 -> not f.fullb.  No early exit.
+hipError_t launch_frontier_summary(const FrontierBufs& f, uint64_t N, uint32_t maj, hipStream_t st);
+
+// The commit half of a sparse round on its own: S |= D | P for the dirty (or,
+// all_d, every) groups, D/P/flags cleared, bitmaps and running totals updated.
+hipError_t launch_frontier_commit(const FrontierBufs& f, uint64_t* S, uint64_t N, uint64_t* partial, uint32_t R,
+                                  bool all_d, uint32_t flags, hipStream_t st);
 
 // Absolute stats of S into partial (zeroed by the caller) + both bitmaps.
 hipError_t launch_frontier_rebuild(const FrontierBufs& f, const uint64_t* S, uint64_t N, uint64_t* partial,

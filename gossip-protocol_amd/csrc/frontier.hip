@@ -92,7 +92,7 @@ __device__ __forceinline__ uint64_t rare_count(const uint64_t* partial, uint64_t
 
 __global__ __launch_bounds__(256) void frontier_summary_kernel(FrontierBufs f, uint64_t N, const uint64_t* partial,
                                                                 uint32_t R, uint32_t maj) {
-  if (rare_count(partial, N, R, maj) == 0) return;
+  if (partial && rare_count(partial, N, R, maj) == 0) return;
   if (maj)
     summary_body<1>(f, N);
   else
@@ -278,8 +278,8 @@ struct GroupStats {
     full += (uint32_t)__popcll(__ballot(valid && nw == fm && old != fm));
     nz += (uint32_t)__popcll(__ballot(valid && nw != 0 && old == 0));
     if (do_hash && nb) {
-      hash += mix64(nw + n * kGold64);
-      if (old) hash -= mix64(old + n * kGold64);
+      hash += mix64(nw + (f.id0 + n) * kGold64);
+      if (old) hash -= mix64(old + (f.id0 + n) * kGold64);
     }
     if (__ballot(nb != 0)) c_lane += (uint32_t)__popcll(transpose64(nb, lane));
   }
@@ -467,6 +467,20 @@ void frontier_carve(uint64_t N, void* base, FrontierBufs* f) {
   f->dirtyP = (uint8_t*)p;
 }
 
+hipError_t launch_frontier_summary(const FrontierBufs& f, uint64_t N, uint32_t maj, hipStream_t st) {
+  frontier_summary_kernel<<<(f.summ_words + 255) / 256, 256, 0, st>>>(f, N, nullptr, 0, maj);
+  return hipGetLastError();
+}
+
+hipError_t launch_frontier_commit(const FrontierBufs& f, uint64_t* S, uint64_t N, uint64_t* partial, uint32_t R,
+                                  bool all_d, uint32_t flags, hipStream_t st) {
+  const uint64_t wchunks = (((N + 63) >> 6) + 63) >> 6;  // 64-group chunks, one per wave
+  const uint64_t cblocks = (wchunks + kCommitThreads / 64 - 1) / (kCommitThreads / 64);
+  frontier_commit_kernel<<<(uint32_t)(cblocks < 4096 ? cblocks : 4096), kCommitThreads, 0, st>>>(f, S, N, partial,
+                                                                                                 R, flags, all_d);
+  return hipGetLastError();
+}
+
 hipError_t launch_frontier_rebuild(const FrontierBufs& f, const uint64_t* S, uint64_t N, uint64_t* partial,
                                    uint32_t R, uint32_t flags, hipStream_t st) {
   frontier_rebuild_kernel<<<commit_grid(N), kCommitThreads, 0, st>>>(f, S, N, partial, R, flags);
@@ -495,10 +509,8 @@ hipError_t launch_frontier_round(const FrontierBufs& f, uint64_t* S, uint64_t N,
     case 3: frontier_scan_kernel<3><<<grid, kScanThreads, 0, st>>>(f, S, N, R, k, t, key0, key1, per, partial, maj, !all_d); break;
     default: return hipErrorInvalidValue;
   }
-  const uint64_t wchunks = (((N + 63) >> 6) + 63) >> 6;  // 64-group chunks, one per wave
-  const uint64_t cblocks = (wchunks + kCommitThreads / 64 - 1) / (kCommitThreads / 64);
-  frontier_commit_kernel<<<(uint32_t)(cblocks < 4096 ? cblocks : 4096), kCommitThreads, 0, st>>>(f, S, N, partial,
-                                                                                                 R, flags, all_d);
+  const hipError_t ce = launch_frontier_commit(f, S, N, partial, R, all_d, flags, st);
+  if (ce != hipSuccess) return ce;
   return launch_round_snapshot(partial, rs, st);
 }
 

@@ -1,0 +1,454 @@
+// sharded.hip — sparse rounds across G shards (sharded.h).
+//
+// Reference hot path: (*NodeState).Gossip, main.go:65-89, whose only
+// cross-node traffic is the per-neighbour SyncRPC (main.go:81).  Here a sparse
+// round's cross-shard traffic is the rare list (all-gather) and the pushes
+// that land on another shard (all-to-all); everything else stays on the GPU
+// that owns the node.  The scan follows frontier.hip's (same tests, same
+// batching of loads before stores), with peers drawn over the global id space.
+#include <hipcub/hipcub.hpp>
+
+#include "philox.h"
+#include "sharded.h"
+#include "wave.h"
+
+namespace gossip {
+
+namespace {
+
+constexpr int kScanThreads = 1024;
+constexpr uint32_t kScanGrid = 256;  // one block per CU: the summary takes 128 KiB of LDS
+constexpr uint32_t kRwWords = 1024;  // own rare-bitmap words staged per chunk (64K nodes)
+constexpr int kScanUnroll = 2;
+constexpr uint32_t kMsgShift = 40;   // message node word: owner << 40 | node at the owner
+
+__device__ __forceinline__ uint64_t word_valid(uint64_t w, uint64_t n) {
+  const uint64_t lo = w << 6;
+  return n >= lo + 64 ? ~0ull : ((1ull << (n - lo)) - 1ull);
+}
+
+// own rare word w: maj 0 -> nonzero nodes, maj 1 -> nodes not yet full
+__device__ __forceinline__ uint64_t own_rare(const FrontierBufs& f, uint64_t w, uint64_t nown, uint32_t maj) {
+  return maj ? (~f.fullb[w] & word_valid(w, nown)) : f.nzb[w];
+}
+
+__global__ __launch_bounds__(256) void wcount_kernel(FrontierBufs f, uint64_t nown, uint32_t maj, uint32_t* wcount) {
+  const uint64_t nw = (nown + 63) >> 6;
+  const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (w < nw) wcount[w] = (uint32_t)__popcll(own_rare(f, w, nown, maj));
+  else if (w == nw) wcount[w] = 0;
+}
+
+__global__ __launch_bounds__(256) void list_kernel(FrontierBufs f, const uint64_t* __restrict__ S, uint64_t nown,
+                                                    uint64_t lo, uint32_t maj, const uint32_t* __restrict__ wpos,
+                                                    SxItem* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nown) return;
+  const uint64_t w = i >> 6;
+  const uint64_t x = own_rare(f, w, nown, maj);  // one word per 64 lanes
+  const uint32_t b = (uint32_t)(i & 63);
+  if (!((x >> b) & 1ull)) return;
+  const uint32_t pos = wpos[w] + (uint32_t)__popcll(x & ((1ull << b) - 1ull));
+  out[pos] = SxItem{lo + i, S[i]};
+}
+
+__global__ __launch_bounds__(256) void setbits_kernel(const SxItem* __restrict__ recv, uint64_t stride, uint32_t G,
+                                                       const uint64_t* __restrict__ cbase, uint64_t* __restrict__ grb) {
+  const uint64_t total = stride * G;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (uint64_t)gridDim.x * 256) {
+    const uint32_t q = (uint32_t)(i / stride);
+    if (i - q * stride >= cbase[q + 1] - cbase[q]) continue;  // padding of a shorter list
+    const uint64_t p = recv[i].node;
+    atomicOr((unsigned long long*)&grb[p >> 6], 1ull << (p & 63));
+  }
+}
+
+__global__ __launch_bounds__(256) void gcount_kernel(const uint64_t* __restrict__ grb, uint64_t nwg, uint32_t* gcnt) {
+  const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (w < nwg) gcnt[w] = (uint32_t)__popcll(grb[w]);
+  else if (w == nwg) gcnt[w] = 0;
+}
+
+struct ScanArgs {
+  FrontierBufs lf;
+  const uint64_t* S;
+  const SxItem* recv;
+  uint64_t stride;
+  const uint64_t* grb;
+  const uint32_t* gpre;
+  const uint64_t* cbase;
+  const uint32_t* gsumm;
+  uint32_t gglog, gsumm_words;
+  SxItem* msg;
+  uint32_t* msg_cnt;
+  uint64_t N, Nl, lo, nown, per_block;
+  uint32_t G, R, k, t, key0, key1, mark_d;
+};
+
+// S_t of a rare node p (global id) whose bitmap word is rw: own shard from S,
+// another shard from the gathered lists (its rank among the rare nodes, minus
+// the lists before its owner's, is its place in the owner's list)
+__device__ __forceinline__ uint64_t rare_value(const ScanArgs& a, uint32_t p, uint64_t rw, uint32_t pre) {
+  const uint32_t q = (uint32_t)(p / a.Nl);
+  const uint64_t rank = (uint64_t)pre + (uint64_t)__popcll(rw & ((1ull << (p & 63u)) - 1ull));
+  return a.recv[q * a.stride + (rank - a.cbase[q])].value;
+}
+
+template <int MAJ, int MODE>
+__device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const ScanArgs& a) {
+  const uint32_t* summ = (const uint32_t*)summ4;
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t n4 = (a.gsumm_words + 3) / 4;
+  for (uint32_t i = tid; i < n4; i += kScanThreads) summ4[i] = ((const uint4*)a.gsumm)[i];
+
+  constexpr bool kPush = (MODE & 1) != 0, kPull = (MODE & 2) != 0;
+  const uint64_t fm = full_mask1(a.R), maj = MAJ ? fm : 0ull, nm1 = a.N - 1;
+  const uint32_t glog = a.gglog, lo = (uint32_t)a.lo, nown = (uint32_t)a.nown, k = a.k;
+  auto summ_bit = [&](uint32_t p) -> bool { return (summ[p >> (glog + 5)] >> ((p >> glog) & 31u)) & 1u; };
+  const uint64_t below = (1ull << lane) - 1ull;
+  // push delta d (may be 0) to global node p; every lane of the wave calls this
+  // together: a wave reserves its messages' slots with one atomic
+  auto push_to = [&](uint32_t p, uint64_t d) {
+    const bool local = d && (p - lo < nown);
+    if (local) {
+      atomicOr((unsigned long long*)&a.lf.D[p - lo], (unsigned long long)d);
+      if (a.mark_d) a.lf.dirtyD[(p - lo) >> 6] = 1;
+    }
+    const bool remote = d && !local;
+    const uint64_t m = __ballot(remote);
+    if (!m) return;
+    const uint32_t first = (uint32_t)__builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane == first) base = atomicAdd(&a.msg_cnt[a.G], (uint32_t)__popcll(m));
+    base = __shfl(base, first, 64);
+    if (remote) {
+      const uint32_t q = (uint32_t)(p / a.Nl);
+      a.msg[base + (uint32_t)__popcll(m & below)] = SxItem{((uint64_t)q << kMsgShift) | (p - (uint64_t)q * a.Nl), d};
+    }
+  };
+  // node ids are < 2^32 (gossip_create checks N)
+  const uint32_t b0 = blockIdx.x * (uint32_t)a.per_block;
+  const uint32_t b1 = (uint32_t)min<uint64_t>((uint64_t)b0 + a.per_block, a.nown);
+  for (uint32_t c0 = b0; c0 < b1; c0 += kRwWords * 64) {
+    const uint32_t c1 = min(c0 + kRwWords * 64, b1);
+    __syncthreads();  // previous chunk done with rws
+    for (uint32_t i = tid; i < ((c1 - c0 + 63) >> 6); i += kScanThreads)
+      rws[i] = own_rare(a.lf, (c0 >> 6) + i, a.nown, MAJ);
+    __syncthreads();
+    for (uint32_t base = c0; base < c1; base += kScanThreads * kScanUnroll) {
+      uint32_t pp[kScanUnroll][4], hit[kScanUnroll];
+      bool act[kScanUnroll], rn[kScanUnroll];
+      // 1. draws and LDS summary tests
+#pragma unroll
+      for (int u = 0; u < kScanUnroll; ++u) {
+        const uint32_t i = base + u * kScanThreads + tid;
+        const bool valid = i < c1;
+        const uint32_t n = lo + i;
+        rn[u] = valid && ((rws[(i - c0) >> 6] >> lane) & 1ull);
+        act[u] = valid && (rn[u] || !((!kPull && MAJ == 0) || (!kPush && MAJ == 1)));
+        hit[u] = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) pp[u][j] = 0;
+        if (act[u] && k <= 4) {
+          const u32x4 r4 = philox4x32_10(u32x4{n, a.t, 0u, 0u}, a.key0, a.key1);
+#pragma unroll
+          for (uint32_t j = 0; j < 4; ++j) {
+            if (j >= k) break;
+            pp[u][j] = peer_from_word(lane_of(r4, j), nm1, n);
+            if (summ_bit(pp[u][j])) hit[u] |= 1u << j;
+          }
+        }
+      }
+      // 2. exact probes in the global rare bitmap (all issued, then consumed)
+      uint64_t rw[kScanUnroll][4];
+#pragma unroll
+      for (int u = 0; u < kScanUnroll; ++u)
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) rw[u][j] = ((hit[u] >> j) & 1u) ? a.grb[pp[u][j] >> 6] : 0ull;
+#pragma unroll
+      for (int u = 0; u < kScanUnroll; ++u)
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j)
+          if (!((rw[u][j] >> (pp[u][j] & 63u)) & 1ull)) hit[u] &= ~(1u << j);
+      // 3. S_t of the rare ends: own shard directly, other shards through the lists
+      uint32_t pre[kScanUnroll][4];
+#pragma unroll
+      for (int u = 0; u < kScanUnroll; ++u)
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+          const bool remote = ((hit[u] >> j) & 1u) && (pp[u][j] - lo >= nown);
+          pre[u][j] = remote ? a.gpre[pp[u][j] >> 6] : 0u;
+        }
+      uint64_t x[kScanUnroll], vp[kScanUnroll][4];
+#pragma unroll
+      for (int u = 0; u < kScanUnroll; ++u) {
+        const uint32_t i = base + u * kScanThreads + tid;
+        x[u] = rn[u] ? a.S[i] : maj;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+          const uint32_t p = pp[u][j];
+          if (!((hit[u] >> j) & 1u)) vp[u][j] = maj;
+          else if (p - lo < nown) vp[u][j] = a.S[p - lo];
+          else vp[u][j] = rare_value(a, p, rw[u][j], pre[u][j]);
+        }
+      }
+      // 4. deltas in registers, then the stores (frontier.hip: vmcnt retires in order)
+      uint64_t accs[kScanUnroll], dpush[kScanUnroll][4];
+#pragma unroll
+      for (int u = 0; u < kScanUnroll; ++u) {
+        accs[u] = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) dpush[u][j] = 0;
+        if (!act[u] || k > 4) continue;
+        uint64_t acc = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+          if (j >= k) break;
+          if (!rn[u] && !((hit[u] >> j) & 1u)) continue;  // both ends majority: nothing moves
+          if (kPull) acc |= vp[u][j];
+          if (kPush) dpush[u][j] = x[u] & ~vp[u][j];
+        }
+        accs[u] = acc & ~x[u];
+      }
+#pragma unroll
+      for (int u = 0; u < kScanUnroll; ++u)
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) push_to(pp[u][j], dpush[u][j]);
+      // k > 4: the draws are redone edge by edge
+      if (k > 4) {
+#pragma unroll
+        for (int u = 0; u < kScanUnroll; ++u) {
+          if (!act[u]) continue;
+          const uint32_t i = base + u * kScanThreads + tid, n = lo + i;
+          uint64_t acc = 0;
+          u32x4 r4{0, 0, 0, 0};
+          for (uint32_t j = 0; j < k; ++j) {
+            if ((j & 3u) == 0) r4 = philox4x32_10(u32x4{n, a.t, 0u, j >> 2}, a.key0, a.key1);
+            const uint32_t p = peer_from_word(lane_of(r4, j & 3u), nm1, n);
+            uint64_t w = 0;
+            bool rp = summ_bit(p);
+            if (rp) {
+              w = a.grb[p >> 6];
+              rp = (w >> (p & 63u)) & 1ull;
+            }
+            const bool moves = rn[u] || rp;  // else both ends majority: nothing moves
+            uint64_t v = maj;
+            if (rp) v = (p - lo < nown) ? a.S[p - lo] : rare_value(a, p, w, a.gpre[p >> 6]);
+            if (kPull && moves) acc |= v;
+            if (kPush) push_to(p, moves ? x[u] & ~v : 0ull);
+          }
+          accs[u] = acc & ~x[u];
+        }
+      }
+      // pull deltas: whole 8-word chunks (P is zero where there is no delta)
+#pragma unroll
+      for (int u = 0; u < kScanUnroll; ++u) {
+        const uint32_t i = base + u * kScanThreads + tid;
+        const uint64_t pz = __ballot(accs[u] != 0);
+        if (!pz) continue;
+        if (i < c1 && ((pz >> (lane & ~7u)) & 0xFFull)) a.lf.P[i] = accs[u];
+        if (accs[u]) a.lf.dirtyP[i >> 6] = 1;
+      }
+    }
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kScanThreads) void sx_scan_kernel(ScanArgs a, uint32_t maj) {
+  __shared__ uint4 summ4[kSummBits / 128];
+  __shared__ uint64_t rws[kRwWords];
+  if (maj)
+    scan_body<1, MODE>(summ4, rws, a);
+  else
+    scan_body<0, MODE>(summ4, rws, a);
+}
+
+// Messages grouped by owner, in two passes over the same per-block chunks:
+// count (LDS histogram, one global atomic per block and owner), then scatter
+// (each block reserves its run per owner once, then places its messages).
+constexpr uint32_t kMaxShards = 1024;
+constexpr uint32_t kGroupBlocks = 512;
+
+__device__ __forceinline__ void chunk_of(uint32_t total, uint32_t* b, uint32_t* e) {
+  const uint32_t per = (total + gridDim.x - 1) / gridDim.x;
+  *b = min(blockIdx.x * per, total);
+  *e = min(*b + per, total);
+}
+
+__global__ __launch_bounds__(256) void owner_count_kernel(const SxItem* __restrict__ msg, uint32_t* cnt, uint32_t G) {
+  __shared__ uint32_t h[kMaxShards];
+  for (uint32_t q = threadIdx.x; q < G; q += 256) h[q] = 0;
+  __syncthreads();
+  uint32_t b, e;
+  chunk_of(cnt[G], &b, &e);
+  for (uint32_t i = b + threadIdx.x; i < e; i += 256) atomicAdd(&h[(uint32_t)(msg[i].node >> kMsgShift)], 1u);
+  __syncthreads();
+  for (uint32_t q = threadIdx.x; q < G; q += 256)
+    if (h[q]) atomicAdd(&cnt[q], h[q]);
+}
+
+__global__ __launch_bounds__(256) void owner_scatter_kernel(const SxItem* __restrict__ msg, SxItem* __restrict__ out,
+                                                             const uint32_t* __restrict__ cnt, uint32_t* fill,
+                                                             uint32_t G) {
+  __shared__ uint32_t h[kMaxShards], base[kMaxShards];
+  for (uint32_t q = threadIdx.x; q < G; q += 256) h[q] = 0;
+  __syncthreads();
+  uint32_t b, e;
+  chunk_of(cnt[G], &b, &e);
+  for (uint32_t i = b + threadIdx.x; i < e; i += 256) atomicAdd(&h[(uint32_t)(msg[i].node >> kMsgShift)], 1u);
+  __syncthreads();
+  if (threadIdx.x == 0) {  // owner q's messages start after those of owners < q
+    uint32_t off = 0;
+    for (uint32_t q = 0; q < G; ++q) {
+      base[q] = off + (h[q] ? atomicAdd(&fill[q], h[q]) : 0u);
+      off += cnt[q];
+    }
+  }
+  __syncthreads();
+  for (uint32_t q = threadIdx.x; q < G; q += 256) h[q] = 0;
+  __syncthreads();
+  for (uint32_t i = b + threadIdx.x; i < e; i += 256) {
+    const SxItem m = msg[i];
+    const uint32_t q = (uint32_t)(m.node >> kMsgShift);
+    out[base[q] + atomicAdd(&h[q], 1u)] = SxItem{m.node & ((1ull << kMsgShift) - 1ull), m.value};
+  }
+}
+
+__global__ __launch_bounds__(256) void apply_kernel(FrontierBufs f, const SxItem* __restrict__ in, uint64_t n,
+                                                     uint32_t mark_d) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    const SxItem m = in[i];
+    atomicOr((unsigned long long*)&f.D[m.node], (unsigned long long)m.value);
+    if (mark_d) f.dirtyD[m.node >> 6] = 1;
+  }
+}
+
+size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+size_t scan_tmp_bytes(uint64_t n) {
+  size_t bytes = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
+  return bytes;
+}
+
+uint32_t grid_for(uint64_t n, uint32_t block, uint32_t cap) {
+  const uint64_t g = (n + block - 1) / block;
+  return (uint32_t)(g == 0 ? 1 : (g < cap ? g : cap));
+}
+
+}  // namespace
+
+size_t sx_bytes(const SxGeom& g) {
+  const uint64_t nwl = (g.nown + 63) / 64, nwg = (g.N + 63) / 64;
+  const uint32_t glog = frontier_glog(g.N);
+  const size_t sw = ((((g.N + (1ull << glog) - 1) >> glog) + 127) / 128) * 4;
+  const size_t tmp = std::max(scan_tmp_bytes(nwl + 1), scan_tmp_bytes(nwg + 1));
+  const uint64_t cap = (uint64_t)g.k * g.nown;
+  return 2 * al256((nwl + 1) * 4) + al256(g.Nl * sizeof(SxItem)) + al256(nwg * 8) + 2 * al256((nwg + 1) * 4) +
+         al256(sw * 4) + al256((g.G + 1) * 8) + 2 * al256(cap * sizeof(SxItem)) + al256((g.G + 2) * 4) +
+         al256(g.G * 4) + al256(tmp);
+}
+
+void sx_carve(const SxGeom& g, void* base, SxBufs* b) {
+  const uint64_t nwl = (g.nown + 63) / 64, nwg = (g.N + 63) / 64;
+  char* p = (char*)base;
+  auto take = [&](size_t bytes) {
+    char* r = p;
+    p += al256(bytes);
+    return r;
+  };
+  b->wcount = (uint32_t*)take((nwl + 1) * 4);
+  b->wpos = (uint32_t*)take((nwl + 1) * 4);
+  b->rare_send = (SxItem*)take(g.Nl * sizeof(SxItem));  // Nl >= any shard's count: the driver sends max-count items
+  b->grb = (uint64_t*)take(nwg * 8);
+  b->gcnt = (uint32_t*)take((nwg + 1) * 4);
+  b->gpre = (uint32_t*)take((nwg + 1) * 4);
+  b->gsum = FrontierBufs{};
+  b->gsum.glog = frontier_glog(g.N);
+  b->gsum.summ_words = (uint32_t)((((g.N + (1ull << b->gsum.glog) - 1) >> b->gsum.glog) + 127) / 128) * 4;
+  b->gsum.nzb = b->grb;
+  b->gsum.summ = (uint32_t*)take((size_t)b->gsum.summ_words * 4);
+  b->cbase = (uint64_t*)take((g.G + 1) * 8);
+  b->cap = (uint64_t)g.k * g.nown;
+  b->msg = (SxItem*)take(b->cap * sizeof(SxItem));
+  b->msg_out = (SxItem*)take(b->cap * sizeof(SxItem));
+  b->msg_cnt = (uint32_t*)take((g.G + 2) * 4);
+  b->msg_fill = (uint32_t*)take(g.G * 4);
+  b->tmp_bytes = std::max(scan_tmp_bytes(nwl + 1), scan_tmp_bytes(nwg + 1));
+  b->tmp = take(b->tmp_bytes);
+}
+
+hipError_t sx_compact(const SxGeom& g, const SxBufs& b, const FrontierBufs& lf, const uint64_t* S, uint32_t maj,
+                      hipStream_t st) {
+  const uint64_t nwl = (g.nown + 63) / 64;
+  wcount_kernel<<<grid_for(nwl + 1, 256, 1u << 30), 256, 0, st>>>(lf, g.nown, maj, b.wcount);
+  size_t tb = b.tmp_bytes;
+  hipError_t e = hipcub::DeviceScan::ExclusiveSum(b.tmp, tb, b.wcount, b.wpos, (int)(nwl + 1), st);
+  if (e != hipSuccess) return e;
+  list_kernel<<<grid_for(g.nown, 256, 1u << 30), 256, 0, st>>>(lf, S, g.nown, g.lo, maj, b.wpos, b.rare_send);
+  return hipGetLastError();
+}
+
+hipError_t sx_index(const SxGeom& g, const SxBufs& b, const SxItem* recv, uint64_t stride, hipStream_t st) {
+  const uint64_t nwg = (g.N + 63) / 64;
+  hipError_t e = hipMemsetAsync(b.grb, 0, nwg * 8, st);
+  if (e != hipSuccess) return e;
+  if (stride) setbits_kernel<<<grid_for(stride * g.G, 256, 4096), 256, 0, st>>>(recv, stride, g.G, b.cbase, b.grb);
+  gcount_kernel<<<grid_for(nwg + 1, 256, 1u << 30), 256, 0, st>>>(b.grb, nwg, b.gcnt);
+  size_t tb = b.tmp_bytes;
+  e = hipcub::DeviceScan::ExclusiveSum(b.tmp, tb, b.gcnt, b.gpre, (int)(nwg + 1), st);
+  if (e != hipSuccess) return e;
+  return launch_frontier_summary(b.gsum, g.N, 0, st);
+}
+
+hipError_t sx_scan(const SxGeom& g, const SxBufs& b, const FrontierBufs& lf, const uint64_t* S, const SxItem* recv,
+                   uint64_t stride, uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t maj, bool all_d,
+                   hipStream_t st) {
+  hipError_t e = hipMemsetAsync(b.msg_cnt, 0, (g.G + 2) * 4, st);
+  if (e == hipSuccess) e = hipMemsetAsync(b.msg_fill, 0, g.G * 4, st);
+  if (e != hipSuccess) return e;
+  ScanArgs a{};
+  a.lf = lf;
+  a.S = S;
+  a.recv = recv;
+  a.stride = stride;
+  a.grb = b.grb;
+  a.gpre = b.gpre;
+  a.cbase = b.cbase;
+  a.gsumm = b.gsum.summ;
+  a.gglog = b.gsum.glog;
+  a.gsumm_words = b.gsum.summ_words;
+  a.msg = b.msg;
+  a.msg_cnt = b.msg_cnt;
+  a.N = g.N;
+  a.Nl = g.Nl;
+  a.lo = g.lo;
+  a.nown = g.nown;
+  a.G = g.G;
+  a.R = g.R;
+  a.k = g.k;
+  a.t = t;
+  a.key0 = key0;
+  a.key1 = key1;
+  a.mark_d = all_d ? 0u : 1u;
+  const uint64_t chunks = (g.nown + kScanThreads - 1) / kScanThreads;
+  const uint32_t grid = (uint32_t)(chunks < kScanGrid ? (chunks ? chunks : 1) : kScanGrid);
+  a.per_block = ((g.nown + grid - 1) / grid + kScanThreads - 1) / kScanThreads * kScanThreads;
+  switch (mode) {
+    case 1: sx_scan_kernel<1><<<grid, kScanThreads, 0, st>>>(a, maj); break;
+    case 2: sx_scan_kernel<2><<<grid, kScanThreads, 0, st>>>(a, maj); break;
+    case 3: sx_scan_kernel<3><<<grid, kScanThreads, 0, st>>>(a, maj); break;
+    default: return hipErrorInvalidValue;
+  }
+  owner_count_kernel<<<kGroupBlocks, 256, 0, st>>>(b.msg, b.msg_cnt, g.G);
+  owner_scatter_kernel<<<kGroupBlocks, 256, 0, st>>>(b.msg, b.msg_out, b.msg_cnt, b.msg_fill, g.G);
+  return hipGetLastError();
+}
+
+hipError_t sx_apply(const FrontierBufs& lf, const SxItem* in, uint64_t n, bool all_d, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  apply_kernel<<<grid_for(n, 256, 4096), 256, 0, st>>>(lf, in, n, all_d ? 0u : 1u);
+  return hipGetLastError();
+}
+
+}  // namespace gossip

@@ -68,6 +68,13 @@ SIGNATURES = [
     ("exchange_buffers", C.c_int, [P, C.POINTER(P), C.POINTER(P), U64P]),
     ("round_compute", C.c_int, [P, U64P]),
     ("round_commit", C.c_int, [P, U64P, C.POINTER(RoundStats)]),
+    ("sharded_plan", C.c_int, [P, U64P, C.POINTER(C.c_int32)]),
+    ("local_totals", C.c_int, [P, U64P]),
+    ("sparse_rare", C.c_int, [P, C.POINTER(P), U64P]),
+    ("sparse_rare_recv", C.c_int, [P, C.c_uint64, C.POINTER(P)]),
+    ("sparse_scan", C.c_int, [P, U64P, C.POINTER(P), U64P]),
+    ("sparse_msg_recv", C.c_int, [P, C.c_uint64, C.POINTER(P)]),
+    ("sparse_commit", C.c_int, [P, C.c_uint64, U64P]),
     ("read_bitset", C.c_int, [P, C.c_uint64, U64P, C.c_uint32]),
     ("read_shard", C.c_int, [P, U64P, C.c_uint64]),
     ("read_versions", C.c_int, [P, C.c_uint64, U32P, C.c_uint32, U32P]),

@@ -102,6 +102,10 @@ class AbiEngine:
     def _fn(self, name):
         return getattr(self._lib, self._p + name)
 
+    def supports(self, name: str) -> bool:
+        """Whether the bound library exports gossip_<name> (the CPU oracle has no sparse sharded rounds)."""
+        return hasattr(self._lib, self._p + name)
+
     def _check(self, rc: int):
         if rc != 0:
             raise GossipError(rc, self._fn("last_error")(self._h).decode(errors="replace"))
@@ -212,6 +216,50 @@ class AbiEngine:
         self._check(self._fn("round_commit")(self._h, total.ctypes.data_as(_abi.U64P), C.byref(st)))
         return st.as_dict()
 
+    # -- sparse sharded rounds (include/gossip.h; gossip_hip.sharded drives them) --
+    def sharded_plan(self, total=None) -> int:
+        """-1: needs global totals (local_totals + all-reduce), 0: dense round, 1: sparse round."""
+        kind = C.c_int32()
+        t = None if total is None else np.ascontiguousarray(total, dtype=np.uint64)
+        self._check(self._fn("sharded_plan")(self._h, None if t is None else t.ctypes.data_as(_abi.U64P),
+                                             C.byref(kind)))
+        return kind.value
+
+    def local_totals(self) -> np.ndarray:
+        out = np.zeros(self.partial_len(), dtype=np.uint64)
+        self._check(self._fn("local_totals")(self._h, out.ctypes.data_as(_abi.U64P)))
+        return out
+
+    def sparse_rare(self):
+        """(device pointer, count) of this shard's rare list (16-B items)."""
+        ptr, count = C.c_void_p(), C.c_uint64()
+        self._check(self._fn("sparse_rare")(self._h, C.byref(ptr), C.byref(count)))
+        return ptr.value, count.value
+
+    def sparse_rare_recv(self, stride: int) -> int:
+        ptr = C.c_void_p()
+        self._check(self._fn("sparse_rare_recv")(self._h, stride, C.byref(ptr)))
+        return ptr.value
+
+    def sparse_scan(self, counts):
+        """(device pointer, items per owner) of the push messages for other shards."""
+        c = np.ascontiguousarray(counts, dtype=np.uint64)
+        out = np.zeros(len(c), dtype=np.uint64)
+        ptr = C.c_void_p()
+        self._check(self._fn("sparse_scan")(self._h, c.ctypes.data_as(_abi.U64P), C.byref(ptr),
+                                            out.ctypes.data_as(_abi.U64P)))
+        return ptr.value, out
+
+    def sparse_msg_recv(self, items: int) -> int:
+        ptr = C.c_void_p()
+        self._check(self._fn("sparse_msg_recv")(self._h, items, C.byref(ptr)))
+        return ptr.value
+
+    def sparse_commit(self, items: int) -> np.ndarray:
+        out = np.zeros(self.partial_len(), dtype=np.uint64)
+        self._check(self._fn("sparse_commit")(self._h, items, out.ctypes.data_as(_abi.U64P)))
+        return out
+
 
 class Engine(AbiEngine):
     """The HIP engine (libgossip_hip.so) on one gfx950 device."""
@@ -224,6 +272,10 @@ class Engine(AbiEngine):
         cfg = make_config(n_nodes, n_rumors, mode, fanout, seed, flags, device, shard_rank, shard_count,
                           churn_fail, churn_recover)
         super().__init__(load_library(), "gossip_", cfg)
+        if device < 0:  # the caller's current HIP device (torch is only plumbing, imported on demand)
+            import torch
+            device = torch.cuda.current_device()
+        self.device = device
 
     def set_stream(self, hip_stream: int):
         self._check(self._fn("set_stream")(self._h, C.c_void_p(hip_stream)))

@@ -1,12 +1,20 @@
 """Sharded rounds across ranks: one engine per GPU, node ids
-split into contiguous shards, one all-gather of the exchange image per round
-plus a tiny all-reduce of the stats partials.
+split into contiguous shards.
 
 Reference anchor: the only cross-node traffic of the reference is the
-per-neighbour SyncRPC of (*NodeState).Gossip (main.go:81).  Here a round's
-cross-shard traffic is a single RCCL all-gather over xGMI (torch.distributed
-backend "nccl" is RCCL on ROCm); on CPU the same code runs over gloo, which is
-how the N>1 path is tested without a GPU.
+per-neighbour SyncRPC of (*NodeState).Gossip (main.go:81).  Here each round is
+one of two exchanges over RCCL (torch.distributed backend "nccl" is RCCL on
+ROCm; on CPU the same code runs over gloo, which is how the N>1 path is tested
+without a GPU):
+
+  dense round   all-gather of every shard's state slice (the exchange image),
+                then an all-reduce of the stats partials;
+  sparse round  (the engine's plan, when one class of nodes is rare) all-gather
+                of each shard's rare nodes {id, value}, all-to-all of the pushes
+                that land on another shard, all-reduce of the partials.
+
+The engine decides the kind from the global totals it was last given, so every
+rank takes the same branch.
 """
 from __future__ import annotations
 
@@ -15,6 +23,8 @@ import ctypes as C
 import numpy as np
 import torch
 import torch.distributed as dist
+
+ITEM_WORDS = 2  # sparse exchange items are {uint64 node, uint64 value}
 
 
 class _DevPtr:
@@ -26,9 +36,12 @@ class _DevPtr:
         }
 
 
-def _as_tensor(ptr: int, nbytes: int, on_device: bool) -> torch.Tensor:
+def _as_tensor(ptr: int, nbytes: int, on_device: bool, device: int | None = None) -> torch.Tensor:
+    dev = torch.device("cuda", torch.cuda.current_device() if device is None else device) if on_device else "cpu"
+    if nbytes == 0:
+        return torch.empty(0, dtype=torch.int64, device=dev)
     if on_device:
-        return torch.as_tensor(_DevPtr(ptr, nbytes), device=torch.device("cuda", torch.cuda.current_device()))
+        return torch.as_tensor(_DevPtr(ptr, nbytes), device=dev)
     arr = np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_int64)), shape=(nbytes // 8,))
     return torch.from_numpy(arr)
 
@@ -37,31 +50,107 @@ def _device_collectives(group) -> bool:
     return dist.get_backend(group) == "nccl"
 
 
+class _Comm:
+    """The collectives a round needs, on engine memory: in place over RCCL for
+    device engines, staged through host tensors over gloo."""
+
+    def __init__(self, engine, group):
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.on_device = engine.on_device
+        self.direct = engine.on_device and self.world > 1 and _device_collectives(group)
+
+    def _sync(self):
+        if self.on_device:
+            torch.cuda.synchronize()
+
+    def all_gather(self, recv: torch.Tensor, send: torch.Tensor):
+        if self.direct:
+            dist.all_gather_into_tensor(recv, send, group=self.group)
+            return
+        host = torch.empty(recv.numel(), dtype=torch.int64)
+        dist.all_gather_into_tensor(host, send.cpu() if self.on_device else send.clone(), group=self.group)
+        recv.copy_(host)
+        self._sync()
+
+    def all_to_all(self, recv: torch.Tensor, send: torch.Tensor, recv_splits, send_splits):
+        if self.direct:
+            dist.all_to_all_single(recv, send, output_split_sizes=recv_splits, input_split_sizes=send_splits,
+                                   group=self.group)
+            return
+        host = torch.empty(recv.numel(), dtype=torch.int64)
+        dist.all_to_all_single(host, send.cpu() if self.on_device else send.clone(), output_split_sizes=recv_splits,
+                               input_split_sizes=send_splits, group=self.group)
+        recv.copy_(host)
+        self._sync()
+
+    def small(self, values) -> torch.Tensor:
+        t = torch.as_tensor(np.asarray(values, dtype=np.int64).copy())
+        return t.cuda() if self.direct else t
+
+    def all_reduce_sum(self, partial: np.ndarray) -> np.ndarray:
+        t = self.small(partial.view(np.int64))
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        return t.cpu().numpy().view(np.uint64)
+
+    def all_gather_small(self, value: int) -> list:
+        out = self.small(np.zeros(self.world))
+        dist.all_gather_into_tensor(out, self.small([value]), group=self.group)
+        return [int(x) for x in out.cpu()]
+
+    def all_to_all_small(self, values) -> list:
+        out = self.small(np.zeros(self.world))
+        dist.all_to_all_single(out, self.small(values), group=self.group)
+        return [int(x) for x in out.cpu()]
+
+
+def _plan(engine, comm: _Comm) -> int:
+    if not engine.supports("sharded_plan"):
+        return 0
+    kind = engine.sharded_plan()
+    if kind < 0:  # no global totals yet (after reset / inject): all-reduce the shards' own
+        kind = engine.sharded_plan(comm.all_reduce_sum(engine.local_totals()) if comm.world > 1
+                                   else engine.local_totals())
+    return kind
+
+
+def _dense_round(engine, comm: _Comm) -> np.ndarray:
+    send_p, recv_p, nbytes = engine.exchange_buffers()
+    if comm.world > 1:
+        recv = _as_tensor(recv_p, nbytes * comm.world, engine.on_device)
+        send = _as_tensor(send_p, nbytes, engine.on_device)
+        # RCCL all-gather in place: the send slice lies inside the image
+        comm.all_gather(recv, send)
+    return engine.round_compute()
+
+
+def _sparse_round(engine, comm: _Comm) -> np.ndarray:
+    w = comm.world
+    send_p, count = engine.sparse_rare()
+    counts = comm.all_gather_small(count)
+    stride = max(counts)
+    recv_p = engine.sparse_rare_recv(stride)
+    if stride:
+        comm.all_gather(_as_tensor(recv_p, stride * 16 * w, engine.on_device),
+                        _as_tensor(send_p, stride * 16, engine.on_device))
+    out_p, out_counts = engine.sparse_scan(counts)
+    out_counts = [int(c) for c in out_counts]
+    in_counts = comm.all_to_all_small(out_counts)
+    n_in = sum(in_counts)
+    in_p = engine.sparse_msg_recv(n_in)
+    if sum(out_counts) or n_in:
+        comm.all_to_all(_as_tensor(in_p, n_in * 16, engine.on_device),
+                        _as_tensor(out_p, sum(out_counts) * 16, engine.on_device),
+                        [c * ITEM_WORDS for c in in_counts], [c * ITEM_WORDS for c in out_counts])
+    return engine.sparse_commit(n_in)
+
+
 def sharded_round(engine, group=None) -> dict:
     """Runs one round of a sharded engine; every rank must call it."""
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
-    send_p, recv_p, nbytes = engine.exchange_buffers()
-    on_dev = engine.on_device and world > 1 and _device_collectives(group)
-    if world > 1:
-        recv = _as_tensor(recv_p, nbytes * world, engine.on_device)
-        send = _as_tensor(send_p, nbytes, engine.on_device)
-        if on_dev:
-            # RCCL all-gather in place: the send slice lies inside the image
-            dist.all_gather_into_tensor(recv, send, group=group)
-        else:
-            # gloo (CPU): disjoint host buffers; device engines stage through host
-            host = torch.empty(nbytes // 8 * world, dtype=torch.int64)
-            dist.all_gather_into_tensor(host, send.cpu() if engine.on_device else send.clone(), group=group)
-            recv.copy_(host)
-            if engine.on_device:
-                torch.cuda.synchronize()
-    partial = engine.round_compute()
-    if world > 1:
-        t = torch.from_numpy(partial.view(np.int64).copy())
-        if on_dev:
-            t = t.cuda()
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
-        partial = t.cpu().numpy().view(np.uint64)
+    comm = _Comm(engine, group)
+    partial = _sparse_round(engine, comm) if _plan(engine, comm) == 1 else _dense_round(engine, comm)
+    if comm.world > 1:
+        partial = comm.all_reduce_sum(partial)
     return engine.round_commit(partial)
 
 
@@ -76,3 +165,81 @@ def sharded_run(engine, max_rounds: int, group=None) -> list:
         if st["converged"] or (engine.cfg.mode == 0 and st["messages"] == 0):
             break
     return out
+
+
+# -- single-process driver ---------------------------------------------------
+
+def _sync_all(engines):
+    for d in sorted({e.device for e in engines}):
+        torch.cuda.synchronize(d)
+
+
+def _lockstep_sum(parts):
+    tot = np.zeros_like(parts[0])
+    for p in parts:
+        tot = tot + p  # uint64 wraps like the RCCL int64 sum
+    return tot
+
+
+def _lockstep_dense(engines):
+    G = len(engines)
+    bufs = [e.exchange_buffers() for e in engines]
+    for e, (_, recv_p, nbytes) in zip(engines, bufs):
+        recv = _as_tensor(recv_p, nbytes * G, True, e.device)
+        for q, (send_q, _, _) in enumerate(bufs):
+            if engines[q] is not e:
+                recv[q * nbytes // 8:(q + 1) * nbytes // 8].copy_(_as_tensor(send_q, nbytes, True, engines[q].device))
+    _sync_all(engines)
+    return [e.round_compute() for e in engines]
+
+
+def _lockstep_sparse(engines):
+    G = len(engines)
+    rare = [e.sparse_rare() for e in engines]
+    counts = [c for _, c in rare]
+    stride = max(counts)
+    recvs = [e.sparse_rare_recv(stride) for e in engines]
+    if stride:
+        for e, rp in zip(engines, recvs):
+            recv = _as_tensor(rp, stride * 16 * G, True, e.device)
+            for q, (sp, _) in enumerate(rare):
+                recv[q * stride * ITEM_WORDS:(q + 1) * stride * ITEM_WORDS].copy_(
+                    _as_tensor(sp, stride * 16, True, engines[q].device))
+        _sync_all(engines)
+    scans = [e.sparse_scan(counts) for e in engines]
+    outs = [(p, [int(c) for c in cnt]) for p, cnt in scans]
+    n_in = [sum(outs[q][1][r] for q in range(G)) for r in range(G)]
+    ins = [e.sparse_msg_recv(n) for e, n in zip(engines, n_in)]
+    for r in range(G):
+        dst = _as_tensor(ins[r], n_in[r] * 16, True, engines[r].device)
+        at = 0
+        for q, (sp, cnt) in enumerate(outs):
+            off = sum(cnt[:r])
+            if cnt[r]:
+                src = _as_tensor(sp, sum(cnt) * 16, True, engines[q].device)
+                dst[at * ITEM_WORDS:(at + cnt[r]) * ITEM_WORDS].copy_(src[off * ITEM_WORDS:(off + cnt[r]) * ITEM_WORDS])
+                at += cnt[r]
+    _sync_all(engines)
+    return [e.sparse_commit(n) for e, n in zip(engines, n_in)]
+
+
+def lockstep_run(engines, max_rounds: int):
+    """One process driving G shard engines (one per GPU, or several on one) through the
+    same rounds as sharded_run, with device copies in place of the collectives.
+    Returns (per-round stats, per-round kind: 0 dense / 1 sparse)."""
+    stats, kinds = [], []
+    for _ in range(max_rounds):
+        ks = [e.sharded_plan() for e in engines]
+        if ks[0] < 0:
+            tot = _lockstep_sum([e.local_totals() for e in engines])
+            ks = [e.sharded_plan(tot) for e in engines]
+        assert len(set(ks)) == 1
+        kinds.append(ks[0])
+        parts = _lockstep_sparse(engines) if ks[0] == 1 else _lockstep_dense(engines)
+        tot = _lockstep_sum(parts)
+        st = [e.round_commit(tot) for e in engines]
+        assert all(s == st[0] for s in st)
+        stats.append(st[0])
+        if st[0]["converged"]:
+            break
+    return stats, kinds

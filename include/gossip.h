@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define GOSSIP_ABI_VERSION 1u
+#define GOSSIP_ABI_VERSION 2u
 
 /* Dissemination modes. */
 enum gossip_mode {
@@ -137,11 +137,39 @@ int gossip_step(gossip_engine_t* eng, uint32_t max_rounds, gossip_round_stats_t*
  *             → gossip_round_compute → all-reduce(SUM) of the partial vector
  *             → gossip_round_commit.
  * partial layout (uint64): [0]=full_nodes [1]=alive_nodes [2]=messages
- *                          [3]=state_hash [4..4+R)=infected per rumor.      */
+ *                          [3]=state_hash [4..4+R)=infected per rumor
+ *                          [4+R]=nonzero nodes (length gossip_partial_len). */
 uint64_t gossip_partial_len(const gossip_engine_t* eng);
 int gossip_exchange_buffers(gossip_engine_t* eng, void** send, void** recv, uint64_t* send_bytes);
 int gossip_round_compute(gossip_engine_t* eng, uint64_t* partial);
 int gossip_round_commit(gossip_engine_t* eng, const uint64_t* total, gossip_round_stats_t* stats);
+
+/* --- sparse sharded rounds (random modes, W == 1, G > 1) ------
+ * partial_len is 5 + R for these engines: [4+R] = nonzero nodes.  Each round
+ * starts with gossip_sharded_plan(total = the global totals of S_t, or NULL
+ * to reuse the ones the last gossip_round_commit received):
+ *   kind -1: no global totals yet -> gossip_local_totals, all-reduce(SUM),
+ *            plan again with the sum;
+ *   kind  0: dense round -> the exchange_buffers / round_compute sequence;
+ *   kind  1: sparse round:
+ *     gossip_sparse_rare(&send, &count)        own rare nodes, 16-B items {node, value}
+ *     all-gather of count, stride = max count
+ *     gossip_sparse_rare_recv(stride, &recv)   room for G * stride items; all-gather
+ *                                              stride items from every rank into it
+ *     gossip_sparse_scan(counts, &send, send_counts[G])  pushes for other shards,
+ *                                              grouped by owner (16-B items)
+ *     all-to-all of the counts, then of the items (owner q gets send_counts[q])
+ *     gossip_sparse_msg_recv(total_in, &recv)  room for the incoming items
+ *     gossip_sparse_commit(total_in, partial)  -> all-reduce(SUM) -> gossip_round_commit.
+ * The device buffers stay valid until the next call on the engine; the engine
+ * synchronizes its stream before returning a buffer to the driver. */
+int gossip_sharded_plan(gossip_engine_t* eng, const uint64_t* total, int32_t* kind);
+int gossip_local_totals(gossip_engine_t* eng, uint64_t* partial);
+int gossip_sparse_rare(gossip_engine_t* eng, void** send, uint64_t* count);
+int gossip_sparse_rare_recv(gossip_engine_t* eng, uint64_t stride, void** recv);
+int gossip_sparse_scan(gossip_engine_t* eng, const uint64_t* counts, void** send, uint64_t* send_counts);
+int gossip_sparse_msg_recv(gossip_engine_t* eng, uint64_t items, void** recv);
+int gossip_sparse_commit(gossip_engine_t* eng, uint64_t items, uint64_t* partial);
 
 /* Readout ("read" handler, main.go:123-130).  Bitset of one node (nwords >= W),
  * or the whole owned shard in logical order out[w * Nl_owned + i]. */

@@ -1,0 +1,67 @@
+"""GPU: G shard engines on one device, driven in lockstep through the sharded
+round protocol (include/gossip.h) with device copies standing in
+for the RCCL collectives, equal a single-engine run bit for bit — per-round
+stats, per-rumor counts and the final state.  Sparse rounds (rare-list
+all-gather + push all-to-all) and dense rounds (state all-gather) are forced
+one at a time and mixed as the engines plan them."""
+import numpy as np
+import pytest
+import torch
+
+from gossip_hip import Engine
+from gossip_hip.sharded import lockstep_run as run_lockstep
+
+pytestmark = pytest.mark.gpu
+
+
+CASES = [("pushpull", 2, 64, 1 << 20, 0x5EED0004, 4), ("push", 3, 1, 300001, 7, 3),
+         ("pull", 1, 5, 100000, 11, 2), ("pushpull", 6, 7, 50001, 3, 2)]
+IDS = ["pushpull-1M-G4", "push-ragged-G3", "pull-G2", "pushpull-k6-G2"]
+PLANS = {"auto": {}, "sparse": {"GOSSIP_SPARSE_FRAC": "1.0"}, "sparse_alld": {"GOSSIP_SPARSE_FRAC": "1.0",
+         "GOSSIP_ALLD_FRAC": "0"}, "dense": {"GOSSIP_SPARSE_FRAC": "-1"}}
+
+
+@pytest.mark.parametrize("plan", list(PLANS))
+@pytest.mark.parametrize("case", CASES, ids=IDS)
+def test_lockstep_shards_equal_one_engine(case, plan, monkeypatch):
+    mode, k, R, N, seed, G = case
+    for var in ("GOSSIP_SPARSE_FRAC", "GOSSIP_ALLD_FRAC"):
+        monkeypatch.delenv(var, raising=False)
+    ref = Engine(N, R, mode, k, seed, flags=1)
+    ref.inject_random()
+    want = ref.step(200)
+    full = ref.read_shard()
+    ref.close()
+    for var, val in PLANS[plan].items():
+        monkeypatch.setenv(var, val)
+    engines = [Engine(N, R, mode, k, seed, flags=1, shard_rank=r, shard_count=G) for r in range(G)]
+    for e in engines:
+        e.inject_random()
+    got, kinds = run_lockstep(engines, 200)
+    assert got == want.stats
+    for e in engines:
+        assert np.array_equal(e.read_shard(), full[:, e.lo:e.hi])
+    if plan in ("sparse", "sparse_alld"):
+        assert set(kinds) == {1}
+    elif plan == "dense":
+        assert set(kinds) == {0}
+    for e in engines:
+        e.close()
+
+
+def test_lockstep_inject_between_steps():
+    """Client broadcasts between runs invalidate the global totals; the next plan re-derives them."""
+    N, R, G = 200003, 11, 2
+    ref = Engine(N, R, "pushpull", 2, 5, flags=1)
+    engines = [Engine(N, R, "pushpull", 2, 5, flags=1, shard_rank=r, shard_count=G) for r in range(G)]
+    outs_ref, outs = [], []
+    for node, rumor in [(17, 0), (N - 1, 3), (N // 2, 10)]:
+        ref.inject(node, rumor)
+        for e in engines:
+            e.inject(node, rumor)
+        outs_ref.append(ref.step(5).stats)
+        outs.append(run_lockstep(engines, 5)[0])
+    assert outs == outs_ref
+    full = ref.read_shard()
+    for e in engines:
+        assert np.array_equal(e.read_shard(), full[:, e.lo:e.hi])

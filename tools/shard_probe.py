@@ -1,0 +1,66 @@
+"""Per-rank cost of sharded rounds at G shards x 2^24 nodes, all G engines on one GPU in
+one process (gossip_hip.sharded.lockstep_run): every engine call is timed (that is one
+rank's device work), and the bytes each exchange moves per rank are recorded.  The link
+time of a real G-GPU run is not measured here: DESIGN.md §5 prices it."""
+import os, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "gossip-protocol_amd"))
+import numpy as np
+import torch
+from gossip_hip import Engine
+from gossip_hip import sharded as sh
+
+G = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+LG = int(sys.argv[2]) if len(sys.argv) > 2 else 24
+CALLS = ("sparse_rare", "sparse_scan", "sparse_commit", "round_compute", "exchange_buffers", "local_totals")
+
+
+class Timed:
+    def __init__(self, e, log):
+        self._e, self._log = e, log
+
+    def __getattr__(self, name):
+        f = getattr(self._e, name)
+        if name not in CALLS:
+            return f
+        def g(*a):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            r = f(*a)
+            torch.cuda.synchronize()
+            self._log.append((name, (time.perf_counter() - t0) * 1e3))
+            return r
+        return g
+
+
+engines = [Engine(G << LG, 64, "pushpull", 2, 0x5EED0004, shard_rank=r, shard_count=G) for r in range(G)]
+for rep in range(2):
+    logs = [[] for _ in engines]
+    tes = [Timed(e, l) for e, l in zip(engines, logs)]
+    for e in engines:
+        e.reset(); e.inject_random()
+    rounds = []
+    for t in range(64):
+        for l in logs: l.clear()
+        ks = [e.sharded_plan() for e in engines]
+        if ks[0] < 0:
+            tot = sh._lockstep_sum([e.local_totals() for e in engines]); ks = [e.sharded_plan(tot) for e in engines]
+        if ks[0] == 1:
+            parts = sh._lockstep_sparse(tes)
+        else:
+            parts = sh._lockstep_dense(tes)
+        tot = sh._lockstep_sum(parts)
+        st = [e.round_commit(tot) for e in engines]
+        per_rank = np.mean([sum(ms for _, ms in l) for l in logs])
+        calls = {}
+        for l in logs:
+            for name, ms in l:
+                calls[name] = calls.get(name, 0.0) + ms / len(logs)
+        rounds.append((t, ks[0], per_rank, int(st[0]["full_nodes"]), calls))
+        if st[0]["converged"]:
+            break
+    if rep == 1:
+        for t, k, ms, full, calls in rounds:
+            br = " ".join(f"{n}={v:.3f}" for n, v in calls.items())
+            print(f"G={G} round {t:2d} {'sparse' if k else 'dense '} per-rank {ms:7.3f} ms  full={full}  [{br}]", flush=True)
+        print(f"G={G} rounds={len(rounds)} sum per-rank {sum(r[2] for r in rounds):.2f} ms", flush=True)
