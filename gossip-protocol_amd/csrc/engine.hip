@@ -681,6 +681,10 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
       return bail(GOSSIP_ENOMEM);
     }
     e->sx = true;
+    // a dense sharded round all-gathers every shard's state (7/8 of the image per GPU at G = 8);
+    // a sparse one moves 16 B per rare node plus the cross-shard pushes, so sparse rounds pay
+    // off up to a larger rare fraction than on one GPU (tools/shard_probe.py)
+    e->sparse_frac = 0.25;
     if (const char* f = getenv("GOSSIP_SPARSE_FRAC")) e->sparse_frac = atof(f);
     if (const char* f = getenv("GOSSIP_ALLD_FRAC")) e->alld_frac = atof(f);
   }

@@ -79,8 +79,9 @@ struct ScanArgs {
   const uint64_t* cbase;
   const uint32_t* gsumm;
   uint32_t gglog, gsumm_words;
-  SxItem* msg;
-  uint32_t* msg_cnt;
+  SxItem* msg;          // block b's messages at msg[b * seg_cap, ...)
+  uint32_t* blk_cnt;    // [grid] messages per block
+  uint64_t seg_cap;     // k * per_block: every owned node sends at most k pushes
   uint64_t N, Nl, lo, nown, per_block;
   uint32_t G, R, k, t, key0, key1, mark_d;
 };
@@ -95,7 +96,7 @@ __device__ __forceinline__ uint64_t rare_value(const ScanArgs& a, uint32_t p, ui
 }
 
 template <int MAJ, int MODE>
-__device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const ScanArgs& a) {
+__device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, uint32_t* lcnt, const ScanArgs& a) {
   const uint32_t* summ = (const uint32_t*)summ4;
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t n4 = (a.gsumm_words + 3) / 4;
@@ -119,11 +120,12 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Sca
     if (!m) return;
     const uint32_t first = (uint32_t)__builtin_ctzll(m);
     uint32_t base = 0;
-    if (lane == first) base = atomicAdd(&a.msg_cnt[a.G], (uint32_t)__popcll(m));
+    if (lane == first) base = atomicAdd(lcnt, (uint32_t)__popcll(m));  // the block's own segment: an LDS counter
     base = __shfl(base, first, 64);
     if (remote) {
       const uint32_t q = (uint32_t)(p / a.Nl);
-      a.msg[base + (uint32_t)__popcll(m & below)] = SxItem{((uint64_t)q << kMsgShift) | (p - (uint64_t)q * a.Nl), d};
+      a.msg[blockIdx.x * a.seg_cap + base + (uint32_t)__popcll(m & below)] =
+          SxItem{((uint64_t)q << kMsgShift) | (p - (uint64_t)q * a.Nl), d};
     }
   };
   // node ids are < 2^32 (gossip_create checks N)
@@ -257,45 +259,46 @@ template <int MODE>
 __global__ __launch_bounds__(kScanThreads) void sx_scan_kernel(ScanArgs a, uint32_t maj) {
   __shared__ uint4 summ4[kSummBits / 128];
   __shared__ uint64_t rws[kRwWords];
+  __shared__ uint32_t lcnt;
+  if (threadIdx.x == 0) lcnt = 0;  // (scan_body syncs before the first use)
   if (maj)
-    scan_body<1, MODE>(summ4, rws, a);
+    scan_body<1, MODE>(summ4, rws, &lcnt, a);
   else
-    scan_body<0, MODE>(summ4, rws, a);
+    scan_body<0, MODE>(summ4, rws, &lcnt, a);
+  __syncthreads();
+  if (threadIdx.x == 0) a.blk_cnt[blockIdx.x] = lcnt;
 }
 
-// Messages grouped by owner, in two passes over the same per-block chunks:
-// count (LDS histogram, one global atomic per block and owner), then scatter
-// (each block reserves its run per owner once, then places its messages).
+// Messages grouped by owner, in two passes over the scan blocks' segments
+// (one group block per segment): count (LDS histogram, one global atomic per
+// block and owner), then scatter (each block reserves its run per owner once,
+// then places its messages).
 constexpr uint32_t kMaxShards = 1024;
-constexpr uint32_t kGroupBlocks = 512;
 
-__device__ __forceinline__ void chunk_of(uint32_t total, uint32_t* b, uint32_t* e) {
-  const uint32_t per = (total + gridDim.x - 1) / gridDim.x;
-  *b = min(blockIdx.x * per, total);
-  *e = min(*b + per, total);
-}
-
-__global__ __launch_bounds__(256) void owner_count_kernel(const SxItem* __restrict__ msg, uint32_t* cnt, uint32_t G) {
+__global__ __launch_bounds__(256) void owner_count_kernel(const SxItem* __restrict__ msg, uint64_t seg_cap,
+                                                           const uint32_t* __restrict__ blk_cnt, uint32_t* cnt,
+                                                           uint32_t G) {
   __shared__ uint32_t h[kMaxShards];
   for (uint32_t q = threadIdx.x; q < G; q += 256) h[q] = 0;
   __syncthreads();
-  uint32_t b, e;
-  chunk_of(cnt[G], &b, &e);
-  for (uint32_t i = b + threadIdx.x; i < e; i += 256) atomicAdd(&h[(uint32_t)(msg[i].node >> kMsgShift)], 1u);
+  const SxItem* seg = msg + blockIdx.x * seg_cap;
+  const uint32_t n = blk_cnt[blockIdx.x];
+  for (uint32_t i = threadIdx.x; i < n; i += 256) atomicAdd(&h[(uint32_t)(seg[i].node >> kMsgShift)], 1u);
   __syncthreads();
   for (uint32_t q = threadIdx.x; q < G; q += 256)
     if (h[q]) atomicAdd(&cnt[q], h[q]);
 }
 
-__global__ __launch_bounds__(256) void owner_scatter_kernel(const SxItem* __restrict__ msg, SxItem* __restrict__ out,
-                                                             const uint32_t* __restrict__ cnt, uint32_t* fill,
-                                                             uint32_t G) {
+__global__ __launch_bounds__(256) void owner_scatter_kernel(const SxItem* __restrict__ msg, uint64_t seg_cap,
+                                                             const uint32_t* __restrict__ blk_cnt,
+                                                             SxItem* __restrict__ out, const uint32_t* __restrict__ cnt,
+                                                             uint32_t* fill, uint32_t G) {
   __shared__ uint32_t h[kMaxShards], base[kMaxShards];
   for (uint32_t q = threadIdx.x; q < G; q += 256) h[q] = 0;
   __syncthreads();
-  uint32_t b, e;
-  chunk_of(cnt[G], &b, &e);
-  for (uint32_t i = b + threadIdx.x; i < e; i += 256) atomicAdd(&h[(uint32_t)(msg[i].node >> kMsgShift)], 1u);
+  const SxItem* seg = msg + blockIdx.x * seg_cap;
+  const uint32_t n = blk_cnt[blockIdx.x];
+  for (uint32_t i = threadIdx.x; i < n; i += 256) atomicAdd(&h[(uint32_t)(seg[i].node >> kMsgShift)], 1u);
   __syncthreads();
   if (threadIdx.x == 0) {  // owner q's messages start after those of owners < q
     uint32_t off = 0;
@@ -307,8 +310,8 @@ __global__ __launch_bounds__(256) void owner_scatter_kernel(const SxItem* __rest
   __syncthreads();
   for (uint32_t q = threadIdx.x; q < G; q += 256) h[q] = 0;
   __syncthreads();
-  for (uint32_t i = b + threadIdx.x; i < e; i += 256) {
-    const SxItem m = msg[i];
+  for (uint32_t i = threadIdx.x; i < n; i += 256) {
+    const SxItem m = seg[i];
     const uint32_t q = (uint32_t)(m.node >> kMsgShift);
     out[base[q] + atomicAdd(&h[q], 1u)] = SxItem{m.node & ((1ull << kMsgShift) - 1ull), m.value};
   }
@@ -324,6 +327,19 @@ __global__ __launch_bounds__(256) void apply_kernel(FrontierBufs f, const SxItem
 }
 
 size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// scan geometry (also sizes the message buffer: one segment of k * per_block items per block)
+uint32_t scan_grid(uint64_t nown) {
+  const uint64_t chunks = (nown + kScanThreads - 1) / kScanThreads;
+  return (uint32_t)(chunks < kScanGrid ? (chunks ? chunks : 1) : kScanGrid);
+}
+uint64_t scan_per_block(uint64_t nown, uint32_t grid) {
+  return ((nown + grid - 1) / grid + kScanThreads - 1) / kScanThreads * kScanThreads;
+}
+uint64_t msg_cap(const SxGeom& g) {
+  const uint32_t grid = scan_grid(g.nown);
+  return (uint64_t)g.k * scan_per_block(g.nown, grid) * grid;
+}
 
 size_t scan_tmp_bytes(uint64_t n) {
   size_t bytes = 0;
@@ -343,9 +359,9 @@ size_t sx_bytes(const SxGeom& g) {
   const uint32_t glog = frontier_glog(g.N);
   const size_t sw = ((((g.N + (1ull << glog) - 1) >> glog) + 127) / 128) * 4;
   const size_t tmp = std::max(scan_tmp_bytes(nwl + 1), scan_tmp_bytes(nwg + 1));
-  const uint64_t cap = (uint64_t)g.k * g.nown;
+  const uint64_t cap = msg_cap(g);
   return 2 * al256((nwl + 1) * 4) + al256(g.Nl * sizeof(SxItem)) + al256(nwg * 8) + 2 * al256((nwg + 1) * 4) +
-         al256(sw * 4) + al256((g.G + 1) * 8) + 2 * al256(cap * sizeof(SxItem)) + al256((g.G + 2) * 4) +
+         al256(sw * 4) + al256((g.G + 1) * 8) + 2 * al256(cap * sizeof(SxItem)) + al256((g.G + 2 + kScanGrid) * 4) +
          al256(g.G * 4) + al256(tmp);
 }
 
@@ -369,10 +385,10 @@ void sx_carve(const SxGeom& g, void* base, SxBufs* b) {
   b->gsum.nzb = b->grb;
   b->gsum.summ = (uint32_t*)take((size_t)b->gsum.summ_words * 4);
   b->cbase = (uint64_t*)take((g.G + 1) * 8);
-  b->cap = (uint64_t)g.k * g.nown;
+  b->cap = msg_cap(g);
   b->msg = (SxItem*)take(b->cap * sizeof(SxItem));
   b->msg_out = (SxItem*)take(b->cap * sizeof(SxItem));
-  b->msg_cnt = (uint32_t*)take((g.G + 2) * 4);
+  b->msg_cnt = (uint32_t*)take((g.G + 2 + kScanGrid) * 4);  // then the scan blocks' message counts
   b->msg_fill = (uint32_t*)take(g.G * 4);
   b->tmp_bytes = std::max(scan_tmp_bytes(nwl + 1), scan_tmp_bytes(nwg + 1));
   b->tmp = take(b->tmp_bytes);
@@ -419,7 +435,7 @@ hipError_t sx_scan(const SxGeom& g, const SxBufs& b, const FrontierBufs& lf, con
   a.gglog = b.gsum.glog;
   a.gsumm_words = b.gsum.summ_words;
   a.msg = b.msg;
-  a.msg_cnt = b.msg_cnt;
+  a.blk_cnt = b.msg_cnt + g.G + 2;
   a.N = g.N;
   a.Nl = g.Nl;
   a.lo = g.lo;
@@ -431,17 +447,18 @@ hipError_t sx_scan(const SxGeom& g, const SxBufs& b, const FrontierBufs& lf, con
   a.key0 = key0;
   a.key1 = key1;
   a.mark_d = all_d ? 0u : 1u;
-  const uint64_t chunks = (g.nown + kScanThreads - 1) / kScanThreads;
-  const uint32_t grid = (uint32_t)(chunks < kScanGrid ? (chunks ? chunks : 1) : kScanGrid);
-  a.per_block = ((g.nown + grid - 1) / grid + kScanThreads - 1) / kScanThreads * kScanThreads;
+  const uint32_t grid = scan_grid(g.nown);
+  a.per_block = scan_per_block(g.nown, grid);
+  a.seg_cap = (uint64_t)g.k * a.per_block;  // grid * seg_cap <= k * (nown rounded up): sx_carve's cap
   switch (mode) {
     case 1: sx_scan_kernel<1><<<grid, kScanThreads, 0, st>>>(a, maj); break;
     case 2: sx_scan_kernel<2><<<grid, kScanThreads, 0, st>>>(a, maj); break;
     case 3: sx_scan_kernel<3><<<grid, kScanThreads, 0, st>>>(a, maj); break;
     default: return hipErrorInvalidValue;
   }
-  owner_count_kernel<<<kGroupBlocks, 256, 0, st>>>(b.msg, b.msg_cnt, g.G);
-  owner_scatter_kernel<<<kGroupBlocks, 256, 0, st>>>(b.msg, b.msg_out, b.msg_cnt, b.msg_fill, g.G);
+  const uint32_t* blk = b.msg_cnt + g.G + 2;
+  owner_count_kernel<<<grid, 256, 0, st>>>(b.msg, a.seg_cap, blk, b.msg_cnt, g.G);
+  owner_scatter_kernel<<<grid, 256, 0, st>>>(b.msg, a.seg_cap, blk, b.msg_out, b.msg_cnt, b.msg_fill, g.G);
   return hipGetLastError();
 }
 
