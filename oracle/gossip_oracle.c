@@ -40,6 +40,16 @@ struct oracle_sim {
   /* ANTIENTROPY: V[n*K + c], alive bytes, global max vector */
   uint32_t *V, *Vn, *target;
   uint8_t *alive, *alive_n;
+  /* sparse sharded rounds (include/gossip.h; the engine's csrc/sharded.hip):
+   * items are {node, value} pairs of uint64 */
+  uint64_t* gtot;           /* global totals of S_t [5 + R] */
+  int gtot_valid, planned, last_sparse;
+  uint32_t maj;
+  double sparse_frac;
+  uint64_t *rare_send, *rare_recv, stride; /* [Nl] items; [G * stride] items */
+  uint64_t *msg_send, *msg_recv, msg_cap;  /* [k * nown] items grouped by owner; received items */
+  uint64_t* D;                             /* pending push deltas of the owned nodes */
+  uint64_t* counts;                        /* rare list lengths of the current round [G] */
 };
 
 /* ---------------- Philox4x32-10 (Random123; rocRAND philox4x32_10.h:270-302) ---- */
@@ -150,6 +160,15 @@ int oracle_create(const gossip_config_t* cfg, int threads, oracle_sim_t** out) {
     uint32_t bits = s->R - 64 * w;
     s->fullm[w] = bits >= 64 ? ~0ull : ((1ull << bits) - 1);
   }
+  s->gtot = (uint64_t*)calloc(5 + s->R, 8);
+  s->counts = (uint64_t*)calloc(G, 8);
+  s->sparse_frac = 0.25;
+  const char* f = getenv("GOSSIP_SPARSE_FRAC");
+  if (f) s->sparse_frac = atof(f);
+  if (!s->gtot || !s->counts) {
+    oracle_destroy(s);
+    return GOSSIP_ENOMEM;
+  }
   *out = s;
   return GOSSIP_OK;
 }
@@ -159,6 +178,8 @@ void oracle_destroy(oracle_sim_t* s) {
   free(s->S); free(s->Snext); free(s->Sprev); free(s->skip); free(s->send); free(s->recv);
   free(s->fullm); free(s->orow); free(s->ocol); free(s->irow); free(s->icol);
   free(s->V); free(s->Vn); free(s->target); free(s->alive); free(s->alive_n);
+  free(s->gtot); free(s->counts); free(s->rare_send); free(s->rare_recv); free(s->msg_send); free(s->msg_recv);
+  free(s->D);
   free(s);
 }
 
@@ -229,6 +250,7 @@ int oracle_reset(oracle_sim_t* s) {
     memset(s->alive, 1, s->N);
   }
   s->t = 0;
+  s->gtot_valid = s->planned = s->last_sparse = 0;
   return GOSSIP_OK;
 }
 
@@ -242,6 +264,7 @@ int oracle_inject(oracle_sim_t* s, uint64_t node, uint32_t rumor) {
     if (*x > s->target[rumor]) s->target[rumor] = *x;
     return GOSSIP_OK;
   }
+  s->gtot_valid = 0;
   if (node < s->lo || node >= s->hi) return GOSSIP_OK;
   s->S[(size_t)(rumor >> 6) * s->Nl + (node - s->lo)] |= 1ull << (rumor & 63);
   return GOSSIP_OK;
@@ -268,7 +291,8 @@ int oracle_inject_random(oracle_sim_t* s) {
   return GOSSIP_OK;
 }
 
-uint64_t oracle_partial_len(const oracle_sim_t* s) { return 4 + (s ? s->R : 0); }
+/* [0] full [1] alive [2] messages [3] hash [4, 4+R) infected [4+R] nonzero nodes */
+uint64_t oracle_partial_len(const oracle_sim_t* s) { return 5 + (s ? s->R : 0); }
 
 /* Exchange payload: S_t for random modes, the frontier F_t = S_t & ~S_{t-1} for FLOOD. */
 int oracle_exchange_buffers(oracle_sim_t* s, void** send, void** recv, uint64_t* send_bytes) {
@@ -356,6 +380,7 @@ static int ae_round(oracle_sim_t* s, uint64_t* partial) {
   partial[1] = alive;
   partial[2] = msgs;
   partial[3] = hash;
+  partial[4 + s->R] = 0; /* nonzero count: random modes only */
   return GOSSIP_OK;
 }
 
@@ -438,19 +463,20 @@ int oracle_round_compute(oracle_sim_t* s, uint64_t* partial) {
   }
 
   /* stats partials over S_{t+1} */
-  uint64_t full = 0, hash = 0;
+  uint64_t full = 0, hash = 0, nonzero = 0;
   uint64_t* inf = partial + 4;
   memset(inf, 0, (size_t)s->R * 8);
   const int do_hash = (s->cfg.flags & GOSSIP_FLAG_HASH) != 0;
 #pragma omp parallel num_threads(nt) if (nt > 1)
   {
     uint64_t* li = (uint64_t*)calloc(s->R, 8);
-    uint64_t lf = 0, lh = 0;
+    uint64_t lf = 0, lh = 0, lz = 0;
 #pragma omp for schedule(static)
     for (uint64_t i = 0; i < nown; ++i) {
-      int isfull = 1;
+      int isfull = 1, nz = 0;
       for (uint32_t w = 0; w < W; ++w) {
         uint64_t x = Sn[(size_t)w * Nl + i];
+        nz |= x != 0;
         if ((x & s->fullm[w]) != s->fullm[w]) isfull = 0;
         if (x && do_hash) lh += oracle_mix64(x + ((uint64_t)w * N + lo + i) * GOLD64);
         while (x) {
@@ -460,11 +486,13 @@ int oracle_round_compute(oracle_sim_t* s, uint64_t* partial) {
         }
       }
       lf += isfull;
+      lz += nz;
     }
 #pragma omp critical
     {
       full += lf;
       hash += lh;
+      nonzero += lz;
       for (uint32_t r = 0; r < s->R; ++r) inf[r] += li[r];
     }
     free(li);
@@ -473,6 +501,7 @@ int oracle_round_compute(oracle_sim_t* s, uint64_t* partial) {
   partial[1] = nown;
   partial[2] = msgs;
   partial[3] = hash;
+  partial[4 + s->R] = nonzero;
   return GOSSIP_OK;
 }
 
@@ -484,9 +513,12 @@ int oracle_round_commit(oracle_sim_t* s, const uint64_t* total, gossip_round_sta
     uint8_t* ta = s->alive; s->alive = s->alive_n; s->alive_n = ta;
   } else if (s->mode == GOSSIP_MODE_FLOOD) { /* S_{t-1} <- S_t <- S_{t+1} */
     tmp = s->Sprev; s->Sprev = s->S; s->S = s->Snext; s->Snext = tmp;
-  } else {
+  } else if (!s->last_sparse) { /* sparse sharded rounds update S in place */
     tmp = s->S; s->S = s->Snext; s->Snext = tmp;
   }
+  s->last_sparse = 0;
+  memcpy(s->gtot, total, oracle_partial_len(s) * 8);
+  s->gtot_valid = 1;
   if (st) {
     st->round = s->t;
     st->full_nodes = total[0];
@@ -496,6 +528,193 @@ int oracle_round_commit(oracle_sim_t* s, const uint64_t* total, gossip_round_sta
     st->state_hash = (s->cfg.flags & GOSSIP_FLAG_HASH) ? total[3] : 0;
   }
   s->t++;
+  return GOSSIP_OK;
+}
+
+/* ---------------- sparse sharded rounds (include/gossip.h) --------
+ * Plain restatement of the engine's protocol for the driver tests: the same
+ * plan rule, items and phases; lookups by binary search in the sorted lists. */
+
+static int sparse_ok(const oracle_sim_t* s) {
+  return s->G > 1 && s->W == 1 && s->mode >= GOSSIP_MODE_PUSH && s->mode <= GOSSIP_MODE_PUSHPULL;
+}
+
+/* rare under maj: 0 -> nonzero, 1 -> not full (one word: W == 1) */
+static inline int is_rare(const oracle_sim_t* s, uint64_t x) { return s->maj ? x != s->fullm[0] : x != 0; }
+
+/* totals of the owned nodes' S (same layout as round_compute) */
+static void own_totals(const oracle_sim_t* s, uint64_t* partial) {
+  memset(partial, 0, oracle_partial_len(s) * 8);
+  const int do_hash = (s->cfg.flags & GOSSIP_FLAG_HASH) != 0;
+  for (uint64_t i = 0; i < s->nown; ++i) {
+    uint64_t x = s->S[i];
+    partial[0] += (x & s->fullm[0]) == s->fullm[0];
+    partial[4 + s->R] += x != 0;
+    if (x && do_hash) partial[3] += oracle_mix64(x + (s->lo + i) * GOLD64);
+    while (x) {
+      partial[4 + __builtin_ctzll(x)]++;
+      x &= x - 1;
+    }
+  }
+  partial[1] = s->nown;
+}
+
+int oracle_local_totals(oracle_sim_t* s, uint64_t* partial) {
+  if (!s || !partial || !sparse_ok(s)) return GOSSIP_EINVAL;
+  own_totals(s, partial);
+  return GOSSIP_OK;
+}
+
+int oracle_sharded_plan(oracle_sim_t* s, const uint64_t* total, int32_t* kind) {
+  if (!s || !kind) return GOSSIP_EINVAL;
+  s->planned = 0;
+  if (!sparse_ok(s)) {
+    *kind = 0;
+    return GOSSIP_OK;
+  }
+  if (total) {
+    memcpy(s->gtot, total, oracle_partial_len(s) * 8);
+    s->gtot_valid = 1;
+  }
+  if (!s->gtot_valid) {
+    *kind = -1;
+    return GOSSIP_OK;
+  }
+  const double nz = (double)s->gtot[4 + s->R], notfull = (double)s->N - (double)s->gtot[0];
+  s->maj = notfull < nz;
+  s->planned = (notfull < nz ? notfull : nz) <= s->sparse_frac * (double)s->N;
+  *kind = s->planned;
+  return GOSSIP_OK;
+}
+
+int oracle_sparse_rare(oracle_sim_t* s, void** send, uint64_t* count) {
+  if (!s || !send || !count || !s->planned) return GOSSIP_ESTATE;
+  if (!s->rare_send && !(s->rare_send = (uint64_t*)calloc(2 * s->Nl, 8))) return GOSSIP_ENOMEM;
+  uint64_t c = 0;
+  for (uint64_t i = 0; i < s->nown; ++i)
+    if (is_rare(s, s->S[i])) {
+      s->rare_send[2 * c] = s->lo + i;
+      s->rare_send[2 * c + 1] = s->S[i];
+      ++c;
+    }
+  *send = s->rare_send;
+  *count = c;
+  return GOSSIP_OK;
+}
+
+int oracle_sparse_rare_recv(oracle_sim_t* s, uint64_t stride, void** recv) {
+  if (!s || !recv || !s->planned || stride > s->Nl) return GOSSIP_EINVAL;
+  free(s->rare_recv);
+  s->rare_recv = (uint64_t*)calloc(2 * (stride * s->G + 1), 8);
+  if (!s->rare_recv) return GOSSIP_ENOMEM;
+  s->stride = stride;
+  *recv = s->rare_recv;
+  return GOSSIP_OK;
+}
+
+/* S_t of node p if it is rare (in its owner's list), else -1 */
+static int rare_lookup(const oracle_sim_t* s, uint64_t p, uint64_t* v) {
+  uint64_t q = p / s->Nl, lo = 0, hi = s->counts[q];
+  const uint64_t* list = s->rare_recv + 2 * q * s->stride;
+  while (lo < hi) {
+    uint64_t mid = (lo + hi) / 2;
+    if (list[2 * mid] < p) lo = mid + 1; else hi = mid;
+  }
+  if (lo < s->counts[q] && list[2 * lo] == p) {
+    *v = list[2 * lo + 1];
+    return 1;
+  }
+  return 0;
+}
+
+int oracle_sparse_scan(oracle_sim_t* s, const uint64_t* counts, void** send, uint64_t* send_counts) {
+  if (!s || !counts || !send || !send_counts || !s->planned || !s->rare_recv) return GOSSIP_EINVAL;
+  for (uint32_t q = 0; q < s->G; ++q) {
+    if (counts[q] > s->stride) return GOSSIP_EINVAL;
+    s->counts[q] = counts[q];
+  }
+  const uint64_t cap = (uint64_t)s->k * s->nown + 1;
+  if (!s->msg_send && !(s->msg_send = (uint64_t*)calloc(2 * cap, 8))) return GOSSIP_ENOMEM;
+  if (!s->D && !(s->D = (uint64_t*)calloc(s->Nl, 8))) return GOSSIP_ENOMEM;
+  /* pending pushes per owner, then grouped */
+  uint64_t* tmp = (uint64_t*)malloc(3 * cap * 8);
+  if (!tmp) return GOSSIP_ENOMEM;
+  uint64_t nt = 0;
+  const uint32_t key[2] = {(uint32_t)s->cfg.seed, (uint32_t)(s->cfg.seed >> 32)};
+  const int do_pull = s->mode != GOSSIP_MODE_PUSH, do_push = s->mode != GOSSIP_MODE_PULL;
+  const uint64_t majv = s->maj ? s->fullm[0] : 0;
+  memcpy(s->Snext, s->S, s->Nl * 8); /* pulls land in Snext; S stays S_t during the scan */
+  for (uint64_t i = 0; i < s->nown; ++i) {
+    const uint32_t n = (uint32_t)(s->lo + i);
+    const uint64_t x = s->S[i];
+    const int rn = is_rare(s, x);
+    uint32_t r[4] = {0, 0, 0, 0};
+    for (uint32_t j = 0; j < s->k; ++j) {
+      if ((j & 3) == 0) {
+        uint32_t ctr[4] = {n, s->t, 0u, j >> 2};
+        oracle_philox4x32_10(ctr, key, r);
+      }
+      const uint32_t p = peer_from_word(r[j & 3], s->N, n);
+      uint64_t v = majv;
+      int rp;
+      if (p >= s->lo && p < s->hi) {
+        v = s->S[p - s->lo];
+        rp = is_rare(s, v);
+        if (!rp) v = majv;
+      } else {
+        rp = rare_lookup(s, p, &v);
+      }
+      if (!rn && !rp) continue; /* both ends majority: nothing moves */
+      if (do_pull) s->Snext[i] |= v;
+      if (do_push && (x & ~v)) {
+        if (p >= s->lo && p < s->hi) {
+          s->D[p - s->lo] |= x & ~v;
+        } else {
+          const uint64_t q = p / s->Nl;
+          tmp[3 * nt] = q;
+          tmp[3 * nt + 1] = p - q * s->Nl;
+          tmp[3 * nt + 2] = x & ~v;
+          ++nt;
+        }
+      }
+    }
+  }
+  uint64_t c = 0;
+  for (uint32_t q = 0; q < s->G; ++q) {
+    send_counts[q] = 0;
+    for (uint64_t m = 0; m < nt; ++m)
+      if (tmp[3 * m] == q) {
+        s->msg_send[2 * c] = tmp[3 * m + 1];
+        s->msg_send[2 * c + 1] = tmp[3 * m + 2];
+        ++c;
+        ++send_counts[q];
+      }
+  }
+  free(tmp);
+  *send = s->msg_send;
+  return GOSSIP_OK;
+}
+
+int oracle_sparse_msg_recv(oracle_sim_t* s, uint64_t items, void** recv) {
+  if (!s || !recv || !s->planned) return GOSSIP_EINVAL;
+  free(s->msg_recv);
+  s->msg_recv = (uint64_t*)calloc(2 * (items + 1), 8);
+  if (!s->msg_recv) return GOSSIP_ENOMEM;
+  s->msg_cap = items;
+  *recv = s->msg_recv;
+  return GOSSIP_OK;
+}
+
+int oracle_sparse_commit(oracle_sim_t* s, uint64_t items, uint64_t* partial) {
+  if (!s || !partial || !s->planned || items > s->msg_cap || !s->D) return GOSSIP_EINVAL;
+  for (uint64_t m = 0; m < items; ++m) s->D[s->msg_recv[2 * m]] |= s->msg_recv[2 * m + 1];
+  for (uint64_t i = 0; i < s->nown; ++i) {
+    s->S[i] = s->Snext[i] | s->D[i];
+    s->D[i] = 0;
+  }
+  own_totals(s, partial);
+  s->planned = 0;
+  s->last_sparse = 1;
   return GOSSIP_OK;
 }
 

@@ -51,6 +51,14 @@ uint64_t oracle_partial_len(const oracle_sim_t* s);
 int oracle_exchange_buffers(oracle_sim_t* s, void** send, void** recv, uint64_t* send_bytes);
 int oracle_round_compute(oracle_sim_t* s, uint64_t* partial);
 int oracle_round_commit(oracle_sim_t* s, const uint64_t* total, gossip_round_stats_t* stats);
+/* sparse sharded rounds: the protocol of include/gossip.h (gossip_sharded_plan ...) */
+int oracle_sharded_plan(oracle_sim_t* s, const uint64_t* total, int32_t* kind);
+int oracle_local_totals(oracle_sim_t* s, uint64_t* partial);
+int oracle_sparse_rare(oracle_sim_t* s, void** send, uint64_t* count);
+int oracle_sparse_rare_recv(oracle_sim_t* s, uint64_t stride, void** recv);
+int oracle_sparse_scan(oracle_sim_t* s, const uint64_t* counts, void** send, uint64_t* send_counts);
+int oracle_sparse_msg_recv(oracle_sim_t* s, uint64_t items, void** recv);
+int oracle_sparse_commit(oracle_sim_t* s, uint64_t items, uint64_t* partial);
 
 int oracle_read_bitset(oracle_sim_t* s, uint64_t node, uint64_t* out, uint32_t nwords);
 int oracle_read_shard(oracle_sim_t* s, uint64_t* out, uint64_t n_words);

@@ -1,8 +1,9 @@
 """CPU, world_size 2 over gloo: the sharded round protocol of
-gossip_hip.sharded (all-gather of the exchange image + all-reduce of the stats
-partials) reproduces the unsharded run bit for bit.  The shard
-kernels here are the oracle's; on GPU the same orchestration drives the HIP
-engine over RCCL."""
+gossip_hip.sharded reproduces the unsharded run bit for bit, with dense rounds
+(all-gather of the exchange image) and sparse rounds (all-gather of the rare
+lists + all-to-all of the cross-shard pushes), forced or as planned
+(DESIGN.md §5).  The shard engines here are the oracle's; on GPU the same
+driver code runs the HIP engine over RCCL."""
 import os
 import socket
 import sys
@@ -33,7 +34,10 @@ def _grid(n):
     return [[int(v[1:]) for v in t[f"n{i}"]] for i in range(n)]
 
 
-def _worker(rank, world, port, case, q):
+PLANS = {"auto": None, "sparse": "1.0", "dense": "-1"}  # GOSSIP_SPARSE_FRAC
+
+
+def _worker(rank, world, port, case, q, frac=None):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [os.path.join(root, "gossip-protocol_amd"), os.path.join(root, "oracle")]
     import torch.distributed as dist
@@ -41,6 +45,8 @@ def _worker(rank, world, port, case, q):
     from gossip_hip.sharded import sharded_run
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    if frac is not None:
+        os.environ["GOSSIP_SPARSE_FRAC"] = frac
     dist.init_process_group("gloo", rank=rank, world_size=world)
     mode, k, R, N, seed, topo = case
     e = op.OracleEngine(N, R, mode, k, seed, flags=1, shard_rank=rank, shard_count=world)
@@ -54,8 +60,11 @@ def _worker(rank, world, port, case, q):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("plan", list(PLANS))
 @pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
-def test_two_ranks_equal_one(case):
+def test_two_ranks_equal_one(case, plan):
+    if case[0] == "flood" and plan != "auto":
+        pytest.skip("FLOOD rounds are always dense (no sparse protocol)")
     import oracle_py as op
     mode, k, R, N, seed, topo = case
     ref = op.OracleEngine(N, R, mode, k, seed, flags=1)
@@ -70,7 +79,7 @@ def test_two_ranks_equal_one(case):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, case, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, case, q, PLANS[plan])) for r in range(2)]
     for p in procs:
         p.start()
     got = [q.get(timeout=120) for _ in range(2)]
