@@ -1040,7 +1040,7 @@ int gossip_step(gossip_engine_t* e, uint32_t max_rounds, gossip_round_stats_t* s
   if (e->mode == GOSSIP_MODE_FLOOD && !e->has_topo) return e->fail(GOSSIP_ESTATE, "FLOOD needs a topology");
   if (int rc = set_dev(e)) return rc;
   if (e->binned) return step_planned(e, max_rounds, stats, infected, rounds_done);
-  std::vector<uint64_t> part(4 + e->R);
+  std::vector<uint64_t> part(part_len(e));
   uint32_t r = 0;
   while (r < max_rounds) {
     uint64_t *send = nullptr, *img = nullptr;
