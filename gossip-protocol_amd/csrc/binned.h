@@ -44,10 +44,12 @@ size_t bin_bytes(const BinGeom& g);
 void bin_carve(const BinGeom& g, void* base, BinBufs* b);
 
 // One dense round, in place on S.  The totals in partial are cleared and
-// recomputed (layout as stats_kernel's plus [4+R] = nonzero nodes); the last
-// apply block hands them to the host through rs.
+// recomputed (layout as stats_kernel's plus [4+R] = nonzero nodes); a
+// one-block kernel hands them to the host through rs.  filt (needs exact
+// nzb/fullb): bit 0 drops pulls from empty peers, bit 1 pushes into full
+// peers — exact, it only removes edges that move nothing.
 hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, uint64_t* partial, uint32_t R,
-                               uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t flags,
-                               const RoundSync& rs, hipStream_t st);
+                               uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t filt,
+                               uint32_t flags, const RoundSync& rs, hipStream_t st);
 
 }  // namespace gossip

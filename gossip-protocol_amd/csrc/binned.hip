@@ -40,8 +40,8 @@ constexpr int kUnrollServe = 16;
 constexpr int kUnrollSeq = 8;  // records in flight per lane in the sequential response walker
 // record id word: p_local [0,14) | n_local [14,27) | flags.  K1 rewrites every
 // id each round, so a flag never outlives its round.
-constexpr uint32_t kIdVZ = 1u << 27;  // sender value is 0: no value stored
-constexpr uint32_t kIdVF = 1u << 28;  // sender value is the full mask: no value stored
+constexpr uint32_t kIdVZ = 1u << 27;  // no push on this record (sender empty, or the peer already full)
+constexpr uint32_t kIdVF = 1u << 28;  // no pull (sender full, or the peer empty)
 constexpr uint32_t kIdNMask = (1u << 13) - 1u;
 
 __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {
@@ -51,18 +51,32 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {
   return (b & 7u) * (n >> 3) + (b >> 3);
 }
 
-// which edges of a sender carry information: a push needs S_t[n] != 0, a pull
-// request is pointless once the sender already holds every rumor
-__device__ __forceinline__ bool edge_needed(uint32_t mode, uint64_t v, uint64_t fm) {
-  const bool push = (mode == 1 || mode == 3) && v != 0;
-  const bool pull = (mode == 2 || mode == 3) && v != fm;
-  return push || pull;
+// Which directions an edge n -> p carries (bit 0 push, bit 1 pull; 0: no
+// record).  From the sender alone: a push needs S_t[n] != 0, a pull is
+// pointless once n holds every rumor.  filt bit 0 also drops pull-only edges
+// whose peer is empty, bit 1 push-only edges whose peer is full (the peer's
+// class from the occupancy bitmaps): exact, such an edge moves no bit.
+__device__ __forceinline__ uint32_t sender_dirs(uint32_t mode, uint64_t v, uint64_t fm) {
+  const uint32_t push = (mode == 1 || mode == 3) && v != 0;
+  const uint32_t pull = (mode == 2 || mode == 3) && v != fm;
+  return push | (pull << 1);
 }
+
+__device__ __forceinline__ uint32_t peer_filter(uint32_t d, uint32_t p, uint32_t filt, const uint64_t* nzb,
+                                                const uint64_t* fullb) {
+  // only one-way edges are probed: a two-way record stays anyway
+  if ((filt & 1u) && d == 2u && !((nzb[p >> 6] >> (p & 63u)) & 1ull)) d = 0u;
+  if ((filt & 2u) && d == 1u && ((fullb[p >> 6] >> (p & 63u)) & 1ull)) d = 0u;
+  return d;
+}
+
+// record flags: kIdVZ = no push on this record, kIdVF = no pull
+__device__ __forceinline__ uint32_t dir_flags(uint32_t d) { return ((d & 1u) ? 0u : kIdVZ) | ((d & 2u) ? 0u : kIdVF); }
 
 template <int KREG>  // KREG > 0: the k (<= KREG) peers of each sender stay in registers between passes
 __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const uint64_t* __restrict__ S, BinBufs b,
                                                                   uint32_t R, uint32_t t, uint32_t key0,
-                                                                  uint32_t key1, uint32_t mode) {
+                                                                  uint32_t key1, uint32_t mode, uint32_t filt) {
   __shared__ uint32_t cur[kMaxTilesD];
   __shared__ uint32_t st_ids[kRecPerRegion];  // p_local | n_local << 14, sorted by destination tile
   __shared__ uint64_t sval[kMaxSenders];      // S_t of each sender, once (not once per record)
@@ -101,26 +115,73 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
   }
   if (s + gridDim.x < g.nt_s) load_values(s + gridDim.x, vn);
   __syncthreads();
-  // pass A: per-destination-tile counts
+  // pass A: per-destination-tile counts of the records (edges that carry something)
   uint32_t pr[KREG > 0 ? kQ * KREG : 1];
+  uint32_t ed[KREG > 0 ? kQ : 1];  // 2 bits per edge j: directions (sender_dirs, then peer_filter)
+  if (KREG > 0) {
 #pragma unroll
-  for (uint32_t q = 0; q < kQ; ++q) {
-    const uint32_t i = tid + q * kEmitThreads;
-    if (i >= nsend) break;
-    if (!edge_needed(mode, v[q], fm)) continue;
-    const uint32_t n = (uint32_t)(base + i);
-    if (KREG > 0) {
+    for (uint32_t q = 0; q < kQ; ++q) {
+      const uint32_t i = tid + q * kEmitThreads;
+      ed[q] = 0;
+#pragma unroll
+      for (int j = 0; j < KREG; ++j) pr[q * KREG + j] = 0;
+      const uint32_t d = i < nsend ? sender_dirs(mode, v[q], fm) : 0u;
+      if (!d) continue;
+      const uint32_t n = (uint32_t)(base + i);
       const u32x4 x = philox4x32_10(u32x4{n, t, 0u, 0u}, key0, key1);
 #pragma unroll
       for (int j = 0; j < KREG; ++j) {
         pr[q * KREG + j] = peer_from_word(lane_of(x, j), nm1, n);
-        if ((uint32_t)j < g.k) atomicAdd(&cur[pr[q * KREG + j] >> kTileDLog], 1u);
+        if ((uint32_t)j < g.k) ed[q] |= d << (2 * j);
       }
-    } else {
+    }
+    if (filt) {  // every probe issued before any is used (32-bit words: half the registers)
+      const uint32_t* nz32 = (const uint32_t*)b.nzb;
+      const uint32_t* full32 = (const uint32_t*)b.fullb;
+      uint32_t wz[KREG > 0 ? kQ * KREG : 1];
+#pragma unroll
+      for (uint32_t q = 0; q < kQ; ++q)
+#pragma unroll
+        for (int j = 0; j < KREG; ++j) {
+          const uint32_t p = pr[q * KREG + j];
+          // only edges that carry nothing else are probed: a two-way record stays anyway
+          wz[q * KREG + j] = ((filt & 1u) && ((ed[q] >> (2 * j)) & 3u) == 2u) ? nz32[p >> 5] : ~0u;
+        }
+#pragma unroll
+      for (uint32_t q = 0; q < kQ; ++q)
+#pragma unroll
+        for (int j = 0; j < KREG; ++j)
+          if (!((wz[q * KREG + j] >> (pr[q * KREG + j] & 31u)) & 1u)) ed[q] &= ~(2u << (2 * j));
+#pragma unroll
+      for (uint32_t q = 0; q < kQ; ++q)
+#pragma unroll
+        for (int j = 0; j < KREG; ++j) {
+          const uint32_t p = pr[q * KREG + j];
+          wz[q * KREG + j] = ((filt & 2u) && ((ed[q] >> (2 * j)) & 3u) == 1u) ? full32[p >> 5] : 0u;
+        }
+#pragma unroll
+      for (uint32_t q = 0; q < kQ; ++q)
+#pragma unroll
+        for (int j = 0; j < KREG; ++j)
+          if ((wz[q * KREG + j] >> (pr[q * KREG + j] & 31u)) & 1u) ed[q] &= ~(1u << (2 * j));
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < kQ; ++q)
+#pragma unroll
+      for (int j = 0; j < KREG; ++j)
+        if ((ed[q] >> (2 * j)) & 3u) atomicAdd(&cur[pr[q * KREG + j] >> kTileDLog], 1u);
+  } else {
+    for (uint32_t q = 0; q < kQ; ++q) {
+      const uint32_t i = tid + q * kEmitThreads;
+      if (i >= nsend) break;
+      const uint32_t d = sender_dirs(mode, v[q], fm);
+      if (!d) continue;
+      const uint32_t n = (uint32_t)(base + i);
       u32x4 x{0, 0, 0, 0};
       for (uint32_t j = 0; j < g.k; ++j) {
         if ((j & 3u) == 0) x = philox4x32_10(u32x4{n, t, 0u, j >> 2}, key0, key1);
-        atomicAdd(&cur[peer_from_word(lane_of(x, j & 3u), nm1, n) >> kTileDLog], 1u);
+        const uint32_t p = peer_from_word(lane_of(x, j & 3u), nm1, n);
+        if (peer_filter(d, p, filt, b.nzb, b.fullb)) atomicAdd(&cur[p >> kTileDLog], 1u);
       }
     }
   }
@@ -160,28 +221,36 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
   if (tid == 0) off[g.nt_d] = (uint16_t)total;
   __syncthreads();
 
-  // pass B: the same draws again, each record to its slot
+  // pass B: each record to its slot (k <= KREG: the peers and directions from
+  // registers; else the same draws and probes again)
+  if (KREG > 0) {
 #pragma unroll
-  for (uint32_t q = 0; q < kQ; ++q) {
-    const uint32_t i = tid + q * kEmitThreads;
-    if (i >= nsend) break;
-    if (!edge_needed(mode, v[q], fm)) continue;
-    const uint32_t n = (uint32_t)(base + i);
-    if (KREG > 0) {
+    for (uint32_t q = 0; q < kQ; ++q) {
+      const uint32_t i = tid + q * kEmitThreads;
 #pragma unroll
       for (int j = 0; j < KREG; ++j) {
-        if ((uint32_t)j >= g.k) break;
+        const uint32_t d = (ed[q] >> (2 * j)) & 3u;
+        if (!d) continue;
         const uint32_t p = pr[q * KREG + j];
         const uint32_t pos = atomicAdd(&cur[p >> kTileDLog], 1u);
-        st_ids[pos] = (p & (kTileD - 1)) | (i << kTileDLog);
+        st_ids[pos] = (p & (kTileD - 1)) | (i << kTileDLog) | dir_flags(d);
       }
-    } else {
+    }
+  } else {
+    for (uint32_t q = 0; q < kQ; ++q) {
+      const uint32_t i = tid + q * kEmitThreads;
+      if (i >= nsend) break;
+      const uint32_t d0 = sender_dirs(mode, v[q], fm);
+      if (!d0) continue;
+      const uint32_t n = (uint32_t)(base + i);
       u32x4 x{0, 0, 0, 0};
       for (uint32_t j = 0; j < g.k; ++j) {
         if ((j & 3u) == 0) x = philox4x32_10(u32x4{n, t, 0u, j >> 2}, key0, key1);
         const uint32_t p = peer_from_word(lane_of(x, j & 3u), nm1, n);
+        const uint32_t d = peer_filter(d0, p, filt, b.nzb, b.fullb);
+        if (!d) continue;
         const uint32_t pos = atomicAdd(&cur[p >> kTileDLog], 1u);
-        st_ids[pos] = (p & (kTileD - 1)) | (i << kTileDLog);
+        st_ids[pos] = (p & (kTileD - 1)) | (i << kTileDLog) | dir_flags(d);
       }
     }
   }
@@ -191,13 +260,11 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
   uint64_t* gvals = b.vals + (size_t)s * g.rp;
   for (uint32_t e = tid; e < total; e += kEmitThreads) {
     const uint32_t id = st_ids[e];
-    const uint64_t x = sval[id >> kTileDLog];
-    // the flags let K2/K3 skip work; the value is stored all the same, so the
+    // every value slot is stored (also where the flags say no push), so the
     // region is written without holes (a partly written 64-B chunk costs HBM
-    // a read-modify-write: profiles/r01_experiments/microbench5.jsonl)
-    const uint32_t fl = x == 0 ? kIdVZ : (x == fm ? kIdVF : 0u);
-    gids[e] = id | fl;
-    gvals[e] = x;
+    // a read-modify-write: profiles/r01_experiments/microbench5_scattered_pieces.jsonl)
+    gids[e] = id;
+    gvals[e] = sval[(id >> kTileDLog) & kIdNMask];
   }
 #pragma unroll
   for (uint32_t q = 0; q < kQ; ++q) v[q] = vn[q];
@@ -525,13 +592,14 @@ void bin_carve(const BinGeom& g, void* base, BinBufs* b) {
 }
 
 hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, uint64_t* partial, uint32_t R,
-                               uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t flags,
-                               const RoundSync& rs, hipStream_t st) {
+                               uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t filt,
+                               uint32_t flags, const RoundSync& rs, hipStream_t st) {
+  if (!b.nzb || !b.fullb) filt = 0;  // the bitmaps exist only with the frontier buffers
   const uint32_t eg = g.nt_s < kEmitGrid ? g.nt_s : kEmitGrid;  // persistent: one block per CU
   if (g.k <= 2)
-    bin_emit_kernel<2><<<eg, kEmitThreads, 0, st>>>(g, S, b, R, t, key0, key1, mode);
+    bin_emit_kernel<2><<<eg, kEmitThreads, 0, st>>>(g, S, b, R, t, key0, key1, mode, filt);
   else
-    bin_emit_kernel<0><<<eg, kEmitThreads, 0, st>>>(g, S, b, R, t, key0, key1, mode);
+    bin_emit_kernel<0><<<eg, kEmitThreads, 0, st>>>(g, S, b, R, t, key0, key1, mode, filt);
   const dim3 tg((g.nt_d + 1 + 31) / 32, (g.nt_s + 31) / 32);
   transpose_u16_kernel<<<tg, dim3(32, 8), 0, st>>>(b.off, b.offT, g.nt_s, g.nt_d + 1, partial, rs.plen);
   if (mode == 2 || mode == 3) bin_serve_kernel<<<g.nt_d, kTileThreads, 0, st>>>(g, S, b, R);

@@ -79,6 +79,7 @@ struct gossip_engine {
   void* fr_mem = nullptr;
   bool fr_valid = false;          // partial_d holds the totals of S and the bitmaps are exact
   double sparse_frac = 1.0 / 16;  // rare fraction at or below which a round runs sparse
+  double filter_frac = 0.3;       // dense rounds filter edges by the peer's class above this empty / full fraction
   double alld_frac = 1.0 / 64;    // sparse rounds with k * rare >= alld_frac * N commit every group's D (bench sweep)
   // pipelined rounds (binned engines): the host picks each round's path from the
   // totals it has read, predicted forward over the rounds still in flight, and
@@ -334,6 +335,15 @@ bool choose_sparse(const gossip_engine* e, const Est& x, uint32_t* maj, bool* al
   return rare <= e->sparse_frac * (double)e->N;
 }
 
+// dense rounds: probe the peer's class in emit when many edges would move
+// nothing (pulls from empty peers early in a run, pushes into full peers late)
+uint32_t dense_filter(const gossip_engine* e, const Est& x) {
+  const double N = (double)e->N, empty = 1.0 - x.nz / N, full = x.full / N;
+  const bool pull = e->mode == GOSSIP_MODE_PULL || e->mode == GOSSIP_MODE_PUSHPULL;
+  const bool push = e->mode == GOSSIP_MODE_PUSH || e->mode == GOSSIP_MODE_PUSHPULL;
+  return (pull && empty > e->filter_frac ? 1u : 0u) | (push && full > e->filter_frac ? 2u : 0u);
+}
+
 RoundSync ring_sync(gossip_engine* e, uint32_t slot) {
   RoundSync rs;
   rs.ring = e->ring_d + (size_t)slot * (part_len(e) + 1);
@@ -342,12 +352,13 @@ RoundSync ring_sync(gossip_engine* e, uint32_t slot) {
   return rs;
 }
 
-int launch_round_path(gossip_engine* e, uint32_t t, bool sparse, uint32_t maj, bool all_d, const RoundSync& rs) {
+int launch_round_path(gossip_engine* e, uint32_t t, bool sparse, uint32_t maj, bool all_d, uint32_t filt,
+                      const RoundSync& rs) {
   if (sparse)
     HIP_OK(e, launch_frontier_round(e->fb, e->S, e->N, e->partial_d, e->R, e->k, t, e->key0, e->key1, e->mode, maj,
                                     all_d, e->cfg.flags, rs, e->stream));
   else
-    HIP_OK(e, launch_binned_round(e->bg, e->bb, e->S, e->partial_d, e->R, t, e->key0, e->key1, e->mode,
+    HIP_OK(e, launch_binned_round(e->bg, e->bb, e->S, e->partial_d, e->R, t, e->key0, e->key1, e->mode, filt,
                                   e->cfg.flags, rs, e->stream));
   return GOSSIP_OK;
 }
@@ -404,7 +415,7 @@ int step_planned(gossip_engine* e, uint32_t max_rounds, gossip_round_stats_t* st
       const uint32_t slot = launched % kRing;
       const RoundSync rs = ring_sync(e, slot);
       want[slot] = rs.seq;
-      if (int rc = launch_round_path(e, t0 + launched, sparse, maj, all_d, rs)) return rc;
+      if (int rc = launch_round_path(e, t0 + launched, sparse, maj, all_d, dense_filter(e, x), rs)) return rc;
       ++launched;
     }
     if (done == launched) break;
@@ -465,9 +476,10 @@ int compute_round(gossip_engine* e, const uint64_t* gathered) {
     if ((rc = read_totals(e, &tot))) return rc;
     uint32_t maj = 0;
     bool all_d = false;
-    const bool sparse = choose_sparse(e, est_of(e, tot.data()), &maj, &all_d);
+    const Est x = est_of(e, tot.data());
+    const bool sparse = choose_sparse(e, x, &maj, &all_d);
     if ((rc = timer_begin(e, 0))) return rc;
-    if ((rc = launch_round_path(e, e->t, sparse, maj, all_d, ring_sync(e, 0)))) return rc;
+    if ((rc = launch_round_path(e, e->t, sparse, maj, all_d, dense_filter(e, x), ring_sync(e, 0)))) return rc;
     return timer_end(e, 0);  // stats are fused into the round kernels
   } else {
     // timer 0 covers the whole S_t -> S_{t+1} transform (seed copy + round kernel)
@@ -659,6 +671,7 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
       e->frontier = true;
       if (const char* f = getenv("GOSSIP_SPARSE_FRAC")) e->sparse_frac = atof(f);
       if (const char* f = getenv("GOSSIP_ALLD_FRAC")) e->alld_frac = atof(f);
+      if (const char* f = getenv("GOSSIP_FILTER_FRAC")) e->filter_frac = atof(f);
     }
     if (const char* a = getenv("GOSSIP_AHEAD")) e->ahead = std::max(1, std::min((int)kRing - 1, atoi(a)));
     if (hipHostMalloc((void**)&e->ring_h, kRing * (part_len(e) + 1) * 8, hipHostMallocMapped) != hipSuccess ||

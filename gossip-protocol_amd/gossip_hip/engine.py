@@ -272,10 +272,10 @@ class Engine(AbiEngine):
         cfg = make_config(n_nodes, n_rumors, mode, fanout, seed, flags, device, shard_rank, shard_count,
                           churn_fail, churn_recover)
         super().__init__(load_library(), "gossip_", cfg)
-        if device < 0:  # the caller's current HIP device (torch is only plumbing, imported on demand)
-            import torch
-            device = torch.cuda.current_device()
-        self.device = device
+        # None = the caller's current HIP device.  torch is not touched here: it bundles its own
+        # HIP runtime, which cannot initialise after this library's in a process that did not
+        # import torch first (the drivers in gossip_hip.sharded resolve None themselves)
+        self.device = device if device >= 0 else None
 
     def set_stream(self, hip_stream: int):
         self._check(self._fn("set_stream")(self._h, C.c_void_p(hip_stream)))

@@ -170,7 +170,7 @@ def sharded_run(engine, max_rounds: int, group=None) -> list:
 # -- single-process driver ---------------------------------------------------
 
 def _sync_all(engines):
-    for d in sorted({e.device for e in engines}):
+    for d in {e.device for e in engines}:
         torch.cuda.synchronize(d)
 
 

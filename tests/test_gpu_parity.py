@@ -35,18 +35,20 @@ def test_device_philox_kat(golden):
 #   sparse — every round on the frontier kernels (GOSSIP_SPARSE_FRAC=1 lifts the sparsity test),
 #            pushes tracked by per-group dirty flags
 #   sparse_alld — the same, but every round's commit reads D of every group (no push flags)
+#   dense_filter — every round dense, emit dropping edges by the peer's class (occupancy bitmaps)
 #   direct — the random-access kernels
-PATHS = ["auto", "dense", "sparse", "sparse_alld", "direct"]
-_PATH_FLAGS = {"auto": 0, "dense": FLAG_DENSE, "sparse": 0, "sparse_alld": 0, "direct": FLAG_DIRECT}
+PATHS = ["auto", "dense", "dense_filter", "sparse", "sparse_alld", "direct"]
+_PATH_FLAGS = {"auto": 0, "dense": FLAG_DENSE, "dense_filter": 0, "sparse": 0, "sparse_alld": 0, "direct": FLAG_DIRECT}
 # GOSSIP_ALLD_FRAC: 0 = every sparse round commits every group's D, huge = none does
-_PATH_ENV = {"sparse": {"GOSSIP_SPARSE_FRAC": "1.0", "GOSSIP_ALLD_FRAC": "1e30"},
+_PATH_ENV = {"dense_filter": {"GOSSIP_SPARSE_FRAC": "-1", "GOSSIP_FILTER_FRAC": "0"},
+             "sparse": {"GOSSIP_SPARSE_FRAC": "1.0", "GOSSIP_ALLD_FRAC": "1e30"},
              "sparse_alld": {"GOSSIP_SPARSE_FRAC": "1.0", "GOSSIP_ALLD_FRAC": "0"}}
 
 
 @pytest.fixture
 def path(request, monkeypatch):
     name = request.param
-    for var in ("GOSSIP_SPARSE_FRAC", "GOSSIP_ALLD_FRAC"):
+    for var in ("GOSSIP_SPARSE_FRAC", "GOSSIP_ALLD_FRAC", "GOSSIP_FILTER_FRAC"):
         monkeypatch.delenv(var, raising=False)
     for var, val in _PATH_ENV.get(name, {}).items():
         monkeypatch.setenv(var, val)
