@@ -150,6 +150,13 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
           }
         }
       }
+      // a wave with no rare end anywhere in this batch has nothing to do (most waves in light rounds)
+      {
+        bool any = false;
+#pragma unroll
+        for (int u = 0; u < kScanUnroll; ++u) any = any || rn[u] || hit[u] != 0u || (k > 4 && act[u]);  // k > 4: no hits yet
+        if (!__ballot(any)) continue;
+      }
       // 2. summary hits: exact test in the rare bitmap (2 MiB at 2^24 nodes, L2-resident)
       // (all probes issued before any is consumed: one wait for the lot)
       if (glog) {

@@ -161,6 +161,13 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, uint32_t*
           }
         }
       }
+      // a wave with no rare end anywhere in this batch has nothing to do (most waves in light rounds)
+      {
+        bool any = false;
+#pragma unroll
+        for (int u = 0; u < kScanUnroll; ++u) any = any || rn[u] || hit[u] != 0u || (k > 4 && act[u]);  // k > 4: no hits yet
+        if (!__ballot(any)) continue;
+      }
       // 2. exact probes in the global rare bitmap (all issued, then consumed)
       uint64_t rw[kScanUnroll][4];
 #pragma unroll
