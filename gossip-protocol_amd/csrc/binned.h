@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "philox.h"
 #include "round.h"
 
 namespace gossip {
@@ -50,6 +51,6 @@ void bin_carve(const BinGeom& g, void* base, BinBufs* b);
 // peers — exact, it only removes edges that move nothing.
 hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, uint64_t* partial, uint32_t R,
                                uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t filt,
-                               uint32_t flags, const RoundSync& rs, hipStream_t st);
+                               const Faults& fa, uint32_t flags, const RoundSync& rs, hipStream_t st);
 
 }  // namespace gossip

@@ -73,10 +73,13 @@ __device__ __forceinline__ uint32_t peer_filter(uint32_t d, uint32_t p, uint32_t
 // record flags: kIdVZ = no push on this record, kIdVF = no pull
 __device__ __forceinline__ uint32_t dir_flags(uint32_t d) { return ((d & 1u) ? 0u : kIdVZ) | ((d & 2u) ? 0u : kIdVF); }
 
-template <int KREG>  // KREG > 0: the k (<= KREG) peers of each sender stay in registers between passes
+// KREG > 0: the k (<= KREG) peers of each sender stay in registers between passes.
+// FAULTS: edge loss / partitions active; off, none of that code exists.
+template <int KREG, bool FAULTS>
 __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const uint64_t* __restrict__ S, BinBufs b,
                                                                   uint32_t R, uint32_t t, uint32_t key0,
-                                                                  uint32_t key1, uint32_t mode, uint32_t filt) {
+                                                                  uint32_t key1, uint32_t mode, uint32_t filt,
+                                                                  Faults fa) {
   __shared__ uint32_t cur[kMaxTilesD];
   __shared__ uint32_t st_ids[kRecPerRegion];  // p_local | n_local << 14, sorted by destination tile
   __shared__ uint64_t sval[kMaxSenders];      // S_t of each sender, once (not once per record)
@@ -129,10 +132,13 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
       if (!d) continue;
       const uint32_t n = (uint32_t)(base + i);
       const u32x4 x = philox4x32_10(u32x4{n, t, 0u, 0u}, key0, key1);
+      const u32x4 lw = FAULTS && fa.loss ? loss_draws(n, t, 0u, key0, key1) : u32x4{0, 0, 0, 0};
+      const Reach rc = FAULTS ? reach_of(n, fa) : Reach{0u, 0xFFFFFFFFu};  // n's partition block
 #pragma unroll
       for (int j = 0; j < KREG; ++j) {
         pr[q * KREG + j] = peer_from_word(lane_of(x, j), nm1, n);
-        if ((uint32_t)j < g.k) ed[q] |= d << (2 * j);
+        const bool lost = FAULTS && edge_lost(fa, rc, pr[q * KREG + j], lane_of(lw, j));
+        if ((uint32_t)j < g.k && !lost) ed[q] |= d << (2 * j);
       }
     }
     if (filt) {  // every probe issued before any is used (32-bit words: half the registers)
@@ -177,10 +183,15 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
       const uint32_t d = sender_dirs(mode, v[q], fm);
       if (!d) continue;
       const uint32_t n = (uint32_t)(base + i);
-      u32x4 x{0, 0, 0, 0};
+      u32x4 x{0, 0, 0, 0}, lw{0, 0, 0, 0};
+      const Reach rc = FAULTS ? reach_of(n, fa) : Reach{0u, 0xFFFFFFFFu};  // n's partition block (§2.8)
       for (uint32_t j = 0; j < g.k; ++j) {
-        if ((j & 3u) == 0) x = philox4x32_10(u32x4{n, t, 0u, j >> 2}, key0, key1);
+        if ((j & 3u) == 0) {
+          x = philox4x32_10(u32x4{n, t, 0u, j >> 2}, key0, key1);
+          if (FAULTS && fa.loss) lw = loss_draws(n, t, j >> 2, key0, key1);
+        }
         const uint32_t p = peer_from_word(lane_of(x, j & 3u), nm1, n);
+        if (FAULTS && edge_lost(fa, rc, p, lane_of(lw, j & 3u))) continue;
         if (peer_filter(d, p, filt, b.nzb, b.fullb)) atomicAdd(&cur[p >> kTileDLog], 1u);
       }
     }
@@ -243,10 +254,15 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
       const uint32_t d0 = sender_dirs(mode, v[q], fm);
       if (!d0) continue;
       const uint32_t n = (uint32_t)(base + i);
-      u32x4 x{0, 0, 0, 0};
+      u32x4 x{0, 0, 0, 0}, lw{0, 0, 0, 0};
+      const Reach rc = FAULTS ? reach_of(n, fa) : Reach{0u, 0xFFFFFFFFu};  // n's partition block (§2.8)
       for (uint32_t j = 0; j < g.k; ++j) {
-        if ((j & 3u) == 0) x = philox4x32_10(u32x4{n, t, 0u, j >> 2}, key0, key1);
+        if ((j & 3u) == 0) {
+          x = philox4x32_10(u32x4{n, t, 0u, j >> 2}, key0, key1);
+          if (FAULTS && fa.loss) lw = loss_draws(n, t, j >> 2, key0, key1);
+        }
         const uint32_t p = peer_from_word(lane_of(x, j & 3u), nm1, n);
+        if (FAULTS && edge_lost(fa, rc, p, lane_of(lw, j & 3u))) continue;
         const uint32_t d = peer_filter(d0, p, filt, b.nzb, b.fullb);
         if (!d) continue;
         const uint32_t pos = atomicAdd(&cur[p >> kTileDLog], 1u);
@@ -593,13 +609,16 @@ void bin_carve(const BinGeom& g, void* base, BinBufs* b) {
 
 hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, uint64_t* partial, uint32_t R,
                                uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t filt,
-                               uint32_t flags, const RoundSync& rs, hipStream_t st) {
+                               const Faults& fa, uint32_t flags, const RoundSync& rs, hipStream_t st) {
   if (!b.nzb || !b.fullb) filt = 0;  // the bitmaps exist only with the frontier buffers
   const uint32_t eg = g.nt_s < kEmitGrid ? g.nt_s : kEmitGrid;  // persistent: one block per CU
-  if (g.k <= 2)
-    bin_emit_kernel<2><<<eg, kEmitThreads, 0, st>>>(g, S, b, R, t, key0, key1, mode, filt);
-  else
-    bin_emit_kernel<0><<<eg, kEmitThreads, 0, st>>>(g, S, b, R, t, key0, key1, mode, filt);
+#define GOSSIP_EMIT(KR, F) bin_emit_kernel<KR, F><<<eg, kEmitThreads, 0, st>>>(g, S, b, R, t, key0, key1, mode, filt, fa)
+  if (g.k <= 2) {
+    if (fa.any()) GOSSIP_EMIT(2, true); else GOSSIP_EMIT(2, false);
+  } else {
+    if (fa.any()) GOSSIP_EMIT(0, true); else GOSSIP_EMIT(0, false);
+  }
+#undef GOSSIP_EMIT
   const dim3 tg((g.nt_d + 1 + 31) / 32, (g.nt_s + 31) / 32);
   transpose_u16_kernel<<<tg, dim3(32, 8), 0, st>>>(b.off, b.offT, g.nt_s, g.nt_d + 1, partial, rs.plen);
   if (mode == 2 || mode == 3) bin_serve_kernel<<<g.nt_d, kTileThreads, 0, st>>>(g, S, b, R);

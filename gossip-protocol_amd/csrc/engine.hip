@@ -48,6 +48,7 @@ struct gossip_engine {
   uint32_t R = 0, W = 0, k = 0, mode = 0, G = 1, rank = 0;
   uint32_t t = 0;
   uint32_t key0 = 0, key1 = 0;
+  Faults fa{};  // lost edges
 
   // Random modes: two gathered images [G][W][Nl]; S_t is this rank's slice of
   // img[cur], S_{t+1} its slice of img[cur^1], so the all-gather runs in place.
@@ -183,6 +184,7 @@ RoundArgs make_args(gossip_engine* e, const uint64_t* gathered) {
   a.t = e->t;
   a.key0 = e->key0;
   a.key1 = e->key1;
+  a.fa = e->fa;
   a.flags = e->cfg.flags;
   a.mode = e->mode;
   a.Sprev = e->Sprev;
@@ -305,7 +307,9 @@ Est est_of(const gossip_engine* e, const uint64_t* tot) {
 // choice, never a result.
 Est predict(const gossip_engine* e, const Est& x) {
   Est y;
-  const double N = (double)e->N, k = (double)e->k;
+  // lost edges (§2.8) thin the fanout; a partition keeps ~1/P of the peers
+  const double keep = (1.0 - (double)e->fa.loss / 4294967296.0) * (e->fa.parts > 1 ? 1.0 / e->fa.parts : 1.0);
+  const double N = (double)e->N, k = (double)e->k * keep;
   const bool push = e->mode == GOSSIP_MODE_PUSH || e->mode == GOSSIP_MODE_PUSHPULL;
   const bool pull = e->mode == GOSSIP_MODE_PULL || e->mode == GOSSIP_MODE_PUSHPULL;
   double all_miss = 1.0, all_hit = 1.0;
@@ -356,10 +360,10 @@ int launch_round_path(gossip_engine* e, uint32_t t, bool sparse, uint32_t maj, b
                       const RoundSync& rs) {
   if (sparse)
     HIP_OK(e, launch_frontier_round(e->fb, e->S, e->N, e->partial_d, e->R, e->k, t, e->key0, e->key1, e->mode, maj,
-                                    all_d, e->cfg.flags, rs, e->stream));
+                                    all_d, e->fa, e->cfg.flags, rs, e->stream));
   else
     HIP_OK(e, launch_binned_round(e->bg, e->bb, e->S, e->partial_d, e->R, t, e->key0, e->key1, e->mode, filt,
-                                  e->cfg.flags, rs, e->stream));
+                                  e->fa, e->cfg.flags, rs, e->stream));
   return GOSSIP_OK;
 }
 
@@ -571,6 +575,11 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
       g_create_error = "reserved fields must be zero";
       return GOSSIP_EINVAL;
     }
+  if ((cfg->edge_loss || cfg->partitions > 1) &&
+      (cfg->mode == GOSSIP_MODE_FLOOD || cfg->mode == GOSSIP_MODE_ANTIENTROPY)) {
+    g_create_error = "edge_loss / partitions apply to the random modes (PUSH, PULL, PUSHPULL)";
+    return GOSSIP_ENOTSUP;
+  }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
     g_create_error = "no HIP device (libgossip_hip has no CPU fallback)";
@@ -604,6 +613,7 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
   e->nown = e->hi - e->lo;
   e->key0 = (uint32_t)cfg->seed;
   e->key1 = (uint32_t)(cfg->seed >> 32);
+  e->fa = Faults{cfg->edge_loss, cfg->partitions, cfg->n_nodes};
   e->timing = (cfg->flags & GOSSIP_FLAG_TIMING) != 0;
 
   auto bail = [&](int rc) {
@@ -1011,7 +1021,7 @@ int gossip_sparse_scan(gossip_engine_t* e, const uint64_t* counts, void** send, 
   if (int rc = timer_begin(e, 0)) return rc;
   HIP_OK(e, sx_index(e->sg, e->sb, e->rare_recv, e->sx_stride, e->stream));
   HIP_OK(e, sx_scan(e->sg, e->sb, e->lf, e->S, e->rare_recv, e->sx_stride, e->t, e->key0, e->key1, e->mode,
-                    e->sx_maj, e->sx_alld, e->stream));
+                    e->sx_maj, e->sx_alld, e->fa, e->stream));
   if (int rc = timer_end(e, 0)) return rc;
   HIP_OK(e, hipStreamSynchronize(e->stream));  // cb is read by the copy above
   HIP_OK(e, hipMemcpyAsync(e->sx_host, e->sb.msg_cnt, (e->G + 1) * 4, hipMemcpyDeviceToHost, e->stream));
@@ -1042,6 +1052,14 @@ int gossip_sparse_commit(gossip_engine_t* e, uint64_t items, uint64_t* partial) 
   if (int rc = timer_collect(e)) return rc;
   e->sx_planned = false;
   e->last_sparse = true;
+  return GOSSIP_OK;
+}
+
+int gossip_set_faults(gossip_engine_t* e, uint32_t edge_loss, uint32_t partitions) {
+  if (!e) return GOSSIP_EINVAL;
+  if ((edge_loss || partitions > 1) && (e->mode == GOSSIP_MODE_FLOOD || e->mode == GOSSIP_MODE_ANTIENTROPY))
+    return e->fail(GOSSIP_ENOTSUP, "edge_loss / partitions apply to the random modes");
+  e->fa = Faults{edge_loss, partitions, e->N};
   return GOSSIP_OK;
 }
 

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "philox.h"
 #include "round.h"
 
 namespace gossip {
@@ -63,6 +64,7 @@ hipError_t launch_frontier_inject(const FrontierBufs& f, uint64_t* S, uint64_t N
 // store per push costs about as much as the push atomic itself).  Exact either way.
 hipError_t launch_frontier_round(const FrontierBufs& f, uint64_t* S, uint64_t N, uint64_t* partial, uint32_t R,
                                  uint32_t k, uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t maj,
-                                 bool all_d, uint32_t flags, const RoundSync& rs, hipStream_t st);
+                                 bool all_d, const Faults& fa, uint32_t flags, const RoundSync& rs,
+                                 hipStream_t st);
 
 }  // namespace gossip

@@ -105,11 +105,11 @@ __global__ __launch_bounds__(256) void frontier_summary_kernel(FrontierBufs f, u
 // A summary hit is confirmed in the exact rare bitmap before S_t[p] is read
 // (the bitmap is L2-resident; S is not).  Pull deltas belong to the node's own
 // lane and are plain stores to P; push deltas are atomic ORs into D.
-template <int MAJ, int MODE>
+template <int MAJ, int MODE, bool FAULTS>  // FAULTS: edge loss / partitions active (§2.8)
 __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const FrontierBufs& f,
                                           const uint64_t* __restrict__ S, uint64_t N, uint32_t R, uint32_t k,
                                           uint32_t t, uint32_t key0, uint32_t key1, uint64_t per_block,
-                                          bool mark_d) {
+                                          bool mark_d, const Faults& fa) {
   const uint32_t* summ = (const uint32_t*)summ4;
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t n4 = (f.summ_words + 3) / 4;
@@ -128,9 +128,9 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
     __syncthreads();
     for (uint32_t base = c0; base < c1; base += kScanThreads * kScanUnroll) {
       uint64_t x[kScanUnroll], vp[kScanUnroll][4];
-      uint32_t pp[kScanUnroll][4], hit[kScanUnroll];
+      uint32_t pp[kScanUnroll][4], hit[kScanUnroll], live[kScanUnroll];
       bool act[kScanUnroll], rn[kScanUnroll];
-      // 1. draws and LDS summary tests (no global memory)
+      // 1. draws and LDS summary tests (no global memory); live = edges not lost (§2.8)
 #pragma unroll
       for (int u = 0; u < kScanUnroll; ++u) {
         const uint32_t n = base + u * kScanThreads + tid;
@@ -140,13 +140,22 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
         // pull into a full one are no-ops, so those nodes skip the draws entirely
         act[u] = valid && (rn[u] || !((!kPull && MAJ == 0) || (!kPush && MAJ == 1)));
         hit[u] = 0;
+        live[u] = 0;
         if (act[u] && k <= 4) {
           const u32x4 r4 = philox4x32_10(u32x4{n, t, 0u, 0u}, key0, key1);
+          u32x4 lw{0, 0, 0, 0};
+          Reach rc{0u, 0xFFFFFFFFu};
+          if (FAULTS) {
+            if (fa.loss) lw = loss_draws(n, t, 0u, key0, key1);
+            rc = reach_of(n, fa);  // n's partition block
+          }
 #pragma unroll
           for (uint32_t j = 0; j < 4; ++j) {
             if (j >= k) break;
             pp[u][j] = peer_from_word(lane_of(r4, j), nm1, n);
-            if (summ_bit(pp[u][j])) hit[u] |= 1u << j;
+            const bool lost = FAULTS && edge_lost(fa, rc, pp[u][j], lane_of(lw, j));
+            live[u] |= (lost ? 0u : 1u) << j;
+            if (!lost && summ_bit(pp[u][j])) hit[u] |= 1u << j;
           }
         }
       }
@@ -197,6 +206,7 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) {
           if (j >= k) break;
+          if (!((live[u] >> j) & 1u)) continue;             // lost edge
           if (!rn[u] && !((hit[u] >> j) & 1u)) continue;  // both ends majority: nothing moves
           if (kPull) acc |= vp[u][j];
           if (kPush) dpush[u][j] = x[u] & ~vp[u][j];
@@ -219,10 +229,15 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
           if (!act[u]) continue;
           const uint32_t n = base + u * kScanThreads + tid;
           uint64_t acc = 0;
-          u32x4 r4{0, 0, 0, 0};
+          u32x4 r4{0, 0, 0, 0}, lw{0, 0, 0, 0};
+          const Reach rc = FAULTS ? reach_of(n, fa) : Reach{0u, 0xFFFFFFFFu};  // n's partition block (§2.8)
           for (uint32_t j = 0; j < k; ++j) {
-            if ((j & 3u) == 0) r4 = philox4x32_10(u32x4{n, t, 0u, j >> 2}, key0, key1);
+            if ((j & 3u) == 0) {
+              r4 = philox4x32_10(u32x4{n, t, 0u, j >> 2}, key0, key1);
+              if (FAULTS && fa.loss) lw = loss_draws(n, t, j >> 2, key0, key1);
+            }
             const uint32_t p = peer_from_word(lane_of(r4, j & 3u), nm1, n);
+            if (FAULTS && edge_lost(fa, rc, p, lane_of(lw, j & 3u))) continue;
             bool rp = summ_bit(p);
             if (rp && glog) rp = (rare_word<MAJ>(f, p >> 6, N) >> (p & 63u)) & 1ull;
             if (!rn[u] && !rp) continue;  // both ends majority: nothing moves
@@ -253,19 +268,19 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
   }
 }
 
-template <int MODE>
+template <int MODE, bool FAULTS>
 __global__ __launch_bounds__(kScanThreads) void frontier_scan_kernel(FrontierBufs f, const uint64_t* __restrict__ S,
                                                                       uint64_t N, uint32_t R, uint32_t k, uint32_t t,
                                                                       uint32_t key0, uint32_t key1, uint64_t per_block,
                                                                       const uint64_t* partial, uint32_t maj,
-                                                                      uint32_t mark_d) {
+                                                                      uint32_t mark_d, Faults fa) {
   __shared__ uint4 summ4[kSummBits / 128];
   __shared__ uint64_t rws[kRwWords];
   if (rare_count(partial, N, R, maj) == 0) return;  // converged (or nothing injected): nothing moves
   if (maj)
-    scan_body<1, MODE>(summ4, rws, f, S, N, R, k, t, key0, key1, per_block, mark_d != 0);
+    scan_body<1, MODE, FAULTS>(summ4, rws, f, S, N, R, k, t, key0, key1, per_block, mark_d != 0, fa);
   else
-    scan_body<0, MODE>(summ4, rws, f, S, N, R, k, t, key0, key1, per_block, mark_d != 0);
+    scan_body<0, MODE, FAULTS>(summ4, rws, f, S, N, R, k, t, key0, key1, per_block, mark_d != 0, fa);
 }
 
 // Stats of one 64-node group whose words went from old to nw (old == 0 in a
@@ -504,18 +519,24 @@ hipError_t launch_frontier_inject(const FrontierBufs& f, uint64_t* S, uint64_t N
 
 hipError_t launch_frontier_round(const FrontierBufs& f, uint64_t* S, uint64_t N, uint64_t* partial, uint32_t R,
                                  uint32_t k, uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t maj,
-                                 bool all_d, uint32_t flags, const RoundSync& rs, hipStream_t st) {
+                                 bool all_d, const Faults& fa, uint32_t flags, const RoundSync& rs,
+                                 hipStream_t st) {
   frontier_summary_kernel<<<(f.summ_words + 255) / 256, 256, 0, st>>>(f, N, partial, R, maj);
   const uint64_t chunks = (N + kScanThreads - 1) / kScanThreads;
   const uint32_t grid = (uint32_t)(chunks < kScanGrid ? chunks : kScanGrid);
   // contiguous node range per block, a multiple of the block width (so lanes map to bitmap bits)
   const uint64_t per = ((N + grid - 1) / grid + kScanThreads - 1) / kScanThreads * kScanThreads;
+#define GOSSIP_SCAN(MODE, FAULTS)                                                                           \
+  frontier_scan_kernel<MODE, FAULTS><<<grid, kScanThreads, 0, st>>>(f, S, N, R, k, t, key0, key1, per, partial, \
+                                                                    maj, !all_d, fa)
+  const bool faults = fa.any();
   switch (mode) {
-    case 1: frontier_scan_kernel<1><<<grid, kScanThreads, 0, st>>>(f, S, N, R, k, t, key0, key1, per, partial, maj, !all_d); break;
-    case 2: frontier_scan_kernel<2><<<grid, kScanThreads, 0, st>>>(f, S, N, R, k, t, key0, key1, per, partial, maj, !all_d); break;
-    case 3: frontier_scan_kernel<3><<<grid, kScanThreads, 0, st>>>(f, S, N, R, k, t, key0, key1, per, partial, maj, !all_d); break;
+    case 1: if (faults) GOSSIP_SCAN(1, true); else GOSSIP_SCAN(1, false); break;
+    case 2: if (faults) GOSSIP_SCAN(2, true); else GOSSIP_SCAN(2, false); break;
+    case 3: if (faults) GOSSIP_SCAN(3, true); else GOSSIP_SCAN(3, false); break;
     default: return hipErrorInvalidValue;
   }
+#undef GOSSIP_SCAN
   const hipError_t ce = launch_frontier_commit(f, S, N, partial, R, all_d, flags, st);
   if (ce != hipSuccess) return ce;
   return launch_round_snapshot(partial, rs, st);

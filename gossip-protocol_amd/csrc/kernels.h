@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "philox.h"
+
 namespace gossip {
 
 struct RoundArgs {
@@ -19,6 +21,7 @@ struct RoundArgs {
   uint32_t key0, key1;
   uint32_t flags;
   uint32_t mode;
+  Faults fa;              // random modes: lost edges (philox.h)
   // FLOOD only
   const uint64_t* Sprev;  // own shard S_{t-1}
   uint64_t* skip;         // own shard sender-skip masks

@@ -52,10 +52,15 @@ __global__ __launch_bounds__(kBlock) void round_random_kernel(RoundArgs a, uint6
     if (ONE_WORD) {
       const uint64_t vs = a.G[s];
       uint64_t acc = 0;
-      u32x4 x{0, 0, 0, 0};
+      u32x4 x{0, 0, 0, 0}, lw{0, 0, 0, 0};
+      const Reach rc = reach_of(n, a.fa);  // n's partition block
       for (uint32_t j = 0; j < a.k; ++j) {
-        if ((j & 3u) == 0) x = philox4x32_10(u32x4{n, a.t, 0u, j >> 2}, a.key0, a.key1);
+        if ((j & 3u) == 0) {
+          x = philox4x32_10(u32x4{n, a.t, 0u, j >> 2}, a.key0, a.key1);
+          if (a.fa.loss) lw = loss_draws(n, a.t, j >> 2, a.key0, a.key1);
+        }
         const uint32_t p = peer_from_word(lane_of(x, j & 3u), nm1, n);
+        if (a.fa.any() && edge_lost(a.fa, rc, p, lane_of(lw, j & 3u))) continue;
         const bool pown = ((uint64_t)p - a.lo) < a.nown;
         const bool need = (PULL && own) || (PUSH && pown && vs != 0);
         if (!need) continue;
@@ -71,10 +76,15 @@ __global__ __launch_bounds__(kBlock) void round_random_kernel(RoundArgs a, uint6
         if (nb) atomicOr((unsigned long long*)&a.Snext[s - a.lo], (unsigned long long)nb);
       }
     } else {
-      u32x4 x{0, 0, 0, 0};
+      u32x4 x{0, 0, 0, 0}, lw{0, 0, 0, 0};
+      const Reach rc = reach_of(n, a.fa);  // n's partition block
       for (uint32_t j = 0; j < a.k; ++j) {
-        if ((j & 3u) == 0) x = philox4x32_10(u32x4{n, a.t, 0u, j >> 2}, a.key0, a.key1);
+        if ((j & 3u) == 0) {
+          x = philox4x32_10(u32x4{n, a.t, 0u, j >> 2}, a.key0, a.key1);
+          if (a.fa.loss) lw = loss_draws(n, a.t, j >> 2, a.key0, a.key1);
+        }
         const uint32_t p = peer_from_word(lane_of(x, j & 3u), nm1, n);
+        if (a.fa.any() && edge_lost(a.fa, rc, p, lane_of(lw, j & 3u))) continue;
         const bool pown = ((uint64_t)p - a.lo) < a.nown;
         for (uint32_t w = 0; w < a.W; ++w) {
           const uint64_t vs = a.G[gidx<false>(s, w, a.Nl, a.W)];

@@ -50,6 +50,43 @@ __host__ __device__ __forceinline__ uint32_t peer_from_word(uint32_t x, uint64_t
   return p + (p >= n ? 1u : 0u);
 }
 
+// Fault model (the reference's lossy SyncRPC,
+// main.go:77-87): the edge n -> p_j(n) of round t is lost in both directions
+// when a partition separates its ends (nodes split into `parts` contiguous
+// blocks) or when its loss draw, stream tag 4, falls below `loss` (P = loss/2^32).
+struct Faults {
+  uint32_t loss;   // 0: no loss
+  uint32_t parts;  // 0 or 1: no partition
+  uint64_t N;
+  __host__ __device__ bool any() const { return loss != 0 || parts > 1; }
+};
+
+__host__ __device__ __forceinline__ uint32_t part_of(uint32_t n, const Faults& f) {
+  return (uint32_t)(((uint64_t)n * f.parts) / f.N);
+}
+
+// Nodes reachable from n: [lo, hi) = n's partition block (q = part_of(n): the
+// nodes m with q*N <= m*P < (q+1)*N), or everything.  Computed once per node,
+// so the per-edge test is a range check.
+struct Reach {
+  uint32_t lo, hi;
+};
+__host__ __device__ __forceinline__ Reach reach_of(uint32_t n, const Faults& f) {
+  if (f.parts <= 1) return Reach{0u, 0xFFFFFFFFu};
+  const uint64_t q = part_of(n, f);
+  return Reach{(uint32_t)((q * f.N + f.parts - 1) / f.parts), (uint32_t)(((q + 1) * f.N + f.parts - 1) / f.parts)};
+}
+
+// the loss draws of edges 4q .. 4q+3 of node n in round t
+__host__ __device__ __forceinline__ u32x4 loss_draws(uint32_t n, uint32_t t, uint32_t q, uint32_t k0, uint32_t k1) {
+  return philox4x32_10(u32x4{n, t, 4u, q}, k0, k1);
+}
+
+// edge n -> p lost?  rc = reach_of(n), lossw = lane j & 3 of loss_draws(n, t, j >> 2)
+__host__ __device__ __forceinline__ bool edge_lost(const Faults& f, const Reach& rc, uint32_t p, uint32_t lossw) {
+  return p < rc.lo || p >= rc.hi || lossw < f.loss;
+}
+
 // Rumor origins: stream tag 2.
 __host__ __device__ __forceinline__ uint32_t origin_of(uint32_t r, uint64_t N, uint32_t k0, uint32_t k1) {
   const u32x4 x = philox4x32_10(u32x4{r, 0u, 2u, 0u}, k0, k1);

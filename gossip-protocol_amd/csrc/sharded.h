@@ -20,6 +20,7 @@
 #include <stdint.h>
 
 #include "frontier.h"
+#include "philox.h"
 
 namespace gossip {
 
@@ -63,7 +64,7 @@ hipError_t sx_index(const SxGeom& g, const SxBufs& b, const SxItem* recv, uint64
 // 4. scan of the owned nodes; messages grouped by owner into b.msg_out, counts in b.msg_cnt
 hipError_t sx_scan(const SxGeom& g, const SxBufs& b, const FrontierBufs& lf, const uint64_t* S, const SxItem* recv,
                    uint64_t stride, uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t maj, bool all_d,
-                   hipStream_t st);
+                   const Faults& fa, hipStream_t st);
 // 6. received pushes into D (and the push-dirty flags unless all_d)
 hipError_t sx_apply(const FrontierBufs& lf, const SxItem* in, uint64_t n, bool all_d, hipStream_t st);
 

@@ -84,6 +84,7 @@ struct ScanArgs {
   uint64_t seg_cap;     // k * per_block: every owned node sends at most k pushes
   uint64_t N, Nl, lo, nown, per_block;
   uint32_t G, R, k, t, key0, key1, mark_d;
+  Faults fa;
 };
 
 // S_t of a rare node p (global id) whose bitmap word is rw: own shard from S,
@@ -138,7 +139,7 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, uint32_t*
       rws[i] = own_rare(a.lf, (c0 >> 6) + i, a.nown, MAJ);
     __syncthreads();
     for (uint32_t base = c0; base < c1; base += kScanThreads * kScanUnroll) {
-      uint32_t pp[kScanUnroll][4], hit[kScanUnroll];
+      uint32_t pp[kScanUnroll][4], hit[kScanUnroll], live[kScanUnroll];
       bool act[kScanUnroll], rn[kScanUnroll];
       // 1. draws and LDS summary tests
 #pragma unroll
@@ -149,15 +150,20 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, uint32_t*
         rn[u] = valid && ((rws[(i - c0) >> 6] >> lane) & 1ull);
         act[u] = valid && (rn[u] || !((!kPull && MAJ == 0) || (!kPush && MAJ == 1)));
         hit[u] = 0;
+        live[u] = 0;  // edges not lost
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) pp[u][j] = 0;
         if (act[u] && k <= 4) {
           const u32x4 r4 = philox4x32_10(u32x4{n, a.t, 0u, 0u}, a.key0, a.key1);
+          const u32x4 lw = a.fa.loss ? loss_draws(n, a.t, 0u, a.key0, a.key1) : u32x4{0, 0, 0, 0};
+          const Reach rc = reach_of(n, a.fa);  // n's partition block
 #pragma unroll
           for (uint32_t j = 0; j < 4; ++j) {
             if (j >= k) break;
             pp[u][j] = peer_from_word(lane_of(r4, j), nm1, n);
-            if (summ_bit(pp[u][j])) hit[u] |= 1u << j;
+            const bool lost = a.fa.any() && edge_lost(a.fa, rc, pp[u][j], lane_of(lw, j));
+            live[u] |= (lost ? 0u : 1u) << j;
+            if (!lost && summ_bit(pp[u][j])) hit[u] |= 1u << j;
           }
         }
       }
@@ -213,6 +219,7 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, uint32_t*
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) {
           if (j >= k) break;
+          if (!((live[u] >> j) & 1u)) continue;             // lost edge
           if (!rn[u] && !((hit[u] >> j) & 1u)) continue;  // both ends majority: nothing moves
           if (kPull) acc |= vp[u][j];
           if (kPush) dpush[u][j] = x[u] & ~vp[u][j];
@@ -230,17 +237,22 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, uint32_t*
           if (!act[u]) continue;
           const uint32_t i = base + u * kScanThreads + tid, n = lo + i;
           uint64_t acc = 0;
-          u32x4 r4{0, 0, 0, 0};
+          u32x4 r4{0, 0, 0, 0}, lw{0, 0, 0, 0};
+          const Reach rc = reach_of(n, a.fa);  // n's partition block
           for (uint32_t j = 0; j < k; ++j) {
-            if ((j & 3u) == 0) r4 = philox4x32_10(u32x4{n, a.t, 0u, j >> 2}, a.key0, a.key1);
+            if ((j & 3u) == 0) {
+              r4 = philox4x32_10(u32x4{n, a.t, 0u, j >> 2}, a.key0, a.key1);
+              if (a.fa.loss) lw = loss_draws(n, a.t, j >> 2, a.key0, a.key1);
+            }
             const uint32_t p = peer_from_word(lane_of(r4, j & 3u), nm1, n);
+            const bool lost = a.fa.any() && edge_lost(a.fa, rc, p, lane_of(lw, j & 3u));
             uint64_t w = 0;
             bool rp = summ_bit(p);
             if (rp) {
               w = a.grb[p >> 6];
               rp = (w >> (p & 63u)) & 1ull;
             }
-            const bool moves = rn[u] || rp;  // else both ends majority: nothing moves
+            const bool moves = !lost && (rn[u] || rp);  // else lost, or both ends majority: nothing moves
             uint64_t v = maj;
             if (rp) v = (p - lo < nown) ? a.S[p - lo] : rare_value(a, p, w, a.gpre[p >> 6]);
             if (kPull && moves) acc |= v;
@@ -426,7 +438,7 @@ hipError_t sx_index(const SxGeom& g, const SxBufs& b, const SxItem* recv, uint64
 
 hipError_t sx_scan(const SxGeom& g, const SxBufs& b, const FrontierBufs& lf, const uint64_t* S, const SxItem* recv,
                    uint64_t stride, uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t maj, bool all_d,
-                   hipStream_t st) {
+                   const Faults& fa, hipStream_t st) {
   hipError_t e = hipMemsetAsync(b.msg_cnt, 0, (g.G + 2) * 4, st);
   if (e == hipSuccess) e = hipMemsetAsync(b.msg_fill, 0, g.G * 4, st);
   if (e != hipSuccess) return e;
@@ -454,6 +466,7 @@ hipError_t sx_scan(const SxGeom& g, const SxBufs& b, const FrontierBufs& lf, con
   a.key0 = key0;
   a.key1 = key1;
   a.mark_d = all_d ? 0u : 1u;
+  a.fa = fa;
   const uint32_t grid = scan_grid(g.nown);
   a.per_block = scan_per_block(g.nown, grid);
   a.seg_cap = (uint64_t)g.k * a.per_block;  // grid * seg_cap <= k * (nown rounded up): sx_carve's cap

@@ -6,11 +6,12 @@ torch.distributed.  See DESIGN.md.
 """
 from ._abi import (FLAG_DENSE, FLAG_DIRECT, FLAG_HASH, FLAG_TIMING, MODE_FLOOD, MODE_PULL, MODE_PUSH, MODE_PUSHPULL, MODES,
                    Config, RoundStats)
-from .engine import AbiEngine, Engine, GossipError, LIB_PATH, StepResult, load_library, make_config, peer
+from .engine import (AbiEngine, Engine, GossipError, LIB_PATH, StepResult, load_library, loss_threshold, make_config,
+                     peer)
 from .maelstrom import Cluster, grid_topology, line_topology, total_topology, tree_topology
 
 __all__ = [
     "AbiEngine", "Engine", "GossipError", "StepResult", "Config", "RoundStats", "MODES", "MODE_FLOOD",
     "MODE_PUSH", "MODE_PULL", "MODE_PUSHPULL", "FLAG_DENSE", "FLAG_DIRECT", "FLAG_HASH", "FLAG_TIMING", "LIB_PATH", "load_library",
-    "make_config", "peer", "Cluster", "grid_topology", "line_topology", "total_topology", "tree_topology",
+    "make_config", "loss_threshold", "peer", "Cluster", "grid_topology", "line_topology", "total_topology", "tree_topology",
 ]

@@ -31,7 +31,9 @@ class Config(C.Structure):
         ("shard_count", C.c_uint32),
         ("churn_fail", C.c_uint32),
         ("churn_recover", C.c_uint32),
-        ("reserved", C.c_uint32 * 3),
+        ("edge_loss", C.c_uint32),
+        ("partitions", C.c_uint32),
+        ("reserved", C.c_uint32 * 1),
     ]
 
 
@@ -63,6 +65,7 @@ SIGNATURES = [
     ("reset", C.c_int, [P]),
     ("inject", C.c_int, [P, C.c_uint64, C.c_uint32]),
     ("inject_random", C.c_int, [P]),
+    ("set_faults", C.c_int, [P, C.c_uint32, C.c_uint32]),
     ("step", C.c_int, [P, C.c_uint32, C.POINTER(RoundStats), U64P, U32P]),
     ("partial_len", C.c_uint64, [P]),
     ("exchange_buffers", C.c_int, [P, C.POINTER(P), C.POINTER(P), U64P]),

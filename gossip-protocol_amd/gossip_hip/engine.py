@@ -62,7 +62,7 @@ def churn_threshold(p: float) -> int:
 
 def make_config(n_nodes: int, n_rumors: int = 1, mode="push", fanout: int = 1, seed: int = 0,
                 flags: int = 0, device: int = -1, shard_rank: int = 0, shard_count: int = 1,
-                churn_fail: int = 0, churn_recover: int = 0) -> Config:
+                churn_fail: int = 0, churn_recover: int = 0, edge_loss: int = 0, partitions: int = 0) -> Config:
     cfg = Config()
     cfg.n_nodes = n_nodes
     cfg.n_rumors = n_rumors
@@ -75,7 +75,14 @@ def make_config(n_nodes: int, n_rumors: int = 1, mode="push", fanout: int = 1, s
     cfg.shard_count = shard_count
     cfg.churn_fail = churn_fail
     cfg.churn_recover = churn_recover
+    cfg.edge_loss = edge_loss
+    cfg.partitions = partitions
     return cfg
+
+
+def loss_threshold(p: float) -> int:
+    """Probability -> the u32 edge_loss threshold (an edge is lost iff its Philox draw < x)."""
+    return min(int(round(p * 2**32)), 2**32 - 1)
 
 
 class AbiEngine:
@@ -141,6 +148,10 @@ class AbiEngine:
         self._check(self._fn("set_topology_csr")(
             self._h, row_ptr.ctypes.data_as(_abi.U32P), colp.ctypes.data_as(_abi.U32P),
             C.c_uint64(row_ptr.size - 1), C.c_uint64(col.size)))
+
+    def set_faults(self, edge_loss: int = 0, partitions: int = 0):
+        """Fault model for the following rounds."""
+        self._check(self._fn("set_faults")(self._h, edge_loss, partitions))
 
     def reset(self):
         self._check(self._fn("reset")(self._h))
@@ -268,9 +279,9 @@ class Engine(AbiEngine):
 
     def __init__(self, n_nodes: int, n_rumors: int = 1, mode="push", fanout: int = 1, seed: int = 0,
                  flags: int = 0, device: int = -1, shard_rank: int = 0, shard_count: int = 1,
-                 churn_fail: int = 0, churn_recover: int = 0):
+                 churn_fail: int = 0, churn_recover: int = 0, edge_loss: int = 0, partitions: int = 0):
         cfg = make_config(n_nodes, n_rumors, mode, fanout, seed, flags, device, shard_rank, shard_count,
-                          churn_fail, churn_recover)
+                          churn_fail, churn_recover, edge_loss, partitions)
         super().__init__(load_library(), "gossip_", cfg)
         # None = the caller's current HIP device.  torch is not touched here: it bundles its own
         # HIP runtime, which cannot initialise after this library's in a process that did not

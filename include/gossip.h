@@ -80,7 +80,11 @@ typedef struct gossip_config {
   uint32_t shard_count; /* G >= 1, Nl = ceil(N/G)                                     */
   uint32_t churn_fail;    /* ANTIENTROPY: P(alive -> dead) per round, as x / 2^32      */
   uint32_t churn_recover; /* ANTIENTROPY: P(dead -> alive) per round, as x / 2^32      */
-  uint32_t reserved[3]; /* must be zero                                               */
+  uint32_t edge_loss;   /* random modes: P(an edge's exchange is lost) per round, x / 2^32
+                           (the reference's lossy SyncRPC, main.go:77-87) */
+  uint32_t partitions;  /* random modes: 0/1 = none, P > 1 = nodes split into P contiguous
+                           blocks that cannot reach each other                          */
+  uint32_t reserved[1]; /* must be zero                                               */
 } gossip_config_t;
 
 /* Stats of one round t: they describe S_{t+1}, the state the round produced. */
@@ -125,6 +129,10 @@ int gossip_inject(gossip_engine_t* eng, uint64_t node, uint32_t rumor);
 /* Injects every rumor r < R at origin(r) = Philox tag-2 draw.
  * ANTIENTROPY: initial versions V[n][c] = Philox tag-3 draw & 0xFFFF. */
 int gossip_inject_random(gossip_engine_t* eng);
+
+/* Fault model for the rounds that follow (random modes): same meaning as the
+ * config fields; e.g. heal a partition between steps with partitions = 0. */
+int gossip_set_faults(gossip_engine_t* eng, uint32_t edge_loss, uint32_t partitions);
 
 /* Runs rounds until converged or max_rounds rounds have run (single shard only,
  * G == 1).  stats: max_rounds entries or NULL; infected: max_rounds * R counters

@@ -85,6 +85,22 @@ uint32_t oracle_peer(uint64_t seed, uint64_t N, uint32_t n, uint32_t t, uint32_t
 }
 
 /* Rumor origin, Philox stream tag 2. */
+/* Fault model (the reference's lossy SyncRPC, main.go:77-87):
+ * the edge n -> p_j(n) of round t is lost, both directions, when a partition
+ * (nodes split into P contiguous blocks, block(n) = n*P/N) separates n and p,
+ * or when Philox({n, t, 4, j>>2}, key)[j&3] < edge_loss. */
+static int edge_lost(const gossip_config_t* cfg, uint64_t N, uint32_t n, uint32_t p, uint32_t t, uint32_t j,
+                     const uint32_t key[2]) {
+  if (cfg->partitions > 1 &&
+      (uint64_t)n * cfg->partitions / N != (uint64_t)p * cfg->partitions / N) return 1;
+  if (cfg->edge_loss) {
+    uint32_t ctr[4] = {n, t, 4u, j >> 2}, x[4];
+    oracle_philox4x32_10(ctr, key, x);
+    if (x[j & 3] < cfg->edge_loss) return 1;
+  }
+  return 0;
+}
+
 uint32_t oracle_origin(uint64_t seed, uint64_t N, uint32_t r) {
   uint32_t ctr[4] = {r, 0u, 2u, 0u};
   uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
@@ -113,6 +129,8 @@ int oracle_create(const gossip_config_t* cfg, int threads, oracle_sim_t** out) {
   uint32_t G = cfg->shard_count ? cfg->shard_count : 1;
   if (cfg->shard_rank >= G) return GOSSIP_EINVAL;
   if (cfg->mode == GOSSIP_MODE_ANTIENTROPY && (G != 1 || cfg->n_rumors > 64)) return GOSSIP_ENOTSUP;
+  if ((cfg->edge_loss || cfg->partitions > 1) &&
+      (cfg->mode == GOSSIP_MODE_FLOOD || cfg->mode == GOSSIP_MODE_ANTIENTROPY)) return GOSSIP_ENOTSUP;
   oracle_sim_t* s = (oracle_sim_t*)calloc(1, sizeof(*s));
   if (!s) return GOSSIP_ENOMEM;
   s->cfg = *cfg;
@@ -434,6 +452,7 @@ int oracle_round_compute(oracle_sim_t* s, uint64_t* partial) {
             oracle_philox4x32_10(ctr, key, x);
           }
           uint32_t p = peer_from_word(x[j & 3], N, n);
+          if (edge_lost(&s->cfg, N, n, p, t, j, key)) continue;
           for (uint32_t w = 0; w < W; ++w) Sn[(size_t)w * Nl + i] |= gword(s, g, p, w);
         }
       }
@@ -450,6 +469,7 @@ int oracle_round_compute(oracle_sim_t* s, uint64_t* partial) {
           }
           uint32_t p = peer_from_word(x[j & 3], N, n);
           if (p < lo || p >= lo + nown) continue;
+          if (edge_lost(&s->cfg, N, n, p, t, j, key)) continue;
           for (uint32_t w = 0; w < W; ++w) {
             uint64_t v = gword(s, g, n, w);
             if (!v) continue;
@@ -655,6 +675,7 @@ int oracle_sparse_scan(oracle_sim_t* s, const uint64_t* counts, void** send, uin
         oracle_philox4x32_10(ctr, key, r);
       }
       const uint32_t p = peer_from_word(r[j & 3], s->N, n);
+      if (edge_lost(&s->cfg, s->N, n, p, s->t, j, key)) continue;
       uint64_t v = majv;
       int rp;
       if (p >= s->lo && p < s->hi) {
@@ -715,6 +736,15 @@ int oracle_sparse_commit(oracle_sim_t* s, uint64_t items, uint64_t* partial) {
   own_totals(s, partial);
   s->planned = 0;
   s->last_sparse = 1;
+  return GOSSIP_OK;
+}
+
+int oracle_set_faults(oracle_sim_t* s, uint32_t edge_loss, uint32_t partitions) {
+  if (!s) return GOSSIP_EINVAL;
+  if ((edge_loss || partitions > 1) && (s->mode == GOSSIP_MODE_FLOOD || s->mode == GOSSIP_MODE_ANTIENTROPY))
+    return GOSSIP_ENOTSUP;
+  s->cfg.edge_loss = edge_loss;
+  s->cfg.partitions = partitions;
   return GOSSIP_OK;
 }
 

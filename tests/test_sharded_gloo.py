@@ -14,6 +14,7 @@ import torch.multiprocessing as mp
 
 CASES = [
     ("pushpull", 2, 64, 3000, 0x5EED0004, None),
+    ("pushpull-faults", 2, 64, 3000, 0x5EED0004, None),
     ("push", 3, 1, 2001, 0x5EED0001, None),
     ("pull", 2, 70, 1001, 11, None),
     ("flood", 0, 3, 49, 0, "grid"),
@@ -34,6 +35,11 @@ def _grid(n):
     return [[int(v[1:]) for v in t[f"n{i}"]] for i in range(n)]
 
 
+def _faults(name):
+    """pushpull-faults: 25 % edge loss and 3 partitions"""
+    return {"edge_loss": 1 << 30, "partitions": 3} if name.endswith("-faults") else {}
+
+
 PLANS = {"auto": None, "sparse": "1.0", "dense": "-1"}  # GOSSIP_SPARSE_FRAC
 
 
@@ -49,7 +55,7 @@ def _worker(rank, world, port, case, q, frac=None):
         os.environ["GOSSIP_SPARSE_FRAC"] = frac
     dist.init_process_group("gloo", rank=rank, world_size=world)
     mode, k, R, N, seed, topo = case
-    e = op.OracleEngine(N, R, mode, k, seed, flags=1, shard_rank=rank, shard_count=world)
+    e = op.OracleEngine(N, R, mode.split("-")[0], k, seed, flags=1, shard_rank=rank, shard_count=world, **_faults(mode))
     if topo:
         e.set_topology(_grid(N))
         e.inject(0, 0); e.inject(N - 1, 1); e.inject(N // 2, 2)
@@ -67,7 +73,7 @@ def test_two_ranks_equal_one(case, plan):
         pytest.skip("FLOOD rounds are always dense (no sparse protocol)")
     import oracle_py as op
     mode, k, R, N, seed, topo = case
-    ref = op.OracleEngine(N, R, mode, k, seed, flags=1)
+    ref = op.OracleEngine(N, R, mode.split("-")[0], k, seed, flags=1, **_faults(mode))
     if topo:
         ref.set_topology(_grid(N))
         ref.inject(0, 0); ref.inject(N - 1, 1); ref.inject(N // 2, 2)
