@@ -1,4 +1,4 @@
-// antientropy.h — version-vector anti-entropy kernels (DESIGN.md §2.7).
+// antientropy.h — version-vector anti-entropy kernels (DESIGN.md §2.7, §3.8).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -6,23 +6,43 @@
 namespace gossip {
 
 struct AeArgs {
-  const uint32_t* V;     // S_t rows  [N][K]
-  uint32_t* Vn;          // S_{t+1} rows (seeded with a copy of V)
-  const uint8_t* alive;  // alive flags before round t's churn
-  uint8_t* alive_n;      // after
+  uint32_t* V;             // S_t rows [N][K] (sparse rounds update them in place)
+  uint32_t* Vn;            // dense rounds: S_{t+1} rows
+  // alive + stale bitmaps, interleaved so one 16-B read answers both for a peer:
+  // word 2w = alive bits, word 2w+1 = stale bits (row != target) of nodes 64w .. 64w+63
+  const uint64_t* ab;      // before round t: alive after round t-1, stale of S_t
+  uint64_t* abn;           // round t: alive after its churn; stale of S_t, then of S_{t+1}
   const uint32_t* target;  // global max vector (constant between injections)
   uint64_t* partial;
   uint64_t N;
   uint32_t K, L, k, t;
   uint32_t key0, key1, fail, rec;
   uint32_t flags;
+  // sparse rounds: the scan's blocks own contiguous node ranges
+  // (spc chunks of 64 nodes each) and list their edges in a segment of segcap
+  uint64_t* aux;     // [0] stale nodes (stats kernels), [1] largest segment count (scan)
+  uint32_t* segn;    // [nseg] edges each scan block found
+  uint32_t* eid;     // [nseg][segcap][2] edge ends (n, p)
+  uint32_t* erow;    // [nseg][segcap][2][K] S_t rows of the two ends
+  uint32_t* claim;   // [N] epoch of the last fix-up pass that owned the node
+  uint32_t nseg, spc, segcap;
+  uint32_t epoch;
 };
 
 uint32_t ae_lanes(uint32_t K);
 hipError_t launch_ae_init(uint32_t* V, uint32_t* target, uint64_t N, uint32_t K, uint32_t k0, uint32_t k1,
                           hipStream_t st);
 hipError_t launch_ae_inject(uint32_t* V, uint32_t* target, uint64_t node, uint32_t K, uint32_t c, hipStream_t st);
+hipError_t launch_ae_fill_alive(uint64_t* ab, uint64_t N, hipStream_t st);
+// churn of round t: ab -> abn (alive bits churned, stale bits carried)
+hipError_t launch_ae_churn(const AeArgs& a, hipStream_t st);
+// dense round (after the churn): pull pass writes every row of Vn, push pass atomicMax into Vn
 hipError_t launch_ae_round(const AeArgs& a, hipStream_t st);
-hipError_t launch_ae_stats(const AeArgs& a, const uint32_t* V, const uint8_t* alive, hipStream_t st);
+// stats of (V, the alive bits of ab); write_stale also rebuilds ab's stale bits and aux[0]
+hipError_t launch_ae_stats(const AeArgs& a, const uint32_t* V, uint64_t* ab, bool write_stale, hipStream_t st);
+// sparse round (after the churn): scan (edges touching a stale node), gather, apply in
+// place, fix-up (stale bits, hash delta into partial[3]), then stats from the bitmaps
+hipError_t launch_ae_sparse(const AeArgs& a, hipStream_t st);
+hipError_t launch_ae_sparse_stats(const AeArgs& a, hipStream_t st);
 
 }  // namespace gossip

@@ -1,4 +1,4 @@
-// antientropy.hip — version-vector anti-entropy with churn (configs[4]; DESIGN.md §2.7).
+// antientropy.hip — version-vector anti-entropy with churn (configs[4]; DESIGN.md §2.7, §3.8).
 //
 // Each node holds K uint32 versions (AoS rows V[n*K + c], so a peer's whole
 // vector is one contiguous K*4-byte row).  Round t: churn by Philox tag 1,
@@ -7,23 +7,55 @@
 // reference's only failure handling is retry-until-acked (main.go:77-87);
 // churn here is the build-defined fault model of SURVEY.md §5.
 //
-// Lanes: L = next power of two >= K lanes per node (a wave holds 64/L nodes);
-// lane c of a node owns component c, the group's first lane draws the Philox
-// numbers and broadcasts them.  Writes go to V' (seeded with a copy of V) by
-// atomicMax, so concurrent pushes and pulls into one row commute.
+// Every kernel walks 64-node chunks, one chunk per wave.  The node phase runs
+// one lane per node (churn, Philox peers, the peer's churn: three Philox
+// calls, spread over all 64 lanes); the row phase runs L = next power of two
+// >= K lanes per node, 64/L nodes per sub-step, with the node phase's results
+// handed over by shuffles.
+//
+// Two round paths, chosen per round by the host (engine.hip):
+// - dense: V' seeded with a copy of V; both directions of every exchange are
+//   atomicMax into V' (only components that grow);
+// - sparse (most of a run: once nearly every alive node holds the global max
+//   vector, only exchanges touching a stale node can change anything): the
+//   scan lists the exchanges with a stale end, the rows of both ends are
+//   snapshotted, then merged in place, and a fix-up pass updates the stale
+//   bitmap and the hash for each touched node once (claimed by epoch).
 #include "antientropy.h"
 #include "philox.h"
+#include "wave.h"
 
 namespace gossip {
 
 namespace {
 
 constexpr int kAeBlock = 256;
+constexpr int kAeWaves = kAeBlock / 64;
 
 __device__ __forceinline__ bool churned(uint8_t alive, uint32_t n, uint32_t t, uint32_t k0, uint32_t k1,
                                         uint32_t fail, uint32_t rec) {
   const uint32_t x = philox4x32_10(u32x4{n, t, 1u, 0u}, k0, k1).x;
   return alive ? !(x < fail) : (x < rec);
+}
+
+__device__ __forceinline__ uint64_t wave_id() { return (uint64_t)blockIdx.x * kAeWaves + (threadIdx.x >> 6); }
+__device__ __forceinline__ uint64_t wave_count() { return (uint64_t)gridDim.x * kAeWaves; }
+
+// block sum of one u64 per lane, added to *dst by one atomic
+__device__ __forceinline__ void block_add(uint64_t v, uint64_t* red, uint64_t* dst) {
+  v = wave_sum64(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t s = 0;
+    for (int w = 0; w < kAeWaves; ++w) s += red[w];
+    if (s) atomicAdd((unsigned long long*)dst, (unsigned long long)s);
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ uint64_t hash_term(uint32_t v, uint32_t c, uint64_t n, uint64_t N) {
+  return v ? mix64((uint64_t)v + ((uint64_t)c * N + n) * kGold64) : 0ull;
 }
 
 __global__ __launch_bounds__(kAeBlock) void ae_init_kernel(uint32_t* V, uint64_t N, uint32_t K, uint32_t k0,
@@ -52,113 +84,362 @@ __global__ void ae_inject_kernel(uint32_t* V, uint32_t* target, uint64_t node, u
   atomicMax(&target[c], v);
 }
 
-__global__ __launch_bounds__(kAeBlock) void ae_round_kernel(AeArgs a) {
+__device__ __forceinline__ bool alive_bit(const uint64_t* ab, uint32_t n) { return (ab[2 * (n >> 6)] >> (n & 63)) & 1ull; }
+
+// alive and stale bit of n with one 16-B load
+__device__ __forceinline__ void alive_stale(const uint64_t* ab, uint32_t n, bool* al, bool* st) {
+  const uint4 w = *reinterpret_cast<const uint4*>(ab + 2 * (n >> 6));
+  const uint32_t sh = n & 31;
+  const uint32_t aw = (n & 32) ? w.y : w.x, sw = (n & 32) ? w.w : w.z;
+  *al = (aw >> sh) & 1u;
+  *st = (sw >> sh) & 1u;
+}
+
+// peer j of node n in round t; x carries the Philox words across j
+__device__ __forceinline__ uint32_t peer_j(const AeArgs& a, uint32_t n, uint32_t j, u32x4& x) {
+  if ((j & 3u) == 0) x = philox4x32_10(u32x4{n, a.t, 0u, j >> 2}, a.key0, a.key1);
+  return peer_from_word(lane_of(x, j & 3u), a.N - 1, n);
+}
+
+__global__ __launch_bounds__(kAeBlock) void ae_fill_alive_kernel(uint64_t* ab, uint64_t N) {
+  const uint64_t nw = (N + 63) / 64;
+  for (uint64_t w = (uint64_t)blockIdx.x * kAeBlock + threadIdx.x; w < nw; w += (uint64_t)gridDim.x * kAeBlock) {
+    ab[2 * w] = (w + 1) * 64 <= N ? ~0ull : ((1ull << (N & 63)) - 1ull);
+    ab[2 * w + 1] = 0;
+  }
+}
+
+// churn of round t, one lane per node: ab -> abn (bits past N stay 0), stale bits carried
+__global__ __launch_bounds__(kAeBlock) void ae_churn_kernel(AeArgs a) {
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t lead = lane & ~(a.L - 1);  // first lane of this node's group
-  const uint32_t c = lane & (a.L - 1);
-  const uint64_t nodes_per_block = kAeBlock / a.L;
+  const uint64_t chunks = (a.N + 63) / 64;
+  for (uint64_t ch = wave_id(); ch < chunks; ch += wave_count()) {
+    const uint64_t n = ch * 64 + lane;
+    bool al = false;
+    if (n < a.N) al = churned((a.ab[2 * ch] >> lane) & 1ull, (uint32_t)n, a.t, a.key0, a.key1, a.fail, a.rec);
+    const uint64_t b = __ballot(al);
+    if (lane == 0) a.abn[2 * ch] = b;
+    if (lane == 1) a.abn[2 * ch + 1] = a.ab[2 * ch + 1];
+  }
+}
+
+// ---------------------------------------------------------------- dense round
+// Row phase layout: sub-step i of a chunk covers nodes i*per .. i*per+per-1, lane
+// (sub, c) holds component c of node i*per + sub.  Each lane keeps its L values
+// in registers across the exchanges.
+
+// pull pass: Vn[n] = max(V[n], V[p_j] for every exchange j of n) — plain stores of every row
+template <uint32_t L>
+__global__ __launch_bounds__(kAeBlock) void ae_pull_kernel(AeArgs a) {
+  constexpr uint32_t per = 64 / L;
+  __shared__ uint64_t red[kAeWaves];
+  const uint32_t lane = threadIdx.x & 63, sub = lane / L, c = lane % L;
+  const uint32_t* __restrict__ V = a.V;
+  uint32_t* __restrict__ Vn = a.Vn;
+  const uint64_t chunks = (a.N + 63) / 64;
   uint64_t msgs = 0;
-  for (uint64_t base = (uint64_t)blockIdx.x * nodes_per_block; base < a.N; base += (uint64_t)gridDim.x * nodes_per_block) {
-    const uint64_t n64 = base + threadIdx.x / a.L;
-    const bool valid = n64 < a.N;
-    const uint32_t n = (uint32_t)(valid ? n64 : a.N - 1);
-    // churn of n (leader draws, group shares; every lane takes part in the shuffle)
-    int aln = 0;
-    if (c == 0) aln = churned(a.alive[n], n, a.t, a.key0, a.key1, a.fail, a.rec);
-    aln = __shfl(aln, (int)lead, 64);
-    if (valid && c == 0) a.alive_n[n] = (uint8_t)aln;
-    const uint64_t vn_idx = (uint64_t)n * a.K + c;
-    const bool mine = valid && aln && c < a.K;
-    const uint32_t vn = mine ? a.V[vn_idx] : 0u;
+  for (uint64_t ch = wave_id(); ch < chunks; ch += wave_count()) {
+    const uint32_t n = (uint32_t)(ch * 64 + lane);
+    const bool aln = (a.abn[2 * ch] >> lane) & 1ull;
+    uint32_t acc[L];
+#pragma unroll
+    for (uint32_t i = 0; i < L; ++i) {
+      const uint64_t node = ch * 64 + i * per + sub;
+      acc[i] = (node < a.N && c < a.K) ? V[node * a.K + c] : 0u;
+    }
     u32x4 x{0, 0, 0, 0};
     for (uint32_t j = 0; j < a.k; ++j) {
       uint32_t p = 0;
-      int alp = 0;
-      if (c == 0) {
-        if ((j & 3u) == 0) x = philox4x32_10(u32x4{n, a.t, 0u, j >> 2}, a.key0, a.key1);
-        p = peer_from_word(lane_of(x, j & 3u), a.N - 1, n);
-        alp = churned(a.alive[p], p, a.t, a.key0, a.key1, a.fail, a.rec);
+      bool ex = false;
+      if (aln) {
+        p = peer_j(a, n, j, x);
+        ex = alive_bit(a.abn, p);
       }
-      p = (uint32_t)__shfl((int)p, (int)lead, 64);
-      alp = __shfl(alp, (int)lead, 64);
-      if (!(mine && alp)) continue;
-      if (c == 0) ++msgs;
-      const uint64_t vp_idx = (uint64_t)p * a.K + c;
-      const uint32_t vp = a.V[vp_idx];
-      if (vp > vn) atomicMax(&a.Vn[vn_idx], vp);  // pull
-      if (vn > vp) atomicMax(&a.Vn[vp_idx], vn);  // push
+      msgs += ex ? 1u : 0u;
+      if (!__ballot(ex)) continue;
+#pragma unroll
+      for (uint32_t i = 0; i < L; ++i) {
+        const uint32_t src = i * per + sub;
+        const uint32_t pp = (uint32_t)__shfl((int)p, (int)src, 64);
+        const int e = __shfl((int)ex, (int)src, 64);
+        if (e && c < a.K) acc[i] = max(acc[i], V[(uint64_t)pp * a.K + c]);
+      }
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < L; ++i) {
+      const uint64_t node = ch * 64 + i * per + sub;
+      if (node < a.N && c < a.K) Vn[node * a.K + c] = acc[i];
     }
   }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) msgs += __shfl_xor(msgs, off, 64);
-  if (lane == 0 && msgs) atomicAdd((unsigned long long*)&a.partial[2], (unsigned long long)msgs);
+  block_add(msgs, red, &a.partial[2]);
 }
 
-// stats of V_{t+1}: alive count, alive nodes equal to the global max vector,
-// per-component counts (lane c of every group), optional hash
-__global__ __launch_bounds__(kAeBlock) void ae_stats_kernel(AeArgs a, const uint32_t* __restrict__ V,
-                                                            const uint8_t* __restrict__ alive) {
+// push pass: atomicMax(Vn[p_j], V[n]) on the components where V[n] > V[p_j]
+template <uint32_t L>
+__global__ __launch_bounds__(kAeBlock) void ae_push_kernel(AeArgs a) {
+  constexpr uint32_t per = 64 / L;
+  const uint32_t lane = threadIdx.x & 63, sub = lane / L, c = lane % L;
+  const uint32_t* __restrict__ V = a.V;
+  uint32_t* __restrict__ Vn = a.Vn;
+  const uint64_t chunks = (a.N + 63) / 64;
+  for (uint64_t ch = wave_id(); ch < chunks; ch += wave_count()) {
+    const uint32_t n = (uint32_t)(ch * 64 + lane);
+    const bool aln = (a.abn[2 * ch] >> lane) & 1ull;
+    if (!__ballot(aln)) continue;
+    uint32_t own[L];
+#pragma unroll
+    for (uint32_t i = 0; i < L; ++i) {
+      const uint64_t node = ch * 64 + i * per + sub;
+      own[i] = (node < a.N && c < a.K) ? V[node * a.K + c] : 0u;
+    }
+    u32x4 x{0, 0, 0, 0};
+    for (uint32_t j = 0; j < a.k; ++j) {
+      uint32_t p = 0;
+      bool ex = false;
+      if (aln) {
+        p = peer_j(a, n, j, x);
+        ex = alive_bit(a.abn, p);
+      }
+      if (!__ballot(ex)) continue;
+      uint32_t vp[L], pp[L];
+      bool go[L];
+#pragma unroll
+      for (uint32_t i = 0; i < L; ++i) {
+        const uint32_t src = i * per + sub;
+        pp[i] = (uint32_t)__shfl((int)p, (int)src, 64);
+        go[i] = __shfl((int)ex, (int)src, 64) && c < a.K;
+        vp[i] = go[i] ? V[(uint64_t)pp[i] * a.K + c] : 0u;
+      }
+#pragma unroll
+      for (uint32_t i = 0; i < L; ++i)
+        if (go[i] && own[i] > vp[i]) atomicMax(&Vn[(uint64_t)pp[i] * a.K + c], own[i]);
+    }
+  }
+}
+
+// stats of (V, alive bits of ab): alive count, alive nodes equal to the global max
+// vector, per-component counts, optional hash; write_stale: stale bits of ab + aux[0]
+template <uint32_t L>
+__global__ __launch_bounds__(kAeBlock) void ae_stats_kernel(AeArgs a, const uint32_t* __restrict__ V, uint64_t* ab,
+                                                            bool write_stale) {
+  constexpr uint32_t per = 64 / L;
+  constexpr uint64_t gmask = L >= 64 ? ~0ull : ((1ull << L) - 1ull);
   __shared__ uint32_t cnt[64];
-  __shared__ uint64_t red[3][kAeBlock / 64];
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t c = lane & (a.L - 1);
-  const uint32_t groups = 64 / a.L;
-  const uint64_t kmask = a.K >= 64 ? ~0ull : ((1ull << a.K) - 1ull);
+  __shared__ uint64_t red[kAeWaves];
+  const uint32_t lane = threadIdx.x & 63, sub = lane / L, c = lane % L;
   if (threadIdx.x < 64) cnt[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t tgt = c < a.K ? a.target[c] : 0u;
-  uint64_t hash = 0, full = 0, nalive = 0;
+  const uint64_t chunks = (a.N + 63) / 64;
+  uint64_t hash = 0, full = 0, nalive = 0, nstale = 0;
   uint32_t c_lane = 0;
-  const uint64_t nodes_per_block = kAeBlock / a.L;
-  for (uint64_t base = (uint64_t)blockIdx.x * nodes_per_block; base < a.N; base += (uint64_t)gridDim.x * nodes_per_block) {
-    const uint64_t n = base + threadIdx.x / a.L;
-    const bool valid = n < a.N && c < a.K;
-    const uint32_t v = valid ? V[n * a.K + c] : 0u;
-    const bool al = n < a.N && alive[n];
-    if ((a.flags & 1u) && v) hash += mix64((uint64_t)v + ((uint64_t)c * a.N + n) * kGold64);
-    const uint64_t eq = __ballot(valid && v == tgt);
-    const uint64_t ok = __ballot(valid && al && v == tgt);
-    const uint64_t lead_alive = __ballot(c == 0 && al);
-    nalive += (uint64_t)__popcll(lead_alive);
-    for (uint32_t g = 0; g < groups; ++g) {
-      const bool allk = ((eq >> (g * a.L)) & kmask) == kmask;
-      full += (allk && ((lead_alive >> (g * a.L)) & 1ull)) ? 1u : 0u;
-    }
-    // lane c (< K) of group 0 counts component c over all groups of the wave
-    if (lane < a.K) {
-      uint32_t s = 0;
-      for (uint32_t g = 0; g < groups; ++g) s += (uint32_t)((ok >> (g * a.L + lane)) & 1ull);
-      c_lane += s;
-    }
-  }
-  if (lane < a.K && c_lane) atomicAdd(&cnt[lane], c_lane);
+  for (uint64_t ch = wave_id(); ch < chunks; ch += wave_count()) {
+    uint32_t v[L];
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) hash += __shfl_xor(hash, off, 64);
-  if (lane == 0) {
-    red[0][wave] = hash;
-    red[1][wave] = full;
-    red[2][wave] = nalive;
+    for (uint32_t i = 0; i < L; ++i) {
+      const uint64_t node = ch * 64 + i * per + sub;
+      v[i] = (node < a.N && c < a.K) ? V[node * a.K + c] : 0u;
+    }
+    const uint64_t aw = ab[2 * ch];  // bits past N are 0
+    uint64_t stale = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < L; ++i) {
+      const uint64_t node = ch * 64 + i * per + sub;
+      const bool valid = node < a.N && c < a.K;
+      const bool al = (aw >> (i * per + sub)) & 1ull;
+      if (a.flags & 1u) hash += valid ? hash_term(v[i], c, node, a.N) : 0ull;
+      c_lane += (valid && al && v[i] == tgt) ? 1u : 0u;
+      const uint64_t bad = __ballot(valid && v[i] != tgt);
+      if (per == 64) {
+        stale = bad;
+      } else {
+#pragma unroll
+        for (uint32_t g = 0; g < per; ++g) stale |= (((bad >> (g * L)) & gmask) ? 1ull : 0ull) << (i * per + g);
+      }
+    }
+    nalive += (uint64_t)__popcll(aw);
+    full += (uint64_t)__popcll(aw & ~stale);
+    nstale += (uint64_t)__popcll(stale);
+    if (write_stale && lane == 0) ab[2 * ch + 1] = stale;
+  }
+  if (c < a.K && c_lane) atomicAdd(&cnt[c], c_lane);
+  // full / nalive / nstale are wave-uniform: count them once per wave
+  if (lane != 0) full = nalive = nstale = 0;
+  block_add(hash, red, &a.partial[3]);
+  block_add(full, red, &a.partial[0]);
+  block_add(nalive, red, &a.partial[1]);
+  if (write_stale) block_add(nstale, red, &a.aux[0]);
+  if (threadIdx.x < a.K && cnt[threadIdx.x])
+    atomicAdd((unsigned long long*)&a.partial[4 + threadIdx.x], (unsigned long long)cnt[threadIdx.x]);
+}
+
+// --------------------------------------------------------------- sparse round
+// Scan: block b owns chunks [b*spc, (b+1)*spc) and lists, into its own segment,
+// the exchanges with a stale end (LDS slot counter); past segcap only counted.
+__global__ __launch_bounds__(kAeBlock) void ae_sparse_scan_kernel(AeArgs a) {
+  __shared__ uint64_t red[kAeWaves];
+  __shared__ uint32_t scnt;
+  const uint32_t lane = threadIdx.x & 63;
+  if (threadIdx.x == 0) scnt = 0;
+  __syncthreads();
+  const uint64_t chunks = (a.N + 63) / 64;
+  const uint64_t c0 = (uint64_t)blockIdx.x * a.spc;
+  const uint64_t c1 = c0 + a.spc < chunks ? c0 + a.spc : chunks;
+  uint32_t* eid = a.eid + (size_t)blockIdx.x * a.segcap * 2;
+  const uint64_t below = (1ull << lane) - 1ull;
+  uint64_t msgs = 0;
+  for (uint64_t ch = c0 + (threadIdx.x >> 6); ch < c1; ch += kAeWaves) {
+    const uint32_t n = (uint32_t)(ch * 64 + lane);
+    const bool aln = (a.abn[2 * ch] >> lane) & 1ull;
+    const bool own_stale = (a.abn[2 * ch + 1] >> lane) & 1ull;
+    u32x4 x{0, 0, 0, 0};
+    for (uint32_t j = 0; j < a.k; ++j) {
+      uint32_t p = 0;
+      bool ex = false, pst = false;
+      if (aln) {
+        p = peer_j(a, n, j, x);
+        alive_stale(a.abn, p, &ex, &pst);
+      }
+      msgs += ex ? 1u : 0u;
+      const bool need = ex && (own_stale || pst);
+      const uint64_t m = __ballot(need);
+      if (!m) continue;
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(&scnt, (uint32_t)__popcll(m));
+      base = (uint32_t)__shfl((int)base, 0, 64);
+      const uint32_t slot = base + (uint32_t)__popcll(m & below);
+      if (need && slot < a.segcap) {
+        eid[2 * slot] = n;
+        eid[2 * slot + 1] = p;
+      }
+    }
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint64_t h = 0, f = 0, al = 0;
-    for (int w = 0; w < kAeBlock / 64; ++w) {
-      h += red[0][w];
-      f += red[1][w];
-      al += red[2][w];
-    }
-    if (f) atomicAdd((unsigned long long*)&a.partial[0], (unsigned long long)f);
-    if (al) atomicAdd((unsigned long long*)&a.partial[1], (unsigned long long)al);
-    if (h) atomicAdd((unsigned long long*)&a.partial[3], (unsigned long long)h);
+    a.segn[blockIdx.x] = scnt;
+    if (scnt) atomicMax((unsigned long long*)&a.aux[1], (unsigned long long)scnt);
   }
-  if (threadIdx.x < a.K && cnt[threadIdx.x])
-    atomicAdd((unsigned long long*)&a.partial[4 + threadIdx.x], (unsigned long long)cnt[threadIdx.x]);
+  block_add(msgs, red, &a.partial[2]);
+}
+
+// edges of this block's segment, or 0 when any segment overflowed (the host reruns the round dense)
+__device__ __forceinline__ uint32_t segment_edges(const AeArgs& a) {
+  return a.aux[1] > a.segcap ? 0u : a.segn[blockIdx.x];
+}
+
+// snapshot the S_t rows of both ends (before any in-place write)
+template <uint32_t L>
+__global__ __launch_bounds__(kAeBlock) void ae_sparse_gather_kernel(AeArgs a) {
+  constexpr uint32_t epb = kAeBlock / L;  // edges per block step
+  const uint32_t c = threadIdx.x % L;
+  const uint32_t m = segment_edges(a);
+  if (c >= a.K) return;
+  const size_t s0 = (size_t)blockIdx.x * a.segcap;
+  for (uint32_t i = threadIdx.x / L; i < m; i += epb) {
+    const size_t e = s0 + i;
+    const uint32_t n = a.eid[2 * e], p = a.eid[2 * e + 1];
+    const uint32_t vn = a.V[(uint64_t)n * a.K + c], vp = a.V[(uint64_t)p * a.K + c];
+    a.erow[(2 * e) * a.K + c] = vn;
+    a.erow[(2 * e + 1) * a.K + c] = vp;
+  }
+}
+
+// merge in place: both ends take the max of the two snapshots
+template <uint32_t L>
+__global__ __launch_bounds__(kAeBlock) void ae_sparse_apply_kernel(AeArgs a) {
+  constexpr uint32_t epb = kAeBlock / L;
+  const uint32_t c = threadIdx.x % L;
+  const uint32_t m = segment_edges(a);
+  if (c >= a.K) return;
+  const size_t s0 = (size_t)blockIdx.x * a.segcap;
+  for (uint32_t i = threadIdx.x / L; i < m; i += epb) {
+    const size_t e = s0 + i;
+    const uint32_t n = a.eid[2 * e], p = a.eid[2 * e + 1];
+    const uint32_t on = a.erow[(2 * e) * a.K + c], op = a.erow[(2 * e + 1) * a.K + c];
+    if (op > on) atomicMax(&a.V[(uint64_t)n * a.K + c], op);
+    if (on > op) atomicMax(&a.V[(uint64_t)p * a.K + c], on);
+  }
+}
+
+// each touched node once (the first end to claim it this epoch): hash delta
+// old -> new row into partial[3], clear its stale bit when it reached the target
+template <uint32_t L>
+__global__ __launch_bounds__(kAeBlock) void ae_sparse_fix_kernel(AeArgs a) {
+  constexpr uint32_t epb = kAeBlock / L;
+  constexpr uint64_t gmask = L >= 64 ? ~0ull : ((1ull << L) - 1ull);
+  __shared__ uint64_t red[kAeWaves];
+  const uint32_t lane = threadIdx.x & 63, c = lane % L, lead = lane - c;
+  const uint32_t m = segment_edges(a);
+  const uint32_t tgt = c < a.K ? a.target[c] : 0u;
+  const size_t s0 = (size_t)blockIdx.x * a.segcap;
+  uint64_t dh = 0;
+  // the same trip count for every lane of the block, so the ballots see every lane
+  for (uint32_t b = 0; b < m; b += epb) {
+    const uint32_t i = b + threadIdx.x / L;
+    const bool ve = i < m;
+    const size_t e = s0 + i;
+    for (uint32_t end = 0; end < 2; ++end) {
+      const uint32_t xn = ve ? a.eid[2 * e + end] : 0u;
+      int own = 0;
+      if (ve && c == 0) own = atomicMax(&a.claim[xn], a.epoch) < a.epoch;
+      own = __shfl(own, (int)lead, 64);
+      const bool act = own && c < a.K;
+      const uint32_t nv = act ? a.V[(uint64_t)xn * a.K + c] : 0u;
+      const uint32_t ov = act ? a.erow[(2 * e + end) * a.K + c] : 0u;
+      if ((a.flags & 1u) && act) dh += hash_term(nv, c, xn, a.N) - hash_term(ov, c, xn, a.N);
+      const uint64_t bad = __ballot(act && nv != tgt);
+      if (own && c == 0 && !((bad >> lead) & gmask))
+        atomicAnd((unsigned long long*)&a.abn[2 * (xn >> 6) + 1], ~(1ull << (xn & 63)));
+    }
+  }
+  block_add(dh, red, &a.partial[3]);
+}
+
+// stats of the sparse round's result from the bitmaps, one lane per 64-node word:
+// full = alive and not stale; per-component counts add the matching components of
+// the (few) alive stale rows
+__global__ __launch_bounds__(kAeBlock) void ae_sparse_stats_kernel(AeArgs a) {
+  __shared__ uint32_t cnt[64], tgt[64];
+  __shared__ uint64_t red[kAeWaves];
+  if (threadIdx.x < 64) {
+    cnt[threadIdx.x] = 0;
+    tgt[threadIdx.x] = threadIdx.x < a.K ? a.target[threadIdx.x] : 0u;
+  }
+  __syncthreads();
+  const uint64_t words = (a.N + 63) / 64;
+  uint64_t full = 0, nalive = 0, nstale = 0;
+  for (uint64_t w = (uint64_t)blockIdx.x * kAeBlock + threadIdx.x; w < words; w += (uint64_t)gridDim.x * kAeBlock) {
+    const uint4 q = *reinterpret_cast<const uint4*>(a.abn + 2 * w);
+    const uint64_t aw = ((uint64_t)q.y << 32) | q.x, sw = ((uint64_t)q.w << 32) | q.z;
+    nalive += (uint64_t)__popcll(aw);
+    full += (uint64_t)__popcll(aw & ~sw);
+    nstale += (uint64_t)__popcll(sw);
+    for (uint64_t as = aw & sw; as; as &= as - 1) {
+      const uint64_t n = w * 64 + (uint64_t)__builtin_ctzll(as);
+      for (uint32_t c = 0; c < a.K; ++c)
+        if (a.V[n * a.K + c] == tgt[c]) atomicAdd(&cnt[c], 1u);
+    }
+  }
+  const uint64_t f = wave_sum64(full);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = f;
+  __syncthreads();
+  uint64_t bfull = 0;
+  for (int w = 0; w < kAeWaves; ++w) bfull += red[w];
+  __syncthreads();
+  block_add(full, red, &a.partial[0]);
+  block_add(nalive, red, &a.partial[1]);
+  block_add(nstale, red, &a.aux[0]);
+  if (threadIdx.x < a.K && (bfull + cnt[threadIdx.x]))
+    atomicAdd((unsigned long long*)&a.partial[4 + threadIdx.x], (unsigned long long)(bfull + cnt[threadIdx.x]));
 }
 
 uint32_t ae_grid(uint64_t units, uint32_t per_block, uint32_t cap) {
   const uint64_t b = (units + per_block - 1) / per_block;
   return (uint32_t)(b == 0 ? 1 : (b < cap ? b : cap));
 }
+
+// 64-node chunks, one per wave: enough waves to fill 256 CUs several times over
+uint32_t chunk_grid(uint64_t N) { return ae_grid((N + 63) / 64, kAeWaves, 8192); }
 
 }  // namespace
 
@@ -182,15 +463,48 @@ hipError_t launch_ae_inject(uint32_t* V, uint32_t* target, uint64_t node, uint32
   return hipGetLastError();
 }
 
-hipError_t launch_ae_round(const AeArgs& a, hipStream_t st) {
-  const uint32_t npb = kAeBlock / a.L;
-  ae_round_kernel<<<ae_grid(a.N, npb, 1u << 20), kAeBlock, 0, st>>>(a);
+#define AE_LAUNCH_L(KER, L, grid, st, ...)                                  \
+  switch (L) {                                                               \
+    case 1: KER<1><<<(grid), kAeBlock, 0, (st)>>>(__VA_ARGS__); break;       \
+    case 2: KER<2><<<(grid), kAeBlock, 0, (st)>>>(__VA_ARGS__); break;       \
+    case 4: KER<4><<<(grid), kAeBlock, 0, (st)>>>(__VA_ARGS__); break;       \
+    case 8: KER<8><<<(grid), kAeBlock, 0, (st)>>>(__VA_ARGS__); break;       \
+    case 16: KER<16><<<(grid), kAeBlock, 0, (st)>>>(__VA_ARGS__); break;     \
+    case 32: KER<32><<<(grid), kAeBlock, 0, (st)>>>(__VA_ARGS__); break;     \
+    default: KER<64><<<(grid), kAeBlock, 0, (st)>>>(__VA_ARGS__); break;     \
+  }
+
+hipError_t launch_ae_fill_alive(uint64_t* ab, uint64_t N, hipStream_t st) {
+  ae_fill_alive_kernel<<<ae_grid((N + 63) / 64, kAeBlock, 1024), kAeBlock, 0, st>>>(ab, N);
   return hipGetLastError();
 }
 
-hipError_t launch_ae_stats(const AeArgs& a, const uint32_t* V, const uint8_t* alive, hipStream_t st) {
-  const uint32_t npb = kAeBlock / a.L;
-  ae_stats_kernel<<<ae_grid(a.N, npb, 8192), kAeBlock, 0, st>>>(a, V, alive);
+hipError_t launch_ae_churn(const AeArgs& a, hipStream_t st) {
+  ae_churn_kernel<<<chunk_grid(a.N), kAeBlock, 0, st>>>(a);
+  return hipGetLastError();
+}
+
+hipError_t launch_ae_round(const AeArgs& a, hipStream_t st) {
+  AE_LAUNCH_L(ae_pull_kernel, a.L, chunk_grid(a.N), st, a);
+  AE_LAUNCH_L(ae_push_kernel, a.L, chunk_grid(a.N), st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_ae_stats(const AeArgs& a, const uint32_t* V, uint64_t* ab, bool write_stale, hipStream_t st) {
+  AE_LAUNCH_L(ae_stats_kernel, a.L, chunk_grid(a.N), st, a, V, ab, write_stale);
+  return hipGetLastError();
+}
+
+hipError_t launch_ae_sparse(const AeArgs& a, hipStream_t st) {
+  ae_sparse_scan_kernel<<<a.nseg, kAeBlock, 0, st>>>(a);
+  AE_LAUNCH_L(ae_sparse_gather_kernel, a.L, a.nseg, st, a);
+  AE_LAUNCH_L(ae_sparse_apply_kernel, a.L, a.nseg, st, a);
+  AE_LAUNCH_L(ae_sparse_fix_kernel, a.L, a.nseg, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_ae_sparse_stats(const AeArgs& a, hipStream_t st) {
+  ae_sparse_stats_kernel<<<ae_grid((a.N + 63) / 64, kAeBlock, 2048), kAeBlock, 0, st>>>(a);
   return hipGetLastError();
 }
 

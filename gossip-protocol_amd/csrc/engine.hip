@@ -68,7 +68,18 @@ struct gossip_engine {
   bool has_topo = false;
   // ANTIENTROPY: rows V[n*K + c], alive bytes, global max vector
   uint32_t *V = nullptr, *Vn = nullptr, *target = nullptr;
-  uint8_t *alive = nullptr, *alive_n = nullptr;
+  uint64_t *alive = nullptr, *alive_n = nullptr;  // [chunks][2]: alive bits, stale bits (AeArgs::ab)
+  // ANTIENTROPY sparse rounds: stale bitmap of V, edge list + row snapshots,
+  // fix-up claims; aux = [0] stale nodes [1] listed edges (device) / ae_aux_h (pinned host copy)
+  uint64_t *ae_aux = nullptr, *ae_aux_h = nullptr;
+  uint32_t *ae_eid = nullptr, *ae_erow = nullptr, *ae_claim = nullptr, *ae_segn = nullptr;
+  uint32_t ae_nseg = 1, ae_spc = 1, ae_segcap = 1;
+  uint64_t ae_cap = 0, ae_hash = 0, ae_stale = 0, ae_alive = 0, ae_full = 0;
+  uint32_t ae_epoch = 0;
+  int ae_force = -1;             // GOSSIP_AE_SPARSE: -1 auto, 0 never, 1 whenever the bitmap is valid
+  bool ae_sb_valid = false;      // the stale bits of alive, ae_hash and ae_stale describe V
+  bool ae_sparse_last = false;   // the last round ran in place (V not rotated)
+  uint64_t ae_sparse_rounds = 0, ae_overflows = 0;
   // binned (LDS) pipeline for W == 1 random modes on one shard
   bool binned = false;
   BinGeom bg{};
@@ -157,10 +168,11 @@ void free_all(gossip_engine* e) {
   for (void* b : sx)
     if (b) (void)hipFree(b);
   if (e->sx_host) (void)hipHostFree(e->sx_host);
-  void* ae[] = {e->V, e->Vn, e->target, e->alive, e->alive_n};
+  void* ae[] = {e->V, e->Vn, e->target, e->alive, e->alive_n, e->ae_aux, e->ae_claim, e->ae_eid, e->ae_erow, e->ae_segn};
   for (void* b : ae)
     if (b) (void)hipFree(b);
   if (e->partial_h) (void)hipHostFree(e->partial_h);
+  if (e->ae_aux_h) (void)hipHostFree(e->ae_aux_h);
   if (e->ring_h) (void)hipHostFree(e->ring_h);
   for (auto& p : e->ev)
     for (auto& x : p)
@@ -258,8 +270,8 @@ AeArgs make_ae_args(gossip_engine* e) {
   AeArgs a{};
   a.V = e->V;
   a.Vn = e->Vn;
-  a.alive = e->alive;
-  a.alive_n = e->alive_n;
+  a.ab = e->alive;
+  a.abn = e->alive_n;
   a.target = e->target;
   a.partial = e->partial_d;
   a.N = e->N;
@@ -272,6 +284,15 @@ AeArgs make_ae_args(gossip_engine* e) {
   a.fail = e->cfg.churn_fail;
   a.rec = e->cfg.churn_recover;
   a.flags = e->cfg.flags;
+  a.aux = e->ae_aux;
+  a.eid = e->ae_eid;
+  a.erow = e->ae_erow;
+  a.claim = e->ae_claim;
+  a.segn = e->ae_segn;
+  a.nseg = e->ae_nseg;
+  a.spc = e->ae_spc;
+  a.segcap = e->ae_segcap;
+  a.epoch = e->ae_epoch;
   return a;
 }
 
@@ -453,21 +474,83 @@ int step_planned(gossip_engine* e, uint32_t max_rounds, gossip_round_stats_t* st
   return GOSSIP_OK;
 }
 
+// ANTIENTROPY round.  Sparse (in place) when the stale
+// bitmap is valid and the exchanges touching a stale node are predicted to fit
+// the edge list; a list that overflowed leaves V, the bitmap and the claims
+// untouched, and the round is rerun dense.  Stats reach the host every round.
+int ae_read_back(gossip_engine* e) {
+  HIP_OK(e, hipMemcpyAsync(e->partial_h, e->partial_d, part_len(e) * 8, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(e, hipMemcpyAsync(e->ae_aux_h, e->ae_aux, 16, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(e, hipStreamSynchronize(e->stream));
+  return GOSSIP_OK;
+}
+
+bool ae_plan_sparse(const gossip_engine* e) {
+  if (!e->ae_sb_valid || e->ae_force == 0) return false;
+  if (e->ae_force == 1) return true;
+  // exchanges with a stale end ~ 2k x (alive stale after churn): the alive stale
+  // nodes that survive plus the stale dead ones that revive (x1.5 margin)
+  const double alive_stale = (double)(e->ae_alive - e->ae_full);
+  const double dead_stale = std::max(0.0, (double)e->ae_stale - alive_stale);
+  const double rec = e->cfg.churn_recover / 4294967296.0;
+  const double pred = 3.0 * e->k * (alive_stale + dead_stale * rec) + 1024.0;
+  return pred <= 0.7 * (double)e->ae_cap;  // the largest segment, not the mean, must fit
+}
+
+int ae_round(gossip_engine* e) {
+  int rc;
+  bool sparse = ae_plan_sparse(e);
+  e->ae_sparse_last = false;
+  if (sparse) {
+    if (++e->ae_epoch == 0) {  // claims hold epochs: restart them after a wrap
+      HIP_OK(e, hipMemsetAsync(e->ae_claim, 0, (size_t)e->N * 4, e->stream));
+      e->ae_epoch = 1;
+    }
+    const AeArgs a = make_ae_args(e);
+    HIP_OK(e, hipMemsetAsync(e->ae_aux, 0, 16, e->stream));
+    if ((rc = timer_begin(e, 0))) return rc;
+    HIP_OK(e, launch_ae_churn(a, e->stream));
+    HIP_OK(e, launch_ae_sparse(a, e->stream));
+    if ((rc = timer_end(e, 0))) return rc;
+    if ((rc = timer_begin(e, 1))) return rc;
+    HIP_OK(e, launch_ae_sparse_stats(a, e->stream));
+    if ((rc = timer_end(e, 1))) return rc;
+    if ((rc = ae_read_back(e))) return rc;
+    if (e->ae_aux_h[1] > e->ae_segcap) {  // overflow: only alive_n was written
+      if ((rc = timer_collect(e))) return rc;
+      ++e->ae_overflows;
+      sparse = false;
+      HIP_OK(e, hipMemsetAsync(e->partial_d, 0, part_len(e) * 8, e->stream));
+    }
+  }
+  if (!sparse) {
+    const AeArgs a = make_ae_args(e);
+    HIP_OK(e, hipMemsetAsync(e->ae_aux, 0, 16, e->stream));
+    if ((rc = timer_begin(e, 0))) return rc;
+    HIP_OK(e, launch_ae_churn(a, e->stream));
+    HIP_OK(e, launch_ae_round(a, e->stream));
+    if ((rc = timer_end(e, 0))) return rc;
+    if ((rc = timer_begin(e, 1))) return rc;
+    HIP_OK(e, launch_ae_stats(a, e->Vn, e->alive_n, true, e->stream));
+    if ((rc = timer_end(e, 1))) return rc;
+    if ((rc = ae_read_back(e))) return rc;
+  }
+  // sparse rounds return the hash delta of the rows they changed
+  e->ae_hash = sparse ? e->ae_hash + e->partial_h[3] : e->partial_h[3];
+  e->ae_stale = e->ae_aux_h[0];
+  e->ae_full = e->partial_h[0];
+  e->ae_alive = e->partial_h[1];
+  e->ae_sb_valid = true;
+  e->ae_sparse_last = sparse;
+  if (sparse) ++e->ae_sparse_rounds;
+  return GOSSIP_OK;
+}
+
 // compute S_{t+1} of the owned shard from the gathered image + partial stats (device)
 int compute_round(gossip_engine* e, const uint64_t* gathered) {
   const size_t bytes = (size_t)e->W * e->Nl * 8;
   if (!e->binned) HIP_OK(e, hipMemsetAsync(e->partial_d, 0, part_len(e) * 8, e->stream));
-  if (e->mode == GOSSIP_MODE_ANTIENTROPY) {
-    int rc;
-    const AeArgs a = make_ae_args(e);
-    if ((rc = timer_begin(e, 0))) return rc;
-    HIP_OK(e, hipMemcpyAsync(e->Vn, e->V, e->N * e->R * 4, hipMemcpyDeviceToDevice, e->stream));
-    HIP_OK(e, launch_ae_round(a, e->stream));
-    if ((rc = timer_end(e, 0))) return rc;
-    if ((rc = timer_begin(e, 1))) return rc;
-    HIP_OK(e, launch_ae_stats(a, e->Vn, e->alive_n, e->stream));
-    return timer_end(e, 1);
-  }
+  if (e->mode == GOSSIP_MODE_ANTIENTROPY) return ae_round(e);
   RoundArgs a = make_args(e, gathered);
   int rc;
   if (e->mode == GOSSIP_MODE_FLOOD) {
@@ -505,7 +588,7 @@ int compute_round(gossip_engine* e, const uint64_t* gathered) {
 
 void rotate(gossip_engine* e) {
   if (e->mode == GOSSIP_MODE_ANTIENTROPY) {
-    std::swap(e->V, e->Vn);
+    if (!e->ae_sparse_last) std::swap(e->V, e->Vn);  // sparse rounds merge in place
     std::swap(e->alive, e->alive_n);
   } else if (e->mode == GOSSIP_MODE_FLOOD) {
     uint64_t* tmp = e->Sprev;
@@ -650,10 +733,30 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
   };
   if (e->mode == GOSSIP_MODE_ANTIENTROPY) {
     const size_t vb = (size_t)e->N * e->R * 4;
+    const size_t nw = ((size_t)e->N + 63) / 64;
     if (!alloc_raw((void**)&e->V, vb) || !alloc_raw((void**)&e->Vn, vb) || !alloc_raw((void**)&e->target, 256) ||
-        !alloc_raw((void**)&e->alive, e->N) || !alloc_raw((void**)&e->alive_n, e->N))
+        !alloc_raw((void**)&e->alive, nw * 16) || !alloc_raw((void**)&e->alive_n, nw * 16))
       return bail(GOSSIP_ENOMEM);
-    if (hipMemset(e->alive, 1, e->N) != hipSuccess) return bail(GOSSIP_EHIP);
+    if (launch_ae_fill_alive(e->alive, e->N, nullptr) != hipSuccess) return bail(GOSSIP_EHIP);
+    // sparse rounds: scan block b owns ae_spc 64-node chunks and lists
+    // its edges in a segment of ae_segcap; N/8 edges in all covers the churn tail at
+    // configs[4]; small engines get room for every exchange (k per node), so never overflow
+    const uint64_t kn = (uint64_t)e->N * e->k;
+    uint64_t cap = std::min<uint64_t>(kn, std::max<uint64_t>(e->N / 8, 65536));
+    const char* fcap = getenv("GOSSIP_AE_CAP");
+    if (fcap) cap = std::max<uint64_t>(1, strtoull(fcap, nullptr, 10));
+    if (const char* f = getenv("GOSSIP_AE_SPARSE")) e->ae_force = atoi(f);
+    e->ae_nseg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(4096, (nw + 3) / 4));
+    e->ae_spc = (uint32_t)((nw + e->ae_nseg - 1) / e->ae_nseg);
+    e->ae_nseg = (uint32_t)((nw + e->ae_spc - 1) / e->ae_spc);
+    e->ae_segcap = (cap >= kn && !fcap) ? e->k * e->ae_spc * 64 : (uint32_t)((cap + e->ae_nseg - 1) / e->ae_nseg);
+    e->ae_cap = (uint64_t)e->ae_segcap * e->ae_nseg;
+    if (!alloc_raw((void**)&e->ae_aux, 64) ||
+        !alloc_raw((void**)&e->ae_claim, (size_t)e->N * 4) || !alloc_raw((void**)&e->ae_segn, (size_t)e->ae_nseg * 4) ||
+        !alloc_raw((void**)&e->ae_eid, (size_t)e->ae_cap * 8) ||
+        !alloc_raw((void**)&e->ae_erow, (size_t)e->ae_cap * 8 * e->R))
+      return bail(GOSSIP_ENOMEM);
+    if (hipHostMalloc((void**)&e->ae_aux_h, 64) != hipSuccess) return bail(GOSSIP_ENOMEM);
   } else if (e->mode == GOSSIP_MODE_FLOOD) {
     if (!alloc(&e->S, shard) || !alloc(&e->Snext, shard) || !alloc(&e->Sprev, shard) || !alloc(&e->skip, shard) ||
         !alloc(&e->imgF, image))
@@ -808,7 +911,8 @@ int gossip_reset(gossip_engine_t* e) {
   if (e->mode == GOSSIP_MODE_ANTIENTROPY) {
     HIP_OK(e, hipMemsetAsync(e->V, 0, e->N * e->R * 4, e->stream));
     HIP_OK(e, hipMemsetAsync(e->target, 0, 256, e->stream));
-    HIP_OK(e, hipMemsetAsync(e->alive, 1, e->N, e->stream));
+    HIP_OK(e, launch_ae_fill_alive(e->alive, e->N, e->stream));
+    e->ae_sb_valid = false;
   } else if (e->mode == GOSSIP_MODE_FLOOD) {
     HIP_OK(e, hipMemsetAsync(e->S, 0, shard, e->stream));
     HIP_OK(e, hipMemsetAsync(e->Snext, 0, shard, e->stream));
@@ -839,6 +943,7 @@ int gossip_inject(gossip_engine_t* e, uint64_t node, uint32_t rumor) {
   if (int rc = set_dev(e)) return rc;
   if (e->mode == GOSSIP_MODE_ANTIENTROPY) {
     HIP_OK(e, launch_ae_inject(e->V, e->target, node, e->R, rumor, e->stream));
+    e->ae_sb_valid = false;  // the target may have moved
     return GOSSIP_OK;
   }
   if (e->frontier && e->fr_valid) {
@@ -856,6 +961,7 @@ int gossip_inject_random(gossip_engine_t* e) {
   if (int rc = set_dev(e)) return rc;
   if (e->mode == GOSSIP_MODE_ANTIENTROPY) {
     HIP_OK(e, launch_ae_init(e->V, e->target, e->N, e->R, e->key0, e->key1, e->stream));
+    e->ae_sb_valid = false;
     return GOSSIP_OK;
   }
   if (e->frontier && e->fr_valid) {
@@ -894,6 +1000,7 @@ int gossip_round_compute(gossip_engine_t* e, uint64_t* partial) {
   if (int rc = timer_collect(e)) return rc;
   std::memcpy(partial, e->partial_h, part_len(e) * 8);
   if (e->mode != GOSSIP_MODE_ANTIENTROPY) partial[1] = e->nown;
+  else partial[3] = (e->cfg.flags & GOSSIP_FLAG_HASH) ? e->ae_hash : 0;
   e->last_sparse = false;
   return GOSSIP_OK;
 }
@@ -1120,9 +1227,9 @@ int gossip_read_versions(gossip_engine_t* e, uint64_t node, uint32_t* out, uint3
   HIP_OK(e, hipStreamSynchronize(e->stream));
   HIP_OK(e, hipMemcpy(out, e->V + node * e->R, e->R * 4, hipMemcpyDeviceToHost));
   if (alive) {
-    uint8_t a = 0;
-    HIP_OK(e, hipMemcpy(&a, e->alive + node, 1, hipMemcpyDeviceToHost));
-    *alive = a;
+    uint64_t w = 0;
+    HIP_OK(e, hipMemcpy(&w, e->alive + 2 * (node / 64), 8, hipMemcpyDeviceToHost));
+    *alive = (uint32_t)((w >> (node & 63)) & 1ull);
   }
   return GOSSIP_OK;
 }
@@ -1141,7 +1248,7 @@ int gossip_state_hash(gossip_engine_t* e, uint64_t* out) {
     AeArgs a = make_ae_args(e);
     a.flags |= GOSSIP_FLAG_HASH;
     HIP_OK(e, hipMemsetAsync(e->partial_d, 0, part_len(e) * 8, e->stream));
-    HIP_OK(e, launch_ae_stats(a, e->V, e->alive, e->stream));
+    HIP_OK(e, launch_ae_stats(a, e->V, e->alive, false, e->stream));
     HIP_OK(e, hipMemcpyAsync(e->partial_h, e->partial_d, part_len(e) * 8, hipMemcpyDeviceToHost, e->stream));
     HIP_OK(e, hipStreamSynchronize(e->stream));
     *out = e->partial_h[3];

@@ -1,0 +1,77 @@
+"""GPU parity of the ANTIENTROPY round paths against the CPU oracle,
+bit-exact per round: stats, per-component counts, hash, and the rows and alive flags read back.
+
+Paths (all must agree with the oracle and with each other):
+  auto     — dense rounds until the stale nodes are few, then sparse in-place rounds
+  dense    — GOSSIP_AE_SPARSE=0: every round dense (copy + atomicMax kernel)
+  sparse   — GOSSIP_AE_SPARSE=1: every round after the first sparse (the edge list holds k*N)
+  overflow — sparse forced with a 64-edge list: rounds whose list overflows are rerun dense
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_py as op
+from gossip_hip import Engine
+from gossip_hip.engine import churn_threshold as ct
+
+pytestmark = pytest.mark.gpu
+THREADS = min(16, os.cpu_count() or 1)
+PATHS = {"auto": {}, "dense": {"GOSSIP_AE_SPARSE": "0"}, "sparse": {"GOSSIP_AE_SPARSE": "1"},
+         "overflow": {"GOSSIP_AE_SPARSE": "1", "GOSSIP_AE_CAP": "64"}}
+
+
+def _engine(monkeypatch, path, *args, **kw):
+    for k in ("GOSSIP_AE_SPARSE", "GOSSIP_AE_CAP"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in PATHS[path].items():
+        monkeypatch.setenv(k, v)
+    return Engine(*args, **kw)
+
+
+def _compare(e, o, N, K, rounds, probe):
+    a, b = e.step(rounds), o.step(rounds)
+    assert a.rounds == b.rounds
+    assert a.stats == b.stats
+    assert np.array_equal(a.infected, b.infected)
+    for node in probe:
+        (ve, ae), (vo, ao) = e.read_versions(node), o.read_versions(node)
+        assert np.array_equal(ve, vo) and ae == ao, node
+    assert e.state_hash() == o.state_hash()
+    return a
+
+
+@pytest.mark.parametrize("path", list(PATHS))
+@pytest.mark.parametrize("N,K,k,fail,rec", [
+    (1 << 16, 16, 1, 0.01, 0.1),
+    (50_001, 5, 2, 0.05, 0.3),
+    (4099, 64, 3, 0.02, 0.2),
+    (777, 1, 1, 0.0, 0.0),
+])
+def test_antientropy_paths_vs_oracle(monkeypatch, path, N, K, k, fail, rec):
+    seed = 0x5EED0005 + K
+    kw = dict(flags=1, churn_fail=ct(fail), churn_recover=ct(rec))
+    e = _engine(monkeypatch, path, N, K, "antientropy", k, seed, **kw)
+    o = op.OracleEngine(N, K, "antientropy", k, seed, threads=THREADS, **kw)
+    probe = (0, 1, N // 3, N // 2, N - 1)
+    for x in (e, o):
+        x.inject_random()
+    _compare(e, o, N, K, 6, probe)           # a few rounds, then a client write mid-run
+    for x in (e, o):
+        x.inject(N // 2, K - 1)
+        x.inject(3, 0)
+    res = _compare(e, o, N, K, 400, probe)
+    assert res.converged
+
+
+def test_antientropy_sparse_tail_1M(monkeypatch):
+    """configs[4] shape at 2^20: the churn tail runs sparse (auto) and matches the oracle."""
+    N, K, k, seed = 1 << 20, 16, 1, 0x5EED0005
+    kw = dict(flags=1, churn_fail=ct(0.01), churn_recover=ct(0.1))
+    e = _engine(monkeypatch, "auto", N, K, "antientropy", k, seed, **kw)
+    o = op.OracleEngine(N, K, "antientropy", k, seed, threads=THREADS, **kw)
+    for x in (e, o):
+        x.inject_random()
+    res = _compare(e, o, N, K, 300, (0, 7, N // 5, N - 2))
+    assert res.converged and res.rounds > 40
