@@ -25,6 +25,7 @@ struct AeArgs {
   uint32_t* eid;     // [nseg][segcap][2] edge ends (n, p)
   uint32_t* erow;    // [nseg][segcap][2][K] S_t rows of the two ends
   uint32_t* claim;   // [N] epoch of the last fix-up pass that owned the node
+  void* pmask;       // dense rounds: [N][k] push masks (components where V[n] > V[p_j]), L bits each
   uint32_t nseg, spc, segcap;
   uint32_t epoch;
 };

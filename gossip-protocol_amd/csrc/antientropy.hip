@@ -22,6 +22,9 @@
 //   snapshotted, then merged in place, and a fix-up pass updates the stale
 //   bitmap and the hash for each touched node once (claimed by epoch).
 #include "antientropy.h"
+
+#include <type_traits>
+
 #include "philox.h"
 #include "wave.h"
 
@@ -128,24 +131,37 @@ __global__ __launch_bounds__(kAeBlock) void ae_churn_kernel(AeArgs a) {
 // (sub, c) holds component c of node i*per + sub.  Each lane keeps its L values
 // in registers across the exchanges.
 
-// pull pass: Vn[n] = max(V[n], V[p_j] for every exchange j of n) — plain stores of every row
+template <uint32_t L>
+struct MaskOf {  // one bit per lane of a node's group
+  using T = typename std::conditional<L <= 8, uint8_t,
+            typename std::conditional<L <= 16, uint16_t,
+            typename std::conditional<L <= 32, uint32_t, uint64_t>::type>::type>::type;
+};
+
+// pull pass: Vn[n] = max(V[n], V[p_j] for every exchange j of n) — plain stores of
+// every row — and, per exchange, the mask of components where V[n] > V[p_j]: the
+// push pass then needs neither the peer's row nor its alive bit
 template <uint32_t L>
 __global__ __launch_bounds__(kAeBlock) void ae_pull_kernel(AeArgs a) {
+  using MT = typename MaskOf<L>::T;
   constexpr uint32_t per = 64 / L;
+  constexpr uint64_t gmask = L >= 64 ? ~0ull : ((1ull << L) - 1ull);
   __shared__ uint64_t red[kAeWaves];
   const uint32_t lane = threadIdx.x & 63, sub = lane / L, c = lane % L;
   const uint32_t* __restrict__ V = a.V;
   uint32_t* __restrict__ Vn = a.Vn;
+  MT* __restrict__ pm = reinterpret_cast<MT*>(a.pmask);
   const uint64_t chunks = (a.N + 63) / 64;
   uint64_t msgs = 0;
   for (uint64_t ch = wave_id(); ch < chunks; ch += wave_count()) {
     const uint32_t n = (uint32_t)(ch * 64 + lane);
     const bool aln = (a.abn[2 * ch] >> lane) & 1ull;
-    uint32_t acc[L];
+    uint32_t own[L], acc[L];
 #pragma unroll
     for (uint32_t i = 0; i < L; ++i) {
       const uint64_t node = ch * 64 + i * per + sub;
-      acc[i] = (node < a.N && c < a.K) ? V[node * a.K + c] : 0u;
+      own[i] = (node < a.N && c < a.K) ? V[node * a.K + c] : 0u;
+      acc[i] = own[i];
     }
     u32x4 x{0, 0, 0, 0};
     for (uint32_t j = 0; j < a.k; ++j) {
@@ -156,13 +172,26 @@ __global__ __launch_bounds__(kAeBlock) void ae_pull_kernel(AeArgs a) {
         ex = alive_bit(a.abn, p);
       }
       msgs += ex ? 1u : 0u;
-      if (!__ballot(ex)) continue;
+      if (!__ballot(ex)) {
+        if (ch * 64 + lane < a.N) pm[(ch * 64 + lane) * a.k + j] = 0;
+        continue;
+      }
+      uint32_t vp[L];
+      bool go[L];
 #pragma unroll
       for (uint32_t i = 0; i < L; ++i) {
         const uint32_t src = i * per + sub;
         const uint32_t pp = (uint32_t)__shfl((int)p, (int)src, 64);
-        const int e = __shfl((int)ex, (int)src, 64);
-        if (e && c < a.K) acc[i] = max(acc[i], V[(uint64_t)pp * a.K + c]);
+        go[i] = __shfl((int)ex, (int)src, 64) && c < a.K;
+        vp[i] = go[i] ? V[(uint64_t)pp * a.K + c] : 0u;
+      }
+      // lane (sub, 0) stores the push mask of node i*per + sub
+#pragma unroll
+      for (uint32_t i = 0; i < L; ++i) {
+        acc[i] = max(acc[i], vp[i]);
+        const uint64_t m = __ballot(go[i] && own[i] > vp[i]);
+        const uint64_t node = ch * 64 + i * per + sub;
+        if (c == 0 && node < a.N) pm[node * a.k + j] = (MT)((m >> (sub * L)) & gmask);
       }
     }
 #pragma unroll
@@ -174,45 +203,36 @@ __global__ __launch_bounds__(kAeBlock) void ae_pull_kernel(AeArgs a) {
   block_add(msgs, red, &a.partial[2]);
 }
 
-// push pass: atomicMax(Vn[p_j], V[n]) on the components where V[n] > V[p_j]
+// push pass: atomicMax(Vn[p_j][c], V[n][c]) for the components c of the pull pass's mask
 template <uint32_t L>
 __global__ __launch_bounds__(kAeBlock) void ae_push_kernel(AeArgs a) {
+  using MT = typename MaskOf<L>::T;
   constexpr uint32_t per = 64 / L;
   const uint32_t lane = threadIdx.x & 63, sub = lane / L, c = lane % L;
   const uint32_t* __restrict__ V = a.V;
   uint32_t* __restrict__ Vn = a.Vn;
+  const MT* __restrict__ pm = reinterpret_cast<const MT*>(a.pmask);
   const uint64_t chunks = (a.N + 63) / 64;
   for (uint64_t ch = wave_id(); ch < chunks; ch += wave_count()) {
-    const uint32_t n = (uint32_t)(ch * 64 + lane);
-    const bool aln = (a.abn[2 * ch] >> lane) & 1ull;
-    if (!__ballot(aln)) continue;
-    uint32_t own[L];
-#pragma unroll
-    for (uint32_t i = 0; i < L; ++i) {
-      const uint64_t node = ch * 64 + i * per + sub;
-      own[i] = (node < a.N && c < a.K) ? V[node * a.K + c] : 0u;
-    }
+    const uint64_t nl = ch * 64 + lane;
+    const uint32_t n = (uint32_t)nl;
     u32x4 x{0, 0, 0, 0};
     for (uint32_t j = 0; j < a.k; ++j) {
+      const uint64_t mw = nl < a.N ? (uint64_t)pm[nl * a.k + j] : 0ull;
+      // Philox words for j..j+3 are drawn at j % 4 == 0 whatever the masks say
       uint32_t p = 0;
-      bool ex = false;
-      if (aln) {
-        p = peer_j(a, n, j, x);
-        ex = alive_bit(a.abn, p);
-      }
-      if (!__ballot(ex)) continue;
-      uint32_t vp[L], pp[L];
-      bool go[L];
+      if ((j & 3u) == 0 || mw) p = peer_j(a, n, j, x);
+      if (!__ballot(mw != 0)) continue;
 #pragma unroll
       for (uint32_t i = 0; i < L; ++i) {
         const uint32_t src = i * per + sub;
-        pp[i] = (uint32_t)__shfl((int)p, (int)src, 64);
-        go[i] = __shfl((int)ex, (int)src, 64) && c < a.K;
-        vp[i] = go[i] ? V[(uint64_t)pp[i] * a.K + c] : 0u;
+        const uint32_t pp = (uint32_t)__shfl((int)p, (int)src, 64);
+        const uint64_t m = __shfl(mw, (int)src, 64);
+        if ((m >> c) & 1ull) {
+          const uint64_t node = ch * 64 + src;
+          atomicMax(&Vn[(uint64_t)pp * a.K + c], V[node * a.K + c]);
+        }
       }
-#pragma unroll
-      for (uint32_t i = 0; i < L; ++i)
-        if (go[i] && own[i] > vp[i]) atomicMax(&Vn[(uint64_t)pp[i] * a.K + c], own[i]);
     }
   }
 }

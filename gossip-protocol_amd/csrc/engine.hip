@@ -73,6 +73,7 @@ struct gossip_engine {
   // fix-up claims; aux = [0] stale nodes [1] listed edges (device) / ae_aux_h (pinned host copy)
   uint64_t *ae_aux = nullptr, *ae_aux_h = nullptr;
   uint32_t *ae_eid = nullptr, *ae_erow = nullptr, *ae_claim = nullptr, *ae_segn = nullptr;
+  void* ae_pmask = nullptr;  // dense rounds: [N][k] push masks
   uint32_t ae_nseg = 1, ae_spc = 1, ae_segcap = 1;
   uint64_t ae_cap = 0, ae_hash = 0, ae_stale = 0, ae_alive = 0, ae_full = 0;
   uint32_t ae_epoch = 0;
@@ -168,7 +169,7 @@ void free_all(gossip_engine* e) {
   for (void* b : sx)
     if (b) (void)hipFree(b);
   if (e->sx_host) (void)hipHostFree(e->sx_host);
-  void* ae[] = {e->V, e->Vn, e->target, e->alive, e->alive_n, e->ae_aux, e->ae_claim, e->ae_eid, e->ae_erow, e->ae_segn};
+  void* ae[] = {e->V, e->Vn, e->target, e->alive, e->alive_n, e->ae_aux, e->ae_claim, e->ae_eid, e->ae_erow, e->ae_segn, e->ae_pmask};
   for (void* b : ae)
     if (b) (void)hipFree(b);
   if (e->partial_h) (void)hipHostFree(e->partial_h);
@@ -289,6 +290,7 @@ AeArgs make_ae_args(gossip_engine* e) {
   a.erow = e->ae_erow;
   a.claim = e->ae_claim;
   a.segn = e->ae_segn;
+  a.pmask = e->ae_pmask;
   a.nseg = e->ae_nseg;
   a.spc = e->ae_spc;
   a.segcap = e->ae_segcap;
@@ -754,7 +756,8 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
     if (!alloc_raw((void**)&e->ae_aux, 64) ||
         !alloc_raw((void**)&e->ae_claim, (size_t)e->N * 4) || !alloc_raw((void**)&e->ae_segn, (size_t)e->ae_nseg * 4) ||
         !alloc_raw((void**)&e->ae_eid, (size_t)e->ae_cap * 8) ||
-        !alloc_raw((void**)&e->ae_erow, (size_t)e->ae_cap * 8 * e->R))
+        !alloc_raw((void**)&e->ae_erow, (size_t)e->ae_cap * 8 * e->R) ||
+        !alloc_raw(&e->ae_pmask, (size_t)e->N * e->k * std::max<uint32_t>(1, ae_lanes(e->R) / 8)))
       return bail(GOSSIP_ENOMEM);
     if (hipHostMalloc((void**)&e->ae_aux_h, 64) != hipSuccess) return bail(GOSSIP_ENOMEM);
   } else if (e->mode == GOSSIP_MODE_FLOOD) {
