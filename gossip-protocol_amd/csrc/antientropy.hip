@@ -238,12 +238,14 @@ __global__ __launch_bounds__(kAeBlock) void ae_push_kernel(AeArgs a) {
 }
 
 // stats of (V, alive bits of ab): alive count, alive nodes equal to the global max
-// vector, per-component counts, optional hash; write_stale: stale bits of ab + aux[0]
+// vector, per-component counts, optional hash; write_stale: stale bits of ab + aux[0].
+// Here lane (sub, c) holds component c of nodes sub*L .. sub*L+L-1 (one per sub-step),
+// so a group's "differs" bits OR-reduce across its L lanes into its nodes' stale bits.
 template <uint32_t L>
 __global__ __launch_bounds__(kAeBlock) void ae_stats_kernel(AeArgs a, const uint32_t* __restrict__ V, uint64_t* ab,
                                                             bool write_stale) {
+  using BT = typename std::conditional<(L > 32), uint64_t, uint32_t>::type;
   constexpr uint32_t per = 64 / L;
-  constexpr uint64_t gmask = L >= 64 ? ~0ull : ((1ull << L) - 1ull);
   __shared__ uint32_t cnt[64];
   __shared__ uint64_t red[kAeWaves];
   const uint32_t lane = threadIdx.x & 63, sub = lane / L, c = lane % L;
@@ -257,25 +259,29 @@ __global__ __launch_bounds__(kAeBlock) void ae_stats_kernel(AeArgs a, const uint
     uint32_t v[L];
 #pragma unroll
     for (uint32_t i = 0; i < L; ++i) {
-      const uint64_t node = ch * 64 + i * per + sub;
+      const uint64_t node = ch * 64 + sub * L + i;
       v[i] = (node < a.N && c < a.K) ? V[node * a.K + c] : 0u;
     }
     const uint64_t aw = ab[2 * ch];  // bits past N are 0
-    uint64_t stale = 0;
+    BT bad = 0;
 #pragma unroll
     for (uint32_t i = 0; i < L; ++i) {
-      const uint64_t node = ch * 64 + i * per + sub;
+      const uint64_t node = ch * 64 + sub * L + i;
       const bool valid = node < a.N && c < a.K;
-      const bool al = (aw >> (i * per + sub)) & 1ull;
+      const bool al = (aw >> (sub * L + i)) & 1ull;
       if (a.flags & 1u) hash += valid ? hash_term(v[i], c, node, a.N) : 0ull;
       c_lane += (valid && al && v[i] == tgt) ? 1u : 0u;
-      const uint64_t bad = __ballot(valid && v[i] != tgt);
-      if (per == 64) {
-        stale = bad;
-      } else {
+      bad |= (BT)(valid && v[i] != tgt) << i;
+    }
 #pragma unroll
-        for (uint32_t g = 0; g < per; ++g) stale |= (((bad >> (g * L)) & gmask) ? 1ull : 0ull) << (i * per + g);
-      }
+    for (uint32_t off = 1; off < L; off <<= 1) bad |= (BT)__shfl_xor(bad, (int)off, 64);
+    uint64_t stale = 0;
+    if (per <= L) {  // few groups: fetch each group's bits
+#pragma unroll
+      for (uint32_t g = 0; g < per; ++g) stale |= (uint64_t)__shfl(bad, (int)(g * L), 64) << (g * L);
+    } else {  // few bits per group: one ballot per bit, over the group leaders
+#pragma unroll
+      for (uint32_t i = 0; i < L; ++i) stale |= __ballot(c == 0 && ((bad >> i) & 1u)) << i;
     }
     nalive += (uint64_t)__popcll(aw);
     full += (uint64_t)__popcll(aw & ~stale);

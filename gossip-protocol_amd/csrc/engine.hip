@@ -33,7 +33,7 @@ namespace {
 
 thread_local std::string g_create_error;
 
-constexpr int kTimers = 2;  // 0 = round kernel, 1 = stats kernel
+constexpr int kTimers = 3;  // 0 = round kernel, 1 = stats kernel, 2 = ANTIENTROPY sparse round kernels
 
 }  // namespace
 
@@ -119,10 +119,10 @@ struct gossip_engine {
   uint64_t* sx_host = nullptr;  // pinned: [G + 2] counts / list bases
 
   hipEvent_t ev[kTimers][2] = {};
-  double time_ms[kTimers] = {0, 0};
-  uint64_t launches[kTimers] = {0, 0};
+  double time_ms[kTimers] = {0, 0, 0};
+  uint64_t launches[kTimers] = {0, 0, 0};
   bool timing = false;
-  bool ev_pending[kTimers] = {false, false};
+  bool ev_pending[kTimers] = {false, false, false};
 
   int fail(int code, const char* fmt, ...) {
     char buf[512];
@@ -510,10 +510,10 @@ int ae_round(gossip_engine* e) {
     }
     const AeArgs a = make_ae_args(e);
     HIP_OK(e, hipMemsetAsync(e->ae_aux, 0, 16, e->stream));
-    if ((rc = timer_begin(e, 0))) return rc;
+    if ((rc = timer_begin(e, 2))) return rc;
     HIP_OK(e, launch_ae_churn(a, e->stream));
     HIP_OK(e, launch_ae_sparse(a, e->stream));
-    if ((rc = timer_end(e, 0))) return rc;
+    if ((rc = timer_end(e, 2))) return rc;
     if ((rc = timer_begin(e, 1))) return rc;
     HIP_OK(e, launch_ae_sparse_stats(a, e->stream));
     if ((rc = timer_end(e, 1))) return rc;

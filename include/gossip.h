@@ -204,7 +204,8 @@ int gossip_philox_device(gossip_engine_t* eng, const uint32_t* ctr4, const uint3
 
 /* GOSSIP_FLAG_TIMING: accumulated device time (ms) and count of `which`:
  * 0 = the whole S_t -> S_{t+1} transform of a round (all its kernels),
- * 1 = the separate stats kernel (direct path only; fused in the binned path). */
+ * 1 = the separate stats kernel (direct path only; fused in the binned path),
+ * 2 = ANTIENTROPY sparse rounds' kernels (their stats pass counts under 1; dense rounds under 0). */
 int gossip_kernel_time(const gossip_engine_t* eng, uint32_t which, double* total_ms, uint64_t* launches);
 int gossip_reset_timing(gossip_engine_t* eng);
 
