@@ -8,14 +8,16 @@
 // churn here is the build-defined fault model of SURVEY.md §5.
 //
 // Every kernel walks 64-node chunks, one chunk per wave.  The node phase runs
-// one lane per node (churn, Philox peers, the peer's churn: three Philox
-// calls, spread over all 64 lanes); the row phase runs L = next power of two
-// >= K lanes per node, 64/L nodes per sub-step, with the node phase's results
-// handed over by shuffles.
+// one lane per node (Philox peer draw, the peer's alive bit from the churn
+// kernel's bitmap); the row phase runs L = next power of two >= K lanes per
+// node, 64/L nodes per sub-step, with the node phase's results handed over by
+// shuffles.  Alive and stale bits share one [chunks][2] array (AeArgs::ab).
 //
-// Two round paths, chosen per round by the host (engine.hip):
-// - dense: V' seeded with a copy of V; both directions of every exchange are
-//   atomicMax into V' (only components that grow);
+// Two round paths, chosen per round by the host (engine.hip), both after the
+// churn kernel:
+// - dense: a pull pass writes every row of V' = max(V[n], V[p_j]) and the
+//   per-exchange push masks; a push pass atomicMax-es V[n] into V'[p_j] for the
+//   masked components only;
 // - sparse (most of a run: once nearly every alive node holds the global max
 //   vector, only exchanges touching a stale node can change anything): the
 //   scan lists the exchanges with a stale end, the rows of both ends are
