@@ -20,6 +20,19 @@ constexpr uint32_t kRecPerRegion = 16384;  // records staged per sender tile (LD
 constexpr uint32_t kMaxSenders = 8192;     // senders per sender tile (their values staged once, 8 B each)
 constexpr uint32_t kMaxTilesD = 4096;     // N <= 2^26 on this path (and <= 4096 sender regions)
 
+// Sharded dense rounds (sb_*): the pull pass stages no sender values, so its
+// tile counters cover the whole image (N <= kSbMaxTiles * kTileD = 2^27).
+constexpr uint32_t kSbMaxTiles = 8192;
+
+// One emit pass of a sharded dense round: senders [snd0, snd0 + nsnd) (global
+// ids), edges whose peer lies in [dst0, dst0 + dstn), directions in dmask
+// (bit 0 push, bit 1 pull); wvals = 0: the records carry no sender value
+// (the pull pass).
+struct EmitRange {
+  uint64_t snd0, nsnd, dst0, dstn;
+  uint32_t dmask, wvals;
+};
+
 struct BinGeom {
   uint64_t N;
   uint32_t k;
@@ -52,5 +65,28 @@ void bin_carve(const BinGeom& g, void* base, BinBufs* b);
 hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, uint64_t* partial, uint32_t R,
                                uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t filt,
                                const Faults& fa, uint32_t flags, const RoundSync& rs, hipStream_t st);
+
+// Dense round of a sharded engine (G > 1) after the state all-gather
+// (DESIGN.md §5): push pass P = every sender of the image, records for the
+// own nodes' tiles; pull pass Q = the own senders, records for every tile of
+// the image, served from LDS images of the gathered state; apply over the
+// own tiles writes S_{t+1} of the own slice, its occupancy bitmaps and the
+// own nodes' totals (global ids in the hash).
+struct SbGeom {
+  BinGeom p, q;
+  uint64_t lo, nown;
+};
+struct SbBufs {
+  BinBufs p, q;
+};
+bool sb_path_ok(uint64_t N, uint32_t k, uint64_t nown);
+SbGeom make_sb_geom(uint64_t N, uint32_t k, uint64_t lo, uint64_t nown);
+size_t sb_bytes(const SbGeom& g);
+void sb_carve(const SbGeom& g, void* base, SbBufs* b);
+// image: the gathered S_t (global ids); Snext: the own slice of S_{t+1};
+// nzb/fullb: bitmaps over the own nodes; partial must be zero on entry.
+hipError_t launch_sb_round(const SbGeom& g, const SbBufs& b, const uint64_t* image, uint64_t* Snext,
+                           uint64_t* partial, uint32_t R, uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode,
+                           const Faults& fa, uint32_t flags, uint64_t* nzb, uint64_t* fullb, hipStream_t st);
 
 }  // namespace gossip

@@ -75,31 +75,48 @@ __device__ __forceinline__ uint32_t dir_flags(uint32_t d) { return ((d & 1u) ? 0
 
 // KREG > 0: the k (<= KREG) peers of each sender stay in registers between passes.
 // FAULTS: edge loss / partitions active; off, none of that code exists.
-template <int KREG, bool FAULTS>
+// V = 0: one shard.  V = 1, 2: one pass of a sharded dense round (EmitRange):
+// senders [snd0, snd0 + nsnd) of the gathered image S (global ids), only edges
+// whose peer lies in [dst0, dst0 + dstn), only the directions in dmask, tiles
+// counted from dst0.  V = 2 (pull pass) stores no sender values, so its tile
+// counters can cover kSbMaxTiles tiles of the whole image.
+template <int KREG, bool FAULTS, int V>
 __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const uint64_t* __restrict__ S, BinBufs b,
                                                                   uint32_t R, uint32_t t, uint32_t key0,
                                                                   uint32_t key1, uint32_t mode, uint32_t filt,
-                                                                  Faults fa) {
-  __shared__ uint32_t cur[kMaxTilesD];
+                                                                  Faults fa, EmitRange er) {
+  constexpr bool SHARD = V != 0;
+  constexpr uint32_t kMaxT = V == 2 ? kSbMaxTiles : kMaxTilesD;
+  constexpr uint32_t kMaxS = kMaxSenders;
+  __shared__ uint32_t cur[kMaxT];
   __shared__ uint32_t st_ids[kRecPerRegion];  // p_local | n_local << 14, sorted by destination tile
-  __shared__ uint64_t sval[kMaxSenders];      // S_t of each sender, once (not once per record)
+  __shared__ uint64_t sval[V == 2 ? 1 : kMaxS];  // S_t of each sender, once (not once per record)
   __shared__ uint32_t wsum[kEmitThreads / 64];
   __shared__ uint32_t wpre[kEmitThreads / 64 + 1];
 
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint64_t nm1 = g.N - 1, fm = full_mask1(R);
-  constexpr uint32_t kQ = kMaxSenders / kEmitThreads;  // senders per thread upper bound
+  constexpr uint32_t kQ = kMaxS / kEmitThreads;  // senders per thread upper bound
+  const uint64_t snd0 = SHARD ? er.snd0 : 0ull, nsnd = SHARD ? er.nsnd : g.N;
+  const uint32_t dmask = SHARD ? er.dmask : 3u;
+  // destination tile of peer p, false when p lies outside the pass's range
+  auto tile_of = [&](uint32_t p, uint32_t* tl, uint32_t* pl) -> bool {
+    const uint32_t rel = SHARD ? p - (uint32_t)er.dst0 : p;
+    *tl = rel >> kTileDLog;
+    *pl = rel & (kTileD - 1);
+    return !SHARD || rel < (uint32_t)er.dstn;
+  };
 
   // persistent over sender regions s = blockIdx.x, +gridDim.x, ...: the next
   // region's sender values are loaded while this one is sorted and written
   auto load_values = [&](uint32_t s, uint64_t* v) {
     const uint64_t base = (uint64_t)s << g.ts_log;
-    const uint32_t nsend = (uint32_t)min<uint64_t>(g.ts, g.N - base);
+    const uint32_t nsend = (uint32_t)min<uint64_t>(g.ts, nsnd - base);
 #pragma unroll
     for (uint32_t q = 0; q < kQ; ++q) {
       const uint32_t i = tid + q * kEmitThreads;
       // clamp, never branch around a load: a guarded load is waited on alone
-      const uint64_t x = S[base + min(i, nsend - 1)];
+      const uint64_t x = S[snd0 + base + min(i, nsend - 1)];
       v[q] = i < nsend ? x : 0ull;
     }
   };
@@ -107,14 +124,14 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
   if (blockIdx.x < g.nt_s) load_values(blockIdx.x, v);
   for (uint32_t s = blockIdx.x; s < g.nt_s; s += gridDim.x) {
   const uint64_t base = (uint64_t)s << g.ts_log;
-  const uint32_t nsend = (uint32_t)min<uint64_t>(g.ts, g.N - base);
+  const uint32_t nsend = (uint32_t)min<uint64_t>(g.ts, nsnd - base);
   __syncthreads();  // the previous region's write-out has read cur/st_ids/sval
 
   for (uint32_t d = tid; d < g.nt_d; d += kEmitThreads) cur[d] = 0;
 #pragma unroll
   for (uint32_t q = 0; q < kQ; ++q) {
     const uint32_t i = tid + q * kEmitThreads;
-    if (i < g.ts) sval[i] = v[q];
+    if (V != 2 && i < g.ts) sval[i] = v[q];
   }
   if (s + gridDim.x < g.nt_s) load_values(s + gridDim.x, vn);
   __syncthreads();
@@ -128,9 +145,9 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
       ed[q] = 0;
 #pragma unroll
       for (int j = 0; j < KREG; ++j) pr[q * KREG + j] = 0;
-      const uint32_t d = i < nsend ? sender_dirs(mode, v[q], fm) : 0u;
+      const uint32_t d = i < nsend ? sender_dirs(mode, v[q], fm) & dmask : 0u;
       if (!d) continue;
-      const uint32_t n = (uint32_t)(base + i);
+      const uint32_t n = (uint32_t)(snd0 + base + i);
       const u32x4 x = philox4x32_10(u32x4{n, t, 0u, 0u}, key0, key1);
       const u32x4 lw = FAULTS && fa.loss ? loss_draws(n, t, 0u, key0, key1) : u32x4{0, 0, 0, 0};
       const Reach rc = FAULTS ? reach_of(n, fa) : Reach{0u, 0xFFFFFFFFu};  // n's partition block
@@ -138,7 +155,9 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
       for (int j = 0; j < KREG; ++j) {
         pr[q * KREG + j] = peer_from_word(lane_of(x, j), nm1, n);
         const bool lost = FAULTS && edge_lost(fa, rc, pr[q * KREG + j], lane_of(lw, j));
-        if ((uint32_t)j < g.k && !lost) ed[q] |= d << (2 * j);
+        uint32_t tl, pl;
+        const bool in = tile_of(pr[q * KREG + j], &tl, &pl);
+        if ((uint32_t)j < g.k && !lost && in) ed[q] |= d << (2 * j);
       }
     }
     if (filt) {  // every probe issued before any is used (32-bit words: half the registers)
@@ -175,14 +194,18 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
     for (uint32_t q = 0; q < kQ; ++q)
 #pragma unroll
       for (int j = 0; j < KREG; ++j)
-        if ((ed[q] >> (2 * j)) & 3u) atomicAdd(&cur[pr[q * KREG + j] >> kTileDLog], 1u);
+        if ((ed[q] >> (2 * j)) & 3u) {
+          uint32_t tl, pl;
+          tile_of(pr[q * KREG + j], &tl, &pl);
+          atomicAdd(&cur[tl], 1u);
+        }
   } else {
     for (uint32_t q = 0; q < kQ; ++q) {
       const uint32_t i = tid + q * kEmitThreads;
       if (i >= nsend) break;
-      const uint32_t d = sender_dirs(mode, v[q], fm);
+      const uint32_t d = sender_dirs(mode, v[q], fm) & dmask;
       if (!d) continue;
-      const uint32_t n = (uint32_t)(base + i);
+      const uint32_t n = (uint32_t)(snd0 + base + i);
       u32x4 x{0, 0, 0, 0}, lw{0, 0, 0, 0};
       const Reach rc = FAULTS ? reach_of(n, fa) : Reach{0u, 0xFFFFFFFFu};  // n's partition block (§2.8)
       for (uint32_t j = 0; j < g.k; ++j) {
@@ -192,7 +215,9 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
         }
         const uint32_t p = peer_from_word(lane_of(x, j & 3u), nm1, n);
         if (FAULTS && edge_lost(fa, rc, p, lane_of(lw, j & 3u))) continue;
-        if (peer_filter(d, p, filt, b.nzb, b.fullb)) atomicAdd(&cur[p >> kTileDLog], 1u);
+        uint32_t tl, pl;
+        if (!tile_of(p, &tl, &pl)) continue;
+        if (peer_filter(d, p, filt, b.nzb, b.fullb)) atomicAdd(&cur[tl], 1u);
       }
     }
   }
@@ -242,18 +267,19 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
       for (int j = 0; j < KREG; ++j) {
         const uint32_t d = (ed[q] >> (2 * j)) & 3u;
         if (!d) continue;
-        const uint32_t p = pr[q * KREG + j];
-        const uint32_t pos = atomicAdd(&cur[p >> kTileDLog], 1u);
-        st_ids[pos] = (p & (kTileD - 1)) | (i << kTileDLog) | dir_flags(d);
+        uint32_t tl, pl;
+        tile_of(pr[q * KREG + j], &tl, &pl);
+        const uint32_t pos = atomicAdd(&cur[tl], 1u);
+        st_ids[pos] = pl | (i << kTileDLog) | dir_flags(d);
       }
     }
   } else {
     for (uint32_t q = 0; q < kQ; ++q) {
       const uint32_t i = tid + q * kEmitThreads;
       if (i >= nsend) break;
-      const uint32_t d0 = sender_dirs(mode, v[q], fm);
+      const uint32_t d0 = sender_dirs(mode, v[q], fm) & dmask;
       if (!d0) continue;
-      const uint32_t n = (uint32_t)(base + i);
+      const uint32_t n = (uint32_t)(snd0 + base + i);
       u32x4 x{0, 0, 0, 0}, lw{0, 0, 0, 0};
       const Reach rc = FAULTS ? reach_of(n, fa) : Reach{0u, 0xFFFFFFFFu};  // n's partition block (§2.8)
       for (uint32_t j = 0; j < g.k; ++j) {
@@ -263,10 +289,12 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
         }
         const uint32_t p = peer_from_word(lane_of(x, j & 3u), nm1, n);
         if (FAULTS && edge_lost(fa, rc, p, lane_of(lw, j & 3u))) continue;
+        uint32_t tl, pl;
+        if (!tile_of(p, &tl, &pl)) continue;
         const uint32_t d = peer_filter(d0, p, filt, b.nzb, b.fullb);
         if (!d) continue;
-        const uint32_t pos = atomicAdd(&cur[p >> kTileDLog], 1u);
-        st_ids[pos] = (p & (kTileD - 1)) | (i << kTileDLog) | dir_flags(d);
+        const uint32_t pos = atomicAdd(&cur[tl], 1u);
+        st_ids[pos] = pl | (i << kTileDLog) | dir_flags(d);
       }
     }
   }
@@ -280,7 +308,7 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
     // region is written without holes (a partly written 64-B chunk costs HBM
     // a read-modify-write: profiles/r01_experiments/microbench5_scattered_pieces.jsonl)
     gids[e] = id;
-    gvals[e] = sval[(id >> kTileDLog) & kIdNMask];
+    if (V != 2) gvals[e] = sval[(id >> kTileDLog) & kIdNMask];
   }
 #pragma unroll
   for (uint32_t q = 0; q < kQ; ++q) v[q] = vn[q];
@@ -311,7 +339,8 @@ __global__ __launch_bounds__(256) void transpose_u16_kernel(const uint16_t* __re
 // Writes the finished tile (LDS) to S_{t+1} and folds the round stats
 // (definitions as in stats_kernel): fully-informed count by ballot, per-rumor
 // counts as column popcounts of each wave's 64x64 bit matrix, optional hash.
-__device__ __forceinline__ void tile_epilogue(const unsigned long long* acc, uint64_t node0, uint64_t N,
+// hid0: global id of node 0 (sharded rounds hash global ids)
+__device__ __forceinline__ void tile_epilogue(const unsigned long long* acc, uint64_t node0, uint64_t N, uint64_t hid0,
                                               uint64_t* __restrict__ Snext, uint64_t* __restrict__ partial,
                                               uint32_t R, uint32_t flags, uint32_t* cnt, uint64_t* red_hash,
                                               uint32_t* red_full, uint32_t* red_nz, uint64_t* __restrict__ nzb,
@@ -327,7 +356,7 @@ __device__ __forceinline__ void tile_epilogue(const unsigned long long* acc, uin
     const bool valid = n < N;
     const uint64_t x = valid ? (uint64_t)acc[i] : 0ull;
     if (valid) Snext[n] = x;
-    if (do_hash && x) hash += mix64(x + n * kGold64);
+    if (do_hash && x) hash += mix64(x + (hid0 + n) * kGold64);
     const uint64_t fw = __ballot(valid && x == fm);
     const uint64_t nz = __ballot(x != 0);
     full += (uint32_t)__popcll(fw);
@@ -442,11 +471,11 @@ __device__ __forceinline__ void load_tile(unsigned long long* img, const uint64_
   constexpr uint32_t kQ = kTileD / kTileThreads / 2;
   const uint32_t tid = threadIdx.x;
   uint4 x[kQ];
-  if (node0 + kTileD <= N) {
+  if (node0 + kTileD <= N && ((uintptr_t)(S + node0) & 15u) == 0) {  // (a shard slice may start 8-B aligned)
     const uint4* src = (const uint4*)(S + node0);
 #pragma unroll
     for (uint32_t q = 0; q < kQ; ++q) x[q] = src[q * kTileThreads + tid];
-  } else {  // last, ragged tile
+  } else {  // last, ragged tile (or an 8-B aligned slice)
 #pragma unroll
     for (uint32_t q = 0; q < kQ; ++q) {
       const uint64_t n = node0 + 2ull * (q * kTileThreads + tid);
@@ -490,9 +519,13 @@ __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, cons
 
 // K3 — one block per tile X: acc = S_t[X]; OR in the pushes aimed at X (its
 // runs) and the pull responses owed to X's own senders (their regions, read
-// sequentially); write S_{t+1}[X] and fold the stats.
-__global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, const uint64_t* S,
-                                                                  uint64_t* Snext, BinBufs b,  // may alias S
+// sequentially); write S_{t+1}[X] and fold the stats.  One shard: g = gq, b =
+// bq.  Sharded dense round: g/b the push pass (every sender, tiles of the own
+// nodes), gq/bq the pull pass (own senders, tiles of the whole image); S and
+// Snext are the own slices (Nn nodes, global ids from hid0).
+__global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinBufs b, BinGeom gq, BinBufs bq,
+                                                                  const uint64_t* S, uint64_t* Snext,  // may alias
+                                                                  uint64_t Nn, uint64_t hid0,
                                                                   uint64_t* __restrict__ partial, uint32_t R,
                                                                   uint32_t mode, uint32_t flags) {
   __shared__ unsigned long long acc[kTileD];
@@ -505,12 +538,11 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, cons
   const uint32_t tid = threadIdx.x;
   const uint32_t X = xcd_remap(blockIdx.x, g.nt_d);
   const uint64_t node0 = (uint64_t)X << kTileDLog;
-  load_tile(acc, S, node0, g.N);
+  load_tile(acc, S, node0, Nn);
   if (tid < 64) cnt[tid] = 0;
   __syncthreads();
   const uint32_t* __restrict__ gids = b.ids;
   const uint64_t* __restrict__ gvals = b.vals;
-  const uint64_t* __restrict__ gresp = b.resp;
   if (mode == 1 || mode == 3) {  // pushes aimed at this tile
     const uint16_t* rowb = b.offT + (size_t)X * g.nt_s;
     for_each_run_record<kUnroll>(g, rowb, rowb + g.nt_s, wmask, wlist, [&](const int32_t* rec) {
@@ -531,12 +563,14 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, cons
     });
   }
   if (mode == 2 || mode == 3) {  // responses owed to this tile's own senders
-    const uint32_t per = kTileD >> g.ts_log;
-    const uint32_t s0 = X * per, s1 = min(s0 + per, g.nt_s);
+    const uint32_t* __restrict__ qids = bq.ids;
+    const uint64_t* __restrict__ gresp = bq.resp;
+    const uint32_t per = kTileD >> gq.ts_log;
+    const uint32_t s0 = X * per, s1 = min(s0 + per, gq.nt_s);
     for (uint32_t s = s0; s < s1; ++s) {
-      const uint32_t total = b.off[(size_t)s * (g.nt_d + 1) + g.nt_d];
-      const size_t reg = (size_t)s * g.rp;
-      const uint32_t nb = (s - s0) << g.ts_log;
+      const uint32_t total = bq.off[(size_t)s * (gq.nt_d + 1) + gq.nt_d];
+      const size_t reg = (size_t)s * gq.rp;
+      const uint32_t nb = (s - s0) << gq.ts_log;
       for (uint32_t p0 = 0; p0 < total; p0 += kTileThreads * kUnrollSeq) {
         uint64_t r[kUnrollSeq];
         uint32_t id[kUnrollSeq];
@@ -544,7 +578,7 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, cons
 #pragma unroll
         for (int u = 0; u < kUnrollSeq; ++u) {
           const uint32_t pos = min(p0 + u * kTileThreads + tid, total - 1);
-          id[u] = gids[reg + pos];
+          id[u] = qids[reg + pos];
           r[u] = gresp[reg + pos];
         }
 #pragma unroll
@@ -558,7 +592,7 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, cons
     }
   }
   __syncthreads();
-  tile_epilogue(acc, node0, g.N, Snext, partial, R, flags, cnt, red_hash, red_full, red_nz, b.nzb, b.fullb);
+  tile_epilogue(acc, node0, Nn, hid0, Snext, partial, R, flags, cnt, red_hash, red_full, red_nz, b.nzb, b.fullb);
 }
 
 }  // namespace
@@ -612,7 +646,8 @@ hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, 
                                const Faults& fa, uint32_t flags, const RoundSync& rs, hipStream_t st) {
   if (!b.nzb || !b.fullb) filt = 0;  // the bitmaps exist only with the frontier buffers
   const uint32_t eg = g.nt_s < kEmitGrid ? g.nt_s : kEmitGrid;  // persistent: one block per CU
-#define GOSSIP_EMIT(KR, F) bin_emit_kernel<KR, F><<<eg, kEmitThreads, 0, st>>>(g, S, b, R, t, key0, key1, mode, filt, fa)
+#define GOSSIP_EMIT(KR, F) \
+  bin_emit_kernel<KR, F, 0><<<eg, kEmitThreads, 0, st>>>(g, S, b, R, t, key0, key1, mode, filt, fa, EmitRange{})
   if (g.k <= 2) {
     if (fa.any()) GOSSIP_EMIT(2, true); else GOSSIP_EMIT(2, false);
   } else {
@@ -624,8 +659,74 @@ hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, 
   if (mode == 2 || mode == 3) bin_serve_kernel<<<g.nt_d, kTileThreads, 0, st>>>(g, S, b, R);
   // in place: K3 of tile X reads and writes only S[X] (push values and pull
   // responses come from the record buffers), and K1/K2 have finished reading S_t
-  bin_apply_kernel<<<g.nt_d, kTileThreads, 0, st>>>(g, S, S, b, partial, R, mode, flags);
+  bin_apply_kernel<<<g.nt_d, kTileThreads, 0, st>>>(g, b, g, b, S, S, g.N, 0, partial, R, mode, flags);
   return launch_round_snapshot(partial, rs, st);
+}
+
+// --- sharded dense rounds ------------------------------------------------
+
+bool sb_path_ok(uint64_t N, uint32_t k, uint64_t nown) {
+  if (k == 0 || k > 64 || N < 2 || nown == 0) return false;
+  const SbGeom g = make_sb_geom(N, k, 0, nown);
+  return g.q.nt_d <= kSbMaxTiles && g.p.nt_d <= kMaxTilesD && (uint64_t)g.p.nt_s * g.p.rp < (1ull << 31);
+}
+
+SbGeom make_sb_geom(uint64_t N, uint32_t k, uint64_t lo, uint64_t nown) {
+  SbGeom g{};
+  g.lo = lo;
+  g.nown = nown;
+  // region sizes as on one shard (make_bin_geom); peers are drawn over the global id space
+  g.p = g.q = make_bin_geom(N, k);
+  g.p.nt_s = (uint32_t)((N + g.p.ts - 1) / g.p.ts);      // every sender
+  g.p.nt_d = (uint32_t)((nown + kTileD - 1) / kTileD);   // own tiles
+  g.q.nt_s = (uint32_t)((nown + g.q.ts - 1) / g.q.ts);   // own senders
+  g.q.nt_d = (uint32_t)((N + kTileD - 1) / kTileD);      // every tile of the image
+  return g;
+}
+
+size_t sb_bytes(const SbGeom& g) { return bin_bytes(g.p) + bin_bytes(g.q); }
+
+void sb_carve(const SbGeom& g, void* base, SbBufs* b) {
+  bin_carve(g.p, base, &b->p);
+  bin_carve(g.q, (char*)base + bin_bytes(g.p), &b->q);
+  b->p.nzb = b->p.fullb = b->q.nzb = b->q.fullb = nullptr;
+}
+
+hipError_t launch_sb_round(const SbGeom& g, const SbBufs& b, const uint64_t* image, uint64_t* Snext,
+                           uint64_t* partial, uint32_t R, uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode,
+                           const Faults& fa, uint32_t flags, uint64_t* nzb, uint64_t* fullb, hipStream_t st) {
+  const bool push = mode == 1 || mode == 3, pull = mode == 2 || mode == 3;
+  auto emit = [&](const BinGeom& gg, const BinBufs& bb, const EmitRange& er, bool vals) {
+    const uint32_t eg = gg.nt_s < kEmitGrid ? gg.nt_s : kEmitGrid;
+#define GOSSIP_EMIT(KR, F, VV) \
+  bin_emit_kernel<KR, F, VV><<<eg, kEmitThreads, 0, st>>>(gg, image, bb, R, t, key0, key1, mode, 0u, fa, er)
+#define GOSSIP_EMIT_V(VV)                                                 \
+  if (gg.k <= 2) {                                                        \
+    if (fa.any()) GOSSIP_EMIT(2, true, VV); else GOSSIP_EMIT(2, false, VV); \
+  } else {                                                                \
+    if (fa.any()) GOSSIP_EMIT(0, true, VV); else GOSSIP_EMIT(0, false, VV); \
+  }
+    if (vals) {
+      GOSSIP_EMIT_V(1)
+    } else {
+      GOSSIP_EMIT_V(2)
+    }
+#undef GOSSIP_EMIT_V
+#undef GOSSIP_EMIT
+    const dim3 tg((gg.nt_d + 1 + 31) / 32, (gg.nt_s + 31) / 32);
+    transpose_u16_kernel<<<tg, dim3(32, 8), 0, st>>>(bb.off, bb.offT, gg.nt_s, gg.nt_d + 1, partial, 0u);
+  };
+  if (push) emit(g.p, b.p, EmitRange{0, g.p.N, g.lo, g.nown, 1u, 1u}, true);
+  if (pull) {
+    emit(g.q, b.q, EmitRange{g.lo, g.nown, 0, g.q.N, 2u, 0u}, false);
+    bin_serve_kernel<<<g.q.nt_d, kTileThreads, 0, st>>>(g.q, image, b.q, R);
+  }
+  BinBufs bp = b.p;
+  bp.nzb = nzb;
+  bp.fullb = fullb;
+  bin_apply_kernel<<<g.p.nt_d, kTileThreads, 0, st>>>(g.p, bp, g.q, b.q, image + g.lo, Snext, g.nown, g.lo, partial,
+                                                      R, mode, flags);
+  return hipGetLastError();
 }
 
 }  // namespace gossip

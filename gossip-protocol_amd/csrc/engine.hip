@@ -114,6 +114,11 @@ struct gossip_engine {
   FrontierBufs lf{};
   void *lf_mem = nullptr, *sx_mem = nullptr;
   SxItem* rare_recv = nullptr;
+  // sharded dense rounds on the binned pipeline (binned.h: SbGeom), else the direct kernels
+  bool sbin = false;
+  SbGeom sbg{};
+  SbBufs sbb{};
+  void* sb_mem = nullptr;
   SxItem* msg_recv = nullptr;
   uint64_t rare_recv_cap = 0, msg_recv_cap = 0, sx_stride = 0;
   uint64_t* sx_host = nullptr;  // pinned: [G + 2] counts / list bases
@@ -165,7 +170,7 @@ void free_all(gossip_engine* e) {
     if (b) (void)hipFree(b);
   if (e->bin_mem) (void)hipFree(e->bin_mem);
   if (e->fr_mem) (void)hipFree(e->fr_mem);
-  void* sx[] = {e->lf_mem, e->sx_mem, e->rare_recv, e->msg_recv};
+  void* sx[] = {e->lf_mem, e->sx_mem, e->rare_recv, e->msg_recv, e->sb_mem};
   for (void* b : sx)
     if (b) (void)hipFree(b);
   if (e->sx_host) (void)hipHostFree(e->sx_host);
@@ -570,6 +575,13 @@ int compute_round(gossip_engine* e, const uint64_t* gathered) {
     if ((rc = timer_begin(e, 0))) return rc;
     if ((rc = launch_round_path(e, e->t, sparse, maj, all_d, dense_filter(e, x), ring_sync(e, 0)))) return rc;
     return timer_end(e, 0);  // stats are fused into the round kernels
+  } else if (e->sbin) {  // sharded dense round: binned pipeline over the gathered image
+    if ((rc = timer_begin(e, 0))) return rc;
+    HIP_OK(e, launch_sb_round(e->sbg, e->sbb, gathered, e->Snext, e->partial_d, e->R, e->t, e->key0, e->key1,
+                              e->mode, e->fa, e->cfg.flags, e->lf.nzb, e->lf.fullb, e->stream));
+    if ((rc = timer_end(e, 0))) return rc;
+    e->sx_valid = true;  // totals of the own nodes and exact bitmaps of S_{t+1}, fused into the apply pass
+    return GOSSIP_OK;
   } else {
     // timer 0 covers the whole S_t -> S_{t+1} transform (seed copy + round kernel)
     if ((rc = timer_begin(e, 0))) return rc;
@@ -810,6 +822,13 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
       return bail(GOSSIP_ENOMEM);
     }
     e->sx = true;
+    const char* fsb = getenv("GOSSIP_SB");  // 0: dense sharded rounds on the direct kernels
+    if ((!fsb || atoi(fsb) != 0) && sb_path_ok(e->N, e->k, e->nown)) {
+      e->sbg = make_sb_geom(e->N, e->k, e->lo, e->nown);
+      if (!alloc_raw(&e->sb_mem, sb_bytes(e->sbg))) return bail(GOSSIP_ENOMEM);
+      sb_carve(e->sbg, e->sb_mem, &e->sbb);
+      e->sbin = true;
+    }
     // a dense sharded round all-gathers every shard's state (7/8 of the image per GPU at G = 8);
     // a sparse one moves 16 B per rare node plus the cross-shard pushes, so sparse rounds pay
     // off up to a larger rare fraction than on one GPU (tools/shard_probe.py)

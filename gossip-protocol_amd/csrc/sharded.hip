@@ -52,15 +52,38 @@ __global__ __launch_bounds__(256) void list_kernel(FrontierBufs f, const uint64_
   out[pos] = SxItem{lo + i, S[i]};
 }
 
+// Lists are in id order (and shards in rank order), so the items of one bitmap
+// word sit in consecutive lanes: a segmented OR across the wave leaves one
+// atomic per word a wave touches instead of one per item.
 __global__ __launch_bounds__(256) void setbits_kernel(const SxItem* __restrict__ recv, uint64_t stride, uint32_t G,
                                                        const uint64_t* __restrict__ cbase, uint64_t* __restrict__ grb) {
   const uint64_t total = stride * G;
-  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (uint64_t)gridDim.x * 256) {
-    const uint32_t q = (uint32_t)(i / stride);
-    if (i - q * stride >= cbase[q + 1] - cbase[q]) continue;  // padding of a shorter list
-    const uint64_t p = recv[i].node;
-    atomicOr((unsigned long long*)&grb[p >> 6], 1ull << (p & 63));
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t step = (uint64_t)gridDim.x * 256;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * 256; i0 < total; i0 += step) {  // whole waves iterate together
+    const uint64_t i = i0 + threadIdx.x;
+    bool valid = i < total;
+    uint64_t p = 0;
+    if (valid) {
+      const uint32_t q = (uint32_t)(i / stride);
+      valid = i - q * stride < cbase[q + 1] - cbase[q];  // else padding of a shorter list
+      if (valid) p = recv[i].node;
+    }
+    const uint64_t w = valid ? p >> 6 : ~0ull;
+    uint64_t m = valid ? 1ull << (p & 63) : 0ull;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t y = __shfl_down(m, o, 64), wy = __shfl_down(w, o, 64);
+      if (lane + o < 64 && wy == w) m |= y;
+    }
+    const uint64_t wprev = __shfl_up(w, 1, 64);
+    if (valid && (lane == 0 || wprev != w)) atomicOr((unsigned long long*)&grb[w], (unsigned long long)m);
   }
+}
+
+__global__ __launch_bounds__(256) void zero_kernel(uint4* __restrict__ p, uint64_t n16) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * 256)
+    p[i] = make_uint4(0, 0, 0, 0);
 }
 
 __global__ __launch_bounds__(256) void gcount_kernel(const uint64_t* __restrict__ grb, uint64_t nwg, uint32_t* gcnt) {
@@ -426,8 +449,9 @@ hipError_t sx_compact(const SxGeom& g, const SxBufs& b, const FrontierBufs& lf, 
 
 hipError_t sx_index(const SxGeom& g, const SxBufs& b, const SxItem* recv, uint64_t stride, hipStream_t st) {
   const uint64_t nwg = (g.N + 63) / 64;
-  hipError_t e = hipMemsetAsync(b.grb, 0, nwg * 8, st);
-  if (e != hipSuccess) return e;
+  // grb is 256-B aligned (sx_carve) and padded to 16 B
+  zero_kernel<<<grid_for((nwg + 1) / 2, 256, 2048), 256, 0, st>>>((uint4*)b.grb, (nwg + 1) / 2);
+  hipError_t e;
   if (stride) setbits_kernel<<<grid_for(stride * g.G, 256, 4096), 256, 0, st>>>(recv, stride, g.G, b.cbase, b.grb);
   gcount_kernel<<<grid_for(nwg + 1, 256, 1u << 30), 256, 0, st>>>(b.grb, nwg, b.gcnt);
   size_t tb = b.tmp_bytes;

@@ -18,14 +18,17 @@ CASES = [("pushpull", 2, 64, 1 << 20, 0x5EED0004, 4), ("push", 3, 1, 300001, 7, 
          ("pull", 1, 5, 100000, 11, 2), ("pushpull", 6, 7, 50001, 3, 2)]
 IDS = ["pushpull-1M-G4", "push-ragged-G3", "pull-G2", "pushpull-k6-G2"]
 PLANS = {"auto": {}, "sparse": {"GOSSIP_SPARSE_FRAC": "1.0"}, "sparse_alld": {"GOSSIP_SPARSE_FRAC": "1.0",
-         "GOSSIP_ALLD_FRAC": "0"}, "dense": {"GOSSIP_SPARSE_FRAC": "-1"}}
+         "GOSSIP_ALLD_FRAC": "0"}, "dense": {"GOSSIP_SPARSE_FRAC": "-1"},
+         # dense sharded rounds on the direct kernels instead of the binned push/pull passes
+         "dense_direct": {"GOSSIP_SPARSE_FRAC": "-1", "GOSSIP_SB": "0"}, "auto_direct": {"GOSSIP_SB": "0"}}
+_ENV = ("GOSSIP_SPARSE_FRAC", "GOSSIP_ALLD_FRAC", "GOSSIP_SB")
 
 
 @pytest.mark.parametrize("plan", list(PLANS))
 @pytest.mark.parametrize("case", CASES, ids=IDS)
 def test_lockstep_shards_equal_one_engine(case, plan, monkeypatch):
     mode, k, R, N, seed, G = case
-    for var in ("GOSSIP_SPARSE_FRAC", "GOSSIP_ALLD_FRAC"):
+    for var in _ENV:
         monkeypatch.delenv(var, raising=False)
     ref = Engine(N, R, mode, k, seed, flags=1)
     ref.inject_random()
@@ -43,7 +46,7 @@ def test_lockstep_shards_equal_one_engine(case, plan, monkeypatch):
         assert np.array_equal(e.read_shard(), full[:, e.lo:e.hi])
     if plan in ("sparse", "sparse_alld"):
         assert set(kinds) == {1}
-    elif plan == "dense":
+    elif plan in ("dense", "dense_direct"):
         assert set(kinds) == {0}
     for e in engines:
         e.close()
@@ -65,3 +68,26 @@ def test_lockstep_inject_between_steps():
     full = ref.read_shard()
     for e in engines:
         assert np.array_equal(e.read_shard(), full[:, e.lo:e.hi])
+
+
+def test_lockstep_dense_past_4096_tiles(monkeypatch):
+    """Above 2^26 nodes the pull pass of a dense sharded round bins into more than 4096
+    image tiles (binned.h: kSbMaxTiles); odd shard size, so every slice but the first
+    starts 8-B aligned.  Reference: one engine (direct kernels at this size)."""
+    for var in _ENV:
+        monkeypatch.delenv(var, raising=False)
+    N, R, G = (1 << 26) + 12345, 64, 2
+    ref = Engine(N, R, "pushpull", 2, 0x5EED0004, flags=1)
+    ref.inject_random()
+    want = ref.step(8)
+    full = ref.read_shard()
+    ref.close()
+    monkeypatch.setenv("GOSSIP_SPARSE_FRAC", "-1")
+    engines = [Engine(N, R, "pushpull", 2, 0x5EED0004, flags=1, shard_rank=r, shard_count=G) for r in range(G)]
+    for e in engines:
+        e.inject_random()
+    got, kinds = run_lockstep(engines, 8)
+    assert got == want.stats and set(kinds) == {0}
+    for e in engines:
+        assert np.array_equal(e.read_shard(), full[:, e.lo:e.hi])
+        e.close()
