@@ -942,8 +942,11 @@ int gossip_reset(gossip_engine_t* e) {
     HIP_OK(e, hipMemsetAsync(e->skip, 0, shard, e->stream));
     HIP_OK(e, hipMemsetAsync(e->imgF, 0, shard * e->G, e->stream));
   } else {
-    HIP_OK(e, hipMemsetAsync(e->img[0], 0, shard * e->G, e->stream));
-    HIP_OK(e, hipMemsetAsync(e->img[1], 0, shard * e->G, e->stream));
+    // own slices only: every other slice of an image is written by the all-gather
+    // before a round reads it, and a round writes the whole own slice of S_{t+1};
+    // binned single-shard rounds run in place on S and never read the other image
+    HIP_OK(e, hipMemsetAsync(e->S, 0, shard, e->stream));
+    if (!e->binned) HIP_OK(e, hipMemsetAsync(e->Snext, 0, shard, e->stream));
   }
   e->fr_valid = false;
   e->sx_valid = e->gtot_valid = e->last_sparse = false;
