@@ -190,9 +190,10 @@ def main():
                                     "bin_emit+transpose_u16+bin_serve+bin_apply, + round_snapshot; hipEvents around "
                                     "each step, gaps between rounds included" if world == 1 else
                                     "sharded rounds, hipEvent-timed device work of the hot kernel per round (timer 0): "
-                                    "dense = seed copy + round_random_kernel after the state all-gather, sparse = "
-                                    "rare index + sharded scan between the rare-list all-gather and the push "
-                                    "all-to-all (DESIGN.md §5); collectives not included"),
+                                    "dense = binned push pass (every sender -> own tiles) + pull pass (own senders "
+                                    "-> image tiles) + serve + apply after the state all-gather, sparse = rare index "
+                                    "+ sharded scan between the rare-list all-gather and the push all-to-all "
+                                    "(DESIGN.md §5); collectives not included"),
                          "bytes_per_node_round": bpn, "avg_launch_us": avg_launch_s * 1e6,
                          "rounds_timed": round_launches},
         }
