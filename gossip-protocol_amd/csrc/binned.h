@@ -28,9 +28,21 @@ constexpr uint32_t kSbMaxTiles = 8192;
 // ids), edges whose peer lies in [dst0, dst0 + dstn), directions in dmask
 // (bit 0 push, bit 1 pull); wvals = 0: the records carry no sender value
 // (the pull pass).
+// Indices [lo, lo + n) with [skip0, skip1) spliced out: at(i) = lo + i, moved
+// past the hole.  A launch over part of the regions or tiles.
+struct IdxRange {
+  uint32_t lo, n, skip0, skip1;
+  __host__ __device__ uint32_t at(uint32_t i) const {
+    const uint32_t x = lo + i;
+    return x >= skip0 ? x + (skip1 - skip0) : x;
+  }
+  static IdxRange all(uint32_t n) { return IdxRange{0u, n, 0u, 0u}; }
+};
+
 struct EmitRange {
   uint64_t snd0, nsnd, dst0, dstn;
   uint32_t dmask, wvals;
+  IdxRange rs;  // sender regions of this launch
 };
 
 struct BinGeom {
@@ -85,6 +97,14 @@ size_t sb_bytes(const SbGeom& g);
 void sb_carve(const SbGeom& g, void* base, SbBufs* b);
 // image: the gathered S_t (global ids); Snext: the own slice of S_{t+1};
 // nzb/fullb: bitmaps over the own nodes; partial must be zero on entry.
+// launch_sb_round = launch_sb_pre (reads only the own slice of the image: the
+// pull pass, the push pass over the own senders, serving the own tiles — it may
+// run while the all-gather fills the other slices) + launch_sb_post (the rest).
+hipError_t launch_sb_pre(const SbGeom& g, const SbBufs& b, const uint64_t* image, uint32_t R, uint32_t t,
+                         uint32_t key0, uint32_t key1, uint32_t mode, const Faults& fa, hipStream_t st);
+hipError_t launch_sb_post(const SbGeom& g, const SbBufs& b, const uint64_t* image, uint64_t* Snext,
+                          uint64_t* partial, uint32_t R, uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode,
+                          const Faults& fa, uint32_t flags, uint64_t* nzb, uint64_t* fullb, hipStream_t st);
 hipError_t launch_sb_round(const SbGeom& g, const SbBufs& b, const uint64_t* image, uint64_t* Snext,
                            uint64_t* partial, uint32_t R, uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode,
                            const Faults& fa, uint32_t flags, uint64_t* nzb, uint64_t* fullb, hipStream_t st);

@@ -121,8 +121,14 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
     }
   };
   uint64_t v[kQ], vn[kQ];
-  if (blockIdx.x < g.nt_s) load_values(blockIdx.x, v);
-  for (uint32_t s = blockIdx.x; s < g.nt_s; s += gridDim.x) {
+  // regions r = blockIdx.x, +gridDim.x, ... of the launch; V != 0 launches may
+  // cover a subrange of the regions (er.rs: the part of a dense sharded round
+  // that overlaps the all-gather, or the rest)
+  const uint32_t nr = SHARD ? er.rs.n : g.nt_s;
+  auto region = [&](uint32_t r) -> uint32_t { return SHARD ? er.rs.at(r) : r; };
+  if (blockIdx.x < nr) load_values(region(blockIdx.x), v);
+  for (uint32_t r = blockIdx.x; r < nr; r += gridDim.x) {
+  const uint32_t s = region(r);
   const uint64_t base = (uint64_t)s << g.ts_log;
   const uint32_t nsend = (uint32_t)min<uint64_t>(g.ts, nsnd - base);
   __syncthreads();  // the previous region's write-out has read cur/st_ids/sval
@@ -133,7 +139,7 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
     const uint32_t i = tid + q * kEmitThreads;
     if (V != 2 && i < g.ts) sval[i] = v[q];
   }
-  if (s + gridDim.x < g.nt_s) load_values(s + gridDim.x, vn);
+  if (r + gridDim.x < nr) load_values(region(r + gridDim.x), vn);
   __syncthreads();
   // pass A: per-destination-tile counts of the records (edges that carry something)
   uint32_t pr[KREG > 0 ? kQ * KREG : 1];
@@ -491,11 +497,11 @@ __device__ __forceinline__ void load_tile(unsigned long long* img, const uint64_
 // every record aimed at T from a sender that is not yet fully informed gets
 // its pull response S_t[p] written next to it when nonzero (every one, in dense rounds).
 __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, const uint64_t* __restrict__ S, BinBufs b,
-                                                                  uint32_t R) {
+                                                                  uint32_t R, IdxRange tr) {
   __shared__ unsigned long long img[kTileD];
   __shared__ uint64_t wmask[(kTileThreads / 64) * kUnrollServe];
   __shared__ int32_t wlist[(kTileThreads / 64) * 64];
-  const uint32_t T = xcd_remap(blockIdx.x, g.nt_d);
+  const uint32_t T = tr.at(xcd_remap(blockIdx.x, gridDim.x));  // tiles of this launch (all of them on one shard)
   const uint64_t node0 = (uint64_t)T << kTileDLog;
   load_tile(img, S, node0, g.N);
   __syncthreads();
@@ -656,7 +662,7 @@ hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, 
 #undef GOSSIP_EMIT
   const dim3 tg((g.nt_d + 1 + 31) / 32, (g.nt_s + 31) / 32);
   transpose_u16_kernel<<<tg, dim3(32, 8), 0, st>>>(b.off, b.offT, g.nt_s, g.nt_d + 1, partial, rs.plen);
-  if (mode == 2 || mode == 3) bin_serve_kernel<<<g.nt_d, kTileThreads, 0, st>>>(g, S, b, R);
+  if (mode == 2 || mode == 3) bin_serve_kernel<<<g.nt_d, kTileThreads, 0, st>>>(g, S, b, R, IdxRange::all(g.nt_d));
   // in place: K3 of tile X reads and writes only S[X] (push values and pull
   // responses come from the record buffers), and K1/K2 have finished reading S_t
   bin_apply_kernel<<<g.nt_d, kTileThreads, 0, st>>>(g, b, g, b, S, S, g.N, 0, partial, R, mode, flags);
@@ -692,12 +698,24 @@ void sb_carve(const SbGeom& g, void* base, SbBufs* b) {
   b->p.nzb = b->p.fullb = b->q.nzb = b->q.fullb = nullptr;
 }
 
-hipError_t launch_sb_round(const SbGeom& g, const SbBufs& b, const uint64_t* image, uint64_t* Snext,
-                           uint64_t* partial, uint32_t R, uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode,
-                           const Faults& fa, uint32_t flags, uint64_t* nzb, uint64_t* fullb, hipStream_t st) {
-  const bool push = mode == 1 || mode == 3, pull = mode == 2 || mode == 3;
-  auto emit = [&](const BinGeom& gg, const BinBufs& bb, const EmitRange& er, bool vals) {
-    const uint32_t eg = gg.nt_s < kEmitGrid ? gg.nt_s : kEmitGrid;
+namespace {
+// the P regions and image tiles that lie inside the own slice: they need no
+// remote data, so they run while the all-gather is in flight
+IdxRange own_regions(const SbGeom& g) {
+  const uint64_t a = (g.lo + g.p.ts - 1) / g.p.ts, b = (g.lo + g.nown) / g.p.ts;
+  return b > a ? IdxRange{(uint32_t)a, (uint32_t)(b - a), 0u, 0u} : IdxRange{0u, 0u, 0u, 0u};
+}
+IdxRange own_tiles(const SbGeom& g) {
+  const uint64_t a = (g.lo + kTileD - 1) / kTileD, b = (g.lo + g.nown) / kTileD;
+  return b > a ? IdxRange{(uint32_t)a, (uint32_t)(b - a), 0u, 0u} : IdxRange{0u, 0u, 0u, 0u};
+}
+// every index of [0, n) outside x
+IdxRange rest_of(uint32_t n, const IdxRange& x) { return IdxRange{0u, n - x.n, x.lo, x.lo + x.n}; }
+
+void sb_emit(const BinGeom& gg, const BinBufs& bb, const uint64_t* image, uint32_t R, uint32_t t, uint32_t key0,
+             uint32_t key1, uint32_t mode, const Faults& fa, const EmitRange& er, bool vals, hipStream_t st) {
+  if (er.rs.n == 0) return;
+  const uint32_t eg = er.rs.n < kEmitGrid ? er.rs.n : kEmitGrid;
 #define GOSSIP_EMIT(KR, F, VV) \
   bin_emit_kernel<KR, F, VV><<<eg, kEmitThreads, 0, st>>>(gg, image, bb, R, t, key0, key1, mode, 0u, fa, er)
 #define GOSSIP_EMIT_V(VV)                                                 \
@@ -706,20 +724,51 @@ hipError_t launch_sb_round(const SbGeom& g, const SbBufs& b, const uint64_t* ima
   } else {                                                                \
     if (fa.any()) GOSSIP_EMIT(0, true, VV); else GOSSIP_EMIT(0, false, VV); \
   }
-    if (vals) {
-      GOSSIP_EMIT_V(1)
-    } else {
-      GOSSIP_EMIT_V(2)
-    }
+  if (vals) {
+    GOSSIP_EMIT_V(1)
+  } else {
+    GOSSIP_EMIT_V(2)
+  }
 #undef GOSSIP_EMIT_V
 #undef GOSSIP_EMIT
-    const dim3 tg((gg.nt_d + 1 + 31) / 32, (gg.nt_s + 31) / 32);
-    transpose_u16_kernel<<<tg, dim3(32, 8), 0, st>>>(bb.off, bb.offT, gg.nt_s, gg.nt_d + 1, partial, 0u);
-  };
-  if (push) emit(g.p, b.p, EmitRange{0, g.p.N, g.lo, g.nown, 1u, 1u}, true);
+}
+
+void sb_transpose(const BinGeom& gg, const BinBufs& bb, uint64_t* partial, hipStream_t st) {
+  const dim3 tg((gg.nt_d + 1 + 31) / 32, (gg.nt_s + 31) / 32);
+  transpose_u16_kernel<<<tg, dim3(32, 8), 0, st>>>(bb.off, bb.offT, gg.nt_s, gg.nt_d + 1, partial, 0u);
+}
+
+EmitRange push_range(const SbGeom& g, const IdxRange& rs) { return EmitRange{0, g.p.N, g.lo, g.nown, 1u, 1u, rs}; }
+EmitRange pull_range(const SbGeom& g) {
+  return EmitRange{g.lo, g.nown, 0, g.q.N, 2u, 0u, IdxRange::all(g.q.nt_s)};
+}
+}  // namespace
+
+hipError_t launch_sb_pre(const SbGeom& g, const SbBufs& b, const uint64_t* image, uint32_t R, uint32_t t,
+                         uint32_t key0, uint32_t key1, uint32_t mode, const Faults& fa, hipStream_t st) {
+  const bool push = mode == 1 || mode == 3, pull = mode == 2 || mode == 3;
   if (pull) {
-    emit(g.q, b.q, EmitRange{g.lo, g.nown, 0, g.q.N, 2u, 0u}, false);
-    bin_serve_kernel<<<g.q.nt_d, kTileThreads, 0, st>>>(g.q, image, b.q, R);
+    sb_emit(g.q, b.q, image, R, t, key0, key1, mode, fa, pull_range(g), false, st);
+    sb_transpose(g.q, b.q, nullptr, st);
+    const IdxRange ot = own_tiles(g);
+    if (ot.n) bin_serve_kernel<<<ot.n, kTileThreads, 0, st>>>(g.q, image, b.q, R, ot);
+  }
+  if (push) sb_emit(g.p, b.p, image, R, t, key0, key1, mode, fa, push_range(g, own_regions(g)), true, st);
+  return hipGetLastError();
+}
+
+hipError_t launch_sb_post(const SbGeom& g, const SbBufs& b, const uint64_t* image, uint64_t* Snext,
+                          uint64_t* partial, uint32_t R, uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode,
+                          const Faults& fa, uint32_t flags, uint64_t* nzb, uint64_t* fullb, hipStream_t st) {
+  const bool push = mode == 1 || mode == 3, pull = mode == 2 || mode == 3;
+  if (push) {
+    sb_emit(g.p, b.p, image, R, t, key0, key1, mode, fa, push_range(g, rest_of(g.p.nt_s, own_regions(g))), true,
+            st);
+    sb_transpose(g.p, b.p, nullptr, st);
+  }
+  if (pull) {
+    const IdxRange rt = rest_of(g.q.nt_d, own_tiles(g));
+    if (rt.n) bin_serve_kernel<<<rt.n, kTileThreads, 0, st>>>(g.q, image, b.q, R, rt);
   }
   BinBufs bp = b.p;
   bp.nzb = nzb;
@@ -727,6 +776,14 @@ hipError_t launch_sb_round(const SbGeom& g, const SbBufs& b, const uint64_t* ima
   bin_apply_kernel<<<g.p.nt_d, kTileThreads, 0, st>>>(g.p, bp, g.q, b.q, image + g.lo, Snext, g.nown, g.lo, partial,
                                                       R, mode, flags);
   return hipGetLastError();
+}
+
+hipError_t launch_sb_round(const SbGeom& g, const SbBufs& b, const uint64_t* image, uint64_t* Snext,
+                           uint64_t* partial, uint32_t R, uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode,
+                           const Faults& fa, uint32_t flags, uint64_t* nzb, uint64_t* fullb, hipStream_t st) {
+  const hipError_t e = launch_sb_pre(g, b, image, R, t, key0, key1, mode, fa, st);
+  if (e != hipSuccess) return e;
+  return launch_sb_post(g, b, image, Snext, partial, R, t, key0, key1, mode, fa, flags, nzb, fullb, st);
 }
 
 }  // namespace gossip

@@ -70,6 +70,7 @@ SIGNATURES = [
     ("partial_len", C.c_uint64, [P]),
     ("exchange_buffers", C.c_int, [P, C.POINTER(P), C.POINTER(P), U64P]),
     ("round_compute", C.c_int, [P, U64P]),
+    ("dense_prepare", C.c_int, [P]),
     ("round_commit", C.c_int, [P, U64P, C.POINTER(RoundStats)]),
     ("sharded_plan", C.c_int, [P, U64P, C.POINTER(C.c_int32)]),
     ("local_totals", C.c_int, [P, U64P]),

@@ -216,6 +216,11 @@ class AbiEngine:
         self._check(self._fn("exchange_buffers")(self._h, C.byref(send), C.byref(recv), C.byref(nbytes)))
         return send.value, recv.value, nbytes.value
 
+    def dense_prepare(self):
+        """Enqueues the own-slice part of a dense sharded round (no-op where the engine has none)."""
+        if self.supports("dense_prepare"):
+            self._check(self._fn("dense_prepare")(self._h))
+
     def round_compute(self) -> np.ndarray:
         out = np.zeros(self.partial_len(), dtype=np.uint64)
         self._check(self._fn("round_compute")(self._h, out.ctypes.data_as(_abi.U64P)))

@@ -73,6 +73,14 @@ class _Comm:
         recv.copy_(host)
         self._sync()
 
+    def all_gather_async(self, recv: torch.Tensor, send: torch.Tensor):
+        """Device collectives: returns the pending work (the caller's stream waits on wait());
+        staged collectives complete before returning None."""
+        if self.direct:
+            return dist.all_gather_into_tensor(recv, send, group=self.group, async_op=True)
+        self.all_gather(recv, send)
+        return None
+
     def all_to_all(self, recv: torch.Tensor, send: torch.Tensor, recv_splits, send_splits):
         if self.direct:
             dist.all_to_all_single(recv, send, output_split_sizes=recv_splits, input_split_sizes=send_splits,
@@ -119,8 +127,12 @@ def _dense_round(engine, comm: _Comm) -> np.ndarray:
     if comm.world > 1:
         recv = _as_tensor(recv_p, nbytes * comm.world, engine.on_device)
         send = _as_tensor(send_p, nbytes, engine.on_device)
-        # RCCL all-gather in place: the send slice lies inside the image
-        comm.all_gather(recv, send)
+        # RCCL all-gather in place (the send slice lies inside the image), in flight
+        # while the engine runs the part of the round that reads only its own slice
+        work = comm.all_gather_async(recv, send)
+        engine.dense_prepare()
+        if work is not None:
+            work.wait()
     return engine.round_compute()
 
 
@@ -184,6 +196,8 @@ def _lockstep_sum(parts):
 def _lockstep_dense(engines):
     G = len(engines)
     bufs = [e.exchange_buffers() for e in engines]
+    for e in engines:  # on the engines' streams, concurrent with the copies below (disjoint slices)
+        e.dense_prepare()
     for e, (_, recv_p, nbytes) in zip(engines, bufs):
         recv = _as_tensor(recv_p, nbytes * G, True, e.device)
         for q, (send_q, _, _) in enumerate(bufs):

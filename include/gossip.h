@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define GOSSIP_ABI_VERSION 2u
+#define GOSSIP_ABI_VERSION 3u
 
 /* Dissemination modes. */
 enum gossip_mode {
@@ -150,6 +150,13 @@ int gossip_step(gossip_engine_t* eng, uint32_t max_rounds, gossip_round_stats_t*
 uint64_t gossip_partial_len(const gossip_engine_t* eng);
 int gossip_exchange_buffers(gossip_engine_t* eng, void** send, void** recv, uint64_t* send_bytes);
 int gossip_round_compute(gossip_engine_t* eng, uint64_t* partial);
+/* Optional, dense sharded rounds (after gossip_exchange_buffers, while the
+ * all-gather is in flight on another stream): enqueues on the engine's stream
+ * the part of the round that reads only the own slice of the image (the pull
+ * pass, the push pass over the own senders, serving the own tiles);
+ * gossip_round_compute then enqueues the rest.  Returns 0 and does nothing on
+ * engines without that path. */
+int gossip_dense_prepare(gossip_engine_t* eng);
 int gossip_round_commit(gossip_engine_t* eng, const uint64_t* total, gossip_round_stats_t* stats);
 
 /* --- sparse sharded rounds (random modes, W == 1, G > 1) ------

@@ -12,7 +12,8 @@ from gossip_hip import sharded as sh
 
 G = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 LG = int(sys.argv[2]) if len(sys.argv) > 2 else 24
-CALLS = ("sparse_rare", "sparse_scan", "sparse_commit", "round_compute", "exchange_buffers", "local_totals")
+CALLS = ("sparse_rare", "sparse_scan", "sparse_commit", "dense_prepare", "round_compute", "exchange_buffers",
+         "local_totals")
 
 
 class Timed:
