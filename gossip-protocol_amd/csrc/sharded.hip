@@ -39,17 +39,29 @@ __global__ __launch_bounds__(256) void wcount_kernel(FrontierBufs f, uint64_t no
   else if (w == nw) wcount[w] = 0;
 }
 
+// One wave per 64 bitmap words: lane i loads word i, the wave then visits only
+// the nonzero words (lane b writes node b of the word), so empty stretches of
+// the bitmap cost one load per 64 words.
 __global__ __launch_bounds__(256) void list_kernel(FrontierBufs f, const uint64_t* __restrict__ S, uint64_t nown,
                                                     uint64_t lo, uint32_t maj, const uint32_t* __restrict__ wpos,
                                                     SxItem* __restrict__ out) {
-  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= nown) return;
-  const uint64_t w = i >> 6;
-  const uint64_t x = own_rare(f, w, nown, maj);  // one word per 64 lanes
-  const uint32_t b = (uint32_t)(i & 63);
-  if (!((x >> b) & 1ull)) return;
-  const uint32_t pos = wpos[w] + (uint32_t)__popcll(x & ((1ull << b) - 1ull));
-  out[pos] = SxItem{lo + i, S[i]};
+  const uint64_t nw = (nown + 63) >> 6;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t w0 = ((uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u));  // this wave's first word
+  const uint64_t wl = w0 + lane;
+  const uint64_t x = wl < nw ? own_rare(f, wl, nown, maj) : 0ull;
+  const uint32_t pl = wl < nw ? wpos[wl] : 0u;
+  uint64_t nzw = __ballot(x != 0);
+  while (nzw) {
+    const uint32_t src = (uint32_t)__builtin_ctzll(nzw);
+    nzw &= nzw - 1;
+    const uint64_t xw = __shfl(x, src, 64);
+    const uint32_t pos0 = __shfl(pl, src, 64);
+    if ((xw >> lane) & 1ull) {
+      const uint64_t i = ((w0 + src) << 6) + lane;
+      out[pos0 + (uint32_t)__popcll(xw & ((1ull << lane) - 1ull))] = SxItem{lo + i, S[i]};
+    }
+  }
 }
 
 // Lists are in id order (and shards in rank order), so the items of one bitmap
@@ -443,7 +455,7 @@ hipError_t sx_compact(const SxGeom& g, const SxBufs& b, const FrontierBufs& lf, 
   size_t tb = b.tmp_bytes;
   hipError_t e = hipcub::DeviceScan::ExclusiveSum(b.tmp, tb, b.wcount, b.wpos, (int)(nwl + 1), st);
   if (e != hipSuccess) return e;
-  list_kernel<<<grid_for(g.nown, 256, 1u << 30), 256, 0, st>>>(lf, S, g.nown, g.lo, maj, b.wpos, b.rare_send);
+  list_kernel<<<grid_for(nwl, 256, 1u << 30), 256, 0, st>>>(lf, S, g.nown, g.lo, maj, b.wpos, b.rare_send);
   return hipGetLastError();
 }
 
