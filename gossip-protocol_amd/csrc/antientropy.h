@@ -28,7 +28,21 @@ struct AeArgs {
   void* pmask;       // dense rounds: [N][k] push masks (components where V[n] > V[p_j]), L bits each
   uint32_t nseg, spc, segcap;
   uint32_t epoch;
+  // binned sparse scan: the exchanges of every alive sender,
+  // counting-sorted by the peer's tile (2^btl nodes) per region of 2^brs senders;
+  // one block per tile then reads the tile's alive / stale bits from LDS and
+  // lists the edges into segment = tile (nseg == bnt)
+  uint64_t* brec;    // [bnreg][2^brs * k] records: n | p_local << 32 | stale(n) << 51
+  uint16_t* boff;    // [bnreg][bnt + 1] run starts inside each region
+  uint32_t btl, bnt, brs, bnreg;
+  uint32_t spb;      // blocks per segment in the gather / apply / fix kernels
 };
+
+// binned sparse-scan geometry for N nodes, k exchanges per node
+struct AeBinGeom {
+  uint32_t tl, nt, rs, nreg;
+};
+AeBinGeom ae_bin_geom(uint64_t N, uint32_t k);
 
 uint32_t ae_lanes(uint32_t K);
 hipError_t launch_ae_init(uint32_t* V, uint32_t* target, uint64_t N, uint32_t K, uint32_t k0, uint32_t k1,
@@ -44,6 +58,9 @@ hipError_t launch_ae_stats(const AeArgs& a, const uint32_t* V, uint64_t* ab, boo
 // sparse round (after the churn): scan (edges touching a stale node), gather, apply in
 // place, fix-up (stale bits, hash delta into partial[3]), then stats from the bitmaps
 hipError_t launch_ae_sparse(const AeArgs& a, hipStream_t st);
+// the same round with the binned scan (a.brec set, a.nseg == a.bnt); its first
+// pass also does the churn (no launch_ae_churn before it)
+hipError_t launch_ae_sparse_binned(const AeArgs& a, hipStream_t st);
 hipError_t launch_ae_sparse_stats(const AeArgs& a, hipStream_t st);
 
 }  // namespace gossip

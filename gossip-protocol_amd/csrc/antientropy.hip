@@ -350,10 +350,210 @@ __global__ __launch_bounds__(kAeBlock) void ae_sparse_scan_kernel(AeArgs a) {
   block_add(msgs, red, &a.partial[2]);
 }
 
-// edges of this block's segment, or 0 when any segment overflowed (the host reruns the round dense)
-__device__ __forceinline__ uint32_t segment_edges(const AeArgs& a) {
-  return a.aux[1] > a.segcap ? 0u : a.segn[blockIdx.x];
+// Binned scan, pass 1 (one block per region of 2^brs senders, persistent): the
+// round's churn (ab -> abn), then every alive sender's exchanges counting-sorted
+// by the peer's tile in LDS and
+// written out as one contiguous region; the random reads of the peers' alive /
+// stale bits move to pass 2, where each tile's bits sit in LDS.
+constexpr int kAeBinThreads = 1024;
+constexpr uint32_t kAeBinRec = 16384;    // records per region (LDS)
+constexpr uint32_t kAeBinTiles = 4096;
+constexpr uint32_t kAeBinQ = kAeBinRec / kAeBinThreads;  // k == 1: senders per thread, peers in registers
+
+template <bool K1>
+__global__ __launch_bounds__(kAeBinThreads) void ae_bin_emit_kernel(AeArgs a) {
+  __shared__ uint32_t cur[kAeBinTiles];
+  __shared__ uint64_t st[kAeBinRec];
+  __shared__ uint32_t wsum[kAeBinThreads / 64];
+  __shared__ uint32_t wpre[kAeBinThreads / 64 + 1];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t rs = 1u << a.brs, rp = rs * a.k, nt = a.bnt;
+  const uint64_t tmask = (1ull << a.btl) - 1ull;
+  for (uint32_t s = blockIdx.x; s < a.bnreg; s += gridDim.x) {
+    const uint64_t base = (uint64_t)s << a.brs;
+    __syncthreads();  // the previous region's write-out has read st / cur
+    for (uint32_t d = tid; d < nt; d += kAeBinThreads) cur[d] = 0;
+    __syncthreads();
+    // pass A: tile counts (k == 1: the peer and the stale bit stay in registers)
+    uint32_t pr[K1 ? kAeBinQ : 1];
+    uint32_t live = 0, stl = 0;
+    const uint32_t nq = K1 ? kAeBinQ : rs / kAeBinThreads;  // rs is a multiple of the block (>= 1024 senders)
+#pragma unroll
+    for (uint32_t q = 0; q < nq; ++q) {
+      // the round's churn (ae_churn_kernel's work, fused): a wave holds one 64-node chunk
+      const uint64_t n = base + q * kAeBinThreads + tid;
+      const uint64_t ch = n >> 6;
+      const bool in = n < a.N;
+      const uint64_t aw = in ? a.ab[2 * ch] : 0ull, sw = in ? a.ab[2 * ch + 1] : 0ull;
+      const bool al = in && churned((aw >> lane) & 1ull, (uint32_t)n, a.t, a.key0, a.key1, a.fail, a.rec);
+      const uint64_t nb = __ballot(al);
+      if (in && lane == 0) a.abn[2 * ch] = nb;
+      if (in && lane == 1) a.abn[2 * ch + 1] = sw;  // stale bits of S_t carried
+      if (!al) continue;
+      live |= 1u << q;
+      stl |= (uint32_t)((sw >> lane) & 1ull) << q;
+      u32x4 x{0, 0, 0, 0};
+      for (uint32_t j = 0; j < a.k; ++j) {
+        const uint32_t p = peer_j(a, (uint32_t)n, j, x);
+        if (K1) pr[q] = p;
+        atomicAdd(&cur[p >> a.btl], 1u);
+      }
+    }
+    __syncthreads();
+    // exclusive scan of cur[0, nt)
+    const uint32_t per = (nt + kAeBinThreads - 1) / kAeBinThreads;
+    const uint32_t lo = min(tid * per, nt), hi = min(lo + per, nt);
+    uint32_t mine = 0;
+    for (uint32_t d = lo; d < hi; ++d) mine += cur[d];
+    uint32_t inc = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o, 64);
+      if (lane >= (uint32_t)o) inc += y;
+    }
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t acc = 0;
+      for (int w = 0; w < kAeBinThreads / 64; ++w) {
+        wpre[w] = acc;
+        acc += wsum[w];
+      }
+      wpre[kAeBinThreads / 64] = acc;
+    }
+    __syncthreads();
+    uint32_t run = wpre[wave] + inc - mine;
+    uint16_t* off = a.boff + (size_t)s * (nt + 1);
+    for (uint32_t d = lo; d < hi; ++d) {
+      const uint32_t c = cur[d];
+      cur[d] = run;
+      off[d] = (uint16_t)run;
+      run += c;
+    }
+    const uint32_t total = wpre[kAeBinThreads / 64];
+    if (tid == 0) off[nt] = (uint16_t)total;
+    __syncthreads();
+    // pass B: records to their slots
+#pragma unroll
+    for (uint32_t q = 0; q < nq; ++q) {
+      if (!((live >> q) & 1u)) continue;
+      const uint64_t n = base + q * kAeBinThreads + tid;
+      const uint64_t sb = (uint64_t)((stl >> q) & 1u) << 51;
+      if (K1) {
+        const uint32_t p = pr[q];
+        st[atomicAdd(&cur[p >> a.btl], 1u)] = n | ((uint64_t)(p & tmask) << 32) | sb;
+      } else {
+        u32x4 x{0, 0, 0, 0};
+        for (uint32_t j = 0; j < a.k; ++j) {
+          const uint32_t p = peer_j(a, (uint32_t)n, j, x);
+          st[atomicAdd(&cur[p >> a.btl], 1u)] = n | ((uint64_t)(p & tmask) << 32) | sb;
+        }
+      }
+    }
+    __syncthreads();
+    uint64_t* out = a.brec + (size_t)s * rp;
+    for (uint32_t e = tid; e < total; e += kAeBinThreads) out[e] = st[e];
+  }
 }
+
+// Binned scan, pass 2 (one block per tile T): the tile's alive and stale bits in
+// LDS; every record aimed at T (its run in each region, walked 64 runs per wave,
+// lane-strided) counts a message when the peer is alive and lists the exchange
+// into segment T when either end is stale.
+constexpr uint32_t kAeBinTileWords = 8192;  // tiles of up to 2^19 nodes
+
+__global__ __launch_bounds__(kAeBinThreads) void ae_bin_scan_kernel(AeArgs a) {
+  __shared__ uint64_t wa[kAeBinTileWords], ws[kAeBinTileWords];
+  __shared__ uint32_t scnt;
+  __shared__ uint64_t red[kAeBinThreads / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t T = blockIdx.x, nt = a.bnt;
+  const uint32_t tw = 1u << (a.btl - 6);  // words per tile
+  const uint64_t w0 = (uint64_t)T * tw, nw = (a.N + 63) / 64;
+  if (tid == 0) scnt = 0;
+  for (uint32_t w = tid; w < tw; w += kAeBinThreads) {
+    const bool in = w0 + w < nw;
+    wa[w] = in ? a.abn[2 * (w0 + w)] : 0ull;
+    ws[w] = in ? a.abn[2 * (w0 + w) + 1] : 0ull;
+  }
+  __syncthreads();
+  uint32_t* eid = a.eid + (size_t)T * a.segcap * 2;
+  const uint32_t rp = (1u << a.brs) * a.k;
+  const uint64_t below = (1ull << lane) - 1ull;
+  const uint32_t tmask = (1u << a.btl) - 1u;
+  uint64_t msgs = 0;
+  for (uint32_t r0 = wave * 64; r0 < a.bnreg; r0 += (kAeBinThreads / 64) * 64) {
+    const uint32_t r = r0 + lane;
+    uint32_t be = 0, en = 0;
+    if (r < a.bnreg) {
+      const uint16_t* o = a.boff + (size_t)r * (nt + 1) + T;
+      be = o[0];
+      en = o[1];
+    }
+    const uint32_t len = en - be;
+    uint32_t inc = len;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o, 64);
+      if (lane >= (uint32_t)o) inc += y;
+    }
+    const uint32_t exc = inc - len, total = __shfl(inc, 63, 64);
+    const uint64_t rbase = (uint64_t)r * rp + be - exc;  // record of flat index f in this lane's run: rbase + f
+    constexpr int U = 4;
+    for (uint32_t f0 = 0; f0 < total; f0 += 64 * U) {
+      uint64_t rec[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t f = f0 + u * 64 + lane;
+        // owner run: the last lane whose run starts at or before f (a non-empty run)
+        uint32_t ow = 0;
+#pragma unroll
+        for (uint32_t step = 32; step; step >>= 1) {
+          const uint32_t c = ow + step;
+          if (c < 64 && (uint32_t)__shfl((int)exc, (int)c, 64) <= f) ow = c;
+        }
+        const uint64_t rb = (uint64_t)__shfl((long long)rbase, (int)ow, 64);
+        rec[u] = f < total ? a.brec[rb + f] : ~0ull;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool valid = rec[u] != ~0ull;
+        const uint32_t n = (uint32_t)rec[u];
+        const uint32_t pl = (uint32_t)(rec[u] >> 32) & tmask;
+        const bool ex = valid && ((wa[pl >> 6] >> (pl & 63)) & 1ull);  // n is alive (pass 1)
+        msgs += ex ? 1u : 0u;
+        const bool need = ex && (((rec[u] >> 51) & 1ull) || ((ws[pl >> 6] >> (pl & 63)) & 1ull));
+        const uint64_t m = __ballot(need);
+        if (!m) continue;
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&scnt, (uint32_t)__popcll(m));
+        base = (uint32_t)__shfl((int)base, 0, 64);
+        const uint32_t slot = base + (uint32_t)__popcll(m & below);
+        if (need && slot < a.segcap) {
+          eid[2 * slot] = n;
+          eid[2 * slot + 1] = (T << a.btl) | pl;
+        }
+      }
+    }
+  }
+  msgs = wave_sum64(msgs);
+  if (lane == 0) red[wave] = msgs;
+  __syncthreads();
+  if (tid == 0) {
+    uint64_t sm = 0;
+    for (int w = 0; w < kAeBinThreads / 64; ++w) sm += red[w];
+    if (sm) atomicAdd((unsigned long long*)&a.partial[2], (unsigned long long)sm);
+    a.segn[T] = scnt;
+    if (scnt) atomicMax((unsigned long long*)&a.aux[1], (unsigned long long)scnt);
+  }
+}
+
+// edges of this block's segment, or 0 when any segment overflowed (the host reruns the round dense)
+// (a.spb blocks share a segment: block = segment * spb + sub, edges sub, sub + spb, ... of each step)
+__device__ __forceinline__ uint32_t segment_edges(const AeArgs& a) {
+  return a.aux[1] > a.segcap ? 0u : a.segn[blockIdx.x / a.spb];
+}
+__device__ __forceinline__ size_t segment_base(const AeArgs& a) { return (size_t)(blockIdx.x / a.spb) * a.segcap; }
 
 // snapshot the S_t rows of both ends (before any in-place write)
 template <uint32_t L>
@@ -362,8 +562,8 @@ __global__ __launch_bounds__(kAeBlock) void ae_sparse_gather_kernel(AeArgs a) {
   const uint32_t c = threadIdx.x % L;
   const uint32_t m = segment_edges(a);
   if (c >= a.K) return;
-  const size_t s0 = (size_t)blockIdx.x * a.segcap;
-  for (uint32_t i = threadIdx.x / L; i < m; i += epb) {
+  const size_t s0 = segment_base(a);
+  for (uint32_t i = (blockIdx.x % a.spb) * epb + threadIdx.x / L; i < m; i += epb * a.spb) {
     const size_t e = s0 + i;
     const uint32_t n = a.eid[2 * e], p = a.eid[2 * e + 1];
     const uint32_t vn = a.V[(uint64_t)n * a.K + c], vp = a.V[(uint64_t)p * a.K + c];
@@ -379,8 +579,8 @@ __global__ __launch_bounds__(kAeBlock) void ae_sparse_apply_kernel(AeArgs a) {
   const uint32_t c = threadIdx.x % L;
   const uint32_t m = segment_edges(a);
   if (c >= a.K) return;
-  const size_t s0 = (size_t)blockIdx.x * a.segcap;
-  for (uint32_t i = threadIdx.x / L; i < m; i += epb) {
+  const size_t s0 = segment_base(a);
+  for (uint32_t i = (blockIdx.x % a.spb) * epb + threadIdx.x / L; i < m; i += epb * a.spb) {
     const size_t e = s0 + i;
     const uint32_t n = a.eid[2 * e], p = a.eid[2 * e + 1];
     const uint32_t on = a.erow[(2 * e) * a.K + c], op = a.erow[(2 * e + 1) * a.K + c];
@@ -399,10 +599,10 @@ __global__ __launch_bounds__(kAeBlock) void ae_sparse_fix_kernel(AeArgs a) {
   const uint32_t lane = threadIdx.x & 63, c = lane % L, lead = lane - c;
   const uint32_t m = segment_edges(a);
   const uint32_t tgt = c < a.K ? a.target[c] : 0u;
-  const size_t s0 = (size_t)blockIdx.x * a.segcap;
+  const size_t s0 = segment_base(a);
   uint64_t dh = 0;
   // the same trip count for every lane of the block, so the ballots see every lane
-  for (uint32_t b = 0; b < m; b += epb) {
+  for (uint32_t b = (blockIdx.x % a.spb) * epb; b < m; b += epb * a.spb) {
     const uint32_t i = b + threadIdx.x / L;
     const bool ve = i < m;
     const size_t e = s0 + i;
@@ -525,9 +725,37 @@ hipError_t launch_ae_stats(const AeArgs& a, const uint32_t* V, uint64_t* ab, boo
 
 hipError_t launch_ae_sparse(const AeArgs& a, hipStream_t st) {
   ae_sparse_scan_kernel<<<a.nseg, kAeBlock, 0, st>>>(a);
-  AE_LAUNCH_L(ae_sparse_gather_kernel, a.L, a.nseg, st, a);
-  AE_LAUNCH_L(ae_sparse_apply_kernel, a.L, a.nseg, st, a);
-  AE_LAUNCH_L(ae_sparse_fix_kernel, a.L, a.nseg, st, a);
+  AE_LAUNCH_L(ae_sparse_gather_kernel, a.L, a.nseg * a.spb, st, a);
+  AE_LAUNCH_L(ae_sparse_apply_kernel, a.L, a.nseg * a.spb, st, a);
+  AE_LAUNCH_L(ae_sparse_fix_kernel, a.L, a.nseg * a.spb, st, a);
+  return hipGetLastError();
+}
+
+AeBinGeom ae_bin_geom(uint64_t N, uint32_t k) {
+  AeBinGeom g{};
+  uint32_t lg = 0;
+  while ((1ull << lg) < N) ++lg;
+  g.tl = lg > 8 ? lg - 8 : 0;  // ~256 tiles, one block per CU
+  if (g.tl < 12) g.tl = 12;
+  if (g.tl > 19) g.tl = 19;    // LDS: 2 x 2^tl bits
+  g.nt = (uint32_t)((N + (1ull << g.tl) - 1) >> g.tl);
+  uint32_t rs = kAeBinRec;  // 2^brs senders * k records <= kAeBinRec, at least one block of senders
+  g.rs = 14;
+  while (g.rs > 10 && (rs >> (14 - g.rs)) * k > kAeBinRec) --g.rs;
+  g.nreg = (uint32_t)((N + (1ull << g.rs) - 1) >> g.rs);
+  return g;
+}
+
+hipError_t launch_ae_sparse_binned(const AeArgs& a, hipStream_t st) {
+  const uint32_t eg = a.bnreg < 256 ? a.bnreg : 256;
+  if (a.k == 1 && (1u << a.brs) == kAeBinRec)
+    ae_bin_emit_kernel<true><<<eg, kAeBinThreads, 0, st>>>(a);
+  else
+    ae_bin_emit_kernel<false><<<eg, kAeBinThreads, 0, st>>>(a);
+  ae_bin_scan_kernel<<<a.bnt, kAeBinThreads, 0, st>>>(a);
+  AE_LAUNCH_L(ae_sparse_gather_kernel, a.L, a.nseg * a.spb, st, a);
+  AE_LAUNCH_L(ae_sparse_apply_kernel, a.L, a.nseg * a.spb, st, a);
+  AE_LAUNCH_L(ae_sparse_fix_kernel, a.L, a.nseg * a.spb, st, a);
   return hipGetLastError();
 }
 

@@ -75,6 +75,10 @@ struct gossip_engine {
   uint32_t *ae_eid = nullptr, *ae_erow = nullptr, *ae_claim = nullptr, *ae_segn = nullptr;
   void* ae_pmask = nullptr;  // dense rounds: [N][k] push masks
   uint32_t ae_nseg = 1, ae_spc = 1, ae_segcap = 1;
+  bool ae_bin = false;  // binned sparse scan (AeArgs::brec)
+  AeBinGeom ae_bg{};
+  uint64_t* ae_brec = nullptr;
+  uint16_t* ae_boff = nullptr;
   uint64_t ae_cap = 0, ae_hash = 0, ae_stale = 0, ae_alive = 0, ae_full = 0;
   uint32_t ae_epoch = 0;
   int ae_force = -1;             // GOSSIP_AE_SPARSE: -1 auto, 0 never, 1 whenever the bitmap is valid
@@ -177,7 +181,8 @@ void free_all(gossip_engine* e) {
   for (void* b : sx)
     if (b) (void)hipFree(b);
   if (e->sx_host) (void)hipHostFree(e->sx_host);
-  void* ae[] = {e->V, e->Vn, e->target, e->alive, e->alive_n, e->ae_aux, e->ae_claim, e->ae_eid, e->ae_erow, e->ae_segn, e->ae_pmask};
+  void* ae[] = {e->V, e->Vn, e->target, e->alive, e->alive_n, e->ae_aux, e->ae_claim, e->ae_eid, e->ae_erow, e->ae_segn, e->ae_pmask,
+                e->ae_brec, e->ae_boff};
   for (void* b : ae)
     if (b) (void)hipFree(b);
   if (e->partial_h) (void)hipHostFree(e->partial_h);
@@ -310,6 +315,13 @@ AeArgs make_ae_args(gossip_engine* e) {
   a.nseg = e->ae_nseg;
   a.spc = e->ae_spc;
   a.segcap = e->ae_segcap;
+  a.brec = e->ae_brec;
+  a.boff = e->ae_boff;
+  a.btl = e->ae_bg.tl;
+  a.bnt = e->ae_bg.nt;
+  a.brs = e->ae_bg.rs;
+  a.bnreg = e->ae_bg.nreg;
+  a.spb = std::max<uint32_t>(1, 4096 / e->ae_nseg);  // ~4096 blocks over the edge list
   a.epoch = e->ae_epoch;
   return a;
 }
@@ -527,8 +539,12 @@ int ae_round(gossip_engine* e) {
     const AeArgs a = make_ae_args(e);
     HIP_OK(e, hipMemsetAsync(e->ae_aux, 0, 16, e->stream));
     if ((rc = timer_begin(e, 2))) return rc;
-    HIP_OK(e, launch_ae_churn(a, e->stream));
-    HIP_OK(e, launch_ae_sparse(a, e->stream));
+    if (e->ae_bin) {
+      HIP_OK(e, launch_ae_sparse_binned(a, e->stream));  // churn fused into its first pass
+    } else {
+      HIP_OK(e, launch_ae_churn(a, e->stream));
+      HIP_OK(e, launch_ae_sparse(a, e->stream));
+    }
     if ((rc = timer_end(e, 2))) return rc;
     if ((rc = timer_begin(e, 1))) return rc;
     HIP_OK(e, launch_ae_sparse_stats(a, e->stream));
@@ -776,15 +792,35 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
     const char* fcap = getenv("GOSSIP_AE_CAP");
     if (fcap) cap = std::max<uint64_t>(1, strtoull(fcap, nullptr, 10));
     if (const char* f = getenv("GOSSIP_AE_SPARSE")) e->ae_force = atoi(f);
-    e->ae_nseg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(4096, (nw + 3) / 4));
-    e->ae_spc = (uint32_t)((nw + e->ae_nseg - 1) / e->ae_nseg);
-    e->ae_nseg = (uint32_t)((nw + e->ae_spc - 1) / e->ae_spc);
-    e->ae_segcap = (cap >= kn && !fcap) ? e->k * e->ae_spc * 64 : (uint32_t)((cap + e->ae_nseg - 1) / e->ae_nseg);
-    e->ae_cap = (uint64_t)e->ae_segcap * e->ae_nseg;
+    const char* fbin = getenv("GOSSIP_AE_BINSCAN");  // 0: the direct scan (random bitmap probes)
+    e->ae_bin = (!fbin || atoi(fbin) != 0) && e->k <= 16;
+    if (e->ae_bin) {
+      // binned scan: segment = peer tile; the direct scan's blocks cover ae_spc chunks each
+      e->ae_bg = ae_bin_geom(e->N, e->k);
+      e->ae_nseg = e->ae_bg.nt;
+      e->ae_spc = (uint32_t)((nw + e->ae_nseg - 1) / e->ae_nseg);
+      // a tile's segment holds every exchange on small engines, else twice its share of the
+      // planned capacity (a larger segment overflows and the round reruns dense)
+      e->ae_segcap = (cap >= kn && !fcap) ? (uint32_t)kn : (uint32_t)((2 * cap + e->ae_nseg - 1) / e->ae_nseg);
+      e->ae_cap = std::min<uint64_t>(cap, (uint64_t)e->ae_segcap * e->ae_nseg);
+    } else {
+      e->ae_nseg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(4096, (nw + 3) / 4));
+      e->ae_spc = (uint32_t)((nw + e->ae_nseg - 1) / e->ae_nseg);
+      e->ae_nseg = (uint32_t)((nw + e->ae_spc - 1) / e->ae_spc);
+      e->ae_segcap = (cap >= kn && !fcap) ? e->k * e->ae_spc * 64 : (uint32_t)((cap + e->ae_nseg - 1) / e->ae_nseg);
+      e->ae_cap = (uint64_t)e->ae_segcap * e->ae_nseg;
+    }
+    const size_t seg_edges = (size_t)e->ae_segcap * e->ae_nseg;
+    if (e->ae_bin) {
+      const size_t recs = (size_t)e->ae_bg.nreg * ((size_t)e->k << e->ae_bg.rs);
+      if (!alloc_raw((void**)&e->ae_brec, recs * 8) ||
+          !alloc_raw((void**)&e->ae_boff, (size_t)e->ae_bg.nreg * (e->ae_bg.nt + 1) * 2))
+        return bail(GOSSIP_ENOMEM);
+    }
     if (!alloc_raw((void**)&e->ae_aux, 64) ||
         !alloc_raw((void**)&e->ae_claim, (size_t)e->N * 4) || !alloc_raw((void**)&e->ae_segn, (size_t)e->ae_nseg * 4) ||
-        !alloc_raw((void**)&e->ae_eid, (size_t)e->ae_cap * 8) ||
-        !alloc_raw((void**)&e->ae_erow, (size_t)e->ae_cap * 8 * e->R) ||
+        !alloc_raw((void**)&e->ae_eid, seg_edges * 8) ||
+        !alloc_raw((void**)&e->ae_erow, seg_edges * 8 * e->R) ||
         !alloc_raw(&e->ae_pmask, (size_t)e->N * e->k * std::max<uint32_t>(1, ae_lanes(e->R) / 8)))
       return bail(GOSSIP_ENOMEM);
     if (hipHostMalloc((void**)&e->ae_aux_h, 64) != hipSuccess) return bail(GOSSIP_ENOMEM);

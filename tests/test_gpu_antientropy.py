@@ -6,6 +6,8 @@ Paths (all must agree with the oracle and with each other):
   dense    — GOSSIP_AE_SPARSE=0: every round dense (copy + atomicMax kernel)
   sparse   — GOSSIP_AE_SPARSE=1: every round after the first sparse (the edge list holds k*N)
   overflow — sparse forced with a 64-edge list: rounds whose list overflows are rerun dense
+  *_direct — GOSSIP_AE_BINSCAN=0: the sparse scan probes the peers' bitmap words directly
+             instead of binning the exchanges by the peer's tile
 """
 import os
 
@@ -19,11 +21,14 @@ from gossip_hip.engine import churn_threshold as ct
 pytestmark = pytest.mark.gpu
 THREADS = min(16, os.cpu_count() or 1)
 PATHS = {"auto": {}, "dense": {"GOSSIP_AE_SPARSE": "0"}, "sparse": {"GOSSIP_AE_SPARSE": "1"},
-         "overflow": {"GOSSIP_AE_SPARSE": "1", "GOSSIP_AE_CAP": "64"}}
+         "overflow": {"GOSSIP_AE_SPARSE": "1", "GOSSIP_AE_CAP": "64"},
+         # sparse rounds with the direct scan (random bitmap probes) instead of the binned one
+         "sparse_direct": {"GOSSIP_AE_SPARSE": "1", "GOSSIP_AE_BINSCAN": "0"},
+         "auto_direct": {"GOSSIP_AE_BINSCAN": "0"}}
 
 
 def _engine(monkeypatch, path, *args, **kw):
-    for k in ("GOSSIP_AE_SPARSE", "GOSSIP_AE_CAP"):
+    for k in ("GOSSIP_AE_SPARSE", "GOSSIP_AE_CAP", "GOSSIP_AE_BINSCAN"):
         monkeypatch.delenv(k, raising=False)
     for k, v in PATHS[path].items():
         monkeypatch.setenv(k, v)
