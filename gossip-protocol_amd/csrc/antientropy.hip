@@ -225,16 +225,24 @@ __global__ __launch_bounds__(kAeBlock) void ae_push_kernel(AeArgs a) {
       uint32_t p = 0;
       if ((j & 3u) == 0 || mw) p = peer_j(a, n, j, x);
       if (!__ballot(mw != 0)) continue;
+      // every load in flight first: the pushed component and the peer's current
+      // S_{t+1} value (its pull pass is done; values only grow, so a component
+      // already at or above the pushed one needs no atomic)
+      uint32_t vv[L], cv[L], dst[L];
+      bool on[L];
 #pragma unroll
       for (uint32_t i = 0; i < L; ++i) {
         const uint32_t src = i * per + sub;
         const uint32_t pp = (uint32_t)__shfl((int)p, (int)src, 64);
         const uint64_t m = __shfl(mw, (int)src, 64);
-        if ((m >> c) & 1ull) {
-          const uint64_t node = ch * 64 + src;
-          atomicMax(&Vn[(uint64_t)pp * a.K + c], V[node * a.K + c]);
-        }
+        on[i] = (m >> c) & 1ull;
+        dst[i] = pp;
+        vv[i] = on[i] ? V[(ch * 64 + src) * a.K + c] : 0u;
+        cv[i] = on[i] ? Vn[(uint64_t)pp * a.K + c] : 0u;
       }
+#pragma unroll
+      for (uint32_t i = 0; i < L; ++i)
+        if (on[i] && vv[i] > cv[i]) atomicMax(&Vn[(uint64_t)dst[i] * a.K + c], vv[i]);
     }
   }
 }
