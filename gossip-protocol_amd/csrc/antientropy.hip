@@ -643,19 +643,34 @@ __global__ __launch_bounds__(kAeBlock) void ae_sparse_stats_kernel(AeArgs a) {
   }
   __syncthreads();
   const uint64_t words = (a.N + 63) / 64;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t ctg = lane < a.K ? tgt[lane] : 0u;
   uint64_t full = 0, nalive = 0, nstale = 0;
-  for (uint64_t w = (uint64_t)blockIdx.x * kAeBlock + threadIdx.x; w < words; w += (uint64_t)gridDim.x * kAeBlock) {
-    const uint4 q = *reinterpret_cast<const uint4*>(a.abn + 2 * w);
-    const uint64_t aw = ((uint64_t)q.y << 32) | q.x, sw = ((uint64_t)q.w << 32) | q.z;
+  uint32_t c_lane = 0;  // lane c: alive stale nodes whose component c equals the target
+  // whole waves iterate together (the stale rows are read one row per wave step)
+  for (uint64_t w0 = (uint64_t)blockIdx.x * kAeBlock + (threadIdx.x & ~63u); w0 < words;
+       w0 += (uint64_t)gridDim.x * kAeBlock) {
+    const uint64_t w = w0 + lane;
+    uint64_t aw = 0, sw = 0;
+    if (w < words) {
+      const uint4 q = *reinterpret_cast<const uint4*>(a.abn + 2 * w);
+      aw = ((uint64_t)q.y << 32) | q.x;
+      sw = ((uint64_t)q.w << 32) | q.z;
+    }
     nalive += (uint64_t)__popcll(aw);
     full += (uint64_t)__popcll(aw & ~sw);
     nstale += (uint64_t)__popcll(sw);
-    for (uint64_t as = aw & sw; as; as &= as - 1) {
-      const uint64_t n = w * 64 + (uint64_t)__builtin_ctzll(as);
-      for (uint32_t c = 0; c < a.K; ++c)
-        if (a.V[n * a.K + c] == tgt[c]) atomicAdd(&cnt[c], 1u);
+    const uint64_t as = aw & sw;
+    for (uint64_t pend = __ballot(as != 0); pend; pend &= pend - 1) {
+      const int src = __builtin_ctzll(pend);
+      const uint64_t ws = (uint64_t)__shfl((long long)w, src, 64);
+      for (uint64_t bits = (uint64_t)__shfl((long long)as, src, 64); bits; bits &= bits - 1) {
+        const uint64_t n = ws * 64 + (uint64_t)__builtin_ctzll(bits);
+        if (lane < a.K && a.V[n * a.K + lane] == ctg) ++c_lane;  // one row per wave: lane = component
+      }
     }
   }
+  if (lane < a.K && c_lane) atomicAdd(&cnt[lane], c_lane);
   const uint64_t f = wave_sum64(full);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = f;
   __syncthreads();
@@ -768,7 +783,8 @@ hipError_t launch_ae_sparse_binned(const AeArgs& a, hipStream_t st) {
 }
 
 hipError_t launch_ae_sparse_stats(const AeArgs& a, hipStream_t st) {
-  ae_sparse_stats_kernel<<<ae_grid((a.N + 63) / 64, kAeBlock, 2048), kAeBlock, 0, st>>>(a);
+  // few blocks: each adds its totals with three same-address atomics
+  ae_sparse_stats_kernel<<<ae_grid((a.N + 63) / 64, kAeBlock, 256), kAeBlock, 0, st>>>(a);
   return hipGetLastError();
 }
 
