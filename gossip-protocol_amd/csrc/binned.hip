@@ -35,6 +35,7 @@ namespace {
 constexpr int kEmitThreads = 1024;
 constexpr uint32_t kEmitGrid = 256;  // one persistent emit block per CU
 constexpr int kTileThreads = 1024;
+constexpr uint32_t kServeGrid = 256;  // persistent serve: one block per CU (the tile image takes 128 KiB of LDS)
 constexpr int kUnroll = 16;       // records in flight per lane in the run walkers (32 spills in K3)
 constexpr int kUnrollServe = 16;
 constexpr int kUnrollSeq = 8;  // records in flight per lane in the sequential response walker
@@ -493,6 +494,25 @@ __device__ __forceinline__ void load_tile(unsigned long long* img, const uint64_
   for (uint32_t q = 0; q < kQ; ++q) ((uint4*)img)[q * kTileThreads + tid] = x[q];
 }
 
+// Tile image in registers (the next tile's loads fly during the current walk).
+constexpr uint32_t kTileQ = kTileD / kTileThreads / 2;  // uint4 per thread
+__device__ __forceinline__ void tile_regs_load(uint4 (&x)[kTileQ], const uint64_t* __restrict__ S, uint64_t node0,
+                                               uint64_t N) {
+  const uint32_t tid = threadIdx.x;
+  if (node0 + kTileD <= N && ((uintptr_t)(S + node0) & 15u) == 0) {
+    const uint4* src = (const uint4*)(S + node0);
+#pragma unroll
+    for (uint32_t q = 0; q < kTileQ; ++q) x[q] = src[q * kTileThreads + tid];
+  } else {
+#pragma unroll
+    for (uint32_t q = 0; q < kTileQ; ++q) {
+      const uint64_t n = node0 + 2ull * (q * kTileThreads + tid);
+      const uint64_t a = n < N ? S[n] : 0ull, b = n + 1 < N ? S[n + 1] : 0ull;
+      x[q] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+    }
+  }
+}
+
 // K2 — one block per destination tile T (pull modes): LDS image of S_t[T];
 // every record aimed at T from a sender that is not yet fully informed gets
 // its pull response S_t[p] written next to it when nonzero (every one, in dense rounds).
@@ -501,10 +521,20 @@ __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, cons
   __shared__ unsigned long long img[kTileD];
   __shared__ uint64_t wmask[(kTileThreads / 64) * kUnrollServe];
   __shared__ int32_t wlist[(kTileThreads / 64) * 64];
-  const uint32_t T = tr.at(xcd_remap(blockIdx.x, gridDim.x));  // tiles of this launch (all of them on one shard)
-  const uint64_t node0 = (uint64_t)T << kTileDLog;
-  load_tile(img, S, node0, g.N);
+  // persistent: virtual block v = blockIdx.x, +gridDim.x, ... serves tile
+  // tr.at(xcd_remap(v, tr.n)) (the XCD of v is that of blockIdx.x, as with one
+  // block per tile); the next tile's image loads into registers during a walk
+  const uint32_t nv = tr.n;
+  auto tile_of = [&](uint32_t v) { return tr.at(xcd_remap(v, nv)); };
+  uint4 x[kTileQ];
+  if (blockIdx.x < nv) tile_regs_load(x, S, (uint64_t)tile_of(blockIdx.x) << kTileDLog, g.N);
+  for (uint32_t v = blockIdx.x; v < nv; v += gridDim.x) {
+  const uint32_t T = tile_of(v);
+  __syncthreads();  // the previous walk is done with img
+#pragma unroll
+  for (uint32_t q = 0; q < kTileQ; ++q) ((uint4*)img)[q * kTileThreads + threadIdx.x] = x[q];
   __syncthreads();
+  if (v + gridDim.x < nv) tile_regs_load(x, S, (uint64_t)tile_of(v + gridDim.x) << kTileDLog, g.N);
   const uint32_t* gids = b.ids;
   uint64_t* __restrict__ gresp = b.resp;
   const uint16_t* rowb = b.offT + (size_t)T * g.nt_s;
@@ -521,7 +551,10 @@ __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, cons
       gresp[rec[u]] = img[id[u] & (kTileD - 1)];
     }
   });
+  }
 }
+
+uint32_t serve_grid(uint32_t tiles) { return tiles < kServeGrid ? tiles : kServeGrid; }
 
 // K3 — one block per tile X: acc = S_t[X]; OR in the pushes aimed at X (its
 // runs) and the pull responses owed to X's own senders (their regions, read
@@ -662,7 +695,8 @@ hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, 
 #undef GOSSIP_EMIT
   const dim3 tg((g.nt_d + 1 + 31) / 32, (g.nt_s + 31) / 32);
   transpose_u16_kernel<<<tg, dim3(32, 8), 0, st>>>(b.off, b.offT, g.nt_s, g.nt_d + 1, partial, rs.plen);
-  if (mode == 2 || mode == 3) bin_serve_kernel<<<g.nt_d, kTileThreads, 0, st>>>(g, S, b, R, IdxRange::all(g.nt_d));
+  if (mode == 2 || mode == 3)
+    bin_serve_kernel<<<serve_grid(g.nt_d), kTileThreads, 0, st>>>(g, S, b, R, IdxRange::all(g.nt_d));
   // in place: K3 of tile X reads and writes only S[X] (push values and pull
   // responses come from the record buffers), and K1/K2 have finished reading S_t
   bin_apply_kernel<<<g.nt_d, kTileThreads, 0, st>>>(g, b, g, b, S, S, g.N, 0, partial, R, mode, flags);
@@ -751,7 +785,7 @@ hipError_t launch_sb_pre(const SbGeom& g, const SbBufs& b, const uint64_t* image
     sb_emit(g.q, b.q, image, R, t, key0, key1, mode, fa, pull_range(g), false, st);
     sb_transpose(g.q, b.q, nullptr, st);
     const IdxRange ot = own_tiles(g);
-    if (ot.n) bin_serve_kernel<<<ot.n, kTileThreads, 0, st>>>(g.q, image, b.q, R, ot);
+    if (ot.n) bin_serve_kernel<<<serve_grid(ot.n), kTileThreads, 0, st>>>(g.q, image, b.q, R, ot);
   }
   if (push) sb_emit(g.p, b.p, image, R, t, key0, key1, mode, fa, push_range(g, own_regions(g)), true, st);
   return hipGetLastError();
@@ -768,7 +802,7 @@ hipError_t launch_sb_post(const SbGeom& g, const SbBufs& b, const uint64_t* imag
   }
   if (pull) {
     const IdxRange rt = rest_of(g.q.nt_d, own_tiles(g));
-    if (rt.n) bin_serve_kernel<<<rt.n, kTileThreads, 0, st>>>(g.q, image, b.q, R, rt);
+    if (rt.n) bin_serve_kernel<<<serve_grid(rt.n), kTileThreads, 0, st>>>(g.q, image, b.q, R, rt);
   }
   BinBufs bp = b.p;
   bp.nzb = nzb;
