@@ -23,6 +23,8 @@
 //
 // OR is commutative and idempotent and every read is of S_t, so the record
 // order inside a run (decided by LDS atomics) never changes a result bit.
+#include <cstdlib>
+
 #include "binned.h"
 #include "philox.h"
 #include "round.h"
@@ -36,6 +38,11 @@ constexpr int kEmitThreads = 1024;
 constexpr uint32_t kEmitGrid = 256;  // one persistent emit block per CU
 constexpr int kTileThreads = 1024;
 constexpr uint32_t kServeGrid = 256;  // persistent serve: one block per CU (the tile image takes 128 KiB of LDS)
+constexpr uint32_t kApplyGrid = 256;  // persistent apply, likewise
+#ifndef GOSSIP_APPLY_PRE
+#define GOSSIP_APPLY_PRE 0
+#endif
+constexpr uint32_t kApplyPre = GOSSIP_APPLY_PRE;  // uint4 slots per thread of the next tile prefetched in apply
 constexpr int kUnroll = 16;       // records in flight per lane in the run walkers (32 spills in K3)
 constexpr int kUnrollServe = 16;
 constexpr int kUnrollSeq = 8;  // records in flight per lane in the sequential response walker
@@ -496,17 +503,19 @@ __device__ __forceinline__ void load_tile(unsigned long long* img, const uint64_
 
 // Tile image in registers (the next tile's loads fly during the current walk).
 constexpr uint32_t kTileQ = kTileD / kTileThreads / 2;  // uint4 per thread
-__device__ __forceinline__ void tile_regs_load(uint4 (&x)[kTileQ], const uint64_t* __restrict__ S, uint64_t node0,
+// Slots [Q0, Q0 + Q) of this thread's part of the tile (x[i] = slot Q0 + i).
+template <uint32_t Q0 = 0, uint32_t Q = kTileQ>
+__device__ __forceinline__ void tile_regs_load(uint4 (&x)[Q], const uint64_t* __restrict__ S, uint64_t node0,
                                                uint64_t N) {
   const uint32_t tid = threadIdx.x;
   if (node0 + kTileD <= N && ((uintptr_t)(S + node0) & 15u) == 0) {
     const uint4* src = (const uint4*)(S + node0);
 #pragma unroll
-    for (uint32_t q = 0; q < kTileQ; ++q) x[q] = src[q * kTileThreads + tid];
+    for (uint32_t q = 0; q < Q; ++q) x[q] = src[(Q0 + q) * kTileThreads + tid];
   } else {
 #pragma unroll
-    for (uint32_t q = 0; q < kTileQ; ++q) {
-      const uint64_t n = node0 + 2ull * (q * kTileThreads + tid);
+    for (uint32_t q = 0; q < Q; ++q) {
+      const uint64_t n = node0 + 2ull * ((Q0 + q) * kTileThreads + tid);
       const uint64_t a = n < N ? S[n] : 0ull, b = n + 1 < N ? S[n + 1] : 0ull;
       x[q] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
     }
@@ -575,9 +584,29 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
   __shared__ uint64_t wmask[(kTileThreads / 64) * kUnroll];
   __shared__ int32_t wlist[(kTileThreads / 64) * 64];
   const uint32_t tid = threadIdx.x;
-  const uint32_t X = xcd_remap(blockIdx.x, g.nt_d);
+  // persistent (grid apply_grid(nt_d)): virtual block v = blockIdx.x,
+  // +gridDim.x, ... applies tile xcd_remap(v, nt_d) (same XCD as blockIdx.x);
+  // the next tile's S_t loads into registers during the current tile's work.  In
+  // place stays safe: only this block reads or writes S[X] of its tiles.
+  const uint32_t nv = g.nt_d;
+  constexpr uint32_t kPre = kApplyPre;
+  constexpr uint32_t kPreN = kPre ? kPre : 1;  // (kPre = 0: xt unused)
+  uint4 xt[kPreN];
+  if (kPre && blockIdx.x < nv) tile_regs_load<0, kPreN>(xt, S, (uint64_t)xcd_remap(blockIdx.x, nv) << kTileDLog, Nn);
+  for (uint32_t v = blockIdx.x; v < nv; v += gridDim.x) {
+  const uint32_t X = xcd_remap(v, nv);
   const uint64_t node0 = (uint64_t)X << kTileDLog;
-  load_tile(acc, S, node0, Nn);
+  __syncthreads();  // the previous epilogue is done with acc and cnt
+  {
+    uint4 xr[kTileQ - kPre];
+    tile_regs_load<kPre, kTileQ - kPre>(xr, S, node0, Nn);
+    if constexpr (kPre > 0) {
+#pragma unroll
+      for (uint32_t q = 0; q < kPre; ++q) ((uint4*)acc)[q * kTileThreads + tid] = xt[q];
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < kTileQ - kPre; ++q) ((uint4*)acc)[(kPre + q) * kTileThreads + tid] = xr[q];
+  }
   if (tid < 64) cnt[tid] = 0;
   __syncthreads();
   const uint32_t* __restrict__ gids = b.ids;
@@ -630,8 +659,21 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
       }
     }
   }
+  // kApplyPre slots of the next tile's loads fly during the epilogue (all 8,
+  // or during the walks, spill: 4 spill 22 VGPRs)
+  if (kPre && v + gridDim.x < nv) tile_regs_load<0, kPreN>(xt, S, (uint64_t)xcd_remap(v + gridDim.x, nv) << kTileDLog, Nn);
   __syncthreads();
   tile_epilogue(acc, node0, Nn, hid0, Snext, partial, R, flags, cnt, red_hash, red_full, red_nz, b.nzb, b.fullb);
+  }
+}
+
+// Apply grid: one persistent block per CU (GOSSIP_APPLY_GRID=0: one block per tile).
+uint32_t apply_grid(uint32_t tiles) {
+  static const uint32_t cap = [] {
+    const char* e = getenv("GOSSIP_APPLY_GRID");
+    return e ? (uint32_t)strtoul(e, nullptr, 10) : kApplyGrid;
+  }();
+  return cap == 0 || tiles < cap ? tiles : cap;
 }
 
 }  // namespace
@@ -699,7 +741,7 @@ hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, 
     bin_serve_kernel<<<serve_grid(g.nt_d), kTileThreads, 0, st>>>(g, S, b, R, IdxRange::all(g.nt_d));
   // in place: K3 of tile X reads and writes only S[X] (push values and pull
   // responses come from the record buffers), and K1/K2 have finished reading S_t
-  bin_apply_kernel<<<g.nt_d, kTileThreads, 0, st>>>(g, b, g, b, S, S, g.N, 0, partial, R, mode, flags);
+  bin_apply_kernel<<<apply_grid(g.nt_d), kTileThreads, 0, st>>>(g, b, g, b, S, S, g.N, 0, partial, R, mode, flags);
   return launch_round_snapshot(partial, rs, st);
 }
 
@@ -807,7 +849,7 @@ hipError_t launch_sb_post(const SbGeom& g, const SbBufs& b, const uint64_t* imag
   BinBufs bp = b.p;
   bp.nzb = nzb;
   bp.fullb = fullb;
-  bin_apply_kernel<<<g.p.nt_d, kTileThreads, 0, st>>>(g.p, bp, g.q, b.q, image + g.lo, Snext, g.nown, g.lo, partial,
+  bin_apply_kernel<<<apply_grid(g.p.nt_d), kTileThreads, 0, st>>>(g.p, bp, g.q, b.q, image + g.lo, Snext, g.nown, g.lo, partial,
                                                       R, mode, flags);
   return hipGetLastError();
 }

@@ -7,6 +7,6 @@ for spec in "$@"; do
   name=${spec%%:*}; macros=${spec#*:}; defs=""
   for m in ${macros//,/ }; do [ -n "$m" ] && [ "$m" != "$name" ] && defs="$defs -D$m"; done
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wall -Wno-unused-result $defs \
-    csrc/engine.hip csrc/kernels.hip csrc/binned.hip csrc/frontier.hip csrc/antientropy.hip -o ../exp/lib$name.so &
+    csrc/engine.hip csrc/kernels.hip csrc/binned.hip csrc/frontier.hip csrc/sharded.hip csrc/antientropy.hip -o ../exp/lib$name.so &
 done
 wait
