@@ -43,7 +43,10 @@ constexpr uint32_t kApplyGrid = 256;  // persistent apply, likewise
 #define GOSSIP_APPLY_PRE 0
 #endif
 constexpr uint32_t kApplyPre = GOSSIP_APPLY_PRE;  // uint4 slots per thread of the next tile prefetched in apply
-constexpr int kUnroll = 16;       // records in flight per lane in the run walkers (32 spills in K3)
+#ifndef GOSSIP_APPLY_UNROLL
+#define GOSSIP_APPLY_UNROLL 16
+#endif
+constexpr int kUnroll = GOSSIP_APPLY_UNROLL;  // records in flight per lane in the run walkers (32 spills in K3)
 constexpr int kUnrollServe = 16;
 constexpr int kUnrollSeq = 8;  // records in flight per lane in the sequential response walker
 // record id word: p_local [0,14) | n_local [14,27) | flags.  K1 rewrites every
