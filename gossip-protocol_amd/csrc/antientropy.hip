@@ -274,12 +274,16 @@ __global__ __launch_bounds__(kAeBlock) void ae_stats_kernel(AeArgs a, const uint
     }
     const uint64_t aw = ab[2 * ch];  // bits past N are 0
     BT bad = 0;
+    // hash_term's (c*N + node) * kGold64 for node = ch*64 + sub*L + i, stepped
+    // by kGold64 per i (mod 2^64: one 64-bit multiply per L terms, bit-exact)
+    uint64_t hb = ((uint64_t)c * a.N + ch * 64 + sub * L) * kGold64;
 #pragma unroll
     for (uint32_t i = 0; i < L; ++i) {
       const uint64_t node = ch * 64 + sub * L + i;
       const bool valid = node < a.N && c < a.K;
       const bool al = (aw >> (sub * L + i)) & 1ull;
-      if (a.flags & 1u) hash += valid ? hash_term(v[i], c, node, a.N) : 0ull;
+      if (a.flags & 1u) hash += valid && v[i] ? mix64((uint64_t)v[i] + hb) : 0ull;
+      hb += kGold64;
       c_lane += (valid && al && v[i] == tgt) ? 1u : 0u;
       bad |= (BT)(valid && v[i] != tgt) << i;
     }
