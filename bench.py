@@ -40,23 +40,22 @@ def alg_bytes_per_node_round(mode: str, k: int, words: int) -> int:
 
 
 def load_pmc(workload: str):
-    """HBM traffic per round-kernel launch from the committed PMC passes (profiles/)."""
-    path = os.path.join(ROOT, "profiles", "pmc_round_kernel.json")
+    """PMC HBM traffic per dense round (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM), summed over
+    the dense round's kernels, from the committed passes (tools/gpu_pmc_dense.sh -> profiles/)."""
+    path = os.path.join(ROOT, "profiles", "pmc_dense_round.json")
     try:
         with open(path) as f:
             d = json.load(f)
         if d.get("workload") == workload:
-            return d.get("hbm_bytes_per_launch")
+            return d.get("hbm_bytes_per_dense_round"), os.path.relpath(path, ROOT)
     except (OSError, ValueError):
         pass
-    return None
+    return None, None
 
 
-def cpu_baseline(n_nodes: int, seed: int, budget_s: float = 12.0):
-    """Oracle (C restatement, OpenMP) on the host cores, same workload, bounded sample."""
+def _omp_run(n_nodes: int, seed: int, threads: int, budget_s: float):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py as op
-    threads = min(16, os.cpu_count() or 1)
     o = op.OracleEngine(n_nodes, RUMORS, MODE, FANOUT, seed, threads=threads)
     o.inject_random()
     rounds, t0 = 0, time.perf_counter()
@@ -66,35 +65,50 @@ def cpu_baseline(n_nodes: int, seed: int, budget_s: float = 12.0):
         if res.converged:
             break
     dt = time.perf_counter() - t0
-    return {"value": n_nodes * rounds / dt, "unit": "node-updates/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/gossip_oracle.c OpenMP x{threads}, first {rounds} rounds of the same "
-                      f"{n_nodes}-node push-pull k=2 R=64 run ({dt:.1f}s)"}
+    o.close()
+    return n_nodes * rounds / dt, rounds, dt
+
+
+def cpu_baseline(n_nodes: int, seed: int, budget_s: float = 10.0):
+    """The oracle (C restatement of the same rounds, `kind: port`; the reference itself is Go and not
+    buildable here) on the host cores, same workload, bounded sample: OpenMP on this job's host-core
+    share, and one thread."""
+    nproc = os.cpu_count() or 1
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = nproc
+    # the GPU box gives each GPU job a share of the host (OMP_NUM_THREADS, 16 there); here: every core
+    threads = max(1, min(avail, int(os.environ.get("OMP_NUM_THREADS", avail))))
+    v, rounds, dt = _omp_run(n_nodes, seed, threads, budget_s)
+    v1, rounds1, dt1 = _omp_run(n_nodes, seed, 1, budget_s)
+    return {"value": v, "unit": "node-updates/s", "cores": threads, "kind": "port",
+            "single_thread": {"value": v1, "rounds": rounds1, "seconds": dt1},
+            "nproc": nproc, "affinity_cpus": avail,
+            "sample": f"oracle/gossip_oracle.c, first {rounds} rounds ({dt:.1f} s) of the same {n_nodes}-node "
+                      f"push-pull k=2 R=64 run on {threads} OpenMP threads (the host share of this job; "
+                      f"nproc {nproc}); single thread: first {rounds1} rounds ({dt1:.1f} s)"}
 
 
 def dense_only(n_nodes: int, seed: int, device: int, steps: int = 2):
     """Every round on the binned (dense) pipeline, same workload: the per-round cost the sparse
     frontier rounds avoid, reported beside the headline so that saving never hides in `frac`."""
     from gossip_hip import FLAG_DENSE, FLAG_TIMING, Engine
-    prev = os.environ.get("GOSSIP_AHEAD")
-    os.environ["GOSSIP_AHEAD"] = "1"  # no round enqueued past convergence inside the timed region
-    try:
-        e = Engine(n_nodes, RUMORS, MODE, FANOUT, seed, flags=FLAG_TIMING | FLAG_DENSE, device=device)
-    finally:
-        if prev is None:
-            os.environ.pop("GOSSIP_AHEAD")
-        else:
-            os.environ["GOSSIP_AHEAD"] = prev
+    # ahead 1: no round enqueued past convergence inside the timed region
+    e = Engine(n_nodes, RUMORS, MODE, FANOUT, seed, flags=FLAG_TIMING | FLAG_DENSE, device=device,
+               params={"ahead": 1})
     e.reset(); e.inject_random(); e.step(64, with_infected=False)
     e.reset_timing()
     for _ in range(steps):
         e.reset(); e.inject_random(); e.step(64, with_infected=False)
-    ms, n = e.kernel_time(0)
+    ms, n = e.kernel_time(3)
     e.close()
     us = ms * 1e3 / max(n, 1)
     bpn = alg_bytes_per_node_round(MODE, FANOUT, 1)
     return {"avg_round_us": us, "achieved_GBps": bpn * n_nodes / us / 1e3,
             "frac": bpn * n_nodes / us / 1e3 / HBM_PEAK_GBS, "rounds_timed": n,
-            "note": "GOSSIP_FLAG_DENSE: every round on bin_emit+transpose+serve+apply, same workload"}
+            "note": "GOSSIP_FLAG_DENSE: every round of the step on bin_emit+transpose+serve+apply (also the "
+                    "nearly empty / nearly full ones), same workload"}
 
 
 def main():
@@ -158,14 +172,26 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
-    round_ms, round_launches = eng.kernel_time(0)
     total_rounds = sum(rounds)
     value = n_total * total_rounds / dt
     nown = eng.hi - eng.lo
     bpn = alg_bytes_per_node_round(MODE, FANOUT, 1)
-    avg_launch_s = round_ms / 1e3 / max(round_launches, 1)
-    achieved = bpn * nown / avg_launch_s / 1e9
     workload = f"pushpull k=2 R=64, 2^{int(np.log2(args.nodes_per_gpu))} nodes/GPU x {world}"
+    alg_round = bpn * nown  # algorithmic bytes of one round over this rank's nodes
+    if world == 1:
+        # the dominant kernel = the dense round (emit + transpose + serve + apply), hipEvents around each
+        # dense round on the engine's stream, inside the timed steps (timer 3); the whole step beside it
+        dense_ms, dense_n = eng.kernel_time(3)
+        sparse_ms, sparse_n = eng.kernel_time(4)
+        step_ms, step_rounds = eng.kernel_time(0)
+        dense_s = dense_ms / 1e3 / max(dense_n, 1)
+        achieved = alg_round / dense_s / 1e9
+        step_round_s = step_ms / 1e3 / max(step_rounds, 1)
+    else:
+        round_ms, round_launches = eng.kernel_time(0)
+        dense_s = round_ms / 1e3 / max(round_launches, 1)
+        dense_n = round_launches
+        achieved = alg_round / dense_s / 1e9
 
     if rank == 0:
         out = {
@@ -185,23 +211,34 @@ def main():
                        "mode": MODE, "seed": hex(seed), "rounds_to_converge": rounds[0],
                        "parallelism": f"shard{world}" if world > 1 else "single"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": load_pmc(workload),
-                         "kernel": ("round pipeline: sparse rounds frontier_summary+scan+commit, dense rounds "
-                                    "bin_emit+transpose_u16+bin_serve+bin_apply, + round_snapshot; hipEvents around "
-                                    "each step, gaps between rounds included" if world == 1 else
-                                    "sharded rounds, hipEvent-timed device work of the hot kernel per round (timer 0): "
-                                    "dense = binned push pass (every sender -> own tiles) + pull pass (own senders "
-                                    "-> image tiles) + serve + apply after the state all-gather, sparse = rare index "
-                                    "+ sharded scan between the rare-list all-gather and the push all-to-all "
-                                    "(DESIGN.md §5); collectives not included"),
-                         "bytes_per_node_round": bpn, "avg_launch_us": avg_launch_s * 1e6,
-                         "rounds_timed": round_launches},
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "bytes_per_node_round": bpn, "alg_bytes_per_launch": alg_round,
+                         "avg_launch_us": dense_s * 1e6, "rounds_timed": dense_n},
         }
-        traffic = out["roofline"]["traffic"]
-        if traffic:
-            out["roofline"]["traffic_GBps"] = traffic / avg_launch_s / 1e9  # PMC bytes per round / round time
+        rl = out["roofline"]
+        if world == 1:
+            rl["kernel"] = ("dense round = bin_emit + transpose_u16 + bin_serve + bin_apply (one launch each per "
+                            "round), hipEvents around each dense round of the timed steps; achieved = 64 B x "
+                            "nodes / average dense-round time (SURVEY.md §8(d))")
+            traffic, src = load_pmc(workload)
+            if traffic:
+                rl["traffic"] = traffic
+                rl["traffic_ratio"] = traffic / alg_round
+                rl["traffic_GBps"] = traffic / dense_s / 1e9
+                rl["traffic_source"] = src
+            rl["step_frac"] = {"achieved": alg_round / step_round_s / 1e9,
+                               "frac": alg_round / step_round_s / 1e9 / HBM_PEAK_GBS,
+                               "avg_round_us": step_round_s * 1e6, "rounds": step_rounds,
+                               "note": "whole step (sparse rounds at the dense byte count, gaps included)"}
+            rl["sparse_rounds"] = {"avg_round_us": sparse_ms * 1e3 / max(sparse_n, 1), "rounds_timed": sparse_n}
+        else:
+            rl["kernel"] = ("sharded rounds, hipEvent-timed device work of the hot kernels per round (timer 0): "
+                            "dense = binned push pass (every sender -> own tiles) + pull pass (own senders -> "
+                            "image tiles) + serve + apply after the state all-gather, sparse = rare index + "
+                            "sharded scan between the rare-list all-gather and the push all-to-all "
+                            "(DESIGN.md §5); collectives not included")
         if world == 1 and not args.no_dense_only:
-            out["roofline"]["dense_only"] = dense_only(n_total, seed, local)
+            rl["dense_only"] = dense_only(n_total, seed, local)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(n_total, seed)
         print(json.dumps(out), flush=True)

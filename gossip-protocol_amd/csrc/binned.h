@@ -51,6 +51,7 @@ struct BinGeom {
   uint32_t ts, ts_log;   // sender tile size (power of two <= kMaxSenders, ts * k <= kRecPerRegion)
   uint32_t rp;           // records per sender region = ts * k
   uint32_t nt_s, nt_d;   // sender tiles, destination tiles
+  uint32_t apply_grid;   // host only: persistent apply blocks (0 = one per tile; gossip_set_param)
 };
 
 BinGeom make_bin_geom(uint64_t N, uint32_t k);

@@ -23,8 +23,6 @@
 //
 // OR is commutative and idempotent and every read is of S_t, so the record
 // order inside a run (decided by LDS atomics) never changes a result bit.
-#include <cstdlib>
-
 #include "binned.h"
 #include "philox.h"
 #include "round.h"
@@ -481,29 +479,6 @@ __device__ __forceinline__ void for_each_run_record(const BinGeom& g, const uint
   }
 }
 
-// LDS image of S_t[node0, node0 + kTileD): every load of the tile in flight at
-// once (8 x 16 B per lane), then the LDS stores.
-__device__ __forceinline__ void load_tile(unsigned long long* img, const uint64_t* __restrict__ S, uint64_t node0,
-                                          uint64_t N) {
-  constexpr uint32_t kQ = kTileD / kTileThreads / 2;
-  const uint32_t tid = threadIdx.x;
-  uint4 x[kQ];
-  if (node0 + kTileD <= N && ((uintptr_t)(S + node0) & 15u) == 0) {  // (a shard slice may start 8-B aligned)
-    const uint4* src = (const uint4*)(S + node0);
-#pragma unroll
-    for (uint32_t q = 0; q < kQ; ++q) x[q] = src[q * kTileThreads + tid];
-  } else {  // last, ragged tile (or an 8-B aligned slice)
-#pragma unroll
-    for (uint32_t q = 0; q < kQ; ++q) {
-      const uint64_t n = node0 + 2ull * (q * kTileThreads + tid);
-      const uint64_t a = n < N ? S[n] : 0ull, b = n + 1 < N ? S[n + 1] : 0ull;
-      x[q] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
-    }
-  }
-#pragma unroll
-  for (uint32_t q = 0; q < kQ; ++q) ((uint4*)img)[q * kTileThreads + tid] = x[q];
-}
-
 // Tile image in registers (the next tile's loads fly during the current walk).
 constexpr uint32_t kTileQ = kTileD / kTileThreads / 2;  // uint4 per thread
 // Slots [Q0, Q0 + Q) of this thread's part of the tile (x[i] = slot Q0 + i).
@@ -670,13 +645,10 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
   }
 }
 
-// Apply grid: one persistent block per CU (GOSSIP_APPLY_GRID=0: one block per tile).
-uint32_t apply_grid(uint32_t tiles) {
-  static const uint32_t cap = [] {
-    const char* e = getenv("GOSSIP_APPLY_GRID");
-    return e ? (uint32_t)strtoul(e, nullptr, 10) : kApplyGrid;
-  }();
-  return cap == 0 || tiles < cap ? tiles : cap;
+// Apply grid: one persistent block per CU (BinGeom::apply_grid = 0: one block per tile).
+uint32_t apply_grid(const BinGeom& g) {
+  const uint32_t cap = g.apply_grid;
+  return cap == 0 || g.nt_d < cap ? g.nt_d : cap;
 }
 
 }  // namespace
@@ -695,6 +667,7 @@ BinGeom make_bin_geom(uint64_t N, uint32_t k) {
   g.rp = ts * k;
   g.nt_s = (uint32_t)((N + ts - 1) / ts);
   g.nt_d = (uint32_t)((N + kTileD - 1) / kTileD);
+  g.apply_grid = kApplyGrid;
   return g;
 }
 
@@ -744,8 +717,8 @@ hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, 
     bin_serve_kernel<<<serve_grid(g.nt_d), kTileThreads, 0, st>>>(g, S, b, R, IdxRange::all(g.nt_d));
   // in place: K3 of tile X reads and writes only S[X] (push values and pull
   // responses come from the record buffers), and K1/K2 have finished reading S_t
-  bin_apply_kernel<<<apply_grid(g.nt_d), kTileThreads, 0, st>>>(g, b, g, b, S, S, g.N, 0, partial, R, mode, flags);
-  return launch_round_snapshot(partial, rs, st);
+  bin_apply_kernel<<<apply_grid(g), kTileThreads, 0, st>>>(g, b, g, b, S, S, g.N, 0, partial, R, mode, flags);
+  return hipGetLastError();  // the engine enqueues the round's snapshot (round.h) after its timing event
 }
 
 // --- sharded dense rounds ------------------------------------------------
@@ -852,7 +825,7 @@ hipError_t launch_sb_post(const SbGeom& g, const SbBufs& b, const uint64_t* imag
   BinBufs bp = b.p;
   bp.nzb = nzb;
   bp.fullb = fullb;
-  bin_apply_kernel<<<apply_grid(g.p.nt_d), kTileThreads, 0, st>>>(g.p, bp, g.q, b.q, image + g.lo, Snext, g.nown, g.lo, partial,
+  bin_apply_kernel<<<apply_grid(g.p), kTileThreads, 0, st>>>(g.p, bp, g.q, b.q, image + g.lo, Snext, g.nown, g.lo, partial,
                                                       R, mode, flags);
   return hipGetLastError();
 }

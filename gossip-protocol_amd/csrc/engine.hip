@@ -33,7 +33,10 @@ namespace {
 
 thread_local std::string g_create_error;
 
-constexpr int kTimers = 3;  // 0 = round kernel, 1 = stats kernel, 2 = ANTIENTROPY sparse round kernels
+// 0 = round kernel (binned engines: the whole step), 1 = stats kernel, 2 = ANTIENTROPY sparse round
+// kernels, 3 = dense rounds of a binned engine (emit..apply, per round), 4 = its sparse rounds
+constexpr int kTimers = 5;
+constexpr uint32_t kRing = 8;
 
 }  // namespace
 
@@ -131,10 +134,14 @@ struct gossip_engine {
   uint64_t* sx_host = nullptr;  // pinned: [G + 2] counts / list bases
 
   hipEvent_t ev[kTimers][2] = {};
-  double time_ms[kTimers] = {0, 0, 0};
-  uint64_t launches[kTimers] = {0, 0, 0};
+  double time_ms[kTimers] = {};
+  uint64_t launches[kTimers] = {};
   bool timing = false;
-  bool ev_pending[kTimers] = {false, false, false};
+  bool ev_pending[kTimers] = {};
+  // per-round events of the pipelined rounds (timers 3 and 4), one pair per ring slot
+  hipEvent_t evr[kRing][2] = {};
+  int64_t evr_round[kRing] = {-1, -1, -1, -1, -1, -1, -1, -1};
+  int evr_kind[kRing] = {};
 
   int fail(int code, const char* fmt, ...) {
     char buf[512];
@@ -193,6 +200,9 @@ void free_all(gossip_engine* e) {
       if (x) (void)hipEventDestroy(x);
   for (auto& x : e->ev_pre)
     if (x) (void)hipEventDestroy(x);
+  for (auto& p : e->evr)
+    for (auto& x : p)
+      if (x) (void)hipEventDestroy(x);
   if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
 }
 
@@ -326,8 +336,6 @@ AeArgs make_ae_args(gossip_engine* e) {
   return a;
 }
 
-constexpr uint32_t kRing = 8;
-
 // Binned engines: make partial_d hold the exact totals of S (and the bitmaps
 // exact) when an untracked write (plain inject) left them stale.
 int prepare_planned(gossip_engine* e) {
@@ -407,14 +415,43 @@ RoundSync ring_sync(gossip_engine* e, uint32_t slot) {
   return rs;
 }
 
+// Folds the per-round events of ring slot `slot` into timer 3 (dense) or 4
+// (sparse) when that round is below `limit` (rounds enqueued past convergence
+// are not counted).
+int round_timer_collect(gossip_engine* e, uint32_t slot, int64_t limit) {
+  if (e->evr_round[slot] < 0) return GOSSIP_OK;
+  HIP_OK(e, hipEventSynchronize(e->evr[slot][1]));
+  if (e->evr_round[slot] < limit) {
+    float ms = 0.f;
+    HIP_OK(e, hipEventElapsedTime(&ms, e->evr[slot][0], e->evr[slot][1]));
+    e->time_ms[e->evr_kind[slot]] += ms;
+    e->launches[e->evr_kind[slot]] += 1;
+  }
+  e->evr_round[slot] = -1;
+  return GOSSIP_OK;
+}
+
+// One pipelined round: its kernels (bracketed by the slot's events when timing),
+// then the snapshot of the totals into ring slot `slot` (rs).
 int launch_round_path(gossip_engine* e, uint32_t t, bool sparse, uint32_t maj, bool all_d, uint32_t filt,
-                      const RoundSync& rs) {
+                      const RoundSync& rs, int slot) {
+  const bool timed = e->timing && slot >= 0;
+  if (timed) {
+    if (int rc = round_timer_collect(e, (uint32_t)slot, INT64_MAX)) return rc;
+    HIP_OK(e, hipEventRecord(e->evr[slot][0], e->stream));
+  }
   if (sparse)
     HIP_OK(e, launch_frontier_round(e->fb, e->S, e->N, e->partial_d, e->R, e->k, t, e->key0, e->key1, e->mode, maj,
                                     all_d, e->fa, e->cfg.flags, rs, e->stream));
   else
     HIP_OK(e, launch_binned_round(e->bg, e->bb, e->S, e->partial_d, e->R, t, e->key0, e->key1, e->mode, filt,
                                   e->fa, e->cfg.flags, rs, e->stream));
+  if (timed) {
+    HIP_OK(e, hipEventRecord(e->evr[slot][1], e->stream));
+    e->evr_round[slot] = t;
+    e->evr_kind[slot] = sparse ? 4 : 3;
+  }
+  HIP_OK(e, launch_round_snapshot(e->partial_d, rs, e->stream));
   return GOSSIP_OK;
 }
 
@@ -470,7 +507,7 @@ int step_planned(gossip_engine* e, uint32_t max_rounds, gossip_round_stats_t* st
       const uint32_t slot = launched % kRing;
       const RoundSync rs = ring_sync(e, slot);
       want[slot] = rs.seq;
-      if (int rc = launch_round_path(e, t0 + launched, sparse, maj, all_d, dense_filter(e, x), rs)) return rc;
+      if (int rc = launch_round_path(e, t0 + launched, sparse, maj, all_d, dense_filter(e, x), rs, (int)slot)) return rc;
       ++launched;
     }
     if (done == launched) break;
@@ -498,6 +535,8 @@ int step_planned(gossip_engine* e, uint32_t max_rounds, gossip_round_stats_t* st
     HIP_OK(e, hipEventElapsedTime(&ms, e->ev[0][0], e->ev[0][1]));
     e->time_ms[0] += ms;
     e->launches[0] += done;
+    for (uint32_t s = 0; s < kRing; ++s)
+      if (int rc = round_timer_collect(e, s, (int64_t)t0 + done)) return rc;
   }
   e->t = t0 + done;
   if (rounds_done) *rounds_done = done;
@@ -600,7 +639,7 @@ int compute_round(gossip_engine* e, const uint64_t* gathered) {
     const Est x = est_of(e, tot.data());
     const bool sparse = choose_sparse(e, x, &maj, &all_d);
     if ((rc = timer_begin(e, 0))) return rc;
-    if ((rc = launch_round_path(e, e->t, sparse, maj, all_d, dense_filter(e, x), ring_sync(e, 0)))) return rc;
+    if ((rc = launch_round_path(e, e->t, sparse, maj, all_d, dense_filter(e, x), ring_sync(e, 0), -1))) return rc;
     return timer_end(e, 0);  // stats are fused into the round kernels
   } else if (e->sbin) {  // sharded dense round: binned pipeline over the gathered image
     if ((rc = timer_begin(e, 0))) return rc;
@@ -645,6 +684,44 @@ void rotate(gossip_engine* e) {
     e->cur ^= 1;
     bind_slices(e);
   }
+}
+
+// ANTIENTROPY sparse-round edge lists.  cap_req = 0: the
+// default capacity (N/8 edges covers the churn tail at configs[4]; small
+// engines get room for every exchange, k per node, so never overflow); else
+// exactly cap_req edges (gossip_set_param "ae_cap": the overflow tests).
+int ae_alloc_lists(gossip_engine* e, uint64_t cap_req) {
+  const uint64_t nw = (e->N + 63) / 64;
+  const uint64_t kn = (uint64_t)e->N * e->k;
+  const bool forced = cap_req != 0;
+  const uint64_t cap = forced ? cap_req : std::min<uint64_t>(kn, std::max<uint64_t>(e->N / 8, 65536));
+  if (e->ae_bin) {
+    // binned scan: segment = peer tile.  A tile's segment holds every exchange on small
+    // engines, else twice its share of the planned capacity (a larger segment overflows
+    // and the round reruns dense)
+    e->ae_nseg = e->ae_bg.nt;
+    e->ae_spc = (uint32_t)((nw + e->ae_nseg - 1) / e->ae_nseg);
+    e->ae_segcap = (cap >= kn && !forced) ? (uint32_t)kn : (uint32_t)((2 * cap + e->ae_nseg - 1) / e->ae_nseg);
+    e->ae_cap = std::min<uint64_t>(cap, (uint64_t)e->ae_segcap * e->ae_nseg);
+  } else {  // direct scan: block b owns ae_spc 64-node chunks and lists its edges in segment b
+    e->ae_nseg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(4096, (nw + 3) / 4));
+    e->ae_spc = (uint32_t)((nw + e->ae_nseg - 1) / e->ae_nseg);
+    e->ae_nseg = (uint32_t)((nw + e->ae_spc - 1) / e->ae_spc);
+    e->ae_segcap = (cap >= kn && !forced) ? e->k * e->ae_spc * 64 : (uint32_t)((cap + e->ae_nseg - 1) / e->ae_nseg);
+    e->ae_cap = (uint64_t)e->ae_segcap * e->ae_nseg;
+  }
+  void* old[] = {e->ae_segn, e->ae_eid, e->ae_erow};
+  for (void* p : old)
+    if (p) HIP_OK(e, hipFree(p));
+  e->ae_segn = e->ae_eid = e->ae_erow = nullptr;
+  const size_t seg_edges = (size_t)e->ae_segcap * e->ae_nseg;
+  if (hipMalloc((void**)&e->ae_segn, (size_t)e->ae_nseg * 4) != hipSuccess ||
+      hipMalloc((void**)&e->ae_eid, seg_edges * 8) != hipSuccess ||
+      hipMalloc((void**)&e->ae_erow, seg_edges * 8 * e->R) != hipSuccess)
+    return e->fail(GOSSIP_ENOMEM, "hipMalloc of the ANTIENTROPY edge lists (%llu edges) failed",
+                   (unsigned long long)seg_edges);
+  HIP_OK(e, hipMemset(e->ae_segn, 0, (size_t)e->ae_nseg * 4));
+  return GOSSIP_OK;
 }
 
 void fill_stats(gossip_engine* e, const uint64_t* total, gossip_round_stats_t* st) {
@@ -699,11 +776,10 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
     g_create_error = "shard_rank >= shard_count";
     return GOSSIP_EINVAL;
   }
-  for (uint32_t r : cfg->reserved)
-    if (r) {
-      g_create_error = "reserved fields must be zero";
-      return GOSSIP_EINVAL;
-    }
+  if (cfg->stall_rounds > 16) {
+    g_create_error = "stall_rounds must be in [0, 16]";
+    return GOSSIP_EINVAL;
+  }
   if ((cfg->edge_loss || cfg->partitions > 1) &&
       (cfg->mode == GOSSIP_MODE_FLOOD || cfg->mode == GOSSIP_MODE_ANTIENTROPY)) {
     g_create_error = "edge_loss / partitions apply to the random modes (PUSH, PULL, PUSHPULL)";
@@ -784,45 +860,18 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
         !alloc_raw((void**)&e->alive, nw * 16) || !alloc_raw((void**)&e->alive_n, nw * 16))
       return bail(GOSSIP_ENOMEM);
     if (launch_ae_fill_alive(e->alive, e->N, nullptr) != hipSuccess) return bail(GOSSIP_EHIP);
-    // sparse rounds: scan block b owns ae_spc 64-node chunks and lists
-    // its edges in a segment of ae_segcap; N/8 edges in all covers the churn tail at
-    // configs[4]; small engines get room for every exchange (k per node), so never overflow
-    const uint64_t kn = (uint64_t)e->N * e->k;
-    uint64_t cap = std::min<uint64_t>(kn, std::max<uint64_t>(e->N / 8, 65536));
-    const char* fcap = getenv("GOSSIP_AE_CAP");
-    if (fcap) cap = std::max<uint64_t>(1, strtoull(fcap, nullptr, 10));
-    if (const char* f = getenv("GOSSIP_AE_SPARSE")) e->ae_force = atoi(f);
-    const char* fbin = getenv("GOSSIP_AE_BINSCAN");  // 0: the direct scan (random bitmap probes)
-    e->ae_bin = (!fbin || atoi(fbin) != 0) && e->k <= 16;
+    e->ae_bin = !(cfg->flags & GOSSIP_FLAG_AE_DIRECT_SCAN) && e->k <= 16;  // else the direct scan
     if (e->ae_bin) {
-      // binned scan: segment = peer tile; the direct scan's blocks cover ae_spc chunks each
       e->ae_bg = ae_bin_geom(e->N, e->k);
-      e->ae_nseg = e->ae_bg.nt;
-      e->ae_spc = (uint32_t)((nw + e->ae_nseg - 1) / e->ae_nseg);
-      // a tile's segment holds every exchange on small engines, else twice its share of the
-      // planned capacity (a larger segment overflows and the round reruns dense)
-      e->ae_segcap = (cap >= kn && !fcap) ? (uint32_t)kn : (uint32_t)((2 * cap + e->ae_nseg - 1) / e->ae_nseg);
-      e->ae_cap = std::min<uint64_t>(cap, (uint64_t)e->ae_segcap * e->ae_nseg);
-    } else {
-      e->ae_nseg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(4096, (nw + 3) / 4));
-      e->ae_spc = (uint32_t)((nw + e->ae_nseg - 1) / e->ae_nseg);
-      e->ae_nseg = (uint32_t)((nw + e->ae_spc - 1) / e->ae_spc);
-      e->ae_segcap = (cap >= kn && !fcap) ? e->k * e->ae_spc * 64 : (uint32_t)((cap + e->ae_nseg - 1) / e->ae_nseg);
-      e->ae_cap = (uint64_t)e->ae_segcap * e->ae_nseg;
-    }
-    const size_t seg_edges = (size_t)e->ae_segcap * e->ae_nseg;
-    if (e->ae_bin) {
       const size_t recs = (size_t)e->ae_bg.nreg * ((size_t)e->k << e->ae_bg.rs);
       if (!alloc_raw((void**)&e->ae_brec, recs * 8) ||
           !alloc_raw((void**)&e->ae_boff, (size_t)e->ae_bg.nreg * (e->ae_bg.nt + 1) * 2))
         return bail(GOSSIP_ENOMEM);
     }
-    if (!alloc_raw((void**)&e->ae_aux, 64) ||
-        !alloc_raw((void**)&e->ae_claim, (size_t)e->N * 4) || !alloc_raw((void**)&e->ae_segn, (size_t)e->ae_nseg * 4) ||
-        !alloc_raw((void**)&e->ae_eid, seg_edges * 8) ||
-        !alloc_raw((void**)&e->ae_erow, seg_edges * 8 * e->R) ||
+    if (!alloc_raw((void**)&e->ae_aux, 64) || !alloc_raw((void**)&e->ae_claim, (size_t)e->N * 4) ||
         !alloc_raw(&e->ae_pmask, (size_t)e->N * e->k * std::max<uint32_t>(1, ae_lanes(e->R) / 8)))
       return bail(GOSSIP_ENOMEM);
+    if (ae_alloc_lists(e, 0) != GOSSIP_OK) return bail(GOSSIP_ENOMEM);
     if (hipHostMalloc((void**)&e->ae_aux_h, 64) != hipSuccess) return bail(GOSSIP_ENOMEM);
   } else if (e->mode == GOSSIP_MODE_FLOOD) {
     if (!alloc(&e->S, shard) || !alloc(&e->Snext, shard) || !alloc(&e->Sprev, shard) || !alloc(&e->skip, shard) ||
@@ -849,11 +898,7 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
       e->bb.nzb = e->fb.nzb;
       e->bb.fullb = e->fb.fullb;
       e->frontier = true;
-      if (const char* f = getenv("GOSSIP_SPARSE_FRAC")) e->sparse_frac = atof(f);
-      if (const char* f = getenv("GOSSIP_ALLD_FRAC")) e->alld_frac = atof(f);
-      if (const char* f = getenv("GOSSIP_FILTER_FRAC")) e->filter_frac = atof(f);
     }
-    if (const char* a = getenv("GOSSIP_AHEAD")) e->ahead = std::max(1, std::min((int)kRing - 1, atoi(a)));
     if (hipHostMalloc((void**)&e->ring_h, kRing * (part_len(e) + 1) * 8, hipHostMallocMapped) != hipSuccess ||
         hipHostGetDevicePointer((void**)&e->ring_d, e->ring_h, 0) != hipSuccess) {
       e->err = "round ring allocation failed";
@@ -874,8 +919,7 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
       return bail(GOSSIP_ENOMEM);
     }
     e->sx = true;
-    const char* fsb = getenv("GOSSIP_SB");  // 0: dense sharded rounds on the direct kernels
-    if ((!fsb || atoi(fsb) != 0) && sb_path_ok(e->N, e->k, e->nown)) {
+    if (!(cfg->flags & GOSSIP_FLAG_SHARD_DIRECT) && sb_path_ok(e->N, e->k, e->nown)) {
       e->sbg = make_sb_geom(e->N, e->k, e->lo, e->nown);
       if (!alloc_raw(&e->sb_mem, sb_bytes(e->sbg))) return bail(GOSSIP_ENOMEM);
       sb_carve(e->sbg, e->sb_mem, &e->sbb);
@@ -885,8 +929,6 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
     // a sparse one moves 16 B per rare node plus the cross-shard pushes, so sparse rounds pay
     // off up to a larger rare fraction than on one GPU (tools/shard_probe.py)
     e->sparse_frac = 0.25;
-    if (const char* f = getenv("GOSSIP_SPARSE_FRAC")) e->sparse_frac = atof(f);
-    if (const char* f = getenv("GOSSIP_ALLD_FRAC")) e->alld_frac = atof(f);
   }
   if (hipHostMalloc((void**)&e->partial_h, part_len(e) * 8, hipHostMallocDefault) != hipSuccess) {
     e->err = "hipHostMalloc failed";
@@ -904,6 +946,12 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
         e->err = "hipEventCreate failed";
         return bail(GOSSIP_EHIP);
       }
+    for (auto& p : e->evr)
+      for (auto& x : p)
+        if (hipEventCreate(&x) != hipSuccess) {
+          e->err = "hipEventCreate failed";
+          return bail(GOSSIP_EHIP);
+        }
   }
   // the zeroing above ran on the null stream, which the engine's non-blocking
   // stream does not wait for: finish it before any engine work is enqueued
@@ -918,7 +966,7 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
 void gossip_destroy(gossip_engine_t* eng) {
   if (!eng) return;
   (void)hipSetDevice(eng->device);
-  if (eng->stream) (void)hipStreamSynchronize(eng->stream);
+  (void)hipStreamSynchronize(eng->stream);  // (the null stream too, when bound)
   free_all(eng);
   delete eng;
 }
@@ -926,11 +974,42 @@ void gossip_destroy(gossip_engine_t* eng) {
 int gossip_set_stream(gossip_engine_t* e, void* hip_stream) {
   if (!e) return GOSSIP_EINVAL;
   if (int rc = set_dev(e)) return rc;
+  if (!e->own_stream && e->stream == (hipStream_t)hip_stream) return GOSSIP_OK;
   HIP_OK(e, hipStreamSynchronize(e->stream));
-  if (hip_stream) {
-    if (e->own_stream) HIP_OK(e, hipStreamDestroy(e->stream));
-    e->stream = (hipStream_t)hip_stream;
-    e->own_stream = false;
+  if (e->own_stream) HIP_OK(e, hipStreamDestroy(e->stream));
+  // NULL is the legacy null stream (torch's default stream), not "keep my own":
+  // a caller handing over its current stream is then ordered with its collectives
+  e->stream = (hipStream_t)hip_stream;
+  e->own_stream = false;
+  return GOSSIP_OK;
+}
+
+int gossip_set_param(gossip_engine_t* e, const char* name, double v) {
+  if (!e || !name) return GOSSIP_EINVAL;
+  const std::string n(name);
+  if (n == "sparse_frac") {
+    e->sparse_frac = v;
+  } else if (n == "alld_frac") {
+    e->alld_frac = v;
+  } else if (n == "filter_frac") {
+    e->filter_frac = v;
+  } else if (n == "ahead") {
+    if (v < 1 || v > kRing - 1) return e->fail(GOSSIP_EINVAL, "ahead must be in [1, %u]", kRing - 1);
+    e->ahead = (uint32_t)v;
+  } else if (n == "apply_grid") {
+    if (v < 0 || v > 65536) return e->fail(GOSSIP_EINVAL, "apply_grid must be in [0, 65536]");
+    e->bg.apply_grid = e->sbg.p.apply_grid = (uint32_t)v;
+  } else if (n == "ae_sparse") {
+    if (v != -1 && v != 0 && v != 1) return e->fail(GOSSIP_EINVAL, "ae_sparse must be -1, 0 or 1");
+    e->ae_force = (int)v;
+  } else if (n == "ae_cap") {
+    if (e->mode != GOSSIP_MODE_ANTIENTROPY) return e->fail(GOSSIP_ESTATE, "ae_cap needs ANTIENTROPY mode");
+    if (v < 0 || v > 4e9) return e->fail(GOSSIP_EINVAL, "ae_cap must be in [0, 4e9] (0 = default)");
+    if (int rc = set_dev(e)) return rc;
+    HIP_OK(e, hipStreamSynchronize(e->stream));
+    return ae_alloc_lists(e, (uint64_t)v);
+  } else {
+    return e->fail(GOSSIP_EINVAL, "unknown parameter '%s'", name);
   }
   return GOSSIP_OK;
 }
@@ -1008,6 +1087,8 @@ int gossip_reset(gossip_engine_t* e) {
   }
   e->fr_valid = false;
   e->sx_valid = e->gtot_valid = e->last_sparse = false;
+  // a dense_prepare or sparse plan of the old state must not leak into the next round
+  e->sb_pre = e->ev_pre_pending = e->sx_planned = false;
   if (e->frontier) {  // all-zero state: zero totals, empty bitmaps (D, P and dirty flags are zero between rounds)
     const size_t nwb = (e->N + 63) / 64 * 8;
     HIP_OK(e, hipMemsetAsync(e->fb.nzb, 0, nwb, e->stream));
@@ -1395,6 +1476,7 @@ int gossip_reset_timing(gossip_engine_t* e) {
     e->time_ms[w] = 0;
     e->launches[w] = 0;
   }
+  for (auto& r : e->evr_round) r = -1;  // (pending per-round events are dropped with the totals)
   return GOSSIP_OK;
 }
 

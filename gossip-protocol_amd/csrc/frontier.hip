@@ -538,8 +538,7 @@ hipError_t launch_frontier_round(const FrontierBufs& f, uint64_t* S, uint64_t N,
   }
 #undef GOSSIP_SCAN
   const hipError_t ce = launch_frontier_commit(f, S, N, partial, R, all_d, flags, st);
-  if (ce != hipSuccess) return ce;
-  return launch_round_snapshot(partial, rs, st);
+  return ce;  // the engine enqueues the round's snapshot (round.h) after its timing event
 }
 
 }  // namespace gossip

@@ -14,6 +14,8 @@ FLAG_HASH = 1 << 0
 FLAG_TIMING = 1 << 1
 FLAG_DIRECT = 1 << 2
 FLAG_DENSE = 1 << 3
+FLAG_SHARD_DIRECT = 1 << 4
+FLAG_AE_DIRECT_SCAN = 1 << 5
 
 STATUS = {0: "OK", -1: "EINVAL", -2: "EHIP", -3: "ENOMEM", -4: "ESTATE", -5: "ENODEV", -6: "ENOTSUP"}
 
@@ -33,7 +35,7 @@ class Config(C.Structure):
         ("churn_recover", C.c_uint32),
         ("edge_loss", C.c_uint32),
         ("partitions", C.c_uint32),
-        ("reserved", C.c_uint32 * 1),
+        ("stall_rounds", C.c_uint32),
     ]
 
 
@@ -66,6 +68,7 @@ SIGNATURES = [
     ("inject", C.c_int, [P, C.c_uint64, C.c_uint32]),
     ("inject_random", C.c_int, [P]),
     ("set_faults", C.c_int, [P, C.c_uint32, C.c_uint32]),
+    ("set_param", C.c_int, [P, C.c_char_p, C.c_double]),
     ("step", C.c_int, [P, C.c_uint32, C.POINTER(RoundStats), U64P, U32P]),
     ("partial_len", C.c_uint64, [P]),
     ("exchange_buffers", C.c_int, [P, C.POINTER(P), C.POINTER(P), U64P]),

@@ -62,7 +62,8 @@ def churn_threshold(p: float) -> int:
 
 def make_config(n_nodes: int, n_rumors: int = 1, mode="push", fanout: int = 1, seed: int = 0,
                 flags: int = 0, device: int = -1, shard_rank: int = 0, shard_count: int = 1,
-                churn_fail: int = 0, churn_recover: int = 0, edge_loss: int = 0, partitions: int = 0) -> Config:
+                churn_fail: int = 0, churn_recover: int = 0, edge_loss: int = 0, partitions: int = 0,
+                stall_rounds: int = 0) -> Config:
     cfg = Config()
     cfg.n_nodes = n_nodes
     cfg.n_rumors = n_rumors
@@ -77,6 +78,7 @@ def make_config(n_nodes: int, n_rumors: int = 1, mode="push", fanout: int = 1, s
     cfg.churn_recover = churn_recover
     cfg.edge_loss = edge_loss
     cfg.partitions = partitions
+    cfg.stall_rounds = stall_rounds
     return cfg
 
 
@@ -90,7 +92,7 @@ class AbiEngine:
 
     on_device = False
 
-    def __init__(self, lib: C.CDLL, prefix: str, cfg: Config, create_extra=()):
+    def __init__(self, lib: C.CDLL, prefix: str, cfg: Config, create_extra=(), params=None):
         self._lib, self._p = lib, prefix
         self.cfg = cfg
         h = C.c_void_p()
@@ -104,6 +106,8 @@ class AbiEngine:
         lo, hi = C.c_uint64(), C.c_uint64()
         self._check(self._fn("shard_range")(self._h, C.byref(lo), C.byref(hi)))
         self.lo, self.hi = lo.value, hi.value
+        for name, value in (params or {}).items():
+            self.set_param(name, value)
 
     # -- plumbing ---------------------------------------------------------
     def _fn(self, name):
@@ -148,6 +152,10 @@ class AbiEngine:
         self._check(self._fn("set_topology_csr")(
             self._h, row_ptr.ctypes.data_as(_abi.U32P), colp.ctypes.data_as(_abi.U32P),
             C.c_uint64(row_ptr.size - 1), C.c_uint64(col.size)))
+
+    def set_param(self, name: str, value: float):
+        """Tuning / path-selection knob (gossip_set_param): moves time, never a result bit."""
+        self._check(self._fn("set_param")(self._h, name.encode(), C.c_double(value)))
 
     def set_faults(self, edge_loss: int = 0, partitions: int = 0):
         """Fault model for the following rounds."""
@@ -284,17 +292,22 @@ class Engine(AbiEngine):
 
     def __init__(self, n_nodes: int, n_rumors: int = 1, mode="push", fanout: int = 1, seed: int = 0,
                  flags: int = 0, device: int = -1, shard_rank: int = 0, shard_count: int = 1,
-                 churn_fail: int = 0, churn_recover: int = 0, edge_loss: int = 0, partitions: int = 0):
+                 churn_fail: int = 0, churn_recover: int = 0, edge_loss: int = 0, partitions: int = 0,
+                 stall_rounds: int = 0, params=None):
         cfg = make_config(n_nodes, n_rumors, mode, fanout, seed, flags, device, shard_rank, shard_count,
-                          churn_fail, churn_recover, edge_loss, partitions)
-        super().__init__(load_library(), "gossip_", cfg)
+                          churn_fail, churn_recover, edge_loss, partitions, stall_rounds)
+        super().__init__(load_library(), "gossip_", cfg, params=params)
         # None = the caller's current HIP device.  torch is not touched here: it bundles its own
         # HIP runtime, which cannot initialise after this library's in a process that did not
         # import torch first (the drivers in gossip_hip.sharded resolve None themselves)
         self.device = device if device >= 0 else None
 
     def set_stream(self, hip_stream: int):
-        self._check(self._fn("set_stream")(self._h, C.c_void_p(hip_stream)))
+        """Binds the engine to a HIP stream handle (0 = the null stream, torch's default)."""
+        if getattr(self, "_stream", None) == hip_stream:
+            return
+        self._check(self._fn("set_stream")(self._h, C.c_void_p(hip_stream or None)))
+        self._stream = hip_stream
 
     def kernel_time(self, which: int):
         ms, n = C.c_double(), C.c_uint64()

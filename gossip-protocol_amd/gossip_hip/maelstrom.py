@@ -56,41 +56,94 @@ def tree_topology(n: int, branching: int = 2) -> dict:
 
 
 class Cluster:
-    """N Maelstrom nodes in one engine, FLOOD mode (reference-faithful)."""
+    """N Maelstrom nodes in one or more engines, FLOOD mode (reference-faithful).
 
-    def __init__(self, n_nodes: int, max_values: int = 64, engine_factory=None):
-        factory = engine_factory or (lambda **kw: Engine(**kw))
-        self.engine = factory(n_nodes=n_nodes, n_rumors=max_values, mode="flood", fanout=0, seed=0)
+    The reference's MessageKeeper holds any number of values (main.go:35-39).  Each
+    engine holds `page_values` rumor slots; the values fill pages in arrival order and a
+    full page opens the next engine.  FLOOD rounds are independent per value bit, so a
+    value's flood in its page is exactly its flood in one big engine.
+
+    Broadcasts before any `topology`: the reference gossips them over a nil topology
+    (main.go:72 ranges over no neighbours) and never forwards them later; here the page
+    runs one round over an empty topology, which marks them forwarded (S_{t-1} = S_t).
+    """
+
+    def __init__(self, n_nodes: int, max_values: int = 0, engine_factory=None, page_values: int = 1024):
+        self._factory = engine_factory or (lambda **kw: Engine(**kw))
         self.n = n_nodes
+        self.max_values = max_values          # 0 = no limit
+        self.page_values = max(1, min(page_values, 4096) if not max_values else min(page_values, max_values, 4096))
         self.ids = [node_id(i) for i in range(n_nodes)]
         self.index = {s: i for i, s in enumerate(self.ids)}
-        self.slot_of = {}    # value -> slot   (≙ MessageKeeper.broadcasted, main.go:24)
-        self.values = []     # slot -> value   (≙ MessageKeeper.messages, main.go:23)
+        self.slot_of = {}    # value -> global slot   (≙ MessageKeeper.broadcasted, main.go:24)
+        self.values = []     # global slot -> value   (≙ MessageKeeper.messages, main.go:23)
+        self.pages = []      # engines; slot s lives in pages[s // page_values], bit s % page_values
+        self.adj = [[] for _ in range(n_nodes)]
         self.has_topology = False
+        self._dirty = set()  # pages with values injected since their last gossip
+        self._new_page()
+
+    @property
+    def engine(self):
+        """The first page (single-page clusters: the engine)."""
+        return self.pages[0]
+
+    def _new_page(self):
+        e = self._factory(n_nodes=self.n, n_rumors=self.page_values, mode="flood", fanout=0, seed=0)
+        e.set_topology(self.adj)  # empty until the topology message arrives
+        self.pages.append(e)
+        return e
 
     def topology(self, topo: dict) -> None:
         """`topology` handler (main.go:132-149): replaces the neighbour map wholesale."""
         adj = [[] for _ in range(self.n)]
         for src, nbrs in topo.items():
             adj[self.index[src]] = [self.index[v] for v in nbrs]
-        self.engine.set_topology(adj)
+        self.adj = adj
+        for e in self.pages:
+            e.set_topology(adj)
         self.has_topology = True
 
     def broadcast(self, node: str, message: int) -> None:
         """Client `broadcast` of `message` to `node` (main.go:102-121)."""
         slot = self.slot_of.get(message)
         if slot is None:
-            if len(self.values) >= self.engine.n_rumors:
-                raise ValueError(f"more than {self.engine.n_rumors} distinct values")
+            if self.max_values and len(self.values) >= self.max_values:
+                raise ValueError(f"more than {self.max_values} distinct values")
             slot = len(self.values)
             self.slot_of[message] = slot
             self.values.append(message)
-        self.engine.inject(self.index[node], slot)
+            if slot // self.page_values >= len(self.pages):
+                self._new_page()
+        p = slot // self.page_values
+        self.pages[p].inject(self.index[node], slot % self.page_values)
+        self._dirty.add(p)
 
     def gossip(self, max_rounds: int = 1 << 16):
-        """Runs flood rounds until every node holds every value or nothing is in flight."""
-        return self.engine.step(max_rounds)
+        """Runs flood rounds until every node holds every value or nothing is in flight
+        (every page that received a broadcast since its last gossip).  Returns the
+        result of the last page stepped; `messages` of all pages are summed per round."""
+        res = None
+        for p in sorted(self._dirty):
+            r = self.pages[p].step(max_rounds if self.has_topology else 1)
+            if res is None:
+                res = r
+            else:  # merge: rounds = the longest flood, messages added per round
+                for i, st in enumerate(r.stats):
+                    if i < len(res.stats):
+                        res.stats[i]["messages"] += st["messages"]
+                    else:
+                        res.stats.append(dict(st))
+                res.rounds = max(res.rounds, r.rounds)
+        self._dirty.clear()
+        if res is None:
+            res = self.pages[0].step(0)
+        return res
 
     def read(self, node: str) -> list:
         """`read` handler (main.go:123-130)."""
-        return [self.values[s] for s in self.engine.read(self.index[node]) if s < len(self.values)]
+        out = []
+        for p, e in enumerate(self.pages):
+            base = p * self.page_values
+            out.extend(self.values[base + s] for s in e.read(self.index[node]) if base + s < len(self.values))
+        return out

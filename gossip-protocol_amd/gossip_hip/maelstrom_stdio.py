@@ -18,7 +18,10 @@ Handler errors reply like the maelstrom Go library: code 10 (not supported)
 for an unknown type, 13 (crash) for a body that does not decode
 (main.go:104-106, 138-140 return the unmarshal error to the library).
 
-    python -m gossip_hip.maelstrom_stdio --max-values 64 < requests.jsonl
+    python -m gossip_hip.maelstrom_stdio < requests.jsonl
+
+Any number of distinct values (the reference's MessageKeeper has no limit,
+main.go:35-39): they fill engine pages of --page-values rumor slots each.
 """
 from __future__ import annotations
 
@@ -35,8 +38,9 @@ ERR_CRASH = 13
 class MaelstromServer:
     """Answers Maelstrom messages addressed to any node of one in-engine cluster."""
 
-    def __init__(self, max_values: int = 64, engine_factory=None):
+    def __init__(self, max_values: int = 0, engine_factory=None, page_values: int = 1024):
         self.max_values = max_values
+        self.page_values = page_values
         self.engine_factory = engine_factory
         self.cluster: Cluster | None = None
         self.node_ids: list[str] = []
@@ -64,7 +68,7 @@ class MaelstromServer:
         if self.cluster is None:
             self.node_ids = list(ids)
             kw = {} if self.engine_factory is None else {"engine_factory": self.engine_factory}
-            self.cluster = Cluster(len(ids), max_values=self.max_values, **kw)
+            self.cluster = Cluster(len(ids), max_values=self.max_values, page_values=self.page_values, **kw)
             if self.cluster.ids != self.node_ids:
                 raise ValueError("node_ids must be n0..n{N-1}")
         elif list(ids) != self.node_ids:
@@ -88,7 +92,7 @@ class MaelstromServer:
         self.stats["broadcasts"] += 1
         before = set(self.cluster.read(req["dest"]))
         self.cluster.broadcast(req["dest"], msg)
-        if msg not in before and self.topology_set:  # dedupe (main.go:113), then Gossip (:118)
+        if msg not in before:  # dedupe (main.go:113), then Gossip (:118); no topology yet: nil neighbours
             res = self.cluster.gossip()
             self.stats["gossip_rounds"] += res.rounds
             self.stats["gossip_messages"] += sum(s["messages"] for s in res.stats)
@@ -130,9 +134,10 @@ class MaelstromServer:
 
 def main(argv=None) -> None:
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
-    ap.add_argument("--max-values", type=int, default=64, help="distinct broadcast values (rumor slots)")
+    ap.add_argument("--max-values", type=int, default=0, help="limit on distinct broadcast values (0 = none)")
+    ap.add_argument("--page-values", type=int, default=1024, help="rumor slots per engine page (<= 4096)")
     args = ap.parse_args(argv)
-    MaelstromServer(args.max_values).serve()
+    MaelstromServer(args.max_values, page_values=args.page_values).serve()
 
 
 if __name__ == "__main__":

@@ -157,9 +157,22 @@ def _sparse_round(engine, comm: _Comm) -> np.ndarray:
     return engine.sparse_commit(n_in)
 
 
+def _bind_stream(engine, comm: _Comm):
+    """Device collectives are enqueued on torch's current stream (the RCCL stream waits for
+    it, and work.wait() / a synchronous collective make it wait in turn): the engine must
+    launch on that same stream, or its kernels could read the image before the all-gather
+    wrote it.  torch's default stream is the null stream (cuda_stream 0), which
+    gossip_set_stream binds as such."""
+    if comm.direct:
+        engine.set_stream(torch.cuda.current_stream().cuda_stream)
+
+
 def sharded_round(engine, group=None) -> dict:
-    """Runs one round of a sharded engine; every rank must call it."""
+    """Runs one round of a sharded engine; every rank must call it.  With RCCL the engine is
+    bound to the caller's current torch stream, so every kernel is ordered after the
+    collectives that feed it."""
     comm = _Comm(engine, group)
+    _bind_stream(engine, comm)
     partial = _sparse_round(engine, comm) if _plan(engine, comm) == 1 else _dense_round(engine, comm)
     if comm.world > 1:
         partial = comm.all_reduce_sum(partial)

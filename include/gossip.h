@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define GOSSIP_ABI_VERSION 3u
+#define GOSSIP_ABI_VERSION 4u
 
 /* Dissemination modes. */
 enum gossip_mode {
@@ -63,8 +63,12 @@ enum gossip_flags {
   GOSSIP_FLAG_TIMING = 1u << 1, /* bracket hot kernels with hipEvents (gossip_kernel_time) */
   GOSSIP_FLAG_DIRECT = 1u << 2, /* random modes: direct random-access kernels instead of the
                                    binned (LDS) pipeline — same results, for A/B checks */
-  GOSSIP_FLAG_DENSE = 1u << 3   /* random modes: every round on the dense binned pipeline, no
+  GOSSIP_FLAG_DENSE = 1u << 3,  /* random modes: every round on the dense binned pipeline, no
                                    sparse (frontier) rounds — same results, for A/B checks */
+  GOSSIP_FLAG_SHARD_DIRECT = 1u << 4,  /* sharded engines: dense rounds on the direct kernels instead
+                                          of the binned push / pull passes — same results, A/B */
+  GOSSIP_FLAG_AE_DIRECT_SCAN = 1u << 5 /* ANTIENTROPY: sparse rounds probe the peers' bitmap words
+                                          directly instead of binning by tile — same results, A/B */
 };
 
 typedef struct gossip_config {
@@ -82,9 +86,14 @@ typedef struct gossip_config {
   uint32_t churn_recover; /* ANTIENTROPY: P(dead -> alive) per round, as x / 2^32      */
   uint32_t edge_loss;   /* random modes: P(an edge's exchange is lost) per round, x / 2^32
                            (the reference's lossy SyncRPC, main.go:77-87) */
-  uint32_t partitions;  /* random modes: 0/1 = none, P > 1 = nodes split into P contiguous
-                           blocks that cannot reach each other                          */
-  uint32_t reserved[1]; /* must be zero                                               */
+  uint32_t partitions;  /* random modes and FLOOD: 0/1 = none, P > 1 = nodes split into P
+                           contiguous blocks that cannot reach each other               */
+  uint32_t stall_rounds; /* 0 = off.  D > 0: the reference's deadline stall (DESIGN.md §2.9,
+                           main.go:77-87: one 2 s context per neighbour, retried forever
+                           once it expired).  FLOOD: a value still undelivered on an edge
+                           D rounds after its first attempt is never sent on it again.
+                           Random modes: a node whose exchanges were lost in D rounds in a
+                           row stops initiating exchanges until reset.  <= 16.           */
 } gossip_config_t;
 
 /* Stats of one round t: they describe S_{t+1}, the state the round produced. */
@@ -110,8 +119,25 @@ void gossip_destroy(gossip_engine_t* eng);
 /* Last error message of eng, or of the last failed gossip_create when eng is NULL. */
 const char* gossip_last_error(const gossip_engine_t* eng);
 
-/* Launch all work on this hipStream_t (NULL = the engine's own stream). */
+/* Launch all work on this hipStream_t from now on.  NULL binds the legacy null
+ * stream (torch's default stream is the null stream: its cuda_stream is 0), so a
+ * caller that passes its current stream is always ordered with the work it
+ * enqueues there, e.g. RCCL collectives.  The engine finishes the work on its
+ * previous stream first. */
 int gossip_set_stream(gossip_engine_t* eng, void* hip_stream);
+
+/* Tuning and path-selection knobs, for tests and benchmarks (the library reads no
+ * environment variables).  Every value only moves time, never a result bit:
+ *   "sparse_frac"  random modes: a round runs sparse when the rare class is at most
+ *                  this fraction of N (default 1/16, sharded 1/4; < 0 never, >= 1 always)
+ *   "alld_frac"    sparse rounds commit every group's D once k x rare >= this x N
+ *   "filter_frac"  dense rounds drop edges by the peer's class above this empty/full fraction
+ *   "ahead"        rounds enqueued ahead of the stats read back (1..7, default 2)
+ *   "apply_grid"   persistent blocks of the dense apply pass (0 = one block per tile)
+ *   "ae_sparse"    ANTIENTROPY: -1 plan sparse rounds (default), 0 never, 1 whenever valid
+ *   "ae_cap"       ANTIENTROPY: edge-list capacity of sparse rounds (reallocates the list)
+ * Unknown names return GOSSIP_EINVAL. */
+int gossip_set_param(gossip_engine_t* eng, const char* name, double value);
 
 /* FLOOD peer source: directed adjacency Topology[u] = col[row_ptr[u]..row_ptr[u+1]),
  * global node ids, n == N.  Copied; never retained. */
@@ -130,8 +156,9 @@ int gossip_inject(gossip_engine_t* eng, uint64_t node, uint32_t rumor);
  * ANTIENTROPY: initial versions V[n][c] = Philox tag-3 draw & 0xFFFF. */
 int gossip_inject_random(gossip_engine_t* eng);
 
-/* Fault model for the rounds that follow (random modes): same meaning as the
- * config fields; e.g. heal a partition between steps with partitions = 0. */
+/* Fault model for the rounds that follow: same meaning as the config fields;
+ * e.g. heal a partition between steps with partitions = 0.  FLOOD with faults
+ * retries undelivered values every round (one shard only). */
 int gossip_set_faults(gossip_engine_t* eng, uint32_t edge_loss, uint32_t partitions);
 
 /* Runs rounds until converged or max_rounds rounds have run (single shard only,
@@ -210,9 +237,12 @@ int gossip_philox_device(gossip_engine_t* eng, const uint32_t* ctr4, const uint3
                          uint32_t* out4, uint32_t n);
 
 /* GOSSIP_FLAG_TIMING: accumulated device time (ms) and count of `which`:
- * 0 = the whole S_t -> S_{t+1} transform of a round (all its kernels),
+ * 0 = the whole S_t -> S_{t+1} transform of a round (all its kernels; binned engines: the
+ *     whole gossip_step, gaps between rounds included, launches = rounds),
  * 1 = the separate stats kernel (direct path only; fused in the binned path),
- * 2 = ANTIENTROPY sparse rounds' kernels (their stats pass counts under 1; dense rounds under 0). */
+ * 2 = ANTIENTROPY sparse rounds' kernels (their stats pass counts under 1; dense rounds under 0),
+ * 3 = dense rounds of a binned engine: emit + transpose + serve + apply of each round,
+ * 4 = sparse (frontier) rounds of a binned engine: summary + scan + commit of each round. */
 int gossip_kernel_time(const gossip_engine_t* eng, uint32_t which, double* total_ms, uint64_t* launches);
 int gossip_reset_timing(gossip_engine_t* eng);
 

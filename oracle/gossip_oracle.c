@@ -181,8 +181,6 @@ int oracle_create(const gossip_config_t* cfg, int threads, oracle_sim_t** out) {
   s->gtot = (uint64_t*)calloc(5 + s->R, 8);
   s->counts = (uint64_t*)calloc(G, 8);
   s->sparse_frac = 0.25;
-  const char* f = getenv("GOSSIP_SPARSE_FRAC");
-  if (f) s->sparse_frac = atof(f);
   if (!s->gtot || !s->counts) {
     oracle_destroy(s);
     return GOSSIP_ENOMEM;
@@ -737,6 +735,21 @@ int oracle_sparse_commit(oracle_sim_t* s, uint64_t items, uint64_t* partial) {
   s->planned = 0;
   s->last_sparse = 1;
   return GOSSIP_OK;
+}
+
+/* gossip_set_param: the engine's tuning knobs.  Only sparse_frac matters here (it picks the
+ * sharded round protocol, which the gloo tests exercise); the rest steer engine kernel
+ * choices that this restatement does not have, and are accepted as no-ops. */
+int oracle_set_param(oracle_sim_t* s, const char* name, double value) {
+  if (!s || !name) return GOSSIP_EINVAL;
+  if (!strcmp(name, "sparse_frac")) {
+    s->sparse_frac = value;
+    return GOSSIP_OK;
+  }
+  const char* known[] = {"alld_frac", "filter_frac", "ahead", "apply_grid", "ae_sparse", "ae_cap"};
+  for (size_t i = 0; i < sizeof known / sizeof known[0]; ++i)
+    if (!strcmp(name, known[i])) return GOSSIP_OK;
+  return GOSSIP_EINVAL;
 }
 
 int oracle_set_faults(oracle_sim_t* s, uint32_t edge_loss, uint32_t partitions) {

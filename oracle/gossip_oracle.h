@@ -45,6 +45,7 @@ int oracle_reset(oracle_sim_t* s);
 int oracle_inject(oracle_sim_t* s, uint64_t node, uint32_t rumor);
 int oracle_inject_random(oracle_sim_t* s);
 int oracle_set_faults(oracle_sim_t* s, uint32_t edge_loss, uint32_t partitions);
+int oracle_set_param(oracle_sim_t* s, const char* name, double value);
 int oracle_step(oracle_sim_t* s, uint32_t max_rounds, gossip_round_stats_t* stats,
                 uint64_t* infected, uint32_t* rounds_done);
 

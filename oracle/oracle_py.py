@@ -48,10 +48,10 @@ class OracleEngine(AbiEngine):
 
     def __init__(self, n_nodes, n_rumors=1, mode="push", fanout=1, seed=0, flags=0,
                  shard_rank=0, shard_count=1, threads=1, device=-1, churn_fail=0, churn_recover=0,
-                 edge_loss=0, partitions=0):
+                 edge_loss=0, partitions=0, stall_rounds=0, params=None):
         cfg = make_config(n_nodes, n_rumors, mode, fanout, seed, flags, -1, shard_rank, shard_count,
-                          churn_fail, churn_recover, edge_loss, partitions)
-        super().__init__(load_oracle(), "oracle_", cfg, create_extra=(C.c_int(threads),))
+                          churn_fail, churn_recover, edge_loss, partitions, stall_rounds)
+        super().__init__(load_oracle(), "oracle_", cfg, create_extra=(C.c_int(threads),), params=params)
 
 
 def philox(ctr, key):

@@ -29,7 +29,16 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert eng_mod.load_library().gossip_abi_version() == 3
+    assert eng_mod.load_library().gossip_abi_version() == 4
+
+
+def test_library_reads_no_environment():
+    """Path knobs are gossip_set_param / config flags: an inherited environment variable
+    cannot change a production caller's round path."""
+    csrc = os.path.join(ROOT, "gossip-protocol_amd", "csrc")
+    for name in os.listdir(csrc):
+        src = open(os.path.join(csrc, name)).read()
+        assert "getenv" not in src, name
 
 
 def test_struct_layout():
@@ -66,3 +75,5 @@ def test_bad_config_rejected():
     assert lib.gossip_create(C.byref(cfg), C.byref(h)) == -6
     cfg = eng_mod.make_config(100, 1, 7, 1, 1)  # unknown mode
     assert lib.gossip_create(C.byref(cfg), C.byref(h)) == -6
+    cfg = eng_mod.make_config(100, 1, "push", 2, 1, stall_rounds=17)  # deadline out of range
+    assert lib.gossip_create(C.byref(cfg), C.byref(h)) == -1

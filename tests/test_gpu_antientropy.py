@@ -3,10 +3,10 @@ bit-exact per round: stats, per-component counts, hash, and the rows and alive f
 
 Paths (all must agree with the oracle and with each other):
   auto     — dense rounds until the stale nodes are few, then sparse in-place rounds
-  dense    — GOSSIP_AE_SPARSE=0: every round dense (copy + atomicMax kernel)
-  sparse   — GOSSIP_AE_SPARSE=1: every round after the first sparse (the edge list holds k*N)
-  overflow — sparse forced with a 64-edge list: rounds whose list overflows are rerun dense
-  *_direct — GOSSIP_AE_BINSCAN=0: the sparse scan probes the peers' bitmap words directly
+  dense    — ae_sparse = 0: every round dense (copy + atomicMax kernel)
+  sparse   — ae_sparse = 1: every round after the first sparse (the edge list holds k*N)
+  overflow — sparse forced with a 64-edge list (ae_cap): rounds whose list overflows are rerun dense
+  *_direct — FLAG_AE_DIRECT_SCAN: the sparse scan probes the peers' bitmap words directly
              instead of binning the exchanges by the peer's tile
 """
 import os
@@ -15,24 +15,22 @@ import numpy as np
 import pytest
 
 import oracle_py as op
-from gossip_hip import Engine
+from gossip_hip import FLAG_AE_DIRECT_SCAN, Engine
 from gossip_hip.engine import churn_threshold as ct
 
 pytestmark = pytest.mark.gpu
 THREADS = min(16, os.cpu_count() or 1)
-PATHS = {"auto": {}, "dense": {"GOSSIP_AE_SPARSE": "0"}, "sparse": {"GOSSIP_AE_SPARSE": "1"},
-         "overflow": {"GOSSIP_AE_SPARSE": "1", "GOSSIP_AE_CAP": "64"},
+# (flags, gossip_set_param knobs) per path
+PATHS = {"auto": (0, {}), "dense": (0, {"ae_sparse": 0}), "sparse": (0, {"ae_sparse": 1}),
+         "overflow": (0, {"ae_sparse": 1, "ae_cap": 64}),
          # sparse rounds with the direct scan (random bitmap probes) instead of the binned one
-         "sparse_direct": {"GOSSIP_AE_SPARSE": "1", "GOSSIP_AE_BINSCAN": "0"},
-         "auto_direct": {"GOSSIP_AE_BINSCAN": "0"}}
+         "sparse_direct": (FLAG_AE_DIRECT_SCAN, {"ae_sparse": 1}),
+         "auto_direct": (FLAG_AE_DIRECT_SCAN, {})}
 
 
-def _engine(monkeypatch, path, *args, **kw):
-    for k in ("GOSSIP_AE_SPARSE", "GOSSIP_AE_CAP", "GOSSIP_AE_BINSCAN"):
-        monkeypatch.delenv(k, raising=False)
-    for k, v in PATHS[path].items():
-        monkeypatch.setenv(k, v)
-    return Engine(*args, **kw)
+def _engine(path, *args, flags=0, **kw):
+    pf, params = PATHS[path]
+    return Engine(*args, flags=flags | pf, params=params, **kw)
 
 
 def _compare(e, o, N, K, rounds, probe):
@@ -54,10 +52,10 @@ def _compare(e, o, N, K, rounds, probe):
     (4099, 64, 3, 0.02, 0.2),
     (777, 1, 1, 0.0, 0.0),
 ])
-def test_antientropy_paths_vs_oracle(monkeypatch, path, N, K, k, fail, rec):
+def test_antientropy_paths_vs_oracle(path, N, K, k, fail, rec):
     seed = 0x5EED0005 + K
     kw = dict(flags=1, churn_fail=ct(fail), churn_recover=ct(rec))
-    e = _engine(monkeypatch, path, N, K, "antientropy", k, seed, **kw)
+    e = _engine(path, N, K, "antientropy", k, seed, **kw)
     o = op.OracleEngine(N, K, "antientropy", k, seed, threads=THREADS, **kw)
     probe = (0, 1, N // 3, N // 2, N - 1)
     for x in (e, o):
@@ -70,11 +68,11 @@ def test_antientropy_paths_vs_oracle(monkeypatch, path, N, K, k, fail, rec):
     assert res.converged
 
 
-def test_antientropy_sparse_tail_1M(monkeypatch):
+def test_antientropy_sparse_tail_1M():
     """configs[4] shape at 2^20: the churn tail runs sparse (auto) and matches the oracle."""
     N, K, k, seed = 1 << 20, 16, 1, 0x5EED0005
     kw = dict(flags=1, churn_fail=ct(0.01), churn_recover=ct(0.1))
-    e = _engine(monkeypatch, "auto", N, K, "antientropy", k, seed, **kw)
+    e = _engine("auto", N, K, "antientropy", k, seed, **kw)
     o = op.OracleEngine(N, K, "antientropy", k, seed, threads=THREADS, **kw)
     for x in (e, o):
         x.inject_random()

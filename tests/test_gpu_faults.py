@@ -18,10 +18,9 @@ CASES = [  # mode, k, R, N, seed, edge_loss, partitions
     ("pushpull", 6, 7, 1500, 3, loss_threshold(0.25), 2),
 ]
 IDS = ["pushpull-loss", "push-loss-parts", "pull-loss-parts", "pushpull-k6"]
-PATHS = {"auto": (0, {}), "dense": (FLAG_DENSE, {}), "dense_filter": (0, {"GOSSIP_SPARSE_FRAC": "-1", "GOSSIP_FILTER_FRAC": "0"}),
-         "sparse": (0, {"GOSSIP_SPARSE_FRAC": "1.0", "GOSSIP_ALLD_FRAC": "1e30"}),
-         "sparse_alld": (0, {"GOSSIP_SPARSE_FRAC": "1.0", "GOSSIP_ALLD_FRAC": "0"}), "direct": (FLAG_DIRECT, {})}
-_ENV = ("GOSSIP_SPARSE_FRAC", "GOSSIP_ALLD_FRAC", "GOSSIP_FILTER_FRAC")
+PATHS = {"auto": (0, {}), "dense": (FLAG_DENSE, {}), "dense_filter": (0, {"sparse_frac": -1, "filter_frac": 0}),
+         "sparse": (0, {"sparse_frac": 1.0, "alld_frac": 1e30}),
+         "sparse_alld": (0, {"sparse_frac": 1.0, "alld_frac": 0}), "direct": (FLAG_DIRECT, {})}
 
 
 def _oracle(case, rounds=200):
@@ -33,15 +32,11 @@ def _oracle(case, rounds=200):
 
 @pytest.mark.parametrize("path", list(PATHS))
 @pytest.mark.parametrize("case", CASES, ids=IDS)
-def test_faults_every_path_equals_oracle(case, path, monkeypatch):
+def test_faults_every_path_equals_oracle(case, path):
     mode, k, R, N, seed, loss, parts = case
     want, full = _oracle(case)
-    flags, env = PATHS[path]
-    for v in _ENV:
-        monkeypatch.delenv(v, raising=False)
-    for v, x in env.items():
-        monkeypatch.setenv(v, x)
-    e = Engine(N, R, mode, k, seed, flags=1 | flags, edge_loss=loss, partitions=parts)
+    flags, params = PATHS[path]
+    e = Engine(N, R, mode, k, seed, flags=1 | flags, edge_loss=loss, partitions=parts, params=params)
     e.inject_random()
     got = e.step(200)
     assert got.stats == want.stats
@@ -51,16 +46,13 @@ def test_faults_every_path_equals_oracle(case, path, monkeypatch):
 
 
 @pytest.mark.parametrize("plan", ["auto", "sparse", "dense"])
-def test_faults_sharded_lockstep(plan, monkeypatch):
+def test_faults_sharded_lockstep(plan):
     case = ("pushpull", 2, 64, 30011, 0x5EED0004, loss_threshold(0.25), 3)
     mode, k, R, N, seed, loss, parts = case
     want, full = _oracle(case)
-    for v in _ENV:
-        monkeypatch.delenv(v, raising=False)
-    if plan != "auto":
-        monkeypatch.setenv("GOSSIP_SPARSE_FRAC", "1.0" if plan == "sparse" else "-1")
-    engines = [Engine(N, R, mode, k, seed, flags=1, shard_rank=r, shard_count=3, edge_loss=loss, partitions=parts)
-               for r in range(3)]
+    params = {} if plan == "auto" else {"sparse_frac": 1.0 if plan == "sparse" else -1}
+    engines = [Engine(N, R, mode, k, seed, flags=1, shard_rank=r, shard_count=3, edge_loss=loss, partitions=parts,
+                      params=params) for r in range(3)]
     for e in engines:
         e.inject_random()
     got, _ = lockstep_run(engines, 200)

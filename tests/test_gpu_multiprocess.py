@@ -1,7 +1,10 @@
-"""GPU, two processes on one device: the sharded round protocol through real
-process boundaries (gloo collectives staged through host memory) with HIP
-shard engines equals a single-engine run bit for bit.  On a multi-GPU node
-the same code path uses RCCL (backend "nccl") instead."""
+"""GPU, two processes: the sharded round protocol through real process
+boundaries with HIP shard engines equals a single-engine run bit for bit.
+
+  gloo — both ranks on device 0, collectives staged through host memory;
+  nccl — RCCL collectives on engine memory, in place, with the engines bound to
+         torch's current stream (gossip_hip.sharded._bind_stream).  Needs two
+         devices (RCCL rejects two ranks on one GPU); skipped on a one-GPU box."""
 import os
 import socket
 import sys
@@ -21,7 +24,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, case, q):
+def _worker(rank, world, port, case, q, backend="gloo"):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [os.path.join(root, "gossip-protocol_amd")]
     import torch
@@ -30,19 +33,27 @@ def _worker(rank, world, port, case, q):
     from gossip_hip.sharded import sharded_run
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = rank if backend == "nccl" else 0
+    torch.cuda.set_device(dev)
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", dev))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     mode, k, R, N, seed = case
-    e = Engine(N, R, mode, k, seed, flags=1, device=0, shard_rank=rank, shard_count=world)
+    e = Engine(N, R, mode, k, seed, flags=1, device=dev, shard_rank=rank, shard_count=world)
     e.inject_random()
     stats = sharded_run(e, 100)
     q.put((rank, e.lo, e.hi, stats, e.read_shard()))
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("backend", ["gloo", "nccl"])
 @pytest.mark.parametrize("case", [("pushpull", 2, 64, 1 << 20, 0x5EED0004), ("push", 3, 1, 300001, 7)],
                          ids=["pushpull-1M", "push-ragged"])
-def test_two_processes_equal_one_engine(case):
+def test_two_processes_equal_one_engine(case, backend):
+    import torch
+    if backend == "nccl" and torch.cuda.device_count() < 2:
+        pytest.skip("RCCL needs one device per rank")
     from gossip_hip import Engine
     mode, k, R, N, seed = case
     ref = Engine(N, R, mode, k, seed, flags=1, device=0)
@@ -52,7 +63,7 @@ def test_two_processes_equal_one_engine(case):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, case, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, case, q, backend)) for r in range(2)]
     for p in procs:
         p.start()
     got = [q.get(timeout=180) for _ in range(2)]

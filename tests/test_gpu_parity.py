@@ -32,34 +32,31 @@ def test_device_philox_kat(golden):
 # round paths of the random modes, all bit-identical:
 #   auto   — default: sparse frontier rounds while one class dominates, dense binned rounds otherwise
 #   dense  — every round on the binned LDS pipeline
-#   sparse — every round on the frontier kernels (GOSSIP_SPARSE_FRAC=1 lifts the sparsity test),
+#   sparse — every round on the frontier kernels (sparse_frac = 1 lifts the sparsity test),
 #            pushes tracked by per-group dirty flags
 #   sparse_alld — the same, but every round's commit reads D of every group (no push flags)
 #   dense_filter — every round dense, emit dropping edges by the peer's class (occupancy bitmaps)
 #   direct — the random-access kernels
 PATHS = ["auto", "dense", "dense_filter", "sparse", "sparse_alld", "direct"]
 _PATH_FLAGS = {"auto": 0, "dense": FLAG_DENSE, "dense_filter": 0, "sparse": 0, "sparse_alld": 0, "direct": FLAG_DIRECT}
-# GOSSIP_ALLD_FRAC: 0 = every sparse round commits every group's D, huge = none does
-_PATH_ENV = {"dense_filter": {"GOSSIP_SPARSE_FRAC": "-1", "GOSSIP_FILTER_FRAC": "0"},
-             "sparse": {"GOSSIP_SPARSE_FRAC": "1.0", "GOSSIP_ALLD_FRAC": "1e30"},
-             "sparse_alld": {"GOSSIP_SPARSE_FRAC": "1.0", "GOSSIP_ALLD_FRAC": "0"}}
+# gossip_set_param knobs; alld_frac: 0 = every sparse round commits every group's D, huge = none does
+_PATH_PARAMS = {"dense_filter": {"sparse_frac": -1, "filter_frac": 0},
+                "sparse": {"sparse_frac": 1.0, "alld_frac": 1e30},
+                "sparse_alld": {"sparse_frac": 1.0, "alld_frac": 0}}
 
 
 @pytest.fixture
-def path(request, monkeypatch):
+def path(request):
+    """(flags, params) of one round path"""
     name = request.param
-    for var in ("GOSSIP_SPARSE_FRAC", "GOSSIP_ALLD_FRAC", "GOSSIP_FILTER_FRAC"):
-        monkeypatch.delenv(var, raising=False)
-    for var, val in _PATH_ENV.get(name, {}).items():
-        monkeypatch.setenv(var, val)
-    return _PATH_FLAGS[name]
+    return _PATH_FLAGS[name], _PATH_PARAMS.get(name, {})
 
 
 @pytest.mark.parametrize("path", PATHS, indirect=True)
 @pytest.mark.parametrize("idx", range(8))
 def test_random_golden(golden, idx, path):
     c = golden["random"][idx]
-    e = Engine(c["N"], c["R"], c["mode"], c["k"], c["seed"], flags=1 | path)
+    e = Engine(c["N"], c["R"], c["mode"], c["k"], c["seed"], flags=1 | path[0], params=path[1])
     inject_case(e, c["inject"])
     res = e.step(256)
     assert res.rounds == len(c["rounds"])
@@ -98,9 +95,9 @@ def _oracle_run(cfg, inj, rounds, threads):
     return _ORACLE_CACHE[key]
 
 
-def _compare(cfg, inj="random", rounds=256, threads=THREADS, path=0):
+def _compare(cfg, inj="random", rounds=256, threads=THREADS, path=(0, {})):
     N, R, mode, k, seed = cfg
-    e = Engine(N, R, mode, k, seed, flags=1 | path)
+    e = Engine(N, R, mode, k, seed, flags=1 | path[0], params=path[1])
     inject_case(e, inj)
     re_ = e.step(rounds)
     ro, oshard = _oracle_run(cfg, inj, rounds, threads)
@@ -152,7 +149,7 @@ def test_inject_between_steps(path):
     """A client broadcast between rounds (main.go:102-117) invalidates the
     engine's running totals and occupancy bitmaps; the next round rebuilds them."""
     cfg = (200003, 11, "pushpull", 2, 0x5EED0007)
-    e = Engine(*cfg, flags=1 | path)
+    e = Engine(*cfg, flags=1 | path[0], params=path[1])
     o = op.OracleEngine(*cfg, flags=1, threads=THREADS)
     for x in (e, o):
         x.inject(5, 0)

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 import torch
 
-from gossip_hip import Engine
+from gossip_hip import FLAG_SHARD_DIRECT, Engine
 from gossip_hip.sharded import lockstep_run as run_lockstep
 
 pytestmark = pytest.mark.gpu
@@ -17,27 +17,25 @@ pytestmark = pytest.mark.gpu
 CASES = [("pushpull", 2, 64, 1 << 20, 0x5EED0004, 4), ("push", 3, 1, 300001, 7, 3),
          ("pull", 1, 5, 100000, 11, 2), ("pushpull", 6, 7, 50001, 3, 2)]
 IDS = ["pushpull-1M-G4", "push-ragged-G3", "pull-G2", "pushpull-k6-G2"]
-PLANS = {"auto": {}, "sparse": {"GOSSIP_SPARSE_FRAC": "1.0"}, "sparse_alld": {"GOSSIP_SPARSE_FRAC": "1.0",
-         "GOSSIP_ALLD_FRAC": "0"}, "dense": {"GOSSIP_SPARSE_FRAC": "-1"},
+# (flags, gossip_set_param knobs) per plan
+PLANS = {"auto": (0, {}), "sparse": (0, {"sparse_frac": 1.0}), "sparse_alld": (0, {"sparse_frac": 1.0, "alld_frac": 0}),
+         "dense": (0, {"sparse_frac": -1}),
          # dense sharded rounds on the direct kernels instead of the binned push/pull passes
-         "dense_direct": {"GOSSIP_SPARSE_FRAC": "-1", "GOSSIP_SB": "0"}, "auto_direct": {"GOSSIP_SB": "0"}}
-_ENV = ("GOSSIP_SPARSE_FRAC", "GOSSIP_ALLD_FRAC", "GOSSIP_SB")
+         "dense_direct": (FLAG_SHARD_DIRECT, {"sparse_frac": -1}), "auto_direct": (FLAG_SHARD_DIRECT, {})}
 
 
 @pytest.mark.parametrize("plan", list(PLANS))
 @pytest.mark.parametrize("case", CASES, ids=IDS)
-def test_lockstep_shards_equal_one_engine(case, plan, monkeypatch):
+def test_lockstep_shards_equal_one_engine(case, plan):
     mode, k, R, N, seed, G = case
-    for var in _ENV:
-        monkeypatch.delenv(var, raising=False)
     ref = Engine(N, R, mode, k, seed, flags=1)
     ref.inject_random()
     want = ref.step(200)
     full = ref.read_shard()
     ref.close()
-    for var, val in PLANS[plan].items():
-        monkeypatch.setenv(var, val)
-    engines = [Engine(N, R, mode, k, seed, flags=1, shard_rank=r, shard_count=G) for r in range(G)]
+    flags, params = PLANS[plan]
+    engines = [Engine(N, R, mode, k, seed, flags=1 | flags, shard_rank=r, shard_count=G, params=params)
+               for r in range(G)]
     for e in engines:
         e.inject_random()
     got, kinds = run_lockstep(engines, 200)
@@ -70,20 +68,18 @@ def test_lockstep_inject_between_steps():
         assert np.array_equal(e.read_shard(), full[:, e.lo:e.hi])
 
 
-def test_lockstep_dense_past_4096_tiles(monkeypatch):
+def test_lockstep_dense_past_4096_tiles():
     """Above 2^26 nodes the pull pass of a dense sharded round bins into more than 4096
     image tiles (binned.h: kSbMaxTiles); odd shard size, so every slice but the first
     starts 8-B aligned.  Reference: one engine (direct kernels at this size)."""
-    for var in _ENV:
-        monkeypatch.delenv(var, raising=False)
     N, R, G = (1 << 26) + 12345, 64, 2
     ref = Engine(N, R, "pushpull", 2, 0x5EED0004, flags=1)
     ref.inject_random()
     want = ref.step(8)
     full = ref.read_shard()
     ref.close()
-    monkeypatch.setenv("GOSSIP_SPARSE_FRAC", "-1")
-    engines = [Engine(N, R, "pushpull", 2, 0x5EED0004, flags=1, shard_rank=r, shard_count=G) for r in range(G)]
+    engines = [Engine(N, R, "pushpull", 2, 0x5EED0004, flags=1, shard_rank=r, shard_count=G,
+                      params={"sparse_frac": -1}) for r in range(G)]
     for e in engines:
         e.inject_random()
     got, kinds = run_lockstep(engines, 8)

@@ -74,3 +74,40 @@ def test_stdio_errors_oracle():
 @pytest.mark.gpu
 def test_stdio_cluster_gpu():
     _check_cluster(MaelstromServer(max_values=8))
+
+
+def _oracle_factory(**kw):
+    return op.OracleEngine(**kw)
+
+
+def test_stdio_many_values_pages_oracle():
+    """A standard broadcast workload sends thousands of distinct values (the reference's
+    MessageKeeper has no limit, main.go:35-39): they spill over engine pages."""
+    s = MaelstromServer(engine_factory=_oracle_factory, page_values=64)
+    n = 9
+    values = [(f"n{i % n}", 10_000 + i) for i in range(300)]
+    replies = _run(s, _script(n, values))
+    assert len(s.cluster.pages) == 5  # ceil(300 / 64)
+    for r in replies:
+        if r["body"]["type"] == "read_ok":
+            assert sorted(r["body"]["messages"]) == [v for _, v in values]
+    assert [r["body"]["type"] for r in replies].count("broadcast_ok") == 300
+
+
+def test_broadcast_before_topology_is_never_forwarded():
+    """main.go:72 ranges over a nil Topology for a broadcast that arrives before `topology`:
+    the value is recorded and acked but never forwarded, also not after the topology
+    arrives; later values flood as usual."""
+    n = 9
+    ids = [f"n{i}" for i in range(n)]
+    s = MaelstromServer(engine_factory=_oracle_factory)
+    msgs = [{"src": "c0", "dest": i, "body": {"type": "init", "msg_id": 1, "node_id": i, "node_ids": ids}}
+            for i in ids]
+    msgs.append({"src": "c2", "dest": "n4", "body": {"type": "broadcast", "message": 5, "msg_id": 3}})
+    msgs += [{"src": "c1", "dest": i, "body": {"type": "topology", "msg_id": 2, "topology": grid_topology(n)}}
+             for i in ids]
+    msgs.append({"src": "c2", "dest": "n0", "body": {"type": "broadcast", "message": 6, "msg_id": 4}})
+    msgs += [{"src": "c3", "dest": i, "body": {"type": "read", "msg_id": 99}} for i in ids]
+    reads = {r["src"]: sorted(r["body"]["messages"]) for r in _run(s, msgs) if r["body"]["type"] == "read_ok"}
+    assert reads["n4"] == [5, 6]
+    assert all(reads[i] == [6] for i in ids if i != "n4")

@@ -40,7 +40,7 @@ def _faults(name):
     return {"edge_loss": 1 << 30, "partitions": 3} if name.endswith("-faults") else {}
 
 
-PLANS = {"auto": None, "sparse": "1.0", "dense": "-1"}  # GOSSIP_SPARSE_FRAC
+PLANS = {"auto": None, "sparse": 1.0, "dense": -1}  # sparse_frac (gossip_set_param)
 
 
 def _worker(rank, world, port, case, q, frac=None):
@@ -51,11 +51,10 @@ def _worker(rank, world, port, case, q, frac=None):
     from gossip_hip.sharded import sharded_run
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    if frac is not None:
-        os.environ["GOSSIP_SPARSE_FRAC"] = frac
     dist.init_process_group("gloo", rank=rank, world_size=world)
     mode, k, R, N, seed, topo = case
-    e = op.OracleEngine(N, R, mode.split("-")[0], k, seed, flags=1, shard_rank=rank, shard_count=world, **_faults(mode))
+    e = op.OracleEngine(N, R, mode.split("-")[0], k, seed, flags=1, shard_rank=rank, shard_count=world, **_faults(mode),
+                        params={} if frac is None else {"sparse_frac": frac})
     if topo:
         e.set_topology(_grid(N))
         e.inject(0, 0); e.inject(N - 1, 1); e.inject(N // 2, 2)
