@@ -18,7 +18,8 @@ constexpr uint32_t kTileD = 16384;   // destination tile (nodes): one 128 KiB LD
 constexpr uint32_t kTileDLog = 14;
 constexpr uint32_t kRecPerRegion = 16384;  // records staged per sender tile (LDS, 4 B each)
 constexpr uint32_t kMaxSenders = 8192;     // senders per sender tile (their values staged once, 8 B each)
-constexpr uint32_t kMaxTilesD = 4096;     // N <= 2^26 on this path (and <= 4096 sender regions)
+constexpr uint32_t kMaxTilesD = 4096;     // tiles with sender values staged in LDS (N <= 2^26); past it, up to
+                                          // kSbMaxTiles (2^27 nodes), emit re-reads them from S
 
 // Sharded dense rounds (sb_*): the pull pass stages no sender values, so its
 // tile counters cover the whole image (N <= kSbMaxTiles * kTileD = 2^27).

@@ -88,18 +88,22 @@ __device__ __forceinline__ uint32_t dir_flags(uint32_t d) { return ((d & 1u) ? 0
 // senders [snd0, snd0 + nsnd) of the gathered image S (global ids), only edges
 // whose peer lies in [dst0, dst0 + dstn), only the directions in dmask, tiles
 // counted from dst0.  V = 2 (pull pass) stores no sender values, so its tile
-// counters can cover kSbMaxTiles tiles of the whole image.
+// counters can cover kSbMaxTiles tiles of the whole image.  V = 3: one shard
+// past 4096 tiles (N > 2^26): the sender values are not staged in LDS (the
+// tile counters take that room) but re-read from S — the region's slice, which
+// this block has just streamed, so the reads hit L2.
 template <int KREG, bool FAULTS, int V>
 __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const uint64_t* __restrict__ S, BinBufs b,
                                                                   uint32_t R, uint32_t t, uint32_t key0,
                                                                   uint32_t key1, uint32_t mode, uint32_t filt,
                                                                   Faults fa, EmitRange er) {
-  constexpr bool SHARD = V != 0;
-  constexpr uint32_t kMaxT = V == 2 ? kSbMaxTiles : kMaxTilesD;
+  constexpr bool SHARD = V == 1 || V == 2;
+  constexpr bool STAGE = V == 0 || V == 1;  // sender values staged in LDS
+  constexpr uint32_t kMaxT = V >= 2 ? kSbMaxTiles : kMaxTilesD;
   constexpr uint32_t kMaxS = kMaxSenders;
   __shared__ uint32_t cur[kMaxT];
   __shared__ uint32_t st_ids[kRecPerRegion];  // p_local | n_local << 14, sorted by destination tile
-  __shared__ uint64_t sval[V == 2 ? 1 : kMaxS];  // S_t of each sender, once (not once per record)
+  __shared__ uint64_t sval[STAGE ? kMaxS : 1];  // S_t of each sender, once (not once per record)
   __shared__ uint32_t wsum[kEmitThreads / 64];
   __shared__ uint32_t wpre[kEmitThreads / 64 + 1];
 
@@ -146,7 +150,7 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
 #pragma unroll
   for (uint32_t q = 0; q < kQ; ++q) {
     const uint32_t i = tid + q * kEmitThreads;
-    if (V != 2 && i < g.ts) sval[i] = v[q];
+    if (STAGE && i < g.ts) sval[i] = v[q];
   }
   if (r + gridDim.x < nr) load_values(region(r + gridDim.x), vn);
   __syncthreads();
@@ -323,7 +327,8 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
     // region is written without holes (a partly written 64-B chunk costs HBM
     // a read-modify-write: profiles/r01_experiments/microbench5_scattered_pieces.jsonl)
     gids[e] = id;
-    if (V != 2) gvals[e] = sval[(id >> kTileDLog) & kIdNMask];
+    if (STAGE) gvals[e] = sval[(id >> kTileDLog) & kIdNMask];
+    if (V == 3) gvals[e] = S[base + ((id >> kTileDLog) & kIdNMask)];
   }
 #pragma unroll
   for (uint32_t q = 0; q < kQ; ++q) v[q] = vn[q];
@@ -674,7 +679,8 @@ BinGeom make_bin_geom(uint64_t N, uint32_t k) {
 bool bin_path_ok(uint64_t N, uint32_t k, uint32_t W, uint32_t G) {
   if (W != 1 || G != 1 || k == 0 || k > 64 || N < 2) return false;
   const BinGeom g = make_bin_geom(N, k);
-  return g.nt_d <= kMaxTilesD && (uint64_t)g.nt_s * g.rp < (1ull << 31);  // record indices are int32
+  // past 4096 tiles the emit re-reads sender values from S (V = 3); record indices are int32
+  return g.nt_d <= kSbMaxTiles && (uint64_t)g.nt_s * g.rp < (1ull << 31);
 }
 
 size_t bin_bytes(const BinGeom& g) {
@@ -703,13 +709,20 @@ hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, 
                                const Faults& fa, uint32_t flags, const RoundSync& rs, hipStream_t st) {
   if (!b.nzb || !b.fullb) filt = 0;  // the bitmaps exist only with the frontier buffers
   const uint32_t eg = g.nt_s < kEmitGrid ? g.nt_s : kEmitGrid;  // persistent: one block per CU
-#define GOSSIP_EMIT(KR, F) \
-  bin_emit_kernel<KR, F, 0><<<eg, kEmitThreads, 0, st>>>(g, S, b, R, t, key0, key1, mode, filt, fa, EmitRange{})
-  if (g.k <= 2) {
-    if (fa.any()) GOSSIP_EMIT(2, true); else GOSSIP_EMIT(2, false);
-  } else {
-    if (fa.any()) GOSSIP_EMIT(0, true); else GOSSIP_EMIT(0, false);
+#define GOSSIP_EMIT(KR, F, VV) \
+  bin_emit_kernel<KR, F, VV><<<eg, kEmitThreads, 0, st>>>(g, S, b, R, t, key0, key1, mode, filt, fa, EmitRange{})
+#define GOSSIP_EMIT_V(VV)                                                 \
+  if (g.k <= 2) {                                                        \
+    if (fa.any()) GOSSIP_EMIT(2, true, VV); else GOSSIP_EMIT(2, false, VV); \
+  } else {                                                                \
+    if (fa.any()) GOSSIP_EMIT(0, true, VV); else GOSSIP_EMIT(0, false, VV); \
   }
+  if (g.nt_d <= kMaxTilesD) {
+    GOSSIP_EMIT_V(0)
+  } else {
+    GOSSIP_EMIT_V(3)
+  }
+#undef GOSSIP_EMIT_V
 #undef GOSSIP_EMIT
   const dim3 tg((g.nt_d + 1 + 31) / 32, (g.nt_s + 31) / 32);
   transpose_u16_kernel<<<tg, dim3(32, 8), 0, st>>>(b.off, b.offT, g.nt_s, g.nt_d + 1, partial, rs.plen);
