@@ -69,6 +69,14 @@ struct gossip_engine {
   uint64_t* scratch_d = nullptr;  // 8 B
   uint32_t *orow = nullptr, *ocol = nullptr, *irow = nullptr, *icol = nullptr;
   bool has_topo = false;
+  // stall mode, random modes: streak per node, all N nodes on every shard
+  uint8_t* stall_d = nullptr;
+  // FLOOD with faults, one shard: per out-edge pending values and first senders
+  bool flood_edges = false;
+  uint32_t fe_np = 1;
+  uint64_t fe_E = 0;
+  uint64_t *fe_pend[2] = {nullptr, nullptr}, *fe_skip[2] = {nullptr, nullptr};
+  uint32_t* fe_ieo = nullptr;
   // ANTIENTROPY: rows V[n*K + c], alive bytes, global max vector
   uint32_t *V = nullptr, *Vn = nullptr, *target = nullptr;
   uint64_t *alive = nullptr, *alive_n = nullptr;  // [chunks][2]: alive bits, stale bits (AeArgs::ab)
@@ -179,8 +187,11 @@ void free_all(gossip_engine* e) {
   }
   for (uint64_t* b : bufs)
     if (b) (void)hipFree(b);
-  uint32_t* tb[] = {e->orow, e->ocol, e->irow, e->icol};
+  uint32_t* tb[] = {e->orow, e->ocol, e->irow, e->icol, e->fe_ieo};
   for (uint32_t* b : tb)
+    if (b) (void)hipFree(b);
+  void* fe[] = {e->stall_d, e->fe_pend[0], e->fe_pend[1], e->fe_skip[0], e->fe_skip[1]};
+  for (void* b : fe)
     if (b) (void)hipFree(b);
   if (e->bin_mem) (void)hipFree(e->bin_mem);
   if (e->fr_mem) (void)hipFree(e->fr_mem);
@@ -452,6 +463,9 @@ int launch_round_path(gossip_engine* e, uint32_t t, bool sparse, uint32_t maj, b
     e->evr_kind[slot] = sparse ? 4 : 3;
   }
   HIP_OK(e, launch_round_snapshot(e->partial_d, rs, e->stream));
+  // stall streaks after round t (gossip_round_commit does it for rounds not run from here)
+  if (e->stall_d && slot >= 0)
+    HIP_OK(e, launch_stall_update(e->stall_d, e->N, e->k, t, e->key0, e->key1, e->fa, e->stream));
   return GOSSIP_OK;
 }
 
@@ -628,7 +642,13 @@ int compute_round(gossip_engine* e, const uint64_t* gathered) {
   int rc;
   if (e->mode == GOSSIP_MODE_FLOOD) {
     if ((rc = timer_begin(e, 0))) return rc;
-    HIP_OK(e, launch_round_flood(a, e->stream));
+    if (e->flood_edges)
+      HIP_OK(e, launch_round_flood_faults(a, FloodEdges{e->fe_pend[0], e->fe_pend[1], e->fe_skip[0], e->fe_skip[1],
+                                                        e->fe_ieo, std::max<uint64_t>(e->fe_E, 1), e->fe_np,
+                                                        e->cfg.stall_rounds},
+                                          e->stream));
+    else
+      HIP_OK(e, launch_round_flood(a, e->stream));
     if ((rc = timer_end(e, 0))) return rc;
   } else if (e->binned) {  // one round, path chosen from the exact totals of S_t
     if ((rc = prepare_planned(e))) return rc;
@@ -680,6 +700,10 @@ void rotate(gossip_engine* e) {
     e->Sprev = e->S;
     e->S = e->Snext;
     e->Snext = tmp;
+    if (e->flood_edges) {
+      std::swap(e->fe_pend[0], e->fe_pend[1]);
+      std::swap(e->fe_skip[0], e->fe_skip[1]);
+    }
   } else if (!e->binned) {  // binned rounds run in place
     e->cur ^= 1;
     bind_slices(e);
@@ -780,9 +804,10 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
     g_create_error = "stall_rounds must be in [0, 16]";
     return GOSSIP_EINVAL;
   }
-  if ((cfg->edge_loss || cfg->partitions > 1) &&
-      (cfg->mode == GOSSIP_MODE_FLOOD || cfg->mode == GOSSIP_MODE_ANTIENTROPY)) {
-    g_create_error = "edge_loss / partitions apply to the random modes (PUSH, PULL, PUSHPULL)";
+  const bool faulty = cfg->edge_loss || cfg->partitions > 1 || cfg->stall_rounds;
+  if (faulty && (cfg->mode == GOSSIP_MODE_ANTIENTROPY || (cfg->mode == GOSSIP_MODE_FLOOD && G != 1))) {
+    g_create_error = "edge_loss / partitions / stall_rounds apply to the random modes and to one-shard FLOOD "
+                     "(ANTIENTROPY's fault model is churn)";
     return GOSSIP_ENOTSUP;
   }
   int ndev = 0;
@@ -820,6 +845,8 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
   e->key1 = (uint32_t)(cfg->seed >> 32);
   e->fa = Faults{cfg->edge_loss, cfg->partitions, cfg->n_nodes};
   e->timing = (cfg->flags & GOSSIP_FLAG_TIMING) != 0;
+  e->flood_edges = e->mode == GOSSIP_MODE_FLOOD && faulty;
+  e->fe_np = cfg->stall_rounds > 1 ? cfg->stall_rounds - 1 : 1;
 
   auto bail = [&](int rc) {
     g_create_error = e->err;
@@ -846,6 +873,14 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
     return hipMemset(*p, 0, bytes) == hipSuccess;
   };
   if (!alloc(&e->partial_d, part_len(e) * 8) || !alloc(&e->scratch_d, 8)) return bail(GOSSIP_ENOMEM);
+  if (cfg->stall_rounds && e->mode >= GOSSIP_MODE_PUSH && e->mode <= GOSSIP_MODE_PUSHPULL) {
+    if (hipMalloc((void**)&e->stall_d, e->N) != hipSuccess || hipMemset(e->stall_d, 0, e->N) != hipSuccess) {
+      e->err = "hipMalloc of the stall streaks failed";
+      return bail(GOSSIP_ENOMEM);
+    }
+    e->fa.stall = e->stall_d;
+    e->fa.D = cfg->stall_rounds;
+  }
   auto alloc_raw = [&](void** p, size_t bytes) {
     if (hipMalloc(p, bytes) != hipSuccess) {
       e->err = "hipMalloc of " + std::to_string(bytes) + " bytes failed";
@@ -1038,12 +1073,15 @@ int gossip_set_topology_csr(gossip_engine_t* e, const uint32_t* row_ptr, const u
   std::vector<uint32_t> irow(n + 1, 0), icol(ocol.size());
   for (uint32_t v : ocol) irow[v + 1]++;
   for (uint64_t v = 0; v < n; ++v) irow[v + 1] += irow[v];
-  std::vector<uint32_t> fill(irow.begin(), irow.end() - 1);
+  std::vector<uint32_t> fill(irow.begin(), irow.end() - 1), ieo(ocol.size());
   for (uint64_t u = 0; u < n; ++u)
-    for (uint32_t q = orow[u]; q < orow[u + 1]; ++q) icol[fill[ocol[q]]++] = (uint32_t)u;
+    for (uint32_t q = orow[u]; q < orow[u + 1]; ++q) {
+      ieo[fill[ocol[q]]] = q;  // in-edge -> its out-edge id (FLOOD retry state)
+      icol[fill[ocol[q]]++] = (uint32_t)u;
+    }
   if (int rc = set_dev(e)) return rc;
   HIP_OK(e, hipStreamSynchronize(e->stream));
-  uint32_t** bufs[] = {&e->orow, &e->ocol, &e->irow, &e->icol};
+  uint32_t** bufs[] = {&e->orow, &e->ocol, &e->irow, &e->icol, &e->fe_ieo};
   for (uint32_t** b : bufs)
     if (*b) {
       HIP_OK(e, hipFree(*b));
@@ -1058,6 +1096,25 @@ int gossip_set_topology_csr(gossip_engine_t* e, const uint32_t* row_ptr, const u
   if (!ocol.empty()) {
     HIP_OK(e, hipMemcpy(e->ocol, ocol.data(), ocol.size() * 4, hipMemcpyHostToDevice));
     HIP_OK(e, hipMemcpy(e->icol, icol.data(), icol.size() * 4, hipMemcpyHostToDevice));
+  }
+  if (e->flood_edges) {  // fresh per-edge state for the new topology: nothing pending, no first senders
+    for (uint64_t** b : {&e->fe_pend[0], &e->fe_pend[1], &e->fe_skip[0], &e->fe_skip[1]})
+      if (*b) {
+        HIP_OK(e, hipFree(*b));
+        *b = nullptr;
+      }
+    e->fe_E = ocol.size();
+    const size_t E1 = std::max<size_t>(ocol.size(), 1);
+    const size_t pb = (size_t)e->fe_np * e->W * E1 * 8, sb = (size_t)e->W * E1 * 8;
+    if (hipMalloc((void**)&e->fe_ieo, E1 * 4) != hipSuccess || hipMalloc((void**)&e->fe_pend[0], pb) != hipSuccess ||
+        hipMalloc((void**)&e->fe_pend[1], pb) != hipSuccess || hipMalloc((void**)&e->fe_skip[0], sb) != hipSuccess ||
+        hipMalloc((void**)&e->fe_skip[1], sb) != hipSuccess)
+      return e->fail(GOSSIP_ENOMEM, "FLOOD edge-state allocation failed");
+    for (int b = 0; b < 2; ++b) {
+      HIP_OK(e, hipMemset(e->fe_pend[b], 0, pb));
+      HIP_OK(e, hipMemset(e->fe_skip[b], 0, sb));
+    }
+    if (!ieo.empty()) HIP_OK(e, hipMemcpy(e->fe_ieo, ieo.data(), ieo.size() * 4, hipMemcpyHostToDevice));
   }
   e->has_topo = true;
   return GOSSIP_OK;
@@ -1084,6 +1141,13 @@ int gossip_reset(gossip_engine_t* e) {
     // binned single-shard rounds run in place on S and never read the other image
     HIP_OK(e, hipMemsetAsync(e->S, 0, shard, e->stream));
     if (!e->binned) HIP_OK(e, hipMemsetAsync(e->Snext, 0, shard, e->stream));
+  }
+  if (e->stall_d) HIP_OK(e, hipMemsetAsync(e->stall_d, 0, e->N, e->stream));
+  if (e->flood_edges && e->fe_pend[0]) {
+    for (int b = 0; b < 2; ++b) {
+      HIP_OK(e, hipMemsetAsync(e->fe_pend[b], 0, (size_t)e->fe_np * e->W * std::max<uint64_t>(e->fe_E, 1) * 8, e->stream));
+      HIP_OK(e, hipMemsetAsync(e->fe_skip[b], 0, (size_t)e->W * std::max<uint64_t>(e->fe_E, 1) * 8, e->stream));
+    }
   }
   e->fr_valid = false;
   e->sx_valid = e->gtot_valid = e->last_sparse = false;
@@ -1186,6 +1250,10 @@ int gossip_round_compute(gossip_engine_t* e, uint64_t* partial) {
 
 int gossip_round_commit(gossip_engine_t* e, const uint64_t* total, gossip_round_stats_t* st) {
   if (!e || !total) return GOSSIP_EINVAL;
+  if (e->stall_d) {  // stall streaks after round t, every shard over all N nodes
+    if (int rc = set_dev(e)) return rc;
+    HIP_OK(e, launch_stall_update(e->stall_d, e->N, e->k, e->t, e->key0, e->key1, e->fa, e->stream));
+  }
   if (!e->last_sparse) rotate(e);  // sparse sharded rounds update S in place
   e->last_sparse = false;
   if (e->sx) {  // global totals of S_{t+1}: the next round's plan
@@ -1343,9 +1411,11 @@ int gossip_sparse_commit(gossip_engine_t* e, uint64_t items, uint64_t* partial) 
 
 int gossip_set_faults(gossip_engine_t* e, uint32_t edge_loss, uint32_t partitions) {
   if (!e) return GOSSIP_EINVAL;
-  if ((edge_loss || partitions > 1) && (e->mode == GOSSIP_MODE_FLOOD || e->mode == GOSSIP_MODE_ANTIENTROPY))
-    return e->fail(GOSSIP_ENOTSUP, "edge_loss / partitions apply to the random modes");
-  e->fa = Faults{edge_loss, partitions, e->N};
+  if ((edge_loss || partitions > 1) &&
+      (e->mode == GOSSIP_MODE_ANTIENTROPY || (e->mode == GOSSIP_MODE_FLOOD && !e->flood_edges)))
+    return e->fail(GOSSIP_ENOTSUP, "faults: random modes, or a FLOOD engine created with faults or stall_rounds "
+                                   "(its per-edge retry state)");
+  e->fa = Faults{edge_loss, partitions, e->N, e->stall_d, e->cfg.stall_rounds};
   return GOSSIP_OK;
 }
 

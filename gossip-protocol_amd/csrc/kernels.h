@@ -28,7 +28,23 @@ struct RoundArgs {
   const uint32_t *orow, *ocol, *irow, *icol;
 };
 
+// FLOOD with faults: per out-edge state of one shard (G == 1).
+// Edge e = CSR position in the sorted out-rows; ieo[q] = out-edge id of in-edge q.
+struct FloodEdges {
+  const uint64_t* pend;  // [np][W][E] values pending on e, by attempts made (np = max(1, D - 1))
+  uint64_t* pend_n;
+  const uint64_t* skipE;  // [W][E] values whose first sender at the edge's source was its target
+  uint64_t* skipE_n;
+  const uint32_t* ieo;
+  uint64_t E;
+  uint32_t np, D;
+};
+
 hipError_t launch_round_random(const RoundArgs& a, hipStream_t st);
+hipError_t launch_round_flood_faults(const RoundArgs& a, const FloodEdges& fe, hipStream_t st);
+// Stall streaks after round t (random modes), all N nodes; fa.stall is the array.
+hipError_t launch_stall_update(uint8_t* stall, uint64_t N, uint32_t k, uint32_t t, uint32_t key0, uint32_t key1,
+                               const Faults& fa, hipStream_t st);
 hipError_t launch_round_flood(const RoundArgs& a, hipStream_t st);
 hipError_t launch_stats(const RoundArgs& a, hipStream_t st);
 hipError_t launch_frontier(const uint64_t* S, const uint64_t* Sprev, uint64_t* F, uint64_t n, hipStream_t st);

@@ -150,6 +150,116 @@ __global__ __launch_bounds__(kBlock) void round_flood_kernel(RoundArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// FLOOD with faults (main.go:72-87): edge e = (u -> w), slot j of
+// u's sorted row.  In round t u attempts on e the values it learned in t-1 minus
+// those whose first sender was w (:73), plus every value still pending on e; one
+// RPC per value per attempt.  Lost as a random-mode edge (partition, or the loss
+// draw Philox({u, t, 4, j>>2})[j&3]); a lost value is retried next round, forever
+// (D = 0) or until attempted D times (the expired 2 s context, :77-78).  One lane
+// per node: it keeps the books of its own out-edges (attempts, what stays pending)
+// and receives over its in-edges (first sender = lowest id u that delivered).
+// Reads: S, Sprev, pend, skipE (round t); writes: Snext[v], pend_n and skipE_n of
+// v's own out-edges — no two lanes write one word.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool flood_edge_lost(const Faults& fa, uint32_t u, uint32_t w, uint32_t j, uint32_t t,
+                                                uint32_t k0, uint32_t k1) {
+  const uint32_t lw = fa.loss ? lane_of(loss_draws(u, t, j >> 2, k0, k1), j & 3u) : 0u;
+  return edge_lost(fa, reach_of(u, fa), w, lw);
+}
+
+__device__ __forceinline__ uint64_t flood_attempt(const RoundArgs& a, const FloodEdges& fe, uint32_t u, uint32_t x,
+                                                  uint64_t e, uint64_t* fresh) {
+  const uint64_t i = (uint64_t)x * a.Nl + u;
+  const uint64_t f = a.S[i] & ~a.Sprev[i] & ~fe.skipE[(uint64_t)x * fe.E + e];
+  uint64_t att = f;
+  for (uint32_t q = 0; q < fe.np; ++q) att |= fe.pend[((uint64_t)q * a.W + x) * fe.E + e];
+  *fresh = f;
+  return att;
+}
+
+__global__ __launch_bounds__(kBlock) void round_flood_faults_kernel(RoundArgs a, FloodEdges fe) {
+  uint64_t msgs = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t v64 = (uint64_t)blockIdx.x * kBlock + threadIdx.x; v64 < a.N; v64 += stride) {
+    const uint32_t v = (uint32_t)v64;
+    const uint32_t ob = a.orow[v], oe = a.orow[v + 1], deg = oe - ob;
+    // sender side: v's out-edges
+    for (uint32_t e = ob; e < oe; ++e) {
+      const bool lost = flood_edge_lost(a.fa, v, a.ocol[e], e - ob, a.t, a.key0, a.key1);
+      for (uint32_t x = 0; x < a.W; ++x) {
+        uint64_t fresh;
+        const uint64_t att = flood_attempt(a, fe, v, x, e, &fresh);
+        msgs += (uint64_t)__popcll(att);
+        for (uint32_t q = 0; q < fe.np; ++q) {  // what stays pending, by attempts made
+          uint64_t nv = 0;
+          if (lost) nv = fe.D == 0 ? (q == 0 ? att : 0ull)
+                                   : (q == 0 ? (fe.D >= 2 ? fresh : 0ull) : fe.pend[((uint64_t)(q - 1) * a.W + x) * fe.E + e]);
+          fe.pend_n[((uint64_t)q * a.W + x) * fe.E + e] = nv;
+        }
+        fe.skipE_n[(uint64_t)x * fe.E + e] = 0;
+      }
+    }
+    // receiver side: attempts delivered over v's in-edges
+    const uint32_t ib = a.irow[v], ie = a.irow[v + 1];
+    for (uint32_t x = 0; x < a.W; ++x) {
+      const uint64_t li = (uint64_t)x * a.Nl + v;
+      const uint64_t sv = a.S[li];
+      uint64_t acc = sv;
+      for (uint32_t q = ib; q < ie; ++q) {
+        const uint32_t u = a.icol[q], eo = fe.ieo[q];
+        if (flood_edge_lost(a.fa, u, v, eo - a.orow[u], a.t, a.key0, a.key1)) continue;
+        uint64_t fresh;
+        acc |= flood_attempt(a, fe, u, x, eo, &fresh);
+      }
+      const uint64_t nw = acc & ~sv;
+      uint64_t seen = 0;
+      for (uint32_t q = ib; q < ie && seen != nw; ++q) {
+        const uint32_t u = a.icol[q], eo = fe.ieo[q];
+        if (flood_edge_lost(a.fa, u, v, eo - a.orow[u], a.t, a.key0, a.key1)) continue;
+        uint64_t fresh;
+        const uint64_t c = flood_attempt(a, fe, u, x, eo, &fresh) & nw & ~seen;
+        if (!c) continue;
+        seen |= c;
+        uint32_t lo = 0, hi = deg;  // u in Adj(v)?  then v will not send these back to u (main.go:73)
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (a.ocol[ob + mid] < u) lo = mid + 1; else hi = mid;
+        }
+        if (lo < deg && a.ocol[ob + lo] == u) fe.skipE_n[(uint64_t)x * fe.E + ob + lo] |= c;
+      }
+      a.Snext[li] = acc;
+    }
+  }
+  msgs = wave_sum_u64(msgs);
+  if ((threadIdx.x & 63) == 0 && msgs) atomicAdd((unsigned long long*)&a.partial[2], (unsigned long long)msgs);
+}
+
+// Stall streaks after round t: a node not yet stalled counts the
+// round when any of its k exchanges was lost, else starts over.  Draws only: the
+// streaks never depend on S.
+__global__ __launch_bounds__(kBlock) void stall_update_kernel(uint8_t* __restrict__ st, uint64_t N, uint32_t k,
+                                                              uint32_t t, uint32_t key0, uint32_t key1, Faults fa) {
+  fa.stall = nullptr;  // the partition block of a node that is not stalled
+  const uint64_t nm1 = N - 1;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < N; i += (uint64_t)gridDim.x * kBlock) {
+    const uint32_t n = (uint32_t)i;
+    const uint32_t c = st[i];
+    if (c >= fa.D) continue;
+    const Reach rc = reach_of(n, fa);
+    bool any = false;
+    u32x4 x{0, 0, 0, 0}, lw{0, 0, 0, 0};
+    for (uint32_t j = 0; j < k && !any; ++j) {
+      if ((j & 3u) == 0) {
+        x = philox4x32_10(u32x4{n, t, 0u, j >> 2}, key0, key1);
+        if (fa.loss) lw = loss_draws(n, t, j >> 2, key0, key1);
+      }
+      any = edge_lost(fa, rc, peer_from_word(lane_of(x, j & 3u), nm1, n), lane_of(lw, j & 3u));
+    }
+    st[i] = (uint8_t)(any ? c + 1 : 0);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Stats of S_{t+1} (convergence detection): per-rumor infected counts by
 // wave64 ballot + popcount, fully-informed node count, optional state hash.
 // partial = [full, alive, messages, hash, infected[R]].
@@ -276,6 +386,17 @@ hipError_t launch_round_random(const RoundArgs& a, hipStream_t st) {
 
 hipError_t launch_round_flood(const RoundArgs& a, hipStream_t st) {
   round_flood_kernel<<<grid_for(a.nown, 8192), kBlock, 0, st>>>(a);
+  return hipGetLastError();
+}
+
+hipError_t launch_round_flood_faults(const RoundArgs& a, const FloodEdges& fe, hipStream_t st) {
+  round_flood_faults_kernel<<<grid_for(a.N, 8192), kBlock, 0, st>>>(a, fe);
+  return hipGetLastError();
+}
+
+hipError_t launch_stall_update(uint8_t* stall, uint64_t N, uint32_t k, uint32_t t, uint32_t key0, uint32_t key1,
+                               const Faults& fa, hipStream_t st) {
+  stall_update_kernel<<<grid_for(N, 8192), kBlock, 0, st>>>(stall, N, k, t, key0, key1, fa);
   return hipGetLastError();
 }
 

@@ -54,11 +54,16 @@ __host__ __device__ __forceinline__ uint32_t peer_from_word(uint32_t x, uint64_t
 // main.go:77-87): the edge n -> p_j(n) of round t is lost in both directions
 // when a partition separates its ends (nodes split into `parts` contiguous
 // blocks) or when its loss draw, stream tag 4, falls below `loss` (P = loss/2^32).
+// Stall mode (main.go:77-87, the expired 2 s context): a node
+// whose initiated exchanges were lost in D rounds in a row initiates none until
+// reset.  stall = the per-node streaks of all N nodes (random modes), or null.
 struct Faults {
   uint32_t loss;   // 0: no loss
   uint32_t parts;  // 0 or 1: no partition
   uint64_t N;
-  __host__ __device__ bool any() const { return loss != 0 || parts > 1; }
+  const uint8_t* stall = nullptr;
+  uint32_t D = 0;
+  __host__ __device__ bool any() const { return loss != 0 || parts > 1 || stall != nullptr; }
 };
 
 __host__ __device__ __forceinline__ uint32_t part_of(uint32_t n, const Faults& f) {
@@ -71,7 +76,9 @@ __host__ __device__ __forceinline__ uint32_t part_of(uint32_t n, const Faults& f
 struct Reach {
   uint32_t lo, hi;
 };
+// A stalled initiator reaches nobody: every edge it would start is lost.
 __host__ __device__ __forceinline__ Reach reach_of(uint32_t n, const Faults& f) {
+  if (f.stall && f.stall[n] >= f.D) return Reach{0xFFFFFFFFu, 0u};
   if (f.parts <= 1) return Reach{0u, 0xFFFFFFFFu};
   const uint64_t q = part_of(n, f);
   return Reach{(uint32_t)((q * f.N + f.parts - 1) / f.parts), (uint32_t)(((q + 1) * f.N + f.parts - 1) / f.parts)};

@@ -50,6 +50,13 @@ struct oracle_sim {
   uint64_t *msg_send, *msg_recv, msg_cap;  /* [k * nown] items grouped by owner; received items */
   uint64_t* D;                             /* pending push deltas of the owned nodes */
   uint64_t* counts;                        /* rare list lengths of the current round [G] */
+  /* stall mode: random modes, lost-exchange streak per node (all N) */
+  uint8_t* streak;
+  /* FLOOD with faults: per out-edge state, [slot][W][E] / [W][E]; ieo = out-edge id of in-edge */
+  int flood_edges;
+  uint32_t npend;
+  uint64_t *pend, *pend_n, *skipE, *skipE_n;
+  uint32_t* ieo;
 };
 
 /* ---------------- Philox4x32-10 (Random123; rocRAND philox4x32_10.h:270-302) ---- */
@@ -101,6 +108,18 @@ static int edge_lost(const gossip_config_t* cfg, uint64_t N, uint32_t n, uint32_
   return 0;
 }
 
+/* Stall mode (main.go:77-87: a neighbour's 2 s context expires and the
+ * goroutine retries forever): a node whose initiated exchanges were lost in stall_rounds
+ * rounds in a row initiates none until reset.  It still answers pulls and takes pushes. */
+static inline int stalled(const oracle_sim_t* s, uint32_t n) {
+  return s->streak && s->streak[n] >= s->cfg.stall_rounds;
+}
+
+/* edge n -> p (slot j of initiator n, round t) carries nothing this round */
+static inline int lost_edge(const oracle_sim_t* s, uint32_t n, uint32_t p, uint32_t j, const uint32_t key[2]) {
+  return stalled(s, n) || edge_lost(&s->cfg, s->N, n, p, s->t, j, key);
+}
+
 uint32_t oracle_origin(uint64_t seed, uint64_t N, uint32_t r) {
   uint32_t ctr[4] = {r, 0u, 2u, 0u};
   uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
@@ -129,8 +148,10 @@ int oracle_create(const gossip_config_t* cfg, int threads, oracle_sim_t** out) {
   uint32_t G = cfg->shard_count ? cfg->shard_count : 1;
   if (cfg->shard_rank >= G) return GOSSIP_EINVAL;
   if (cfg->mode == GOSSIP_MODE_ANTIENTROPY && (G != 1 || cfg->n_rumors > 64)) return GOSSIP_ENOTSUP;
-  if ((cfg->edge_loss || cfg->partitions > 1) &&
-      (cfg->mode == GOSSIP_MODE_FLOOD || cfg->mode == GOSSIP_MODE_ANTIENTROPY)) return GOSSIP_ENOTSUP;
+  if (cfg->stall_rounds > 16) return GOSSIP_EINVAL;
+  const int faulty = cfg->edge_loss || cfg->partitions > 1 || cfg->stall_rounds;
+  if (faulty && (cfg->mode == GOSSIP_MODE_ANTIENTROPY || (cfg->mode == GOSSIP_MODE_FLOOD && G != 1)))
+    return GOSSIP_ENOTSUP;
   oracle_sim_t* s = (oracle_sim_t*)calloc(1, sizeof(*s));
   if (!s) return GOSSIP_ENOMEM;
   s->cfg = *cfg;
@@ -181,6 +202,13 @@ int oracle_create(const gossip_config_t* cfg, int threads, oracle_sim_t** out) {
   s->gtot = (uint64_t*)calloc(5 + s->R, 8);
   s->counts = (uint64_t*)calloc(G, 8);
   s->sparse_frac = 0.25;
+  s->flood_edges = s->mode == GOSSIP_MODE_FLOOD && faulty;
+  s->npend = cfg->stall_rounds > 1 ? cfg->stall_rounds - 1 : 1;
+  if (cfg->stall_rounds && s->mode >= GOSSIP_MODE_PUSH && s->mode <= GOSSIP_MODE_PUSHPULL &&
+      !(s->streak = (uint8_t*)calloc(s->N, 1))) {
+    oracle_destroy(s);
+    return GOSSIP_ENOMEM;
+  }
   if (!s->gtot || !s->counts) {
     oracle_destroy(s);
     return GOSSIP_ENOMEM;
@@ -196,6 +224,7 @@ void oracle_destroy(oracle_sim_t* s) {
   free(s->V); free(s->Vn); free(s->target); free(s->alive); free(s->alive_n);
   free(s->gtot); free(s->counts); free(s->rare_send); free(s->rare_recv); free(s->msg_send); free(s->msg_recv);
   free(s->D);
+  free(s->streak); free(s->pend); free(s->pend_n); free(s->skipE); free(s->skipE_n); free(s->ieo);
   free(s);
 }
 
@@ -238,17 +267,28 @@ int oracle_set_topology_csr(oracle_sim_t* s, const uint32_t* row_ptr, const uint
   for (uint64_t e = 0; e < E; ++e) irow[ocol[e] + 1]++;
   for (uint64_t v = 0; v < n; ++v) irow[v + 1] += irow[v];
   uint32_t* fill = (uint32_t*)malloc((n + 1) * 4);
-  if (!fill) {
-    free(orow); free(ocol); free(irow); free(icol);
+  uint32_t* ieo = (uint32_t*)malloc((n_edges ? n_edges : 1) * 4);
+  if (!fill || !ieo) {
+    free(orow); free(ocol); free(irow); free(icol); free(fill); free(ieo);
     return GOSSIP_ENOMEM;
   }
   memcpy(fill, irow, (n + 1) * 4);
   for (uint64_t u = 0; u < n; ++u) /* ascending u => each in-row sorted */
-    for (uint32_t e = orow[u]; e < orow[u + 1]; ++e) icol[fill[ocol[e]]++] = (uint32_t)u;
+    for (uint32_t e = orow[u]; e < orow[u + 1]; ++e) {
+      ieo[fill[ocol[e]]] = e;
+      icol[fill[ocol[e]]++] = (uint32_t)u;
+    }
   free(fill);
-  free(s->orow); free(s->ocol); free(s->irow); free(s->icol);
-  s->orow = orow; s->ocol = ocol; s->irow = irow; s->icol = icol;
+  free(s->orow); free(s->ocol); free(s->irow); free(s->icol); free(s->ieo);
+  s->orow = orow; s->ocol = ocol; s->irow = irow; s->icol = icol; s->ieo = ieo;
   s->E = E;
+  if (s->flood_edges) { /* fresh per-edge state: nothing pending, no first senders */
+    const size_t pe = (size_t)s->npend * s->W * (E ? E : 1), se = (size_t)s->W * (E ? E : 1);
+    free(s->pend); free(s->pend_n); free(s->skipE); free(s->skipE_n);
+    s->pend = (uint64_t*)calloc(pe, 8); s->pend_n = (uint64_t*)calloc(pe, 8);
+    s->skipE = (uint64_t*)calloc(se, 8); s->skipE_n = (uint64_t*)calloc(se, 8);
+    if (!s->pend || !s->pend_n || !s->skipE || !s->skipE_n) return GOSSIP_ENOMEM;
+  }
   s->has_topo = 1;
   return GOSSIP_OK;
 }
@@ -264,6 +304,11 @@ int oracle_reset(oracle_sim_t* s) {
     memset(s->V, 0, (size_t)s->N * s->R * 4);
     memset(s->target, 0, (size_t)s->R * 4);
     memset(s->alive, 1, s->N);
+  }
+  if (s->streak) memset(s->streak, 0, s->N);
+  if (s->pend) {
+    memset(s->pend, 0, (size_t)s->npend * s->W * (s->E ? s->E : 1) * 8);
+    memset(s->skipE, 0, (size_t)s->W * (s->E ? s->E : 1) * 8);
   }
   s->t = 0;
   s->gtot_valid = s->planned = s->last_sparse = 0;
@@ -400,6 +445,105 @@ static int ae_round(oracle_sim_t* s, uint64_t* partial) {
   return GOSSIP_OK;
 }
 
+/* FLOOD with faults (main.go:72-87).  Edge e = (u -> w), slot j of u's
+ * sorted row.  In round t u attempts on e every value it learned in t-1 (minus those whose
+ * first sender was w: main.go:73) plus every value still pending on e; each attempt is one
+ * RPC.  The attempt is lost like a random-mode edge (partition, or Philox({u, t, 4, j>>2})
+ * [j&3] < edge_loss); a lost value is retried next round — forever (stall_rounds 0), or
+ * until it was attempted stall_rounds times (the expired 2 s context).  w's first sender
+ * of a value is the lowest-id u whose attempt delivered it. */
+static int flood_lost(const oracle_sim_t* s, uint32_t u, uint32_t w, uint32_t j, const uint32_t key[2]) {
+  return edge_lost(&s->cfg, s->N, u, w, s->t, j, key);
+}
+
+static uint64_t flood_faults_round(oracle_sim_t* s, uint64_t* Sn) {
+  const uint64_t N = s->N, E = s->E ? s->E : 1;
+  const uint32_t W = s->W, D = s->cfg.stall_rounds, np = s->npend;
+  const uint32_t key[2] = {(uint32_t)s->cfg.seed, (uint32_t)(s->cfg.seed >> 32)};
+  uint64_t msgs = 0;
+  memset(s->pend_n, 0, (size_t)np * W * E * 8);
+  memset(s->skipE_n, 0, (size_t)W * E * 8);
+  /* sender side: every out-edge's attempt, messages, what stays pending */
+  for (uint64_t u = 0; u < N; ++u)
+    for (uint32_t e = s->orow[u]; e < s->orow[u + 1]; ++e) {
+      const int lost = flood_lost(s, (uint32_t)u, s->ocol[e], e - s->orow[u], key);
+      for (uint32_t x = 0; x < W; ++x) {
+        const size_t i = (size_t)x * N + u;
+        const uint64_t fresh = s->S[i] & ~s->Sprev[i] & ~s->skipE[(size_t)x * E + e];
+        uint64_t att = fresh;
+        for (uint32_t a = 0; a < np; ++a) att |= s->pend[((size_t)a * W + x) * E + e];
+        msgs += popc64(att);
+        if (!lost) continue;
+        if (D == 0) {
+          s->pend_n[(size_t)x * E + e] = att;
+        } else {
+          if (D >= 2) s->pend_n[(size_t)x * E + e] = fresh;
+          for (uint32_t a = 0; a + 1 < np; ++a)
+            s->pend_n[((size_t)(a + 1) * W + x) * E + e] = s->pend[((size_t)a * W + x) * E + e];
+        }
+      }
+    }
+  /* receiver side: delivered attempts of the in-edges, ascending sender id */
+  for (uint64_t w = 0; w < N; ++w) {
+    const uint32_t ob = s->orow[w], deg = s->orow[w + 1] - ob;
+    for (uint32_t x = 0; x < W; ++x) {
+      const size_t i = (size_t)x * N + w;
+      uint64_t acc = s->S[i];
+      for (uint32_t q = s->irow[w]; q < s->irow[w + 1]; ++q) {
+        const uint32_t u = s->icol[q], eo = s->ieo[q];
+        if (flood_lost(s, u, (uint32_t)w, eo - s->orow[u], key)) continue;
+        const size_t iu = (size_t)x * N + u;
+        uint64_t att = s->S[iu] & ~s->Sprev[iu] & ~s->skipE[(size_t)x * E + eo];
+        for (uint32_t a = 0; a < np; ++a) att |= s->pend[((size_t)a * W + x) * E + eo];
+        acc |= att;
+      }
+      const uint64_t nw = acc & ~s->S[i];
+      uint64_t seen = 0;
+      for (uint32_t q = s->irow[w]; q < s->irow[w + 1] && seen != nw; ++q) {
+        const uint32_t u = s->icol[q], eo = s->ieo[q];
+        if (flood_lost(s, u, (uint32_t)w, eo - s->orow[u], key)) continue;
+        const size_t iu = (size_t)x * N + u;
+        uint64_t att = s->S[iu] & ~s->Sprev[iu] & ~s->skipE[(size_t)x * E + eo];
+        for (uint32_t a = 0; a < np; ++a) att |= s->pend[((size_t)a * W + x) * E + eo];
+        const uint64_t c = att & nw & ~seen;
+        if (!c) continue;
+        seen |= c;
+        uint32_t lo = 0, hi = deg; /* is u in Adj(w)?  then w skips it for these values */
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi) / 2;
+          if (s->ocol[ob + mid] < u) lo = mid + 1; else hi = mid;
+        }
+        if (lo < deg && s->ocol[ob + lo] == u) s->skipE_n[(size_t)x * E + ob + lo] |= c;
+      }
+      Sn[i] = acc;
+    }
+  }
+  uint64_t* t;
+  t = s->pend; s->pend = s->pend_n; s->pend_n = t;
+  t = s->skipE; s->skipE = s->skipE_n; s->skipE_n = t;
+  return msgs;
+}
+
+/* Stall streaks after round t (random modes): every node that is not
+ * stalled counts a round in which any of its k exchanges was lost, and resets on a round
+ * with none lost.  Depends only on the draws and the fault model, never on S. */
+static void stall_update(oracle_sim_t* s) {
+  const uint32_t key[2] = {(uint32_t)s->cfg.seed, (uint32_t)(s->cfg.seed >> 32)};
+  for (uint64_t n = 0; n < s->N; ++n) {
+    if (s->streak[n] >= s->cfg.stall_rounds) continue;
+    int any = 0;
+    uint32_t x[4] = {0, 0, 0, 0};
+    for (uint32_t j = 0; j < s->k && !any; ++j) {
+      if ((j & 3) == 0) {
+        uint32_t ctr[4] = {(uint32_t)n, s->t, 0u, j >> 2};
+        oracle_philox4x32_10(ctr, key, x);
+      }
+      any = edge_lost(&s->cfg, s->N, (uint32_t)n, peer_from_word(x[j & 3], s->N, (uint32_t)n), s->t, j, key);
+    }
+    s->streak[n] = any ? (uint8_t)(s->streak[n] + 1) : 0;
+  }
+}
+
 int oracle_round_compute(oracle_sim_t* s, uint64_t* partial) {
   if (!s || !partial) return GOSSIP_EINVAL;
   if (s->mode == GOSSIP_MODE_ANTIENTROPY) return ae_round(s, partial);
@@ -412,7 +556,10 @@ int oracle_round_compute(oracle_sim_t* s, uint64_t* partial) {
   memcpy(Sn, s->S, (size_t)W * Nl * 8); /* S_{t+1} starts as S_t (OR is monotone) */
   uint64_t msgs = 0;
 
-  if (s->mode == GOSSIP_MODE_FLOOD) {
+  if (s->mode == GOSSIP_MODE_FLOOD && s->flood_edges) {
+    if (!s->has_topo) return GOSSIP_ESTATE;
+    msgs = flood_faults_round(s, Sn);
+  } else if (s->mode == GOSSIP_MODE_FLOOD) {
     if (!s->has_topo) return GOSSIP_ESTATE;
     /* main.go:72-75: every node that learned a value last round (frontier F)
      * sends it to each topology neighbour except the one it came from. */
@@ -450,7 +597,7 @@ int oracle_round_compute(oracle_sim_t* s, uint64_t* partial) {
             oracle_philox4x32_10(ctr, key, x);
           }
           uint32_t p = peer_from_word(x[j & 3], N, n);
-          if (edge_lost(&s->cfg, N, n, p, t, j, key)) continue;
+          if (lost_edge(s, n, p, j, key)) continue;
           for (uint32_t w = 0; w < W; ++w) Sn[(size_t)w * Nl + i] |= gword(s, g, p, w);
         }
       }
@@ -467,7 +614,7 @@ int oracle_round_compute(oracle_sim_t* s, uint64_t* partial) {
           }
           uint32_t p = peer_from_word(x[j & 3], N, n);
           if (p < lo || p >= lo + nown) continue;
-          if (edge_lost(&s->cfg, N, n, p, t, j, key)) continue;
+          if (lost_edge(s, n, p, j, key)) continue;
           for (uint32_t w = 0; w < W; ++w) {
             uint64_t v = gword(s, g, n, w);
             if (!v) continue;
@@ -535,6 +682,7 @@ int oracle_round_commit(oracle_sim_t* s, const uint64_t* total, gossip_round_sta
     tmp = s->S; s->S = s->Snext; s->Snext = tmp;
   }
   s->last_sparse = 0;
+  if (s->streak) stall_update(s); /* (uses s->t: the round just computed) */
   memcpy(s->gtot, total, oracle_partial_len(s) * 8);
   s->gtot_valid = 1;
   if (st) {
@@ -673,7 +821,7 @@ int oracle_sparse_scan(oracle_sim_t* s, const uint64_t* counts, void** send, uin
         oracle_philox4x32_10(ctr, key, r);
       }
       const uint32_t p = peer_from_word(r[j & 3], s->N, n);
-      if (edge_lost(&s->cfg, s->N, n, p, s->t, j, key)) continue;
+      if (lost_edge(s, n, p, j, key)) continue;
       uint64_t v = majv;
       int rp;
       if (p >= s->lo && p < s->hi) {
@@ -754,8 +902,9 @@ int oracle_set_param(oracle_sim_t* s, const char* name, double value) {
 
 int oracle_set_faults(oracle_sim_t* s, uint32_t edge_loss, uint32_t partitions) {
   if (!s) return GOSSIP_EINVAL;
-  if ((edge_loss || partitions > 1) && (s->mode == GOSSIP_MODE_FLOOD || s->mode == GOSSIP_MODE_ANTIENTROPY))
-    return GOSSIP_ENOTSUP;
+  if ((edge_loss || partitions > 1) &&
+      (s->mode == GOSSIP_MODE_ANTIENTROPY || (s->mode == GOSSIP_MODE_FLOOD && !s->flood_edges)))
+    return GOSSIP_ENOTSUP; /* FLOOD retries need the per-edge state: create with faults or stall_rounds */
   s->cfg.edge_loss = edge_loss;
   s->cfg.partitions = partitions;
   return GOSSIP_OK;

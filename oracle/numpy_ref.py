@@ -110,15 +110,50 @@ def stats_of(S: np.ndarray, R: int):
     return full, [int(x) for x in inf]
 
 
-class Sim:
-    """Unsharded reference loop.  mode: 'flood' | 'push' | 'pull' | 'pushpull'."""
+def loss_draw(seed: int, nodes, t: int, j: int) -> np.ndarray:
+    """Philox({n, t, 4, j>>2})[j&3]: the loss draw of edge j of node n in round t."""
+    n = np.asarray(nodes, dtype=np.uint32)
+    x = philox4x32_10(n, np.uint32(t), np.uint32(4), np.uint32(j >> 2), seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
+    return x[j & 3]
 
-    def __init__(self, n_nodes, n_rumors, mode, fanout=0, seed=0, topology=None):
+
+def edge_lost(seed, N, loss, parts, n, p, t, j) -> np.ndarray:
+    """The edge n -> p (slot j of n, round t) is lost: partition or loss draw."""
+    n = np.asarray(n, dtype=np.int64)
+    p = np.asarray(p, dtype=np.int64)
+    lost = np.zeros(n.shape, dtype=bool)
+    if parts > 1:
+        lost |= (n * parts) // N != (p * parts) // N
+    if loss:
+        lost |= loss_draw(seed, n, t, j) < np.uint32(loss)
+    return lost
+
+
+def popcount(x) -> int:
+    return bin(int(x)).count("1")
+
+
+class Sim:
+    """Unsharded reference loop.  mode: 'flood' | 'push' | 'pull' | 'pushpull'.
+
+    Faults (the reference's lossy SyncRPC with a 2 s context and
+    unbounded retries, main.go:77-87): edge_loss / partitions lose edges; stall_rounds D
+    restates the expired-context stall —
+      random modes: a node whose initiated exchanges were lost (any of them) in D rounds in
+        a row stops initiating exchanges (it still answers pulls and receives pushes);
+      flood: a value is retried on a lost edge every round; with D > 0 it is dropped from
+        that edge after D failed attempts.
+    """
+
+    def __init__(self, n_nodes, n_rumors, mode, fanout=0, seed=0, topology=None, edge_loss=0, partitions=0,
+                 stall_rounds=0):
         self.N, self.R, self.mode, self.k, self.seed = n_nodes, n_rumors, mode, fanout, seed
+        self.loss, self.parts, self.D = edge_loss, partitions, stall_rounds
         self.W = (n_rumors + 63) // 64
         self.S = np.zeros((self.W, n_nodes), dtype=np.uint64)
         self.Sprev = np.zeros_like(self.S)
         self.t = 0
+        self.streak = np.zeros(n_nodes, dtype=np.int64)  # random modes, stall_rounds > 0
         self.adj = None
         if topology is not None:
             # rows as sets (DESIGN.md §2.4)
@@ -132,6 +167,12 @@ class Sim:
             self.dst = np.array(dst, dtype=np.int64)
             self.deg = np.array([len(r) for r in self.adj], dtype=np.int64)
             self.skip = np.zeros_like(self.S)
+            # flood with faults: per out-edge state (edge e = position in the CSR of sorted rows)
+            self.edge_faults = bool(edge_loss or partitions > 1 or stall_rounds)
+            E = len(self.src)
+            self.row0 = np.concatenate([[0], np.cumsum(self.deg)]).astype(np.int64)
+            self.skipE = np.zeros((self.W, E), dtype=np.uint64)                 # first sender = target
+            self.pend = np.zeros((max(1, stall_rounds - 1), self.W, E), dtype=np.uint64)  # by attempts made
 
     def inject(self, node, rumor):
         self.S[rumor // 64, node] |= np.uint64(1 << (rumor % 64))
@@ -140,11 +181,60 @@ class Sim:
         for r, o in enumerate(origins(self.seed, self.N, self.R)):
             self.inject(int(o), r)
 
+    def _flood_faults_round(self, S, Sn):
+        """FLOOD with per-edge retries: edge e = (u -> w), slot j of u."""
+        F = S & ~self.Sprev
+        E = len(self.src)
+        D = self.D
+        msgs = 0
+        nslots = self.pend.shape[0]
+        new_pend = np.zeros_like(self.pend)
+        new_skipE = np.zeros_like(self.skipE)
+        delivered = np.zeros((self.W, E), dtype=np.uint64)
+        for e in range(E):
+            u, w = int(self.src[e]), int(self.dst[e])
+            j = e - int(self.row0[u])
+            lost = bool(edge_lost(self.seed, self.N, self.loss, self.parts, [u], [w], self.t, j)[0])
+            for x in range(self.W):
+                fresh = F[x][u] & ~self.skipE[x][e]
+                att = fresh
+                for a in range(nslots):
+                    att |= self.pend[a][x][e]
+                msgs += popcount(att)
+                if not lost:
+                    delivered[x][e] = att
+                elif D == 0:
+                    new_pend[0][x][e] = att           # retried every round, forever
+                else:                                 # attempts made: fresh 1, slot a: a + 2
+                    if D >= 2:
+                        new_pend[0][x][e] = fresh
+                    for a in range(nslots - 1):
+                        new_pend[a + 1][x][e] = self.pend[a][x][e]
+        # receivers: OR of delivered attempts; first (lowest-id) sender of each new bit
+        for x in range(self.W):
+            for e in range(E):
+                Sn[x][self.dst[e]] |= delivered[x][e]
+            new = Sn[x] & ~S[x]
+            seen = np.zeros(self.N, dtype=np.uint64)
+            for e in np.lexsort((self.src, self.dst)):
+                u, w = int(self.src[e]), int(self.dst[e])
+                c = delivered[x][e] & new[w] & ~seen[w]
+                if c:
+                    seen[w] |= c
+                    if u in self.adj[w]:  # w will not send these back to u (main.go:73)
+                        back = int(self.row0[w]) + self.adj[w].index(u)
+                        new_skipE[x][back] |= c
+        self.pend, self.skipE = new_pend, new_skipE
+        return msgs
+
     def round(self):
         S = self.S
         Sn = S.copy()
         msgs = 0
-        if self.mode == "flood":
+        if self.mode == "flood" and self.edge_faults:
+            msgs = self._flood_faults_round(S, Sn)
+            self.Sprev = S
+        elif self.mode == "flood":
             F = S & ~self.Sprev
             for w in range(self.W):
                 # messages sent this round: |F[v]|*deg(v) - skipped senders (main.go:72-75)
@@ -168,13 +258,22 @@ class Sim:
             self.Sprev = S
         else:
             P = peers(self.seed, self.N, self.t, self.k).astype(np.int64)
+            n = np.arange(self.N, dtype=np.int64)
+            lost = np.stack([edge_lost(self.seed, self.N, self.loss, self.parts, n, P[:, j], self.t, j)
+                             for j in range(self.k)], axis=1)
+            stalled = self.streak >= self.D if self.D else np.zeros(self.N, dtype=bool)
+            live = ~lost & ~stalled[:, None]  # a stalled node initiates nothing
             for w in range(self.W):
-                if self.mode in ("pull", "pushpull"):
-                    for j in range(self.k):
-                        Sn[w] |= S[w][P[:, j]]
-                if self.mode in ("push", "pushpull"):
-                    for j in range(self.k):
-                        np.bitwise_or.at(Sn[w], P[:, j], S[w])
+                for j in range(self.k):
+                    src = n[live[:, j]]
+                    dst = P[live[:, j], j]
+                    if self.mode in ("pull", "pushpull"):
+                        np.bitwise_or.at(Sn[w], src, S[w][dst])
+                    if self.mode in ("push", "pushpull"):
+                        np.bitwise_or.at(Sn[w], dst, S[w][src])
+            if self.D:
+                lost_any = lost.any(axis=1)
+                self.streak = np.where(stalled, self.streak, np.where(lost_any, self.streak + 1, 0))
         self.S = Sn
         full, inf = stats_of(Sn, self.R)
         st = dict(round=self.t, full=full, converged=int(full == self.N), messages=msgs,

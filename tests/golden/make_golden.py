@@ -53,6 +53,31 @@ FLOOD_CASES = [
 ]
 
 
+LOSS = lambda p: min(int(round(p * 2**32)), 2**32 - 1)  # noqa: E731  (gossip_hip.loss_threshold)
+
+# random modes under faults and the stall mode (§2.9): name, N, R, mode, k, seed,
+# injection, edge_loss, partitions, stall_rounds, max_rounds
+RANDOM_FAULT_CASES = [
+    ("pushpull_loss30", 2000, 8, "pushpull", 2, 9, "random", LOSS(0.3), 0, 0, 200),
+    ("pushpull_stall3_loss10", 3000, 64, "pushpull", 2, 0x5EED0003, "random", LOSS(0.1), 0, 3, 200),
+    ("push_stall2_parts2", 2001, 1, "push", 3, 7, [(0, 0), (1500, 0)], LOSS(0.05), 2, 2, 60),
+    ("pull_stall1_loss2", 1500, 5, "pull", 2, 11, "random", LOSS(0.02), 0, 1, 200),
+    ("pushpull_k6_stall4", 1000, 7, "pushpull", 6, 3, "random", LOSS(0.25), 2, 4, 80),
+]
+
+# FLOOD with faults: per-edge retries, dropped after stall_rounds attempts (§2.9):
+# name, N, R, adjacency, injection, edge_loss, partitions, stall_rounds, max_rounds
+FLOOD_FAULT_CASES = [
+    ("grid25_loss30_retry", 25, 2, adj(grid_topology(25), 25), [(0, 0), (24, 1)], LOSS(0.3), 0, 0, 80),
+    ("grid25_loss30_stall2", 25, 2, adj(grid_topology(25), 25), [(0, 0), (24, 1)], LOSS(0.3), 0, 2, 80),
+    ("tree3_40_parts2_stall3", 40, 2, adj(tree_topology(40, 3), 40), [(0, 0), (39, 1)], LOSS(0.1), 2, 3, 60),
+    ("directed_ring_loss50_stall1", 6, 2, [[1, 1], [2], [3, 0], [4], [0, 4], [5]], [(0, 0), (2, 1)],
+     LOSS(0.5), 0, 1, 40),
+    ("line16_parts4_retry", 16, 1, adj(line_topology(16), 16), [(7, 0)], 0, 4, 0, 30),
+    ("grid25_70vals_loss20_stall3", 25, 70, adj(grid_topology(25), 25), [(i % 25, i) for i in range(70)],
+     LOSS(0.2), 0, 3, 80),
+]
+
 AE_CASES = [
     # name, N, K, fanout, seed, fail, recover  (thresholds = probability * 2^32)
     ("ae_cfg5_small", 4096, 16, 1, 0x5EED0005, int(0.01 * 2**32), int(0.1 * 2**32)),
@@ -72,7 +97,8 @@ def run_case(sim, inj, max_rounds=256):
 
 
 def main():
-    out = {"philox_kat": KAT, "peers": [], "origins": [], "random": [], "flood": [], "antientropy": []}
+    out = {"philox_kat": KAT, "peers": [], "origins": [], "random": [], "flood": [], "antientropy": [],
+           "random_faults": [], "flood_faults": []}
     for seed, N, t in [(0x5EED0001, 1 << 20, 0), (0x5EED0003, 1 << 24, 5), (7, 1000, 3), (0, 2, 0)]:
         nodes = sorted(set([i for i in range(16) if i < N] + [N - 1]))
         p = nr.peers(seed, N, t, 6, nodes=nodes)
@@ -92,6 +118,20 @@ def main():
         reads = {i: [r for r in range(R) if (int(sim.S[r // 64, i]) >> (r % 64)) & 1] for i in range(N)}
         out["flood"].append({"name": name, "N": N, "R": R, "adj": A, "inject": inj, "rounds": rounds,
                              "reads": reads})
+    for name, N, R, mode, k, seed, inj, loss, parts, stall, mr in RANDOM_FAULT_CASES:
+        sim = nr.Sim(N, R, mode, k, seed, edge_loss=loss, partitions=parts, stall_rounds=stall)
+        rounds = run_case(sim, inj, mr)
+        out["random_faults"].append({"name": name, "N": N, "R": R, "mode": mode, "k": k, "seed": seed,
+                                     "inject": inj, "edge_loss": loss, "partitions": parts, "stall_rounds": stall,
+                                     "max_rounds": mr, "rounds": rounds, "final_hash": nr.state_hash(sim.S),
+                                     "stalled": int((sim.streak >= stall).sum()) if stall else 0})
+    for name, N, R, A, inj, loss, parts, stall, mr in FLOOD_FAULT_CASES:
+        sim = nr.Sim(N, R, "flood", topology=A, edge_loss=loss, partitions=parts, stall_rounds=stall)
+        rounds = run_case(sim, inj, mr)
+        reads = {i: [r for r in range(R) if (int(sim.S[r // 64, i]) >> (r % 64)) & 1] for i in range(N)}
+        out["flood_faults"].append({"name": name, "N": N, "R": R, "adj": A, "inject": inj, "edge_loss": loss,
+                                    "partitions": parts, "stall_rounds": stall, "max_rounds": mr,
+                                    "rounds": rounds, "reads": reads})
     for name, N, K, k, seed, fail, rec in AE_CASES:
         sim = nr.AntiEntropySim(N, K, k, seed, fail, rec)
         sim.inject_random()

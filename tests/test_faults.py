@@ -46,9 +46,35 @@ def test_loss_only_slows():
     assert rounds[0] <= rounds[1] <= rounds[2] and rounds[0] < rounds[2]
 
 
-def test_faults_rejected_for_flood():
+def test_flood_faults_single_shard_only():
+    """FLOOD retries keep per-edge state on one shard; a sharded FLOOD engine, or
+    an ANTIENTROPY one (churn is its fault model), rejects faults."""
+    op.OracleEngine(25, 1, "flood", 0, 0, edge_loss=1)
     with pytest.raises(Exception):
-        op.OracleEngine(25, 1, "flood", 0, 0, edge_loss=1)
+        op.OracleEngine(25, 1, "flood", 0, 0, edge_loss=1, shard_count=2)
+    with pytest.raises(Exception):
+        op.OracleEngine(25, 1, "antientropy", 1, 0, stall_rounds=2)
+    e = op.OracleEngine(25, 1, "flood", 0, 0)  # created without faults: no per-edge state to retry from
+    with pytest.raises(Exception):
+        e.set_faults(1, 0)
+
+
+def test_stall_mode_properties():
+    """Stall mode: more stall-prone settings never spread further; without losses
+    nothing ever stalls; a long partition stalls every node that keeps losing its exchanges."""
+    N = 3000
+    full = []
+    for d in (0, 6, 3, 1):
+        e = op.OracleEngine(N, 8, "pushpull", 2, 9, flags=1, edge_loss=loss_threshold(0.15), stall_rounds=d)
+        e.inject_random()
+        res = e.step(60)
+        full.append(res.stats[-1]["full_nodes"])
+    assert full[0] == N and full[0] >= full[1] >= full[2] >= full[3] and full[3] < N
+    a = op.OracleEngine(N, 8, "pushpull", 2, 9, flags=1, stall_rounds=1)
+    b = op.OracleEngine(N, 8, "pushpull", 2, 9, flags=1)
+    for x in (a, b):
+        x.inject_random()
+    assert a.step(60).stats == b.step(60).stats
 
 
 def test_loss_threshold():

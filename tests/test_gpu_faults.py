@@ -75,3 +75,74 @@ def test_heal_partition_gpu():
     a, b = ref.step(100), e.step(100)
     assert a.stats == b.stats and b.converged
     assert np.array_equal(ref.read_shard(), e.read_shard())
+
+
+# --- stall mode and FLOOD retries, against the numpy goldens -------------------
+
+@pytest.mark.parametrize("path", list(PATHS))
+@pytest.mark.parametrize("idx", range(5))
+def test_random_faults_stall_golden_every_path(golden, idx, path):
+    """Edge loss / partitions and the stall mode on every round path (auto, dense, dense with the
+    peer-class filter, sparse, sparse all-D, direct) equal the numpy restatement round by round."""
+    from conftest import inject_case
+    c = golden["random_faults"][idx]
+    flags, params = PATHS[path]
+    e = Engine(c["N"], c["R"], c["mode"], c["k"], c["seed"], flags=1 | flags, edge_loss=c["edge_loss"],
+               partitions=c["partitions"], stall_rounds=c["stall_rounds"], params=params)
+    inject_case(e, c["inject"])
+    res = e.step(c["max_rounds"])
+    assert res.rounds == len(c["rounds"])
+    for got, inf, want in zip(res.stats, res.infected, c["rounds"]):
+        assert (got["full_nodes"], got["converged"], got["state_hash"]) == (want["full"], want["converged"], want["hash"])
+        assert [int(x) for x in inf] == want["infected"]
+    assert e.state_hash() == c["final_hash"]
+    e.close()
+
+
+@pytest.mark.parametrize("idx", range(6))
+def test_flood_faults_golden_gpu(golden, idx):
+    """FLOOD with per-edge retries and the deadline stall (round_flood_faults_kernel)."""
+    from conftest import inject_case
+    c = golden["flood_faults"][idx]
+    e = Engine(c["N"], c["R"], "flood", 0, 0, flags=1, edge_loss=c["edge_loss"], partitions=c["partitions"],
+               stall_rounds=c["stall_rounds"])
+    e.set_topology(c["adj"])
+    inject_case(e, c["inject"])
+    res = e.step(c["max_rounds"])
+    assert [s["messages"] for s in res.stats] == [r["messages"] for r in c["rounds"]]
+    assert [s["state_hash"] for s in res.stats] == [r["hash"] for r in c["rounds"]]
+    assert [s["full_nodes"] for s in res.stats] == [r["full"] for r in c["rounds"]]
+    for node, want in c["reads"].items():
+        assert e.read(int(node)) == want
+
+
+@pytest.mark.parametrize("idx", range(7))
+def test_flood_edge_kernel_without_losses_equals_flood_gpu(golden, idx):
+    """The per-edge FLOOD kernel with nothing lost reproduces the fault-free goldens."""
+    from conftest import inject_case
+    c = golden["flood"][idx]
+    e = Engine(c["N"], c["R"], "flood", 0, 0, flags=1, stall_rounds=1)
+    e.set_topology(c["adj"])
+    inject_case(e, c["inject"])
+    res = e.step(256)
+    assert [s["messages"] for s in res.stats] == [r["messages"] for r in c["rounds"]]
+    assert [s["state_hash"] for s in res.stats] == [r["hash"] for r in c["rounds"]]
+
+
+@pytest.mark.parametrize("plan", ["auto", "sparse", "dense"])
+def test_stall_sharded_lockstep(plan):
+    """Stall streaks are kept for all N nodes on every shard: G = 3 lockstep equals the oracle."""
+    N, R, k, seed, loss, D = 30011, 64, 2, 0x5EED0004, loss_threshold(0.1), 3
+    ref = op.OracleEngine(N, R, "pushpull", k, seed, flags=1, edge_loss=loss, stall_rounds=D)
+    ref.inject_random()
+    want, full = ref.step(200), ref.read_shard()
+    params = {} if plan == "auto" else {"sparse_frac": 1.0 if plan == "sparse" else -1}
+    engines = [Engine(N, R, "pushpull", k, seed, flags=1, shard_rank=r, shard_count=3, edge_loss=loss,
+                      stall_rounds=D, params=params) for r in range(3)]
+    for e in engines:
+        e.inject_random()
+    got, _ = lockstep_run(engines, 200)
+    assert got == want.stats
+    for e in engines:
+        assert np.array_equal(e.read_shard(), full[:, e.lo:e.hi])
+        e.close()

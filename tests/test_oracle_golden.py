@@ -81,3 +81,50 @@ def test_antientropy_golden(golden, idx):
         assert [int(x) for x in inf] == want["infected"]
     v, alive = e.read_versions(0)
     assert [int(x) for x in v] == c["node0"] and alive == c["node0_alive"]
+
+
+def _check_rounds(res, c, with_messages=False):
+    assert res.rounds == len(c["rounds"])
+    for got, inf, want in zip(res.stats, res.infected, c["rounds"]):
+        assert (got["round"], got["full_nodes"], got["converged"], got["state_hash"]) == \
+            (want["round"], want["full"], want["converged"], want["hash"])
+        if with_messages:
+            assert got["messages"] == want["messages"]
+        assert [int(x) for x in inf] == want["infected"]
+
+
+@pytest.mark.parametrize("idx", range(5))
+def test_random_faults_stall_golden(golden, idx):
+    """Edge loss / partitions and the stall mode (§2.9) against the numpy restatement."""
+    c = golden["random_faults"][idx]
+    e = op.OracleEngine(c["N"], c["R"], c["mode"], c["k"], c["seed"], flags=1, edge_loss=c["edge_loss"],
+                        partitions=c["partitions"], stall_rounds=c["stall_rounds"])
+    inject_case(e, c["inject"])
+    _check_rounds(e.step(c["max_rounds"]), c)
+    assert e.state_hash() == c["final_hash"]
+
+
+@pytest.mark.parametrize("idx", range(6))
+def test_flood_faults_golden(golden, idx):
+    """FLOOD with per-edge retries, dropped after stall_rounds attempts."""
+    c = golden["flood_faults"][idx]
+    e = op.OracleEngine(c["N"], c["R"], "flood", 0, flags=1, edge_loss=c["edge_loss"], partitions=c["partitions"],
+                        stall_rounds=c["stall_rounds"])
+    e.set_topology(c["adj"])
+    inject_case(e, c["inject"])
+    _check_rounds(e.step(c["max_rounds"]), c, with_messages=True)
+    for node, want in c["reads"].items():
+        assert e.read(int(node)) == want
+
+
+@pytest.mark.parametrize("idx", range(7))
+def test_flood_edge_state_without_faults_equals_flood(golden, idx):
+    """The per-edge retry formulation with faults switched off after create reduces to plain FLOOD
+    (same messages and states as the fault-free goldens)."""
+    c = golden["flood"][idx]
+    e = op.OracleEngine(c["N"], c["R"], "flood", 0, flags=1, stall_rounds=1)  # per-edge state, nothing lost
+    e.set_topology(c["adj"])
+    inject_case(e, c["inject"])
+    res = e.step(256)
+    assert [s["messages"] for s in res.stats] == [r["messages"] for r in c["rounds"]]
+    assert [s["state_hash"] for s in res.stats] == [r["hash"] for r in c["rounds"]]

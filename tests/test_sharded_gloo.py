@@ -15,6 +15,7 @@ import torch.multiprocessing as mp
 CASES = [
     ("pushpull", 2, 64, 3000, 0x5EED0004, None),
     ("pushpull-faults", 2, 64, 3000, 0x5EED0004, None),
+    ("pushpull-stall", 2, 64, 3000, 0x5EED0004, None),
     ("push", 3, 1, 2001, 0x5EED0001, None),
     ("pull", 2, 70, 1001, 11, None),
     ("flood", 0, 3, 49, 0, "grid"),
@@ -36,8 +37,13 @@ def _grid(n):
 
 
 def _faults(name):
-    """pushpull-faults: 25 % edge loss and 3 partitions"""
-    return {"edge_loss": 1 << 30, "partitions": 3} if name.endswith("-faults") else {}
+    """pushpull-faults: 25 % edge loss and 3 partitions; pushpull-stall: 10 % loss
+    and the stall mode with a 3-round deadline (§2.9)"""
+    if name.endswith("-faults"):
+        return {"edge_loss": 1 << 30, "partitions": 3}
+    if name.endswith("-stall"):
+        return {"edge_loss": 429496730, "stall_rounds": 3}
+    return {}
 
 
 PLANS = {"auto": None, "sparse": 1.0, "dense": -1}  # sparse_frac (gossip_set_param)
