@@ -1,0 +1,48 @@
+// ae_sharded.h — anti-entropy rounds with rows sharded over G engines (DESIGN.md §5.3,
+// SURVEY.md §8(e) "Design B": request / reply buckets over all-to-all, max-merge on the owner).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gossip {
+
+struct AexArgs {
+  const uint32_t* V;        // own rows S_t [Nl][K] (node lo + i)
+  uint32_t* Vn;             // own rows S_{t+1}
+  const uint64_t* alive;    // alive bits of every node before round t (global, G*Nl/64 words)
+  uint64_t* alive_n;        // after round t's churn
+  const uint64_t* stale;    // stale bits of S_t of every node (the all-gathered image)
+  uint64_t* stale_own;      // stale bits of S_{t+1} of the own nodes (next round's all-gather slice)
+  const uint32_t* target;   // global max vector [K]
+  uint64_t* partial;        // [0] full [1] alive [2] messages [3] hash [4..4+K) per component
+  uint64_t* cnt;            // [G + 1] items per owner (the last: own-own exchanges)
+  uint32_t* bcnt;           // [blocks][G + 1] per-block counts (aex_block_table_words)
+  uint64_t* boff;           // [blocks][G + 1] per-block offsets
+  uint32_t* req;            // request items, grouped by owner: {p, n, row[K]} padded to rw words
+  uint32_t* loc;            // own-own exchanges {n_local, p_local}
+  uint64_t N, Nl, lo, nown;
+  uint32_t G, rank, K, L, k, t, key0, key1, fail, rec, flags, rw, pw;
+};
+
+// entries of the per-block tables (bcnt, boff) for nown own nodes and G shards
+size_t aex_block_table_words(uint64_t nown, uint32_t G);
+
+// churn of round t over all N nodes (alive -> alive_n); then the own nodes' exchanges:
+// messages counted, those with a stale end listed (count pass, scan, fill pass)
+hipError_t launch_aex_requests(const AexArgs& a, hipStream_t st);
+// requests received (m items): max-merge into Vn, responses V_t[p] in the received order
+hipError_t launch_aex_serve(const AexArgs& a, const uint32_t* in, uint64_t m, uint32_t* resp, hipStream_t st);
+// the responses to the own requests (in request order), the own-own exchanges, then the
+// stats of S_{t+1} and its own stale bits
+hipError_t launch_aex_finish(const AexArgs& a, const uint32_t* resp, uint64_t nreq, uint64_t nloc, hipStream_t st);
+// own stale bits of V against target (after set_target)
+hipError_t launch_aex_stale(const AexArgs& a, const uint32_t* V, hipStream_t st);
+// initial versions of the own rows (Philox tag 3 with global node ids)
+hipError_t launch_aex_init(uint32_t* V, uint64_t lo, uint64_t nown, uint32_t K, uint32_t k0, uint32_t k1,
+                           hipStream_t st);
+// every node alive (n < N), as plain bitmap words
+hipError_t launch_aex_fill_alive(uint64_t* alive, uint64_t N, uint64_t words, hipStream_t st);
+// max over the own rows into out[K] (zeroed here)
+hipError_t launch_aex_local_max(const uint32_t* V, uint64_t nown, uint32_t K, uint32_t* out, hipStream_t st);
+
+}  // namespace gossip

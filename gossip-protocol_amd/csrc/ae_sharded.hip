@@ -1,0 +1,348 @@
+// ae_sharded.hip — anti-entropy (configs[4]) with the rows sharded by node id over G
+// engines: SURVEY.md §8(e) "Design B" — all-to-all of request buckets (the pushed
+// row) and reply buckets (the pulled row), max-merge on the owner; the global max
+// vector by an all-reduce MAX (ncclMax) of the shards' maxima.
+//
+// Reference: (*NodeState).Gossip, main.go:65-89 — here each exchange of the round
+// model is one SyncRPC-shaped request/reply between the two ends'
+// owners.  Every shard keeps the alive bits of all N nodes (churn is a per-node
+// Philox draw, tag 1, so no exchange is needed for it) and receives every shard's
+// stale bits (row != target) each round: an exchange between two rows equal to the
+// target moves nothing, so only exchanges with a stale end travel.
+#include "ae_sharded.h"
+
+#include "philox.h"
+#include "wave.h"
+
+namespace gossip {
+
+namespace {
+
+constexpr int kAxBlock = 256;
+constexpr uint32_t kAxMaxG = 1024;
+
+__device__ __forceinline__ bool bit_of(const uint64_t* w, uint64_t n) { return (w[n >> 6] >> (n & 63)) & 1ull; }
+
+__global__ __launch_bounds__(kAxBlock) void aex_churn_kernel(AexArgs a) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t words = a.G * a.Nl / 64;
+  for (uint64_t w = (uint64_t)blockIdx.x * (kAxBlock / 64) + (threadIdx.x >> 6); w < words;
+       w += (uint64_t)gridDim.x * (kAxBlock / 64)) {
+    const uint64_t n = w * 64 + lane;
+    bool al = false;
+    if (n < a.N) {
+      const bool was = (a.alive[w] >> lane) & 1ull;
+      const uint32_t x = philox4x32_10(u32x4{(uint32_t)n, a.t, 1u, 0u}, a.key0, a.key1).x;
+      al = was ? !(x < a.fail) : (x < a.rec);
+    }
+    const uint64_t b = __ballot(al);
+    if (lane == 0) a.alive_n[w] = b;
+  }
+}
+
+// Node range of block b (contiguous, so the fill pass reproduces the count pass's
+// per-block counts exactly).
+__device__ __forceinline__ void block_range(const AexArgs& a, uint64_t* i0, uint64_t* i1) {
+  const uint64_t per = (a.nown + gridDim.x - 1) / gridDim.x;
+  *i0 = min<uint64_t>((uint64_t)blockIdx.x * per, a.nown);
+  *i1 = min<uint64_t>(*i0 + per, a.nown);
+}
+
+// FILL = false: per-block item counts per owner (+ own-own exchanges in slot G) into
+// bcnt[b][G + 1] and the messages into partial[2].  FILL = true: the same walk, items
+// written at boff[b][q] + LDS cursor (request items {p, n, row[K]}, own-own pairs).
+template <bool FILL>
+__global__ __launch_bounds__(kAxBlock) void aex_list_kernel(AexArgs a, uint32_t* bcnt, const uint64_t* boff) {
+  __shared__ uint32_t c[kAxMaxG + 1];
+  __shared__ uint64_t red[kAxBlock / 64];
+  for (uint32_t q = threadIdx.x; q <= a.G; q += kAxBlock) c[q] = 0;
+  __syncthreads();
+  uint64_t i0, i1;
+  block_range(a, &i0, &i1);
+  const uint64_t nm1 = a.N - 1;
+  uint64_t msgs = 0;
+  for (uint64_t i = i0 + threadIdx.x; i < i1; i += kAxBlock) {
+    const uint64_t n = a.lo + i;
+    if (!bit_of(a.alive_n, n)) continue;
+    const bool sn = bit_of(a.stale, n);
+    u32x4 x{0, 0, 0, 0};
+    for (uint32_t j = 0; j < a.k; ++j) {
+      if ((j & 3u) == 0) x = philox4x32_10(u32x4{(uint32_t)n, a.t, 0u, j >> 2}, a.key0, a.key1);
+      const uint32_t p = peer_from_word(lane_of(x, j & 3u), nm1, (uint32_t)n);
+      if (!bit_of(a.alive_n, p)) continue;
+      ++msgs;
+      if (!sn && !bit_of(a.stale, p)) continue;  // two target rows: nothing moves
+      const uint32_t q = (uint32_t)(p / a.Nl);
+      const uint32_t slot = q == a.rank ? a.G : q;
+      const uint32_t pos = atomicAdd(&c[slot], 1u);
+      if (!FILL) continue;
+      const uint64_t at = boff[(uint64_t)blockIdx.x * (a.G + 1) + slot] + pos;
+      if (slot == a.G) {
+        a.loc[2 * at] = (uint32_t)i;
+        a.loc[2 * at + 1] = (uint32_t)(p - a.lo);
+      } else {
+        uint32_t* it = a.req + at * a.rw;
+        it[0] = p;
+        it[1] = (uint32_t)n;
+        const uint32_t* row = a.V + i * a.K;
+        for (uint32_t cc = 0; cc < a.K; ++cc) it[2 + cc] = row[cc];
+      }
+    }
+  }
+  __syncthreads();
+  if (!FILL) {
+    for (uint32_t q = threadIdx.x; q <= a.G; q += kAxBlock) bcnt[(uint64_t)blockIdx.x * (a.G + 1) + q] = c[q];
+    msgs = wave_sum64(msgs);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = msgs;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint64_t s = 0;
+      for (int w = 0; w < kAxBlock / 64; ++w) s += red[w];
+      if (s) atomicAdd((unsigned long long*)&a.partial[2], (unsigned long long)s);
+    }
+  }
+}
+
+// One block per slot q (owners 0..G-1, then G = own-own): exclusive scan of the
+// per-block counts; requests are laid out by owner (cnt[q] items from base[q]),
+// the own-own list from 0.
+__global__ __launch_bounds__(kAxBlock) void aex_scan_kernel(AexArgs a, const uint32_t* bcnt, uint64_t* boff,
+                                                            uint32_t nblocks) {
+  const uint32_t q = blockIdx.x;
+  __shared__ uint64_t tot[kAxBlock / 64];
+  __shared__ uint64_t qbase;
+  if (threadIdx.x == 0) {
+    uint64_t b = 0;  // owner q's requests start after those of owners < q
+    if (q < a.G)
+      for (uint32_t r = 0; r < q; ++r) b += a.cnt[r];
+    qbase = b;
+  }
+  __syncthreads();
+  // serial over chunks of the block list, a wave scan each (nblocks is a few thousand at most)
+  uint64_t run = qbase;
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (uint32_t b0 = 0; b0 < nblocks; b0 += kAxBlock) {
+    const uint32_t b = b0 + threadIdx.x;
+    const uint64_t v = b < nblocks ? bcnt[(uint64_t)b * (a.G + 1) + q] : 0;
+    uint64_t inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t y = __shfl_up(inc, o, 64);
+      if (lane >= (uint32_t)o) inc += y;
+    }
+    if (lane == 63) tot[wave] = inc;
+    __syncthreads();
+    uint64_t before = 0, all = 0;
+    for (int w = 0; w < kAxBlock / 64; ++w) {
+      before += w < (int)wave ? tot[w] : 0;
+      all += tot[w];
+    }
+    if (b < nblocks) boff[(uint64_t)b * (a.G + 1) + q] = run + before + inc - v;
+    run += all;
+    __syncthreads();
+  }
+}
+
+// per-owner totals from the per-block counts (cnt[q], q <= G)
+__global__ __launch_bounds__(kAxBlock) void aex_total_kernel(AexArgs a, const uint32_t* bcnt, uint32_t nblocks) {
+  const uint32_t q = blockIdx.x;
+  uint64_t s = 0;
+  for (uint32_t b = threadIdx.x; b < nblocks; b += kAxBlock) s += bcnt[(uint64_t)b * (a.G + 1) + q];
+  __shared__ uint64_t red[kAxBlock / 64];
+  s = wave_sum64(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (int w = 0; w < kAxBlock / 64; ++w) t += red[w];
+    a.cnt[q] = t;
+  }
+}
+
+// requests received: lanes = components of one item; max-merge the pushed row into
+// Vn[p] (only where it is larger than S_t: Vn >= S_t throughout), answer S_t[p]
+__global__ __launch_bounds__(kAxBlock) void aex_serve_kernel(AexArgs a, const uint32_t* __restrict__ in, uint64_t m,
+                                                             uint32_t* __restrict__ resp) {
+  const uint32_t per = kAxBlock / a.L, c = threadIdx.x % a.L;
+  for (uint64_t it = (uint64_t)blockIdx.x * per + threadIdx.x / a.L; it < m; it += (uint64_t)gridDim.x * per) {
+    if (c >= a.K) continue;
+    const uint64_t pl = in[it * a.rw] - a.lo;
+    const uint32_t vp = a.V[pl * a.K + c];
+    resp[it * a.pw + c] = vp;
+    const uint32_t rv = in[it * a.rw + 2 + c];
+    if (rv > vp) atomicMax(&a.Vn[pl * a.K + c], rv);
+  }
+}
+
+// the replies to the own requests (request order) and the own-own exchanges
+__global__ __launch_bounds__(kAxBlock) void aex_merge_kernel(AexArgs a, const uint32_t* __restrict__ resp,
+                                                             uint64_t nreq, uint64_t nloc) {
+  const uint32_t per = kAxBlock / a.L, c = threadIdx.x % a.L;
+  for (uint64_t it = (uint64_t)blockIdx.x * per + threadIdx.x / a.L; it < nreq + nloc;
+       it += (uint64_t)gridDim.x * per) {
+    if (c >= a.K) continue;
+    if (it < nreq) {
+      const uint64_t nl = a.req[it * a.rw + 1] - a.lo;
+      const uint32_t rv = resp[it * a.pw + c];
+      if (rv > a.V[nl * a.K + c]) atomicMax(&a.Vn[nl * a.K + c], rv);
+    } else {
+      const uint64_t e = it - nreq;
+      const uint64_t nl = a.loc[2 * e], pl = a.loc[2 * e + 1];
+      const uint32_t vn = a.V[nl * a.K + c], vp = a.V[pl * a.K + c];
+      if (vp > vn) atomicMax(&a.Vn[nl * a.K + c], vp);
+      if (vn > vp) atomicMax(&a.Vn[pl * a.K + c], vn);
+    }
+  }
+}
+
+// Stats of the own rows R (S_{t+1}) with the alive bits after the churn, one wave per
+// 64 own nodes, one lane per node: full, alive, per-component counts, hash (global
+// ids, every node as on one shard), and the own stale words (STATS = false: the
+// stale words only).
+template <bool STATS>
+__global__ __launch_bounds__(kAxBlock) void aex_stats_kernel(AexArgs a, const uint32_t* __restrict__ R) {
+  __shared__ uint32_t cnt[64];
+  __shared__ uint32_t tgt[64];
+  __shared__ uint64_t red[3][kAxBlock / 64];
+  if (threadIdx.x < 64) {
+    cnt[threadIdx.x] = 0;
+    tgt[threadIdx.x] = threadIdx.x < a.K ? a.target[threadIdx.x] : 0u;
+  }
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t chunks = (a.nown + 63) / 64;
+  uint64_t hash = 0, full = 0, nal = 0;
+  for (uint64_t ch = (uint64_t)blockIdx.x * (kAxBlock / 64) + (threadIdx.x >> 6); ch < chunks;
+       ch += (uint64_t)gridDim.x * (kAxBlock / 64)) {
+    const uint64_t i = ch * 64 + lane;
+    const bool valid = i < a.nown;
+    const uint64_t n = a.lo + i;
+    const bool al = valid && bit_of(a.alive_n, n);
+    bool stale = false;
+    for (uint32_t c = 0; c < a.K; ++c) {
+      const uint32_t v = valid ? R[i * a.K + c] : 0u;
+      if (STATS && (a.flags & 1u) && v) hash += mix64((uint64_t)v + ((uint64_t)c * a.N + n) * kGold64);
+      const bool eq = valid && v == tgt[c];
+      stale = stale || (valid && !eq);
+      if (STATS) {
+        const uint64_t m = __ballot(eq && al);
+        if (lane == 0 && m) atomicAdd(&cnt[c], (uint32_t)__popcll(m));
+      }
+    }
+    const uint64_t sw = __ballot(stale);
+    if (lane == 0 && a.stale_own) a.stale_own[ch] = sw;
+    if (STATS) {
+      full += (uint64_t)__popcll(__ballot(al && !stale));
+      nal += (uint64_t)__popcll(__ballot(al));
+    }
+  }
+  if (!STATS) return;
+  if (lane != 0) full = nal = 0;  // wave-uniform: counted once per wave
+  hash = wave_sum64(hash);
+  full = wave_sum64(full);
+  nal = wave_sum64(nal);
+  if (lane == 0) {
+    red[0][threadIdx.x >> 6] = hash;
+    red[1][threadIdx.x >> 6] = full;
+    red[2][threadIdx.x >> 6] = nal;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    uint64_t s = 0;
+    for (int w = 0; w < kAxBlock / 64; ++w) s += red[threadIdx.x][w];
+    const uint32_t slot = threadIdx.x == 0 ? 3u : threadIdx.x == 1 ? 0u : 1u;
+    if (s) atomicAdd((unsigned long long*)&a.partial[slot], (unsigned long long)s);
+  }
+  if (threadIdx.x < a.K && cnt[threadIdx.x])
+    atomicAdd((unsigned long long*)&a.partial[4 + threadIdx.x], (unsigned long long)cnt[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(kAxBlock) void aex_init_kernel(uint32_t* V, uint64_t lo, uint64_t nown, uint32_t K,
+                                                            uint32_t k0, uint32_t k1) {
+  const uint32_t c4 = (K + 3) / 4;
+  for (uint64_t x = (uint64_t)blockIdx.x * kAxBlock + threadIdx.x; x < nown * c4; x += (uint64_t)gridDim.x * kAxBlock) {
+    const uint64_t i = x / c4;
+    const uint32_t q = (uint32_t)(x % c4);
+    const u32x4 r = philox4x32_10(u32x4{(uint32_t)(lo + i), q, 3u, 0u}, k0, k1);
+    for (uint32_t s = 0; s < 4 && 4 * q + s < K; ++s) V[i * K + 4 * q + s] = lane_of(r, s) & 0xFFFFu;
+  }
+}
+
+__global__ __launch_bounds__(kAxBlock) void aex_fill_alive_kernel(uint64_t* alive, uint64_t N, uint64_t words) {
+  for (uint64_t w = (uint64_t)blockIdx.x * kAxBlock + threadIdx.x; w < words; w += (uint64_t)gridDim.x * kAxBlock)
+    alive[w] = (w + 1) * 64 <= N ? ~0ull : (w * 64 < N ? (1ull << (N & 63)) - 1ull : 0ull);
+}
+
+__global__ __launch_bounds__(kAxBlock) void aex_max_kernel(const uint32_t* V, uint64_t nown, uint32_t K, uint32_t* out) {
+  __shared__ uint32_t m[64];
+  if (threadIdx.x < 64) m[threadIdx.x] = 0;
+  __syncthreads();
+  for (uint64_t x = (uint64_t)blockIdx.x * kAxBlock + threadIdx.x; x < nown * K; x += (uint64_t)gridDim.x * kAxBlock)
+    atomicMax(&m[x % K], V[x]);
+  __syncthreads();
+  if (threadIdx.x < K && m[threadIdx.x]) atomicMax(&out[threadIdx.x], m[threadIdx.x]);
+}
+
+uint32_t ax_grid(uint64_t units, uint32_t per_block, uint32_t cap) {
+  const uint64_t b = (units + per_block - 1) / per_block;
+  return (uint32_t)(b == 0 ? 1 : (b < cap ? b : cap));
+}
+
+uint32_t list_blocks(uint64_t nown) { return ax_grid(nown, 4 * kAxBlock, 2048); }
+
+}  // namespace
+
+size_t aex_block_table_words(uint64_t nown, uint32_t G) { return (size_t)list_blocks(nown) * (G + 1); }
+
+hipError_t launch_aex_requests(const AexArgs& a, hipStream_t st) {
+  if (a.G > kAxMaxG) return hipErrorInvalidValue;
+  const uint32_t words = (uint32_t)(a.G * a.Nl / 64);
+  aex_churn_kernel<<<ax_grid(words, kAxBlock / 64, 8192), kAxBlock, 0, st>>>(a);
+  const uint32_t nb = list_blocks(a.nown);
+  uint32_t* bcnt = a.bcnt;
+  uint64_t* boff = a.boff;
+  aex_list_kernel<false><<<nb, kAxBlock, 0, st>>>(a, bcnt, nullptr);
+  aex_total_kernel<<<a.G + 1, kAxBlock, 0, st>>>(a, bcnt, nb);
+  aex_scan_kernel<<<a.G + 1, kAxBlock, 0, st>>>(a, bcnt, boff, nb);
+  aex_list_kernel<true><<<nb, kAxBlock, 0, st>>>(a, bcnt, boff);
+  return hipGetLastError();
+}
+
+hipError_t launch_aex_serve(const AexArgs& a, const uint32_t* in, uint64_t m, uint32_t* resp, hipStream_t st) {
+  if (m == 0) return hipSuccess;
+  aex_serve_kernel<<<ax_grid(m, kAxBlock / a.L, 65536), kAxBlock, 0, st>>>(a, in, m, resp);
+  return hipGetLastError();
+}
+
+hipError_t launch_aex_finish(const AexArgs& a, const uint32_t* resp, uint64_t nreq, uint64_t nloc, hipStream_t st) {
+  if (nreq + nloc)
+    aex_merge_kernel<<<ax_grid(nreq + nloc, kAxBlock / a.L, 65536), kAxBlock, 0, st>>>(a, resp, nreq, nloc);
+  aex_stats_kernel<true><<<ax_grid((a.nown + 63) / 64, kAxBlock / 64, 8192), kAxBlock, 0, st>>>(a, a.Vn);
+  return hipGetLastError();
+}
+
+hipError_t launch_aex_stale(const AexArgs& a, const uint32_t* V, hipStream_t st) {
+  aex_stats_kernel<false><<<ax_grid((a.nown + 63) / 64, kAxBlock / 64, 8192), kAxBlock, 0, st>>>(a, V);
+  return hipGetLastError();
+}
+
+hipError_t launch_aex_init(uint32_t* V, uint64_t lo, uint64_t nown, uint32_t K, uint32_t k0, uint32_t k1,
+                           hipStream_t st) {
+  if (nown == 0) return hipSuccess;
+  aex_init_kernel<<<ax_grid(nown * ((K + 3) / 4), kAxBlock, 65536), kAxBlock, 0, st>>>(V, lo, nown, K, k0, k1);
+  return hipGetLastError();
+}
+
+hipError_t launch_aex_fill_alive(uint64_t* alive, uint64_t N, uint64_t words, hipStream_t st) {
+  aex_fill_alive_kernel<<<ax_grid(words, kAxBlock, 1024), kAxBlock, 0, st>>>(alive, N, words);
+  return hipGetLastError();
+}
+
+hipError_t launch_aex_local_max(const uint32_t* V, uint64_t nown, uint32_t K, uint32_t* out, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(out, 0, K * 4, st);
+  if (e != hipSuccess || nown == 0) return e;
+  aex_max_kernel<<<ax_grid(nown * K, kAxBlock, 4096), kAxBlock, 0, st>>>(V, nown, K, out);
+  return hipGetLastError();
+}
+
+}  // namespace gossip

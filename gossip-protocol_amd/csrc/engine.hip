@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../../include/gossip.h"
+#include "ae_sharded.h"
 #include "antientropy.h"
 #include "binned.h"
 #include "frontier.h"
@@ -96,6 +97,15 @@ struct gossip_engine {
   bool ae_sb_valid = false;      // the stale bits of alive, ae_hash and ae_stale describe V
   bool ae_sparse_last = false;   // the last round ran in place (V not rotated)
   uint64_t ae_sparse_rounds = 0, ae_overflows = 0;
+  // sharded ANTIENTROPY (G > 1): V/Vn = own rows [Nl][K], alive/alive_n =
+  // plain alive bitmaps of all N nodes, aex_stale = every shard's stale words (all-gather image)
+  bool aex = false;
+  bool aex_target_ok = false;
+  uint32_t aex_rw = 0, aex_pw = 0;
+  uint64_t *aex_stale = nullptr, *aex_cnt = nullptr, *aex_boff = nullptr, *aex_cnt_h = nullptr;
+  uint32_t *aex_bcnt = nullptr, *aex_req = nullptr, *aex_loc = nullptr, *aex_in = nullptr, *aex_resp_out = nullptr,
+           *aex_resp_in = nullptr, *aex_tmp = nullptr;
+  uint64_t aex_req_cap = 0, aex_in_cap = 0, aex_out_cap = 0, aex_nin = 0, aex_nreq = 0, aex_nloc = 0;
   // binned (LDS) pipeline for W == 1 random modes on one shard
   bool binned = false;
   BinGeom bg{};
@@ -200,7 +210,9 @@ void free_all(gossip_engine* e) {
     if (b) (void)hipFree(b);
   if (e->sx_host) (void)hipHostFree(e->sx_host);
   void* ae[] = {e->V, e->Vn, e->target, e->alive, e->alive_n, e->ae_aux, e->ae_claim, e->ae_eid, e->ae_erow, e->ae_segn, e->ae_pmask,
-                e->ae_brec, e->ae_boff};
+                e->ae_brec, e->ae_boff, e->aex_stale, e->aex_cnt, e->aex_boff, e->aex_bcnt, e->aex_req, e->aex_loc,
+                e->aex_in, e->aex_resp_out, e->aex_resp_in, e->aex_tmp};
+  if (e->aex_cnt_h) (void)hipHostFree(e->aex_cnt_h);
   for (void* b : ae)
     if (b) (void)hipFree(b);
   if (e->partial_h) (void)hipHostFree(e->partial_h);
@@ -281,6 +293,11 @@ int timer_collect(gossip_engine* e) {
 // exchange payload for this round: S_t (random modes) or F_t (FLOOD); the
 // send slice lies inside the gathered image, so the all-gather is in place.
 int prepare_send(gossip_engine* e, uint64_t** send, uint64_t** image) {
+  if (e->aex) {  // sharded ANTIENTROPY: the own stale words into every shard's image
+    *send = e->aex_stale + (size_t)e->rank * e->Nl / 64;
+    *image = e->aex_stale;
+    return GOSSIP_OK;
+  }
   if (e->mode == GOSSIP_MODE_ANTIENTROPY) {  // single shard: nothing to exchange
     *send = *image = nullptr;
     return GOSSIP_OK;
@@ -710,6 +727,41 @@ void rotate(gossip_engine* e) {
   }
 }
 
+AexArgs make_aex_args(gossip_engine* e) {
+  AexArgs a{};
+  a.V = e->V;
+  a.Vn = e->Vn;
+  a.alive = e->alive;
+  a.alive_n = e->alive_n;
+  a.stale = e->aex_stale;
+  a.stale_own = e->aex_stale + (size_t)e->rank * e->Nl / 64;
+  a.target = e->target;
+  a.partial = e->partial_d;
+  a.cnt = e->aex_cnt;
+  a.bcnt = e->aex_bcnt;
+  a.boff = e->aex_boff;
+  a.req = e->aex_req;
+  a.loc = e->aex_loc;
+  a.N = e->N;
+  a.Nl = e->Nl;
+  a.lo = e->lo;
+  a.nown = e->nown;
+  a.G = e->G;
+  a.rank = e->rank;
+  a.K = e->R;
+  a.L = ae_lanes(e->R);
+  a.k = e->k;
+  a.t = e->t;
+  a.key0 = e->key0;
+  a.key1 = e->key1;
+  a.fail = e->cfg.churn_fail;
+  a.rec = e->cfg.churn_recover;
+  a.flags = e->cfg.flags;
+  a.rw = e->aex_rw;
+  a.pw = e->aex_pw;
+  return a;
+}
+
 // ANTIENTROPY sparse-round edge lists.  cap_req = 0: the
 // default capacity (N/8 edges covers the churn tail at configs[4]; small
 // engines get room for every exchange, k per node, so never overflow); else
@@ -786,9 +838,12 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
     g_create_error = "unknown mode";
     return GOSSIP_ENOTSUP;
   }
-  if (cfg->mode == GOSSIP_MODE_ANTIENTROPY &&
-      ((cfg->shard_count ? cfg->shard_count : 1) != 1 || cfg->n_rumors > 64)) {
-    g_create_error = "ANTIENTROPY runs on one shard with at most 64 components";
+  if (cfg->mode == GOSSIP_MODE_ANTIENTROPY && cfg->n_rumors > 64) {
+    g_create_error = "ANTIENTROPY has at most 64 components";
+    return GOSSIP_ENOTSUP;
+  }
+  if (cfg->mode == GOSSIP_MODE_ANTIENTROPY && (cfg->shard_count ? cfg->shard_count : 1) > 1024) {
+    g_create_error = "sharded ANTIENTROPY supports at most 1024 shards";
     return GOSSIP_ENOTSUP;
   }
   if (cfg->mode != GOSSIP_MODE_FLOOD && (cfg->fanout == 0 || cfg->fanout > 64)) {
@@ -838,6 +893,8 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
   e->G = G;
   e->rank = cfg->shard_rank;
   e->Nl = (e->N + G - 1) / G;
+  e->aex = e->mode == GOSSIP_MODE_ANTIENTROPY && G > 1;
+  if (e->aex) e->Nl = (e->Nl + 63) / 64 * 64;  // 64-aligned row blocks: whole bitmap words per shard
   e->lo = std::min<uint64_t>((uint64_t)e->rank * e->Nl, e->N);
   e->hi = std::min<uint64_t>(e->lo + e->Nl, e->N);
   e->nown = e->hi - e->lo;
@@ -888,7 +945,24 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
     }
     return hipMemset(*p, 0, bytes) == hipSuccess;
   };
-  if (e->mode == GOSSIP_MODE_ANTIENTROPY) {
+  if (e->aex) {  // sharded ANTIENTROPY
+    const size_t vb = std::max<size_t>((size_t)e->Nl * e->R * 4, 4);
+    const size_t gw = (size_t)G * e->Nl / 64;  // bitmap words of all shards
+    e->aex_rw = (e->R + 2 + 1) / 2 * 2;        // request item {p, n, row[K]}, padded to 8 B
+    e->aex_pw = (e->R + 1) / 2 * 2;            // response item row[K], padded to 8 B
+    e->aex_req_cap = std::max<uint64_t>(e->nown * e->k, 1);
+    const size_t tab = aex_block_table_words(e->nown, G);
+    if (!alloc_raw((void**)&e->V, vb) || !alloc_raw((void**)&e->Vn, vb) || !alloc_raw((void**)&e->target, 256) ||
+        !alloc_raw((void**)&e->alive, gw * 8) || !alloc_raw((void**)&e->alive_n, gw * 8) ||
+        !alloc_raw((void**)&e->aex_stale, gw * 8) || !alloc_raw((void**)&e->aex_cnt, (G + 1) * 8) ||
+        !alloc_raw((void**)&e->aex_bcnt, tab * 4) || !alloc_raw((void**)&e->aex_boff, tab * 8) ||
+        !alloc_raw((void**)&e->aex_req, e->aex_req_cap * e->aex_rw * 4) ||
+        !alloc_raw((void**)&e->aex_loc, e->aex_req_cap * 8) ||
+        !alloc_raw((void**)&e->aex_resp_in, e->aex_req_cap * e->aex_pw * 4) || !alloc_raw((void**)&e->aex_tmp, 256))
+      return bail(GOSSIP_ENOMEM);
+    if (hipHostMalloc((void**)&e->aex_cnt_h, (G + 1) * 8) != hipSuccess) return bail(GOSSIP_ENOMEM);
+    if (launch_aex_fill_alive(e->alive, e->N, gw, nullptr) != hipSuccess) return bail(GOSSIP_EHIP);
+  } else if (e->mode == GOSSIP_MODE_ANTIENTROPY) {
     const size_t vb = (size_t)e->N * e->R * 4;
     const size_t nw = ((size_t)e->N + 63) / 64;
     if (!alloc_raw((void**)&e->V, vb) || !alloc_raw((void**)&e->Vn, vb) || !alloc_raw((void**)&e->target, 256) ||
@@ -1124,7 +1198,12 @@ int gossip_reset(gossip_engine_t* e) {
   if (!e) return GOSSIP_EINVAL;
   if (int rc = set_dev(e)) return rc;
   const size_t shard = (size_t)e->W * e->Nl * 8;
-  if (e->mode == GOSSIP_MODE_ANTIENTROPY) {
+  if (e->aex) {
+    HIP_OK(e, hipMemsetAsync(e->V, 0, (size_t)e->Nl * e->R * 4, e->stream));
+    HIP_OK(e, hipMemsetAsync(e->target, 0, 256, e->stream));
+    HIP_OK(e, launch_aex_fill_alive(e->alive, e->N, (uint64_t)e->G * e->Nl / 64, e->stream));
+    e->aex_target_ok = false;
+  } else if (e->mode == GOSSIP_MODE_ANTIENTROPY) {
     HIP_OK(e, hipMemsetAsync(e->V, 0, e->N * e->R * 4, e->stream));
     HIP_OK(e, hipMemsetAsync(e->target, 0, 256, e->stream));
     HIP_OK(e, launch_ae_fill_alive(e->alive, e->N, e->stream));
@@ -1169,6 +1248,12 @@ int gossip_inject(gossip_engine_t* e, uint64_t node, uint32_t rumor) {
   if (node >= e->N || rumor >= e->R) return e->fail(GOSSIP_EINVAL, "inject(%llu, %u) out of range",
                                                     (unsigned long long)node, rumor);
   if (int rc = set_dev(e)) return rc;
+  if (e->aex) {  // a local write on the owner; the global max vector is re-derived before the next round
+    if (node >= e->lo && node < e->hi)
+      HIP_OK(e, launch_ae_inject(e->V, e->aex_tmp, node - e->lo, e->R, rumor, e->stream));
+    e->aex_target_ok = false;
+    return GOSSIP_OK;
+  }
   if (e->mode == GOSSIP_MODE_ANTIENTROPY) {
     HIP_OK(e, launch_ae_inject(e->V, e->target, node, e->R, rumor, e->stream));
     e->ae_sb_valid = false;  // the target may have moved
@@ -1187,6 +1272,11 @@ int gossip_inject(gossip_engine_t* e, uint64_t node, uint32_t rumor) {
 int gossip_inject_random(gossip_engine_t* e) {
   if (!e) return GOSSIP_EINVAL;
   if (int rc = set_dev(e)) return rc;
+  if (e->aex) {
+    HIP_OK(e, launch_aex_init(e->V, e->lo, e->nown, e->R, e->key0, e->key1, e->stream));
+    e->aex_target_ok = false;
+    return GOSSIP_OK;
+  }
   if (e->mode == GOSSIP_MODE_ANTIENTROPY) {
     HIP_OK(e, launch_ae_init(e->V, e->target, e->N, e->R, e->key0, e->key1, e->stream));
     e->ae_sb_valid = false;
@@ -1214,7 +1304,7 @@ int gossip_exchange_buffers(gossip_engine_t* e, void** send, void** recv, uint64
   HIP_OK(e, hipStreamSynchronize(e->stream));
   if (send) *send = s;
   if (recv) *recv = img;
-  if (send_bytes) *send_bytes = (uint64_t)e->W * e->Nl * 8;
+  if (send_bytes) *send_bytes = e->aex ? e->Nl / 8 : (uint64_t)e->W * e->Nl * 8;
   return GOSSIP_OK;
 }
 
@@ -1235,6 +1325,7 @@ int gossip_dense_prepare(gossip_engine_t* e) {
 
 int gossip_round_compute(gossip_engine_t* e, uint64_t* partial) {
   if (!e || !partial) return GOSSIP_EINVAL;
+  if (e->aex) return e->fail(GOSSIP_ESTATE, "sharded ANTIENTROPY rounds run through the gossip_ae_* calls");
   if (e->mode == GOSSIP_MODE_FLOOD && !e->has_topo) return e->fail(GOSSIP_ESTATE, "FLOOD needs a topology");
   if (int rc = set_dev(e)) return rc;
   if (int rc = compute_round(e, current_image(e))) return rc;
@@ -1316,6 +1407,10 @@ int gossip_local_totals(gossip_engine_t* e, uint64_t* partial) {
 int gossip_sharded_plan(gossip_engine_t* e, const uint64_t* total, int32_t* kind) {
   if (!e || !kind) return GOSSIP_EINVAL;
   e->sx_planned = false;
+  if (e->aex) {  // 2: an anti-entropy exchange round; -2: the global max vector is needed first
+    *kind = e->aex_target_ok ? 2 : -2;
+    return GOSSIP_OK;
+  }
   if (!e->sx) {
     *kind = 0;
     return GOSSIP_OK;
@@ -1409,6 +1504,116 @@ int gossip_sparse_commit(gossip_engine_t* e, uint64_t items, uint64_t* partial) 
   return GOSSIP_OK;
 }
 
+// --- sharded ANTIENTROPY (include/gossip.h) -------------------------
+
+namespace {
+int aex_check(gossip_engine* e) {
+  if (!e) return GOSSIP_EINVAL;
+  if (!e->aex) return e->fail(GOSSIP_ENOTSUP, "gossip_ae_* calls drive sharded ANTIENTROPY engines (G > 1)");
+  return set_dev(e);
+}
+}  // namespace
+
+uint32_t gossip_ae_item_words(const gossip_engine_t* e, uint32_t which) {
+  if (!e || !e->aex) return 0;
+  return which == 0 ? e->aex_rw : e->aex_pw;
+}
+
+int gossip_ae_local_target(gossip_engine_t* e, uint32_t* out) {
+  if (!out) return GOSSIP_EINVAL;
+  if (int rc = aex_check(e)) return rc;
+  HIP_OK(e, launch_aex_local_max(e->V, e->nown, e->R, e->aex_tmp, e->stream));
+  HIP_OK(e, hipMemcpyAsync(e->partial_h, e->aex_tmp, e->R * 4, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(e, hipStreamSynchronize(e->stream));
+  std::memcpy(out, e->partial_h, e->R * 4);
+  return GOSSIP_OK;
+}
+
+int gossip_ae_set_target(gossip_engine_t* e, const uint32_t* target) {
+  if (!target) return GOSSIP_EINVAL;
+  if (int rc = aex_check(e)) return rc;
+  std::memcpy(e->partial_h, target, e->R * 4);
+  HIP_OK(e, hipMemcpyAsync(e->target, e->partial_h, e->R * 4, hipMemcpyHostToDevice, e->stream));
+  HIP_OK(e, launch_aex_stale(make_aex_args(e), e->V, e->stream));  // own stale words of S_t
+  HIP_OK(e, hipStreamSynchronize(e->stream));
+  e->aex_target_ok = true;
+  return GOSSIP_OK;
+}
+
+int gossip_ae_requests(gossip_engine_t* e, void** send, uint64_t* send_counts) {
+  if (!send || !send_counts) return GOSSIP_EINVAL;
+  if (int rc = aex_check(e)) return rc;
+  if (!e->aex_target_ok) return e->fail(GOSSIP_ESTATE, "the global max vector is stale: gossip_ae_set_target first");
+  const AexArgs a = make_aex_args(e);
+  HIP_OK(e, hipMemsetAsync(e->partial_d, 0, part_len(e) * 8, e->stream));
+  HIP_OK(e, hipMemcpyAsync(e->Vn, e->V, std::max<size_t>((size_t)e->nown * e->R * 4, 0), hipMemcpyDeviceToDevice,
+                           e->stream));  // S_{t+1} starts as S_t (max only grows)
+  if (int rc = timer_begin(e, 0)) return rc;
+  HIP_OK(e, launch_aex_requests(a, e->stream));
+  HIP_OK(e, hipMemcpyAsync(e->aex_cnt_h, e->aex_cnt, (e->G + 1) * 8, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(e, hipStreamSynchronize(e->stream));
+  uint64_t nreq = 0;
+  for (uint32_t q = 0; q < e->G; ++q) {
+    send_counts[q] = e->aex_cnt_h[q];
+    nreq += e->aex_cnt_h[q];
+  }
+  e->aex_nreq = nreq;
+  e->aex_nloc = e->aex_cnt_h[e->G];
+  *send = e->aex_req;
+  return GOSSIP_OK;
+}
+
+int gossip_ae_request_recv(gossip_engine_t* e, uint64_t items, void** recv) {
+  if (!recv) return GOSSIP_EINVAL;
+  if (int rc = aex_check(e)) return rc;
+  if (items > e->aex_in_cap || !e->aex_in) {  // grow both the inbox and the replies to it
+    const uint64_t want = std::max<uint64_t>(items + items / 4, 1024);
+    for (uint32_t** b : {&e->aex_in, &e->aex_resp_out})
+      if (*b) {
+        HIP_OK(e, hipFree(*b));
+        *b = nullptr;
+      }
+    e->aex_in_cap = 0;
+    HIP_OK(e, hipMalloc((void**)&e->aex_in, want * e->aex_rw * 4));
+    HIP_OK(e, hipMalloc((void**)&e->aex_resp_out, want * e->aex_pw * 4));
+    e->aex_in_cap = want;
+  }
+  e->aex_nin = items;
+  *recv = e->aex_in;
+  return GOSSIP_OK;
+}
+
+int gossip_ae_serve(gossip_engine_t* e, void** send) {
+  if (!send) return GOSSIP_EINVAL;
+  if (int rc = aex_check(e)) return rc;
+  if (!e->aex_in) return e->fail(GOSSIP_ESTATE, "gossip_ae_request_recv first");
+  HIP_OK(e, launch_aex_serve(make_aex_args(e), e->aex_in, e->aex_nin, e->aex_resp_out, e->stream));
+  HIP_OK(e, hipStreamSynchronize(e->stream));
+  *send = e->aex_resp_out;
+  return GOSSIP_OK;
+}
+
+int gossip_ae_response_recv(gossip_engine_t* e, void** recv) {
+  if (!recv) return GOSSIP_EINVAL;
+  if (int rc = aex_check(e)) return rc;
+  *recv = e->aex_resp_in;  // room for every own request (nown * k items)
+  return GOSSIP_OK;
+}
+
+int gossip_ae_finish(gossip_engine_t* e, uint64_t* partial) {
+  if (!partial) return GOSSIP_EINVAL;
+  if (int rc = aex_check(e)) return rc;
+  HIP_OK(e, launch_aex_finish(make_aex_args(e), e->aex_resp_in, e->aex_nreq, e->aex_nloc, e->stream));
+  if (int rc = timer_end(e, 0)) return rc;
+  HIP_OK(e, hipMemcpyAsync(e->partial_h, e->partial_d, part_len(e) * 8, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(e, hipStreamSynchronize(e->stream));
+  if (int rc = timer_collect(e)) return rc;
+  std::memcpy(partial, e->partial_h, part_len(e) * 8);
+  partial[4 + e->R] = 0;  // (nonzero count: random modes only)
+  e->last_sparse = false;
+  return GOSSIP_OK;
+}
+
 int gossip_set_faults(gossip_engine_t* e, uint32_t edge_loss, uint32_t partitions) {
   if (!e) return GOSSIP_EINVAL;
   if ((edge_loss || partitions > 1) &&
@@ -1472,14 +1677,36 @@ int gossip_read_versions(gossip_engine_t* e, uint64_t node, uint32_t* out, uint3
   if (!e || !out) return GOSSIP_EINVAL;
   if (e->mode != GOSSIP_MODE_ANTIENTROPY) return e->fail(GOSSIP_ESTATE, "read_versions needs ANTIENTROPY mode");
   if (node >= e->N || ncomp < e->R) return e->fail(GOSSIP_EINVAL, "bad node or component count");
+  if (e->aex && (node < e->lo || node >= e->hi))
+    return e->fail(GOSSIP_EINVAL, "node %llu not in this shard", (unsigned long long)node);
   if (int rc = set_dev(e)) return rc;
   HIP_OK(e, hipStreamSynchronize(e->stream));
+  if (e->aex) {
+    HIP_OK(e, hipMemcpy(out, e->V + (node - e->lo) * e->R, e->R * 4, hipMemcpyDeviceToHost));
+    if (alive) {
+      uint64_t w = 0;
+      HIP_OK(e, hipMemcpy(&w, e->alive + node / 64, 8, hipMemcpyDeviceToHost));
+      *alive = (uint32_t)((w >> (node & 63)) & 1ull);
+    }
+    return GOSSIP_OK;
+  }
   HIP_OK(e, hipMemcpy(out, e->V + node * e->R, e->R * 4, hipMemcpyDeviceToHost));
   if (alive) {
     uint64_t w = 0;
     HIP_OK(e, hipMemcpy(&w, e->alive + 2 * (node / 64), 8, hipMemcpyDeviceToHost));
     *alive = (uint32_t)((w >> (node & 63)) & 1ull);
   }
+  return GOSSIP_OK;
+}
+
+int gossip_read_rows(gossip_engine_t* e, uint32_t* out, uint64_t n_values) {
+  if (!e || !out) return GOSSIP_EINVAL;
+  if (e->mode != GOSSIP_MODE_ANTIENTROPY) return e->fail(GOSSIP_ESTATE, "read_rows needs ANTIENTROPY mode");
+  if (n_values < e->nown * e->R) return e->fail(GOSSIP_EINVAL, "output too small");
+  if (int rc = set_dev(e)) return rc;
+  HIP_OK(e, hipStreamSynchronize(e->stream));
+  const uint32_t* src = e->aex ? e->V : e->V + e->lo * e->R;
+  HIP_OK(e, hipMemcpy(out, src, e->nown * e->R * 4, hipMemcpyDeviceToHost));
   return GOSSIP_OK;
 }
 
@@ -1493,6 +1720,19 @@ int gossip_shard_range(const gossip_engine_t* e, uint64_t* lo, uint64_t* hi) {
 int gossip_state_hash(gossip_engine_t* e, uint64_t* out) {
   if (!e || !out) return GOSSIP_EINVAL;
   if (int rc = set_dev(e)) return rc;
+  if (e->aex) {  // this shard's part: hash terms of the own rows (global ids); shards' parts add up
+    AexArgs a = make_aex_args(e);
+    a.flags |= GOSSIP_FLAG_HASH;
+    a.Vn = e->V;
+    a.alive_n = e->alive;
+    a.stale_own = nullptr;  // (the stale words are not wanted here)
+    HIP_OK(e, hipMemsetAsync(e->partial_d, 0, part_len(e) * 8, e->stream));
+    HIP_OK(e, launch_aex_finish(a, nullptr, 0, 0, e->stream));
+    HIP_OK(e, hipMemcpyAsync(e->partial_h, e->partial_d, part_len(e) * 8, hipMemcpyDeviceToHost, e->stream));
+    HIP_OK(e, hipStreamSynchronize(e->stream));
+    *out = e->partial_h[3];
+    return GOSSIP_OK;
+  }
   if (e->mode == GOSSIP_MODE_ANTIENTROPY) {  // the stats kernel's hash of the current rows
     AeArgs a = make_ae_args(e);
     a.flags |= GOSSIP_FLAG_HASH;

@@ -82,7 +82,16 @@ SIGNATURES = [
     ("sparse_scan", C.c_int, [P, U64P, C.POINTER(P), U64P]),
     ("sparse_msg_recv", C.c_int, [P, C.c_uint64, C.POINTER(P)]),
     ("sparse_commit", C.c_int, [P, C.c_uint64, U64P]),
+    ("ae_item_words", C.c_uint32, [P, C.c_uint32]),
+    ("ae_local_target", C.c_int, [P, U32P]),
+    ("ae_set_target", C.c_int, [P, U32P]),
+    ("ae_requests", C.c_int, [P, C.POINTER(P), U64P]),
+    ("ae_request_recv", C.c_int, [P, C.c_uint64, C.POINTER(P)]),
+    ("ae_serve", C.c_int, [P, C.POINTER(P)]),
+    ("ae_response_recv", C.c_int, [P, C.POINTER(P)]),
+    ("ae_finish", C.c_int, [P, U64P]),
     ("read_bitset", C.c_int, [P, C.c_uint64, U64P, C.c_uint32]),
+    ("read_rows", C.c_int, [P, U32P, C.c_uint64]),
     ("read_shard", C.c_int, [P, U64P, C.c_uint64]),
     ("read_versions", C.c_int, [P, C.c_uint64, U32P, C.c_uint32, U32P]),
     ("shard_range", C.c_int, [P, U64P, U64P]),

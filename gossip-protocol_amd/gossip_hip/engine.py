@@ -200,6 +200,13 @@ class AbiEngine:
                                               C.c_uint32(self.n_rumors), C.byref(alive)))
         return out, bool(alive.value)
 
+    def read_rows(self) -> np.ndarray:
+        """ANTIENTROPY: the owned rows, [nodes, K] uint32."""
+        n = self.hi - self.lo
+        out = np.zeros(n * self.n_rumors, dtype=np.uint32)
+        self._check(self._fn("read_rows")(self._h, out.ctypes.data_as(_abi.U32P), C.c_uint64(out.size)))
+        return out.reshape(n, self.n_rumors)
+
     def read_shard(self) -> np.ndarray:
         n = self.hi - self.lo
         out = np.zeros(self.n_words * n, dtype=np.uint64)
@@ -278,6 +285,47 @@ class AbiEngine:
         ptr = C.c_void_p()
         self._check(self._fn("sparse_msg_recv")(self._h, items, C.byref(ptr)))
         return ptr.value
+
+    # -- sharded ANTIENTROPY (include/gossip.h gossip_ae_*; gossip_hip.sharded drives them) --
+    def ae_item_words(self, which: int) -> int:
+        """uint32 words of a request (0) or response (1) item, padded to 8 bytes."""
+        return int(self._fn("ae_item_words")(self._h, which))
+
+    def ae_local_target(self) -> np.ndarray:
+        out = np.zeros(self.n_rumors, dtype=np.uint32)
+        self._check(self._fn("ae_local_target")(self._h, out.ctypes.data_as(_abi.U32P)))
+        return out
+
+    def ae_set_target(self, target) -> None:
+        t = np.ascontiguousarray(target, dtype=np.uint32)
+        self._check(self._fn("ae_set_target")(self._h, t.ctypes.data_as(_abi.U32P)))
+
+    def ae_requests(self):
+        """(device pointer, items per owner) of this round's request items."""
+        ptr = C.c_void_p()
+        out = np.zeros(self.cfg.shard_count, dtype=np.uint64)
+        self._check(self._fn("ae_requests")(self._h, C.byref(ptr), out.ctypes.data_as(_abi.U64P)))
+        return ptr.value, [int(x) for x in out]
+
+    def ae_request_recv(self, items: int) -> int:
+        ptr = C.c_void_p()
+        self._check(self._fn("ae_request_recv")(self._h, C.c_uint64(items), C.byref(ptr)))
+        return ptr.value
+
+    def ae_serve(self) -> int:
+        ptr = C.c_void_p()
+        self._check(self._fn("ae_serve")(self._h, C.byref(ptr)))
+        return ptr.value
+
+    def ae_response_recv(self) -> int:
+        ptr = C.c_void_p()
+        self._check(self._fn("ae_response_recv")(self._h, C.byref(ptr)))
+        return ptr.value
+
+    def ae_finish(self) -> np.ndarray:
+        out = np.zeros(self.partial_len(), dtype=np.uint64)
+        self._check(self._fn("ae_finish")(self._h, out.ctypes.data_as(_abi.U64P)))
+        return out
 
     def sparse_commit(self, items: int) -> np.ndarray:
         out = np.zeros(self.partial_len(), dtype=np.uint64)

@@ -11,7 +11,11 @@ without a GPU):
                 then an all-reduce of the stats partials;
   sparse round  (the engine's plan, when one class of nodes is rare) all-gather
                 of each shard's rare nodes {id, value}, all-to-all of the pushes
-                that land on another shard, all-reduce of the partials.
+                that land on another shard, all-reduce of the partials;
+  ANTIENTROPY   ("Design B") all-gather of the stale bits,
+                all-to-all of request items {p, n, V_t[n]} to p's owner and of its
+                replies V_t[p], all-reduce of the partials; the global max vector
+                by an all-reduce MAX (ncclMax) after any injection.
 
 The engine decides the kind from the global totals it was last given, so every
 rank takes the same branch.
@@ -96,6 +100,11 @@ class _Comm:
         t = torch.as_tensor(np.asarray(values, dtype=np.int64).copy())
         return t.cuda() if self.direct else t
 
+    def all_reduce_max(self, values: np.ndarray) -> np.ndarray:
+        t = self.small(np.asarray(values, dtype=np.int64))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return t.cpu().numpy()
+
     def all_reduce_sum(self, partial: np.ndarray) -> np.ndarray:
         t = self.small(partial.view(np.int64))
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
@@ -116,6 +125,10 @@ def _plan(engine, comm: _Comm) -> int:
     if not engine.supports("sharded_plan"):
         return 0
     kind = engine.sharded_plan()
+    if kind == -2:  # ANTIENTROPY: the global max vector after an injection (ncclMax over the shards)
+        t = engine.ae_local_target()
+        engine.ae_set_target(comm.all_reduce_max(t) if comm.world > 1 else t)
+        kind = engine.sharded_plan()
     if kind < 0:  # no global totals yet (after reset / inject): all-reduce the shards' own
         kind = engine.sharded_plan(comm.all_reduce_sum(engine.local_totals()) if comm.world > 1
                                    else engine.local_totals())
@@ -167,13 +180,42 @@ def _bind_stream(engine, comm: _Comm):
         engine.set_stream(torch.cuda.current_stream().cuda_stream)
 
 
+def _ae_round(engine, comm: _Comm) -> np.ndarray:
+    w = comm.world
+    rw, pw = engine.ae_item_words(0), engine.ae_item_words(1)  # uint32 words, even: whole int64s
+    send_p, recv_p, nbytes = engine.exchange_buffers()  # own stale words -> every shard's image
+    if w > 1:
+        comm.all_gather(_as_tensor(recv_p, nbytes * w, engine.on_device), _as_tensor(send_p, nbytes, engine.on_device))
+    req_p, counts = engine.ae_requests()
+    in_counts = comm.all_to_all_small(counts) if w > 1 else counts
+    n_in = sum(in_counts)
+    in_p = engine.ae_request_recv(n_in)
+    if sum(counts) or n_in:
+        comm.all_to_all(_as_tensor(in_p, n_in * rw * 4, engine.on_device),
+                        _as_tensor(req_p, sum(counts) * rw * 4, engine.on_device),
+                        [c * rw // 2 for c in in_counts], [c * rw // 2 for c in counts])
+    resp_p = engine.ae_serve()  # replies in the received order
+    back_p = engine.ae_response_recv()
+    if sum(counts) or n_in:
+        comm.all_to_all(_as_tensor(back_p, sum(counts) * pw * 4, engine.on_device),
+                        _as_tensor(resp_p, n_in * pw * 4, engine.on_device),
+                        [c * pw // 2 for c in counts], [c * pw // 2 for c in in_counts])
+    return engine.ae_finish()
+
+
 def sharded_round(engine, group=None) -> dict:
     """Runs one round of a sharded engine; every rank must call it.  With RCCL the engine is
     bound to the caller's current torch stream, so every kernel is ordered after the
     collectives that feed it."""
     comm = _Comm(engine, group)
     _bind_stream(engine, comm)
-    partial = _sparse_round(engine, comm) if _plan(engine, comm) == 1 else _dense_round(engine, comm)
+    kind = _plan(engine, comm)
+    if kind == 2:
+        partial = _ae_round(engine, comm)
+    elif kind == 1:
+        partial = _sparse_round(engine, comm)
+    else:
+        partial = _dense_round(engine, comm)
     if comm.world > 1:
         partial = comm.all_reduce_sum(partial)
     return engine.round_commit(partial)
@@ -250,6 +292,46 @@ def _lockstep_sparse(engines):
     return [e.sparse_commit(n) for e, n in zip(engines, n_in)]
 
 
+def _lockstep_ae(engines):
+    G = len(engines)
+    rw, pw = engines[0].ae_item_words(0), engines[0].ae_item_words(1)
+    bufs = [e.exchange_buffers() for e in engines]
+    for e, (_, recv_p, nbytes) in zip(engines, bufs):  # all-gather of the stale words
+        recv = _as_tensor(recv_p, nbytes * G, True, e.device)
+        for q, (send_q, _, _) in enumerate(bufs):
+            if engines[q] is not e:
+                recv[q * nbytes // 8:(q + 1) * nbytes // 8].copy_(_as_tensor(send_q, nbytes, True, engines[q].device))
+    _sync_all(engines)
+    reqs = [e.ae_requests() for e in engines]  # (ptr, counts[owner])
+    n_in = [sum(reqs[q][1][r] for q in range(G)) for r in range(G)]
+    inbox = [e.ae_request_recv(n) for e, n in zip(engines, n_in)]
+    w64 = rw // 2
+    for r in range(G):  # all-to-all: owner r receives from q = 0..G-1 in order
+        dst = _as_tensor(inbox[r], n_in[r] * rw * 4, True, engines[r].device)
+        at = 0
+        for q, (rp, cnt) in enumerate(reqs):
+            if cnt[r]:
+                src = _as_tensor(rp, sum(cnt) * rw * 4, True, engines[q].device)
+                off = sum(cnt[:r])
+                dst[at * w64:(at + cnt[r]) * w64].copy_(src[off * w64:(off + cnt[r]) * w64])
+                at += cnt[r]
+    _sync_all(engines)
+    resp = [e.ae_serve() for e in engines]
+    back = [e.ae_response_recv() for e in engines]
+    p64 = pw // 2
+    for q, (_, cnt) in enumerate(reqs):  # replies return to requester q in its request order
+        dst = _as_tensor(back[q], sum(cnt) * pw * 4, True, engines[q].device)
+        at = 0
+        for r in range(G):
+            if cnt[r]:
+                src = _as_tensor(resp[r], n_in[r] * pw * 4, True, engines[r].device)
+                start = sum(reqs[q2][1][r] for q2 in range(q))  # where q's items landed in r's inbox
+                dst[at * p64:(at + cnt[r]) * p64].copy_(src[start * p64:(start + cnt[r]) * p64])
+                at += cnt[r]
+    _sync_all(engines)
+    return [e.ae_finish() for e in engines]
+
+
 def lockstep_run(engines, max_rounds: int):
     """One process driving G shard engines (one per GPU, or several on one) through the
     same rounds as sharded_run, with device copies in place of the collectives.
@@ -257,12 +339,18 @@ def lockstep_run(engines, max_rounds: int):
     stats, kinds = [], []
     for _ in range(max_rounds):
         ks = [e.sharded_plan() for e in engines]
-        if ks[0] < 0:
+        if ks[0] == -2:  # ANTIENTROPY: global max vector = elementwise max of the shards' (ncclMax)
+            t = np.maximum.reduce([e.ae_local_target() for e in engines])
+            for e in engines:
+                e.ae_set_target(t)
+            ks = [e.sharded_plan() for e in engines]
+        if ks[0] == -1:
             tot = _lockstep_sum([e.local_totals() for e in engines])
             ks = [e.sharded_plan(tot) for e in engines]
         assert len(set(ks)) == 1
         kinds.append(ks[0])
-        parts = _lockstep_sparse(engines) if ks[0] == 1 else _lockstep_dense(engines)
+        parts = (_lockstep_ae(engines) if ks[0] == 2 else _lockstep_sparse(engines) if ks[0] == 1
+                 else _lockstep_dense(engines))
         tot = _lockstep_sum(parts)
         st = [e.round_commit(tot) for e in engines]
         assert all(s == st[0] for s in st)

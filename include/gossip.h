@@ -213,12 +213,40 @@ int gossip_sparse_scan(gossip_engine_t* eng, const uint64_t* counts, void** send
 int gossip_sparse_msg_recv(gossip_engine_t* eng, uint64_t items, void** recv);
 int gossip_sparse_commit(gossip_engine_t* eng, uint64_t items, uint64_t* partial);
 
+/* --- sharded ANTIENTROPY rounds (G > 1; DESIGN.md §5.3, "Design B") --------------
+ * Rows are sharded by node id in 64-aligned blocks (Nl = ceil(ceil(N/G)/64)*64); every
+ * shard keeps the alive bits of all N nodes (churn is a per-node Philox draw) and, per
+ * round, receives every shard's stale bits (row != the global max vector).  An exchange
+ * (n, p_j(n,t)) between two alive nodes with a stale end whose peer lives on another
+ * shard becomes one request item {p, n, V_t[n]} to p's owner, who max-merges it into p
+ * and answers V_t[p], which n's owner max-merges into n.  Items are uint32 words padded
+ * to 8 bytes: request = gossip_ae_item_words(eng, 0) words, response = (eng, 1).
+ * Per round:
+ *   gossip_sharded_plan -> kind -2: the global max vector is stale (after reset / inject):
+ *        gossip_ae_local_target(out[K]) -> all-reduce(MAX) -> gossip_ae_set_target; plan again
+ *   kind 2: gossip_exchange_buffers(send = own stale words, recv = all shards') -> all-gather
+ *        gossip_ae_requests(&send, send_counts[G])          churn + request items by owner
+ *        all-to-all of the counts; gossip_ae_request_recv(total_in, &recv); all-to-all items
+ *        gossip_ae_serve(&send)                             responses, in the received order
+ *        gossip_ae_response_recv(&recv); all-to-all back (the counts swapped)
+ *        gossip_ae_finish(partial)                          -> all-reduce(SUM) -> gossip_round_commit */
+uint32_t gossip_ae_item_words(const gossip_engine_t* eng, uint32_t which);
+int gossip_ae_local_target(gossip_engine_t* eng, uint32_t* out);
+int gossip_ae_set_target(gossip_engine_t* eng, const uint32_t* target);
+int gossip_ae_requests(gossip_engine_t* eng, void** send, uint64_t* send_counts);
+int gossip_ae_request_recv(gossip_engine_t* eng, uint64_t items, void** recv);
+int gossip_ae_serve(gossip_engine_t* eng, void** send);
+int gossip_ae_response_recv(gossip_engine_t* eng, void** recv);
+int gossip_ae_finish(gossip_engine_t* eng, uint64_t* partial);
+
 /* Readout ("read" handler, main.go:123-130).  Bitset of one node (nwords >= W),
  * or the whole owned shard in logical order out[w * Nl_owned + i]. */
 int gossip_read_bitset(gossip_engine_t* eng, uint64_t node, uint64_t* out, uint32_t nwords);
 int gossip_read_shard(gossip_engine_t* eng, uint64_t* out, uint64_t n_words);
-/* ANTIENTROPY readout: the K versions of one node, and its alive flag. */
+/* ANTIENTROPY readout: the K versions of one node (owned by this shard), and its alive flag. */
 int gossip_read_versions(gossip_engine_t* eng, uint64_t node, uint32_t* out, uint32_t ncomp, uint32_t* alive);
+/* ANTIENTROPY readout of every owned row: out[i * K + c] for owned node lo + i. */
+int gossip_read_rows(gossip_engine_t* eng, uint32_t* out, uint64_t n_values);
 /* Owned node range [lo, hi). */
 int gossip_shard_range(const gossip_engine_t* eng, uint64_t* lo, uint64_t* hi);
 

@@ -57,6 +57,13 @@ struct oracle_sim {
   uint32_t npend;
   uint64_t *pend, *pend_n, *skipE, *skipE_n;
   uint32_t* ieo;
+  /* sharded ANTIENTROPY (G > 1): V/Vn = own rows [Nl][K], alive bytes of all N,
+   * aex_stale = every shard's stale words (the all-gather image), request / reply items */
+  int aex, aex_target_ok;
+  uint32_t rw, pw;
+  uint64_t* aex_stale;
+  uint32_t *req, *loc, *in, *resp_out, *resp_in;
+  uint64_t nreq, nloc, nin, in_cap, aex_msgs;
 };
 
 /* ---------------- Philox4x32-10 (Random123; rocRAND philox4x32_10.h:270-302) ---- */
@@ -147,7 +154,7 @@ int oracle_create(const gossip_config_t* cfg, int threads, oracle_sim_t** out) {
   if (cfg->mode != GOSSIP_MODE_FLOOD && (cfg->fanout == 0 || cfg->fanout > 64)) return GOSSIP_EINVAL;
   uint32_t G = cfg->shard_count ? cfg->shard_count : 1;
   if (cfg->shard_rank >= G) return GOSSIP_EINVAL;
-  if (cfg->mode == GOSSIP_MODE_ANTIENTROPY && (G != 1 || cfg->n_rumors > 64)) return GOSSIP_ENOTSUP;
+  if (cfg->mode == GOSSIP_MODE_ANTIENTROPY && (cfg->n_rumors > 64 || G > 1024)) return GOSSIP_ENOTSUP;
   if (cfg->stall_rounds > 16) return GOSSIP_EINVAL;
   const int faulty = cfg->edge_loss || cfg->partitions > 1 || cfg->stall_rounds;
   if (faulty && (cfg->mode == GOSSIP_MODE_ANTIENTROPY || (cfg->mode == GOSSIP_MODE_FLOOD && G != 1)))
@@ -164,6 +171,8 @@ int oracle_create(const gossip_config_t* cfg, int threads, oracle_sim_t** out) {
   s->G = G;
   s->rank = cfg->shard_rank;
   s->Nl = (s->N + G - 1) / G;
+  s->aex = s->mode == GOSSIP_MODE_ANTIENTROPY && G > 1;
+  if (s->aex) s->Nl = (s->Nl + 63) / 64 * 64; /* 64-aligned row blocks, as the engine */
   s->lo = (uint64_t)s->rank * s->Nl;
   s->hi = s->lo + s->Nl < s->N ? s->lo + s->Nl : s->N;
   if (s->lo > s->hi) s->lo = s->hi;
@@ -179,8 +188,18 @@ int oracle_create(const gossip_config_t* cfg, int threads, oracle_sim_t** out) {
     s->skip = (uint64_t*)calloc(shard, 8);
   }
   if (s->mode == GOSSIP_MODE_ANTIENTROPY) {
-    s->V = (uint32_t*)calloc((size_t)s->N * s->R, 4);
-    s->Vn = (uint32_t*)calloc((size_t)s->N * s->R, 4);
+    const size_t rows = s->aex ? s->Nl : s->N;
+    s->V = (uint32_t*)calloc(rows * s->R + 1, 4);
+    s->Vn = (uint32_t*)calloc(rows * s->R + 1, 4);
+    if (s->aex) {
+      s->rw = (s->R + 3) / 2 * 2;
+      s->pw = (s->R + 1) / 2 * 2;
+      s->aex_stale = (uint64_t*)calloc((size_t)G * s->Nl / 64 + 1, 8);
+      const size_t cap = (size_t)s->nown * s->k + 1;
+      s->req = (uint32_t*)calloc(cap * s->rw, 4);
+      s->loc = (uint32_t*)calloc(cap * 2, 4);
+      s->resp_in = (uint32_t*)calloc(cap * s->pw, 4);
+    }
     s->target = (uint32_t*)calloc(s->R, 4);
     s->alive = (uint8_t*)malloc(s->N);
     s->alive_n = (uint8_t*)malloc(s->N);
@@ -225,6 +244,7 @@ void oracle_destroy(oracle_sim_t* s) {
   free(s->gtot); free(s->counts); free(s->rare_send); free(s->rare_recv); free(s->msg_send); free(s->msg_recv);
   free(s->D);
   free(s->streak); free(s->pend); free(s->pend_n); free(s->skipE); free(s->skipE_n); free(s->ieo);
+  free(s->aex_stale); free(s->req); free(s->loc); free(s->in); free(s->resp_out); free(s->resp_in);
   free(s);
 }
 
@@ -300,8 +320,9 @@ int oracle_reset(oracle_sim_t* s) {
   memset(s->Snext, 0, shard);
   if (s->Sprev) memset(s->Sprev, 0, shard);
   if (s->skip) memset(s->skip, 0, shard);
+  s->aex_target_ok = 0;
   if (s->V) {
-    memset(s->V, 0, (size_t)s->N * s->R * 4);
+    memset(s->V, 0, (size_t)(s->aex ? s->Nl : s->N) * s->R * 4);
     memset(s->target, 0, (size_t)s->R * 4);
     memset(s->alive, 1, s->N);
   }
@@ -319,6 +340,11 @@ int oracle_reset(oracle_sim_t* s) {
  * the bit set.  Injected bits carry no sender in Adj, so skip stays 0 for them. */
 int oracle_inject(oracle_sim_t* s, uint64_t node, uint32_t rumor) {
   if (!s || node >= s->N || rumor >= s->R) return GOSSIP_EINVAL;
+  if (s->aex) { /* a local write on the owner; the global max vector is re-derived before a round */
+    if (node >= s->lo && node < s->hi) s->V[(node - s->lo) * s->R + rumor] += 1;
+    s->aex_target_ok = 0;
+    return GOSSIP_OK;
+  }
   if (s->mode == GOSSIP_MODE_ANTIENTROPY) { /* a local write of key `rumor` */
     uint32_t* x = &s->V[node * s->R + rumor];
     *x += 1;
@@ -336,13 +362,14 @@ int oracle_inject_random(oracle_sim_t* s) {
   if (s->mode == GOSSIP_MODE_ANTIENTROPY) { /* V[n][c] = Philox({n, c/4, 3, 0})[c%4] & 0xFFFF */
     const uint32_t key[2] = {(uint32_t)s->cfg.seed, (uint32_t)(s->cfg.seed >> 32)};
     memset(s->target, 0, (size_t)s->R * 4);
-    for (uint64_t n = 0; n < s->N; ++n)
+    s->aex_target_ok = 0;
+    for (uint64_t n = s->aex ? s->lo : 0; n < (s->aex ? s->hi : s->N); ++n)
       for (uint32_t c = 0; c < s->R; c += 4) {
         uint32_t ctr[4] = {(uint32_t)n, c >> 2, 3u, 0u}, x[4];
         oracle_philox4x32_10(ctr, key, x);
         for (uint32_t q = 0; q < 4 && c + q < s->R; ++q) {
           uint32_t v = x[q] & 0xFFFFu;
-          s->V[n * s->R + c + q] = v;
+          s->V[(n - (s->aex ? s->lo : 0)) * s->R + c + q] = v;
           if (v > s->target[c + q]) s->target[c + q] = v;
         }
       }
@@ -358,6 +385,12 @@ uint64_t oracle_partial_len(const oracle_sim_t* s) { return 5 + (s ? s->R : 0); 
 /* Exchange payload: S_t for random modes, the frontier F_t = S_t & ~S_{t-1} for FLOOD. */
 int oracle_exchange_buffers(oracle_sim_t* s, void** send, void** recv, uint64_t* send_bytes) {
   if (!s) return GOSSIP_EINVAL;
+  if (s->aex) { /* own stale words into every shard's image */
+    if (send) *send = s->aex_stale + (size_t)s->rank * s->Nl / 64;
+    if (recv) *recv = s->aex_stale;
+    if (send_bytes) *send_bytes = s->Nl / 8;
+    return GOSSIP_OK;
+  }
   if (s->mode == GOSSIP_MODE_ANTIENTROPY) return GOSSIP_OK; /* single shard: nothing to exchange */
   size_t shard = (size_t)s->W * s->Nl;
   if (s->mode == GOSSIP_MODE_FLOOD)
@@ -734,6 +767,10 @@ int oracle_local_totals(oracle_sim_t* s, uint64_t* partial) {
 int oracle_sharded_plan(oracle_sim_t* s, const uint64_t* total, int32_t* kind) {
   if (!s || !kind) return GOSSIP_EINVAL;
   s->planned = 0;
+  if (s->aex) {
+    *kind = s->aex_target_ok ? 2 : -2;
+    return GOSSIP_OK;
+  }
   if (!sparse_ok(s)) {
     *kind = 0;
     return GOSSIP_OK;
@@ -977,9 +1014,174 @@ int oracle_state_hash(oracle_sim_t* s, uint64_t* out) {
 
 int oracle_read_versions(oracle_sim_t* s, uint64_t node, uint32_t* out, uint32_t ncomp, uint32_t* alive) {
   if (!s || !out || !s->V || node >= s->N || ncomp < s->R) return GOSSIP_EINVAL;
-  memcpy(out, s->V + node * s->R, (size_t)s->R * 4);
+  if (s->aex && (node < s->lo || node >= s->hi)) return GOSSIP_EINVAL;
+  memcpy(out, s->V + (node - (s->aex ? s->lo : 0)) * s->R, (size_t)s->R * 4);
   if (alive) *alive = s->alive[node];
   return GOSSIP_OK;
 }
 
 uint32_t oracle_round_index(const oracle_sim_t* s) { return s ? s->t : 0; }
+
+int oracle_read_rows(oracle_sim_t* s, uint32_t* out, uint64_t n_values) {
+  if (!s || !out || !s->V || n_values < s->nown * s->R) return GOSSIP_EINVAL;
+  memcpy(out, s->V + (s->aex ? 0 : s->lo * s->R), (size_t)s->nown * s->R * 4);
+  return GOSSIP_OK;
+}
+
+/* ---------------- sharded ANTIENTROPY (include/gossip.h gossip_ae_*) --------
+ * Rows sharded in 64-aligned blocks; every shard churns the alive flags of all N nodes (a
+ * per-node Philox draw) and receives every shard's stale words per round.  An exchange
+ * (n, p_j(n,t)) of two alive nodes with a stale end and p on another shard is a request item
+ * {p, n, V_t[n]} to p's owner, who max-merges it into p and answers V_t[p]. */
+static inline int stale_bit(const oracle_sim_t* s, uint64_t n) { return (s->aex_stale[n >> 6] >> (n & 63)) & 1; }
+
+static void aex_own_stale(oracle_sim_t* s, const uint32_t* V) {
+  uint64_t* own = s->aex_stale + (size_t)s->rank * s->Nl / 64;
+  memset(own, 0, s->Nl / 8);
+  for (uint64_t i = 0; i < s->nown; ++i)
+    for (uint32_t c = 0; c < s->R; ++c)
+      if (V[i * s->R + c] != s->target[c]) {
+        own[i >> 6] |= 1ull << (i & 63);
+        break;
+      }
+}
+
+uint32_t oracle_ae_item_words(const oracle_sim_t* s, uint32_t which) {
+  return s && s->aex ? (which == 0 ? s->rw : s->pw) : 0;
+}
+
+int oracle_ae_local_target(oracle_sim_t* s, uint32_t* out) {
+  if (!s || !out || !s->aex) return GOSSIP_EINVAL;
+  memset(out, 0, (size_t)s->R * 4);
+  for (uint64_t i = 0; i < s->nown; ++i)
+    for (uint32_t c = 0; c < s->R; ++c)
+      if (s->V[i * s->R + c] > out[c]) out[c] = s->V[i * s->R + c];
+  return GOSSIP_OK;
+}
+
+int oracle_ae_set_target(oracle_sim_t* s, const uint32_t* target) {
+  if (!s || !target || !s->aex) return GOSSIP_EINVAL;
+  memcpy(s->target, target, (size_t)s->R * 4);
+  aex_own_stale(s, s->V);
+  s->aex_target_ok = 1;
+  return GOSSIP_OK;
+}
+
+int oracle_ae_requests(oracle_sim_t* s, void** send, uint64_t* send_counts) {
+  if (!s || !send || !send_counts || !s->aex || !s->aex_target_ok) return GOSSIP_EINVAL;
+  const uint32_t key[2] = {(uint32_t)s->cfg.seed, (uint32_t)(s->cfg.seed >> 32)};
+  const uint32_t K = s->R;
+  for (uint64_t n = 0; n < s->N; ++n)
+    s->alive_n[n] = (uint8_t)churned(s->alive[n], (uint32_t)n, s->t, key, s->cfg.churn_fail, s->cfg.churn_recover);
+  memcpy(s->Vn, s->V, (size_t)s->nown * K * 4);
+  s->aex_msgs = 0;
+  s->nreq = s->nloc = 0;
+  for (uint32_t q = 0; q < s->G; ++q) send_counts[q] = 0;
+  /* pass 0: messages and own-own pairs; pass q + 1: the requests to owner q, in node order */
+  for (uint32_t pass = 0; pass <= s->G; ++pass) {
+    for (uint64_t i = 0; i < s->nown; ++i) {
+      const uint64_t n = s->lo + i;
+      if (!s->alive_n[n]) continue;
+      uint32_t x[4] = {0, 0, 0, 0};
+      for (uint32_t j = 0; j < s->k; ++j) {
+        if ((j & 3) == 0) {
+          uint32_t ctr[4] = {(uint32_t)n, s->t, 0u, j >> 2};
+          oracle_philox4x32_10(ctr, key, x);
+        }
+        const uint32_t p = peer_from_word(x[j & 3], s->N, (uint32_t)n);
+        if (!s->alive_n[p]) continue;
+        if (pass == 0) ++s->aex_msgs;
+        if (!stale_bit(s, n) && !stale_bit(s, p)) continue;
+        const uint32_t q = (uint32_t)(p / s->Nl);
+        if (pass == 0) {
+          if (q == s->rank) {
+            s->loc[2 * s->nloc] = (uint32_t)i;
+            s->loc[2 * s->nloc + 1] = (uint32_t)(p - s->lo);
+            ++s->nloc;
+          }
+        } else if (q == pass - 1 && q != s->rank) {
+          uint32_t* it = s->req + s->nreq * s->rw;
+          it[0] = p;
+          it[1] = (uint32_t)n;
+          memcpy(it + 2, s->V + i * K, (size_t)K * 4);
+          ++s->nreq;
+          ++send_counts[q];
+        }
+      }
+    }
+  }
+  *send = s->req;
+  return GOSSIP_OK;
+}
+
+int oracle_ae_request_recv(oracle_sim_t* s, uint64_t items, void** recv) {
+  if (!s || !recv || !s->aex) return GOSSIP_EINVAL;
+  if (items > s->in_cap || !s->in) {
+    free(s->in);
+    free(s->resp_out);
+    s->in = (uint32_t*)calloc((items + 1) * s->rw, 4);
+    s->resp_out = (uint32_t*)calloc((items + 1) * s->pw, 4);
+    if (!s->in || !s->resp_out) return GOSSIP_ENOMEM;
+    s->in_cap = items;
+  }
+  s->nin = items;
+  *recv = s->in;
+  return GOSSIP_OK;
+}
+
+int oracle_ae_serve(oracle_sim_t* s, void** send) {
+  if (!s || !send || !s->aex || !s->in) return GOSSIP_EINVAL;
+  const uint32_t K = s->R;
+  for (uint64_t m = 0; m < s->nin; ++m) {
+    const uint32_t* it = s->in + m * s->rw;
+    const uint64_t pl = it[0] - s->lo;
+    for (uint32_t c = 0; c < K; ++c) {
+      s->resp_out[m * s->pw + c] = s->V[pl * K + c];
+      if (it[2 + c] > s->Vn[pl * K + c]) s->Vn[pl * K + c] = it[2 + c];
+    }
+  }
+  *send = s->resp_out;
+  return GOSSIP_OK;
+}
+
+int oracle_ae_response_recv(oracle_sim_t* s, void** recv) {
+  if (!s || !recv || !s->aex) return GOSSIP_EINVAL;
+  *recv = s->resp_in;
+  return GOSSIP_OK;
+}
+
+int oracle_ae_finish(oracle_sim_t* s, uint64_t* partial) {
+  if (!s || !partial || !s->aex) return GOSSIP_EINVAL;
+  const uint32_t K = s->R;
+  for (uint64_t m = 0; m < s->nreq; ++m) {
+    const uint64_t nl = s->req[m * s->rw + 1] - s->lo;
+    for (uint32_t c = 0; c < K; ++c)
+      if (s->resp_in[m * s->pw + c] > s->Vn[nl * K + c]) s->Vn[nl * K + c] = s->resp_in[m * s->pw + c];
+  }
+  for (uint64_t e = 0; e < s->nloc; ++e) {
+    const uint64_t nl = s->loc[2 * e], pl = s->loc[2 * e + 1];
+    for (uint32_t c = 0; c < K; ++c) {
+      const uint32_t a = s->V[nl * K + c], b = s->V[pl * K + c];
+      if (b > s->Vn[nl * K + c]) s->Vn[nl * K + c] = b;
+      if (a > s->Vn[pl * K + c]) s->Vn[pl * K + c] = a;
+    }
+  }
+  memset(partial, 0, oracle_partial_len(s) * 8);
+  for (uint64_t i = 0; i < s->nown; ++i) {
+    const uint64_t n = s->lo + i;
+    int isfull = 1;
+    for (uint32_t c = 0; c < K; ++c) {
+      const uint32_t v = s->Vn[i * K + c];
+      if (v && (s->cfg.flags & GOSSIP_FLAG_HASH)) partial[3] += oracle_mix64((uint64_t)v + ((uint64_t)c * s->N + n) * GOLD64);
+      if (v != s->target[c]) isfull = 0;
+      else if (s->alive_n[n]) partial[4 + c]++;
+    }
+    if (s->alive_n[n]) {
+      partial[1]++;
+      partial[0] += isfull;
+    }
+  }
+  partial[2] = s->aex_msgs;
+  aex_own_stale(s, s->Vn);
+  return GOSSIP_OK;
+}

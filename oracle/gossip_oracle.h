@@ -62,6 +62,16 @@ int oracle_sparse_scan(oracle_sim_t* s, const uint64_t* counts, void** send, uin
 int oracle_sparse_msg_recv(oracle_sim_t* s, uint64_t items, void** recv);
 int oracle_sparse_commit(oracle_sim_t* s, uint64_t items, uint64_t* partial);
 
+uint32_t oracle_ae_item_words(const oracle_sim_t* s, uint32_t which);
+int oracle_ae_local_target(oracle_sim_t* s, uint32_t* out);
+int oracle_ae_set_target(oracle_sim_t* s, const uint32_t* target);
+int oracle_ae_requests(oracle_sim_t* s, void** send, uint64_t* send_counts);
+int oracle_ae_request_recv(oracle_sim_t* s, uint64_t items, void** recv);
+int oracle_ae_serve(oracle_sim_t* s, void** send);
+int oracle_ae_response_recv(oracle_sim_t* s, void** recv);
+int oracle_ae_finish(oracle_sim_t* s, uint64_t* partial);
+int oracle_read_rows(oracle_sim_t* s, uint32_t* out, uint64_t n_values);
+
 int oracle_read_bitset(oracle_sim_t* s, uint64_t node, uint64_t* out, uint32_t nwords);
 int oracle_read_shard(oracle_sim_t* s, uint64_t* out, uint64_t n_words);
 int oracle_read_versions(oracle_sim_t* s, uint64_t node, uint32_t* out, uint32_t ncomp, uint32_t* alive);

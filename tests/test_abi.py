@@ -71,7 +71,9 @@ def test_bad_config_rejected():
     assert b"n_nodes" in lib.gossip_last_error(None)
     cfg = eng_mod.make_config(100, 1, "push", 0, 1)  # fanout 0
     assert lib.gossip_create(C.byref(cfg), C.byref(h)) == -1
-    cfg = eng_mod.make_config(100, 16, "antientropy", 1, 1, shard_count=2)  # one shard only
+    cfg = eng_mod.make_config(100, 16, "antientropy", 1, 1, shard_count=2048)  # sharded: <= 1024 shards
+    assert lib.gossip_create(C.byref(cfg), C.byref(h)) == -6
+    cfg = eng_mod.make_config(100, 65, "antientropy", 1, 1)  # <= 64 components
     assert lib.gossip_create(C.byref(cfg), C.byref(h)) == -6
     cfg = eng_mod.make_config(100, 1, 7, 1, 1)  # unknown mode
     assert lib.gossip_create(C.byref(cfg), C.byref(h)) == -6

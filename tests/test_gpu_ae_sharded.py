@@ -1,0 +1,82 @@
+"""GPU: sharded anti-entropy (SURVEY.md §8(e) Design B, row f4).
+
+G HIP shard engines driven in lockstep through the gossip_ae_* protocol (stale-bit
+all-gather, request / reply all-to-all, max-merge on the owner, the global max vector by a
+MAX reduction) on one device — device copies stand in for RCCL, which the multi-GPU driver
+(gossip_hip.sharded) uses — must equal the single-engine run and the oracle bit for bit:
+per-round alive / full / messages / hash / per-component counts, and every row.
+Reference: (*NodeState).Gossip, main.go:65-89 (each exchange = one request/reply)."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_py as op
+from gossip_hip import Engine
+from gossip_hip.engine import churn_threshold as ct
+from gossip_hip.sharded import lockstep_run
+
+pytestmark = pytest.mark.gpu
+THREADS = min(16, os.cpu_count() or 1)
+
+CASES = [  # N, K, fanout, seed, fail, recover, G
+    (1 << 16, 16, 1, 0x5EED0005, 0.01, 0.1, 4),
+    (50_001, 5, 2, 0x5EED000A, 0.05, 0.3, 3),
+    (4099, 64, 3, 3, 0.02, 0.2, 2),
+    (777, 1, 1, 11, 0.0, 0.0, 2),
+]
+
+
+def _run_single(cls, N, K, k, seed, fail, rec, **kw):
+    e = cls(N, K, "antientropy", k, seed, flags=1, churn_fail=ct(fail), churn_recover=ct(rec), **kw)
+    e.inject_random()
+    a = e.step(5)
+    e.inject(N // 2, K - 1)
+    e.inject(3, 0)
+    b = e.step(400)
+    return a.stats + b.stats, e.read_rows(), e
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"N{c[0]}-K{c[1]}-k{c[2]}-G{c[6]}" for c in CASES])
+def test_ae_lockstep_equals_single_engine_and_oracle(case):
+    N, K, k, seed, fail, rec, G = case
+    want, rows, ref = _run_single(Engine, N, K, k, seed, fail, rec)
+    ref.close()
+    ostats, orows, _ = _run_single(op.OracleEngine, N, K, k, seed, fail, rec, threads=THREADS)
+    assert ostats == want and np.array_equal(orows, rows)
+    engines = [Engine(N, K, "antientropy", k, seed, flags=1, shard_rank=r, shard_count=G, churn_fail=ct(fail),
+                      churn_recover=ct(rec)) for r in range(G)]
+    for e in engines:
+        e.inject_random()
+    a, kinds = lockstep_run(engines, 5)
+    for e in engines:
+        e.inject(N // 2, K - 1)
+        e.inject(3, 0)
+    b, _ = lockstep_run(engines, 400)
+    assert set(kinds) == {2}
+    assert a + b == want
+    for e in engines:
+        assert np.array_equal(e.read_rows(), rows[e.lo:e.hi])
+        e.close()
+
+
+def test_cfg5_64M_G8_lockstep_equals_single_engine():
+    """configs[4] at full size: 2^26 nodes, K = 16, fanout 1, churn 1 % / 10 %, as 8 shards of
+    2^23 rows against the one-GPU engine, to convergence."""
+    N, K, k, seed, fail, rec, G = 1 << 26, 16, 1, 0x5EED0005, 0.01, 0.1, 8
+    ref = Engine(N, K, "antientropy", k, seed, flags=1, churn_fail=ct(fail), churn_recover=ct(rec))
+    ref.inject_random()
+    want = ref.step(400)
+    rows = ref.read_rows()
+    ref.close()
+    assert want.converged
+    engines = [Engine(N, K, "antientropy", k, seed, flags=1, shard_rank=r, shard_count=G, churn_fail=ct(fail),
+                      churn_recover=ct(rec)) for r in range(G)]
+    for e in engines:
+        e.inject_random()
+    got, _ = lockstep_run(engines, 400)
+    assert got == want.stats
+    for e in engines:
+        assert e.hi - e.lo == 1 << 23
+        assert np.array_equal(e.read_rows(), rows[e.lo:e.hi])
+        e.close()

@@ -100,3 +100,66 @@ def test_two_ranks_equal_one(case, plan):
     for rank, lo, hi, stats, shard in got:
         assert stats == want.stats
         assert np.array_equal(shard, full[:, lo:hi])
+
+
+AE_CASES = [  # N, K, fanout, seed, fail, recover
+    (5000, 5, 2, 7, 0.05, 0.3),
+    (4099, 16, 1, 0x5EED0005, 0.01, 0.1),
+    (777, 64, 3, 3, 0.0, 0.0),
+]
+
+
+def _ae_worker(rank, world, port, case, q):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "gossip-protocol_amd"), os.path.join(root, "oracle")]
+    import torch.distributed as dist
+    import oracle_py as op
+    from gossip_hip.engine import churn_threshold as ct
+    from gossip_hip.sharded import sharded_run
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    N, K, k, seed, fail, rec = case
+    e = op.OracleEngine(N, K, "antientropy", k, seed, flags=1, shard_rank=rank, shard_count=world,
+                        churn_fail=ct(fail), churn_recover=ct(rec))
+    e.inject_random()
+    first = sharded_run(e, 4)
+    e.inject(N - 1, 0)  # a client write mid-run: the global max vector is re-derived (MAX all-reduce)
+    e.inject(N // 3, K - 1)
+    rest = sharded_run(e, 300)
+    q.put((rank, e.lo, e.hi, first + rest, e.read_rows()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("case", AE_CASES, ids=[f"N{c[0]}-K{c[1]}-k{c[2]}" for c in AE_CASES])
+def test_antientropy_sharded_equals_one(case, world):
+    """Sharded anti-entropy (Design B: stale-bit all-gather, request/reply
+    all-to-all, max-merge on the owner, ncclMax for the global max vector) over gloo equals the
+    one-shard run bit for bit: per-round stats (alive, full, messages, hash, per-component
+    counts) and every row."""
+    import oracle_py as op
+    from gossip_hip.engine import churn_threshold as ct
+    N, K, k, seed, fail, rec = case
+    ref = op.OracleEngine(N, K, "antientropy", k, seed, flags=1, churn_fail=ct(fail), churn_recover=ct(rec))
+    ref.inject_random()
+    a = ref.step(4)
+    ref.inject(N - 1, 0)
+    ref.inject(N // 3, K - 1)
+    b = ref.step(300)
+    want = a.stats + b.stats
+    rows = ref.read_rows()
+    assert b.converged
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ae_worker, args=(r, world, port, case, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for rank, lo, hi, stats, own in got:
+        assert [dict(s, round=0) for s in stats] == [dict(s, round=0) for s in want]
+        assert np.array_equal(own, rows[lo:hi])
