@@ -1,0 +1,567 @@
+// Package gossipgpu binds the MI355X gossip-round engine (libgossip_hip.so, the C ABI of
+// include/gossip.h, ABI v4) for Go hosts such as 0xSherlokMo/gossip-protocol's main.go.
+//
+// The reference floods each value once to its topology neighbours with blocking SyncRPCs
+// ((*NodeState).Gossip, main.go:65-89), one process per node.  Here one Engine holds every
+// node's state in HBM and runs the dissemination as synchronous rounds:
+//
+//	topology handler  (main.go:132-149)  -> SetTopology / SetTopologyMap
+//	broadcast handler (main.go:102-121)  -> Inject, then Step (replaces State.Gossip, :118)
+//	read handler      (main.go:123-130)  -> Read
+//
+// Errors are *Error values carrying the gossip_status code and gossip_last_error().  One
+// Engine serializes its calls with a mutex (the library is not thread-safe per engine; the
+// reference guards MessageKeeper with sync.RWMutex, main.go:25).  Host slices are read only
+// for the duration of a call and never retained (the cgo pointer rules).
+//
+// Build: make -C gossip-protocol_amd (hipcc, gfx950); then go build ./... here.  This image
+// has no Go toolchain, so the package is checked by tests/test_go_binding.py (every call and
+// config field against include/gossip.h), not compiled.
+package gossipgpu
+
+/*
+#cgo CFLAGS: -I${SRCDIR}/../include
+#cgo LDFLAGS: -L${SRCDIR}/../gossip-protocol_amd/gossip_hip -lgossip_hip -Wl,-rpath,${SRCDIR}/../gossip-protocol_amd/gossip_hip
+#include <stdlib.h>
+#include "gossip.h"
+*/
+import "C"
+
+import (
+	"fmt"
+	"sort"
+	"strconv"
+	"sync"
+	"unsafe"
+)
+
+// ABIVersion is the gossip.h version this binding is written against.
+const ABIVersion = 4
+
+// Mode is a dissemination rule (DESIGN.md §2).
+type Mode uint32
+
+const (
+	Flood       Mode = Mode(C.GOSSIP_MODE_FLOOD) // the reference's own algorithm, main.go:65-89
+	Push        Mode = Mode(C.GOSSIP_MODE_PUSH)
+	Pull        Mode = Mode(C.GOSSIP_MODE_PULL)
+	PushPull    Mode = Mode(C.GOSSIP_MODE_PUSHPULL)
+	AntiEntropy Mode = Mode(C.GOSSIP_MODE_ANTIENTROPY)
+)
+
+// Flags select optional outputs and A/B round paths (results never change).
+type Flags uint32
+
+const (
+	FlagHash         Flags = Flags(C.GOSSIP_FLAG_HASH)
+	FlagTiming       Flags = Flags(C.GOSSIP_FLAG_TIMING)
+	FlagDirect       Flags = Flags(C.GOSSIP_FLAG_DIRECT)
+	FlagDense        Flags = Flags(C.GOSSIP_FLAG_DENSE)
+	FlagShardDirect  Flags = Flags(C.GOSSIP_FLAG_SHARD_DIRECT)
+	FlagAEDirectScan Flags = Flags(C.GOSSIP_FLAG_AE_DIRECT_SCAN)
+)
+
+// Config mirrors gossip_config_t.  Probabilities are thresholds x / 2^32 (Threshold).
+type Config struct {
+	Nodes        uint64 // N, 2 <= N < 2^32
+	Rumors       uint32 // R rumor slots (ANTIENTROPY: K version components)
+	Mode         Mode
+	Fanout       uint32 // Philox peers per node per round (random modes, ANTIENTROPY)
+	Flags        Flags
+	Seed         uint64
+	Device       int32 // HIP device ordinal, -1 = current
+	ShardRank    uint32
+	ShardCount   uint32 // 0 or 1: one engine holds every node
+	ChurnFail    uint32 // ANTIENTROPY churn
+	ChurnRecover uint32
+	EdgeLoss     uint32 // fault model (DESIGN.md §2.8)
+	Partitions   uint32
+	StallRounds  uint32 // the reference's expired-context stall (DESIGN.md §2.9), 0 = off
+}
+
+// Threshold converts a probability into the x / 2^32 threshold of the config fields.
+func Threshold(p float64) uint32 {
+	if p <= 0 {
+		return 0
+	}
+	if p >= 1 {
+		return ^uint32(0)
+	}
+	return uint32(p * 4294967296.0)
+}
+
+// Error is a failed call: the gossip_status code and the engine's message.
+type Error struct {
+	Code int
+	Msg  string
+}
+
+var statusNames = map[int]string{
+	int(C.GOSSIP_EINVAL): "EINVAL", int(C.GOSSIP_EHIP): "EHIP", int(C.GOSSIP_ENOMEM): "ENOMEM",
+	int(C.GOSSIP_ESTATE): "ESTATE", int(C.GOSSIP_ENODEV): "ENODEV", int(C.GOSSIP_ENOTSUP): "ENOTSUP",
+}
+
+func (e *Error) Error() string { return fmt.Sprintf("gossip %s: %s", statusNames[e.Code], e.Msg) }
+
+// RoundStats mirrors gossip_round_stats_t: the state S_{t+1} that round t produced.
+type RoundStats struct {
+	Round      uint32
+	Converged  bool
+	FullNodes  uint64
+	AliveNodes uint64
+	Messages   uint64 // FLOOD: broadcast RPCs sent; ANTIENTROPY: exchanges between alive nodes
+	StateHash  uint64 // FlagHash only
+}
+
+// Engine is one gossip_engine_t.
+type Engine struct {
+	mu  sync.Mutex
+	h   *C.gossip_engine_t
+	cfg Config
+}
+
+func (e *Engine) fail(rc C.int) error {
+	return &Error{Code: int(rc), Msg: C.GoString(C.gossip_last_error(e.h))}
+}
+
+// New creates an engine (NewState / NewMessageKeeper, main.go:28-33, 91-97).  It fails with
+// ENODEV without a gfx950 device: the library has no CPU fallback.
+func New(cfg Config) (*Engine, error) {
+	if v := uint32(C.gossip_abi_version()); v != ABIVersion {
+		return nil, fmt.Errorf("gossipgpu: libgossip_hip ABI %d, binding written for %d", v, ABIVersion)
+	}
+	c := C.gossip_config_t{
+		n_nodes: C.uint64_t(cfg.Nodes), n_rumors: C.uint32_t(cfg.Rumors), mode: C.uint32_t(cfg.Mode),
+		fanout: C.uint32_t(cfg.Fanout), flags: C.uint32_t(cfg.Flags), seed: C.uint64_t(cfg.Seed),
+		device: C.int32_t(cfg.Device), shard_rank: C.uint32_t(cfg.ShardRank), shard_count: C.uint32_t(cfg.ShardCount),
+		churn_fail: C.uint32_t(cfg.ChurnFail), churn_recover: C.uint32_t(cfg.ChurnRecover),
+		edge_loss: C.uint32_t(cfg.EdgeLoss), partitions: C.uint32_t(cfg.Partitions),
+		stall_rounds: C.uint32_t(cfg.StallRounds),
+	}
+	var h *C.gossip_engine_t
+	if rc := C.gossip_create(&c, &h); rc != 0 {
+		return nil, &Error{Code: int(rc), Msg: C.GoString(C.gossip_last_error(nil))}
+	}
+	return &Engine{h: h, cfg: cfg}, nil
+}
+
+// Close releases every device buffer.
+func (e *Engine) Close() {
+	e.mu.Lock()
+	defer e.mu.Unlock()
+	if e.h != nil {
+		C.gossip_destroy(e.h)
+		e.h = nil
+	}
+}
+
+func u32p(s []uint32) *C.uint32_t {
+	if len(s) == 0 {
+		return nil
+	}
+	return (*C.uint32_t)(unsafe.Pointer(&s[0]))
+}
+
+func u64p(s []uint64) *C.uint64_t {
+	if len(s) == 0 {
+		return nil
+	}
+	return (*C.uint64_t)(unsafe.Pointer(&s[0]))
+}
+
+// SetTopology installs Topology[u] = col[rowPtr[u]:rowPtr[u+1]] (the topology handler,
+// main.go:132-149, State.Topology = body.Topology at :142).  Rows are sets.
+func (e *Engine) SetTopology(rowPtr, col []uint32) error {
+	e.mu.Lock()
+	defer e.mu.Unlock()
+	if len(rowPtr) == 0 {
+		return &Error{Code: int(C.GOSSIP_EINVAL), Msg: "empty row_ptr"}
+	}
+	rc := C.gossip_set_topology_csr(e.h, u32p(rowPtr), u32p(col), C.uint64_t(len(rowPtr)-1), C.uint64_t(len(col)))
+	if rc != 0 {
+		return e.fail(rc)
+	}
+	return nil
+}
+
+// NodeIndex maps a Maelstrom node id "n<k>" to k.
+func NodeIndex(id string) (uint32, error) {
+	if len(id) < 2 || id[0] != 'n' {
+		return 0, fmt.Errorf("gossipgpu: node id %q is not n<k>", id)
+	}
+	k, err := strconv.ParseUint(id[1:], 10, 32)
+	return uint32(k), err
+}
+
+// SetTopologyMap installs the body of a Maelstrom topology message (map node id -> neighbour ids).
+func (e *Engine) SetTopologyMap(topo map[string][]string) error {
+	rows := make([][]uint32, e.cfg.Nodes)
+	for src, nbrs := range topo {
+		u, err := NodeIndex(src)
+		if err != nil {
+			return err
+		}
+		if uint64(u) >= e.cfg.Nodes {
+			return fmt.Errorf("gossipgpu: node %s outside the cluster", src)
+		}
+		for _, d := range nbrs {
+			v, err := NodeIndex(d)
+			if err != nil {
+				return err
+			}
+			rows[u] = append(rows[u], v)
+		}
+		sort.Slice(rows[u], func(a, b int) bool { return rows[u][a] < rows[u][b] })
+	}
+	rowPtr := make([]uint32, e.cfg.Nodes+1)
+	var col []uint32
+	for u, r := range rows {
+		col = append(col, r...)
+		rowPtr[u+1] = uint32(len(col))
+	}
+	return e.SetTopology(rowPtr, col)
+}
+
+func (e *Engine) call(rc C.int) error {
+	if rc != 0 {
+		return e.fail(rc)
+	}
+	return nil
+}
+
+// Reset clears every rumor bit (and versions / alive flags) and the round index.
+func (e *Engine) Reset() error {
+	e.mu.Lock()
+	defer e.mu.Unlock()
+	return e.call(C.gossip_reset(e.h))
+}
+
+// Inject is a client broadcast of rumor slot `slot` at `node` (main.go:102-117; a repeat is
+// the dedupe of :113).  ANTIENTROPY: a local write of component `slot`.
+func (e *Engine) Inject(node uint64, slot uint32) error {
+	e.mu.Lock()
+	defer e.mu.Unlock()
+	return e.call(C.gossip_inject(e.h, C.uint64_t(node), C.uint32_t(slot)))
+}
+
+// InjectRandom puts every rumor at its Philox origin (ANTIENTROPY: random initial versions).
+func (e *Engine) InjectRandom() error {
+	e.mu.Lock()
+	defer e.mu.Unlock()
+	return e.call(C.gossip_inject_random(e.h))
+}
+
+// SetFaults changes the fault model between steps (e.g. heal a partition with parts = 0).
+func (e *Engine) SetFaults(edgeLoss, partitions uint32) error {
+	e.mu.Lock()
+	defer e.mu.Unlock()
+	return e.call(C.gossip_set_faults(e.h, C.uint32_t(edgeLoss), C.uint32_t(partitions)))
+}
+
+// SetParam sets a tuning / path-selection knob (gossip_set_param); results never change.
+func (e *Engine) SetParam(name string, value float64) error {
+	e.mu.Lock()
+	defer e.mu.Unlock()
+	cs := C.CString(name)
+	defer C.free(unsafe.Pointer(cs))
+	return e.call(C.gossip_set_param(e.h, cs, C.double(value)))
+}
+
+// SetStream binds a hipStream_t (nil: the null stream).
+func (e *Engine) SetStream(stream unsafe.Pointer) error {
+	e.mu.Lock()
+	defer e.mu.Unlock()
+	return e.call(C.gossip_set_stream(e.h, stream))
+}
+
+// Step runs rounds until every node holds every rumor (FLOOD also: until a round sends
+// nothing) or maxRounds ran; one shard only.  It replaces State.Gossip (main.go:118).
+// infected[t][r] = nodes holding rumor r after round t.
+func (e *Engine) Step(maxRounds uint32) ([]RoundStats, [][]uint64, error) {
+	e.mu.Lock()
+	defer e.mu.Unlock()
+	if maxRounds == 0 {
+		return nil, nil, nil
+	}
+	st := make([]C.gossip_round_stats_t, maxRounds)
+	R := uint64(e.cfg.Rumors)
+	inf := make([]uint64, uint64(maxRounds)*R)
+	var done C.uint32_t
+	if rc := C.gossip_step(e.h, C.uint32_t(maxRounds), &st[0], u64p(inf), &done); rc != 0 {
+		return nil, nil, e.fail(rc)
+	}
+	n := int(done)
+	out := make([]RoundStats, n)
+	rows := make([][]uint64, n)
+	for i := 0; i < n; i++ {
+		out[i] = RoundStats{Round: uint32(st[i].round), Converged: st[i].converged != 0,
+			FullNodes: uint64(st[i].full_nodes), AliveNodes: uint64(st[i].alive_nodes),
+			Messages: uint64(st[i].messages), StateHash: uint64(st[i].state_hash)}
+		rows[i] = inf[uint64(i)*R : uint64(i+1)*R]
+	}
+	return out, rows, nil
+}
+
+// ReadBitset is the word form of the read handler (main.go:123-130).
+func (e *Engine) ReadBitset(node uint64) ([]uint64, error) {
+	e.mu.Lock()
+	defer e.mu.Unlock()
+	w := (e.cfg.Rumors + 63) / 64
+	out := make([]uint64, w)
+	if rc := C.gossip_read_bitset(e.h, C.uint64_t(node), u64p(out), C.uint32_t(w)); rc != 0 {
+		return nil, e.fail(rc)
+	}
+	return out, nil
+}
+
+// Read returns the rumor slots node holds (the read handler, main.go:123-130).
+func (e *Engine) Read(node uint64) ([]uint32, error) {
+	words, err := e.ReadBitset(node)
+	if err != nil {
+		return nil, err
+	}
+	var slots []uint32
+	for r := uint32(0); r < e.cfg.Rumors; r++ {
+		if (words[r/64]>>(r%64))&1 == 1 {
+			slots = append(slots, r)
+		}
+	}
+	return slots, nil
+}
+
+// ReadShard returns the owned shard's words, out[w*n + i] for owned node lo + i.
+func (e *Engine) ReadShard() ([]uint64, error) {
+	lo, hi := e.ShardRange()
+	e.mu.Lock()
+	defer e.mu.Unlock()
+	out := make([]uint64, uint64((e.cfg.Rumors+63)/64)*(hi-lo))
+	if rc := C.gossip_read_shard(e.h, u64p(out), C.uint64_t(len(out))); rc != 0 {
+		return nil, e.fail(rc)
+	}
+	return out, nil
+}
+
+// ReadVersions returns one node's K versions and its alive flag (ANTIENTROPY).
+func (e *Engine) ReadVersions(node uint64) ([]uint32, bool, error) {
+	e.mu.Lock()
+	defer e.mu.Unlock()
+	out := make([]uint32, e.cfg.Rumors)
+	var alive C.uint32_t
+	if rc := C.gossip_read_versions(e.h, C.uint64_t(node), u32p(out), C.uint32_t(len(out)), &alive); rc != 0 {
+		return nil, false, e.fail(rc)
+	}
+	return out, alive != 0, nil
+}
+
+// ReadRows returns every owned row (ANTIENTROPY), out[i*K + c].
+func (e *Engine) ReadRows() ([]uint32, error) {
+	lo, hi := e.ShardRange()
+	e.mu.Lock()
+	defer e.mu.Unlock()
+	out := make([]uint32, (hi-lo)*uint64(e.cfg.Rumors))
+	if rc := C.gossip_read_rows(e.h, u32p(out), C.uint64_t(len(out))); rc != 0 {
+		return nil, e.fail(rc)
+	}
+	return out, nil
+}
+
+// StateHash is the order-independent state hash (DESIGN.md §2.5).
+func (e *Engine) StateHash() (uint64, error) {
+	e.mu.Lock()
+	defer e.mu.Unlock()
+	var h C.uint64_t
+	if rc := C.gossip_state_hash(e.h, &h); rc != 0 {
+		return 0, e.fail(rc)
+	}
+	return uint64(h), nil
+}
+
+// ShardRange is the owned node range [lo, hi).
+func (e *Engine) ShardRange() (lo, hi uint64) {
+	var l, h C.uint64_t
+	C.gossip_shard_range(e.h, &l, &h)
+	return uint64(l), uint64(h)
+}
+
+// RoundIndex is t, the rounds run since the last reset.
+func (e *Engine) RoundIndex() uint32 { return uint32(C.gossip_round_index(e.h)) }
+
+// KernelTime returns a FlagTiming timer's accumulated device ms and launch count.
+func (e *Engine) KernelTime(which uint32) (float64, uint64, error) {
+	var ms C.double
+	var n C.uint64_t
+	if rc := C.gossip_kernel_time(e.h, C.uint32_t(which), &ms, &n); rc != 0 {
+		return 0, 0, e.fail(rc)
+	}
+	return float64(ms), uint64(n), nil
+}
+
+// ResetTiming clears the FlagTiming timers.
+func (e *Engine) ResetTiming() error { return e.call(C.gossip_reset_timing(e.h)) }
+
+// PhiloxDevice runs Philox4x32-10 on the device for known-answer tests (ctr: 4 words per counter).
+func (e *Engine) PhiloxDevice(ctr []uint32, key [2]uint32) ([]uint32, error) {
+	e.mu.Lock()
+	defer e.mu.Unlock()
+	out := make([]uint32, len(ctr))
+	k := []uint32{key[0], key[1]}
+	if rc := C.gossip_philox_device(e.h, u32p(ctr), u32p(k), u32p(out), C.uint32_t(len(ctr)/4)); rc != 0 {
+		return nil, e.fail(rc)
+	}
+	return out, nil
+}
+
+// Peer is p_j(node, round) exactly as the kernels draw it.
+func Peer(seed, nodes uint64, node, round, j uint32) uint32 {
+	return uint32(C.gossip_peer(C.uint64_t(seed), C.uint64_t(nodes), C.uint32_t(node), C.uint32_t(round), C.uint32_t(j)))
+}
+
+// --- sharded rounds (G > 1): the host runs the collectives on its own RCCL communicator -----
+// Device pointers are returned as uintptr; see include/gossip.h and DESIGN.md §5 for the
+// order of calls (gossip_hip/sharded.py is the same sequence in Python).
+
+// PartialLen is the length of the stats partial vector that is all-reduced (SUM) each round.
+func (e *Engine) PartialLen() uint64 { return uint64(C.gossip_partial_len(e.h)) }
+
+// ShardedPlan: -1 / -2 need totals / the global max vector first; 0 dense, 1 sparse, 2 anti-entropy.
+func (e *Engine) ShardedPlan(total []uint64) (int32, error) {
+	var kind C.int32_t
+	if rc := C.gossip_sharded_plan(e.h, u64p(total), &kind); rc != 0 {
+		return 0, e.fail(rc)
+	}
+	return int32(kind), nil
+}
+
+// LocalTotals are the owned nodes' totals (to all-reduce before planning).
+func (e *Engine) LocalTotals() ([]uint64, error) {
+	out := make([]uint64, e.PartialLen())
+	return out, e.call(C.gossip_local_totals(e.h, u64p(out)))
+}
+
+// ExchangeBuffers returns the send slice and the gathered image of an all-gather (in place).
+func (e *Engine) ExchangeBuffers() (send, recv uintptr, bytes uint64, err error) {
+	var s, r unsafe.Pointer
+	var n C.uint64_t
+	if rc := C.gossip_exchange_buffers(e.h, &s, &r, &n); rc != 0 {
+		return 0, 0, 0, e.fail(rc)
+	}
+	return uintptr(s), uintptr(r), uint64(n), nil
+}
+
+// DensePrepare enqueues the own-slice part of a dense round while the all-gather runs.
+func (e *Engine) DensePrepare() error { return e.call(C.gossip_dense_prepare(e.h)) }
+
+// RoundCompute computes a dense round's S_{t+1} and returns its partial stats.
+func (e *Engine) RoundCompute() ([]uint64, error) {
+	out := make([]uint64, e.PartialLen())
+	return out, e.call(C.gossip_round_compute(e.h, u64p(out)))
+}
+
+// RoundCommit takes the all-reduced totals and ends the round.
+func (e *Engine) RoundCommit(total []uint64) (RoundStats, error) {
+	var st C.gossip_round_stats_t
+	if rc := C.gossip_round_commit(e.h, u64p(total), &st); rc != 0 {
+		return RoundStats{}, e.fail(rc)
+	}
+	return RoundStats{Round: uint32(st.round), Converged: st.converged != 0, FullNodes: uint64(st.full_nodes),
+		AliveNodes: uint64(st.alive_nodes), Messages: uint64(st.messages), StateHash: uint64(st.state_hash)}, nil
+}
+
+// SparseRare: the own rare nodes (16-B items) of a sparse round.
+func (e *Engine) SparseRare() (send uintptr, count uint64, err error) {
+	var s unsafe.Pointer
+	var n C.uint64_t
+	if rc := C.gossip_sparse_rare(e.h, &s, &n); rc != 0 {
+		return 0, 0, e.fail(rc)
+	}
+	return uintptr(s), uint64(n), nil
+}
+
+// SparseRareRecv: room for G * stride rare items.
+func (e *Engine) SparseRareRecv(stride uint64) (uintptr, error) {
+	var r unsafe.Pointer
+	if rc := C.gossip_sparse_rare_recv(e.h, C.uint64_t(stride), &r); rc != 0 {
+		return 0, e.fail(rc)
+	}
+	return uintptr(r), nil
+}
+
+// SparseScan: the pushes for other shards, grouped by owner.
+func (e *Engine) SparseScan(counts []uint64) (send uintptr, sendCounts []uint64, err error) {
+	var s unsafe.Pointer
+	sendCounts = make([]uint64, len(counts))
+	if rc := C.gossip_sparse_scan(e.h, u64p(counts), &s, u64p(sendCounts)); rc != 0 {
+		return 0, nil, e.fail(rc)
+	}
+	return uintptr(s), sendCounts, nil
+}
+
+// SparseMsgRecv: room for the incoming push items.
+func (e *Engine) SparseMsgRecv(items uint64) (uintptr, error) {
+	var r unsafe.Pointer
+	if rc := C.gossip_sparse_msg_recv(e.h, C.uint64_t(items), &r); rc != 0 {
+		return 0, e.fail(rc)
+	}
+	return uintptr(r), nil
+}
+
+// SparseCommit ends a sparse round with the received pushes.
+func (e *Engine) SparseCommit(items uint64) ([]uint64, error) {
+	out := make([]uint64, e.PartialLen())
+	return out, e.call(C.gossip_sparse_commit(e.h, C.uint64_t(items), u64p(out)))
+}
+
+// AEItemWords: uint32 words of a request (0) or reply (1) item of sharded ANTIENTROPY.
+func (e *Engine) AEItemWords(which uint32) uint32 { return uint32(C.gossip_ae_item_words(e.h, C.uint32_t(which))) }
+
+// AELocalTarget: the max over the owned rows (all-reduce it with MAX, then AESetTarget).
+func (e *Engine) AELocalTarget() ([]uint32, error) {
+	out := make([]uint32, e.cfg.Rumors)
+	return out, e.call(C.gossip_ae_local_target(e.h, u32p(out)))
+}
+
+// AESetTarget installs the global max vector.
+func (e *Engine) AESetTarget(target []uint32) error { return e.call(C.gossip_ae_set_target(e.h, u32p(target))) }
+
+// AERequests: this round's request items grouped by owner.
+func (e *Engine) AERequests() (send uintptr, counts []uint64, err error) {
+	var s unsafe.Pointer
+	counts = make([]uint64, e.cfg.ShardCount)
+	if rc := C.gossip_ae_requests(e.h, &s, u64p(counts)); rc != 0 {
+		return 0, nil, e.fail(rc)
+	}
+	return uintptr(s), counts, nil
+}
+
+// AERequestRecv: room for the incoming requests.
+func (e *Engine) AERequestRecv(items uint64) (uintptr, error) {
+	var r unsafe.Pointer
+	if rc := C.gossip_ae_request_recv(e.h, C.uint64_t(items), &r); rc != 0 {
+		return 0, e.fail(rc)
+	}
+	return uintptr(r), nil
+}
+
+// AEServe merges the received requests and returns the replies (received order).
+func (e *Engine) AEServe() (uintptr, error) {
+	var s unsafe.Pointer
+	if rc := C.gossip_ae_serve(e.h, &s); rc != 0 {
+		return 0, e.fail(rc)
+	}
+	return uintptr(s), nil
+}
+
+// AEResponseRecv: room for the replies to the own requests (request order).
+func (e *Engine) AEResponseRecv() (uintptr, error) {
+	var r unsafe.Pointer
+	if rc := C.gossip_ae_response_recv(e.h, &r); rc != 0 {
+		return 0, e.fail(rc)
+	}
+	return uintptr(r), nil
+}
+
+// AEFinish merges the replies and returns the round's partial stats.
+func (e *Engine) AEFinish() ([]uint64, error) {
+	out := make([]uint64, e.PartialLen())
+	return out, e.call(C.gossip_ae_finish(e.h, u64p(out)))
+}

@@ -9,16 +9,24 @@
 //   PeerFromWord    peer_from_word         gossip_oracle.c:74  (replaces Topology[node.ID()], main.go:72)
 //   Origin          oracle_origin          gossip_oracle.c:104 (Philox stream tag 2)
 //   Mix64           oracle_mix64           gossip_oracle.c:112 (state hash term)
-//   Sim.Round       oracle_round_compute   random modes: push, pull, push-pull over S_t (main.go:65-89 as rounds)
+//   Sim.Round       oracle_round_compute   random modes: push, pull, push-pull over S_t (main.go:65-89 as rounds),
+//                                          with the fault model (EdgeLost: edge_lost) and the stall mode (stall_update)
+//   FloodSim.Round  oracle_round_compute   FLOOD, the reference's own algorithm (main.go:65-89): every node forwards
+//                                          the values it learned last round to Topology[self] (:72) except their
+//                                          first sender (:73-75); dedupe :113; messages = RPCs sent
+//   FloodSim (faults) flood_faults_round   per-edge retries, dropped after StallRounds attempts (main.go:77-87)
 //   AESim.Round     ae_round               gossip_oracle.c:355 (version-vector max-merge, Philox churn tag 1)
-// FLOOD (the topology flood of main.go:65-89 with its sender skip) and the
-// fault model are pinned by the C oracle and the Python property tests only.
 //
 // Status in this image: no Go toolchain exists here or on the GPU box, so this
 // package has not been compiled or run ("go test" in this directory checks it
 // against tests/golden/golden.json, the fixtures the C oracle and the HIP
 // engine are tested against).
 package gossipref
+
+import (
+	"math/bits"
+	"sort"
+)
 
 // Philox4x32_10 is the counter-based generator every random choice is drawn from.
 func Philox4x32_10(ctr [4]uint32, key [2]uint32) [4]uint32 {
@@ -74,6 +82,24 @@ func Mix64(z uint64) uint64 {
 	return z
 }
 
+// EdgeLost: the edge n -> p (slot j of initiator n) of round t is lost, both
+// directions, when a partition (nodes split into parts contiguous blocks) separates
+// its ends or its loss draw Philox({n, t, 4, j/4})[j%4] is below loss (DESIGN.md §2.8).
+func EdgeLost(seed, N uint64, loss, parts, n, p, t, j uint32) bool {
+	if parts > 1 && (uint64(n)*uint64(parts))/N != (uint64(p)*uint64(parts))/N {
+		return true
+	}
+	if loss != 0 {
+		x := Philox4x32_10([4]uint32{n, t, 4, j >> 2}, Key(seed))
+		if x[j&3] < loss {
+			return true
+		}
+	}
+	return false
+}
+
+func popcount(x uint64) uint64 { return uint64(bits.OnesCount64(x)) }
+
 // RoundStats are the per-round observables the engine reports (gossip_round_stats_t).
 type RoundStats struct {
 	Round     uint32
@@ -103,6 +129,19 @@ type Sim struct {
 	T    uint32
 	S    [][]uint64
 	full []uint64 // per word: the bits of the rumors that exist
+	// fault model (SetFaults): edge loss threshold, partitions, stall deadline (DESIGN.md §2.8-2.9)
+	Loss, Parts, StallRounds uint32
+	streak                   []uint8 // lost-exchange streak per node (stall mode)
+}
+
+// SetFaults sets the fault model of the rounds that follow; stallRounds > 0 turns on the
+// stall mode (a node whose exchanges were lost in stallRounds rounds in a row initiates
+// none until the simulation is rebuilt: the reference's expired 2 s context, main.go:77-87).
+func (s *Sim) SetFaults(loss, parts, stallRounds uint32) {
+	s.Loss, s.Parts, s.StallRounds = loss, parts, stallRounds
+	if stallRounds > 0 && s.streak == nil {
+		s.streak = make([]uint8, s.N)
+	}
 }
 
 // NewSim is gossip_create for one shard on the CPU.
@@ -144,11 +183,20 @@ func (s *Sim) Round() RoundStats {
 	push := s.Mode == Push || s.Mode == PushPull
 	for n := uint64(0); n < s.N; n++ {
 		var x [4]uint32
+		stalled := s.StallRounds > 0 && uint32(s.streak[n]) >= s.StallRounds
+		lostAny := false
 		for j := uint32(0); j < s.K; j++ {
 			if j&3 == 0 {
 				x = Philox4x32_10([4]uint32{uint32(n), s.T, 0, j >> 2}, key)
 			}
 			p := uint64(PeerFromWord(x[j&3], s.N, uint32(n)))
+			if EdgeLost(s.Seed, s.N, s.Loss, s.Parts, uint32(n), uint32(p), s.T, j) {
+				lostAny = true
+				continue
+			}
+			if stalled { // a stalled node initiates nothing; it still answers and receives
+				continue
+			}
 			for w := uint32(0); w < s.W; w++ {
 				if pull {
 					next[w][n] |= s.S[w][p]
@@ -156,6 +204,13 @@ func (s *Sim) Round() RoundStats {
 				if push {
 					next[w][p] |= s.S[w][n]
 				}
+			}
+		}
+		if s.StallRounds > 0 && !stalled { // only n's own streak depends on n's own edges
+			if lostAny {
+				s.streak[n]++
+			} else {
+				s.streak[n] = 0
 			}
 		}
 	}
@@ -194,6 +249,265 @@ func (s *Sim) Run(maxRounds int) []RoundStats {
 		out = append(out, st)
 		if st.Converged {
 			break
+		}
+	}
+	return out
+}
+
+// FloodSim is FLOOD over a harness topology (the reference's own algorithm, main.go:65-89).
+type FloodSim struct {
+	N        uint64
+	R, W     uint32
+	T        uint32
+	Seed     uint64
+	Loss     uint32 // faults (NewFloodSim with any of them on: per-edge retries, DESIGN.md §2.9)
+	Parts    uint32
+	Stall    uint32
+	adj      [][]uint32   // Topology[u] as a sorted set
+	row0     []uint64     // CSR start of u's out-edges
+	inSrc    [][]uint32   // in-neighbours of v, ascending
+	inEdge   [][]uint64   // their out-edge ids
+	S, Sprev [][]uint64   // [W][N]
+	skip     [][]uint64   // fault-free: values whose first sender is in Adj(v)
+	faults   bool
+	pend     [][][]uint64 // [slot][W][E] values pending on an edge, by attempts made
+	skipE    [][]uint64   // [W][E] values whose first sender at the edge's source is its target
+	full     []uint64
+}
+
+// NewFloodSim builds the topology (rows as sets, main.go:132-149 / DESIGN.md §2.4).
+func NewFloodSim(N uint64, R uint32, adj [][]uint32, seed uint64, loss, parts, stall uint32) *FloodSim {
+	W := (R + 63) / 64
+	f := &FloodSim{N: N, R: R, W: W, Seed: seed, Loss: loss, Parts: parts, Stall: stall}
+	f.faults = loss != 0 || parts > 1 || stall != 0
+	f.adj = make([][]uint32, N)
+	f.row0 = make([]uint64, N+1)
+	f.inSrc = make([][]uint32, N)
+	f.inEdge = make([][]uint64, N)
+	var E uint64
+	for u := uint64(0); u < N; u++ {
+		row := append([]uint32(nil), adj[u]...)
+		sort.Slice(row, func(a, b int) bool { return row[a] < row[b] })
+		var set []uint32
+		for i, v := range row {
+			if i == 0 || v != row[i-1] {
+				set = append(set, v)
+			}
+		}
+		f.adj[u] = set
+		f.row0[u] = E
+		E += uint64(len(set))
+	}
+	f.row0[N] = E
+	for u := uint64(0); u < N; u++ { // ascending u: every in-list sorted
+		for i, v := range f.adj[u] {
+			f.inSrc[v] = append(f.inSrc[v], uint32(u))
+			f.inEdge[v] = append(f.inEdge[v], f.row0[u]+uint64(i))
+		}
+	}
+	f.S, f.Sprev, f.skip = make([][]uint64, W), make([][]uint64, W), make([][]uint64, W)
+	f.full = make([]uint64, W)
+	for w := uint32(0); w < W; w++ {
+		f.S[w], f.Sprev[w], f.skip[w] = make([]uint64, N), make([]uint64, N), make([]uint64, N)
+		if b := R - 64*w; b >= 64 {
+			f.full[w] = ^uint64(0)
+		} else {
+			f.full[w] = (uint64(1) << b) - 1
+		}
+	}
+	slots := uint32(1)
+	if stall > 1 {
+		slots = stall - 1
+	}
+	f.pend = make([][][]uint64, slots)
+	for a := range f.pend {
+		f.pend[a] = make([][]uint64, W)
+		for w := range f.pend[a] {
+			f.pend[a][w] = make([]uint64, E)
+		}
+	}
+	f.skipE = make([][]uint64, W)
+	for w := range f.skipE {
+		f.skipE[w] = make([]uint64, E)
+	}
+	return f
+}
+
+// Inject is a client broadcast (main.go:102-117).
+func (f *FloodSim) Inject(n uint64, r uint32) { f.S[r/64][n] |= uint64(1) << (r % 64) }
+
+func contains(row []uint32, x uint32) (int, bool) {
+	i := sort.Search(len(row), func(i int) bool { return row[i] >= x })
+	return i, i < len(row) && row[i] == x
+}
+
+func (f *FloodSim) lost(u, w uint32, j uint64) bool {
+	return EdgeLost(f.Seed, f.N, f.Loss, f.Parts, u, w, f.T, uint32(j))
+}
+
+// attempt: what edge e of u carries in this round (new values minus the skip, plus the pending ones)
+func (f *FloodSim) attempt(w uint32, u uint64, e uint64) (att, fresh uint64) {
+	fresh = f.S[w][u] &^ f.Sprev[w][u] &^ f.skipE[w][e]
+	att = fresh
+	for a := range f.pend {
+		att |= f.pend[a][w][e]
+	}
+	return att, fresh
+}
+
+// Round: one synchronous FLOOD round.
+func (f *FloodSim) Round() RoundStats {
+	N := f.N
+	next := make([][]uint64, f.W)
+	for w := range next {
+		next[w] = append([]uint64(nil), f.S[w]...)
+	}
+	var msgs uint64
+	if !f.faults {
+		for v := uint64(0); v < N; v++ {
+			deg := uint64(len(f.adj[v]))
+			for w := uint32(0); w < f.W; w++ {
+				fv := f.S[w][v] &^ f.Sprev[w][v]
+				msgs += popcount(fv)*deg - popcount(fv&f.skip[w][v])
+				acc := f.S[w][v]
+				for _, u := range f.inSrc[v] {
+					acc |= f.S[w][u] &^ f.Sprev[w][u]
+				}
+				nw := acc &^ f.S[w][v]
+				var seen, sk uint64
+				for _, u := range f.inSrc[v] {
+					if seen == nw {
+						break
+					}
+					c := (f.S[w][u] &^ f.Sprev[w][u]) & nw &^ seen
+					if _, in := contains(f.adj[v], u); c != 0 && in {
+						sk |= c // sender skip, main.go:73
+					}
+					seen |= c
+				}
+				next[w][v] = acc
+				f.skip[w][v] = sk
+			}
+		}
+	} else {
+		E := f.row0[N]
+		slots := len(f.pend)
+		pendN := make([][][]uint64, slots)
+		for a := range pendN {
+			pendN[a] = make([][]uint64, f.W)
+			for w := range pendN[a] {
+				pendN[a][w] = make([]uint64, E)
+			}
+		}
+		skipN := make([][]uint64, f.W)
+		for w := range skipN {
+			skipN[w] = make([]uint64, E)
+		}
+		for u := uint64(0); u < N; u++ { // sender side: attempts, messages, what stays pending
+			for i, v := range f.adj[u] {
+				e := f.row0[u] + uint64(i)
+				lost := f.lost(uint32(u), v, uint64(i))
+				for w := uint32(0); w < f.W; w++ {
+					att, fresh := f.attempt(w, u, e)
+					msgs += popcount(att)
+					if !lost {
+						continue
+					}
+					if f.Stall == 0 {
+						pendN[0][w][e] = att
+					} else {
+						if f.Stall >= 2 {
+							pendN[0][w][e] = fresh
+						}
+						for a := 0; a+1 < slots; a++ {
+							pendN[a+1][w][e] = f.pend[a][w][e]
+						}
+					}
+				}
+			}
+		}
+		for v := uint64(0); v < N; v++ { // receiver side: delivered attempts, ascending sender id
+			for w := uint32(0); w < f.W; w++ {
+				acc := f.S[w][v]
+				for q, u := range f.inSrc[v] {
+					e := f.inEdge[v][q]
+					if f.lost(u, uint32(v), e-f.row0[u]) {
+						continue
+					}
+					att, _ := f.attempt(w, uint64(u), e)
+					acc |= att
+				}
+				nw := acc &^ f.S[w][v]
+				var seen uint64
+				for q, u := range f.inSrc[v] {
+					if seen == nw {
+						break
+					}
+					e := f.inEdge[v][q]
+					if f.lost(u, uint32(v), e-f.row0[u]) {
+						continue
+					}
+					att, _ := f.attempt(w, uint64(u), e)
+					c := att & nw &^ seen
+					if c == 0 {
+						continue
+					}
+					seen |= c
+					if i, in := contains(f.adj[v], u); in { // v will not send these back to u
+						skipN[w][f.row0[v]+uint64(i)] |= c
+					}
+				}
+				next[w][v] = acc
+			}
+		}
+		f.pend, f.skipE = pendN, skipN
+	}
+	f.Sprev, f.S = f.S, next
+	st := RoundStats{Round: f.T, Alive: N, Messages: msgs, Infected: make([]uint64, f.R)}
+	for n := uint64(0); n < N; n++ {
+		isFull := true
+		for w := uint32(0); w < f.W; w++ {
+			x := f.S[w][n]
+			if x&f.full[w] != f.full[w] {
+				isFull = false
+			}
+			if x != 0 {
+				st.Hash += Mix64(x + (uint64(w)*N+n)*gold64)
+			}
+			for b := uint32(0); b < 64 && 64*w+b < f.R; b++ {
+				if (x>>b)&1 == 1 {
+					st.Infected[64*w+b]++
+				}
+			}
+		}
+		if isFull {
+			st.Full++
+		}
+	}
+	st.Converged = st.Full == st.Alive
+	f.T++
+	return st
+}
+
+// Run rounds until converged, or a round that sends nothing (quiescence), or maxRounds.
+func (f *FloodSim) Run(maxRounds int) []RoundStats {
+	var out []RoundStats
+	for i := 0; i < maxRounds; i++ {
+		st := f.Round()
+		out = append(out, st)
+		if st.Converged || st.Messages == 0 {
+			break
+		}
+	}
+	return out
+}
+
+// Read is the read handler (main.go:123-130): the slots node n holds.
+func (f *FloodSim) Read(n uint64) []uint32 {
+	var out []uint32
+	for r := uint32(0); r < f.R; r++ {
+		if (f.S[r/64][n]>>(r%64))&1 == 1 {
+			out = append(out, r)
 		}
 	}
 	return out

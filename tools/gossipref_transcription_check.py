@@ -1,4 +1,5 @@
-"""Line-by-line Python transcription of oracle/gossipref (Go) Sim.Round / AESim.Round, run on
+"""Line-by-line Python transcription of oracle/gossipref (Go) Sim.Round (with EdgeLost and the stall
+mode), FloodSim.Round (fault-free and per-edge retry paths) and AESim.Round, run on
 tests/golden/golden.json.  Neither this image nor the GPU box has a Go toolchain, so this is how
 the Go restatement's semantics were checked here (the Go test itself: cd oracle/gossipref && go test).
 Slow pure-Python loops (about a minute); not part of the pytest suites."""
@@ -38,8 +39,18 @@ def mix(z):  # gossipref.Mix64
     return z ^ (z >> 31)
 
 
-def random_case(c):  # gossipref.Sim
+def edge_lost(seed, N, loss, parts, n, p, t, j):  # gossipref.EdgeLost
+    if parts > 1 and (n * parts) // N != (p * parts) // N:
+        return True
+    if loss != 0 and philox([n, t, 4, j >> 2], key(seed))[j & 3] < loss:
+        return True
+    return False
+
+
+def random_case(c, max_rounds=256):  # gossipref.Sim (+ SetFaults)
     N, R, k, seed = c["N"], c["R"], c["k"], c["seed"]
+    loss, parts, stall = c.get("edge_loss", 0), c.get("partitions", 0), c.get("stall_rounds", 0)
+    streak = [0] * N
     W = (R + 63) // 64
     mode = {"push": 1, "pull": 2, "pushpull": 3}[c["mode"]]
     full = [(M64 if R - 64 * w >= 64 else (1 << (R - 64 * w)) - 1) for w in range(W)]
@@ -49,19 +60,28 @@ def random_case(c):  # gossipref.Sim
     for n, r in inj:
         S[r // 64][n] |= 1 << (r % 64)
     out = []
-    for t in range(256):
+    for t in range(max_rounds):
         nx = [row[:] for row in S]
         for n in range(N):
             x = None
+            stalled = stall > 0 and streak[n] >= stall
+            lost_any = False
             for j in range(k):
                 if j & 3 == 0:
                     x = philox([n, t, 0, j >> 2], key(seed))
                 p = pfw(x[j & 3], N, n)
+                if edge_lost(seed, N, loss, parts, n, p, t, j):
+                    lost_any = True
+                    continue
+                if stalled:
+                    continue
                 for w in range(W):
                     if mode & 2:
                         nx[w][n] |= S[w][p]
                     if mode & 1:
                         nx[w][p] |= S[w][n]
+            if stall > 0 and not stalled:
+                streak[n] = streak[n] + 1 if lost_any else 0
         S = nx
         h = fc = 0
         inf = [0] * R
@@ -79,6 +99,135 @@ def random_case(c):  # gossipref.Sim
         out.append(dict(round=t, full=fc, converged=int(fc == N), messages=0, hash=h, infected=inf))
         if fc == N:
             break
+    return out
+
+
+def pc(x):
+    return bin(x).count("1")
+
+
+def flood_case(c):  # gossipref.FloodSim
+    N, R, A = c["N"], c["R"], c["adj"]
+    loss, parts, stall = c.get("edge_loss", 0), c.get("partitions", 0), c.get("stall_rounds", 0)
+    max_rounds = c.get("max_rounds", 256)
+    seed = 0
+    W = (R + 63) // 64
+    faults = loss != 0 or parts > 1 or stall != 0
+    adj = [sorted(set(r)) for r in A]
+    row0, E = [], 0
+    for u in range(N):
+        row0.append(E)
+        E += len(adj[u])
+    row0.append(E)
+    in_src, in_edge = [[] for _ in range(N)], [[] for _ in range(N)]
+    for u in range(N):
+        for i, v in enumerate(adj[u]):
+            in_src[v].append(u)
+            in_edge[v].append(row0[u] + i)
+    S = [[0] * N for _ in range(W)]
+    Sp = [[0] * N for _ in range(W)]
+    skip = [[0] * N for _ in range(W)]
+    full = [(M64 if R - 64 * w >= 64 else (1 << (R - 64 * w)) - 1) for w in range(W)]
+    slots = stall - 1 if stall > 1 else 1
+    pend = [[[0] * E for _ in range(W)] for _ in range(slots)]
+    skipE = [[0] * E for _ in range(W)]
+    for n, r in c["inject"]:
+        S[r // 64][n] |= 1 << (r % 64)
+
+    def attempt(w, u, e):
+        fresh = S[w][u] & ~Sp[w][u] & ~skipE[w][e] & M64
+        att = fresh
+        for a in range(slots):
+            att |= pend[a][w][e]
+        return att, fresh
+
+    out = []
+    for t in range(max_rounds):
+        nx = [row[:] for row in S]
+        msgs = 0
+        if not faults:
+            for v in range(N):
+                deg = len(adj[v])
+                for w in range(W):
+                    fv = S[w][v] & ~Sp[w][v] & M64
+                    msgs += pc(fv) * deg - pc(fv & skip[w][v])
+                    acc = S[w][v]
+                    for u in in_src[v]:
+                        acc |= S[w][u] & ~Sp[w][u] & M64
+                    nw = acc & ~S[w][v] & M64
+                    seen = sk = 0
+                    for u in in_src[v]:
+                        if seen == nw:
+                            break
+                        cc = (S[w][u] & ~Sp[w][u]) & nw & ~seen & M64
+                        if cc and u in adj[v]:
+                            sk |= cc
+                        seen |= cc
+                    nx[w][v] = acc
+                    skip[w][v] = sk
+        else:
+            pn = [[[0] * E for _ in range(W)] for _ in range(slots)]
+            sn = [[0] * E for _ in range(W)]
+            for u in range(N):
+                for i, v in enumerate(adj[u]):
+                    e = row0[u] + i
+                    lost = edge_lost(seed, N, loss, parts, u, v, t, i)
+                    for w in range(W):
+                        att, fresh = attempt(w, u, e)
+                        msgs += pc(att)
+                        if not lost:
+                            continue
+                        if stall == 0:
+                            pn[0][w][e] = att
+                        else:
+                            if stall >= 2:
+                                pn[0][w][e] = fresh
+                            for a in range(slots - 1):
+                                pn[a + 1][w][e] = pend[a][w][e]
+            for v in range(N):
+                for w in range(W):
+                    acc = S[w][v]
+                    for q, u in enumerate(in_src[v]):
+                        e = in_edge[v][q]
+                        if edge_lost(seed, N, loss, parts, u, v, t, e - row0[u]):
+                            continue
+                        acc |= attempt(w, u, e)[0]
+                    nw = acc & ~S[w][v] & M64
+                    seen = 0
+                    for q, u in enumerate(in_src[v]):
+                        if seen == nw:
+                            break
+                        e = in_edge[v][q]
+                        if edge_lost(seed, N, loss, parts, u, v, t, e - row0[u]):
+                            continue
+                        cc = attempt(w, u, e)[0] & nw & ~seen & M64
+                        if not cc:
+                            continue
+                        seen |= cc
+                        if u in adj[v]:
+                            sn[w][row0[v] + adj[v].index(u)] |= cc
+                    nx[w][v] = acc
+            pend, skipE = pn, sn
+        Sp, S = S, nx
+        h = fc = 0
+        inf = [0] * R
+        for n in range(N):
+            f = True
+            for w in range(W):
+                x = S[w][n]
+                f = f and x & full[w] == full[w]
+                if x:
+                    h = (h + mix(x + (w * N + n) * G)) & M64
+                for b in range(64):
+                    if 64 * w + b < R and (x >> b) & 1:
+                        inf[64 * w + b] += 1
+            fc += f
+        out.append(dict(round=t, full=fc, converged=int(fc == N), messages=msgs, hash=h, infected=inf))
+        if fc == N or msgs == 0:
+            break
+    for node, want in c["reads"].items():
+        n = int(node)
+        assert [r for r in range(R) if (S[r // 64][n] >> (r % 64)) & 1] == want, (c["name"], node)
     return out
 
 
@@ -141,6 +290,12 @@ if __name__ == "__main__":
         assert philox(v["ctr"], v["key"]) == v["out"]
     for c in d["random"]:
         assert random_case(c) == c["rounds"], c["name"]
+        print("ok", c["name"])
+    for c in d["random_faults"]:
+        assert random_case(c, c["max_rounds"]) == c["rounds"], c["name"]
+        print("ok", c["name"])
+    for c in d["flood"] + d["flood_faults"]:
+        assert flood_case(c) == c["rounds"], c["name"]
         print("ok", c["name"])
     for c in d["antientropy"]:
         assert ae_case(c) == c["rounds"], c["name"]
