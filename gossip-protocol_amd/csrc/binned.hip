@@ -47,6 +47,30 @@ constexpr uint32_t kApplyPre = GOSSIP_APPLY_PRE;  // uint4 slots per thread of t
 constexpr int kUnroll = GOSSIP_APPLY_UNROLL;  // records in flight per lane in the run walkers (32 spills in K3)
 constexpr int kUnrollServe = 16;
 constexpr int kUnrollSeq = 8;  // records in flight per lane in the sequential response walker
+#ifndef GOSSIP_APPLY_SPLIT
+#define GOSSIP_APPLY_SPLIT 1
+#endif
+// push-pull apply: the block's waves split between the push walk (fragmented runs)
+// and the response walk (sequential regions), which then run side by side
+constexpr bool kApplySplit = GOSSIP_APPLY_SPLIT != 0;
+#ifndef GOSSIP_NT_REC
+#define GOSSIP_NT_REC 1  // emit's record stores (bench: serve -28 us, apply -10 us per dense round)
+#endif
+// Record buffers are written once and read once (or twice) per round: the
+// accesses in GOSSIP_NT_REC's mask carry the non-temporal hint, so the streamed
+// records do not displace the state image from the caches.  Bits: 1 emit
+// stores, 2 serve id loads, 4 serve response stores, 8 apply push loads, 16
+// apply response-walk loads.
+template <int BIT, typename T>
+__device__ __forceinline__ void rec_st(T* p, T v) {
+  if constexpr ((GOSSIP_NT_REC & BIT) != 0) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+template <int BIT, typename T>
+__device__ __forceinline__ T rec_ld(const T* p) {
+  if constexpr ((GOSSIP_NT_REC & BIT) != 0) return __builtin_nontemporal_load(p);
+  else return *p;
+}
 // record id word: p_local [0,14) | n_local [14,27) | flags.  K1 rewrites every
 // id each round, so a flag never outlives its round.
 constexpr uint32_t kIdVZ = 1u << 27;  // no push on this record (sender empty, or the peer already full)
@@ -326,9 +350,9 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
     // every value slot is stored (also where the flags say no push), so the
     // region is written without holes (a partly written 64-B chunk costs HBM
     // a read-modify-write: profiles/r01_experiments/microbench5_scattered_pieces.jsonl)
-    gids[e] = id;
-    if (STAGE) gvals[e] = sval[(id >> kTileDLog) & kIdNMask];
-    if (V == 3) gvals[e] = S[base + ((id >> kTileDLog) & kIdNMask)];
+    rec_st<1>(&gids[e], id);
+    if (STAGE) rec_st<1>(&gvals[e], sval[(id >> kTileDLog) & kIdNMask]);
+    if (V == 3) rec_st<1>(&gvals[e], S[base + ((id >> kTileDLog) & kIdNMask)]);
   }
 #pragma unroll
   for (uint32_t q = 0; q < kQ; ++q) v[q] = vn[q];
@@ -370,29 +394,72 @@ __device__ __forceinline__ void tile_epilogue(const unsigned long long* acc, uin
   const bool do_hash = (flags & 1u) != 0;
   uint64_t hash = 0;
   uint32_t full = 0, nzc = 0, c_lane = 0;
-  for (uint32_t q = 0; q < kTileD / kTileThreads; ++q) {
-    const uint32_t i = q * kTileThreads + tid;
-    const uint64_t n = node0 + i;
-    const bool valid = n < N;
-    const uint64_t x = valid ? (uint64_t)acc[i] : 0ull;
-    if (valid) Snext[n] = x;
-    if (do_hash && x) hash += mix64(x + (hid0 + n) * kGold64);
-    const uint64_t fw = __ballot(valid && x == fm);
-    const uint64_t nz = __ballot(x != 0);
-    full += (uint32_t)__popcll(fw);
-    nzc += (uint32_t)__popcll(nz);
-    // a wave holds 64 consecutive nodes: one word of each occupancy bitmap
-    if (nzb && lane == 0 && (n - lane) < N) {
-      nzb[n >> 6] = nz;
-      fullb[n >> 6] = fw;
+  // Per-rumor counts: the lane's 16 words are summed bit-sliced (a carry-save
+  // adder tree: planes of weight 1, 2, 4, 8, 16 per rumor bit), then each
+  // plane's 64x64 matrix is transposed once per wave — five transposes for
+  // 1024 nodes instead of sixteen.
+  constexpr uint32_t kQ = kTileD / kTileThreads;
+  static_assert(kQ == 16, "tile_epilogue: the adder tree sums 16 words per lane");
+  uint64_t plane[5];
+  {
+    uint64_t ones = 0, twos = 0, fours = 0, eights = 0, sixteens = 0;
+    auto csa = [](uint64_t& h, uint64_t& l, uint64_t a, uint64_t b, uint64_t c) {
+      const uint64_t u = a ^ b;
+      h = (a & b) | (u & c);
+      l = u ^ c;
+    };
+    uint64_t xs[2], twosA, twosB, foursA, foursB, eightsA, eightsB;
+    uint64_t hash_key = (hid0 + node0 + tid) * kGold64;
+    auto word = [&](uint32_t q) -> uint64_t {
+      const uint32_t i = q * kTileThreads + tid;
+      const uint64_t n = node0 + i;
+      const bool valid = n < N;
+      const uint64_t x = valid ? (uint64_t)acc[i] : 0ull;
+      if (valid) Snext[n] = x;
+      if (do_hash && x) hash += mix64(x + hash_key);
+      hash_key += (uint64_t)kTileThreads * kGold64;
+      const uint64_t fw = __ballot(valid && x == fm);
+      const uint64_t nz = __ballot(x != 0);
+      full += (uint32_t)__popcll(fw);
+      nzc += (uint32_t)__popcll(nz);
+      // a wave holds 64 consecutive nodes: one word of each occupancy bitmap
+      if (nzb && lane == 0 && (n - lane) < N) {
+        nzb[n >> 6] = nz;
+        fullb[n >> 6] = fw;
+      }
+      return x;
+    };
+#pragma unroll
+    for (uint32_t h8 = 0; h8 < 2; ++h8) {
+#pragma unroll
+      for (uint32_t h4 = 0; h4 < 2; ++h4) {
+        xs[0] = word(h8 * 8 + h4 * 4 + 0);
+        xs[1] = word(h8 * 8 + h4 * 4 + 1);
+        csa(twosA, ones, ones, xs[0], xs[1]);
+        xs[0] = word(h8 * 8 + h4 * 4 + 2);
+        xs[1] = word(h8 * 8 + h4 * 4 + 3);
+        csa(twosB, ones, ones, xs[0], xs[1]);
+        if (h4 == 0) csa(foursA, twos, twos, twosA, twosB);
+        else csa(foursB, twos, twos, twosA, twosB);
+      }
+      if (h8 == 0) csa(eightsA, fours, fours, foursA, foursB);
+      else csa(eightsB, fours, fours, foursA, foursB);
     }
-    if (nz == 0) continue;
-    const uint64_t fl = __ballot(x == fm);
-    if (fl == nz) {
-      c_lane += (uint32_t)__popcll(nz);
-    } else {
-      c_lane += (uint32_t)__popcll(transpose64(x, lane));
+    csa(sixteens, eights, eights, eightsA, eightsB);
+    plane[0] = ones;
+    plane[1] = twos;
+    plane[2] = fours;
+    plane[3] = eights;
+    plane[4] = sixteens;
+  }
+#pragma unroll
+  for (uint32_t p = 0; p < 5; ++p) {
+    if (__ballot(plane[p] != 0) == 0) continue;
+    if (__ballot(plane[p] != fm) == 0) {  // every lane has every rumor at this weight
+      c_lane += 64u << p;
+      continue;
     }
+    c_lane += (uint32_t)__popcll(transpose64(plane[p], lane)) << p;
   }
   if (lane < R && c_lane) atomicAdd(&cnt[lane], c_lane);  // bits >= R are never set
   hash = wave_sum64(hash);
@@ -432,16 +499,19 @@ __device__ __forceinline__ void wave_sync() {
 // list of the window's runs: rank = (run starts at or before it) - 1, one
 // popcount and one LDS read per record, no search.  fn(rec) receives the
 // global record index s * rp + pos, or -1 past the end.
-// LDS per wave: wmask[U] u64, wlist[64] i32.
+// LDS per wave: wmask[U] u64, wlist[64] i32.  The walk is shared by the waves
+// [w0, w0 + nwaves) of the block (nwaves = 0: every wave).
 template <int U, typename F>
 __device__ __forceinline__ void for_each_run_record(const BinGeom& g, const uint16_t* rowb, const uint16_t* rowe,
-                                                    uint64_t* wmask_all, int32_t* wlist_all, F&& fn) {
+                                                    uint64_t* wmask_all, int32_t* wlist_all, F&& fn,
+                                                    uint32_t w0 = 0, uint32_t nwaves = 0) {
   constexpr uint32_t kWin = 64 * U;
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (nwaves == 0) nwaves = blockDim.x >> 6;
   uint64_t* wm = wmask_all + wave * U;
   int32_t* wl = wlist_all + wave * 64;
   const uint64_t below = (1ull << lane) - 1ull, upto = (2ull << lane) - 1ull;  // lane 63: 2 << 63 wraps to all ones
-  for (uint32_t s0 = wave * 64; s0 < g.nt_s; s0 += nwaves * 64) {
+  for (uint32_t s0 = (wave - w0) * 64; s0 < g.nt_s; s0 += nwaves * 64) {
     const uint32_t s = s0 + lane;
     const uint32_t sc = min(s, g.nt_s - 1);
     const uint32_t be0 = rowb[sc], en0 = rowe[sc];
@@ -533,14 +603,14 @@ __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, cons
   for_each_run_record<kUnrollServe>(g, rowb, rowb + g.nt_s, wmask, wlist, [&](const int32_t* rec) {
     uint32_t id[kUnrollServe];
 #pragma unroll
-    for (int u = 0; u < kUnrollServe; ++u) id[u] = gids[rec[u] >= 0 ? rec[u] : 0];
+    for (int u = 0; u < kUnrollServe; ++u) id[u] = rec_ld<2>(&gids[rec[u] >= 0 ? rec[u] : 0]);
 #pragma unroll
     for (int u = 0; u < kUnrollServe; ++u) {
       // a fully informed sender needs nothing; otherwise the whole S_t[p] goes
       // back (bits n already holds are harmless to OR), so no value is read
       // dense rounds: every response is written (K3 tells stale slots by kIdVF)
       if (rec[u] < 0 || (id[u] & kIdVF)) continue;
-      gresp[rec[u]] = img[id[u] & (kTileD - 1)];
+      rec_st<4>(&gresp[rec[u]], (uint64_t)img[id[u] & (kTileD - 1)]);
     }
   });
   }
@@ -594,15 +664,21 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
   __syncthreads();
   const uint32_t* __restrict__ gids = b.ids;
   const uint64_t* __restrict__ gvals = b.vals;
-  if (mode == 1 || mode == 3) {  // pushes aimed at this tile
+  const uint32_t wave = tid >> 6, nwav = kTileThreads / 64;
+  const bool split = kApplySplit && mode == 3;
+  const bool do_push = (mode == 1 || mode == 3) && (!split || wave < nwav / 2);
+  const bool do_pull = (mode == 2 || mode == 3) && (!split || wave >= nwav / 2);
+  // split: waves [0, 8) walk the pushes, [8, 16) the responses (threads 512..1023)
+  const uint32_t qt0 = split ? kTileThreads / 2 : 0u, qnt = split ? kTileThreads / 2 : kTileThreads;
+  if (do_push) {  // pushes aimed at this tile
     const uint16_t* rowb = b.offT + (size_t)X * g.nt_s;
     for_each_run_record<kUnroll>(g, rowb, rowb + g.nt_s, wmask, wlist, [&](const int32_t* rec) {
       uint32_t id[kUnroll];
       uint64_t v[kUnroll];
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) id[u] = gids[rec[u] >= 0 ? rec[u] : 0];
+      for (int u = 0; u < kUnroll; ++u) id[u] = rec_ld<8>(&gids[rec[u] >= 0 ? rec[u] : 0]);
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) v[u] = gvals[rec[u] >= 0 ? rec[u] : 0];  // not behind the id: both loads fly together
+      for (int u = 0; u < kUnroll; ++u) v[u] = rec_ld<8>(&gvals[rec[u] >= 0 ? rec[u] : 0]);  // not behind the id: both loads fly together
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u)
         v[u] = rec[u] < 0 || (id[u] & kIdVZ) ? 0ull : v[u];  // every value is stored (K1)
@@ -611,9 +687,9 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
         const uint32_t p = id[u] & (kTileD - 1);
         if (v[u] && (v[u] & ~acc[p])) atomicOr(&acc[p], (unsigned long long)v[u]);
       }
-    });
+    }, 0u, split ? nwav / 2 : 0u);
   }
-  if (mode == 2 || mode == 3) {  // responses owed to this tile's own senders
+  if (do_pull) {  // responses owed to this tile's own senders
     const uint32_t* __restrict__ qids = bq.ids;
     const uint64_t* __restrict__ gresp = bq.resp;
     const uint32_t per = kTileD >> gq.ts_log;
@@ -622,20 +698,21 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
       const uint32_t total = bq.off[(size_t)s * (gq.nt_d + 1) + gq.nt_d];
       const size_t reg = (size_t)s * gq.rp;
       const uint32_t nb = (s - s0) << gq.ts_log;
-      for (uint32_t p0 = 0; p0 < total; p0 += kTileThreads * kUnrollSeq) {
+      const uint32_t qtid = tid - qt0;
+      for (uint32_t p0 = 0; p0 < total; p0 += qnt * kUnrollSeq) {
         uint64_t r[kUnrollSeq];
         uint32_t id[kUnrollSeq];
         // id and response loads are independent: both fly together
 #pragma unroll
         for (int u = 0; u < kUnrollSeq; ++u) {
-          const uint32_t pos = min(p0 + u * kTileThreads + tid, total - 1);
-          id[u] = qids[reg + pos];
-          r[u] = gresp[reg + pos];
+          const uint32_t pos = min(p0 + u * qnt + qtid, total - 1);
+          id[u] = rec_ld<16>(&qids[reg + pos]);
+          r[u] = rec_ld<16>(&gresp[reg + pos]);
         }
 #pragma unroll
         for (int u = 0; u < kUnrollSeq; ++u) {
           // a full sender's slot was never written this round (K2 skips it)
-          if (p0 + u * kTileThreads + tid >= total || (id[u] & kIdVF)) continue;
+          if (p0 + u * qnt + qtid >= total || (id[u] & kIdVF)) continue;
           const uint32_t node = nb + ((id[u] >> kTileDLog) & kIdNMask);
           if (r[u] & ~acc[node]) atomicOr(&acc[node], (unsigned long long)r[u]);
         }

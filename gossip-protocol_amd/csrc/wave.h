@@ -16,6 +16,8 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
 // 64x64 bit-matrix transpose across a wave64: on entry lane i holds row i, on
 // exit lane j holds column j (bit i = bit j of lane i's input word).  Popcount
 // of the result = how many of the wave's 64 words have bit `lane` set.
+// (A DPP / permlane-swap form with no ds_bpermute measured slower in the apply
+// epilogue: DESIGN.md §3.7.)
 __device__ __forceinline__ uint64_t transpose64(uint64_t x, uint32_t lane) {
   constexpr uint64_t kMask[6] = {0x00000000FFFFFFFFull, 0x0000FFFF0000FFFFull, 0x00FF00FF00FF00FFull,
                                  0x0F0F0F0F0F0F0F0Full, 0x3333333333333333ull, 0x5555555555555555ull};
