@@ -111,4 +111,52 @@ hipError_t launch_sb_round(const SbGeom& g, const SbBufs& b, const uint64_t* ima
                            uint64_t* partial, uint32_t R, uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode,
                            const Faults& fa, uint32_t flags, uint64_t* nzb, uint64_t* fullb, hipStream_t st);
 
+// Exchange dense rounds of a sharded engine: no state image.
+// Each shard emits one item per live edge of its own senders, grouped by the
+// owner of the peer ({p at its owner | direction flags, S_t[n]}); the items go
+// to their owners (all-to-all); each owner bins what it received by its own
+// destination tile, answers the pulls from LDS images of S_t and returns the
+// replies in the received order (all-to-all back); then every shard ORs the
+// pushes it received and the replies to its own pulls into LDS images of its
+// tiles.  Per-shard work is O(nodes per shard) at any G.
+constexpr uint32_t kXdNoPush = 1u << 30;  // wire item id: p at the owner [0, 30) | these two flags
+constexpr uint32_t kXdNoPull = 1u << 31;
+constexpr uint32_t kXdBinRegion = 16384;  // received items binned per LDS region
+struct XdGeom {
+  uint64_t N, Nl, lo, nown;
+  uint32_t G, rank, k;
+  BinGeom s;  // own senders: ts, ts_log, rp (region records), nt_s regions; nt_d own tiles; N = nown
+  BinGeom r;  // received items: rp = kXdBinRegion, nt_s regions of this round (xd_bin_regions), nt_d own tiles
+};
+struct XdBufs {
+  uint32_t *rcnt, *roff;      // [s.nt_s][G] items per (sender region, owner) and their send positions
+  uint32_t* rlofs;            // [s.nt_s][G + 1] each region's owner runs in its own order (prefix)
+  uint32_t* ocnt;             // [G] items per owner
+  uint32_t* sid;              // send items, owner-major [cap_s]
+  uint64_t* sval;
+  uint16_t* snl;              // the sender of each send item (index in its region), kept here
+  uint64_t* rep_in;           // replies to the send items, in send order [cap_s]
+  uint32_t* rid;              // received items [cap_r]
+  uint64_t* rval;
+  BinBufs rb;                 // received items binned by own tile (regions of kXdBinRegion)
+  uint64_t* rep_out;          // replies to the received items, in received order [cap_r]
+};
+bool xd_path_ok(uint64_t N, uint32_t k, uint64_t Nl, uint32_t G);
+XdGeom make_xd_geom(uint64_t N, uint32_t k, uint64_t Nl, uint64_t lo, uint64_t nown, uint32_t G, uint32_t rank);
+uint64_t xd_send_cap(const XdGeom& g);
+size_t xd_send_bytes(const XdGeom& g);  // rcnt .. rep_in
+void xd_carve_send(const XdGeom& g, void* base, XdBufs* b);
+size_t xd_recv_bytes(const XdGeom& g, uint64_t cap_r);  // rid .. rep_out
+void xd_carve_recv(const XdGeom& g, uint64_t cap_r, void* base, XdBufs* b);
+// own senders' items: counts per (region, owner), send positions, then the items
+hipError_t launch_xd_requests(const XdGeom& g, const XdBufs& b, const uint64_t* S, uint32_t R, uint32_t t,
+                              uint32_t key0, uint32_t key1, uint32_t mode, const Faults& fa, hipStream_t st);
+// n_in received items: bin by own tile, serve the pulls from S_t, replies in received order (b.rep_out)
+hipError_t launch_xd_serve(XdGeom g, const XdBufs& b, const uint64_t* S, uint64_t n_in, uint32_t R,
+                           hipStream_t st);
+// S_{t+1} = S_t | pushes received | replies to the own pulls, stats of the own nodes (global ids in the hash)
+hipError_t launch_xd_apply(XdGeom g, const XdBufs& b, const uint64_t* S, uint64_t* Snext, uint64_t n_in,
+                           uint64_t* partial, uint32_t R, uint32_t mode, uint32_t flags, uint64_t* nzb,
+                           uint64_t* fullb, hipStream_t st);
+
 }  // namespace gossip

@@ -106,6 +106,47 @@ __device__ __forceinline__ uint32_t peer_filter(uint32_t d, uint32_t p, uint32_t
 // record flags: kIdVZ = no push on this record, kIdVF = no pull
 __device__ __forceinline__ uint32_t dir_flags(uint32_t d) { return ((d & 1u) ? 0u : kIdVZ) | ((d & 2u) ? 0u : kIdVF); }
 
+// Region counting sort, middle step: cur[0, nt) holds the records per
+// destination tile; writes each run's start to off_row[0, nt] (u16, the total
+// last), turns cur into the fill pointers and returns the total.  Every thread
+// of the (kEmitThreads) block calls it; it ends with a barrier.
+__device__ __forceinline__ uint32_t region_offsets(uint32_t* cur, uint32_t nt, uint16_t* off_row, uint32_t* wsum,
+                                                   uint32_t* wpre) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t per = (nt + kEmitThreads - 1) / kEmitThreads;
+  const uint32_t lo = min(tid * per, nt), hi = min(lo + per, nt);
+  uint32_t mine = 0;
+  for (uint32_t d = lo; d < hi; ++d) mine += cur[d];
+  uint32_t inc = mine;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if (lane >= (uint32_t)o) inc += y;
+  }
+  if (lane == 63) wsum[wave] = inc;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t a = 0;
+    for (int w = 0; w < kEmitThreads / 64; ++w) {
+      wpre[w] = a;
+      a += wsum[w];
+    }
+    wpre[kEmitThreads / 64] = a;
+  }
+  __syncthreads();
+  uint32_t run = wpre[wave] + inc - mine;
+  for (uint32_t d = lo; d < hi; ++d) {
+    const uint32_t c = cur[d];
+    cur[d] = run;
+    off_row[d] = (uint16_t)run;
+    run += c;
+  }
+  const uint32_t total = wpre[kEmitThreads / 64];
+  if (tid == 0) off_row[nt] = (uint16_t)total;
+  __syncthreads();
+  return total;
+}
+
 // KREG > 0: the k (<= KREG) peers of each sender stay in registers between passes.
 // FAULTS: edge loss / partitions active; off, none of that code exists.
 // V = 0: one shard.  V = 1, 2: one pass of a sharded dense round (EmitRange):
@@ -131,7 +172,7 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
   __shared__ uint32_t wsum[kEmitThreads / 64];
   __shared__ uint32_t wpre[kEmitThreads / 64 + 1];
 
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t tid = threadIdx.x;
   const uint64_t nm1 = g.N - 1, fm = full_mask1(R);
   constexpr uint32_t kQ = kMaxS / kEmitThreads;  // senders per thread upper bound
   const uint64_t snd0 = SHARD ? er.snd0 : 0ull, nsnd = SHARD ? er.nsnd : g.N;
@@ -266,39 +307,7 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
   }
   __syncthreads();
 
-  // exclusive scan of cur[0, nt_d)
-  const uint32_t per = (g.nt_d + kEmitThreads - 1) / kEmitThreads;
-  const uint32_t lo = min(tid * per, g.nt_d), hi = min(lo + per, g.nt_d);
-  uint32_t mine = 0;
-  for (uint32_t d = lo; d < hi; ++d) mine += cur[d];
-  uint32_t inc = mine;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(inc, o, 64);
-    if (lane >= (uint32_t)o) inc += y;
-  }
-  if (lane == 63) wsum[wave] = inc;
-  __syncthreads();
-  if (tid == 0) {
-    uint32_t a = 0;
-    for (int w = 0; w < kEmitThreads / 64; ++w) {
-      wpre[w] = a;
-      a += wsum[w];
-    }
-    wpre[kEmitThreads / 64] = a;
-  }
-  __syncthreads();
-  uint32_t run = wpre[wave] + inc - mine;
-  uint16_t* off = b.off + (size_t)s * (g.nt_d + 1);
-  for (uint32_t d = lo; d < hi; ++d) {
-    const uint32_t c = cur[d];
-    cur[d] = run;
-    off[d] = (uint16_t)run;
-    run += c;
-  }
-  const uint32_t total = wpre[kEmitThreads / 64];
-  if (tid == 0) off[g.nt_d] = (uint16_t)total;
-  __syncthreads();
+  const uint32_t total = region_offsets(cur, g.nt_d, b.off + (size_t)s * (g.nt_d + 1), wsum, wpre);
 
   // pass B: each record to its slot (k <= KREG: the peers and directions from
   // registers; else the same draws and probes again)
@@ -554,6 +563,32 @@ __device__ __forceinline__ void for_each_run_record(const BinGeom& g, const uint
   }
 }
 
+// The pushes aimed at tile X (its runs in every sender region) ORed into acc,
+// by the waves [0, nwaves) (0: all).  VZ: the record id's no-push flag.
+template <uint32_t VZ>
+__device__ __forceinline__ void push_walk(const BinGeom& g, const BinBufs& b, uint32_t X, unsigned long long* acc,
+                                          uint64_t* wmask, int32_t* wlist, uint32_t nwaves) {
+  const uint32_t* __restrict__ gids = b.ids;
+  const uint64_t* __restrict__ gvals = b.vals;
+  const uint16_t* rowb = b.offT + (size_t)X * g.nt_s;
+  for_each_run_record<kUnroll>(g, rowb, rowb + g.nt_s, wmask, wlist, [&](const int32_t* rec) {
+    uint32_t id[kUnroll];
+    uint64_t v[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) id[u] = rec_ld<8>(&gids[rec[u] >= 0 ? rec[u] : 0]);
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) v[u] = rec_ld<8>(&gvals[rec[u] >= 0 ? rec[u] : 0]);  // not behind the id: both loads fly together
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u)
+      v[u] = rec[u] < 0 || (id[u] & VZ) ? 0ull : v[u];  // every value is stored (K1)
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const uint32_t p = id[u] & (kTileD - 1);
+      if (v[u] && (v[u] & ~acc[p])) atomicOr(&acc[p], (unsigned long long)v[u]);
+    }
+  }, 0u, nwaves);
+}
+
 // Tile image in registers (the next tile's loads fly during the current walk).
 constexpr uint32_t kTileQ = kTileD / kTileThreads / 2;  // uint4 per thread
 // Slots [Q0, Q0 + Q) of this thread's part of the tile (x[i] = slot Q0 + i).
@@ -578,6 +613,8 @@ __device__ __forceinline__ void tile_regs_load(uint4 (&x)[Q], const uint64_t* __
 // K2 — one block per destination tile T (pull modes): LDS image of S_t[T];
 // every record aimed at T from a sender that is not yet fully informed gets
 // its pull response S_t[p] written next to it when nonzero (every one, in dense rounds).
+// VF: the record id's no-pull flag (kIdVF; exchange rounds' binned items: kXbVF).
+template <uint32_t VF>
 __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, const uint64_t* __restrict__ S, BinBufs b,
                                                                   uint32_t R, IdxRange tr) {
   __shared__ unsigned long long img[kTileD];
@@ -609,7 +646,7 @@ __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, cons
       // a fully informed sender needs nothing; otherwise the whole S_t[p] goes
       // back (bits n already holds are harmless to OR), so no value is read
       // dense rounds: every response is written (K3 tells stale slots by kIdVF)
-      if (rec[u] < 0 || (id[u] & kIdVF)) continue;
+      if (rec[u] < 0 || (id[u] & VF)) continue;
       rec_st<4>(&gresp[rec[u]], (uint64_t)img[id[u] & (kTileD - 1)]);
     }
   });
@@ -662,33 +699,13 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
   }
   if (tid < 64) cnt[tid] = 0;
   __syncthreads();
-  const uint32_t* __restrict__ gids = b.ids;
-  const uint64_t* __restrict__ gvals = b.vals;
   const uint32_t wave = tid >> 6, nwav = kTileThreads / 64;
   const bool split = kApplySplit && mode == 3;
   const bool do_push = (mode == 1 || mode == 3) && (!split || wave < nwav / 2);
   const bool do_pull = (mode == 2 || mode == 3) && (!split || wave >= nwav / 2);
   // split: waves [0, 8) walk the pushes, [8, 16) the responses (threads 512..1023)
   const uint32_t qt0 = split ? kTileThreads / 2 : 0u, qnt = split ? kTileThreads / 2 : kTileThreads;
-  if (do_push) {  // pushes aimed at this tile
-    const uint16_t* rowb = b.offT + (size_t)X * g.nt_s;
-    for_each_run_record<kUnroll>(g, rowb, rowb + g.nt_s, wmask, wlist, [&](const int32_t* rec) {
-      uint32_t id[kUnroll];
-      uint64_t v[kUnroll];
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) id[u] = rec_ld<8>(&gids[rec[u] >= 0 ? rec[u] : 0]);
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) v[u] = rec_ld<8>(&gvals[rec[u] >= 0 ? rec[u] : 0]);  // not behind the id: both loads fly together
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u)
-        v[u] = rec[u] < 0 || (id[u] & kIdVZ) ? 0ull : v[u];  // every value is stored (K1)
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        const uint32_t p = id[u] & (kTileD - 1);
-        if (v[u] && (v[u] & ~acc[p])) atomicOr(&acc[p], (unsigned long long)v[u]);
-      }
-    }, 0u, split ? nwav / 2 : 0u);
-  }
+  if (do_push) push_walk<kIdVZ>(g, b, X, acc, wmask, wlist, split ? nwav / 2 : 0u);  // pushes aimed at this tile
   if (do_pull) {  // responses owed to this tile's own senders
     const uint32_t* __restrict__ qids = bq.ids;
     const uint64_t* __restrict__ gresp = bq.resp;
@@ -804,7 +821,7 @@ hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, 
   const dim3 tg((g.nt_d + 1 + 31) / 32, (g.nt_s + 31) / 32);
   transpose_u16_kernel<<<tg, dim3(32, 8), 0, st>>>(b.off, b.offT, g.nt_s, g.nt_d + 1, partial, rs.plen);
   if (mode == 2 || mode == 3)
-    bin_serve_kernel<<<serve_grid(g.nt_d), kTileThreads, 0, st>>>(g, S, b, R, IdxRange::all(g.nt_d));
+    bin_serve_kernel<kIdVF><<<serve_grid(g.nt_d), kTileThreads, 0, st>>>(g, S, b, R, IdxRange::all(g.nt_d));
   // in place: K3 of tile X reads and writes only S[X] (push values and pull
   // responses come from the record buffers), and K1/K2 have finished reading S_t
   bin_apply_kernel<<<apply_grid(g), kTileThreads, 0, st>>>(g, b, g, b, S, S, g.N, 0, partial, R, mode, flags);
@@ -893,7 +910,7 @@ hipError_t launch_sb_pre(const SbGeom& g, const SbBufs& b, const uint64_t* image
     sb_emit(g.q, b.q, image, R, t, key0, key1, mode, fa, pull_range(g), false, st);
     sb_transpose(g.q, b.q, nullptr, st);
     const IdxRange ot = own_tiles(g);
-    if (ot.n) bin_serve_kernel<<<serve_grid(ot.n), kTileThreads, 0, st>>>(g.q, image, b.q, R, ot);
+    if (ot.n) bin_serve_kernel<kIdVF><<<serve_grid(ot.n), kTileThreads, 0, st>>>(g.q, image, b.q, R, ot);
   }
   if (push) sb_emit(g.p, b.p, image, R, t, key0, key1, mode, fa, push_range(g, own_regions(g)), true, st);
   return hipGetLastError();
@@ -910,7 +927,7 @@ hipError_t launch_sb_post(const SbGeom& g, const SbBufs& b, const uint64_t* imag
   }
   if (pull) {
     const IdxRange rt = rest_of(g.q.nt_d, own_tiles(g));
-    if (rt.n) bin_serve_kernel<<<serve_grid(rt.n), kTileThreads, 0, st>>>(g.q, image, b.q, R, rt);
+    if (rt.n) bin_serve_kernel<kIdVF><<<serve_grid(rt.n), kTileThreads, 0, st>>>(g.q, image, b.q, R, rt);
   }
   BinBufs bp = b.p;
   bp.nzb = nzb;
@@ -926,6 +943,416 @@ hipError_t launch_sb_round(const SbGeom& g, const SbBufs& b, const uint64_t* ima
   const hipError_t e = launch_sb_pre(g, b, image, R, t, key0, key1, mode, fa, st);
   if (e != hipSuccess) return e;
   return launch_sb_post(g, b, image, Snext, partial, R, t, key0, key1, mode, fa, flags, nzb, fullb, st);
+}
+
+
+// --- exchange dense rounds (binned.h: XdGeom) ---------------
+
+namespace {
+
+constexpr uint32_t kXdMaxG = 256;
+// binned received item: p_local [0, 14) | slot in its region [14, 28) | no push | no pull
+constexpr uint32_t kXbVZ = 1u << 28;
+constexpr uint32_t kXbVF = 1u << 29;
+constexpr uint32_t kXbSlotMask = kXdBinRegion - 1u;
+constexpr uint32_t kXdPref = 2048;
+constexpr int kUnrollXd = 4;  // replies in flight per lane in apply (each finds its owner run first)  // apply's LDS copy of its regions' (G + 1)-entry prefix rows
+
+__device__ __forceinline__ uint32_t xd_owner(uint32_t p, uint32_t Nl32, uint32_t G) {
+  const uint32_t o = p / Nl32;
+  return o < G ? o : G - 1u;
+}
+
+// the live edges n -> p of sender n in round t (draws as bin_emit's; a lost edge
+// carries nothing in either direction)
+template <bool FAULTS, typename F>
+__device__ __forceinline__ void xd_edges(uint32_t k, uint32_t n, uint64_t nm1, uint32_t t, uint32_t key0,
+                                         uint32_t key1, const Faults& fa, F&& fn) {
+  u32x4 x{0, 0, 0, 0}, lw{0, 0, 0, 0};
+  const Reach rc = FAULTS ? reach_of(n, fa) : Reach{0u, 0xFFFFFFFFu};
+  for (uint32_t j = 0; j < k; ++j) {
+    if ((j & 3u) == 0) {
+      x = philox4x32_10(u32x4{n, t, 0u, j >> 2}, key0, key1);
+      if (FAULTS && fa.loss) lw = loss_draws(n, t, j >> 2, key0, key1);
+    }
+    const uint32_t p = peer_from_word(lane_of(x, j & 3u), nm1, n);
+    if (FAULTS && edge_lost(fa, rc, p, lane_of(lw, j & 3u))) continue;
+    fn(p);
+  }
+}
+
+// items per (sender region, owner of the peer)
+template <bool FAULTS>
+__global__ __launch_bounds__(kEmitThreads) void xd_count_kernel(XdGeom g, const uint64_t* __restrict__ S,
+                                                                 uint32_t* __restrict__ rcnt, uint32_t R, uint32_t t,
+                                                                 uint32_t key0, uint32_t key1, uint32_t mode,
+                                                                 Faults fa) {
+  __shared__ uint32_t cnt[kXdMaxG];
+  const uint32_t tid = threadIdx.x, Nl32 = (uint32_t)g.Nl;
+  const uint64_t fm = full_mask1(R), nm1 = g.N - 1;
+  for (uint32_t s = blockIdx.x; s < g.s.nt_s; s += gridDim.x) {
+    __syncthreads();
+    for (uint32_t o = tid; o < g.G; o += kEmitThreads) cnt[o] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)s << g.s.ts_log;
+    const uint32_t nsend = (uint32_t)min<uint64_t>(g.s.ts, g.nown - base);
+    for (uint32_t i = tid; i < nsend; i += kEmitThreads) {
+      if (!sender_dirs(mode, S[base + i], fm)) continue;
+      xd_edges<FAULTS>(g.k, (uint32_t)(g.lo + base + i), nm1, t, key0, key1, fa,
+                       [&](uint32_t p) { atomicAdd(&cnt[xd_owner(p, Nl32, g.G)], 1u); });
+    }
+    __syncthreads();
+    for (uint32_t o = tid; o < g.G; o += kEmitThreads) rcnt[(size_t)s * g.G + o] = cnt[o];
+  }
+}
+
+// send positions: owner-major, then sender region; ocnt = items per owner
+__global__ __launch_bounds__(1024) void xd_scan_kernel(const uint32_t* __restrict__ rcnt, uint32_t* __restrict__ roff,
+                                                        uint32_t* __restrict__ ocnt, uint32_t nrs, uint32_t G) {
+  __shared__ uint32_t scratch[1024 / 64 + 1];
+  const uint32_t per = (nrs + 1023) / 1024;
+  const uint32_t lo = min(threadIdx.x * per, nrs), hi = min(lo + per, nrs);
+  uint32_t base = 0;
+  for (uint32_t o = 0; o < G; ++o) {
+    uint32_t mine = 0;
+    for (uint32_t s = lo; s < hi; ++s) mine += rcnt[(size_t)s * G + o];
+    uint32_t total;
+    uint32_t run = base + block_exscan<1024>(mine, scratch, &total);
+    for (uint32_t s = lo; s < hi; ++s) {
+      const uint32_t c = rcnt[(size_t)s * G + o];
+      roff[(size_t)s * G + o] = run;
+      run += c;
+    }
+    if (threadIdx.x == 0) ocnt[o] = total;
+    base += total;
+  }
+}
+
+// the items of sender region s, counting-sorted by owner in LDS and written to
+// their send positions; rlofs[s] = the region's owner runs (G + 1 prefix)
+template <bool FAULTS>
+__global__ __launch_bounds__(kEmitThreads) void xd_emit_kernel(XdGeom g, const uint64_t* __restrict__ S, XdBufs b,
+                                                                uint32_t* __restrict__ rlofs, uint32_t R, uint32_t t,
+                                                                uint32_t key0, uint32_t key1, uint32_t mode,
+                                                                Faults fa) {
+  __shared__ uint32_t cur[kXdMaxG];
+  __shared__ uint32_t lofs[kXdMaxG + 1];
+  __shared__ uint32_t st_id[kRecPerRegion];
+  __shared__ uint16_t st_nl[kRecPerRegion];
+  const uint32_t tid = threadIdx.x, Nl32 = (uint32_t)g.Nl, G = g.G;
+  const uint64_t fm = full_mask1(R), nm1 = g.N - 1;
+  for (uint32_t s = blockIdx.x; s < g.s.nt_s; s += gridDim.x) {
+    __syncthreads();  // the previous region's write-out is done with the LDS
+    if (tid == 0) {
+      uint32_t a = 0;
+      for (uint32_t o = 0; o < G; ++o) {
+        lofs[o] = a;
+        cur[o] = a;
+        a += b.rcnt[(size_t)s * G + o];
+      }
+      lofs[G] = a;
+    }
+    __syncthreads();
+    for (uint32_t o = tid; o <= G; o += kEmitThreads) rlofs[(size_t)s * (G + 1) + o] = lofs[o];
+    const uint64_t base = (uint64_t)s << g.s.ts_log;
+    const uint32_t nsend = (uint32_t)min<uint64_t>(g.s.ts, g.nown - base);
+    for (uint32_t i = tid; i < nsend; i += kEmitThreads) {
+      const uint32_t d = sender_dirs(mode, S[base + i], fm);
+      if (!d) continue;
+      const uint32_t fl = ((d & 1u) ? 0u : kXdNoPush) | ((d & 2u) ? 0u : kXdNoPull);
+      xd_edges<FAULTS>(g.k, (uint32_t)(g.lo + base + i), nm1, t, key0, key1, fa, [&](uint32_t p) {
+        const uint32_t o = xd_owner(p, Nl32, G);
+        const uint32_t pos = atomicAdd(&cur[o], 1u);
+        st_id[pos] = (p - o * Nl32) | fl;
+        st_nl[pos] = (uint16_t)i;
+      });
+    }
+    __syncthreads();
+    const uint32_t total = lofs[G];
+    for (uint32_t e = tid; e < total; e += kEmitThreads) {
+      uint32_t lo = 0, hi = G;  // the owner: the last o with lofs[o] <= e
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (lofs[mid] <= e) lo = mid;
+        else hi = mid;
+      }
+      const size_t dst = (size_t)b.roff[(size_t)s * G + lo] + (e - lofs[lo]);
+      const uint32_t id = st_id[e], nl = st_nl[e];
+      rec_st<1>(&b.sid[dst], id);
+      rec_st<1>(&b.snl[dst], (uint16_t)nl);
+      rec_st<1>(&b.sval[dst], (uint64_t)((id & kXdNoPush) ? 0ull : S[base + nl]));  // the region's slice: L2 hits
+    }
+  }
+}
+
+// received items binned by own destination tile (one region of kXdBinRegion
+// items per pass of the block); the binned id keeps the item's slot
+__global__ __launch_bounds__(kEmitThreads) void xd_bin_kernel(XdGeom g, XdBufs b, uint64_t n_in) {
+  __shared__ uint32_t cur[kSbMaxTiles];
+  __shared__ uint32_t st[kXdBinRegion];
+  __shared__ uint32_t wsum[kEmitThreads / 64];
+  __shared__ uint32_t wpre[kEmitThreads / 64 + 1];
+  constexpr uint32_t kQ = kXdBinRegion / kEmitThreads;
+  const uint32_t tid = threadIdx.x, nt = g.r.nt_d;
+  for (uint32_t r = blockIdx.x; r < g.r.nt_s; r += gridDim.x) {
+    __syncthreads();
+    for (uint32_t d = tid; d < nt; d += kEmitThreads) cur[d] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)r * kXdBinRegion;
+    const uint32_t nitems = (uint32_t)min<uint64_t>(kXdBinRegion, n_in - base);
+    uint32_t id[kQ];
+#pragma unroll
+    for (uint32_t q = 0; q < kQ; ++q) {
+      const uint32_t i = tid + q * kEmitThreads;
+      id[q] = i < nitems ? b.rid[base + i] : 0u;
+      if (i < nitems) atomicAdd(&cur[min((id[q] & (kXdNoPush - 1u)) >> kTileDLog, nt - 1u)], 1u);
+    }
+    __syncthreads();
+    const uint32_t total = region_offsets(cur, nt, b.rb.off + (size_t)r * (nt + 1), wsum, wpre);
+    uint32_t* gids = b.rb.ids + (size_t)r * g.r.rp;
+    uint64_t* gvals = b.rb.vals + (size_t)r * g.r.rp;
+#pragma unroll
+    for (uint32_t q = 0; q < kQ; ++q) {
+      const uint32_t i = tid + q * kEmitThreads;
+      if (i >= nitems) continue;
+      const uint32_t p = id[q] & (kXdNoPush - 1u);
+      const uint32_t pos = atomicAdd(&cur[min(p >> kTileDLog, nt - 1u)], 1u);  // (p < nown: emit's items)
+      st[pos] = (p & (kTileD - 1)) | (i << kTileDLog) | ((id[q] & kXdNoPush) ? kXbVZ : 0u) |
+                ((id[q] & kXdNoPull) ? kXbVF : 0u);
+    }
+    __syncthreads();
+    for (uint32_t e = tid; e < total; e += kEmitThreads) {
+      const uint32_t x = st[e];
+      rec_st<1>(&gids[e], x);
+      // the region's values were streamed in with the ids' lines: L2 hits
+      rec_st<1>(&gvals[e], (uint64_t)((x & kXbVZ) ? 0ull : b.rval[base + ((x >> kTileDLog) & kXbSlotMask)]));
+    }
+  }
+}
+
+// the responses (binned order) back to the received order, one region per pass
+__global__ __launch_bounds__(kEmitThreads) void xd_unperm_kernel(XdGeom g, XdBufs b, uint64_t n_in) {
+  __shared__ uint64_t buf[kXdBinRegion];
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t r = blockIdx.x; r < g.r.nt_s; r += gridDim.x) {
+    __syncthreads();
+    const uint64_t base = (uint64_t)r * kXdBinRegion;
+    const uint32_t nitems = (uint32_t)min<uint64_t>(kXdBinRegion, n_in - base);
+    const uint32_t* gids = b.rb.ids + (size_t)r * g.r.rp;
+    const uint64_t* gresp = b.rb.resp + (size_t)r * g.r.rp;
+    for (uint32_t e = tid; e < nitems; e += kEmitThreads) {
+      const uint32_t x = gids[e];
+      buf[(x >> kTileDLog) & kXbSlotMask] = (x & kXbVF) ? 0ull : gresp[e];  // serve wrote only the pulls
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < nitems; i += kEmitThreads) b.rep_out[base + i] = buf[i];
+  }
+}
+
+// S_{t+1}[X] = S_t[X] | pushes received for X | replies to the pulls of X's own senders
+__global__ __launch_bounds__(kTileThreads) void xd_apply_kernel(XdGeom g, XdBufs b, const uint32_t* __restrict__ rlofs,
+                                                                 const uint64_t* S, uint64_t* Snext,
+                                                                 uint64_t* __restrict__ partial, uint32_t R,
+                                                                 uint32_t mode, uint32_t flags, uint64_t* nzb,
+                                                                 uint64_t* fullb) {
+  __shared__ unsigned long long acc[kTileD];
+  __shared__ uint32_t cnt[64];
+  __shared__ uint64_t red_hash[kTileThreads / 64];
+  __shared__ uint32_t red_full[kTileThreads / 64];
+  __shared__ uint32_t red_nz[kTileThreads / 64];
+  __shared__ uint64_t wmask[(kTileThreads / 64) * kUnroll];
+  __shared__ int32_t wlist[(kTileThreads / 64) * 64];
+  __shared__ uint32_t pl[kXdPref];  // the tile's sender regions: owner-run prefix rows (G + 1 each)
+  __shared__ uint32_t po[kXdPref];  // and the runs' send positions (G each, stride G + 1)
+  const uint32_t tid = threadIdx.x, G = g.G;
+  const uint32_t nv = g.r.nt_d;
+  const uint32_t per = kTileD >> g.s.ts_log;
+  const uint32_t wave = tid >> 6, nwav = kTileThreads / 64;
+  const bool split = kApplySplit && mode == 3;
+  const bool do_push = (mode == 1 || mode == 3) && (!split || wave < nwav / 2);
+  const bool do_pull = (mode == 2 || mode == 3) && (!split || wave >= nwav / 2);
+  const uint32_t qt0 = split ? kTileThreads / 2 : 0u, qnt = split ? kTileThreads / 2 : kTileThreads;
+  for (uint32_t v = blockIdx.x; v < nv; v += gridDim.x) {
+    const uint32_t X = xcd_remap(v, nv);
+    const uint64_t node0 = (uint64_t)X << kTileDLog;
+    const uint32_t s0 = X * per, s1 = min(s0 + per, g.s.nt_s);
+    __syncthreads();  // the previous epilogue is done with acc, cnt and the prefix rows
+    {
+      uint4 xr[kTileQ];
+      tile_regs_load(xr, S, node0, g.nown);
+#pragma unroll
+      for (uint32_t q = 0; q < kTileQ; ++q) ((uint4*)acc)[q * kTileThreads + tid] = xr[q];
+    }
+    for (uint32_t i = tid; i < (s1 - s0) * (G + 1); i += kTileThreads) {
+      const uint32_t s = s0 + i / (G + 1), o = i % (G + 1);
+      pl[i] = rlofs[(size_t)s * (G + 1) + o];
+      po[i] = o < G ? b.roff[(size_t)s * G + o] : 0u;
+    }
+    if (tid < 64) cnt[tid] = 0;
+    __syncthreads();
+    if (do_push) push_walk<kXbVZ>(g.r, b.rb, X, acc, wmask, wlist, split ? nwav / 2 : 0u);
+    if (do_pull) {  // replies, in send order: region s's items are G runs (one per owner)
+      const uint32_t qtid = tid - qt0;
+      for (uint32_t s = s0; s < s1; ++s) {
+        const uint32_t* rl = pl + (s - s0) * (G + 1);
+        const uint32_t* ro = po + (s - s0) * (G + 1);
+        const uint32_t total = rl[G];
+        const uint32_t nb = (s - s0) << g.s.ts_log;
+        for (uint32_t f0 = 0; f0 < total; f0 += qnt * kUnrollXd) {
+          uint64_t rv[kUnrollXd];
+          uint32_t nl[kUnrollXd];
+#pragma unroll
+          for (int u = 0; u < kUnrollXd; ++u) {
+            const uint32_t f = min(f0 + u * qnt + qtid, total - 1);
+            uint32_t lo = 0, hi = G;  // f's owner run
+            while (hi - lo > 1) {
+              const uint32_t mid = (lo + hi) >> 1;
+              if (rl[mid] <= f) lo = mid;
+              else hi = mid;
+            }
+            const size_t pos = (size_t)ro[lo] + (f - rl[lo]);
+            rv[u] = rec_ld<16>(&b.rep_in[pos]);
+            nl[u] = b.snl[pos];
+          }
+#pragma unroll
+          for (int u = 0; u < kUnrollXd; ++u) {
+            if (f0 + u * qnt + qtid >= total) continue;
+            const uint32_t node = nb + nl[u];
+            if (rv[u] & ~acc[node]) atomicOr(&acc[node], (unsigned long long)rv[u]);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    tile_epilogue(acc, node0, g.nown, g.lo, Snext, partial, R, flags, cnt, red_hash, red_full, red_nz, nzb, fullb);
+  }
+}
+
+}  // namespace
+
+bool xd_path_ok(uint64_t N, uint32_t k, uint64_t Nl, uint32_t G) {
+  if (G < 2 || G > kXdMaxG || k == 0 || k > 64 || N < 2 || Nl >= (1ull << 30) || N > 0xFFFFFFFFull) return false;
+  const BinGeom s = make_bin_geom(Nl, k);
+  const uint32_t per = kTileD >> s.ts_log;
+  // apply's prefix rows; tiles of one shard; send positions and record indices fit u32 / int32
+  return (uint64_t)per * (G + 1) <= kXdPref && (Nl + kTileD - 1) / kTileD <= kSbMaxTiles &&
+         (uint64_t)k * Nl < (1ull << 31);
+}
+
+XdGeom make_xd_geom(uint64_t N, uint32_t k, uint64_t Nl, uint64_t lo, uint64_t nown, uint32_t G, uint32_t rank) {
+  XdGeom g{};
+  g.N = N;
+  g.Nl = Nl;
+  g.lo = lo;
+  g.nown = nown;
+  g.G = G;
+  g.rank = rank;
+  g.k = k;
+  g.s = make_bin_geom(nown ? nown : 1, k);
+  g.r = g.s;
+  g.r.N = nown;
+  g.r.ts = kXdBinRegion;
+  g.r.ts_log = kTileDLog;
+  g.r.rp = kXdBinRegion;
+  g.r.nt_s = 0;  // set per round from the received count
+  return g;
+}
+
+uint64_t xd_send_cap(const XdGeom& g) { return (uint64_t)g.k * g.nown; }
+
+namespace {
+size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+}  // namespace
+
+size_t xd_send_bytes(const XdGeom& g) {
+  const size_t cap = xd_send_cap(g) + 1, tab = (size_t)g.s.nt_s * g.G;
+  return 2 * al256(tab * 4) + al256((tab + g.s.nt_s) * 4) + al256(g.G * 4) + al256(cap * 4) + al256(cap * 8) +
+         al256(cap * 2) + al256(cap * 8);
+}
+
+void xd_carve_send(const XdGeom& g, void* base, XdBufs* b) {
+  const size_t cap = xd_send_cap(g) + 1, tab = (size_t)g.s.nt_s * g.G;
+  char* p = (char*)base;
+  auto take = [&](size_t bytes) {
+    char* r = p;
+    p += al256(bytes);
+    return r;
+  };
+  b->rcnt = (uint32_t*)take(tab * 4);
+  b->roff = (uint32_t*)take(tab * 4);
+  b->rlofs = (uint32_t*)take((tab + g.s.nt_s) * 4);
+  b->ocnt = (uint32_t*)take(g.G * 4);
+  b->sid = (uint32_t*)take(cap * 4);
+  b->sval = (uint64_t*)take(cap * 8);
+  b->snl = (uint16_t*)take(cap * 2);
+  b->rep_in = (uint64_t*)take(cap * 8);
+}
+
+namespace {
+uint32_t xd_regions(uint64_t cap_r) { return (uint32_t)((cap_r + kXdBinRegion - 1) / kXdBinRegion); }
+}  // namespace
+
+size_t xd_recv_bytes(const XdGeom& g, uint64_t cap_r) {
+  const uint32_t nr = xd_regions(cap_r) ? xd_regions(cap_r) : 1;
+  const size_t recs = (size_t)nr * kXdBinRegion, offs = (size_t)nr * (g.r.nt_d + 1);
+  return al256(recs * 4) + al256(recs * 8) + al256(recs * 4) + 3 * al256(recs * 8) + 2 * al256(offs * 2);
+}
+
+void xd_carve_recv(const XdGeom& g, uint64_t cap_r, void* base, XdBufs* b) {
+  const uint32_t nr = xd_regions(cap_r) ? xd_regions(cap_r) : 1;
+  const size_t recs = (size_t)nr * kXdBinRegion, offs = (size_t)nr * (g.r.nt_d + 1);
+  char* p = (char*)base;
+  auto take = [&](size_t bytes) {
+    char* r = p;
+    p += al256(bytes);
+    return r;
+  };
+  b->rid = (uint32_t*)take(recs * 4);
+  b->rval = (uint64_t*)take(recs * 8);
+  b->rb.ids = (uint32_t*)take(recs * 4);
+  b->rb.vals = (uint64_t*)take(recs * 8);
+  b->rb.resp = (uint64_t*)take(recs * 8);
+  b->rep_out = (uint64_t*)take(recs * 8);
+  b->rb.off = (uint16_t*)take(offs * 2);
+  b->rb.offT = (uint16_t*)take(offs * 2);
+  b->rb.nzb = b->rb.fullb = nullptr;
+}
+
+hipError_t launch_xd_requests(const XdGeom& g, const XdBufs& b, const uint64_t* S, uint32_t R, uint32_t t,
+                              uint32_t key0, uint32_t key1, uint32_t mode, const Faults& fa, hipStream_t st) {
+  if (g.nown == 0) return hipMemsetAsync(b.ocnt, 0, g.G * 4, st);
+  const uint32_t eg = g.s.nt_s < kEmitGrid ? g.s.nt_s : kEmitGrid;
+  if (fa.any()) xd_count_kernel<true><<<eg, kEmitThreads, 0, st>>>(g, S, b.rcnt, R, t, key0, key1, mode, fa);
+  else xd_count_kernel<false><<<eg, kEmitThreads, 0, st>>>(g, S, b.rcnt, R, t, key0, key1, mode, fa);
+  xd_scan_kernel<<<1, 1024, 0, st>>>(b.rcnt, b.roff, b.ocnt, g.s.nt_s, g.G);
+  if (fa.any()) xd_emit_kernel<true><<<eg, kEmitThreads, 0, st>>>(g, S, b, b.rlofs, R, t, key0, key1, mode, fa);
+  else xd_emit_kernel<false><<<eg, kEmitThreads, 0, st>>>(g, S, b, b.rlofs, R, t, key0, key1, mode, fa);
+  return hipGetLastError();
+}
+
+hipError_t launch_xd_serve(XdGeom g, const XdBufs& b, const uint64_t* S, uint64_t n_in, uint32_t R,
+                           hipStream_t st) {
+  g.r.nt_s = xd_regions(n_in);
+  if (g.r.nt_s == 0) return hipSuccess;
+  const uint32_t eg = g.r.nt_s < kEmitGrid ? g.r.nt_s : kEmitGrid;
+  xd_bin_kernel<<<eg, kEmitThreads, 0, st>>>(g, b, n_in);
+  const dim3 tg((g.r.nt_d + 1 + 31) / 32, (g.r.nt_s + 31) / 32);
+  transpose_u16_kernel<<<tg, dim3(32, 8), 0, st>>>(b.rb.off, b.rb.offT, g.r.nt_s, g.r.nt_d + 1, nullptr, 0u);
+  bin_serve_kernel<kXbVF><<<serve_grid(g.r.nt_d), kTileThreads, 0, st>>>(g.r, S, b.rb, R, IdxRange::all(g.r.nt_d));
+  // replies back to the received order in LDS (writing them there from serve, scattered,
+  // measured 4x slower: profiles/r02_xd)
+  xd_unperm_kernel<<<eg, kEmitThreads, 0, st>>>(g, b, n_in);
+  return hipGetLastError();
+}
+
+hipError_t launch_xd_apply(XdGeom g, const XdBufs& b, const uint64_t* S, uint64_t* Snext, uint64_t n_in,
+                           uint64_t* partial, uint32_t R, uint32_t mode, uint32_t flags, uint64_t* nzb,
+                           uint64_t* fullb, hipStream_t st) {
+  if (g.nown == 0) return hipSuccess;
+  g.r.nt_s = xd_regions(n_in);
+  const uint32_t grid = g.r.nt_d < kApplyGrid ? g.r.nt_d : kApplyGrid;
+  xd_apply_kernel<<<grid, kTileThreads, 0, st>>>(g, b, b.rlofs, S, Snext, partial, R, mode, flags, nzb, fullb);
+  return hipGetLastError();
 }
 
 }  // namespace gossip

@@ -116,7 +116,8 @@ struct gossip_engine {
   FrontierBufs fb{};
   void* fr_mem = nullptr;
   bool fr_valid = false;          // partial_d holds the totals of S and the bitmaps are exact
-  double sparse_frac = 1.0 / 16;  // rare fraction at or below which a round runs sparse
+  double sparse_frac = 1.0 / 16;  // rare fraction at or below which a round runs sparse (sparse_frac_of)
+  bool sparse_frac_set = false;   // set by gossip_set_param (else the sharded defaults apply)
   double filter_frac = 0.3;       // dense rounds filter edges by the peer's class above this empty / full fraction
   double alld_frac = 1.0 / 64;    // sparse rounds with k * rare >= alld_frac * N commit every group's D (bench sweep)
   // pipelined rounds (binned engines): the host picks each round's path from the
@@ -149,6 +150,14 @@ struct gossip_engine {
   bool ev_pre_pending = false;
   SxItem* msg_recv = nullptr;
   uint64_t rare_recv_cap = 0, msg_recv_cap = 0, sx_stride = 0;
+  // exchange dense rounds (binned.h: XdGeom), buffers allocated at the first one
+  bool xd = false, xd_planned = false;
+  uint32_t xd_shards = 6;  // gossip_set_param "xd_shards": G at which dense rounds become exchange rounds
+  XdGeom xg{};
+  XdBufs xb{};
+  void *xd_smem = nullptr, *xd_rmem = nullptr;
+  uint64_t xd_rcap = 0, xd_nin = 0;
+  uint32_t* xd_cnt_h = nullptr;  // pinned [G]
   uint64_t* sx_host = nullptr;  // pinned: [G + 2] counts / list bases
 
   hipEvent_t ev[kTimers][2] = {};
@@ -205,7 +214,8 @@ void free_all(gossip_engine* e) {
     if (b) (void)hipFree(b);
   if (e->bin_mem) (void)hipFree(e->bin_mem);
   if (e->fr_mem) (void)hipFree(e->fr_mem);
-  void* sx[] = {e->lf_mem, e->sx_mem, e->rare_recv, e->msg_recv, e->sb_mem};
+  void* sx[] = {e->lf_mem, e->sx_mem, e->rare_recv, e->msg_recv, e->sb_mem, e->xd_smem, e->xd_rmem};
+  if (e->xd_cnt_h) (void)hipHostFree(e->xd_cnt_h);
   for (void* b : sx)
     if (b) (void)hipFree(b);
   if (e->sx_host) (void)hipHostFree(e->sx_host);
@@ -415,6 +425,15 @@ Est predict(const gossip_engine* e, const Est& x) {
   return y;
 }
 
+// the sparse-round threshold: gossip_set_param's, else the default of the engine's dense
+// round kind — a sharded dense round that all-gathers the state costs more than an
+// exchange round, so sparse rounds pay off up to a larger rare fraction before it
+// (tools/shard_probe.py sweeps, profiles/r02_xd)
+double sparse_frac_of(const gossip_engine* e) {
+  if (e->sparse_frac_set || !e->sx) return e->sparse_frac;
+  return e->xd && e->xd_shards && e->G >= e->xd_shards ? 0.1 : 0.25;
+}
+
 // sparse when the smaller rare class is at most sparse_frac * N; maj = which
 // class is rare; all_d once the rare ends' pushes (~k per rare node) reach
 // alld_frac * N (launch_frontier_round)
@@ -423,7 +442,7 @@ bool choose_sparse(const gossip_engine* e, const Est& x, uint32_t* maj, bool* al
   const double lo = x.nz, hi = (double)e->N - x.full, rare = std::min(lo, hi);
   *maj = hi < lo ? 1u : 0u;
   *all_d = rare * (double)e->k >= e->alld_frac * (double)e->N;
-  return rare <= e->sparse_frac * (double)e->N;
+  return rare <= sparse_frac_of(e) * (double)e->N;
 }
 
 // dense rounds: probe the peer's class in emit when many edges would move
@@ -1034,10 +1053,15 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
       sb_carve(e->sbg, e->sb_mem, &e->sbb);
       e->sbin = true;
     }
-    // a dense sharded round all-gathers every shard's state (7/8 of the image per GPU at G = 8);
-    // a sparse one moves 16 B per rare node plus the cross-shard pushes, so sparse rounds pay
-    // off up to a larger rare fraction than on one GPU (tools/shard_probe.py)
-    e->sparse_frac = 0.25;
+    if (xd_path_ok(e->N, e->k, e->Nl, G)) {
+      e->xg = make_xd_geom(e->N, e->k, e->Nl, e->lo, e->nown, G, e->rank);
+      if (hipHostMalloc((void**)&e->xd_cnt_h, G * 4, hipHostMallocDefault) != hipSuccess) {
+        e->err = "hipHostMalloc failed";
+        return bail(GOSSIP_ENOMEM);
+      }
+      e->xd = true;
+    }
+    // sharded sparse rounds pay off up to a larger rare fraction than on one GPU: sparse_frac_of
   }
   if (hipHostMalloc((void**)&e->partial_h, part_len(e) * 8, hipHostMallocDefault) != hipSuccess) {
     e->err = "hipHostMalloc failed";
@@ -1098,6 +1122,7 @@ int gossip_set_param(gossip_engine_t* e, const char* name, double v) {
   const std::string n(name);
   if (n == "sparse_frac") {
     e->sparse_frac = v;
+    e->sparse_frac_set = true;
   } else if (n == "alld_frac") {
     e->alld_frac = v;
   } else if (n == "filter_frac") {
@@ -1108,6 +1133,9 @@ int gossip_set_param(gossip_engine_t* e, const char* name, double v) {
   } else if (n == "apply_grid") {
     if (v < 0 || v > 65536) return e->fail(GOSSIP_EINVAL, "apply_grid must be in [0, 65536]");
     e->bg.apply_grid = e->sbg.p.apply_grid = (uint32_t)v;
+  } else if (n == "xd_shards") {
+    if (v < 0 || v > 1024) return e->fail(GOSSIP_EINVAL, "xd_shards must be in [0, 1024] (0 = never)");
+    e->xd_shards = (uint32_t)v;
   } else if (n == "ae_sparse") {
     if (v != -1 && v != 0 && v != 1) return e->fail(GOSSIP_EINVAL, "ae_sparse must be -1, 0 or 1");
     e->ae_force = (int)v;
@@ -1406,7 +1434,7 @@ int gossip_local_totals(gossip_engine_t* e, uint64_t* partial) {
 
 int gossip_sharded_plan(gossip_engine_t* e, const uint64_t* total, int32_t* kind) {
   if (!e || !kind) return GOSSIP_EINVAL;
-  e->sx_planned = false;
+  e->sx_planned = e->xd_planned = false;
   if (e->aex) {  // 2: an anti-entropy exchange round; -2: the global max vector is needed first
     *kind = e->aex_target_ok ? 2 : -2;
     return GOSSIP_OK;
@@ -1428,7 +1456,8 @@ int gossip_sharded_plan(gossip_engine_t* e, const uint64_t* total, int32_t* kind
   e->sx_planned = choose_sparse(e, est_of(e, e->gtot.data()), &maj, &all_d);
   e->sx_maj = maj;
   e->sx_alld = all_d;
-  *kind = e->sx_planned ? 1 : 0;
+  e->xd_planned = !e->sx_planned && e->xd && e->xd_shards && e->G >= e->xd_shards;
+  *kind = e->sx_planned ? 1 : e->xd_planned ? 3 : 0;
   return GOSSIP_OK;
 }
 
@@ -1501,6 +1530,96 @@ int gossip_sparse_commit(gossip_engine_t* e, uint64_t items, uint64_t* partial) 
   if (int rc = timer_collect(e)) return rc;
   e->sx_planned = false;
   e->last_sparse = true;
+  return GOSSIP_OK;
+}
+
+// --- exchange dense rounds (include/gossip.h) -----------------------
+
+namespace {
+int xd_check(gossip_engine* e) {
+  if (!e) return GOSSIP_EINVAL;
+  if (!e->xd) return e->fail(GOSSIP_ENOTSUP, "exchange dense rounds need G > 1, W == 1 and a random mode");
+  if (!e->xd_planned) return e->fail(GOSSIP_ESTATE, "gossip_sharded_plan did not plan an exchange round");
+  return set_dev(e);
+}
+}  // namespace
+
+int gossip_xd_requests(gossip_engine_t* e, void** ids, void** vals, uint64_t* send_counts) {
+  if (!ids || !vals || !send_counts) return GOSSIP_EINVAL;
+  if (int rc = xd_check(e)) return rc;
+  if (!e->xd_smem) {
+    const size_t bytes = xd_send_bytes(e->xg);
+    if (hipMalloc(&e->xd_smem, bytes) != hipSuccess) {
+      e->xd_smem = nullptr;
+      return e->fail(GOSSIP_ENOMEM, "hipMalloc of %zu bytes (exchange send buffers) failed", bytes);
+    }
+    xd_carve_send(e->xg, e->xd_smem, &e->xb);
+  }
+  HIP_OK(e, hipMemsetAsync(e->partial_d, 0, part_len(e) * 8, e->stream));
+  if (int rc = timer_begin(e, 0)) return rc;
+  HIP_OK(e, launch_xd_requests(e->xg, e->xb, e->S, e->R, e->t, e->key0, e->key1, e->mode, e->fa, e->stream));
+  HIP_OK(e, hipMemcpyAsync(e->xd_cnt_h, e->xb.ocnt, e->G * 4, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(e, hipStreamSynchronize(e->stream));
+  for (uint32_t q = 0; q < e->G; ++q) send_counts[q] = e->xd_cnt_h[q];
+  *ids = e->xb.sid;
+  *vals = e->xb.sval;
+  return GOSSIP_OK;
+}
+
+int gossip_xd_request_recv(gossip_engine_t* e, uint64_t items, void** ids, void** vals) {
+  if (!ids || !vals) return GOSSIP_EINVAL;
+  if (int rc = xd_check(e)) return rc;
+  if (items >= (1ull << 31)) return e->fail(GOSSIP_EINVAL, "%llu items exceed one exchange round", (unsigned long long)items);
+  if (!e->xd_rmem || items > e->xd_rcap) {
+    HIP_OK(e, hipStreamSynchronize(e->stream));
+    if (e->xd_rmem) HIP_OK(e, hipFree(e->xd_rmem));
+    e->xd_rmem = nullptr;
+    e->xd_rcap = 0;
+    const uint64_t want = std::min<uint64_t>(std::max<uint64_t>(items + items / 4, kXdBinRegion), (1ull << 31) - 1);
+    const size_t bytes = xd_recv_bytes(e->xg, want);
+    if (hipMalloc(&e->xd_rmem, bytes) != hipSuccess) {
+      e->xd_rmem = nullptr;
+      return e->fail(GOSSIP_ENOMEM, "hipMalloc of %zu bytes (exchange receive buffers) failed", bytes);
+    }
+    xd_carve_recv(e->xg, want, e->xd_rmem, &e->xb);
+    e->xd_rcap = want;
+  }
+  e->xd_nin = items;
+  *ids = e->xb.rid;
+  *vals = e->xb.rval;
+  return GOSSIP_OK;
+}
+
+int gossip_xd_serve(gossip_engine_t* e, void** replies) {
+  if (!replies) return GOSSIP_EINVAL;
+  if (int rc = xd_check(e)) return rc;
+  if (!e->xd_rmem) return e->fail(GOSSIP_ESTATE, "gossip_xd_request_recv first");
+  HIP_OK(e, launch_xd_serve(e->xg, e->xb, e->S, e->xd_nin, e->R, e->stream));
+  HIP_OK(e, hipStreamSynchronize(e->stream));
+  *replies = e->xb.rep_out;
+  return GOSSIP_OK;
+}
+
+int gossip_xd_response_recv(gossip_engine_t* e, void** replies) {
+  if (!replies) return GOSSIP_EINVAL;
+  if (int rc = xd_check(e)) return rc;
+  if (!e->xd_smem) return e->fail(GOSSIP_ESTATE, "gossip_xd_requests first");
+  *replies = e->xb.rep_in;  // room for every own item (k x nown)
+  return GOSSIP_OK;
+}
+
+int gossip_xd_finish(gossip_engine_t* e, uint64_t* partial) {
+  if (!partial) return GOSSIP_EINVAL;
+  if (int rc = xd_check(e)) return rc;
+  if (!e->xd_smem || !e->xd_rmem) return e->fail(GOSSIP_ESTATE, "gossip_xd_finish before the exchange");
+  HIP_OK(e, launch_xd_apply(e->xg, e->xb, e->S, e->Snext, e->xd_nin, e->partial_d, e->R, e->mode, e->cfg.flags,
+                            e->lf.nzb, e->lf.fullb, e->stream));
+  if (int rc = timer_end(e, 0)) return rc;
+  if (int rc = copy_partial_out(e, partial)) return rc;
+  if (int rc = timer_collect(e)) return rc;
+  e->sx_valid = true;  // totals of the own nodes and exact bitmaps of S_{t+1}, fused into the apply
+  e->xd_planned = false;
+  e->last_sparse = false;
   return GOSSIP_OK;
 }
 

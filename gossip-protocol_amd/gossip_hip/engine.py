@@ -327,6 +327,34 @@ class AbiEngine:
         self._check(self._fn("ae_finish")(self._h, out.ctypes.data_as(_abi.U64P)))
         return out
 
+    # -- exchange dense rounds (include/gossip.h gossip_xd_*; gossip_hip.sharded drives them) --
+    def xd_requests(self):
+        """(ids pointer, values pointer, items per owner) of this round's items (uint32 ids, uint64 values)."""
+        ids, vals = C.c_void_p(), C.c_void_p()
+        out = np.zeros(self.cfg.shard_count, dtype=np.uint64)
+        self._check(self._fn("xd_requests")(self._h, C.byref(ids), C.byref(vals), out.ctypes.data_as(_abi.U64P)))
+        return ids.value, vals.value, [int(x) for x in out]
+
+    def xd_request_recv(self, items: int):
+        ids, vals = C.c_void_p(), C.c_void_p()
+        self._check(self._fn("xd_request_recv")(self._h, C.c_uint64(items), C.byref(ids), C.byref(vals)))
+        return ids.value, vals.value
+
+    def xd_serve(self) -> int:
+        ptr = C.c_void_p()
+        self._check(self._fn("xd_serve")(self._h, C.byref(ptr)))
+        return ptr.value
+
+    def xd_response_recv(self) -> int:
+        ptr = C.c_void_p()
+        self._check(self._fn("xd_response_recv")(self._h, C.byref(ptr)))
+        return ptr.value
+
+    def xd_finish(self) -> np.ndarray:
+        out = np.zeros(self.partial_len(), dtype=np.uint64)
+        self._check(self._fn("xd_finish")(self._h, out.ctypes.data_as(_abi.U64P)))
+        return out
+
     def sparse_commit(self, items: int) -> np.ndarray:
         out = np.zeros(self.partial_len(), dtype=np.uint64)
         self._check(self._fn("sparse_commit")(self._h, items, out.ctypes.data_as(_abi.U64P)))

@@ -12,6 +12,10 @@ without a GPU):
   sparse round  (the engine's plan, when one class of nodes is rare) all-gather
                 of each shard's rare nodes {id, value}, all-to-all of the pushes
                 that land on another shard, all-reduce of the partials;
+  exchange      (kind 3, DESIGN.md §5.2: dense rounds at G >= the "xd_shards" param) no
+                image: all-to-all of one item per live edge {p at its owner | flags,
+                S_t[n]} to p's owner, all-to-all of the pull replies back, all-reduce of
+                the partials;
   ANTIENTROPY   ("Design B") all-gather of the stale bits,
                 all-to-all of request items {p, n, V_t[n]} to p's owner and of its
                 replies V_t[p], all-reduce of the partials; the global max vector
@@ -34,19 +38,22 @@ ITEM_WORDS = 2  # sparse exchange items are {uint64 node, uint64 value}
 class _DevPtr:
     """Zero-copy view of engine-owned device memory for torch collectives."""
 
-    def __init__(self, ptr: int, nbytes: int):
+    def __init__(self, ptr: int, nbytes: int, width: int = 8):
         self.__cuda_array_interface__ = {
-            "shape": (nbytes // 8,), "typestr": "<i8", "data": (ptr, False), "version": 3, "strides": None,
+            "shape": (nbytes // width,), "typestr": f"<i{width}", "data": (ptr, False), "version": 3, "strides": None,
         }
 
 
-def _as_tensor(ptr: int, nbytes: int, on_device: bool, device: int | None = None) -> torch.Tensor:
+def _as_tensor(ptr: int, nbytes: int, on_device: bool, device: int | None = None, width: int = 8) -> torch.Tensor:
+    """int64 (width 8) or int32 (width 4) view of nbytes at ptr."""
     dev = torch.device("cuda", torch.cuda.current_device() if device is None else device) if on_device else "cpu"
+    dt = torch.int64 if width == 8 else torch.int32
     if nbytes == 0:
-        return torch.empty(0, dtype=torch.int64, device=dev)
+        return torch.empty(0, dtype=dt, device=dev)
     if on_device:
-        return torch.as_tensor(_DevPtr(ptr, nbytes), device=dev)
-    arr = np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_int64)), shape=(nbytes // 8,))
+        return torch.as_tensor(_DevPtr(ptr, nbytes, width), device=dev)
+    arr = np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_int64 if width == 8 else C.c_int32)),
+                                shape=(nbytes // width,))
     return torch.from_numpy(arr)
 
 
@@ -90,7 +97,7 @@ class _Comm:
             dist.all_to_all_single(recv, send, output_split_sizes=recv_splits, input_split_sizes=send_splits,
                                    group=self.group)
             return
-        host = torch.empty(recv.numel(), dtype=torch.int64)
+        host = torch.empty(recv.numel(), dtype=recv.dtype)
         dist.all_to_all_single(host, send.cpu() if self.on_device else send.clone(), output_split_sizes=recv_splits,
                                input_split_sizes=send_splits, group=self.group)
         recv.copy_(host)
@@ -163,11 +170,33 @@ def _sparse_round(engine, comm: _Comm) -> np.ndarray:
     in_counts = comm.all_to_all_small(out_counts)
     n_in = sum(in_counts)
     in_p = engine.sparse_msg_recv(n_in)
-    if sum(out_counts) or n_in:
-        comm.all_to_all(_as_tensor(in_p, n_in * 16, engine.on_device),
-                        _as_tensor(out_p, sum(out_counts) * 16, engine.on_device),
-                        [c * ITEM_WORDS for c in in_counts], [c * ITEM_WORDS for c in out_counts])
+    # every rank joins the collective, also one with nothing to send or receive (G > 2)
+    comm.all_to_all(_as_tensor(in_p, n_in * 16, engine.on_device),
+                    _as_tensor(out_p, sum(out_counts) * 16, engine.on_device),
+                    [c * ITEM_WORDS for c in in_counts], [c * ITEM_WORDS for c in out_counts])
     return engine.sparse_commit(n_in)
+
+
+def _xd_round(engine, comm: _Comm) -> np.ndarray:
+    ids_p, vals_p, counts = engine.xd_requests()
+    in_counts = comm.all_to_all_small(counts) if comm.world > 1 else counts
+    n_in, n_out = sum(in_counts), sum(counts)
+    rid_p, rval_p = engine.xd_request_recv(n_in)
+    dev = engine.on_device
+    if comm.world > 1:
+        comm.all_to_all(_as_tensor(rid_p, n_in * 4, dev, width=4), _as_tensor(ids_p, n_out * 4, dev, width=4),
+                        in_counts, counts)
+        comm.all_to_all(_as_tensor(rval_p, n_in * 8, dev), _as_tensor(vals_p, n_out * 8, dev), in_counts, counts)
+    else:
+        _as_tensor(rid_p, n_in * 4, dev, width=4).copy_(_as_tensor(ids_p, n_out * 4, dev, width=4))
+        _as_tensor(rval_p, n_in * 8, dev).copy_(_as_tensor(vals_p, n_out * 8, dev))
+    rep_p = engine.xd_serve()  # replies in the received order
+    back_p = engine.xd_response_recv()
+    if comm.world > 1:
+        comm.all_to_all(_as_tensor(back_p, n_out * 8, dev), _as_tensor(rep_p, n_in * 8, dev), counts, in_counts)
+    else:
+        _as_tensor(back_p, n_out * 8, dev).copy_(_as_tensor(rep_p, n_in * 8, dev))
+    return engine.xd_finish()
 
 
 def _bind_stream(engine, comm: _Comm):
@@ -190,13 +219,13 @@ def _ae_round(engine, comm: _Comm) -> np.ndarray:
     in_counts = comm.all_to_all_small(counts) if w > 1 else counts
     n_in = sum(in_counts)
     in_p = engine.ae_request_recv(n_in)
-    if sum(counts) or n_in:
+    if w > 1:  # (every rank joins, also one with nothing to send or receive)
         comm.all_to_all(_as_tensor(in_p, n_in * rw * 4, engine.on_device),
                         _as_tensor(req_p, sum(counts) * rw * 4, engine.on_device),
                         [c * rw // 2 for c in in_counts], [c * rw // 2 for c in counts])
     resp_p = engine.ae_serve()  # replies in the received order
     back_p = engine.ae_response_recv()
-    if sum(counts) or n_in:
+    if w > 1:
         comm.all_to_all(_as_tensor(back_p, sum(counts) * pw * 4, engine.on_device),
                         _as_tensor(resp_p, n_in * pw * 4, engine.on_device),
                         [c * pw // 2 for c in counts], [c * pw // 2 for c in in_counts])
@@ -212,6 +241,8 @@ def sharded_round(engine, group=None) -> dict:
     kind = _plan(engine, comm)
     if kind == 2:
         partial = _ae_round(engine, comm)
+    elif kind == 3:
+        partial = _xd_round(engine, comm)
     elif kind == 1:
         partial = _sparse_round(engine, comm)
     else:
@@ -332,10 +363,43 @@ def _lockstep_ae(engines):
     return [e.ae_finish() for e in engines]
 
 
+def _lockstep_xd(engines):
+    G = len(engines)
+    reqs = [e.xd_requests() for e in engines]  # (ids, vals, counts[owner])
+    n_in = [sum(reqs[q][2][r] for q in range(G)) for r in range(G)]
+    inbox = [e.xd_request_recv(n) for e, n in zip(engines, n_in)]
+    for r in range(G):  # all-to-all: owner r receives from q = 0..G-1 in order
+        di = _as_tensor(inbox[r][0], n_in[r] * 4, True, engines[r].device, width=4)
+        dv = _as_tensor(inbox[r][1], n_in[r] * 8, True, engines[r].device)
+        at = 0
+        for q, (ip, vp, cnt) in enumerate(reqs):
+            if cnt[r]:
+                off, tot = sum(cnt[:r]), sum(cnt)
+                si = _as_tensor(ip, tot * 4, True, engines[q].device, width=4)
+                sv = _as_tensor(vp, tot * 8, True, engines[q].device)
+                di[at:at + cnt[r]].copy_(si[off:off + cnt[r]])
+                dv[at:at + cnt[r]].copy_(sv[off:off + cnt[r]])
+                at += cnt[r]
+    _sync_all(engines)
+    reps = [e.xd_serve() for e in engines]
+    back = [e.xd_response_recv() for e in engines]
+    for q, (_, _, cnt) in enumerate(reqs):  # replies return to q in its send order
+        dst = _as_tensor(back[q], sum(cnt) * 8, True, engines[q].device)
+        at = 0
+        for r in range(G):
+            if cnt[r]:
+                src = _as_tensor(reps[r], n_in[r] * 8, True, engines[r].device)
+                start = sum(reqs[q2][2][r] for q2 in range(q))  # where q's items landed in r's inbox
+                dst[at:at + cnt[r]].copy_(src[start:start + cnt[r]])
+                at += cnt[r]
+    _sync_all(engines)
+    return [e.xd_finish() for e in engines]
+
+
 def lockstep_run(engines, max_rounds: int):
     """One process driving G shard engines (one per GPU, or several on one) through the
     same rounds as sharded_run, with device copies in place of the collectives.
-    Returns (per-round stats, per-round kind: 0 dense / 1 sparse)."""
+    Returns (per-round stats, per-round kind: 0 dense / 1 sparse / 2 ANTIENTROPY / 3 exchange dense)."""
     stats, kinds = [], []
     for _ in range(max_rounds):
         ks = [e.sharded_plan() for e in engines]
@@ -349,8 +413,8 @@ def lockstep_run(engines, max_rounds: int):
             ks = [e.sharded_plan(tot) for e in engines]
         assert len(set(ks)) == 1
         kinds.append(ks[0])
-        parts = (_lockstep_ae(engines) if ks[0] == 2 else _lockstep_sparse(engines) if ks[0] == 1
-                 else _lockstep_dense(engines))
+        parts = (_lockstep_ae(engines) if ks[0] == 2 else _lockstep_xd(engines) if ks[0] == 3
+                 else _lockstep_sparse(engines) if ks[0] == 1 else _lockstep_dense(engines))
         tot = _lockstep_sum(parts)
         st = [e.round_commit(tot) for e in engines]
         assert all(s == st[0] for s in st)

@@ -36,7 +36,7 @@ import (
 )
 
 // ABIVersion is the gossip.h version this binding is written against.
-const ABIVersion = 4
+const ABIVersion = 5
 
 // Mode is a dissemination rule (DESIGN.md §2).
 type Mode uint32
@@ -59,6 +59,12 @@ const (
 	FlagDense        Flags = Flags(C.GOSSIP_FLAG_DENSE)
 	FlagShardDirect  Flags = Flags(C.GOSSIP_FLAG_SHARD_DIRECT)
 	FlagAEDirectScan Flags = Flags(C.GOSSIP_FLAG_AE_DIRECT_SCAN)
+)
+
+// Exchange dense round item id flags (gossip_xd_requests).
+const (
+	XDNoPush uint32 = uint32(C.GOSSIP_XD_NO_PUSH)
+	XDNoPull uint32 = uint32(C.GOSSIP_XD_NO_PULL)
 )
 
 // Config mirrors gossip_config_t.  Probabilities are thresholds x / 2^32 (Threshold).
@@ -564,4 +570,48 @@ func (e *Engine) AEResponseRecv() (uintptr, error) {
 func (e *Engine) AEFinish() ([]uint64, error) {
 	out := make([]uint64, e.PartialLen())
 	return out, e.call(C.gossip_ae_finish(e.h, u64p(out)))
+}
+
+// XDRequests: the items of an exchange dense round (plan kind 3) grouped by owner: ids (uint32,
+// p at its owner | XDNoPush / XDNoPull) and values (uint64), two device arrays.
+func (e *Engine) XDRequests() (ids, vals uintptr, counts []uint64, err error) {
+	var i, v unsafe.Pointer
+	counts = make([]uint64, e.cfg.ShardCount)
+	if rc := C.gossip_xd_requests(e.h, &i, &v, u64p(counts)); rc != 0 {
+		return 0, 0, nil, e.fail(rc)
+	}
+	return uintptr(i), uintptr(v), counts, nil
+}
+
+// XDRequestRecv: room for the incoming items (ids and values).
+func (e *Engine) XDRequestRecv(items uint64) (ids, vals uintptr, err error) {
+	var i, v unsafe.Pointer
+	if rc := C.gossip_xd_request_recv(e.h, C.uint64_t(items), &i, &v); rc != 0 {
+		return 0, 0, e.fail(rc)
+	}
+	return uintptr(i), uintptr(v), nil
+}
+
+// XDServe applies the received pushes and returns the pull replies (received order).
+func (e *Engine) XDServe() (uintptr, error) {
+	var s unsafe.Pointer
+	if rc := C.gossip_xd_serve(e.h, &s); rc != 0 {
+		return 0, e.fail(rc)
+	}
+	return uintptr(s), nil
+}
+
+// XDResponseRecv: room for the replies to the own items (send order).
+func (e *Engine) XDResponseRecv() (uintptr, error) {
+	var r unsafe.Pointer
+	if rc := C.gossip_xd_response_recv(e.h, &r); rc != 0 {
+		return 0, e.fail(rc)
+	}
+	return uintptr(r), nil
+}
+
+// XDFinish merges the replies and returns the round's partial stats.
+func (e *Engine) XDFinish() ([]uint64, error) {
+	out := make([]uint64, e.PartialLen())
+	return out, e.call(C.gossip_xd_finish(e.h, u64p(out)))
 }

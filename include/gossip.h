@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define GOSSIP_ABI_VERSION 4u
+#define GOSSIP_ABI_VERSION 5u
 
 /* Dissemination modes. */
 enum gossip_mode {
@@ -129,13 +129,16 @@ int gossip_set_stream(gossip_engine_t* eng, void* hip_stream);
 /* Tuning and path-selection knobs, for tests and benchmarks (the library reads no
  * environment variables).  Every value only moves time, never a result bit:
  *   "sparse_frac"  random modes: a round runs sparse when the rare class is at most
- *                  this fraction of N (default 1/16, sharded 1/4; < 0 never, >= 1 always)
+ *                  this fraction of N (default 1/16; sharded 1/4, or 1/10 when the dense
+ *                  rounds are exchange rounds; < 0 never, >= 1 always)
  *   "alld_frac"    sparse rounds commit every group's D once k x rare >= this x N
  *   "filter_frac"  dense rounds drop edges by the peer's class above this empty/full fraction
  *   "ahead"        rounds enqueued ahead of the stats read back (1..7, default 2)
  *   "apply_grid"   persistent blocks of the dense apply pass (0 = one block per tile)
  *   "ae_sparse"    ANTIENTROPY: -1 plan sparse rounds (default), 0 never, 1 whenever valid
  *   "ae_cap"       ANTIENTROPY: edge-list capacity of sparse rounds (reallocates the list)
+ *   "xd_shards"    sharded random modes: dense rounds run as exchange rounds (kind 3) when
+ *                  G >= this (default 6; 0 = never, always the state all-gather)
  * Unknown names return GOSSIP_EINVAL. */
 int gossip_set_param(gossip_engine_t* eng, const char* name, double value);
 
@@ -193,6 +196,7 @@ int gossip_round_commit(gossip_engine_t* eng, const uint64_t* total, gossip_roun
  *   kind -1: no global totals yet -> gossip_local_totals, all-reduce(SUM),
  *            plan again with the sum;
  *   kind  0: dense round -> the exchange_buffers / round_compute sequence;
+ *   kind  3: exchange dense round (no state image; see the gossip_xd_* calls below);
  *   kind  1: sparse round:
  *     gossip_sparse_rare(&send, &count)        own rare nodes, 16-B items {node, value}
  *     all-gather of count, stride = max count
@@ -238,6 +242,27 @@ int gossip_ae_request_recv(gossip_engine_t* eng, uint64_t items, void** recv);
 int gossip_ae_serve(gossip_engine_t* eng, void** send);
 int gossip_ae_response_recv(gossip_engine_t* eng, void** recv);
 int gossip_ae_finish(gossip_engine_t* eng, uint64_t* partial);
+
+/* --- exchange dense rounds (random modes, W == 1, G > 1) --------------
+ * A dense round without the state all-gather.  Every live edge n -> p_j(n,t) of an own
+ * sender becomes one item for p's owner: id = (p - owner * Nl) | GOSSIP_XD_NO_PUSH /
+ * GOSSIP_XD_NO_PULL flags (uint32) and S_t[n] (uint64, 0 without a push), in two arrays.
+ * The owner ORs the pushes into S_{t+1}[p] and answers each pull with S_t[p] (uint64, in
+ * the received order); the sender's owner ORs the replies into S_{t+1}[n].
+ * Per round, after gossip_sharded_plan -> kind 3:
+ *   gossip_xd_requests(&ids, &vals, send_counts[G])   items grouped by owner
+ *   all-to-all of the counts; gossip_xd_request_recv(total_in, &ids, &vals);
+ *   all-to-all of the ids (uint32) and of the values (uint64)
+ *   gossip_xd_serve(&replies)                          total_in replies, received order
+ *   gossip_xd_response_recv(&replies); all-to-all back (the counts swapped)
+ *   gossip_xd_finish(partial)                          -> all-reduce(SUM) -> gossip_round_commit */
+#define GOSSIP_XD_NO_PUSH (1u << 30)
+#define GOSSIP_XD_NO_PULL (1u << 31)
+int gossip_xd_requests(gossip_engine_t* eng, void** ids, void** vals, uint64_t* send_counts);
+int gossip_xd_request_recv(gossip_engine_t* eng, uint64_t items, void** ids, void** vals);
+int gossip_xd_serve(gossip_engine_t* eng, void** replies);
+int gossip_xd_response_recv(gossip_engine_t* eng, void** replies);
+int gossip_xd_finish(gossip_engine_t* eng, uint64_t* partial);
 
 /* Readout ("read" handler, main.go:123-130).  Bitset of one node (nwords >= W),
  * or the whole owned shard in logical order out[w * Nl_owned + i]. */

@@ -64,6 +64,13 @@ struct oracle_sim {
   uint64_t* aex_stale;
   uint32_t *req, *loc, *in, *resp_out, *resp_in;
   uint64_t nreq, nloc, nin, in_cap, aex_msgs;
+  /* exchange dense rounds (kind 3): items {p at owner | flags, S_t[n]} by owner;
+   * xnode = the own sender of each send item; replies in send / received order */
+  int xd_planned, sparse_frac_set;
+  uint32_t xd_shards;
+  uint32_t *xid, *xrid;
+  uint64_t *xval, *xrval, *xrep_out, *xrep_in, *xnode;
+  uint64_t xn_out, xn_in;
 };
 
 /* ---------------- Philox4x32-10 (Random123; rocRAND philox4x32_10.h:270-302) ---- */
@@ -221,6 +228,7 @@ int oracle_create(const gossip_config_t* cfg, int threads, oracle_sim_t** out) {
   s->gtot = (uint64_t*)calloc(5 + s->R, 8);
   s->counts = (uint64_t*)calloc(G, 8);
   s->sparse_frac = 0.25;
+  s->xd_shards = 6;
   s->flood_edges = s->mode == GOSSIP_MODE_FLOOD && faulty;
   s->npend = cfg->stall_rounds > 1 ? cfg->stall_rounds - 1 : 1;
   if (cfg->stall_rounds && s->mode >= GOSSIP_MODE_PUSH && s->mode <= GOSSIP_MODE_PUSHPULL &&
@@ -245,6 +253,7 @@ void oracle_destroy(oracle_sim_t* s) {
   free(s->D);
   free(s->streak); free(s->pend); free(s->pend_n); free(s->skipE); free(s->skipE_n); free(s->ieo);
   free(s->aex_stale); free(s->req); free(s->loc); free(s->in); free(s->resp_out); free(s->resp_in);
+  free(s->xid); free(s->xrid); free(s->xval); free(s->xrval); free(s->xrep_out); free(s->xrep_in); free(s->xnode);
   free(s);
 }
 
@@ -741,12 +750,12 @@ static int sparse_ok(const oracle_sim_t* s) {
 /* rare under maj: 0 -> nonzero, 1 -> not full (one word: W == 1) */
 static inline int is_rare(const oracle_sim_t* s, uint64_t x) { return s->maj ? x != s->fullm[0] : x != 0; }
 
-/* totals of the owned nodes' S (same layout as round_compute) */
-static void own_totals(const oracle_sim_t* s, uint64_t* partial) {
+/* totals of the owned nodes' state X (same layout as round_compute) */
+static void totals_of(const oracle_sim_t* s, const uint64_t* X, uint64_t* partial) {
   memset(partial, 0, oracle_partial_len(s) * 8);
   const int do_hash = (s->cfg.flags & GOSSIP_FLAG_HASH) != 0;
   for (uint64_t i = 0; i < s->nown; ++i) {
-    uint64_t x = s->S[i];
+    uint64_t x = X[i];
     partial[0] += (x & s->fullm[0]) == s->fullm[0];
     partial[4 + s->R] += x != 0;
     if (x && do_hash) partial[3] += oracle_mix64(x + (s->lo + i) * GOLD64);
@@ -758,6 +767,8 @@ static void own_totals(const oracle_sim_t* s, uint64_t* partial) {
   partial[1] = s->nown;
 }
 
+static void own_totals(const oracle_sim_t* s, uint64_t* partial) { totals_of(s, s->S, partial); }
+
 int oracle_local_totals(oracle_sim_t* s, uint64_t* partial) {
   if (!s || !partial || !sparse_ok(s)) return GOSSIP_EINVAL;
   own_totals(s, partial);
@@ -766,7 +777,7 @@ int oracle_local_totals(oracle_sim_t* s, uint64_t* partial) {
 
 int oracle_sharded_plan(oracle_sim_t* s, const uint64_t* total, int32_t* kind) {
   if (!s || !kind) return GOSSIP_EINVAL;
-  s->planned = 0;
+  s->planned = s->xd_planned = 0;
   if (s->aex) {
     *kind = s->aex_target_ok ? 2 : -2;
     return GOSSIP_OK;
@@ -785,8 +796,11 @@ int oracle_sharded_plan(oracle_sim_t* s, const uint64_t* total, int32_t* kind) {
   }
   const double nz = (double)s->gtot[4 + s->R], notfull = (double)s->N - (double)s->gtot[0];
   s->maj = notfull < nz;
-  s->planned = (notfull < nz ? notfull : nz) <= s->sparse_frac * (double)s->N;
-  *kind = s->planned;
+  /* the engine's default threshold (engine.hip sparse_frac_of): 1/10 before exchange rounds */
+  const double frac = s->sparse_frac_set ? s->sparse_frac : s->xd_shards && s->G >= s->xd_shards ? 0.1 : 0.25;
+  s->planned = (notfull < nz ? notfull : nz) <= frac * (double)s->N;
+  s->xd_planned = !s->planned && s->xd_shards && s->G >= s->xd_shards;
+  *kind = s->planned ? 1 : s->xd_planned ? 3 : 0;
   return GOSSIP_OK;
 }
 
@@ -922,6 +936,109 @@ int oracle_sparse_commit(oracle_sim_t* s, uint64_t items, uint64_t* partial) {
   return GOSSIP_OK;
 }
 
+/* ---------------- exchange dense rounds (include/gossip.h gossip_xd_*) ----
+ * Each live edge n -> p of an own sender is one item for p's owner: id = (p - owner*Nl) |
+ * NO_PUSH / NO_PULL, value = S_t[n] (0 without a push) — the directions as the engine's
+ * sender_dirs (a push needs S_t[n] != 0, a pull S_t[n] != full).  The owner ORs pushes into
+ * S_{t+1}[p] and replies S_t[p] to pulls in the received order; the replies are ORed into
+ * S_{t+1}[n].  (main.go:65-89: each exchange is one request and its reply.) */
+#define XD_NO_PUSH (1u << 30)
+#define XD_NO_PULL (1u << 31)
+
+int oracle_xd_requests(oracle_sim_t* s, void** ids, void** vals, uint64_t* send_counts) {
+  if (!s || !ids || !vals || !send_counts || !s->xd_planned) return GOSSIP_ESTATE;
+  const uint64_t cap = (uint64_t)s->k * s->nown + 1;
+  if (!s->xid && !(s->xid = (uint32_t*)calloc(cap, 4))) return GOSSIP_ENOMEM;
+  if (!s->xval && !(s->xval = (uint64_t*)calloc(cap, 8))) return GOSSIP_ENOMEM;
+  if (!s->xnode && !(s->xnode = (uint64_t*)calloc(cap, 8))) return GOSSIP_ENOMEM;
+  if (!s->xrep_in && !(s->xrep_in = (uint64_t*)calloc(cap, 8))) return GOSSIP_ENOMEM;
+  const uint32_t key[2] = {(uint32_t)s->cfg.seed, (uint32_t)(s->cfg.seed >> 32)};
+  const int can_push = s->mode != GOSSIP_MODE_PULL, can_pull = s->mode != GOSSIP_MODE_PUSH;
+  memcpy(s->Snext, s->S, s->Nl * 8); /* S_{t+1} starts as S_t */
+  uint64_t* pos = (uint64_t*)calloc(s->G + 1, 8);
+  if (!pos) return GOSSIP_ENOMEM;
+  for (int pass = 0; pass < 2; ++pass) { /* count per owner, then place (owner-major, sender order) */
+    if (pass == 1)
+      for (uint32_t q = 0, a = 0; q <= s->G; ++q) {
+        const uint64_t c = q < s->G ? pos[q] : 0;
+        if (q < s->G) send_counts[q] = c;
+        pos[q] = a;
+        a += (uint32_t)c;
+      }
+    for (uint64_t i = 0; i < s->nown; ++i) {
+      const uint32_t n = (uint32_t)(s->lo + i);
+      const uint64_t x = s->S[i];
+      const int push = can_push && x != 0, pull = can_pull && x != s->fullm[0];
+      if (!push && !pull) continue;
+      uint32_t r[4] = {0, 0, 0, 0};
+      for (uint32_t j = 0; j < s->k; ++j) {
+        if ((j & 3) == 0) {
+          uint32_t ctr[4] = {n, s->t, 0u, j >> 2};
+          oracle_philox4x32_10(ctr, key, r);
+        }
+        const uint32_t p = peer_from_word(r[j & 3], s->N, n);
+        if (lost_edge(s, n, p, j, key)) continue;
+        const uint64_t q = p / s->Nl;
+        if (pass == 0) {
+          pos[q]++;
+          continue;
+        }
+        const uint64_t at = pos[q]++;
+        s->xid[at] = (uint32_t)(p - q * s->Nl) | (push ? 0u : XD_NO_PUSH) | (pull ? 0u : XD_NO_PULL);
+        s->xval[at] = push ? x : 0;
+        s->xnode[at] = i;
+      }
+    }
+  }
+  s->xn_out = 0;
+  for (uint32_t q = 0; q < s->G; ++q) s->xn_out += send_counts[q];
+  free(pos);
+  *ids = s->xid;
+  *vals = s->xval;
+  return GOSSIP_OK;
+}
+
+int oracle_xd_request_recv(oracle_sim_t* s, uint64_t items, void** ids, void** vals) {
+  if (!s || !ids || !vals || !s->xd_planned) return GOSSIP_ESTATE;
+  free(s->xrid); free(s->xrval); free(s->xrep_out);
+  s->xrid = (uint32_t*)calloc(items + 1, 4);
+  s->xrval = (uint64_t*)calloc(items + 1, 8);
+  s->xrep_out = (uint64_t*)calloc(items + 1, 8);
+  if (!s->xrid || !s->xrval || !s->xrep_out) return GOSSIP_ENOMEM;
+  s->xn_in = items;
+  *ids = s->xrid;
+  *vals = s->xrval;
+  return GOSSIP_OK;
+}
+
+int oracle_xd_serve(oracle_sim_t* s, void** replies) {
+  if (!s || !replies || !s->xd_planned || !s->xrid) return GOSSIP_ESTATE;
+  for (uint64_t i = 0; i < s->xn_in; ++i) {
+    const uint32_t id = s->xrid[i];
+    const uint64_t p = id & (XD_NO_PUSH - 1u);
+    if (p >= s->nown) return GOSSIP_EINVAL;
+    if (!(id & XD_NO_PUSH)) s->Snext[p] |= s->xrval[i];
+    s->xrep_out[i] = (id & XD_NO_PULL) ? 0 : s->S[p];
+  }
+  *replies = s->xrep_out;
+  return GOSSIP_OK;
+}
+
+int oracle_xd_response_recv(oracle_sim_t* s, void** replies) {
+  if (!s || !replies || !s->xd_planned || !s->xrep_in) return GOSSIP_ESTATE;
+  *replies = s->xrep_in;
+  return GOSSIP_OK;
+}
+
+int oracle_xd_finish(oracle_sim_t* s, uint64_t* partial) {
+  if (!s || !partial || !s->xd_planned || !s->xrep_in) return GOSSIP_ESTATE;
+  for (uint64_t j = 0; j < s->xn_out; ++j) s->Snext[s->xnode[j]] |= s->xrep_in[j];
+  totals_of(s, s->Snext, partial);
+  s->xd_planned = 0;
+  s->last_sparse = 0;
+  return GOSSIP_OK;
+}
+
 /* gossip_set_param: the engine's tuning knobs.  Only sparse_frac matters here (it picks the
  * sharded round protocol, which the gloo tests exercise); the rest steer engine kernel
  * choices that this restatement does not have, and are accepted as no-ops. */
@@ -929,6 +1046,12 @@ int oracle_set_param(oracle_sim_t* s, const char* name, double value) {
   if (!s || !name) return GOSSIP_EINVAL;
   if (!strcmp(name, "sparse_frac")) {
     s->sparse_frac = value;
+    s->sparse_frac_set = 1;
+    return GOSSIP_OK;
+  }
+  if (!strcmp(name, "xd_shards")) {
+    if (value < 0 || value > 1024) return GOSSIP_EINVAL;
+    s->xd_shards = (uint32_t)value;
     return GOSSIP_OK;
   }
   const char* known[] = {"alld_frac", "filter_frac", "ahead", "apply_grid", "ae_sparse", "ae_cap"};

@@ -5,8 +5,8 @@ Three results must agree bit for bit, round by round (stats, per-rumor counts) a
 final state:
   * G = 8 shard engines of 2^24 nodes each, driven in lockstep through the sharded round
     protocol on one device (device copies stand in for the RCCL collectives; the 8-GPU
-    node runs the same engine calls over RCCL: gossip_hip.sharded), for the auto, sparse
-    and dense round plans;
+    node runs the same engine calls over RCCL: gossip_hip.sharded), for the auto, sparse,
+    dense (state all-gather) and exchange round plans;
   * one engine holding all 2^27 nodes (the binned path past 4096 tiles, binned.hip V = 3);
   * the OpenMP oracle (oracle/gossip_oracle.c) at 2^27.
 Reference: (*NodeState).Gossip, main.go:65-89, restated as rounds."""
@@ -23,7 +23,10 @@ pytestmark = pytest.mark.gpu
 
 N, R, K, SEED, G = 1 << 27, 64, 2, 0x5EED0004, 8
 THREADS = min(16, os.cpu_count() or 1)
-PLANS = {"auto": {}, "sparse": {"sparse_frac": 1.0}, "dense": {"sparse_frac": -1}}
+# auto: sparse rounds and exchange dense rounds (G = 8 >= xd_shards); dense: every round on the
+# state all-gather; exchange: every round an exchange dense round
+PLANS = {"auto": {}, "sparse": {"sparse_frac": 1.0}, "dense": {"sparse_frac": -1, "xd_shards": 0},
+         "exchange": {"sparse_frac": -1}, "auto_image": {"xd_shards": 0}}
 
 
 @pytest.fixture(scope="module")
@@ -60,6 +63,8 @@ def test_cfg4_G8_lockstep_equals_single_engine(single_engine_run, plan):
         assert set(kinds) == {1}
     elif plan == "dense":
         assert set(kinds) == {0}
+    elif plan == "exchange":
+        assert set(kinds) == {3}
     for e in engines:
         assert e.hi - e.lo == 1 << 24
         assert np.array_equal(e.read_shard(), full[:, e.lo:e.hi])

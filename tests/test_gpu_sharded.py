@@ -19,9 +19,12 @@ CASES = [("pushpull", 2, 64, 1 << 20, 0x5EED0004, 4), ("push", 3, 1, 300001, 7, 
 IDS = ["pushpull-1M-G4", "push-ragged-G3", "pull-G2", "pushpull-k6-G2"]
 # (flags, gossip_set_param knobs) per plan
 PLANS = {"auto": (0, {}), "sparse": (0, {"sparse_frac": 1.0}), "sparse_alld": (0, {"sparse_frac": 1.0, "alld_frac": 0}),
-         "dense": (0, {"sparse_frac": -1}),
+         "dense": (0, {"sparse_frac": -1, "xd_shards": 0}),
+         # dense rounds as exchange rounds (items to the peer's owner, replies back)
+         "exchange": (0, {"sparse_frac": -1, "xd_shards": 2}), "auto_exchange": (0, {"xd_shards": 2}),
          # dense sharded rounds on the direct kernels instead of the binned push/pull passes
-         "dense_direct": (FLAG_SHARD_DIRECT, {"sparse_frac": -1}), "auto_direct": (FLAG_SHARD_DIRECT, {})}
+         "dense_direct": (FLAG_SHARD_DIRECT, {"sparse_frac": -1, "xd_shards": 0}),
+         "auto_direct": (FLAG_SHARD_DIRECT, {"xd_shards": 0})}
 
 
 @pytest.mark.parametrize("plan", list(PLANS))
@@ -46,6 +49,8 @@ def test_lockstep_shards_equal_one_engine(case, plan):
         assert set(kinds) == {1}
     elif plan in ("dense", "dense_direct"):
         assert set(kinds) == {0}
+    elif plan == "exchange":
+        assert set(kinds) == {3}
     for e in engines:
         e.close()
 
@@ -78,12 +83,37 @@ def test_lockstep_dense_past_4096_tiles():
     want = ref.step(8)
     full = ref.read_shard()
     ref.close()
-    engines = [Engine(N, R, "pushpull", 2, 0x5EED0004, flags=1, shard_rank=r, shard_count=G,
-                      params={"sparse_frac": -1}) for r in range(G)]
+    for plan, kind in (({"sparse_frac": -1, "xd_shards": 0}, 0), ({"sparse_frac": -1, "xd_shards": 2}, 3)):
+        engines = [Engine(N, R, "pushpull", 2, 0x5EED0004, flags=1, shard_rank=r, shard_count=G, params=plan)
+                   for r in range(G)]
+        for e in engines:
+            e.inject_random()
+        got, kinds = run_lockstep(engines, 8)
+        assert got == want.stats and set(kinds) == {kind}
+        for e in engines:
+            assert np.array_equal(e.read_shard(), full[:, e.lo:e.hi])
+            e.close()
+
+
+@pytest.mark.parametrize("faults", [dict(edge_loss=1 << 29, partitions=3), dict(edge_loss=1 << 29, stall_rounds=2),
+                                    dict(edge_loss=1 << 30, partitions=2, stall_rounds=3)],
+                         ids=["loss-partitions", "loss-stall", "all"])
+def test_lockstep_exchange_faults_stall(faults):
+    """Exchange dense rounds (every round) with edge loss, partitions and the stall mode
+    (DESIGN.md §2.8-2.9), G = 5 ragged shards, against one engine."""
+    N, R, G = 400009, 64, 5
+    ref = Engine(N, R, "pushpull", 2, 0x5EED0006, flags=1, **faults)
+    ref.inject_random()
+    want = ref.step(60)
+    full = ref.read_shard()
+    ref.close()
+    engines = [Engine(N, R, "pushpull", 2, 0x5EED0006, flags=1, shard_rank=r, shard_count=G,
+                      params={"xd_shards": 2, "sparse_frac": -1}, **faults) for r in range(G)]
     for e in engines:
         e.inject_random()
-    got, kinds = run_lockstep(engines, 8)
-    assert got == want.stats and set(kinds) == {0}
+    got, kinds = run_lockstep(engines, 60)
+    assert got == want.stats and set(kinds) == {3}
     for e in engines:
         assert np.array_equal(e.read_shard(), full[:, e.lo:e.hi])
         e.close()
+

@@ -46,10 +46,18 @@ def _faults(name):
     return {}
 
 
-PLANS = {"auto": None, "sparse": 1.0, "dense": -1}  # sparse_frac (gossip_set_param)
+# gossip_set_param knobs: sparse_frac picks sparse rounds, xd_shards the exchange dense rounds
+# (kind 3) instead of the state all-gather
+PLANS = {
+    "auto": {},
+    "sparse": {"sparse_frac": 1.0},
+    "dense": {"sparse_frac": -1, "xd_shards": 0},
+    "exchange": {"sparse_frac": -1, "xd_shards": 2},
+    "auto-exchange": {"xd_shards": 2},
+}
 
 
-def _worker(rank, world, port, case, q, frac=None):
+def _worker(rank, world, port, case, q, params=None):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [os.path.join(root, "gossip-protocol_amd"), os.path.join(root, "oracle")]
     import torch.distributed as dist
@@ -60,7 +68,7 @@ def _worker(rank, world, port, case, q, frac=None):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     mode, k, R, N, seed, topo = case
     e = op.OracleEngine(N, R, mode.split("-")[0], k, seed, flags=1, shard_rank=rank, shard_count=world, **_faults(mode),
-                        params={} if frac is None else {"sparse_frac": frac})
+                        params=params or {})
     if topo:
         e.set_topology(_grid(N))
         e.inject(0, 0); e.inject(N - 1, 1); e.inject(N // 2, 2)
@@ -73,7 +81,7 @@ def _worker(rank, world, port, case, q, frac=None):
 
 @pytest.mark.parametrize("plan", list(PLANS))
 @pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
-def test_two_ranks_equal_one(case, plan):
+def test_two_ranks_equal_one(case, plan, world=2):
     if case[0] == "flood" and plan != "auto":
         pytest.skip("FLOOD rounds are always dense (no sparse protocol)")
     import oracle_py as op
@@ -90,16 +98,24 @@ def test_two_ranks_equal_one(case, plan):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, case, q, PLANS[plan])) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, case, q, PLANS[plan])) for r in range(world)]
     for p in procs:
         p.start()
-    got = [q.get(timeout=120) for _ in range(2)]
+    got = [q.get(timeout=120) for _ in range(world)]
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
     for rank, lo, hi, stats, shard in got:
         assert stats == want.stats
         assert np.array_equal(shard, full[:, lo:hi])
+
+
+@pytest.mark.parametrize("plan", ["exchange", "auto-exchange"])
+@pytest.mark.parametrize("case", CASES[:5], ids=[c[0] for c in CASES[:5]])
+def test_three_ranks_exchange_equal_one(case, plan):
+    """Exchange dense rounds (items to the peer's owner, replies back) with
+    ragged shards: world 3."""
+    test_two_ranks_equal_one(case, plan, world=3)
 
 
 AE_CASES = [  # N, K, fanout, seed, fail, recover

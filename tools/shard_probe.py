@@ -8,12 +8,18 @@ sys.path.insert(0, os.path.join(ROOT, "gossip-protocol_amd"))
 import numpy as np
 import torch
 from gossip_hip import Engine
+from gossip_hip import engine as _eng
 from gossip_hip import sharded as sh
+
+if os.environ.get("GOSSIP_LIB"):  # a library variant (tools/build_variants.sh)
+    _eng.load_library(os.environ["GOSSIP_LIB"])
 
 G = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 LG = int(sys.argv[2]) if len(sys.argv) > 2 else 24
 CALLS = ("sparse_rare", "sparse_scan", "sparse_commit", "dense_prepare", "round_compute", "exchange_buffers",
-         "local_totals")
+         "local_totals", "xd_requests", "xd_request_recv", "xd_serve", "xd_response_recv", "xd_finish")
+# argv[3:]: gossip_set_param knobs as name=value (e.g. xd_shards=0: dense rounds on the state all-gather)
+PARAMS = {a.split("=")[0]: float(a.split("=")[1]) for a in sys.argv[3:]}
 
 
 class Timed:
@@ -34,7 +40,8 @@ class Timed:
         return g
 
 
-engines = [Engine(G << LG, 64, "pushpull", 2, 0x5EED0004, shard_rank=r, shard_count=G) for r in range(G)]
+engines = [Engine(G << LG, 64, "pushpull", 2, 0x5EED0004, shard_rank=r, shard_count=G, params=PARAMS)
+           for r in range(G)]
 for rep in range(2):
     logs = [[] for _ in engines]
     tes = [Timed(e, l) for e, l in zip(engines, logs)]
@@ -48,6 +55,8 @@ for rep in range(2):
             tot = sh._lockstep_sum([e.local_totals() for e in engines]); ks = [e.sharded_plan(tot) for e in engines]
         if ks[0] == 1:
             parts = sh._lockstep_sparse(tes)
+        elif ks[0] == 3:
+            parts = sh._lockstep_xd(tes)
         else:
             parts = sh._lockstep_dense(tes)
         tot = sh._lockstep_sum(parts)
@@ -63,5 +72,5 @@ for rep in range(2):
     if rep == 1:
         for t, k, ms, full, calls in rounds:
             br = " ".join(f"{n}={v:.3f}" for n, v in calls.items())
-            print(f"G={G} round {t:2d} {'sparse' if k else 'dense '} per-rank {ms:7.3f} ms  full={full}  [{br}]", flush=True)
+            print(f"G={G} round {t:2d} {['dense ', 'sparse', 'ae', 'xdense'][k]} per-rank {ms:7.3f} ms  full={full}  [{br}]", flush=True)
         print(f"G={G} rounds={len(rounds)} sum per-rank {sum(r[2] for r in rounds):.2f} ms", flush=True)
