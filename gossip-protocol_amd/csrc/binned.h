@@ -121,7 +121,12 @@ hipError_t launch_sb_round(const SbGeom& g, const SbBufs& b, const uint64_t* ima
 // tiles.  Per-shard work is O(nodes per shard) at any G.
 constexpr uint32_t kXdNoPush = 1u << 30;  // wire item id: p at the owner [0, 30) | these two flags
 constexpr uint32_t kXdNoPull = 1u << 31;
-constexpr uint32_t kXdBinRegion = 16384;  // received items binned per LDS region
+#ifndef GOSSIP_XD_REGION
+#define GOSSIP_XD_REGION 8192
+#endif
+// received items binned per LDS region (<= 16384; at <= 8192 their values are staged in LDS
+// too: G = 8 probe 17.44 ms against 17.62 ms with 16384, profiles/r02_xd)
+constexpr uint32_t kXdBinRegion = GOSSIP_XD_REGION;
 struct XdGeom {
   uint64_t N, Nl, lo, nown;
   uint32_t G, rank, k;

@@ -1006,26 +1006,29 @@ __global__ __launch_bounds__(kEmitThreads) void xd_count_kernel(XdGeom g, const 
   }
 }
 
-// send positions: owner-major, then sender region; ocnt = items per owner
+// send positions: owner-major, then sender region; ocnt = items per owner.  One
+// block per owner o: the items of owners < o (its base) and o's column scan.
 __global__ __launch_bounds__(1024) void xd_scan_kernel(const uint32_t* __restrict__ rcnt, uint32_t* __restrict__ roff,
                                                         uint32_t* __restrict__ ocnt, uint32_t nrs, uint32_t G) {
   __shared__ uint32_t scratch[1024 / 64 + 1];
+  const uint32_t o = blockIdx.x;
   const uint32_t per = (nrs + 1023) / 1024;
   const uint32_t lo = min(threadIdx.x * per, nrs), hi = min(lo + per, nrs);
-  uint32_t base = 0;
-  for (uint32_t o = 0; o < G; ++o) {
-    uint32_t mine = 0;
-    for (uint32_t s = lo; s < hi; ++s) mine += rcnt[(size_t)s * G + o];
-    uint32_t total;
-    uint32_t run = base + block_exscan<1024>(mine, scratch, &total);
-    for (uint32_t s = lo; s < hi; ++s) {
-      const uint32_t c = rcnt[(size_t)s * G + o];
-      roff[(size_t)s * G + o] = run;
-      run += c;
-    }
-    if (threadIdx.x == 0) ocnt[o] = total;
-    base += total;
+  uint32_t before = 0, mine = 0;
+  for (uint32_t s = lo; s < hi; ++s) {
+    const uint32_t* row = rcnt + (size_t)s * G;
+    for (uint32_t q = 0; q < o; ++q) before += row[q];
+    mine += row[o];
   }
+  uint32_t base, total;
+  (void)block_exscan<1024>(before, scratch, &base);
+  uint32_t run = base + block_exscan<1024>(mine, scratch, &total);
+  for (uint32_t s = lo; s < hi; ++s) {
+    const uint32_t c = rcnt[(size_t)s * G + o];
+    roff[(size_t)s * G + o] = run;
+    run += c;
+  }
+  if (threadIdx.x == 0) ocnt[o] = total;
 }
 
 // the items of sender region s, counting-sorted by owner in LDS and written to
@@ -1088,8 +1091,11 @@ __global__ __launch_bounds__(kEmitThreads) void xd_emit_kernel(XdGeom g, const u
 // received items binned by own destination tile (one region of kXdBinRegion
 // items per pass of the block); the binned id keeps the item's slot
 __global__ __launch_bounds__(kEmitThreads) void xd_bin_kernel(XdGeom g, XdBufs b, uint64_t n_in) {
+  // regions of <= 8192 items also stage the values in LDS (all global accesses in order)
+  constexpr bool kStageV = kXdBinRegion <= 8192;
   __shared__ uint32_t cur[kSbMaxTiles];
   __shared__ uint32_t st[kXdBinRegion];
+  __shared__ uint64_t sv[kStageV ? kXdBinRegion : 1];
   __shared__ uint32_t wsum[kEmitThreads / 64];
   __shared__ uint32_t wpre[kEmitThreads / 64 + 1];
   constexpr uint32_t kQ = kXdBinRegion / kEmitThreads;
@@ -1101,10 +1107,12 @@ __global__ __launch_bounds__(kEmitThreads) void xd_bin_kernel(XdGeom g, XdBufs b
     const uint64_t base = (uint64_t)r * kXdBinRegion;
     const uint32_t nitems = (uint32_t)min<uint64_t>(kXdBinRegion, n_in - base);
     uint32_t id[kQ];
+    uint64_t iv[kStageV ? kQ : 1];
 #pragma unroll
     for (uint32_t q = 0; q < kQ; ++q) {
       const uint32_t i = tid + q * kEmitThreads;
       id[q] = i < nitems ? b.rid[base + i] : 0u;
+      if constexpr (kStageV) iv[q] = b.rval[base + min(i, nitems - 1)];
       if (i < nitems) atomicAdd(&cur[min((id[q] & (kXdNoPush - 1u)) >> kTileDLog, nt - 1u)], 1u);
     }
     __syncthreads();
@@ -1119,12 +1127,18 @@ __global__ __launch_bounds__(kEmitThreads) void xd_bin_kernel(XdGeom g, XdBufs b
       const uint32_t pos = atomicAdd(&cur[min(p >> kTileDLog, nt - 1u)], 1u);  // (p < nown: emit's items)
       st[pos] = (p & (kTileD - 1)) | (i << kTileDLog) | ((id[q] & kXdNoPush) ? kXbVZ : 0u) |
                 ((id[q] & kXdNoPull) ? kXbVF : 0u);
+      if constexpr (kStageV) sv[pos] = (id[q] & kXdNoPush) ? 0ull : iv[q];
     }
     __syncthreads();
     for (uint32_t e = tid; e < total; e += kEmitThreads) {
       const uint32_t x = st[e];
       rec_st<1>(&gids[e], x);
-      // the region's values were streamed in with the ids' lines: L2 hits
+      if constexpr (kStageV) {
+        rec_st<1>(&gvals[e], (uint64_t)sv[e]);
+        continue;
+      }
+      // the region's values were streamed in with the ids' lines: L2 hits (all of a
+      // thread's gathers in flight at once measured slower: 239 -> 323 us)
       rec_st<1>(&gvals[e], (uint64_t)((x & kXbVZ) ? 0ull : b.rval[base + ((x >> kTileDLog) & kXbSlotMask)]));
     }
   }
@@ -1140,10 +1154,19 @@ __global__ __launch_bounds__(kEmitThreads) void xd_unperm_kernel(XdGeom g, XdBuf
     const uint32_t nitems = (uint32_t)min<uint64_t>(kXdBinRegion, n_in - base);
     const uint32_t* gids = b.rb.ids + (size_t)r * g.r.rp;
     const uint64_t* gresp = b.rb.resp + (size_t)r * g.r.rp;
-    for (uint32_t e = tid; e < nitems; e += kEmitThreads) {
-      const uint32_t x = gids[e];
-      buf[(x >> kTileDLog) & kXbSlotMask] = (x & kXbVF) ? 0ull : gresp[e];  // serve wrote only the pulls
+    constexpr uint32_t kQ = kXdBinRegion / kEmitThreads;
+    uint32_t x[kQ];
+    uint64_t rv[kQ];
+#pragma unroll
+    for (uint32_t q = 0; q < kQ; ++q) {
+      const uint32_t e = min(tid + q * kEmitThreads, nitems - 1);  // (nitems >= 1)
+      x[q] = gids[e];
+      rv[q] = gresp[e];
     }
+#pragma unroll
+    for (uint32_t q = 0; q < kQ; ++q)
+      if (tid + q * kEmitThreads < nitems)
+        buf[(x[q] >> kTileDLog) & kXbSlotMask] = (x[q] & kXbVF) ? 0ull : rv[q];  // serve wrote only the pulls
     __syncthreads();
     for (uint32_t i = tid; i < nitems; i += kEmitThreads) b.rep_out[base + i] = buf[i];
   }
@@ -1252,7 +1275,7 @@ XdGeom make_xd_geom(uint64_t N, uint32_t k, uint64_t Nl, uint64_t lo, uint64_t n
   g.r = g.s;
   g.r.N = nown;
   g.r.ts = kXdBinRegion;
-  g.r.ts_log = kTileDLog;
+  g.r.ts_log = 31 - __builtin_clz(kXdBinRegion);
   g.r.rp = kXdBinRegion;
   g.r.nt_s = 0;  // set per round from the received count
   return g;
@@ -1324,7 +1347,7 @@ hipError_t launch_xd_requests(const XdGeom& g, const XdBufs& b, const uint64_t* 
   const uint32_t eg = g.s.nt_s < kEmitGrid ? g.s.nt_s : kEmitGrid;
   if (fa.any()) xd_count_kernel<true><<<eg, kEmitThreads, 0, st>>>(g, S, b.rcnt, R, t, key0, key1, mode, fa);
   else xd_count_kernel<false><<<eg, kEmitThreads, 0, st>>>(g, S, b.rcnt, R, t, key0, key1, mode, fa);
-  xd_scan_kernel<<<1, 1024, 0, st>>>(b.rcnt, b.roff, b.ocnt, g.s.nt_s, g.G);
+  xd_scan_kernel<<<g.G, 1024, 0, st>>>(b.rcnt, b.roff, b.ocnt, g.s.nt_s, g.G);
   if (fa.any()) xd_emit_kernel<true><<<eg, kEmitThreads, 0, st>>>(g, S, b, b.rlofs, R, t, key0, key1, mode, fa);
   else xd_emit_kernel<false><<<eg, kEmitThreads, 0, st>>>(g, S, b, b.rlofs, R, t, key0, key1, mode, fa);
   return hipGetLastError();
