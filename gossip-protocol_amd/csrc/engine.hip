@@ -1497,11 +1497,12 @@ int gossip_sparse_scan(gossip_engine_t* e, const uint64_t* counts, void** send, 
   }
   HIP_OK(e, hipMemcpyAsync(e->sb.cbase, cb, (e->G + 1) * 8, hipMemcpyHostToDevice, e->stream));
   if (int rc = timer_begin(e, 0)) return rc;
-  HIP_OK(e, sx_index(e->sg, e->sb, e->rare_recv, e->sx_stride, e->stream));
-  HIP_OK(e, sx_scan(e->sg, e->sb, e->lf, e->S, e->rare_recv, e->sx_stride, e->t, e->key0, e->key1, e->mode,
+  const uint64_t rare = cb[e->G];
+  HIP_OK(e, sx_index(e->sg, e->sb, e->rare_recv, e->sx_stride, rare, e->stream));
+  HIP_OK(e, sx_scan(e->sg, e->sb, e->lf, e->S, e->rare_recv, e->sx_stride, rare, e->t, e->key0, e->key1, e->mode,
                     e->sx_maj, e->sx_alld, e->fa, e->stream));
   if (int rc = timer_end(e, 0)) return rc;
-  HIP_OK(e, hipStreamSynchronize(e->stream));  // cb is read by the copy above
+  // (the copy below lands in cb's pinned buffer after the copy that read it: same stream)
   HIP_OK(e, hipMemcpyAsync(e->sx_host, e->sb.msg_cnt, (e->G + 1) * 4, hipMemcpyDeviceToHost, e->stream));
   HIP_OK(e, hipStreamSynchronize(e->stream));
   const uint32_t* c = (const uint32_t*)e->sx_host;

@@ -21,6 +21,9 @@ constexpr uint32_t kScanGrid = 256;  // one block per CU: the summary takes 128 
 constexpr uint32_t kRwWords = 1024;  // own rare-bitmap words staged per chunk (64K nodes)
 constexpr int kScanUnroll = 2;
 constexpr uint32_t kMsgShift = 40;   // message node word: owner << 40 | node at the owner
+// up to this many rare nodes (all shards), the index skips the per-word ranks and the
+// summary pass over all N nodes: a value is found by binary search in its owner's list
+constexpr uint64_t kSmallIndex = 1ull << 16;
 
 __device__ __forceinline__ uint64_t word_valid(uint64_t w, uint64_t n) {
   const uint64_t lo = w << 6;
@@ -67,8 +70,10 @@ __global__ __launch_bounds__(256) void list_kernel(FrontierBufs f, const uint64_
 // Lists are in id order (and shards in rank order), so the items of one bitmap
 // word sit in consecutive lanes: a segmented OR across the wave leaves one
 // atomic per word a wave touches instead of one per item.
+template <bool SUMM>
 __global__ __launch_bounds__(256) void setbits_kernel(const SxItem* __restrict__ recv, uint64_t stride, uint32_t G,
-                                                       const uint64_t* __restrict__ cbase, uint64_t* __restrict__ grb) {
+                                                       const uint64_t* __restrict__ cbase, uint64_t* __restrict__ grb,
+                                                       uint32_t* __restrict__ summ, uint32_t glog) {
   const uint64_t total = stride * G;
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t step = (uint64_t)gridDim.x * 256;
@@ -90,6 +95,11 @@ __global__ __launch_bounds__(256) void setbits_kernel(const SxItem* __restrict__
     }
     const uint64_t wprev = __shfl_up(w, 1, 64);
     if (valid && (lane == 0 || wprev != w)) atomicOr((unsigned long long*)&grb[w], (unsigned long long)m);
+    // small lists: the LDS summary straight from the items (one bit per 2^glog nodes)
+    if (SUMM && valid) {
+      const uint64_t gb = p >> glog;
+      atomicOr(&summ[gb >> 5], 1u << (gb & 31u));
+    }
   }
 }
 
@@ -125,8 +135,19 @@ struct ScanArgs {
 // S_t of a rare node p (global id) whose bitmap word is rw: own shard from S,
 // another shard from the gathered lists (its rank among the rare nodes, minus
 // the lists before its owner's, is its place in the owner's list)
+// Small lists (a.gpre null, sx_index): p's place in its owner's list by binary search.
 __device__ __forceinline__ uint64_t rare_value(const ScanArgs& a, uint32_t p, uint64_t rw, uint32_t pre) {
   const uint32_t q = (uint32_t)(p / a.Nl);
+  if (!a.gpre) {
+    const SxItem* list = a.recv + q * a.stride;
+    uint64_t lo = 0, hi = a.cbase[q + 1] - a.cbase[q];
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (list[mid].node < p) lo = mid + 1;
+      else hi = mid;
+    }
+    return list[lo].value;  // p is in the list: its grb bit is set
+  }
   const uint64_t rank = (uint64_t)pre + (uint64_t)__popcll(rw & ((1ull << (p & 63u)) - 1ull));
   return a.recv[q * a.stride + (rank - a.cbase[q])].value;
 }
@@ -227,7 +248,7 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, uint32_t*
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) {
           const bool remote = ((hit[u] >> j) & 1u) && (pp[u][j] - lo >= nown);
-          pre[u][j] = remote ? a.gpre[pp[u][j] >> 6] : 0u;
+          pre[u][j] = remote && a.gpre ? a.gpre[pp[u][j] >> 6] : 0u;
         }
       uint64_t x[kScanUnroll], vp[kScanUnroll][4];
 #pragma unroll
@@ -289,7 +310,7 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, uint32_t*
             }
             const bool moves = !lost && (rn[u] || rp);  // else lost, or both ends majority: nothing moves
             uint64_t v = maj;
-            if (rp) v = (p - lo < nown) ? a.S[p - lo] : rare_value(a, p, w, a.gpre[p >> 6]);
+            if (rp) v = (p - lo < nown) ? a.S[p - lo] : rare_value(a, p, w, a.gpre ? a.gpre[p >> 6] : 0u);
             if (kPull && moves) acc |= v;
             if (kPush) push_to(p, moves ? x[u] & ~v : 0ull);
           }
@@ -459,12 +480,25 @@ hipError_t sx_compact(const SxGeom& g, const SxBufs& b, const FrontierBufs& lf, 
   return hipGetLastError();
 }
 
-hipError_t sx_index(const SxGeom& g, const SxBufs& b, const SxItem* recv, uint64_t stride, hipStream_t st) {
+bool sx_small_index(uint64_t rare) { return rare <= kSmallIndex; }
+
+hipError_t sx_index(const SxGeom& g, const SxBufs& b, const SxItem* recv, uint64_t stride, uint64_t rare,
+                    hipStream_t st) {
   const uint64_t nwg = (g.N + 63) / 64;
   // grb is 256-B aligned (sx_carve) and padded to 16 B
   zero_kernel<<<grid_for((nwg + 1) / 2, 256, 2048), 256, 0, st>>>((uint4*)b.grb, (nwg + 1) / 2);
   hipError_t e;
-  if (stride) setbits_kernel<<<grid_for(stride * g.G, 256, 4096), 256, 0, st>>>(recv, stride, g.G, b.cbase, b.grb);
+  if (sx_small_index(rare)) {  // no per-word ranks (values by binary search), summary from the items
+    const uint64_t n16 = (b.gsum.summ_words + 3) / 4;
+    zero_kernel<<<grid_for(n16, 256, 2048), 256, 0, st>>>((uint4*)b.gsum.summ, n16);
+    if (stride)
+      setbits_kernel<true><<<grid_for(stride * g.G, 256, 4096), 256, 0, st>>>(recv, stride, g.G, b.cbase, b.grb,
+                                                                             b.gsum.summ, b.gsum.glog);
+    return hipGetLastError();
+  }
+  if (stride)
+    setbits_kernel<false><<<grid_for(stride * g.G, 256, 4096), 256, 0, st>>>(recv, stride, g.G, b.cbase, b.grb,
+                                                                            nullptr, 0u);
   gcount_kernel<<<grid_for(nwg + 1, 256, 1u << 30), 256, 0, st>>>(b.grb, nwg, b.gcnt);
   size_t tb = b.tmp_bytes;
   e = hipcub::DeviceScan::ExclusiveSum(b.tmp, tb, b.gcnt, b.gpre, (int)(nwg + 1), st);
@@ -473,8 +507,8 @@ hipError_t sx_index(const SxGeom& g, const SxBufs& b, const SxItem* recv, uint64
 }
 
 hipError_t sx_scan(const SxGeom& g, const SxBufs& b, const FrontierBufs& lf, const uint64_t* S, const SxItem* recv,
-                   uint64_t stride, uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t maj, bool all_d,
-                   const Faults& fa, hipStream_t st) {
+                   uint64_t stride, uint64_t rare, uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode,
+                   uint32_t maj, bool all_d, const Faults& fa, hipStream_t st) {
   hipError_t e = hipMemsetAsync(b.msg_cnt, 0, (g.G + 2) * 4, st);
   if (e == hipSuccess) e = hipMemsetAsync(b.msg_fill, 0, g.G * 4, st);
   if (e != hipSuccess) return e;
@@ -484,7 +518,7 @@ hipError_t sx_scan(const SxGeom& g, const SxBufs& b, const FrontierBufs& lf, con
   a.recv = recv;
   a.stride = stride;
   a.grb = b.grb;
-  a.gpre = b.gpre;
+  a.gpre = sx_small_index(rare) ? nullptr : b.gpre;
   a.cbase = b.cbase;
   a.gsumm = b.gsum.summ;
   a.gglog = b.gsum.glog;
