@@ -233,10 +233,9 @@ def main():
             rl["sparse_rounds"] = {"avg_round_us": sparse_ms * 1e3 / max(sparse_n, 1), "rounds_timed": sparse_n}
         else:
             rl["kernel"] = ("sharded rounds, hipEvent-timed device work of the hot kernels per round (timer 0): "
-                            "dense = binned push pass (every sender -> own tiles) + pull pass (own senders -> "
-                            "image tiles) + serve + apply after the state all-gather, sparse = rare index + "
-                            "sharded scan between the rare-list all-gather and the push all-to-all "
-                            "(DESIGN.md §5); collectives not included")
+                            "dense = exchange round (count + emit, bin + serve + unpermute, apply; G >= 6) or the "
+                            "binned push / pull passes + serve + apply after the state all-gather (G < 6), "
+                            "sparse = rare index + sharded scan (DESIGN.md §5); collectives not included")
         if world == 1 and not args.no_dense_only:
             rl["dense_only"] = dense_only(n_total, seed, local)
         if world == 1 and not args.no_cpu_baseline:

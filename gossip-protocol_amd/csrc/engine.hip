@@ -281,14 +281,16 @@ int timer_end(gossip_engine* e, int which) {
 }
 
 // called after a stream sync: fold finished event pairs into the totals
-int timer_collect(gossip_engine* e) {
+// count = false: a piece of a round whose last piece counts the launch (exchange rounds
+// time their three engine calls, not the collectives between them)
+int timer_collect(gossip_engine* e, bool count = true) {
   if (!e->timing) return GOSSIP_OK;
   for (int w = 0; w < kTimers; ++w) {
     if (!e->ev_pending[w]) continue;
     float ms = 0.f;
     HIP_OK(e, hipEventElapsedTime(&ms, e->ev[w][0], e->ev[w][1]));
     e->time_ms[w] += ms;
-    e->launches[w] += 1;
+    e->launches[w] += count ? 1 : 0;
     e->ev_pending[w] = false;
   }
   if (e->ev_pre_pending) {  // the prepared part of a dense sharded round counts with timer 0
@@ -1559,8 +1561,10 @@ int gossip_xd_requests(gossip_engine_t* e, void** ids, void** vals, uint64_t* se
   HIP_OK(e, hipMemsetAsync(e->partial_d, 0, part_len(e) * 8, e->stream));
   if (int rc = timer_begin(e, 0)) return rc;
   HIP_OK(e, launch_xd_requests(e->xg, e->xb, e->S, e->R, e->t, e->key0, e->key1, e->mode, e->fa, e->stream));
+  if (int rc = timer_end(e, 0)) return rc;
   HIP_OK(e, hipMemcpyAsync(e->xd_cnt_h, e->xb.ocnt, e->G * 4, hipMemcpyDeviceToHost, e->stream));
   HIP_OK(e, hipStreamSynchronize(e->stream));
+  if (int rc = timer_collect(e, false)) return rc;
   for (uint32_t q = 0; q < e->G; ++q) send_counts[q] = e->xd_cnt_h[q];
   *ids = e->xb.sid;
   *vals = e->xb.sval;
@@ -1595,8 +1599,11 @@ int gossip_xd_serve(gossip_engine_t* e, void** replies) {
   if (!replies) return GOSSIP_EINVAL;
   if (int rc = xd_check(e)) return rc;
   if (!e->xd_rmem) return e->fail(GOSSIP_ESTATE, "gossip_xd_request_recv first");
+  if (int rc = timer_begin(e, 0)) return rc;
   HIP_OK(e, launch_xd_serve(e->xg, e->xb, e->S, e->xd_nin, e->R, e->stream));
+  if (int rc = timer_end(e, 0)) return rc;
   HIP_OK(e, hipStreamSynchronize(e->stream));
+  if (int rc = timer_collect(e, false)) return rc;
   *replies = e->xb.rep_out;
   return GOSSIP_OK;
 }
@@ -1613,6 +1620,7 @@ int gossip_xd_finish(gossip_engine_t* e, uint64_t* partial) {
   if (!partial) return GOSSIP_EINVAL;
   if (int rc = xd_check(e)) return rc;
   if (!e->xd_smem || !e->xd_rmem) return e->fail(GOSSIP_ESTATE, "gossip_xd_finish before the exchange");
+  if (int rc = timer_begin(e, 0)) return rc;
   HIP_OK(e, launch_xd_apply(e->xg, e->xb, e->S, e->Snext, e->xd_nin, e->partial_d, e->R, e->mode, e->cfg.flags,
                             e->lf.nzb, e->lf.fullb, e->stream));
   if (int rc = timer_end(e, 0)) return rc;
