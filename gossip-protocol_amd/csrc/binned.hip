@@ -981,18 +981,17 @@ __device__ __forceinline__ void xd_edges(uint32_t k, uint32_t n, uint64_t nm1, u
   }
 }
 
-// items per (sender region, owner of the peer).  A sender's directions depend only on its
-// class (empty / full / mixed), read from the exact occupancy bitmaps of S_t (1/32 of S's bytes).
+// items per (sender region, owner of the peer).  (Reading the senders' classes from the
+// occupancy bitmaps instead of S_t made count + emit slower: S_t streamed here is still
+// in the MALL when emit reads it, profiles/r02_xd/variants3.)
 template <bool FAULTS>
-__global__ __launch_bounds__(kEmitThreads) void xd_count_kernel(XdGeom g, const uint64_t* __restrict__ nzb,
-                                                                 const uint64_t* __restrict__ fullb,
-                                                                 uint32_t* __restrict__ rcnt, uint32_t t,
+__global__ __launch_bounds__(kEmitThreads) void xd_count_kernel(XdGeom g, const uint64_t* __restrict__ S,
+                                                                 uint32_t* __restrict__ rcnt, uint32_t R, uint32_t t,
                                                                  uint32_t key0, uint32_t key1, uint32_t mode,
                                                                  Faults fa) {
   __shared__ uint32_t cnt[kXdMaxG];
   const uint32_t tid = threadIdx.x, Nl32 = (uint32_t)g.Nl;
-  const uint64_t nm1 = g.N - 1;
-  const bool can_push = mode == 1 || mode == 3, can_pull = mode == 2 || mode == 3;
+  const uint64_t fm = full_mask1(R), nm1 = g.N - 1;
   for (uint32_t s = blockIdx.x; s < g.s.nt_s; s += gridDim.x) {
     __syncthreads();
     for (uint32_t o = tid; o < g.G; o += kEmitThreads) cnt[o] = 0;
@@ -1000,12 +999,10 @@ __global__ __launch_bounds__(kEmitThreads) void xd_count_kernel(XdGeom g, const 
     const uint64_t base = (uint64_t)s << g.s.ts_log;
     const uint32_t nsend = (uint32_t)min<uint64_t>(g.s.ts, g.nown - base);
     // (one LDS atomic per edge: aggregating a wave's lanes per owner with ballots measured
-    // 2.6x slower, profiles/r02_xd)
+    // 2.6x slower, profiles/r02_xd/variants3)
     for (uint32_t i = tid; i < nsend; i += kEmitThreads) {
-      const uint64_t n = base + i;
-      const bool nz = (nzb[n >> 6] >> (n & 63)) & 1ull, full = (fullb[n >> 6] >> (n & 63)) & 1ull;
-      if (!((can_push && nz) || (can_pull && !full))) continue;  // = sender_dirs(mode, S_t[n]) != 0
-      xd_edges<FAULTS>(g.k, (uint32_t)(g.lo + n), nm1, t, key0, key1, fa,
+      if (!sender_dirs(mode, S[base + i], fm)) continue;
+      xd_edges<FAULTS>(g.k, (uint32_t)(g.lo + base + i), nm1, t, key0, key1, fa,
                        [&](uint32_t p) { atomicAdd(&cnt[xd_owner(p, Nl32, g.G)], 1u); });
     }
     __syncthreads();
@@ -1073,7 +1070,6 @@ __global__ __launch_bounds__(kEmitThreads) void xd_emit_kernel(XdGeom g, const u
       xd_edges<FAULTS>(g.k, (uint32_t)(g.lo + base + i), nm1, t, key0, key1, fa, [&](uint32_t p) {
         const uint32_t o = xd_owner(p, Nl32, G);
         const uint32_t pos = atomicAdd(&cur[o], 1u);
-        if (pos >= kRecPerRegion) return;  // (never: the count pass saw the same edges; keeps LDS in bounds)
         st_id[pos] = (p - o * Nl32) | fl;
         st_nl[pos] = (uint16_t)i;
       });
@@ -1349,18 +1345,13 @@ void xd_carve_recv(const XdGeom& g, uint64_t cap_r, void* base, XdBufs* b) {
   b->rb.nzb = b->rb.fullb = nullptr;
 }
 
-hipError_t launch_xd_requests(const XdGeom& g, const XdBufs& b, const uint64_t* S, const uint64_t* nzb,
-                              const uint64_t* fullb, uint32_t R, uint32_t t, uint32_t key0, uint32_t key1,
-                              uint32_t mode, const Faults& fa, hipStream_t st) {
+hipError_t launch_xd_requests(const XdGeom& g, const XdBufs& b, const uint64_t* S, uint32_t R, uint32_t t,
+                              uint32_t key0, uint32_t key1, uint32_t mode, const Faults& fa, hipStream_t st) {
   if (g.nown == 0) return hipMemsetAsync(b.ocnt, 0, g.G * 4, st);
   const uint32_t eg = g.s.nt_s < kEmitGrid ? g.s.nt_s : kEmitGrid;
-#ifndef GOSSIP_XD_COUNT_GRID
-#define GOSSIP_XD_COUNT_GRID 256
-#endif
-  // the count pass holds 1 KiB of LDS: more blocks than CUs hide the draws' latency
-  const uint32_t cg = g.s.nt_s < GOSSIP_XD_COUNT_GRID ? g.s.nt_s : GOSSIP_XD_COUNT_GRID;
-  if (fa.any()) xd_count_kernel<true><<<cg, kEmitThreads, 0, st>>>(g, nzb, fullb, b.rcnt, t, key0, key1, mode, fa);
-  else xd_count_kernel<false><<<cg, kEmitThreads, 0, st>>>(g, nzb, fullb, b.rcnt, t, key0, key1, mode, fa);
+  // (1024 blocks instead of one per CU: same time, profiles/r02_xd/variants3)
+  if (fa.any()) xd_count_kernel<true><<<eg, kEmitThreads, 0, st>>>(g, S, b.rcnt, R, t, key0, key1, mode, fa);
+  else xd_count_kernel<false><<<eg, kEmitThreads, 0, st>>>(g, S, b.rcnt, R, t, key0, key1, mode, fa);
   xd_scan_kernel<<<g.G, 1024, 0, st>>>(b.rcnt, b.roff, b.ocnt, g.s.nt_s, g.G);
   if (fa.any()) xd_emit_kernel<true><<<eg, kEmitThreads, 0, st>>>(g, S, b, b.rlofs, R, t, key0, key1, mode, fa);
   else xd_emit_kernel<false><<<eg, kEmitThreads, 0, st>>>(g, S, b, b.rlofs, R, t, key0, key1, mode, fa);

@@ -1558,11 +1558,9 @@ int gossip_xd_requests(gossip_engine_t* e, void** ids, void** vals, uint64_t* se
     }
     xd_carve_send(e->xg, e->xd_smem, &e->xb);
   }
-  if (int rc = sx_prepare(e)) return rc;  // exact occupancy bitmaps of S_t (the senders' classes)
   HIP_OK(e, hipMemsetAsync(e->partial_d, 0, part_len(e) * 8, e->stream));
   if (int rc = timer_begin(e, 0)) return rc;
-  HIP_OK(e, launch_xd_requests(e->xg, e->xb, e->S, e->lf.nzb, e->lf.fullb, e->R, e->t, e->key0, e->key1, e->mode,
-                               e->fa, e->stream));
+  HIP_OK(e, launch_xd_requests(e->xg, e->xb, e->S, e->R, e->t, e->key0, e->key1, e->mode, e->fa, e->stream));
   if (int rc = timer_end(e, 0)) return rc;
   HIP_OK(e, hipMemcpyAsync(e->xd_cnt_h, e->xb.ocnt, e->G * 4, hipMemcpyDeviceToHost, e->stream));
   HIP_OK(e, hipStreamSynchronize(e->stream));

@@ -152,7 +152,8 @@ __device__ __forceinline__ uint64_t rare_value(const ScanArgs& a, uint32_t p, ui
   return a.recv[q * a.stride + (rank - a.cbase[q])].value;
 }
 
-template <int MAJ, int MODE>
+// FAULTS: edge loss / partitions / stall active; off, none of that code exists
+template <int MAJ, int MODE, bool FAULTS>
 __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, uint32_t* lcnt, const ScanArgs& a) {
   const uint32_t* summ = (const uint32_t*)summ4;
   const uint32_t tid = threadIdx.x, lane = tid & 63;
@@ -211,13 +212,13 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, uint32_t*
         for (uint32_t j = 0; j < 4; ++j) pp[u][j] = 0;
         if (act[u] && k <= 4) {
           const u32x4 r4 = philox4x32_10(u32x4{n, a.t, 0u, 0u}, a.key0, a.key1);
-          const u32x4 lw = a.fa.loss ? loss_draws(n, a.t, 0u, a.key0, a.key1) : u32x4{0, 0, 0, 0};
-          const Reach rc = reach_of(n, a.fa);  // n's partition block
+          const u32x4 lw = FAULTS && a.fa.loss ? loss_draws(n, a.t, 0u, a.key0, a.key1) : u32x4{0, 0, 0, 0};
+          const Reach rc = FAULTS ? reach_of(n, a.fa) : Reach{0u, 0xFFFFFFFFu};  // n's partition block (§2.8)
 #pragma unroll
           for (uint32_t j = 0; j < 4; ++j) {
             if (j >= k) break;
             pp[u][j] = peer_from_word(lane_of(r4, j), nm1, n);
-            const bool lost = a.fa.any() && edge_lost(a.fa, rc, pp[u][j], lane_of(lw, j));
+            const bool lost = FAULTS && edge_lost(a.fa, rc, pp[u][j], lane_of(lw, j));
             live[u] |= (lost ? 0u : 1u) << j;
             if (!lost && summ_bit(pp[u][j])) hit[u] |= 1u << j;
           }
@@ -294,14 +295,14 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, uint32_t*
           const uint32_t i = base + u * kScanThreads + tid, n = lo + i;
           uint64_t acc = 0;
           u32x4 r4{0, 0, 0, 0}, lw{0, 0, 0, 0};
-          const Reach rc = reach_of(n, a.fa);  // n's partition block
+          const Reach rc = FAULTS ? reach_of(n, a.fa) : Reach{0u, 0xFFFFFFFFu};  // n's partition block (§2.8)
           for (uint32_t j = 0; j < k; ++j) {
             if ((j & 3u) == 0) {
               r4 = philox4x32_10(u32x4{n, a.t, 0u, j >> 2}, a.key0, a.key1);
-              if (a.fa.loss) lw = loss_draws(n, a.t, j >> 2, a.key0, a.key1);
+              if (FAULTS && a.fa.loss) lw = loss_draws(n, a.t, j >> 2, a.key0, a.key1);
             }
             const uint32_t p = peer_from_word(lane_of(r4, j & 3u), nm1, n);
-            const bool lost = a.fa.any() && edge_lost(a.fa, rc, p, lane_of(lw, j & 3u));
+            const bool lost = FAULTS && edge_lost(a.fa, rc, p, lane_of(lw, j & 3u));
             uint64_t w = 0;
             bool rp = summ_bit(p);
             if (rp) {
@@ -330,16 +331,16 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, uint32_t*
   }
 }
 
-template <int MODE>
+template <int MODE, bool FAULTS>
 __global__ __launch_bounds__(kScanThreads) void sx_scan_kernel(ScanArgs a, uint32_t maj) {
   __shared__ uint4 summ4[kSummBits / 128];
   __shared__ uint64_t rws[kRwWords];
   __shared__ uint32_t lcnt;
   if (threadIdx.x == 0) lcnt = 0;  // (scan_body syncs before the first use)
   if (maj)
-    scan_body<1, MODE>(summ4, rws, &lcnt, a);
+    scan_body<1, MODE, FAULTS>(summ4, rws, &lcnt, a);
   else
-    scan_body<0, MODE>(summ4, rws, &lcnt, a);
+    scan_body<0, MODE, FAULTS>(summ4, rws, &lcnt, a);
   __syncthreads();
   if (threadIdx.x == 0) a.blk_cnt[blockIdx.x] = lcnt;
 }
@@ -540,12 +541,16 @@ hipError_t sx_scan(const SxGeom& g, const SxBufs& b, const FrontierBufs& lf, con
   const uint32_t grid = scan_grid(g.nown);
   a.per_block = scan_per_block(g.nown, grid);
   a.seg_cap = (uint64_t)g.k * a.per_block;  // grid * seg_cap <= k * (nown rounded up): sx_carve's cap
+#define GOSSIP_SX_SCAN(M)                                                     \
+  if (fa.any()) sx_scan_kernel<M, true><<<grid, kScanThreads, 0, st>>>(a, maj); \
+  else sx_scan_kernel<M, false><<<grid, kScanThreads, 0, st>>>(a, maj);
   switch (mode) {
-    case 1: sx_scan_kernel<1><<<grid, kScanThreads, 0, st>>>(a, maj); break;
-    case 2: sx_scan_kernel<2><<<grid, kScanThreads, 0, st>>>(a, maj); break;
-    case 3: sx_scan_kernel<3><<<grid, kScanThreads, 0, st>>>(a, maj); break;
+    case 1: GOSSIP_SX_SCAN(1) break;
+    case 2: GOSSIP_SX_SCAN(2) break;
+    case 3: GOSSIP_SX_SCAN(3) break;
     default: return hipErrorInvalidValue;
   }
+#undef GOSSIP_SX_SCAN
   const uint32_t* blk = b.msg_cnt + g.G + 2;
   owner_count_kernel<<<grid, 256, 0, st>>>(b.msg, a.seg_cap, blk, b.msg_cnt, g.G);
   owner_scatter_kernel<<<grid, 256, 0, st>>>(b.msg, a.seg_cap, blk, b.msg_out, b.msg_cnt, b.msg_fill, g.G);
