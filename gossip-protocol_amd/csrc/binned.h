@@ -55,7 +55,9 @@ struct BinGeom {
   uint32_t apply_grid;   // host only: persistent apply blocks (0 = one per tile; gossip_set_param)
 };
 
-BinGeom make_bin_geom(uint64_t N, uint32_t k);
+// big: regions of up to 2 * kMaxSenders senders and 2 * kRecPerRegion records (one shard
+// past kMaxTilesD tiles: the emit's 16-bit packed tile counters, binned.hip V = 4)
+BinGeom make_bin_geom(uint64_t N, uint32_t k, bool big = false);
 bool bin_path_ok(uint64_t N, uint32_t k, uint32_t W, uint32_t G);
 
 struct BinBufs {

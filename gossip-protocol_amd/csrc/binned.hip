@@ -71,11 +71,11 @@ __device__ __forceinline__ T rec_ld(const T* p) {
   if constexpr ((GOSSIP_NT_REC & BIT) != 0) return __builtin_nontemporal_load(p);
   else return *p;
 }
-// record id word: p_local [0,14) | n_local [14,27) | flags.  K1 rewrites every
+// record id word: p_local [0,14) | n_local [14,28) | flags.  K1 rewrites every
 // id each round, so a flag never outlives its round.
-constexpr uint32_t kIdVZ = 1u << 27;  // no push on this record (sender empty, or the peer already full)
-constexpr uint32_t kIdVF = 1u << 28;  // no pull (sender full, or the peer empty)
-constexpr uint32_t kIdNMask = (1u << 13) - 1u;
+constexpr uint32_t kIdVZ = 1u << 28;  // no push on this record (sender empty, or the peer already full)
+constexpr uint32_t kIdVF = 1u << 29;  // no pull (sender full, or the peer empty)
+constexpr uint32_t kIdNMask = (1u << 14) - 1u;
 
 __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {
   // blocks are dealt round-robin over the 8 XCDs: give each XCD a contiguous
@@ -147,6 +147,48 @@ __device__ __forceinline__ uint32_t region_offsets(uint32_t* cur, uint32_t nt, u
   return total;
 }
 
+// region_offsets over 16-bit counters packed two per word (tile d in half d & 1 of
+// cur[d >> 1]; regions of <= 32768 records, so no half overflows)
+__device__ __forceinline__ uint32_t region_offsets_packed(uint32_t* cur, uint32_t nt, uint16_t* off_row,
+                                                          uint32_t* wsum, uint32_t* wpre) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t nw = (nt + 1) >> 1;  // this thread: whole words [lo, hi)
+  const uint32_t per = (nw + kEmitThreads - 1) / kEmitThreads;
+  const uint32_t lo = min(tid * per, nw), hi = min(lo + per, nw);
+  uint32_t mine = 0;
+  for (uint32_t w = lo; w < hi; ++w) mine += (cur[w] & 0xFFFFu) + (cur[w] >> 16);
+  uint32_t inc = mine;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if (lane >= (uint32_t)o) inc += y;
+  }
+  if (lane == 63) wsum[wave] = inc;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t a = 0;
+    for (int w = 0; w < kEmitThreads / 64; ++w) {
+      wpre[w] = a;
+      a += wsum[w];
+    }
+    wpre[kEmitThreads / 64] = a;
+  }
+  __syncthreads();
+  uint32_t run = wpre[wave] + inc - mine;
+  for (uint32_t w = lo; w < hi; ++w) {
+    const uint32_t c0 = cur[w] & 0xFFFFu, c1 = cur[w] >> 16;
+    const uint32_t r0 = run, r1 = run + c0;
+    cur[w] = r0 | (r1 << 16);
+    off_row[2 * w] = (uint16_t)r0;
+    if (2 * w + 1 < nt) off_row[2 * w + 1] = (uint16_t)r1;
+    run = r1 + c1;
+  }
+  const uint32_t total = wpre[kEmitThreads / 64];
+  if (tid == 0) off_row[nt] = (uint16_t)total;
+  __syncthreads();
+  return total;
+}
+
 // KREG > 0: the k (<= KREG) peers of each sender stay in registers between passes.
 // FAULTS: edge loss / partitions active; off, none of that code exists.
 // V = 0: one shard.  V = 1, 2: one pass of a sharded dense round (EmitRange):
@@ -156,7 +198,10 @@ __device__ __forceinline__ uint32_t region_offsets(uint32_t* cur, uint32_t nt, u
 // counters can cover kSbMaxTiles tiles of the whole image.  V = 3: one shard
 // past 4096 tiles (N > 2^26): the sender values are not staged in LDS (the
 // tile counters take that room) but re-read from S — the region's slice, which
-// this block has just streamed, so the reads hit L2.
+// this block has just streamed, so the reads hit L2.  V = 4: as V = 3 with regions
+// twice as large (up to 16384 senders, 32768 records; 16-bit tile counters packed in
+// pairs make the room), so the runs stay twice as long at N > 2^26; no next-region
+// prefetch (its registers).
 template <int KREG, bool FAULTS, int V>
 __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const uint64_t* __restrict__ S, BinBufs b,
                                                                   uint32_t R, uint32_t t, uint32_t key0,
@@ -164,10 +209,11 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
                                                                   Faults fa, EmitRange er) {
   constexpr bool SHARD = V == 1 || V == 2;
   constexpr bool STAGE = V == 0 || V == 1;  // sender values staged in LDS
+  constexpr bool BIG = V == 4;               // packed 16-bit tile counters, double regions
   constexpr uint32_t kMaxT = V >= 2 ? kSbMaxTiles : kMaxTilesD;
-  constexpr uint32_t kMaxS = kMaxSenders;
-  __shared__ uint32_t cur[kMaxT];
-  __shared__ uint32_t st_ids[kRecPerRegion];  // p_local | n_local << 14, sorted by destination tile
+  constexpr uint32_t kMaxS = BIG ? 2 * kMaxSenders : kMaxSenders;
+  __shared__ uint32_t cur[BIG ? kMaxT / 2 : kMaxT];
+  __shared__ uint32_t st_ids[BIG ? 2 * kRecPerRegion : kRecPerRegion];  // p_local | n_local << 14, by tile
   __shared__ uint64_t sval[STAGE ? kMaxS : 1];  // S_t of each sender, once (not once per record)
   __shared__ uint32_t wsum[kEmitThreads / 64];
   __shared__ uint32_t wpre[kEmitThreads / 64 + 1];
@@ -204,20 +250,33 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
   // that overlaps the all-gather, or the rest)
   const uint32_t nr = SHARD ? er.rs.n : g.nt_s;
   auto region = [&](uint32_t r) -> uint32_t { return SHARD ? er.rs.at(r) : r; };
-  if (blockIdx.x < nr) load_values(region(blockIdx.x), v);
+  auto count_tile = [&](uint32_t tl) {
+    if constexpr (BIG) atomicAdd(&cur[tl >> 1], 1u << ((tl & 1u) << 4));
+    else atomicAdd(&cur[tl], 1u);
+  };
+  auto place_tile = [&](uint32_t tl) -> uint32_t {
+    if constexpr (BIG) {
+      const uint32_t sh = (tl & 1u) << 4;
+      return (atomicAdd(&cur[tl >> 1], 1u << sh) >> sh) & 0xFFFFu;
+    } else {
+      return atomicAdd(&cur[tl], 1u);
+    }
+  };
+  if (!BIG && blockIdx.x < nr) load_values(region(blockIdx.x), v);
   for (uint32_t r = blockIdx.x; r < nr; r += gridDim.x) {
   const uint32_t s = region(r);
   const uint64_t base = (uint64_t)s << g.ts_log;
   const uint32_t nsend = (uint32_t)min<uint64_t>(g.ts, nsnd - base);
   __syncthreads();  // the previous region's write-out has read cur/st_ids/sval
 
-  for (uint32_t d = tid; d < g.nt_d; d += kEmitThreads) cur[d] = 0;
+  for (uint32_t d = tid; d < (BIG ? (g.nt_d + 1) >> 1 : g.nt_d); d += kEmitThreads) cur[d] = 0;
+  if (BIG) load_values(s, v);
 #pragma unroll
   for (uint32_t q = 0; q < kQ; ++q) {
     const uint32_t i = tid + q * kEmitThreads;
     if (STAGE && i < g.ts) sval[i] = v[q];
   }
-  if (r + gridDim.x < nr) load_values(region(r + gridDim.x), vn);
+  if (!BIG && r + gridDim.x < nr) load_values(region(r + gridDim.x), vn);
   __syncthreads();
   // pass A: per-destination-tile counts of the records (edges that carry something)
   uint32_t pr[KREG > 0 ? kQ * KREG : 1];
@@ -281,7 +340,7 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
         if ((ed[q] >> (2 * j)) & 3u) {
           uint32_t tl, pl;
           tile_of(pr[q * KREG + j], &tl, &pl);
-          atomicAdd(&cur[tl], 1u);
+          count_tile(tl);
         }
   } else {
     for (uint32_t q = 0; q < kQ; ++q) {
@@ -301,13 +360,15 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
         if (FAULTS && edge_lost(fa, rc, p, lane_of(lw, j & 3u))) continue;
         uint32_t tl, pl;
         if (!tile_of(p, &tl, &pl)) continue;
-        if (peer_filter(d, p, filt, b.nzb, b.fullb)) atomicAdd(&cur[tl], 1u);
+        if (peer_filter(d, p, filt, b.nzb, b.fullb)) count_tile(tl);
       }
     }
   }
   __syncthreads();
 
-  const uint32_t total = region_offsets(cur, g.nt_d, b.off + (size_t)s * (g.nt_d + 1), wsum, wpre);
+  uint16_t* off_row = b.off + (size_t)s * (g.nt_d + 1);
+  const uint32_t total = BIG ? region_offsets_packed(cur, g.nt_d, off_row, wsum, wpre)
+                             : region_offsets(cur, g.nt_d, off_row, wsum, wpre);
 
   // pass B: each record to its slot (k <= KREG: the peers and directions from
   // registers; else the same draws and probes again)
@@ -321,7 +382,7 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
         if (!d) continue;
         uint32_t tl, pl;
         tile_of(pr[q * KREG + j], &tl, &pl);
-        const uint32_t pos = atomicAdd(&cur[tl], 1u);
+        const uint32_t pos = place_tile(tl);
         st_ids[pos] = pl | (i << kTileDLog) | dir_flags(d);
       }
     }
@@ -345,7 +406,7 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
         if (!tile_of(p, &tl, &pl)) continue;
         const uint32_t d = peer_filter(d0, p, filt, b.nzb, b.fullb);
         if (!d) continue;
-        const uint32_t pos = atomicAdd(&cur[tl], 1u);
+        const uint32_t pos = place_tile(tl);
         st_ids[pos] = pl | (i << kTileDLog) | dir_flags(d);
       }
     }
@@ -361,10 +422,12 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
     // a read-modify-write: profiles/r01_experiments/microbench5_scattered_pieces.jsonl)
     rec_st<1>(&gids[e], id);
     if (STAGE) rec_st<1>(&gvals[e], sval[(id >> kTileDLog) & kIdNMask]);
-    if (V == 3) rec_st<1>(&gvals[e], S[base + ((id >> kTileDLog) & kIdNMask)]);
+    if (V >= 3) rec_st<1>(&gvals[e], S[base + ((id >> kTileDLog) & kIdNMask)]);
   }
+  if constexpr (!BIG) {
 #pragma unroll
-  for (uint32_t q = 0; q < kQ; ++q) v[q] = vn[q];
+    for (uint32_t q = 0; q < kQ; ++q) v[q] = vn[q];
+  }
   }
 }
 
@@ -752,12 +815,12 @@ uint32_t apply_grid(const BinGeom& g) {
 
 }  // namespace
 
-BinGeom make_bin_geom(uint64_t N, uint32_t k) {
+BinGeom make_bin_geom(uint64_t N, uint32_t k, bool big) {
   BinGeom g{};
   g.N = N;
   g.k = k;
-  uint32_t ts = kMaxSenders, lg = 13;
-  while (ts * k > kRecPerRegion) {
+  uint32_t ts = big ? 2 * kMaxSenders : kMaxSenders, lg = big ? 14 : 13;
+  while (ts * k > (big ? 2 * kRecPerRegion : kRecPerRegion)) {
     ts >>= 1;
     --lg;
   }
@@ -811,7 +874,11 @@ hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, 
   } else {                                                                \
     if (fa.any()) GOSSIP_EMIT(0, true, VV); else GOSSIP_EMIT(0, false, VV); \
   }
-  if (g.nt_d <= kMaxTilesD) {
+  if (g.ts > kMaxSenders || g.rp > kRecPerRegion) {  // make_bin_geom(big): V = 4
+    // the draws are redone in the placement pass: 16 senders per lane keep no room for
+    // their peers in registers (KREG = 2 spills 78 VGPRs)
+    if (fa.any()) GOSSIP_EMIT(0, true, 4); else GOSSIP_EMIT(0, false, 4);
+  } else if (g.nt_d <= kMaxTilesD) {
     GOSSIP_EMIT_V(0)
   } else {
     GOSSIP_EMIT_V(3)

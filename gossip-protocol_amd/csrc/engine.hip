@@ -1013,7 +1013,11 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
   bind_slices(e);
   if (e->mode != GOSSIP_MODE_FLOOD && e->mode != GOSSIP_MODE_ANTIENTROPY && !(cfg->flags & GOSSIP_FLAG_DIRECT) &&
       bin_path_ok(e->N, e->k, e->W, G)) {
-    e->bg = make_bin_geom(e->N, e->k);
+#ifndef GOSSIP_EMIT_BIG_TILES
+#define GOSSIP_EMIT_BIG_TILES 4096
+#endif
+    // past this many tiles the emit regions double (longer runs per tile, binned.hip V = 4)
+    e->bg = make_bin_geom(e->N, e->k, (e->N + kTileD - 1) / kTileD > GOSSIP_EMIT_BIG_TILES);
     const size_t bytes = bin_bytes(e->bg);
     if (hipMalloc(&e->bin_mem, bytes) != hipSuccess) {
       e->err = "hipMalloc of " + std::to_string(bytes) + " bytes (bins) failed";
