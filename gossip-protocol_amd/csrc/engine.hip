@@ -158,6 +158,15 @@ struct gossip_engine {
   void *xd_smem = nullptr, *xd_rmem = nullptr;
   uint64_t xd_rcap = 0, xd_nin = 0;
   uint32_t* xd_cnt_h = nullptr;  // pinned [G]
+  // class-coded state exchange for dense image rounds (sharded.h cc_*), plan kind 4
+  bool cc_planned = false;
+  double cc_frac = 0.75;  // gossip_set_param "cc_frac": at most this global fraction of mixed nodes
+  uint64_t* cc_bits = nullptr;  // [G][2][nwl] every shard's nz / full bitmaps (all-gather in place)
+  uint64_t* cc_vals = nullptr;  // [G][stride] the shards' mixed words
+  uint64_t cc_vals_cap = 0, cc_stride = 0;
+  uint32_t *cc_cnt = nullptr, *cc_pre = nullptr;
+  void* cc_tmp = nullptr;
+  size_t cc_tmp_bytes = 0;
   uint64_t* sx_host = nullptr;  // pinned: [G + 2] counts / list bases
 
   hipEvent_t ev[kTimers][2] = {};
@@ -214,7 +223,8 @@ void free_all(gossip_engine* e) {
     if (b) (void)hipFree(b);
   if (e->bin_mem) (void)hipFree(e->bin_mem);
   if (e->fr_mem) (void)hipFree(e->fr_mem);
-  void* sx[] = {e->lf_mem, e->sx_mem, e->rare_recv, e->msg_recv, e->sb_mem, e->xd_smem, e->xd_rmem};
+  void* sx[] = {e->lf_mem, e->sx_mem, e->rare_recv, e->msg_recv, e->sb_mem, e->xd_smem, e->xd_rmem,
+                e->cc_bits, e->cc_vals, e->cc_cnt, e->cc_pre, e->cc_tmp};
   if (e->xd_cnt_h) (void)hipHostFree(e->xd_cnt_h);
   for (void* b : sx)
     if (b) (void)hipFree(b);
@@ -1139,6 +1149,9 @@ int gossip_set_param(gossip_engine_t* e, const char* name, double v) {
   } else if (n == "apply_grid") {
     if (v < 0 || v > 65536) return e->fail(GOSSIP_EINVAL, "apply_grid must be in [0, 65536]");
     e->bg.apply_grid = e->sbg.p.apply_grid = (uint32_t)v;
+  } else if (n == "cc_frac") {
+    if (v < 0 || v > 1) return e->fail(GOSSIP_EINVAL, "cc_frac must be in [0, 1] (0 = never)");
+    e->cc_frac = v;
   } else if (n == "xd_shards") {
     if (v < 0 || v > 1024) return e->fail(GOSSIP_EINVAL, "xd_shards must be in [0, 1024] (0 = never)");
     e->xd_shards = (uint32_t)v;
@@ -1265,7 +1278,7 @@ int gossip_reset(gossip_engine_t* e) {
   e->fr_valid = false;
   e->sx_valid = e->gtot_valid = e->last_sparse = false;
   // a dense_prepare or sparse plan of the old state must not leak into the next round
-  e->sb_pre = e->ev_pre_pending = e->sx_planned = false;
+  e->sb_pre = e->ev_pre_pending = e->sx_planned = e->xd_planned = e->cc_planned = false;
   if (e->frontier) {  // all-zero state: zero totals, empty bitmaps (D, P and dirty flags are zero between rounds)
     const size_t nwb = (e->N + 63) / 64 * 8;
     HIP_OK(e, hipMemsetAsync(e->fb.nzb, 0, nwb, e->stream));
@@ -1440,7 +1453,7 @@ int gossip_local_totals(gossip_engine_t* e, uint64_t* partial) {
 
 int gossip_sharded_plan(gossip_engine_t* e, const uint64_t* total, int32_t* kind) {
   if (!e || !kind) return GOSSIP_EINVAL;
-  e->sx_planned = e->xd_planned = false;
+  e->sx_planned = e->xd_planned = e->cc_planned = false;
   if (e->aex) {  // 2: an anti-entropy exchange round; -2: the global max vector is needed first
     *kind = e->aex_target_ok ? 2 : -2;
     return GOSSIP_OK;
@@ -1463,7 +1476,10 @@ int gossip_sharded_plan(gossip_engine_t* e, const uint64_t* total, int32_t* kind
   e->sx_maj = maj;
   e->sx_alld = all_d;
   e->xd_planned = !e->sx_planned && e->xd && e->xd_shards && e->G >= e->xd_shards;
-  *kind = e->sx_planned ? 1 : e->xd_planned ? 3 : 0;
+  // dense on the state image: class-coded when few nodes are mixed (neither empty nor full)
+  const double mixed = ((double)e->gtot[4 + e->R] - (double)e->gtot[0]) / (double)e->N;
+  e->cc_planned = !e->sx_planned && !e->xd_planned && e->cc_frac > 0 && mixed <= e->cc_frac;
+  *kind = e->sx_planned ? 1 : e->xd_planned ? 3 : e->cc_planned ? 4 : 0;
   return GOSSIP_OK;
 }
 
@@ -1537,6 +1553,79 @@ int gossip_sparse_commit(gossip_engine_t* e, uint64_t items, uint64_t* partial) 
   if (int rc = timer_collect(e)) return rc;
   e->sx_planned = false;
   e->last_sparse = true;
+  return GOSSIP_OK;
+}
+
+// --- class-coded state exchange (include/gossip.h gossip_cc_*) --------
+
+namespace {
+int cc_check(gossip_engine* e) {
+  if (!e) return GOSSIP_EINVAL;
+  if (!e->cc_planned) return e->fail(GOSSIP_ESTATE, "gossip_sharded_plan did not plan a class-coded round");
+  return set_dev(e);
+}
+}  // namespace
+
+int gossip_cc_send(gossip_engine_t* e, void** bits, uint64_t* bits_bytes, void** vals, uint64_t* count) {
+  if (!bits || !bits_bytes || !vals || !count) return GOSSIP_EINVAL;
+  if (int rc = cc_check(e)) return rc;
+  const uint64_t nwl = (e->Nl + 63) / 64;
+  if (!e->cc_bits) {
+    const size_t tab = ((size_t)e->G * nwl + 1) * 4;
+    e->cc_tmp_bytes = cc_scan_bytes(e->sg);
+    if (hipMalloc((void**)&e->cc_bits, (size_t)e->G * 2 * nwl * 8) != hipSuccess ||
+        hipMalloc((void**)&e->cc_cnt, tab) != hipSuccess || hipMalloc((void**)&e->cc_pre, tab) != hipSuccess ||
+        hipMalloc(&e->cc_tmp, std::max<size_t>(e->cc_tmp_bytes, 1)) != hipSuccess)
+      return e->fail(GOSSIP_ENOMEM, "hipMalloc of the class-coded exchange buffers failed");
+    HIP_OK(e, hipMemsetAsync(e->cc_bits, 0, (size_t)e->G * 2 * nwl * 8, e->stream));
+  }
+  if (int rc = sx_prepare(e)) return rc;  // exact occupancy bitmaps of S_t
+  uint64_t* own = e->cc_bits + (size_t)e->rank * 2 * nwl;
+  const uint64_t nwo = (e->nown + 63) / 64;  // (a short last shard: its tail words stay unused)
+  HIP_OK(e, hipMemcpyAsync(own, e->lf.nzb, nwo * 8, hipMemcpyDeviceToDevice, e->stream));
+  HIP_OK(e, hipMemcpyAsync(own + nwl, e->lf.fullb, nwo * 8, hipMemcpyDeviceToDevice, e->stream));
+  uint64_t* out = (uint64_t*)e->sb.rare_send;  // Nl 16-B items of room: Nl words here
+  HIP_OK(e, cc_compact(e->sg, e->sb, e->lf, e->S, out, e->stream));
+  e->sx_host[0] = 0;
+  HIP_OK(e, hipMemcpyAsync(e->sx_host, e->sb.wpos + nwo, 4, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(e, hipStreamSynchronize(e->stream));
+  *count = e->sx_host[0] & 0xFFFFFFFFull;
+  *bits = own;
+  *bits_bytes = 2 * nwl * 8;
+  *vals = out;
+  return GOSSIP_OK;
+}
+
+int gossip_cc_recv(gossip_engine_t* e, uint64_t stride, void** bits_image, void** vals) {
+  if (!bits_image || !vals) return GOSSIP_EINVAL;
+  if (int rc = cc_check(e)) return rc;
+  if (!e->cc_bits) return e->fail(GOSSIP_ESTATE, "gossip_cc_send first");
+  if (stride > e->Nl) return e->fail(GOSSIP_EINVAL, "stride %llu > nodes per shard", (unsigned long long)stride);
+  const uint64_t want = std::max<uint64_t>(stride * e->G, 1);
+  if (want > e->cc_vals_cap) {
+    HIP_OK(e, hipStreamSynchronize(e->stream));
+    if (e->cc_vals) HIP_OK(e, hipFree(e->cc_vals));
+    e->cc_vals = nullptr;
+    e->cc_vals_cap = 0;
+    const uint64_t cap = want + want / 4;
+    HIP_OK(e, hipMalloc((void**)&e->cc_vals, cap * 8));
+    e->cc_vals_cap = cap;
+  }
+  e->cc_stride = stride;
+  *bits_image = e->cc_bits;
+  *vals = e->cc_vals;
+  return GOSSIP_OK;
+}
+
+int gossip_cc_expand(gossip_engine_t* e, const uint64_t* counts) {
+  if (!counts) return GOSSIP_EINVAL;
+  if (int rc = cc_check(e)) return rc;
+  if (!e->cc_vals) return e->fail(GOSSIP_ESTATE, "gossip_cc_recv first");
+  for (uint32_t q = 0; q < e->G; ++q)
+    if (counts[q] > e->cc_stride) return e->fail(GOSSIP_EINVAL, "shard %u sent more mixed words than the stride", q);
+  HIP_OK(e, cc_expand(e->sg, e->cc_bits, e->cc_vals, e->cc_stride, e->cc_cnt, e->cc_pre, e->cc_tmp, e->cc_tmp_bytes,
+                      current_image(e), e->R, e->stream));
+  e->cc_planned = false;  // the round goes on as a dense one: gossip_dense_prepare, gossip_round_compute
   return GOSSIP_OK;
 }
 

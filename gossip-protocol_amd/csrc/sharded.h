@@ -70,4 +70,15 @@ hipError_t sx_scan(const SxGeom& g, const SxBufs& b, const FrontierBufs& lf, con
 // 6. received pushes into D (and the push-dirty flags unless all_d)
 hipError_t sx_apply(const FrontierBufs& lf, const SxItem* in, uint64_t n, bool all_d, hipStream_t st);
 
+// Class-coded state exchange for dense rounds on the state image: a shard
+// sends its two occupancy bitmaps (empty / full) and the words of its mixed nodes only.
+// The own mixed words in id order -> out; their count at b.wpos[nwl]
+hipError_t cc_compact(const SxGeom& g, const SxBufs& b, const FrontierBufs& lf, const uint64_t* S, uint64_t* out,
+                      hipStream_t st);
+size_t cc_scan_bytes(const SxGeom& g);  // device-scan scratch of cc_expand
+// bits = every shard's [nz, full] bitmaps ([q][2][nwl] words), vals = shard q's mixed words at
+// q * stride: writes the other shards' slices of image (cnt, pre: G * nwl + 1 words each)
+hipError_t cc_expand(const SxGeom& g, const uint64_t* bits, const uint64_t* vals, uint64_t stride, uint32_t* cnt,
+                     uint32_t* pre, void* tmp, size_t tmp_bytes, uint64_t* image, uint32_t R, hipStream_t st);
+
 }  // namespace gossip

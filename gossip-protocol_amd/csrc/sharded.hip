@@ -428,7 +428,109 @@ uint32_t grid_for(uint64_t n, uint32_t block, uint32_t cap) {
   return (uint32_t)(g == 0 ? 1 : (g < cap ? g : cap));
 }
 
+// --- class-coded state exchange (dense rounds on the state image) ---------------
+// A node's word is 0 (empty), all ones (full) or mixed; the two occupancy bits say which,
+// so a shard sends its bitmaps and the words of its mixed nodes only.
+
+__device__ __forceinline__ uint64_t cc_mixed(uint64_t nz, uint64_t full) { return nz & ~full; }
+
+// own mixed nodes per bitmap word
+__global__ __launch_bounds__(256) void cc_wcount_kernel(const uint64_t* __restrict__ nzb,
+                                                        const uint64_t* __restrict__ fullb, uint64_t nown,
+                                                        uint32_t* wcount) {
+  const uint64_t nw = (nown + 63) >> 6;
+  const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (w < nw) wcount[w] = (uint32_t)__popcll(cc_mixed(nzb[w], fullb[w]) & word_valid(w, nown));
+  else if (w == nw) wcount[w] = 0;
+}
+
+// the own mixed words in id order (a wave visits only the nonzero bitmap words, as list_kernel)
+__global__ __launch_bounds__(256) void cc_list_kernel(const uint64_t* __restrict__ nzb,
+                                                      const uint64_t* __restrict__ fullb,
+                                                      const uint64_t* __restrict__ S, uint64_t nown,
+                                                      const uint32_t* __restrict__ wpos, uint64_t* __restrict__ out) {
+  const uint64_t nw = (nown + 63) >> 6;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t w0 = (uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u);
+  const uint64_t wl = w0 + lane;
+  const uint64_t x = wl < nw ? cc_mixed(nzb[wl], fullb[wl]) & word_valid(wl, nown) : 0ull;
+  const uint32_t pl = wl < nw ? wpos[wl] : 0u;
+  uint64_t nzw = __ballot(x != 0);
+  while (nzw) {
+    const uint32_t src = (uint32_t)__builtin_ctzll(nzw);
+    nzw &= nzw - 1;
+    const uint64_t xw = __shfl(x, src, 64);
+    const uint32_t pos0 = __shfl(pl, src, 64);
+    if ((xw >> lane) & 1ull) out[pos0 + (uint32_t)__popcll(xw & ((1ull << lane) - 1ull))] = S[((w0 + src) << 6) + lane];
+  }
+}
+
+// mixed nodes per word of every shard's gathered bitmaps ([q][0 nz, 1 full][nwl])
+__global__ __launch_bounds__(256) void cc_wcount_all_kernel(const uint64_t* __restrict__ bits, uint64_t nwl,
+                                                            uint32_t G, uint32_t* cnt) {
+  const uint64_t total = (uint64_t)G * nwl;
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < total) {
+    const uint64_t q = i / nwl, w = i - q * nwl;
+    cnt[i] = (uint32_t)__popcll(cc_mixed(bits[(2 * q) * nwl + w], bits[(2 * q + 1) * nwl + w]));
+  } else if (i == total) {
+    cnt[i] = 0;
+  }
+}
+
+// the other shards' slices of the state image from their bits and mixed words
+__global__ __launch_bounds__(256) void cc_expand_kernel(const uint64_t* __restrict__ bits,
+                                                        const uint64_t* __restrict__ vals, uint64_t stride,
+                                                        const uint32_t* __restrict__ pre, uint64_t* __restrict__ image,
+                                                        uint64_t N, uint64_t Nl, uint32_t G, uint32_t rank,
+                                                        uint32_t R) {
+  const uint64_t nwl = (Nl + 63) >> 6, fm = full_mask1(R);
+  const uint64_t step = (uint64_t)gridDim.x * 256;
+  const uint64_t q = blockIdx.y;  // one grid row per shard
+  if (q == rank) return;          // the own slice is already in place
+  const uint64_t nq = q * Nl < N ? min(Nl, N - q * Nl) : 0ull;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nq; i += step) {
+    const uint64_t j = q * Nl + i;
+    const uint64_t w = i >> 6;
+    const uint64_t nz = bits[(2 * q) * nwl + w], full = bits[(2 * q + 1) * nwl + w];
+    const uint64_t bit = 1ull << (i & 63);
+    uint64_t v = 0;
+    if (full & bit) {
+      v = fm;
+    } else if (nz & bit) {
+      const uint64_t rank_in = (uint64_t)pre[q * nwl + w] - pre[q * nwl] + __popcll(cc_mixed(nz, full) & (bit - 1));
+      v = vals[q * stride + rank_in];
+    }
+    image[j] = v;
+  }
+}
+
 }  // namespace
+
+hipError_t cc_compact(const SxGeom& g, const SxBufs& b, const FrontierBufs& lf, const uint64_t* S, uint64_t* out,
+                      hipStream_t st) {
+  const uint64_t nwl = (g.nown + 63) / 64;
+  cc_wcount_kernel<<<grid_for(nwl + 1, 256, 1u << 30), 256, 0, st>>>(lf.nzb, lf.fullb, g.nown, b.wcount);
+  size_t tb = b.tmp_bytes;
+  hipError_t e = hipcub::DeviceScan::ExclusiveSum(b.tmp, tb, b.wcount, b.wpos, (int)(nwl + 1), st);
+  if (e != hipSuccess) return e;
+  cc_list_kernel<<<grid_for(nwl, 256, 1u << 30), 256, 0, st>>>(lf.nzb, lf.fullb, S, g.nown, b.wpos, out);
+  return hipGetLastError();
+}
+
+size_t cc_scan_bytes(const SxGeom& g) { return scan_tmp_bytes((uint64_t)g.G * ((g.Nl + 63) / 64) + 1); }
+
+hipError_t cc_expand(const SxGeom& g, const uint64_t* bits, const uint64_t* vals, uint64_t stride, uint32_t* cnt,
+                     uint32_t* pre, void* tmp, size_t tmp_bytes, uint64_t* image, uint32_t R, hipStream_t st) {
+  const uint64_t nwl = (g.Nl + 63) / 64, tot = (uint64_t)g.G * nwl;
+  cc_wcount_all_kernel<<<grid_for(tot + 1, 256, 1u << 30), 256, 0, st>>>(bits, nwl, g.G, cnt);
+  size_t tb = tmp_bytes;
+  hipError_t e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, pre, (int)(tot + 1), st);
+  if (e != hipSuccess) return e;
+  const dim3 grid(grid_for(g.Nl, 256, 2048), g.G);
+  cc_expand_kernel<<<grid, 256, 0, st>>>(bits, vals, stride, pre, image, g.N, g.Nl, g.G, g.rank, R);
+  return hipGetLastError();
+}
 
 size_t sx_bytes(const SxGeom& g) {
   const uint64_t nwl = (g.nown + 63) / 64, nwg = (g.N + 63) / 64;

@@ -95,6 +95,9 @@ SIGNATURES = [
     ("xd_serve", C.c_int, [P, C.POINTER(P)]),
     ("xd_response_recv", C.c_int, [P, C.POINTER(P)]),
     ("xd_finish", C.c_int, [P, U64P]),
+    ("cc_send", C.c_int, [P, C.POINTER(P), U64P, C.POINTER(P), U64P]),
+    ("cc_recv", C.c_int, [P, C.c_uint64, C.POINTER(P), C.POINTER(P)]),
+    ("cc_expand", C.c_int, [P, U64P]),
     ("read_bitset", C.c_int, [P, C.c_uint64, U64P, C.c_uint32]),
     ("read_rows", C.c_int, [P, U32P, C.c_uint64]),
     ("read_shard", C.c_int, [P, U64P, C.c_uint64]),

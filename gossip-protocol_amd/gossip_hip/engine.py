@@ -355,6 +355,24 @@ class AbiEngine:
         self._check(self._fn("xd_finish")(self._h, out.ctypes.data_as(_abi.U64P)))
         return out
 
+    # -- class-coded state all-gather (include/gossip.h gossip_cc_*; gossip_hip.sharded drives them) --
+    def cc_send(self):
+        """(own bitmaps pointer, their bytes, own mixed words pointer, word count)."""
+        bits, vals = C.c_void_p(), C.c_void_p()
+        nb, n = C.c_uint64(), C.c_uint64()
+        self._check(self._fn("cc_send")(self._h, C.byref(bits), C.byref(nb), C.byref(vals), C.byref(n)))
+        return bits.value, nb.value, vals.value, n.value
+
+    def cc_recv(self, stride: int):
+        """(bitmap image pointer, mixed words image pointer) for stride words per shard."""
+        bits, vals = C.c_void_p(), C.c_void_p()
+        self._check(self._fn("cc_recv")(self._h, C.c_uint64(stride), C.byref(bits), C.byref(vals)))
+        return bits.value, vals.value
+
+    def cc_expand(self, counts) -> None:
+        c = np.ascontiguousarray(counts, dtype=np.uint64)
+        self._check(self._fn("cc_expand")(self._h, c.ctypes.data_as(_abi.U64P)))
+
     def sparse_commit(self, items: int) -> np.ndarray:
         out = np.zeros(self.partial_len(), dtype=np.uint64)
         self._check(self._fn("sparse_commit")(self._h, items, out.ctypes.data_as(_abi.U64P)))

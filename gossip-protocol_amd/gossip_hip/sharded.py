@@ -16,6 +16,9 @@ without a GPU):
                 image: all-to-all of one item per live edge {p at its owner | flags,
                 S_t[n]} to p's owner, all-to-all of the pull replies back, all-reduce of
                 the partials;
+  class-coded   (kind 4, DESIGN.md §5.1: dense rounds while few nodes are mixed) the
+                state all-gather as each shard's two occupancy bitmaps (empty / full)
+                plus the words of its mixed nodes, expanded into the image on arrival;
   ANTIENTROPY   ("Design B") all-gather of the stale bits,
                 all-to-all of request items {p, n, V_t[n]} to p's owner and of its
                 replies V_t[p], all-reduce of the partials; the global max vector
@@ -199,6 +202,29 @@ def _xd_round(engine, comm: _Comm) -> np.ndarray:
     return engine.xd_finish()
 
 
+def _cc_round(engine, comm: _Comm) -> np.ndarray:
+    bits_p, nbytes, vals_p, count = engine.cc_send()
+    w, dev = comm.world, engine.on_device
+    counts = comm.all_gather_small(count) if w > 1 else [count]
+    stride = max(counts)
+    img_p, rvals_p = engine.cc_recv(stride)
+    if w > 1:
+        # the bitmaps in place (the own slot lies inside the image); the mixed words padded to
+        # the stride.  Both in flight while the engine runs the own-slice part of the round.
+        works = [comm.all_gather_async(_as_tensor(img_p, nbytes * w, dev), _as_tensor(bits_p, nbytes, dev))]
+        if stride:
+            works.append(comm.all_gather_async(_as_tensor(rvals_p, stride * 8 * w, dev),
+                                               _as_tensor(vals_p, stride * 8, dev)))
+        engine.dense_prepare()
+        for work in works:
+            if work is not None:
+                work.wait()
+    elif count:
+        _as_tensor(rvals_p, count * 8, dev).copy_(_as_tensor(vals_p, count * 8, dev))
+    engine.cc_expand(counts)
+    return engine.round_compute()
+
+
 def _bind_stream(engine, comm: _Comm):
     """Device collectives are enqueued on torch's current stream (the RCCL stream waits for
     it, and work.wait() / a synchronous collective make it wait in turn): the engine must
@@ -232,17 +258,21 @@ def _ae_round(engine, comm: _Comm) -> np.ndarray:
     return engine.ae_finish()
 
 
-def sharded_round(engine, group=None) -> dict:
+def sharded_round(engine, group=None, kinds: list | None = None) -> dict:
     """Runs one round of a sharded engine; every rank must call it.  With RCCL the engine is
     bound to the caller's current torch stream, so every kernel is ordered after the
-    collectives that feed it."""
+    collectives that feed it.  kinds: the round's plan kind is appended to it."""
     comm = _Comm(engine, group)
     _bind_stream(engine, comm)
     kind = _plan(engine, comm)
+    if kinds is not None:
+        kinds.append(kind)
     if kind == 2:
         partial = _ae_round(engine, comm)
     elif kind == 3:
         partial = _xd_round(engine, comm)
+    elif kind == 4:
+        partial = _cc_round(engine, comm)
     elif kind == 1:
         partial = _sparse_round(engine, comm)
     else:
@@ -252,13 +282,13 @@ def sharded_round(engine, group=None) -> dict:
     return engine.round_commit(partial)
 
 
-def sharded_run(engine, max_rounds: int, group=None) -> list:
-    """Rounds until converged (same stop rule as gossip_step)."""
+def sharded_run(engine, max_rounds: int, group=None, kinds: list | None = None) -> list:
+    """Rounds until converged (same stop rule as gossip_step); kinds collects the plan kinds."""
     if engine.on_device and torch.cuda.is_available():
         engine.set_stream(torch.cuda.current_stream().cuda_stream)
     out = []
     for _ in range(max_rounds):
-        st = sharded_round(engine, group)
+        st = sharded_round(engine, group, kinds)
         out.append(st)
         if st["converged"] or (engine.cfg.mode == 0 and st["messages"] == 0):
             break
@@ -396,10 +426,34 @@ def _lockstep_xd(engines):
     return [e.xd_finish() for e in engines]
 
 
+def _lockstep_cc(engines):
+    G = len(engines)
+    sends = [e.cc_send() for e in engines]  # (bits, bits bytes, mixed words, count)
+    counts = [c for _, _, _, c in sends]
+    stride = max(counts)
+    recvs = [e.cc_recv(stride) for e in engines]
+    for e in engines:  # the own-slice part, on the engines' streams
+        e.dense_prepare()
+    for e, (img_p, vals_p) in zip(engines, recvs):
+        nb = sends[0][1]
+        img = _as_tensor(img_p, nb * G, True, e.device)
+        vals = _as_tensor(vals_p, stride * 8 * G, True, e.device)
+        for q, (bp, _, sp, _) in enumerate(sends):
+            if engines[q] is not e:
+                img[q * nb // 8:(q + 1) * nb // 8].copy_(_as_tensor(bp, nb, True, engines[q].device))
+            if stride:
+                vals[q * stride:(q + 1) * stride].copy_(_as_tensor(sp, stride * 8, True, engines[q].device))
+    _sync_all(engines)
+    for e in engines:
+        e.cc_expand(counts)
+    return [e.round_compute() for e in engines]
+
+
 def lockstep_run(engines, max_rounds: int):
     """One process driving G shard engines (one per GPU, or several on one) through the
     same rounds as sharded_run, with device copies in place of the collectives.
-    Returns (per-round stats, per-round kind: 0 dense / 1 sparse / 2 ANTIENTROPY / 3 exchange dense)."""
+    Returns (per-round stats, per-round kind: 0 dense / 1 sparse / 2 ANTIENTROPY / 3 exchange dense /
+    4 class-coded dense)."""
     stats, kinds = [], []
     for _ in range(max_rounds):
         ks = [e.sharded_plan() for e in engines]
@@ -413,8 +467,8 @@ def lockstep_run(engines, max_rounds: int):
             ks = [e.sharded_plan(tot) for e in engines]
         assert len(set(ks)) == 1
         kinds.append(ks[0])
-        parts = (_lockstep_ae(engines) if ks[0] == 2 else _lockstep_xd(engines) if ks[0] == 3
-                 else _lockstep_sparse(engines) if ks[0] == 1 else _lockstep_dense(engines))
+        run = {1: _lockstep_sparse, 2: _lockstep_ae, 3: _lockstep_xd, 4: _lockstep_cc}.get(ks[0], _lockstep_dense)
+        parts = run(engines)
         tot = _lockstep_sum(parts)
         st = [e.round_commit(tot) for e in engines]
         assert all(s == st[0] for s in st)

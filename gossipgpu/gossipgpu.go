@@ -1,5 +1,5 @@
 // Package gossipgpu binds the MI355X gossip-round engine (libgossip_hip.so, the C ABI of
-// include/gossip.h, ABI v4) for Go hosts such as 0xSherlokMo/gossip-protocol's main.go.
+// include/gossip.h, ABI v6) for Go hosts such as 0xSherlokMo/gossip-protocol's main.go.
 //
 // The reference floods each value once to its topology neighbours with blocking SyncRPCs
 // ((*NodeState).Gossip, main.go:65-89), one process per node.  Here one Engine holds every
@@ -36,7 +36,7 @@ import (
 )
 
 // ABIVersion is the gossip.h version this binding is written against.
-const ABIVersion = 5
+const ABIVersion = 6
 
 // Mode is a dissemination rule (DESIGN.md §2).
 type Mode uint32
@@ -614,4 +614,34 @@ func (e *Engine) XDResponseRecv() (uintptr, error) {
 func (e *Engine) XDFinish() ([]uint64, error) {
 	out := make([]uint64, e.PartialLen())
 	return out, e.call(C.gossip_xd_finish(e.h, u64p(out)))
+}
+
+// CCSend: the own occupancy bitmaps of a class-coded dense round (plan kind 4; [nz][full], bitsBytes
+// bytes, the own slot of the gathered bitmap image) and the own mixed words (count uint64 words).
+func (e *Engine) CCSend() (bits uintptr, bitsBytes uint64, vals uintptr, count uint64, err error) {
+	var b, v unsafe.Pointer
+	var nb, n C.uint64_t
+	if rc := C.gossip_cc_send(e.h, &b, &nb, &v, &n); rc != 0 {
+		return 0, 0, 0, 0, e.fail(rc)
+	}
+	return uintptr(b), uint64(nb), uintptr(v), uint64(n), nil
+}
+
+// CCRecv: the gathered bitmap image (ShardCount slots of bitsBytes) and room for stride mixed
+// words from every shard.
+func (e *Engine) CCRecv(stride uint64) (bitsImage, vals uintptr, err error) {
+	var b, v unsafe.Pointer
+	if rc := C.gossip_cc_recv(e.h, C.uint64_t(stride), &b, &v); rc != 0 {
+		return 0, 0, e.fail(rc)
+	}
+	return uintptr(b), uintptr(v), nil
+}
+
+// CCExpand rebuilds the state image from the gathered bitmaps and mixed words (counts: every
+// shard's count); the round then goes on with DensePrepare / RoundCompute.
+func (e *Engine) CCExpand(counts []uint64) error {
+	if len(counts) != int(e.cfg.ShardCount) {
+		return fmt.Errorf("gossipgpu: CCExpand wants %d counts", e.cfg.ShardCount)
+	}
+	return e.call(C.gossip_cc_expand(e.h, u64p(counts)))
 }

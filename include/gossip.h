@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define GOSSIP_ABI_VERSION 5u
+#define GOSSIP_ABI_VERSION 6u
 
 /* Dissemination modes. */
 enum gossip_mode {
@@ -139,6 +139,9 @@ int gossip_set_stream(gossip_engine_t* eng, void* hip_stream);
  *   "ae_cap"       ANTIENTROPY: edge-list capacity of sparse rounds (reallocates the list)
  *   "xd_shards"    sharded random modes: dense rounds run as exchange rounds (kind 3) when
  *                  G >= this (default 6; 0 = never, always the state all-gather)
+ *   "cc_frac"      sharded random modes: dense rounds on the state image exchange it
+ *                  class-coded (kind 4) while the mixed nodes (neither empty nor full) are
+ *                  at most this fraction of N (default 0.75; 0 never, 1 always)
  * Unknown names return GOSSIP_EINVAL. */
 int gossip_set_param(gossip_engine_t* eng, const char* name, double value);
 
@@ -197,6 +200,7 @@ int gossip_round_commit(gossip_engine_t* eng, const uint64_t* total, gossip_roun
  *            plan again with the sum;
  *   kind  0: dense round -> the exchange_buffers / round_compute sequence;
  *   kind  3: exchange dense round (no state image; see the gossip_xd_* calls below);
+ *   kind  4: dense round on a class-coded state all-gather (gossip_cc_* below);
  *   kind  1: sparse round:
  *     gossip_sparse_rare(&send, &count)        own rare nodes, 16-B items {node, value}
  *     all-gather of count, stride = max count
@@ -263,6 +267,24 @@ int gossip_xd_request_recv(gossip_engine_t* eng, uint64_t items, void** ids, voi
 int gossip_xd_serve(gossip_engine_t* eng, void** replies);
 int gossip_xd_response_recv(gossip_engine_t* eng, void** replies);
 int gossip_xd_finish(gossip_engine_t* eng, uint64_t* partial);
+
+/* --- class-coded state all-gather (random modes, W == 1, G > 1) --------
+ * A dense round on the state image whose all-gather sends, per shard, its two occupancy
+ * bitmaps of S_t (bit i of word w: node lo + 64w + i nonzero / full) and the words of its
+ * mixed nodes (nonzero, not full) in id order; empty and full nodes are implied.
+ * Per round, after gossip_sharded_plan -> kind 4:
+ *   gossip_cc_send(&bits, &bits_bytes, &vals, &count)  own bitmaps ([nz][full], bits_bytes
+ *                                                      = 2 * 8 * ceil(Nl / 64)), count words
+ *   all-gather of count, stride = max count
+ *   gossip_cc_recv(stride, &bits_image, &vals_image)   all-gather bits_bytes from every rank
+ *                                                      into bits_image (the own slot is bits:
+ *                                                      in place) and stride words into vals_image
+ *   gossip_cc_expand(counts[G])                        the state image from the two
+ *   then as kind 0 without gossip_exchange_buffers: gossip_dense_prepare (optional),
+ *   gossip_round_compute -> all-reduce(SUM) -> gossip_round_commit. */
+int gossip_cc_send(gossip_engine_t* eng, void** bits, uint64_t* bits_bytes, void** vals, uint64_t* count);
+int gossip_cc_recv(gossip_engine_t* eng, uint64_t stride, void** bits_image, void** vals_image);
+int gossip_cc_expand(gossip_engine_t* eng, const uint64_t* counts);
 
 /* Readout ("read" handler, main.go:123-130).  Bitset of one node (nwords >= W),
  * or the whole owned shard in logical order out[w * Nl_owned + i]. */

@@ -71,6 +71,11 @@ struct oracle_sim {
   uint32_t *xid, *xrid;
   uint64_t *xval, *xrval, *xrep_out, *xrep_in, *xnode;
   uint64_t xn_out, xn_in;
+  /* class-coded state all-gather (kind 4): every shard's [nz][full] bitmaps
+   * ([G][2][nwl]), the own mixed words, every shard's at q * cc_stride */
+  int cc_planned;
+  double cc_frac;
+  uint64_t *cc_bits, *cc_send, *cc_vals, cc_stride;
 };
 
 /* ---------------- Philox4x32-10 (Random123; rocRAND philox4x32_10.h:270-302) ---- */
@@ -229,6 +234,7 @@ int oracle_create(const gossip_config_t* cfg, int threads, oracle_sim_t** out) {
   s->counts = (uint64_t*)calloc(G, 8);
   s->sparse_frac = 0.25;
   s->xd_shards = 6;
+  s->cc_frac = 0.75;
   s->flood_edges = s->mode == GOSSIP_MODE_FLOOD && faulty;
   s->npend = cfg->stall_rounds > 1 ? cfg->stall_rounds - 1 : 1;
   if (cfg->stall_rounds && s->mode >= GOSSIP_MODE_PUSH && s->mode <= GOSSIP_MODE_PUSHPULL &&
@@ -254,6 +260,7 @@ void oracle_destroy(oracle_sim_t* s) {
   free(s->streak); free(s->pend); free(s->pend_n); free(s->skipE); free(s->skipE_n); free(s->ieo);
   free(s->aex_stale); free(s->req); free(s->loc); free(s->in); free(s->resp_out); free(s->resp_in);
   free(s->xid); free(s->xrid); free(s->xval); free(s->xrval); free(s->xrep_out); free(s->xrep_in); free(s->xnode);
+  free(s->cc_bits); free(s->cc_send); free(s->cc_vals);
   free(s);
 }
 
@@ -777,7 +784,7 @@ int oracle_local_totals(oracle_sim_t* s, uint64_t* partial) {
 
 int oracle_sharded_plan(oracle_sim_t* s, const uint64_t* total, int32_t* kind) {
   if (!s || !kind) return GOSSIP_EINVAL;
-  s->planned = s->xd_planned = 0;
+  s->planned = s->xd_planned = s->cc_planned = 0;
   if (s->aex) {
     *kind = s->aex_target_ok ? 2 : -2;
     return GOSSIP_OK;
@@ -800,7 +807,10 @@ int oracle_sharded_plan(oracle_sim_t* s, const uint64_t* total, int32_t* kind) {
   const double frac = s->sparse_frac_set ? s->sparse_frac : s->xd_shards && s->G >= s->xd_shards ? 0.1 : 0.25;
   s->planned = (notfull < nz ? notfull : nz) <= frac * (double)s->N;
   s->xd_planned = !s->planned && s->xd_shards && s->G >= s->xd_shards;
-  *kind = s->planned ? 1 : s->xd_planned ? 3 : 0;
+  /* the engine's class-coded all-gather: at most cc_frac mixed (nonzero, not full) nodes */
+  const double mixed = ((double)s->gtot[4 + s->R] - (double)s->gtot[0]) / (double)s->N;
+  s->cc_planned = !s->planned && !s->xd_planned && s->cc_frac > 0 && mixed <= s->cc_frac;
+  *kind = s->planned ? 1 : s->xd_planned ? 3 : s->cc_planned ? 4 : 0;
   return GOSSIP_OK;
 }
 
@@ -1039,6 +1049,78 @@ int oracle_xd_finish(oracle_sim_t* s, uint64_t* partial) {
   return GOSSIP_OK;
 }
 
+/* ---- class-coded state all-gather (include/gossip.h gossip_cc_*; the engine's
+ * csrc/sharded.hip cc_compact / cc_expand).  The image the dense round reads is the
+ * all-gathered S_t of oracle_exchange_buffers, rebuilt from each shard's classes:
+ * empty -> 0, full -> the R-bit mask, mixed -> its word (in id order). ---- */
+static uint64_t cc_full(const oracle_sim_t* s) { return s->R >= 64 ? ~0ull : ((1ull << s->R) - 1ull); }
+
+int oracle_cc_send(oracle_sim_t* s, void** bits, uint64_t* bits_bytes, void** vals, uint64_t* count) {
+  if (!s || !bits || !bits_bytes || !vals || !count) return GOSSIP_EINVAL;
+  if (!s->cc_planned) return GOSSIP_ESTATE;
+  const uint64_t nwl = (s->Nl + 63) / 64, fm = cc_full(s);
+  if (!s->cc_bits && !(s->cc_bits = (uint64_t*)calloc(2 * nwl * s->G, 8))) return GOSSIP_ENOMEM;
+  if (!s->cc_send && !(s->cc_send = (uint64_t*)calloc(s->Nl + 1, 8))) return GOSSIP_ENOMEM;
+  uint64_t* own = s->cc_bits + (size_t)s->rank * 2 * nwl;
+  memset(own, 0, 2 * nwl * 8);
+  uint64_t c = 0;
+  for (uint64_t i = 0; i < s->nown; ++i) {
+    const uint64_t v = s->S[i], bit = 1ull << (i & 63);
+    if (!v) continue;
+    own[i / 64] |= bit;
+    if (v == fm) own[nwl + i / 64] |= bit;
+    else s->cc_send[c++] = v;
+  }
+  *bits = own;
+  *bits_bytes = 2 * nwl * 8;
+  *vals = s->cc_send;
+  *count = c;
+  return GOSSIP_OK;
+}
+
+int oracle_cc_recv(oracle_sim_t* s, uint64_t stride, void** bits_image, void** vals_image) {
+  if (!s || !bits_image || !vals_image) return GOSSIP_EINVAL;
+  if (!s->cc_planned || !s->cc_bits) return GOSSIP_ESTATE;
+  if (stride > s->Nl) return GOSSIP_EINVAL;
+  free(s->cc_vals);
+  if (!(s->cc_vals = (uint64_t*)calloc(stride * s->G + 1, 8))) return GOSSIP_ENOMEM;
+  s->cc_stride = stride;
+  *bits_image = s->cc_bits;
+  *vals_image = s->cc_vals;
+  return GOSSIP_OK;
+}
+
+int oracle_cc_expand(oracle_sim_t* s, const uint64_t* counts) {
+  if (!s || !counts) return GOSSIP_EINVAL;
+  if (!s->cc_planned || !s->cc_vals) return GOSSIP_ESTATE;
+  const uint64_t nwl = (s->Nl + 63) / 64, fm = cc_full(s);
+  for (uint32_t q = 0; q < s->G; ++q) {
+    if (counts[q] > s->cc_stride) return GOSSIP_EINVAL;
+    uint64_t* img = s->recv + (size_t)q * s->Nl;
+    if (q == s->rank) {
+      memcpy(img, s->S, s->Nl * 8);
+      continue;
+    }
+    const uint64_t *nz = s->cc_bits + (size_t)q * 2 * nwl, *full = nz + nwl;
+    const uint64_t nq = (uint64_t)q * s->Nl < s->N ? (s->N - (uint64_t)q * s->Nl < s->Nl ? s->N - (uint64_t)q * s->Nl : s->Nl) : 0;
+    uint64_t c = 0;
+    for (uint64_t i = 0; i < nq; ++i) {
+      const uint64_t bit = 1ull << (i & 63);
+      uint64_t v = 0;
+      if (full[i / 64] & bit) v = fm;
+      else if (nz[i / 64] & bit) {
+        if (c >= counts[q]) return GOSSIP_EINVAL; /* more mixed nodes than words sent */
+        v = s->cc_vals[q * s->cc_stride + c++];
+      }
+      img[i] = v;
+    }
+    for (uint64_t i = nq; i < s->Nl; ++i) img[i] = 0;
+    if (c != counts[q]) return GOSSIP_EINVAL;
+  }
+  s->cc_planned = 0;
+  return GOSSIP_OK;
+}
+
 /* gossip_set_param: the engine's tuning knobs.  Only sparse_frac matters here (it picks the
  * sharded round protocol, which the gloo tests exercise); the rest steer engine kernel
  * choices that this restatement does not have, and are accepted as no-ops. */
@@ -1047,6 +1129,11 @@ int oracle_set_param(oracle_sim_t* s, const char* name, double value) {
   if (!strcmp(name, "sparse_frac")) {
     s->sparse_frac = value;
     s->sparse_frac_set = 1;
+    return GOSSIP_OK;
+  }
+  if (!strcmp(name, "cc_frac")) {
+    if (value < 0 || value > 1) return GOSSIP_EINVAL;
+    s->cc_frac = value;
     return GOSSIP_OK;
   }
   if (!strcmp(name, "xd_shards")) {

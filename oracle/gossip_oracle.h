@@ -76,6 +76,9 @@ int oracle_xd_request_recv(oracle_sim_t* s, uint64_t items, void** ids, void** v
 int oracle_xd_serve(oracle_sim_t* s, void** replies);
 int oracle_xd_response_recv(oracle_sim_t* s, void** replies);
 int oracle_xd_finish(oracle_sim_t* s, uint64_t* partial);
+int oracle_cc_send(oracle_sim_t* s, void** bits, uint64_t* bits_bytes, void** vals, uint64_t* count);
+int oracle_cc_recv(oracle_sim_t* s, uint64_t stride, void** bits_image, void** vals_image);
+int oracle_cc_expand(oracle_sim_t* s, const uint64_t* counts);
 
 int oracle_read_bitset(oracle_sim_t* s, uint64_t node, uint64_t* out, uint32_t nwords);
 int oracle_read_shard(oracle_sim_t* s, uint64_t* out, uint64_t n_words);

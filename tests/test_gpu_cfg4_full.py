@@ -24,9 +24,12 @@ pytestmark = pytest.mark.gpu
 N, R, K, SEED, G = 1 << 27, 64, 2, 0x5EED0004, 8
 THREADS = min(16, os.cpu_count() or 1)
 # auto: sparse rounds and exchange dense rounds (G = 8 >= xd_shards); dense: every round on the
-# state all-gather; exchange: every round an exchange dense round
-PLANS = {"auto": {}, "sparse": {"sparse_frac": 1.0}, "dense": {"sparse_frac": -1, "xd_shards": 0},
-         "exchange": {"sparse_frac": -1}, "auto_image": {"xd_shards": 0}}
+# state all-gather; exchange: every round an exchange dense round; classcoded:
+# every round on the class-coded all-gather (§5.1); auto_image: sparse rounds and dense rounds
+# on the image, class-coded while few nodes are mixed
+PLANS = {"auto": {}, "sparse": {"sparse_frac": 1.0}, "dense": {"sparse_frac": -1, "xd_shards": 0, "cc_frac": 0},
+         "exchange": {"sparse_frac": -1}, "classcoded": {"sparse_frac": -1, "xd_shards": 0, "cc_frac": 1},
+         "auto_image": {"xd_shards": 0}}
 
 
 @pytest.fixture(scope="module")
@@ -65,6 +68,8 @@ def test_cfg4_G8_lockstep_equals_single_engine(single_engine_run, plan):
         assert set(kinds) == {0}
     elif plan == "exchange":
         assert set(kinds) == {3}
+    elif plan == "classcoded":
+        assert set(kinds) == {4}
     for e in engines:
         assert e.hi - e.lo == 1 << 24
         assert np.array_equal(e.read_shard(), full[:, e.lo:e.hi])

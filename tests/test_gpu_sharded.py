@@ -19,11 +19,14 @@ CASES = [("pushpull", 2, 64, 1 << 20, 0x5EED0004, 4), ("push", 3, 1, 300001, 7, 
 IDS = ["pushpull-1M-G4", "push-ragged-G3", "pull-G2", "pushpull-k6-G2"]
 # (flags, gossip_set_param knobs) per plan
 PLANS = {"auto": (0, {}), "sparse": (0, {"sparse_frac": 1.0}), "sparse_alld": (0, {"sparse_frac": 1.0, "alld_frac": 0}),
-         "dense": (0, {"sparse_frac": -1, "xd_shards": 0}),
+         "dense": (0, {"sparse_frac": -1, "xd_shards": 0, "cc_frac": 0}),
+         # the state all-gather class-coded (bitmaps + mixed words)
+         "classcoded": (0, {"sparse_frac": -1, "xd_shards": 0, "cc_frac": 1}),
          # dense rounds as exchange rounds (items to the peer's owner, replies back)
          "exchange": (0, {"sparse_frac": -1, "xd_shards": 2}), "auto_exchange": (0, {"xd_shards": 2}),
          # dense sharded rounds on the direct kernels instead of the binned push/pull passes
-         "dense_direct": (FLAG_SHARD_DIRECT, {"sparse_frac": -1, "xd_shards": 0}),
+         "dense_direct": (FLAG_SHARD_DIRECT, {"sparse_frac": -1, "xd_shards": 0, "cc_frac": 0}),
+         "classcoded_direct": (FLAG_SHARD_DIRECT, {"sparse_frac": -1, "xd_shards": 0, "cc_frac": 1}),
          "auto_direct": (FLAG_SHARD_DIRECT, {"xd_shards": 0})}
 
 
@@ -51,6 +54,10 @@ def test_lockstep_shards_equal_one_engine(case, plan):
         assert set(kinds) == {0}
     elif plan == "exchange":
         assert set(kinds) == {3}
+    elif plan in ("classcoded", "classcoded_direct"):
+        assert set(kinds) == {4}
+    elif plan in ("auto", "auto_direct"):
+        assert 4 in kinds  # G < xd_shards: dense rounds with few mixed nodes go class-coded
     for e in engines:
         e.close()
 
@@ -83,7 +90,8 @@ def test_lockstep_dense_past_4096_tiles():
     want = ref.step(8)
     full = ref.read_shard()
     ref.close()
-    for plan, kind in (({"sparse_frac": -1, "xd_shards": 0}, 0), ({"sparse_frac": -1, "xd_shards": 2}, 3)):
+    for plan, kind in (({"sparse_frac": -1, "xd_shards": 0, "cc_frac": 0}, 0), ({"sparse_frac": -1, "xd_shards": 2}, 3),
+                       ({"sparse_frac": -1, "xd_shards": 0, "cc_frac": 1}, 4)):
         engines = [Engine(N, R, "pushpull", 2, 0x5EED0004, flags=1, shard_rank=r, shard_count=G, params=plan)
                    for r in range(G)]
         for e in engines:
@@ -95,12 +103,14 @@ def test_lockstep_dense_past_4096_tiles():
             e.close()
 
 
+@pytest.mark.parametrize("plan", [({"xd_shards": 2, "sparse_frac": -1}, 3),
+                                  ({"xd_shards": 0, "sparse_frac": -1, "cc_frac": 1}, 4)], ids=["exchange", "classcoded"])
 @pytest.mark.parametrize("faults", [dict(edge_loss=1 << 29, partitions=3), dict(edge_loss=1 << 29, stall_rounds=2),
                                     dict(edge_loss=1 << 30, partitions=2, stall_rounds=3)],
                          ids=["loss-partitions", "loss-stall", "all"])
-def test_lockstep_exchange_faults_stall(faults):
-    """Exchange dense rounds (every round) with edge loss, partitions and the stall mode
-    (DESIGN.md §2.8-2.9), G = 5 ragged shards, against one engine."""
+def test_lockstep_exchange_faults_stall(faults, plan):
+    """Exchange dense rounds and class-coded all-gathers (every round) with edge loss,
+    partitions and the stall mode, G = 5 ragged shards, against one engine."""
     N, R, G = 400009, 64, 5
     ref = Engine(N, R, "pushpull", 2, 0x5EED0006, flags=1, **faults)
     ref.inject_random()
@@ -108,11 +118,11 @@ def test_lockstep_exchange_faults_stall(faults):
     full = ref.read_shard()
     ref.close()
     engines = [Engine(N, R, "pushpull", 2, 0x5EED0006, flags=1, shard_rank=r, shard_count=G,
-                      params={"xd_shards": 2, "sparse_frac": -1}, **faults) for r in range(G)]
+                      params=plan[0], **faults) for r in range(G)]
     for e in engines:
         e.inject_random()
     got, kinds = run_lockstep(engines, 60)
-    assert got == want.stats and set(kinds) == {3}
+    assert got == want.stats and set(kinds) == {plan[1]}
     for e in engines:
         assert np.array_equal(e.read_shard(), full[:, e.lo:e.hi])
         e.close()

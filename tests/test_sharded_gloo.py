@@ -47,14 +47,18 @@ def _faults(name):
 
 
 # gossip_set_param knobs: sparse_frac picks sparse rounds, xd_shards the exchange dense rounds
-# (kind 3) instead of the state all-gather
+# (kind 3) instead of the state all-gather, cc_frac the class-coded all-gather
+# (kind 4, §5.1) instead of the plain one
 PLANS = {
     "auto": {},
     "sparse": {"sparse_frac": 1.0},
-    "dense": {"sparse_frac": -1, "xd_shards": 0},
+    "dense": {"sparse_frac": -1, "xd_shards": 0, "cc_frac": 0},
     "exchange": {"sparse_frac": -1, "xd_shards": 2},
     "auto-exchange": {"xd_shards": 2},
+    "classcoded": {"sparse_frac": -1, "xd_shards": 0, "cc_frac": 1},
 }
+# the kinds every round of a plan must have (random modes)
+PLAN_KINDS = {"sparse": {1}, "dense": {0}, "exchange": {3}, "classcoded": {4}}
 
 
 def _worker(rank, world, port, case, q, params=None):
@@ -74,8 +78,9 @@ def _worker(rank, world, port, case, q, params=None):
         e.inject(0, 0); e.inject(N - 1, 1); e.inject(N // 2, 2)
     else:
         e.inject_random()
-    stats = sharded_run(e, 200)
-    q.put((rank, e.lo, e.hi, stats, e.read_shard()))
+    kinds = []
+    stats = sharded_run(e, 200, kinds=kinds)
+    q.put((rank, e.lo, e.hi, stats, e.read_shard(), kinds))
     dist.destroy_process_group()
 
 
@@ -105,16 +110,22 @@ def test_two_ranks_equal_one(case, plan, world=2):
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    for rank, lo, hi, stats, shard in got:
+    for rank, lo, hi, stats, shard, kinds in got:
         assert stats == want.stats
         assert np.array_equal(shard, full[:, lo:hi])
+        if topo is not None or R > 64:
+            assert set(kinds) == {0}  # FLOOD and W > 1: the plain state all-gather only
+        elif plan in PLAN_KINDS:
+            assert set(kinds) == PLAN_KINDS[plan]
+        elif plan == "auto":
+            assert 4 in kinds and 1 in kinds  # sparse rounds and class-coded dense rounds at G < xd_shards
 
 
-@pytest.mark.parametrize("plan", ["exchange", "auto-exchange"])
+@pytest.mark.parametrize("plan", ["exchange", "auto-exchange", "classcoded"])
 @pytest.mark.parametrize("case", CASES[:5], ids=[c[0] for c in CASES[:5]])
 def test_three_ranks_exchange_equal_one(case, plan):
-    """Exchange dense rounds (items to the peer's owner, replies back) with
-    ragged shards: world 3."""
+    """Exchange dense rounds (items to the peer's owner, replies back) and the
+    class-coded all-gather (§5.1) with ragged shards: world 3."""
     test_two_ranks_equal_one(case, plan, world=3)
 
 
