@@ -161,12 +161,9 @@ struct gossip_engine {
   // class-coded state exchange for dense image rounds (sharded.h cc_*), plan kind 4
   bool cc_planned = false;
   double cc_frac = 0.75;  // gossip_set_param "cc_frac": at most this global fraction of mixed nodes
-  uint64_t* cc_bits = nullptr;  // [G][2][nwl] every shard's nz / full bitmaps (all-gather in place)
+  uint64_t* cc_bits = nullptr;  // [G][cc_slot_words] every shard's bitmaps + prefix (all-gather in place)
   uint64_t* cc_vals = nullptr;  // [G][stride] the shards' mixed words
   uint64_t cc_vals_cap = 0, cc_stride = 0;
-  uint32_t *cc_cnt = nullptr, *cc_pre = nullptr;
-  void* cc_tmp = nullptr;
-  size_t cc_tmp_bytes = 0;
   uint64_t* sx_host = nullptr;  // pinned: [G + 2] counts / list bases
 
   hipEvent_t ev[kTimers][2] = {};
@@ -224,7 +221,7 @@ void free_all(gossip_engine* e) {
   if (e->bin_mem) (void)hipFree(e->bin_mem);
   if (e->fr_mem) (void)hipFree(e->fr_mem);
   void* sx[] = {e->lf_mem, e->sx_mem, e->rare_recv, e->msg_recv, e->sb_mem, e->xd_smem, e->xd_rmem,
-                e->cc_bits, e->cc_vals, e->cc_cnt, e->cc_pre, e->cc_tmp};
+                e->cc_bits, e->cc_vals};
   if (e->xd_cnt_h) (void)hipHostFree(e->xd_cnt_h);
   for (void* b : sx)
     if (b) (void)hipFree(b);
@@ -1569,29 +1566,25 @@ int cc_check(gossip_engine* e) {
 int gossip_cc_send(gossip_engine_t* e, void** bits, uint64_t* bits_bytes, void** vals, uint64_t* count) {
   if (!bits || !bits_bytes || !vals || !count) return GOSSIP_EINVAL;
   if (int rc = cc_check(e)) return rc;
-  const uint64_t nwl = (e->Nl + 63) / 64;
+  const uint64_t nwl = (e->Nl + 63) / 64, slot = cc_slot_words(e->Nl);
   if (!e->cc_bits) {
-    const size_t tab = ((size_t)e->G * nwl + 1) * 4;
-    e->cc_tmp_bytes = cc_scan_bytes(e->sg);
-    if (hipMalloc((void**)&e->cc_bits, (size_t)e->G * 2 * nwl * 8) != hipSuccess ||
-        hipMalloc((void**)&e->cc_cnt, tab) != hipSuccess || hipMalloc((void**)&e->cc_pre, tab) != hipSuccess ||
-        hipMalloc(&e->cc_tmp, std::max<size_t>(e->cc_tmp_bytes, 1)) != hipSuccess)
-      return e->fail(GOSSIP_ENOMEM, "hipMalloc of the class-coded exchange buffers failed");
-    HIP_OK(e, hipMemsetAsync(e->cc_bits, 0, (size_t)e->G * 2 * nwl * 8, e->stream));
+    HIP_OK(e, hipMalloc((void**)&e->cc_bits, (size_t)e->G * slot * 8));
+    HIP_OK(e, hipMemsetAsync(e->cc_bits, 0, (size_t)e->G * slot * 8, e->stream));
   }
   if (int rc = sx_prepare(e)) return rc;  // exact occupancy bitmaps of S_t
-  uint64_t* own = e->cc_bits + (size_t)e->rank * 2 * nwl;
-  const uint64_t nwo = (e->nown + 63) / 64;  // (a short last shard: its tail words stay unused)
-  HIP_OK(e, hipMemcpyAsync(own, e->lf.nzb, nwo * 8, hipMemcpyDeviceToDevice, e->stream));
-  HIP_OK(e, hipMemcpyAsync(own + nwl, e->lf.fullb, nwo * 8, hipMemcpyDeviceToDevice, e->stream));
   uint64_t* out = (uint64_t*)e->sb.rare_send;  // Nl 16-B items of room: Nl words here
   HIP_OK(e, cc_compact(e->sg, e->sb, e->lf, e->S, out, e->stream));
+  uint64_t* own = e->cc_bits + (size_t)e->rank * slot;
+  const uint64_t nwo = (e->nown + 63) / 64;  // (a short last shard: its tail words stay zero)
+  HIP_OK(e, hipMemcpyAsync(own, e->lf.nzb, nwo * 8, hipMemcpyDeviceToDevice, e->stream));
+  HIP_OK(e, hipMemcpyAsync(own + nwl, e->lf.fullb, nwo * 8, hipMemcpyDeviceToDevice, e->stream));
+  HIP_OK(e, hipMemcpyAsync(own + 2 * nwl, e->sb.wpos, nwo * 4, hipMemcpyDeviceToDevice, e->stream));
   e->sx_host[0] = 0;
   HIP_OK(e, hipMemcpyAsync(e->sx_host, e->sb.wpos + nwo, 4, hipMemcpyDeviceToHost, e->stream));
   HIP_OK(e, hipStreamSynchronize(e->stream));
   *count = e->sx_host[0] & 0xFFFFFFFFull;
   *bits = own;
-  *bits_bytes = 2 * nwl * 8;
+  *bits_bytes = slot * 8;
   *vals = out;
   return GOSSIP_OK;
 }
@@ -1623,8 +1616,7 @@ int gossip_cc_expand(gossip_engine_t* e, const uint64_t* counts) {
   if (!e->cc_vals) return e->fail(GOSSIP_ESTATE, "gossip_cc_recv first");
   for (uint32_t q = 0; q < e->G; ++q)
     if (counts[q] > e->cc_stride) return e->fail(GOSSIP_EINVAL, "shard %u sent more mixed words than the stride", q);
-  HIP_OK(e, cc_expand(e->sg, e->cc_bits, e->cc_vals, e->cc_stride, e->cc_cnt, e->cc_pre, e->cc_tmp, e->cc_tmp_bytes,
-                      current_image(e), e->R, e->stream));
+  HIP_OK(e, cc_expand(e->sg, e->cc_bits, e->cc_vals, e->cc_stride, current_image(e), e->R, e->stream));
   e->cc_planned = false;  // the round goes on as a dense one: gossip_dense_prepare, gossip_round_compute
   return GOSSIP_OK;
 }

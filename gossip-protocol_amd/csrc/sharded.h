@@ -71,14 +71,19 @@ hipError_t sx_scan(const SxGeom& g, const SxBufs& b, const FrontierBufs& lf, con
 hipError_t sx_apply(const FrontierBufs& lf, const SxItem* in, uint64_t n, bool all_d, hipStream_t st);
 
 // Class-coded state exchange for dense rounds on the state image: a shard
-// sends its two occupancy bitmaps (empty / full) and the words of its mixed nodes only.
-// The own mixed words in id order -> out; their count at b.wpos[nwl]
+// sends its two occupancy bitmaps (empty / full), the mixed nodes before each bitmap word,
+// and the words of its mixed nodes only.  A shard's slot: [nz: nwl words][full: nwl words]
+// [prefix: nwl uint32, padded to whole words], nwl = ceil(Nl / 64).
+inline uint64_t cc_slot_words(uint64_t Nl) {
+  const uint64_t nwl = (Nl + 63) / 64;
+  return 2 * nwl + (nwl + 1) / 2;
+}
+// The own mixed words in id order -> out; the prefix at b.wpos, their count at b.wpos[nwl]
 hipError_t cc_compact(const SxGeom& g, const SxBufs& b, const FrontierBufs& lf, const uint64_t* S, uint64_t* out,
                       hipStream_t st);
-size_t cc_scan_bytes(const SxGeom& g);  // device-scan scratch of cc_expand
-// bits = every shard's [nz, full] bitmaps ([q][2][nwl] words), vals = shard q's mixed words at
-// q * stride: writes the other shards' slices of image (cnt, pre: G * nwl + 1 words each)
-hipError_t cc_expand(const SxGeom& g, const uint64_t* bits, const uint64_t* vals, uint64_t stride, uint32_t* cnt,
-                     uint32_t* pre, void* tmp, size_t tmp_bytes, uint64_t* image, uint32_t R, hipStream_t st);
+// slots = every shard's slot ([G][cc_slot_words]), vals = shard q's mixed words at q * stride:
+// writes the other shards' slices of image
+hipError_t cc_expand(const SxGeom& g, const uint64_t* slots, const uint64_t* vals, uint64_t stride,
+                     uint64_t* image, uint32_t R, hipStream_t st);
 
 }  // namespace gossip

@@ -465,43 +465,46 @@ __global__ __launch_bounds__(256) void cc_list_kernel(const uint64_t* __restrict
   }
 }
 
-// mixed nodes per word of every shard's gathered bitmaps ([q][0 nz, 1 full][nwl])
-__global__ __launch_bounds__(256) void cc_wcount_all_kernel(const uint64_t* __restrict__ bits, uint64_t nwl,
-                                                            uint32_t G, uint32_t* cnt) {
-  const uint64_t total = (uint64_t)G * nwl;
-  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i < total) {
-    const uint64_t q = i / nwl, w = i - q * nwl;
-    cnt[i] = (uint32_t)__popcll(cc_mixed(bits[(2 * q) * nwl + w], bits[(2 * q + 1) * nwl + w]));
-  } else if (i == total) {
-    cnt[i] = 0;
-  }
-}
-
-// the other shards' slices of the state image from their bits and mixed words
-__global__ __launch_bounds__(256) void cc_expand_kernel(const uint64_t* __restrict__ bits,
+// The other shards' slices of the state image from their slots and mixed words.  A wave
+// expands kCcUnroll bitmap words (64 nodes each) per step, their loads issued together.
+constexpr uint32_t kCcUnroll = 4;
+__global__ __launch_bounds__(256) void cc_expand_kernel(const uint64_t* __restrict__ slots, uint64_t slot_words,
                                                         const uint64_t* __restrict__ vals, uint64_t stride,
-                                                        const uint32_t* __restrict__ pre, uint64_t* __restrict__ image,
-                                                        uint64_t N, uint64_t Nl, uint32_t G, uint32_t rank,
-                                                        uint32_t R) {
-  const uint64_t nwl = (Nl + 63) >> 6, fm = full_mask1(R);
-  const uint64_t step = (uint64_t)gridDim.x * 256;
+                                                        uint64_t* __restrict__ image, uint64_t N, uint64_t Nl,
+                                                        uint32_t rank, uint32_t R) {
   const uint64_t q = blockIdx.y;  // one grid row per shard
   if (q == rank) return;          // the own slice is already in place
-  const uint64_t nq = q * Nl < N ? min(Nl, N - q * Nl) : 0ull;
-  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nq; i += step) {
-    const uint64_t j = q * Nl + i;
-    const uint64_t w = i >> 6;
-    const uint64_t nz = bits[(2 * q) * nwl + w], full = bits[(2 * q + 1) * nwl + w];
-    const uint64_t bit = 1ull << (i & 63);
-    uint64_t v = 0;
-    if (full & bit) {
-      v = fm;
-    } else if (nz & bit) {
-      const uint64_t rank_in = (uint64_t)pre[q * nwl + w] - pre[q * nwl] + __popcll(cc_mixed(nz, full) & (bit - 1));
-      v = vals[q * stride + rank_in];
+  const uint64_t nwl = (Nl + 63) >> 6, fm = full_mask1(R);
+  const uint64_t nq = q * Nl < N ? min(Nl, N - q * Nl) : 0ull, nwq = (nq + 63) >> 6;
+  const uint64_t* nzb = slots + q * slot_words;
+  const uint64_t* fb = nzb + nwl;
+  const uint32_t* pre = (const uint32_t*)(fb + nwl);
+  const uint64_t* qv = vals + q * stride;
+  uint64_t* img = image + q * Nl;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t below = (1ull << lane) - 1ull, bit = 1ull << lane;
+  const uint64_t wave = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = (uint64_t)gridDim.x * 4;
+  for (uint64_t w0 = wave * kCcUnroll; w0 < nwq; w0 += nwaves * kCcUnroll) {
+    uint64_t nz[kCcUnroll], fu[kCcUnroll];
+    uint32_t pr[kCcUnroll];
+#pragma unroll
+    for (uint32_t u = 0; u < kCcUnroll; ++u) {
+      const bool in = w0 + u < nwq;
+      nz[u] = in ? nzb[w0 + u] : 0ull;
+      fu[u] = in ? fb[w0 + u] : 0ull;
+      pr[u] = in ? pre[w0 + u] : 0u;
     }
-    image[j] = v;
+    uint64_t v[kCcUnroll];
+#pragma unroll
+    for (uint32_t u = 0; u < kCcUnroll; ++u) {
+      const uint64_t mixed = cc_mixed(nz[u], fu[u]);
+      v[u] = (fu[u] & bit) ? fm : (mixed & bit) ? qv[pr[u] + (uint32_t)__popcll(mixed & below)] : 0ull;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kCcUnroll; ++u) {
+      const uint64_t i = ((w0 + u) << 6) + lane;
+      if (i < nq) img[i] = v[u];
+    }
   }
 }
 
@@ -518,17 +521,11 @@ hipError_t cc_compact(const SxGeom& g, const SxBufs& b, const FrontierBufs& lf, 
   return hipGetLastError();
 }
 
-size_t cc_scan_bytes(const SxGeom& g) { return scan_tmp_bytes((uint64_t)g.G * ((g.Nl + 63) / 64) + 1); }
-
-hipError_t cc_expand(const SxGeom& g, const uint64_t* bits, const uint64_t* vals, uint64_t stride, uint32_t* cnt,
-                     uint32_t* pre, void* tmp, size_t tmp_bytes, uint64_t* image, uint32_t R, hipStream_t st) {
-  const uint64_t nwl = (g.Nl + 63) / 64, tot = (uint64_t)g.G * nwl;
-  cc_wcount_all_kernel<<<grid_for(tot + 1, 256, 1u << 30), 256, 0, st>>>(bits, nwl, g.G, cnt);
-  size_t tb = tmp_bytes;
-  hipError_t e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, pre, (int)(tot + 1), st);
-  if (e != hipSuccess) return e;
-  const dim3 grid(grid_for(g.Nl, 256, 2048), g.G);
-  cc_expand_kernel<<<grid, 256, 0, st>>>(bits, vals, stride, pre, image, g.N, g.Nl, g.G, g.rank, R);
+hipError_t cc_expand(const SxGeom& g, const uint64_t* slots, const uint64_t* vals, uint64_t stride,
+                     uint64_t* image, uint32_t R, hipStream_t st) {
+  const uint64_t nwl = (g.Nl + 63) / 64;
+  const dim3 grid(grid_for((nwl + kCcUnroll - 1) / kCcUnroll, 4, 2048), g.G);
+  cc_expand_kernel<<<grid, 256, 0, st>>>(slots, cc_slot_words(g.Nl), vals, stride, image, g.N, g.Nl, g.rank, R);
   return hipGetLastError();
 }
 

@@ -270,11 +270,12 @@ int gossip_xd_finish(gossip_engine_t* eng, uint64_t* partial);
 
 /* --- class-coded state all-gather (random modes, W == 1, G > 1) --------
  * A dense round on the state image whose all-gather sends, per shard, its two occupancy
- * bitmaps of S_t (bit i of word w: node lo + 64w + i nonzero / full) and the words of its
- * mixed nodes (nonzero, not full) in id order; empty and full nodes are implied.
+ * bitmaps of S_t (bit i of word w: node lo + 64w + i nonzero / full), the number of mixed
+ * nodes (nonzero, not full) before each bitmap word, and the words of its mixed nodes in id
+ * order; empty and full nodes are implied.  A shard's slot, nwl = ceil(Nl / 64):
+ * [nz: nwl uint64][full: nwl uint64][prefix: nwl uint32, padded to 8 bytes] = bits_bytes.
  * Per round, after gossip_sharded_plan -> kind 4:
- *   gossip_cc_send(&bits, &bits_bytes, &vals, &count)  own bitmaps ([nz][full], bits_bytes
- *                                                      = 2 * 8 * ceil(Nl / 64)), count words
+ *   gossip_cc_send(&bits, &bits_bytes, &vals, &count)  own slot, own count mixed words
  *   all-gather of count, stride = max count
  *   gossip_cc_recv(stride, &bits_image, &vals_image)   all-gather bits_bytes from every rank
  *                                                      into bits_image (the own slot is bits:

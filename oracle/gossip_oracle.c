@@ -71,8 +71,9 @@ struct oracle_sim {
   uint32_t *xid, *xrid;
   uint64_t *xval, *xrval, *xrep_out, *xrep_in, *xnode;
   uint64_t xn_out, xn_in;
-  /* class-coded state all-gather (kind 4): every shard's [nz][full] bitmaps
-   * ([G][2][nwl]), the own mixed words, every shard's at q * cc_stride */
+  /* class-coded state all-gather (kind 4): every shard's slot ([nz][full]
+   * bitmaps, nwl words each, then nwl uint32 prefixes: the mixed nodes before each bitmap
+   * word), the own mixed words, every shard's at q * cc_stride */
   int cc_planned;
   double cc_frac;
   uint64_t *cc_bits, *cc_send, *cc_vals, cc_stride;
@@ -1054,25 +1055,28 @@ int oracle_xd_finish(oracle_sim_t* s, uint64_t* partial) {
  * all-gathered S_t of oracle_exchange_buffers, rebuilt from each shard's classes:
  * empty -> 0, full -> the R-bit mask, mixed -> its word (in id order). ---- */
 static uint64_t cc_full(const oracle_sim_t* s) { return s->R >= 64 ? ~0ull : ((1ull << s->R) - 1ull); }
+static uint64_t cc_slot(uint64_t nwl) { return 2 * nwl + (nwl + 1) / 2; } /* sharded.h cc_slot_words */
 
 int oracle_cc_send(oracle_sim_t* s, void** bits, uint64_t* bits_bytes, void** vals, uint64_t* count) {
   if (!s || !bits || !bits_bytes || !vals || !count) return GOSSIP_EINVAL;
   if (!s->cc_planned) return GOSSIP_ESTATE;
   const uint64_t nwl = (s->Nl + 63) / 64, fm = cc_full(s);
-  if (!s->cc_bits && !(s->cc_bits = (uint64_t*)calloc(2 * nwl * s->G, 8))) return GOSSIP_ENOMEM;
+  if (!s->cc_bits && !(s->cc_bits = (uint64_t*)calloc(cc_slot(nwl) * s->G, 8))) return GOSSIP_ENOMEM;
   if (!s->cc_send && !(s->cc_send = (uint64_t*)calloc(s->Nl + 1, 8))) return GOSSIP_ENOMEM;
-  uint64_t* own = s->cc_bits + (size_t)s->rank * 2 * nwl;
-  memset(own, 0, 2 * nwl * 8);
+  uint64_t* own = s->cc_bits + (size_t)s->rank * cc_slot(nwl);
+  uint32_t* pre = (uint32_t*)(own + 2 * nwl);
+  memset(own, 0, cc_slot(nwl) * 8);
   uint64_t c = 0;
   for (uint64_t i = 0; i < s->nown; ++i) {
     const uint64_t v = s->S[i], bit = 1ull << (i & 63);
+    if ((i & 63) == 0) pre[i / 64] = (uint32_t)c;
     if (!v) continue;
     own[i / 64] |= bit;
     if (v == fm) own[nwl + i / 64] |= bit;
     else s->cc_send[c++] = v;
   }
   *bits = own;
-  *bits_bytes = 2 * nwl * 8;
+  *bits_bytes = cc_slot(nwl) * 8;
   *vals = s->cc_send;
   *count = c;
   return GOSSIP_OK;
@@ -1101,12 +1105,14 @@ int oracle_cc_expand(oracle_sim_t* s, const uint64_t* counts) {
       memcpy(img, s->S, s->Nl * 8);
       continue;
     }
-    const uint64_t *nz = s->cc_bits + (size_t)q * 2 * nwl, *full = nz + nwl;
+    const uint64_t *nz = s->cc_bits + (size_t)q * cc_slot(nwl), *full = nz + nwl;
+    const uint32_t* pre = (const uint32_t*)(full + nwl);
     const uint64_t nq = (uint64_t)q * s->Nl < s->N ? (s->N - (uint64_t)q * s->Nl < s->Nl ? s->N - (uint64_t)q * s->Nl : s->Nl) : 0;
     uint64_t c = 0;
     for (uint64_t i = 0; i < nq; ++i) {
       const uint64_t bit = 1ull << (i & 63);
       uint64_t v = 0;
+      if ((i & 63) == 0 && pre[i / 64] != c) return GOSSIP_EINVAL; /* the prefix the sender wrote */
       if (full[i / 64] & bit) v = fm;
       else if (nz[i / 64] & bit) {
         if (c >= counts[q]) return GOSSIP_EINVAL; /* more mixed nodes than words sent */

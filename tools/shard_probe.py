@@ -17,14 +17,18 @@ if os.environ.get("GOSSIP_LIB"):  # a library variant (tools/build_variants.sh)
 G = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 LG = int(sys.argv[2]) if len(sys.argv) > 2 else 24
 CALLS = ("sparse_rare", "sparse_scan", "sparse_commit", "dense_prepare", "round_compute", "exchange_buffers",
-         "local_totals", "xd_requests", "xd_request_recv", "xd_serve", "xd_response_recv", "xd_finish")
+         "local_totals", "xd_requests", "xd_request_recv", "xd_serve", "xd_response_recv", "xd_finish",
+         "cc_send", "cc_recv", "cc_expand")
 # argv[3:]: gossip_set_param knobs as name=value (e.g. xd_shards=0: dense rounds on the state all-gather)
 PARAMS = {a.split("=")[0]: float(a.split("=")[1]) for a in sys.argv[3:]}
 
 
 class Timed:
+    """Times the engine calls of one rank; gathered: state bytes the rank receives this round."""
+
     def __init__(self, e, log):
         self._e, self._log = e, log
+        self.gathered = 0
 
     def __getattr__(self, name):
         f = getattr(self._e, name)
@@ -36,6 +40,12 @@ class Timed:
             r = f(*a)
             torch.cuda.synchronize()
             self._log.append((name, (time.perf_counter() - t0) * 1e3))
+            if name == "exchange_buffers":
+                self.gathered = (G - 1) * r[2]
+            elif name == "cc_send":
+                self.gathered = (G - 1) * r[1]
+            elif name == "cc_recv":
+                self.gathered += (G - 1) * a[0] * 8
             return r
         return g
 
@@ -50,6 +60,7 @@ for rep in range(2):
     rounds = []
     for t in range(64):
         for l in logs: l.clear()
+        for te in tes: te.gathered = 0
         ks = [e.sharded_plan() for e in engines]
         if ks[0] < 0:
             tot = sh._lockstep_sum([e.local_totals() for e in engines]); ks = [e.sharded_plan(tot) for e in engines]
@@ -57,6 +68,8 @@ for rep in range(2):
             parts = sh._lockstep_sparse(tes)
         elif ks[0] == 3:
             parts = sh._lockstep_xd(tes)
+        elif ks[0] == 4:
+            parts = sh._lockstep_cc(tes)
         else:
             parts = sh._lockstep_dense(tes)
         tot = sh._lockstep_sum(parts)
@@ -66,11 +79,14 @@ for rep in range(2):
         for l in logs:
             for name, ms in l:
                 calls[name] = calls.get(name, 0.0) + ms / len(logs)
-        rounds.append((t, ks[0], per_rank, int(st[0]["full_nodes"]), calls))
+        rounds.append((t, ks[0], per_rank, int(st[0]["full_nodes"]), calls, tes[0].gathered))
         if st[0]["converged"]:
             break
     if rep == 1:
-        for t, k, ms, full, calls in rounds:
+        for t, k, ms, full, calls, gb in rounds:
             br = " ".join(f"{n}={v:.3f}" for n, v in calls.items())
-            print(f"G={G} round {t:2d} {['dense ', 'sparse', 'ae', 'xdense'][k]} per-rank {ms:7.3f} ms  full={full}  [{br}]", flush=True)
-        print(f"G={G} rounds={len(rounds)} sum per-rank {sum(r[2] for r in rounds):.2f} ms", flush=True)
+            kind = ['dense ', 'sparse', 'ae', 'xdense', 'ccoded'][k]
+            print(f"G={G} round {t:2d} {kind} per-rank {ms:7.3f} ms  full={full}  gathered={gb / 2**20:.1f} MiB  [{br}]",
+                  flush=True)
+        print(f"G={G} rounds={len(rounds)} sum per-rank {sum(r[2] for r in rounds):.2f} ms  "
+              f"gathered per rank {sum(r[5] for r in rounds) / 2**20:.1f} MiB", flush=True)
