@@ -490,12 +490,14 @@ void frontier_carve(uint64_t N, void* base, FrontierBufs* f) {
 }
 
 hipError_t launch_frontier_summary(const FrontierBufs& f, uint64_t N, uint32_t maj, hipStream_t st) {
+  if (N == 0) return hipSuccess;  // a shard without nodes
   frontier_summary_kernel<<<(f.summ_words + 255) / 256, 256, 0, st>>>(f, N, nullptr, 0, maj);
   return hipGetLastError();
 }
 
 hipError_t launch_frontier_commit(const FrontierBufs& f, uint64_t* S, uint64_t N, uint64_t* partial, uint32_t R,
                                   bool all_d, uint32_t flags, hipStream_t st) {
+  if (N == 0) return hipSuccess;  // a shard without nodes
   const uint64_t wchunks = (((N + 63) >> 6) + 63) >> 6;  // 64-group chunks, one per wave
   const uint64_t cblocks = (wchunks + kCommitThreads / 64 - 1) / (kCommitThreads / 64);
   frontier_commit_kernel<<<(uint32_t)(cblocks < 4096 ? cblocks : 4096), kCommitThreads, 0, st>>>(f, S, N, partial,
@@ -505,6 +507,7 @@ hipError_t launch_frontier_commit(const FrontierBufs& f, uint64_t* S, uint64_t N
 
 hipError_t launch_frontier_rebuild(const FrontierBufs& f, const uint64_t* S, uint64_t N, uint64_t* partial,
                                    uint32_t R, uint32_t flags, hipStream_t st) {
+  if (N == 0) return hipSuccess;  // a shard without nodes
   frontier_rebuild_kernel<<<commit_grid(N), kCommitThreads, 0, st>>>(f, S, N, partial, R, flags);
   return hipGetLastError();
 }
@@ -521,6 +524,7 @@ hipError_t launch_frontier_round(const FrontierBufs& f, uint64_t* S, uint64_t N,
                                  uint32_t k, uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t maj,
                                  bool all_d, const Faults& fa, uint32_t flags, const RoundSync& rs,
                                  hipStream_t st) {
+  if (N == 0) return hipSuccess;  // a shard without nodes
   frontier_summary_kernel<<<(f.summ_words + 255) / 256, 256, 0, st>>>(f, N, partial, R, maj);
   const uint64_t chunks = (N + kScanThreads - 1) / kScanThreads;
   const uint32_t grid = (uint32_t)(chunks < kScanGrid ? chunks : kScanGrid);

@@ -611,7 +611,7 @@ hipError_t sx_scan(const SxGeom& g, const SxBufs& b, const FrontierBufs& lf, con
                    uint32_t maj, bool all_d, const Faults& fa, hipStream_t st) {
   hipError_t e = hipMemsetAsync(b.msg_cnt, 0, (g.G + 2) * 4, st);
   if (e == hipSuccess) e = hipMemsetAsync(b.msg_fill, 0, g.G * 4, st);
-  if (e != hipSuccess) return e;
+  if (e != hipSuccess || g.nown == 0) return e;  // a shard without nodes sends nothing
   ScanArgs a{};
   a.lf = lf;
   a.S = S;

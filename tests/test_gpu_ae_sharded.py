@@ -24,6 +24,7 @@ CASES = [  # N, K, fanout, seed, fail, recover, G
     (50_001, 5, 2, 0x5EED000A, 0.05, 0.3, 3),
     (4099, 64, 3, 3, 0.02, 0.2, 2),
     (777, 1, 1, 11, 0.0, 0.0, 2),
+    (100, 8, 1, 5, 0.05, 0.3, 4),  # 64-node row blocks: shards of 64, 36, 0 and 0 nodes
 ]
 
 

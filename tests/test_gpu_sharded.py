@@ -15,8 +15,10 @@ pytestmark = pytest.mark.gpu
 
 
 CASES = [("pushpull", 2, 64, 1 << 20, 0x5EED0004, 4), ("push", 3, 1, 300001, 7, 3),
-         ("pull", 1, 5, 100000, 11, 2), ("pushpull", 6, 7, 50001, 3, 2)]
-IDS = ["pushpull-1M-G4", "push-ragged-G3", "pull-G2", "pushpull-k6-G2"]
+         ("pull", 1, 5, 100000, 11, 2), ("pushpull", 6, 7, 50001, 3, 2),
+         # tiny clusters whose last shard owns no node (3, 3, 3, 3, 0 and 3, 3, 3, 0)
+         ("pushpull", 2, 5, 12, 3, 5), ("push", 1, 1, 9, 5, 4)]
+IDS = ["pushpull-1M-G4", "push-ragged-G3", "pull-G2", "pushpull-k6-G2", "pushpull-N12-G5-empty", "push-N9-G4-empty"]
 # (flags, gossip_set_param knobs) per plan
 PLANS = {"auto": (0, {}), "sparse": (0, {"sparse_frac": 1.0}), "sparse_alld": (0, {"sparse_frac": 1.0, "alld_frac": 0}),
          "dense": (0, {"sparse_frac": -1, "xd_shards": 0, "cc_frac": 0}),

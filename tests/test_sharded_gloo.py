@@ -190,3 +190,15 @@ def test_antientropy_sharded_equals_one(case, world):
     for rank, lo, hi, stats, own in got:
         assert [dict(s, round=0) for s in stats] == [dict(s, round=0) for s in want]
         assert np.array_equal(own, rows[lo:hi])
+
+
+@pytest.mark.parametrize("plan", ["auto", "sparse", "dense", "exchange", "classcoded"])
+def test_empty_shard_equal_one(plan):
+    """N = 12 over 5 ranks: shards of 3, 3, 3, 3 and 0 nodes (the last rank owns none and
+    still joins every collective)."""
+    test_two_ranks_equal_one(("pushpull", 2, 5, 12, 3, None), plan, world=5)
+
+
+def test_antientropy_empty_shards_equal_one():
+    """100 nodes over 4 ranks in 64-node row blocks: shards of 64, 36, 0 and 0 nodes."""
+    test_antientropy_sharded_equals_one((100, 8, 1, 5, 0.05, 0.3), world=4)
