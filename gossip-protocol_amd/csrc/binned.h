@@ -155,9 +155,17 @@ size_t xd_send_bytes(const XdGeom& g);  // rcnt .. rep_in
 void xd_carve_send(const XdGeom& g, void* base, XdBufs* b);
 size_t xd_recv_bytes(const XdGeom& g, uint64_t cap_r);  // rid .. rep_out
 void xd_carve_recv(const XdGeom& g, uint64_t cap_r, void* base, XdBufs* b);
+// Edge filter of an exchange round (filt = 0: none): cls = every shard's occupancy bitmaps
+// of S_t, [nz: nwl u64][full: nwl u64] per shard (gossip_xd_classes, all-gathered).
+struct XdFilter {
+  const uint64_t* cls;
+  uint32_t nwl, filt;  // filt bit 0: drop pull-only edges into empty peers, bit 1: push-only into full
+  uint8_t* keep;       // [nown] the count pass's verdict per sender (bit j: edge j kept; k <= 8), read by emit
+};
 // own senders' items: counts per (region, owner), send positions, then the items
 hipError_t launch_xd_requests(const XdGeom& g, const XdBufs& b, const uint64_t* S, uint32_t R, uint32_t t,
-                              uint32_t key0, uint32_t key1, uint32_t mode, const Faults& fa, hipStream_t st);
+                              uint32_t key0, uint32_t key1, uint32_t mode, const Faults& fa, const XdFilter& xf,
+                              hipStream_t st);
 // n_in received items: bin by own tile, serve the pulls from S_t, replies in received order (b.rep_out)
 hipError_t launch_xd_serve(XdGeom g, const XdBufs& b, const uint64_t* S, uint64_t n_in, uint32_t R,
                            hipStream_t st);

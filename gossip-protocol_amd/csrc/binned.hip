@@ -53,6 +53,20 @@ constexpr int kUnrollSeq = 8;  // records in flight per lane in the sequential r
 // push-pull apply: the block's waves split between the push walk (fragmented runs)
 // and the response walk (sequential regions), which then run side by side
 constexpr bool kApplySplit = GOSSIP_APPLY_SPLIT != 0;
+#ifndef GOSSIP_GROUP
+#define GOSSIP_GROUP 0
+#endif
+// Run walkers load records GS at a time (GS = 2: 8-B id pairs, 16-B value / response pairs;
+// GS = 4: 16-B id quads, two 16-B value pairs; 0: one record per lane): a group at either
+// end of a run is shared with the neighbouring runs and masked.  The one-record walkers left
+// the CU's texture address / data units 72 / 86 % busy in apply on lane-wise 4- and 8-B
+// accesses (profiles/r02_s2b/pmc_sq.json).
+constexpr int kGS = GOSSIP_GROUP;
+constexpr bool kQuad = kGS != 0;
+static_assert(kGS == 0 || kGS == 2 || kGS == 4, "GOSSIP_GROUP: 0, 2 or 4 records per lane");
+constexpr int kGSn = kGS ? kGS : 1;
+constexpr int kUnrollQ = 16 / kGSn;     // groups (16 records) in flight per lane in the run walkers
+constexpr int kUnrollQSeq = 16 / kGSn;  // groups in flight per lane in apply's sequential response walk
 #ifndef GOSSIP_NT_REC
 #define GOSSIP_NT_REC 1  // emit's record stores (bench: serve -28 us, apply -10 us per dense round)
 #endif
@@ -71,6 +85,64 @@ __device__ __forceinline__ T rec_ld(const T* p) {
   if constexpr ((GOSSIP_NT_REC & BIT) != 0) return __builtin_nontemporal_load(p);
   else return *p;
 }
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));  // the nontemporal builtins take native vectors
+template <int BIT>
+__device__ __forceinline__ uint4 rec_ld4(const uint4* p) {
+  if constexpr ((GOSSIP_NT_REC & BIT) != 0) {
+    const v4u32 x = __builtin_nontemporal_load((const v4u32*)p);
+    return make_uint4(x.x, x.y, x.z, x.w);
+  } else {
+    return *p;
+  }
+}
+template <int BIT>
+__device__ __forceinline__ void rec_st4(uint4* p, uint4 v) {
+  if constexpr ((GOSSIP_NT_REC & BIT) != 0) {
+    const v4u32 x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, (v4u32*)p);
+  } else {
+    *p = v;
+  }
+}
+typedef uint32_t v2u32 __attribute__((ext_vector_type(2)));
+template <int BIT>
+__device__ __forceinline__ uint2 rec_ld2(const uint2* p) {
+  if constexpr ((GOSSIP_NT_REC & BIT) != 0) {
+    const v2u32 x = __builtin_nontemporal_load((const v2u32*)p);
+    return make_uint2(x.x, x.y);
+  } else {
+    return *p;
+  }
+}
+__device__ __forceinline__ uint4 u64x2(uint64_t a, uint64_t b) {
+  return make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+}
+// group g of GS records: ids (4 B each) and 8-B values / responses, vector loads and stores
+template <int GS, int BIT>
+__device__ __forceinline__ void grp_ids(const uint32_t* base, size_t g, uint32_t (&o)[GS]) {
+  if constexpr (GS == 4) {
+    const uint4 x = rec_ld4<BIT>((const uint4*)base + g);
+    o[0] = x.x; o[1] = x.y; o[2] = x.z; o[3] = x.w;
+  } else {
+    const uint2 x = rec_ld2<BIT>((const uint2*)base + g);
+    o[0] = x.x; o[1] = x.y;
+  }
+}
+template <int GS, int BIT>
+__device__ __forceinline__ void grp_vals(const uint64_t* base, size_t g, uint64_t (&o)[GS]) {
+#pragma unroll
+  for (int h = 0; h < GS / 2; ++h) {
+    const uint4 x = rec_ld4<BIT>((const uint4*)base + g * (GS / 2) + h);
+    o[2 * h] = (uint64_t)x.y << 32 | x.x;
+    o[2 * h + 1] = (uint64_t)x.w << 32 | x.z;
+  }
+}
+template <int GS, int BIT>
+__device__ __forceinline__ void grp_store(uint64_t* base, size_t g, const uint64_t (&v)[GS]) {
+#pragma unroll
+  for (int h = 0; h < GS / 2; ++h) rec_st4<BIT>((uint4*)base + g * (GS / 2) + h, u64x2(v[2 * h], v[2 * h + 1]));
+}
+
 // record id word: p_local [0,14) | n_local [14,28) | flags.  K1 rewrites every
 // id each round, so a flag never outlives its round.
 constexpr uint32_t kIdVZ = 1u << 28;  // no push on this record (sender empty, or the peer already full)
@@ -626,14 +698,108 @@ __device__ __forceinline__ void for_each_run_record(const BinGeom& g, const uint
   }
 }
 
+// for_each_run_record four records at a time: the records [be, en) of run (s, T) lie in
+// the 16-B-aligned quads [be/4, ceil(en/4)) of region s (rp % 4 == 0: make_bin_geom); the
+// quads at either end may also hold records of the neighbouring runs (other tiles), so each
+// quad comes with a 4-bit mask of this run's records.  fn(q, m): quad index q (records
+// 4q .. 4q+3 of the region-major record array), mask m; q = -1, m = 0 past the end.
+// LDS per wave: wmask[U] u64, wlist / wbe / wen [64] i32.
+template <int U, int GS, typename F>
+__device__ __forceinline__ void for_each_run_group(const BinGeom& g, const uint16_t* rowb, const uint16_t* rowe,
+                                                  uint64_t* wmask_all, int32_t* wlist_all, int32_t* wbe_all,
+                                                  int32_t* wen_all, F&& fn, uint32_t w0 = 0, uint32_t nwaves = 0) {
+  constexpr uint32_t kWin = 64 * U;
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (nwaves == 0) nwaves = blockDim.x >> 6;
+  uint64_t* wm = wmask_all + wave * U;
+  int32_t* wl = wlist_all + wave * 64;
+  int32_t* wb = wbe_all + wave * 64;
+  int32_t* we = wen_all + wave * 64;
+  const uint64_t below = (1ull << lane) - 1ull, upto = (2ull << lane) - 1ull;
+  const uint32_t rq = g.rp / GS;  // groups per region
+  for (uint32_t s0 = (wave - w0) * 64; s0 < g.nt_s; s0 += nwaves * 64) {
+    const uint32_t s = s0 + lane;
+    const uint32_t sc = min(s, g.nt_s - 1);
+    const uint32_t be0 = rowb[sc], en0 = rowe[sc];
+    const uint32_t be = s < g.nt_s ? be0 : 0u, en = s < g.nt_s ? en0 : 0u;
+    const uint32_t qb = be / GS, nq = en > be ? (en + GS - 1u) / GS - qb : 0u;
+    uint32_t inc = nq;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o, 64);
+      if (lane >= (uint32_t)o) inc += y;
+    }
+    const uint32_t exc = inc - nq;
+    const uint32_t total = __shfl(inc, 63, 64);
+    const int32_t basep = (int32_t)(s * rq + qb - exc);  // quad = basep(owner) + f
+    const int32_t abe = (int32_t)(s * g.rp + be), aen = (int32_t)(s * g.rp + en);
+    for (uint32_t f0 = 0; f0 < total; f0 += kWin) {
+      if (lane < (uint32_t)U) wm[lane] = 0;
+      wave_sync();
+      const bool in = nq != 0 && exc < f0 + kWin && exc + nq > f0;
+      const uint64_t inm = __ballot(in);
+      if (in) {
+        const uint32_t pos = exc > f0 ? exc - f0 : 0u;
+        atomicOr((unsigned long long*)&wm[pos >> 6], 1ull << (pos & 63u));
+        const uint32_t k = __popcll(inm & below);
+        wl[k] = basep;
+        wb[k] = abe;
+        we[k] = aen;
+      }
+      wave_sync();
+      int32_t q[U];
+      uint32_t m[U];
+      uint32_t pre = 0;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint64_t w = wm[u];
+        const uint32_t r = (pre + (uint32_t)__popcll(w & upto) - 1u) & 63u;
+        pre += (uint32_t)__popcll(w);
+        const uint32_t f = f0 + u * 64 + lane;
+        const int32_t qq = wl[r] + (int32_t)f;
+        constexpr uint32_t kAll = (1u << GS) - 1u;
+        const int32_t lo = wb[r] - GS * qq, hi = we[r] - GS * qq;  // this run's records in the group: [lo, hi)
+        const uint32_t mhi = hi >= GS ? kAll : hi <= 0 ? 0u : (1u << hi) - 1u;
+        const uint32_t mlo = lo <= 0 ? kAll : lo >= GS ? 0u : (kAll << lo) & kAll;
+        q[u] = f < total ? qq : -1;
+        m[u] = f < total ? (mhi & mlo) : 0u;
+      }
+      wave_sync();  // the next window rewrites wm/wl/wb/we
+      fn(q, m);
+    }
+  }
+}
+
 // The pushes aimed at tile X (its runs in every sender region) ORed into acc,
 // by the waves [0, nwaves) (0: all).  VZ: the record id's no-push flag.
 template <uint32_t VZ>
 __device__ __forceinline__ void push_walk(const BinGeom& g, const BinBufs& b, uint32_t X, unsigned long long* acc,
-                                          uint64_t* wmask, int32_t* wlist, uint32_t nwaves) {
+                                          uint64_t* wmask, int32_t* wlist, int32_t* wbe, int32_t* wen,
+                                          uint32_t nwaves) {
   const uint32_t* __restrict__ gids = b.ids;
   const uint64_t* __restrict__ gvals = b.vals;
   const uint16_t* rowb = b.offT + (size_t)X * g.nt_s;
+  if constexpr (kQuad) {
+    for_each_run_group<kUnrollQ, kGSn>(g, rowb, rowb + g.nt_s, wmask, wlist, wbe, wen, [&](const int32_t* q, const uint32_t* m) {
+      uint32_t id[kUnrollQ][kGSn];
+      uint64_t va[kUnrollQ][kGSn];
+#pragma unroll
+      for (int u = 0; u < kUnrollQ; ++u) grp_ids<kGSn, 8>(gids, q[u] >= 0 ? q[u] : 0, id[u]);
+#pragma unroll
+      for (int u = 0; u < kUnrollQ; ++u) grp_vals<kGSn, 8>(gvals, q[u] >= 0 ? q[u] : 0, va[u]);
+#pragma unroll
+      for (int u = 0; u < kUnrollQ; ++u)
+#pragma unroll
+        for (int i = 0; i < kGSn; ++i) {
+          const uint32_t idw = id[u][i];
+          const uint64_t v = va[u][i];
+          if (!((m[u] >> i) & 1u) || (idw & VZ) || !v) continue;  // every value is stored (K1)
+          const uint32_t p = idw & (kTileD - 1);
+          if (v & ~acc[p]) atomicOr(&acc[p], (unsigned long long)v);
+        }
+    }, 0u, nwaves);
+    return;
+  }
   for_each_run_record<kUnroll>(g, rowb, rowb + g.nt_s, wmask, wlist, [&](const int32_t* rec) {
     uint32_t id[kUnroll];
     uint64_t v[kUnroll];
@@ -681,8 +847,10 @@ template <uint32_t VF>
 __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, const uint64_t* __restrict__ S, BinBufs b,
                                                                   uint32_t R, IdxRange tr) {
   __shared__ unsigned long long img[kTileD];
-  __shared__ uint64_t wmask[(kTileThreads / 64) * kUnrollServe];
+  __shared__ uint64_t wmask[(kTileThreads / 64) * (kUnrollServe > kUnrollQ ? kUnrollServe : kUnrollQ)];
   __shared__ int32_t wlist[(kTileThreads / 64) * 64];
+  __shared__ int32_t wbe[kQuad ? (kTileThreads / 64) * 64 : 1];
+  __shared__ int32_t wen[kQuad ? (kTileThreads / 64) * 64 : 1];
   // persistent: virtual block v = blockIdx.x, +gridDim.x, ... serves tile
   // tr.at(xcd_remap(v, tr.n)) (the XCD of v is that of blockIdx.x, as with one
   // block per tile); the next tile's image loads into registers during a walk
@@ -700,6 +868,29 @@ __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, cons
   const uint32_t* gids = b.ids;
   uint64_t* __restrict__ gresp = b.resp;
   const uint16_t* rowb = b.offT + (size_t)T * g.nt_s;
+  if constexpr (kQuad) {
+    for_each_run_group<kUnrollQ, kGSn>(g, rowb, rowb + g.nt_s, wmask, wlist, wbe, wen, [&](const int32_t* q, const uint32_t* m) {
+      uint32_t id[kUnrollQ][kGSn];
+#pragma unroll
+      for (int u = 0; u < kUnrollQ; ++u) grp_ids<kGSn, 2>(gids, q[u] >= 0 ? q[u] : 0, id[u]);
+#pragma unroll
+      for (int u = 0; u < kUnrollQ; ++u) {
+        if (!m[u]) continue;
+        uint64_t r[kGSn];
+#pragma unroll
+        for (int i = 0; i < kGSn; ++i) r[i] = (uint64_t)img[id[u][i] & (kTileD - 1)];
+        if (m[u] == (1u << kGSn) - 1u) {  // the whole group is this tile's: 16-B stores (no-pull slots
+                                          // get S_t[p] too, unread: the consumers skip records flagged VF)
+          grp_store<kGSn, 4>(gresp, q[u], r);
+          continue;
+        }
+#pragma unroll
+        for (int i = 0; i < kGSn; ++i)  // a run end: only this tile's records (the rest are other blocks')
+          if (((m[u] >> i) & 1u) && !(id[u][i] & VF)) rec_st<4>(&gresp[kGSn * (size_t)q[u] + i], r[i]);
+      }
+    });
+    continue;
+  }
   for_each_run_record<kUnrollServe>(g, rowb, rowb + g.nt_s, wmask, wlist, [&](const int32_t* rec) {
     uint32_t id[kUnrollServe];
 #pragma unroll
@@ -736,6 +927,8 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
   __shared__ uint32_t red_nz[kTileThreads / 64];
   __shared__ uint64_t wmask[(kTileThreads / 64) * kUnroll];
   __shared__ int32_t wlist[(kTileThreads / 64) * 64];
+  __shared__ int32_t wbe[kQuad ? (kTileThreads / 64) * 64 : 1];
+  __shared__ int32_t wen[kQuad ? (kTileThreads / 64) * 64 : 1];
   const uint32_t tid = threadIdx.x;
   // persistent (grid apply_grid(nt_d)): virtual block v = blockIdx.x,
   // +gridDim.x, ... applies tile xcd_remap(v, nt_d) (same XCD as blockIdx.x);
@@ -768,9 +961,10 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
   const bool do_pull = (mode == 2 || mode == 3) && (!split || wave >= nwav / 2);
   // split: waves [0, 8) walk the pushes, [8, 16) the responses (threads 512..1023)
   const uint32_t qt0 = split ? kTileThreads / 2 : 0u, qnt = split ? kTileThreads / 2 : kTileThreads;
-  if (do_push) push_walk<kIdVZ>(g, b, X, acc, wmask, wlist, split ? nwav / 2 : 0u);  // pushes aimed at this tile
+  if (do_push) push_walk<kIdVZ>(g, b, X, acc, wmask, wlist, wbe, wen, split ? nwav / 2 : 0u);  // pushes aimed at this tile
   if (do_pull) {  // responses owed to this tile's own senders
     const uint32_t* __restrict__ qids = bq.ids;
+    auto qids_base = [](const BinBufs& bb) { return bb.ids; };
     const uint64_t* __restrict__ gresp = bq.resp;
     const uint32_t per = kTileD >> gq.ts_log;
     const uint32_t s0 = X * per, s1 = min(s0 + per, gq.nt_s);
@@ -779,6 +973,36 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
       const size_t reg = (size_t)s * gq.rp;
       const uint32_t nb = (s - s0) << gq.ts_log;
       const uint32_t qtid = tid - qt0;
+      if constexpr (kQuad) {  // the region's records GS at a time (rp % GS == 0: whole groups)
+        const uint32_t nq = (total + kGSn - 1) / kGSn;
+        const uint32_t* __restrict__ rids = qids_base(bq) + reg;
+        const uint64_t* __restrict__ rres = gresp + reg;
+        for (uint32_t p0 = 0; p0 < nq; p0 += qnt * kUnrollQSeq) {
+          uint32_t id[kUnrollQSeq][kGSn];
+          uint64_t ra[kUnrollQSeq][kGSn];
+#pragma unroll
+          for (int u = 0; u < kUnrollQSeq; ++u) {
+            const uint32_t qi = min(p0 + u * qnt + qtid, nq - 1);
+            grp_ids<kGSn, 16>(rids, qi, id[u]);
+            grp_vals<kGSn, 16>(rres, qi, ra[u]);
+          }
+#pragma unroll
+          for (int u = 0; u < kUnrollQSeq; ++u) {
+            const uint32_t qi = p0 + u * qnt + qtid;
+            if (qi >= nq) continue;
+#pragma unroll
+            for (int i = 0; i < kGSn; ++i) {
+              const uint32_t idw = id[u][i];
+              // a full sender's slot was never written this round (K2 skips it)
+              if (kGSn * qi + i >= total || (idw & kIdVF)) continue;
+              const uint32_t node = nb + ((idw >> kTileDLog) & kIdNMask);
+              const uint64_t r = ra[u][i];
+              if (r & ~acc[node]) atomicOr(&acc[node], (unsigned long long)r);
+            }
+          }
+        }
+        continue;
+      }
       for (uint32_t p0 = 0; p0 < total; p0 += qnt * kUnrollSeq) {
         uint64_t r[kUnrollSeq];
         uint32_t id[kUnrollSeq];
@@ -1030,6 +1254,18 @@ __device__ __forceinline__ uint32_t xd_owner(uint32_t p, uint32_t Nl32, uint32_t
   return o < G ? o : G - 1u;
 }
 
+// The exchange-round edge filter: xf.cls holds every shard's occupancy
+// bitmaps of S_t ([nz: nwl words][full: nwl words] per shard, all-gathered); a one-way
+// edge is dropped when it moves nothing — a pull-only edge (empty sender) whose peer is
+// empty (filt bit 0), a push-only edge (full sender) whose peer is full (bit 1).  Returns
+// the directions kept (sender_dirs' bits), 0 = no item.
+__device__ __forceinline__ uint32_t xd_filter(const XdFilter& xf, uint32_t d, uint32_t o, uint32_t pl) {
+  const uint64_t* slot = xf.cls + (size_t)o * 2 * xf.nwl;
+  if ((xf.filt & 1u) && d == 2u && !((slot[pl >> 6] >> (pl & 63u)) & 1ull)) return 0u;
+  if ((xf.filt & 2u) && d == 1u && ((slot[xf.nwl + (pl >> 6)] >> (pl & 63u)) & 1ull)) return 0u;
+  return d;
+}
+
 // the live edges n -> p of sender n in round t (draws as bin_emit's; a lost edge
 // carries nothing in either direction)
 template <bool FAULTS, typename F>
@@ -1044,7 +1280,7 @@ __device__ __forceinline__ void xd_edges(uint32_t k, uint32_t n, uint64_t nm1, u
     }
     const uint32_t p = peer_from_word(lane_of(x, j & 3u), nm1, n);
     if (FAULTS && edge_lost(fa, rc, p, lane_of(lw, j & 3u))) continue;
-    fn(p);
+    fn(p, j);
   }
 }
 
@@ -1055,7 +1291,7 @@ template <bool FAULTS>
 __global__ __launch_bounds__(kEmitThreads) void xd_count_kernel(XdGeom g, const uint64_t* __restrict__ S,
                                                                  uint32_t* __restrict__ rcnt, uint32_t R, uint32_t t,
                                                                  uint32_t key0, uint32_t key1, uint32_t mode,
-                                                                 Faults fa) {
+                                                                 Faults fa, XdFilter xf) {
   __shared__ uint32_t cnt[kXdMaxG];
   const uint32_t tid = threadIdx.x, Nl32 = (uint32_t)g.Nl;
   const uint64_t fm = full_mask1(R), nm1 = g.N - 1;
@@ -1068,9 +1304,16 @@ __global__ __launch_bounds__(kEmitThreads) void xd_count_kernel(XdGeom g, const 
     // (one LDS atomic per edge: aggregating a wave's lanes per owner with ballots measured
     // 2.6x slower, profiles/r02_xd/variants3)
     for (uint32_t i = tid; i < nsend; i += kEmitThreads) {
-      if (!sender_dirs(mode, S[base + i], fm)) continue;
-      xd_edges<FAULTS>(g.k, (uint32_t)(g.lo + base + i), nm1, t, key0, key1, fa,
-                       [&](uint32_t p) { atomicAdd(&cnt[xd_owner(p, Nl32, g.G)], 1u); });
+      const uint32_t d = sender_dirs(mode, S[base + i], fm);
+      uint32_t keep = 0;  // filtered rounds: edge j survives the class probe (emit reads it, no second probe)
+      if (d)
+        xd_edges<FAULTS>(g.k, (uint32_t)(g.lo + base + i), nm1, t, key0, key1, fa, [&](uint32_t p, uint32_t j) {
+          const uint32_t o = xd_owner(p, Nl32, g.G);
+          if (xf.filt && !xd_filter(xf, d, o, p - o * Nl32)) return;
+          keep |= 1u << j;
+          atomicAdd(&cnt[o], 1u);
+        });
+      if (xf.filt) xf.keep[base + i] = (uint8_t)keep;
     }
     __syncthreads();
     for (uint32_t o = tid; o < g.G; o += kEmitThreads) rcnt[(size_t)s * g.G + o] = cnt[o];
@@ -1108,7 +1351,7 @@ template <bool FAULTS>
 __global__ __launch_bounds__(kEmitThreads) void xd_emit_kernel(XdGeom g, const uint64_t* __restrict__ S, XdBufs b,
                                                                 uint32_t* __restrict__ rlofs, uint32_t R, uint32_t t,
                                                                 uint32_t key0, uint32_t key1, uint32_t mode,
-                                                                Faults fa) {
+                                                                Faults fa, XdFilter xf) {
   __shared__ uint32_t cur[kXdMaxG];
   __shared__ uint32_t lofs[kXdMaxG + 1];
   __shared__ uint32_t st_id[kRecPerRegion];
@@ -1133,11 +1376,13 @@ __global__ __launch_bounds__(kEmitThreads) void xd_emit_kernel(XdGeom g, const u
     for (uint32_t i = tid; i < nsend; i += kEmitThreads) {
       const uint32_t d = sender_dirs(mode, S[base + i], fm);
       if (!d) continue;
-      const uint32_t fl = ((d & 1u) ? 0u : kXdNoPush) | ((d & 2u) ? 0u : kXdNoPull);
-      xd_edges<FAULTS>(g.k, (uint32_t)(g.lo + base + i), nm1, t, key0, key1, fa, [&](uint32_t p) {
-        const uint32_t o = xd_owner(p, Nl32, G);
+      const uint32_t keep = xf.filt ? xf.keep[base + i] : ~0u;
+      xd_edges<FAULTS>(g.k, (uint32_t)(g.lo + base + i), nm1, t, key0, key1, fa, [&](uint32_t p, uint32_t j) {
+        if (!((keep >> j) & 1u)) return;  // dropped by the count pass's class probe
+        const uint32_t o = xd_owner(p, Nl32, G), pl = p - o * Nl32;
+        const uint32_t de = d;
         const uint32_t pos = atomicAdd(&cur[o], 1u);
-        st_id[pos] = (p - o * Nl32) | fl;
+        st_id[pos] = pl | ((de & 1u) ? 0u : kXdNoPush) | ((de & 2u) ? 0u : kXdNoPull);
         st_nl[pos] = (uint16_t)i;
       });
     }
@@ -1256,6 +1501,8 @@ __global__ __launch_bounds__(kTileThreads) void xd_apply_kernel(XdGeom g, XdBufs
   __shared__ uint32_t red_nz[kTileThreads / 64];
   __shared__ uint64_t wmask[(kTileThreads / 64) * kUnroll];
   __shared__ int32_t wlist[(kTileThreads / 64) * 64];
+  __shared__ int32_t wbe[kQuad ? (kTileThreads / 64) * 64 : 1];
+  __shared__ int32_t wen[kQuad ? (kTileThreads / 64) * 64 : 1];
   __shared__ uint32_t pl[kXdPref];  // the tile's sender regions: owner-run prefix rows (G + 1 each)
   __shared__ uint32_t po[kXdPref];  // and the runs' send positions (G each, stride G + 1)
   const uint32_t tid = threadIdx.x, G = g.G;
@@ -1284,7 +1531,7 @@ __global__ __launch_bounds__(kTileThreads) void xd_apply_kernel(XdGeom g, XdBufs
     }
     if (tid < 64) cnt[tid] = 0;
     __syncthreads();
-    if (do_push) push_walk<kXbVZ>(g.r, b.rb, X, acc, wmask, wlist, split ? nwav / 2 : 0u);
+    if (do_push) push_walk<kXbVZ>(g.r, b.rb, X, acc, wmask, wlist, wbe, wen, split ? nwav / 2 : 0u);
     if (do_pull) {  // replies, in send order: region s's items are G runs (one per owner)
       const uint32_t qtid = tid - qt0;
       for (uint32_t s = s0; s < s1; ++s) {
@@ -1413,15 +1660,16 @@ void xd_carve_recv(const XdGeom& g, uint64_t cap_r, void* base, XdBufs* b) {
 }
 
 hipError_t launch_xd_requests(const XdGeom& g, const XdBufs& b, const uint64_t* S, uint32_t R, uint32_t t,
-                              uint32_t key0, uint32_t key1, uint32_t mode, const Faults& fa, hipStream_t st) {
+                              uint32_t key0, uint32_t key1, uint32_t mode, const Faults& fa, const XdFilter& xf,
+                              hipStream_t st) {
   if (g.nown == 0) return hipMemsetAsync(b.ocnt, 0, g.G * 4, st);
   const uint32_t eg = g.s.nt_s < kEmitGrid ? g.s.nt_s : kEmitGrid;
   // (1024 blocks instead of one per CU: same time, profiles/r02_xd/variants3)
-  if (fa.any()) xd_count_kernel<true><<<eg, kEmitThreads, 0, st>>>(g, S, b.rcnt, R, t, key0, key1, mode, fa);
-  else xd_count_kernel<false><<<eg, kEmitThreads, 0, st>>>(g, S, b.rcnt, R, t, key0, key1, mode, fa);
+  if (fa.any()) xd_count_kernel<true><<<eg, kEmitThreads, 0, st>>>(g, S, b.rcnt, R, t, key0, key1, mode, fa, xf);
+  else xd_count_kernel<false><<<eg, kEmitThreads, 0, st>>>(g, S, b.rcnt, R, t, key0, key1, mode, fa, xf);
   xd_scan_kernel<<<g.G, 1024, 0, st>>>(b.rcnt, b.roff, b.ocnt, g.s.nt_s, g.G);
-  if (fa.any()) xd_emit_kernel<true><<<eg, kEmitThreads, 0, st>>>(g, S, b, b.rlofs, R, t, key0, key1, mode, fa);
-  else xd_emit_kernel<false><<<eg, kEmitThreads, 0, st>>>(g, S, b, b.rlofs, R, t, key0, key1, mode, fa);
+  if (fa.any()) xd_emit_kernel<true><<<eg, kEmitThreads, 0, st>>>(g, S, b, b.rlofs, R, t, key0, key1, mode, fa, xf);
+  else xd_emit_kernel<false><<<eg, kEmitThreads, 0, st>>>(g, S, b, b.rlofs, R, t, key0, key1, mode, fa, xf);
   return hipGetLastError();
 }
 

@@ -119,6 +119,7 @@ struct gossip_engine {
   double sparse_frac = 1.0 / 16;  // rare fraction at or below which a round runs sparse (sparse_frac_of)
   bool sparse_frac_set = false;   // set by gossip_set_param (else the sharded defaults apply)
   double filter_frac = 0.3;       // dense rounds filter edges by the peer's class above this empty / full fraction
+  double xd_filter_frac = 0.6;    // exchange rounds likewise (their probe hits a G-shard class image: G = 8 sweep)
   double alld_frac = 1.0 / 64;    // sparse rounds with k * rare >= alld_frac * N commit every group's D (bench sweep)
   // pipelined rounds (binned engines): the host picks each round's path from the
   // totals it has read, predicted forward over the rounds still in flight, and
@@ -158,6 +159,10 @@ struct gossip_engine {
   void *xd_smem = nullptr, *xd_rmem = nullptr;
   uint64_t xd_rcap = 0, xd_nin = 0;
   uint32_t* xd_cnt_h = nullptr;  // pinned [G]
+  uint32_t xd_filt = 0;          // this round's edge filter (dense_filter of the global totals)
+  bool xd_cls_ok = false;        // gossip_xd_classes handed out the own bitmaps for this round
+  uint64_t* xd_cls = nullptr;    // [G][2 * nwl] every shard's occupancy bitmaps of S_t (all-gather in place)
+  uint8_t* xd_keep = nullptr;    // [nown] per sender: the edges that survive the filter (count pass -> emit)
   // class-coded state exchange for dense image rounds (sharded.h cc_*), plan kind 4
   bool cc_planned = false;
   double cc_frac = 0.75;  // gossip_set_param "cc_frac": at most this global fraction of mixed nodes
@@ -221,7 +226,7 @@ void free_all(gossip_engine* e) {
   if (e->bin_mem) (void)hipFree(e->bin_mem);
   if (e->fr_mem) (void)hipFree(e->fr_mem);
   void* sx[] = {e->lf_mem, e->sx_mem, e->rare_recv, e->msg_recv, e->sb_mem, e->xd_smem, e->xd_rmem,
-                e->cc_bits, e->cc_vals};
+                e->cc_bits, e->cc_vals, e->xd_cls, e->xd_keep};
   if (e->xd_cnt_h) (void)hipHostFree(e->xd_cnt_h);
   for (void* b : sx)
     if (b) (void)hipFree(b);
@@ -456,11 +461,11 @@ bool choose_sparse(const gossip_engine* e, const Est& x, uint32_t* maj, bool* al
 
 // dense rounds: probe the peer's class in emit when many edges would move
 // nothing (pulls from empty peers early in a run, pushes into full peers late)
-uint32_t dense_filter(const gossip_engine* e, const Est& x) {
+uint32_t dense_filter(const gossip_engine* e, const Est& x, double frac) {
   const double N = (double)e->N, empty = 1.0 - x.nz / N, full = x.full / N;
   const bool pull = e->mode == GOSSIP_MODE_PULL || e->mode == GOSSIP_MODE_PUSHPULL;
   const bool push = e->mode == GOSSIP_MODE_PUSH || e->mode == GOSSIP_MODE_PUSHPULL;
-  return (pull && empty > e->filter_frac ? 1u : 0u) | (push && full > e->filter_frac ? 2u : 0u);
+  return (pull && empty > frac ? 1u : 0u) | (push && full > frac ? 2u : 0u);
 }
 
 RoundSync ring_sync(gossip_engine* e, uint32_t slot) {
@@ -566,7 +571,7 @@ int step_planned(gossip_engine* e, uint32_t max_rounds, gossip_round_stats_t* st
       const uint32_t slot = launched % kRing;
       const RoundSync rs = ring_sync(e, slot);
       want[slot] = rs.seq;
-      if (int rc = launch_round_path(e, t0 + launched, sparse, maj, all_d, dense_filter(e, x), rs, (int)slot)) return rc;
+      if (int rc = launch_round_path(e, t0 + launched, sparse, maj, all_d, dense_filter(e, x, e->filter_frac), rs, (int)slot)) return rc;
       ++launched;
     }
     if (done == launched) break;
@@ -704,7 +709,7 @@ int compute_round(gossip_engine* e, const uint64_t* gathered) {
     const Est x = est_of(e, tot.data());
     const bool sparse = choose_sparse(e, x, &maj, &all_d);
     if ((rc = timer_begin(e, 0))) return rc;
-    if ((rc = launch_round_path(e, e->t, sparse, maj, all_d, dense_filter(e, x), ring_sync(e, 0), -1))) return rc;
+    if ((rc = launch_round_path(e, e->t, sparse, maj, all_d, dense_filter(e, x, e->filter_frac), ring_sync(e, 0), -1))) return rc;
     return timer_end(e, 0);  // stats are fused into the round kernels
   } else if (e->sbin) {  // sharded dense round: binned pipeline over the gathered image
     if ((rc = timer_begin(e, 0))) return rc;
@@ -1140,6 +1145,8 @@ int gossip_set_param(gossip_engine_t* e, const char* name, double v) {
     e->alld_frac = v;
   } else if (n == "filter_frac") {
     e->filter_frac = v;
+  } else if (n == "xd_filter_frac") {
+    e->xd_filter_frac = v;
   } else if (n == "ahead") {
     if (v < 1 || v > kRing - 1) return e->fail(GOSSIP_EINVAL, "ahead must be in [1, %u]", kRing - 1);
     e->ahead = (uint32_t)v;
@@ -1473,6 +1480,11 @@ int gossip_sharded_plan(gossip_engine_t* e, const uint64_t* total, int32_t* kind
   e->sx_maj = maj;
   e->sx_alld = all_d;
   e->xd_planned = !e->sx_planned && e->xd && e->xd_shards && e->G >= e->xd_shards;
+  // exchange rounds drop the one-way edges into empty / full peers when many nodes are (the
+  // global totals are exact: no prediction), after an all-gather of the class bitmaps
+  // (k <= 8: one keep byte per sender carries the count pass's probes to the emit pass)
+  e->xd_filt = e->xd_planned && e->k <= 8 ? dense_filter(e, est_of(e, e->gtot.data()), e->xd_filter_frac) : 0u;
+  e->xd_cls_ok = false;
   // dense on the state image: class-coded when few nodes are mixed (neither empty nor full)
   const double mixed = ((double)e->gtot[4 + e->R] - (double)e->gtot[0]) / (double)e->N;
   e->cc_planned = !e->sx_planned && !e->xd_planned && e->cc_frac > 0 && mixed <= e->cc_frac;
@@ -1632,9 +1644,37 @@ int xd_check(gossip_engine* e) {
 }
 }  // namespace
 
+int gossip_xd_classes(gossip_engine_t* e, void** send, void** image, uint64_t* bytes) {
+  if (!send || !image || !bytes) return GOSSIP_EINVAL;
+  if (int rc = xd_check(e)) return rc;
+  *send = *image = nullptr;
+  *bytes = 0;
+  if (!e->xd_filt) return GOSSIP_OK;  // no filter this round: nothing to gather
+  const uint64_t nwl = (e->Nl + 63) / 64;
+  if (!e->xd_cls) {
+    HIP_OK(e, hipMalloc((void**)&e->xd_cls, (size_t)e->G * 2 * nwl * 8));
+    HIP_OK(e, hipMemsetAsync(e->xd_cls, 0, (size_t)e->G * 2 * nwl * 8, e->stream));
+    HIP_OK(e, hipMalloc((void**)&e->xd_keep, e->nown + 1));
+  }
+  if (int rc = sx_prepare(e)) return rc;  // exact occupancy bitmaps of S_t
+  uint64_t* own = e->xd_cls + (size_t)e->rank * 2 * nwl;
+  const uint64_t nwo = (e->nown + 63) / 64;  // (a short last shard: its tail words stay zero)
+  HIP_OK(e, hipMemcpyAsync(own, e->lf.nzb, nwo * 8, hipMemcpyDeviceToDevice, e->stream));
+  HIP_OK(e, hipMemcpyAsync(own + nwl, e->lf.fullb, nwo * 8, hipMemcpyDeviceToDevice, e->stream));
+  HIP_OK(e, hipStreamSynchronize(e->stream));
+  e->xd_cls_ok = true;
+  *send = own;
+  *image = e->xd_cls;
+  *bytes = 2 * nwl * 8;
+  return GOSSIP_OK;
+}
+
 int gossip_xd_requests(gossip_engine_t* e, void** ids, void** vals, uint64_t* send_counts) {
   if (!ids || !vals || !send_counts) return GOSSIP_EINVAL;
   if (int rc = xd_check(e)) return rc;
+  // a filtering round reads the gathered bitmaps: without gossip_xd_classes it runs unfiltered
+  // (the filter only drops edges that move nothing, so either way the round is the same)
+  const XdFilter xf{e->xd_cls, (uint32_t)((e->Nl + 63) / 64), e->xd_cls_ok ? e->xd_filt : 0u, e->xd_keep};
   if (!e->xd_smem) {
     const size_t bytes = xd_send_bytes(e->xg);
     if (hipMalloc(&e->xd_smem, bytes) != hipSuccess) {
@@ -1645,7 +1685,7 @@ int gossip_xd_requests(gossip_engine_t* e, void** ids, void** vals, uint64_t* se
   }
   HIP_OK(e, hipMemsetAsync(e->partial_d, 0, part_len(e) * 8, e->stream));
   if (int rc = timer_begin(e, 0)) return rc;
-  HIP_OK(e, launch_xd_requests(e->xg, e->xb, e->S, e->R, e->t, e->key0, e->key1, e->mode, e->fa, e->stream));
+  HIP_OK(e, launch_xd_requests(e->xg, e->xb, e->S, e->R, e->t, e->key0, e->key1, e->mode, e->fa, xf, e->stream));
   if (int rc = timer_end(e, 0)) return rc;
   HIP_OK(e, hipMemcpyAsync(e->xd_cnt_h, e->xb.ocnt, e->G * 4, hipMemcpyDeviceToHost, e->stream));
   HIP_OK(e, hipStreamSynchronize(e->stream));
@@ -1712,7 +1752,7 @@ int gossip_xd_finish(gossip_engine_t* e, uint64_t* partial) {
   if (int rc = copy_partial_out(e, partial)) return rc;
   if (int rc = timer_collect(e)) return rc;
   e->sx_valid = true;  // totals of the own nodes and exact bitmaps of S_{t+1}, fused into the apply
-  e->xd_planned = false;
+  e->xd_planned = e->xd_cls_ok = false;
   e->last_sparse = false;
   return GOSSIP_OK;
 }

@@ -90,6 +90,7 @@ SIGNATURES = [
     ("ae_serve", C.c_int, [P, C.POINTER(P)]),
     ("ae_response_recv", C.c_int, [P, C.POINTER(P)]),
     ("ae_finish", C.c_int, [P, U64P]),
+    ("xd_classes", C.c_int, [P, C.POINTER(P), C.POINTER(P), U64P]),
     ("xd_requests", C.c_int, [P, C.POINTER(P), C.POINTER(P), U64P]),
     ("xd_request_recv", C.c_int, [P, C.c_uint64, C.POINTER(P), C.POINTER(P)]),
     ("xd_serve", C.c_int, [P, C.POINTER(P)]),

@@ -328,6 +328,13 @@ class AbiEngine:
         return out
 
     # -- exchange dense rounds (include/gossip.h gossip_xd_*; gossip_hip.sharded drives them) --
+    def xd_classes(self):
+        """(own bitmaps pointer, image pointer, bytes per shard): bytes > 0 when this round filters
+        edges by the peer's class — all-gather bytes from every rank into the image first."""
+        send, img, nb = C.c_void_p(), C.c_void_p(), C.c_uint64()
+        self._check(self._fn("xd_classes")(self._h, C.byref(send), C.byref(img), C.byref(nb)))
+        return send.value, img.value, int(nb.value)
+
     def xd_requests(self):
         """(ids pointer, values pointer, items per owner) of this round's items (uint32 ids, uint64 values)."""
         ids, vals = C.c_void_p(), C.c_void_p()

@@ -15,7 +15,9 @@ without a GPU):
   exchange      (kind 3, DESIGN.md §5.2: dense rounds at G >= the "xd_shards" param) no
                 image: all-to-all of one item per live edge {p at its owner | flags,
                 S_t[n]} to p's owner, all-to-all of the pull replies back, all-reduce of
-                the partials;
+                the partials; when many nodes are empty or full, first an all-gather of
+                every shard's occupancy bitmaps, so the one-way edges that move nothing
+                (into an empty / full peer) are never sent;
   class-coded   (kind 4, DESIGN.md §5.1: dense rounds while few nodes are mixed) the
                 state all-gather as each shard's two occupancy bitmaps (empty / full)
                 plus the words of its mixed nodes, expanded into the image on arrival;
@@ -181,6 +183,9 @@ def _sparse_round(engine, comm: _Comm) -> np.ndarray:
 
 
 def _xd_round(engine, comm: _Comm) -> np.ndarray:
+    cls_p, img_p, nb = engine.xd_classes()
+    if nb and comm.world > 1:  # every shard's class bitmaps (in place): the edge filter of this round
+        comm.all_gather(_as_tensor(img_p, nb * comm.world, engine.on_device), _as_tensor(cls_p, nb, engine.on_device))
     ids_p, vals_p, counts = engine.xd_requests()
     in_counts = comm.all_to_all_small(counts) if comm.world > 1 else counts
     n_in, n_out = sum(in_counts), sum(counts)
@@ -298,7 +303,7 @@ def sharded_run(engine, max_rounds: int, group=None, kinds: list | None = None) 
 # -- single-process driver ---------------------------------------------------
 
 def _sync_all(engines):
-    for d in {e.device for e in engines}:
+    for d in {e.device for e in engines if e.on_device}:
         torch.cuda.synchronize(d)
 
 
@@ -393,20 +398,37 @@ def _lockstep_ae(engines):
     return [e.ae_finish() for e in engines]
 
 
-def _lockstep_xd(engines):
+def _lockstep_xd(engines, items: list | None = None):
+    """Exchange round of G engines in one process (device or host engines: copies in place of the
+    collectives); items gets each shard's per-owner item counts."""
     G = len(engines)
+
+    def view(e, ptr, nbytes, width=8):
+        return _as_tensor(ptr, nbytes, e.on_device, e.device if e.on_device else None, width=width)
+
+    cls = [e.xd_classes() for e in engines]
+    if cls[0][2]:  # the class bitmaps of every shard into every image (the own slot is in place)
+        nb = cls[0][2]
+        for e, (_, img_p, _) in zip(engines, cls):
+            img = view(e, img_p, nb * G)
+            for q, (send_q, _, _) in enumerate(cls):
+                if engines[q] is not e:
+                    img[q * nb // 8:(q + 1) * nb // 8].copy_(view(engines[q], send_q, nb))
+        _sync_all(engines)
     reqs = [e.xd_requests() for e in engines]  # (ids, vals, counts[owner])
+    if items is not None:
+        items.append([list(r[2]) for r in reqs])
     n_in = [sum(reqs[q][2][r] for q in range(G)) for r in range(G)]
     inbox = [e.xd_request_recv(n) for e, n in zip(engines, n_in)]
     for r in range(G):  # all-to-all: owner r receives from q = 0..G-1 in order
-        di = _as_tensor(inbox[r][0], n_in[r] * 4, True, engines[r].device, width=4)
-        dv = _as_tensor(inbox[r][1], n_in[r] * 8, True, engines[r].device)
+        di = view(engines[r], inbox[r][0], n_in[r] * 4, width=4)
+        dv = view(engines[r], inbox[r][1], n_in[r] * 8)
         at = 0
         for q, (ip, vp, cnt) in enumerate(reqs):
             if cnt[r]:
                 off, tot = sum(cnt[:r]), sum(cnt)
-                si = _as_tensor(ip, tot * 4, True, engines[q].device, width=4)
-                sv = _as_tensor(vp, tot * 8, True, engines[q].device)
+                si = view(engines[q], ip, tot * 4, width=4)
+                sv = view(engines[q], vp, tot * 8)
                 di[at:at + cnt[r]].copy_(si[off:off + cnt[r]])
                 dv[at:at + cnt[r]].copy_(sv[off:off + cnt[r]])
                 at += cnt[r]
@@ -414,11 +436,11 @@ def _lockstep_xd(engines):
     reps = [e.xd_serve() for e in engines]
     back = [e.xd_response_recv() for e in engines]
     for q, (_, _, cnt) in enumerate(reqs):  # replies return to q in its send order
-        dst = _as_tensor(back[q], sum(cnt) * 8, True, engines[q].device)
+        dst = view(engines[q], back[q], sum(cnt) * 8)
         at = 0
         for r in range(G):
             if cnt[r]:
-                src = _as_tensor(reps[r], n_in[r] * 8, True, engines[r].device)
+                src = view(engines[r], reps[r], n_in[r] * 8)
                 start = sum(reqs[q2][2][r] for q2 in range(q))  # where q's items landed in r's inbox
                 dst[at:at + cnt[r]].copy_(src[start:start + cnt[r]])
                 at += cnt[r]
@@ -449,11 +471,12 @@ def _lockstep_cc(engines):
     return [e.round_compute() for e in engines]
 
 
-def lockstep_run(engines, max_rounds: int):
+def lockstep_run(engines, max_rounds: int, items: list | None = None):
     """One process driving G shard engines (one per GPU, or several on one) through the
     same rounds as sharded_run, with device copies in place of the collectives.
     Returns (per-round stats, per-round kind: 0 dense / 1 sparse / 2 ANTIENTROPY / 3 exchange dense /
-    4 class-coded dense)."""
+    4 class-coded dense).  items (exchange rounds; host engines too): per round, each shard's
+    item counts per owner."""
     stats, kinds = [], []
     for _ in range(max_rounds):
         ks = [e.sharded_plan() for e in engines]
@@ -467,8 +490,10 @@ def lockstep_run(engines, max_rounds: int):
             ks = [e.sharded_plan(tot) for e in engines]
         assert len(set(ks)) == 1
         kinds.append(ks[0])
-        run = {1: _lockstep_sparse, 2: _lockstep_ae, 3: _lockstep_xd, 4: _lockstep_cc}.get(ks[0], _lockstep_dense)
-        parts = run(engines)
+        if ks[0] == 3:
+            parts = _lockstep_xd(engines, items)
+        else:
+            parts = {1: _lockstep_sparse, 2: _lockstep_ae, 4: _lockstep_cc}.get(ks[0], _lockstep_dense)(engines)
         tot = _lockstep_sum(parts)
         st = [e.round_commit(tot) for e in engines]
         assert all(s == st[0] for s in st)

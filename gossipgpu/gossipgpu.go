@@ -36,7 +36,7 @@ import (
 )
 
 // ABIVersion is the gossip.h version this binding is written against.
-const ABIVersion = 6
+const ABIVersion = 7
 
 // Mode is a dissemination rule (DESIGN.md §2).
 type Mode uint32
@@ -570,6 +570,18 @@ func (e *Engine) AEResponseRecv() (uintptr, error) {
 func (e *Engine) AEFinish() ([]uint64, error) {
 	out := make([]uint64, e.PartialLen())
 	return out, e.call(C.gossip_ae_finish(e.h, u64p(out)))
+}
+
+// XDClasses: with bytes > 0 this exchange round filters its edges by the peer's class: the
+// driver all-gathers bytes from every rank's send slot into image (own slot in place) before
+// XDRequests.  bytes == 0: nothing to gather.
+func (e *Engine) XDClasses() (send, image uintptr, bytes uint64, err error) {
+	var s, i unsafe.Pointer
+	var n C.uint64_t
+	if rc := C.gossip_xd_classes(e.h, &s, &i, &n); rc != 0 {
+		return 0, 0, 0, e.fail(rc)
+	}
+	return uintptr(s), uintptr(i), uint64(n), nil
 }
 
 // XDRequests: the items of an exchange dense round (plan kind 3) grouped by owner: ids (uint32,

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define GOSSIP_ABI_VERSION 6u
+#define GOSSIP_ABI_VERSION 7u
 
 /* Dissemination modes. */
 enum gossip_mode {
@@ -133,6 +133,7 @@ int gossip_set_stream(gossip_engine_t* eng, void* hip_stream);
  *                  rounds are exchange rounds; < 0 never, >= 1 always)
  *   "alld_frac"    sparse rounds commit every group's D once k x rare >= this x N
  *   "filter_frac"  dense rounds drop edges by the peer's class above this empty/full fraction
+ *   "xd_filter_frac"  exchange dense rounds likewise (default 0.6; >= 1 never)
  *   "ahead"        rounds enqueued ahead of the stats read back (1..7, default 2)
  *   "apply_grid"   persistent blocks of the dense apply pass (0 = one block per tile)
  *   "ae_sparse"    ANTIENTROPY: -1 plan sparse rounds (default), 0 never, 1 whenever valid
@@ -254,6 +255,16 @@ int gossip_ae_finish(gossip_engine_t* eng, uint64_t* partial);
  * The owner ORs the pushes into S_{t+1}[p] and answers each pull with S_t[p] (uint64, in
  * the received order); the sender's owner ORs the replies into S_{t+1}[n].
  * Per round, after gossip_sharded_plan -> kind 3:
+ *   gossip_xd_classes(&send, &image, &bytes)          bytes > 0: this round drops the one-way
+ *                                                      edges that move nothing (a pull-only edge
+ *                                                      into an empty peer, a push-only edge into a
+ *                                                      full one; "xd_filter_frac"; fanout <= 8): all-gather
+ *                                                      bytes from every rank's send into image (the
+ *                                                      own slot is send: in place).  A shard's slot,
+ *                                                      nwl = ceil(Nl / 64): [nz: nwl uint64][full:
+ *                                                      nwl uint64], occupancy bitmaps of S_t.
+ *                                                      Skipping the call runs the round unfiltered
+ *                                                      (same result, more items).
  *   gossip_xd_requests(&ids, &vals, send_counts[G])   items grouped by owner
  *   all-to-all of the counts; gossip_xd_request_recv(total_in, &ids, &vals);
  *   all-to-all of the ids (uint32) and of the values (uint64)
@@ -262,6 +273,7 @@ int gossip_ae_finish(gossip_engine_t* eng, uint64_t* partial);
  *   gossip_xd_finish(partial)                          -> all-reduce(SUM) -> gossip_round_commit */
 #define GOSSIP_XD_NO_PUSH (1u << 30)
 #define GOSSIP_XD_NO_PULL (1u << 31)
+int gossip_xd_classes(gossip_engine_t* eng, void** send, void** image, uint64_t* bytes);
 int gossip_xd_requests(gossip_engine_t* eng, void** ids, void** vals, uint64_t* send_counts);
 int gossip_xd_request_recv(gossip_engine_t* eng, uint64_t items, void** ids, void** vals);
 int gossip_xd_serve(gossip_engine_t* eng, void** replies);

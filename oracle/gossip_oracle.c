@@ -71,6 +71,13 @@ struct oracle_sim {
   uint32_t *xid, *xrid;
   uint64_t *xval, *xrval, *xrep_out, *xrep_in, *xnode;
   uint64_t xn_out, xn_in;
+  /* the exchange round's edge filter: filt bit 0 drops pull-only edges into empty peers, bit 1
+   * push-only edges into full peers (decided from the global totals, threshold xd_filter_frac);
+   * xcls = every shard's [nz][full] occupancy bitmaps of S_t (nwl words each) */
+  uint32_t xd_filt;
+  int xcls_ok;
+  double xd_filter_frac;
+  uint64_t* xcls;
   /* class-coded state all-gather (kind 4): every shard's slot ([nz][full]
    * bitmaps, nwl words each, then nwl uint32 prefixes: the mixed nodes before each bitmap
    * word), the own mixed words, every shard's at q * cc_stride */
@@ -236,6 +243,7 @@ int oracle_create(const gossip_config_t* cfg, int threads, oracle_sim_t** out) {
   s->sparse_frac = 0.25;
   s->xd_shards = 6;
   s->cc_frac = 0.75;
+  s->xd_filter_frac = 0.6; /* engine.hip xd_filter_frac */
   s->flood_edges = s->mode == GOSSIP_MODE_FLOOD && faulty;
   s->npend = cfg->stall_rounds > 1 ? cfg->stall_rounds - 1 : 1;
   if (cfg->stall_rounds && s->mode >= GOSSIP_MODE_PUSH && s->mode <= GOSSIP_MODE_PUSHPULL &&
@@ -261,7 +269,7 @@ void oracle_destroy(oracle_sim_t* s) {
   free(s->streak); free(s->pend); free(s->pend_n); free(s->skipE); free(s->skipE_n); free(s->ieo);
   free(s->aex_stale); free(s->req); free(s->loc); free(s->in); free(s->resp_out); free(s->resp_in);
   free(s->xid); free(s->xrid); free(s->xval); free(s->xrval); free(s->xrep_out); free(s->xrep_in); free(s->xnode);
-  free(s->cc_bits); free(s->cc_send); free(s->cc_vals);
+  free(s->cc_bits); free(s->cc_send); free(s->cc_vals); free(s->xcls);
   free(s);
 }
 
@@ -808,6 +816,15 @@ int oracle_sharded_plan(oracle_sim_t* s, const uint64_t* total, int32_t* kind) {
   const double frac = s->sparse_frac_set ? s->sparse_frac : s->xd_shards && s->G >= s->xd_shards ? 0.1 : 0.25;
   s->planned = (notfull < nz ? notfull : nz) <= frac * (double)s->N;
   s->xd_planned = !s->planned && s->xd_shards && s->G >= s->xd_shards;
+  /* the engine's dense_filter of the global totals (engine.hip): pulls from empty peers once more
+   * than xd_filter_frac of the nodes are empty, pushes into full peers likewise */
+  s->xd_filt = 0;
+  s->xcls_ok = 0;
+  if (s->xd_planned && s->k <= 8) { /* the engine keeps one verdict byte per sender: k <= 8 */
+    const double empty = 1.0 - nz / (double)s->N, full = (double)s->gtot[0] / (double)s->N;
+    const int can_pull = s->mode != GOSSIP_MODE_PUSH, can_push = s->mode != GOSSIP_MODE_PULL;
+    s->xd_filt = (can_pull && empty > s->xd_filter_frac ? 1u : 0u) | (can_push && full > s->xd_filter_frac ? 2u : 0u);
+  }
   /* the engine's class-coded all-gather: at most cc_frac mixed (nonzero, not full) nodes */
   const double mixed = ((double)s->gtot[4 + s->R] - (double)s->gtot[0]) / (double)s->N;
   s->cc_planned = !s->planned && !s->xd_planned && s->cc_frac > 0 && mixed <= s->cc_frac;
@@ -956,6 +973,40 @@ int oracle_sparse_commit(oracle_sim_t* s, uint64_t items, uint64_t* partial) {
 #define XD_NO_PUSH (1u << 30)
 #define XD_NO_PULL (1u << 31)
 
+/* The own slot of the class image ([nz][full], nwl words each) when this round filters. */
+int oracle_xd_classes(oracle_sim_t* s, void** send, void** image, uint64_t* bytes) {
+  if (!s || !send || !image || !bytes) return GOSSIP_EINVAL;
+  if (!s->xd_planned) return GOSSIP_ESTATE;
+  *send = *image = NULL;
+  *bytes = 0;
+  if (!s->xd_filt) return GOSSIP_OK;
+  const uint64_t nwl = (s->Nl + 63) / 64, fm = s->fullm[0];
+  if (!s->xcls && !(s->xcls = (uint64_t*)calloc(2 * nwl * s->G, 8))) return GOSSIP_ENOMEM;
+  uint64_t* own = s->xcls + (size_t)s->rank * 2 * nwl;
+  memset(own, 0, 2 * nwl * 8);
+  for (uint64_t i = 0; i < s->nown; ++i) {
+    if (s->S[i]) own[i / 64] |= 1ull << (i & 63);
+    if (s->S[i] == fm) own[nwl + i / 64] |= 1ull << (i & 63);
+  }
+  s->xcls_ok = 1;
+  *send = own;
+  *image = s->xcls;
+  *bytes = 2 * nwl * 8;
+  return GOSSIP_OK;
+}
+
+/* directions kept of edge n -> p (bit 0 push, bit 1 pull) under the round's filter: a one-way
+ * edge into a peer that cannot gain (push into full) or give (pull from empty) moves nothing */
+static int xd_keep(const oracle_sim_t* s, int push, int pull, uint64_t p) {
+  if (!s->xcls_ok || !s->xd_filt) return push | (pull << 1);
+  const uint64_t nwl = (s->Nl + 63) / 64, q = p / s->Nl, pl = p - q * s->Nl;
+  const uint64_t* slot = s->xcls + (size_t)q * 2 * nwl;
+  const int nz = (int)((slot[pl / 64] >> (pl & 63)) & 1), full = (int)((slot[nwl + pl / 64] >> (pl & 63)) & 1);
+  if ((s->xd_filt & 1u) && !push && pull && !nz) return 0;
+  if ((s->xd_filt & 2u) && push && !pull && full) return 0;
+  return push | (pull << 1);
+}
+
 int oracle_xd_requests(oracle_sim_t* s, void** ids, void** vals, uint64_t* send_counts) {
   if (!s || !ids || !vals || !send_counts || !s->xd_planned) return GOSSIP_ESTATE;
   const uint64_t cap = (uint64_t)s->k * s->nown + 1;
@@ -989,14 +1040,16 @@ int oracle_xd_requests(oracle_sim_t* s, void** ids, void** vals, uint64_t* send_
         }
         const uint32_t p = peer_from_word(r[j & 3], s->N, n);
         if (lost_edge(s, n, p, j, key)) continue;
+        const int d = xd_keep(s, push, pull, p);
+        if (!d) continue;
         const uint64_t q = p / s->Nl;
         if (pass == 0) {
           pos[q]++;
           continue;
         }
         const uint64_t at = pos[q]++;
-        s->xid[at] = (uint32_t)(p - q * s->Nl) | (push ? 0u : XD_NO_PUSH) | (pull ? 0u : XD_NO_PULL);
-        s->xval[at] = push ? x : 0;
+        s->xid[at] = (uint32_t)(p - q * s->Nl) | ((d & 1) ? 0u : XD_NO_PUSH) | ((d & 2) ? 0u : XD_NO_PULL);
+        s->xval[at] = (d & 1) ? x : 0;
         s->xnode[at] = i;
       }
     }
@@ -1045,7 +1098,7 @@ int oracle_xd_finish(oracle_sim_t* s, uint64_t* partial) {
   if (!s || !partial || !s->xd_planned || !s->xrep_in) return GOSSIP_ESTATE;
   for (uint64_t j = 0; j < s->xn_out; ++j) s->Snext[s->xnode[j]] |= s->xrep_in[j];
   totals_of(s, s->Snext, partial);
-  s->xd_planned = 0;
+  s->xd_planned = s->xcls_ok = 0;
   s->last_sparse = 0;
   return GOSSIP_OK;
 }
@@ -1145,6 +1198,11 @@ int oracle_set_param(oracle_sim_t* s, const char* name, double value) {
   if (!strcmp(name, "xd_shards")) {
     if (value < 0 || value > 1024) return GOSSIP_EINVAL;
     s->xd_shards = (uint32_t)value;
+    return GOSSIP_OK;
+  }
+  if (!strcmp(name, "xd_filter_frac")) {
+    if (value < 0 || value > 1) return GOSSIP_EINVAL;
+    s->xd_filter_frac = value;
     return GOSSIP_OK;
   }
   const char* known[] = {"alld_frac", "filter_frac", "ahead", "apply_grid", "ae_sparse", "ae_cap"};

@@ -71,6 +71,7 @@ int oracle_ae_serve(oracle_sim_t* s, void** send);
 int oracle_ae_response_recv(oracle_sim_t* s, void** recv);
 int oracle_ae_finish(oracle_sim_t* s, uint64_t* partial);
 int oracle_read_rows(oracle_sim_t* s, uint32_t* out, uint64_t n_values);
+int oracle_xd_classes(oracle_sim_t* s, void** send, void** image, uint64_t* bytes);
 int oracle_xd_requests(oracle_sim_t* s, void** ids, void** vals, uint64_t* send_counts);
 int oracle_xd_request_recv(oracle_sim_t* s, uint64_t items, void** ids, void** vals);
 int oracle_xd_serve(oracle_sim_t* s, void** replies);

@@ -26,6 +26,8 @@ PLANS = {"auto": (0, {}), "sparse": (0, {"sparse_frac": 1.0}), "sparse_alld": (0
          "classcoded": (0, {"sparse_frac": -1, "xd_shards": 0, "cc_frac": 1}),
          # dense rounds as exchange rounds (items to the peer's owner, replies back)
          "exchange": (0, {"sparse_frac": -1, "xd_shards": 2}), "auto_exchange": (0, {"xd_shards": 2}),
+         # exchange rounds that never drop edges by the peer's class (filter_frac 1)
+         "exchange_unfiltered": (0, {"sparse_frac": -1, "xd_shards": 2, "xd_filter_frac": 1.0}),
          # dense sharded rounds on the direct kernels instead of the binned push/pull passes
          "dense_direct": (FLAG_SHARD_DIRECT, {"sparse_frac": -1, "xd_shards": 0, "cc_frac": 0}),
          "classcoded_direct": (FLAG_SHARD_DIRECT, {"sparse_frac": -1, "xd_shards": 0, "cc_frac": 1}),
@@ -54,7 +56,7 @@ def test_lockstep_shards_equal_one_engine(case, plan):
         assert set(kinds) == {1}
     elif plan in ("dense", "dense_direct"):
         assert set(kinds) == {0}
-    elif plan == "exchange":
+    elif plan in ("exchange", "exchange_unfiltered"):
         assert set(kinds) == {3}
     elif plan in ("classcoded", "classcoded_direct"):
         assert set(kinds) == {4}
@@ -129,3 +131,32 @@ def test_lockstep_exchange_faults_stall(faults, plan):
         assert np.array_equal(e.read_shard(), full[:, e.lo:e.hi])
         e.close()
 
+
+
+@pytest.mark.parametrize("filter_frac", [0.3, 1.0], ids=["filtered", "unfiltered"])
+def test_exchange_items_equal_oracle(filter_frac):
+    """Every round an exchange round at G = 3: the items each shard sends to each owner (after
+    the class filter of DESIGN.md §5.2 in the rounds where it applies) are the oracle's, count for
+    count, round for round, and so are the stats; the filtered run sends fewer items."""
+    import oracle_py as op
+    N, G, R, k, seed = 200003, 3, 64, 2, 0x5EED0004
+    params = {"sparse_frac": -1, "xd_shards": 2, "xd_filter_frac": filter_frac}
+    runs = []
+    for mk in (lambda r: Engine(N, R, "pushpull", k, seed, flags=1, shard_rank=r, shard_count=G, params=params),
+               lambda r: op.OracleEngine(N, R, "pushpull", k, seed, flags=1, shard_rank=r, shard_count=G,
+                                         params=params)):
+        engines = [mk(r) for r in range(G)]
+        for e in engines:
+            e.inject_random()
+        items = []
+        stats, kinds = run_lockstep(engines, 200, items=items)
+        assert set(kinds) == {3}
+        runs.append((stats, items))
+        if engines[0].on_device:
+            for e in engines:
+                e.close()
+    (hs, hi), (os_, oi) = runs
+    assert hs == os_ and hi == oi
+    sent = sum(sum(map(sum, r)) for r in hi)
+    if filter_frac < 1:  # unfiltered, every round sends k items per node (no node is empty and full)
+        assert sent < 0.8 * k * N * len(hi)

@@ -54,11 +54,13 @@ PLANS = {
     "sparse": {"sparse_frac": 1.0},
     "dense": {"sparse_frac": -1, "xd_shards": 0, "cc_frac": 0},
     "exchange": {"sparse_frac": -1, "xd_shards": 2},
+    # exchange rounds that never filter edges by the peer's class
+    "exchange-unfiltered": {"sparse_frac": -1, "xd_shards": 2, "xd_filter_frac": 1.0},
     "auto-exchange": {"xd_shards": 2},
     "classcoded": {"sparse_frac": -1, "xd_shards": 0, "cc_frac": 1},
 }
 # the kinds every round of a plan must have (random modes)
-PLAN_KINDS = {"sparse": {1}, "dense": {0}, "exchange": {3}, "classcoded": {4}}
+PLAN_KINDS = {"sparse": {1}, "dense": {0}, "exchange": {3}, "exchange-unfiltered": {3}, "classcoded": {4}}
 
 
 def _worker(rank, world, port, case, q, params=None):
@@ -202,3 +204,68 @@ def test_empty_shard_equal_one(plan):
 def test_antientropy_empty_shards_equal_one():
     """100 nodes over 4 ranks in 64-node row blocks: shards of 64, 36, 0 and 0 nodes."""
     test_antientropy_sharded_equals_one((100, 8, 1, 5, 0.05, 0.3), world=4)
+
+
+def _host_xd_requests(engines, filter_frac):
+    """One exchange round's planning on G oracle shards in this process (host copies in place of
+    the collectives): the class-bitmap all-gather when the round filters, then the items per owner."""
+    import ctypes as C
+    G = len(engines)
+    for e in engines:
+        e.set_param("xd_filter_frac", filter_frac)
+    tot = sum(e.local_totals() for e in engines)
+    assert all(e.sharded_plan(tot) == 3 for e in engines)
+    cls = [e.xd_classes() for e in engines]
+    nb = cls[0][2]
+    assert all(c[2] == nb for c in cls)
+    if nb:
+        for r, (_, img, _) in enumerate(cls):
+            for q, (send_q, _, _) in enumerate(cls):
+                if q != r:
+                    C.memmove(img + q * nb, send_q, nb)
+    return nb, [e.xd_requests()[2] for e in engines]
+
+
+def test_exchange_filter_drops_idle_edges():
+    """With 64 rumors at their origins almost every node is empty: the filtered exchange round
+    sends no pull-only item into an empty peer (oracle restatement of csrc/binned.hip xd_filter),
+    so far fewer items than unfiltered; the rounds still equal one engine (test_two_ranks_equal_one)."""
+    import oracle_py as op
+    N, G = 6000, 3
+    out = {}
+    for ff in (1.0, 0.3):
+        engines = [op.OracleEngine(N, 64, "pushpull", 2, 9, flags=1, shard_rank=r, shard_count=G,
+                                   params={"sparse_frac": -1, "xd_shards": 2}) for r in range(G)]
+        for e in engines:
+            e.inject_random()
+        out[ff] = _host_xd_requests(engines, ff)
+    nb_off, cnt_off = out[1.0]
+    nb_on, cnt_on = out[0.3]
+    assert nb_off == 0 and nb_on == 2 * ((N + G - 1) // G + 63) // 64 * 8
+    sent_off = sum(map(sum, cnt_off))
+    sent_on = sum(map(sum, cnt_on))
+    # unfiltered: every node's k edges (all pull-only or two-way); filtered: only edges touching
+    # one of the <= 64 nonempty nodes survive
+    assert sent_off == 2 * N
+    assert 0 < sent_on <= 4 * 64
+
+
+def test_host_lockstep_filtered_exchange_equals_one():
+    """The lockstep driver over host (oracle) shards, every round an exchange round with the class
+    filter: the stats equal one engine, and the early (empty-majority) and late (full-majority)
+    rounds send a fraction of the k items per node of an unfiltered round."""
+    import oracle_py as op
+    from gossip_hip.sharded import lockstep_run
+    N, G, k = 30011, 3, 2
+    ref = op.OracleEngine(N, 64, "pushpull", k, 5, flags=1)
+    ref.inject_random()
+    want = ref.step(200)
+    engines = [op.OracleEngine(N, 64, "pushpull", k, 5, flags=1, shard_rank=r, shard_count=G,
+                               params={"sparse_frac": -1, "xd_shards": 2}) for r in range(G)]
+    for e in engines:
+        e.inject_random()
+    items = []
+    stats, kinds = lockstep_run(engines, 200, items=items)
+    assert stats == want.stats and set(kinds) == {3}
+    sent = [sum(map(sum, r)) for r in items]
+    assert sent[0] < k * N // 10 and sent[-1] < k * N // 10 and max(sent) == k * N

@@ -1,6 +1,9 @@
 """Per-rank cost of sharded rounds at G shards x 2^24 nodes, all G engines on one GPU in
 one process (gossip_hip.sharded.lockstep_run): every engine call is timed (that is one
-rank's device work), and the bytes each exchange moves per rank are recorded.  The link
+rank's device work), and the bytes each exchange moves per rank are recorded ("gathered":
+state all-gathers as received; exchange rounds: the class bitmaps received plus 20 B per item
+the rank sends off-rank, its 12-B item out and 8-B reply back, which by symmetry is what it
+also receives).  The link
 time of a real G-GPU run is not measured here: DESIGN.md §5 prices it."""
 import os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -17,7 +20,7 @@ if os.environ.get("GOSSIP_LIB"):  # a library variant (tools/build_variants.sh)
 G = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 LG = int(sys.argv[2]) if len(sys.argv) > 2 else 24
 CALLS = ("sparse_rare", "sparse_scan", "sparse_commit", "dense_prepare", "round_compute", "exchange_buffers",
-         "local_totals", "xd_requests", "xd_request_recv", "xd_serve", "xd_response_recv", "xd_finish",
+         "local_totals", "xd_classes", "xd_requests", "xd_request_recv", "xd_serve", "xd_response_recv", "xd_finish",
          "cc_send", "cc_recv", "cc_expand")
 # argv[3:]: gossip_set_param knobs as name=value (e.g. xd_shards=0: dense rounds on the state all-gather)
 PARAMS = {a.split("=")[0]: float(a.split("=")[1]) for a in sys.argv[3:]}
@@ -26,8 +29,8 @@ PARAMS = {a.split("=")[0]: float(a.split("=")[1]) for a in sys.argv[3:]}
 class Timed:
     """Times the engine calls of one rank; gathered: state bytes the rank receives this round."""
 
-    def __init__(self, e, log):
-        self._e, self._log = e, log
+    def __init__(self, e, log, rank):
+        self._e, self._log, self._rank = e, log, rank
         self.gathered = 0
 
     def __getattr__(self, name):
@@ -46,6 +49,10 @@ class Timed:
                 self.gathered = (G - 1) * r[1]
             elif name == "cc_recv":
                 self.gathered += (G - 1) * a[0] * 8
+            elif name == "xd_classes":
+                self.gathered = (G - 1) * r[2]
+            elif name == "xd_requests":  # items in (12 B) and replies in (8 B), ~ the items it sends off-rank
+                self.gathered += 20 * (sum(r[2]) - r[2][self._rank])
             return r
         return g
 
@@ -54,7 +61,7 @@ engines = [Engine(G << LG, 64, "pushpull", 2, 0x5EED0004, shard_rank=r, shard_co
            for r in range(G)]
 for rep in range(2):
     logs = [[] for _ in engines]
-    tes = [Timed(e, l) for e, l in zip(engines, logs)]
+    tes = [Timed(e, l, r) for r, (e, l) in enumerate(zip(engines, logs))]
     for e in engines:
         e.reset(); e.inject_random()
     rounds = []
