@@ -45,8 +45,19 @@ constexpr uint32_t kApplyPre = GOSSIP_APPLY_PRE;  // uint4 slots per thread of t
 #define GOSSIP_APPLY_UNROLL 16
 #endif
 constexpr int kUnroll = GOSSIP_APPLY_UNROLL;  // records in flight per lane in the run walkers (32 spills in K3)
-constexpr int kUnrollServe = 16;
-constexpr int kUnrollSeq = 8;  // records in flight per lane in the sequential response walker
+#ifndef GOSSIP_SERVE_UNROLL
+#define GOSSIP_SERVE_UNROLL 16
+#endif
+#ifndef GOSSIP_SEQ_UNROLL
+#define GOSSIP_SEQ_UNROLL 8
+#endif
+#ifndef GOSSIP_APPLY_PUSH_WAVES
+#define GOSSIP_APPLY_PUSH_WAVES 8
+#endif
+constexpr int kUnrollServe = GOSSIP_SERVE_UNROLL;
+constexpr int kUnrollSeq = GOSSIP_SEQ_UNROLL;  // records in flight per lane in the sequential response walker
+// push-pull apply: waves [0, kPushWaves) walk the pushes, the rest the responses
+constexpr uint32_t kPushWaves = GOSSIP_APPLY_PUSH_WAVES;
 #ifndef GOSSIP_APPLY_SPLIT
 #define GOSSIP_APPLY_SPLIT 1
 #endif
@@ -957,11 +968,11 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
   __syncthreads();
   const uint32_t wave = tid >> 6, nwav = kTileThreads / 64;
   const bool split = kApplySplit && mode == 3;
-  const bool do_push = (mode == 1 || mode == 3) && (!split || wave < nwav / 2);
-  const bool do_pull = (mode == 2 || mode == 3) && (!split || wave >= nwav / 2);
-  // split: waves [0, 8) walk the pushes, [8, 16) the responses (threads 512..1023)
-  const uint32_t qt0 = split ? kTileThreads / 2 : 0u, qnt = split ? kTileThreads / 2 : kTileThreads;
-  if (do_push) push_walk<kIdVZ>(g, b, X, acc, wmask, wlist, wbe, wen, split ? nwav / 2 : 0u);  // pushes aimed at this tile
+  const bool do_push = (mode == 1 || mode == 3) && (!split || wave < kPushWaves);
+  const bool do_pull = (mode == 2 || mode == 3) && (!split || wave >= kPushWaves);
+  // split: waves [0, kPushWaves) walk the pushes, the others the responses
+  const uint32_t qt0 = split ? kPushWaves * 64 : 0u, qnt = split ? kTileThreads - kPushWaves * 64 : kTileThreads;
+  if (do_push) push_walk<kIdVZ>(g, b, X, acc, wmask, wlist, wbe, wen, split ? kPushWaves : 0u);  // pushes aimed at this tile
   if (do_pull) {  // responses owed to this tile's own senders
     const uint32_t* __restrict__ qids = bq.ids;
     auto qids_base = [](const BinBufs& bb) { return bb.ids; };
