@@ -445,7 +445,9 @@ Est predict(const gossip_engine* e, const Est& x) {
 // (tools/shard_probe.py sweeps, profiles/r02_xd)
 double sparse_frac_of(const gossip_engine* e) {
   if (e->sparse_frac_set || !e->sx) return e->sparse_frac;
-  return e->xd && e->xd_shards && e->G >= e->xd_shards ? 0.1 : 0.25;
+  // before exchange rounds: 1/25 (a round with ~5 % rare nodes is cheaper as a class-filtered
+  // exchange round, profiles/r02_xdfilt/); before state all-gathers: 1/4
+  return e->xd && e->xd_shards && e->G >= e->xd_shards ? 0.04 : 0.25;
 }
 
 // sparse when the smaller rare class is at most sparse_frac * N; maj = which

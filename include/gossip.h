@@ -129,7 +129,7 @@ int gossip_set_stream(gossip_engine_t* eng, void* hip_stream);
 /* Tuning and path-selection knobs, for tests and benchmarks (the library reads no
  * environment variables).  Every value only moves time, never a result bit:
  *   "sparse_frac"  random modes: a round runs sparse when the rare class is at most
- *                  this fraction of N (default 1/16; sharded 1/4, or 1/10 when the dense
+ *                  this fraction of N (default 1/16; sharded 1/4, or 1/25 when the dense
  *                  rounds are exchange rounds; < 0 never, >= 1 always)
  *   "alld_frac"    sparse rounds commit every group's D once k x rare >= this x N
  *   "filter_frac"  dense rounds drop edges by the peer's class above this empty/full fraction

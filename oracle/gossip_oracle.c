@@ -812,8 +812,8 @@ int oracle_sharded_plan(oracle_sim_t* s, const uint64_t* total, int32_t* kind) {
   }
   const double nz = (double)s->gtot[4 + s->R], notfull = (double)s->N - (double)s->gtot[0];
   s->maj = notfull < nz;
-  /* the engine's default threshold (engine.hip sparse_frac_of): 1/10 before exchange rounds */
-  const double frac = s->sparse_frac_set ? s->sparse_frac : s->xd_shards && s->G >= s->xd_shards ? 0.1 : 0.25;
+  /* the engine's default threshold (engine.hip sparse_frac_of): 1/25 before exchange rounds */
+  const double frac = s->sparse_frac_set ? s->sparse_frac : s->xd_shards && s->G >= s->xd_shards ? 0.04 : 0.25;
   s->planned = (notfull < nz ? notfull : nz) <= frac * (double)s->N;
   s->xd_planned = !s->planned && s->xd_shards && s->G >= s->xd_shards;
   /* the engine's dense_filter of the global totals (engine.hip): pulls from empty peers once more
