@@ -20,6 +20,9 @@ struct AexArgs {
   uint64_t* boff;           // [blocks][G + 1] per-block offsets
   uint32_t* req;            // request items, grouped by owner: {p, n, row[K]} padded to rw words
   uint32_t* loc;            // own-own exchanges {n_local, p_local}
+  uint64_t* dirty;          // [ceil(Nl / 64)] own rows of Vn raised above S_t this round (serve / merge);
+                            // null: not tracked (a round with many items: the next one copies every row)
+  uint8_t* verdict;         // [nown] per own node, from the count pass: bit j = exchange j listed (k <= 8)
   uint64_t N, Nl, lo, nown;
   uint32_t G, rank, K, L, k, t, key0, key1, fail, rec, flags, rw, pw;
 };
@@ -27,6 +30,10 @@ struct AexArgs {
 // entries of the per-block tables (bcnt, boff) for nown own nodes and G shards
 size_t aex_block_table_words(uint64_t nown, uint32_t G);
 
+// Vn = S_t before round t: patch = Vn holds S_{t-1} and dirty marks the rows round t-1 raised
+// (the only rows where S_t differs): those rows are copied from V; else a full copy.  Both
+// leave dirty cleared for round t.
+hipError_t launch_aex_seed_next(AexArgs a, uint64_t* dirty, bool patch, hipStream_t st);
 // churn of round t over all N nodes (alive -> alive_n); then the own nodes' exchanges:
 // messages counted, those with a stale end listed (count pass, scan, fill pass)
 hipError_t launch_aex_requests(const AexArgs& a, hipStream_t st);

@@ -11,6 +11,9 @@
 // target moves nothing, so only exchanges with a stale end travel.
 #include "ae_sharded.h"
 
+#include <algorithm>
+#include <type_traits>
+
 #include "philox.h"
 #include "wave.h"
 
@@ -61,17 +64,33 @@ __global__ __launch_bounds__(kAxBlock) void aex_list_kernel(AexArgs a, uint32_t*
   block_range(a, &i0, &i1);
   const uint64_t nm1 = a.N - 1;
   uint64_t msgs = 0;
+  // k <= 8: the count pass leaves each node's listed exchanges in a verdict byte, and the fill
+  // pass redraws only the peers of nodes that list one (late rounds: a few thousand)
+  const bool verdicts = a.k <= 8;
   for (uint64_t i = i0 + threadIdx.x; i < i1; i += kAxBlock) {
     const uint64_t n = a.lo + i;
-    if (!bit_of(a.alive_n, n)) continue;
+    uint32_t vb = 0;
+    if (FILL && verdicts) {
+      vb = a.verdict[i];
+      if (!vb) continue;
+    } else if (!bit_of(a.alive_n, n)) {
+      if (!FILL && verdicts) a.verdict[i] = 0;
+      continue;
+    }
     const bool sn = bit_of(a.stale, n);
     u32x4 x{0, 0, 0, 0};
+    uint32_t listed = 0;
     for (uint32_t j = 0; j < a.k; ++j) {
       if ((j & 3u) == 0) x = philox4x32_10(u32x4{(uint32_t)n, a.t, 0u, j >> 2}, a.key0, a.key1);
       const uint32_t p = peer_from_word(lane_of(x, j & 3u), nm1, (uint32_t)n);
-      if (!bit_of(a.alive_n, p)) continue;
-      ++msgs;
-      if (!sn && !bit_of(a.stale, p)) continue;  // two target rows: nothing moves
+      if (FILL && verdicts) {
+        if (!((vb >> j) & 1u)) continue;
+      } else {
+        if (!bit_of(a.alive_n, p)) continue;
+        ++msgs;
+        if (!sn && !bit_of(a.stale, p)) continue;  // two target rows: nothing moves
+        listed |= 1u << j;
+      }
       const uint32_t q = (uint32_t)(p / a.Nl);
       const uint32_t slot = q == a.rank ? a.G : q;
       const uint32_t pos = atomicAdd(&c[slot], 1u);
@@ -88,6 +107,7 @@ __global__ __launch_bounds__(kAxBlock) void aex_list_kernel(AexArgs a, uint32_t*
         for (uint32_t cc = 0; cc < a.K; ++cc) it[2 + cc] = row[cc];
       }
     }
+    if (!FILL && verdicts) a.verdict[i] = (uint8_t)listed;
   }
   __syncthreads();
   if (!FILL) {
@@ -161,6 +181,12 @@ __global__ __launch_bounds__(kAxBlock) void aex_total_kernel(AexArgs a, const ui
 
 // requests received: lanes = components of one item; max-merge the pushed row into
 // Vn[p] (only where it is larger than S_t: Vn >= S_t throughout), answer S_t[p]
+// Marks own row i of Vn raised above S_t (the next round's patch copies it, launch_aex_seed_next).
+// (dirty = null: not tracked this round — many rows change, the next round copies them all)
+__device__ __forceinline__ void mark_dirty(const AexArgs& a, uint64_t i) {
+  if (a.dirty) atomicOr((unsigned long long*)&a.dirty[i >> 6], 1ull << (i & 63));
+}
+
 __global__ __launch_bounds__(kAxBlock) void aex_serve_kernel(AexArgs a, const uint32_t* __restrict__ in, uint64_t m,
                                                              uint32_t* __restrict__ resp) {
   const uint32_t per = kAxBlock / a.L, c = threadIdx.x % a.L;
@@ -170,7 +196,10 @@ __global__ __launch_bounds__(kAxBlock) void aex_serve_kernel(AexArgs a, const ui
     const uint32_t vp = a.V[pl * a.K + c];
     resp[it * a.pw + c] = vp;
     const uint32_t rv = in[it * a.rw + 2 + c];
-    if (rv > vp) atomicMax(&a.Vn[pl * a.K + c], rv);
+    if (rv > vp) {
+      atomicMax(&a.Vn[pl * a.K + c], rv);
+      mark_dirty(a, pl);
+    }
   }
 }
 
@@ -184,59 +213,84 @@ __global__ __launch_bounds__(kAxBlock) void aex_merge_kernel(AexArgs a, const ui
     if (it < nreq) {
       const uint64_t nl = a.req[it * a.rw + 1] - a.lo;
       const uint32_t rv = resp[it * a.pw + c];
-      if (rv > a.V[nl * a.K + c]) atomicMax(&a.Vn[nl * a.K + c], rv);
+      if (rv > a.V[nl * a.K + c]) {
+        atomicMax(&a.Vn[nl * a.K + c], rv);
+        mark_dirty(a, nl);
+      }
     } else {
       const uint64_t e = it - nreq;
       const uint64_t nl = a.loc[2 * e], pl = a.loc[2 * e + 1];
       const uint32_t vn = a.V[nl * a.K + c], vp = a.V[pl * a.K + c];
-      if (vp > vn) atomicMax(&a.Vn[nl * a.K + c], vp);
-      if (vn > vp) atomicMax(&a.Vn[pl * a.K + c], vn);
+      if (vp > vn) {
+        atomicMax(&a.Vn[nl * a.K + c], vp);
+        mark_dirty(a, nl);
+      }
+      if (vn > vp) {
+        atomicMax(&a.Vn[pl * a.K + c], vn);
+        mark_dirty(a, pl);
+      }
     }
   }
 }
 
-// Stats of the own rows R (S_{t+1}) with the alive bits after the churn, one wave per
-// 64 own nodes, one lane per node: full, alive, per-component counts, hash (global
-// ids, every node as on one shard), and the own stale words (STATS = false: the
-// stale words only).
-template <bool STATS>
+// Stats of the own rows R (S_{t+1}) with the alive bits after the churn: full, alive,
+// per-component counts, hash (global ids, every node as on one shard), and the own stale
+// words (STATS = false: the stale words only).  One wave per 64 own nodes (lo is 64-aligned:
+// the chunk is one word of the global bitmaps); lane (sub, c) holds component c of nodes
+// sub*L .. sub*L+L-1, one per sub-step, so every row load is a coalesced 4K-byte row and a
+// group's "differs" bits OR-reduce across its L lanes (antientropy.hip ae_stats_kernel).
+template <uint32_t L, bool STATS>
 __global__ __launch_bounds__(kAxBlock) void aex_stats_kernel(AexArgs a, const uint32_t* __restrict__ R) {
+  using BT = typename std::conditional<(L > 32), uint64_t, uint32_t>::type;
+  constexpr uint32_t per = 64 / L;
   __shared__ uint32_t cnt[64];
-  __shared__ uint32_t tgt[64];
   __shared__ uint64_t red[3][kAxBlock / 64];
-  if (threadIdx.x < 64) {
-    cnt[threadIdx.x] = 0;
-    tgt[threadIdx.x] = threadIdx.x < a.K ? a.target[threadIdx.x] : 0u;
-  }
+  if (threadIdx.x < 64) cnt[threadIdx.x] = 0;
   __syncthreads();
-  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t lane = threadIdx.x & 63, sub = lane / L, c = lane % L;
+  const uint32_t tgt = c < a.K ? a.target[c] : 0u;
   const uint64_t chunks = (a.nown + 63) / 64;
   uint64_t hash = 0, full = 0, nal = 0;
+  uint32_t c_lane = 0;
   for (uint64_t ch = (uint64_t)blockIdx.x * (kAxBlock / 64) + (threadIdx.x >> 6); ch < chunks;
        ch += (uint64_t)gridDim.x * (kAxBlock / 64)) {
-    const uint64_t i = ch * 64 + lane;
-    const bool valid = i < a.nown;
-    const uint64_t n = a.lo + i;
-    const bool al = valid && bit_of(a.alive_n, n);
-    bool stale = false;
-    for (uint32_t c = 0; c < a.K; ++c) {
-      const uint32_t v = valid ? R[i * a.K + c] : 0u;
-      if (STATS && (a.flags & 1u) && v) hash += mix64((uint64_t)v + ((uint64_t)c * a.N + n) * kGold64);
-      const bool eq = valid && v == tgt[c];
-      stale = stale || (valid && !eq);
-      if (STATS) {
-        const uint64_t m = __ballot(eq && al);
-        if (lane == 0 && m) atomicAdd(&cnt[c], (uint32_t)__popcll(m));
-      }
+    uint32_t v[L];
+#pragma unroll
+    for (uint32_t i = 0; i < L; ++i) {
+      const uint64_t il = ch * 64 + sub * L + i;
+      v[i] = (il < a.nown && c < a.K) ? R[il * a.K + c] : 0u;
     }
-    const uint64_t sw = __ballot(stale);
-    if (lane == 0 && a.stale_own) a.stale_own[ch] = sw;
+    const uint64_t aw = a.alive_n[a.lo / 64 + ch];  // (nodes past nown: not alive, no row)
+    BT bad = 0;
+    uint64_t hb = ((uint64_t)c * a.N + a.lo + ch * 64 + sub * L) * kGold64;  // stepped by kGold64 per node
+#pragma unroll
+    for (uint32_t i = 0; i < L; ++i) {
+      const uint64_t il = ch * 64 + sub * L + i;
+      const bool valid = il < a.nown && c < a.K;
+      const bool al = (aw >> (sub * L + i)) & 1ull;
+      if (STATS && (a.flags & 1u)) hash += valid && v[i] ? mix64((uint64_t)v[i] + hb) : 0ull;
+      hb += kGold64;
+      if (STATS) c_lane += (valid && al && v[i] == tgt) ? 1u : 0u;
+      bad |= (BT)(valid && v[i] != tgt) << i;
+    }
+#pragma unroll
+    for (uint32_t off = 1; off < L; off <<= 1) bad |= (BT)__shfl_xor(bad, (int)off, 64);
+    uint64_t stale = 0;
+    if (per <= L) {
+#pragma unroll
+      for (uint32_t g = 0; g < per; ++g) stale |= (uint64_t)__shfl(bad, (int)(g * L), 64) << (g * L);
+    } else {
+#pragma unroll
+      for (uint32_t i = 0; i < L; ++i) stale |= __ballot(c == 0 && ((bad >> i) & 1u)) << i;
+    }
+    if (lane == 0 && a.stale_own) a.stale_own[ch] = stale;
     if (STATS) {
-      full += (uint64_t)__popcll(__ballot(al && !stale));
-      nal += (uint64_t)__popcll(__ballot(al));
+      full += (uint64_t)__popcll(aw & ~stale);
+      nal += (uint64_t)__popcll(aw);
     }
   }
   if (!STATS) return;
+  if (c < a.K && c_lane) atomicAdd(&cnt[c], c_lane);
   if (lane != 0) full = nal = 0;  // wave-uniform: counted once per wave
   hash = wave_sum64(hash);
   full = wave_sum64(full);
@@ -248,13 +302,35 @@ __global__ __launch_bounds__(kAxBlock) void aex_stats_kernel(AexArgs a, const ui
   }
   __syncthreads();
   if (threadIdx.x < 3) {
-    uint64_t s = 0;
-    for (int w = 0; w < kAxBlock / 64; ++w) s += red[threadIdx.x][w];
+    uint64_t sum = 0;
+    for (int w = 0; w < kAxBlock / 64; ++w) sum += red[threadIdx.x][w];
     const uint32_t slot = threadIdx.x == 0 ? 3u : threadIdx.x == 1 ? 0u : 1u;
-    if (s) atomicAdd((unsigned long long*)&a.partial[slot], (unsigned long long)s);
+    if (sum) atomicAdd((unsigned long long*)&a.partial[slot], (unsigned long long)sum);
   }
   if (threadIdx.x < a.K && cnt[threadIdx.x])
     atomicAdd((unsigned long long*)&a.partial[4 + threadIdx.x], (unsigned long long)cnt[threadIdx.x]);
+}
+
+// Vn rows the previous round raised (dirty) := V rows, dirty cleared: one wave per 64 rows,
+// lanes as in the stats pass (coalesced rows); clean words cost one load.
+template <uint32_t L>
+__global__ __launch_bounds__(kAxBlock) void aex_patch_kernel(AexArgs a) {
+  constexpr uint32_t per = 64 / L;
+  const uint32_t lane = threadIdx.x & 63, sub = lane / L, c = lane % L;
+  const uint64_t chunks = (a.nown + 63) / 64;
+  for (uint64_t ch = (uint64_t)blockIdx.x * (kAxBlock / 64) + (threadIdx.x >> 6); ch < chunks;
+       ch += (uint64_t)gridDim.x * (kAxBlock / 64)) {
+    const uint64_t dw = a.dirty[ch];
+    if (!dw) continue;
+#pragma unroll
+    for (uint32_t i = 0; i < L; ++i) {
+      const uint32_t b = sub * L + i;
+      const uint64_t il = ch * 64 + b;
+      if (((dw >> b) & 1ull) && c < a.K) a.Vn[il * a.K + c] = a.V[il * a.K + c];
+    }
+    if (lane == 0) a.dirty[ch] = 0;
+  }
+  (void)per;
 }
 
 __global__ __launch_bounds__(kAxBlock) void aex_init_kernel(uint32_t* V, uint64_t lo, uint64_t nown, uint32_t K,
@@ -314,15 +390,53 @@ hipError_t launch_aex_serve(const AexArgs& a, const uint32_t* in, uint64_t m, ui
   return hipGetLastError();
 }
 
+namespace {
+template <bool STATS>
+void stats_l(const AexArgs& a, const uint32_t* R, hipStream_t st) {
+  const uint32_t g = ax_grid((a.nown + 63) / 64, kAxBlock / 64, 8192);
+  switch (a.L) {
+    case 1: aex_stats_kernel<1, STATS><<<g, kAxBlock, 0, st>>>(a, R); break;
+    case 2: aex_stats_kernel<2, STATS><<<g, kAxBlock, 0, st>>>(a, R); break;
+    case 4: aex_stats_kernel<4, STATS><<<g, kAxBlock, 0, st>>>(a, R); break;
+    case 8: aex_stats_kernel<8, STATS><<<g, kAxBlock, 0, st>>>(a, R); break;
+    case 16: aex_stats_kernel<16, STATS><<<g, kAxBlock, 0, st>>>(a, R); break;
+    case 32: aex_stats_kernel<32, STATS><<<g, kAxBlock, 0, st>>>(a, R); break;
+    default: aex_stats_kernel<64, STATS><<<g, kAxBlock, 0, st>>>(a, R); break;
+  }
+}
+}  // namespace
+
 hipError_t launch_aex_finish(const AexArgs& a, const uint32_t* resp, uint64_t nreq, uint64_t nloc, hipStream_t st) {
   if (nreq + nloc)
     aex_merge_kernel<<<ax_grid(nreq + nloc, kAxBlock / a.L, 65536), kAxBlock, 0, st>>>(a, resp, nreq, nloc);
-  aex_stats_kernel<true><<<ax_grid((a.nown + 63) / 64, kAxBlock / 64, 8192), kAxBlock, 0, st>>>(a, a.Vn);
+  stats_l<true>(a, a.Vn, st);
   return hipGetLastError();
 }
 
 hipError_t launch_aex_stale(const AexArgs& a, const uint32_t* V, hipStream_t st) {
-  aex_stats_kernel<false><<<ax_grid((a.nown + 63) / 64, kAxBlock / 64, 8192), kAxBlock, 0, st>>>(a, V);
+  stats_l<false>(a, V, st);
+  return hipGetLastError();
+}
+
+hipError_t launch_aex_seed_next(AexArgs a, uint64_t* dirty, bool patch, hipStream_t st) {
+  a.dirty = dirty;  // (the round's own args may not track it)
+  const uint64_t nw = (a.nown + 63) / 64;
+  if (!patch) {
+    hipError_t e = hipMemcpyAsync(a.Vn, a.V, (size_t)a.nown * a.K * 4, hipMemcpyDeviceToDevice, st);
+    if (e == hipSuccess) e = hipMemsetAsync(a.dirty, 0, std::max<uint64_t>(nw, 1) * 8, st);
+    return e;
+  }
+  if (nw == 0) return hipSuccess;
+  const uint32_t g = ax_grid(nw, kAxBlock / 64, 8192);
+  switch (a.L) {
+    case 1: aex_patch_kernel<1><<<g, kAxBlock, 0, st>>>(a); break;
+    case 2: aex_patch_kernel<2><<<g, kAxBlock, 0, st>>>(a); break;
+    case 4: aex_patch_kernel<4><<<g, kAxBlock, 0, st>>>(a); break;
+    case 8: aex_patch_kernel<8><<<g, kAxBlock, 0, st>>>(a); break;
+    case 16: aex_patch_kernel<16><<<g, kAxBlock, 0, st>>>(a); break;
+    case 32: aex_patch_kernel<32><<<g, kAxBlock, 0, st>>>(a); break;
+    default: aex_patch_kernel<64><<<g, kAxBlock, 0, st>>>(a); break;
+  }
   return hipGetLastError();
 }
 

@@ -106,6 +106,12 @@ struct gossip_engine {
   uint32_t *aex_bcnt = nullptr, *aex_req = nullptr, *aex_loc = nullptr, *aex_in = nullptr, *aex_resp_out = nullptr,
            *aex_resp_in = nullptr, *aex_tmp = nullptr;
   uint64_t aex_req_cap = 0, aex_in_cap = 0, aex_out_cap = 0, aex_nin = 0, aex_nreq = 0, aex_nloc = 0;
+  // Vn seeding (launch_aex_seed_next): after a completed round Vn holds S_{t-1} and aex_dirty marks the
+  // rows that round raised, so the next round copies only those; any direct write (reset, inject) voids it
+  uint64_t* aex_dirty = nullptr;  // [ceil(Nl / 64)]
+  uint8_t* aex_verdict = nullptr;  // [nown] the count pass's listed exchanges per own node
+  bool aex_patch_ok = false, aex_round_done = false;
+  bool aex_track = false;  // this round marks the rows it raises (few items: ae_request_recv decides)
   // binned (LDS) pipeline for W == 1 random modes on one shard
   bool binned = false;
   BinGeom bg{};
@@ -233,7 +239,7 @@ void free_all(gossip_engine* e) {
   if (e->sx_host) (void)hipHostFree(e->sx_host);
   void* ae[] = {e->V, e->Vn, e->target, e->alive, e->alive_n, e->ae_aux, e->ae_claim, e->ae_eid, e->ae_erow, e->ae_segn, e->ae_pmask,
                 e->ae_brec, e->ae_boff, e->aex_stale, e->aex_cnt, e->aex_boff, e->aex_bcnt, e->aex_req, e->aex_loc,
-                e->aex_in, e->aex_resp_out, e->aex_resp_in, e->aex_tmp};
+                e->aex_in, e->aex_resp_out, e->aex_resp_in, e->aex_tmp, e->aex_dirty, e->aex_verdict};
   if (e->aex_cnt_h) (void)hipHostFree(e->aex_cnt_h);
   for (void* b : ae)
     if (b) (void)hipFree(b);
@@ -777,6 +783,8 @@ AexArgs make_aex_args(gossip_engine* e) {
   a.boff = e->aex_boff;
   a.req = e->aex_req;
   a.loc = e->aex_loc;
+  a.dirty = e->aex_track ? e->aex_dirty : nullptr;
+  a.verdict = e->aex_verdict;
   a.N = e->N;
   a.Nl = e->Nl;
   a.lo = e->lo;
@@ -993,7 +1001,9 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
         !alloc_raw((void**)&e->aex_bcnt, tab * 4) || !alloc_raw((void**)&e->aex_boff, tab * 8) ||
         !alloc_raw((void**)&e->aex_req, e->aex_req_cap * e->aex_rw * 4) ||
         !alloc_raw((void**)&e->aex_loc, e->aex_req_cap * 8) ||
-        !alloc_raw((void**)&e->aex_resp_in, e->aex_req_cap * e->aex_pw * 4) || !alloc_raw((void**)&e->aex_tmp, 256))
+        !alloc_raw((void**)&e->aex_resp_in, e->aex_req_cap * e->aex_pw * 4) || !alloc_raw((void**)&e->aex_tmp, 256) ||
+        !alloc_raw((void**)&e->aex_dirty, std::max<size_t>((e->Nl + 63) / 64, 1) * 8) ||
+        !alloc_raw((void**)&e->aex_verdict, std::max<uint64_t>(e->nown, 1)))
       return bail(GOSSIP_ENOMEM);
     if (hipHostMalloc((void**)&e->aex_cnt_h, (G + 1) * 8) != hipSuccess) return bail(GOSSIP_ENOMEM);
     if (launch_aex_fill_alive(e->alive, e->N, gw, nullptr) != hipSuccess) return bail(GOSSIP_EHIP);
@@ -1255,7 +1265,7 @@ int gossip_reset(gossip_engine_t* e) {
     HIP_OK(e, hipMemsetAsync(e->V, 0, (size_t)e->Nl * e->R * 4, e->stream));
     HIP_OK(e, hipMemsetAsync(e->target, 0, 256, e->stream));
     HIP_OK(e, launch_aex_fill_alive(e->alive, e->N, (uint64_t)e->G * e->Nl / 64, e->stream));
-    e->aex_target_ok = false;
+    e->aex_target_ok = e->aex_patch_ok = false;
   } else if (e->mode == GOSSIP_MODE_ANTIENTROPY) {
     HIP_OK(e, hipMemsetAsync(e->V, 0, e->N * e->R * 4, e->stream));
     HIP_OK(e, hipMemsetAsync(e->target, 0, 256, e->stream));
@@ -1304,7 +1314,7 @@ int gossip_inject(gossip_engine_t* e, uint64_t node, uint32_t rumor) {
   if (e->aex) {  // a local write on the owner; the global max vector is re-derived before the next round
     if (node >= e->lo && node < e->hi)
       HIP_OK(e, launch_ae_inject(e->V, e->aex_tmp, node - e->lo, e->R, rumor, e->stream));
-    e->aex_target_ok = false;
+    e->aex_target_ok = e->aex_patch_ok = false;
     return GOSSIP_OK;
   }
   if (e->mode == GOSSIP_MODE_ANTIENTROPY) {
@@ -1327,7 +1337,7 @@ int gossip_inject_random(gossip_engine_t* e) {
   if (int rc = set_dev(e)) return rc;
   if (e->aex) {
     HIP_OK(e, launch_aex_init(e->V, e->lo, e->nown, e->R, e->key0, e->key1, e->stream));
-    e->aex_target_ok = false;
+    e->aex_target_ok = e->aex_patch_ok = false;
     return GOSSIP_OK;
   }
   if (e->mode == GOSSIP_MODE_ANTIENTROPY) {
@@ -1399,6 +1409,10 @@ int gossip_round_commit(gossip_engine_t* e, const uint64_t* total, gossip_round_
     HIP_OK(e, launch_stall_update(e->stall_d, e->N, e->k, e->t, e->key0, e->key1, e->fa, e->stream));
   }
   if (!e->last_sparse) rotate(e);  // sparse sharded rounds update S in place
+  if (e->aex) {  // V = S_{t+1}, Vn = S_t, aex_dirty = the rows where they differ
+    e->aex_patch_ok = e->aex_round_done;
+    e->aex_round_done = false;
+  }
   e->last_sparse = false;
   if (e->sx) {  // global totals of S_{t+1}: the next round's plan
     e->gtot.assign(total, total + part_len(e));
@@ -1801,8 +1815,9 @@ int gossip_ae_requests(gossip_engine_t* e, void** send, uint64_t* send_counts) {
   if (!e->aex_target_ok) return e->fail(GOSSIP_ESTATE, "the global max vector is stale: gossip_ae_set_target first");
   const AexArgs a = make_aex_args(e);
   HIP_OK(e, hipMemsetAsync(e->partial_d, 0, part_len(e) * 8, e->stream));
-  HIP_OK(e, hipMemcpyAsync(e->Vn, e->V, std::max<size_t>((size_t)e->nown * e->R * 4, 0), hipMemcpyDeviceToDevice,
-                           e->stream));  // S_{t+1} starts as S_t (max only grows)
+  // S_{t+1} starts as S_t (max only grows): the rows the last round raised, or every row
+  HIP_OK(e, launch_aex_seed_next(a, e->aex_dirty, e->aex_patch_ok, e->stream));
+  e->aex_patch_ok = e->aex_round_done = e->aex_track = false;
   if (int rc = timer_begin(e, 0)) return rc;
   HIP_OK(e, launch_aex_requests(a, e->stream));
   HIP_OK(e, hipMemcpyAsync(e->aex_cnt_h, e->aex_cnt, (e->G + 1) * 8, hipMemcpyDeviceToHost, e->stream));
@@ -1834,6 +1849,9 @@ int gossip_ae_request_recv(gossip_engine_t* e, uint64_t items, void** recv) {
     e->aex_in_cap = want;
   }
   e->aex_nin = items;
+  // few items (each raises at most one own row): mark the raised rows so the next round seeds
+  // S_{t+2} from them alone; many: it copies every row (atomics on the marks would cost more)
+  e->aex_track = e->aex_nreq + 2 * e->aex_nloc + items <= e->nown / 16;
   *recv = e->aex_in;
   return GOSSIP_OK;
 }
@@ -1866,6 +1884,8 @@ int gossip_ae_finish(gossip_engine_t* e, uint64_t* partial) {
   std::memcpy(partial, e->partial_h, part_len(e) * 8);
   partial[4 + e->R] = 0;  // (nonzero count: random modes only)
   e->last_sparse = false;
+  e->aex_round_done = e->aex_track;
+  e->aex_track = false;
   return GOSSIP_OK;
 }
 

@@ -89,14 +89,19 @@ for rep in range(2):
         tot = sh._lockstep_sum(parts)
         st = [te.round_commit(tot) for te in tes]
         per_rank = np.mean([sum(ms for _, ms in lg) for lg in logs])
-        rounds.append((t, per_rank, tes[0].recv, int(st[0]["alive_nodes"]), int(st[0]["full_nodes"])))
+        calls = {}
+        for lg in logs:
+            for name, ms in lg:
+                calls[name] = calls.get(name, 0.0) + ms / len(logs)
+        rounds.append((t, per_rank, tes[0].recv, int(st[0]["alive_nodes"]), int(st[0]["full_nodes"]), calls))
         if st[0]["converged"]:
             break
     if rep == 1:
-        for t, ms, rb, alive, full in rounds:
+        for t, ms, rb, alive, full, calls in rounds:
             if t < 16 or t % 10 == 0 or t == len(rounds) - 1:
+                br = " ".join(f"{n}={v:.3f}" for n, v in calls.items()) if t in (0, 50) else ""
                 print(f"G={G} round {t:3d} per-rank {ms:7.3f} ms  recv {rb / 2**20:7.1f} MiB  alive={alive} "
-                      f"stale={alive - full}", flush=True)
+                      f"stale={alive - full}  {br}", flush=True)
         tot_ms = sum(r[1] for r in rounds)
         print(f"G={G} N=2^{int(np.log2(N))} rounds={len(rounds)} sum per-rank {tot_ms:.1f} ms  "
               f"recv per rank {sum(r[2] for r in rounds) / 2**20:.1f} MiB  "
