@@ -9,10 +9,12 @@ namespace gossip {
 struct AexArgs {
   const uint32_t* V;        // own rows S_t [Nl][K] (node lo + i)
   uint32_t* Vn;             // own rows S_{t+1}
-  const uint64_t* alive;    // alive bits of every node before round t (global, G*Nl/64 words)
-  uint64_t* alive_n;        // after round t's churn
-  const uint64_t* stale;    // stale bits of S_t of every node (the all-gathered image)
-  uint64_t* stale_own;      // stale bits of S_{t+1} of the own nodes (next round's all-gather slice)
+  // The all-gathered image, one word pair per 64 nodes (global ids; a shard's slot is its
+  // Nl / 64 pairs, 64-aligned): [w][0] alive bits after round t's churn, [w][1] stale bits of
+  // S_t (row != target).  The owner computes both for its nodes (churn at gossip_exchange_buffers,
+  // stale bits of S_{t+1} in the stats pass), so one 16-B load answers both for any peer.
+  uint64_t* img;
+  bool write_stale;         // the stats pass writes the own stale words (not for gossip_state_hash)
   const uint32_t* target;   // global max vector [K]
   uint64_t* partial;        // [0] full [1] alive [2] messages [3] hash [4..4+K) per component
   uint64_t* cnt;            // [G + 1] items per owner (the last: own-own exchanges)
@@ -34,8 +36,10 @@ size_t aex_block_table_words(uint64_t nown, uint32_t G);
 // (the only rows where S_t differs): those rows are copied from V; else a full copy.  Both
 // leave dirty cleared for round t.
 hipError_t launch_aex_seed_next(AexArgs a, uint64_t* dirty, bool patch, hipStream_t st);
-// churn of round t over all N nodes (alive -> alive_n); then the own nodes' exchanges:
-// messages counted, those with a stale end listed (count pass, scan, fill pass)
+// churn of round t of the own nodes, in place in the own slot's alive words (round t - 1 -> t)
+hipError_t launch_aex_churn(const AexArgs& a, hipStream_t st);
+// the own nodes' exchanges of round t (after the all-gather): messages counted, those with a
+// stale end listed (count pass, scan, fill pass)
 hipError_t launch_aex_requests(const AexArgs& a, hipStream_t st);
 // requests received (m items): max-merge into Vn, responses V_t[p] in the received order
 hipError_t launch_aex_serve(const AexArgs& a, const uint32_t* in, uint64_t m, uint32_t* resp, hipStream_t st);
@@ -47,8 +51,8 @@ hipError_t launch_aex_stale(const AexArgs& a, const uint32_t* V, hipStream_t st)
 // initial versions of the own rows (Philox tag 3 with global node ids)
 hipError_t launch_aex_init(uint32_t* V, uint64_t lo, uint64_t nown, uint32_t K, uint32_t k0, uint32_t k1,
                            hipStream_t st);
-// every node alive (n < N), as plain bitmap words
-hipError_t launch_aex_fill_alive(uint64_t* alive, uint64_t N, uint64_t words, hipStream_t st);
+// every own node alive (the own slot's alive words; nodes >= N not)
+hipError_t launch_aex_fill_alive(const AexArgs& a, hipStream_t st);
 // max over the own rows into out[K] (zeroed here)
 hipError_t launch_aex_local_max(const uint32_t* V, uint64_t nown, uint32_t K, uint32_t* out, hipStream_t st);
 

@@ -5,10 +5,10 @@
 //
 // Reference: (*NodeState).Gossip, main.go:65-89 — here each exchange of the round
 // model is one SyncRPC-shaped request/reply between the two ends'
-// owners.  Every shard keeps the alive bits of all N nodes (churn is a per-node
-// Philox draw, tag 1, so no exchange is needed for it) and receives every shard's
-// stale bits (row != target) each round: an exchange between two rows equal to the
-// target moves nothing, so only exchanges with a stale end travel.
+// owners.  Every shard receives every shard's alive bits (its churn: a per-node Philox
+// draw, tag 1) and stale bits (row != target) each round, one 16-B word pair per 64 nodes:
+// an exchange between two rows equal to the target moves nothing, so only exchanges with
+// a stale end travel.
 #include "ae_sharded.h"
 
 #include <algorithm>
@@ -24,22 +24,30 @@ namespace {
 constexpr int kAxBlock = 256;
 constexpr uint32_t kAxMaxG = 1024;
 
-__device__ __forceinline__ bool bit_of(const uint64_t* w, uint64_t n) { return (w[n >> 6] >> (n & 63)) & 1ull; }
+// {alive, stale} word pair of the 64 nodes around global node n (one 16-B load)
+__device__ __forceinline__ uint4 pair_of(const uint64_t* img, uint64_t n) { return ((const uint4*)img)[n >> 6]; }
+__device__ __forceinline__ bool alive_in(const uint4& w, uint64_t n) {
+  return (((n & 63) < 32 ? w.x >> (n & 31) : w.y >> (n & 31)) & 1u) != 0;
+}
+__device__ __forceinline__ bool stale_in(const uint4& w, uint64_t n) {
+  return (((n & 63) < 32 ? w.z >> (n & 31) : w.w >> (n & 31)) & 1u) != 0;
+}
 
+// the own nodes' churn of round t: alive words of the own slot, round t - 1 -> t, in place
 __global__ __launch_bounds__(kAxBlock) void aex_churn_kernel(AexArgs a) {
   const uint32_t lane = threadIdx.x & 63;
-  const uint64_t words = a.G * a.Nl / 64;
-  for (uint64_t w = (uint64_t)blockIdx.x * (kAxBlock / 64) + (threadIdx.x >> 6); w < words;
-       w += (uint64_t)gridDim.x * (kAxBlock / 64)) {
-    const uint64_t n = w * 64 + lane;
+  const uint64_t chunks = (a.nown + 63) / 64, w0 = a.lo / 64;
+  for (uint64_t ch = (uint64_t)blockIdx.x * (kAxBlock / 64) + (threadIdx.x >> 6); ch < chunks;
+       ch += (uint64_t)gridDim.x * (kAxBlock / 64)) {
+    const uint64_t w = w0 + ch, n = w * 64 + lane;
     bool al = false;
-    if (n < a.N) {
-      const bool was = (a.alive[w] >> lane) & 1ull;
+    if (ch * 64 + lane < a.nown) {
+      const bool was = (a.img[2 * w] >> lane) & 1ull;
       const uint32_t x = philox4x32_10(u32x4{(uint32_t)n, a.t, 1u, 0u}, a.key0, a.key1).x;
       al = was ? !(x < a.fail) : (x < a.rec);
     }
     const uint64_t b = __ballot(al);
-    if (lane == 0) a.alive_n[w] = b;
+    if (lane == 0) a.img[2 * w] = b;
   }
 }
 
@@ -70,14 +78,18 @@ __global__ __launch_bounds__(kAxBlock) void aex_list_kernel(AexArgs a, uint32_t*
   for (uint64_t i = i0 + threadIdx.x; i < i1; i += kAxBlock) {
     const uint64_t n = a.lo + i;
     uint32_t vb = 0;
+    bool sn = false;
     if (FILL && verdicts) {
       vb = a.verdict[i];
       if (!vb) continue;
-    } else if (!bit_of(a.alive_n, n)) {
-      if (!FILL && verdicts) a.verdict[i] = 0;
-      continue;
+    } else {
+      const uint4 wn = pair_of(a.img, n);
+      if (!alive_in(wn, n)) {
+        if (!FILL && verdicts) a.verdict[i] = 0;
+        continue;
+      }
+      sn = stale_in(wn, n);
     }
-    const bool sn = bit_of(a.stale, n);
     u32x4 x{0, 0, 0, 0};
     uint32_t listed = 0;
     for (uint32_t j = 0; j < a.k; ++j) {
@@ -86,9 +98,10 @@ __global__ __launch_bounds__(kAxBlock) void aex_list_kernel(AexArgs a, uint32_t*
       if (FILL && verdicts) {
         if (!((vb >> j) & 1u)) continue;
       } else {
-        if (!bit_of(a.alive_n, p)) continue;
+        const uint4 wp = pair_of(a.img, p);
+        if (!alive_in(wp, p)) continue;
         ++msgs;
-        if (!sn && !bit_of(a.stale, p)) continue;  // two target rows: nothing moves
+        if (!sn && !stale_in(wp, p)) continue;  // two target rows: nothing moves
         listed |= 1u << j;
       }
       const uint32_t q = (uint32_t)(p / a.Nl);
@@ -260,7 +273,7 @@ __global__ __launch_bounds__(kAxBlock) void aex_stats_kernel(AexArgs a, const ui
       const uint64_t il = ch * 64 + sub * L + i;
       v[i] = (il < a.nown && c < a.K) ? R[il * a.K + c] : 0u;
     }
-    const uint64_t aw = a.alive_n[a.lo / 64 + ch];  // (nodes past nown: not alive, no row)
+    const uint64_t aw = a.img[2 * (a.lo / 64 + ch)];  // (nodes past nown: not alive, no row)
     BT bad = 0;
     uint64_t hb = ((uint64_t)c * a.N + a.lo + ch * 64 + sub * L) * kGold64;  // stepped by kGold64 per node
 #pragma unroll
@@ -283,7 +296,7 @@ __global__ __launch_bounds__(kAxBlock) void aex_stats_kernel(AexArgs a, const ui
 #pragma unroll
       for (uint32_t i = 0; i < L; ++i) stale |= __ballot(c == 0 && ((bad >> i) & 1u)) << i;
     }
-    if (lane == 0 && a.stale_own) a.stale_own[ch] = stale;
+    if (lane == 0 && a.write_stale) a.img[2 * (a.lo / 64 + ch) + 1] = stale;
     if (STATS) {
       full += (uint64_t)__popcll(aw & ~stale);
       nal += (uint64_t)__popcll(aw);
@@ -344,9 +357,12 @@ __global__ __launch_bounds__(kAxBlock) void aex_init_kernel(uint32_t* V, uint64_
   }
 }
 
-__global__ __launch_bounds__(kAxBlock) void aex_fill_alive_kernel(uint64_t* alive, uint64_t N, uint64_t words) {
-  for (uint64_t w = (uint64_t)blockIdx.x * kAxBlock + threadIdx.x; w < words; w += (uint64_t)gridDim.x * kAxBlock)
-    alive[w] = (w + 1) * 64 <= N ? ~0ull : (w * 64 < N ? (1ull << (N & 63)) - 1ull : 0ull);
+__global__ __launch_bounds__(kAxBlock) void aex_fill_alive_kernel(AexArgs a) {
+  const uint64_t chunks = (a.nown + 63) / 64, w0 = a.lo / 64;
+  for (uint64_t ch = (uint64_t)blockIdx.x * kAxBlock + threadIdx.x; ch < chunks; ch += (uint64_t)gridDim.x * kAxBlock) {
+    const uint64_t left = a.nown - ch * 64;
+    a.img[2 * (w0 + ch)] = left >= 64 ? ~0ull : (1ull << left) - 1ull;
+  }
 }
 
 __global__ __launch_bounds__(kAxBlock) void aex_max_kernel(const uint32_t* V, uint64_t nown, uint32_t K, uint32_t* out) {
@@ -370,10 +386,14 @@ uint32_t list_blocks(uint64_t nown) { return ax_grid(nown, 4 * kAxBlock, 2048); 
 
 size_t aex_block_table_words(uint64_t nown, uint32_t G) { return (size_t)list_blocks(nown) * (G + 1); }
 
+hipError_t launch_aex_churn(const AexArgs& a, hipStream_t st) {
+  if (a.nown == 0) return hipSuccess;
+  aex_churn_kernel<<<ax_grid((a.nown + 63) / 64, kAxBlock / 64, 8192), kAxBlock, 0, st>>>(a);
+  return hipGetLastError();
+}
+
 hipError_t launch_aex_requests(const AexArgs& a, hipStream_t st) {
   if (a.G > kAxMaxG) return hipErrorInvalidValue;
-  const uint32_t words = (uint32_t)(a.G * a.Nl / 64);
-  aex_churn_kernel<<<ax_grid(words, kAxBlock / 64, 8192), kAxBlock, 0, st>>>(a);
   const uint32_t nb = list_blocks(a.nown);
   uint32_t* bcnt = a.bcnt;
   uint64_t* boff = a.boff;
@@ -447,8 +467,9 @@ hipError_t launch_aex_init(uint32_t* V, uint64_t lo, uint64_t nown, uint32_t K, 
   return hipGetLastError();
 }
 
-hipError_t launch_aex_fill_alive(uint64_t* alive, uint64_t N, uint64_t words, hipStream_t st) {
-  aex_fill_alive_kernel<<<ax_grid(words, kAxBlock, 1024), kAxBlock, 0, st>>>(alive, N, words);
+hipError_t launch_aex_fill_alive(const AexArgs& a, hipStream_t st) {
+  if (a.nown == 0) return hipSuccess;
+  aex_fill_alive_kernel<<<ax_grid((a.nown + 63) / 64, kAxBlock, 1024), kAxBlock, 0, st>>>(a);
   return hipGetLastError();
 }
 

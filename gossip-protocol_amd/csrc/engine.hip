@@ -97,12 +97,13 @@ struct gossip_engine {
   bool ae_sb_valid = false;      // the stale bits of alive, ae_hash and ae_stale describe V
   bool ae_sparse_last = false;   // the last round ran in place (V not rotated)
   uint64_t ae_sparse_rounds = 0, ae_overflows = 0;
-  // sharded ANTIENTROPY (G > 1): V/Vn = own rows [Nl][K], alive/alive_n =
-  // plain alive bitmaps of all N nodes, aex_stale = every shard's stale words (all-gather image)
+  // sharded ANTIENTROPY (G > 1): V/Vn = own rows [Nl][K], aex_img = every
+  // shard's {alive, stale} word pairs (the all-gather image, ae_sharded.h AexArgs::img)
   bool aex = false;
   bool aex_target_ok = false;
   uint32_t aex_rw = 0, aex_pw = 0;
-  uint64_t *aex_stale = nullptr, *aex_cnt = nullptr, *aex_boff = nullptr, *aex_cnt_h = nullptr;
+  uint64_t *aex_img = nullptr, *aex_cnt = nullptr, *aex_boff = nullptr, *aex_cnt_h = nullptr;
+  uint64_t aex_churned = ~0ull;  // the round whose churn the own alive words hold
   uint32_t *aex_bcnt = nullptr, *aex_req = nullptr, *aex_loc = nullptr, *aex_in = nullptr, *aex_resp_out = nullptr,
            *aex_resp_in = nullptr, *aex_tmp = nullptr;
   uint64_t aex_req_cap = 0, aex_in_cap = 0, aex_out_cap = 0, aex_nin = 0, aex_nreq = 0, aex_nloc = 0;
@@ -238,7 +239,7 @@ void free_all(gossip_engine* e) {
     if (b) (void)hipFree(b);
   if (e->sx_host) (void)hipHostFree(e->sx_host);
   void* ae[] = {e->V, e->Vn, e->target, e->alive, e->alive_n, e->ae_aux, e->ae_claim, e->ae_eid, e->ae_erow, e->ae_segn, e->ae_pmask,
-                e->ae_brec, e->ae_boff, e->aex_stale, e->aex_cnt, e->aex_boff, e->aex_bcnt, e->aex_req, e->aex_loc,
+                e->ae_brec, e->ae_boff, e->aex_img, e->aex_cnt, e->aex_boff, e->aex_bcnt, e->aex_req, e->aex_loc,
                 e->aex_in, e->aex_resp_out, e->aex_resp_in, e->aex_tmp, e->aex_dirty, e->aex_verdict};
   if (e->aex_cnt_h) (void)hipHostFree(e->aex_cnt_h);
   for (void* b : ae)
@@ -320,12 +321,18 @@ int timer_collect(gossip_engine* e, bool count = true) {
   return GOSSIP_OK;
 }
 
+AexArgs make_aex_args(gossip_engine* e);
+
 // exchange payload for this round: S_t (random modes) or F_t (FLOOD); the
 // send slice lies inside the gathered image, so the all-gather is in place.
 int prepare_send(gossip_engine* e, uint64_t** send, uint64_t** image) {
-  if (e->aex) {  // sharded ANTIENTROPY: the own stale words into every shard's image
-    *send = e->aex_stale + (size_t)e->rank * e->Nl / 64;
-    *image = e->aex_stale;
+  if (e->aex) {  // sharded ANTIENTROPY: the own {alive, stale} word pairs into every shard's image
+    if (e->aex_churned != e->t) {  // the own nodes' churn of round t, once
+      HIP_OK(e, launch_aex_churn(make_aex_args(e), e->stream));
+      e->aex_churned = e->t;
+    }
+    *send = e->aex_img + (size_t)e->rank * e->Nl / 32;
+    *image = e->aex_img;
     return GOSSIP_OK;
   }
   if (e->mode == GOSSIP_MODE_ANTIENTROPY) {  // single shard: nothing to exchange
@@ -772,10 +779,8 @@ AexArgs make_aex_args(gossip_engine* e) {
   AexArgs a{};
   a.V = e->V;
   a.Vn = e->Vn;
-  a.alive = e->alive;
-  a.alive_n = e->alive_n;
-  a.stale = e->aex_stale;
-  a.stale_own = e->aex_stale + (size_t)e->rank * e->Nl / 64;
+  a.img = e->aex_img;
+  a.write_stale = true;
   a.target = e->target;
   a.partial = e->partial_d;
   a.cnt = e->aex_cnt;
@@ -996,8 +1001,7 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
     e->aex_req_cap = std::max<uint64_t>(e->nown * e->k, 1);
     const size_t tab = aex_block_table_words(e->nown, G);
     if (!alloc_raw((void**)&e->V, vb) || !alloc_raw((void**)&e->Vn, vb) || !alloc_raw((void**)&e->target, 256) ||
-        !alloc_raw((void**)&e->alive, gw * 8) || !alloc_raw((void**)&e->alive_n, gw * 8) ||
-        !alloc_raw((void**)&e->aex_stale, gw * 8) || !alloc_raw((void**)&e->aex_cnt, (G + 1) * 8) ||
+        !alloc_raw((void**)&e->aex_img, gw * 16) || !alloc_raw((void**)&e->aex_cnt, (G + 1) * 8) ||
         !alloc_raw((void**)&e->aex_bcnt, tab * 4) || !alloc_raw((void**)&e->aex_boff, tab * 8) ||
         !alloc_raw((void**)&e->aex_req, e->aex_req_cap * e->aex_rw * 4) ||
         !alloc_raw((void**)&e->aex_loc, e->aex_req_cap * 8) ||
@@ -1006,7 +1010,7 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
         !alloc_raw((void**)&e->aex_verdict, std::max<uint64_t>(e->nown, 1)))
       return bail(GOSSIP_ENOMEM);
     if (hipHostMalloc((void**)&e->aex_cnt_h, (G + 1) * 8) != hipSuccess) return bail(GOSSIP_ENOMEM);
-    if (launch_aex_fill_alive(e->alive, e->N, gw, nullptr) != hipSuccess) return bail(GOSSIP_EHIP);
+    if (launch_aex_fill_alive(make_aex_args(e), nullptr) != hipSuccess) return bail(GOSSIP_EHIP);
   } else if (e->mode == GOSSIP_MODE_ANTIENTROPY) {
     const size_t vb = (size_t)e->N * e->R * 4;
     const size_t nw = ((size_t)e->N + 63) / 64;
@@ -1264,7 +1268,8 @@ int gossip_reset(gossip_engine_t* e) {
   if (e->aex) {
     HIP_OK(e, hipMemsetAsync(e->V, 0, (size_t)e->Nl * e->R * 4, e->stream));
     HIP_OK(e, hipMemsetAsync(e->target, 0, 256, e->stream));
-    HIP_OK(e, launch_aex_fill_alive(e->alive, e->N, (uint64_t)e->G * e->Nl / 64, e->stream));
+    HIP_OK(e, launch_aex_fill_alive(make_aex_args(e), e->stream));
+    e->aex_churned = ~0ull;
     e->aex_target_ok = e->aex_patch_ok = false;
   } else if (e->mode == GOSSIP_MODE_ANTIENTROPY) {
     HIP_OK(e, hipMemsetAsync(e->V, 0, e->N * e->R * 4, e->stream));
@@ -1367,7 +1372,7 @@ int gossip_exchange_buffers(gossip_engine_t* e, void** send, void** recv, uint64
   HIP_OK(e, hipStreamSynchronize(e->stream));
   if (send) *send = s;
   if (recv) *recv = img;
-  if (send_bytes) *send_bytes = e->aex ? e->Nl / 8 : (uint64_t)e->W * e->Nl * 8;
+  if (send_bytes) *send_bytes = e->aex ? e->Nl / 4 : (uint64_t)e->W * e->Nl * 8;
   return GOSSIP_OK;
 }
 
@@ -1813,6 +1818,7 @@ int gossip_ae_requests(gossip_engine_t* e, void** send, uint64_t* send_counts) {
   if (!send || !send_counts) return GOSSIP_EINVAL;
   if (int rc = aex_check(e)) return rc;
   if (!e->aex_target_ok) return e->fail(GOSSIP_ESTATE, "the global max vector is stale: gossip_ae_set_target first");
+  if (e->aex_churned != e->t) return e->fail(GOSSIP_ESTATE, "gossip_exchange_buffers (and its all-gather) first");
   const AexArgs a = make_aex_args(e);
   HIP_OK(e, hipMemsetAsync(e->partial_d, 0, part_len(e) * 8, e->stream));
   // S_{t+1} starts as S_t (max only grows): the rows the last round raised, or every row
@@ -1958,9 +1964,9 @@ int gossip_read_versions(gossip_engine_t* e, uint64_t node, uint32_t* out, uint3
   HIP_OK(e, hipStreamSynchronize(e->stream));
   if (e->aex) {
     HIP_OK(e, hipMemcpy(out, e->V + (node - e->lo) * e->R, e->R * 4, hipMemcpyDeviceToHost));
-    if (alive) {
+    if (alive) {  // after the last completed round's churn (the own slot of the image)
       uint64_t w = 0;
-      HIP_OK(e, hipMemcpy(&w, e->alive + node / 64, 8, hipMemcpyDeviceToHost));
+      HIP_OK(e, hipMemcpy(&w, e->aex_img + 2 * (node / 64), 8, hipMemcpyDeviceToHost));
       *alive = (uint32_t)((w >> (node & 63)) & 1ull);
     }
     return GOSSIP_OK;
@@ -1999,8 +2005,7 @@ int gossip_state_hash(gossip_engine_t* e, uint64_t* out) {
     AexArgs a = make_aex_args(e);
     a.flags |= GOSSIP_FLAG_HASH;
     a.Vn = e->V;
-    a.alive_n = e->alive;
-    a.stale_own = nullptr;  // (the stale words are not wanted here)
+    a.write_stale = false;  // (the stale words are not wanted here)
     HIP_OK(e, hipMemsetAsync(e->partial_d, 0, part_len(e) * 8, e->stream));
     HIP_OK(e, launch_aex_finish(a, nullptr, 0, 0, e->stream));
     HIP_OK(e, hipMemcpyAsync(e->partial_h, e->partial_d, part_len(e) * 8, hipMemcpyDeviceToHost, e->stream));

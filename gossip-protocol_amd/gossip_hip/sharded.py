@@ -21,7 +21,7 @@ without a GPU):
   class-coded   (kind 4, DESIGN.md §5.1: dense rounds while few nodes are mixed) the
                 state all-gather as each shard's two occupancy bitmaps (empty / full)
                 plus the words of its mixed nodes, expanded into the image on arrival;
-  ANTIENTROPY   ("Design B") all-gather of the stale bits,
+  ANTIENTROPY   ("Design B") all-gather of the alive and stale bits,
                 all-to-all of request items {p, n, V_t[n]} to p's owner and of its
                 replies V_t[p], all-reduce of the partials; the global max vector
                 by an all-reduce MAX (ncclMax) after any injection.

@@ -223,9 +223,9 @@ int gossip_sparse_msg_recv(gossip_engine_t* eng, uint64_t items, void** recv);
 int gossip_sparse_commit(gossip_engine_t* eng, uint64_t items, uint64_t* partial);
 
 /* --- sharded ANTIENTROPY rounds (G > 1; DESIGN.md §5.3, "Design B") --------------
- * Rows are sharded by node id in 64-aligned blocks (Nl = ceil(ceil(N/G)/64)*64); every
- * shard keeps the alive bits of all N nodes (churn is a per-node Philox draw) and, per
- * round, receives every shard's stale bits (row != the global max vector).  An exchange
+ * Rows are sharded by node id in 64-aligned blocks (Nl = ceil(ceil(N/G)/64)*64); per round
+ * every shard churns its own nodes (a per-node Philox draw) and receives every shard's alive
+ * bits and stale bits (row != the global max vector).  An exchange
  * (n, p_j(n,t)) between two alive nodes with a stale end whose peer lives on another
  * shard becomes one request item {p, n, V_t[n]} to p's owner, who max-merges it into p
  * and answers V_t[p], which n's owner max-merges into n.  Items are uint32 words padded
@@ -233,7 +233,8 @@ int gossip_sparse_commit(gossip_engine_t* eng, uint64_t items, uint64_t* partial
  * Per round:
  *   gossip_sharded_plan -> kind -2: the global max vector is stale (after reset / inject):
  *        gossip_ae_local_target(out[K]) -> all-reduce(MAX) -> gossip_ae_set_target; plan again
- *   kind 2: gossip_exchange_buffers(send = own stale words, recv = all shards') -> all-gather
+ *   kind 2: gossip_exchange_buffers(send = the own slot: per 64 own nodes their alive bits after
+ *        this round's churn and their stale bits of S_t; recv = every shard's) -> all-gather
  *        gossip_ae_requests(&send, send_counts[G])          churn + request items by owner
  *        all-to-all of the counts; gossip_ae_request_recv(total_in, &recv); all-to-all items
  *        gossip_ae_serve(&send)                             responses, in the received order

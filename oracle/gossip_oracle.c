@@ -58,10 +58,12 @@ struct oracle_sim {
   uint64_t *pend, *pend_n, *skipE, *skipE_n;
   uint32_t* ieo;
   /* sharded ANTIENTROPY (G > 1): V/Vn = own rows [Nl][K], alive bytes of all N,
-   * aex_stale = every shard's stale words (the all-gather image), request / reply items */
+   * aex_img = every shard's {alive, stale} word pairs per 64 nodes (the all-gather image: the
+   * owner churns its nodes at exchange_buffers, aex_churned = that round), request / reply items */
   int aex, aex_target_ok;
+  uint32_t aex_churned;
   uint32_t rw, pw;
-  uint64_t* aex_stale;
+  uint64_t* aex_img;
   uint32_t *req, *loc, *in, *resp_out, *resp_in;
   uint64_t nreq, nloc, nin, in_cap, aex_msgs;
   /* exchange dense rounds (kind 3): items {p at owner | flags, S_t[n]} by owner;
@@ -85,6 +87,10 @@ struct oracle_sim {
   double cc_frac;
   uint64_t *cc_bits, *cc_send, *cc_vals, cc_stride;
 };
+
+static inline int churned(int alive, uint32_t n, uint32_t t, const uint32_t key[2], uint32_t fail, uint32_t rec);
+static inline int alive_bit(const oracle_sim_t* s, uint64_t n);
+static void aex_own_fill_alive(oracle_sim_t* s);
 
 /* ---------------- Philox4x32-10 (Random123; rocRAND philox4x32_10.h:270-302) ---- */
 void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
@@ -214,7 +220,7 @@ int oracle_create(const gossip_config_t* cfg, int threads, oracle_sim_t** out) {
     if (s->aex) {
       s->rw = (s->R + 3) / 2 * 2;
       s->pw = (s->R + 1) / 2 * 2;
-      s->aex_stale = (uint64_t*)calloc((size_t)G * s->Nl / 64 + 1, 8);
+      s->aex_img = (uint64_t*)calloc(2 * ((size_t)G * s->Nl / 64 + 1), 8);
       const size_t cap = (size_t)s->nown * s->k + 1;
       s->req = (uint32_t*)calloc(cap * s->rw, 4);
       s->loc = (uint32_t*)calloc(cap * 2, 4);
@@ -228,6 +234,7 @@ int oracle_create(const gossip_config_t* cfg, int threads, oracle_sim_t** out) {
       return GOSSIP_ENOMEM;
     }
     memset(s->alive, 1, s->N);
+    if (s->aex) aex_own_fill_alive(s);
   }
   if (!s->S || !s->Snext || !s->send || (G > 1 && !s->recv) || !s->fullm ||
       (s->mode == GOSSIP_MODE_FLOOD && (!s->Sprev || !s->skip))) {
@@ -267,7 +274,7 @@ void oracle_destroy(oracle_sim_t* s) {
   free(s->gtot); free(s->counts); free(s->rare_send); free(s->rare_recv); free(s->msg_send); free(s->msg_recv);
   free(s->D);
   free(s->streak); free(s->pend); free(s->pend_n); free(s->skipE); free(s->skipE_n); free(s->ieo);
-  free(s->aex_stale); free(s->req); free(s->loc); free(s->in); free(s->resp_out); free(s->resp_in);
+  free(s->aex_img); free(s->req); free(s->loc); free(s->in); free(s->resp_out); free(s->resp_in);
   free(s->xid); free(s->xrid); free(s->xval); free(s->xrval); free(s->xrep_out); free(s->xrep_in); free(s->xnode);
   free(s->cc_bits); free(s->cc_send); free(s->cc_vals); free(s->xcls);
   free(s);
@@ -350,6 +357,7 @@ int oracle_reset(oracle_sim_t* s) {
     memset(s->V, 0, (size_t)(s->aex ? s->Nl : s->N) * s->R * 4);
     memset(s->target, 0, (size_t)s->R * 4);
     memset(s->alive, 1, s->N);
+    if (s->aex) aex_own_fill_alive(s);
   }
   if (s->streak) memset(s->streak, 0, s->N);
   if (s->pend) {
@@ -410,10 +418,21 @@ uint64_t oracle_partial_len(const oracle_sim_t* s) { return 5 + (s ? s->R : 0); 
 /* Exchange payload: S_t for random modes, the frontier F_t = S_t & ~S_{t-1} for FLOOD. */
 int oracle_exchange_buffers(oracle_sim_t* s, void** send, void** recv, uint64_t* send_bytes) {
   if (!s) return GOSSIP_EINVAL;
-  if (s->aex) { /* own stale words into every shard's image */
-    if (send) *send = s->aex_stale + (size_t)s->rank * s->Nl / 64;
-    if (recv) *recv = s->aex_stale;
-    if (send_bytes) *send_bytes = s->Nl / 8;
+  if (s->aex) { /* the own {alive, stale} word pairs into every shard's image, after the own churn */
+    if (s->aex_churned != s->t) {
+      const uint32_t key[2] = {(uint32_t)s->cfg.seed, (uint32_t)(s->cfg.seed >> 32)};
+      uint64_t* own = s->aex_img + (size_t)s->rank * s->Nl / 32;
+      for (uint64_t i = 0; i < s->nown; ++i) {
+        const uint64_t bit = 1ull << (i & 63), n = s->lo + i;
+        const int al = churned((own[2 * (i >> 6)] & bit) != 0, (uint32_t)n, s->t, key, s->cfg.churn_fail,
+                               s->cfg.churn_recover);
+        own[2 * (i >> 6)] = al ? own[2 * (i >> 6)] | bit : own[2 * (i >> 6)] & ~bit;
+      }
+      s->aex_churned = s->t;
+    }
+    if (send) *send = s->aex_img + (size_t)s->rank * s->Nl / 32;
+    if (recv) *recv = s->aex_img;
+    if (send_bytes) *send_bytes = s->Nl / 4;
     return GOSSIP_OK;
   }
   if (s->mode == GOSSIP_MODE_ANTIENTROPY) return GOSSIP_OK; /* single shard: nothing to exchange */
@@ -1290,7 +1309,7 @@ int oracle_read_versions(oracle_sim_t* s, uint64_t node, uint32_t* out, uint32_t
   if (!s || !out || !s->V || node >= s->N || ncomp < s->R) return GOSSIP_EINVAL;
   if (s->aex && (node < s->lo || node >= s->hi)) return GOSSIP_EINVAL;
   memcpy(out, s->V + (node - (s->aex ? s->lo : 0)) * s->R, (size_t)s->R * 4);
-  if (alive) *alive = s->alive[node];
+  if (alive) *alive = s->aex ? (uint32_t)alive_bit(s, node) : s->alive[node];
   return GOSSIP_OK;
 }
 
@@ -1307,17 +1326,27 @@ int oracle_read_rows(oracle_sim_t* s, uint32_t* out, uint64_t n_values) {
  * per-node Philox draw) and receives every shard's stale words per round.  An exchange
  * (n, p_j(n,t)) of two alive nodes with a stale end and p on another shard is a request item
  * {p, n, V_t[n]} to p's owner, who max-merges it into p and answers V_t[p]. */
-static inline int stale_bit(const oracle_sim_t* s, uint64_t n) { return (s->aex_stale[n >> 6] >> (n & 63)) & 1; }
+static inline int alive_bit(const oracle_sim_t* s, uint64_t n) { return (s->aex_img[2 * (n >> 6)] >> (n & 63)) & 1; }
+static inline int stale_bit(const oracle_sim_t* s, uint64_t n) { return (s->aex_img[2 * (n >> 6) + 1] >> (n & 63)) & 1; }
 
 static void aex_own_stale(oracle_sim_t* s, const uint32_t* V) {
-  uint64_t* own = s->aex_stale + (size_t)s->rank * s->Nl / 64;
-  memset(own, 0, s->Nl / 8);
+  uint64_t* own = s->aex_img + (size_t)s->rank * s->Nl / 32;
+  for (uint64_t w = 0; w < s->Nl / 64; ++w) own[2 * w + 1] = 0;
   for (uint64_t i = 0; i < s->nown; ++i)
     for (uint32_t c = 0; c < s->R; ++c)
       if (V[i * s->R + c] != s->target[c]) {
-        own[i >> 6] |= 1ull << (i & 63);
+        own[2 * (i >> 6) + 1] |= 1ull << (i & 63);
         break;
       }
+}
+
+/* every own node alive (before round 0's churn) */
+static void aex_own_fill_alive(oracle_sim_t* s) {
+  if (!s->aex_img) return; /* (allocation failed: create reports it) */
+  uint64_t* own = s->aex_img + (size_t)s->rank * s->Nl / 32;
+  for (uint64_t w = 0; w < s->Nl / 64; ++w) own[2 * w] = 0;
+  for (uint64_t i = 0; i < s->nown; ++i) own[2 * (i >> 6)] |= 1ull << (i & 63);
+  s->aex_churned = UINT32_MAX;
 }
 
 uint32_t oracle_ae_item_words(const oracle_sim_t* s, uint32_t which) {
@@ -1343,10 +1372,9 @@ int oracle_ae_set_target(oracle_sim_t* s, const uint32_t* target) {
 
 int oracle_ae_requests(oracle_sim_t* s, void** send, uint64_t* send_counts) {
   if (!s || !send || !send_counts || !s->aex || !s->aex_target_ok) return GOSSIP_EINVAL;
+  if (s->aex_churned != s->t) return GOSSIP_ESTATE; /* oracle_exchange_buffers (and its all-gather) first */
   const uint32_t key[2] = {(uint32_t)s->cfg.seed, (uint32_t)(s->cfg.seed >> 32)};
   const uint32_t K = s->R;
-  for (uint64_t n = 0; n < s->N; ++n)
-    s->alive_n[n] = (uint8_t)churned(s->alive[n], (uint32_t)n, s->t, key, s->cfg.churn_fail, s->cfg.churn_recover);
   memcpy(s->Vn, s->V, (size_t)s->nown * K * 4);
   s->aex_msgs = 0;
   s->nreq = s->nloc = 0;
@@ -1355,7 +1383,7 @@ int oracle_ae_requests(oracle_sim_t* s, void** send, uint64_t* send_counts) {
   for (uint32_t pass = 0; pass <= s->G; ++pass) {
     for (uint64_t i = 0; i < s->nown; ++i) {
       const uint64_t n = s->lo + i;
-      if (!s->alive_n[n]) continue;
+      if (!alive_bit(s, n)) continue;
       uint32_t x[4] = {0, 0, 0, 0};
       for (uint32_t j = 0; j < s->k; ++j) {
         if ((j & 3) == 0) {
@@ -1363,7 +1391,7 @@ int oracle_ae_requests(oracle_sim_t* s, void** send, uint64_t* send_counts) {
           oracle_philox4x32_10(ctr, key, x);
         }
         const uint32_t p = peer_from_word(x[j & 3], s->N, (uint32_t)n);
-        if (!s->alive_n[p]) continue;
+        if (!alive_bit(s, p)) continue;
         if (pass == 0) ++s->aex_msgs;
         if (!stale_bit(s, n) && !stale_bit(s, p)) continue;
         const uint32_t q = (uint32_t)(p / s->Nl);
@@ -1448,9 +1476,9 @@ int oracle_ae_finish(oracle_sim_t* s, uint64_t* partial) {
       const uint32_t v = s->Vn[i * K + c];
       if (v && (s->cfg.flags & GOSSIP_FLAG_HASH)) partial[3] += oracle_mix64((uint64_t)v + ((uint64_t)c * s->N + n) * GOLD64);
       if (v != s->target[c]) isfull = 0;
-      else if (s->alive_n[n]) partial[4 + c]++;
+      else if (alive_bit(s, n)) partial[4 + c]++;
     }
-    if (s->alive_n[n]) {
+    if (alive_bit(s, n)) {
       partial[1]++;
       partial[0] += isfull;
     }

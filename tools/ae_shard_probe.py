@@ -63,7 +63,7 @@ print(f"one GPU: N=2^{int(np.log2(N))} {res.rounds} rounds in {one_ms:.1f} ms wa
       f"{N * res.rounds / one_ms / 1e6:.3g} G node-updates/s", flush=True)
 ref.close()
 
-engines = [Engine(N, K, "antientropy", k, seed, flags=1, shard_rank=r, shard_count=G, **kw) for r in range(G)]
+engines = [Engine(N, K, "antientropy", k, seed, flags=0, shard_rank=r, shard_count=G, **kw) for r in range(G)]
 for r, e in enumerate(engines):
     e.shard_rank_ = r
 for rep in range(2):
