@@ -22,6 +22,9 @@ namespace gossip {
 namespace {
 
 constexpr int kAxBlock = 256;
+#ifndef GOSSIP_AEX_STATS_GRID
+#define GOSSIP_AEX_STATS_GRID 1024
+#endif
 constexpr uint32_t kAxMaxG = 1024;
 
 // {alive, stale} word pair of the 64 nodes around global node n (one 16-B load)
@@ -413,7 +416,9 @@ hipError_t launch_aex_serve(const AexArgs& a, const uint32_t* in, uint64_t m, ui
 namespace {
 template <bool STATS>
 void stats_l(const AexArgs& a, const uint32_t* R, hipStream_t st) {
-  const uint32_t g = ax_grid((a.nown + 63) / 64, kAxBlock / 64, 8192);
+  // 1024 blocks (each wave walks ~32 chunks): every block ends in ~20 same-address atomics on
+  // the partials, which at 8192 blocks cost as much as the rows (2^23 rows: 157 us min)
+  const uint32_t g = ax_grid((a.nown + 63) / 64, kAxBlock / 64, GOSSIP_AEX_STATS_GRID);
   switch (a.L) {
     case 1: aex_stats_kernel<1, STATS><<<g, kAxBlock, 0, st>>>(a, R); break;
     case 2: aex_stats_kernel<2, STATS><<<g, kAxBlock, 0, st>>>(a, R); break;
@@ -447,7 +452,7 @@ hipError_t launch_aex_seed_next(AexArgs a, uint64_t* dirty, bool patch, hipStrea
     return e;
   }
   if (nw == 0) return hipSuccess;
-  const uint32_t g = ax_grid(nw, kAxBlock / 64, 8192);
+  const uint32_t g = ax_grid(nw, kAxBlock / 64, 512);  // mostly clean words: few waves suffice
   switch (a.L) {
     case 1: aex_patch_kernel<1><<<g, kAxBlock, 0, st>>>(a); break;
     case 2: aex_patch_kernel<2><<<g, kAxBlock, 0, st>>>(a); break;

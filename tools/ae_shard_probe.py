@@ -14,7 +14,11 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 from gossip_hip import FLAG_TIMING, Engine  # noqa: E402
 from gossip_hip import sharded as sh  # noqa: E402
+from gossip_hip import engine as _eng  # noqa: E402
 from gossip_hip.engine import churn_threshold as ct  # noqa: E402
+
+if os.environ.get("GOSSIP_LIB"):  # a library variant (tools/build_variants.sh)
+    _eng.load_library(os.environ["GOSSIP_LIB"])
 
 G = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 N = 1 << (int(sys.argv[2]) if len(sys.argv) > 2 else 26)
