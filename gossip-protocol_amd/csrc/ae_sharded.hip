@@ -67,63 +67,93 @@ __device__ __forceinline__ void block_range(const AexArgs& a, uint64_t* i0, uint
 // written at boff[b][q] + LDS cursor (request items {p, n, row[K]}, own-own pairs).
 template <bool FILL>
 __global__ __launch_bounds__(kAxBlock) void aex_list_kernel(AexArgs a, uint32_t* bcnt, const uint64_t* boff) {
+  constexpr uint32_t kStage = kAxBlock * 8;  // items one pass of the block lists at most (k <= 8)
   __shared__ uint32_t c[kAxMaxG + 1];
   __shared__ uint64_t red[kAxBlock / 64];
+  __shared__ uint32_t st_at[FILL ? kStage : 1], st_i[FILL ? kStage : 1], st_p[FILL ? kStage : 1];
+  __shared__ uint32_t st_n;
   for (uint32_t q = threadIdx.x; q <= a.G; q += kAxBlock) c[q] = 0;
+  if (threadIdx.x == 0) st_n = 0;
   __syncthreads();
   uint64_t i0, i1;
   block_range(a, &i0, &i1);
   const uint64_t nm1 = a.N - 1;
   uint64_t msgs = 0;
   // k <= 8: the count pass leaves each node's listed exchanges in a verdict byte, and the fill
-  // pass redraws only the peers of nodes that list one (late rounds: a few thousand)
+  // pass redraws only the peers of nodes that list one (late rounds: a few thousand); the
+  // request items it lists are staged in LDS and their rows copied by L lanes per item
+  // (coalesced 4K-byte rows: a lane per item reading its own row was 1.4 ms of a G = 8 round)
   const bool verdicts = a.k <= 8;
-  for (uint64_t i = i0 + threadIdx.x; i < i1; i += kAxBlock) {
+  for (uint64_t b0 = i0; b0 < i1; b0 += kAxBlock) {  // block-uniform trip count (the staging barriers)
+    const uint64_t i = b0 + threadIdx.x;
     const uint64_t n = a.lo + i;
     uint32_t vb = 0;
-    bool sn = false;
-    if (FILL && verdicts) {
+    bool sn = false, go = i < i1;
+    if (go && FILL && verdicts) {
       vb = a.verdict[i];
-      if (!vb) continue;
-    } else {
+      go = vb != 0;
+    } else if (go) {
       const uint4 wn = pair_of(a.img, n);
       if (!alive_in(wn, n)) {
         if (!FILL && verdicts) a.verdict[i] = 0;
-        continue;
+        go = false;
       }
-      sn = stale_in(wn, n);
+      sn = go && stale_in(wn, n);
     }
-    u32x4 x{0, 0, 0, 0};
-    uint32_t listed = 0;
-    for (uint32_t j = 0; j < a.k; ++j) {
-      if ((j & 3u) == 0) x = philox4x32_10(u32x4{(uint32_t)n, a.t, 0u, j >> 2}, a.key0, a.key1);
-      const uint32_t p = peer_from_word(lane_of(x, j & 3u), nm1, (uint32_t)n);
-      if (FILL && verdicts) {
-        if (!((vb >> j) & 1u)) continue;
-      } else {
-        const uint4 wp = pair_of(a.img, p);
-        if (!alive_in(wp, p)) continue;
-        ++msgs;
-        if (!sn && !stale_in(wp, p)) continue;  // two target rows: nothing moves
-        listed |= 1u << j;
+    if (go) {
+      u32x4 x{0, 0, 0, 0};
+      uint32_t listed = 0;
+      for (uint32_t j = 0; j < a.k; ++j) {
+        if ((j & 3u) == 0) x = philox4x32_10(u32x4{(uint32_t)n, a.t, 0u, j >> 2}, a.key0, a.key1);
+        const uint32_t p = peer_from_word(lane_of(x, j & 3u), nm1, (uint32_t)n);
+        if (FILL && verdicts) {
+          if (!((vb >> j) & 1u)) continue;
+        } else {
+          const uint4 wp = pair_of(a.img, p);
+          if (!alive_in(wp, p)) continue;
+          ++msgs;
+          if (!sn && !stale_in(wp, p)) continue;  // two target rows: nothing moves
+          listed |= 1u << j;
+        }
+        const uint32_t q = (uint32_t)(p / a.Nl);
+        const uint32_t slot = q == a.rank ? a.G : q;
+        const uint32_t pos = atomicAdd(&c[slot], 1u);
+        if (!FILL) continue;
+        const uint64_t at = boff[(uint64_t)blockIdx.x * (a.G + 1) + slot] + pos;
+        if (slot == a.G) {
+          a.loc[2 * at] = (uint32_t)i;
+          a.loc[2 * at + 1] = (uint32_t)(p - a.lo);
+        } else if (verdicts) {
+          const uint32_t e = atomicAdd(&st_n, 1u);
+          st_at[e] = (uint32_t)at;
+          st_i[e] = (uint32_t)i;
+          st_p[e] = p;
+        } else {
+          uint32_t* it = a.req + at * a.rw;
+          it[0] = p;
+          it[1] = (uint32_t)n;
+          const uint32_t* row = a.V + i * a.K;
+          for (uint32_t cc = 0; cc < a.K; ++cc) it[2 + cc] = row[cc];
+        }
       }
-      const uint32_t q = (uint32_t)(p / a.Nl);
-      const uint32_t slot = q == a.rank ? a.G : q;
-      const uint32_t pos = atomicAdd(&c[slot], 1u);
-      if (!FILL) continue;
-      const uint64_t at = boff[(uint64_t)blockIdx.x * (a.G + 1) + slot] + pos;
-      if (slot == a.G) {
-        a.loc[2 * at] = (uint32_t)i;
-        a.loc[2 * at + 1] = (uint32_t)(p - a.lo);
-      } else {
-        uint32_t* it = a.req + at * a.rw;
-        it[0] = p;
-        it[1] = (uint32_t)n;
-        const uint32_t* row = a.V + i * a.K;
-        for (uint32_t cc = 0; cc < a.K; ++cc) it[2 + cc] = row[cc];
-      }
+      if (!FILL && verdicts) a.verdict[i] = (uint8_t)listed;
     }
-    if (!FILL && verdicts) a.verdict[i] = (uint8_t)listed;
+    if (FILL && verdicts) {
+      __syncthreads();
+      const uint32_t m = st_n, L = a.L, per = kAxBlock / L, cc = threadIdx.x % L;
+      for (uint32_t e = threadIdx.x / L; e < m; e += per) {
+        uint32_t* it = a.req + (uint64_t)st_at[e] * a.rw;
+        const uint32_t il = st_i[e];
+        if (cc < a.K) it[2 + cc] = a.V[(uint64_t)il * a.K + cc];
+        if (cc == 0) {
+          it[0] = st_p[e];
+          it[1] = (uint32_t)(a.lo + il);
+        }
+      }
+      __syncthreads();  // every copy has read st_n and the stage
+      if (threadIdx.x == 0) st_n = 0;
+      __syncthreads();  // the next pass stages after the reset
+    }
   }
   __syncthreads();
   if (!FILL) {
