@@ -64,20 +64,6 @@ constexpr uint32_t kPushWaves = GOSSIP_APPLY_PUSH_WAVES;
 // push-pull apply: the block's waves split between the push walk (fragmented runs)
 // and the response walk (sequential regions), which then run side by side
 constexpr bool kApplySplit = GOSSIP_APPLY_SPLIT != 0;
-#ifndef GOSSIP_GROUP
-#define GOSSIP_GROUP 0
-#endif
-// Run walkers load records GS at a time (GS = 2: 8-B id pairs, 16-B value / response pairs;
-// GS = 4: 16-B id quads, two 16-B value pairs; 0: one record per lane): a group at either
-// end of a run is shared with the neighbouring runs and masked.  The one-record walkers left
-// the CU's texture address / data units 72 / 86 % busy in apply on lane-wise 4- and 8-B
-// accesses (profiles/r02_s2b/pmc_sq.json).
-constexpr int kGS = GOSSIP_GROUP;
-constexpr bool kQuad = kGS != 0;
-static_assert(kGS == 0 || kGS == 2 || kGS == 4, "GOSSIP_GROUP: 0, 2 or 4 records per lane");
-constexpr int kGSn = kGS ? kGS : 1;
-constexpr int kUnrollQ = 16 / kGSn;     // groups (16 records) in flight per lane in the run walkers
-constexpr int kUnrollQSeq = 16 / kGSn;  // groups in flight per lane in apply's sequential response walk
 #ifndef GOSSIP_NT_REC
 #define GOSSIP_NT_REC 1  // emit's record stores (bench: serve -28 us, apply -10 us per dense round)
 #endif
@@ -96,64 +82,6 @@ __device__ __forceinline__ T rec_ld(const T* p) {
   if constexpr ((GOSSIP_NT_REC & BIT) != 0) return __builtin_nontemporal_load(p);
   else return *p;
 }
-typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));  // the nontemporal builtins take native vectors
-template <int BIT>
-__device__ __forceinline__ uint4 rec_ld4(const uint4* p) {
-  if constexpr ((GOSSIP_NT_REC & BIT) != 0) {
-    const v4u32 x = __builtin_nontemporal_load((const v4u32*)p);
-    return make_uint4(x.x, x.y, x.z, x.w);
-  } else {
-    return *p;
-  }
-}
-template <int BIT>
-__device__ __forceinline__ void rec_st4(uint4* p, uint4 v) {
-  if constexpr ((GOSSIP_NT_REC & BIT) != 0) {
-    const v4u32 x = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(x, (v4u32*)p);
-  } else {
-    *p = v;
-  }
-}
-typedef uint32_t v2u32 __attribute__((ext_vector_type(2)));
-template <int BIT>
-__device__ __forceinline__ uint2 rec_ld2(const uint2* p) {
-  if constexpr ((GOSSIP_NT_REC & BIT) != 0) {
-    const v2u32 x = __builtin_nontemporal_load((const v2u32*)p);
-    return make_uint2(x.x, x.y);
-  } else {
-    return *p;
-  }
-}
-__device__ __forceinline__ uint4 u64x2(uint64_t a, uint64_t b) {
-  return make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
-}
-// group g of GS records: ids (4 B each) and 8-B values / responses, vector loads and stores
-template <int GS, int BIT>
-__device__ __forceinline__ void grp_ids(const uint32_t* base, size_t g, uint32_t (&o)[GS]) {
-  if constexpr (GS == 4) {
-    const uint4 x = rec_ld4<BIT>((const uint4*)base + g);
-    o[0] = x.x; o[1] = x.y; o[2] = x.z; o[3] = x.w;
-  } else {
-    const uint2 x = rec_ld2<BIT>((const uint2*)base + g);
-    o[0] = x.x; o[1] = x.y;
-  }
-}
-template <int GS, int BIT>
-__device__ __forceinline__ void grp_vals(const uint64_t* base, size_t g, uint64_t (&o)[GS]) {
-#pragma unroll
-  for (int h = 0; h < GS / 2; ++h) {
-    const uint4 x = rec_ld4<BIT>((const uint4*)base + g * (GS / 2) + h);
-    o[2 * h] = (uint64_t)x.y << 32 | x.x;
-    o[2 * h + 1] = (uint64_t)x.w << 32 | x.z;
-  }
-}
-template <int GS, int BIT>
-__device__ __forceinline__ void grp_store(uint64_t* base, size_t g, const uint64_t (&v)[GS]) {
-#pragma unroll
-  for (int h = 0; h < GS / 2; ++h) rec_st4<BIT>((uint4*)base + g * (GS / 2) + h, u64x2(v[2 * h], v[2 * h + 1]));
-}
-
 // record id word: p_local [0,14) | n_local [14,28) | flags.  K1 rewrites every
 // id each round, so a flag never outlives its round.
 constexpr uint32_t kIdVZ = 1u << 28;  // no push on this record (sender empty, or the peer already full)
@@ -709,108 +637,14 @@ __device__ __forceinline__ void for_each_run_record(const BinGeom& g, const uint
   }
 }
 
-// for_each_run_record four records at a time: the records [be, en) of run (s, T) lie in
-// the 16-B-aligned quads [be/4, ceil(en/4)) of region s (rp % 4 == 0: make_bin_geom); the
-// quads at either end may also hold records of the neighbouring runs (other tiles), so each
-// quad comes with a 4-bit mask of this run's records.  fn(q, m): quad index q (records
-// 4q .. 4q+3 of the region-major record array), mask m; q = -1, m = 0 past the end.
-// LDS per wave: wmask[U] u64, wlist / wbe / wen [64] i32.
-template <int U, int GS, typename F>
-__device__ __forceinline__ void for_each_run_group(const BinGeom& g, const uint16_t* rowb, const uint16_t* rowe,
-                                                  uint64_t* wmask_all, int32_t* wlist_all, int32_t* wbe_all,
-                                                  int32_t* wen_all, F&& fn, uint32_t w0 = 0, uint32_t nwaves = 0) {
-  constexpr uint32_t kWin = 64 * U;
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (nwaves == 0) nwaves = blockDim.x >> 6;
-  uint64_t* wm = wmask_all + wave * U;
-  int32_t* wl = wlist_all + wave * 64;
-  int32_t* wb = wbe_all + wave * 64;
-  int32_t* we = wen_all + wave * 64;
-  const uint64_t below = (1ull << lane) - 1ull, upto = (2ull << lane) - 1ull;
-  const uint32_t rq = g.rp / GS;  // groups per region
-  for (uint32_t s0 = (wave - w0) * 64; s0 < g.nt_s; s0 += nwaves * 64) {
-    const uint32_t s = s0 + lane;
-    const uint32_t sc = min(s, g.nt_s - 1);
-    const uint32_t be0 = rowb[sc], en0 = rowe[sc];
-    const uint32_t be = s < g.nt_s ? be0 : 0u, en = s < g.nt_s ? en0 : 0u;
-    const uint32_t qb = be / GS, nq = en > be ? (en + GS - 1u) / GS - qb : 0u;
-    uint32_t inc = nq;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(inc, o, 64);
-      if (lane >= (uint32_t)o) inc += y;
-    }
-    const uint32_t exc = inc - nq;
-    const uint32_t total = __shfl(inc, 63, 64);
-    const int32_t basep = (int32_t)(s * rq + qb - exc);  // quad = basep(owner) + f
-    const int32_t abe = (int32_t)(s * g.rp + be), aen = (int32_t)(s * g.rp + en);
-    for (uint32_t f0 = 0; f0 < total; f0 += kWin) {
-      if (lane < (uint32_t)U) wm[lane] = 0;
-      wave_sync();
-      const bool in = nq != 0 && exc < f0 + kWin && exc + nq > f0;
-      const uint64_t inm = __ballot(in);
-      if (in) {
-        const uint32_t pos = exc > f0 ? exc - f0 : 0u;
-        atomicOr((unsigned long long*)&wm[pos >> 6], 1ull << (pos & 63u));
-        const uint32_t k = __popcll(inm & below);
-        wl[k] = basep;
-        wb[k] = abe;
-        we[k] = aen;
-      }
-      wave_sync();
-      int32_t q[U];
-      uint32_t m[U];
-      uint32_t pre = 0;
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint64_t w = wm[u];
-        const uint32_t r = (pre + (uint32_t)__popcll(w & upto) - 1u) & 63u;
-        pre += (uint32_t)__popcll(w);
-        const uint32_t f = f0 + u * 64 + lane;
-        const int32_t qq = wl[r] + (int32_t)f;
-        constexpr uint32_t kAll = (1u << GS) - 1u;
-        const int32_t lo = wb[r] - GS * qq, hi = we[r] - GS * qq;  // this run's records in the group: [lo, hi)
-        const uint32_t mhi = hi >= GS ? kAll : hi <= 0 ? 0u : (1u << hi) - 1u;
-        const uint32_t mlo = lo <= 0 ? kAll : lo >= GS ? 0u : (kAll << lo) & kAll;
-        q[u] = f < total ? qq : -1;
-        m[u] = f < total ? (mhi & mlo) : 0u;
-      }
-      wave_sync();  // the next window rewrites wm/wl/wb/we
-      fn(q, m);
-    }
-  }
-}
-
 // The pushes aimed at tile X (its runs in every sender region) ORed into acc,
 // by the waves [0, nwaves) (0: all).  VZ: the record id's no-push flag.
 template <uint32_t VZ>
 __device__ __forceinline__ void push_walk(const BinGeom& g, const BinBufs& b, uint32_t X, unsigned long long* acc,
-                                          uint64_t* wmask, int32_t* wlist, int32_t* wbe, int32_t* wen,
-                                          uint32_t nwaves) {
+                                          uint64_t* wmask, int32_t* wlist, uint32_t nwaves) {
   const uint32_t* __restrict__ gids = b.ids;
   const uint64_t* __restrict__ gvals = b.vals;
   const uint16_t* rowb = b.offT + (size_t)X * g.nt_s;
-  if constexpr (kQuad) {
-    for_each_run_group<kUnrollQ, kGSn>(g, rowb, rowb + g.nt_s, wmask, wlist, wbe, wen, [&](const int32_t* q, const uint32_t* m) {
-      uint32_t id[kUnrollQ][kGSn];
-      uint64_t va[kUnrollQ][kGSn];
-#pragma unroll
-      for (int u = 0; u < kUnrollQ; ++u) grp_ids<kGSn, 8>(gids, q[u] >= 0 ? q[u] : 0, id[u]);
-#pragma unroll
-      for (int u = 0; u < kUnrollQ; ++u) grp_vals<kGSn, 8>(gvals, q[u] >= 0 ? q[u] : 0, va[u]);
-#pragma unroll
-      for (int u = 0; u < kUnrollQ; ++u)
-#pragma unroll
-        for (int i = 0; i < kGSn; ++i) {
-          const uint32_t idw = id[u][i];
-          const uint64_t v = va[u][i];
-          if (!((m[u] >> i) & 1u) || (idw & VZ) || !v) continue;  // every value is stored (K1)
-          const uint32_t p = idw & (kTileD - 1);
-          if (v & ~acc[p]) atomicOr(&acc[p], (unsigned long long)v);
-        }
-    }, 0u, nwaves);
-    return;
-  }
   for_each_run_record<kUnroll>(g, rowb, rowb + g.nt_s, wmask, wlist, [&](const int32_t* rec) {
     uint32_t id[kUnroll];
     uint64_t v[kUnroll];
@@ -858,10 +692,8 @@ template <uint32_t VF>
 __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, const uint64_t* __restrict__ S, BinBufs b,
                                                                   uint32_t R, IdxRange tr) {
   __shared__ unsigned long long img[kTileD];
-  __shared__ uint64_t wmask[(kTileThreads / 64) * (kUnrollServe > kUnrollQ ? kUnrollServe : kUnrollQ)];
+  __shared__ uint64_t wmask[(kTileThreads / 64) * kUnrollServe];
   __shared__ int32_t wlist[(kTileThreads / 64) * 64];
-  __shared__ int32_t wbe[kQuad ? (kTileThreads / 64) * 64 : 1];
-  __shared__ int32_t wen[kQuad ? (kTileThreads / 64) * 64 : 1];
   // persistent: virtual block v = blockIdx.x, +gridDim.x, ... serves tile
   // tr.at(xcd_remap(v, tr.n)) (the XCD of v is that of blockIdx.x, as with one
   // block per tile); the next tile's image loads into registers during a walk
@@ -879,29 +711,6 @@ __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, cons
   const uint32_t* gids = b.ids;
   uint64_t* __restrict__ gresp = b.resp;
   const uint16_t* rowb = b.offT + (size_t)T * g.nt_s;
-  if constexpr (kQuad) {
-    for_each_run_group<kUnrollQ, kGSn>(g, rowb, rowb + g.nt_s, wmask, wlist, wbe, wen, [&](const int32_t* q, const uint32_t* m) {
-      uint32_t id[kUnrollQ][kGSn];
-#pragma unroll
-      for (int u = 0; u < kUnrollQ; ++u) grp_ids<kGSn, 2>(gids, q[u] >= 0 ? q[u] : 0, id[u]);
-#pragma unroll
-      for (int u = 0; u < kUnrollQ; ++u) {
-        if (!m[u]) continue;
-        uint64_t r[kGSn];
-#pragma unroll
-        for (int i = 0; i < kGSn; ++i) r[i] = (uint64_t)img[id[u][i] & (kTileD - 1)];
-        if (m[u] == (1u << kGSn) - 1u) {  // the whole group is this tile's: 16-B stores (no-pull slots
-                                          // get S_t[p] too, unread: the consumers skip records flagged VF)
-          grp_store<kGSn, 4>(gresp, q[u], r);
-          continue;
-        }
-#pragma unroll
-        for (int i = 0; i < kGSn; ++i)  // a run end: only this tile's records (the rest are other blocks')
-          if (((m[u] >> i) & 1u) && !(id[u][i] & VF)) rec_st<4>(&gresp[kGSn * (size_t)q[u] + i], r[i]);
-      }
-    });
-    continue;
-  }
   for_each_run_record<kUnrollServe>(g, rowb, rowb + g.nt_s, wmask, wlist, [&](const int32_t* rec) {
     uint32_t id[kUnrollServe];
 #pragma unroll
@@ -938,8 +747,6 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
   __shared__ uint32_t red_nz[kTileThreads / 64];
   __shared__ uint64_t wmask[(kTileThreads / 64) * kUnroll];
   __shared__ int32_t wlist[(kTileThreads / 64) * 64];
-  __shared__ int32_t wbe[kQuad ? (kTileThreads / 64) * 64 : 1];
-  __shared__ int32_t wen[kQuad ? (kTileThreads / 64) * 64 : 1];
   const uint32_t tid = threadIdx.x;
   // persistent (grid apply_grid(nt_d)): virtual block v = blockIdx.x,
   // +gridDim.x, ... applies tile xcd_remap(v, nt_d) (same XCD as blockIdx.x);
@@ -972,10 +779,9 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
   const bool do_pull = (mode == 2 || mode == 3) && (!split || wave >= kPushWaves);
   // split: waves [0, kPushWaves) walk the pushes, the others the responses
   const uint32_t qt0 = split ? kPushWaves * 64 : 0u, qnt = split ? kTileThreads - kPushWaves * 64 : kTileThreads;
-  if (do_push) push_walk<kIdVZ>(g, b, X, acc, wmask, wlist, wbe, wen, split ? kPushWaves : 0u);  // pushes aimed at this tile
+  if (do_push) push_walk<kIdVZ>(g, b, X, acc, wmask, wlist, split ? kPushWaves : 0u);  // pushes aimed at this tile
   if (do_pull) {  // responses owed to this tile's own senders
     const uint32_t* __restrict__ qids = bq.ids;
-    auto qids_base = [](const BinBufs& bb) { return bb.ids; };
     const uint64_t* __restrict__ gresp = bq.resp;
     const uint32_t per = kTileD >> gq.ts_log;
     const uint32_t s0 = X * per, s1 = min(s0 + per, gq.nt_s);
@@ -984,36 +790,6 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
       const size_t reg = (size_t)s * gq.rp;
       const uint32_t nb = (s - s0) << gq.ts_log;
       const uint32_t qtid = tid - qt0;
-      if constexpr (kQuad) {  // the region's records GS at a time (rp % GS == 0: whole groups)
-        const uint32_t nq = (total + kGSn - 1) / kGSn;
-        const uint32_t* __restrict__ rids = qids_base(bq) + reg;
-        const uint64_t* __restrict__ rres = gresp + reg;
-        for (uint32_t p0 = 0; p0 < nq; p0 += qnt * kUnrollQSeq) {
-          uint32_t id[kUnrollQSeq][kGSn];
-          uint64_t ra[kUnrollQSeq][kGSn];
-#pragma unroll
-          for (int u = 0; u < kUnrollQSeq; ++u) {
-            const uint32_t qi = min(p0 + u * qnt + qtid, nq - 1);
-            grp_ids<kGSn, 16>(rids, qi, id[u]);
-            grp_vals<kGSn, 16>(rres, qi, ra[u]);
-          }
-#pragma unroll
-          for (int u = 0; u < kUnrollQSeq; ++u) {
-            const uint32_t qi = p0 + u * qnt + qtid;
-            if (qi >= nq) continue;
-#pragma unroll
-            for (int i = 0; i < kGSn; ++i) {
-              const uint32_t idw = id[u][i];
-              // a full sender's slot was never written this round (K2 skips it)
-              if (kGSn * qi + i >= total || (idw & kIdVF)) continue;
-              const uint32_t node = nb + ((idw >> kTileDLog) & kIdNMask);
-              const uint64_t r = ra[u][i];
-              if (r & ~acc[node]) atomicOr(&acc[node], (unsigned long long)r);
-            }
-          }
-        }
-        continue;
-      }
       for (uint32_t p0 = 0; p0 < total; p0 += qnt * kUnrollSeq) {
         uint64_t r[kUnrollSeq];
         uint32_t id[kUnrollSeq];
@@ -1512,8 +1288,6 @@ __global__ __launch_bounds__(kTileThreads) void xd_apply_kernel(XdGeom g, XdBufs
   __shared__ uint32_t red_nz[kTileThreads / 64];
   __shared__ uint64_t wmask[(kTileThreads / 64) * kUnroll];
   __shared__ int32_t wlist[(kTileThreads / 64) * 64];
-  __shared__ int32_t wbe[kQuad ? (kTileThreads / 64) * 64 : 1];
-  __shared__ int32_t wen[kQuad ? (kTileThreads / 64) * 64 : 1];
   __shared__ uint32_t pl[kXdPref];  // the tile's sender regions: owner-run prefix rows (G + 1 each)
   __shared__ uint32_t po[kXdPref];  // and the runs' send positions (G each, stride G + 1)
   const uint32_t tid = threadIdx.x, G = g.G;
@@ -1542,7 +1316,7 @@ __global__ __launch_bounds__(kTileThreads) void xd_apply_kernel(XdGeom g, XdBufs
     }
     if (tid < 64) cnt[tid] = 0;
     __syncthreads();
-    if (do_push) push_walk<kXbVZ>(g.r, b.rb, X, acc, wmask, wlist, wbe, wen, split ? nwav / 2 : 0u);
+    if (do_push) push_walk<kXbVZ>(g.r, b.rb, X, acc, wmask, wlist, split ? nwav / 2 : 0u);
     if (do_pull) {  // replies, in send order: region s's items are G runs (one per owner)
       const uint32_t qtid = tid - qt0;
       for (uint32_t s = s0; s < s1; ++s) {
