@@ -44,8 +44,10 @@ hipError_t launch_aex_requests(const AexArgs& a, hipStream_t st);
 // requests received (m items): max-merge into Vn, responses V_t[p] in the received order
 hipError_t launch_aex_serve(const AexArgs& a, const uint32_t* in, uint64_t m, uint32_t* resp, hipStream_t st);
 // the responses to the own requests (in request order), the own-own exchanges, then the
-// stats of S_{t+1} and its own stale bits
-hipError_t launch_aex_finish(const AexArgs& a, const uint32_t* resp, uint64_t nreq, uint64_t nloc, hipStream_t st);
+// stats of S_{t+1} and its own stale bits: a full pass, or (inc, with a.dirty tracked and the
+// own stale words of S_t in the image) over the raised rows only, partial[3] = the hash delta
+hipError_t launch_aex_finish(const AexArgs& a, const uint32_t* resp, uint64_t nreq, uint64_t nloc, bool inc,
+                             hipStream_t st);
 // own stale bits of V against target (after set_target)
 hipError_t launch_aex_stale(const AexArgs& a, const uint32_t* V, hipStream_t st);
 // initial versions of the own rows (Philox tag 3 with global node ids)

@@ -357,6 +357,95 @@ __global__ __launch_bounds__(kAxBlock) void aex_stats_kernel(AexArgs a, const ui
     atomicAdd((unsigned long long*)&a.partial[4 + threadIdx.x], (unsigned long long)cnt[threadIdx.x]);
 }
 
+// Incremental stats of a round that tracked its raised rows: only dirty rows can
+// differ between S_t (V) and S_{t+1} (Vn), so their stale bits are recomputed and their hash terms
+// swapped (partial[3] gets the delta); full / alive from the bitmaps; per-component counts = the
+// alive non-stale nodes plus the matching components of the alive stale rows (few in such rounds).
+// One wave per own chunk, lanes as in aex_stats_kernel.
+template <uint32_t L>
+__global__ __launch_bounds__(kAxBlock) void aex_stats_inc_kernel(AexArgs a) {
+  using BT = typename std::conditional<(L > 32), uint64_t, uint32_t>::type;
+  constexpr uint32_t per = 64 / L;
+  __shared__ uint32_t cnt[64];
+  __shared__ uint64_t red[4][kAxBlock / 64];
+  if (threadIdx.x < 64) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63, sub = lane / L, c = lane % L;
+  const uint32_t tgt = c < a.K ? a.target[c] : 0u;
+  const uint64_t chunks = (a.nown + 63) / 64;
+  uint64_t dhash = 0, full = 0, nal = 0, fullw = 0;
+  uint32_t c_lane = 0;
+  for (uint64_t ch = (uint64_t)blockIdx.x * (kAxBlock / 64) + (threadIdx.x >> 6); ch < chunks;
+       ch += (uint64_t)gridDim.x * (kAxBlock / 64)) {
+    uint64_t* pw = a.img + 2 * (a.lo / 64 + ch);
+    const uint64_t aw = pw[0], dw = a.dirty[ch];
+    uint64_t sw = pw[1];
+    if (dw) {  // the raised rows: stale bits of S_{t+1}, hash terms old -> new
+      BT bad = 0;
+      uint64_t hb = ((uint64_t)c * a.N + a.lo + ch * 64 + sub * L) * kGold64;
+#pragma unroll
+      for (uint32_t i = 0; i < L; ++i) {
+        const uint32_t b = sub * L + i;
+        if (((dw >> b) & 1ull) && c < a.K) {
+          const uint64_t il = ch * 64 + b;
+          const uint32_t vn = a.Vn[il * a.K + c], vo = a.V[il * a.K + c];
+          if (a.flags & 1u) dhash += (vn ? mix64((uint64_t)vn + hb) : 0ull) - (vo ? mix64((uint64_t)vo + hb) : 0ull);
+          bad |= (BT)(vn != tgt) << i;
+        }
+        hb += kGold64;
+      }
+#pragma unroll
+      for (uint32_t off = 1; off < L; off <<= 1) bad |= (BT)__shfl_xor(bad, (int)off, 64);
+      uint64_t st = 0;
+      if (per <= L) {
+#pragma unroll
+        for (uint32_t g = 0; g < per; ++g) st |= (uint64_t)__shfl(bad, (int)(g * L), 64) << (g * L);
+      } else {
+#pragma unroll
+        for (uint32_t i = 0; i < L; ++i) st |= __ballot(c == 0 && ((bad >> i) & 1u)) << i;
+      }
+      sw = (sw & ~dw) | (st & dw);
+      if (lane == 0) pw[1] = sw;
+    }
+    const uint64_t as = aw & sw;
+    fullw += (uint64_t)__popcll(aw & ~sw);
+    if (as) {  // alive stale rows: their components that match the target
+#pragma unroll
+      for (uint32_t i = 0; i < L; ++i) {
+        const uint32_t b = sub * L + i;
+        if (((as >> b) & 1ull) && c < a.K) c_lane += a.Vn[(ch * 64 + b) * a.K + c] == tgt ? 1u : 0u;
+      }
+    }
+    nal += (uint64_t)__popcll(aw);
+  }
+  full = fullw;
+  if (c < a.K && c_lane) atomicAdd(&cnt[c], c_lane);
+  if (lane != 0) full = nal = fullw = 0;  // wave-uniform: counted once per wave
+  dhash = wave_sum64(dhash);
+  full = wave_sum64(full);
+  nal = wave_sum64(nal);
+  if (lane == 0) {
+    red[0][threadIdx.x >> 6] = dhash;
+    red[1][threadIdx.x >> 6] = full;
+    red[2][threadIdx.x >> 6] = nal;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    uint64_t sum = 0;
+    for (int w = 0; w < kAxBlock / 64; ++w) sum += red[threadIdx.x][w];
+    const uint32_t slot = threadIdx.x == 0 ? 3u : threadIdx.x == 1 ? 0u : 1u;
+    if (sum) atomicAdd((unsigned long long*)&a.partial[slot], (unsigned long long)sum);
+  }
+  __syncthreads();
+  // every alive non-stale node matches the target in every component
+  if (threadIdx.x < a.K) {
+    uint64_t f = 0;
+    for (int w = 0; w < kAxBlock / 64; ++w) f += red[1][w];
+    const uint64_t add = f + cnt[threadIdx.x];
+    if (add) atomicAdd((unsigned long long*)&a.partial[4 + threadIdx.x], (unsigned long long)add);
+  }
+}
+
 // Vn rows the previous round raised (dirty) := V rows, dirty cleared: one wave per 64 rows,
 // lanes as in the stats pass (coalesced rows); clean words cost one load.
 template <uint32_t L>
@@ -461,10 +550,24 @@ void stats_l(const AexArgs& a, const uint32_t* R, hipStream_t st) {
 }
 }  // namespace
 
-hipError_t launch_aex_finish(const AexArgs& a, const uint32_t* resp, uint64_t nreq, uint64_t nloc, hipStream_t st) {
+hipError_t launch_aex_finish(const AexArgs& a, const uint32_t* resp, uint64_t nreq, uint64_t nloc, bool inc,
+                             hipStream_t st) {
   if (nreq + nloc)
     aex_merge_kernel<<<ax_grid(nreq + nloc, kAxBlock / a.L, 65536), kAxBlock, 0, st>>>(a, resp, nreq, nloc);
-  stats_l<true>(a, a.Vn, st);
+  if (!inc || !a.dirty) {
+    stats_l<true>(a, a.Vn, st);
+    return hipGetLastError();
+  }
+  const uint32_t g = ax_grid((a.nown + 63) / 64, kAxBlock / 64, GOSSIP_AEX_STATS_GRID);
+  switch (a.L) {
+    case 1: aex_stats_inc_kernel<1><<<g, kAxBlock, 0, st>>>(a); break;
+    case 2: aex_stats_inc_kernel<2><<<g, kAxBlock, 0, st>>>(a); break;
+    case 4: aex_stats_inc_kernel<4><<<g, kAxBlock, 0, st>>>(a); break;
+    case 8: aex_stats_inc_kernel<8><<<g, kAxBlock, 0, st>>>(a); break;
+    case 16: aex_stats_inc_kernel<16><<<g, kAxBlock, 0, st>>>(a); break;
+    case 32: aex_stats_inc_kernel<32><<<g, kAxBlock, 0, st>>>(a); break;
+    default: aex_stats_inc_kernel<64><<<g, kAxBlock, 0, st>>>(a); break;
+  }
   return hipGetLastError();
 }
 

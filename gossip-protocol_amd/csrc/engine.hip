@@ -113,6 +113,9 @@ struct gossip_engine {
   uint8_t* aex_verdict = nullptr;  // [nown] the count pass's listed exchanges per own node
   bool aex_patch_ok = false, aex_round_done = false;
   bool aex_track = false;  // this round marks the rows it raises (few items: ae_request_recv decides)
+  // incremental stats (launch_aex_finish inc): the own stale words and hash part of S_t are exact
+  bool aex_inc_ok = false;
+  uint64_t aex_hash_own = 0;  // this shard's part of the state hash of the last committed round
   // binned (LDS) pipeline for W == 1 random modes on one shard
   bool binned = false;
   BinGeom bg{};
@@ -1270,7 +1273,7 @@ int gossip_reset(gossip_engine_t* e) {
     HIP_OK(e, hipMemsetAsync(e->target, 0, 256, e->stream));
     HIP_OK(e, launch_aex_fill_alive(make_aex_args(e), e->stream));
     e->aex_churned = ~0ull;
-    e->aex_target_ok = e->aex_patch_ok = false;
+    e->aex_target_ok = e->aex_patch_ok = e->aex_inc_ok = false;
   } else if (e->mode == GOSSIP_MODE_ANTIENTROPY) {
     HIP_OK(e, hipMemsetAsync(e->V, 0, e->N * e->R * 4, e->stream));
     HIP_OK(e, hipMemsetAsync(e->target, 0, 256, e->stream));
@@ -1319,7 +1322,7 @@ int gossip_inject(gossip_engine_t* e, uint64_t node, uint32_t rumor) {
   if (e->aex) {  // a local write on the owner; the global max vector is re-derived before the next round
     if (node >= e->lo && node < e->hi)
       HIP_OK(e, launch_ae_inject(e->V, e->aex_tmp, node - e->lo, e->R, rumor, e->stream));
-    e->aex_target_ok = e->aex_patch_ok = false;
+    e->aex_target_ok = e->aex_patch_ok = e->aex_inc_ok = false;
     return GOSSIP_OK;
   }
   if (e->mode == GOSSIP_MODE_ANTIENTROPY) {
@@ -1342,7 +1345,7 @@ int gossip_inject_random(gossip_engine_t* e) {
   if (int rc = set_dev(e)) return rc;
   if (e->aex) {
     HIP_OK(e, launch_aex_init(e->V, e->lo, e->nown, e->R, e->key0, e->key1, e->stream));
-    e->aex_target_ok = e->aex_patch_ok = false;
+    e->aex_target_ok = e->aex_patch_ok = e->aex_inc_ok = false;
     return GOSSIP_OK;
   }
   if (e->mode == GOSSIP_MODE_ANTIENTROPY) {
@@ -1811,6 +1814,7 @@ int gossip_ae_set_target(gossip_engine_t* e, const uint32_t* target) {
   HIP_OK(e, launch_aex_stale(make_aex_args(e), e->V, e->stream));  // own stale words of S_t
   HIP_OK(e, hipStreamSynchronize(e->stream));
   e->aex_target_ok = true;
+  e->aex_inc_ok = false;  // (the next round's stats: a full pass)
   return GOSSIP_OK;
 }
 
@@ -1882,13 +1886,17 @@ int gossip_ae_response_recv(gossip_engine_t* e, void** recv) {
 int gossip_ae_finish(gossip_engine_t* e, uint64_t* partial) {
   if (!partial) return GOSSIP_EINVAL;
   if (int rc = aex_check(e)) return rc;
-  HIP_OK(e, launch_aex_finish(make_aex_args(e), e->aex_resp_in, e->aex_nreq, e->aex_nloc, e->stream));
+  const bool inc = e->aex_inc_ok && e->aex_track;  // a round with few items: stats over its raised rows
+  HIP_OK(e, launch_aex_finish(make_aex_args(e), e->aex_resp_in, e->aex_nreq, e->aex_nloc, inc, e->stream));
   if (int rc = timer_end(e, 0)) return rc;
   HIP_OK(e, hipMemcpyAsync(e->partial_h, e->partial_d, part_len(e) * 8, hipMemcpyDeviceToHost, e->stream));
   HIP_OK(e, hipStreamSynchronize(e->stream));
   if (int rc = timer_collect(e)) return rc;
   std::memcpy(partial, e->partial_h, part_len(e) * 8);
   partial[4 + e->R] = 0;  // (nonzero count: random modes only)
+  if (inc) partial[3] += e->aex_hash_own;  // the kernel added the raised rows' hash delta
+  e->aex_hash_own = partial[3];
+  e->aex_inc_ok = true;
   e->last_sparse = false;
   e->aex_round_done = e->aex_track;
   e->aex_track = false;
@@ -2007,7 +2015,7 @@ int gossip_state_hash(gossip_engine_t* e, uint64_t* out) {
     a.Vn = e->V;
     a.write_stale = false;  // (the stale words are not wanted here)
     HIP_OK(e, hipMemsetAsync(e->partial_d, 0, part_len(e) * 8, e->stream));
-    HIP_OK(e, launch_aex_finish(a, nullptr, 0, 0, e->stream));
+    HIP_OK(e, launch_aex_finish(a, nullptr, 0, 0, false, e->stream));
     HIP_OK(e, hipMemcpyAsync(e->partial_h, e->partial_d, part_len(e) * 8, hipMemcpyDeviceToHost, e->stream));
     HIP_OK(e, hipStreamSynchronize(e->stream));
     *out = e->partial_h[3];
