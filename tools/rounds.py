@@ -26,7 +26,9 @@ seq = sorted((int(r["Start_Timestamp"]), short(r["Kernel_Name"]),
 ks = [x for x in seq if x[1]]
 rounds, cur = [], []
 for x in ks:
-    if x[1] in STARTS and cur and cur[-1][1] not in ("rebuild", "inject"):
+    # (a dense round whose records the previous round's apply emitted starts at its transpose)
+    starts = x[1] in STARTS or (x[1] == "u16" and cur and cur[-1][1] == "snap")
+    if starts and cur and cur[-1][1] not in ("rebuild", "inject"):
         rounds.append(cur)
         cur = []
     cur.append(x)
