@@ -78,14 +78,9 @@ void bin_carve(const BinGeom& g, void* base, BinBufs* b);
 // one-block kernel hands them to the host through rs.  filt (needs exact
 // nzb/fullb): bit 0 drops pulls from empty peers, bit 1 pushes into full
 // peers — exact, it only removes edges that move nothing.
-// pre_emitted: this round's records are already in b (the previous round's apply emitted them);
-// next: the apply also emits round t + 1's records into next (its ids, vals, off; resp and offT
-// may be b's), from each tile's finished LDS image — fused_emit_ok(g, fa) only.
-bool fused_emit_ok(const BinGeom& g, const Faults& fa);
 hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, uint64_t* partial, uint32_t R,
                                uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t filt,
-                               const Faults& fa, uint32_t flags, const RoundSync& rs, hipStream_t st,
-                               bool pre_emitted = false, const BinBufs* next = nullptr);
+                               const Faults& fa, uint32_t flags, const RoundSync& rs, hipStream_t st);
 
 // Dense round of a sharded engine (G > 1) after the state all-gather
 // (DESIGN.md §5): push pass P = every sender of the image, records for the

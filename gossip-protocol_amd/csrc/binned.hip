@@ -729,101 +729,18 @@ __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, cons
 
 uint32_t serve_grid(uint32_t tiles) { return tiles < kServeGrid ? tiles : kServeGrid; }
 
-// Emit of round t + 1 fused into round t's apply: after tile X's epilogue
-// acc holds S_{t+1}[X], the sender values of the tile's two regions.  Region s0's records are
-// counting-sorted in the upper half of acc (u32 view) while the upper half's values wait in
-// registers, then move down for region s0 + 1.  Same records, offsets and layout as bin_emit
-// (V = 0, k <= 2, no faults, no peer filter) into the next record set en.b.
-struct EmitNext {
-  BinBufs b;  // the next round's ids / vals / off (its resp, offT are this round's: read before)
-  uint32_t t, on;
-};
-
-__device__ __forceinline__ void fused_emit(const BinGeom& g, const EmitNext& en, unsigned long long* acc,
-                                           uint32_t* cur, uint32_t* wsum, uint32_t* wpre, uint32_t X, uint32_t R,
-                                           uint32_t key0, uint32_t key1, uint32_t mode) {
-  const uint32_t tid = threadIdx.x;
-  constexpr uint32_t kQ = kMaxSenders / kTileThreads;
-  static_assert(kTileThreads == kEmitThreads, "region_offsets assumes the emit block");
-  const uint32_t per = kTileD >> g.ts_log;
-  const uint32_t s0 = X * per, s1 = min(s0 + per, g.nt_s);
-  const uint64_t nm1 = g.N - 1, fm = full_mask1(R);
-  uint64_t hold[kQ];  // values of the tile's upper region
-#pragma unroll
-  for (uint32_t q = 0; q < kQ; ++q) hold[q] = acc[kMaxSenders + q * kTileThreads + tid];
-  const uint64_t* sval = (const uint64_t*)acc;
-  uint32_t* st_ids = (uint32_t*)(acc + kMaxSenders);
-  for (uint32_t s = s0; s < s1; ++s) {
-    __syncthreads();  // the epilogue / the previous region's write-out are done with acc
-    if (s > s0) {
-#pragma unroll
-      for (uint32_t q = 0; q < kQ; ++q) acc[q * kTileThreads + tid] = hold[q];
-    }
-    for (uint32_t d = tid; d < g.nt_d; d += kTileThreads) cur[d] = 0;
-    __syncthreads();
-    const uint64_t base = (uint64_t)s << g.ts_log;
-    const uint32_t nsend = (uint32_t)min<uint64_t>(g.ts, g.N - base);
-    uint32_t pr[kQ * 2], ed[kQ];
-#pragma unroll
-    for (uint32_t q = 0; q < kQ; ++q) {
-      const uint32_t i = tid + q * kTileThreads;
-      ed[q] = 0;
-      pr[2 * q] = pr[2 * q + 1] = 0;
-      const uint32_t d = i < nsend ? sender_dirs(mode, sval[i], fm) : 0u;
-      if (!d) continue;
-      const uint32_t n = (uint32_t)(base + i);
-      const u32x4 x = philox4x32_10(u32x4{n, en.t, 0u, 0u}, key0, key1);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        pr[2 * q + j] = peer_from_word(lane_of(x, j), nm1, n);
-        if ((uint32_t)j < g.k) {
-          ed[q] |= d << (2 * j);
-          atomicAdd(&cur[pr[2 * q + j] >> kTileDLog], 1u);
-        }
-      }
-    }
-    __syncthreads();
-    const uint32_t total = region_offsets(cur, g.nt_d, en.b.off + (size_t)s * (g.nt_d + 1), wsum, wpre);
-#pragma unroll
-    for (uint32_t q = 0; q < kQ; ++q) {
-      const uint32_t i = tid + q * kTileThreads;
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const uint32_t d = (ed[q] >> (2 * j)) & 3u;
-        if (!d) continue;
-        const uint32_t p = pr[2 * q + j];
-        const uint32_t pos = atomicAdd(&cur[p >> kTileDLog], 1u);
-        st_ids[pos] = (p & (kTileD - 1)) | (i << kTileDLog) | dir_flags(d);
-      }
-    }
-    __syncthreads();
-    uint32_t* gids = en.b.ids + (size_t)s * g.rp;
-    uint64_t* gvals = en.b.vals + (size_t)s * g.rp;
-    for (uint32_t e = tid; e < total; e += kTileThreads) {
-      const uint32_t id = st_ids[e];
-      rec_st<1>(&gids[e], id);
-      rec_st<1>(&gvals[e], sval[(id >> kTileDLog) & kIdNMask]);
-    }
-  }
-}
-
 // K3 — one block per tile X: acc = S_t[X]; OR in the pushes aimed at X (its
 // runs) and the pull responses owed to X's own senders (their regions, read
 // sequentially); write S_{t+1}[X] and fold the stats.  One shard: g = gq, b =
 // bq.  Sharded dense round: g/b the push pass (every sender, tiles of the own
 // nodes), gq/bq the pull pass (own senders, tiles of the whole image); S and
 // Snext are the own slices (Nn nodes, global ids from hid0).
-template <bool EMIT>
 __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinBufs b, BinGeom gq, BinBufs bq,
                                                                   const uint64_t* S, uint64_t* Snext,  // may alias
                                                                   uint64_t Nn, uint64_t hid0,
                                                                   uint64_t* __restrict__ partial, uint32_t R,
-                                                                  uint32_t mode, uint32_t flags, EmitNext en,
-                                                                  uint32_t key0, uint32_t key1) {
+                                                                  uint32_t mode, uint32_t flags) {
   __shared__ unsigned long long acc[kTileD];
-  __shared__ uint32_t ecur[EMIT ? kMaxTilesD : 1];  // the fused emit's tile counters
-  __shared__ uint32_t ewsum[EMIT ? kEmitThreads / 64 : 1];
-  __shared__ uint32_t ewpre[EMIT ? kEmitThreads / 64 + 1 : 1];
   __shared__ uint32_t cnt[64];
   __shared__ uint64_t red_hash[kTileThreads / 64];
   __shared__ uint32_t red_full[kTileThreads / 64];
@@ -898,7 +815,6 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
   if (kPre && v + gridDim.x < nv) tile_regs_load<0, kPreN>(xt, S, (uint64_t)xcd_remap(v + gridDim.x, nv) << kTileDLog, Nn);
   __syncthreads();
   tile_epilogue(acc, node0, Nn, hid0, Snext, partial, R, flags, cnt, red_hash, red_full, red_nz, b.nzb, b.fullb);
-  if constexpr (EMIT) fused_emit(g, en, acc, ecur, ewsum, ewpre, X, R, key0, key1, mode);
   }
 }
 
@@ -956,17 +872,10 @@ void bin_carve(const BinGeom& g, void* base, BinBufs* b) {
   b->offT = (uint16_t*)p;
 }
 
-bool fused_emit_ok(const BinGeom& g, const Faults& fa) {
-  return g.k <= 2 && !fa.any() && g.nt_d <= kMaxTilesD && g.ts == kMaxSenders && g.rp <= kRecPerRegion &&
-         (kTileD >> g.ts_log) == 2;
-}
-
 hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, uint64_t* partial, uint32_t R,
                                uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t filt,
-                               const Faults& fa, uint32_t flags, const RoundSync& rs, hipStream_t st,
-                               bool pre_emitted, const BinBufs* next) {
+                               const Faults& fa, uint32_t flags, const RoundSync& rs, hipStream_t st) {
   if (!b.nzb || !b.fullb) filt = 0;  // the bitmaps exist only with the frontier buffers
-  if (next && !fused_emit_ok(g, fa)) return hipErrorInvalidValue;
   const uint32_t eg = g.nt_s < kEmitGrid ? g.nt_s : kEmitGrid;  // persistent: one block per CU
 #define GOSSIP_EMIT(KR, F, VV) \
   bin_emit_kernel<KR, F, VV><<<eg, kEmitThreads, 0, st>>>(g, S, b, R, t, key0, key1, mode, filt, fa, EmitRange{})
@@ -976,8 +885,7 @@ hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, 
   } else {                                                                \
     if (fa.any()) GOSSIP_EMIT(0, true, VV); else GOSSIP_EMIT(0, false, VV); \
   }
-  if (pre_emitted) {  // the previous round's apply emitted this round's records (fused_emit)
-  } else if (g.ts > kMaxSenders || g.rp > kRecPerRegion) {  // make_bin_geom(big): V = 4
+  if (g.ts > kMaxSenders || g.rp > kRecPerRegion) {  // make_bin_geom(big): V = 4
     // the draws are redone in the placement pass: 16 senders per lane keep no room for
     // their peers in registers (KREG = 2 spills 78 VGPRs)
     if (fa.any()) GOSSIP_EMIT(0, true, 4); else GOSSIP_EMIT(0, false, 4);
@@ -994,14 +902,7 @@ hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, 
     bin_serve_kernel<kIdVF><<<serve_grid(g.nt_d), kTileThreads, 0, st>>>(g, S, b, R, IdxRange::all(g.nt_d));
   // in place: K3 of tile X reads and writes only S[X] (push values and pull
   // responses come from the record buffers), and K1/K2 have finished reading S_t
-  if (next) {  // and the next round's emit from each finished tile (fused_emit; its records go to *next)
-    EmitNext en{*next, t + 1, 1u};
-    bin_apply_kernel<true><<<apply_grid(g), kTileThreads, 0, st>>>(g, b, g, b, S, S, g.N, 0, partial, R, mode, flags,
-                                                                   en, key0, key1);
-  } else {
-    bin_apply_kernel<false><<<apply_grid(g), kTileThreads, 0, st>>>(g, b, g, b, S, S, g.N, 0, partial, R, mode,
-                                                                    flags, EmitNext{}, 0u, 0u);
-  }
+  bin_apply_kernel<<<apply_grid(g), kTileThreads, 0, st>>>(g, b, g, b, S, S, g.N, 0, partial, R, mode, flags);
   return hipGetLastError();  // the engine enqueues the round's snapshot (round.h) after its timing event
 }
 
@@ -1109,8 +1010,8 @@ hipError_t launch_sb_post(const SbGeom& g, const SbBufs& b, const uint64_t* imag
   BinBufs bp = b.p;
   bp.nzb = nzb;
   bp.fullb = fullb;
-  bin_apply_kernel<false><<<apply_grid(g.p), kTileThreads, 0, st>>>(g.p, bp, g.q, b.q, image + g.lo, Snext, g.nown,
-                                                             g.lo, partial, R, mode, flags, EmitNext{}, 0u, 0u);
+  bin_apply_kernel<<<apply_grid(g.p), kTileThreads, 0, st>>>(g.p, bp, g.q, b.q, image + g.lo, Snext, g.nown, g.lo, partial,
+                                                      R, mode, flags);
   return hipGetLastError();
 }
 

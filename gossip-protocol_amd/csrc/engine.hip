@@ -121,14 +121,6 @@ struct gossip_engine {
   BinGeom bg{};
   BinBufs bb{};
   void* bin_mem = nullptr;
-  // fused emit (binned.h launch_binned_round next): a dense round's apply emits the next round's
-  // records into the other record set; bb2 = the second set's ids / vals / off (resp, offT and the
-  // bitmaps shared with bb), bset = the set holding the records of round pre_t
-  BinBufs bb2{};
-  void* bin_mem2 = nullptr;
-  uint32_t bset = 0;
-  uint64_t pre_t = ~0ull;
-  bool fuse_emit = true;  // gossip_set_param "fuse_emit"
   // frontier (sparse-round) path, on top of the binned one
   bool frontier = false;
   FrontierBufs fb{};
@@ -242,7 +234,6 @@ void free_all(gossip_engine* e) {
   for (void* b : fe)
     if (b) (void)hipFree(b);
   if (e->bin_mem) (void)hipFree(e->bin_mem);
-  if (e->bin_mem2) (void)hipFree(e->bin_mem2);
   if (e->fr_mem) (void)hipFree(e->fr_mem);
   void* sx[] = {e->lf_mem, e->sx_mem, e->rare_recv, e->msg_recv, e->sb_mem, e->xd_smem, e->xd_rmem,
                 e->cc_bits, e->cc_vals, e->xd_cls, e->xd_keep};
@@ -521,45 +512,19 @@ int round_timer_collect(gossip_engine* e, uint32_t slot, int64_t limit) {
 
 // One pipelined round: its kernels (bracketed by the slot's events when timing),
 // then the snapshot of the totals into ring slot `slot` (rs).
-// The second record set for fused emits (allocated at the first one).
-bool ensure_bb2(gossip_engine* e) {
-  if (e->bin_mem2) return true;
-  const size_t recs = (size_t)e->bg.nt_s * e->bg.rp;
-  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-  const size_t bytes = al(recs * 4) + al(recs * 8) + al((size_t)e->bg.nt_s * (e->bg.nt_d + 1) * 2);
-  if (hipMalloc(&e->bin_mem2, bytes) != hipSuccess) {
-    e->bin_mem2 = nullptr;
-    return false;
-  }
-  e->bb2 = e->bb;
-  char* p = (char*)e->bin_mem2;
-  e->bb2.ids = (uint32_t*)p;
-  e->bb2.vals = (uint64_t*)(p + al(recs * 4));
-  e->bb2.off = (uint16_t*)(p + al(recs * 4) + al(recs * 8));
-  return true;
-}
-
 int launch_round_path(gossip_engine* e, uint32_t t, bool sparse, uint32_t maj, bool all_d, uint32_t filt,
-                      const RoundSync& rs, int slot, bool fuse_next = false) {
+                      const RoundSync& rs, int slot) {
   const bool timed = e->timing && slot >= 0;
   if (timed) {
     if (int rc = round_timer_collect(e, (uint32_t)slot, INT64_MAX)) return rc;
     HIP_OK(e, hipEventRecord(e->evr[slot][0], e->stream));
   }
-  if (sparse) {
+  if (sparse)
     HIP_OK(e, launch_frontier_round(e->fb, e->S, e->N, e->partial_d, e->R, e->k, t, e->key0, e->key1, e->mode, maj,
                                     all_d, e->fa, e->cfg.flags, rs, e->stream));
-    e->pre_t = ~0ull;  // records emitted for this round (if any) go unused
-  } else {
-    const bool pre = e->pre_t == t;
-    const BinBufs& cur = e->bset ? e->bb2 : e->bb;
-    const bool fuse = fuse_next && e->fuse_emit && fused_emit_ok(e->bg, e->fa) && ensure_bb2(e);
-    const BinBufs* nxt = fuse ? (e->bset ? &e->bb : &e->bb2) : nullptr;
-    HIP_OK(e, launch_binned_round(e->bg, cur, e->S, e->partial_d, e->R, t, e->key0, e->key1, e->mode, filt, e->fa,
-                                  e->cfg.flags, rs, e->stream, pre, nxt));
-    if (fuse) e->bset ^= 1u;
-    e->pre_t = fuse ? (uint64_t)t + 1 : ~0ull;
-  }
+  else
+    HIP_OK(e, launch_binned_round(e->bg, e->bb, e->S, e->partial_d, e->R, t, e->key0, e->key1, e->mode, filt,
+                                  e->fa, e->cfg.flags, rs, e->stream));
   if (timed) {
     HIP_OK(e, hipEventRecord(e->evr[slot][1], e->stream));
     e->evr_round[slot] = t;
@@ -621,16 +586,10 @@ int step_planned(gossip_engine* e, uint32_t max_rounds, gossip_round_stats_t* st
       uint32_t maj = 0;
       bool all_d = false;
       const bool sparse = choose_sparse(e, x, &maj, &all_d);
-      // a dense round predicted to be followed by another emits that one's records in its apply
-      uint32_t maj1 = 0;
-      bool all_d1 = false;
-      const bool next_dense = !sparse && launched + 1 < max_rounds && !choose_sparse(e, predict(e, x), &maj1, &all_d1);
       const uint32_t slot = launched % kRing;
       const RoundSync rs = ring_sync(e, slot);
       want[slot] = rs.seq;
-      if (int rc = launch_round_path(e, t0 + launched, sparse, maj, all_d, dense_filter(e, x, e->filter_frac), rs,
-                                     (int)slot, next_dense))
-        return rc;
+      if (int rc = launch_round_path(e, t0 + launched, sparse, maj, all_d, dense_filter(e, x, e->filter_frac), rs, (int)slot)) return rc;
       ++launched;
     }
     if (done == launched) break;
@@ -1198,10 +1157,7 @@ int gossip_set_stream(gossip_engine_t* e, void* hip_stream) {
 int gossip_set_param(gossip_engine_t* e, const char* name, double v) {
   if (!e || !name) return GOSSIP_EINVAL;
   const std::string n(name);
-  e->pre_t = ~0ull;  // (a knob may change the next round's path or records)
-  if (n == "fuse_emit") {
-    e->fuse_emit = v != 0;
-  } else if (n == "sparse_frac") {
+  if (n == "sparse_frac") {
     e->sparse_frac = v;
     e->sparse_frac_set = true;
   } else if (n == "alld_frac") {
@@ -1310,7 +1266,6 @@ int gossip_set_topology_csr(gossip_engine_t* e, const uint32_t* row_ptr, const u
 
 int gossip_reset(gossip_engine_t* e) {
   if (!e) return GOSSIP_EINVAL;
-  e->pre_t = ~0ull;  // records a fused emit made for the next round would be stale
   if (int rc = set_dev(e)) return rc;
   const size_t shard = (size_t)e->W * e->Nl * 8;
   if (e->aex) {
@@ -1361,7 +1316,6 @@ int gossip_reset(gossip_engine_t* e) {
 
 int gossip_inject(gossip_engine_t* e, uint64_t node, uint32_t rumor) {
   if (!e) return GOSSIP_EINVAL;
-  e->pre_t = ~0ull;  // records a fused emit made for the next round would be stale
   if (node >= e->N || rumor >= e->R) return e->fail(GOSSIP_EINVAL, "inject(%llu, %u) out of range",
                                                     (unsigned long long)node, rumor);
   if (int rc = set_dev(e)) return rc;
@@ -1388,7 +1342,6 @@ int gossip_inject(gossip_engine_t* e, uint64_t node, uint32_t rumor) {
 
 int gossip_inject_random(gossip_engine_t* e) {
   if (!e) return GOSSIP_EINVAL;
-  e->pre_t = ~0ull;  // records a fused emit made for the next round would be stale
   if (int rc = set_dev(e)) return rc;
   if (e->aex) {
     HIP_OK(e, launch_aex_init(e->V, e->lo, e->nown, e->R, e->key0, e->key1, e->stream));
@@ -1952,7 +1905,6 @@ int gossip_ae_finish(gossip_engine_t* e, uint64_t* partial) {
 
 int gossip_set_faults(gossip_engine_t* e, uint32_t edge_loss, uint32_t partitions) {
   if (!e) return GOSSIP_EINVAL;
-  e->pre_t = ~0ull;  // records a fused emit made for the next round would be stale
   if ((edge_loss || partitions > 1) &&
       (e->mode == GOSSIP_MODE_ANTIENTROPY || (e->mode == GOSSIP_MODE_FLOOD && !e->flood_edges)))
     return e->fail(GOSSIP_ENOTSUP, "faults: random modes, or a FLOOD engine created with faults or stall_rounds "

@@ -134,8 +134,6 @@ int gossip_set_stream(gossip_engine_t* eng, void* hip_stream);
  *   "alld_frac"    sparse rounds commit every group's D once k x rare >= this x N
  *   "filter_frac"  dense rounds drop edges by the peer's class above this empty/full fraction
  *   "xd_filter_frac"  exchange dense rounds likewise (default 0.6; >= 1 never)
- *   "fuse_emit"    one-shard dense rounds: a dense round's apply also emits the records of a next
- *                  dense round (default 1; 0 = every dense round runs its own emit)
  *   "ahead"        rounds enqueued ahead of the stats read back (1..7, default 2)
  *   "apply_grid"   persistent blocks of the dense apply pass (0 = one block per tile)
  *   "ae_sparse"    ANTIENTROPY: -1 plan sparse rounds (default), 0 never, 1 whenever valid
