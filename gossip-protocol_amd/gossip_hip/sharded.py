@@ -70,11 +70,13 @@ class _Comm:
     """The collectives a round needs, on engine memory: in place over RCCL for
     device engines, staged through host tensors over gloo."""
 
-    def __init__(self, engine, group):
+    def __init__(self, engine, group, direct: bool | None = None):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.on_device = engine.on_device
         self.direct = engine.on_device and self.world > 1 and _device_collectives(group)
+        if direct is not None:  # tests: the collectives on engine memory as RCCL would run them
+            self.direct = direct and self.world > 1
 
     def _sync(self):
         if self.on_device:
@@ -110,7 +112,7 @@ class _Comm:
 
     def small(self, values) -> torch.Tensor:
         t = torch.as_tensor(np.asarray(values, dtype=np.int64).copy())
-        return t.cuda() if self.direct else t
+        return t.cuda() if self.direct and self.on_device else t
 
     def all_reduce_max(self, values: np.ndarray) -> np.ndarray:
         t = self.small(np.asarray(values, dtype=np.int64))
@@ -236,7 +238,7 @@ def _bind_stream(engine, comm: _Comm):
     launch on that same stream, or its kernels could read the image before the all-gather
     wrote it.  torch's default stream is the null stream (cuda_stream 0), which
     gossip_set_stream binds as such."""
-    if comm.direct:
+    if comm.direct and comm.on_device:
         engine.set_stream(torch.cuda.current_stream().cuda_stream)
 
 
@@ -263,11 +265,12 @@ def _ae_round(engine, comm: _Comm) -> np.ndarray:
     return engine.ae_finish()
 
 
-def sharded_round(engine, group=None, kinds: list | None = None) -> dict:
+def sharded_round(engine, group=None, kinds: list | None = None, direct: bool | None = None) -> dict:
     """Runs one round of a sharded engine; every rank must call it.  With RCCL the engine is
     bound to the caller's current torch stream, so every kernel is ordered after the
-    collectives that feed it.  kinds: the round's plan kind is appended to it."""
-    comm = _Comm(engine, group)
+    collectives that feed it.  kinds: the round's plan kind is appended to it.  direct (tests):
+    force the in-place collective path that RCCL takes, also for host engines over gloo."""
+    comm = _Comm(engine, group, direct)
     _bind_stream(engine, comm)
     kind = _plan(engine, comm)
     if kinds is not None:
@@ -287,13 +290,13 @@ def sharded_round(engine, group=None, kinds: list | None = None) -> dict:
     return engine.round_commit(partial)
 
 
-def sharded_run(engine, max_rounds: int, group=None, kinds: list | None = None) -> list:
+def sharded_run(engine, max_rounds: int, group=None, kinds: list | None = None, direct: bool | None = None) -> list:
     """Rounds until converged (same stop rule as gossip_step); kinds collects the plan kinds."""
     if engine.on_device and torch.cuda.is_available():
         engine.set_stream(torch.cuda.current_stream().cuda_stream)
     out = []
     for _ in range(max_rounds):
-        st = sharded_round(engine, group, kinds)
+        st = sharded_round(engine, group, kinds, direct)
         out.append(st)
         if st["converged"] or (engine.cfg.mode == 0 and st["messages"] == 0):
             break

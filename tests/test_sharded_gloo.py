@@ -63,7 +63,7 @@ PLANS = {
 PLAN_KINDS = {"sparse": {1}, "dense": {0}, "exchange": {3}, "exchange-unfiltered": {3}, "classcoded": {4}}
 
 
-def _worker(rank, world, port, case, q, params=None):
+def _worker(rank, world, port, case, q, params=None, direct=None):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [os.path.join(root, "gossip-protocol_amd"), os.path.join(root, "oracle")]
     import torch.distributed as dist
@@ -81,14 +81,14 @@ def _worker(rank, world, port, case, q, params=None):
     else:
         e.inject_random()
     kinds = []
-    stats = sharded_run(e, 200, kinds=kinds)
+    stats = sharded_run(e, 200, kinds=kinds, direct=direct)
     q.put((rank, e.lo, e.hi, stats, e.read_shard(), kinds))
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("plan", list(PLANS))
 @pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
-def test_two_ranks_equal_one(case, plan, world=2):
+def test_two_ranks_equal_one(case, plan, world=2, direct=None):
     if case[0] == "flood" and plan != "auto":
         pytest.skip("FLOOD rounds are always dense (no sparse protocol)")
     import oracle_py as op
@@ -105,7 +105,7 @@ def test_two_ranks_equal_one(case, plan, world=2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, case, q, PLANS[plan])) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, case, q, PLANS[plan], direct)) for r in range(world)]
     for p in procs:
         p.start()
     got = [q.get(timeout=120) for _ in range(world)]
@@ -123,6 +123,15 @@ def test_two_ranks_equal_one(case, plan, world=2):
             assert 4 in kinds and 1 in kinds  # sparse rounds and class-coded dense rounds at G < xd_shards
 
 
+@pytest.mark.parametrize("plan", ["auto", "sparse", "dense", "exchange", "classcoded"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_direct_collective_path_equals_one(plan, world):
+    """The driver's RCCL branch (collectives in place on the engines' own buffers: all-gathers
+    whose send slice lies inside the image, all-to-alls on engine memory, async work.wait()),
+    forced over gloo on host engines: the rounds still equal one engine."""
+    test_two_ranks_equal_one(CASES[0], plan, world=world, direct=True)
+
+
 @pytest.mark.parametrize("plan", ["exchange", "auto-exchange", "classcoded"])
 @pytest.mark.parametrize("case", CASES[:5], ids=[c[0] for c in CASES[:5]])
 def test_three_ranks_exchange_equal_one(case, plan):
@@ -138,7 +147,7 @@ AE_CASES = [  # N, K, fanout, seed, fail, recover
 ]
 
 
-def _ae_worker(rank, world, port, case, q):
+def _ae_worker(rank, world, port, case, q, direct=None):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [os.path.join(root, "gossip-protocol_amd"), os.path.join(root, "oracle")]
     import torch.distributed as dist
@@ -152,17 +161,17 @@ def _ae_worker(rank, world, port, case, q):
     e = op.OracleEngine(N, K, "antientropy", k, seed, flags=1, shard_rank=rank, shard_count=world,
                         churn_fail=ct(fail), churn_recover=ct(rec))
     e.inject_random()
-    first = sharded_run(e, 4)
+    first = sharded_run(e, 4, direct=direct)
     e.inject(N - 1, 0)  # a client write mid-run: the global max vector is re-derived (MAX all-reduce)
     e.inject(N // 3, K - 1)
-    rest = sharded_run(e, 300)
+    rest = sharded_run(e, 300, direct=direct)
     q.put((rank, e.lo, e.hi, first + rest, e.read_rows()))
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("case", AE_CASES, ids=[f"N{c[0]}-K{c[1]}-k{c[2]}" for c in AE_CASES])
-def test_antientropy_sharded_equals_one(case, world):
+def test_antientropy_sharded_equals_one(case, world, direct=None):
     """Sharded anti-entropy (Design B: stale-bit all-gather, request/reply
     all-to-all, max-merge on the owner, ncclMax for the global max vector) over gloo equals the
     one-shard run bit for bit: per-round stats (alive, full, messages, hash, per-component
@@ -182,7 +191,7 @@ def test_antientropy_sharded_equals_one(case, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_ae_worker, args=(r, world, port, case, q)) for r in range(world)]
+    procs = [ctx.Process(target=_ae_worker, args=(r, world, port, case, q, direct)) for r in range(world)]
     for p in procs:
         p.start()
     got = [q.get(timeout=120) for _ in range(world)]
@@ -269,3 +278,9 @@ def test_host_lockstep_filtered_exchange_equals_one():
     assert stats == want.stats and set(kinds) == {3}
     sent = [sum(map(sum, r)) for r in items]
     assert sent[0] < k * N // 10 and sent[-1] < k * N // 10 and max(sent) == k * N
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_antientropy_direct_collective_path_equals_one(world):
+    """Sharded anti-entropy through the driver's RCCL branch (forced over gloo on host engines)."""
+    test_antientropy_sharded_equals_one(AE_CASES[1], world, direct=True)
