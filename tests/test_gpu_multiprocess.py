@@ -2,6 +2,9 @@
 boundaries with HIP shard engines equals a single-engine run bit for bit.
 
   gloo — both ranks on device 0, collectives staged through host memory;
+  gloo-dev — both ranks on device 0, the RCCL branch of gossip_hip.sharded forced
+         (direct=True): gloo's device collectives on engine memory in place, the
+         all-gathers async with work.wait(), the engines bound to torch's stream;
   nccl — RCCL collectives on engine memory, in place, with the engines bound to
          torch's current stream (gossip_hip.sharded._bind_stream).  Needs two
          devices (RCCL rejects two ranks on one GPU); skipped on a one-GPU box."""
@@ -35,31 +38,47 @@ def _worker(rank, world, port, case, q, backend="gloo"):
     os.environ["MASTER_PORT"] = str(port)
     dev = rank if backend == "nccl" else 0
     torch.cuda.set_device(dev)
+    direct = True if backend == "gloo-dev" else None
     if backend == "nccl":
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", dev))
     else:
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    mode, k, R, N, seed = case
-    e = Engine(N, R, mode, k, seed, flags=1, device=dev, shard_rank=rank, shard_count=world)
+    mode, k, R, N, seed, params = case
+    kw = _ae_kw(mode)
+    e = Engine(N, R, mode, k, seed, flags=1, device=dev, shard_rank=rank, shard_count=world, params=params, **kw)
     e.inject_random()
-    stats = sharded_run(e, 100)
-    q.put((rank, e.lo, e.hi, stats, e.read_shard()))
+    stats = sharded_run(e, 400, direct=direct)
+    q.put((rank, e.lo, e.hi, stats, _state(e)))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("backend", ["gloo", "nccl"])
-@pytest.mark.parametrize("case", [("pushpull", 2, 64, 1 << 20, 0x5EED0004), ("push", 3, 1, 300001, 7)],
-                         ids=["pushpull-1M", "push-ragged"])
+def _ae_kw(mode):
+    from gossip_hip.engine import churn_threshold as ct
+    return dict(churn_fail=ct(0.01), churn_recover=ct(0.1)) if mode == "antientropy" else {}
+
+
+def _state(e):
+    return e.read_rows() if e.cfg.mode == 4 else e.read_shard()
+
+
+CASES = [("pushpull", 2, 64, 1 << 20, 0x5EED0004, None),
+         ("push", 3, 1, 300001, 7, None),
+         ("pushpull", 2, 64, (1 << 20) + 77, 0x5EED0004, {"xd_shards": 2}),  # dense rounds as exchange rounds
+         ("antientropy", 1, 16, 1 << 18, 0x5EED0005, None)]
+
+
+@pytest.mark.parametrize("backend", ["gloo", "gloo-dev", "nccl"])
+@pytest.mark.parametrize("case", CASES, ids=["pushpull-1M", "push-ragged", "pushpull-exchange", "antientropy"])
 def test_two_processes_equal_one_engine(case, backend):
     import torch
     if backend == "nccl" and torch.cuda.device_count() < 2:
         pytest.skip("RCCL needs one device per rank")
     from gossip_hip import Engine
-    mode, k, R, N, seed = case
-    ref = Engine(N, R, mode, k, seed, flags=1, device=0)
+    mode, k, R, N, seed, _ = case
+    ref = Engine(N, R, mode, k, seed, flags=1, device=0, **_ae_kw(mode))
     ref.inject_random()
-    want = ref.step(100)
-    full = ref.read_shard()
+    want = ref.step(400)
+    full = _state(ref)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -72,4 +91,4 @@ def test_two_processes_equal_one_engine(case, backend):
         assert p.exitcode == 0
     for rank, lo, hi, stats, shard in got:
         assert stats == want.stats
-        assert np.array_equal(shard, full[:, lo:hi])
+        assert np.array_equal(shard, full[lo:hi] if mode == "antientropy" else full[:, lo:hi])
