@@ -119,6 +119,9 @@ def main():
     ap.add_argument("--nodes-per-gpu", type=int, default=NODES_PER_GPU)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dense-only", action="store_true", help="skip the all-dense comparison run (profiling)")
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
+                    help="collectives for N > 1: nccl (= RCCL, the measured path) or gloo (a rehearsal of the "
+                         "multi-rank code on a box with fewer GPUs than ranks: ranks share devices)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -126,9 +129,13 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and not (world == 1 and args.gpus == 1):
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if args.backend == "gloo":
+        local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
-    if world > 1:
+    if world > 1 and args.backend == "nccl":
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    elif world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
 
     from gossip_hip import FLAG_TIMING, Engine
     from gossip_hip.sharded import sharded_run
@@ -168,7 +175,7 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([dt], device="cuda", dtype=torch.float64)
+        t = torch.tensor([dt], device="cuda" if args.backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
@@ -210,6 +217,7 @@ def main():
             "config": {"workload": workload, "nodes": n_total, "rumors": RUMORS, "fanout": FANOUT,
                        "mode": MODE, "seed": hex(seed), "rounds_to_converge": rounds[0],
                        "parallelism": f"shard{world}" if world > 1 else "single"},
+            **({"backend": "gloo (rehearsal: not a measurement)"} if world > 1 and args.backend == "gloo" else {}),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "bytes_per_node_round": bpn, "alg_bytes_per_launch": alg_round,
