@@ -124,7 +124,7 @@ def test_two_ranks_equal_one(case, plan, world=2, direct=None):
 
 
 @pytest.mark.parametrize("plan", ["auto", "sparse", "dense", "exchange", "classcoded"])
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [3])  # ragged shards; world 2 of the same protocol runs on the GPU box
 def test_direct_collective_path_equals_one(plan, world):
     """The driver's RCCL branch (collectives in place on the engines' own buffers: all-gathers
     whose send slice lies inside the image, all-to-alls on engine memory, async work.wait()),
@@ -280,7 +280,7 @@ def test_host_lockstep_filtered_exchange_equals_one():
     assert sent[0] < k * N // 10 and sent[-1] < k * N // 10 and max(sent) == k * N
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [3])
 def test_antientropy_direct_collective_path_equals_one(world):
     """Sharded anti-entropy through the driver's RCCL branch (forced over gloo on host engines)."""
     test_antientropy_sharded_equals_one(AE_CASES[1], world, direct=True)
