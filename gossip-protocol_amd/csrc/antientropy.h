@@ -32,7 +32,7 @@ struct AeArgs {
   // counting-sorted by the peer's tile (2^btl nodes) per region of 2^brs senders;
   // one block per tile then reads the tile's alive / stale bits from LDS and
   // lists the edges into segment = tile (nseg == bnt)
-  uint64_t* brec;    // [bnreg][2^brs * k] records: n | p_local << 32 | stale(n) << 51
+  uint32_t* brec;    // [bnreg][2^brs * k] records: p_local | (n - region base) << btl | stale(n) << (btl + brs)
   uint16_t* boff;    // [bnreg][bnt + 1] run starts inside each region
   uint32_t btl, bnt, brs, bnreg;
   uint32_t spb;      // blocks per segment in the gather / apply / fix kernels
@@ -43,6 +43,7 @@ struct AeBinGeom {
   uint32_t tl, nt, rs, nreg;
 };
 AeBinGeom ae_bin_geom(uint64_t N, uint32_t k);
+bool ae_bin_fits(const AeBinGeom& g);  // the emit's LDS tile counters cover g.nt (else the direct scan)
 
 uint32_t ae_lanes(uint32_t K);
 hipError_t launch_ae_init(uint32_t* V, uint32_t* target, uint64_t N, uint32_t K, uint32_t k0, uint32_t k1,

@@ -366,21 +366,35 @@ __global__ __launch_bounds__(kAeBlock) void ae_sparse_scan_kernel(AeArgs a) {
 // round's churn (ab -> abn), then every alive sender's exchanges counting-sorted
 // by the peer's tile in LDS and
 // written out as one contiguous region; the random reads of the peers' alive /
-// stale bits move to pass 2, where each tile's bits sit in LDS.
+// stale bits move to pass 2, where each tile's bits sit in LDS.  A record is one
+// u32 (ae_rec): 80 KiB of LDS per block, so two blocks share a CU and one's
+// write-out overlaps the other's draws.
 constexpr int kAeBinThreads = 1024;
 constexpr uint32_t kAeBinRec = 16384;    // records per region (LDS)
-constexpr uint32_t kAeBinTiles = 4096;
+constexpr uint32_t kAeBinTiles = 4032;  // (two emit blocks fit 160 KiB of LDS)
 constexpr uint32_t kAeBinQ = kAeBinRec / kAeBinThreads;  // k == 1: senders per thread, peers in registers
 
+// record: p_local (btl bits) | n - region base (brs bits) << btl | stale(n) << (btl + brs)
+__device__ __forceinline__ uint32_t ae_rec(uint32_t pl, uint32_t nl, uint32_t stale, uint32_t btl, uint32_t brs) {
+  return pl | (nl << btl) | (stale << (btl + brs));
+}
+
+#ifndef GOSSIP_AE_EMIT_WAVES
+#define GOSSIP_AE_EMIT_WAVES 8  // waves per SIMD: 8 = two blocks per CU (<= 64 VGPRs)
+#endif
+#ifndef GOSSIP_AE_EMIT_K1
+#define GOSSIP_AE_EMIT_K1 1  // k == 1 keeps the peers of pass A in registers (24 VGPRs spill at 8 waves;
+                             // still 0.516 vs 0.568 ms per sparse round redrawing them, profiles/r02_ae_one)
+#endif
 template <bool K1>
-__global__ __launch_bounds__(kAeBinThreads) void ae_bin_emit_kernel(AeArgs a) {
+__global__ __launch_bounds__(kAeBinThreads, GOSSIP_AE_EMIT_WAVES) void ae_bin_emit_kernel(AeArgs a) {
   __shared__ uint32_t cur[kAeBinTiles];
-  __shared__ uint64_t st[kAeBinRec];
+  __shared__ uint32_t st[kAeBinRec];
   __shared__ uint32_t wsum[kAeBinThreads / 64];
   __shared__ uint32_t wpre[kAeBinThreads / 64 + 1];
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t rs = 1u << a.brs, rp = rs * a.k, nt = a.bnt;
-  const uint64_t tmask = (1ull << a.btl) - 1ull;
+  const uint32_t tmask = (1u << a.btl) - 1u;
   for (uint32_t s = blockIdx.x; s < a.bnreg; s += gridDim.x) {
     const uint64_t base = (uint64_t)s << a.brs;
     __syncthreads();  // the previous region's write-out has read st / cur
@@ -450,21 +464,22 @@ __global__ __launch_bounds__(kAeBinThreads) void ae_bin_emit_kernel(AeArgs a) {
     for (uint32_t q = 0; q < nq; ++q) {
       if (!((live >> q) & 1u)) continue;
       const uint64_t n = base + q * kAeBinThreads + tid;
-      const uint64_t sb = (uint64_t)((stl >> q) & 1u) << 51;
+      const uint32_t nl = q * kAeBinThreads + tid, sb = (stl >> q) & 1u;
       if (K1) {
         const uint32_t p = pr[q];
-        st[atomicAdd(&cur[p >> a.btl], 1u)] = n | ((uint64_t)(p & tmask) << 32) | sb;
+        st[atomicAdd(&cur[p >> a.btl], 1u)] = ae_rec(p & tmask, nl, sb, a.btl, a.brs);
       } else {
         u32x4 x{0, 0, 0, 0};
         for (uint32_t j = 0; j < a.k; ++j) {
           const uint32_t p = peer_j(a, (uint32_t)n, j, x);
-          st[atomicAdd(&cur[p >> a.btl], 1u)] = n | ((uint64_t)(p & tmask) << 32) | sb;
+          st[atomicAdd(&cur[p >> a.btl], 1u)] = ae_rec(p & tmask, nl, sb, a.btl, a.brs);
         }
       }
     }
     __syncthreads();
-    uint64_t* out = a.brec + (size_t)s * rp;
-    for (uint32_t e = tid; e < total; e += kAeBinThreads) out[e] = st[e];
+    // 16-B stores (the region's slot has room for rp records; the tail past total is never read)
+    uint4* out = (uint4*)(a.brec + (size_t)s * rp);
+    for (uint32_t e = tid; e * 4 < total; e += kAeBinThreads) out[e] = ((const uint4*)st)[e];
   }
 }
 
@@ -472,7 +487,8 @@ __global__ __launch_bounds__(kAeBinThreads) void ae_bin_emit_kernel(AeArgs a) {
 // LDS; every record aimed at T (its run in each region, walked 64 runs per wave,
 // lane-strided) counts a message when the peer is alive and lists the exchange
 // into segment T when either end is stale.
-constexpr uint32_t kAeBinTileWords = 8192;  // tiles of up to 2^19 nodes
+constexpr uint32_t kAeBinTileLog = 17;  // tiles of up to 2^17 nodes (ae_rec's fields, 32 KiB of LDS)
+constexpr uint32_t kAeBinTileWords = 1u << (kAeBinTileLog - 6);
 
 __global__ __launch_bounds__(kAeBinThreads) void ae_bin_scan_kernel(AeArgs a) {
   __shared__ uint64_t wa[kAeBinTileWords], ws[kAeBinTileWords];
@@ -511,9 +527,10 @@ __global__ __launch_bounds__(kAeBinThreads) void ae_bin_scan_kernel(AeArgs a) {
     }
     const uint32_t exc = inc - len, total = __shfl(inc, 63, 64);
     const uint64_t rbase = (uint64_t)r * rp + be - exc;  // record of flat index f in this lane's run: rbase + f
+    const uint32_t nmask = (1u << a.brs) - 1u;
     constexpr int U = 4;
     for (uint32_t f0 = 0; f0 < total; f0 += 64 * U) {
-      uint64_t rec[U];
+      uint32_t rec[U], reg[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint32_t f = f0 + u * 64 + lane;
@@ -525,16 +542,17 @@ __global__ __launch_bounds__(kAeBinThreads) void ae_bin_scan_kernel(AeArgs a) {
           if (c < 64 && (uint32_t)__shfl((int)exc, (int)c, 64) <= f) ow = c;
         }
         const uint64_t rb = (uint64_t)__shfl((long long)rbase, (int)ow, 64);
-        rec[u] = f < total ? a.brec[rb + f] : ~0ull;
+        rec[u] = f < total ? a.brec[rb + f] : 0u;
+        reg[u] = f < total ? r0 + ow : ~0u;  // the record's region (~0: past the end)
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const bool valid = rec[u] != ~0ull;
-        const uint32_t n = (uint32_t)rec[u];
-        const uint32_t pl = (uint32_t)(rec[u] >> 32) & tmask;
+        const bool valid = reg[u] != ~0u;
+        const uint32_t n = (reg[u] << a.brs) + ((rec[u] >> a.btl) & nmask);
+        const uint32_t pl = rec[u] & tmask;
         const bool ex = valid && ((wa[pl >> 6] >> (pl & 63)) & 1ull);  // n is alive (pass 1)
         msgs += ex ? 1u : 0u;
-        const bool need = ex && (((rec[u] >> 51) & 1ull) || ((ws[pl >> 6] >> (pl & 63)) & 1ull));
+        const bool need = ex && (((rec[u] >> (a.btl + a.brs)) & 1u) || ((ws[pl >> 6] >> (pl & 63)) & 1ull));
         const uint64_t m = __ballot(need);
         if (!m) continue;
         uint32_t base = 0;
@@ -760,22 +778,24 @@ hipError_t launch_ae_sparse(const AeArgs& a, hipStream_t st) {
 
 AeBinGeom ae_bin_geom(uint64_t N, uint32_t k) {
   AeBinGeom g{};
-  uint32_t lg = 0;
-  while ((1ull << lg) < N) ++lg;
-  g.tl = lg > 8 ? lg - 8 : 0;  // ~256 tiles, one block per CU
-  if (g.tl < 12) g.tl = 12;
-  if (g.tl > 19) g.tl = 19;    // LDS: 2 x 2^tl bits
-  g.nt = (uint32_t)((N + (1ull << g.tl) - 1) >> g.tl);
   uint32_t rs = kAeBinRec;  // 2^brs senders * k records <= kAeBinRec, at least one block of senders
   g.rs = 14;
   while (g.rs > 10 && (rs >> (14 - g.rs)) * k > kAeBinRec) --g.rs;
   g.nreg = (uint32_t)((N + (1ull << g.rs) - 1) >> g.rs);
+  uint32_t lg = 0;
+  while ((1ull << lg) < N) ++lg;
+  g.tl = lg > 8 ? lg - 8 : 0;  // ~256 tiles, one block per CU
+  if (g.tl < 12) g.tl = 12;
+  if (g.tl > kAeBinTileLog) g.tl = kAeBinTileLog;  // with rs <= 14, a record's fields fill one u32 (ae_rec)
+  g.nt = (uint32_t)((N + (1ull << g.tl) - 1) >> g.tl);
   return g;
 }
 
+bool ae_bin_fits(const AeBinGeom& g) { return g.nt <= kAeBinTiles; }
+
 hipError_t launch_ae_sparse_binned(const AeArgs& a, hipStream_t st) {
-  const uint32_t eg = a.bnreg < 256 ? a.bnreg : 256;
-  if (a.k == 1 && (1u << a.brs) == kAeBinRec)
+  const uint32_t eg = a.bnreg < 512 ? a.bnreg : 512;  // two blocks per CU
+  if (GOSSIP_AE_EMIT_K1 && a.k == 1 && (1u << a.brs) == kAeBinRec)
     ae_bin_emit_kernel<true><<<eg, kAeBinThreads, 0, st>>>(a);
   else
     ae_bin_emit_kernel<false><<<eg, kAeBinThreads, 0, st>>>(a);

@@ -89,7 +89,7 @@ struct gossip_engine {
   uint32_t ae_nseg = 1, ae_spc = 1, ae_segcap = 1;
   bool ae_bin = false;  // binned sparse scan (AeArgs::brec)
   AeBinGeom ae_bg{};
-  uint64_t* ae_brec = nullptr;
+  uint32_t* ae_brec = nullptr;
   uint16_t* ae_boff = nullptr;
   uint64_t ae_cap = 0, ae_hash = 0, ae_stale = 0, ae_alive = 0, ae_full = 0;
   uint32_t ae_epoch = 0;
@@ -1021,11 +1021,11 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
         !alloc_raw((void**)&e->alive, nw * 16) || !alloc_raw((void**)&e->alive_n, nw * 16))
       return bail(GOSSIP_ENOMEM);
     if (launch_ae_fill_alive(e->alive, e->N, nullptr) != hipSuccess) return bail(GOSSIP_EHIP);
-    e->ae_bin = !(cfg->flags & GOSSIP_FLAG_AE_DIRECT_SCAN) && e->k <= 16;  // else the direct scan
+    e->ae_bg = ae_bin_geom(e->N, e->k);
+    e->ae_bin = !(cfg->flags & GOSSIP_FLAG_AE_DIRECT_SCAN) && e->k <= 16 && ae_bin_fits(e->ae_bg);  // else the direct scan
     if (e->ae_bin) {
-      e->ae_bg = ae_bin_geom(e->N, e->k);
       const size_t recs = (size_t)e->ae_bg.nreg * ((size_t)e->k << e->ae_bg.rs);
-      if (!alloc_raw((void**)&e->ae_brec, recs * 8) ||
+      if (!alloc_raw((void**)&e->ae_brec, recs * 4) ||
           !alloc_raw((void**)&e->ae_boff, (size_t)e->ae_bg.nreg * (e->ae_bg.nt + 1) * 2))
         return bail(GOSSIP_ENOMEM);
     }

@@ -8,6 +8,9 @@ import os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "gossip-protocol_amd"))
 from gossip_hip import FLAG_TIMING, Engine, loss_threshold
+from gossip_hip import engine as _eng
+if os.environ.get("GOSSIP_LIB"):  # a library variant (tools/build_variants.sh)
+    _eng.load_library(os.environ["GOSSIP_LIB"])
 LG = int(sys.argv[1]) if len(sys.argv) > 1 else 26
 N, K, k = 1 << LG, 16, 1
 e = Engine(N, K, "antientropy", k, 0x5EED0005, flags=1 | FLAG_TIMING,
