@@ -35,7 +35,13 @@ namespace gossip {
 namespace {
 
 constexpr int kScanThreads = 1024;
-constexpr uint32_t kScanGrid = 256;  // one block per CU: the summary takes 128 KiB of LDS
+#ifndef GOSSIP_SCAN_GRID
+#define GOSSIP_SCAN_GRID 256
+#endif
+#ifndef GOSSIP_SCAN_WAVES
+#define GOSSIP_SCAN_WAVES 4
+#endif
+constexpr uint32_t kScanGrid = GOSSIP_SCAN_GRID;  // one block per CU: the summary takes 128 KiB of LDS
 constexpr int kCommitThreads = 256;
 constexpr uint32_t kRwWords = 1024;  // rare-bitmap words staged per scan chunk (64K nodes)
 constexpr int kScanUnroll = 2;       // nodes per lane per scan step
@@ -269,7 +275,7 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
 }
 
 template <int MODE, bool FAULTS>
-__global__ __launch_bounds__(kScanThreads) void frontier_scan_kernel(FrontierBufs f, const uint64_t* __restrict__ S,
+__global__ __launch_bounds__(kScanThreads, GOSSIP_SCAN_WAVES) void frontier_scan_kernel(FrontierBufs f, const uint64_t* __restrict__ S,
                                                                       uint64_t N, uint32_t R, uint32_t k, uint32_t t,
                                                                       uint32_t key0, uint32_t key1, uint64_t per_block,
                                                                       const uint64_t* partial, uint32_t maj,

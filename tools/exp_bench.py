@@ -22,5 +22,9 @@ for i in range(int(os.environ.get("EXP_STEPS", 4))):
     e.inject_random()
     r = e.step(64, with_infected=False)
 ms, n = e.kernel_time(3)
+sms, sn = e.kernel_time(4)
+tms, tn = e.kernel_time(0)
+steps = int(os.environ.get("EXP_STEPS", 4)) - 1
 print(f"{os.environ.get('GOSSIP_LIB', 'default')}: rounds {r.rounds}, dense rounds {n}, "
-      f"{ms * 1e3 / max(n, 1):.1f} us per dense round")
+      f"{ms * 1e3 / max(n, 1):.1f} us per dense round, sparse {sms * 1e3 / max(sn, 1):.1f} us per round, "
+      f"step {tms / max(steps, 1):.3f} ms of device time")
