@@ -36,6 +36,16 @@ namespace {
 
 constexpr int kAeBlock = 256;
 constexpr int kAeWaves = kAeBlock / 64;
+// dense-round kernels: minimum waves per SIMD the compiler must fit (1 = no limit on VGPRs)
+#ifndef GOSSIP_AE_PULL_WAVES
+#define GOSSIP_AE_PULL_WAVES 1
+#endif
+#ifndef GOSSIP_AE_PUSH_WAVES
+#define GOSSIP_AE_PUSH_WAVES 1
+#endif
+#ifndef GOSSIP_AE_STATS_WAVES
+#define GOSSIP_AE_STATS_WAVES 1
+#endif
 
 __device__ __forceinline__ bool churned(uint8_t alive, uint32_t n, uint32_t t, uint32_t k0, uint32_t k1,
                                         uint32_t fail, uint32_t rec) {
@@ -144,7 +154,7 @@ struct MaskOf {  // one bit per lane of a node's group
 // every row — and, per exchange, the mask of components where V[n] > V[p_j]: the
 // push pass then needs neither the peer's row nor its alive bit
 template <uint32_t L>
-__global__ __launch_bounds__(kAeBlock) void ae_pull_kernel(AeArgs a) {
+__global__ __launch_bounds__(kAeBlock, GOSSIP_AE_PULL_WAVES) void ae_pull_kernel(AeArgs a) {
   using MT = typename MaskOf<L>::T;
   constexpr uint32_t per = 64 / L;
   constexpr uint64_t gmask = L >= 64 ? ~0ull : ((1ull << L) - 1ull);
@@ -207,7 +217,7 @@ __global__ __launch_bounds__(kAeBlock) void ae_pull_kernel(AeArgs a) {
 
 // push pass: atomicMax(Vn[p_j][c], V[n][c]) for the components c of the pull pass's mask
 template <uint32_t L>
-__global__ __launch_bounds__(kAeBlock) void ae_push_kernel(AeArgs a) {
+__global__ __launch_bounds__(kAeBlock, GOSSIP_AE_PUSH_WAVES) void ae_push_kernel(AeArgs a) {
   using MT = typename MaskOf<L>::T;
   constexpr uint32_t per = 64 / L;
   const uint32_t lane = threadIdx.x & 63, sub = lane / L, c = lane % L;
@@ -252,7 +262,7 @@ __global__ __launch_bounds__(kAeBlock) void ae_push_kernel(AeArgs a) {
 // Here lane (sub, c) holds component c of nodes sub*L .. sub*L+L-1 (one per sub-step),
 // so a group's "differs" bits OR-reduce across its L lanes into its nodes' stale bits.
 template <uint32_t L>
-__global__ __launch_bounds__(kAeBlock) void ae_stats_kernel(AeArgs a, const uint32_t* __restrict__ V, uint64_t* ab,
+__global__ __launch_bounds__(kAeBlock, GOSSIP_AE_STATS_WAVES) void ae_stats_kernel(AeArgs a, const uint32_t* __restrict__ V, uint64_t* ab,
                                                             bool write_stale) {
   using BT = typename std::conditional<(L > 32), uint64_t, uint32_t>::type;
   constexpr uint32_t per = 64 / L;
