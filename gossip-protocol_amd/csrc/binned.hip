@@ -1029,6 +1029,17 @@ hipError_t launch_sb_round(const SbGeom& g, const SbBufs& b, const uint64_t* ima
 namespace {
 
 constexpr uint32_t kXdMaxG = 256;
+// sender regions of the exchange rounds: at most this many items (xd_emit stages them in
+// LDS, 6 B each), and the count / emit grid.  8192 items and 512 blocks (two emit blocks per
+// CU) measured the same at G = 8 (9.81 vs 9.81-9.87 ms per rank, profiles/r02_xd/region)
+#ifndef GOSSIP_XD_SEND_REGION
+#define GOSSIP_XD_SEND_REGION 16384
+#endif
+#ifndef GOSSIP_XD_EMIT_GRID
+#define GOSSIP_XD_EMIT_GRID 256
+#endif
+constexpr uint32_t kXdSendRegion = GOSSIP_XD_SEND_REGION;
+static_assert(kXdSendRegion <= kRecPerRegion, "xd sender regions: at most kRecPerRegion items");
 // binned received item: p_local [0, 14) | slot in its region [14, 28) | no push | no pull
 constexpr uint32_t kXbVZ = 1u << 28;
 constexpr uint32_t kXbVF = 1u << 29;
@@ -1141,8 +1152,8 @@ __global__ __launch_bounds__(kEmitThreads) void xd_emit_kernel(XdGeom g, const u
                                                                 Faults fa, XdFilter xf) {
   __shared__ uint32_t cur[kXdMaxG];
   __shared__ uint32_t lofs[kXdMaxG + 1];
-  __shared__ uint32_t st_id[kRecPerRegion];
-  __shared__ uint16_t st_nl[kRecPerRegion];
+  __shared__ uint32_t st_id[kXdSendRegion];
+  __shared__ uint16_t st_nl[kXdSendRegion];
   const uint32_t tid = threadIdx.x, Nl32 = (uint32_t)g.Nl, G = g.G;
   const uint64_t fm = full_mask1(R), nm1 = g.N - 1;
   for (uint32_t s = blockIdx.x; s < g.s.nt_s; s += gridDim.x) {
@@ -1375,6 +1386,12 @@ XdGeom make_xd_geom(uint64_t N, uint32_t k, uint64_t Nl, uint64_t lo, uint64_t n
   g.rank = rank;
   g.k = k;
   g.s = make_bin_geom(nown ? nown : 1, k);
+  while (g.s.ts > 64 && g.s.ts * k > kXdSendRegion) {
+    g.s.ts >>= 1;
+    --g.s.ts_log;
+  }
+  g.s.rp = g.s.ts * k;
+  g.s.nt_s = (uint32_t)(((nown ? nown : 1) + g.s.ts - 1) / g.s.ts);
   g.r = g.s;
   g.r.N = nown;
   g.r.ts = kXdBinRegion;
@@ -1448,8 +1465,8 @@ hipError_t launch_xd_requests(const XdGeom& g, const XdBufs& b, const uint64_t* 
                               uint32_t key0, uint32_t key1, uint32_t mode, const Faults& fa, const XdFilter& xf,
                               hipStream_t st) {
   if (g.nown == 0) return hipMemsetAsync(b.ocnt, 0, g.G * 4, st);
-  const uint32_t eg = g.s.nt_s < kEmitGrid ? g.s.nt_s : kEmitGrid;
-  // (1024 blocks instead of one per CU: same time, profiles/r02_xd/variants3)
+  const uint32_t eg = g.s.nt_s < GOSSIP_XD_EMIT_GRID ? g.s.nt_s : GOSSIP_XD_EMIT_GRID;
+  // (count: 1024 blocks instead of one per CU took the same time, profiles/r02_xd/variants3)
   if (fa.any()) xd_count_kernel<true><<<eg, kEmitThreads, 0, st>>>(g, S, b.rcnt, R, t, key0, key1, mode, fa, xf);
   else xd_count_kernel<false><<<eg, kEmitThreads, 0, st>>>(g, S, b.rcnt, R, t, key0, key1, mode, fa, xf);
   xd_scan_kernel<<<g.G, 1024, 0, st>>>(b.rcnt, b.roff, b.ocnt, g.s.nt_s, g.G);
