@@ -3,13 +3,17 @@
 
 A step is one full dissemination run of the hot path: reset, inject the 64
 rumors at their Philox origins, then push-pull rounds (fanout 2) until every
-node holds every rumor.  node-updates = nodes x rounds.  Workload per GPU is
-2^24 nodes (configs[2]; at 8 GPUs this is configs[3], 2^27 nodes sharded
-2^24/GPU, weak scaling).  State is resident in HBM; nothing crosses PCIe in
-the timed region except the per-round 8-byte-per-rumor stats readback.
+node holds every rumor.  node-updates = nodes x rounds.  The workload is the
+north-star sweep, configs[3]: 2^27 nodes, push-pull k=2, R=64, seed
+0x5EED0004, at every GPU count (1/2/4/8 GPUs, strong
+scaling; N > 1 shards the node ids).  At one GPU the configs[2]
+workload (2^24 nodes, seed 0x5EED0003) is timed beside it as `secondary`.
+State is resident in HBM; nothing crosses PCIe in the timed region except the
+per-round 8-byte-per-rumor stats readback.
 
 Single GPU:  python bench.py [--steps K --warmup W]
 N GPUs:      python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+Weak scaling instead (fixed nodes per GPU): --nodes-per-gpu M
 """
 from __future__ import annotations
 
@@ -26,7 +30,10 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-NODES_PER_GPU = 1 << 24
+NODES_TOTAL = 1 << 27      # configs[3], the north-star sweep (all GPU counts)
+SEED_TOTAL = 0x5EED0004
+NODES_SECONDARY = 1 << 24  # configs[2], one GPU
+SEED_SECONDARY = 0x5EED0003
 RUMORS = 64
 FANOUT = 2
 MODE = "pushpull"
@@ -41,15 +48,16 @@ def alg_bytes_per_node_round(mode: str, k: int, words: int) -> int:
 
 def load_pmc(workload: str):
     """PMC HBM traffic per dense round (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM), summed over
-    the dense round's kernels, from the committed passes (tools/gpu_pmc_dense.sh -> profiles/)."""
-    path = os.path.join(ROOT, "profiles", "pmc_dense_round.json")
-    try:
-        with open(path) as f:
-            d = json.load(f)
+    the dense round's kernels, from the committed passes (tools/pmc_dense.py -> profiles/pmc_dense_*.json)."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_dense_*.json"))):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
         if d.get("workload") == workload:
             return d.get("hbm_bytes_per_dense_round"), os.path.relpath(path, ROOT)
-    except (OSError, ValueError):
-        pass
     return None, None
 
 
@@ -69,25 +77,29 @@ def _omp_run(n_nodes: int, seed: int, threads: int, budget_s: float):
     return n_nodes * rounds / dt, rounds, dt
 
 
-def cpu_baseline(n_nodes: int, seed: int, budget_s: float = 10.0):
+def cpu_baseline(n_nodes: int, seed: int, budget_s: float = 8.0):
     """The oracle (C restatement of the same rounds, `kind: port`; the reference itself is Go and not
-    buildable here) on the host cores, same workload, bounded sample: OpenMP on this job's host-core
-    share, and one thread."""
+    buildable here) on the host, same workload, bounded samples (whole rounds from the start of the run,
+    about `budget_s` each): OpenMP on every CPU this process may run on (the headline), the job's
+    host-core share (OMP_NUM_THREADS, 16 on the GPU box) beside it, and one thread."""
     nproc = os.cpu_count() or 1
     try:
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = nproc
-    # the GPU box gives each GPU job a share of the host (OMP_NUM_THREADS, 16 there); here: every core
-    threads = max(1, min(avail, int(os.environ.get("OMP_NUM_THREADS", avail))))
-    v, rounds, dt = _omp_run(n_nodes, seed, threads, budget_s)
+    share = max(1, min(avail, int(os.environ.get("OMP_NUM_THREADS", avail))))
+    v, rounds, dt = _omp_run(n_nodes, seed, avail, budget_s)
+    out = {"value": v, "unit": "node-updates/s", "cores": avail, "kind": "port",
+           "nproc": nproc, "affinity_cpus": avail,
+           "sample": f"oracle/gossip_oracle.c, first {rounds} rounds ({dt:.1f} s) of the same {n_nodes}-node "
+                     f"push-pull k=2 R=64 run on {avail} OpenMP threads (every affinity CPU; nproc {nproc})"}
+    if share != avail:
+        vs, rs, ds = _omp_run(n_nodes, seed, share, budget_s)
+        out["host_share"] = {"value": vs, "cores": share, "rounds": rs, "seconds": ds,
+                             "note": "OMP_NUM_THREADS: this job's share of the host"}
     v1, rounds1, dt1 = _omp_run(n_nodes, seed, 1, budget_s)
-    return {"value": v, "unit": "node-updates/s", "cores": threads, "kind": "port",
-            "single_thread": {"value": v1, "rounds": rounds1, "seconds": dt1},
-            "nproc": nproc, "affinity_cpus": avail,
-            "sample": f"oracle/gossip_oracle.c, first {rounds} rounds ({dt:.1f} s) of the same {n_nodes}-node "
-                      f"push-pull k=2 R=64 run on {threads} OpenMP threads (the host share of this job; "
-                      f"nproc {nproc}); single thread: first {rounds1} rounds ({dt1:.1f} s)"}
+    out["single_thread"] = {"value": v1, "rounds": rounds1, "seconds": dt1}
+    return out
 
 
 def dense_only(n_nodes: int, seed: int, device: int, steps: int = 2):
@@ -107,8 +119,78 @@ def dense_only(n_nodes: int, seed: int, device: int, steps: int = 2):
     bpn = alg_bytes_per_node_round(MODE, FANOUT, 1)
     return {"avg_round_us": us, "achieved_GBps": bpn * n_nodes / us / 1e3,
             "frac": bpn * n_nodes / us / 1e3 / HBM_PEAK_GBS, "rounds_timed": n,
-            "note": "GOSSIP_FLAG_DENSE: every round of the step on bin_emit+transpose+serve+apply (also the "
-                    "nearly empty / nearly full ones), same workload"}
+            "note": "GOSSIP_FLAG_DENSE: every round of the step on the dense pipeline (also the nearly empty / "
+                    "nearly full ones), same workload"}
+
+
+def workload_name(nodes: int, world: int, per_gpu: bool) -> str:
+    lg = int(np.log2(nodes))
+    if per_gpu:
+        return f"pushpull k=2 R=64, 2^{lg} nodes/GPU x {world}"
+    return f"pushpull k=2 R=64, 2^{lg} nodes over {world} GPU" + ("s" if world > 1 else "")
+
+
+def single_gpu_roofline(eng, nodes: int, workload: str) -> dict:
+    """The dominant kernel group = the dense round (every kernel of one dense round), hipEvents around
+    each dense round on the engine's stream inside the timed steps (engine timer 3)."""
+    bpn = alg_bytes_per_node_round(MODE, FANOUT, 1)
+    alg_round = bpn * nodes  # algorithmic bytes of one round (SURVEY.md §8(d))
+    dense_ms, dense_n = eng.kernel_time(3)
+    sparse_ms, sparse_n = eng.kernel_time(4)
+    step_ms, step_rounds = eng.kernel_time(0)
+    dense_s = dense_ms / 1e3 / max(dense_n, 1)
+    achieved = alg_round / dense_s / 1e9
+    step_round_s = step_ms / 1e3 / max(step_rounds, 1)
+    rl = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+          "bytes_per_node_round": bpn, "alg_bytes_per_launch": alg_round,
+          "avg_launch_us": dense_s * 1e6, "rounds_timed": dense_n,
+          "kernel": ("dense round = every kernel of one dense round (bin_emit, transpose, serve, apply; one "
+                     "launch each), hipEvents around each dense round of the timed steps; achieved = 64 B x "
+                     "nodes / average dense-round time (SURVEY.md §8(d))")}
+    traffic, src = load_pmc(workload)
+    if traffic:
+        rl["traffic"] = traffic
+        rl["traffic_ratio"] = traffic / alg_round
+        rl["traffic_GBps"] = traffic / dense_s / 1e9
+        rl["traffic_source"] = src
+    rl["step_frac"] = {"achieved": alg_round / step_round_s / 1e9,
+                       "frac": alg_round / step_round_s / 1e9 / HBM_PEAK_GBS,
+                       "avg_round_us": step_round_s * 1e6, "rounds": step_rounds,
+                       "note": "whole step (sparse rounds at the dense byte count, gaps included)"}
+    rl["sparse_rounds"] = {"avg_round_us": sparse_ms * 1e3 / max(sparse_n, 1), "rounds_timed": sparse_n}
+    return rl
+
+
+def secondary_run(device: int, steps: int, warmup: int) -> dict:
+    """configs[2] on the same GPU (2^24 nodes: the state fits the 256 MiB Infinity Cache), same step."""
+    from gossip_hip import FLAG_TIMING, Engine
+    n = NODES_SECONDARY
+    e = Engine(n, RUMORS, MODE, FANOUT, SEED_SECONDARY, flags=FLAG_TIMING, device=device)
+
+    def one():
+        e.reset(); e.inject_random()
+        return e.step(64, with_infected=False)
+    for _ in range(warmup):
+        one()
+    e.reset_timing()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rounds = 0
+    for _ in range(steps):
+        res = one()
+        assert res.converged
+        rounds += res.rounds
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    wl = workload_name(n, 1, False)
+    rl = single_gpu_roofline(e, n, wl)
+    e.close()
+    return {"workload": wl, "nodes": n, "seed": hex(SEED_SECONDARY), "value": n * rounds / dt,
+            "ms_per_step": dt * 1e3 / steps, "rounds_to_converge": rounds // steps,
+            "roofline_frac": rl["frac"], "avg_dense_round_us": rl["avg_launch_us"],
+            "traffic": rl["traffic"], "step_frac": rl["step_frac"]["frac"],
+            "sparse_avg_round_us": rl["sparse_rounds"]["avg_round_us"]}
 
 
 def main():
@@ -116,9 +198,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--nodes-per-gpu", type=int, default=NODES_PER_GPU)
+    ap.add_argument("--nodes", type=int, default=NODES_TOTAL, help="total nodes (strong scaling; default 2^27)")
+    ap.add_argument("--nodes-per-gpu", type=int, default=0, help="weak scaling: this many nodes per GPU")
+    ap.add_argument("--seed", type=lambda x: int(x, 0), default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dense-only", action="store_true", help="skip the all-dense comparison run (profiling)")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the configs[2] line (profiling)")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="collectives for N > 1: nccl (= RCCL, the measured path) or gloo (a rehearsal of the "
                          "multi-rank code on a box with fewer GPUs than ranks: ranks share devices)")
@@ -140,8 +225,12 @@ def main():
     from gossip_hip import FLAG_TIMING, Engine
     from gossip_hip.sharded import sharded_run
 
-    n_total = args.nodes_per_gpu * world
-    seed = 0x5EED0003 if world == 1 else 0x5EED0004
+    per_gpu = args.nodes_per_gpu > 0
+    n_total = args.nodes_per_gpu * world if per_gpu else args.nodes
+    if args.seed is not None:
+        seed = args.seed
+    else:
+        seed = SEED_TOTAL if n_total >= NODES_TOTAL or world > 1 else SEED_SECONDARY
     eng = Engine(n_total, RUMORS, MODE, FANOUT, seed, flags=FLAG_TIMING, device=local,
                  shard_rank=rank, shard_count=world)
     if world > 1:
@@ -183,22 +272,22 @@ def main():
     value = n_total * total_rounds / dt
     nown = eng.hi - eng.lo
     bpn = alg_bytes_per_node_round(MODE, FANOUT, 1)
-    workload = f"pushpull k=2 R=64, 2^{int(np.log2(args.nodes_per_gpu))} nodes/GPU x {world}"
-    alg_round = bpn * nown  # algorithmic bytes of one round over this rank's nodes
+    workload = workload_name(args.nodes_per_gpu if per_gpu else n_total, world, per_gpu)
     if world == 1:
-        # the dominant kernel = the dense round (emit + transpose + serve + apply), hipEvents around each
-        # dense round on the engine's stream, inside the timed steps (timer 3); the whole step beside it
-        dense_ms, dense_n = eng.kernel_time(3)
-        sparse_ms, sparse_n = eng.kernel_time(4)
-        step_ms, step_rounds = eng.kernel_time(0)
-        dense_s = dense_ms / 1e3 / max(dense_n, 1)
-        achieved = alg_round / dense_s / 1e9
-        step_round_s = step_ms / 1e3 / max(step_rounds, 1)
+        rl = single_gpu_roofline(eng, n_total, workload)
     else:
+        alg_round = bpn * nown  # algorithmic bytes of one round over this rank's nodes
         round_ms, round_launches = eng.kernel_time(0)
         dense_s = round_ms / 1e3 / max(round_launches, 1)
-        dense_n = round_launches
         achieved = alg_round / dense_s / 1e9
+        rl = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+              "frac": achieved / HBM_PEAK_GBS, "traffic": None, "bytes_per_node_round": bpn,
+              "alg_bytes_per_launch": alg_round, "avg_launch_us": dense_s * 1e6, "rounds_timed": round_launches,
+              "kernel": ("sharded rounds, hipEvent-timed device work of the hot kernels per round (timer 0): "
+                         "dense = exchange round (count + emit, bin + serve + unpermute, apply; G >= 6) or the "
+                         "binned push / pull passes + serve + apply after the state all-gather (G < 6), "
+                         "sparse = rare index + sharded scan (DESIGN.md §5); collectives not included")}
+    eng.close()
 
     if rank == 0:
         out = {
@@ -210,42 +299,20 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": dt * 1e3 / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if per_gpu else "strong",
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic (64 rumors injected at Philox tag-2 origins)",
-            "config": {"workload": workload, "nodes": n_total, "rumors": RUMORS, "fanout": FANOUT,
-                       "mode": MODE, "seed": hex(seed), "rounds_to_converge": rounds[0],
+            "config": {"workload": workload, "nodes": n_total, "nodes_per_gpu": nown, "rumors": RUMORS,
+                       "fanout": FANOUT, "mode": MODE, "seed": hex(seed), "rounds_to_converge": rounds[0],
                        "parallelism": f"shard{world}" if world > 1 else "single"},
             **({"backend": "gloo (rehearsal: not a measurement)"} if world > 1 and args.backend == "gloo" else {}),
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "bytes_per_node_round": bpn, "alg_bytes_per_launch": alg_round,
-                         "avg_launch_us": dense_s * 1e6, "rounds_timed": dense_n},
+            "roofline": rl,
         }
-        rl = out["roofline"]
-        if world == 1:
-            rl["kernel"] = ("dense round = bin_emit + transpose_u16 + bin_serve + bin_apply (one launch each per "
-                            "round), hipEvents around each dense round of the timed steps; achieved = 64 B x "
-                            "nodes / average dense-round time (SURVEY.md §8(d))")
-            traffic, src = load_pmc(workload)
-            if traffic:
-                rl["traffic"] = traffic
-                rl["traffic_ratio"] = traffic / alg_round
-                rl["traffic_GBps"] = traffic / dense_s / 1e9
-                rl["traffic_source"] = src
-            rl["step_frac"] = {"achieved": alg_round / step_round_s / 1e9,
-                               "frac": alg_round / step_round_s / 1e9 / HBM_PEAK_GBS,
-                               "avg_round_us": step_round_s * 1e6, "rounds": step_rounds,
-                               "note": "whole step (sparse rounds at the dense byte count, gaps included)"}
-            rl["sparse_rounds"] = {"avg_round_us": sparse_ms * 1e3 / max(sparse_n, 1), "rounds_timed": sparse_n}
-        else:
-            rl["kernel"] = ("sharded rounds, hipEvent-timed device work of the hot kernels per round (timer 0): "
-                            "dense = exchange round (count + emit, bin + serve + unpermute, apply; G >= 6) or the "
-                            "binned push / pull passes + serve + apply after the state all-gather (G < 6), "
-                            "sparse = rare index + sharded scan (DESIGN.md §5); collectives not included")
         if world == 1 and not args.no_dense_only:
             rl["dense_only"] = dense_only(n_total, seed, local)
+        if world == 1 and not args.no_secondary and n_total != NODES_SECONDARY:
+            out["secondary"] = secondary_run(local, max(args.steps, 5), max(args.warmup, 2))
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(n_total, seed)
         print(json.dumps(out), flush=True)
