@@ -399,7 +399,7 @@ __device__ __forceinline__ uint32_t ae_rec(uint32_t pl, uint32_t nl, uint32_t st
 template <bool K1>
 __global__ __launch_bounds__(kAeBinThreads, GOSSIP_AE_EMIT_WAVES) void ae_bin_emit_kernel(AeArgs a) {
   __shared__ uint32_t cur[kAeBinTiles];
-  __shared__ uint32_t st[kAeBinRec];
+  __shared__ __align__(16) uint32_t st[kAeBinRec];  // read back as uint4
   __shared__ uint32_t wsum[kAeBinThreads / 64];
   __shared__ uint32_t wpre[kAeBinThreads / 64 + 1];
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;

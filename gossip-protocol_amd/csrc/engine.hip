@@ -578,9 +578,13 @@ int step_planned(gossip_engine* e, uint32_t max_rounds, gossip_round_stats_t* st
   std::vector<uint64_t> want(kRing, 0);
   uint32_t launched = 0, done = 0;
   bool stop = false;
+  // the stall streaks are not idempotent: a round enqueued past convergence would
+  // advance them for a round the next step runs again, so stall engines run one
+  // round ahead only
+  const uint32_t ahead = e->stall_d ? 1u : e->ahead;
   if (e->timing) HIP_OK(e, hipEventRecord(e->ev[0][0], e->stream));
   while (done < max_rounds) {
-    while (!stop && launched < max_rounds && launched - done < e->ahead) {
+    while (!stop && launched < max_rounds && launched - done < ahead) {
       Est x = base;
       for (uint32_t i = done; i < launched; ++i) x = predict(e, x);
       uint32_t maj = 0;
@@ -1183,6 +1187,7 @@ int gossip_set_param(gossip_engine_t* e, const char* name, double v) {
     e->ae_force = (int)v;
   } else if (n == "ae_cap") {
     if (e->mode != GOSSIP_MODE_ANTIENTROPY) return e->fail(GOSSIP_ESTATE, "ae_cap needs ANTIENTROPY mode");
+    if (e->aex) return e->fail(GOSSIP_ENOTSUP, "ae_cap: sharded ANTIENTROPY engines keep no edge lists");
     if (v < 0 || v > 4e9) return e->fail(GOSSIP_EINVAL, "ae_cap must be in [0, 4e9] (0 = default)");
     if (int rc = set_dev(e)) return rc;
     HIP_OK(e, hipStreamSynchronize(e->stream));

@@ -207,8 +207,12 @@ func (s *server) handle(req envelope) error {
 }
 
 func main() {
-	page := flag.Uint("page-values", 1024, "rumor slots per engine page (<= 4096)")
+	page := flag.Uint("page-values", 1024, "rumor slots per engine page (1..4096)")
 	flag.Parse()
+	if *page < 1 || *page > 4096 { // the engine's rumor slots (gossip_create), as gossip_hip.Cluster
+		fmt.Fprintln(os.Stderr, "-page-values must be in [1, 4096]")
+		os.Exit(2)
+	}
 	s := &server{pageValues: uint32(*page), slotOf: map[int64]uint32{}, msgID: map[string]int64{},
 		out: bufio.NewWriter(os.Stdout)}
 	in := bufio.NewScanner(os.Stdin)

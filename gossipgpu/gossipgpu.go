@@ -429,45 +429,57 @@ func Peer(seed, nodes uint64, node, round, j uint32) uint32 {
 // PartialLen is the length of the stats partial vector that is all-reduced (SUM) each round.
 func (e *Engine) PartialLen() uint64 { return uint64(C.gossip_partial_len(e.h)) }
 
+// locked runs one cgo call under e.mu (one engine is not thread-safe, include/gossip.h).
+func (e *Engine) locked(f func() C.int) error {
+	e.mu.Lock()
+	defer e.mu.Unlock()
+	return e.call(f())
+}
+
 // ShardedPlan: -1 / -2 need totals / the global max vector first; 0 dense, 1 sparse, 2 anti-entropy.
+// total is nil or the all-reduced totals (PartialLen words; the max vector: Rumors words).
 func (e *Engine) ShardedPlan(total []uint64) (int32, error) {
-	var kind C.int32_t
-	if rc := C.gossip_sharded_plan(e.h, u64p(total), &kind); rc != 0 {
-		return 0, e.fail(rc)
+	if total != nil && uint64(len(total)) < e.PartialLen() {
+		return 0, fmt.Errorf("gossipgpu: ShardedPlan wants %d totals", e.PartialLen())
 	}
-	return int32(kind), nil
+	var kind C.int32_t
+	err := e.locked(func() C.int { return C.gossip_sharded_plan(e.h, u64p(total), &kind) })
+	return int32(kind), err
 }
 
 // LocalTotals are the owned nodes' totals (to all-reduce before planning).
 func (e *Engine) LocalTotals() ([]uint64, error) {
 	out := make([]uint64, e.PartialLen())
-	return out, e.call(C.gossip_local_totals(e.h, u64p(out)))
+	return out, e.locked(func() C.int { return C.gossip_local_totals(e.h, u64p(out)) })
 }
 
 // ExchangeBuffers returns the send slice and the gathered image of an all-gather (in place).
 func (e *Engine) ExchangeBuffers() (send, recv uintptr, bytes uint64, err error) {
 	var s, r unsafe.Pointer
 	var n C.uint64_t
-	if rc := C.gossip_exchange_buffers(e.h, &s, &r, &n); rc != 0 {
-		return 0, 0, 0, e.fail(rc)
-	}
-	return uintptr(s), uintptr(r), uint64(n), nil
+	err = e.locked(func() C.int { return C.gossip_exchange_buffers(e.h, &s, &r, &n) })
+	return uintptr(s), uintptr(r), uint64(n), err
 }
 
 // DensePrepare enqueues the own-slice part of a dense round while the all-gather runs.
-func (e *Engine) DensePrepare() error { return e.call(C.gossip_dense_prepare(e.h)) }
+func (e *Engine) DensePrepare() error {
+	return e.locked(func() C.int { return C.gossip_dense_prepare(e.h) })
+}
 
 // RoundCompute computes a dense round's S_{t+1} and returns its partial stats.
 func (e *Engine) RoundCompute() ([]uint64, error) {
 	out := make([]uint64, e.PartialLen())
-	return out, e.call(C.gossip_round_compute(e.h, u64p(out)))
+	return out, e.locked(func() C.int { return C.gossip_round_compute(e.h, u64p(out)) })
 }
 
-// RoundCommit takes the all-reduced totals and ends the round.
+// RoundCommit takes the all-reduced totals (PartialLen words) and ends the round.
 func (e *Engine) RoundCommit(total []uint64) (RoundStats, error) {
+	if uint64(len(total)) < e.PartialLen() {
+		return RoundStats{}, fmt.Errorf("gossipgpu: RoundCommit wants %d totals", e.PartialLen())
+	}
 	var st C.gossip_round_stats_t
-	if rc := C.gossip_round_commit(e.h, u64p(total), &st); rc != 0 {
-		return RoundStats{}, e.fail(rc)
+	if err := e.locked(func() C.int { return C.gossip_round_commit(e.h, u64p(total), &st) }); err != nil {
+		return RoundStats{}, err
 	}
 	return RoundStats{Round: uint32(st.round), Converged: st.converged != 0, FullNodes: uint64(st.full_nodes),
 		AliveNodes: uint64(st.alive_nodes), Messages: uint64(st.messages), StateHash: uint64(st.state_hash)}, nil
@@ -477,44 +489,39 @@ func (e *Engine) RoundCommit(total []uint64) (RoundStats, error) {
 func (e *Engine) SparseRare() (send uintptr, count uint64, err error) {
 	var s unsafe.Pointer
 	var n C.uint64_t
-	if rc := C.gossip_sparse_rare(e.h, &s, &n); rc != 0 {
-		return 0, 0, e.fail(rc)
-	}
-	return uintptr(s), uint64(n), nil
+	err = e.locked(func() C.int { return C.gossip_sparse_rare(e.h, &s, &n) })
+	return uintptr(s), uint64(n), err
 }
 
 // SparseRareRecv: room for G * stride rare items.
 func (e *Engine) SparseRareRecv(stride uint64) (uintptr, error) {
 	var r unsafe.Pointer
-	if rc := C.gossip_sparse_rare_recv(e.h, C.uint64_t(stride), &r); rc != 0 {
-		return 0, e.fail(rc)
-	}
-	return uintptr(r), nil
+	err := e.locked(func() C.int { return C.gossip_sparse_rare_recv(e.h, C.uint64_t(stride), &r) })
+	return uintptr(r), err
 }
 
-// SparseScan: the pushes for other shards, grouped by owner.
+// SparseScan: the pushes for other shards, grouped by owner (counts: every shard's rare count).
 func (e *Engine) SparseScan(counts []uint64) (send uintptr, sendCounts []uint64, err error) {
+	if len(counts) != int(e.cfg.ShardCount) {
+		return 0, nil, fmt.Errorf("gossipgpu: SparseScan wants %d counts", e.cfg.ShardCount)
+	}
 	var s unsafe.Pointer
 	sendCounts = make([]uint64, len(counts))
-	if rc := C.gossip_sparse_scan(e.h, u64p(counts), &s, u64p(sendCounts)); rc != 0 {
-		return 0, nil, e.fail(rc)
-	}
-	return uintptr(s), sendCounts, nil
+	err = e.locked(func() C.int { return C.gossip_sparse_scan(e.h, u64p(counts), &s, u64p(sendCounts)) })
+	return uintptr(s), sendCounts, err
 }
 
 // SparseMsgRecv: room for the incoming push items.
 func (e *Engine) SparseMsgRecv(items uint64) (uintptr, error) {
 	var r unsafe.Pointer
-	if rc := C.gossip_sparse_msg_recv(e.h, C.uint64_t(items), &r); rc != 0 {
-		return 0, e.fail(rc)
-	}
-	return uintptr(r), nil
+	err := e.locked(func() C.int { return C.gossip_sparse_msg_recv(e.h, C.uint64_t(items), &r) })
+	return uintptr(r), err
 }
 
 // SparseCommit ends a sparse round with the received pushes.
 func (e *Engine) SparseCommit(items uint64) ([]uint64, error) {
 	out := make([]uint64, e.PartialLen())
-	return out, e.call(C.gossip_sparse_commit(e.h, C.uint64_t(items), u64p(out)))
+	return out, e.locked(func() C.int { return C.gossip_sparse_commit(e.h, C.uint64_t(items), u64p(out)) })
 }
 
 // AEItemWords: uint32 words of a request (0) or reply (1) item of sharded ANTIENTROPY.
@@ -523,53 +530,50 @@ func (e *Engine) AEItemWords(which uint32) uint32 { return uint32(C.gossip_ae_it
 // AELocalTarget: the max over the owned rows (all-reduce it with MAX, then AESetTarget).
 func (e *Engine) AELocalTarget() ([]uint32, error) {
 	out := make([]uint32, e.cfg.Rumors)
-	return out, e.call(C.gossip_ae_local_target(e.h, u32p(out)))
+	return out, e.locked(func() C.int { return C.gossip_ae_local_target(e.h, u32p(out)) })
 }
 
-// AESetTarget installs the global max vector.
-func (e *Engine) AESetTarget(target []uint32) error { return e.call(C.gossip_ae_set_target(e.h, u32p(target))) }
+// AESetTarget installs the global max vector (Rumors words).
+func (e *Engine) AESetTarget(target []uint32) error {
+	if len(target) != int(e.cfg.Rumors) {
+		return fmt.Errorf("gossipgpu: AESetTarget wants %d components", e.cfg.Rumors)
+	}
+	return e.locked(func() C.int { return C.gossip_ae_set_target(e.h, u32p(target)) })
+}
 
 // AERequests: this round's request items grouped by owner.
 func (e *Engine) AERequests() (send uintptr, counts []uint64, err error) {
 	var s unsafe.Pointer
 	counts = make([]uint64, e.cfg.ShardCount)
-	if rc := C.gossip_ae_requests(e.h, &s, u64p(counts)); rc != 0 {
-		return 0, nil, e.fail(rc)
-	}
-	return uintptr(s), counts, nil
+	err = e.locked(func() C.int { return C.gossip_ae_requests(e.h, &s, u64p(counts)) })
+	return uintptr(s), counts, err
 }
 
 // AERequestRecv: room for the incoming requests.
 func (e *Engine) AERequestRecv(items uint64) (uintptr, error) {
 	var r unsafe.Pointer
-	if rc := C.gossip_ae_request_recv(e.h, C.uint64_t(items), &r); rc != 0 {
-		return 0, e.fail(rc)
-	}
-	return uintptr(r), nil
+	err := e.locked(func() C.int { return C.gossip_ae_request_recv(e.h, C.uint64_t(items), &r) })
+	return uintptr(r), err
 }
 
 // AEServe merges the received requests and returns the replies (received order).
 func (e *Engine) AEServe() (uintptr, error) {
 	var s unsafe.Pointer
-	if rc := C.gossip_ae_serve(e.h, &s); rc != 0 {
-		return 0, e.fail(rc)
-	}
-	return uintptr(s), nil
+	err := e.locked(func() C.int { return C.gossip_ae_serve(e.h, &s) })
+	return uintptr(s), err
 }
 
 // AEResponseRecv: room for the replies to the own requests (request order).
 func (e *Engine) AEResponseRecv() (uintptr, error) {
 	var r unsafe.Pointer
-	if rc := C.gossip_ae_response_recv(e.h, &r); rc != 0 {
-		return 0, e.fail(rc)
-	}
-	return uintptr(r), nil
+	err := e.locked(func() C.int { return C.gossip_ae_response_recv(e.h, &r) })
+	return uintptr(r), err
 }
 
 // AEFinish merges the replies and returns the round's partial stats.
 func (e *Engine) AEFinish() ([]uint64, error) {
 	out := make([]uint64, e.PartialLen())
-	return out, e.call(C.gossip_ae_finish(e.h, u64p(out)))
+	return out, e.locked(func() C.int { return C.gossip_ae_finish(e.h, u64p(out)) })
 }
 
 // XDClasses: with bytes > 0 this exchange round filters its edges by the peer's class: the
@@ -578,10 +582,8 @@ func (e *Engine) AEFinish() ([]uint64, error) {
 func (e *Engine) XDClasses() (send, image uintptr, bytes uint64, err error) {
 	var s, i unsafe.Pointer
 	var n C.uint64_t
-	if rc := C.gossip_xd_classes(e.h, &s, &i, &n); rc != 0 {
-		return 0, 0, 0, e.fail(rc)
-	}
-	return uintptr(s), uintptr(i), uint64(n), nil
+	err = e.locked(func() C.int { return C.gossip_xd_classes(e.h, &s, &i, &n) })
+	return uintptr(s), uintptr(i), uint64(n), err
 }
 
 // XDRequests: the items of an exchange dense round (plan kind 3) grouped by owner: ids (uint32,
@@ -589,43 +591,35 @@ func (e *Engine) XDClasses() (send, image uintptr, bytes uint64, err error) {
 func (e *Engine) XDRequests() (ids, vals uintptr, counts []uint64, err error) {
 	var i, v unsafe.Pointer
 	counts = make([]uint64, e.cfg.ShardCount)
-	if rc := C.gossip_xd_requests(e.h, &i, &v, u64p(counts)); rc != 0 {
-		return 0, 0, nil, e.fail(rc)
-	}
-	return uintptr(i), uintptr(v), counts, nil
+	err = e.locked(func() C.int { return C.gossip_xd_requests(e.h, &i, &v, u64p(counts)) })
+	return uintptr(i), uintptr(v), counts, err
 }
 
 // XDRequestRecv: room for the incoming items (ids and values).
 func (e *Engine) XDRequestRecv(items uint64) (ids, vals uintptr, err error) {
 	var i, v unsafe.Pointer
-	if rc := C.gossip_xd_request_recv(e.h, C.uint64_t(items), &i, &v); rc != 0 {
-		return 0, 0, e.fail(rc)
-	}
-	return uintptr(i), uintptr(v), nil
+	err = e.locked(func() C.int { return C.gossip_xd_request_recv(e.h, C.uint64_t(items), &i, &v) })
+	return uintptr(i), uintptr(v), err
 }
 
 // XDServe applies the received pushes and returns the pull replies (received order).
 func (e *Engine) XDServe() (uintptr, error) {
 	var s unsafe.Pointer
-	if rc := C.gossip_xd_serve(e.h, &s); rc != 0 {
-		return 0, e.fail(rc)
-	}
-	return uintptr(s), nil
+	err := e.locked(func() C.int { return C.gossip_xd_serve(e.h, &s) })
+	return uintptr(s), err
 }
 
 // XDResponseRecv: room for the replies to the own items (send order).
 func (e *Engine) XDResponseRecv() (uintptr, error) {
 	var r unsafe.Pointer
-	if rc := C.gossip_xd_response_recv(e.h, &r); rc != 0 {
-		return 0, e.fail(rc)
-	}
-	return uintptr(r), nil
+	err := e.locked(func() C.int { return C.gossip_xd_response_recv(e.h, &r) })
+	return uintptr(r), err
 }
 
 // XDFinish merges the replies and returns the round's partial stats.
 func (e *Engine) XDFinish() ([]uint64, error) {
 	out := make([]uint64, e.PartialLen())
-	return out, e.call(C.gossip_xd_finish(e.h, u64p(out)))
+	return out, e.locked(func() C.int { return C.gossip_xd_finish(e.h, u64p(out)) })
 }
 
 // CCSend: the own occupancy bitmaps of a class-coded dense round (plan kind 4; [nz][full], bitsBytes
@@ -633,20 +627,16 @@ func (e *Engine) XDFinish() ([]uint64, error) {
 func (e *Engine) CCSend() (bits uintptr, bitsBytes uint64, vals uintptr, count uint64, err error) {
 	var b, v unsafe.Pointer
 	var nb, n C.uint64_t
-	if rc := C.gossip_cc_send(e.h, &b, &nb, &v, &n); rc != 0 {
-		return 0, 0, 0, 0, e.fail(rc)
-	}
-	return uintptr(b), uint64(nb), uintptr(v), uint64(n), nil
+	err = e.locked(func() C.int { return C.gossip_cc_send(e.h, &b, &nb, &v, &n) })
+	return uintptr(b), uint64(nb), uintptr(v), uint64(n), err
 }
 
 // CCRecv: the gathered bitmap image (ShardCount slots of bitsBytes) and room for stride mixed
 // words from every shard.
 func (e *Engine) CCRecv(stride uint64) (bitsImage, vals uintptr, err error) {
 	var b, v unsafe.Pointer
-	if rc := C.gossip_cc_recv(e.h, C.uint64_t(stride), &b, &v); rc != 0 {
-		return 0, 0, e.fail(rc)
-	}
-	return uintptr(b), uintptr(v), nil
+	err = e.locked(func() C.int { return C.gossip_cc_recv(e.h, C.uint64_t(stride), &b, &v) })
+	return uintptr(b), uintptr(v), err
 }
 
 // CCExpand rebuilds the state image from the gathered bitmaps and mixed words (counts: every
@@ -655,5 +645,5 @@ func (e *Engine) CCExpand(counts []uint64) error {
 	if len(counts) != int(e.cfg.ShardCount) {
 		return fmt.Errorf("gossipgpu: CCExpand wants %d counts", e.cfg.ShardCount)
 	}
-	return e.call(C.gossip_cc_expand(e.h, u64p(counts)))
+	return e.locked(func() C.int { return C.gossip_cc_expand(e.h, u64p(counts)) })
 }
