@@ -224,7 +224,7 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
   constexpr uint32_t kMaxT = V >= 2 ? kSbMaxTiles : kMaxTilesD;
   constexpr uint32_t kMaxS = BIG ? 2 * kMaxSenders : kMaxSenders;
   __shared__ uint32_t cur[BIG ? kMaxT / 2 : kMaxT];
-  __shared__ uint32_t st_ids[BIG ? 2 * kRecPerRegion : kRecPerRegion];  // p_local | n_local << 14, by tile
+  __shared__ __align__(16) uint32_t st_ids[BIG ? 2 * kRecPerRegion : kRecPerRegion];  // p_local | n_local << 14, by tile (BIG: then the u64 sender values)
   __shared__ uint64_t sval[STAGE ? kMaxS : 1];  // S_t of each sender, once (not once per record)
   __shared__ uint32_t wsum[kEmitThreads / 64];
   __shared__ uint32_t wpre[kEmitThreads / 64 + 1];
@@ -426,6 +426,31 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
 
   uint32_t* gids = b.ids + (size_t)s * g.rp;
   uint64_t* gvals = b.vals + (size_t)s * g.rp;
+  if constexpr (BIG) {
+    // ids out first (kept in registers), then the region's sender values take the
+    // staging room and each record's value is read from LDS: the values are the
+    // ones in v[] (no second read of S), and no record gathers its sender's word
+    // from L2 / MALL (a 64-B fetch per 8-B value at 2^27 nodes: emit 158 B of
+    // fetch per node, profiles/r03_a/pmc_dense_2p27.json)
+    constexpr uint32_t kE = 2 * kRecPerRegion / kEmitThreads;
+    uint32_t idr[kE];
+#pragma unroll
+    for (uint32_t q = 0; q < kE; ++q) {
+      const uint32_t e = tid + q * kEmitThreads;
+      idr[q] = e < total ? st_ids[e] : 0u;
+      if (e < total) rec_st<1>(&gids[e], idr[q]);
+    }
+    __syncthreads();  // every staged id is in registers
+    uint64_t* sv = (uint64_t*)st_ids;  // 2 * kRecPerRegion u32 = kMaxS u64
+#pragma unroll
+    for (uint32_t q = 0; q < kQ; ++q) sv[tid + q * kEmitThreads] = v[q];
+    __syncthreads();
+#pragma unroll
+    for (uint32_t q = 0; q < kE; ++q) {
+      const uint32_t e = tid + q * kEmitThreads;
+      if (e < total) rec_st<1>(&gvals[e], sv[(idr[q] >> kTileDLog) & kIdNMask]);
+    }
+  } else
   for (uint32_t e = tid; e < total; e += kEmitThreads) {
     const uint32_t id = st_ids[e];
     // every value slot is stored (also where the flags say no push), so the

@@ -129,6 +129,7 @@ struct gossip_engine {
   double sparse_frac = 1.0 / 16;  // rare fraction at or below which a round runs sparse (sparse_frac_of)
   bool sparse_frac_set = false;   // set by gossip_set_param (else the sharded defaults apply)
   double filter_frac = 0.3;       // dense rounds filter edges by the peer's class above this empty / full fraction
+  bool filter_frac_set = false;   // else off past 2^25 nodes (filter_frac_of)
   double xd_filter_frac = 0.6;    // exchange rounds likewise (their probe hits a G-shard class image: G = 8 sweep)
   double alld_frac = 1.0 / 64;    // sparse rounds with k * rare >= alld_frac * N commit every group's D (bench sweep)
   // pipelined rounds (binned engines): the host picks each round's path from the
@@ -486,6 +487,15 @@ uint32_t dense_filter(const gossip_engine* e, const Est& x, double frac) {
   return (pull && empty > frac ? 1u : 0u) | (push && full > frac ? 2u : 0u);
 }
 
+// the one-shard dense filter's threshold: gossip_set_param's, else 0.3 while the occupancy
+// bitmaps (N/8 bytes each) fit an XCD's 4 MiB L2; past that every probe is a 64-B fetch from
+// the MALL or HBM and the probes cost more than the edges they drop (2^27 nodes: emit
+// 2.3 -> 6.3 ms, serve + apply -1.6 ms; profiles/r03_a/rounds.txt)
+double filter_frac_of(const gossip_engine* e) {
+  if (e->filter_frac_set) return e->filter_frac;
+  return e->N <= (1ull << 25) ? e->filter_frac : 2.0;
+}
+
 RoundSync ring_sync(gossip_engine* e, uint32_t slot) {
   RoundSync rs;
   rs.ring = e->ring_d + (size_t)slot * (part_len(e) + 1);
@@ -593,7 +603,7 @@ int step_planned(gossip_engine* e, uint32_t max_rounds, gossip_round_stats_t* st
       const uint32_t slot = launched % kRing;
       const RoundSync rs = ring_sync(e, slot);
       want[slot] = rs.seq;
-      if (int rc = launch_round_path(e, t0 + launched, sparse, maj, all_d, dense_filter(e, x, e->filter_frac), rs, (int)slot)) return rc;
+      if (int rc = launch_round_path(e, t0 + launched, sparse, maj, all_d, dense_filter(e, x, filter_frac_of(e)), rs, (int)slot)) return rc;
       ++launched;
     }
     if (done == launched) break;
@@ -731,7 +741,7 @@ int compute_round(gossip_engine* e, const uint64_t* gathered) {
     const Est x = est_of(e, tot.data());
     const bool sparse = choose_sparse(e, x, &maj, &all_d);
     if ((rc = timer_begin(e, 0))) return rc;
-    if ((rc = launch_round_path(e, e->t, sparse, maj, all_d, dense_filter(e, x, e->filter_frac), ring_sync(e, 0), -1))) return rc;
+    if ((rc = launch_round_path(e, e->t, sparse, maj, all_d, dense_filter(e, x, filter_frac_of(e)), ring_sync(e, 0), -1))) return rc;
     return timer_end(e, 0);  // stats are fused into the round kernels
   } else if (e->sbin) {  // sharded dense round: binned pipeline over the gathered image
     if ((rc = timer_begin(e, 0))) return rc;
@@ -1168,6 +1178,7 @@ int gossip_set_param(gossip_engine_t* e, const char* name, double v) {
     e->alld_frac = v;
   } else if (n == "filter_frac") {
     e->filter_frac = v;
+    e->filter_frac_set = true;
   } else if (n == "xd_filter_frac") {
     e->xd_filter_frac = v;
   } else if (n == "ahead") {
