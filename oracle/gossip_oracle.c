@@ -471,15 +471,33 @@ static inline int churned(int alive, uint32_t n, uint32_t t, const uint32_t key[
   return alive ? !(x[0] < fail) : (x[0] < rec);
 }
 
-/* Anti-entropy round: push-pull max-merge over alive-alive edges. */
+/* max-merge into a row word another thread may also be merging into (OpenMP rounds); max is
+ * commutative and idempotent, so the result does not depend on the order of the merges */
+static inline void max_merge_u32(uint32_t* p, uint32_t v, int shared) {
+  if (!shared) {
+    if (v > *p) *p = v;
+    return;
+  }
+  uint32_t cur = __atomic_load_n(p, __ATOMIC_RELAXED);
+  while (v > cur && !__atomic_compare_exchange_n(p, &cur, v, 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {
+  }
+}
+
+/* Anti-entropy round: push-pull max-merge over alive-alive edges (each
+ * exchange restates one request/reply of main.go:77-81).  threads > 1: the same round on
+ * OpenMP threads (reads are of V = S_t, merges into Vn are atomic maxima). */
 static int ae_round(oracle_sim_t* s, uint64_t* partial) {
   const uint64_t N = s->N;
   const uint32_t K = s->R, k = s->k, t = s->t;
   const uint32_t key[2] = {(uint32_t)s->cfg.seed, (uint32_t)(s->cfg.seed >> 32)};
   const uint32_t fail = s->cfg.churn_fail, rec = s->cfg.churn_recover;
+  const int nt = s->threads, shared = nt > 1;
+#pragma omp parallel for num_threads(nt) if (nt > 1) schedule(static)
   for (uint64_t n = 0; n < N; ++n) s->alive_n[n] = (uint8_t)churned(s->alive[n], (uint32_t)n, t, key, fail, rec);
-  memcpy(s->Vn, s->V, (size_t)N * K * 4);
+#pragma omp parallel for num_threads(nt) if (nt > 1) schedule(static)
+  for (uint64_t n = 0; n < N; ++n) memcpy(s->Vn + n * K, s->V + n * K, (size_t)K * 4);
   uint64_t msgs = 0;
+#pragma omp parallel for num_threads(nt) if (nt > 1) schedule(static) reduction(+ : msgs)
   for (uint64_t n = 0; n < N; ++n) {
     if (!s->alive_n[n]) continue;
     uint32_t x[4] = {0, 0, 0, 0};
@@ -493,25 +511,37 @@ static int ae_round(oracle_sim_t* s, uint64_t* partial) {
       ++msgs;
       for (uint32_t c = 0; c < K; ++c) {
         uint32_t a = s->V[n * K + c], b = s->V[(uint64_t)p * K + c];
-        if (b > s->Vn[n * K + c]) s->Vn[n * K + c] = b;                    /* pull */
-        if (a > s->Vn[(uint64_t)p * K + c]) s->Vn[(uint64_t)p * K + c] = a; /* push */
+        max_merge_u32(&s->Vn[n * K + c], b, shared);                /* pull */
+        max_merge_u32(&s->Vn[(uint64_t)p * K + c], a, shared);      /* push */
       }
     }
   }
   uint64_t full = 0, alive = 0, hash = 0;
   uint64_t* inf = partial + 4;
   memset(inf, 0, (size_t)K * 8);
-  for (uint64_t n = 0; n < N; ++n) {
-    int isfull = 1;
-    for (uint32_t c = 0; c < K; ++c) {
-      uint32_t v = s->Vn[n * K + c];
-      if (v && (s->cfg.flags & GOSSIP_FLAG_HASH)) hash += oracle_mix64((uint64_t)v + ((uint64_t)c * N + n) * GOLD64);
-      if (v != s->target[c]) isfull = 0;
-      else if (s->alive_n[n]) inf[c]++;
+#pragma omp parallel num_threads(nt) if (nt > 1)
+  {
+    uint64_t f = 0, a = 0, h = 0, cnt[64] = {0};
+#pragma omp for schedule(static)
+    for (uint64_t n = 0; n < N; ++n) {
+      int isfull = 1;
+      for (uint32_t c = 0; c < K; ++c) {
+        uint32_t v = s->Vn[n * K + c];
+        if (v && (s->cfg.flags & GOSSIP_FLAG_HASH)) h += oracle_mix64((uint64_t)v + ((uint64_t)c * N + n) * GOLD64);
+        if (v != s->target[c]) isfull = 0;
+        else if (s->alive_n[n]) cnt[c]++;
+      }
+      if (s->alive_n[n]) {
+        a++;
+        f += isfull;
+      }
     }
-    if (s->alive_n[n]) {
-      alive++;
-      full += isfull;
+#pragma omp critical
+    {
+      full += f;
+      alive += a;
+      hash += h;
+      for (uint32_t c = 0; c < K; ++c) inf[c] += cnt[c];
     }
   }
   partial[0] = full;

@@ -61,16 +61,45 @@ def test_ae_lockstep_equals_single_engine_and_oracle(case):
         e.close()
 
 
-def test_cfg5_64M_G8_lockstep_equals_single_engine():
-    """configs[4] at full size: 2^26 nodes, K = 16, fanout 1, churn 1 % / 10 %, as 8 shards of
-    2^23 rows against the one-GPU engine, to convergence."""
-    N, K, k, seed, fail, rec, G = 1 << 26, 16, 1, 0x5EED0005, 0.01, 0.1, 8
-    ref = Engine(N, K, "antientropy", k, seed, flags=1, churn_fail=ct(fail), churn_recover=ct(rec))
-    ref.inject_random()
-    want = ref.step(400)
-    rows = ref.read_rows()
-    ref.close()
-    assert want.converged
+CFG5 = (1 << 26, 16, 1, 0x5EED0005, 0.01, 0.1)  # configs[4]: N, K, fanout, seed, fail, recover
+
+
+@pytest.fixture(scope="module")
+def cfg5_oracle():
+    """configs[4] at full size on the OpenMP oracle (oracle/gossip_oracle.c ae_round, the restatement
+    of main.go:65-89 with each exchange one request/reply), to convergence: per-round stats (alive,
+    full, messages, hash), per-component counts and every row."""
+    N, K, k, seed, fail, rec = CFG5
+    o = op.OracleEngine(N, K, "antientropy", k, seed, flags=1, churn_fail=ct(fail), churn_recover=ct(rec),
+                        threads=THREADS)
+    o.inject_random()
+    res = o.step(400)
+    rows = o.read_rows()
+    o.close()
+    assert res.converged
+    return res, rows
+
+
+def test_cfg5_64M_single_engine_equals_oracle(cfg5_oracle):
+    """configs[4] at full size (2^26 nodes, K = 16, fanout 1, churn 1 % / 10 %) on one HIP engine
+    (dense rounds, then sparse rounds as planned) against the oracle."""
+    want, rows = cfg5_oracle
+    N, K, k, seed, fail, rec = CFG5
+    e = Engine(N, K, "antientropy", k, seed, flags=1, churn_fail=ct(fail), churn_recover=ct(rec))
+    e.inject_random()
+    got = e.step(400)
+    assert got.stats == want.stats
+    assert np.array_equal(got.infected, want.infected)
+    assert np.array_equal(e.read_rows(), rows)
+    e.close()
+
+
+def test_cfg5_64M_G8_lockstep_equals_oracle(cfg5_oracle):
+    """configs[4] at full size as 8 shards of 2^23 rows (the sharded ANTIENTROPY protocol, DESIGN.md
+    §5.3) against the oracle, to convergence."""
+    want, rows = cfg5_oracle
+    N, K, k, seed, fail, rec = CFG5
+    G = 8
     engines = [Engine(N, K, "antientropy", k, seed, flags=1, shard_rank=r, shard_count=G, churn_fail=ct(fail),
                       churn_recover=ct(rec)) for r in range(G)]
     for e in engines:

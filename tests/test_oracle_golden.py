@@ -66,11 +66,28 @@ def test_openmp_matches_scalar():
         assert np.array_equal(ra.infected, rb.infected)
 
 
+def test_openmp_antientropy_matches_scalar():
+    from gossip_hip.engine import churn_threshold as ct
+    runs = []
+    for threads in (1, 4):
+        o = op.OracleEngine(30011, 16, "antientropy", 2, 0x5EED0005, flags=1, churn_fail=ct(0.05),
+                            churn_recover=ct(0.2), threads=threads)
+        o.inject_random()
+        runs.append((o.step(300), o.read_rows()))
+        o.close()
+    (ra, rowa), (rb, rowb) = runs
+    assert ra.stats == rb.stats and np.array_equal(ra.infected, rb.infected)
+    assert np.array_equal(rowa, rowb)
+
+
+@pytest.mark.parametrize("threads", [1, 4])
 @pytest.mark.parametrize("idx", range(3))
-def test_antientropy_golden(golden, idx):
+def test_antientropy_golden(golden, idx, threads):
+    """The scalar ANTIENTROPY round and its OpenMP form (atomic max-merges, the checker of the
+    full-size configs[4] GPU tests) both reproduce the numpy goldens."""
     c = golden["antientropy"][idx]
     e = op.OracleEngine(c["N"], c["K"], "antientropy", c["k"], c["seed"], flags=1,
-                        churn_fail=c["fail"], churn_recover=c["recover"])
+                        churn_fail=c["fail"], churn_recover=c["recover"], threads=threads)
     e.inject_random()
     e.inject(c["N"] - 1, 0)
     res = e.step(300)
