@@ -141,8 +141,12 @@ class Sim:
     restates the expired-context stall —
       random modes: a node whose initiated exchanges were lost (any of them) in D rounds in
         a row stops initiating exchanges (it still answers pulls and receives pushes);
-      flood: a value is retried on a lost edge every round; with D > 0 it is dropped from
-        that edge after D failed attempts.
+      flood: one walk per (node, value) down the node's topology row in the topology
+        message's order (duplicates kept), one blocking SyncRPC at a time: a lost attempt
+        holds every later neighbour back until it is delivered (retried each round); after D
+        lost attempts on one neighbour (D > 0) its context has expired and the walk never
+        moves on — it keeps retrying that neighbour every round (each retry a message that
+        delivers when not lost), the later neighbours never get the value from this node.
     """
 
     def __init__(self, n_nodes, n_rumors, mode, fanout=0, seed=0, topology=None, edge_loss=0, partitions=0,
@@ -171,60 +175,60 @@ class Sim:
             self.edge_faults = bool(edge_loss or partitions > 1 or stall_rounds)
             E = len(self.src)
             self.row0 = np.concatenate([[0], np.cumsum(self.deg)]).astype(np.int64)
-            self.skipE = np.zeros((self.W, E), dtype=np.uint64)                 # first sender = target
-            self.pend = np.zeros((max(1, stall_rounds - 1), self.W, E), dtype=np.uint64)  # by attempts made
+            # flood with faults: the walks, rows in the message's order
+            self.rows = [[int(v) for v in topology[u]] for u in range(n_nodes)]
+            self.cur = np.zeros((n_nodes, n_rumors), dtype=np.int64)   # next position in the row
+            self.att = np.zeros((n_nodes, n_rumors), dtype=np.int64)   # lost attempts on that position
+            self.snd = np.full((n_nodes, n_rumors), -1, dtype=np.int64)  # first sender (-1: a client)
 
     def inject(self, node, rumor):
+        if self.adj is not None and self.edge_faults and not self._has(self.S, node, rumor):
+            self.cur[node, rumor], self.att[node, rumor], self.snd[node, rumor] = 0, 0, -1
         self.S[rumor // 64, node] |= np.uint64(1 << (rumor % 64))
+
+    @staticmethod
+    def _has(S, node, x):
+        return (int(S[x // 64, node]) >> (x % 64)) & 1 == 1
 
     def inject_random(self):
         for r, o in enumerate(origins(self.seed, self.N, self.R)):
             self.inject(int(o), r)
 
     def _flood_faults_round(self, S, Sn):
-        """FLOOD with per-edge retries: edge e = (u -> w), slot j of u."""
-        F = S & ~self.Sprev
-        E = len(self.src)
+        """FLOOD with faults (main.go:72-87): every walk of a value u held at the
+        start of the round goes down u's row from its cursor.  Position c of u's row is lost in
+        round t like a random-mode edge (partition, or Philox({u, t, 4, c >> 2})[c & 3] <
+        edge_loss); the first sender is skipped without a message (:73)."""
         D = self.D
         msgs = 0
-        nslots = self.pend.shape[0]
-        new_pend = np.zeros_like(self.pend)
-        new_skipE = np.zeros_like(self.skipE)
-        delivered = np.zeros((self.W, E), dtype=np.uint64)
-        for e in range(E):
-            u, w = int(self.src[e]), int(self.dst[e])
-            j = e - int(self.row0[u])
-            lost = bool(edge_lost(self.seed, self.N, self.loss, self.parts, [u], [w], self.t, j)[0])
-            for x in range(self.W):
-                fresh = F[x][u] & ~self.skipE[x][e]
-                att = fresh
-                for a in range(nslots):
-                    att |= self.pend[a][x][e]
-                msgs += popcount(att)
-                if not lost:
-                    delivered[x][e] = att
-                elif D == 0:
-                    new_pend[0][x][e] = att           # retried every round, forever
-                else:                                 # attempts made: fresh 1, slot a: a + 2
-                    if D >= 2:
-                        new_pend[0][x][e] = fresh
-                    for a in range(nslots - 1):
-                        new_pend[a + 1][x][e] = self.pend[a][x][e]
-        # receivers: OR of delivered attempts; first (lowest-id) sender of each new bit
-        for x in range(self.W):
-            for e in range(E):
-                Sn[x][self.dst[e]] |= delivered[x][e]
-            new = Sn[x] & ~S[x]
-            seen = np.zeros(self.N, dtype=np.uint64)
-            for e in np.lexsort((self.src, self.dst)):
-                u, w = int(self.src[e]), int(self.dst[e])
-                c = delivered[x][e] & new[w] & ~seen[w]
-                if c:
-                    seen[w] |= c
-                    if u in self.adj[w]:  # w will not send these back to u (main.go:73)
-                        back = int(self.row0[w]) + self.adj[w].index(u)
-                        new_skipE[x][back] |= c
-        self.pend, self.skipE = new_pend, new_skipE
+        first = {}  # (w, x) -> lowest u that delivered x to w (w did not hold x)
+        for u in range(self.N):
+            row = self.rows[u]
+            lost_at = {}
+            for x in range(self.R):
+                if not self._has(S, u, x):
+                    continue
+                c, a, s = int(self.cur[u, x]), int(self.att[u, x]), int(self.snd[u, x])
+                while c < len(row):
+                    w = row[c]
+                    if w == s:  # main.go:73
+                        c += 1
+                        continue
+                    msgs += 1
+                    if c not in lost_at:
+                        lost_at[c] = bool(edge_lost(self.seed, self.N, self.loss, self.parts, [u], [w], self.t, c)[0])
+                    if lost_at[c]:
+                        a += 1
+                        break
+                    if not self._has(S, w, x):
+                        first[(w, x)] = min(first.get((w, x), u), u)
+                        Sn[x // 64, w] |= np.uint64(1 << (x % 64))
+                    if D and a >= D:  # expired context: delivered, but the walk never moves on
+                        break
+                    c, a = c + 1, 0
+                self.cur[u, x], self.att[u, x] = c, a
+        for (w, x), u in first.items():  # walks of the values learned this round start next round
+            self.cur[w, x], self.att[w, x], self.snd[w, x] = 0, 0, u
         return msgs
 
     def round(self):

@@ -65,9 +65,17 @@ RANDOM_FAULT_CASES = [
     ("pushpull_k6_stall4", 1000, 7, "pushpull", 6, 3, "random", LOSS(0.25), 2, 4, 80),
 ]
 
-# FLOOD with faults: per-edge retries, dropped after stall_rounds attempts (§2.9):
+# FLOOD with faults: one walk per (node, value) down the node's row in the topology message's
+# order, head-of-line blocked by a lost attempt, stuck for good after stall_rounds lost attempts on
+# one neighbour (§2.9; main.go:72-87):
 # name, N, R, adjacency, injection, edge_loss, partitions, stall_rounds, max_rounds
 FLOOD_FAULT_CASES = [
+    # node 0's first neighbour sits across the partition: the walk never gets past it, so 1 and 2
+    # never hear from 0 (the same row in another order reaches them in round 0)
+    ("hol_partition_blocked", 6, 1, [[3, 1, 2], [0], [0], [4], [5], []], [(0, 0)], 0, 2, 0, 12),
+    ("hol_partition_blocked_stall1", 6, 1, [[3, 1, 2], [0], [0], [4], [5], []], [(0, 0)], 0, 2, 1, 12),
+    ("hol_partition_order", 6, 1, [[1, 2, 3], [0], [0], [4], [5], []], [(0, 0)], 0, 2, 1, 12),
+    ("grid25_loss30_stall1", 25, 3, adj(grid_topology(25), 25), [(0, 0), (24, 1), (12, 2)], LOSS(0.3), 0, 1, 80),
     ("grid25_loss30_retry", 25, 2, adj(grid_topology(25), 25), [(0, 0), (24, 1)], LOSS(0.3), 0, 0, 80),
     ("grid25_loss30_stall2", 25, 2, adj(grid_topology(25), 25), [(0, 0), (24, 1)], LOSS(0.3), 0, 2, 80),
     ("tree3_40_parts2_stall3", 40, 2, adj(tree_topology(40, 3), 40), [(0, 0), (39, 1)], LOSS(0.1), 2, 3, 60),

@@ -13,7 +13,7 @@ import pytest
 
 import oracle_py as op
 from gossip_hip import Engine
-from gossip_hip.engine import churn_threshold as ct
+from gossip_hip.engine import StepResult, churn_threshold as ct
 from gossip_hip.sharded import lockstep_run
 
 pytestmark = pytest.mark.gpu
@@ -65,7 +65,7 @@ CFG5 = (1 << 26, 16, 1, 0x5EED0005, 0.01, 0.1)  # configs[4]: N, K, fanout, seed
 
 
 @pytest.fixture(scope="module")
-def cfg5_oracle():
+def cfg5_oracle(request):
     """configs[4] at full size on the OpenMP oracle (oracle/gossip_oracle.c ae_round, the restatement
     of main.go:65-89 with each exchange one request/reply), to convergence: per-round stats (alive,
     full, messages, hash), per-component counts and every row."""
@@ -73,9 +73,19 @@ def cfg5_oracle():
     o = op.OracleEngine(N, K, "antientropy", k, seed, flags=1, churn_fail=ct(fail), churn_recover=ct(rec),
                         threads=THREADS)
     o.inject_random()
-    res = o.step(400)
+    capman = request.config.pluginmanager.getplugin("capturemanager")
+    stats, inf = [], []
+    while len(stats) < 400:  # in slices, with a progress line: the oracle takes minutes at this size
+        r = o.step(10)
+        stats += r.stats
+        inf.append(r.infected)
+        with capman.global_and_fixture_disabled():  # a progress line past pytest's capture
+            print(f"cfg5 oracle: {len(stats)} rounds", flush=True)
+        if r.converged:
+            break
     rows = o.read_rows()
     o.close()
+    res = StepResult(len(stats), stats, np.concatenate(inf))
     assert res.converged
     return res, rows
 
