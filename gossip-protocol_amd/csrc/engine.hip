@@ -74,10 +74,7 @@ struct gossip_engine {
   uint8_t* stall_d = nullptr;
   // FLOOD with faults, one shard: per out-edge pending values and first senders
   bool flood_edges = false;
-  uint32_t fe_np = 1;
-  uint64_t fe_E = 0;
-  uint64_t *fe_pend[2] = {nullptr, nullptr}, *fe_skip[2] = {nullptr, nullptr};
-  uint32_t* fe_ieo = nullptr;
+  FloodWalks fw{nullptr, nullptr, nullptr, 0u};  // FLOOD with faults: the walks
   // ANTIENTROPY: rows V[n*K + c], alive bytes, global max vector
   uint32_t *V = nullptr, *Vn = nullptr, *target = nullptr;
   uint64_t *alive = nullptr, *alive_n = nullptr;  // [chunks][2]: alive bits, stale bits (AeArgs::ab)
@@ -228,10 +225,10 @@ void free_all(gossip_engine* e) {
   }
   for (uint64_t* b : bufs)
     if (b) (void)hipFree(b);
-  uint32_t* tb[] = {e->orow, e->ocol, e->irow, e->icol, e->fe_ieo};
+  uint32_t* tb[] = {e->orow, e->ocol, e->irow, e->icol, e->fw.cur, e->fw.snd};
   for (uint32_t* b : tb)
     if (b) (void)hipFree(b);
-  void* fe[] = {e->stall_d, e->fe_pend[0], e->fe_pend[1], e->fe_skip[0], e->fe_skip[1]};
+  void* fe[] = {e->stall_d, e->fw.att};
   for (void* b : fe)
     if (b) (void)hipFree(b);
   if (e->bin_mem) (void)hipFree(e->bin_mem);
@@ -724,13 +721,12 @@ int compute_round(gossip_engine* e, const uint64_t* gathered) {
   int rc;
   if (e->mode == GOSSIP_MODE_FLOOD) {
     if ((rc = timer_begin(e, 0))) return rc;
-    if (e->flood_edges)
-      HIP_OK(e, launch_round_flood_faults(a, FloodEdges{e->fe_pend[0], e->fe_pend[1], e->fe_skip[0], e->fe_skip[1],
-                                                        e->fe_ieo, std::max<uint64_t>(e->fe_E, 1), e->fe_np,
-                                                        e->cfg.stall_rounds},
-                                          e->stream));
-    else
+    if (e->flood_edges) {  // S_{t+1} starts as S_t; the walks OR deliveries into it
+      HIP_OK(e, hipMemcpyAsync(e->Snext, e->S, bytes, hipMemcpyDeviceToDevice, e->stream));
+      HIP_OK(e, launch_round_flood_walks(a, e->fw, e->stream));
+    } else {
       HIP_OK(e, launch_round_flood(a, e->stream));
+    }
     if ((rc = timer_end(e, 0))) return rc;
   } else if (e->binned) {  // one round, path chosen from the exact totals of S_t
     if ((rc = prepare_planned(e))) return rc;
@@ -782,10 +778,6 @@ void rotate(gossip_engine* e) {
     e->Sprev = e->S;
     e->S = e->Snext;
     e->Snext = tmp;
-    if (e->flood_edges) {
-      std::swap(e->fe_pend[0], e->fe_pend[1]);
-      std::swap(e->fe_skip[0], e->fe_skip[1]);
-    }
   } else if (!e->binned) {  // binned rounds run in place
     e->cur ^= 1;
     bind_slices(e);
@@ -968,7 +960,7 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
   e->fa = Faults{cfg->edge_loss, cfg->partitions, cfg->n_nodes};
   e->timing = (cfg->flags & GOSSIP_FLAG_TIMING) != 0;
   e->flood_edges = e->mode == GOSSIP_MODE_FLOOD && faulty;
-  e->fe_np = cfg->stall_rounds > 1 ? cfg->stall_rounds - 1 : 1;
+  e->fw.D = cfg->stall_rounds;
 
   auto bail = [&](int rc) {
     g_create_error = e->err;
@@ -1002,6 +994,15 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
     }
     e->fa.stall = e->stall_d;
     e->fa.D = cfg->stall_rounds;
+  }
+  if (e->flood_edges) {  // one walk per (value, node); none running until a value is injected or learned
+    const size_t nw = (size_t)e->R * e->N;
+    if (hipMalloc((void**)&e->fw.cur, nw * 4) != hipSuccess || hipMalloc((void**)&e->fw.snd, nw * 4) != hipSuccess ||
+        hipMalloc((void**)&e->fw.att, nw) != hipSuccess || hipMemset(e->fw.cur, 0xFF, nw * 4) != hipSuccess ||
+        hipMemset(e->fw.snd, 0xFF, nw * 4) != hipSuccess || hipMemset(e->fw.att, 0, nw) != hipSuccess) {
+      e->err = "hipMalloc of the FLOOD walks failed";
+      return bail(GOSSIP_ENOMEM);
+    }
   }
   auto alloc_raw = [&](void** p, size_t bytes) {
     if (hipMalloc(p, bytes) != hipSuccess) {
@@ -1226,22 +1227,21 @@ int gossip_set_topology_csr(gossip_engine_t* e, const uint32_t* row_ptr, const u
   for (uint64_t u = 0; u < n; ++u) {
     const size_t b = ocol.size();
     ocol.insert(ocol.end(), col + row_ptr[u], col + row_ptr[u + 1]);
-    std::sort(ocol.begin() + b, ocol.end());
-    ocol.erase(std::unique(ocol.begin() + b, ocol.end()), ocol.end());
+    if (!e->flood_edges) {  // rows as sets; the walks of FLOOD with faults keep the message's list
+      std::sort(ocol.begin() + b, ocol.end());
+      ocol.erase(std::unique(ocol.begin() + b, ocol.end()), ocol.end());
+    }
     orow[u + 1] = (uint32_t)ocol.size();
   }
   std::vector<uint32_t> irow(n + 1, 0), icol(ocol.size());
   for (uint32_t v : ocol) irow[v + 1]++;
   for (uint64_t v = 0; v < n; ++v) irow[v + 1] += irow[v];
-  std::vector<uint32_t> fill(irow.begin(), irow.end() - 1), ieo(ocol.size());
+  std::vector<uint32_t> fill(irow.begin(), irow.end() - 1);
   for (uint64_t u = 0; u < n; ++u)
-    for (uint32_t q = orow[u]; q < orow[u + 1]; ++q) {
-      ieo[fill[ocol[q]]] = q;  // in-edge -> its out-edge id (FLOOD retry state)
-      icol[fill[ocol[q]]++] = (uint32_t)u;
-    }
+    for (uint32_t q = orow[u]; q < orow[u + 1]; ++q) icol[fill[ocol[q]]++] = (uint32_t)u;
   if (int rc = set_dev(e)) return rc;
   HIP_OK(e, hipStreamSynchronize(e->stream));
-  uint32_t** bufs[] = {&e->orow, &e->ocol, &e->irow, &e->icol, &e->fe_ieo};
+  uint32_t** bufs[] = {&e->orow, &e->ocol, &e->irow, &e->icol};
   for (uint32_t** b : bufs)
     if (*b) {
       HIP_OK(e, hipFree(*b));
@@ -1257,24 +1257,11 @@ int gossip_set_topology_csr(gossip_engine_t* e, const uint32_t* row_ptr, const u
     HIP_OK(e, hipMemcpy(e->ocol, ocol.data(), ocol.size() * 4, hipMemcpyHostToDevice));
     HIP_OK(e, hipMemcpy(e->icol, icol.data(), icol.size() * 4, hipMemcpyHostToDevice));
   }
-  if (e->flood_edges) {  // fresh per-edge state for the new topology: nothing pending, no first senders
-    for (uint64_t** b : {&e->fe_pend[0], &e->fe_pend[1], &e->fe_skip[0], &e->fe_skip[1]})
-      if (*b) {
-        HIP_OK(e, hipFree(*b));
-        *b = nullptr;
-      }
-    e->fe_E = ocol.size();
-    const size_t E1 = std::max<size_t>(ocol.size(), 1);
-    const size_t pb = (size_t)e->fe_np * e->W * E1 * 8, sb = (size_t)e->W * E1 * 8;
-    if (hipMalloc((void**)&e->fe_ieo, E1 * 4) != hipSuccess || hipMalloc((void**)&e->fe_pend[0], pb) != hipSuccess ||
-        hipMalloc((void**)&e->fe_pend[1], pb) != hipSuccess || hipMalloc((void**)&e->fe_skip[0], sb) != hipSuccess ||
-        hipMalloc((void**)&e->fe_skip[1], sb) != hipSuccess)
-      return e->fail(GOSSIP_ENOMEM, "FLOOD edge-state allocation failed");
-    for (int b = 0; b < 2; ++b) {
-      HIP_OK(e, hipMemset(e->fe_pend[b], 0, pb));
-      HIP_OK(e, hipMemset(e->fe_skip[b], 0, sb));
-    }
-    if (!ieo.empty()) HIP_OK(e, hipMemcpy(e->fe_ieo, ieo.data(), ieo.size() * 4, hipMemcpyHostToDevice));
+  if (e->flood_edges) {  // a new topology ends every walk: the values held are not sent again
+    const size_t nw = (size_t)e->R * e->N;
+    HIP_OK(e, hipMemset(e->fw.cur, 0xFF, nw * 4));
+    HIP_OK(e, hipMemset(e->fw.snd, 0xFF, nw * 4));
+    HIP_OK(e, hipMemset(e->fw.att, 0, nw));
   }
   e->has_topo = true;
   return GOSSIP_OK;
@@ -1309,11 +1296,11 @@ int gossip_reset(gossip_engine_t* e) {
     if (!e->binned) HIP_OK(e, hipMemsetAsync(e->Snext, 0, shard, e->stream));
   }
   if (e->stall_d) HIP_OK(e, hipMemsetAsync(e->stall_d, 0, e->N, e->stream));
-  if (e->flood_edges && e->fe_pend[0]) {
-    for (int b = 0; b < 2; ++b) {
-      HIP_OK(e, hipMemsetAsync(e->fe_pend[b], 0, (size_t)e->fe_np * e->W * std::max<uint64_t>(e->fe_E, 1) * 8, e->stream));
-      HIP_OK(e, hipMemsetAsync(e->fe_skip[b], 0, (size_t)e->W * std::max<uint64_t>(e->fe_E, 1) * 8, e->stream));
-    }
+  if (e->flood_edges) {
+    const size_t nw = (size_t)e->R * e->N;
+    HIP_OK(e, hipMemsetAsync(e->fw.cur, 0xFF, nw * 4, e->stream));
+    HIP_OK(e, hipMemsetAsync(e->fw.snd, 0xFF, nw * 4, e->stream));
+    HIP_OK(e, hipMemsetAsync(e->fw.att, 0, nw, e->stream));
   }
   e->fr_valid = false;
   e->sx_valid = e->gtot_valid = e->last_sparse = false;
@@ -1351,7 +1338,8 @@ int gossip_inject(gossip_engine_t* e, uint64_t node, uint32_t rumor) {
                                      e->cfg.flags, e->stream));
     return GOSSIP_OK;
   }
-  HIP_OK(e, launch_inject(e->S, e->Nl, e->lo, e->hi, e->N, e->R, e->key0, e->key1, (int64_t)node, rumor, e->stream));
+  HIP_OK(e, launch_inject(e->S, e->Nl, e->lo, e->hi, e->N, e->R, e->key0, e->key1, (int64_t)node, rumor, e->stream,
+                          e->flood_edges ? &e->fw : nullptr));
   e->fr_valid = e->sx_valid = e->gtot_valid = false;
   return GOSSIP_OK;
 }
@@ -1374,7 +1362,8 @@ int gossip_inject_random(gossip_engine_t* e) {
                                      e->stream));
     return GOSSIP_OK;
   }
-  HIP_OK(e, launch_inject(e->S, e->Nl, e->lo, e->hi, e->N, e->R, e->key0, e->key1, -1, 0, e->stream));
+  HIP_OK(e, launch_inject(e->S, e->Nl, e->lo, e->hi, e->N, e->R, e->key0, e->key1, -1, 0, e->stream,
+                          e->flood_edges ? &e->fw : nullptr));
   e->fr_valid = e->sx_valid = e->gtot_valid = false;
   return GOSSIP_OK;
 }

@@ -28,28 +28,27 @@ struct RoundArgs {
   const uint32_t *orow, *ocol, *irow, *icol;
 };
 
-// FLOOD with faults: per out-edge state of one shard (G == 1).
-// Edge e = CSR position in the sorted out-rows; ieo[q] = out-edge id of in-edge q.
-struct FloodEdges {
-  const uint64_t* pend;  // [np][W][E] values pending on e, by attempts made (np = max(1, D - 1))
-  uint64_t* pend_n;
-  const uint64_t* skipE;  // [W][E] values whose first sender at the edge's source was its target
-  uint64_t* skipE_n;
-  const uint32_t* ieo;
-  uint64_t E;
-  uint32_t np, D;
+// FLOOD with faults: one walk per (value x, node u) of one shard
+// (G == 1), index x * N + u, down u's row in the topology message's order.
+constexpr uint32_t kWalkNone = 0xFFFFFFFFu;  // snd: no first sender (a client's value); cur: no walk
+struct FloodWalks {
+  uint32_t* cur;  // next position in u's row
+  uint8_t* att;   // lost attempts on that position
+  uint32_t* snd;  // first sender of x at u
+  uint32_t D;     // lost attempts that expire a neighbour's context (0: never)
 };
 
 hipError_t launch_round_random(const RoundArgs& a, hipStream_t st);
-hipError_t launch_round_flood_faults(const RoundArgs& a, const FloodEdges& fe, hipStream_t st);
+hipError_t launch_round_flood_walks(const RoundArgs& a, const FloodWalks& fw, hipStream_t st);
 // Stall streaks after round t (random modes), all N nodes; fa.stall is the array.
 hipError_t launch_stall_update(uint8_t* stall, uint64_t N, uint32_t k, uint32_t t, uint32_t key0, uint32_t key1,
                                const Faults& fa, hipStream_t st);
 hipError_t launch_round_flood(const RoundArgs& a, hipStream_t st);
 hipError_t launch_stats(const RoundArgs& a, hipStream_t st);
 hipError_t launch_frontier(const uint64_t* S, const uint64_t* Sprev, uint64_t* F, uint64_t n, hipStream_t st);
+// fw (FLOOD with faults, or null): a value new at its node starts its walk next round
 hipError_t launch_inject(uint64_t* S, uint64_t Nl, uint64_t lo, uint64_t hi, uint64_t N, uint32_t R, uint32_t key0,
-                         uint32_t key1, int64_t node, uint32_t rumor, hipStream_t st);
+                         uint32_t key1, int64_t node, uint32_t rumor, hipStream_t st, const FloodWalks* fw = nullptr);
 hipError_t launch_hash(const uint64_t* S, uint64_t Nl, uint64_t nown, uint32_t W, uint64_t N, uint64_t lo,
                        uint64_t* out, hipStream_t st);
 hipError_t launch_philox(const uint32_t* ctr, uint32_t k0, uint32_t k1, uint32_t* out, uint32_t n, hipStream_t st);

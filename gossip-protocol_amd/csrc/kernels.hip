@@ -150,88 +150,71 @@ __global__ __launch_bounds__(kBlock) void round_flood_kernel(RoundArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// FLOOD with faults (main.go:72-87): edge e = (u -> w), slot j of
-// u's sorted row.  In round t u attempts on e the values it learned in t-1 minus
-// those whose first sender was w (:73), plus every value still pending on e; one
-// RPC per value per attempt.  Lost as a random-mode edge (partition, or the loss
-// draw Philox({u, t, 4, j>>2})[j&3]); a lost value is retried next round, forever
-// (D = 0) or until attempted D times (the expired 2 s context, :77-78).  One lane
-// per node: it keeps the books of its own out-edges (attempts, what stays pending)
-// and receives over its in-edges (first sender = lowest id u that delivered).
-// Reads: S, Sprev, pend, skipE (round t); writes: Snext[v], pend_n and skipE_n of
-// v's own out-edges — no two lanes write one word.
+// FLOOD with faults (main.go:72-87).  The reference forwards a
+// value from one goroutine that walks Topology[node] in order (:72), skips the
+// value's sender (:73) and blocks in SyncRPC on each neighbour until it is acked
+// (:80-87); the neighbour's 2 s context (:77) expires after D lost attempts.
+// One lane per (value x, node u) walk: from position c, the sender is skipped
+// (no message); any other neighbour w costs a message, lost as a random-mode
+// edge (partition, or Philox({u, t, 4, c >> 2})[c & 3] < edge_loss).  A lost
+// attempt ends the walk's round (the later neighbours wait); a delivered one
+// ORs x into S_{t+1}[w] (w's first sender: atomicMin over the lanes that
+// delivered x to w this round — snd stays kWalkNone while w lacks x) and moves
+// on, unless the context has expired: then the walk stays on w for good.
+// Reads S_t only; S_{t+1} starts as a copy of S_t.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ bool flood_edge_lost(const Faults& fa, uint32_t u, uint32_t w, uint32_t j, uint32_t t,
-                                                uint32_t k0, uint32_t k1) {
-  const uint32_t lw = fa.loss ? lane_of(loss_draws(u, t, j >> 2, k0, k1), j & 3u) : 0u;
-  return edge_lost(fa, reach_of(u, fa), w, lw);
-}
-
-__device__ __forceinline__ uint64_t flood_attempt(const RoundArgs& a, const FloodEdges& fe, uint32_t u, uint32_t x,
-                                                  uint64_t e, uint64_t* fresh) {
-  const uint64_t i = (uint64_t)x * a.Nl + u;
-  const uint64_t f = a.S[i] & ~a.Sprev[i] & ~fe.skipE[(uint64_t)x * fe.E + e];
-  uint64_t att = f;
-  for (uint32_t q = 0; q < fe.np; ++q) att |= fe.pend[((uint64_t)q * a.W + x) * fe.E + e];
-  *fresh = f;
-  return att;
-}
-
-__global__ __launch_bounds__(kBlock) void round_flood_faults_kernel(RoundArgs a, FloodEdges fe) {
+__global__ __launch_bounds__(kBlock) void round_flood_walks_kernel(RoundArgs a, FloodWalks fw) {
   uint64_t msgs = 0;
-  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-  for (uint64_t v64 = (uint64_t)blockIdx.x * kBlock + threadIdx.x; v64 < a.N; v64 += stride) {
-    const uint32_t v = (uint32_t)v64;
-    const uint32_t ob = a.orow[v], oe = a.orow[v + 1], deg = oe - ob;
-    // sender side: v's out-edges
-    for (uint32_t e = ob; e < oe; ++e) {
-      const bool lost = flood_edge_lost(a.fa, v, a.ocol[e], e - ob, a.t, a.key0, a.key1);
-      for (uint32_t x = 0; x < a.W; ++x) {
-        uint64_t fresh;
-        const uint64_t att = flood_attempt(a, fe, v, x, e, &fresh);
-        msgs += (uint64_t)__popcll(att);
-        for (uint32_t q = 0; q < fe.np; ++q) {  // what stays pending, by attempts made
-          uint64_t nv = 0;
-          if (lost) nv = fe.D == 0 ? (q == 0 ? att : 0ull)
-                                   : (q == 0 ? (fe.D >= 2 ? fresh : 0ull) : fe.pend[((uint64_t)(q - 1) * a.W + x) * fe.E + e]);
-          fe.pend_n[((uint64_t)q * a.W + x) * fe.E + e] = nv;
-        }
-        fe.skipE_n[(uint64_t)x * fe.E + e] = 0;
+  const uint64_t total = (uint64_t)a.R * a.N, stride = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < total; i += stride) {
+    const uint32_t x = (uint32_t)(i / a.N), u = (uint32_t)(i - (uint64_t)x * a.N);
+    const uint64_t bit = 1ull << (x & 63u);
+    const uint64_t* Sx = a.S + (uint64_t)(x >> 6) * a.Nl;
+    if (!(Sx[u] & bit)) continue;
+    const uint32_t b = a.orow[u], deg = a.orow[u + 1] - b;
+    uint32_t c = fw.cur[i];
+    if (c >= deg) continue;
+    uint32_t at = fw.att[i];
+    const uint32_t snd = fw.snd[i];
+    const Reach rc = reach_of(u, a.fa);
+    while (c < deg) {
+      const uint32_t w = a.ocol[b + c];
+      if (w == snd) {  // main.go:73
+        ++c;
+        continue;
       }
+      ++msgs;
+      const uint32_t lw = a.fa.loss ? lane_of(loss_draws(u, a.t, c >> 2, a.key0, a.key1), c & 3u) : 0u;
+      if (edge_lost(a.fa, rc, w, lw)) {
+        at = at < 255u ? at + 1u : at;
+        break;
+      }
+      if (!(Sx[w] & bit)) {
+        atomicOr((unsigned long long*)&a.Snext[(uint64_t)(x >> 6) * a.Nl + w], (unsigned long long)bit);
+        atomicMin(&fw.snd[(uint64_t)x * a.N + w], u);
+      }
+      if (fw.D && at >= fw.D) break;  // expired context: the walk never moves on
+      ++c;
+      at = 0;
     }
-    // receiver side: attempts delivered over v's in-edges
-    const uint32_t ib = a.irow[v], ie = a.irow[v + 1];
-    for (uint32_t x = 0; x < a.W; ++x) {
-      const uint64_t li = (uint64_t)x * a.Nl + v;
-      const uint64_t sv = a.S[li];
-      uint64_t acc = sv;
-      for (uint32_t q = ib; q < ie; ++q) {
-        const uint32_t u = a.icol[q], eo = fe.ieo[q];
-        if (flood_edge_lost(a.fa, u, v, eo - a.orow[u], a.t, a.key0, a.key1)) continue;
-        uint64_t fresh;
-        acc |= flood_attempt(a, fe, u, x, eo, &fresh);
-      }
-      const uint64_t nw = acc & ~sv;
-      uint64_t seen = 0;
-      for (uint32_t q = ib; q < ie && seen != nw; ++q) {
-        const uint32_t u = a.icol[q], eo = fe.ieo[q];
-        if (flood_edge_lost(a.fa, u, v, eo - a.orow[u], a.t, a.key0, a.key1)) continue;
-        uint64_t fresh;
-        const uint64_t c = flood_attempt(a, fe, u, x, eo, &fresh) & nw & ~seen;
-        if (!c) continue;
-        seen |= c;
-        uint32_t lo = 0, hi = deg;  // u in Adj(v)?  then v will not send these back to u (main.go:73)
-        while (lo < hi) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (a.ocol[ob + mid] < u) lo = mid + 1; else hi = mid;
-        }
-        if (lo < deg && a.ocol[ob + lo] == u) fe.skipE_n[(uint64_t)x * fe.E + ob + lo] |= c;
-      }
-      a.Snext[li] = acc;
-    }
+    fw.cur[i] = c;
+    fw.att[i] = (uint8_t)at;
   }
   msgs = wave_sum_u64(msgs);
   if ((threadIdx.x & 63) == 0 && msgs) atomicAdd((unsigned long long*)&a.partial[2], (unsigned long long)msgs);
+}
+
+// The values learned in round t start their walks in round t + 1 (their first sender is set).
+__global__ __launch_bounds__(kBlock) void flood_walks_learn_kernel(RoundArgs a, FloodWalks fw) {
+  const uint64_t total = (uint64_t)a.R * a.N, stride = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < total; i += stride) {
+    const uint32_t x = (uint32_t)(i / a.N), w = (uint32_t)(i - (uint64_t)x * a.N);
+    const uint64_t bit = 1ull << (x & 63u), wi = (uint64_t)(x >> 6) * a.Nl + w;
+    if ((a.Snext[wi] & bit) && !(a.S[wi] & bit)) {
+      fw.cur[i] = 0;
+      fw.att[i] = 0;
+    }
+  }
 }
 
 // Stall streaks after round t: a node not yet stalled counts the
@@ -329,13 +312,20 @@ __global__ __launch_bounds__(kBlock) void frontier_kernel(const uint64_t* __rest
 // Client broadcast (main.go:102-117): node >= 0 sets one bit; node < 0 injects
 // every rumor r < R at its Philox tag-2 origin.
 __global__ void inject_kernel(uint64_t* S, uint64_t Nl, uint64_t lo, uint64_t hi, uint64_t N, uint32_t R,
-                              uint32_t key0, uint32_t key1, int64_t node, uint32_t rumor) {
+                              uint32_t key0, uint32_t key1, int64_t node, uint32_t rumor, FloodWalks fw) {
   const uint32_t r = node >= 0 ? rumor : blockIdx.x * blockDim.x + threadIdx.x;
   if (node >= 0 && (blockIdx.x | threadIdx.x)) return;
   if (r >= R) return;
   const uint64_t n = node >= 0 ? (uint64_t)node : origin_of(r, N, key0, key1);
   if (n < lo || n >= hi) return;
-  atomicOr((unsigned long long*)&S[(uint64_t)(r >> 6) * Nl + (n - lo)], 1ull << (r & 63));
+  const uint64_t bit = 1ull << (r & 63);
+  const uint64_t old = atomicOr((unsigned long long*)&S[(uint64_t)(r >> 6) * Nl + (n - lo)], (unsigned long long)bit);
+  if (fw.cur && !(old & bit)) {  // a client's value (no sender): its walk starts next round
+    const uint64_t i = (uint64_t)r * N + n;
+    fw.cur[i] = 0;
+    fw.att[i] = 0;
+    fw.snd[i] = kWalkNone;
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void hash_kernel(const uint64_t* S, uint64_t Nl, uint64_t nown, uint32_t W,
@@ -389,8 +379,10 @@ hipError_t launch_round_flood(const RoundArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_round_flood_faults(const RoundArgs& a, const FloodEdges& fe, hipStream_t st) {
-  round_flood_faults_kernel<<<grid_for(a.N, 8192), kBlock, 0, st>>>(a, fe);
+hipError_t launch_round_flood_walks(const RoundArgs& a, const FloodWalks& fw, hipStream_t st) {
+  const uint64_t walks = (uint64_t)a.R * a.N;
+  round_flood_walks_kernel<<<grid_for(walks, 8192), kBlock, 0, st>>>(a, fw);
+  flood_walks_learn_kernel<<<grid_for(walks, 8192), kBlock, 0, st>>>(a, fw);
   return hipGetLastError();
 }
 
@@ -411,9 +403,10 @@ hipError_t launch_frontier(const uint64_t* S, const uint64_t* Sprev, uint64_t* F
 }
 
 hipError_t launch_inject(uint64_t* S, uint64_t Nl, uint64_t lo, uint64_t hi, uint64_t N, uint32_t R, uint32_t key0,
-                         uint32_t key1, int64_t node, uint32_t rumor, hipStream_t st) {
+                         uint32_t key1, int64_t node, uint32_t rumor, hipStream_t st, const FloodWalks* fw) {
   const uint32_t grid = node >= 0 ? 1 : (R + kBlock - 1) / kBlock;
-  inject_kernel<<<grid, kBlock, 0, st>>>(S, Nl, lo, hi, N, R, key0, key1, node, rumor);
+  inject_kernel<<<grid, kBlock, 0, st>>>(S, Nl, lo, hi, N, R, key0, key1, node, rumor,
+                                         fw ? *fw : FloodWalks{nullptr, nullptr, nullptr, 0u});
   return hipGetLastError();
 }
 

@@ -20,6 +20,7 @@
 #endif
 
 #define GOLD64 0x9E3779B97F4A7C15ull
+#define WALK_NONE 0xFFFFFFFFu /* FLOOD walks: no first sender (a client value) */
 
 struct oracle_sim {
   gossip_config_t cfg;
@@ -52,11 +53,12 @@ struct oracle_sim {
   uint64_t* counts;                        /* rare list lengths of the current round [G] */
   /* stall mode: random modes, lost-exchange streak per node (all N) */
   uint8_t* streak;
-  /* FLOOD with faults: per out-edge state, [slot][W][E] / [W][E]; ieo = out-edge id of in-edge */
+  /* FLOOD with faults: one walk per (value x, node u), index x * N + u: next
+   * position in u's row (rows keep the topology message's order), lost attempts there, first
+   * sender (WALK_NONE: a client) */
   int flood_edges;
-  uint32_t npend;
-  uint64_t *pend, *pend_n, *skipE, *skipE_n;
-  uint32_t* ieo;
+  uint32_t *wcur, *wsnd;
+  uint8_t* watt;
   /* sharded ANTIENTROPY (G > 1): V/Vn = own rows [Nl][K], alive bytes of all N,
    * aex_img = every shard's {alive, stale} word pairs per 64 nodes (the all-gather image: the
    * owner churns its nodes at exchange_buffers, aex_churned = that round), request / reply items */
@@ -252,7 +254,15 @@ int oracle_create(const gossip_config_t* cfg, int threads, oracle_sim_t** out) {
   s->cc_frac = 0.75;
   s->xd_filter_frac = 0.6; /* engine.hip xd_filter_frac */
   s->flood_edges = s->mode == GOSSIP_MODE_FLOOD && faulty;
-  s->npend = cfg->stall_rounds > 1 ? cfg->stall_rounds - 1 : 1;
+  if (s->flood_edges) {
+    const size_t nw = (size_t)s->R * s->N;
+    s->wcur = (uint32_t*)malloc(nw * 4);
+    s->wsnd = (uint32_t*)malloc(nw * 4);
+    s->watt = (uint8_t*)calloc(nw, 1);
+    if (!s->wcur || !s->wsnd || !s->watt) { oracle_destroy(s); return GOSSIP_ENOMEM; }
+    memset(s->wcur, 0xFF, nw * 4); /* WALK_DONE */
+    memset(s->wsnd, 0xFF, nw * 4); /* WALK_NONE */
+  }
   if (cfg->stall_rounds && s->mode >= GOSSIP_MODE_PUSH && s->mode <= GOSSIP_MODE_PUSHPULL &&
       !(s->streak = (uint8_t*)calloc(s->N, 1))) {
     oracle_destroy(s);
@@ -273,7 +283,7 @@ void oracle_destroy(oracle_sim_t* s) {
   free(s->V); free(s->Vn); free(s->target); free(s->alive); free(s->alive_n);
   free(s->gtot); free(s->counts); free(s->rare_send); free(s->rare_recv); free(s->msg_send); free(s->msg_recv);
   free(s->D);
-  free(s->streak); free(s->pend); free(s->pend_n); free(s->skipE); free(s->skipE_n); free(s->ieo);
+  free(s->streak); free(s->wcur); free(s->wsnd); free(s->watt);
   free(s->aex_img); free(s->req); free(s->loc); free(s->in); free(s->resp_out); free(s->resp_in);
   free(s->xid); free(s->xrid); free(s->xval); free(s->xrval); free(s->xrep_out); free(s->xrep_in); free(s->xnode);
   free(s->cc_bits); free(s->cc_send); free(s->cc_vals); free(s->xcls);
@@ -309,37 +319,34 @@ int oracle_set_topology_csr(oracle_sim_t* s, const uint32_t* row_ptr, const uint
     uint64_t b = row_ptr[u], e = row_ptr[u + 1];
     uint64_t start = E;
     memcpy(ocol + E, col + b, (e - b) * 4);
-    qsort(ocol + E, e - b, 4, cmp_u32);
-    uint64_t m = 0;
-    for (uint64_t i = 0; i < e - b; ++i)
-      if (m == 0 || ocol[start + m - 1] != ocol[start + i]) ocol[start + m++] = ocol[start + i];
+    uint64_t m = e - b;
+    if (!s->flood_edges) { /* rows as sets; the walks of FLOOD with faults keep the message's order */
+      qsort(ocol + E, e - b, 4, cmp_u32);
+      m = 0;
+      for (uint64_t i = 0; i < e - b; ++i)
+        if (m == 0 || ocol[start + m - 1] != ocol[start + i]) ocol[start + m++] = ocol[start + i];
+    }
     E += m;
     orow[u + 1] = (uint32_t)E;
   }
   for (uint64_t e = 0; e < E; ++e) irow[ocol[e] + 1]++;
   for (uint64_t v = 0; v < n; ++v) irow[v + 1] += irow[v];
   uint32_t* fill = (uint32_t*)malloc((n + 1) * 4);
-  uint32_t* ieo = (uint32_t*)malloc((n_edges ? n_edges : 1) * 4);
-  if (!fill || !ieo) {
-    free(orow); free(ocol); free(irow); free(icol); free(fill); free(ieo);
+  if (!fill) {
+    free(orow); free(ocol); free(irow); free(icol);
     return GOSSIP_ENOMEM;
   }
   memcpy(fill, irow, (n + 1) * 4);
   for (uint64_t u = 0; u < n; ++u) /* ascending u => each in-row sorted */
-    for (uint32_t e = orow[u]; e < orow[u + 1]; ++e) {
-      ieo[fill[ocol[e]]] = e;
-      icol[fill[ocol[e]]++] = (uint32_t)u;
-    }
+    for (uint32_t e = orow[u]; e < orow[u + 1]; ++e) icol[fill[ocol[e]]++] = (uint32_t)u;
   free(fill);
-  free(s->orow); free(s->ocol); free(s->irow); free(s->icol); free(s->ieo);
-  s->orow = orow; s->ocol = ocol; s->irow = irow; s->icol = icol; s->ieo = ieo;
+  free(s->orow); free(s->ocol); free(s->irow); free(s->icol);
+  s->orow = orow; s->ocol = ocol; s->irow = irow; s->icol = icol;
   s->E = E;
-  if (s->flood_edges) { /* fresh per-edge state: nothing pending, no first senders */
-    const size_t pe = (size_t)s->npend * s->W * (E ? E : 1), se = (size_t)s->W * (E ? E : 1);
-    free(s->pend); free(s->pend_n); free(s->skipE); free(s->skipE_n);
-    s->pend = (uint64_t*)calloc(pe, 8); s->pend_n = (uint64_t*)calloc(pe, 8);
-    s->skipE = (uint64_t*)calloc(se, 8); s->skipE_n = (uint64_t*)calloc(se, 8);
-    if (!s->pend || !s->pend_n || !s->skipE || !s->skipE_n) return GOSSIP_ENOMEM;
+  if (s->flood_edges) { /* a new topology ends every walk: held values are not sent again */
+    memset(s->wcur, 0xFF, (size_t)s->R * s->N * 4);
+    memset(s->wsnd, 0xFF, (size_t)s->R * s->N * 4);
+    memset(s->watt, 0, (size_t)s->R * s->N);
   }
   s->has_topo = 1;
   return GOSSIP_OK;
@@ -360,9 +367,10 @@ int oracle_reset(oracle_sim_t* s) {
     if (s->aex) aex_own_fill_alive(s);
   }
   if (s->streak) memset(s->streak, 0, s->N);
-  if (s->pend) {
-    memset(s->pend, 0, (size_t)s->npend * s->W * (s->E ? s->E : 1) * 8);
-    memset(s->skipE, 0, (size_t)s->W * (s->E ? s->E : 1) * 8);
+  if (s->flood_edges) {
+    memset(s->wcur, 0xFF, (size_t)s->R * s->N * 4);
+    memset(s->wsnd, 0xFF, (size_t)s->R * s->N * 4);
+    memset(s->watt, 0, (size_t)s->R * s->N);
   }
   s->t = 0;
   s->gtot_valid = s->planned = s->last_sparse = 0;
@@ -386,7 +394,14 @@ int oracle_inject(oracle_sim_t* s, uint64_t node, uint32_t rumor) {
   }
   s->gtot_valid = 0;
   if (node < s->lo || node >= s->hi) return GOSSIP_OK;
-  s->S[(size_t)(rumor >> 6) * s->Nl + (node - s->lo)] |= 1ull << (rumor & 63);
+  uint64_t* w = &s->S[(size_t)(rumor >> 6) * s->Nl + (node - s->lo)];
+  if (s->flood_edges && !(*w & (1ull << (rumor & 63)))) { /* a client's value: its walk starts next round */
+    const size_t i = (size_t)rumor * s->N + node;
+    s->wcur[i] = 0;
+    s->watt[i] = 0;
+    s->wsnd[i] = WALK_NONE;
+  }
+  *w |= 1ull << (rumor & 63);
   return GOSSIP_OK;
 }
 
@@ -552,82 +567,67 @@ static int ae_round(oracle_sim_t* s, uint64_t* partial) {
   return GOSSIP_OK;
 }
 
-/* FLOOD with faults (main.go:72-87).  Edge e = (u -> w), slot j of u's
- * sorted row.  In round t u attempts on e every value it learned in t-1 (minus those whose
- * first sender was w: main.go:73) plus every value still pending on e; each attempt is one
- * RPC.  The attempt is lost like a random-mode edge (partition, or Philox({u, t, 4, j>>2})
- * [j&3] < edge_loss); a lost value is retried next round — forever (stall_rounds 0), or
- * until it was attempted stall_rounds times (the expired 2 s context).  w's first sender
- * of a value is the lowest-id u whose attempt delivered it. */
+/* FLOOD with faults (main.go:72-87): the reference forwards a value from one
+ * goroutine that walks Topology[node] in order (:72), skipping the value's sender (:73), and
+ * blocks in SyncRPC on each neighbour until it is acked (:80-87); a neighbour's 2 s context
+ * (:77) expires after stall_rounds = D lost attempts (D = 0: never).  Round t, every walk of a
+ * value x held by u goes on from its position c: the sender is skipped (no message); any other
+ * neighbour w costs one message, which is lost like a random-mode edge (partition, or
+ * Philox({u, t, 4, c >> 2})[c & 3] < edge_loss; the same for every value at (u, c, t)).  A lost
+ * attempt ends the walk's round (head-of-line: the later neighbours wait); a delivered one gives
+ * w the value and moves on to c + 1 — unless the context has expired, when the walk stays on w
+ * for good (it keeps retrying, and w can still learn x from it).  w's first sender of x is the
+ * lowest u that delivered it in the round w learned it; w's walk of x starts the next round. */
 static int flood_lost(const oracle_sim_t* s, uint32_t u, uint32_t w, uint32_t j, const uint32_t key[2]) {
   return edge_lost(&s->cfg, s->N, u, w, s->t, j, key);
 }
 
+static int holds(const oracle_sim_t* s, const uint64_t* S, uint64_t n, uint32_t x) {
+  return (int)((S[(size_t)(x >> 6) * s->Nl + n] >> (x & 63)) & 1);
+}
+
 static uint64_t flood_faults_round(oracle_sim_t* s, uint64_t* Sn) {
-  const uint64_t N = s->N, E = s->E ? s->E : 1;
-  const uint32_t W = s->W, D = s->cfg.stall_rounds, np = s->npend;
+  const uint64_t N = s->N;
+  const uint32_t R = s->R, D = s->cfg.stall_rounds;
   const uint32_t key[2] = {(uint32_t)s->cfg.seed, (uint32_t)(s->cfg.seed >> 32)};
   uint64_t msgs = 0;
-  memset(s->pend_n, 0, (size_t)np * W * E * 8);
-  memset(s->skipE_n, 0, (size_t)W * E * 8);
-  /* sender side: every out-edge's attempt, messages, what stays pending */
-  for (uint64_t u = 0; u < N; ++u)
-    for (uint32_t e = s->orow[u]; e < s->orow[u + 1]; ++e) {
-      const int lost = flood_lost(s, (uint32_t)u, s->ocol[e], e - s->orow[u], key);
-      for (uint32_t x = 0; x < W; ++x) {
-        const size_t i = (size_t)x * N + u;
-        const uint64_t fresh = s->S[i] & ~s->Sprev[i] & ~s->skipE[(size_t)x * E + e];
-        uint64_t att = fresh;
-        for (uint32_t a = 0; a < np; ++a) att |= s->pend[((size_t)a * W + x) * E + e];
-        msgs += popc64(att);
-        if (!lost) continue;
-        if (D == 0) {
-          s->pend_n[(size_t)x * E + e] = att;
-        } else {
-          if (D >= 2) s->pend_n[(size_t)x * E + e] = fresh;
-          for (uint32_t a = 0; a + 1 < np; ++a)
-            s->pend_n[((size_t)(a + 1) * W + x) * E + e] = s->pend[((size_t)a * W + x) * E + e];
+  for (uint64_t u = 0; u < N; ++u) {
+    const uint32_t b = s->orow[u], deg = s->orow[u + 1] - b;
+    for (uint32_t x = 0; x < R; ++x) {
+      if (!holds(s, s->S, u, x)) continue;
+      const size_t i = (size_t)x * N + u;
+      uint32_t c = s->wcur[i], a = s->watt[i];
+      const uint32_t snd = s->wsnd[i];
+      while (c < deg) {
+        const uint32_t w = s->ocol[b + c];
+        if (w == snd) { /* main.go:73 */
+          ++c;
+          continue;
         }
-      }
-    }
-  /* receiver side: delivered attempts of the in-edges, ascending sender id */
-  for (uint64_t w = 0; w < N; ++w) {
-    const uint32_t ob = s->orow[w], deg = s->orow[w + 1] - ob;
-    for (uint32_t x = 0; x < W; ++x) {
-      const size_t i = (size_t)x * N + w;
-      uint64_t acc = s->S[i];
-      for (uint32_t q = s->irow[w]; q < s->irow[w + 1]; ++q) {
-        const uint32_t u = s->icol[q], eo = s->ieo[q];
-        if (flood_lost(s, u, (uint32_t)w, eo - s->orow[u], key)) continue;
-        const size_t iu = (size_t)x * N + u;
-        uint64_t att = s->S[iu] & ~s->Sprev[iu] & ~s->skipE[(size_t)x * E + eo];
-        for (uint32_t a = 0; a < np; ++a) att |= s->pend[((size_t)a * W + x) * E + eo];
-        acc |= att;
-      }
-      const uint64_t nw = acc & ~s->S[i];
-      uint64_t seen = 0;
-      for (uint32_t q = s->irow[w]; q < s->irow[w + 1] && seen != nw; ++q) {
-        const uint32_t u = s->icol[q], eo = s->ieo[q];
-        if (flood_lost(s, u, (uint32_t)w, eo - s->orow[u], key)) continue;
-        const size_t iu = (size_t)x * N + u;
-        uint64_t att = s->S[iu] & ~s->Sprev[iu] & ~s->skipE[(size_t)x * E + eo];
-        for (uint32_t a = 0; a < np; ++a) att |= s->pend[((size_t)a * W + x) * E + eo];
-        const uint64_t c = att & nw & ~seen;
-        if (!c) continue;
-        seen |= c;
-        uint32_t lo = 0, hi = deg; /* is u in Adj(w)?  then w skips it for these values */
-        while (lo < hi) {
-          const uint32_t mid = (lo + hi) / 2;
-          if (s->ocol[ob + mid] < u) lo = mid + 1; else hi = mid;
+        ++msgs;
+        if (flood_lost(s, (uint32_t)u, w, c, key)) {
+          if (a < 255) ++a;
+          break;
         }
-        if (lo < deg && s->ocol[ob + lo] == u) s->skipE_n[(size_t)x * E + ob + lo] |= c;
+        if (!holds(s, s->S, w, x)) {
+          Sn[(size_t)(x >> 6) * s->Nl + w] |= 1ull << (x & 63);
+          uint32_t* fs = &s->wsnd[(size_t)x * N + w]; /* WALK_NONE while w does not hold x */
+          if ((uint32_t)u < *fs) *fs = (uint32_t)u;
+        }
+        if (D && a >= D) break; /* expired context: the walk never moves on */
+        ++c;
+        a = 0;
       }
-      Sn[i] = acc;
+      s->wcur[i] = c;
+      s->watt[i] = (uint8_t)a;
     }
   }
-  uint64_t* t;
-  t = s->pend; s->pend = s->pend_n; s->pend_n = t;
-  t = s->skipE; s->skipE = s->skipE_n; s->skipE_n = t;
+  for (uint32_t x = 0; x < R; ++x) /* the values learned this round: their walks start next round */
+    for (uint64_t w = 0; w < N; ++w)
+      if (holds(s, Sn, w, x) && !holds(s, s->S, w, x)) {
+        s->wcur[(size_t)x * N + w] = 0;
+        s->watt[(size_t)x * N + w] = 0;
+      }
   return msgs;
 }
 

@@ -14,7 +14,9 @@
 //   FloodSim.Round  oracle_round_compute   FLOOD, the reference's own algorithm (main.go:65-89): every node forwards
 //                                          the values it learned last round to Topology[self] (:72) except their
 //                                          first sender (:73-75); dedupe :113; messages = RPCs sent
-//   FloodSim (faults) flood_faults_round   per-edge retries, dropped after StallRounds attempts (main.go:77-87)
+//   FloodSim (faults) flood_faults_round   one walk per (node, value) down Topology[node] in the message's order,
+//                                          head-of-line blocked by a lost attempt, stuck for good once StallRounds
+//                                          lost attempts expired the neighbour's context (main.go:72-87)
 //   AESim.Round     ae_round               gossip_oracle.c:355 (version-vector max-merge, Philox churn tag 1)
 //
 // Status in this image: no Go toolchain exists here or on the GPU box, so this
@@ -263,15 +265,15 @@ type FloodSim struct {
 	Loss     uint32 // faults (NewFloodSim with any of them on: per-edge retries, DESIGN.md §2.9)
 	Parts    uint32
 	Stall    uint32
-	adj      [][]uint32   // Topology[u] as a sorted set
-	row0     []uint64     // CSR start of u's out-edges
-	inSrc    [][]uint32   // in-neighbours of v, ascending
-	inEdge   [][]uint64   // their out-edge ids
-	S, Sprev [][]uint64   // [W][N]
-	skip     [][]uint64   // fault-free: values whose first sender is in Adj(v)
+	adj      [][]uint32 // Topology[u] as a sorted set
+	rows     [][]uint32 // Topology[u] as the message lists it (the walks, faults on)
+	row0     []uint64   // CSR start of u's out-edges
+	inSrc    [][]uint32 // in-neighbours of v, ascending
+	S, Sprev [][]uint64 // [W][N]
+	skip     [][]uint64 // fault-free: values whose first sender is in Adj(v)
 	faults   bool
-	pend     [][][]uint64 // [slot][W][E] values pending on an edge, by attempts made
-	skipE    [][]uint64   // [W][E] values whose first sender at the edge's source is its target
+	cur, snd [][]uint32 // faults: [R][N] walk position, first sender (walkNone: a client)
+	att      [][]uint8  // faults: [R][N] lost attempts at the walk's position
 	full     []uint64
 }
 
@@ -283,9 +285,10 @@ func NewFloodSim(N uint64, R uint32, adj [][]uint32, seed uint64, loss, parts, s
 	f.adj = make([][]uint32, N)
 	f.row0 = make([]uint64, N+1)
 	f.inSrc = make([][]uint32, N)
-	f.inEdge = make([][]uint64, N)
+	f.rows = make([][]uint32, N)
 	var E uint64
 	for u := uint64(0); u < N; u++ {
+		f.rows[u] = append([]uint32(nil), adj[u]...)
 		row := append([]uint32(nil), adj[u]...)
 		sort.Slice(row, func(a, b int) bool { return row[a] < row[b] })
 		var set []uint32
@@ -300,9 +303,8 @@ func NewFloodSim(N uint64, R uint32, adj [][]uint32, seed uint64, loss, parts, s
 	}
 	f.row0[N] = E
 	for u := uint64(0); u < N; u++ { // ascending u: every in-list sorted
-		for i, v := range f.adj[u] {
+		for _, v := range f.adj[u] {
 			f.inSrc[v] = append(f.inSrc[v], uint32(u))
-			f.inEdge[v] = append(f.inEdge[v], f.row0[u]+uint64(i))
 		}
 	}
 	f.S, f.Sprev, f.skip = make([][]uint64, W), make([][]uint64, W), make([][]uint64, W)
@@ -315,26 +317,27 @@ func NewFloodSim(N uint64, R uint32, adj [][]uint32, seed uint64, loss, parts, s
 			f.full[w] = (uint64(1) << b) - 1
 		}
 	}
-	slots := uint32(1)
-	if stall > 1 {
-		slots = stall - 1
-	}
-	f.pend = make([][][]uint64, slots)
-	for a := range f.pend {
-		f.pend[a] = make([][]uint64, W)
-		for w := range f.pend[a] {
-			f.pend[a][w] = make([]uint64, E)
+	f.cur, f.snd, f.att = make([][]uint32, R), make([][]uint32, R), make([][]uint8, R)
+	for x := uint32(0); x < R; x++ {
+		f.cur[x], f.snd[x], f.att[x] = make([]uint32, N), make([]uint32, N), make([]uint8, N)
+		for n := range f.snd[x] {
+			f.cur[x][n], f.snd[x][n] = walkNone, walkNone
 		}
-	}
-	f.skipE = make([][]uint64, W)
-	for w := range f.skipE {
-		f.skipE[w] = make([]uint64, E)
 	}
 	return f
 }
 
-// Inject is a client broadcast (main.go:102-117).
-func (f *FloodSim) Inject(n uint64, r uint32) { f.S[r/64][n] |= uint64(1) << (r % 64) }
+const walkNone = ^uint32(0)
+
+// Inject is a client broadcast (main.go:102-117); with faults a new value's walk starts next round.
+func (f *FloodSim) Inject(n uint64, r uint32) {
+	if f.faults && !holds(f.S, n, r) {
+		f.cur[r][n], f.att[r][n], f.snd[r][n] = 0, 0, walkNone
+	}
+	f.S[r/64][n] |= uint64(1) << (r % 64)
+}
+
+func holds(S [][]uint64, n uint64, x uint32) bool { return (S[x/64][n]>>(x%64))&1 == 1 }
 
 func contains(row []uint32, x uint32) (int, bool) {
 	i := sort.Search(len(row), func(i int) bool { return row[i] >= x })
@@ -343,16 +346,6 @@ func contains(row []uint32, x uint32) (int, bool) {
 
 func (f *FloodSim) lost(u, w uint32, j uint64) bool {
 	return EdgeLost(f.Seed, f.N, f.Loss, f.Parts, u, w, f.T, uint32(j))
-}
-
-// attempt: what edge e of u carries in this round (new values minus the skip, plus the pending ones)
-func (f *FloodSim) attempt(w uint32, u uint64, e uint64) (att, fresh uint64) {
-	fresh = f.S[w][u] &^ f.Sprev[w][u] &^ f.skipE[w][e]
-	att = fresh
-	for a := range f.pend {
-		att |= f.pend[a][w][e]
-	}
-	return att, fresh
 }
 
 // Round: one synchronous FLOOD round.
@@ -390,77 +383,50 @@ func (f *FloodSim) Round() RoundStats {
 			}
 		}
 	} else {
-		E := f.row0[N]
-		slots := len(f.pend)
-		pendN := make([][][]uint64, slots)
-		for a := range pendN {
-			pendN[a] = make([][]uint64, f.W)
-			for w := range pendN[a] {
-				pendN[a][w] = make([]uint64, E)
-			}
-		}
-		skipN := make([][]uint64, f.W)
-		for w := range skipN {
-			skipN[w] = make([]uint64, E)
-		}
-		for u := uint64(0); u < N; u++ { // sender side: attempts, messages, what stays pending
-			for i, v := range f.adj[u] {
-				e := f.row0[u] + uint64(i)
-				lost := f.lost(uint32(u), v, uint64(i))
-				for w := uint32(0); w < f.W; w++ {
-					att, fresh := f.attempt(w, u, e)
-					msgs += popcount(att)
-					if !lost {
+		// the walks (flood_faults_round): position c of u's row, the sender skipped (main.go:73), a
+		// lost attempt holds the later neighbours back, an expired context never moves on
+		for u := uint64(0); u < N; u++ {
+			row := f.rows[u]
+			for x := uint32(0); x < f.R; x++ {
+				if !holds(f.S, u, x) {
+					continue
+				}
+				c, a, snd := f.cur[x][u], uint32(f.att[x][u]), f.snd[x][u]
+				for c < uint32(len(row)) {
+					w := row[c]
+					if w == snd {
+						c++
 						continue
 					}
-					if f.Stall == 0 {
-						pendN[0][w][e] = att
-					} else {
-						if f.Stall >= 2 {
-							pendN[0][w][e] = fresh
+					msgs++
+					if f.lost(uint32(u), w, uint64(c)) {
+						if a < 255 {
+							a++
 						}
-						for a := 0; a+1 < slots; a++ {
-							pendN[a+1][w][e] = f.pend[a][w][e]
-						}
-					}
-				}
-			}
-		}
-		for v := uint64(0); v < N; v++ { // receiver side: delivered attempts, ascending sender id
-			for w := uint32(0); w < f.W; w++ {
-				acc := f.S[w][v]
-				for q, u := range f.inSrc[v] {
-					e := f.inEdge[v][q]
-					if f.lost(u, uint32(v), e-f.row0[u]) {
-						continue
-					}
-					att, _ := f.attempt(w, uint64(u), e)
-					acc |= att
-				}
-				nw := acc &^ f.S[w][v]
-				var seen uint64
-				for q, u := range f.inSrc[v] {
-					if seen == nw {
 						break
 					}
-					e := f.inEdge[v][q]
-					if f.lost(u, uint32(v), e-f.row0[u]) {
-						continue
+					if !holds(f.S, uint64(w), x) {
+						next[x/64][w] |= uint64(1) << (x % 64)
+						if uint32(u) < f.snd[x][w] {
+							f.snd[x][w] = uint32(u)
+						}
 					}
-					att, _ := f.attempt(w, uint64(u), e)
-					c := att & nw &^ seen
-					if c == 0 {
-						continue
+					if f.Stall != 0 && a >= f.Stall {
+						break
 					}
-					seen |= c
-					if i, in := contains(f.adj[v], u); in { // v will not send these back to u
-						skipN[w][f.row0[v]+uint64(i)] |= c
-					}
+					c++
+					a = 0
 				}
-				next[w][v] = acc
+				f.cur[x][u], f.att[x][u] = c, uint8(a)
 			}
 		}
-		f.pend, f.skipE = pendN, skipN
+		for x := uint32(0); x < f.R; x++ { // values learned this round: walks start next round
+			for w := uint64(0); w < N; w++ {
+				if holds(next, w, x) && !holds(f.S, w, x) {
+					f.cur[x][w], f.att[x][w] = 0, 0
+				}
+			}
+		}
 	}
 	f.Sprev, f.S = f.S, next
 	st := RoundStats{Round: f.T, Alive: N, Messages: msgs, Infected: make([]uint64, f.R)}

@@ -118,9 +118,12 @@ def test_flood_faults_golden_gpu(golden, idx):
 
 @pytest.mark.parametrize("idx", range(7))
 def test_flood_edge_kernel_without_losses_equals_flood_gpu(golden, idx):
-    """The per-edge FLOOD kernel with nothing lost reproduces the fault-free goldens."""
+    """The FLOOD walk kernel with nothing lost reproduces the fault-free goldens (rows without
+    repeated entries: the walks send to each entry, plain FLOOD reads rows as sets)."""
     from conftest import inject_case
     c = golden["flood"][idx]
+    if any(len(set(r)) != len(r) for r in c["adj"]):
+        pytest.skip("repeated row entries: the walks send to each entry")
     e = Engine(c["N"], c["R"], "flood", 0, 0, flags=1, stall_rounds=1)
     e.set_topology(c["adj"])
     inject_case(e, c["inject"])

@@ -136,9 +136,12 @@ def test_flood_faults_golden(golden, idx):
 
 @pytest.mark.parametrize("idx", range(7))
 def test_flood_edge_state_without_faults_equals_flood(golden, idx):
-    """The per-edge retry formulation with faults switched off after create reduces to plain FLOOD
-    (same messages and states as the fault-free goldens)."""
+    """The walk formulation with nothing lost reduces to plain FLOOD (same messages and states as the
+    fault-free goldens) — on rows without repeated entries: the walks keep the topology message's list
+    as it is (a repeated neighbour is sent to twice, main.go:72), plain FLOOD reads rows as sets."""
     c = golden["flood"][idx]
+    if any(len(set(r)) != len(r) for r in c["adj"]):
+        pytest.skip("repeated row entries: the walks send to each entry")
     e = op.OracleEngine(c["N"], c["R"], "flood", 0, flags=1, stall_rounds=1)  # per-edge state, nothing lost
     e.set_topology(c["adj"])
     inject_case(e, c["inject"])

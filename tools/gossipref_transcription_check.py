@@ -119,27 +119,27 @@ def flood_case(c):  # gossipref.FloodSim
         row0.append(E)
         E += len(adj[u])
     row0.append(E)
-    in_src, in_edge = [[] for _ in range(N)], [[] for _ in range(N)]
+    in_src = [[] for _ in range(N)]
     for u in range(N):
-        for i, v in enumerate(adj[u]):
+        for v in adj[u]:
             in_src[v].append(u)
-            in_edge[v].append(row0[u] + i)
+    rows = [list(r) for r in A]  # faults: Topology[u] as the message lists it
     S = [[0] * N for _ in range(W)]
     Sp = [[0] * N for _ in range(W)]
     skip = [[0] * N for _ in range(W)]
     full = [(M64 if R - 64 * w >= 64 else (1 << (R - 64 * w)) - 1) for w in range(W)]
-    slots = stall - 1 if stall > 1 else 1
-    pend = [[[0] * E for _ in range(W)] for _ in range(slots)]
-    skipE = [[0] * E for _ in range(W)]
-    for n, r in c["inject"]:
-        S[r // 64][n] |= 1 << (r % 64)
+    NONE = 0xFFFFFFFF
+    cur = [[NONE] * N for _ in range(R)]
+    snd = [[NONE] * N for _ in range(R)]
+    att = [[0] * N for _ in range(R)]
 
-    def attempt(w, u, e):
-        fresh = S[w][u] & ~Sp[w][u] & ~skipE[w][e] & M64
-        att = fresh
-        for a in range(slots):
-            att |= pend[a][w][e]
-        return att, fresh
+    def holds(X, n, x):
+        return (X[x // 64][n] >> (x % 64)) & 1 == 1
+
+    for n, r in c["inject"]:  # FloodSim.Inject
+        if faults and not holds(S, n, r):
+            cur[r][n], att[r][n], snd[r][n] = 0, 0, NONE
+        S[r // 64][n] |= 1 << (r % 64)
 
     out = []
     for t in range(max_rounds):
@@ -166,48 +166,32 @@ def flood_case(c):  # gossipref.FloodSim
                     nx[w][v] = acc
                     skip[w][v] = sk
         else:
-            pn = [[[0] * E for _ in range(W)] for _ in range(slots)]
-            sn = [[0] * E for _ in range(W)]
             for u in range(N):
-                for i, v in enumerate(adj[u]):
-                    e = row0[u] + i
-                    lost = edge_lost(seed, N, loss, parts, u, v, t, i)
-                    for w in range(W):
-                        att, fresh = attempt(w, u, e)
-                        msgs += pc(att)
-                        if not lost:
+                row = rows[u]
+                for x in range(R):
+                    if not holds(S, u, x):
+                        continue
+                    cc, a, sd = cur[x][u], att[x][u], snd[x][u]
+                    while cc < len(row):
+                        w = row[cc]
+                        if w == sd:
+                            cc += 1
                             continue
-                        if stall == 0:
-                            pn[0][w][e] = att
-                        else:
-                            if stall >= 2:
-                                pn[0][w][e] = fresh
-                            for a in range(slots - 1):
-                                pn[a + 1][w][e] = pend[a][w][e]
-            for v in range(N):
-                for w in range(W):
-                    acc = S[w][v]
-                    for q, u in enumerate(in_src[v]):
-                        e = in_edge[v][q]
-                        if edge_lost(seed, N, loss, parts, u, v, t, e - row0[u]):
-                            continue
-                        acc |= attempt(w, u, e)[0]
-                    nw = acc & ~S[w][v] & M64
-                    seen = 0
-                    for q, u in enumerate(in_src[v]):
-                        if seen == nw:
+                        msgs += 1
+                        if edge_lost(seed, N, loss, parts, u, w, t, cc):
+                            a = min(a + 1, 255)
                             break
-                        e = in_edge[v][q]
-                        if edge_lost(seed, N, loss, parts, u, v, t, e - row0[u]):
-                            continue
-                        cc = attempt(w, u, e)[0] & nw & ~seen & M64
-                        if not cc:
-                            continue
-                        seen |= cc
-                        if u in adj[v]:
-                            sn[w][row0[v] + adj[v].index(u)] |= cc
-                    nx[w][v] = acc
-            pend, skipE = pn, sn
+                        if not holds(S, w, x):
+                            nx[x // 64][w] |= 1 << (x % 64)
+                            snd[x][w] = min(snd[x][w], u)
+                        if stall and a >= stall:
+                            break
+                        cc, a = cc + 1, 0
+                    cur[x][u], att[x][u] = cc, a
+            for x in range(R):
+                for w in range(N):
+                    if holds(nx, w, x) and not holds(S, w, x):
+                        cur[x][w], att[x][w] = 0, 0
         Sp, S = S, nx
         h = fc = 0
         inf = [0] * R
