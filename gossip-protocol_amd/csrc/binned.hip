@@ -1329,7 +1329,7 @@ __global__ __launch_bounds__(kTileThreads) void xd_apply_kernel(XdGeom g, XdBufs
   const uint32_t tid = threadIdx.x, G = g.G;
   const uint32_t nv = g.r.nt_d;
   const uint32_t per = kTileD >> g.s.ts_log;
-  const uint32_t wave = tid >> 6;
+  const uint32_t wave = tid >> 6, nwav = kTileThreads / 64;
   const bool split = kApplySplit && mode == 3;
   const bool do_push = (mode == 1 || mode == 3) && (!split || wave < nwav / 2);
   const bool do_pull = (mode == 2 || mode == 3) && (!split || wave >= nwav / 2);
