@@ -53,6 +53,7 @@ struct BinGeom {
   uint32_t rp;           // records per sender region = ts * k
   uint32_t nt_s, nt_d;   // sender tiles, destination tiles
   uint32_t apply_grid;   // host only: persistent apply blocks (0 = one per tile; gossip_set_param)
+  uint32_t push_waves;   // push-pull apply: waves [0, push_waves) walk the pushes, the rest the responses
 };
 
 // big: regions of up to 2 * kMaxSenders senders and 2 * kRecPerRegion records (one shard

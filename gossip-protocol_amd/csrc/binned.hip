@@ -56,8 +56,13 @@ constexpr int kUnroll = GOSSIP_APPLY_UNROLL;  // records in flight per lane in t
 #endif
 constexpr int kUnrollServe = GOSSIP_SERVE_UNROLL;
 constexpr int kUnrollSeq = GOSSIP_SEQ_UNROLL;  // records in flight per lane in the sequential response walker
-// push-pull apply: waves [0, kPushWaves) walk the pushes, the rest the responses
+// push-pull apply: waves [0, push_waves) walk the pushes, the rest the responses
+// (BinGeom::push_waves, this default up to 2^25 nodes)
 constexpr uint32_t kPushWaves = GOSSIP_APPLY_PUSH_WAVES;
+// past 2^25 nodes the pushes come in short runs (~4 records at 2^27) and their walk
+// sets the pace: 12 of the 16 waves (2^27 apply 2930 -> 2710 us, 10: 2745;
+// profiles/r03_var27); 10 at 2^24 was slower (549 vs 542 us, round 2)
+constexpr uint32_t kPushWavesBig = 12;
 #ifndef GOSSIP_APPLY_SPLIT
 #define GOSSIP_APPLY_SPLIT 1
 #endif
@@ -800,11 +805,12 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
   __syncthreads();
   const uint32_t wave = tid >> 6;
   const bool split = kApplySplit && mode == 3;
-  const bool do_push = (mode == 1 || mode == 3) && (!split || wave < kPushWaves);
-  const bool do_pull = (mode == 2 || mode == 3) && (!split || wave >= kPushWaves);
-  // split: waves [0, kPushWaves) walk the pushes, the others the responses
-  const uint32_t qt0 = split ? kPushWaves * 64 : 0u, qnt = split ? kTileThreads - kPushWaves * 64 : kTileThreads;
-  if (do_push) push_walk<kIdVZ>(g, b, X, acc, wmask, wlist, split ? kPushWaves : 0u);  // pushes aimed at this tile
+  const uint32_t pw = g.push_waves;
+  const bool do_push = (mode == 1 || mode == 3) && (!split || wave < pw);
+  const bool do_pull = (mode == 2 || mode == 3) && (!split || wave >= pw);
+  // split: waves [0, pw) walk the pushes, the others the responses
+  const uint32_t qt0 = split ? pw * 64 : 0u, qnt = split ? kTileThreads - pw * 64 : kTileThreads;
+  if (do_push) push_walk<kIdVZ>(g, b, X, acc, wmask, wlist, split ? pw : 0u);  // pushes aimed at this tile
   if (do_pull) {  // responses owed to this tile's own senders
     const uint32_t* __restrict__ qids = bq.ids;
     const uint64_t* __restrict__ gresp = bq.resp;
@@ -866,6 +872,7 @@ BinGeom make_bin_geom(uint64_t N, uint32_t k, bool big) {
   g.nt_s = (uint32_t)((N + ts - 1) / ts);
   g.nt_d = (uint32_t)((N + kTileD - 1) / kTileD);
   g.apply_grid = kApplyGrid;
+  g.push_waves = N > (1ull << 25) ? kPushWavesBig : kPushWaves;
   return g;
 }
 

@@ -1188,6 +1188,9 @@ int gossip_set_param(gossip_engine_t* e, const char* name, double v) {
   } else if (n == "apply_grid") {
     if (v < 0 || v > 65536) return e->fail(GOSSIP_EINVAL, "apply_grid must be in [0, 65536]");
     e->bg.apply_grid = e->sbg.p.apply_grid = (uint32_t)v;
+  } else if (n == "push_waves") {
+    if (v < 1 || v > 15) return e->fail(GOSSIP_EINVAL, "push_waves must be in [1, 15]");
+    e->bg.push_waves = e->sbg.p.push_waves = e->sbg.q.push_waves = (uint32_t)v;
   } else if (n == "cc_frac") {
     if (v < 0 || v > 1) return e->fail(GOSSIP_EINVAL, "cc_frac must be in [0, 1] (0 = never)");
     e->cc_frac = v;

@@ -133,9 +133,11 @@ int gossip_set_stream(gossip_engine_t* eng, void* hip_stream);
  *                  rounds are exchange rounds; < 0 never, >= 1 always)
  *   "alld_frac"    sparse rounds commit every group's D once k x rare >= this x N
  *   "filter_frac"  dense rounds drop edges by the peer's class above this empty/full fraction
+ *                  (default 0.3 up to 2^25 nodes; past that off: the probes miss the L2)
  *   "xd_filter_frac"  exchange dense rounds likewise (default 0.6; >= 1 never)
  *   "ahead"        rounds enqueued ahead of the stats read back (1..7, default 2)
  *   "apply_grid"   persistent blocks of the dense apply pass (0 = one block per tile)
+ *   "push_waves"   waves of the dense apply pass walking the pushes (of 16; the rest walk the replies)
  *   "ae_sparse"    ANTIENTROPY: -1 plan sparse rounds (default), 0 never, 1 whenever valid
  *   "ae_cap"       ANTIENTROPY: edge-list capacity of sparse rounds (reallocates the list)
  *   "xd_shards"    sharded random modes: dense rounds run as exchange rounds (kind 3) when
@@ -147,7 +149,9 @@ int gossip_set_stream(gossip_engine_t* eng, void* hip_stream);
 int gossip_set_param(gossip_engine_t* eng, const char* name, double value);
 
 /* FLOOD peer source: directed adjacency Topology[u] = col[row_ptr[u]..row_ptr[u+1]),
- * global node ids, n == N.  Copied; never retained. */
+ * global node ids, n == N.  Copied; never retained.  Plain FLOOD reads each row as a set;
+ * an engine created with faults or stall_rounds keeps each row as listed (order and
+ * repeats: the forwarding walk of main.go:72-87) and ends every walk. */
 int gossip_set_topology_csr(gossip_engine_t* eng, const uint32_t* row_ptr, const uint32_t* col,
                             uint64_t n, uint64_t n_edges);
 

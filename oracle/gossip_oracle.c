@@ -1254,7 +1254,7 @@ int oracle_set_param(oracle_sim_t* s, const char* name, double value) {
     s->xd_filter_frac = value;
     return GOSSIP_OK;
   }
-  const char* known[] = {"alld_frac", "filter_frac", "ahead", "apply_grid", "ae_sparse", "ae_cap"};
+  const char* known[] = {"alld_frac", "filter_frac", "ahead", "apply_grid", "push_waves", "ae_sparse", "ae_cap"};
   for (size_t i = 0; i < sizeof known / sizeof known[0]; ++i)
     if (!strcmp(name, known[i])) return GOSSIP_OK;
   return GOSSIP_EINVAL;
