@@ -54,6 +54,7 @@ struct BinGeom {
   uint32_t nt_s, nt_d;   // sender tiles, destination tiles
   uint32_t apply_grid;   // host only: persistent apply blocks (0 = one per tile; gossip_set_param)
   uint32_t push_waves;   // push-pull apply: waves [0, push_waves) walk the pushes, the rest the responses
+  uint32_t aos;          // push records also packed {value, id} (BinBufs::prec; one shard, big regions)
 };
 
 // big: regions of up to 2 * kMaxSenders senders and 2 * kRecPerRegion records (one shard
@@ -63,7 +64,8 @@ bool bin_path_ok(uint64_t N, uint32_t k, uint32_t W, uint32_t G);
 
 struct BinBufs {
   uint32_t* ids;    // [nt_s][rp]   p_local | n_local << 14
-  uint64_t* vals;   // [nt_s][rp]   S_t[sender]
+  uint64_t* vals;   // [nt_s][rp]   S_t[sender] (null with aos)
+  uint32_t* prec;   // aos: [nt_s][rp][3] {S_t[sender] lo, hi, id}: a push in one 12-B piece
   uint64_t* resp;   // [nt_s][rp]   pull response S_t[p] & ~S_t[n]
   uint16_t* off;    // [nt_s][nt_d + 1] run starts inside each sender region
   uint16_t* offT;   // [nt_d + 1][nt_s]

@@ -432,28 +432,30 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
   uint32_t* gids = b.ids + (size_t)s * g.rp;
   uint64_t* gvals = b.vals + (size_t)s * g.rp;
   if constexpr (BIG) {
-    // ids out first (kept in registers), then the region's sender values take the
-    // staging room and each record's value is read from LDS: the values are the
-    // ones in v[] (no second read of S), and no record gathers its sender's word
-    // from L2 / MALL (a 64-B fetch per 8-B value at 2^27 nodes: emit 158 B of
-    // fetch per node, profiles/r03_a/pmc_dense_2p27.json)
-    constexpr uint32_t kE = 2 * kRecPerRegion / kEmitThreads;
-    uint32_t idr[kE];
-#pragma unroll
-    for (uint32_t q = 0; q < kE; ++q) {
-      const uint32_t e = tid + q * kEmitThreads;
-      idr[q] = e < total ? st_ids[e] : 0u;
-      if (e < total) rec_st<1>(&gids[e], idr[q]);
-    }
-    __syncthreads();  // every staged id is in registers
+    // ids out first, then the region's sender values take the staging room and each
+    // push is written packed {value, id} (BinGeom::aos), its value read from LDS: the
+    // values are the ones in v[] (no second read of S), and no record gathers its
+    // sender's word from L2 / MALL (a 64-B fetch per 8-B value at 2^27 nodes: emit 158 B
+    // of fetch per node, profiles/r03_a/pmc_dense_2p27.json).  The ids are read back from
+    // the region just written (plain stores: L2-resident; a register copy of 32 ids per
+    // lane spilled 39 VGPRs).
+    for (uint32_t e = tid; e < total; e += kEmitThreads) gids[e] = st_ids[e];
+    __syncthreads();  // every staged id is out
     uint64_t* sv = (uint64_t*)st_ids;  // 2 * kRecPerRegion u32 = kMaxS u64
 #pragma unroll
     for (uint32_t q = 0; q < kQ; ++q) sv[tid + q * kEmitThreads] = v[q];
     __syncthreads();
-#pragma unroll
-    for (uint32_t q = 0; q < kE; ++q) {
-      const uint32_t e = tid + q * kEmitThreads;
-      if (e < total) rec_st<1>(&gvals[e], sv[(idr[q] >> kTileDLog) & kIdNMask]);
+    typedef uint32_t u32x3 __attribute__((ext_vector_type(3), aligned(4)));  // one 12-B store
+    uint32_t* gprec = b.prec + (size_t)s * g.rp * 3;
+#pragma unroll 4
+    for (uint32_t e = tid; e < total; e += kEmitThreads) {
+      const uint32_t id = gids[e];
+      const uint64_t x = sv[(id >> kTileDLog) & kIdNMask];  // (big regions always pack: g.aos)
+      u32x3 r;
+      r.x = (uint32_t)x;
+      r.y = (uint32_t)(x >> 32);
+      r.z = id;
+      rec_st<1>((u32x3*)(gprec + 3 * e), r);
     }
   } else
   for (uint32_t e = tid; e < total; e += kEmitThreads) {
@@ -674,14 +676,26 @@ __device__ __forceinline__ void push_walk(const BinGeom& g, const BinBufs& b, ui
                                           uint64_t* wmask, int32_t* wlist, uint32_t nwaves) {
   const uint32_t* __restrict__ gids = b.ids;
   const uint64_t* __restrict__ gvals = b.vals;
+  const uint32_t* __restrict__ gprec = b.prec;
+  const bool aos = g.aos != 0;
   const uint16_t* rowb = b.offT + (size_t)X * g.nt_s;
   for_each_run_record<kUnroll>(g, rowb, rowb + g.nt_s, wmask, wlist, [&](const int32_t* rec) {
     uint32_t id[kUnroll];
     uint64_t v[kUnroll];
+    if (aos) {  // {value lo, hi, id}: one 12-B piece per push
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) id[u] = rec_ld<8>(&gids[rec[u] >= 0 ? rec[u] : 0]);
+      for (int u = 0; u < kUnroll; ++u) {
+        const uint32_t* r = &gprec[3ull * (uint32_t)(rec[u] >= 0 ? rec[u] : 0)];
+        const uint32_t lo = rec_ld<8>(&r[0]), hi = rec_ld<8>(&r[1]);
+        id[u] = rec_ld<8>(&r[2]);
+        v[u] = (uint64_t)lo | ((uint64_t)hi << 32);
+      }
+    } else {
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) v[u] = rec_ld<8>(&gvals[rec[u] >= 0 ? rec[u] : 0]);  // not behind the id: both loads fly together
+      for (int u = 0; u < kUnroll; ++u) id[u] = rec_ld<8>(&gids[rec[u] >= 0 ? rec[u] : 0]);
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) v[u] = rec_ld<8>(&gvals[rec[u] >= 0 ? rec[u] : 0]);  // not behind the id: both loads fly together
+    }
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u)
       v[u] = rec[u] < 0 || (id[u] & VZ) ? 0ull : v[u];  // every value is stored (K1)
@@ -873,6 +887,11 @@ BinGeom make_bin_geom(uint64_t N, uint32_t k, bool big) {
   g.nt_d = (uint32_t)((N + kTileD - 1) / kTileD);
   g.apply_grid = kApplyGrid;
   g.push_waves = N > (1ull << 25) ? kPushWavesBig : kPushWaves;
+  // big regions (past kMaxTilesD tiles) make runs of ~4 records, and the apply pass's push
+  // walk is bound by the number of distinct lines it fetches: a push packed as one 12-B
+  // piece beside the 4-B id (for serve and the reply walk) touches fewer than the two
+  // arrays' 16-B + 32-B pieces of a run
+  g.aos = big ? 1u : 0u;
   return g;
 }
 
@@ -886,7 +905,8 @@ bool bin_path_ok(uint64_t N, uint32_t k, uint32_t W, uint32_t G) {
 size_t bin_bytes(const BinGeom& g) {
   const size_t recs = (size_t)g.nt_s * g.rp;
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-  return al(recs * 4) + al(recs * 8) + al(recs * 8) + 2 * al((size_t)g.nt_s * (g.nt_d + 1) * 2);
+  return al(recs * 4) + (g.aos ? al(recs * 12) : al(recs * 8)) + al(recs * 8) +
+         2 * al((size_t)g.nt_s * (g.nt_d + 1) * 2);
 }
 
 void bin_carve(const BinGeom& g, void* base, BinBufs* b) {
@@ -895,8 +915,9 @@ void bin_carve(const BinGeom& g, void* base, BinBufs* b) {
   char* p = (char*)base;
   b->ids = (uint32_t*)p;
   p += al(recs * 4);
-  b->vals = (uint64_t*)p;
-  p += al(recs * 8);
+  b->vals = g.aos ? nullptr : (uint64_t*)p;
+  b->prec = g.aos ? (uint32_t*)p : nullptr;
+  p += g.aos ? al(recs * 12) : al(recs * 8);
   b->resp = (uint64_t*)p;
   p += al(recs * 8);
   b->off = (uint16_t*)p;
