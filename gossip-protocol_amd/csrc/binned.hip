@@ -445,17 +445,14 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
 #pragma unroll
     for (uint32_t q = 0; q < kQ; ++q) sv[tid + q * kEmitThreads] = v[q];
     __syncthreads();
-    typedef uint32_t u32x3 __attribute__((ext_vector_type(3), aligned(4)));  // one 12-B store
     uint32_t* gprec = b.prec + (size_t)s * g.rp * 3;
 #pragma unroll 4
     for (uint32_t e = tid; e < total; e += kEmitThreads) {
       const uint32_t id = gids[e];
       const uint64_t x = sv[(id >> kTileDLog) & kIdNMask];  // (big regions always pack: g.aos)
-      u32x3 r;
-      r.x = (uint32_t)x;
-      r.y = (uint32_t)(x >> 32);
-      r.z = id;
-      rec_st<1>((u32x3*)(gprec + 3 * e), r);
+      rec_st<1>(&gprec[3 * e], (uint32_t)x);
+      rec_st<1>(&gprec[3 * e + 1], (uint32_t)(x >> 32));
+      rec_st<1>(&gprec[3 * e + 2], id);
     }
   } else
   for (uint32_t e = tid; e < total; e += kEmitThreads) {

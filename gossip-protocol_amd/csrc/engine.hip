@@ -26,6 +26,7 @@
 #include <cmath>
 #include <immintrin.h>
 #include "kernels.h"
+#include "multi.h"
 #include "philox.h"
 
 using namespace gossip;
@@ -47,6 +48,7 @@ struct gossip_engine {
   hipStream_t stream = nullptr;
   bool own_stream = false;
   std::string err;
+  gossip::Transport* tr = nullptr;  // the collectives of gossip_step (G > 1), owned (gossip_comm_init_rank)
 
   uint64_t N = 0, Nl = 0, lo = 0, hi = 0, nown = 0;
   uint32_t R = 0, W = 0, k = 0, mode = 0, G = 1, rank = 0;
@@ -1152,6 +1154,9 @@ void gossip_destroy(gossip_engine_t* eng) {
   if (!eng) return;
   (void)hipSetDevice(eng->device);
   (void)hipStreamSynchronize(eng->stream);  // (the null stream too, when bound)
+  delete eng->tr;
+  eng->tr = nullptr;
+  (void)hipSetDevice(eng->device);
   free_all(eng);
   delete eng;
 }
@@ -1921,11 +1926,38 @@ int gossip_set_faults(gossip_engine_t* e, uint32_t edge_loss, uint32_t partition
   return GOSSIP_OK;
 }
 
+int gossip_comm_unique_id(uint8_t* id) {
+  if (!id) return GOSSIP_EINVAL;
+  std::string err;
+  const int rc = rccl_unique_id(id, &err);
+  if (rc) g_create_error = err;
+  return rc;
+}
+
+int gossip_comm_init_rank(gossip_engine_t* e, const uint8_t* id) {
+  if (!e || !id) return GOSSIP_EINVAL;
+  if (e->G < 2) return e->fail(GOSSIP_EINVAL, "gossip_comm_init_rank: shard_count is 1");
+  if (e->tr) return e->fail(GOSSIP_ESTATE, "gossip_comm_init_rank: the engine has its collectives");
+  if (int rc = set_dev(e)) return rc;
+  HIP_OK(e, hipStreamSynchronize(e->stream));
+  std::string err;
+  e->tr = make_rccl_transport({e}, id, &err);
+  if (!e->tr) return e->fail(GOSSIP_ERCCL, "%s", err.c_str());
+  return GOSSIP_OK;
+}
+
 int gossip_step(gossip_engine_t* e, uint32_t max_rounds, gossip_round_stats_t* stats, uint64_t* infected,
                 uint32_t* rounds_done) {
   if (!e) return GOSSIP_EINVAL;
   if (rounds_done) *rounds_done = 0;
-  if (e->G != 1) return e->fail(GOSSIP_ESTATE, "gossip_step drives one shard; use the round_* calls for G > 1");
+  if (e->G != 1) {  // sharded rounds over the engine's own collectives
+    if (!e->tr) return e->fail(GOSSIP_ESTATE, "G > 1: gossip_comm_init_rank first (or run the round_* calls)");
+    if (e->mode == GOSSIP_MODE_FLOOD && !e->has_topo) return e->fail(GOSSIP_ESTATE, "FLOOD needs a topology");
+    std::string err;
+    const int rc = sharded_step({e}, e->tr, max_rounds, stats, infected, rounds_done, &err);
+    if (rc) e->err = err;
+    return rc;
+  }
   if (e->mode == GOSSIP_MODE_FLOOD && !e->has_topo) return e->fail(GOSSIP_ESTATE, "FLOOD needs a topology");
   if (int rc = set_dev(e)) return rc;
   if (e->binned) return step_planned(e, max_rounds, stats, infected, rounds_done);
@@ -2086,4 +2118,99 @@ int gossip_reset_timing(gossip_engine_t* e) {
   return GOSSIP_OK;
 }
 
+// --- one process for all G shards -----------------------------------
+
 }  // extern "C"
+
+struct gossip_group {
+  std::vector<gossip_engine_t*> eng;  // by rank
+  gossip::Transport* tr = nullptr;
+  std::string err;
+};
+
+namespace {
+thread_local std::string g_group_error;
+}  // namespace
+
+extern "C" {
+
+void gossip_group_destroy(gossip_group_t* g) {
+  if (!g) return;
+  delete g->tr;  // (the communicators first: they run on the engines' streams)
+  for (gossip_engine_t* e : g->eng) gossip_destroy(e);
+  delete g;
+}
+
+int gossip_group_create(const gossip_config_t* cfg, uint32_t n_shards, const int32_t* devices, int32_t transport,
+                        gossip_group_t** out) {
+  g_group_error.clear();
+  if (!cfg || !out || n_shards == 0 || transport < 0 || transport > 2) {
+    g_group_error = "gossip_group_create: bad argument";
+    return GOSSIP_EINVAL;
+  }
+  *out = nullptr;
+  auto* g = new gossip_group;
+  bool distinct = true;
+  for (uint32_t r = 0; r < n_shards; ++r) {
+    gossip_config_t c = *cfg;
+    c.shard_rank = r;
+    c.shard_count = n_shards;
+    if (devices) c.device = devices[r];
+    for (uint32_t q = 0; q < r; ++q)
+      if (devices && devices[q] == devices[r]) distinct = false;
+    gossip_engine_t* e = nullptr;
+    if (int rc = gossip_create(&c, &e)) {
+      g_group_error = std::string("shard ") + std::to_string(r) + ": " + gossip_last_error(nullptr);
+      gossip_group_destroy(g);
+      return rc;
+    }
+    g->eng.push_back(e);
+  }
+  if (!devices && n_shards > 1) distinct = false;
+  if (n_shards > 1) {
+    const bool use_rccl = transport == 1 || (transport == 0 && distinct);
+    if (use_rccl && !distinct) {
+      g_group_error = "gossip_group_create: RCCL needs one device per shard";
+      gossip_group_destroy(g);
+      return GOSSIP_EINVAL;
+    }
+    std::string err;
+    g->tr = use_rccl ? make_rccl_transport(g->eng, nullptr, &err) : make_copy_transport(g->eng, &err);
+    if (!g->tr) {
+      g_group_error = err;
+      gossip_group_destroy(g);
+      return use_rccl ? GOSSIP_ERCCL : GOSSIP_EINVAL;
+    }
+  }
+  *out = g;
+  return GOSSIP_OK;
+}
+
+gossip_engine_t* gossip_group_engine(gossip_group_t* g, uint32_t rank) {
+  return g && rank < g->eng.size() ? g->eng[rank] : nullptr;
+}
+
+int32_t gossip_group_transport(const gossip_group_t* g) { return g && g->tr ? g->tr->kind() : 0; }
+
+int gossip_group_step(gossip_group_t* g, uint32_t max_rounds, gossip_round_stats_t* stats, uint64_t* infected,
+                      uint32_t* rounds_done) {
+  if (!g) return GOSSIP_EINVAL;
+  if (g->eng.size() == 1) return gossip_step(g->eng[0], max_rounds, stats, infected, rounds_done);
+  g->err.clear();
+  const int rc = sharded_step(g->eng, g->tr, max_rounds, stats, infected, rounds_done, &g->err);
+  return rc;
+}
+
+const char* gossip_group_last_error(const gossip_group_t* g) { return g ? g->err.c_str() : g_group_error.c_str(); }
+
+}  // extern "C"
+
+// engine internals for the multi-GPU driver (multi.h)
+namespace gossip {
+hipStream_t engine_stream(gossip_engine_t* e) { return e->stream; }
+int engine_device(const gossip_engine_t* e) { return e->device; }
+uint32_t engine_rank(const gossip_engine_t* e) { return e->rank; }
+uint32_t engine_shards(const gossip_engine_t* e) { return e->G; }
+uint32_t engine_rumors(const gossip_engine_t* e) { return e->R; }
+uint32_t engine_mode(const gossip_engine_t* e) { return e->mode; }
+}  // namespace gossip

@@ -17,7 +17,9 @@ FLAG_DENSE = 1 << 3
 FLAG_SHARD_DIRECT = 1 << 4
 FLAG_AE_DIRECT_SCAN = 1 << 5
 
-STATUS = {0: "OK", -1: "EINVAL", -2: "EHIP", -3: "ENOMEM", -4: "ESTATE", -5: "ENODEV", -6: "ENOTSUP"}
+STATUS = {0: "OK", -1: "EINVAL", -2: "EHIP", -3: "ENOMEM", -4: "ESTATE", -5: "ENODEV", -6: "ENOTSUP", -7: "ERCCL"}
+UNIQUE_ID_BYTES = 128
+TRANSPORT_AUTO, TRANSPORT_RCCL, TRANSPORT_COPY = 0, 1, 2
 
 
 class Config(C.Structure):
@@ -110,7 +112,19 @@ SIGNATURES = [
     ("philox_device", C.c_int, [P, U32P, U32P, U32P, C.c_uint32]),
     ("kernel_time", C.c_int, [P, C.c_uint32, C.POINTER(C.c_double), U64P]),
     ("reset_timing", C.c_int, [P]),
+    # multi-GPU driven by the engine
+    ("comm_unique_id", C.c_int, [C.c_char_p]),
+    ("comm_init_rank", C.c_int, [P, C.c_char_p]),
+    ("group_create", C.c_int, [C.POINTER(Config), C.c_uint32, C.POINTER(C.c_int32), C.c_int32, C.POINTER(P)]),
+    ("group_destroy", None, [P]),
+    ("group_engine", P, [P, C.c_uint32]),
+    ("group_transport", C.c_int32, [P]),
+    ("group_step", C.c_int, [P, C.c_uint32, C.POINTER(RoundStats), U64P, U32P]),
+    ("group_last_error", C.c_char_p, [P]),
 ]
+# entry points of the HIP engine only (the oracle library exports the rest under "oracle_")
+ENGINE_ONLY = {"comm_unique_id", "comm_init_rank", "group_create", "group_destroy", "group_engine", "group_transport",
+               "group_step", "group_last_error"}
 
 
 def bind(lib: C.CDLL, prefix: str, names=None) -> C.CDLL:

@@ -410,6 +410,10 @@ class Engine(AbiEngine):
         self._check(self._fn("set_stream")(self._h, C.c_void_p(hip_stream or None)))
         self._stream = hip_stream
 
+    def comm_init_rank(self, unique_id: bytes):
+        """This rank's RCCL communicator (gossip_comm_init_rank): gossip_step then runs sharded rounds."""
+        self._check(self._fn("comm_init_rank")(self._h, unique_id))
+
     def kernel_time(self, which: int):
         ms, n = C.c_double(), C.c_uint64()
         self._check(self._fn("kernel_time")(self._h, C.c_uint32(which), C.byref(ms), C.byref(n)))
@@ -425,6 +429,111 @@ class Engine(AbiEngine):
         self._check(self._fn("philox_device")(self._h, ctr.ctypes.data_as(_abi.U32P), key.ctypes.data_as(_abi.U32P),
                                               out.ctypes.data_as(_abi.U32P), C.c_uint32(ctr.shape[0])))
         return out
+
+
+def comm_unique_id() -> bytes:
+    """ncclGetUniqueId through the library (rank 0; hand the bytes to every rank)."""
+    lib = load_library()
+    buf = C.create_string_buffer(_abi.UNIQUE_ID_BYTES)
+    rc = lib.gossip_comm_unique_id(buf)
+    if rc != 0:
+        raise GossipError(rc, lib.gossip_last_error(None).decode(errors="replace"))
+    return buf.raw
+
+
+class _GroupShard(Engine):
+    """Engine view of one shard of a Group (the group owns and destroys it)."""
+
+    def __init__(self, group: "Group", handle, cfg: Config, device):
+        self._lib, self._p = load_library(), "gossip_"
+        self.cfg = cfg
+        self._h = handle
+        self._group = group
+        self.n_nodes, self.n_rumors = cfg.n_nodes, cfg.n_rumors
+        self.n_words = (cfg.n_rumors + 63) // 64
+        lo, hi = C.c_uint64(), C.c_uint64()
+        self._check(self._fn("shard_range")(self._h, C.byref(lo), C.byref(hi)))
+        self.lo, self.hi = lo.value, hi.value
+        self.device = device
+
+    def close(self):  # owned by the group
+        self._h = None
+
+
+class Group:
+    """All G shards in this process, rounds driven by the library (gossip_group_*):
+    transport 1 = RCCL (distinct devices), 2 = device copies (any devices, also one GPU), 0 = auto."""
+
+    def __init__(self, n_nodes: int, n_rumors: int = 1, mode="push", fanout: int = 1, seed: int = 0,
+                 flags: int = 0, n_shards: int = 2, devices=None, transport: int = _abi.TRANSPORT_AUTO,
+                 churn_fail: int = 0, churn_recover: int = 0, edge_loss: int = 0, partitions: int = 0,
+                 stall_rounds: int = 0, params=None):
+        self._lib = load_library()
+        self.cfg = make_config(n_nodes, n_rumors, mode, fanout, seed, flags, devices[0] if devices else -1, 0,
+                               n_shards, churn_fail, churn_recover, edge_loss, partitions, stall_rounds)
+        devs = (C.c_int32 * n_shards)(*devices) if devices else None
+        h = C.c_void_p()
+        rc = self._lib.gossip_group_create(C.byref(self.cfg), n_shards, devs, transport, C.byref(h))
+        if rc != 0:
+            raise GossipError(rc, self._lib.gossip_group_last_error(None).decode(errors="replace"))
+        self._h = h
+        self.n_rumors = n_rumors
+        self.shards = []
+        for r in range(n_shards):
+            c = Config.from_buffer_copy(self.cfg)
+            c.shard_rank = r
+            self.shards.append(_GroupShard(self, self._lib.gossip_group_engine(self._h, r), c,
+                                           devices[r] if devices else None))
+        for e in self.shards:
+            for name, value in (params or {}).items():
+                e.set_param(name, value)
+
+    @property
+    def transport(self) -> int:
+        return self._lib.gossip_group_transport(self._h)
+
+    def inject_random(self):
+        for e in self.shards:
+            e.inject_random()
+
+    def inject(self, node: int, rumor: int = 0):
+        for e in self.shards:
+            e.inject(node, rumor)
+
+    def reset(self):
+        for e in self.shards:
+            e.reset()
+
+    def step(self, max_rounds: int, with_infected: bool = True) -> StepResult:
+        stats = (RoundStats * max(max_rounds, 1))()
+        inf = np.zeros((max(max_rounds, 1), self.n_rumors), dtype=np.uint64) if with_infected else None
+        done = C.c_uint32()
+        rc = self._lib.gossip_group_step(self._h, max_rounds, stats,
+                                         inf.ctypes.data_as(_abi.U64P) if inf is not None else None, C.byref(done))
+        if rc != 0:
+            raise GossipError(rc, self._lib.gossip_group_last_error(self._h).decode(errors="replace"))
+        r = done.value
+        return StepResult(r, [stats[i].as_dict() for i in range(r)],
+                          inf[:r] if inf is not None else np.zeros((r, 0), np.uint64))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            for e in self.shards:
+                e.close()
+            self._lib.gossip_group_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
 def peer(seed: int, n_nodes: int, node: int, round_: int, j: int) -> int:

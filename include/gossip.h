@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define GOSSIP_ABI_VERSION 7u
+#define GOSSIP_ABI_VERSION 8u
 
 /* Dissemination modes. */
 enum gossip_mode {
@@ -55,7 +55,8 @@ enum gossip_status {
   GOSSIP_ENOMEM = -3, /* device allocation failed                      */
   GOSSIP_ESTATE = -4, /* call out of order (e.g. FLOOD without topology) */
   GOSSIP_ENODEV = -5, /* no usable gfx950 device                        */
-  GOSSIP_ENOTSUP = -6 /* mode/feature not built                         */
+  GOSSIP_ENOTSUP = -6, /* mode/feature not built                        */
+  GOSSIP_ERCCL = -7    /* RCCL (librccl.so.1) missing or a collective failed */
 };
 
 enum gossip_flags {
@@ -89,9 +90,11 @@ typedef struct gossip_config {
   uint32_t partitions;  /* random modes and FLOOD: 0/1 = none, P > 1 = nodes split into P
                            contiguous blocks that cannot reach each other               */
   uint32_t stall_rounds; /* 0 = off.  D > 0: the reference's deadline stall (DESIGN.md §2.9,
-                           main.go:77-87: one 2 s context per neighbour, retried forever
-                           once it expired).  FLOOD: a value still undelivered on an edge
-                           D rounds after its first attempt is never sent on it again.
+                           main.go:72-87: one 2 s context per neighbour, retried forever
+                           once it expired).  FLOOD: a node forwards each value down its
+                           topology row in order, a lost attempt holding back the later
+                           neighbours; after D lost attempts on one neighbour the walk
+                           never moves past it (D = 1: the reference under silent drops).
                            Random modes: a node whose exchanges were lost in D rounds in a
                            row stops initiating exchanges until reset.  <= 16.           */
 } gossip_config_t;
@@ -172,11 +175,46 @@ int gossip_inject_random(gossip_engine_t* eng);
  * retries undelivered values every round (one shard only). */
 int gossip_set_faults(gossip_engine_t* eng, uint32_t edge_loss, uint32_t partitions);
 
-/* Runs rounds until converged or max_rounds rounds have run (single shard only,
- * G == 1).  stats: max_rounds entries or NULL; infected: max_rounds * R counters
- * (row t = per-rumor infected counts after round t) or NULL. */
+/* Runs rounds until converged (FLOOD also: a round that sends nothing) or max_rounds
+ * rounds have run.  stats: max_rounds entries or NULL; infected: max_rounds * R
+ * counters (row t = per-rumor infected counts after round t) or NULL.
+ * G > 1: the engine needs its collectives first (gossip_comm_init_rank below); every
+ * rank calls gossip_step with the same max_rounds and gets the same global stats. */
 int gossip_step(gossip_engine_t* eng, uint32_t max_rounds, gossip_round_stats_t* stats,
                 uint64_t* infected, uint32_t* rounds_done);
+
+/* --- multi-GPU driven by the engine (G > 1) -----------------------
+ * The engine runs every sharded round itself — plan, collectives, kernels — so a host
+ * (the cgo binding, gossipgpu) drives N GPUs through gossip_step alone.  Collectives are
+ * RCCL (librccl.so.1, loaded at first use) on the engine's stream.
+ *   One process (or thread) per GPU: rank 0 calls gossip_comm_unique_id and hands the
+ *   bytes to every rank by its own means; each rank creates its engine (shard_rank =
+ *   rank, shard_count = G, its own device) and calls gossip_comm_init_rank, then
+ *   gossip_step.  (Replaces the per-neighbour SyncRPC of main.go:81 as the only
+ *   cross-node traffic.)
+ *   One process for all G shards: gossip_group_create makes the G engines; transport 1
+ *   = RCCL (ncclCommInitAll; the devices must be distinct), 2 = device copies (any
+ *   devices, also G shards on one GPU: the same protocol without RCCL), 0 = RCCL when
+ *   the devices are distinct, else copies.  gossip_group_step runs the rounds.
+ * The per-kind calls below stay available for a host that runs its own collectives. */
+#define GOSSIP_UNIQUE_ID_BYTES 128
+int gossip_comm_unique_id(uint8_t* id);  /* GOSSIP_UNIQUE_ID_BYTES bytes out */
+int gossip_comm_init_rank(gossip_engine_t* eng, const uint8_t* id);
+
+typedef struct gossip_group gossip_group_t;
+/* devices: n_shards ordinals, or NULL = cfg->device for every shard.  cfg->shard_rank and
+ * cfg->shard_count are set per engine. */
+int gossip_group_create(const gossip_config_t* cfg, uint32_t n_shards, const int32_t* devices, int32_t transport,
+                        gossip_group_t** out);
+void gossip_group_destroy(gossip_group_t* grp);
+/* Engine of shard `rank` (owned by the group: inject, read, set_param ... on it). */
+gossip_engine_t* gossip_group_engine(gossip_group_t* grp, uint32_t rank);
+/* 1 = RCCL, 2 = device copies. */
+int32_t gossip_group_transport(const gossip_group_t* grp);
+int gossip_group_step(gossip_group_t* grp, uint32_t max_rounds, gossip_round_stats_t* stats, uint64_t* infected,
+                      uint32_t* rounds_done);
+/* Last error of the group (or of the last failed gossip_group_create when grp is NULL). */
+const char* gossip_group_last_error(const gossip_group_t* grp);
 
 /* --- sharded rounds (G > 1, one engine per GPU) -------------
  * Per round:  gossip_exchange_buffers → all-gather(send → recv) over RCCL
