@@ -36,7 +36,7 @@ class Transport {
   virtual int32_t kind() const = 0;  // 1 RCCL, 2 device copies
   const std::string& error() const { return err_; }
 
-  // in place: recv[i] = G slots of `bytes`, engine i's own slot holds send[i]
+  // recv[i] = G slots of `bytes`; send[i] may be engine i's own slot (in place)
   virtual int all_gather(const std::vector<void*>& recv, const std::vector<const void*>& send, size_t bytes) = 0;
   // all[r] = the value of rank r (every local engine contributes mine[i])
   virtual int all_gather_u64(const std::vector<uint64_t>& mine, std::vector<uint64_t>* all) = 0;

@@ -257,8 +257,8 @@ class CopyTransport final : public Transport {
     for (size_t i = 0; i < eng_.size(); ++i) {
       HIPT_OK(hipSetDevice(engine_device(eng_[i])));
       for (size_t q = 0; q < eng_.size(); ++q) {
-        if (q == i) continue;  // in place
         char* dst = (char*)recv[i] + (size_t)engine_rank(eng_[q]) * bytes;
+        if (dst == send[q]) continue;  // the own slot of an in-place gather
         HIPT_OK(hipMemcpyAsync(dst, send[q], bytes, hipMemcpyDefault, engine_stream(eng_[i])));
       }
     }
