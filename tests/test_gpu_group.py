@@ -74,16 +74,16 @@ def test_group_antientropy(G):
 
 def test_group_steps_again_after_inject():
     """Rounds after a client broadcast mid-run: the group replans from the shards' own totals."""
-    N, R, G = 200003, 8, 3
+    N, R, G = 200003, 3, 3
     ref = Engine(N, R, "pushpull", 2, 9, flags=1)
     with Group(N, R, "pushpull", 2, 9, flags=1, n_shards=G, devices=[0] * G) as g:
         for x in (ref, g):
             x.inject(5, 0)
-            x.inject(N - 1, 3)
+            x.inject(N - 1, 1)
         a, b = ref.step(4), g.step(4)
         assert a.stats == b.stats
         for x in (ref, g):
-            x.inject(77, 5)
+            x.inject(77, 2)
         a, b = ref.step(100), g.step(100)
         assert a.stats == b.stats and b.converged
         full = ref.read_shard()
