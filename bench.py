@@ -206,7 +206,11 @@ def main():
     ap.add_argument("--no-secondary", action="store_true", help="skip the configs[2] line (profiling)")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="collectives for N > 1: nccl (= RCCL, the measured path) or gloo (a rehearsal of the "
-                         "multi-rank code on a box with fewer GPUs than ranks: ranks share devices)")
+                         "multi-rank code on a box with fewer GPUs than ranks: ranks share devices; --driver torch)")
+    ap.add_argument("--driver", default="engine", choices=("engine", "torch"),
+                    help="N > 1: engine = the library runs every sharded round over its own RCCL communicator "
+                         "(gossip_comm_init_rank + gossip_step, DESIGN.md §5.5); torch = gossip_hip.sharded drives "
+                         "the rounds over torch.distributed")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -233,13 +237,26 @@ def main():
         seed = SEED_TOTAL if n_total >= NODES_TOTAL or world > 1 else SEED_SECONDARY
     eng = Engine(n_total, RUMORS, MODE, FANOUT, seed, flags=FLAG_TIMING, device=local,
                  shard_rank=rank, shard_count=world)
-    if world > 1:
+    driver = args.driver if world > 1 else "engine"
+    driver_note = None
+    if world > 1 and driver == "engine" and args.backend == "gloo":
+        driver, driver_note = "torch", "gloo rehearsal: ranks share devices, which RCCL refuses"
+    if world > 1 and driver == "engine":
+        from gossip_hip import comm_unique_id
+        box = [comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        try:
+            eng.comm_init_rank(box[0])
+        except Exception as exc:  # report it in the line, and measure the torch-driven rounds instead
+            driver, driver_note = "torch", f"engine RCCL init failed: {exc}"
+            print(f"warning: {driver_note}", file=sys.stderr)
+    if world > 1 and driver == "torch":
         eng.set_stream(torch.cuda.current_stream().cuda_stream)
 
     def one_step():
         eng.reset()
         eng.inject_random()
-        if world == 1:
+        if driver == "engine":  # one GPU, or every rank in gossip_step over the engine's RCCL comm
             res = eng.step(64, with_infected=False)
             return res.rounds, res.converged
         st = sharded_run(eng, 64)
@@ -305,7 +322,9 @@ def main():
             "data": "synthetic (64 rumors injected at Philox tag-2 origins)",
             "config": {"workload": workload, "nodes": n_total, "nodes_per_gpu": nown, "rumors": RUMORS,
                        "fanout": FANOUT, "mode": MODE, "seed": hex(seed), "rounds_to_converge": rounds[0],
-                       "parallelism": f"shard{world}" if world > 1 else "single"},
+                       "parallelism": f"shard{world}" if world > 1 else "single",
+                       **({"driver": driver} if world > 1 else {}),
+                       **({"driver_note": driver_note} if driver_note else {})},
             **({"backend": "gloo (rehearsal: not a measurement)"} if world > 1 and args.backend == "gloo" else {}),
             "roofline": rl,
         }

@@ -49,6 +49,9 @@ struct gossip_engine {
   bool own_stream = false;
   std::string err;
   gossip::Transport* tr = nullptr;  // the collectives of gossip_step (G > 1), owned (gossip_comm_init_rank)
+  // rounds driven by the library (a transport here or in a group): the collectives run on the
+  // engine's own stream, so a buffer handed to them needs no stream sync first
+  bool driven = false;
 
   uint64_t N = 0, Nl = 0, lo = 0, hi = 0, nown = 0;
   uint32_t R = 0, W = 0, k = 0, mode = 0, G = 1, rank = 0;
@@ -1385,7 +1388,7 @@ int gossip_exchange_buffers(gossip_engine_t* e, void** send, void** recv, uint64
   uint64_t *s = nullptr, *img = nullptr;
   if (int rc = prepare_send(e, &s, &img)) return rc;
   // the caller's collective runs on another stream: publish the slice first
-  HIP_OK(e, hipStreamSynchronize(e->stream));
+  if (!e->driven) HIP_OK(e, hipStreamSynchronize(e->stream));
   if (send) *send = s;
   if (recv) *recv = img;
   if (send_bytes) *send_bytes = e->aex ? e->Nl / 4 : (uint64_t)e->W * e->Nl * 8;
@@ -1698,7 +1701,7 @@ int gossip_xd_classes(gossip_engine_t* e, void** send, void** image, uint64_t* b
   const uint64_t nwo = (e->nown + 63) / 64;  // (a short last shard: its tail words stay zero)
   HIP_OK(e, hipMemcpyAsync(own, e->lf.nzb, nwo * 8, hipMemcpyDeviceToDevice, e->stream));
   HIP_OK(e, hipMemcpyAsync(own + nwl, e->lf.fullb, nwo * 8, hipMemcpyDeviceToDevice, e->stream));
-  HIP_OK(e, hipStreamSynchronize(e->stream));
+  if (!e->driven) HIP_OK(e, hipStreamSynchronize(e->stream));
   e->xd_cls_ok = true;
   *send = own;
   *image = e->xd_cls;
@@ -1764,7 +1767,7 @@ int gossip_xd_serve(gossip_engine_t* e, void** replies) {
   if (int rc = timer_begin(e, 0)) return rc;
   HIP_OK(e, launch_xd_serve(e->xg, e->xb, e->S, e->xd_nin, e->R, e->stream));
   if (int rc = timer_end(e, 0)) return rc;
-  HIP_OK(e, hipStreamSynchronize(e->stream));
+  if (!e->driven) HIP_OK(e, hipStreamSynchronize(e->stream));
   if (int rc = timer_collect(e, false)) return rc;
   *replies = e->xb.rep_out;
   return GOSSIP_OK;
@@ -1884,7 +1887,7 @@ int gossip_ae_serve(gossip_engine_t* e, void** send) {
   if (int rc = aex_check(e)) return rc;
   if (!e->aex_in) return e->fail(GOSSIP_ESTATE, "gossip_ae_request_recv first");
   HIP_OK(e, launch_aex_serve(make_aex_args(e), e->aex_in, e->aex_nin, e->aex_resp_out, e->stream));
-  HIP_OK(e, hipStreamSynchronize(e->stream));
+  if (!e->driven) HIP_OK(e, hipStreamSynchronize(e->stream));
   *send = e->aex_resp_out;
   return GOSSIP_OK;
 }
@@ -1943,6 +1946,7 @@ int gossip_comm_init_rank(gossip_engine_t* e, const uint8_t* id) {
   std::string err;
   e->tr = make_rccl_transport({e}, id, &err);
   if (!e->tr) return e->fail(GOSSIP_ERCCL, "%s", err.c_str());
+  e->driven = true;
   return GOSSIP_OK;
 }
 
@@ -2181,6 +2185,8 @@ int gossip_group_create(const gossip_config_t* cfg, uint32_t n_shards, const int
       gossip_group_destroy(g);
       return use_rccl ? GOSSIP_ERCCL : GOSSIP_EINVAL;
     }
+    // RCCL: every collective on the engines' streams; copies: the transport drains them itself
+    for (gossip_engine_t* e : g->eng) e->driven = true;
   }
   *out = g;
   return GOSSIP_OK;
