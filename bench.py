@@ -242,11 +242,9 @@ def main():
     if world > 1 and driver == "engine" and args.backend == "gloo":
         driver, driver_note = "torch", "gloo rehearsal: ranks share devices, which RCCL refuses"
     if world > 1 and driver == "engine":
-        from gossip_hip import comm_unique_id
-        box = [comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(box, src=0)
+        from gossip_hip.sharded import init_engine_comm
         try:
-            eng.comm_init_rank(box[0])
+            init_engine_comm(eng)
         except Exception as exc:  # report it in the line, and measure the torch-driven rounds instead
             driver, driver_note = "torch", f"engine RCCL init failed: {exc}"
             print(f"warning: {driver_note}", file=sys.stderr)

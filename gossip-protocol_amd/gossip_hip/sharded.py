@@ -290,6 +290,16 @@ def sharded_round(engine, group=None, kinds: list | None = None, direct: bool | 
     return engine.round_commit(partial)
 
 
+def init_engine_comm(engine, group=None) -> None:
+    """Hands a shard engine its own RCCL communicator (gossip_comm_init_rank): rank 0
+    makes the unique id, torch.distributed carries it; engine.step then runs every sharded round
+    inside the library (plan, collectives on the engine's stream, kernels)."""
+    from .engine import comm_unique_id
+    box = [comm_unique_id() if dist.get_rank(group) == 0 else None]
+    dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+    engine.comm_init_rank(box[0])
+
+
 def sharded_run(engine, max_rounds: int, group=None, kinds: list | None = None, direct: bool | None = None) -> list:
     """Rounds until converged (same stop rule as gossip_step); kinds collects the plan kinds."""
     if engine.on_device and torch.cuda.is_available():

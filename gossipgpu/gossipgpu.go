@@ -1,5 +1,5 @@
 // Package gossipgpu binds the MI355X gossip-round engine (libgossip_hip.so, the C ABI of
-// include/gossip.h, ABI v6) for Go hosts such as 0xSherlokMo/gossip-protocol's main.go.
+// include/gossip.h, ABI v8) for Go hosts such as 0xSherlokMo/gossip-protocol's main.go.
 //
 // The reference floods each value once to its topology neighbours with blocking SyncRPCs
 // ((*NodeState).Gossip, main.go:65-89), one process per node.  Here one Engine holds every
@@ -8,6 +8,11 @@
 //	topology handler  (main.go:132-149)  -> SetTopology / SetTopologyMap
 //	broadcast handler (main.go:102-121)  -> Inject, then Step (replaces State.Gossip, :118)
 //	read handler      (main.go:123-130)  -> Read
+//
+// Several GPUs (DESIGN.md §5.5): one Engine per GPU with ShardRank / ShardCount set; rank 0
+// calls CommUniqueID, every rank gets the bytes and calls CommInitRank, then Step on every
+// rank runs the sharded rounds over the engines' own RCCL communicators.  Or one process
+// holds all shards: NewGroup + Group.Step.
 //
 // Errors are *Error values carrying the gossip_status code and gossip_last_error().  One
 // Engine serializes its calls with a mutex (the library is not thread-safe per engine; the
@@ -36,7 +41,7 @@ import (
 )
 
 // ABIVersion is the gossip.h version this binding is written against.
-const ABIVersion = 7
+const ABIVersion = 8
 
 // Mode is a dissemination rule (DESIGN.md §2).
 type Mode uint32
@@ -105,6 +110,7 @@ type Error struct {
 var statusNames = map[int]string{
 	int(C.GOSSIP_EINVAL): "EINVAL", int(C.GOSSIP_EHIP): "EHIP", int(C.GOSSIP_ENOMEM): "ENOMEM",
 	int(C.GOSSIP_ESTATE): "ESTATE", int(C.GOSSIP_ENODEV): "ENODEV", int(C.GOSSIP_ENOTSUP): "ENOTSUP",
+	int(C.GOSSIP_ERCCL): "ERCCL",
 }
 
 func (e *Error) Error() string { return fmt.Sprintf("gossip %s: %s", statusNames[e.Code], e.Msg) }
@@ -136,7 +142,16 @@ func New(cfg Config) (*Engine, error) {
 	if v := uint32(C.gossip_abi_version()); v != ABIVersion {
 		return nil, fmt.Errorf("gossipgpu: libgossip_hip ABI %d, binding written for %d", v, ABIVersion)
 	}
-	c := C.gossip_config_t{
+	c := cConfig(cfg)
+	var h *C.gossip_engine_t
+	if rc := C.gossip_create(&c, &h); rc != 0 {
+		return nil, &Error{Code: int(rc), Msg: C.GoString(C.gossip_last_error(nil))}
+	}
+	return &Engine{h: h, cfg: cfg}, nil
+}
+
+func cConfig(cfg Config) C.gossip_config_t {
+	return C.gossip_config_t{
 		n_nodes: C.uint64_t(cfg.Nodes), n_rumors: C.uint32_t(cfg.Rumors), mode: C.uint32_t(cfg.Mode),
 		fanout: C.uint32_t(cfg.Fanout), flags: C.uint32_t(cfg.Flags), seed: C.uint64_t(cfg.Seed),
 		device: C.int32_t(cfg.Device), shard_rank: C.uint32_t(cfg.ShardRank), shard_count: C.uint32_t(cfg.ShardCount),
@@ -144,11 +159,6 @@ func New(cfg Config) (*Engine, error) {
 		edge_loss: C.uint32_t(cfg.EdgeLoss), partitions: C.uint32_t(cfg.Partitions),
 		stall_rounds: C.uint32_t(cfg.StallRounds),
 	}
-	var h *C.gossip_engine_t
-	if rc := C.gossip_create(&c, &h); rc != 0 {
-		return nil, &Error{Code: int(rc), Msg: C.GoString(C.gossip_last_error(nil))}
-	}
-	return &Engine{h: h, cfg: cfg}, nil
 }
 
 // Close releases every device buffer.
@@ -281,8 +291,9 @@ func (e *Engine) SetStream(stream unsafe.Pointer) error {
 }
 
 // Step runs rounds until every node holds every rumor (FLOOD also: until a round sends
-// nothing) or maxRounds ran; one shard only.  It replaces State.Gossip (main.go:118).
-// infected[t][r] = nodes holding rumor r after round t.
+// nothing) or maxRounds ran.  It replaces State.Gossip (main.go:118).  With ShardCount > 1
+// the engine needs CommInitRank first and every rank calls Step with the same maxRounds;
+// the stats are global.  infected[t][r] = nodes holding rumor r after round t.
 func (e *Engine) Step(maxRounds uint32) ([]RoundStats, [][]uint64, error) {
 	e.mu.Lock()
 	defer e.mu.Unlock()
@@ -296,7 +307,11 @@ func (e *Engine) Step(maxRounds uint32) ([]RoundStats, [][]uint64, error) {
 	if rc := C.gossip_step(e.h, C.uint32_t(maxRounds), &st[0], u64p(inf), &done); rc != 0 {
 		return nil, nil, e.fail(rc)
 	}
-	n := int(done)
+	out, rows := convertStats(st, inf, int(done), R)
+	return out, rows, nil
+}
+
+func convertStats(st []C.gossip_round_stats_t, inf []uint64, n int, R uint64) ([]RoundStats, [][]uint64) {
 	out := make([]RoundStats, n)
 	rows := make([][]uint64, n)
 	for i := 0; i < n; i++ {
@@ -305,7 +320,110 @@ func (e *Engine) Step(maxRounds uint32) ([]RoundStats, [][]uint64, error) {
 			Messages: uint64(st[i].messages), StateHash: uint64(st[i].state_hash)}
 		rows[i] = inf[uint64(i)*R : uint64(i+1)*R]
 	}
+	return out, rows
+}
+
+// UniqueIDBytes is the size of an RCCL unique id (gossip_comm_unique_id).
+const UniqueIDBytes = int(C.GOSSIP_UNIQUE_ID_BYTES)
+
+// CommUniqueID makes the RCCL unique id (rank 0); hand it to every rank by any channel.
+func CommUniqueID() ([]byte, error) {
+	buf := make([]byte, UniqueIDBytes)
+	if rc := C.gossip_comm_unique_id((*C.uint8_t)(unsafe.Pointer(&buf[0]))); rc != 0 {
+		return nil, &Error{Code: int(rc), Msg: C.GoString(C.gossip_last_error(nil))}
+	}
+	return buf, nil
+}
+
+// CommInitRank joins this engine (ShardRank of ShardCount) to the RCCL communicator of id;
+// Step then runs sharded rounds (DESIGN.md §5.5).  Every rank calls it.
+func (e *Engine) CommInitRank(id []byte) error {
+	if len(id) != UniqueIDBytes {
+		return fmt.Errorf("gossipgpu: CommInitRank wants %d bytes", UniqueIDBytes)
+	}
+	return e.locked(func() C.int { return C.gossip_comm_init_rank(e.h, (*C.uint8_t)(unsafe.Pointer(&id[0]))) })
+}
+
+// Transport of a Group.
+const (
+	TransportAuto int32 = 0 // RCCL when every shard has its own device, else device copies
+	TransportRCCL int32 = 1
+	TransportCopy int32 = 2
+)
+
+// Group is every shard of one run in this process (gossip_group_*): one engine per shard,
+// the rounds driven by the library.
+type Group struct {
+	mu     sync.Mutex
+	g      *C.gossip_group_t
+	cfg    Config
+	shards []*Engine
+}
+
+// NewGroup creates shards engines (devices: one ordinal per shard, or nil = cfg.Device).
+func NewGroup(cfg Config, shards uint32, devices []int32, transport int32) (*Group, error) {
+	if devices != nil && len(devices) != int(shards) {
+		return nil, fmt.Errorf("gossipgpu: NewGroup wants %d devices", shards)
+	}
+	c := cConfig(cfg)
+	var devp *C.int32_t
+	if devices != nil {
+		devp = (*C.int32_t)(unsafe.Pointer(&devices[0]))
+	}
+	var g *C.gossip_group_t
+	if rc := C.gossip_group_create(&c, C.uint32_t(shards), devp, C.int32_t(transport), &g); rc != 0 {
+		return nil, &Error{Code: int(rc), Msg: C.GoString(C.gossip_group_last_error(nil))}
+	}
+	grp := &Group{g: g, cfg: cfg}
+	for r := uint32(0); r < shards; r++ {
+		sc := cfg
+		sc.ShardRank, sc.ShardCount = r, shards
+		grp.shards = append(grp.shards, &Engine{h: C.gossip_group_engine(g, C.uint32_t(r)), cfg: sc})
+	}
+	return grp, nil
+}
+
+// Transport is the group's transport: TransportRCCL or TransportCopy (0 for one shard).
+func (g *Group) Transport() int32 { return int32(C.gossip_group_transport(g.g)) }
+
+// Shard is the engine of shard rank (owned by the group: do not Close it).
+func (g *Group) Shard(rank uint32) *Engine { return g.shards[rank] }
+
+// Step runs rounds over every shard (as Engine.Step).
+func (g *Group) Step(maxRounds uint32) ([]RoundStats, [][]uint64, error) {
+	g.mu.Lock()
+	defer g.mu.Unlock()
+	if maxRounds == 0 {
+		return nil, nil, nil
+	}
+	for _, e := range g.shards { // no shard call may run while the group steps
+		e.mu.Lock()
+		defer e.mu.Unlock()
+	}
+	st := make([]C.gossip_round_stats_t, maxRounds)
+	R := uint64(g.cfg.Rumors)
+	inf := make([]uint64, uint64(maxRounds)*R)
+	var done C.uint32_t
+	if rc := C.gossip_group_step(g.g, C.uint32_t(maxRounds), &st[0], u64p(inf), &done); rc != 0 {
+		return nil, nil, &Error{Code: int(rc), Msg: C.GoString(C.gossip_group_last_error(g.g))}
+	}
+	out, rows := convertStats(st, inf, int(done), R)
 	return out, rows, nil
+}
+
+// Close releases every shard.
+func (g *Group) Close() {
+	g.mu.Lock()
+	defer g.mu.Unlock()
+	if g.g != nil {
+		for _, e := range g.shards {
+			e.mu.Lock()
+			e.h = nil
+			e.mu.Unlock()
+		}
+		C.gossip_group_destroy(g.g)
+		g.g = nil
+	}
 }
 
 // ReadBitset is the word form of the read handler (main.go:123-130).
