@@ -92,10 +92,17 @@ def test_group_steps_again_after_inject():
     ref.close()
 
 
-def test_cfg4_G8_group_equals_one_engine():
-    """configs[3] at full size, 2^27 nodes over 8 shards, every round run by the library."""
-    N, R, k, seed, G = 1 << 27, 64, 2, 0x5EED0004, 8
-    want, full = _one_engine("pushpull", k, R, N, seed)
+@pytest.fixture(scope="module")
+def cfg4_one_engine():
+    return _one_engine("pushpull", 2, 64, 1 << 27, 0x5EED0004)
+
+
+@pytest.mark.parametrize("G", [2, 4, 8])
+def test_cfg4_group_equals_one_engine(cfg4_one_engine, G):
+    """configs[3] at full size, 2^27 nodes over G shards (bench.py's strong-scaling sweep: state
+    all-gather rounds below 6 shards, exchange rounds at 8), every round run by the library."""
+    N, R, k, seed = 1 << 27, 64, 2, 0x5EED0004
+    want, full = cfg4_one_engine
     with Group(N, R, "pushpull", k, seed, flags=1, n_shards=G, devices=[0] * G) as g:
         g.inject_random()
         got = g.step(64)
