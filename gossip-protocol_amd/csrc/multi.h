@@ -38,6 +38,13 @@ class Transport {
 
   // recv[i] = G slots of `bytes`; send[i] may be engine i's own slot (in place)
   virtual int all_gather(const std::vector<void*>& recv, const std::vector<const void*>& send, size_t bytes) = 0;
+  // The same all-gather, started so that work the engines enqueue before join() runs
+  // beside it (RCCL: on a side stream after an event of the engine's stream; join makes
+  // the engine's stream wait for it).  Transports without a side stream finish it here.
+  virtual int all_gather_start(const std::vector<void*>& recv, const std::vector<const void*>& send, size_t bytes) {
+    return all_gather(recv, send, bytes);
+  }
+  virtual int join() { return 0; }
   // all[r] = the value of rank r (every local engine contributes mine[i])
   virtual int all_gather_u64(const std::vector<uint64_t>& mine, std::vector<uint64_t>* all) = 0;
   // sendc[i][q] = items engine i sends to rank q  ->  recvc[i][q] = items engine i gets from rank q

@@ -96,11 +96,61 @@ class RcclTransport final : public Transport {
   ~RcclTransport() override {
     for (size_t i = 0; i < comm_.size(); ++i) {
       (void)hipSetDevice(engine_device(eng_[i]));
+      if (side_.size() > i) {
+        (void)hipStreamSynchronize(side_[i]);
+        (void)hipStreamDestroy(side_[i]);
+        (void)hipEventDestroy(ev_in_[i]);
+        (void)hipEventDestroy(ev_out_[i]);
+      }
       if (scratch_.size() > i && scratch_[i]) (void)hipFree(scratch_[i]);
       (void)R.CommDestroy(comm_[i]);
     }
   }
   int32_t kind() const override { return 1; }
+
+  int all_gather_start(const std::vector<void*>& recv, const std::vector<const void*>& send, size_t bytes) override {
+    if (bytes == 0) return GOSSIP_OK;
+    if (side_.empty()) {  // a side stream per engine for collectives that overlap the engine's work
+      for (gossip_engine_t* e : eng_) {
+        HIPT_OK(hipSetDevice(engine_device(e)));
+        hipStream_t s;
+        hipEvent_t a, b;
+        HIPT_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        HIPT_OK(hipEventCreateWithFlags(&a, hipEventDisableTiming));
+        HIPT_OK(hipEventCreateWithFlags(&b, hipEventDisableTiming));
+        side_.push_back(s);
+        ev_in_.push_back(a);
+        ev_out_.push_back(b);
+      }
+    }
+    for (size_t i = 0; i < eng_.size(); ++i) {  // the side stream starts after the engine's work so far
+      HIPT_OK(hipSetDevice(engine_device(eng_[i])));
+      HIPT_OK(hipEventRecord(ev_in_[i], engine_stream(eng_[i])));
+      HIPT_OK(hipStreamWaitEvent(side_[i], ev_in_[i], 0));
+    }
+    RCCL_OK(R.GroupStart());
+    for (size_t i = 0; i < eng_.size(); ++i) {
+      HIPT_OK(hipSetDevice(engine_device(eng_[i])));
+      RCCL_OK(R.AllGather(send[i], recv[i], bytes, ncclInt8, comm_[i], side_[i]));
+    }
+    RCCL_OK(R.GroupEnd());
+    for (size_t i = 0; i < eng_.size(); ++i) {
+      HIPT_OK(hipSetDevice(engine_device(eng_[i])));
+      HIPT_OK(hipEventRecord(ev_out_[i], side_[i]));
+    }
+    pending_ = true;
+    return GOSSIP_OK;
+  }
+
+  int join() override {
+    if (!pending_) return GOSSIP_OK;
+    pending_ = false;
+    for (size_t i = 0; i < eng_.size(); ++i) {
+      HIPT_OK(hipSetDevice(engine_device(eng_[i])));
+      HIPT_OK(hipStreamWaitEvent(engine_stream(eng_[i]), ev_out_[i], 0));
+    }
+    return GOSSIP_OK;
+  }
 
   int all_gather(const std::vector<void*>& recv, const std::vector<const void*>& send, size_t bytes) override {
     if (bytes == 0) return GOSSIP_OK;
@@ -239,6 +289,9 @@ class RcclTransport final : public Transport {
   uint32_t G_;
   std::vector<void*> scratch_;
   size_t scratch_bytes_ = 0;
+  std::vector<hipStream_t> side_;
+  std::vector<hipEvent_t> ev_in_, ev_out_;
+  bool pending_ = false;
 };
 
 // All G shards in this process: collectives are device copies on the receiving
@@ -400,15 +453,15 @@ struct Driver {
         ENG(i, gossip_cc_recv(L[i], stride, &recv[i], &rvals[i]));
         send[i] = bits[i];
       }
-      TR(tr->all_gather(recv, send, nb[0]));
-      if (stride) {
+      // the bitmaps, then the mixed words, in flight while the own-slice part of the round runs
+      TR(tr->all_gather_start(recv, send, nb[0]));
+      if (stride) {  // (the same side stream: joined together below)
         std::vector<const void*> vs(vals.begin(), vals.end());
-        TR(tr->all_gather(rvals, vs, stride * 8));
+        TR(tr->all_gather_start(rvals, vs, stride * 8));
       }
-      for (size_t i = 0; i < n(); ++i) {
-        ENG(i, gossip_dense_prepare(L[i]));
-        ENG(i, gossip_cc_expand(L[i], counts.data()));
-      }
+      for (size_t i = 0; i < n(); ++i) ENG(i, gossip_dense_prepare(L[i]));
+      TR(tr->join());
+      for (size_t i = 0; i < n(); ++i) ENG(i, gossip_cc_expand(L[i], counts.data()));
     } else {
       std::vector<void*> s(n());
       std::vector<uint64_t> nb(n());
@@ -416,8 +469,10 @@ struct Driver {
         ENG(i, gossip_exchange_buffers(L[i], &s[i], &recv[i], &nb[i]));
         send[i] = s[i];
       }
-      TR(tr->all_gather(recv, send, nb[0]));
+      // the state image in flight while the own-slice part of the round runs
+      TR(tr->all_gather_start(recv, send, nb[0]));
       for (size_t i = 0; i < n(); ++i) ENG(i, gossip_dense_prepare(L[i]));
+      TR(tr->join());
     }
     for (size_t i = 0; i < n(); ++i) ENG(i, gossip_round_compute(L[i], (*part)[i].data()));
     return GOSSIP_OK;
