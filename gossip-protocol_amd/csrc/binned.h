@@ -55,6 +55,7 @@ struct BinGeom {
   uint32_t apply_grid;   // host only: persistent apply blocks (0 = one per tile; gossip_set_param)
   uint32_t push_waves;   // push-pull apply: waves [0, push_waves) walk the pushes, the rest the responses
   uint32_t aos;          // push records also packed {value, id} (BinBufs::prec; one shard, big regions)
+  uint32_t split;        // one shard: record ids as two u16 arrays (BinBufs::dst / src) instead of ids
 };
 
 // big: regions of up to 2 * kMaxSenders senders and 2 * kRecPerRegion records (one shard
@@ -63,7 +64,9 @@ BinGeom make_bin_geom(uint64_t N, uint32_t k, bool big = false);
 bool bin_path_ok(uint64_t N, uint32_t k, uint32_t W, uint32_t G);
 
 struct BinBufs {
-  uint32_t* ids;    // [nt_s][rp]   p_local | n_local << 14
+  uint32_t* ids;    // [nt_s][rp]   p_local | n_local << 14 | flags (null with split)
+  uint16_t* dst;    // split: [nt_s][rp] p_local | no-push << 14 | no-pull << 15 (serve, the push walk)
+  uint16_t* src;    // split: [nt_s][rp] n_local | no-pull << 15 (the reply walk)
   uint64_t* vals;   // [nt_s][rp]   S_t[sender] (null with aos)
   uint32_t* prec;   // aos: [nt_s][rp][3] {S_t[sender] lo, hi, id}: a push in one 12-B piece
   uint64_t* resp;   // [nt_s][rp]   pull response S_t[p] & ~S_t[n]

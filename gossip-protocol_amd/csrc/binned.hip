@@ -93,6 +93,28 @@ constexpr uint32_t kIdVZ = 1u << 28;  // no push on this record (sender empty, o
 constexpr uint32_t kIdVF = 1u << 29;  // no pull (sender full, or the peer empty)
 constexpr uint32_t kIdNMask = (1u << 14) - 1u;
 
+// Split record ids (BinGeom::split, one shard): the id word becomes two u16 arrays, so serve
+// and the push walk read 2 B (dst) instead of 4 and the reply walk 2 B (src): 12 B per node
+// less per dense round.  dst = p_local | no-push << 14 | no-pull << 15; src = n_local |
+// no-pull << 15.  The readers rebuild the u32 id fields they use.
+constexpr uint16_t kDstVZ = 1u << 14, kDstVF = 1u << 15, kSrcVF = 1u << 15;
+#ifndef GOSSIP_SPLIT_IDS
+#define GOSSIP_SPLIT_IDS 1  // 0: u32 ids below kMaxTilesD tiles (A/B; big regions always split)
+#endif
+__device__ __forceinline__ uint16_t dst_of(uint32_t id) {
+  return (uint16_t)((id & (kTileD - 1)) | ((id & kIdVZ) ? kDstVZ : 0u) | ((id & kIdVF) ? kDstVF : 0u));
+}
+__device__ __forceinline__ uint16_t src_of(uint32_t id) {
+  return (uint16_t)(((id >> kTileDLog) & kIdNMask) | ((id & kIdVF) ? kSrcVF : 0u));
+}
+__device__ __forceinline__ uint32_t id_of_dst(uint32_t d) {
+  return (d & (kTileD - 1)) | ((d & kDstVZ) ? kIdVZ : 0u) | ((d & kDstVF) ? kIdVF : 0u);
+}
+__device__ __forceinline__ uint32_t id_of_src(uint32_t s) {
+  return ((s & kIdNMask) << kTileDLog) | ((s & kSrcVF) ? kIdVF : 0u);
+}
+__device__ __forceinline__ uint32_t id_of_pair(uint32_t d, uint32_t s) { return id_of_dst(d) | id_of_src(s); }
+
 __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {
   // blocks are dealt round-robin over the 8 XCDs: give each XCD a contiguous
   // range of tiles so neighbouring runs share its L2 (speed only)
@@ -431,6 +453,10 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
 
   uint32_t* gids = b.ids + (size_t)s * g.rp;
   uint64_t* gvals = b.vals + (size_t)s * g.rp;
+  uint16_t* gdst = b.dst + (size_t)s * g.rp;
+  uint16_t* gsrc = b.src + (size_t)s * g.rp;
+  // the one-shard emits (BinGeom::split); V = 1, 2: sharded passes
+  constexpr bool split = (V == 0 && GOSSIP_SPLIT_IDS) || V >= 3;
   if constexpr (BIG) {
     // ids out first, then the region's sender values take the staging room and each
     // push is written packed {value, id} (BinGeom::aos), its value read from LDS: the
@@ -439,7 +465,15 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
     // of fetch per node, profiles/r03_a/pmc_dense_2p27.json).  The ids are read back from
     // the region just written (plain stores: L2-resident; a register copy of 32 ids per
     // lane spilled 39 VGPRs).
-    for (uint32_t e = tid; e < total; e += kEmitThreads) gids[e] = st_ids[e];
+    for (uint32_t e = tid; e < total; e += kEmitThreads) {
+      const uint32_t id = st_ids[e];
+      if (split) {
+        gdst[e] = dst_of(id);
+        gsrc[e] = src_of(id);
+      } else {
+        gids[e] = id;
+      }
+    }
     __syncthreads();  // every staged id is out
     uint64_t* sv = (uint64_t*)st_ids;  // 2 * kRecPerRegion u32 = kMaxS u64
 #pragma unroll
@@ -448,7 +482,7 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
     uint32_t* gprec = b.prec + (size_t)s * g.rp * 3;
 #pragma unroll 4
     for (uint32_t e = tid; e < total; e += kEmitThreads) {
-      const uint32_t id = gids[e];
+      const uint32_t id = split ? id_of_pair(gdst[e], gsrc[e]) : gids[e];
       const uint64_t x = sv[(id >> kTileDLog) & kIdNMask];  // (big regions always pack: g.aos)
       rec_st<1>(&gprec[3 * e], (uint32_t)x);
       rec_st<1>(&gprec[3 * e + 1], (uint32_t)(x >> 32));
@@ -460,7 +494,12 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
     // every value slot is stored (also where the flags say no push), so the
     // region is written without holes (a partly written 64-B chunk costs HBM
     // a read-modify-write: profiles/r01_experiments/microbench5_scattered_pieces.jsonl)
-    rec_st<1>(&gids[e], id);
+    if (split) {
+      rec_st<1>(&gdst[e], dst_of(id));
+      rec_st<1>(&gsrc[e], src_of(id));
+    } else {
+      rec_st<1>(&gids[e], id);
+    }
     if (STAGE) rec_st<1>(&gvals[e], sval[(id >> kTileDLog) & kIdNMask]);
     if (V >= 3) rec_st<1>(&gvals[e], S[base + ((id >> kTileDLog) & kIdNMask)]);
   }
@@ -668,18 +707,19 @@ __device__ __forceinline__ void for_each_run_record(const BinGeom& g, const uint
 
 // The pushes aimed at tile X (its runs in every sender region) ORed into acc,
 // by the waves [0, nwaves) (0: all).  VZ: the record id's no-push flag.
-template <uint32_t VZ>
+// LAYOUT 0: u32 ids + values (sharded passes), 1: split u16 ids + values, 2: split + packed pushes
+template <uint32_t VZ, int LAYOUT>
 __device__ __forceinline__ void push_walk(const BinGeom& g, const BinBufs& b, uint32_t X, unsigned long long* acc,
                                           uint64_t* wmask, int32_t* wlist, uint32_t nwaves) {
   const uint32_t* __restrict__ gids = b.ids;
   const uint64_t* __restrict__ gvals = b.vals;
   const uint32_t* __restrict__ gprec = b.prec;
-  const bool aos = g.aos != 0;
+  constexpr bool aos = LAYOUT == 2, SPLIT = LAYOUT >= 1;
   const uint16_t* rowb = b.offT + (size_t)X * g.nt_s;
   for_each_run_record<kUnroll>(g, rowb, rowb + g.nt_s, wmask, wlist, [&](const int32_t* rec) {
     uint32_t id[kUnroll];
     uint64_t v[kUnroll];
-    if (aos) {  // {value lo, hi, id}: one 12-B piece per push
+    if constexpr (aos) {  // {value lo, hi, id}: one 12-B piece per push
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         const uint32_t* r = &gprec[3ull * (uint32_t)(rec[u] >= 0 ? rec[u] : 0)];
@@ -688,8 +728,13 @@ __device__ __forceinline__ void push_walk(const BinGeom& g, const BinBufs& b, ui
         v[u] = (uint64_t)lo | ((uint64_t)hi << 32);
       }
     } else {
+      if constexpr (SPLIT) {
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) id[u] = rec_ld<8>(&gids[rec[u] >= 0 ? rec[u] : 0]);
+        for (int u = 0; u < kUnroll; ++u) id[u] = id_of_dst(rec_ld<8>(&b.dst[rec[u] >= 0 ? rec[u] : 0]));
+      } else {
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) id[u] = rec_ld<8>(&gids[rec[u] >= 0 ? rec[u] : 0]);
+      }
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) v[u] = rec_ld<8>(&gvals[rec[u] >= 0 ? rec[u] : 0]);  // not behind the id: both loads fly together
     }
@@ -729,7 +774,7 @@ __device__ __forceinline__ void tile_regs_load(uint4 (&x)[Q], const uint64_t* __
 // every record aimed at T from a sender that is not yet fully informed gets
 // its pull response S_t[p] written next to it when nonzero (every one, in dense rounds).
 // VF: the record id's no-pull flag (kIdVF; exchange rounds' binned items: kXbVF).
-template <uint32_t VF>
+template <uint32_t VF, bool SPLIT = false>
 __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, const uint64_t* __restrict__ S, BinBufs b,
                                                                   uint32_t R, IdxRange tr) {
   __shared__ unsigned long long img[kTileD];
@@ -754,8 +799,13 @@ __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, cons
   const uint16_t* rowb = b.offT + (size_t)T * g.nt_s;
   for_each_run_record<kUnrollServe>(g, rowb, rowb + g.nt_s, wmask, wlist, [&](const int32_t* rec) {
     uint32_t id[kUnrollServe];
+    if constexpr (SPLIT) {  // (one shard only: VF == kIdVF)
 #pragma unroll
-    for (int u = 0; u < kUnrollServe; ++u) id[u] = rec_ld<2>(&gids[rec[u] >= 0 ? rec[u] : 0]);
+      for (int u = 0; u < kUnrollServe; ++u) id[u] = id_of_dst(rec_ld<2>(&b.dst[rec[u] >= 0 ? rec[u] : 0]));
+    } else {
+#pragma unroll
+      for (int u = 0; u < kUnrollServe; ++u) id[u] = rec_ld<2>(&gids[rec[u] >= 0 ? rec[u] : 0]);
+    }
 #pragma unroll
     for (int u = 0; u < kUnrollServe; ++u) {
       // a fully informed sender needs nothing; otherwise the whole S_t[p] goes
@@ -776,6 +826,7 @@ uint32_t serve_grid(uint32_t tiles) { return tiles < kServeGrid ? tiles : kServe
 // bq.  Sharded dense round: g/b the push pass (every sender, tiles of the own
 // nodes), gq/bq the pull pass (own senders, tiles of the whole image); S and
 // Snext are the own slices (Nn nodes, global ids from hid0).
+template <int LAYOUT>
 __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinBufs b, BinGeom gq, BinBufs bq,
                                                                   const uint64_t* S, uint64_t* Snext,  // may alias
                                                                   uint64_t Nn, uint64_t hid0,
@@ -821,7 +872,8 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
   const bool do_pull = (mode == 2 || mode == 3) && (!split || wave >= pw);
   // split: waves [0, pw) walk the pushes, the others the responses
   const uint32_t qt0 = split ? pw * 64 : 0u, qnt = split ? kTileThreads - pw * 64 : kTileThreads;
-  if (do_push) push_walk<kIdVZ>(g, b, X, acc, wmask, wlist, split ? pw : 0u);  // pushes aimed at this tile
+  constexpr bool SPLIT = LAYOUT >= 1;
+  if (do_push) push_walk<kIdVZ, LAYOUT>(g, b, X, acc, wmask, wlist, split ? pw : 0u);  // pushes aimed at this tile
   if (do_pull) {  // responses owed to this tile's own senders
     const uint32_t* __restrict__ qids = bq.ids;
     const uint64_t* __restrict__ gresp = bq.resp;
@@ -839,7 +891,8 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
 #pragma unroll
         for (int u = 0; u < kUnrollSeq; ++u) {
           const uint32_t pos = min(p0 + u * qnt + qtid, total - 1);
-          id[u] = rec_ld<16>(&qids[reg + pos]);
+          if constexpr (SPLIT) id[u] = id_of_src(rec_ld<16>(&bq.src[reg + pos]));
+          else id[u] = rec_ld<16>(&qids[reg + pos]);
           r[u] = rec_ld<16>(&gresp[reg + pos]);
         }
 #pragma unroll
@@ -889,6 +942,7 @@ BinGeom make_bin_geom(uint64_t N, uint32_t k, bool big) {
   // piece beside the 4-B id (for serve and the reply walk) touches fewer than the two
   // arrays' 16-B + 32-B pieces of a run
   g.aos = big ? 1u : 0u;
+  g.split = big || GOSSIP_SPLIT_IDS ? 1u : 0u;  // (sharded geometries clear it: their passes keep u32 ids)
   return g;
 }
 
@@ -902,7 +956,7 @@ bool bin_path_ok(uint64_t N, uint32_t k, uint32_t W, uint32_t G) {
 size_t bin_bytes(const BinGeom& g) {
   const size_t recs = (size_t)g.nt_s * g.rp;
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-  return al(recs * 4) + (g.aos ? al(recs * 12) : al(recs * 8)) + al(recs * 8) +
+  return (g.split ? 2 * al(recs * 2) : al(recs * 4)) + (g.aos ? al(recs * 12) : al(recs * 8)) + al(recs * 8) +
          2 * al((size_t)g.nt_s * (g.nt_d + 1) * 2);
 }
 
@@ -910,8 +964,17 @@ void bin_carve(const BinGeom& g, void* base, BinBufs* b) {
   const size_t recs = (size_t)g.nt_s * g.rp;
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   char* p = (char*)base;
-  b->ids = (uint32_t*)p;
-  p += al(recs * 4);
+  b->ids = nullptr;
+  b->dst = b->src = nullptr;
+  if (g.split) {
+    b->dst = (uint16_t*)p;
+    p += al(recs * 2);
+    b->src = (uint16_t*)p;
+    p += al(recs * 2);
+  } else {
+    b->ids = (uint32_t*)p;
+    p += al(recs * 4);
+  }
   b->vals = g.aos ? nullptr : (uint64_t*)p;
   b->prec = g.aos ? (uint32_t*)p : nullptr;
   p += g.aos ? al(recs * 12) : al(recs * 8);
@@ -948,11 +1011,18 @@ hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, 
 #undef GOSSIP_EMIT
   const dim3 tg((g.nt_d + 1 + 31) / 32, (g.nt_s + 31) / 32);
   transpose_u16_kernel<<<tg, dim3(32, 8), 0, st>>>(b.off, b.offT, g.nt_s, g.nt_d + 1, partial, rs.plen);
-  if (mode == 2 || mode == 3)
-    bin_serve_kernel<kIdVF><<<serve_grid(g.nt_d), kTileThreads, 0, st>>>(g, S, b, R, IdxRange::all(g.nt_d));
+  if ((mode == 2 || mode == 3) && g.split)
+    bin_serve_kernel<kIdVF, true><<<serve_grid(g.nt_d), kTileThreads, 0, st>>>(g, S, b, R, IdxRange::all(g.nt_d));
+  else if (mode == 2 || mode == 3)
+    bin_serve_kernel<kIdVF, false><<<serve_grid(g.nt_d), kTileThreads, 0, st>>>(g, S, b, R, IdxRange::all(g.nt_d));
   // in place: K3 of tile X reads and writes only S[X] (push values and pull
   // responses come from the record buffers), and K1/K2 have finished reading S_t
-  bin_apply_kernel<<<apply_grid(g), kTileThreads, 0, st>>>(g, b, g, b, S, S, g.N, 0, partial, R, mode, flags);
+  if (g.aos)
+    bin_apply_kernel<2><<<apply_grid(g), kTileThreads, 0, st>>>(g, b, g, b, S, S, g.N, 0, partial, R, mode, flags);
+  else if (g.split)
+    bin_apply_kernel<1><<<apply_grid(g), kTileThreads, 0, st>>>(g, b, g, b, S, S, g.N, 0, partial, R, mode, flags);
+  else
+    bin_apply_kernel<0><<<apply_grid(g), kTileThreads, 0, st>>>(g, b, g, b, S, S, g.N, 0, partial, R, mode, flags);
   return hipGetLastError();  // the engine enqueues the round's snapshot (round.h) after its timing event
 }
 
@@ -970,6 +1040,7 @@ SbGeom make_sb_geom(uint64_t N, uint32_t k, uint64_t lo, uint64_t nown) {
   g.nown = nown;
   // region sizes as on one shard (make_bin_geom); peers are drawn over the global id space
   g.p = g.q = make_bin_geom(N, k);
+  g.p.split = g.q.split = 0u;
   g.p.nt_s = (uint32_t)((N + g.p.ts - 1) / g.p.ts);      // every sender
   g.p.nt_d = (uint32_t)((nown + kTileD - 1) / kTileD);   // own tiles
   g.q.nt_s = (uint32_t)((nown + g.q.ts - 1) / g.q.ts);   // own senders
@@ -1060,7 +1131,7 @@ hipError_t launch_sb_post(const SbGeom& g, const SbBufs& b, const uint64_t* imag
   BinBufs bp = b.p;
   bp.nzb = nzb;
   bp.fullb = fullb;
-  bin_apply_kernel<<<apply_grid(g.p), kTileThreads, 0, st>>>(g.p, bp, g.q, b.q, image + g.lo, Snext, g.nown, g.lo, partial,
+  bin_apply_kernel<0><<<apply_grid(g.p), kTileThreads, 0, st>>>(g.p, bp, g.q, b.q, image + g.lo, Snext, g.nown, g.lo, partial,
                                                       R, mode, flags);
   return hipGetLastError();
 }
@@ -1377,7 +1448,7 @@ __global__ __launch_bounds__(kTileThreads) void xd_apply_kernel(XdGeom g, XdBufs
     }
     if (tid < 64) cnt[tid] = 0;
     __syncthreads();
-    if (do_push) push_walk<kXbVZ>(g.r, b.rb, X, acc, wmask, wlist, split ? nwav / 2 : 0u);
+    if (do_push) push_walk<kXbVZ, 0>(g.r, b.rb, X, acc, wmask, wlist, split ? nwav / 2 : 0u);
     if (do_pull) {  // replies, in send order: region s's items are G runs (one per owner)
       const uint32_t qtid = tid - qt0;
       for (uint32_t s = s0; s < s1; ++s) {
@@ -1436,6 +1507,7 @@ XdGeom make_xd_geom(uint64_t N, uint32_t k, uint64_t Nl, uint64_t lo, uint64_t n
   g.rank = rank;
   g.k = k;
   g.s = make_bin_geom(nown ? nown : 1, k);
+  g.s.split = 0u;  // exchange items keep u32 ids (p_local | slot << 14 | flags)
   while (g.s.ts > 64 && g.s.ts * k > kXdSendRegion) {
     g.s.ts >>= 1;
     --g.s.ts_log;
