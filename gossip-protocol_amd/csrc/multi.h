@@ -53,6 +53,18 @@ class Transport {
   // bytes: send[i] holds sendb[i][q] bytes for rank q in rank order; recv[i] gets recvb[i][q] from q
   virtual int all_to_all_v(const std::vector<void*>& recv, const std::vector<std::vector<uint64_t>>& recvb,
                            const std::vector<const void*>& send, const std::vector<std::vector<uint64_t>>& sendb) = 0;
+  // several all-to-alls at once (one RCCL group: they share the links instead of queueing)
+  struct A2A {
+    std::vector<void*> recv;
+    std::vector<std::vector<uint64_t>> recvb;
+    std::vector<const void*> send;
+    std::vector<std::vector<uint64_t>> sendb;
+  };
+  virtual int all_to_all_many(const std::vector<A2A>& ops) {
+    for (const A2A& o : ops)
+      if (int rc = all_to_all_v(o.recv, o.recvb, o.send, o.sendb)) return rc;
+    return 0;
+  }
   virtual int all_reduce_sum_u64(const std::vector<std::vector<uint64_t>>& mine, std::vector<uint64_t>* sum) = 0;
   virtual int all_reduce_max_u32(const std::vector<std::vector<uint32_t>>& mine, std::vector<uint32_t>* mx) = 0;
 

@@ -208,18 +208,25 @@ class RcclTransport final : public Transport {
 
   int all_to_all_v(const std::vector<void*>& recv, const std::vector<std::vector<uint64_t>>& recvb,
                    const std::vector<const void*>& send, const std::vector<std::vector<uint64_t>>& sendb) override {
+    return all_to_all_many({A2A{recv, recvb, send, sendb}});
+  }
+
+  int all_to_all_many(const std::vector<A2A>& ops) override {
     // every rank joins, also one with nothing to send or receive
     RCCL_OK(R.GroupStart());
-    for (size_t i = 0; i < eng_.size(); ++i) {
-      HIPT_OK(hipSetDevice(engine_device(eng_[i])));
-      const std::vector<uint64_t> so = prefix(sendb[i]), ro = prefix(recvb[i]);
-      for (uint32_t q = 0; q < G_; ++q) {
-        if (sendb[i][q])
-          RCCL_OK(R.Send((const char*)send[i] + so[q], sendb[i][q], ncclInt8, (int)q, comm_[i], engine_stream(eng_[i])));
-        if (recvb[i][q])
-          RCCL_OK(R.Recv((char*)recv[i] + ro[q], recvb[i][q], ncclInt8, (int)q, comm_[i], engine_stream(eng_[i])));
+    for (const A2A& o : ops)
+      for (size_t i = 0; i < eng_.size(); ++i) {
+        HIPT_OK(hipSetDevice(engine_device(eng_[i])));
+        const std::vector<uint64_t> so = prefix(o.sendb[i]), ro = prefix(o.recvb[i]);
+        for (uint32_t q = 0; q < G_; ++q) {
+          if (o.sendb[i][q])
+            RCCL_OK(R.Send((const char*)o.send[i] + so[q], o.sendb[i][q], ncclInt8, (int)q, comm_[i],
+                           engine_stream(eng_[i])));
+          if (o.recvb[i][q])
+            RCCL_OK(R.Recv((char*)o.recv[i] + ro[q], o.recvb[i][q], ncclInt8, (int)q, comm_[i],
+                           engine_stream(eng_[i])));
+        }
       }
-    }
     RCCL_OK(R.GroupEnd());
     return GOSSIP_OK;
   }
@@ -525,8 +532,9 @@ struct Driver {
         i8[i].push_back(ic[i][q] * 8);
       }
     }
-    TR(tr->all_to_all_v(rid, i4, std::vector<const void*>(ids.begin(), ids.end()), o4));
-    TR(tr->all_to_all_v(rval, i8, std::vector<const void*>(vals.begin(), vals.end()), o8));
+    // the ids and the values in one group: they share the links
+    TR(tr->all_to_all_many({Transport::A2A{rid, i4, std::vector<const void*>(ids.begin(), ids.end()), o4},
+                            Transport::A2A{rval, i8, std::vector<const void*>(vals.begin(), vals.end()), o8}}));
     for (size_t i = 0; i < n(); ++i) {
       ENG(i, gossip_xd_serve(L[i], &rep[i]));  // replies in the received order
       ENG(i, gossip_xd_response_recv(L[i], &back[i]));
