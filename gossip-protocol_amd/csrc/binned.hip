@@ -87,6 +87,37 @@ __device__ __forceinline__ T rec_ld(const T* p) {
   if constexpr ((GOSSIP_NT_REC & BIT) != 0) return __builtin_nontemporal_load(p);
   else return *p;
 }
+// A packed push {value lo, hi, id} moves as one 12-B access (global_load/store_dwordx3):
+// one address per lane instead of three (the run walkers are bound by the vector memory
+// instructions' address work, not bytes: DESIGN.md §3.7)
+typedef uint32_t u32x3v __attribute__((ext_vector_type(3)));
+#ifndef GOSSIP_PREC_X3
+#define GOSSIP_PREC_X3 1
+#endif
+__device__ __forceinline__ void prec_st(uint32_t* p, uint32_t a, uint32_t b, uint32_t c) {
+  if constexpr (GOSSIP_PREC_X3) {
+    u32x3v v = {a, b, c};
+    __builtin_memcpy(p, &v, 12);
+  } else {
+    rec_st<1>(&p[0], a);
+    rec_st<1>(&p[1], b);
+    rec_st<1>(&p[2], c);
+  }
+}
+__device__ __forceinline__ void prec_ld(const uint32_t* p, uint32_t& a, uint32_t& b, uint32_t& c) {
+  if constexpr (GOSSIP_PREC_X3) {
+    u32x3v v;
+    __builtin_memcpy(&v, p, 12);
+    a = v.x;
+    b = v.y;
+    c = v.z;
+  } else {
+    a = rec_ld<8>(&p[0]);
+    b = rec_ld<8>(&p[1]);
+    c = rec_ld<8>(&p[2]);
+  }
+}
+
 // record id word: p_local [0,14) | n_local [14,28) | flags.  K1 rewrites every
 // id each round, so a flag never outlives its round.
 constexpr uint32_t kIdVZ = 1u << 28;  // no push on this record (sender empty, or the peer already full)
@@ -98,6 +129,18 @@ constexpr uint32_t kIdNMask = (1u << 14) - 1u;
 // less per dense round.  dst = p_local | no-push << 14 | no-pull << 15; src = n_local |
 // no-pull << 15.  The readers rebuild the u32 id fields they use.
 constexpr uint16_t kDstVZ = 1u << 14, kDstVF = 1u << 15, kSrcVF = 1u << 15;
+// timing ablations (tools/build_variants.sh; results are wrong): GOSSIP_ABL_SERVE 1 no reply
+// stores, 2 contiguous reply stores; GOSSIP_ABL_APPLY 1 no push walk, 2 no reply walk;
+// GOSSIP_ABL_EMIT 1 no packed push stores
+#ifndef GOSSIP_ABL_SERVE
+#define GOSSIP_ABL_SERVE 0
+#endif
+#ifndef GOSSIP_ABL_APPLY
+#define GOSSIP_ABL_APPLY 0
+#endif
+#ifndef GOSSIP_ABL_EMIT
+#define GOSSIP_ABL_EMIT 0
+#endif
 #ifndef GOSSIP_SPLIT_IDS
 #define GOSSIP_SPLIT_IDS 1  // 0: u32 ids below kMaxTilesD tiles (A/B; big regions always split)
 #endif
@@ -481,12 +524,10 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
     __syncthreads();
     uint32_t* gprec = b.prec + (size_t)s * g.rp * 3;
 #pragma unroll 4
-    for (uint32_t e = tid; e < total; e += kEmitThreads) {
+    for (uint32_t e = tid; e < (GOSSIP_ABL_EMIT == 1 ? 0u : total); e += kEmitThreads) {
       const uint32_t id = split ? id_of_pair(gdst[e], gsrc[e]) : gids[e];
       const uint64_t x = sv[(id >> kTileDLog) & kIdNMask];  // (big regions always pack: g.aos)
-      rec_st<1>(&gprec[3 * e], (uint32_t)x);
-      rec_st<1>(&gprec[3 * e + 1], (uint32_t)(x >> 32));
-      rec_st<1>(&gprec[3 * e + 2], id);
+      prec_st(&gprec[3 * e], (uint32_t)x, (uint32_t)(x >> 32), id);
     }
   } else
   for (uint32_t e = tid; e < total; e += kEmitThreads) {
@@ -510,24 +551,42 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
   }
 }
 
-__global__ __launch_bounds__(256) void transpose_u16_kernel(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
-                                                             uint32_t rows, uint32_t cols,
-                                                             uint64_t* __restrict__ partial, uint32_t plen) {
+// Run offsets [rows][cols] -> [cols][rows] in 64x64 tiles: a (64, 4) block, 16 loads in flight per
+// thread before any store (the 32x32 version with 4 per thread was latency-bound: 149 us for
+// the 134 MB table at 2^27 nodes, 1.8 TB/s), u32 LDS slots so the transposed reads are
+// conflict-free.
+constexpr uint32_t kTrT = 64, kTrRows = 4;
+__global__ __launch_bounds__(kTrT * kTrRows) void transpose_u16_kernel(const uint16_t* __restrict__ in,
+                                                                       uint16_t* __restrict__ out, uint32_t rows,
+                                                                       uint32_t cols, uint64_t* __restrict__ partial,
+                                                                       uint32_t plen) {
   // the dense round's stats are absolute: clear the totals before K3 adds to them
   if (blockIdx.x == 0 && blockIdx.y == 0)
-    for (uint32_t i = threadIdx.y * 32 + threadIdx.x; i < plen; i += 256) partial[i] = 0;
-  // in [rows][cols] -> out [cols][rows]
-  __shared__ uint16_t tile[32][33];
-  const uint32_t c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
-  for (uint32_t y = threadIdx.y; y < 32; y += 8) {
-    const uint32_t r = r0 + y, c = c0 + threadIdx.x;
-    if (r < rows && c < cols) tile[y][threadIdx.x] = in[(size_t)r * cols + c];
+    for (uint32_t i = threadIdx.y * kTrT + threadIdx.x; i < plen; i += kTrT * kTrRows) partial[i] = 0;
+  __shared__ uint32_t tile[kTrT][kTrT + 1];
+  constexpr uint32_t kPer = kTrT / kTrRows;
+  const uint32_t c0 = blockIdx.x * kTrT, r0 = blockIdx.y * kTrT, tx = threadIdx.x, ty = threadIdx.y;
+  uint16_t v[kPer];
+#pragma unroll
+  for (uint32_t i = 0; i < kPer; ++i) {
+    const uint32_t r = r0 + ty + i * kTrRows, c = c0 + tx;
+    v[i] = (r < rows && c < cols) ? in[(size_t)r * cols + c] : (uint16_t)0;
   }
+#pragma unroll
+  for (uint32_t i = 0; i < kPer; ++i) tile[ty + i * kTrRows][tx] = v[i];
   __syncthreads();
-  for (uint32_t y = threadIdx.y; y < 32; y += 8) {
-    const uint32_t c = c0 + y, r = r0 + threadIdx.x;
-    if (r < rows && c < cols) out[(size_t)c * rows + r] = tile[threadIdx.x][y];
+#pragma unroll
+  for (uint32_t i = 0; i < kPer; ++i) {
+    const uint32_t c = c0 + ty + i * kTrRows, r = r0 + tx;
+    if (r < rows && c < cols) out[(size_t)c * rows + r] = (uint16_t)tile[tx][ty + i * kTrRows];
   }
+}
+
+// launch of transpose_u16_kernel over a [rows][cols] table
+void launch_transpose_u16(const uint16_t* in, uint16_t* out, uint32_t rows, uint32_t cols, uint64_t* partial,
+                          uint32_t plen, hipStream_t st) {
+  const dim3 tg((cols + kTrT - 1) / kTrT, (rows + kTrT - 1) / kTrT);
+  transpose_u16_kernel<<<tg, dim3(kTrT, kTrRows), 0, st>>>(in, out, rows, cols, partial, plen);
 }
 
 
@@ -723,8 +782,8 @@ __device__ __forceinline__ void push_walk(const BinGeom& g, const BinBufs& b, ui
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         const uint32_t* r = &gprec[3ull * (uint32_t)(rec[u] >= 0 ? rec[u] : 0)];
-        const uint32_t lo = rec_ld<8>(&r[0]), hi = rec_ld<8>(&r[1]);
-        id[u] = rec_ld<8>(&r[2]);
+        uint32_t lo, hi;
+        prec_ld(r, lo, hi, id[u]);
         v[u] = (uint64_t)lo | ((uint64_t)hi << 32);
       }
     } else {
@@ -797,6 +856,12 @@ __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, cons
   const uint32_t* gids = b.ids;
   uint64_t* __restrict__ gresp = b.resp;
   const uint16_t* rowb = b.offT + (size_t)T * g.nt_s;
+#if GOSSIP_ABL_SERVE
+  uint64_t abl_x = 0;
+  uint32_t abl_c = 0;
+  const uint64_t abl_cap = (uint64_t)g.nt_s * g.rp;
+  const uint32_t abl_zero = R >> 8;  // 0, unknown to the compiler
+#endif
   for_each_run_record<kUnrollServe>(g, rowb, rowb + g.nt_s, wmask, wlist, [&](const int32_t* rec) {
     uint32_t id[kUnrollServe];
     if constexpr (SPLIT) {  // (one shard only: VF == kIdVF)
@@ -812,9 +877,33 @@ __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, cons
       // back (bits n already holds are harmless to OR), so no value is read
       // dense rounds: every response is written (K3 tells stale slots by kIdVF)
       if (rec[u] < 0 || (id[u] & VF)) continue;
+#if GOSSIP_ABL_SERVE == 1  // timing ablation: no reply stores
+      abl_x ^= (uint64_t)img[id[u] & (kTileD - 1)];
+#elif GOSSIP_ABL_SERVE == 3  // timing ablation: the reply overwrites the push value it has just read
+      if (b.prec) {
+        uint32_t* r = &b.prec[3ull * (uint32_t)rec[u]];
+        const uint32_t lo = r[0] & abl_zero, hi = r[1] & abl_zero;
+        const uint64_t y = (uint64_t)img[id[u] & (kTileD - 1)];
+        r[0] = (uint32_t)y | lo;
+        r[1] = (uint32_t)(y >> 32) | hi;
+      } else {
+        uint64_t* r = &b.vals[rec[u]];
+        *r = (uint64_t)img[id[u] & (kTileD - 1)] | (*r & abl_zero);
+      }
+#elif GOSSIP_ABL_SERVE == 2  // timing ablation: reply stores contiguous per wave window
+      const uint64_t q = (uint64_t)T * 32768u + ((((threadIdx.x >> 6) << 11) + abl_c + u * 64 + (threadIdx.x & 63)) & 32767u);
+      rec_st<4>(&gresp[q < abl_cap ? q : abl_cap - 1], (uint64_t)img[id[u] & (kTileD - 1)]);
+#else
       rec_st<4>(&gresp[rec[u]], (uint64_t)img[id[u] & (kTileD - 1)]);
+#endif
     }
+#if GOSSIP_ABL_SERVE == 2
+    abl_c += 64 * kUnrollServe;
+#endif
   });
+#if GOSSIP_ABL_SERVE == 1
+  if (abl_x == 0x123456789abcdefull) gresp[0] = abl_x;
+#endif
   }
 }
 
@@ -868,8 +957,8 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
   const uint32_t wave = tid >> 6;
   const bool split = kApplySplit && mode == 3;
   const uint32_t pw = g.push_waves;
-  const bool do_push = (mode == 1 || mode == 3) && (!split || wave < pw);
-  const bool do_pull = (mode == 2 || mode == 3) && (!split || wave >= pw);
+  const bool do_push = (mode == 1 || mode == 3) && (!split || wave < pw) && GOSSIP_ABL_APPLY != 1;
+  const bool do_pull = (mode == 2 || mode == 3) && (!split || wave >= pw) && GOSSIP_ABL_APPLY != 2;
   // split: waves [0, pw) walk the pushes, the others the responses
   const uint32_t qt0 = split ? pw * 64 : 0u, qnt = split ? kTileThreads - pw * 64 : kTileThreads;
   constexpr bool SPLIT = LAYOUT >= 1;
@@ -1009,8 +1098,7 @@ hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, 
   }
 #undef GOSSIP_EMIT_V
 #undef GOSSIP_EMIT
-  const dim3 tg((g.nt_d + 1 + 31) / 32, (g.nt_s + 31) / 32);
-  transpose_u16_kernel<<<tg, dim3(32, 8), 0, st>>>(b.off, b.offT, g.nt_s, g.nt_d + 1, partial, rs.plen);
+  launch_transpose_u16(b.off, b.offT, g.nt_s, g.nt_d + 1, partial, rs.plen, st);
   if ((mode == 2 || mode == 3) && g.split)
     bin_serve_kernel<kIdVF, true><<<serve_grid(g.nt_d), kTileThreads, 0, st>>>(g, S, b, R, IdxRange::all(g.nt_d));
   else if (mode == 2 || mode == 3)
@@ -1092,8 +1180,7 @@ void sb_emit(const BinGeom& gg, const BinBufs& bb, const uint64_t* image, uint32
 }
 
 void sb_transpose(const BinGeom& gg, const BinBufs& bb, uint64_t* partial, hipStream_t st) {
-  const dim3 tg((gg.nt_d + 1 + 31) / 32, (gg.nt_s + 31) / 32);
-  transpose_u16_kernel<<<tg, dim3(32, 8), 0, st>>>(bb.off, bb.offT, gg.nt_s, gg.nt_d + 1, partial, 0u);
+  launch_transpose_u16(bb.off, bb.offT, gg.nt_s, gg.nt_d + 1, partial, 0u, st);
 }
 
 EmitRange push_range(const SbGeom& g, const IdxRange& rs) { return EmitRange{0, g.p.N, g.lo, g.nown, 1u, 1u, rs}; }
@@ -1603,8 +1690,7 @@ hipError_t launch_xd_serve(XdGeom g, const XdBufs& b, const uint64_t* S, uint64_
   if (g.r.nt_s == 0) return hipSuccess;
   const uint32_t eg = g.r.nt_s < kEmitGrid ? g.r.nt_s : kEmitGrid;
   xd_bin_kernel<<<eg, kEmitThreads, 0, st>>>(g, b, n_in);
-  const dim3 tg((g.r.nt_d + 1 + 31) / 32, (g.r.nt_s + 31) / 32);
-  transpose_u16_kernel<<<tg, dim3(32, 8), 0, st>>>(b.rb.off, b.rb.offT, g.r.nt_s, g.r.nt_d + 1, nullptr, 0u);
+  launch_transpose_u16(b.rb.off, b.rb.offT, g.r.nt_s, g.r.nt_d + 1, nullptr, 0u, st);
   bin_serve_kernel<kXbVF><<<serve_grid(g.r.nt_d), kTileThreads, 0, st>>>(g.r, S, b.rb, R, IdxRange::all(g.r.nt_d));
   // replies back to the received order in LDS (writing them there from serve, scattered,
   // measured 4x slower: profiles/r02_xd)

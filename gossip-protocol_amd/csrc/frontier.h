@@ -31,6 +31,12 @@ struct FrontierBufs {
   uint8_t* dirtyP;    // [ceil(N/64)] group g has a pull delta
   uint32_t glog;      // g = 1 << glog nodes per summary bit
   uint32_t summ_words;
+  // Mid-level summary (one shard, 2^25 < N <= 2^30: the exact bitmaps no longer fit an XCD's
+  // L2): bit b = some rare node in [b*g2, (b+1)*g2), g2 = 1 << g2log (8 up to 2^27 nodes), at
+  // most 2 MiB so it stays L2-resident; a peer that hits the LDS summary is tested here before
+  // its exact bitmap word is fetched from the MALL / HBM.  Null: not kept.
+  uint32_t* summ2;
+  uint32_t g2log, summ2_words;
   uint64_t id0;       // global id of node 0 of these arrays (a shard's first node; 0 on one GPU): the hash uses global ids
 };
 
@@ -42,10 +48,13 @@ void frontier_carve(uint64_t N, void* base, FrontierBufs* f);
 // N-node bitmap pair: maj 0 -> f.nzb, maj 1 -> not f.fullb.  No early exit.
 hipError_t launch_frontier_summary(const FrontierBufs& f, uint64_t N, uint32_t maj, hipStream_t st);
 
+// how a sparse round's push deltas reach its commit (launch_frontier_round)
+constexpr uint32_t kSparseFlags = 0, kSparseAllD = 1, kSparseDirect = 2;
+
 // The commit half of a sparse round on its own: S |= D | P for the dirty (or,
-// all_d, every) groups, D/P/flags cleared, bitmaps and running totals updated.
+// kSparseAllD, every) groups, D/P/flags cleared, bitmaps and running totals updated.
 hipError_t launch_frontier_commit(const FrontierBufs& f, uint64_t* S, uint64_t N, uint64_t* partial, uint32_t R,
-                                  bool all_d, uint32_t flags, hipStream_t st);
+                                  uint32_t dmode, uint32_t flags, hipStream_t st);
 
 // Absolute stats of S into partial (zeroed by the caller) + both bitmaps.
 hipError_t launch_frontier_rebuild(const FrontierBufs& f, const uint64_t* S, uint64_t N, uint64_t* partial,
@@ -62,12 +71,21 @@ hipError_t launch_frontier_inject(const FrontierBufs& f, uint64_t* S, uint64_t N
 // partial holds the totals of S_t on entry and those of S_{t+1} on exit; the
 // last commit block hands them to the host through rs.  With no rare node the
 // round is a no-op (every kernel returns at once).
-// all_d: the scan does not flag push-dirty groups and the commit reads D of
-// every group instead — cheaper once pushes touch most groups (a random byte
-// store per push costs about as much as the push atomic itself).  Exact either way.
+// dmode (how the push deltas reach the commit; exact in every mode):
+//   kSparseFlags  the scan flags the push-dirty groups, the commit visits those;
+//   kSparseAllD   the scan flags none and the commit reads D of every group —
+//                 cheaper once pushes touch most groups (a random byte store per
+//                 push costs about as much as the push atomic itself);
+//   kSparseDirect (maj = 0 only) pushes into a majority (empty) peer are OR-ed
+//                 straight into S: no kernel of the round reads a majority node's
+//                 S_t (its value is known to be 0), so the round stays synchronous.
+//                 Pushes into rare peers still go to D (flagged).  The commit then
+//                 visits every group once, reads D / P only where flagged and
+//                 recomputes the totals absolutely (S is read once; D is neither
+//                 read nor cleared outside the flagged groups).
 hipError_t launch_frontier_round(const FrontierBufs& f, uint64_t* S, uint64_t N, uint64_t* partial, uint32_t R,
                                  uint32_t k, uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t maj,
-                                 bool all_d, const Faults& fa, uint32_t flags, const RoundSync& rs,
+                                 uint32_t dmode, const Faults& fa, uint32_t flags, const RoundSync& rs,
                                  hipStream_t st);
 
 }  // namespace gossip

@@ -96,9 +96,39 @@ __device__ __forceinline__ uint64_t rare_count(const uint64_t* partial, uint64_t
   return maj ? N - partial[0] : partial[4 + R];
 }
 
+// mid-level summary word s (32 bits of g2 <= 64 nodes each) from the exact bitmap
+template <int MAJ>
+__device__ __forceinline__ void summ2_body(const FrontierBufs& f, uint32_t s, uint64_t N) {
+  if (s >= f.summ2_words) return;
+  const uint64_t nwords = (N + 63) >> 6;
+  const uint32_t g2 = 1u << f.g2log, per = 64 / g2;  // summary bits per exact word
+  const uint64_t gm = g2 == 64 ? ~0ull : ((1ull << g2) - 1ull);
+  const uint64_t w0 = (uint64_t)s * 32 / per;
+  uint32_t out = 0;
+  for (uint32_t i = 0; i < 32 / per; ++i) {
+    const uint64_t w = w0 + i;
+    if (w >= nwords) break;
+    const uint64_t x = rare_word<MAJ>(f, w, N);
+    if (!x) continue;
+    for (uint32_t q = 0; q < per; ++q)
+      if ((x >> (q * g2)) & gm) out |= 1u << (i * per + q);
+  }
+  f.summ2[s] = out;
+}
+
+// blocks [0, summ_words / 256): the LDS summary; the rest: the mid-level summary (summ2)
 __global__ __launch_bounds__(256) void frontier_summary_kernel(FrontierBufs f, uint64_t N, const uint64_t* partial,
                                                                 uint32_t R, uint32_t maj) {
   if (partial && rare_count(partial, N, R, maj) == 0) return;
+  const uint32_t b1 = (f.summ_words + 255) / 256;
+  if (blockIdx.x >= b1) {
+    const uint32_t s = (blockIdx.x - b1) * 256 + threadIdx.x;
+    if (maj)
+      summ2_body<1>(f, s, N);
+    else
+      summ2_body<0>(f, s, N);
+    return;
+  }
   if (maj)
     summary_body<1>(f, N);
   else
@@ -112,10 +142,11 @@ __global__ __launch_bounds__(256) void frontier_summary_kernel(FrontierBufs f, u
 // (the bitmap is L2-resident; S is not).  Pull deltas belong to the node's own
 // lane and are plain stores to P; push deltas are atomic ORs into D.
 template <int MAJ, int MODE, bool FAULTS>  // FAULTS: edge loss / partitions active (§2.8)
+// direct (kSparseDirect, MAJ 0): pushes into majority peers go to Sw (= S) instead of D.
 __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const FrontierBufs& f,
-                                          const uint64_t* __restrict__ S, uint64_t N, uint32_t R, uint32_t k,
-                                          uint32_t t, uint32_t key0, uint32_t key1, uint64_t per_block,
-                                          bool mark_d, const Faults& fa) {
+                                          const uint64_t* __restrict__ S, uint64_t* Sw, uint64_t N, uint32_t R,
+                                          uint32_t k, uint32_t t, uint32_t key0, uint32_t key1, uint64_t per_block,
+                                          bool mark_d, bool direct, const Faults& fa) {
   const uint32_t* summ = (const uint32_t*)summ4;
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t n4 = (f.summ_words + 3) / 4;
@@ -173,7 +204,21 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
         if (!__ballot(any)) continue;
       }
       // 2. summary hits: exact test in the rare bitmap (2 MiB at 2^24 nodes, L2-resident)
-      // (all probes issued before any is consumed: one wait for the lot)
+      // (all probes issued before any is consumed: one wait for the lot); past 2^25 nodes
+      // the L2-resident mid-level summary first, so fewer probes reach the exact bitmap
+      if (glog && f.summ2) {
+        uint32_t sw[kScanUnroll][4];
+#pragma unroll
+        for (int u = 0; u < kScanUnroll; ++u)
+#pragma unroll
+          for (uint32_t j = 0; j < 4; ++j)
+            sw[u][j] = ((hit[u] >> j) & 1u) ? f.summ2[pp[u][j] >> (f.g2log + 5)] : 0u;
+#pragma unroll
+        for (int u = 0; u < kScanUnroll; ++u)
+#pragma unroll
+          for (uint32_t j = 0; j < 4; ++j)
+            if (!((sw[u][j] >> ((pp[u][j] >> f.g2log) & 31u)) & 1u)) hit[u] &= ~(1u << j);
+      }
       if (glog) {
         uint64_t rw[kScanUnroll][4];
 #pragma unroll
@@ -225,6 +270,10 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j)
           if (dpush[u][j]) {
+            if (MAJ == 0 && direct && !((hit[u] >> j) & 1u)) {  // an empty peer: nobody reads its S_t
+              atomicOr((unsigned long long*)&Sw[pp[u][j]], (unsigned long long)dpush[u][j]);
+              continue;
+            }
             atomicOr((unsigned long long*)&f.D[pp[u][j]], (unsigned long long)dpush[u][j]);
             if (mark_d) f.dirtyD[pp[u][j] >> 6] = 1;
           }
@@ -245,13 +294,16 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
             const uint32_t p = peer_from_word(lane_of(r4, j & 3u), nm1, n);
             if (FAULTS && edge_lost(fa, rc, p, lane_of(lw, j & 3u))) continue;
             bool rp = summ_bit(p);
+            if (rp && glog && f.summ2) rp = (f.summ2[p >> (f.g2log + 5)] >> ((p >> f.g2log) & 31u)) & 1u;
             if (rp && glog) rp = (rare_word<MAJ>(f, p >> 6, N) >> (p & 63u)) & 1ull;
             if (!rn[u] && !rp) continue;  // both ends majority: nothing moves
             const uint64_t v = rp ? S[p] : maj;
             if (kPull) acc |= v;
             if (kPush) {
               const uint64_t d = x[u] & ~v;
-              if (d) {
+              if (d && MAJ == 0 && direct && !rp) {
+                atomicOr((unsigned long long*)&Sw[p], (unsigned long long)d);
+              } else if (d) {
                 atomicOr((unsigned long long*)&f.D[p], (unsigned long long)d);
                 if (mark_d) f.dirtyD[p >> 6] = 1;
               }
@@ -275,18 +327,18 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
 }
 
 template <int MODE, bool FAULTS>
-__global__ __launch_bounds__(kScanThreads, GOSSIP_SCAN_WAVES) void frontier_scan_kernel(FrontierBufs f, const uint64_t* __restrict__ S,
+__global__ __launch_bounds__(kScanThreads, GOSSIP_SCAN_WAVES) void frontier_scan_kernel(FrontierBufs f, uint64_t* S,
                                                                       uint64_t N, uint32_t R, uint32_t k, uint32_t t,
                                                                       uint32_t key0, uint32_t key1, uint64_t per_block,
                                                                       const uint64_t* partial, uint32_t maj,
-                                                                      uint32_t mark_d, Faults fa) {
+                                                                      uint32_t mark_d, uint32_t direct, Faults fa) {
   __shared__ uint4 summ4[kSummBits / 128];
   __shared__ uint64_t rws[kRwWords];
   if (rare_count(partial, N, R, maj) == 0) return;  // converged (or nothing injected): nothing moves
   if (maj)
-    scan_body<1, MODE, FAULTS>(summ4, rws, f, S, N, R, k, t, key0, key1, per_block, mark_d != 0, fa);
+    scan_body<1, MODE, FAULTS>(summ4, rws, f, S, S, N, R, k, t, key0, key1, per_block, mark_d != 0, false, fa);
   else
-    scan_body<0, MODE, FAULTS>(summ4, rws, f, S, N, R, k, t, key0, key1, per_block, mark_d != 0, fa);
+    scan_body<0, MODE, FAULTS>(summ4, rws, f, S, S, N, R, k, t, key0, key1, per_block, mark_d != 0, direct != 0, fa);
 }
 
 // Stats of one 64-node group whose words went from old to nw (old == 0 in a
@@ -361,11 +413,14 @@ __global__ __launch_bounds__(kCommitThreads) void frontier_rebuild_kernel(Fronti
 
 // K2: a wave takes 64 groups, finds the dirty ones by one coalesced load of
 // their flags, and commits kCommitUnroll of them per step: S |= D | P in
-// place, D, P and the flags back to zero, bitmaps and stats deltas.  all_d:
-// every group's D is read (the scan kept no push flags).
+// place, D, P and the flags back to zero, bitmaps and stats deltas.  dmode
+// kSparseAllD: every group's D is read (the scan kept no push flags);
+// kSparseDirect: every group is visited (majority nodes took pushes in S), D / P
+// read where flagged, and the totals are absolute (partial zeroed before).
 __global__ __launch_bounds__(kCommitThreads) void frontier_commit_kernel(FrontierBufs f, uint64_t* __restrict__ S,
                                                                           uint64_t N, uint64_t* __restrict__ partial,
-                                                                          uint32_t R, uint32_t flags, uint32_t all_d) {
+                                                                          uint32_t R, uint32_t flags, uint32_t dmode) {
+  const bool all_d = dmode == kSparseAllD, abs_t = dmode == kSparseDirect;
   __shared__ uint32_t cnt[64];
   __shared__ uint64_t red[3][kCommitThreads / 64];
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -382,7 +437,7 @@ __global__ __launch_bounds__(kCommitThreads) void frontier_commit_kernel(Frontie
     if (fd && !all_d) f.dirtyD[gl] = 0;
     if (fp) f.dirtyP[gl] = 0;
     const uint64_t mD = __ballot(fd != 0), mP = __ballot(fp != 0);
-    uint64_t mask = mD | mP;
+    uint64_t mask = abs_t ? __ballot(gv) : (mD | mP);
     while (mask) {
       uint32_t gi[kCommitUnroll];
       uint32_t cntg = 0;
@@ -417,7 +472,7 @@ __global__ __launch_bounds__(kCommitThreads) void frontier_commit_kernel(Frontie
         if (valid && ((chg >> sh) & 0xFFull)) S[n] = nw;
         if (valid && ((dz >> sh) & 0xFFull)) f.D[n] = 0;
         if (valid && ((pz >> sh) & 0xFFull)) f.P[n] = 0;
-        gs.add(f, g, n, valid, old[u], nw, fm, do_hash, lane);
+        gs.add(f, g, n, valid, abs_t ? 0ull : old[u], nw, fm, do_hash, lane);
       }
     }
   }
@@ -468,11 +523,23 @@ namespace {
 size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 }  // namespace
 
+// mid-level summary: g2 (log) and u32 words; 0 words below 2^25 or past 2^30 nodes
+uint32_t frontier_g2log(uint64_t N) {
+  uint32_t l = 3;
+  while ((N >> l) > (1ull << 24)) ++l;  // at most 2^24 bits (2 MiB)
+  return l;
+}
+uint32_t frontier_summ2_words(uint64_t N) {
+  if (N <= (1ull << 25) || N > (1ull << 30)) return 0;
+  return (uint32_t)((((N + (1ull << frontier_g2log(N)) - 1) >> frontier_g2log(N)) + 31) / 32);
+}
+
 size_t frontier_bytes(uint64_t N) {
   const size_t nwords = (N + 63) / 64;
   const uint32_t glog = frontier_glog(N);
   const size_t sw = ((((N + (1ull << glog) - 1) >> glog) + 127) / 128) * 4;  // u32 words, uint4-padded
-  return 2 * al256(nwords * 8) + al256(sw * 4) + 2 * al256(N * 8) + 2 * al256(nwords);
+  return 2 * al256(nwords * 8) + al256(sw * 4) + 2 * al256(N * 8) + 2 * al256(nwords) +
+         al256((size_t)frontier_summ2_words(N) * 4);
 }
 
 void frontier_carve(uint64_t N, void* base, FrontierBufs* f) {
@@ -493,21 +560,28 @@ void frontier_carve(uint64_t N, void* base, FrontierBufs* f) {
   f->dirtyD = (uint8_t*)p;
   p += al256(nwords);
   f->dirtyP = (uint8_t*)p;
+  p += al256(nwords);
+  f->g2log = frontier_g2log(N);
+  f->summ2_words = frontier_summ2_words(N);
+  f->summ2 = f->summ2_words ? (uint32_t*)p : nullptr;
 }
 
 hipError_t launch_frontier_summary(const FrontierBufs& f, uint64_t N, uint32_t maj, hipStream_t st) {
   if (N == 0) return hipSuccess;  // a shard without nodes
-  frontier_summary_kernel<<<(f.summ_words + 255) / 256, 256, 0, st>>>(f, N, nullptr, 0, maj);
+  FrontierBufs f1 = f;
+  f1.summ2 = nullptr;  // (sharded scans keep no mid-level summary)
+  f1.summ2_words = 0;
+  frontier_summary_kernel<<<(f.summ_words + 255) / 256, 256, 0, st>>>(f1, N, nullptr, 0, maj);
   return hipGetLastError();
 }
 
 hipError_t launch_frontier_commit(const FrontierBufs& f, uint64_t* S, uint64_t N, uint64_t* partial, uint32_t R,
-                                  bool all_d, uint32_t flags, hipStream_t st) {
+                                  uint32_t dmode, uint32_t flags, hipStream_t st) {
   if (N == 0) return hipSuccess;  // a shard without nodes
   const uint64_t wchunks = (((N + 63) >> 6) + 63) >> 6;  // 64-group chunks, one per wave
   const uint64_t cblocks = (wchunks + kCommitThreads / 64 - 1) / (kCommitThreads / 64);
   frontier_commit_kernel<<<(uint32_t)(cblocks < 4096 ? cblocks : 4096), kCommitThreads, 0, st>>>(f, S, N, partial,
-                                                                                                 R, flags, all_d);
+                                                                                                 R, flags, dmode);
   return hipGetLastError();
 }
 
@@ -528,17 +602,19 @@ hipError_t launch_frontier_inject(const FrontierBufs& f, uint64_t* S, uint64_t N
 
 hipError_t launch_frontier_round(const FrontierBufs& f, uint64_t* S, uint64_t N, uint64_t* partial, uint32_t R,
                                  uint32_t k, uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t maj,
-                                 bool all_d, const Faults& fa, uint32_t flags, const RoundSync& rs,
+                                 uint32_t dmode, const Faults& fa, uint32_t flags, const RoundSync& rs,
                                  hipStream_t st) {
   if (N == 0) return hipSuccess;  // a shard without nodes
-  frontier_summary_kernel<<<(f.summ_words + 255) / 256, 256, 0, st>>>(f, N, partial, R, maj);
+  if (maj != 0 && dmode == kSparseDirect) dmode = kSparseAllD;  // (a full peer takes no push)
+  frontier_summary_kernel<<<(f.summ_words + 255) / 256 + (f.summ2_words + 255) / 256, 256, 0, st>>>(f, N, partial, R,
+                                                                                                   maj);
   const uint64_t chunks = (N + kScanThreads - 1) / kScanThreads;
   const uint32_t grid = (uint32_t)(chunks < kScanGrid ? chunks : kScanGrid);
   // contiguous node range per block, a multiple of the block width (so lanes map to bitmap bits)
   const uint64_t per = ((N + grid - 1) / grid + kScanThreads - 1) / kScanThreads * kScanThreads;
 #define GOSSIP_SCAN(MODE, FAULTS)                                                                           \
   frontier_scan_kernel<MODE, FAULTS><<<grid, kScanThreads, 0, st>>>(f, S, N, R, k, t, key0, key1, per, partial, \
-                                                                    maj, !all_d, fa)
+                                                                    maj, dmode != kSparseAllD, dmode == kSparseDirect, fa)
   const bool faults = fa.any();
   switch (mode) {
     case 1: if (faults) GOSSIP_SCAN(1, true); else GOSSIP_SCAN(1, false); break;
@@ -547,7 +623,12 @@ hipError_t launch_frontier_round(const FrontierBufs& f, uint64_t* S, uint64_t N,
     default: return hipErrorInvalidValue;
   }
 #undef GOSSIP_SCAN
-  const hipError_t ce = launch_frontier_commit(f, S, N, partial, R, all_d, flags, st);
+  // absolute totals: after the scan (it reads the rare count), before the commit adds to them
+  if (dmode == kSparseDirect) {
+    const hipError_t me = hipMemsetAsync(partial, 0, (size_t)rs.plen * 8, st);
+    if (me != hipSuccess) return me;
+  }
+  const hipError_t ce = launch_frontier_commit(f, S, N, partial, R, dmode, flags, st);
   return ce;  // the engine enqueues the round's snapshot (round.h) after its timing event
 }
 

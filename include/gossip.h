@@ -135,6 +135,10 @@ int gossip_set_stream(gossip_engine_t* eng, void* hip_stream);
  *                  this fraction of N (default 1/16; sharded 1/4, or 1/25 when the dense
  *                  rounds are exchange rounds; < 0 never, >= 1 always)
  *   "alld_frac"    sparse rounds commit every group's D once k x rare >= this x N
+ *   "sparse_direct"  such rounds with an empty majority OR the pushes into empty peers
+ *                  straight into the state and recompute the totals (default 1; 0: into D)
+ *   "mid_frac"     past 2^25 nodes sparse rounds test a peer in the L2-resident mid-level
+ *                  summary once this share of peers would hit the LDS summary (default 0.9)
  *   "filter_frac"  dense rounds drop edges by the peer's class above this empty/full fraction
  *                  (default 0.3 up to 2^25 nodes; past that off: the probes miss the L2)
  *   "xd_filter_frac"  exchange dense rounds likewise (default 0.6; >= 1 never)

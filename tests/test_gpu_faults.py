@@ -20,7 +20,8 @@ CASES = [  # mode, k, R, N, seed, edge_loss, partitions
 IDS = ["pushpull-loss", "push-loss-parts", "pull-loss-parts", "pushpull-k6"]
 PATHS = {"auto": (0, {}), "dense": (FLAG_DENSE, {}), "dense_filter": (0, {"sparse_frac": -1, "filter_frac": 0}),
          "sparse": (0, {"sparse_frac": 1.0, "alld_frac": 1e30}),
-         "sparse_alld": (0, {"sparse_frac": 1.0, "alld_frac": 0}), "direct": (FLAG_DIRECT, {})}
+         "sparse_alld": (0, {"sparse_frac": 1.0, "alld_frac": 0, "sparse_direct": 0}),
+         "sparse_direct": (0, {"sparse_frac": 1.0, "alld_frac": 0}), "direct": (FLAG_DIRECT, {})}
 
 
 def _oracle(case, rounds=200):
