@@ -141,6 +141,9 @@ constexpr uint16_t kDstVZ = 1u << 14, kDstVF = 1u << 15, kSrcVF = 1u << 15;
 #ifndef GOSSIP_ABL_EMIT
 #define GOSSIP_ABL_EMIT 0
 #endif
+#ifndef GOSSIP_EMIT_PK
+#define GOSSIP_EMIT_PK 0  // big-region emit keeps each sender's peers in LDS between its passes (0: draws twice)
+#endif
 #ifndef GOSSIP_SPLIT_IDS
 #define GOSSIP_SPLIT_IDS 1  // 0: u32 ids below kMaxTilesD tiles (A/B; big regions always split)
 #endif
@@ -290,7 +293,12 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
                                                                   Faults fa, EmitRange er) {
   constexpr bool SHARD = V == 1 || V == 2;
   constexpr bool STAGE = V == 0 || V == 1;  // sender values staged in LDS
-  constexpr bool BIG = V == 4;               // packed 16-bit tile counters, double regions
+  constexpr bool BIG = V == 4 || V == 5;     // packed 16-bit tile counters, double regions
+  // V = 5: BIG without faults, k <= 2 (the launch checks): the count pass keeps each sender's
+  // peers and edge directions in the LDS staging room ({p0, p1, dirs} in a u64: p < 2^27), so
+  // the placement pass draws no Philox again (one cipher per sender instead of two)
+  constexpr bool PKC = V == 5;
+  constexpr bool PK = PKC;
   constexpr uint32_t kMaxT = V >= 2 ? kSbMaxTiles : kMaxTilesD;
   constexpr uint32_t kMaxS = BIG ? 2 * kMaxSenders : kMaxSenders;
   __shared__ uint32_t cur[BIG ? kMaxT / 2 : kMaxT];
@@ -423,6 +431,30 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
           tile_of(pr[q * KREG + j], &tl, &pl);
           count_tile(tl);
         }
+  } else if (PKC && PK) {
+    uint64_t* pkl = (uint64_t*)st_ids;  // kMaxS u64 = the staging room, free until placement
+#pragma unroll
+    for (uint32_t q = 0; q < kQ; ++q) {
+      const uint32_t i = tid + q * kEmitThreads;
+      uint64_t pk = 0;
+      const uint32_t d = i < nsend ? sender_dirs(mode, v[q], fm) & dmask : 0u;
+      if (d) {
+        const uint32_t n = (uint32_t)(snd0 + base + i);
+        const u32x4 x = philox4x32_10(u32x4{n, t, 0u, 0u}, key0, key1);
+#pragma unroll
+        for (uint32_t j = 0; j < 2; ++j) {
+          if (j >= g.k) break;
+          const uint32_t p = peer_from_word(lane_of(x, j), nm1, n);
+          uint32_t tl, pl;
+          tile_of(p, &tl, &pl);  // (one shard: always inside)
+          const uint32_t dd = peer_filter(d, p, filt, b.nzb, b.fullb);
+          if (!dd) continue;
+          count_tile(tl);
+          pk |= ((uint64_t)p << (27 * j)) | ((uint64_t)dd << (54 + 2 * j));
+        }
+      }
+      pkl[i] = pk;
+    }
   } else {
     for (uint32_t q = 0; q < kQ; ++q) {
       const uint32_t i = tid + q * kEmitThreads;
@@ -465,6 +497,25 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
         tile_of(pr[q * KREG + j], &tl, &pl);
         const uint32_t pos = place_tile(tl);
         st_ids[pos] = pl | (i << kTileDLog) | dir_flags(d);
+      }
+    }
+  } else if (PKC && PK) {
+    uint64_t mine[kQ];
+#pragma unroll
+    for (uint32_t q = 0; q < kQ; ++q) mine[q] = ((const uint64_t*)st_ids)[tid + q * kEmitThreads];
+    __syncthreads();  // every sender's peers are read before any record takes the room
+#pragma unroll
+    for (uint32_t q = 0; q < kQ; ++q) {
+      const uint32_t i = tid + q * kEmitThreads;
+#pragma unroll
+      for (uint32_t j = 0; j < 2; ++j) {
+        const uint32_t dd = (uint32_t)(mine[q] >> (54 + 2 * j)) & 3u;
+        if (!dd) continue;
+        const uint32_t p = (uint32_t)(mine[q] >> (27 * j)) & ((1u << 27) - 1u);
+        uint32_t tl, pl;
+        tile_of(p, &tl, &pl);
+        const uint32_t pos = place_tile(tl);
+        st_ids[pos] = pl | (i << kTileDLog) | dir_flags(dd);
       }
     }
   } else {
@@ -519,8 +570,17 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
     }
     __syncthreads();  // every staged id is out
     uint64_t* sv = (uint64_t*)st_ids;  // 2 * kRecPerRegion u32 = kMaxS u64
+    if (PKC && PK) {  // v[] was let go after the count pass (its registers held the peers): reread
 #pragma unroll
-    for (uint32_t q = 0; q < kQ; ++q) sv[tid + q * kEmitThreads] = v[q];
+      for (uint32_t q = 0; q < kQ; ++q) {
+        const uint32_t i = tid + q * kEmitThreads;
+        const uint64_t x = S[snd0 + base + min(i, nsend - 1)];
+        sv[i] = i < nsend ? x : 0ull;
+      }
+    } else {
+#pragma unroll
+      for (uint32_t q = 0; q < kQ; ++q) sv[tid + q * kEmitThreads] = v[q];
+    }
     __syncthreads();
     uint32_t* gprec = b.prec + (size_t)s * g.rp * 3;
 #pragma unroll 4
@@ -1087,10 +1147,12 @@ hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, 
   } else {                                                                \
     if (fa.any()) GOSSIP_EMIT(0, true, VV); else GOSSIP_EMIT(0, false, VV); \
   }
-  if (g.ts > kMaxSenders || g.rp > kRecPerRegion) {  // make_bin_geom(big): V = 4
-    // the draws are redone in the placement pass: 16 senders per lane keep no room for
-    // their peers in registers (KREG = 2 spills 78 VGPRs)
-    if (fa.any()) GOSSIP_EMIT(0, true, 4); else GOSSIP_EMIT(0, false, 4);
+  if (g.ts > kMaxSenders || g.rp > kRecPerRegion) {  // make_bin_geom(big): V = 4, 5
+    // 16 senders per lane keep no room for their peers in registers (KREG = 2 spills 78
+    // VGPRs): V = 5 keeps them in LDS between the passes, V = 4 draws them again
+    if (fa.any()) GOSSIP_EMIT(0, true, 4);
+    else if (GOSSIP_EMIT_PK && g.k <= 2) GOSSIP_EMIT(0, false, 5);
+    else GOSSIP_EMIT(0, false, 4);
   } else if (g.nt_d <= kMaxTilesD) {
     GOSSIP_EMIT_V(0)
   } else {
