@@ -142,7 +142,7 @@ constexpr uint16_t kDstVZ = 1u << 14, kDstVF = 1u << 15, kSrcVF = 1u << 15;
 #define GOSSIP_ABL_EMIT 0
 #endif
 #ifndef GOSSIP_EMIT_PK
-#define GOSSIP_EMIT_PK 0  // big-region emit keeps each sender's peers in LDS between its passes (0: draws twice)
+#define GOSSIP_EMIT_PK 1  // big-region emit keeps each sender's peers in LDS between its passes (0: draws twice)
 #endif
 #ifndef GOSSIP_SPLIT_IDS
 #define GOSSIP_SPLIT_IDS 1  // 0: u32 ids below kMaxTilesD tiles (A/B; big regions always split)

@@ -148,7 +148,7 @@ struct gossip_engine {
   bool sx = false;
   bool sx_valid = false;    // partial_d holds the owned nodes' totals and lf's bitmaps are exact
   bool gtot_valid = false;  // gtot = global totals of S_t (from the driver's all-reduce)
-  bool sx_planned = false, sx_alld = false, last_sparse = false;
+  bool sx_planned = false, sx_alld = false, sx_mid = false, last_sparse = false;
   uint32_t sx_maj = 0;
   std::vector<uint64_t> gtot;
   SxGeom sg{};
@@ -1545,6 +1545,11 @@ int gossip_sharded_plan(gossip_engine_t* e, const uint64_t* total, int32_t* kind
   e->sx_planned = choose_sparse(e, est_of(e, e->gtot.data()), &maj, &all_d);
   e->sx_maj = maj;
   e->sx_alld = all_d;
+  {  // the mid-level summary of the global rare bitmap (choose_sparse's rule, sharded summary)
+    const Est x = est_of(e, e->gtot.data());
+    const double r = std::min(1.0, std::min(x.nz, (double)e->N - x.full) / (double)e->N);
+    e->sx_mid = e->sb.gsum.summ2 && 1.0 - std::pow(1.0 - r, (double)(1u << e->sb.gsum.glog)) >= e->mid_frac;
+  }
   e->xd_planned = !e->sx_planned && e->xd && e->xd_shards && e->G >= e->xd_shards;
   // exchange rounds drop the one-way edges into empty / full peers when many nodes are (the
   // global totals are exact: no prediction), after an all-gather of the class bitmaps
@@ -1595,9 +1600,9 @@ int gossip_sparse_scan(gossip_engine_t* e, const uint64_t* counts, void** send, 
   HIP_OK(e, hipMemcpyAsync(e->sb.cbase, cb, (e->G + 1) * 8, hipMemcpyHostToDevice, e->stream));
   if (int rc = timer_begin(e, 0)) return rc;
   const uint64_t rare = cb[e->G];
-  HIP_OK(e, sx_index(e->sg, e->sb, e->rare_recv, e->sx_stride, rare, e->stream));
+  HIP_OK(e, sx_index(e->sg, e->sb, e->rare_recv, e->sx_stride, rare, e->stream, e->sx_mid));
   HIP_OK(e, sx_scan(e->sg, e->sb, e->lf, e->S, e->rare_recv, e->sx_stride, rare, e->t, e->key0, e->key1, e->mode,
-                    e->sx_maj, e->sx_alld, e->fa, e->stream));
+                    e->sx_maj, e->sx_alld, e->fa, e->stream, e->sx_mid));
   if (int rc = timer_end(e, 0)) return rc;
   // (the copy below lands in cb's pinned buffer after the copy that read it: same stream)
   HIP_OK(e, hipMemcpyAsync(e->sx_host, e->sb.msg_cnt, (e->G + 1) * 4, hipMemcpyDeviceToHost, e->stream));

@@ -41,11 +41,15 @@ struct FrontierBufs {
 };
 
 uint32_t frontier_glog(uint64_t N);
+// mid-level summary of N nodes: log2 of its group size, its u32 words (0: none below 2^25 or past 2^30 nodes)
+uint32_t frontier_g2log(uint64_t N);
+uint32_t frontier_summ2_words(uint64_t N);
 size_t frontier_bytes(uint64_t N);
 void frontier_carve(uint64_t N, void* base, FrontierBufs* f);
 
 // Coarse summary (f.summ, 1 bit per 2^f.glog nodes) of the rare set of an
-// N-node bitmap pair: maj 0 -> f.nzb, maj 1 -> not f.fullb.  No early exit.
+// N-node bitmap pair: maj 0 -> f.nzb, maj 1 -> not f.fullb, and the mid-level
+// summary f.summ2 when f has one.  No early exit.
 hipError_t launch_frontier_summary(const FrontierBufs& f, uint64_t N, uint32_t maj, hipStream_t st);
 
 // how a sparse round's push deltas reach its commit (launch_frontier_round)

@@ -568,10 +568,8 @@ void frontier_carve(uint64_t N, void* base, FrontierBufs* f) {
 
 hipError_t launch_frontier_summary(const FrontierBufs& f, uint64_t N, uint32_t maj, hipStream_t st) {
   if (N == 0) return hipSuccess;  // a shard without nodes
-  FrontierBufs f1 = f;
-  f1.summ2 = nullptr;  // (sharded scans keep no mid-level summary)
-  f1.summ2_words = 0;
-  frontier_summary_kernel<<<(f.summ_words + 255) / 256, 256, 0, st>>>(f1, N, nullptr, 0, maj);
+  const uint32_t s2 = f.summ2 ? f.summ2_words : 0u;  // the mid-level summary too when f has one
+  frontier_summary_kernel<<<(f.summ_words + 255) / 256 + (s2 + 255) / 256, 256, 0, st>>>(f, N, nullptr, 0, maj);
   return hipGetLastError();
 }
 

@@ -61,12 +61,13 @@ hipError_t sx_compact(const SxGeom& g, const SxBufs& b, const FrontierBufs& lf, 
 // 3. global index from the gathered lists: recv[q * stride + i], i < counts of shard q
 //    (b.cbase must hold the prefix of the counts)
 //    rare = total rare nodes; small totals skip the O(N) per-word ranks and summary pass
+//    mid: also the mid-level summary of the global bitmap (past 2^25 nodes, saturated rounds)
 hipError_t sx_index(const SxGeom& g, const SxBufs& b, const SxItem* recv, uint64_t stride, uint64_t rare,
-                    hipStream_t st);
+                    hipStream_t st, bool mid = false);
 // 4. scan of the owned nodes; messages grouped by owner into b.msg_out, counts in b.msg_cnt
 hipError_t sx_scan(const SxGeom& g, const SxBufs& b, const FrontierBufs& lf, const uint64_t* S, const SxItem* recv,
                    uint64_t stride, uint64_t rare, uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode,
-                   uint32_t maj, bool all_d, const Faults& fa, hipStream_t st);
+                   uint32_t maj, bool all_d, const Faults& fa, hipStream_t st, bool mid = false);
 // 6. received pushes into D (and the push-dirty flags unless all_d)
 hipError_t sx_apply(const FrontierBufs& lf, const SxItem* in, uint64_t n, bool all_d, hipStream_t st);
 

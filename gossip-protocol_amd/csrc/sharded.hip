@@ -124,6 +124,8 @@ struct ScanArgs {
   const uint64_t* cbase;
   const uint32_t* gsumm;
   uint32_t gglog, gsumm_words;
+  const uint32_t* gsumm2;  // mid-level summary of grb (frontier.h FrontierBufs::summ2), or null
+  uint32_t g2log;
   SxItem* msg;          // block b's messages at msg[b * seg_cap, ...)
   uint32_t* blk_cnt;    // [grid] messages per block
   uint64_t seg_cap;     // k * per_block: every owned node sends at most k pushes
@@ -231,7 +233,21 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, uint32_t*
         for (int u = 0; u < kScanUnroll; ++u) any = any || rn[u] || hit[u] != 0u || (k > 4 && act[u]);  // k > 4: no hits yet
         if (!__ballot(any)) continue;
       }
-      // 2. exact probes in the global rare bitmap (all issued, then consumed)
+      // 2. exact probes in the global rare bitmap (all issued, then consumed); in saturated
+      // rounds past 2^25 nodes the L2-resident mid-level summary first
+      if (a.gsumm2) {
+        uint32_t sw[kScanUnroll][4];
+#pragma unroll
+        for (int u = 0; u < kScanUnroll; ++u)
+#pragma unroll
+          for (uint32_t j = 0; j < 4; ++j)
+            sw[u][j] = ((hit[u] >> j) & 1u) ? a.gsumm2[pp[u][j] >> (a.g2log + 5)] : 0u;
+#pragma unroll
+        for (int u = 0; u < kScanUnroll; ++u)
+#pragma unroll
+          for (uint32_t j = 0; j < 4; ++j)
+            if (!((sw[u][j] >> ((pp[u][j] >> a.g2log) & 31u)) & 1u)) hit[u] &= ~(1u << j);
+      }
       uint64_t rw[kScanUnroll][4];
 #pragma unroll
       for (int u = 0; u < kScanUnroll; ++u)
@@ -305,6 +321,7 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, uint32_t*
             const bool lost = FAULTS && edge_lost(a.fa, rc, p, lane_of(lw, j & 3u));
             uint64_t w = 0;
             bool rp = summ_bit(p);
+            if (rp && a.gsumm2) rp = (a.gsumm2[p >> (a.g2log + 5)] >> ((p >> a.g2log) & 31u)) & 1u;
             if (rp) {
               w = a.grb[p >> 6];
               rp = (w >> (p & 63u)) & 1ull;
@@ -536,8 +553,8 @@ size_t sx_bytes(const SxGeom& g) {
   const size_t tmp = std::max(scan_tmp_bytes(nwl + 1), scan_tmp_bytes(nwg + 1));
   const uint64_t cap = msg_cap(g);
   return 2 * al256((nwl + 1) * 4) + al256(g.Nl * sizeof(SxItem)) + al256(nwg * 8) + 2 * al256((nwg + 1) * 4) +
-         al256(sw * 4) + al256((g.G + 1) * 8) + 2 * al256(cap * sizeof(SxItem)) + al256((g.G + 2 + kScanGrid) * 4) +
-         al256(g.G * 4) + al256(tmp);
+         al256(sw * 4) + al256((size_t)frontier_summ2_words(g.N) * 4) + al256((g.G + 1) * 8) +
+         2 * al256(cap * sizeof(SxItem)) + al256((g.G + 2 + kScanGrid) * 4) + al256(g.G * 4) + al256(tmp);
 }
 
 void sx_carve(const SxGeom& g, void* base, SxBufs* b) {
@@ -559,6 +576,9 @@ void sx_carve(const SxGeom& g, void* base, SxBufs* b) {
   b->gsum.summ_words = (uint32_t)((((g.N + (1ull << b->gsum.glog) - 1) >> b->gsum.glog) + 127) / 128) * 4;
   b->gsum.nzb = b->grb;
   b->gsum.summ = (uint32_t*)take((size_t)b->gsum.summ_words * 4);
+  b->gsum.g2log = frontier_g2log(g.N);
+  b->gsum.summ2_words = frontier_summ2_words(g.N);
+  b->gsum.summ2 = b->gsum.summ2_words ? (uint32_t*)take((size_t)b->gsum.summ2_words * 4) : nullptr;
   b->cbase = (uint64_t*)take((g.G + 1) * 8);
   b->cap = msg_cap(g);
   b->msg = (SxItem*)take(b->cap * sizeof(SxItem));
@@ -583,7 +603,7 @@ hipError_t sx_compact(const SxGeom& g, const SxBufs& b, const FrontierBufs& lf, 
 bool sx_small_index(uint64_t rare) { return rare <= kSmallIndex; }
 
 hipError_t sx_index(const SxGeom& g, const SxBufs& b, const SxItem* recv, uint64_t stride, uint64_t rare,
-                    hipStream_t st) {
+                    hipStream_t st, bool mid) {
   const uint64_t nwg = (g.N + 63) / 64;
   // grb is 256-B aligned (sx_carve) and padded to 16 B
   zero_kernel<<<grid_for((nwg + 1) / 2, 256, 2048), 256, 0, st>>>((uint4*)b.grb, (nwg + 1) / 2);
@@ -603,12 +623,14 @@ hipError_t sx_index(const SxGeom& g, const SxBufs& b, const SxItem* recv, uint64
   size_t tb = b.tmp_bytes;
   e = hipcub::DeviceScan::ExclusiveSum(b.tmp, tb, b.gcnt, b.gpre, (int)(nwg + 1), st);
   if (e != hipSuccess) return e;
-  return launch_frontier_summary(b.gsum, g.N, 0, st);
+  FrontierBufs gs = b.gsum;
+  if (!mid) gs.summ2 = nullptr;
+  return launch_frontier_summary(gs, g.N, 0, st);
 }
 
 hipError_t sx_scan(const SxGeom& g, const SxBufs& b, const FrontierBufs& lf, const uint64_t* S, const SxItem* recv,
                    uint64_t stride, uint64_t rare, uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode,
-                   uint32_t maj, bool all_d, const Faults& fa, hipStream_t st) {
+                   uint32_t maj, bool all_d, const Faults& fa, hipStream_t st, bool mid) {
   hipError_t e = hipMemsetAsync(b.msg_cnt, 0, (g.G + 2) * 4, st);
   if (e == hipSuccess) e = hipMemsetAsync(b.msg_fill, 0, g.G * 4, st);
   if (e != hipSuccess || g.nown == 0) return e;  // a shard without nodes sends nothing
@@ -623,6 +645,9 @@ hipError_t sx_scan(const SxGeom& g, const SxBufs& b, const FrontierBufs& lf, con
   a.gsumm = b.gsum.summ;
   a.gglog = b.gsum.glog;
   a.gsumm_words = b.gsum.summ_words;
+  // (small indexes build their summary from the items and no mid-level one: few rare nodes)
+  a.gsumm2 = mid && !sx_small_index(rare) ? b.gsum.summ2 : nullptr;
+  a.g2log = b.gsum.g2log;
   a.msg = b.msg;
   a.blk_cnt = b.msg_cnt + g.G + 2;
   a.N = g.N;
