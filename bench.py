@@ -80,25 +80,35 @@ def _omp_run(n_nodes: int, seed: int, threads: int, budget_s: float):
 def cpu_baseline(n_nodes: int, seed: int, budget_s: float = 8.0):
     """The oracle (C restatement of the same rounds, `kind: port`; the reference itself is Go and not
     buildable here) on the host, same workload, bounded samples (whole rounds from the start of the run,
-    about `budget_s` each): OpenMP on every CPU this process may run on (the headline), the job's
-    host-core share (OMP_NUM_THREADS, 16 on the GPU box) beside it, and one thread."""
+    about `budget_s` each): OpenMP on every CPU this process may run on, the job's host-core share
+    (OMP_NUM_THREADS, 16 on the GPU box) and one thread.  The headline `value` / `cores` is the fastest
+    of them (the oracle's random 8-B accesses share one memory system, so more threads can be slower:
+    the baseline is not understated by a thread count that does not pay); all three are listed."""
     nproc = os.cpu_count() or 1
     try:
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = nproc
     share = max(1, min(avail, int(os.environ.get("OMP_NUM_THREADS", avail))))
+    runs = {}
     v, rounds, dt = _omp_run(n_nodes, seed, avail, budget_s)
-    out = {"value": v, "unit": "node-updates/s", "cores": avail, "kind": "port",
-           "nproc": nproc, "affinity_cpus": avail,
-           "sample": f"oracle/gossip_oracle.c, first {rounds} rounds ({dt:.1f} s) of the same {n_nodes}-node "
-                     f"push-pull k=2 R=64 run on {avail} OpenMP threads (every affinity CPU; nproc {nproc})"}
+    runs["all_cpus"] = {"value": v, "cores": avail, "rounds": rounds, "seconds": dt,
+                        "note": f"every affinity CPU (nproc {nproc})"}
     if share != avail:
         vs, rs, ds = _omp_run(n_nodes, seed, share, budget_s)
-        out["host_share"] = {"value": vs, "cores": share, "rounds": rs, "seconds": ds,
-                             "note": "OMP_NUM_THREADS: this job's share of the host"}
+        runs["host_share"] = {"value": vs, "cores": share, "rounds": rs, "seconds": ds,
+                              "note": "OMP_NUM_THREADS: this job's share of the host"}
     v1, rounds1, dt1 = _omp_run(n_nodes, seed, 1, budget_s)
-    out["single_thread"] = {"value": v1, "rounds": rounds1, "seconds": dt1}
+    runs["single_thread"] = {"value": v1, "cores": 1, "rounds": rounds1, "seconds": dt1}
+    best = max(runs, key=lambda k: runs[k]["value"])
+    b = runs[best]
+    counts = ", ".join(f"{r['cores']} threads" for r in runs.values())
+    out = {"value": b["value"], "unit": "node-updates/s", "cores": b["cores"], "kind": "port",
+           "nproc": nproc, "affinity_cpus": avail, "best_of": best,
+           "sample": f"oracle/gossip_oracle.c, first {b['rounds']} rounds ({b['seconds']:.1f} s) of the same "
+                     f"{n_nodes}-node push-pull k=2 R=64 run on {b['cores']} OpenMP threads (the fastest of "
+                     f"{counts})"}
+    out.update(runs)
     return out
 
 
