@@ -35,6 +35,19 @@ namespace gossip {
 namespace {
 
 constexpr int kScanThreads = 1024;
+#ifndef GOSSIP_SCAN_NT
+#define GOSSIP_SCAN_NT 0  // 1: the scan's S gathers and P stores carry the non-temporal hint (A/B)
+#endif
+template <typename T>
+__device__ __forceinline__ T scan_ld(const T* p) {
+  if constexpr (GOSSIP_SCAN_NT != 0) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <typename T>
+__device__ __forceinline__ void scan_st(T* p, T v) {
+  if constexpr (GOSSIP_SCAN_NT != 0) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
 #ifndef GOSSIP_SCAN_GRID
 #define GOSSIP_SCAN_GRID 256
 #endif
@@ -238,9 +251,9 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
 #pragma unroll
       for (int u = 0; u < kScanUnroll; ++u) {
         const uint32_t n = base + u * kScanThreads + tid;
-        x[u] = rn[u] ? S[n] : maj;
+        x[u] = rn[u] ? scan_ld(&S[n]) : maj;
 #pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) vp[u][j] = ((hit[u] >> j) & 1u) ? S[pp[u][j]] : maj;
+        for (uint32_t j = 0; j < 4; ++j) vp[u][j] = ((hit[u] >> j) & 1u) ? scan_ld(&S[pp[u][j]]) : maj;
       }
       // 4. deltas, in registers: every gather above is consumed here, before
       // the first atomic or store below.  (A load consumed after a store was
@@ -319,7 +332,7 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
         const uint32_t n = base + u * kScanThreads + tid;
         const uint64_t pz = __ballot(accs[u] != 0);
         if (!pz) continue;
-        if (n < c1 && ((pz >> (lane & ~7u)) & 0xFFull)) f.P[n] = accs[u];
+        if (n < c1 && ((pz >> (lane & ~7u)) & 0xFFull)) scan_st(&f.P[n], accs[u]);
         if (accs[u]) f.dirtyP[n >> 6] = 1;
       }
     }
