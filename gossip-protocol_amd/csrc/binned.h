@@ -53,6 +53,7 @@ struct BinGeom {
   uint32_t rp;           // records per sender region = ts * k
   uint32_t nt_s, nt_d;   // sender tiles, destination tiles
   uint32_t apply_grid;   // host only: persistent apply blocks (0 = one per tile; gossip_set_param)
+  uint32_t serve_grid;   // host only: persistent serve blocks of one-shard rounds (0 = one per tile)
   uint32_t push_waves;   // push-pull apply: waves [0, push_waves) walk the pushes, the rest the responses
   uint32_t aos;          // push records also packed {value, id} (BinBufs::prec; one shard, big regions)
   uint32_t split;        // one shard: record ids as two u16 arrays (BinBufs::dst / src) instead of ids

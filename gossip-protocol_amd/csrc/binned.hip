@@ -141,6 +141,9 @@ constexpr uint16_t kDstVZ = 1u << 14, kDstVF = 1u << 15, kSrcVF = 1u << 15;
 #ifndef GOSSIP_ABL_EMIT
 #define GOSSIP_ABL_EMIT 0
 #endif
+#ifndef GOSSIP_AOS_SMALL
+#define GOSSIP_AOS_SMALL 0  // 1: packed {value, id} pushes below 4096 tiles too (A/B)
+#endif
 #ifndef GOSSIP_EMIT_PK
 #define GOSSIP_EMIT_PK 1  // big-region emit keeps each sender's peers in LDS between its passes (0: draws twice)
 #endif
@@ -601,7 +604,12 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
     } else {
       rec_st<1>(&gids[e], id);
     }
-    if (STAGE) rec_st<1>(&gvals[e], sval[(id >> kTileDLog) & kIdNMask]);
+    if (STAGE && V == 0 && g.aos) {  // (GOSSIP_AOS_SMALL) the push packed {value, id} as past 2^26 nodes
+      const uint64_t x = sval[(id >> kTileDLog) & kIdNMask];
+      prec_st(&b.prec[3 * ((size_t)s * g.rp + e)], (uint32_t)x, (uint32_t)(x >> 32), id);
+    } else if (STAGE) {
+      rec_st<1>(&gvals[e], sval[(id >> kTileDLog) & kIdNMask]);
+    }
     if (V >= 3) rec_st<1>(&gvals[e], S[base + ((id >> kTileDLog) & kIdNMask)]);
   }
   if constexpr (!BIG) {
@@ -967,7 +975,7 @@ __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, cons
   }
 }
 
-uint32_t serve_grid(uint32_t tiles) { return tiles < kServeGrid ? tiles : kServeGrid; }
+uint32_t serve_grid(uint32_t tiles, uint32_t cap = kServeGrid) { return cap == 0 || tiles < cap ? tiles : cap; }
 
 // K3 — one block per tile X: acc = S_t[X]; OR in the pushes aimed at X (its
 // runs) and the pull responses owed to X's own senders (their regions, read
@@ -1085,12 +1093,13 @@ BinGeom make_bin_geom(uint64_t N, uint32_t k, bool big) {
   g.nt_s = (uint32_t)((N + ts - 1) / ts);
   g.nt_d = (uint32_t)((N + kTileD - 1) / kTileD);
   g.apply_grid = kApplyGrid;
+  g.serve_grid = kServeGrid;
   g.push_waves = N > (1ull << 25) ? kPushWavesBig : kPushWaves;
   // big regions (past kMaxTilesD tiles) make runs of ~4 records, and the apply pass's push
   // walk is bound by the number of distinct lines it fetches: a push packed as one 12-B
   // piece beside the 4-B id (for serve and the reply walk) touches fewer than the two
   // arrays' 16-B + 32-B pieces of a run
-  g.aos = big ? 1u : 0u;
+  g.aos = big || GOSSIP_AOS_SMALL ? 1u : 0u;
   g.split = big || GOSSIP_SPLIT_IDS ? 1u : 0u;  // (sharded geometries clear it: their passes keep u32 ids)
   return g;
 }
@@ -1162,9 +1171,11 @@ hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, 
 #undef GOSSIP_EMIT
   launch_transpose_u16(b.off, b.offT, g.nt_s, g.nt_d + 1, partial, rs.plen, st);
   if ((mode == 2 || mode == 3) && g.split)
-    bin_serve_kernel<kIdVF, true><<<serve_grid(g.nt_d), kTileThreads, 0, st>>>(g, S, b, R, IdxRange::all(g.nt_d));
+    bin_serve_kernel<kIdVF, true><<<serve_grid(g.nt_d, g.serve_grid), kTileThreads, 0, st>>>(g, S, b, R,
+                                                                                          IdxRange::all(g.nt_d));
   else if (mode == 2 || mode == 3)
-    bin_serve_kernel<kIdVF, false><<<serve_grid(g.nt_d), kTileThreads, 0, st>>>(g, S, b, R, IdxRange::all(g.nt_d));
+    bin_serve_kernel<kIdVF, false><<<serve_grid(g.nt_d, g.serve_grid), kTileThreads, 0, st>>>(g, S, b, R,
+                                                                                           IdxRange::all(g.nt_d));
   // in place: K3 of tile X reads and writes only S[X] (push values and pull
   // responses come from the record buffers), and K1/K2 have finished reading S_t
   if (g.aos)
@@ -1191,6 +1202,7 @@ SbGeom make_sb_geom(uint64_t N, uint32_t k, uint64_t lo, uint64_t nown) {
   // region sizes as on one shard (make_bin_geom); peers are drawn over the global id space
   g.p = g.q = make_bin_geom(N, k);
   g.p.split = g.q.split = 0u;
+  g.p.aos = g.q.aos = 0u;  // (the sharded passes keep u32 ids + values)
   g.p.nt_s = (uint32_t)((N + g.p.ts - 1) / g.p.ts);      // every sender
   g.p.nt_d = (uint32_t)((nown + kTileD - 1) / kTileD);   // own tiles
   g.q.nt_s = (uint32_t)((nown + g.q.ts - 1) / g.q.ts);   // own senders
@@ -1657,6 +1669,7 @@ XdGeom make_xd_geom(uint64_t N, uint32_t k, uint64_t Nl, uint64_t lo, uint64_t n
   g.k = k;
   g.s = make_bin_geom(nown ? nown : 1, k);
   g.s.split = 0u;  // exchange items keep u32 ids (p_local | slot << 14 | flags)
+  g.s.aos = 0u;
   while (g.s.ts > 64 && g.s.ts * k > kXdSendRegion) {
     g.s.ts >>= 1;
     --g.s.ts_log;

@@ -135,7 +135,7 @@ struct gossip_engine {
   double xd_filter_frac = 0.6;    // exchange rounds likewise (their probe hits a G-shard class image: G = 8 sweep)
   double alld_frac = 1.0 / 64;    // sparse rounds with k * rare >= alld_frac * N commit every group's D (bench sweep)
   bool sparse_direct = true;      // ... and with an empty majority take the pushes into empty peers in S (kSparseDirect)
-  double mid_frac = 0.9;          // sparse rounds test peers in the mid-level summary once this share hits the LDS one
+  double mid_frac = 0.5;          // sparse rounds test peers in the mid-level summary once this share hits the LDS one
   // pipelined rounds (binned engines): the host picks each round's path from the
   // totals it has read, predicted forward over the rounds still in flight, and
   // stays up to `ahead` rounds in front
@@ -474,19 +474,11 @@ double sparse_frac_of(const gossip_engine* e) {
 // sparse when the smaller rare class is at most sparse_frac * N; maj = which
 // class is rare; all_d once the rare ends' pushes (~k per rare node) reach
 // alld_frac * N (launch_frontier_round)
-bool choose_sparse(const gossip_engine* e, const Est& x, uint32_t* maj, bool* all_d, bool* mid = nullptr) {
+bool choose_sparse(const gossip_engine* e, const Est& x, uint32_t* maj, bool* all_d) {
   if (!e->frontier && !e->sx) return false;
   const double lo = x.nz, hi = (double)e->N - x.full, rare = std::min(lo, hi);
   *maj = hi < lo ? 1u : 0u;
   *all_d = rare * (double)e->k >= e->alld_frac * (double)e->N;
-  if (mid) {
-    // the mid-level summary (FrontierBufs::summ2) pays once most peers hit the LDS summary
-    // (a g-node group holds a rare node w.p. 1 - (1 - r)^g); below that its extra probe
-    // round trip costs more than the exact probes it saves (2^27 nodes: rounds at ~10-70 %
-    // LDS hits +70..165 us, rounds at ~100 % -0.9..1.0 ms; profiles/r03_h)
-    const double r = std::min(1.0, rare / (double)e->N);
-    *mid = e->fb.summ2 && 1.0 - std::pow(1.0 - r, (double)(1u << e->fb.glog)) >= e->mid_frac;
-  }
   return rare <= sparse_frac_of(e) * (double)e->N;
 }
 
@@ -534,18 +526,19 @@ int round_timer_collect(gossip_engine* e, uint32_t slot, int64_t limit) {
 
 // One pipelined round: its kernels (bracketed by the slot's events when timing),
 // then the snapshot of the totals into ring slot `slot` (rs).
-int launch_round_path(gossip_engine* e, uint32_t t, bool sparse, uint32_t maj, bool all_d, bool mid, uint32_t filt,
+int launch_round_path(gossip_engine* e, uint32_t t, bool sparse, uint32_t maj, bool all_d, uint32_t filt,
                       const RoundSync& rs, int slot) {
   const bool timed = e->timing && slot >= 0;
   if (timed) {
     if (int rc = round_timer_collect(e, (uint32_t)slot, INT64_MAX)) return rc;
     HIP_OK(e, hipEventRecord(e->evr[slot][0], e->stream));
   }
+  // the mid-level summary (FrontierBufs::summ2) pays once many peers hit the LDS summary (a
+  // g-node group holds a rare node w.p. 1 - (1 - r)^g); below that its extra probe round trip
+  // costs more than the exact probes it saves (2^27 nodes: rounds at 1-17 % LDS hits +50..130 us,
+  // at 61 % -920 us; profiles/r03_mid).  The kernels decide from the exact rare count.
   FrontierBufs fb = e->fb;
-  if (!mid) {
-    fb.summ2 = nullptr;
-    fb.summ2_words = 0;
-  }
+  fb.mid_frac = (float)e->mid_frac;
   if (sparse)
     HIP_OK(e, launch_frontier_round(fb, e->S, e->N, e->partial_d, e->R, e->k, t, e->key0, e->key1, e->mode, maj,
                                     !all_d ? kSparseFlags : (maj == 0 && e->sparse_direct ? kSparseDirect : kSparseAllD),
@@ -617,12 +610,11 @@ int step_planned(gossip_engine* e, uint32_t max_rounds, gossip_round_stats_t* st
       for (uint32_t i = done; i < launched; ++i) x = predict(e, x);
       uint32_t maj = 0;
       bool all_d = false;
-      bool mid = false;
-      const bool sparse = choose_sparse(e, x, &maj, &all_d, &mid);
+      const bool sparse = choose_sparse(e, x, &maj, &all_d);
       const uint32_t slot = launched % kRing;
       const RoundSync rs = ring_sync(e, slot);
       want[slot] = rs.seq;
-      if (int rc = launch_round_path(e, t0 + launched, sparse, maj, all_d, mid, dense_filter(e, x, filter_frac_of(e)), rs,
+      if (int rc = launch_round_path(e, t0 + launched, sparse, maj, all_d, dense_filter(e, x, filter_frac_of(e)), rs,
                                      (int)slot))
         return rc;
       ++launched;
@@ -759,10 +751,9 @@ int compute_round(gossip_engine* e, const uint64_t* gathered) {
     uint32_t maj = 0;
     bool all_d = false;
     const Est x = est_of(e, tot.data());
-    bool mid = false;
-    const bool sparse = choose_sparse(e, x, &maj, &all_d, &mid);
+    const bool sparse = choose_sparse(e, x, &maj, &all_d);
     if ((rc = timer_begin(e, 0))) return rc;
-    if ((rc = launch_round_path(e, e->t, sparse, maj, all_d, mid, dense_filter(e, x, filter_frac_of(e)), ring_sync(e, 0),
+    if ((rc = launch_round_path(e, e->t, sparse, maj, all_d, dense_filter(e, x, filter_frac_of(e)), ring_sync(e, 0),
                                 -1)))
       return rc;
     return timer_end(e, 0);  // stats are fused into the round kernels
@@ -1219,6 +1210,9 @@ int gossip_set_param(gossip_engine_t* e, const char* name, double v) {
   } else if (n == "ahead") {
     if (v < 1 || v > kRing - 1) return e->fail(GOSSIP_EINVAL, "ahead must be in [1, %u]", kRing - 1);
     e->ahead = (uint32_t)v;
+  } else if (n == "serve_grid") {
+    if (v < 0 || v > 65536) return e->fail(GOSSIP_EINVAL, "serve_grid must be in [0, 65536]");
+    e->bg.serve_grid = (uint32_t)v;
   } else if (n == "apply_grid") {
     if (v < 0 || v > 65536) return e->fail(GOSSIP_EINVAL, "apply_grid must be in [0, 65536]");
     e->bg.apply_grid = e->sbg.p.apply_grid = (uint32_t)v;

@@ -37,6 +37,9 @@ struct FrontierBufs {
   // its exact bitmap word is fetched from the MALL / HBM.  Null: not kept.
   uint32_t* summ2;
   uint32_t g2log, summ2_words;
+  // one-shard rounds decide on the device, from the exact rare count of S_t: summ2 is built and
+  // used when 1 - (1 - r)^g >= mid_frac (the LDS summary is that saturated)
+  float mid_frac;
   uint64_t id0;       // global id of node 0 of these arrays (a shard's first node; 0 on one GPU): the hash uses global ids
 };
 

@@ -129,12 +129,23 @@ __device__ __forceinline__ void summ2_body(const FrontierBufs& f, uint32_t s, ui
   f.summ2[s] = out;
 }
 
+// whether this round uses the mid-level summary: the share of peers that hit the LDS summary,
+// 1 - (1 - r)^g for a rare fraction r, reaches mid_frac (partial null: the caller decided)
+__device__ __forceinline__ bool use_mid(const FrontierBufs& f, const uint64_t* partial, uint64_t N, uint32_t R,
+                                        uint32_t maj) {
+  if (!f.summ2) return false;
+  if (!partial) return true;
+  const float r = (float)rare_count(partial, N, R, maj) / (float)N;
+  return 1.0f - __expf((float)(1u << f.glog) * log1pf(-fminf(r, 0.999999f))) >= f.mid_frac;
+}
+
 // blocks [0, summ_words / 256): the LDS summary; the rest: the mid-level summary (summ2)
 __global__ __launch_bounds__(256) void frontier_summary_kernel(FrontierBufs f, uint64_t N, const uint64_t* partial,
                                                                 uint32_t R, uint32_t maj) {
   if (partial && rare_count(partial, N, R, maj) == 0) return;
   const uint32_t b1 = (f.summ_words + 255) / 256;
   if (blockIdx.x >= b1) {
+    if (!use_mid(f, partial, N, R, maj)) return;
     const uint32_t s = (blockIdx.x - b1) * 256 + threadIdx.x;
     if (maj)
       summ2_body<1>(f, s, N);
@@ -159,7 +170,7 @@ template <int MAJ, int MODE, bool FAULTS>  // FAULTS: edge loss / partitions act
 __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const FrontierBufs& f,
                                           const uint64_t* __restrict__ S, uint64_t* Sw, uint64_t N, uint32_t R,
                                           uint32_t k, uint32_t t, uint32_t key0, uint32_t key1, uint64_t per_block,
-                                          bool mark_d, bool direct, const Faults& fa) {
+                                          bool mark_d, bool direct, bool mid, const Faults& fa) {
   const uint32_t* summ = (const uint32_t*)summ4;
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t n4 = (f.summ_words + 3) / 4;
@@ -219,7 +230,7 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
       // 2. summary hits: exact test in the rare bitmap (2 MiB at 2^24 nodes, L2-resident)
       // (all probes issued before any is consumed: one wait for the lot); past 2^25 nodes
       // the L2-resident mid-level summary first, so fewer probes reach the exact bitmap
-      if (glog && f.summ2) {
+      if (glog && mid) {
         uint32_t sw[kScanUnroll][4];
 #pragma unroll
         for (int u = 0; u < kScanUnroll; ++u)
@@ -307,7 +318,7 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
             const uint32_t p = peer_from_word(lane_of(r4, j & 3u), nm1, n);
             if (FAULTS && edge_lost(fa, rc, p, lane_of(lw, j & 3u))) continue;
             bool rp = summ_bit(p);
-            if (rp && glog && f.summ2) rp = (f.summ2[p >> (f.g2log + 5)] >> ((p >> f.g2log) & 31u)) & 1u;
+            if (rp && glog && mid) rp = (f.summ2[p >> (f.g2log + 5)] >> ((p >> f.g2log) & 31u)) & 1u;
             if (rp && glog) rp = (rare_word<MAJ>(f, p >> 6, N) >> (p & 63u)) & 1ull;
             if (!rn[u] && !rp) continue;  // both ends majority: nothing moves
             const uint64_t v = rp ? S[p] : maj;
@@ -348,10 +359,12 @@ __global__ __launch_bounds__(kScanThreads, GOSSIP_SCAN_WAVES) void frontier_scan
   __shared__ uint4 summ4[kSummBits / 128];
   __shared__ uint64_t rws[kRwWords];
   if (rare_count(partial, N, R, maj) == 0) return;  // converged (or nothing injected): nothing moves
+  const bool mid = use_mid(f, partial, N, R, maj);  // (the summary kernel built summ2 by the same rule)
   if (maj)
-    scan_body<1, MODE, FAULTS>(summ4, rws, f, S, S, N, R, k, t, key0, key1, per_block, mark_d != 0, false, fa);
+    scan_body<1, MODE, FAULTS>(summ4, rws, f, S, S, N, R, k, t, key0, key1, per_block, mark_d != 0, false, mid, fa);
   else
-    scan_body<0, MODE, FAULTS>(summ4, rws, f, S, S, N, R, k, t, key0, key1, per_block, mark_d != 0, direct != 0, fa);
+    scan_body<0, MODE, FAULTS>(summ4, rws, f, S, S, N, R, k, t, key0, key1, per_block, mark_d != 0, direct != 0,
+                               mid, fa);
 }
 
 // Stats of one 64-node group whose words went from old to nw (old == 0 in a

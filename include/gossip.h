@@ -138,12 +138,14 @@ int gossip_set_stream(gossip_engine_t* eng, void* hip_stream);
  *   "sparse_direct"  such rounds with an empty majority OR the pushes into empty peers
  *                  straight into the state and recompute the totals (default 1; 0: into D)
  *   "mid_frac"     past 2^25 nodes sparse rounds test a peer in the L2-resident mid-level
- *                  summary once this share of peers would hit the LDS summary (default 0.9)
+ *                  summary once this share of peers would hit the LDS summary (default 0.5;
+ *                  decided per round on the device from the exact rare count)
  *   "filter_frac"  dense rounds drop edges by the peer's class above this empty/full fraction
  *                  (default 0.3 up to 2^25 nodes; past that off: the probes miss the L2)
  *   "xd_filter_frac"  exchange dense rounds likewise (default 0.6; >= 1 never)
  *   "ahead"        rounds enqueued ahead of the stats read back (1..7, default 2)
  *   "apply_grid"   persistent blocks of the dense apply pass (0 = one block per tile)
+ *   "serve_grid"   persistent blocks of the one-shard dense serve pass (0 = one block per tile)
  *   "push_waves"   waves of the dense apply pass walking the pushes (of 16; the rest walk the replies)
  *   "ae_sparse"    ANTIENTROPY: -1 plan sparse rounds (default), 0 never, 1 whenever valid
  *   "ae_cap"       ANTIENTROPY: edge-list capacity of sparse rounds (reallocates the list)
