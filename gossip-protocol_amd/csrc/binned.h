@@ -75,6 +75,7 @@ struct BinBufs {
   uint16_t* offT;   // [nt_d + 1][nt_s]
   uint64_t* nzb;    // occupancy bitmaps of S_{t+1} written by K3 (frontier.h), or null
   uint64_t* fullb;
+  uint32_t* xsync;  // [16] per-XCD tile barriers of the persistent serve / apply (GOSSIP_XCD_SYNC), or null
 };
 
 size_t bin_bytes(const BinGeom& g);

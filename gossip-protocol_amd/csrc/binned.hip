@@ -171,6 +171,26 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {
   return (b & 7u) * (n >> 3) + (b >> 3);
 }
 
+#ifndef GOSSIP_XCD_SYNC
+#define GOSSIP_XCD_SYNC 0  // 1: serve, 2: apply, 3: both start every tile with the other blocks of their XCD (A/B)
+#endif
+// Speed only (no data passes between the blocks): the persistent blocks that share an XCD
+// (blockIdx & 7) start tile iteration `it` together, so the neighbouring runs their walks read and
+// write meet in that XCD's L2 at the same time.  Bounded spin: a block that waits too long goes on.
+__device__ __forceinline__ void xcd_tile_barrier(uint32_t* ctr, uint32_t it) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t grp = blockIdx.x & 7u, members = (gridDim.x + 7u - grp) / 8u;
+    atomicAdd(&ctr[grp], 1u);
+    const uint32_t target = members * it;
+    for (int spin = 0; spin < 4000; ++spin) {
+      if (__hip_atomic_load(&ctr[grp], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+}
+
 // Which directions an edge n -> p carries (bit 0 push, bit 1 pull; 0: no
 // record).  From the sender alone: a push needs S_t[n] != 0, a pull is
 // pointless once n holds every rumor.  filt bit 0 also drops pull-only edges
@@ -916,6 +936,7 @@ __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, cons
   if (blockIdx.x < nv) tile_regs_load(x, S, (uint64_t)tile_of(blockIdx.x) << kTileDLog, g.N);
   for (uint32_t v = blockIdx.x; v < nv; v += gridDim.x) {
   const uint32_t T = tile_of(v);
+  if ((GOSSIP_XCD_SYNC & 1) && b.xsync && v != blockIdx.x) xcd_tile_barrier(b.xsync, (v - blockIdx.x) / gridDim.x);
   __syncthreads();  // the previous walk is done with img
 #pragma unroll
   for (uint32_t q = 0; q < kTileQ; ++q) ((uint4*)img)[q * kTileThreads + threadIdx.x] = x[q];
@@ -1009,6 +1030,8 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
   for (uint32_t v = blockIdx.x; v < nv; v += gridDim.x) {
   const uint32_t X = xcd_remap(v, nv);
   const uint64_t node0 = (uint64_t)X << kTileDLog;
+  if ((GOSSIP_XCD_SYNC & 2) && b.xsync && v != blockIdx.x)
+    xcd_tile_barrier(b.xsync + 8, (v - blockIdx.x) / gridDim.x);
   __syncthreads();  // the previous epilogue is done with acc and cnt
   {
     uint4 xr[kTileQ - kPre];
@@ -1115,7 +1138,7 @@ size_t bin_bytes(const BinGeom& g) {
   const size_t recs = (size_t)g.nt_s * g.rp;
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   return (g.split ? 2 * al(recs * 2) : al(recs * 4)) + (g.aos ? al(recs * 12) : al(recs * 8)) + al(recs * 8) +
-         2 * al((size_t)g.nt_s * (g.nt_d + 1) * 2);
+         2 * al((size_t)g.nt_s * (g.nt_d + 1) * 2) + 256;
 }
 
 void bin_carve(const BinGeom& g, void* base, BinBufs* b) {
@@ -1141,6 +1164,8 @@ void bin_carve(const BinGeom& g, void* base, BinBufs* b) {
   b->off = (uint16_t*)p;
   p += al((size_t)g.nt_s * (g.nt_d + 1) * 2);
   b->offT = (uint16_t*)p;
+  p += al((size_t)g.nt_s * (g.nt_d + 1) * 2);
+  b->xsync = (uint32_t*)p;
 }
 
 hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, uint64_t* partial, uint32_t R,
@@ -1170,6 +1195,10 @@ hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, 
 #undef GOSSIP_EMIT_V
 #undef GOSSIP_EMIT
   launch_transpose_u16(b.off, b.offT, g.nt_s, g.nt_d + 1, partial, rs.plen, st);
+  if (GOSSIP_XCD_SYNC && b.xsync) {
+    const hipError_t me = hipMemsetAsync(b.xsync, 0, 16 * sizeof(uint32_t), st);
+    if (me != hipSuccess) return me;
+  }
   if ((mode == 2 || mode == 3) && g.split)
     bin_serve_kernel<kIdVF, true><<<serve_grid(g.nt_d, g.serve_grid), kTileThreads, 0, st>>>(g, S, b, R,
                                                                                           IdxRange::all(g.nt_d));
@@ -1215,6 +1244,7 @@ size_t sb_bytes(const SbGeom& g) { return bin_bytes(g.p) + bin_bytes(g.q); }
 void sb_carve(const SbGeom& g, void* base, SbBufs* b) {
   bin_carve(g.p, base, &b->p);
   bin_carve(g.q, (char*)base + bin_bytes(g.p), &b->q);
+  b->p.xsync = b->q.xsync = nullptr;  // (the tile barriers are the one-shard round's)
   b->p.nzb = b->p.fullb = b->q.nzb = b->q.fullb = nullptr;
 }
 
@@ -1743,6 +1773,7 @@ void xd_carve_recv(const XdGeom& g, uint64_t cap_r, void* base, XdBufs* b) {
   b->rb.off = (uint16_t*)take(offs * 2);
   b->rb.offT = (uint16_t*)take(offs * 2);
   b->rb.nzb = b->rb.fullb = nullptr;
+  b->rb.xsync = nullptr;
 }
 
 hipError_t launch_xd_requests(const XdGeom& g, const XdBufs& b, const uint64_t* S, uint32_t R, uint32_t t,

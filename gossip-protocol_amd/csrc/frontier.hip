@@ -144,8 +144,7 @@ __global__ __launch_bounds__(256) void frontier_summary_kernel(FrontierBufs f, u
                                                                 uint32_t R, uint32_t maj) {
   if (partial && rare_count(partial, N, R, maj) == 0) return;
   const uint32_t b1 = (f.summ_words + 255) / 256;
-  if (blockIdx.x >= b1) {
-    if (!use_mid(f, partial, N, R, maj)) return;
+  if (blockIdx.x >= b1) {  // always built (a few us): the scan alone decides whether to use it
     const uint32_t s = (blockIdx.x - b1) * 256 + threadIdx.x;
     if (maj)
       summ2_body<1>(f, s, N);
@@ -359,7 +358,7 @@ __global__ __launch_bounds__(kScanThreads, GOSSIP_SCAN_WAVES) void frontier_scan
   __shared__ uint4 summ4[kSummBits / 128];
   __shared__ uint64_t rws[kRwWords];
   if (rare_count(partial, N, R, maj) == 0) return;  // converged (or nothing injected): nothing moves
-  const bool mid = use_mid(f, partial, N, R, maj);  // (the summary kernel built summ2 by the same rule)
+  const bool mid = use_mid(f, partial, N, R, maj);  // (the summary kernel built summ2 this round)
   if (maj)
     scan_body<1, MODE, FAULTS>(summ4, rws, f, S, S, N, R, k, t, key0, key1, per_block, mark_d != 0, false, mid, fa);
   else
