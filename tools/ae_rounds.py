@@ -13,7 +13,8 @@ if os.environ.get("GOSSIP_LIB"):  # a library variant (tools/build_variants.sh)
     _eng.load_library(os.environ["GOSSIP_LIB"])
 LG = int(sys.argv[1]) if len(sys.argv) > 1 else 26
 N, K, k = 1 << LG, 16, 1
-e = Engine(N, K, "antientropy", k, 0x5EED0005, flags=1 | FLAG_TIMING,
+HASH = os.environ.get("AE_HASH", "1") != "0"  # AE_HASH=0: no per-round state hash (the reference has none)
+e = Engine(N, K, "antientropy", k, 0x5EED0005, flags=(1 if HASH else 0) | FLAG_TIMING,
            churn_fail=loss_threshold(0.01), churn_recover=loss_threshold(0.1))
 e.reset(); e.inject_random(); e.step(200)          # warm-up run (first-touch, code load)
 e.reset(); e.inject_random(); e.reset_timing()
@@ -39,7 +40,7 @@ rounds = t + 1
 dev = sum(per["dense"]) + sum(per["sparse"])
 bpn = 4 * K * (2 + 2 * k)
 dn = per["dense"]
-print(f"N=2^{LG} K={K} k={k}: {rounds} rounds to converge, device time {dev:.1f} ms "
+print(f"N=2^{LG} K={K} k={k} hash={int(HASH)}: {rounds} rounds to converge, device time {dev:.1f} ms "
       f"(wall {wall * 1e3:.1f} ms incl. per-round host reads)")
 print(f"  dense  rounds: {len(dn)}, {sum(dn) / max(len(dn), 1):.3f} ms each, roofline frac "
       f"{bpn * N / (sum(dn) / max(len(dn), 1) * 1e-3) / 8e12:.3f} at {bpn} B per node-round")
