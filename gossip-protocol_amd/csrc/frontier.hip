@@ -57,7 +57,10 @@ __device__ __forceinline__ void scan_st(T* p, T v) {
 constexpr uint32_t kScanGrid = GOSSIP_SCAN_GRID;  // one block per CU: the summary takes 128 KiB of LDS
 constexpr int kCommitThreads = 256;
 constexpr uint32_t kRwWords = 1024;  // rare-bitmap words staged per scan chunk (64K nodes)
-constexpr int kScanUnroll = 2;       // nodes per lane per scan step
+#ifndef GOSSIP_SCAN_UNROLL
+#define GOSSIP_SCAN_UNROLL 2
+#endif
+constexpr int kScanUnroll = GOSSIP_SCAN_UNROLL;  // nodes per lane per scan step
 constexpr int kCommitUnroll = 4;     // dirty groups per wave per commit step
 
 // valid-node mask of bitmap word w (bits past N are zero in both bitmaps)

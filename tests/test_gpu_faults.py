@@ -133,6 +133,32 @@ def test_flood_edge_kernel_without_losses_equals_flood_gpu(golden, idx):
     assert [s["state_hash"] for s in res.stats] == [r["hash"] for r in c["rounds"]]
 
 
+@pytest.mark.parametrize("path", list(PATHS))
+def test_stall_streaks_across_steps_and_injects(path):
+    """Stall streaks carry across gossip_step calls (short steps, injects between them, a step
+    after convergence) exactly as the oracle carries them: the pipelined step runs no round
+    ahead of the one it waits on when streaks are kept (stall_d is not idempotent)."""
+    N, R, k, seed, loss, D = 3001, 6, 2, 0x5EED0009, loss_threshold(0.05), 2
+    flags, params = PATHS[path]
+    e = Engine(N, R, "pushpull", k, seed, flags=1 | flags, edge_loss=loss, stall_rounds=D, params=params)
+    o = op.OracleEngine(N, R, "pushpull", k, seed, flags=1, edge_loss=loss, stall_rounds=D)
+    for x in (e, o):
+        x.inject(5, 0)
+        x.inject(N - 1, 1)
+    for burst in ([(123, 2)], [(7, 3), (2999, 4)], [(0, 5)]):
+        a, b = e.step(3), o.step(3)
+        assert a.stats == b.stats and np.array_equal(a.infected, b.infected)
+        for x in (e, o):
+            for n, r in burst:
+                x.inject(n, r)
+    a, b = e.step(300), o.step(300)
+    assert a.stats == b.stats and a.converged
+    a, b = e.step(5), o.step(5)  # past convergence: nothing moves, the round counters agree
+    assert a.stats == b.stats
+    assert np.array_equal(e.read_shard(), o.read_shard())
+    e.close()
+
+
 @pytest.mark.parametrize("plan", ["auto", "sparse", "dense"])
 def test_stall_sharded_lockstep(plan):
     """Stall streaks are kept for all N nodes on every shard: G = 3 lockstep equals the oracle."""
