@@ -86,6 +86,7 @@ hipError_t launch_frontier_inject(const FrontierBufs& f, uint64_t* S, uint64_t N
 //   kSparseDirect (maj = 0 only) pushes into a majority (empty) peer are OR-ed
 //                 straight into S: no kernel of the round reads a majority node's
 //                 S_t (its value is known to be 0), so the round stays synchronous.
+//                 A majority node's own pull is OR-ed into its S word the same way.
 //                 Pushes into rare peers still go to D (flagged).  The commit then
 //                 visits every group once, reads D / P only where flagged and
 //                 recomputes the totals absolutely (S is read once; D is neither

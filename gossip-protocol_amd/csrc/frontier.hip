@@ -339,14 +339,18 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
         }
       }
       // pull deltas: whole 8-word chunks (P is zero where there is no delta), so
-      // no store is a partial 64-B chunk
+      // no store is a partial 64-B chunk.  Direct rounds: a majority (empty) node's
+      // pull goes straight into its S word, which nobody reads this round (the
+      // pushes into it are atomic ORs too), so the commit reads no P for it.
 #pragma unroll
       for (int u = 0; u < kScanUnroll; ++u) {
         const uint32_t n = base + u * kScanThreads + tid;
-        const uint64_t pz = __ballot(accs[u] != 0);
+        const bool dmaj = MAJ == 0 && direct && !rn[u];
+        if (dmaj && accs[u]) atomicOr((unsigned long long*)&Sw[n], (unsigned long long)accs[u]);
+        const uint64_t pz = __ballot(!dmaj && accs[u] != 0);
         if (!pz) continue;
-        if (n < c1 && ((pz >> (lane & ~7u)) & 0xFFull)) scan_st(&f.P[n], accs[u]);
-        if (accs[u]) f.dirtyP[n >> 6] = 1;
+        if (n < c1 && ((pz >> (lane & ~7u)) & 0xFFull)) scan_st(&f.P[n], dmaj ? (uint64_t)0 : accs[u]);
+        if (!dmaj && accs[u]) f.dirtyP[n >> 6] = 1;
       }
     }
   }
