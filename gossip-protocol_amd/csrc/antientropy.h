@@ -36,6 +36,7 @@ struct AeArgs {
   uint16_t* boff;    // [bnreg][bnt + 1] run starts inside each region
   uint32_t btl, bnt, brs, bnreg;
   uint32_t spb;      // blocks per segment in the gather / apply / fix kernels
+  uint32_t dcap;     // binned dense rounds: in-edges sorted per LDS pass (0 = the kernel's capacity)
 };
 
 // binned sparse-scan geometry for N nodes, k exchanges per node
@@ -63,5 +64,14 @@ hipError_t launch_ae_sparse(const AeArgs& a, hipStream_t st);
 // pass also does the churn (no launch_ae_churn before it)
 hipError_t launch_ae_sparse_binned(const AeArgs& a, hipStream_t st);
 hipError_t launch_ae_sparse_stats(const AeArgs& a, hipStream_t st);
+// binned dense round: geometry of its 2^14-node tiles (the sparse scan's
+// sender regions), whether the kernels' LDS tables cover it, and the round itself: the
+// emit (churn fused, records into a.brec, run starts into a.boff with a.btl / a.bnt of
+// this geometry), then one block per tile writes every row of Vn, the stale bits of abn
+// and the round's stats (no launch_ae_stats after it); aux[1] != 0: a chunk's in-edges
+// overflowed the LDS list, rerun the round with launch_ae_round
+AeBinGeom ae_dense_geom(uint64_t N, uint32_t k);
+bool ae_dense_fits(const AeBinGeom& g, uint64_t N, uint32_t k, uint32_t K);
+hipError_t launch_ae_dense_binned(const AeArgs& a, hipStream_t st);
 
 }  // namespace gossip

@@ -56,14 +56,15 @@ __device__ __forceinline__ bool churned(uint8_t alive, uint32_t n, uint32_t t, u
 __device__ __forceinline__ uint64_t wave_id() { return (uint64_t)blockIdx.x * kAeWaves + (threadIdx.x >> 6); }
 __device__ __forceinline__ uint64_t wave_count() { return (uint64_t)gridDim.x * kAeWaves; }
 
-// block sum of one u64 per lane, added to *dst by one atomic
+// block sum of one u64 per lane, added to *dst by one atomic (NW waves per block)
+template <int NW = kAeWaves>
 __device__ __forceinline__ void block_add(uint64_t v, uint64_t* red, uint64_t* dst) {
   v = wave_sum64(v);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
   if (threadIdx.x == 0) {
     uint64_t s = 0;
-    for (int w = 0; w < kAeWaves; ++w) s += red[w];
+    for (int w = 0; w < NW; ++w) s += red[w];
     if (s) atomicAdd((unsigned long long*)dst, (unsigned long long)s);
   }
   __syncthreads();
@@ -383,6 +384,7 @@ constexpr int kAeBinThreads = 1024;
 constexpr uint32_t kAeBinRec = 16384;    // records per region (LDS)
 constexpr uint32_t kAeBinTiles = 4032;  // (two emit blocks fit 160 KiB of LDS)
 constexpr uint32_t kAeBinQ = kAeBinRec / kAeBinThreads;  // k == 1: senders per thread, peers in registers
+constexpr uint32_t kAeDTiles = 4096;  // dense rounds: tiles of 2^14 nodes (N <= 2^26)
 
 // record: p_local (btl bits) | n - region base (brs bits) << btl | stale(n) << (btl + brs)
 __device__ __forceinline__ uint32_t ae_rec(uint32_t pl, uint32_t nl, uint32_t stale, uint32_t btl, uint32_t brs) {
@@ -396,9 +398,11 @@ __device__ __forceinline__ uint32_t ae_rec(uint32_t pl, uint32_t nl, uint32_t st
 #define GOSSIP_AE_EMIT_K1 1  // k == 1 keeps the peers of pass A in registers (24 VGPRs spill at 8 waves;
                              // still 0.516 vs 0.568 ms per sparse round redrawing them, profiles/r02_ae_one)
 #endif
-template <bool K1>
-__global__ __launch_bounds__(kAeBinThreads, GOSSIP_AE_EMIT_WAVES) void ae_bin_emit_kernel(AeArgs a) {
-  __shared__ uint32_t cur[kAeBinTiles];
+// NT: LDS tile counters (kAeBinTiles for the sparse scan's tiles, two blocks per CU;
+// kAeDTiles for the dense round's 2^14-node tiles, one block per CU)
+template <bool K1, uint32_t NT>
+__global__ __launch_bounds__(kAeBinThreads, (NT > kAeBinTiles ? 4 : GOSSIP_AE_EMIT_WAVES)) void ae_bin_emit_kernel(AeArgs a) {
+  __shared__ uint32_t cur[NT];
   __shared__ __align__(16) uint32_t st[kAeBinRec];  // read back as uint4
   __shared__ uint32_t wsum[kAeBinThreads / 64];
   __shared__ uint32_t wpre[kAeBinThreads / 64 + 1];
@@ -586,6 +590,469 @@ __global__ __launch_bounds__(kAeBinThreads) void ae_bin_scan_kernel(AeArgs a) {
     a.segn[T] = scnt;
     if (scnt) atomicMax((unsigned long long*)&a.aux[1], (unsigned long long)scnt);
   }
+}
+
+// ---------------------------------------------------------------- binned dense round
+// The push pass above costs ~4e8 global atomicMax per dense round at 2^26 nodes.  Here the
+// exchanges are inverted instead: ae_bin_emit (churn fused) bins every alive sender's
+// exchanges by the peer's tile of 2^14 nodes, and one block per tile counting-sorts the
+// records aimed at it by node in LDS (in-edge lists).  Each node's S_{t+1} row is then the
+// max of its own row, its peers' rows (pull) and the rows of the senders that picked it
+// (push, as 64-B gathers): every row is written once with plain stores, so the stats pass
+// folds into the same kernel.
+constexpr uint32_t kAeDTileLog = 14;
+constexpr uint32_t kAeDTile = 1u << kAeDTileLog;
+constexpr uint32_t kAeDCap = 18432;    // in-edges sorted in LDS per pass (a tile's nodes in ranges)
+constexpr uint32_t kAeDMaxReg = 4096;  // regions in the LDS run table
+// 8 waves per block (one block per CU: the LDS): 256 VGPRs per lane for the 2L gathers in flight
+constexpr uint32_t kAeDThreads = 512;
+
+// every record of tile T (its run in each region, 64 runs per wave, lane-strided), as
+// fn(record, region); rt[r] = run start | run end << 16
+// (rt == nullptr: the run starts come from a.boff, L2-resident, for tile T)
+template <uint32_t NW, typename F>
+__device__ __forceinline__ void ae_tile_records(const AeArgs& a, const uint32_t* rt, uint32_t T, F&& fn) {
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t rp = (1u << a.brs) * a.k;
+  for (uint32_t r0 = wave * 64; r0 < a.bnreg; r0 += NW * 64) {
+    const uint32_t r = r0 + lane;
+    uint32_t w = 0;
+    if (r < a.bnreg) {
+      if (rt) {
+        w = rt[r];
+      } else {
+        const uint16_t* o = a.boff + (size_t)r * (a.bnt + 1) + T;
+        w = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+      }
+    }
+    const uint32_t be = w & 0xFFFFu, len = (w >> 16) - be;
+    uint32_t inc = len;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o, 64);
+      if (lane >= (uint32_t)o) inc += y;
+    }
+    const uint32_t exc = inc - len, total = __shfl(inc, 63, 64);
+    const uint64_t rbase = (uint64_t)r * rp + be - exc;
+    constexpr int U = 4;
+    for (uint32_t f0 = 0; f0 < total; f0 += 64 * U) {
+      uint32_t rec[U], reg[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t f = f0 + u * 64 + lane;
+        uint32_t ow = 0;
+#pragma unroll
+        for (uint32_t step = 32; step; step >>= 1) {
+          const uint32_t cc = ow + step;
+          if (cc < 64 && (uint32_t)__shfl((int)exc, (int)cc, 64) <= f) ow = cc;
+        }
+        const uint64_t rb = (uint64_t)__shfl((long long)rbase, (int)ow, 64);
+        rec[u] = f < total ? a.brec[rb + f] : 0u;
+        reg[u] = f < total ? r0 + ow : ~0u;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (reg[u] != ~0u) fn(rec[u], reg[u]);
+    }
+  }
+}
+
+#ifndef GOSSIP_ABL_AED
+#define GOSSIP_ABL_AED 0  // timing ablations (results wrong): 1 no node phase, 2 no in-edge sort
+#endif
+
+// The in-edge sort of tile T, shared by both apply kernels (NW waves per block).  pos2
+// holds u16 counts, then starts, then (after a fill) ends, packed in pairs: a tile's
+// records stay below 2^16 (k <= 3; a larger total sets aux[1], the host reruns the round).
+struct AeSortSh {
+  uint32_t* pos2;  // [kAeDTile / 2]
+  uint32_t* srt;   // [cap] sender | (node & 63) << 26, sorted by node
+  const uint32_t* rt;  // run table or nullptr
+  uint32_t *wsum, *wpre, *rng;  // [NW], [NW + 1], [3]: range end, range base, total
+};
+
+__device__ __forceinline__ uint32_t ae_pget(const AeSortSh& sh, uint32_t i) {
+  return i >= kAeDTile ? sh.rng[2] : (sh.pos2[i >> 1] >> ((i & 1u) << 4)) & 0xFFFFu;
+}
+
+// counts and their exclusive scan (every thread; ends with a barrier)
+template <uint32_t NW>
+__device__ void ae_sort_count(const AeArgs& a, const AeSortSh& sh, uint32_t T) {
+  constexpr uint32_t nth = NW * 64;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (uint32_t i = tid; i < kAeDTile / 2; i += nth) sh.pos2[i] = 0;
+  __syncthreads();
+  if (GOSSIP_ABL_AED != 2)
+    ae_tile_records<NW>(a, sh.rt, T, [&](uint32_t rec, uint32_t) {
+      const uint32_t pl = rec & (kAeDTile - 1u);
+      atomicAdd(&sh.pos2[pl >> 1], 1u << ((pl & 1u) << 4));
+    });
+  __syncthreads();
+  constexpr uint32_t qw = (kAeDTile / 2 + nth - 1) / nth;  // words per thread
+  const uint32_t w0 = min(tid * qw, kAeDTile / 2), w1 = min(w0 + qw, kAeDTile / 2);
+  uint32_t mine = 0;
+  for (uint32_t i = w0; i < w1; ++i) {
+    const uint32_t w = sh.pos2[i];
+    mine += (w & 0xFFFFu) + (w >> 16);
+  }
+  uint32_t inc = mine;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if (lane >= (uint32_t)o) inc += y;
+  }
+  if (lane == 63) sh.wsum[wave] = inc;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t t = 0;
+    for (uint32_t w = 0; w < NW; ++w) {
+      sh.wpre[w] = t;
+      t += sh.wsum[w];
+    }
+    sh.rng[2] = t;
+    if (t > 0xFFFFu) a.aux[1] = 1ull;  // u16 positions would wrap
+  }
+  __syncthreads();
+  uint32_t run = sh.wpre[wave] + inc - mine;
+  for (uint32_t i = w0; i < w1; ++i) {
+    const uint32_t w = sh.pos2[i];
+    const uint32_t r0 = run, r1 = run + (w & 0xFFFFu);
+    sh.pos2[i] = (r0 & 0xFFFFu) | (r1 << 16);
+    run = r1 + (w >> 16);
+  }
+  __syncthreads();
+}
+
+// the next node range [lo, hi): whole chunks whose in-edges fit cap (at least one chunk),
+// its records sorted into srt; returns hi, *base = the range's first position (barriers)
+template <uint32_t NW>
+__device__ uint32_t ae_sort_range(const AeArgs& a, const AeSortSh& sh, uint32_t T, uint32_t tn, uint32_t lo,
+                                  uint32_t cap, uint32_t* base_out) {
+  if (threadIdx.x == 0) {
+    const uint32_t base = ae_pget(sh, lo), nch = (tn + 63) >> 6;
+    uint32_t l = (lo >> 6) + 1, h = nch;
+    while (l < h) {
+      const uint32_t m = (l + h + 1) >> 1;
+      if (((ae_pget(sh, min(m << 6, tn)) - base) & 0xFFFFu) <= cap) l = m;
+      else h = m - 1;
+    }
+    const uint32_t hi = min(l << 6, tn);
+    sh.rng[0] = hi;
+    sh.rng[1] = base;
+    if (((ae_pget(sh, hi) - base) & 0xFFFFu) > cap) a.aux[1] = 1ull;  // one chunk past the list: host reruns
+  }
+  __syncthreads();
+  const uint32_t hi = sh.rng[0], base = sh.rng[1];
+  const uint32_t nmask = (1u << a.brs) - 1u;
+  if (GOSSIP_ABL_AED != 2 && ae_pget(sh, hi) != base) {
+    ae_tile_records<NW>(a, sh.rt, T, [&](uint32_t rec, uint32_t reg) {
+      const uint32_t pl = rec & (kAeDTile - 1u);
+      if (pl >= lo && pl < hi) {
+        const uint32_t b = (pl & 1u) << 4;
+        const uint32_t s = (((atomicAdd(&sh.pos2[pl >> 1], 1u << b) >> b) & 0xFFFFu) - base) & 0xFFFFu;
+        if (s < cap) sh.srt[s] = ((reg << a.brs) + ((rec >> kAeDTileLog) & nmask)) | ((pl & 63u) << 26);
+      }
+    });
+  }
+  __syncthreads();
+  *base_out = base;
+  return hi;
+}
+
+__device__ __forceinline__ uint32_t ae_tile_of(uint32_t nt) {
+  // XCD-contiguous tiles: the blocks resident on one XCD share run-start and record lines
+  return (nt & 7u) ? blockIdx.x : (blockIdx.x & 7u) * (nt >> 3) + (blockIdx.x >> 3);
+}
+
+template <uint32_t L, uint32_t KJ>  // KJ = k (<= 3)
+__global__ __launch_bounds__(kAeDThreads) void ae_dense_apply_kernel(AeArgs a) {
+  static_assert(L <= 16, "per-wave LDS scratch of 64 x L words");
+  constexpr uint32_t per = 64 / L;
+  constexpr uint64_t gmask = L >= 64 ? ~0ull : ((1ull << L) - 1ull);
+  constexpr uint32_t kW = kAeDThreads / 64;
+  constexpr uint32_t kB = 16;  // in-edge gathers in flight per lane (per edges each)
+  __shared__ uint32_t pos2[kAeDTile / 2];
+  __shared__ uint32_t srt[kAeDCap];
+  __shared__ uint32_t rt[kAeDMaxReg];
+  __shared__ uint32_t scr[kW][64 * L];  // per wave: in-edge max-merges of its chunk, [node][component]
+  __shared__ uint32_t wsum[kW], wpre[kW + 1], rng[3], cnt[64];
+  __shared__ uint64_t red[kW];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, sub = lane / L, c = lane % L;
+  const uint32_t T = ae_tile_of(a.bnt);
+  const uint64_t t0 = (uint64_t)T << kAeDTileLog;
+  const uint32_t tn = (uint32_t)((a.N - t0) < kAeDTile ? (a.N - t0) : kAeDTile);
+  const uint32_t* __restrict__ V = a.V;
+  uint32_t* __restrict__ Vn = a.Vn;
+  for (uint32_t r = tid; r < a.bnreg; r += kAeDThreads) {
+    const uint16_t* o = a.boff + (size_t)r * (a.bnt + 1) + T;
+    rt[r] = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+  }
+  if (tid < 64) cnt[tid] = 0;
+  const AeSortSh sh{pos2, srt, rt, wsum, wpre, rng};
+  ae_sort_count<kW>(a, sh, T);
+  auto pget = [&](uint32_t i) { return ae_pget(sh, i); };
+  const uint32_t tgt = c < a.K ? a.target[c] : 0u;
+  const bool hashing = (a.flags & 1u) != 0;
+  uint64_t msgs = 0, hash = 0, full = 0, nalive = 0, nstale = 0;
+  uint32_t c_lane = 0;
+  const uint32_t cap = (a.dcap && a.dcap < kAeDCap) ? a.dcap : kAeDCap;  // a smaller one tests the ranges
+  uint32_t* sc = scr[wave];
+  for (uint32_t lo = 0; lo < tn;) {
+    uint32_t base;
+    const uint32_t hi = ae_sort_range<kW>(a, sh, T, tn, lo, cap, &base);
+    // node p's in-edges now end at pget(p) and start at pget(p - 1) (base for p = lo)
+    for (uint32_t ch = (lo >> 6) + wave; GOSSIP_ABL_AED != 1 && ch < (hi + 63) >> 6; ch += kW) {
+      const uint64_t gch = (t0 >> 6) + ch;
+      const uint64_t nb = t0 + ((uint64_t)ch << 6);
+      const uint32_t n = (uint32_t)(nb + lane);
+      const uint64_t aw = a.abn[2 * gch];  // alive after this round's churn (bits past N are 0)
+      const bool aln = (aw >> lane) & 1ull;
+      const uint32_t c0 = ch << 6;
+      const uint32_t e0 = ((c0 == lo ? base : pget(c0 - 1)) - base) & 0xFFFFu;
+      const uint32_t ne = ((pget(c0 + 63) - base) & 0xFFFFu) - e0;  // the chunk's in-edges (wave-uniform)
+#pragma unroll
+      for (uint32_t i = 0; i < L; ++i) sc[i * 64 + lane] = 0u;
+      // every gather of the chunk is issued before any is used: own rows, the peers'
+      // rows (before their alive bits are known), the first kB in-edge groups
+      uint32_t acc[L];
+#pragma unroll
+      for (uint32_t i = 0; i < L; ++i) {
+        const uint64_t node = nb + i * per + sub;
+        acc[i] = (node < a.N && c < a.K) ? V[node * a.K + c] : 0u;
+      }
+      // the peers' rows are gathered before their alive bits are known (waiting for
+      // those first costs a round trip per chunk: 7.9 -> 10.4 ms per dense round)
+      uint32_t pj[KJ];
+      bool exj[KJ];
+      u32x4 x{0, 0, 0, 0};
+#pragma unroll
+      for (uint32_t j = 0; j < KJ; ++j) pj[j] = aln ? peer_j(a, n, j, x) : 0u;
+      uint32_t vp[KJ][L];
+#pragma unroll
+      for (uint32_t j = 0; j < KJ; ++j) {
+#pragma unroll
+        for (uint32_t i = 0; i < L; ++i) {
+          const uint32_t src = i * per + sub;
+          const uint32_t pp = (uint32_t)__shfl((int)pj[j], (int)src, 64);
+          const bool go = __shfl((int)aln, (int)src, 64) && c < a.K;
+          vp[j][i] = go ? V[(uint64_t)pp * a.K + c] : 0u;
+        }
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < KJ; ++j) exj[j] = aln && alive_bit(a.abn, pj[j]);
+      auto in_group = [&](uint32_t f0) {
+        uint32_t vi[kB], ti[kB];
+#pragma unroll
+        for (uint32_t b = 0; b < kB; ++b) {
+          const uint32_t f = f0 + b * per + sub;
+          // (clamped: after an overflow, flagged for the host, the list is cut short)
+          const uint32_t m = (f < ne && c < a.K) ? srt[min(e0 + f, cap - 1u)] : 0u;
+          const uint32_t po = m >> 26;
+          const bool on = f < ne && c < a.K && ((aw >> po) & 1ull) && (m & 0x3FFFFFFu) < a.N;  // picked node alive
+          vi[b] = on ? V[(uint64_t)(m & 0x3FFFFFFu) * a.K + c] : 0u;
+          ti[b] = on ? po * L + c : ~0u;
+        }
+#pragma unroll
+        for (uint32_t b = 0; b < kB; ++b)
+          if (ti[b] != ~0u) atomicMax(&sc[ti[b]], vi[b]);
+      };
+      if (ne) in_group(0);
+#pragma unroll
+      for (uint32_t j = 0; j < KJ; ++j) {
+        msgs += exj[j] ? 1u : 0u;
+#pragma unroll
+        for (uint32_t i = 0; i < L; ++i)
+          if (__shfl((int)exj[j], (int)(i * per + sub), 64)) acc[i] = max(acc[i], vp[j][i]);
+      }
+      for (uint32_t f0 = per * kB; f0 < ne; f0 += per * kB) in_group(f0);
+      // S_{t+1} rows and their stats (ae_stats_kernel's, in this layout)
+      uint64_t stale = 0;
+      uint64_t hb = ((uint64_t)c * a.N + nb + sub) * kGold64;
+#pragma unroll
+      for (uint32_t i = 0; i < L; ++i) {
+        acc[i] = max(acc[i], sc[i * 64 + lane]);
+        const uint64_t node = nb + i * per + sub;
+        const bool valid = node < a.N && c < a.K;
+        if (valid) Vn[node * a.K + c] = acc[i];
+        const bool al = (aw >> (i * per + sub)) & 1ull;
+        if (hashing) hash += valid && acc[i] ? mix64((uint64_t)acc[i] + hb) : 0ull;
+        hb += (uint64_t)per * kGold64;
+        c_lane += (valid && al && acc[i] == tgt) ? 1u : 0u;
+        const uint64_t m = __ballot(valid && acc[i] != tgt);
+#pragma unroll
+        for (uint32_t g = 0; g < per; ++g) stale |= (uint64_t)(((m >> (g * L)) & gmask) != 0ull) << (i * per + g);
+      }
+      if (lane == 0) {
+        a.abn[2 * gch + 1] = stale;
+        nalive += (uint64_t)__popcll(aw);
+        full += (uint64_t)__popcll(aw & ~stale);
+        nstale += (uint64_t)__popcll(stale);
+      }
+    }
+    __syncthreads();  // the next range's fill rewrites srt
+    lo = hi;
+  }
+  if (c < a.K && c_lane) atomicAdd(&cnt[c], c_lane);
+  block_add<kW>(msgs, red, &a.partial[2]);
+  block_add<kW>(hash, red, &a.partial[3]);
+  block_add<kW>(full, red, &a.partial[0]);
+  block_add<kW>(nalive, red, &a.partial[1]);
+  block_add<kW>(nstale, red, &a.aux[0]);
+  if (tid < a.K && cnt[tid]) atomicAdd((unsigned long long*)&a.partial[4 + tid], (unsigned long long)cnt[tid]);
+}
+
+// K == 16 (configs[4]): a row is 64 B, moved as four 16-B pieces.  Lane r*4 + q holds
+// components 4q .. 4q+3 of row r of a 16-row piece group, so the gathers need a quarter of
+// the address registers and the kernel fits 16 waves per CU (the LDS table of run starts
+// gives way to the per-wave scratch; the run starts come from L2).
+#ifndef GOSSIP_AEQ_WAVES
+#define GOSSIP_AEQ_WAVES 12  // 12 waves per CU: 168 VGPRs (16 spill at 128)
+#endif
+constexpr uint32_t kAeQThreads = GOSSIP_AEQ_WAVES * 64;
+constexpr uint32_t kAeQCap = GOSSIP_AEQ_WAVES > 12 ? 15360 : 18432;  // sorted in-edges per pass (LDS)
+
+__device__ __forceinline__ uint4 max4(uint4 x, uint4 y) {
+  return uint4{max(x.x, y.x), max(x.y, y.y), max(x.z, y.z), max(x.w, y.w)};
+}
+
+template <uint32_t KJ>
+__global__ __launch_bounds__(kAeQThreads) void ae_dense_apply_q_kernel(AeArgs a) {
+  constexpr uint32_t kW = kAeQThreads / 64;
+  constexpr uint32_t kBQ = 4;  // in-edge piece groups in flight (16 edges each)
+  __shared__ uint32_t pos2[kAeDTile / 2];
+  __shared__ uint32_t srt[kAeQCap];
+  __shared__ __align__(16) uint32_t scr[kW][64 * 16];
+  __shared__ uint32_t wsum[kW], wpre[kW + 1], rng[3], cnt[64];
+  __shared__ uint64_t red[kW];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane >> 2, q = lane & 3;
+  const uint32_t T = ae_tile_of(a.bnt);
+  const uint64_t t0 = (uint64_t)T << kAeDTileLog;
+  const uint32_t tn = (uint32_t)((a.N - t0) < kAeDTile ? (a.N - t0) : kAeDTile);
+  const uint32_t* __restrict__ V = a.V;
+  uint32_t* __restrict__ Vn = a.Vn;
+  if (tid < 64) cnt[tid] = 0;
+  const AeSortSh sh{pos2, srt, nullptr, wsum, wpre, rng};
+  ae_sort_count<kW>(a, sh, T);
+  const uint4 tg = reinterpret_cast<const uint4*>(a.target)[q];
+  const bool hashing = (a.flags & 1u) != 0;
+  uint64_t msgs = 0, hash = 0, full = 0, nalive = 0, nstale = 0;
+  uint32_t cq[4] = {0, 0, 0, 0};
+  const uint32_t cap = (a.dcap && a.dcap < kAeQCap) ? a.dcap : kAeQCap;
+  uint32_t* sc = scr[wave];
+  auto row = [&](uint64_t node) { return reinterpret_cast<const uint4*>(V + node * 16 + q * 4); };
+  for (uint32_t lo = 0; lo < tn;) {
+    uint32_t base;
+    const uint32_t hi = ae_sort_range<kW>(a, sh, T, tn, lo, cap, &base);
+    for (uint32_t ch = (lo >> 6) + wave; GOSSIP_ABL_AED != 1 && ch < (hi + 63) >> 6; ch += kW) {
+      const uint64_t gch = (t0 >> 6) + ch;
+      const uint64_t nb = t0 + ((uint64_t)ch << 6);
+      const uint32_t n = (uint32_t)(nb + lane);
+      const uint64_t aw = a.abn[2 * gch];  // alive after this round's churn (bits past N are 0)
+      const bool aln = (aw >> lane) & 1ull;
+      const uint32_t c0 = ch << 6;
+      const uint32_t e0 = ((c0 == lo ? base : ae_pget(sh, c0 - 1)) - base) & 0xFFFFu;
+      const uint32_t ne = ((ae_pget(sh, c0 + 63) - base) & 0xFFFFu) - e0;  // the chunk's in-edges
+#pragma unroll
+      for (uint32_t g = 0; g < 4; ++g) reinterpret_cast<uint4*>(sc)[g * 64 + lane] = uint4{0, 0, 0, 0};
+      // own rows, the peers' rows (alive bits awaited after), the first in-edge groups
+      uint4 o[4];
+#pragma unroll
+      for (uint32_t g = 0; g < 4; ++g) {
+        const uint64_t node = nb + g * 16 + r;
+        o[g] = node < a.N ? *row(node) : uint4{0, 0, 0, 0};
+      }
+      uint32_t pj[KJ];
+      bool exj[KJ];
+      u32x4 x{0, 0, 0, 0};
+#pragma unroll
+      for (uint32_t j = 0; j < KJ; ++j) pj[j] = aln ? peer_j(a, n, j, x) : 0u;
+      uint4 vp[KJ][4];
+#pragma unroll
+      for (uint32_t j = 0; j < KJ; ++j)
+#pragma unroll
+        for (uint32_t g = 0; g < 4; ++g) {
+          const uint32_t src = g * 16 + r;
+          const uint32_t pp = (uint32_t)__shfl((int)pj[j], (int)src, 64);
+          vp[j][g] = __shfl((int)aln, (int)src, 64) ? *row(pp) : uint4{0, 0, 0, 0};
+        }
+#pragma unroll
+      for (uint32_t j = 0; j < KJ; ++j) exj[j] = aln && alive_bit(a.abn, pj[j]);
+      auto in_group = [&](uint32_t f0) {
+        uint4 vi[kBQ];
+        uint32_t ti[kBQ];
+#pragma unroll
+        for (uint32_t b = 0; b < kBQ; ++b) {
+          const uint32_t f = f0 + b * 16 + r;
+          // (clamped: after an overflow, flagged for the host, the list is cut short)
+          const uint32_t m = f < ne ? srt[min(e0 + f, cap - 1u)] : 0u;
+          const uint32_t po = m >> 26, sn = m & 0x3FFFFFFu;
+          const bool on = f < ne && ((aw >> po) & 1ull) && sn < a.N;  // the picked node is alive
+          vi[b] = on ? *row(sn) : uint4{0, 0, 0, 0};
+          ti[b] = on ? po * 16 + q * 4 : ~0u;
+        }
+#pragma unroll
+        for (uint32_t b = 0; b < kBQ; ++b)
+          if (ti[b] != ~0u) {
+            atomicMax(&sc[ti[b]], vi[b].x);
+            atomicMax(&sc[ti[b] + 1], vi[b].y);
+            atomicMax(&sc[ti[b] + 2], vi[b].z);
+            atomicMax(&sc[ti[b] + 3], vi[b].w);
+          }
+      };
+      if (ne) in_group(0);
+#pragma unroll
+      for (uint32_t j = 0; j < KJ; ++j) {
+        msgs += exj[j] ? 1u : 0u;
+#pragma unroll
+        for (uint32_t g = 0; g < 4; ++g)
+          if (__shfl((int)exj[j], (int)(g * 16 + r), 64)) o[g] = max4(o[g], vp[j][g]);
+      }
+      for (uint32_t f0 = 16 * kBQ; f0 < ne; f0 += 16 * kBQ) in_group(f0);
+      // S_{t+1} rows and their stats (ae_stats_kernel's, in this layout)
+      uint64_t stale = 0;
+#pragma unroll
+      for (uint32_t g = 0; g < 4; ++g) {
+        const uint32_t nr = g * 16 + r;
+        o[g] = max4(o[g], reinterpret_cast<const uint4*>(sc)[nr * 4 + q]);
+        const uint64_t node = nb + nr;
+        const bool valid = node < a.N;
+        if (valid) *reinterpret_cast<uint4*>(Vn + node * 16 + q * 4) = o[g];
+        const bool al = (aw >> nr) & 1ull;
+        const uint32_t v[4] = {o[g].x, o[g].y, o[g].z, o[g].w};
+        const uint32_t tv[4] = {tg.x, tg.y, tg.z, tg.w};
+        bool bad = false;
+#pragma unroll
+        for (uint32_t t = 0; t < 4; ++t) {
+          if (hashing && valid && v[t]) hash += mix64((uint64_t)v[t] + ((uint64_t)(q * 4 + t) * a.N + node) * kGold64);
+          cq[t] += (valid && al && v[t] == tv[t]) ? 1u : 0u;
+          bad |= valid && v[t] != tv[t];
+        }
+        // row nr is stale when any of its four lanes saw a differing component
+        uint64_t m = __ballot(bad);
+        m |= m >> 1;
+        m |= m >> 2;
+#pragma unroll
+        for (uint32_t rr = 0; rr < 16; ++rr) stale |= ((m >> (4 * rr)) & 1ull) << (g * 16 + rr);
+      }
+      if (lane == 0) {
+        a.abn[2 * gch + 1] = stale;
+        nalive += (uint64_t)__popcll(aw);
+        full += (uint64_t)__popcll(aw & ~stale);
+        nstale += (uint64_t)__popcll(stale);
+      }
+    }
+    __syncthreads();  // the next range's fill rewrites srt
+    lo = hi;
+  }
+#pragma unroll
+  for (uint32_t t = 0; t < 4; ++t)
+    if (cq[t]) atomicAdd(&cnt[q * 4 + t], cq[t]);
+  block_add<kW>(msgs, red, &a.partial[2]);
+  block_add<kW>(hash, red, &a.partial[3]);
+  block_add<kW>(full, red, &a.partial[0]);
+  block_add<kW>(nalive, red, &a.partial[1]);
+  block_add<kW>(nstale, red, &a.aux[0]);
+  if (tid < 16 && cnt[tid]) atomicAdd((unsigned long long*)&a.partial[4 + tid], (unsigned long long)cnt[tid]);
 }
 
 // edges of this block's segment, or 0 when any segment overflowed (the host reruns the round dense)
@@ -806,13 +1273,55 @@ bool ae_bin_fits(const AeBinGeom& g) { return g.nt <= kAeBinTiles; }
 hipError_t launch_ae_sparse_binned(const AeArgs& a, hipStream_t st) {
   const uint32_t eg = a.bnreg < 512 ? a.bnreg : 512;  // two blocks per CU
   if (GOSSIP_AE_EMIT_K1 && a.k == 1 && (1u << a.brs) == kAeBinRec)
-    ae_bin_emit_kernel<true><<<eg, kAeBinThreads, 0, st>>>(a);
+    ae_bin_emit_kernel<true, kAeBinTiles><<<eg, kAeBinThreads, 0, st>>>(a);
   else
-    ae_bin_emit_kernel<false><<<eg, kAeBinThreads, 0, st>>>(a);
+    ae_bin_emit_kernel<false, kAeBinTiles><<<eg, kAeBinThreads, 0, st>>>(a);
   ae_bin_scan_kernel<<<a.bnt, kAeBinThreads, 0, st>>>(a);
   AE_LAUNCH_L(ae_sparse_gather_kernel, a.L, a.nseg * a.spb, st, a);
   AE_LAUNCH_L(ae_sparse_apply_kernel, a.L, a.nseg * a.spb, st, a);
   AE_LAUNCH_L(ae_sparse_fix_kernel, a.L, a.nseg * a.spb, st, a);
+  return hipGetLastError();
+}
+
+AeBinGeom ae_dense_geom(uint64_t N, uint32_t k) {
+  AeBinGeom g = ae_bin_geom(N, k);  // the same sender regions
+  g.tl = kAeDTileLog;
+  g.nt = (uint32_t)((N + kAeDTile - 1) >> kAeDTileLog);
+  return g;
+}
+
+// tiles and regions in the LDS tables, senders in 26 bits of a sorted entry, k <= 3
+// (a tile's records below 2^16, u16 positions), K <= 16 (the per-wave scratch)
+bool ae_dense_fits(const AeBinGeom& g, uint64_t N, uint32_t k, uint32_t K) {
+  return g.nt <= kAeDTiles && g.nreg <= kAeDMaxReg && N <= (1ull << 26) && k <= 3 && K <= 16;
+}
+
+hipError_t launch_ae_dense_binned(const AeArgs& a, hipStream_t st) {
+  const uint32_t eg = a.bnreg < 256 ? a.bnreg : 256;  // one block per CU (LDS)
+  if (GOSSIP_AE_EMIT_K1 && a.k == 1 && (1u << a.brs) == kAeBinRec)
+    ae_bin_emit_kernel<true, kAeDTiles><<<eg, kAeBinThreads, 0, st>>>(a);
+  else
+    ae_bin_emit_kernel<false, kAeDTiles><<<eg, kAeBinThreads, 0, st>>>(a);
+#define AE_DENSE_L(KJ)                                                                 \
+  switch (a.L) {                                                                       \
+    case 1: ae_dense_apply_kernel<1, KJ><<<a.bnt, kAeDThreads, 0, st>>>(a); break;     \
+    case 2: ae_dense_apply_kernel<2, KJ><<<a.bnt, kAeDThreads, 0, st>>>(a); break;     \
+    case 4: ae_dense_apply_kernel<4, KJ><<<a.bnt, kAeDThreads, 0, st>>>(a); break;     \
+    case 8: ae_dense_apply_kernel<8, KJ><<<a.bnt, kAeDThreads, 0, st>>>(a); break;     \
+    default: ae_dense_apply_kernel<16, KJ><<<a.bnt, kAeDThreads, 0, st>>>(a); break;   \
+  }
+  if (a.K == 16) {  // 16-B row pieces
+    if (a.k == 1) ae_dense_apply_q_kernel<1><<<a.bnt, kAeQThreads, 0, st>>>(a);
+    else if (a.k == 2) ae_dense_apply_q_kernel<2><<<a.bnt, kAeQThreads, 0, st>>>(a);
+    else ae_dense_apply_q_kernel<3><<<a.bnt, kAeQThreads, 0, st>>>(a);
+  } else if (a.k == 1) {
+    AE_DENSE_L(1)
+  } else if (a.k == 2) {
+    AE_DENSE_L(2)
+  } else {
+    AE_DENSE_L(3)
+  }
+#undef AE_DENSE_L
   return hipGetLastError();
 }
 

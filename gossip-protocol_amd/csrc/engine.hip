@@ -93,6 +93,13 @@ struct gossip_engine {
   AeBinGeom ae_bg{};
   uint32_t* ae_brec = nullptr;
   uint16_t* ae_boff = nullptr;
+  // binned dense rounds: run starts per region over 2^14-node tiles;
+  // ae_dbin = the engine's geometry fits, ae_dbin_on = gossip_set_param "ae_dense_bin"
+  bool ae_dbin = false, ae_dbin_on = true;
+  uint32_t ae_dcap = 0;  // gossip_set_param "ae_dense_cap" (tests: ranges, overflow fallback)
+  AeBinGeom ae_dg{};
+  uint16_t* ae_dboff = nullptr;
+  uint64_t ae_dense_fallbacks = 0;
   uint64_t ae_cap = 0, ae_hash = 0, ae_stale = 0, ae_alive = 0, ae_full = 0;
   uint32_t ae_epoch = 0;
   int ae_force = -1;             // GOSSIP_AE_SPARSE: -1 auto, 0 never, 1 whenever the bitmap is valid
@@ -247,7 +254,7 @@ void free_all(gossip_engine* e) {
     if (b) (void)hipFree(b);
   if (e->sx_host) (void)hipHostFree(e->sx_host);
   void* ae[] = {e->V, e->Vn, e->target, e->alive, e->alive_n, e->ae_aux, e->ae_claim, e->ae_eid, e->ae_erow, e->ae_segn, e->ae_pmask,
-                e->ae_brec, e->ae_boff, e->aex_img, e->aex_cnt, e->aex_boff, e->aex_bcnt, e->aex_req, e->aex_loc,
+                e->ae_brec, e->ae_boff, e->ae_dboff, e->aex_img, e->aex_cnt, e->aex_boff, e->aex_bcnt, e->aex_req, e->aex_loc,
                 e->aex_in, e->aex_resp_out, e->aex_resp_in, e->aex_tmp, e->aex_dirty, e->aex_verdict};
   if (e->aex_cnt_h) (void)hipHostFree(e->aex_cnt_h);
   for (void* b : ae)
@@ -708,14 +715,35 @@ int ae_round(gossip_engine* e) {
   if (!sparse) {
     const AeArgs a = make_ae_args(e);
     HIP_OK(e, hipMemsetAsync(e->ae_aux, 0, 16, e->stream));
-    if ((rc = timer_begin(e, 0))) return rc;
-    HIP_OK(e, launch_ae_churn(a, e->stream));
-    HIP_OK(e, launch_ae_round(a, e->stream));
-    if ((rc = timer_end(e, 0))) return rc;
-    if ((rc = timer_begin(e, 1))) return rc;
-    HIP_OK(e, launch_ae_stats(a, e->Vn, e->alive_n, true, e->stream));
-    if ((rc = timer_end(e, 1))) return rc;
-    if ((rc = ae_read_back(e))) return rc;
+    bool binned = e->ae_dbin && e->ae_dbin_on;
+    if (binned) {  // in-edge gathers, stats fused (no timer-1 part)
+      AeArgs d = a;
+      d.btl = e->ae_dg.tl;
+      d.bnt = e->ae_dg.nt;
+      d.boff = e->ae_dboff;
+      d.dcap = e->ae_dcap;
+      if ((rc = timer_begin(e, 0))) return rc;
+      HIP_OK(e, launch_ae_dense_binned(d, e->stream));
+      if ((rc = timer_end(e, 0))) return rc;
+      if ((rc = ae_read_back(e))) return rc;
+      if (e->ae_aux_h[1]) {  // a chunk's in-edges overflowed the LDS list: rerun with atomics
+        if ((rc = timer_collect(e))) return rc;
+        ++e->ae_dense_fallbacks;
+        binned = false;
+        HIP_OK(e, hipMemsetAsync(e->partial_d, 0, part_len(e) * 8, e->stream));
+        HIP_OK(e, hipMemsetAsync(e->ae_aux, 0, 16, e->stream));
+      }
+    }
+    if (!binned) {
+      if ((rc = timer_begin(e, 0))) return rc;
+      HIP_OK(e, launch_ae_churn(a, e->stream));
+      HIP_OK(e, launch_ae_round(a, e->stream));
+      if ((rc = timer_end(e, 0))) return rc;
+      if ((rc = timer_begin(e, 1))) return rc;
+      HIP_OK(e, launch_ae_stats(a, e->Vn, e->alive_n, true, e->stream));
+      if ((rc = timer_end(e, 1))) return rc;
+      if ((rc = ae_read_back(e))) return rc;
+    }
   }
   // sparse rounds return the hash delta of the rows they changed
   e->ae_hash = sparse ? e->ae_hash + e->partial_h[3] : e->partial_h[3];
@@ -1056,10 +1084,14 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
     if (launch_ae_fill_alive(e->alive, e->N, nullptr) != hipSuccess) return bail(GOSSIP_EHIP);
     e->ae_bg = ae_bin_geom(e->N, e->k);
     e->ae_bin = !(cfg->flags & GOSSIP_FLAG_AE_DIRECT_SCAN) && e->k <= 16 && ae_bin_fits(e->ae_bg);  // else the direct scan
-    if (e->ae_bin) {
+    e->ae_dg = ae_dense_geom(e->N, e->k);
+    e->ae_dbin = ae_dense_fits(e->ae_dg, e->N, e->k, e->R);  // else pull + atomicMax push + stats
+    if (e->ae_dbin && !alloc_raw((void**)&e->ae_dboff, (size_t)e->ae_dg.nreg * (e->ae_dg.nt + 1) * 2))
+      return bail(GOSSIP_ENOMEM);
+    if (e->ae_bin || e->ae_dbin) {
       const size_t recs = (size_t)e->ae_bg.nreg * ((size_t)e->k << e->ae_bg.rs);
       if (!alloc_raw((void**)&e->ae_brec, recs * 4) ||
-          !alloc_raw((void**)&e->ae_boff, (size_t)e->ae_bg.nreg * (e->ae_bg.nt + 1) * 2))
+          (e->ae_bin && !alloc_raw((void**)&e->ae_boff, (size_t)e->ae_bg.nreg * (e->ae_bg.nt + 1) * 2)))
         return bail(GOSSIP_ENOMEM);
     }
     if (!alloc_raw((void**)&e->ae_aux, 64) || !alloc_raw((void**)&e->ae_claim, (size_t)e->N * 4) ||
@@ -1228,6 +1260,12 @@ int gossip_set_param(gossip_engine_t* e, const char* name, double v) {
   } else if (n == "ae_sparse") {
     if (v != -1 && v != 0 && v != 1) return e->fail(GOSSIP_EINVAL, "ae_sparse must be -1, 0 or 1");
     e->ae_force = (int)v;
+  } else if (n == "ae_dense_bin") {
+    if (v != 0 && v != 1) return e->fail(GOSSIP_EINVAL, "ae_dense_bin must be 0 or 1");
+    e->ae_dbin_on = v != 0;
+  } else if (n == "ae_dense_cap") {
+    if (v < 0 || v > 65535) return e->fail(GOSSIP_EINVAL, "ae_dense_cap must be in [0, 65535] (0 = default)");
+    e->ae_dcap = (uint32_t)v;
   } else if (n == "ae_cap") {
     if (e->mode != GOSSIP_MODE_ANTIENTROPY) return e->fail(GOSSIP_ESTATE, "ae_cap needs ANTIENTROPY mode");
     if (e->aex) return e->fail(GOSSIP_ENOTSUP, "ae_cap: sharded ANTIENTROPY engines keep no edge lists");

@@ -149,6 +149,11 @@ int gossip_set_stream(gossip_engine_t* eng, void* hip_stream);
  *   "push_waves"   waves of the dense apply pass walking the pushes (of 16; the rest walk the replies)
  *   "ae_sparse"    ANTIENTROPY: -1 plan sparse rounds (default), 0 never, 1 whenever valid
  *   "ae_cap"       ANTIENTROPY: edge-list capacity of sparse rounds (reallocates the list)
+ *   "ae_dense_bin" ANTIENTROPY: 1 dense rounds as binned in-edge gathers (default, N <= 2^26),
+ *                  0 pull pass + atomicMax push pass + stats pass
+ *   "ae_dense_cap" ANTIENTROPY: in-edges per LDS pass of a binned dense round (0 = default
+ *                  18432; smaller values split tiles into more passes, and a 64-node chunk
+ *                  past it reruns the round with the atomicMax passes)
  *   "xd_shards"    sharded random modes: dense rounds run as exchange rounds (kind 3) when
  *                  G >= this (default 6; 0 = never, always the state all-gather)
  *   "cc_frac"      sharded random modes: dense rounds on the state image exchange it

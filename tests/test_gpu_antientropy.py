@@ -3,7 +3,10 @@ bit-exact per round: stats, per-component counts, hash, and the rows and alive f
 
 Paths (all must agree with the oracle and with each other):
   auto     — dense rounds until the stale nodes are few, then sparse in-place rounds
-  dense    — ae_sparse = 0: every round dense (copy + atomicMax kernel)
+  dense    — ae_sparse = 0: every round dense (binned in-edge gathers, stats fused)
+  dense_atomic — ae_dense_bin = 0: dense rounds as pull pass + atomicMax push pass + stats pass
+  dense_ranges — ae_dense_cap = 256: each tile's in-edges sorted in many LDS passes
+  dense_fallback — ae_dense_cap = 16: every binned dense round overflows and is rerun atomically
   sparse   — ae_sparse = 1: every round after the first sparse (the edge list holds k*N)
   overflow — sparse forced with a 64-edge list (ae_cap): rounds whose list overflows are rerun dense
   *_direct — FLAG_AE_DIRECT_SCAN: the sparse scan probes the peers' bitmap words directly
@@ -22,6 +25,9 @@ pytestmark = pytest.mark.gpu
 THREADS = min(16, os.cpu_count() or 1)
 # (flags, gossip_set_param knobs) per path
 PATHS = {"auto": (0, {}), "dense": (0, {"ae_sparse": 0}), "sparse": (0, {"ae_sparse": 1}),
+         "dense_atomic": (0, {"ae_sparse": 0, "ae_dense_bin": 0}),
+         "dense_ranges": (0, {"ae_sparse": 0, "ae_dense_cap": 256}),
+         "dense_fallback": (0, {"ae_sparse": 0, "ae_dense_cap": 16}),
          "overflow": (0, {"ae_sparse": 1, "ae_cap": 64}),
          # sparse rounds with the direct scan (random bitmap probes) instead of the binned one
          "sparse_direct": (FLAG_AE_DIRECT_SCAN, {"ae_sparse": 1}),

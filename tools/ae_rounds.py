@@ -14,8 +14,10 @@ if os.environ.get("GOSSIP_LIB"):  # a library variant (tools/build_variants.sh)
 LG = int(sys.argv[1]) if len(sys.argv) > 1 else 26
 N, K, k = 1 << LG, 16, 1
 HASH = os.environ.get("AE_HASH", "1") != "0"  # AE_HASH=0: no per-round state hash (the reference has none)
+# AE_DBIN=0: dense rounds as pull + atomicMax push + stats passes (the round-2 kernels)
 e = Engine(N, K, "antientropy", k, 0x5EED0005, flags=(1 if HASH else 0) | FLAG_TIMING,
-           churn_fail=loss_threshold(0.01), churn_recover=loss_threshold(0.1))
+           churn_fail=loss_threshold(0.01), churn_recover=loss_threshold(0.1),
+           params={"ae_dense_bin": int(os.environ.get("AE_DBIN", "1"))})
 e.reset(); e.inject_random(); e.step(200)          # warm-up run (first-touch, code load)
 e.reset(); e.inject_random(); e.reset_timing()
 p0 = p1 = p2 = 0.0
