@@ -918,7 +918,10 @@ __device__ __forceinline__ uint4 max4(uint4 x, uint4 y) {
 template <uint32_t KJ>
 __global__ __launch_bounds__(kAeQThreads) void ae_dense_apply_q_kernel(AeArgs a) {
   constexpr uint32_t kW = kAeQThreads / 64;
-  constexpr uint32_t kBQ = 4;  // in-edge piece groups in flight (16 edges each)
+#ifndef GOSSIP_AEQ_GROUPS
+#define GOSSIP_AEQ_GROUPS 4
+#endif
+  constexpr uint32_t kBQ = GOSSIP_AEQ_GROUPS;  // in-edge piece groups in flight (16 edges each)
   __shared__ uint32_t pos2[kAeDTile / 2];
   __shared__ uint32_t srt[kAeQCap];
   __shared__ __align__(16) uint32_t scr[kW][64 * 16];
@@ -1021,9 +1024,12 @@ __global__ __launch_bounds__(kAeQThreads) void ae_dense_apply_q_kernel(AeArgs a)
         const uint32_t v[4] = {o[g].x, o[g].y, o[g].z, o[g].w};
         const uint32_t tv[4] = {tg.x, tg.y, tg.z, tg.w};
         bool bad = false;
+        // hash_term's ((4q + t) * N + node) * kGold64, stepped by N * kGold64 over t (mod 2^64)
+        uint64_t hb = ((uint64_t)(q * 4) * a.N + node) * kGold64;
+        const uint64_t hstep = a.N * kGold64;
 #pragma unroll
-        for (uint32_t t = 0; t < 4; ++t) {
-          if (hashing && valid && v[t]) hash += mix64((uint64_t)v[t] + ((uint64_t)(q * 4 + t) * a.N + node) * kGold64);
+        for (uint32_t t = 0; t < 4; ++t, hb += hstep) {
+          if (hashing && valid && v[t]) hash += mix64((uint64_t)v[t] + hb);
           cq[t] += (valid && al && v[t] == tv[t]) ? 1u : 0u;
           bad |= valid && v[t] != tv[t];
         }

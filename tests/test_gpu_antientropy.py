@@ -84,3 +84,13 @@ def test_antientropy_sparse_tail_1M():
         x.inject_random()
     res = _compare(e, o, N, K, 300, (0, 7, N // 5, N - 2))
     assert res.converged and res.rounds > 40
+
+
+def test_dense_bin_params():
+    """The binned dense round's knobs are validated; K > 16 engines keep the atomic passes."""
+    e = Engine(4096, 16, "antientropy", 1, 0x5EED0005, flags=1, params={"ae_dense_bin": 1, "ae_dense_cap": 0})
+    for name, bad in (("ae_dense_bin", 2), ("ae_dense_bin", -1), ("ae_dense_cap", -1), ("ae_dense_cap", 70000)):
+        with pytest.raises(Exception):
+            e.set_param(name, bad)
+    e.set_param("ae_dense_bin", 0)
+    e.set_param("ae_dense_cap", 64)
