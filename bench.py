@@ -7,7 +7,8 @@ node holds every rumor.  node-updates = nodes x rounds.  The workload is the
 north-star sweep, configs[3]: 2^27 nodes, push-pull k=2, R=64, seed
 0x5EED0004, at every GPU count (1/2/4/8 GPUs, strong
 scaling; N > 1 shards the node ids).  At one GPU the configs[2]
-workload (2^24 nodes, seed 0x5EED0003) is timed beside it as `secondary`.
+workload (2^24 nodes, seed 0x5EED0003) is timed beside it as `secondary`, and
+configs[4] (anti-entropy with churn, 2^26 nodes x 16 versions) as `antientropy`.
 State is resident in HBM; nothing crosses PCIe in the timed region except the
 per-round 8-byte-per-rumor stats readback.
 
@@ -203,6 +204,46 @@ def secondary_run(device: int, steps: int, warmup: int) -> dict:
             "sparse_avg_round_us": rl["sparse_rounds"]["avg_round_us"]}
 
 
+def antientropy_run(device: int, steps: int, warmup: int) -> dict:
+    """configs[4] on the same GPU: 2^26 nodes x K = 16 u32 versions, k = 1, churn 1 % / 10 %,
+    seed 0x5EED0005, a random write, rounds to convergence.  No per-round state
+    hash (flag 1: the parity tests' check; the reference keeps none).  Dense rounds are priced at
+    SURVEY.md §8(d)'s 4K(2 + 2k) = 256 B per node-round."""
+    from gossip_hip import FLAG_TIMING, Engine, loss_threshold
+    n, K, k, seed = 1 << 26, 16, 1, 0x5EED0005
+    e = Engine(n, K, "antientropy", k, seed, flags=FLAG_TIMING, device=device,
+               churn_fail=loss_threshold(0.01), churn_recover=loss_threshold(0.1))
+
+    def one():
+        e.reset(); e.inject_random()
+        return e.step(400, with_infected=False)
+    for _ in range(warmup):
+        one()
+    e.reset_timing()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rounds = 0
+    for _ in range(steps):
+        res = one()
+        assert res.converged
+        rounds += res.rounds
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    dense_ms, dense_n = e.kernel_time(0)
+    sparse_ms, sparse_n = e.kernel_time(2)
+    e.close()
+    dense_us = dense_ms * 1e3 / max(dense_n, 1)
+    achieved = 4 * K * (2 + 2 * k) * n / (dense_us * 1e-6) / 1e9
+    return {"workload": "antientropy K=16 k=1 churn 1%/10%, 2^26 nodes over 1 GPU (configs[4])", "nodes": n,
+            "seed": hex(seed), "value": n * rounds / dt, "unit": "node-updates/s",
+            "ms_to_converge": dt * 1e3 / steps, "rounds_to_converge": rounds // steps,
+            "dense_rounds": dense_n // steps, "avg_dense_round_us": dense_us,
+            "dense_round_roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                     "frac": achieved / HBM_PEAK_GBS, "bytes_per_node_round": 4 * K * (2 + 2 * k)},
+            "sparse_rounds": sparse_n // steps, "avg_sparse_round_us": sparse_ms * 1e3 / max(sparse_n, 1),
+            "state_hash": False}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -214,6 +255,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dense-only", action="store_true", help="skip the all-dense comparison run (profiling)")
     ap.add_argument("--no-secondary", action="store_true", help="skip the configs[2] line (profiling)")
+    ap.add_argument("--no-antientropy", action="store_true", help="skip the configs[4] line (profiling)")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="collectives for N > 1: nccl (= RCCL, the measured path) or gloo (a rehearsal of the "
                          "multi-rank code on a box with fewer GPUs than ranks: ranks share devices; --driver torch)")
@@ -340,6 +382,8 @@ def main():
             rl["dense_only"] = dense_only(n_total, seed, local)
         if world == 1 and not args.no_secondary and n_total != NODES_SECONDARY:
             out["secondary"] = secondary_run(local, max(args.steps, 5), max(args.warmup, 2))
+        if world == 1 and not args.no_antientropy and not per_gpu and n_total == NODES_TOTAL:
+            out["antientropy"] = antientropy_run(local, 3, 1)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(n_total, seed)
         print(json.dumps(out), flush=True)
