@@ -969,6 +969,13 @@ __global__ __launch_bounds__(kAeQThreads) void ae_dense_apply_q_kernel(AeArgs a)
       u32x4 x{0, 0, 0, 0};
 #pragma unroll
       for (uint32_t j = 0; j < KJ; ++j) pj[j] = aln ? peer_j(a, n, j, x) : 0u;
+#ifndef GOSSIP_AEQ_PROBE
+#define GOSSIP_AEQ_PROBE 0  // 1: the peers' alive bits awaited before their gathers (no dead-peer rows)
+#endif
+      if (GOSSIP_AEQ_PROBE) {
+#pragma unroll
+        for (uint32_t j = 0; j < KJ; ++j) exj[j] = aln && alive_bit(a.abn, pj[j]);
+      }
       uint4 vp[KJ][4];
 #pragma unroll
       for (uint32_t j = 0; j < KJ; ++j)
@@ -976,10 +983,13 @@ __global__ __launch_bounds__(kAeQThreads) void ae_dense_apply_q_kernel(AeArgs a)
         for (uint32_t g = 0; g < 4; ++g) {
           const uint32_t src = g * 16 + r;
           const uint32_t pp = (uint32_t)__shfl((int)pj[j], (int)src, 64);
-          vp[j][g] = __shfl((int)aln, (int)src, 64) ? *row(pp) : uint4{0, 0, 0, 0};
+          const bool go = __shfl((int)(GOSSIP_AEQ_PROBE ? exj[j] : aln), (int)src, 64);
+          vp[j][g] = go ? *row(pp) : uint4{0, 0, 0, 0};
         }
+      if (!GOSSIP_AEQ_PROBE) {
 #pragma unroll
-      for (uint32_t j = 0; j < KJ; ++j) exj[j] = aln && alive_bit(a.abn, pj[j]);
+        for (uint32_t j = 0; j < KJ; ++j) exj[j] = aln && alive_bit(a.abn, pj[j]);
+      }
       auto in_group = [&](uint32_t f0) {
         uint4 vi[kBQ];
         uint32_t ti[kBQ];

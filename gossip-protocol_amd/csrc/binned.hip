@@ -33,7 +33,10 @@ namespace gossip {
 namespace {
 
 constexpr int kEmitThreads = 1024;
-constexpr uint32_t kEmitGrid = 256;  // one persistent emit block per CU
+#ifndef GOSSIP_EMIT_GRID
+#define GOSSIP_EMIT_GRID 256
+#endif
+constexpr uint32_t kEmitGrid = GOSSIP_EMIT_GRID;  // one persistent emit block per CU
 constexpr int kTileThreads = 1024;
 constexpr uint32_t kServeGrid = 256;  // persistent serve: one block per CU (the tile image takes 128 KiB of LDS)
 constexpr uint32_t kApplyGrid = 256;  // persistent apply, likewise
