@@ -148,3 +148,24 @@ def test_flood_edge_state_without_faults_equals_flood(golden, idx):
     res = e.step(256)
     assert [s["messages"] for s in res.stats] == [r["messages"] for r in c["rounds"]]
     assert [s["state_hash"] for s in res.stats] == [r["hash"] for r in c["rounds"]]
+
+
+def test_cfg5_oracle_fixture_is_consistent():
+    """tests/golden/cfg5_oracle.json (configs[4] on the OpenMP oracle, make_cfg5_golden.py) is what the
+    full-size GPU tests compare against: one stats entry and one per-component count row per round,
+    rounds numbered in order, alive counts within N, the last round converged with every alive node full."""
+    import json
+    import os
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "cfg5_oracle.json")
+    with open(path) as f:
+        g = json.load(f)
+    N, K = g["config"]["N"], g["config"]["K"]
+    assert (N, K, g["config"]["seed"]) == (1 << 26, 16, hex(0x5EED0005))
+    assert g["rounds"] == len(g["stats"]) == len(g["infected"])
+    assert [s["round"] for s in g["stats"]] == list(range(g["rounds"]))
+    assert all(len(r) == K for r in g["infected"])
+    assert all(0 < s["alive_nodes"] <= N and s["full_nodes"] <= s["alive_nodes"] for s in g["stats"])
+    last = g["stats"][-1]
+    assert last["converged"] and last["full_nodes"] == last["alive_nodes"]
+    assert all(c == last["alive_nodes"] for c in g["infected"][-1])  # every alive row holds the max vector
+    assert len(g["rows_sha256"]) == 64 and all(len(v) == K for v in g["sample_rows"].values())
