@@ -85,7 +85,10 @@ struct gossip_engine {
   uint64_t *alive = nullptr, *alive_n = nullptr;  // [chunks][2]: alive bits, stale bits (AeArgs::ab)
   // ANTIENTROPY sparse rounds: stale bitmap of V, edge list + row snapshots,
   // fix-up claims; aux = [0] stale nodes [1] listed edges (device) / ae_aux_h (pinned host copy)
+  // (one-engine ANTIENTROPY: aux is the two words after partial_d / partial_h, so one copy and
+  // one memset per round move both)
   uint64_t *ae_aux = nullptr, *ae_aux_h = nullptr;
+  bool ae_aux_alias = false;
   uint32_t *ae_eid = nullptr, *ae_erow = nullptr, *ae_claim = nullptr, *ae_segn = nullptr;
   void* ae_pmask = nullptr;  // dense rounds: [N][k] push masks
   uint32_t ae_nseg = 1, ae_spc = 1, ae_segcap = 1;
@@ -253,6 +256,7 @@ void free_all(gossip_engine* e) {
   for (void* b : sx)
     if (b) (void)hipFree(b);
   if (e->sx_host) (void)hipHostFree(e->sx_host);
+  if (e->ae_aux_alias) e->ae_aux = e->ae_aux_h = nullptr;  // inside partial_d / partial_h
   void* ae[] = {e->V, e->Vn, e->target, e->alive, e->alive_n, e->ae_aux, e->ae_claim, e->ae_eid, e->ae_erow, e->ae_segn, e->ae_pmask,
                 e->ae_brec, e->ae_boff, e->ae_dboff, e->aex_img, e->aex_cnt, e->aex_boff, e->aex_bcnt, e->aex_req, e->aex_loc,
                 e->aex_in, e->aex_resp_out, e->aex_resp_in, e->aex_tmp, e->aex_dirty, e->aex_verdict};
@@ -664,8 +668,7 @@ int step_planned(gossip_engine* e, uint32_t max_rounds, gossip_round_stats_t* st
 // the edge list; a list that overflowed leaves V, the bitmap and the claims
 // untouched, and the round is rerun dense.  Stats reach the host every round.
 int ae_read_back(gossip_engine* e) {
-  HIP_OK(e, hipMemcpyAsync(e->partial_h, e->partial_d, part_len(e) * 8, hipMemcpyDeviceToHost, e->stream));
-  HIP_OK(e, hipMemcpyAsync(e->ae_aux_h, e->ae_aux, 16, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(e, hipMemcpyAsync(e->partial_h, e->partial_d, (part_len(e) + 2) * 8, hipMemcpyDeviceToHost, e->stream));
   HIP_OK(e, hipStreamSynchronize(e->stream));
   return GOSSIP_OK;
 }
@@ -691,8 +694,7 @@ int ae_round(gossip_engine* e) {
       HIP_OK(e, hipMemsetAsync(e->ae_claim, 0, (size_t)e->N * 4, e->stream));
       e->ae_epoch = 1;
     }
-    const AeArgs a = make_ae_args(e);
-    HIP_OK(e, hipMemsetAsync(e->ae_aux, 0, 16, e->stream));
+    const AeArgs a = make_ae_args(e);  // (partial and aux cleared by compute_round)
     if ((rc = timer_begin(e, 2))) return rc;
     if (e->ae_bin) {
       HIP_OK(e, launch_ae_sparse_binned(a, e->stream));  // churn fused into its first pass
@@ -709,12 +711,11 @@ int ae_round(gossip_engine* e) {
       if ((rc = timer_collect(e))) return rc;
       ++e->ae_overflows;
       sparse = false;
-      HIP_OK(e, hipMemsetAsync(e->partial_d, 0, part_len(e) * 8, e->stream));
+      HIP_OK(e, hipMemsetAsync(e->partial_d, 0, (part_len(e) + 2) * 8, e->stream));  // partial and aux
     }
   }
   if (!sparse) {
     const AeArgs a = make_ae_args(e);
-    HIP_OK(e, hipMemsetAsync(e->ae_aux, 0, 16, e->stream));
     bool binned = e->ae_dbin && e->ae_dbin_on;
     if (binned) {  // in-edge gathers, stats fused (no timer-1 part)
       AeArgs d = a;
@@ -730,8 +731,7 @@ int ae_round(gossip_engine* e) {
         if ((rc = timer_collect(e))) return rc;
         ++e->ae_dense_fallbacks;
         binned = false;
-        HIP_OK(e, hipMemsetAsync(e->partial_d, 0, part_len(e) * 8, e->stream));
-        HIP_OK(e, hipMemsetAsync(e->ae_aux, 0, 16, e->stream));
+        HIP_OK(e, hipMemsetAsync(e->partial_d, 0, (part_len(e) + 2) * 8, e->stream));  // partial and aux
       }
     }
     if (!binned) {
@@ -759,7 +759,8 @@ int ae_round(gossip_engine* e) {
 // compute S_{t+1} of the owned shard from the gathered image + partial stats (device)
 int compute_round(gossip_engine* e, const uint64_t* gathered) {
   const size_t bytes = (size_t)e->W * e->Nl * 8;
-  if (!e->binned) HIP_OK(e, hipMemsetAsync(e->partial_d, 0, part_len(e) * 8, e->stream));
+  // (one-engine ANTIENTROPY: the aux words after partial_d too)
+  if (!e->binned) HIP_OK(e, hipMemsetAsync(e->partial_d, 0, (part_len(e) + (e->ae_aux_alias ? 2 : 0)) * 8, e->stream));
   if (e->mode == GOSSIP_MODE_ANTIENTROPY) return ae_round(e);
   RoundArgs a = make_args(e, gathered);
   int rc;
@@ -1032,7 +1033,7 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
     }
     return hipMemset(*p, 0, bytes) == hipSuccess;
   };
-  if (!alloc(&e->partial_d, part_len(e) * 8) || !alloc(&e->scratch_d, 8)) return bail(GOSSIP_ENOMEM);
+  if (!alloc(&e->partial_d, part_len(e) * 8 + 64) || !alloc(&e->scratch_d, 8)) return bail(GOSSIP_ENOMEM);
   if (cfg->stall_rounds && e->mode >= GOSSIP_MODE_PUSH && e->mode <= GOSSIP_MODE_PUSHPULL) {
     if (hipMalloc((void**)&e->stall_d, e->N) != hipSuccess || hipMemset(e->stall_d, 0, e->N) != hipSuccess) {
       e->err = "hipMalloc of the stall streaks failed";
@@ -1094,11 +1095,12 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
           (e->ae_bin && !alloc_raw((void**)&e->ae_boff, (size_t)e->ae_bg.nreg * (e->ae_bg.nt + 1) * 2)))
         return bail(GOSSIP_ENOMEM);
     }
-    if (!alloc_raw((void**)&e->ae_aux, 64) || !alloc_raw((void**)&e->ae_claim, (size_t)e->N * 4) ||
+    e->ae_aux = e->partial_d + part_len(e);
+    e->ae_aux_alias = true;
+    if (!alloc_raw((void**)&e->ae_claim, (size_t)e->N * 4) ||
         !alloc_raw(&e->ae_pmask, (size_t)e->N * e->k * std::max<uint32_t>(1, ae_lanes(e->R) / 8)))
       return bail(GOSSIP_ENOMEM);
     if (ae_alloc_lists(e, 0) != GOSSIP_OK) return bail(GOSSIP_ENOMEM);
-    if (hipHostMalloc((void**)&e->ae_aux_h, 64) != hipSuccess) return bail(GOSSIP_ENOMEM);
   } else if (e->mode == GOSSIP_MODE_FLOOD) {
     if (!alloc(&e->S, shard) || !alloc(&e->Snext, shard) || !alloc(&e->Sprev, shard) || !alloc(&e->skip, shard) ||
         !alloc(&e->imgF, image))
@@ -1165,10 +1167,11 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
     }
     // sharded sparse rounds pay off up to a larger rare fraction than on one GPU: sparse_frac_of
   }
-  if (hipHostMalloc((void**)&e->partial_h, part_len(e) * 8, hipHostMallocDefault) != hipSuccess) {
+  if (hipHostMalloc((void**)&e->partial_h, part_len(e) * 8 + 64, hipHostMallocDefault) != hipSuccess) {
     e->err = "hipHostMalloc failed";
     return bail(GOSSIP_ENOMEM);
   }
+  if (e->ae_aux_alias) e->ae_aux_h = e->partial_h + part_len(e);
   if (e->timing) {
     for (auto& p : e->ev)
       for (auto& x : p)
