@@ -15,9 +15,13 @@
 //
 // Two round paths, chosen per round by the host (engine.hip), both after the
 // churn kernel:
-// - dense: a pull pass writes every row of V' = max(V[n], V[p_j]) and the
-//   per-exchange push masks; a push pass atomicMax-es V[n] into V'[p_j] for the
-//   masked components only;
+// - dense (binned, the default where it fits): the emit bins every alive sender's
+//   exchanges by the peer's 2^14-node tile; one block per tile sorts its in-edges by
+//   node in LDS and writes every row of V' = max(own row, the peers' rows, the rows
+//   of the senders that picked the node) once, with the round's stats;
+// - dense (atomic, the fallback): a pull pass writes every row of V' = max(V[n],
+//   V[p_j]) and the per-exchange push masks; a push pass atomicMax-es V[n] into
+//   V'[p_j] for the masked components only; a stats pass;
 // - sparse (most of a run: once nearly every alive node holds the global max
 //   vector, only exchanges touching a stale node can change anything): the
 //   scan lists the exchanges with a stale end, the rows of both ends are
