@@ -16,7 +16,7 @@ if [ "${SKIP_TESTS:-0}" != "1" ]; then
 fi
 timeout -k 10 400 python bench.py --steps 10 --warmup 3 > $O/bench.json 2> $O/bench.err; ok $?
 cat $O/bench.json
-P="--no-cpu-baseline --no-dense-only --no-secondary"
+P="--no-cpu-baseline --no-dense-only --no-secondary --no-antientropy"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python bench.py --steps 10 --warmup 3 $P > $O/prof.out 2>&1; ok $?
 cp $O/prof/run_kernel_stats.csv $O/kernel_stats.csv 2>/dev/null || find $O/prof -name '*kernel_stats.csv' -exec cp {} $O/kernel_stats.csv \;
 python tools/rounds.py $(find $O/prof -name '*kernel_trace.csv' | head -1) > $O/rounds.txt; ok $?
