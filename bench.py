@@ -39,6 +39,10 @@ RUMORS = 64
 FANOUT = 2
 MODE = "pushpull"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# configs[3] on the OpenMP C oracle (tests/golden/make_cfg4_golden.py): every run of that workload
+# is checked against it, at every GPU count, before and after the timed steps
+FIXTURE = os.path.join(ROOT, "tests", "golden", "cfg4_oracle.json")
+STAT_KEYS = ("round", "converged", "full_nodes", "alive_nodes", "messages")
 
 
 def alg_bytes_per_node_round(mode: str, k: int, words: int) -> int:
@@ -76,6 +80,44 @@ def _omp_run(n_nodes: int, seed: int, threads: int, budget_s: float):
     dt = time.perf_counter() - t0
     o.close()
     return n_nodes * rounds / dt, rounds, dt
+
+
+def load_fixture(n_total: int, seed: int):
+    """The oracle's run of this exact workload, or None (no fixture covers it)."""
+    try:
+        with open(FIXTURE) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    c = d["config"]
+    same = (c["N"], int(c["seed"], 16), c["R"], c["fanout"], c["mode"]) == (n_total, seed, RUMORS, FANOUT, MODE)
+    return d if same else None
+
+
+def global_state_hash(eng, world: int, backend: str) -> int:
+    """DESIGN.md §2.5's state hash of the whole state: each shard hashes its own nodes (global ids)
+    and the parts add up mod 2^64 (summed as four 16-bit limbs, so no collective overflows)."""
+    h = eng.state_hash()
+    if world == 1:
+        return h
+    limbs = torch.tensor([(h >> (16 * i)) & 0xFFFF for i in range(4)], dtype=torch.int64,
+                         device="cuda" if backend == "nccl" else "cpu")
+    dist.all_reduce(limbs, op=dist.ReduceOp.SUM)
+    return sum(int(x) << (16 * i) for i, x in enumerate(limbs.tolist())) & ((1 << 64) - 1)
+
+
+def check_run(stats: list, final_hash: int, fx: dict):
+    """None when a step equals the oracle's run (per-round stats, final state hash), else what differs.
+    The stats are global (all-reduced) and the hash is all-reduced, so every rank gets the same answer."""
+    if len(stats) != fx["rounds"]:
+        return f"{len(stats)} rounds, oracle {fx['rounds']}"
+    for got, want in zip(stats, fx["stats"]):
+        for key in STAT_KEYS:
+            if int(got[key]) != int(want[key]):
+                return f"round {want['round']}: {key} {int(got[key])}, oracle {int(want[key])}"
+    if final_hash != fx["final_state_hash"]:
+        return f"final state hash {final_hash:#x}, oracle {fx['final_state_hash']:#x}"
+    return None
 
 
 def cpu_baseline(n_nodes: int, seed: int, budget_s: float = 8.0):
@@ -259,10 +301,11 @@ def main():
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="collectives for N > 1: nccl (= RCCL, the measured path) or gloo (a rehearsal of the "
                          "multi-rank code on a box with fewer GPUs than ranks: ranks share devices; --driver torch)")
-    ap.add_argument("--driver", default="engine", choices=("engine", "torch"),
-                    help="N > 1: engine = the library runs every sharded round over its own RCCL communicator "
-                         "(gossip_comm_init_rank + gossip_step, DESIGN.md §5.5); torch = gossip_hip.sharded drives "
-                         "the rounds over torch.distributed")
+    ap.add_argument("--driver", default=None, choices=("engine", "torch"),
+                    help="N > 1: torch (default) = gossip_hip.sharded drives the rounds over torch.distributed "
+                         "(RCCL); engine = the library runs every sharded round over its own RCCL communicator "
+                         "(gossip_comm_init_rank + gossip_step, DESIGN.md §5.5; not yet run on distinct GPUs, so "
+                         "opt-in: a run that differs from the oracle fixture falls back to torch)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -289,28 +332,36 @@ def main():
         seed = SEED_TOTAL if n_total >= NODES_TOTAL or world > 1 else SEED_SECONDARY
     eng = Engine(n_total, RUMORS, MODE, FANOUT, seed, flags=FLAG_TIMING, device=local,
                  shard_rank=rank, shard_count=world)
-    driver = args.driver if world > 1 else "engine"
+    driver = (args.driver or "torch") if world > 1 else "engine"
     driver_note = None
     if world > 1 and driver == "engine" and args.backend == "gloo":
         driver, driver_note = "torch", "gloo rehearsal: ranks share devices, which RCCL refuses"
     if world > 1 and driver == "engine":
         from gossip_hip.sharded import init_engine_comm
-        try:
-            init_engine_comm(eng)
-        except Exception as exc:  # report it in the line, and measure the torch-driven rounds instead
-            driver, driver_note = "torch", f"engine RCCL init failed: {exc}"
+        why = init_engine_comm(eng)  # collective: every rank gets the same answer
+        if why:  # report it in the line, and measure the torch-driven rounds instead
+            driver, driver_note = "torch", f"engine RCCL init failed: {why}"
             print(f"warning: {driver_note}", file=sys.stderr)
-    if world > 1 and driver == "torch":
+
+    def use_torch_driver():
         eng.set_stream(torch.cuda.current_stream().cuda_stream)
+
+    if world > 1 and driver == "torch":
+        use_torch_driver()
 
     def one_step():
         eng.reset()
         eng.inject_random()
         if driver == "engine":  # one GPU, or every rank in gossip_step over the engine's RCCL comm
-            res = eng.step(64, with_infected=False)
-            return res.rounds, res.converged
-        st = sharded_run(eng, 64)
-        return len(st), bool(st[-1]["converged"])
+            return eng.step(64, with_infected=False).stats
+        return sharded_run(eng, 64)
+
+    fx = load_fixture(n_total, seed)
+
+    def verify(stats):
+        if fx is None:
+            return "no oracle fixture for this workload"
+        return check_run(stats, global_state_hash(eng, world, args.backend), fx)
 
     def barrier():
         torch.cuda.synchronize()
@@ -318,22 +369,34 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
-        one_step()
+    warm_check = None
+    for i in range(args.warmup):
+        st = one_step()
+        if i == 0 and fx is not None:  # before the timed steps: a wrong result is caught, not timed
+            warm_check = verify(st)
+            if warm_check and world > 1 and driver == "engine":
+                driver_note = (f"the engine-driven run differed from the oracle fixture ({warm_check}): the "
+                               "rounds are driven over torch.distributed instead")
+                print(f"warning: {driver_note}", file=sys.stderr)
+                driver = "torch"
+                use_torch_driver()
     eng.reset_timing()
     barrier()
     t0 = time.perf_counter()
-    rounds = []
+    rounds, last = [], None
     for _ in range(args.steps):
-        r, conv = one_step()
-        assert conv, "run did not converge within 64 rounds"
-        rounds.append(r)
+        last = one_step()
+        assert last[-1]["converged"], "run did not converge within 64 rounds"
+        rounds.append(len(last))
     barrier()
     dt = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([dt], device="cuda" if args.backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    # after the timed region: the last timed step against the oracle's run of the same workload
+    final_check = verify(last) if last is not None else "no timed step"
+    verified = None if fx is None or last is None else final_check is None
 
     total_rounds = sum(rounds)
     value = n_total * total_rounds / dt
@@ -375,6 +438,11 @@ def main():
                        "parallelism": f"shard{world}" if world > 1 else "single",
                        **({"driver": driver} if world > 1 else {}),
                        **({"driver_note": driver_note} if driver_note else {})},
+            "verified": verified,
+            "verification": (f"per-round stats ({', '.join(STAT_KEYS)}) and the final state hash of the last "
+                             f"timed step{' (all ranks, hash summed over the shards)' if world > 1 else ''} equal "
+                             f"the OpenMP oracle's run of the same workload ({os.path.relpath(FIXTURE, ROOT)})"
+                             if verified else final_check),
             **({"backend": "gloo (rehearsal: not a measurement)"} if world > 1 and args.backend == "gloo" else {}),
             "roofline": rl,
         }

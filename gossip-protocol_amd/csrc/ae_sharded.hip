@@ -22,9 +22,7 @@ namespace gossip {
 namespace {
 
 constexpr int kAxBlock = 256;
-#ifndef GOSSIP_AEX_STATS_GRID
-#define GOSSIP_AEX_STATS_GRID 1024
-#endif
+constexpr uint32_t kAxStatsGrid = 1024;  // stats blocks (256 / 8192: slower)
 constexpr uint32_t kAxMaxG = 1024;
 
 // {alive, stale} word pair of the 64 nodes around global node n (one 16-B load)
@@ -537,7 +535,7 @@ template <bool STATS>
 void stats_l(const AexArgs& a, const uint32_t* R, hipStream_t st) {
   // 1024 blocks (each wave walks ~32 chunks): every block ends in ~20 same-address atomics on
   // the partials, which at 8192 blocks cost as much as the rows (2^23 rows: 157 us min)
-  const uint32_t g = ax_grid((a.nown + 63) / 64, kAxBlock / 64, GOSSIP_AEX_STATS_GRID);
+  const uint32_t g = ax_grid((a.nown + 63) / 64, kAxBlock / 64, kAxStatsGrid);
   switch (a.L) {
     case 1: aex_stats_kernel<1, STATS><<<g, kAxBlock, 0, st>>>(a, R); break;
     case 2: aex_stats_kernel<2, STATS><<<g, kAxBlock, 0, st>>>(a, R); break;
@@ -558,7 +556,7 @@ hipError_t launch_aex_finish(const AexArgs& a, const uint32_t* resp, uint64_t nr
     stats_l<true>(a, a.Vn, st);
     return hipGetLastError();
   }
-  const uint32_t g = ax_grid((a.nown + 63) / 64, kAxBlock / 64, GOSSIP_AEX_STATS_GRID);
+  const uint32_t g = ax_grid((a.nown + 63) / 64, kAxBlock / 64, kAxStatsGrid);
   switch (a.L) {
     case 1: aex_stats_inc_kernel<1><<<g, kAxBlock, 0, st>>>(a); break;
     case 2: aex_stats_inc_kernel<2><<<g, kAxBlock, 0, st>>>(a); break;

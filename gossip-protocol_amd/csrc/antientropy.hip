@@ -40,16 +40,8 @@ namespace {
 
 constexpr int kAeBlock = 256;
 constexpr int kAeWaves = kAeBlock / 64;
-// dense-round kernels: minimum waves per SIMD the compiler must fit (1 = no limit on VGPRs)
-#ifndef GOSSIP_AE_PULL_WAVES
-#define GOSSIP_AE_PULL_WAVES 1
-#endif
-#ifndef GOSSIP_AE_PUSH_WAVES
-#define GOSSIP_AE_PUSH_WAVES 1
-#endif
-#ifndef GOSSIP_AE_STATS_WAVES
-#define GOSSIP_AE_STATS_WAVES 1
-#endif
+// fallback dense-round kernels: no minimum waves per SIMD (forcing 3-6 spilled or was no
+// faster: DESIGN.md §3.7)
 
 __device__ __forceinline__ bool churned(uint8_t alive, uint32_t n, uint32_t t, uint32_t k0, uint32_t k1,
                                         uint32_t fail, uint32_t rec) {
@@ -159,7 +151,7 @@ struct MaskOf {  // one bit per lane of a node's group
 // every row — and, per exchange, the mask of components where V[n] > V[p_j]: the
 // push pass then needs neither the peer's row nor its alive bit
 template <uint32_t L>
-__global__ __launch_bounds__(kAeBlock, GOSSIP_AE_PULL_WAVES) void ae_pull_kernel(AeArgs a) {
+__global__ __launch_bounds__(kAeBlock) void ae_pull_kernel(AeArgs a) {
   using MT = typename MaskOf<L>::T;
   constexpr uint32_t per = 64 / L;
   constexpr uint64_t gmask = L >= 64 ? ~0ull : ((1ull << L) - 1ull);
@@ -222,7 +214,7 @@ __global__ __launch_bounds__(kAeBlock, GOSSIP_AE_PULL_WAVES) void ae_pull_kernel
 
 // push pass: atomicMax(Vn[p_j][c], V[n][c]) for the components c of the pull pass's mask
 template <uint32_t L>
-__global__ __launch_bounds__(kAeBlock, GOSSIP_AE_PUSH_WAVES) void ae_push_kernel(AeArgs a) {
+__global__ __launch_bounds__(kAeBlock) void ae_push_kernel(AeArgs a) {
   using MT = typename MaskOf<L>::T;
   constexpr uint32_t per = 64 / L;
   const uint32_t lane = threadIdx.x & 63, sub = lane / L, c = lane % L;
@@ -267,7 +259,7 @@ __global__ __launch_bounds__(kAeBlock, GOSSIP_AE_PUSH_WAVES) void ae_push_kernel
 // Here lane (sub, c) holds component c of nodes sub*L .. sub*L+L-1 (one per sub-step),
 // so a group's "differs" bits OR-reduce across its L lanes into its nodes' stale bits.
 template <uint32_t L>
-__global__ __launch_bounds__(kAeBlock, GOSSIP_AE_STATS_WAVES) void ae_stats_kernel(AeArgs a, const uint32_t* __restrict__ V, uint64_t* ab,
+__global__ __launch_bounds__(kAeBlock) void ae_stats_kernel(AeArgs a, const uint32_t* __restrict__ V, uint64_t* ab,
                                                             bool write_stale) {
   using BT = typename std::conditional<(L > 32), uint64_t, uint32_t>::type;
   constexpr uint32_t per = 64 / L;
@@ -395,17 +387,13 @@ __device__ __forceinline__ uint32_t ae_rec(uint32_t pl, uint32_t nl, uint32_t st
   return pl | (nl << btl) | (stale << (btl + brs));
 }
 
-#ifndef GOSSIP_AE_EMIT_WAVES
-#define GOSSIP_AE_EMIT_WAVES 8  // waves per SIMD: 8 = two blocks per CU (<= 64 VGPRs)
-#endif
-#ifndef GOSSIP_AE_EMIT_K1
-#define GOSSIP_AE_EMIT_K1 1  // k == 1 keeps the peers of pass A in registers (24 VGPRs spill at 8 waves;
-                             // still 0.516 vs 0.568 ms per sparse round redrawing them, profiles/r02_ae_one)
-#endif
+constexpr int kAeEmitWaves = 8;  // waves per SIMD: 8 = two blocks per CU (<= 64 VGPRs; 6 / 4 slower)
+// k == 1 keeps the peers of pass A in registers (24 VGPRs spill at 8 waves; still 0.516 vs
+// 0.568 ms per sparse round redrawing them, profiles/r02_ae_one)
 // NT: LDS tile counters (kAeBinTiles for the sparse scan's tiles, two blocks per CU;
 // kAeDTiles for the dense round's 2^14-node tiles, one block per CU)
 template <bool K1, uint32_t NT>
-__global__ __launch_bounds__(kAeBinThreads, (NT > kAeBinTiles ? 4 : GOSSIP_AE_EMIT_WAVES)) void ae_bin_emit_kernel(AeArgs a) {
+__global__ __launch_bounds__(kAeBinThreads, (NT > kAeBinTiles ? 4 : kAeEmitWaves)) void ae_bin_emit_kernel(AeArgs a) {
   __shared__ uint32_t cur[NT];
   __shared__ __align__(16) uint32_t st[kAeBinRec];  // read back as uint4
   __shared__ uint32_t wsum[kAeBinThreads / 64];
@@ -661,9 +649,6 @@ __device__ __forceinline__ void ae_tile_records(const AeArgs& a, const uint32_t*
   }
 }
 
-#ifndef GOSSIP_ABL_AED
-#define GOSSIP_ABL_AED 0  // timing ablations (results wrong): 1 no node phase, 2 no in-edge sort
-#endif
 
 // The in-edge sort of tile T, shared by both apply kernels (NW waves per block).  pos2
 // holds u16 counts, then starts, then (after a fill) ends, packed in pairs: a tile's
@@ -686,8 +671,7 @@ __device__ void ae_sort_count(const AeArgs& a, const AeSortSh& sh, uint32_t T) {
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (uint32_t i = tid; i < kAeDTile / 2; i += nth) sh.pos2[i] = 0;
   __syncthreads();
-  if (GOSSIP_ABL_AED != 2)
-    ae_tile_records<NW>(a, sh.rt, T, [&](uint32_t rec, uint32_t) {
+  ae_tile_records<NW>(a, sh.rt, T, [&](uint32_t rec, uint32_t) {
       const uint32_t pl = rec & (kAeDTile - 1u);
       atomicAdd(&sh.pos2[pl >> 1], 1u << ((pl & 1u) << 4));
     });
@@ -748,7 +732,7 @@ __device__ uint32_t ae_sort_range(const AeArgs& a, const AeSortSh& sh, uint32_t 
   __syncthreads();
   const uint32_t hi = sh.rng[0], base = sh.rng[1];
   const uint32_t nmask = (1u << a.brs) - 1u;
-  if (GOSSIP_ABL_AED != 2 && ae_pget(sh, hi) != base) {
+  if (ae_pget(sh, hi) != base) {
     ae_tile_records<NW>(a, sh.rt, T, [&](uint32_t rec, uint32_t reg) {
       const uint32_t pl = rec & (kAeDTile - 1u);
       if (pl >= lo && pl < hi) {
@@ -805,7 +789,7 @@ __global__ __launch_bounds__(kAeDThreads) void ae_dense_apply_kernel(AeArgs a) {
     uint32_t base;
     const uint32_t hi = ae_sort_range<kW>(a, sh, T, tn, lo, cap, &base);
     // node p's in-edges now end at pget(p) and start at pget(p - 1) (base for p = lo)
-    for (uint32_t ch = (lo >> 6) + wave; GOSSIP_ABL_AED != 1 && ch < (hi + 63) >> 6; ch += kW) {
+    for (uint32_t ch = (lo >> 6) + wave; ch < (hi + 63) >> 6; ch += kW) {
       const uint64_t gch = (t0 >> 6) + ch;
       const uint64_t nb = t0 + ((uint64_t)ch << 6);
       const uint32_t n = (uint32_t)(nb + lane);
@@ -909,11 +893,8 @@ __global__ __launch_bounds__(kAeDThreads) void ae_dense_apply_kernel(AeArgs a) {
 // components 4q .. 4q+3 of row r of a 16-row piece group, so the gathers need a quarter of
 // the address registers and the kernel fits 16 waves per CU (the LDS table of run starts
 // gives way to the per-wave scratch; the run starts come from L2).
-#ifndef GOSSIP_AEQ_WAVES
-#define GOSSIP_AEQ_WAVES 12  // 12 waves per CU: 168 VGPRs (16 spill at 128)
-#endif
-constexpr uint32_t kAeQThreads = GOSSIP_AEQ_WAVES * 64;
-constexpr uint32_t kAeQCap = GOSSIP_AEQ_WAVES > 12 ? 15360 : 18432;  // sorted in-edges per pass (LDS)
+constexpr uint32_t kAeQThreads = 12 * 64;  // 12 waves per CU: 168 VGPRs (16 waves: 16 spill at 128, slower)
+constexpr uint32_t kAeQCap = 18432;        // sorted in-edges per pass (LDS)
 
 __device__ __forceinline__ uint4 max4(uint4 x, uint4 y) {
   return uint4{max(x.x, y.x), max(x.y, y.y), max(x.z, y.z), max(x.w, y.w)};
@@ -922,10 +903,7 @@ __device__ __forceinline__ uint4 max4(uint4 x, uint4 y) {
 template <uint32_t KJ>
 __global__ __launch_bounds__(kAeQThreads) void ae_dense_apply_q_kernel(AeArgs a) {
   constexpr uint32_t kW = kAeQThreads / 64;
-#ifndef GOSSIP_AEQ_GROUPS
-#define GOSSIP_AEQ_GROUPS 4
-#endif
-  constexpr uint32_t kBQ = GOSSIP_AEQ_GROUPS;  // in-edge piece groups in flight (16 edges each)
+  constexpr uint32_t kBQ = 4;  // in-edge piece groups in flight (16 edges each)
   __shared__ uint32_t pos2[kAeDTile / 2];
   __shared__ uint32_t srt[kAeQCap];
   __shared__ __align__(16) uint32_t scr[kW][64 * 16];
@@ -950,7 +928,7 @@ __global__ __launch_bounds__(kAeQThreads) void ae_dense_apply_q_kernel(AeArgs a)
   for (uint32_t lo = 0; lo < tn;) {
     uint32_t base;
     const uint32_t hi = ae_sort_range<kW>(a, sh, T, tn, lo, cap, &base);
-    for (uint32_t ch = (lo >> 6) + wave; GOSSIP_ABL_AED != 1 && ch < (hi + 63) >> 6; ch += kW) {
+    for (uint32_t ch = (lo >> 6) + wave; ch < (hi + 63) >> 6; ch += kW) {
       const uint64_t gch = (t0 >> 6) + ch;
       const uint64_t nb = t0 + ((uint64_t)ch << 6);
       const uint32_t n = (uint32_t)(nb + lane);
@@ -973,13 +951,8 @@ __global__ __launch_bounds__(kAeQThreads) void ae_dense_apply_q_kernel(AeArgs a)
       u32x4 x{0, 0, 0, 0};
 #pragma unroll
       for (uint32_t j = 0; j < KJ; ++j) pj[j] = aln ? peer_j(a, n, j, x) : 0u;
-#ifndef GOSSIP_AEQ_PROBE
-#define GOSSIP_AEQ_PROBE 0  // 1: the peers' alive bits awaited before their gathers (no dead-peer rows)
-#endif
-      if (GOSSIP_AEQ_PROBE) {
-#pragma unroll
-        for (uint32_t j = 0; j < KJ; ++j) exj[j] = aln && alive_bit(a.abn, pj[j]);
-      }
+      // every peer row is gathered at once; the alive bits are checked after (awaiting them
+      // first costs a round trip per chunk: DESIGN.md §3.8)
       uint4 vp[KJ][4];
 #pragma unroll
       for (uint32_t j = 0; j < KJ; ++j)
@@ -987,10 +960,10 @@ __global__ __launch_bounds__(kAeQThreads) void ae_dense_apply_q_kernel(AeArgs a)
         for (uint32_t g = 0; g < 4; ++g) {
           const uint32_t src = g * 16 + r;
           const uint32_t pp = (uint32_t)__shfl((int)pj[j], (int)src, 64);
-          const bool go = __shfl((int)(GOSSIP_AEQ_PROBE ? exj[j] : aln), (int)src, 64);
+          const bool go = __shfl((int)aln, (int)src, 64);
           vp[j][g] = go ? *row(pp) : uint4{0, 0, 0, 0};
         }
-      if (!GOSSIP_AEQ_PROBE) {
+      {
 #pragma unroll
         for (uint32_t j = 0; j < KJ; ++j) exj[j] = aln && alive_bit(a.abn, pj[j]);
       }
@@ -1292,7 +1265,7 @@ bool ae_bin_fits(const AeBinGeom& g) { return g.nt <= kAeBinTiles; }
 
 hipError_t launch_ae_sparse_binned(const AeArgs& a, hipStream_t st) {
   const uint32_t eg = a.bnreg < 512 ? a.bnreg : 512;  // two blocks per CU
-  if (GOSSIP_AE_EMIT_K1 && a.k == 1 && (1u << a.brs) == kAeBinRec)
+  if (a.k == 1 && (1u << a.brs) == kAeBinRec)
     ae_bin_emit_kernel<true, kAeBinTiles><<<eg, kAeBinThreads, 0, st>>>(a);
   else
     ae_bin_emit_kernel<false, kAeBinTiles><<<eg, kAeBinThreads, 0, st>>>(a);
@@ -1318,7 +1291,7 @@ bool ae_dense_fits(const AeBinGeom& g, uint64_t N, uint32_t k, uint32_t K) {
 
 hipError_t launch_ae_dense_binned(const AeArgs& a, hipStream_t st) {
   const uint32_t eg = a.bnreg < 256 ? a.bnreg : 256;  // one block per CU (LDS)
-  if (GOSSIP_AE_EMIT_K1 && a.k == 1 && (1u << a.brs) == kAeBinRec)
+  if (a.k == 1 && (1u << a.brs) == kAeBinRec)
     ae_bin_emit_kernel<true, kAeDTiles><<<eg, kAeBinThreads, 0, st>>>(a);
   else
     ae_bin_emit_kernel<false, kAeDTiles><<<eg, kAeBinThreads, 0, st>>>(a);

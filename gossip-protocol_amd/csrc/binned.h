@@ -75,7 +75,6 @@ struct BinBufs {
   uint16_t* offT;   // [nt_d + 1][nt_s]
   uint64_t* nzb;    // occupancy bitmaps of S_{t+1} written by K3 (frontier.h), or null
   uint64_t* fullb;
-  uint32_t* xsync;  // [16] per-XCD tile barriers of the persistent serve / apply (GOSSIP_XCD_SYNC), or null
 };
 
 size_t bin_bytes(const BinGeom& g);
@@ -131,12 +130,9 @@ hipError_t launch_sb_round(const SbGeom& g, const SbBufs& b, const uint64_t* ima
 // tiles.  Per-shard work is O(nodes per shard) at any G.
 constexpr uint32_t kXdNoPush = 1u << 30;  // wire item id: p at the owner [0, 30) | these two flags
 constexpr uint32_t kXdNoPull = 1u << 31;
-#ifndef GOSSIP_XD_REGION
-#define GOSSIP_XD_REGION 8192
-#endif
 // received items binned per LDS region (<= 16384; at <= 8192 their values are staged in LDS
 // too: G = 8 probe 17.44 ms against 17.62 ms with 16384, profiles/r02_xd)
-constexpr uint32_t kXdBinRegion = GOSSIP_XD_REGION;
+constexpr uint32_t kXdBinRegion = 8192;
 struct XdGeom {
   uint64_t N, Nl, lo, nown;
   uint32_t G, rank, k;

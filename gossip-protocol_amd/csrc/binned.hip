@@ -33,92 +33,43 @@ namespace gossip {
 namespace {
 
 constexpr int kEmitThreads = 1024;
-#ifndef GOSSIP_EMIT_GRID
-#define GOSSIP_EMIT_GRID 256
-#endif
-constexpr uint32_t kEmitGrid = GOSSIP_EMIT_GRID;  // one persistent emit block per CU
+constexpr uint32_t kEmitGrid = 256;  // one persistent emit block per CU (128 / 64 slower: DESIGN.md §3.7)
 constexpr int kTileThreads = 1024;
 constexpr uint32_t kServeGrid = 256;  // persistent serve: one block per CU (the tile image takes 128 KiB of LDS)
 constexpr uint32_t kApplyGrid = 256;  // persistent apply, likewise
-#ifndef GOSSIP_APPLY_PRE
-#define GOSSIP_APPLY_PRE 0
-#endif
-constexpr uint32_t kApplyPre = GOSSIP_APPLY_PRE;  // uint4 slots per thread of the next tile prefetched in apply
-#ifndef GOSSIP_APPLY_UNROLL
-#define GOSSIP_APPLY_UNROLL 16
-#endif
-constexpr int kUnroll = GOSSIP_APPLY_UNROLL;  // records in flight per lane in the run walkers (32 spills in K3)
-#ifndef GOSSIP_SERVE_UNROLL
-#define GOSSIP_SERVE_UNROLL 16
-#endif
-#ifndef GOSSIP_SEQ_UNROLL
-#define GOSSIP_SEQ_UNROLL 8
-#endif
-#ifndef GOSSIP_APPLY_PUSH_WAVES
-#define GOSSIP_APPLY_PUSH_WAVES 8
-#endif
-constexpr int kUnrollServe = GOSSIP_SERVE_UNROLL;
-constexpr int kUnrollSeq = GOSSIP_SEQ_UNROLL;  // records in flight per lane in the sequential response walker
+constexpr int kUnroll = 16;  // records in flight per lane in the run walkers (32 spills in K3)
+constexpr int kUnrollServe = 16;
+constexpr int kUnrollSeq = 8;  // records in flight per lane in the sequential response walker
 // push-pull apply: waves [0, push_waves) walk the pushes, the rest the responses
 // (BinGeom::push_waves, this default up to 2^25 nodes)
-constexpr uint32_t kPushWaves = GOSSIP_APPLY_PUSH_WAVES;
+constexpr uint32_t kPushWaves = 8;
 // past 2^25 nodes the pushes come in short runs (~4 records at 2^27) and their walk
 // sets the pace: 12 of the 16 waves (2^27 apply 2930 -> 2710 us, 10: 2745;
 // profiles/r03_var27); 10 at 2^24 was slower (549 vs 542 us, round 2)
 constexpr uint32_t kPushWavesBig = 12;
-#ifndef GOSSIP_APPLY_SPLIT
-#define GOSSIP_APPLY_SPLIT 1
-#endif
 // push-pull apply: the block's waves split between the push walk (fragmented runs)
 // and the response walk (sequential regions), which then run side by side
-constexpr bool kApplySplit = GOSSIP_APPLY_SPLIT != 0;
-#ifndef GOSSIP_NT_REC
-#define GOSSIP_NT_REC 1  // emit's record stores (bench: serve -28 us, apply -10 us per dense round)
-#endif
-// Record buffers are written once and read once (or twice) per round: the
-// accesses in GOSSIP_NT_REC's mask carry the non-temporal hint, so the streamed
-// records do not displace the state image from the caches.  Bits: 1 emit
-// stores, 2 serve id loads, 4 serve response stores, 8 apply push loads, 16
-// apply response-walk loads.
-template <int BIT, typename T>
+constexpr bool kApplySplit = true;
+// Record buffers are written once and read once (or twice) per round: emit's record
+// stores carry the non-temporal hint, so the streamed records do not displace the
+// state image from the caches (bench: serve -28 us, apply -10 us per dense round).
+// The same hint on the other record accesses was slower or equal.
+template <typename T>
 __device__ __forceinline__ void rec_st(T* p, T v) {
-  if constexpr ((GOSSIP_NT_REC & BIT) != 0) __builtin_nontemporal_store(v, p);
-  else *p = v;
+  __builtin_nontemporal_store(v, p);
 }
-template <int BIT, typename T>
-__device__ __forceinline__ T rec_ld(const T* p) {
-  if constexpr ((GOSSIP_NT_REC & BIT) != 0) return __builtin_nontemporal_load(p);
-  else return *p;
-}
-// A packed push {value lo, hi, id} moves as one 12-B access (global_load/store_dwordx3):
-// one address per lane instead of three (the run walkers are bound by the vector memory
-// instructions' address work, not bytes: DESIGN.md §3.7)
+// A packed push {value lo, hi, id} moves as one 12-B access (global_load/store_dwordx3)
 typedef uint32_t u32x3v __attribute__((ext_vector_type(3)));
-#ifndef GOSSIP_PREC_X3
-#define GOSSIP_PREC_X3 1
-#endif
 __device__ __forceinline__ void prec_st(uint32_t* p, uint32_t a, uint32_t b, uint32_t c) {
-  if constexpr (GOSSIP_PREC_X3) {
-    u32x3v v = {a, b, c};
-    __builtin_memcpy(p, &v, 12);
-  } else {
-    rec_st<1>(&p[0], a);
-    rec_st<1>(&p[1], b);
-    rec_st<1>(&p[2], c);
-  }
+  u32x3v v = {a, b, c};
+  __builtin_memcpy(p, &v, 12);
 }
 __device__ __forceinline__ void prec_ld(const uint32_t* p, uint32_t& a, uint32_t& b, uint32_t& c) {
-  if constexpr (GOSSIP_PREC_X3) {
-    u32x3v v;
-    __builtin_memcpy(&v, p, 12);
-    a = v.x;
-    b = v.y;
-    c = v.z;
-  } else {
-    a = rec_ld<8>(&p[0]);
-    b = rec_ld<8>(&p[1]);
-    c = rec_ld<8>(&p[2]);
-  }
+  u32x3v v;
+  __builtin_memcpy(&v, p, 12);
+  a = v.x;
+  b = v.y;
+  c = v.z;
 }
 
 // record id word: p_local [0,14) | n_local [14,28) | flags.  K1 rewrites every
@@ -132,27 +83,6 @@ constexpr uint32_t kIdNMask = (1u << 14) - 1u;
 // less per dense round.  dst = p_local | no-push << 14 | no-pull << 15; src = n_local |
 // no-pull << 15.  The readers rebuild the u32 id fields they use.
 constexpr uint16_t kDstVZ = 1u << 14, kDstVF = 1u << 15, kSrcVF = 1u << 15;
-// timing ablations (tools/build_variants.sh; results are wrong): GOSSIP_ABL_SERVE 1 no reply
-// stores, 2 contiguous reply stores; GOSSIP_ABL_APPLY 1 no push walk, 2 no reply walk;
-// GOSSIP_ABL_EMIT 1 no packed push stores
-#ifndef GOSSIP_ABL_SERVE
-#define GOSSIP_ABL_SERVE 0
-#endif
-#ifndef GOSSIP_ABL_APPLY
-#define GOSSIP_ABL_APPLY 0
-#endif
-#ifndef GOSSIP_ABL_EMIT
-#define GOSSIP_ABL_EMIT 0
-#endif
-#ifndef GOSSIP_AOS_SMALL
-#define GOSSIP_AOS_SMALL 0  // 1: packed {value, id} pushes below 4096 tiles too (A/B)
-#endif
-#ifndef GOSSIP_EMIT_PK
-#define GOSSIP_EMIT_PK 1  // big-region emit keeps each sender's peers in LDS between its passes (0: draws twice)
-#endif
-#ifndef GOSSIP_SPLIT_IDS
-#define GOSSIP_SPLIT_IDS 1  // 0: u32 ids below kMaxTilesD tiles (A/B; big regions always split)
-#endif
 __device__ __forceinline__ uint16_t dst_of(uint32_t id) {
   return (uint16_t)((id & (kTileD - 1)) | ((id & kIdVZ) ? kDstVZ : 0u) | ((id & kIdVF) ? kDstVF : 0u));
 }
@@ -172,26 +102,6 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {
   // range of tiles so neighbouring runs share its L2 (speed only)
   if (n & 7u) return b;
   return (b & 7u) * (n >> 3) + (b >> 3);
-}
-
-#ifndef GOSSIP_XCD_SYNC
-#define GOSSIP_XCD_SYNC 0  // 1: serve, 2: apply, 3: both start every tile with the other blocks of their XCD (A/B)
-#endif
-// Speed only (no data passes between the blocks): the persistent blocks that share an XCD
-// (blockIdx & 7) start tile iteration `it` together, so the neighbouring runs their walks read and
-// write meet in that XCD's L2 at the same time.  Bounded spin: a block that waits too long goes on.
-__device__ __forceinline__ void xcd_tile_barrier(uint32_t* ctr, uint32_t it) {
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t grp = blockIdx.x & 7u, members = (gridDim.x + 7u - grp) / 8u;
-    atomicAdd(&ctr[grp], 1u);
-    const uint32_t target = members * it;
-    for (int spin = 0; spin < 4000; ++spin) {
-      if (__hip_atomic_load(&ctr[grp], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
-      __builtin_amdgcn_s_sleep(2);
-    }
-  }
-  __syncthreads();
 }
 
 // Which directions an edge n -> p carries (bit 0 push, bit 1 pull; 0: no
@@ -324,7 +234,6 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
   // peers and edge directions in the LDS staging room ({p0, p1, dirs} in a u64: p < 2^27), so
   // the placement pass draws no Philox again (one cipher per sender instead of two)
   constexpr bool PKC = V == 5;
-  constexpr bool PK = PKC;
   constexpr uint32_t kMaxT = V >= 2 ? kSbMaxTiles : kMaxTilesD;
   constexpr uint32_t kMaxS = BIG ? 2 * kMaxSenders : kMaxSenders;
   __shared__ uint32_t cur[BIG ? kMaxT / 2 : kMaxT];
@@ -457,7 +366,7 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
           tile_of(pr[q * KREG + j], &tl, &pl);
           count_tile(tl);
         }
-  } else if (PKC && PK) {
+  } else if (PKC) {
     uint64_t* pkl = (uint64_t*)st_ids;  // kMaxS u64 = the staging room, free until placement
 #pragma unroll
     for (uint32_t q = 0; q < kQ; ++q) {
@@ -525,7 +434,7 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
         st_ids[pos] = pl | (i << kTileDLog) | dir_flags(d);
       }
     }
-  } else if (PKC && PK) {
+  } else if (PKC) {
     uint64_t mine[kQ];
 #pragma unroll
     for (uint32_t q = 0; q < kQ; ++q) mine[q] = ((const uint64_t*)st_ids)[tid + q * kEmitThreads];
@@ -576,7 +485,7 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
   uint16_t* gdst = b.dst + (size_t)s * g.rp;
   uint16_t* gsrc = b.src + (size_t)s * g.rp;
   // the one-shard emits (BinGeom::split); V = 1, 2: sharded passes
-  constexpr bool split = (V == 0 && GOSSIP_SPLIT_IDS) || V >= 3;
+  constexpr bool split = V == 0 || V >= 3;
   if constexpr (BIG) {
     // ids out first, then the region's sender values take the staging room and each
     // push is written packed {value, id} (BinGeom::aos), its value read from LDS: the
@@ -596,7 +505,7 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
     }
     __syncthreads();  // every staged id is out
     uint64_t* sv = (uint64_t*)st_ids;  // 2 * kRecPerRegion u32 = kMaxS u64
-    if (PKC && PK) {  // v[] was let go after the count pass (its registers held the peers): reread
+    if (PKC) {  // v[] was let go after the count pass (its registers held the peers): reread
 #pragma unroll
       for (uint32_t q = 0; q < kQ; ++q) {
         const uint32_t i = tid + q * kEmitThreads;
@@ -610,7 +519,7 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
     __syncthreads();
     uint32_t* gprec = b.prec + (size_t)s * g.rp * 3;
 #pragma unroll 4
-    for (uint32_t e = tid; e < (GOSSIP_ABL_EMIT == 1 ? 0u : total); e += kEmitThreads) {
+    for (uint32_t e = tid; e < total; e += kEmitThreads) {
       const uint32_t id = split ? id_of_pair(gdst[e], gsrc[e]) : gids[e];
       const uint64_t x = sv[(id >> kTileDLog) & kIdNMask];  // (big regions always pack: g.aos)
       prec_st(&gprec[3 * e], (uint32_t)x, (uint32_t)(x >> 32), id);
@@ -622,18 +531,15 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
     // region is written without holes (a partly written 64-B chunk costs HBM
     // a read-modify-write: profiles/r01_experiments/microbench5_scattered_pieces.jsonl)
     if (split) {
-      rec_st<1>(&gdst[e], dst_of(id));
-      rec_st<1>(&gsrc[e], src_of(id));
+      rec_st(&gdst[e], dst_of(id));
+      rec_st(&gsrc[e], src_of(id));
     } else {
-      rec_st<1>(&gids[e], id);
+      rec_st(&gids[e], id);
     }
-    if (STAGE && V == 0 && g.aos) {  // (GOSSIP_AOS_SMALL) the push packed {value, id} as past 2^26 nodes
-      const uint64_t x = sval[(id >> kTileDLog) & kIdNMask];
-      prec_st(&b.prec[3 * ((size_t)s * g.rp + e)], (uint32_t)x, (uint32_t)(x >> 32), id);
-    } else if (STAGE) {
-      rec_st<1>(&gvals[e], sval[(id >> kTileDLog) & kIdNMask]);
+    if (STAGE) {
+      rec_st(&gvals[e], sval[(id >> kTileDLog) & kIdNMask]);
     }
-    if (V >= 3) rec_st<1>(&gvals[e], S[base + ((id >> kTileDLog) & kIdNMask)]);
+    if (V >= 3) rec_st(&gvals[e], S[base + ((id >> kTileDLog) & kIdNMask)]);
   }
   if constexpr (!BIG) {
 #pragma unroll
@@ -880,13 +786,13 @@ __device__ __forceinline__ void push_walk(const BinGeom& g, const BinBufs& b, ui
     } else {
       if constexpr (SPLIT) {
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) id[u] = id_of_dst(rec_ld<8>(&b.dst[rec[u] >= 0 ? rec[u] : 0]));
+        for (int u = 0; u < kUnroll; ++u) id[u] = id_of_dst(*(&b.dst[rec[u] >= 0 ? rec[u] : 0]));
       } else {
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) id[u] = rec_ld<8>(&gids[rec[u] >= 0 ? rec[u] : 0]);
+        for (int u = 0; u < kUnroll; ++u) id[u] = *(&gids[rec[u] >= 0 ? rec[u] : 0]);
       }
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) v[u] = rec_ld<8>(&gvals[rec[u] >= 0 ? rec[u] : 0]);  // not behind the id: both loads fly together
+      for (int u = 0; u < kUnroll; ++u) v[u] = *(&gvals[rec[u] >= 0 ? rec[u] : 0]);  // not behind the id: both loads fly together
     }
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u)
@@ -939,7 +845,6 @@ __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, cons
   if (blockIdx.x < nv) tile_regs_load(x, S, (uint64_t)tile_of(blockIdx.x) << kTileDLog, g.N);
   for (uint32_t v = blockIdx.x; v < nv; v += gridDim.x) {
   const uint32_t T = tile_of(v);
-  if ((GOSSIP_XCD_SYNC & 1) && b.xsync && v != blockIdx.x) xcd_tile_barrier(b.xsync, (v - blockIdx.x) / gridDim.x);
   __syncthreads();  // the previous walk is done with img
 #pragma unroll
   for (uint32_t q = 0; q < kTileQ; ++q) ((uint4*)img)[q * kTileThreads + threadIdx.x] = x[q];
@@ -948,20 +853,14 @@ __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, cons
   const uint32_t* gids = b.ids;
   uint64_t* __restrict__ gresp = b.resp;
   const uint16_t* rowb = b.offT + (size_t)T * g.nt_s;
-#if GOSSIP_ABL_SERVE
-  uint64_t abl_x = 0;
-  uint32_t abl_c = 0;
-  const uint64_t abl_cap = (uint64_t)g.nt_s * g.rp;
-  const uint32_t abl_zero = R >> 8;  // 0, unknown to the compiler
-#endif
   for_each_run_record<kUnrollServe>(g, rowb, rowb + g.nt_s, wmask, wlist, [&](const int32_t* rec) {
     uint32_t id[kUnrollServe];
     if constexpr (SPLIT) {  // (one shard only: VF == kIdVF)
 #pragma unroll
-      for (int u = 0; u < kUnrollServe; ++u) id[u] = id_of_dst(rec_ld<2>(&b.dst[rec[u] >= 0 ? rec[u] : 0]));
+      for (int u = 0; u < kUnrollServe; ++u) id[u] = id_of_dst(*(&b.dst[rec[u] >= 0 ? rec[u] : 0]));
     } else {
 #pragma unroll
-      for (int u = 0; u < kUnrollServe; ++u) id[u] = rec_ld<2>(&gids[rec[u] >= 0 ? rec[u] : 0]);
+      for (int u = 0; u < kUnrollServe; ++u) id[u] = *(&gids[rec[u] >= 0 ? rec[u] : 0]);
     }
 #pragma unroll
     for (int u = 0; u < kUnrollServe; ++u) {
@@ -969,33 +868,9 @@ __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, cons
       // back (bits n already holds are harmless to OR), so no value is read
       // dense rounds: every response is written (K3 tells stale slots by kIdVF)
       if (rec[u] < 0 || (id[u] & VF)) continue;
-#if GOSSIP_ABL_SERVE == 1  // timing ablation: no reply stores
-      abl_x ^= (uint64_t)img[id[u] & (kTileD - 1)];
-#elif GOSSIP_ABL_SERVE == 3  // timing ablation: the reply overwrites the push value it has just read
-      if (b.prec) {
-        uint32_t* r = &b.prec[3ull * (uint32_t)rec[u]];
-        const uint32_t lo = r[0] & abl_zero, hi = r[1] & abl_zero;
-        const uint64_t y = (uint64_t)img[id[u] & (kTileD - 1)];
-        r[0] = (uint32_t)y | lo;
-        r[1] = (uint32_t)(y >> 32) | hi;
-      } else {
-        uint64_t* r = &b.vals[rec[u]];
-        *r = (uint64_t)img[id[u] & (kTileD - 1)] | (*r & abl_zero);
-      }
-#elif GOSSIP_ABL_SERVE == 2  // timing ablation: reply stores contiguous per wave window
-      const uint64_t q = (uint64_t)T * 32768u + ((((threadIdx.x >> 6) << 11) + abl_c + u * 64 + (threadIdx.x & 63)) & 32767u);
-      rec_st<4>(&gresp[q < abl_cap ? q : abl_cap - 1], (uint64_t)img[id[u] & (kTileD - 1)]);
-#else
-      rec_st<4>(&gresp[rec[u]], (uint64_t)img[id[u] & (kTileD - 1)]);
-#endif
+      gresp[rec[u]] = (uint64_t)img[id[u] & (kTileD - 1)];
     }
-#if GOSSIP_ABL_SERVE == 2
-    abl_c += 64 * kUnrollServe;
-#endif
   });
-#if GOSSIP_ABL_SERVE == 1
-  if (abl_x == 0x123456789abcdefull) gresp[0] = abl_x;
-#endif
   }
 }
 
@@ -1026,33 +901,23 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
   // the next tile's S_t loads into registers during the current tile's work.  In
   // place stays safe: only this block reads or writes S[X] of its tiles.
   const uint32_t nv = g.nt_d;
-  constexpr uint32_t kPre = kApplyPre;
-  constexpr uint32_t kPreN = kPre ? kPre : 1;  // (kPre = 0: xt unused)
-  uint4 xt[kPreN];
-  if (kPre && blockIdx.x < nv) tile_regs_load<0, kPreN>(xt, S, (uint64_t)xcd_remap(blockIdx.x, nv) << kTileDLog, Nn);
   for (uint32_t v = blockIdx.x; v < nv; v += gridDim.x) {
   const uint32_t X = xcd_remap(v, nv);
   const uint64_t node0 = (uint64_t)X << kTileDLog;
-  if ((GOSSIP_XCD_SYNC & 2) && b.xsync && v != blockIdx.x)
-    xcd_tile_barrier(b.xsync + 8, (v - blockIdx.x) / gridDim.x);
   __syncthreads();  // the previous epilogue is done with acc and cnt
   {
-    uint4 xr[kTileQ - kPre];
-    tile_regs_load<kPre, kTileQ - kPre>(xr, S, node0, Nn);
-    if constexpr (kPre > 0) {
+    uint4 xr[kTileQ];
+    tile_regs_load(xr, S, node0, Nn);
 #pragma unroll
-      for (uint32_t q = 0; q < kPre; ++q) ((uint4*)acc)[q * kTileThreads + tid] = xt[q];
-    }
-#pragma unroll
-    for (uint32_t q = 0; q < kTileQ - kPre; ++q) ((uint4*)acc)[(kPre + q) * kTileThreads + tid] = xr[q];
+    for (uint32_t q = 0; q < kTileQ; ++q) ((uint4*)acc)[q * kTileThreads + tid] = xr[q];
   }
   if (tid < 64) cnt[tid] = 0;
   __syncthreads();
   const uint32_t wave = tid >> 6;
   const bool split = kApplySplit && mode == 3;
   const uint32_t pw = g.push_waves;
-  const bool do_push = (mode == 1 || mode == 3) && (!split || wave < pw) && GOSSIP_ABL_APPLY != 1;
-  const bool do_pull = (mode == 2 || mode == 3) && (!split || wave >= pw) && GOSSIP_ABL_APPLY != 2;
+  const bool do_push = (mode == 1 || mode == 3) && (!split || wave < pw);
+  const bool do_pull = (mode == 2 || mode == 3) && (!split || wave >= pw);
   // split: waves [0, pw) walk the pushes, the others the responses
   const uint32_t qt0 = split ? pw * 64 : 0u, qnt = split ? kTileThreads - pw * 64 : kTileThreads;
   constexpr bool SPLIT = LAYOUT >= 1;
@@ -1074,9 +939,9 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
 #pragma unroll
         for (int u = 0; u < kUnrollSeq; ++u) {
           const uint32_t pos = min(p0 + u * qnt + qtid, total - 1);
-          if constexpr (SPLIT) id[u] = id_of_src(rec_ld<16>(&bq.src[reg + pos]));
-          else id[u] = rec_ld<16>(&qids[reg + pos]);
-          r[u] = rec_ld<16>(&gresp[reg + pos]);
+          if constexpr (SPLIT) id[u] = id_of_src(*(&bq.src[reg + pos]));
+          else id[u] = *(&qids[reg + pos]);
+          r[u] = *(&gresp[reg + pos]);
         }
 #pragma unroll
         for (int u = 0; u < kUnrollSeq; ++u) {
@@ -1088,9 +953,6 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
       }
     }
   }
-  // kApplyPre slots of the next tile's loads fly during the epilogue (all 8,
-  // or during the walks, spill: 4 spill 22 VGPRs)
-  if (kPre && v + gridDim.x < nv) tile_regs_load<0, kPreN>(xt, S, (uint64_t)xcd_remap(v + gridDim.x, nv) << kTileDLog, Nn);
   __syncthreads();
   tile_epilogue(acc, node0, Nn, hid0, Snext, partial, R, flags, cnt, red_hash, red_full, red_nz, b.nzb, b.fullb);
   }
@@ -1125,8 +987,8 @@ BinGeom make_bin_geom(uint64_t N, uint32_t k, bool big) {
   // walk is bound by the number of distinct lines it fetches: a push packed as one 12-B
   // piece beside the 4-B id (for serve and the reply walk) touches fewer than the two
   // arrays' 16-B + 32-B pieces of a run
-  g.aos = big || GOSSIP_AOS_SMALL ? 1u : 0u;
-  g.split = big || GOSSIP_SPLIT_IDS ? 1u : 0u;  // (sharded geometries clear it: their passes keep u32 ids)
+  g.aos = big ? 1u : 0u;  // (packed pushes at 2^24: 570 vs 520 us per dense round)
+  g.split = 1u;  // (sharded geometries clear it: their passes keep u32 ids)
   return g;
 }
 
@@ -1167,8 +1029,6 @@ void bin_carve(const BinGeom& g, void* base, BinBufs* b) {
   b->off = (uint16_t*)p;
   p += al((size_t)g.nt_s * (g.nt_d + 1) * 2);
   b->offT = (uint16_t*)p;
-  p += al((size_t)g.nt_s * (g.nt_d + 1) * 2);
-  b->xsync = (uint32_t*)p;
 }
 
 hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, uint64_t* partial, uint32_t R,
@@ -1188,7 +1048,7 @@ hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, 
     // 16 senders per lane keep no room for their peers in registers (KREG = 2 spills 78
     // VGPRs): V = 5 keeps them in LDS between the passes, V = 4 draws them again
     if (fa.any()) GOSSIP_EMIT(0, true, 4);
-    else if (GOSSIP_EMIT_PK && g.k <= 2) GOSSIP_EMIT(0, false, 5);
+    else if (g.k <= 2) GOSSIP_EMIT(0, false, 5);
     else GOSSIP_EMIT(0, false, 4);
   } else if (g.nt_d <= kMaxTilesD) {
     GOSSIP_EMIT_V(0)
@@ -1198,10 +1058,6 @@ hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, 
 #undef GOSSIP_EMIT_V
 #undef GOSSIP_EMIT
   launch_transpose_u16(b.off, b.offT, g.nt_s, g.nt_d + 1, partial, rs.plen, st);
-  if (GOSSIP_XCD_SYNC && b.xsync) {
-    const hipError_t me = hipMemsetAsync(b.xsync, 0, 16 * sizeof(uint32_t), st);
-    if (me != hipSuccess) return me;
-  }
   if ((mode == 2 || mode == 3) && g.split)
     bin_serve_kernel<kIdVF, true><<<serve_grid(g.nt_d, g.serve_grid), kTileThreads, 0, st>>>(g, S, b, R,
                                                                                           IdxRange::all(g.nt_d));
@@ -1247,7 +1103,6 @@ size_t sb_bytes(const SbGeom& g) { return bin_bytes(g.p) + bin_bytes(g.q); }
 void sb_carve(const SbGeom& g, void* base, SbBufs* b) {
   bin_carve(g.p, base, &b->p);
   bin_carve(g.q, (char*)base + bin_bytes(g.p), &b->q);
-  b->p.xsync = b->q.xsync = nullptr;  // (the tile barriers are the one-shard round's)
   b->p.nzb = b->p.fullb = b->q.nzb = b->q.fullb = nullptr;
 }
 
@@ -1347,13 +1202,7 @@ constexpr uint32_t kXdMaxG = 256;
 // sender regions of the exchange rounds: at most this many items (xd_emit stages them in
 // LDS, 6 B each), and the count / emit grid.  8192 items and 512 blocks (two emit blocks per
 // CU) measured the same at G = 8 (9.81 vs 9.81-9.87 ms per rank, profiles/r02_xd/region)
-#ifndef GOSSIP_XD_SEND_REGION
-#define GOSSIP_XD_SEND_REGION 16384
-#endif
-#ifndef GOSSIP_XD_EMIT_GRID
-#define GOSSIP_XD_EMIT_GRID 256
-#endif
-constexpr uint32_t kXdSendRegion = GOSSIP_XD_SEND_REGION;
+constexpr uint32_t kXdSendRegion = 16384;  // (8192: no gain at G = 8)
 static_assert(kXdSendRegion <= kRecPerRegion, "xd sender regions: at most kRecPerRegion items");
 // binned received item: p_local [0, 14) | slot in its region [14, 28) | no push | no pull
 constexpr uint32_t kXbVZ = 1u << 28;
@@ -1510,9 +1359,9 @@ __global__ __launch_bounds__(kEmitThreads) void xd_emit_kernel(XdGeom g, const u
       }
       const size_t dst = (size_t)b.roff[(size_t)s * G + lo] + (e - lofs[lo]);
       const uint32_t id = st_id[e], nl = st_nl[e];
-      rec_st<1>(&b.sid[dst], id);
-      rec_st<1>(&b.snl[dst], (uint16_t)nl);
-      rec_st<1>(&b.sval[dst], (uint64_t)((id & kXdNoPush) ? 0ull : S[base + nl]));  // the region's slice: L2 hits
+      rec_st(&b.sid[dst], id);
+      rec_st(&b.snl[dst], (uint16_t)nl);
+      rec_st(&b.sval[dst], (uint64_t)((id & kXdNoPush) ? 0ull : S[base + nl]));  // the region's slice: L2 hits
     }
   }
 }
@@ -1561,14 +1410,14 @@ __global__ __launch_bounds__(kEmitThreads) void xd_bin_kernel(XdGeom g, XdBufs b
     __syncthreads();
     for (uint32_t e = tid; e < total; e += kEmitThreads) {
       const uint32_t x = st[e];
-      rec_st<1>(&gids[e], x);
+      rec_st(&gids[e], x);
       if constexpr (kStageV) {
-        rec_st<1>(&gvals[e], (uint64_t)sv[e]);
+        rec_st(&gvals[e], (uint64_t)sv[e]);
         continue;
       }
       // the region's values were streamed in with the ids' lines: L2 hits (all of a
       // thread's gathers in flight at once measured slower: 239 -> 323 us)
-      rec_st<1>(&gvals[e], (uint64_t)((x & kXbVZ) ? 0ull : b.rval[base + ((x >> kTileDLog) & kXbSlotMask)]));
+      rec_st(&gvals[e], (uint64_t)((x & kXbVZ) ? 0ull : b.rval[base + ((x >> kTileDLog) & kXbSlotMask)]));
     }
   }
 }
@@ -1663,7 +1512,7 @@ __global__ __launch_bounds__(kTileThreads) void xd_apply_kernel(XdGeom g, XdBufs
               else hi = mid;
             }
             const size_t pos = (size_t)ro[lo] + (f - rl[lo]);
-            rv[u] = rec_ld<16>(&b.rep_in[pos]);
+            rv[u] = *(&b.rep_in[pos]);
             nl[u] = b.snl[pos];
           }
 #pragma unroll
@@ -1776,14 +1625,13 @@ void xd_carve_recv(const XdGeom& g, uint64_t cap_r, void* base, XdBufs* b) {
   b->rb.off = (uint16_t*)take(offs * 2);
   b->rb.offT = (uint16_t*)take(offs * 2);
   b->rb.nzb = b->rb.fullb = nullptr;
-  b->rb.xsync = nullptr;
 }
 
 hipError_t launch_xd_requests(const XdGeom& g, const XdBufs& b, const uint64_t* S, uint32_t R, uint32_t t,
                               uint32_t key0, uint32_t key1, uint32_t mode, const Faults& fa, const XdFilter& xf,
                               hipStream_t st) {
   if (g.nown == 0) return hipMemsetAsync(b.ocnt, 0, g.G * 4, st);
-  const uint32_t eg = g.s.nt_s < GOSSIP_XD_EMIT_GRID ? g.s.nt_s : GOSSIP_XD_EMIT_GRID;
+  const uint32_t eg = g.s.nt_s < kEmitGrid ? g.s.nt_s : kEmitGrid;
   // (count: 1024 blocks instead of one per CU took the same time, profiles/r02_xd/variants3)
   if (fa.any()) xd_count_kernel<true><<<eg, kEmitThreads, 0, st>>>(g, S, b.rcnt, R, t, key0, key1, mode, fa, xf);
   else xd_count_kernel<false><<<eg, kEmitThreads, 0, st>>>(g, S, b.rcnt, R, t, key0, key1, mode, fa, xf);

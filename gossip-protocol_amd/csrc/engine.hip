@@ -49,8 +49,10 @@ struct gossip_engine {
   bool own_stream = false;
   std::string err;
   gossip::Transport* tr = nullptr;  // the collectives of gossip_step (G > 1), owned (gossip_comm_init_rank)
-  // rounds driven by the library (a transport here or in a group): the collectives run on the
-  // engine's own stream, so a buffer handed to them needs no stream sync first
+  // true only while the library itself drives the rounds (sharded_step inside gossip_step /
+  // gossip_group_step: DrivenScope): its collectives run on the engine's own stream (RCCL) or
+  // drain it first (copies), so a buffer handed to them needs no stream sync.  A host that runs
+  // its own collectives through the per-kind calls always gets the publishing sync.
   bool driven = false;
 
   uint64_t N = 0, Nl = 0, lo = 0, hi = 0, nown = 0;
@@ -1111,11 +1113,8 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
   bind_slices(e);
   if (e->mode != GOSSIP_MODE_FLOOD && e->mode != GOSSIP_MODE_ANTIENTROPY && !(cfg->flags & GOSSIP_FLAG_DIRECT) &&
       bin_path_ok(e->N, e->k, e->W, G)) {
-#ifndef GOSSIP_EMIT_BIG_TILES
-#define GOSSIP_EMIT_BIG_TILES 4096
-#endif
-    // past this many tiles the emit regions double (longer runs per tile, binned.hip V = 4)
-    e->bg = make_bin_geom(e->N, e->k, (e->N + kTileD - 1) / kTileD > GOSSIP_EMIT_BIG_TILES);
+    // past kMaxTilesD tiles the emit regions double (longer runs per tile, binned.hip V = 4, 5)
+    e->bg = make_bin_geom(e->N, e->k, (e->N + kTileD - 1) / kTileD > kMaxTilesD);
     const size_t bytes = bin_bytes(e->bg);
     if (hipMalloc(&e->bin_mem, bytes) != hipSuccess) {
       e->err = "hipMalloc of " + std::to_string(bytes) + " bytes (bins) failed";
@@ -1996,6 +1995,24 @@ int gossip_set_faults(gossip_engine_t* e, uint32_t edge_loss, uint32_t partition
   return GOSSIP_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// Marks the engines as driven by the library for the duration of one sharded_step
+// (RCCL: every collective on the engines' streams; copies: the transport drains them).
+struct DrivenScope {
+  std::vector<gossip_engine_t*> eng;
+  explicit DrivenScope(const std::vector<gossip_engine_t*>& l) : eng(l) {
+    for (gossip_engine_t* e : eng) e->driven = true;
+  }
+  ~DrivenScope() {
+    for (gossip_engine_t* e : eng) e->driven = false;
+  }
+};
+}  // namespace
+
+extern "C" {
+
 int gossip_comm_unique_id(uint8_t* id) {
   if (!id) return GOSSIP_EINVAL;
   std::string err;
@@ -2013,7 +2030,6 @@ int gossip_comm_init_rank(gossip_engine_t* e, const uint8_t* id) {
   std::string err;
   e->tr = make_rccl_transport({e}, id, &err);
   if (!e->tr) return e->fail(GOSSIP_ERCCL, "%s", err.c_str());
-  e->driven = true;
   return GOSSIP_OK;
 }
 
@@ -2025,6 +2041,7 @@ int gossip_step(gossip_engine_t* e, uint32_t max_rounds, gossip_round_stats_t* s
     if (!e->tr) return e->fail(GOSSIP_ESTATE, "G > 1: gossip_comm_init_rank first (or run the round_* calls)");
     if (e->mode == GOSSIP_MODE_FLOOD && !e->has_topo) return e->fail(GOSSIP_ESTATE, "FLOOD needs a topology");
     std::string err;
+    const DrivenScope ds({e});
     const int rc = sharded_step({e}, e->tr, max_rounds, stats, infected, rounds_done, &err);
     if (rc) e->err = err;
     return rc;
@@ -2252,8 +2269,6 @@ int gossip_group_create(const gossip_config_t* cfg, uint32_t n_shards, const int
       gossip_group_destroy(g);
       return use_rccl ? GOSSIP_ERCCL : GOSSIP_EINVAL;
     }
-    // RCCL: every collective on the engines' streams; copies: the transport drains them itself
-    for (gossip_engine_t* e : g->eng) e->driven = true;
   }
   *out = g;
   return GOSSIP_OK;
@@ -2270,6 +2285,7 @@ int gossip_group_step(gossip_group_t* g, uint32_t max_rounds, gossip_round_stats
   if (!g) return GOSSIP_EINVAL;
   if (g->eng.size() == 1) return gossip_step(g->eng[0], max_rounds, stats, infected, rounds_done);
   g->err.clear();
+  const DrivenScope ds(g->eng);
   const int rc = sharded_step(g->eng, g->tr, max_rounds, stats, infected, rounds_done, &g->err);
   return rc;
 }

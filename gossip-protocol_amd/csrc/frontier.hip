@@ -35,32 +35,20 @@ namespace gossip {
 namespace {
 
 constexpr int kScanThreads = 1024;
-#ifndef GOSSIP_SCAN_NT
-#define GOSSIP_SCAN_NT 0  // 1: the scan's S gathers and P stores carry the non-temporal hint (A/B)
-#endif
+// (non-temporal hints on the scan's S gathers and P stores: equal)
 template <typename T>
 __device__ __forceinline__ T scan_ld(const T* p) {
-  if constexpr (GOSSIP_SCAN_NT != 0) return __builtin_nontemporal_load(p);
-  else return *p;
+  return *p;
 }
 template <typename T>
 __device__ __forceinline__ void scan_st(T* p, T v) {
-  if constexpr (GOSSIP_SCAN_NT != 0) __builtin_nontemporal_store(v, p);
-  else *p = v;
+  *p = v;
 }
-#ifndef GOSSIP_SCAN_GRID
-#define GOSSIP_SCAN_GRID 256
-#endif
-#ifndef GOSSIP_SCAN_WAVES
-#define GOSSIP_SCAN_WAVES 4
-#endif
-constexpr uint32_t kScanGrid = GOSSIP_SCAN_GRID;  // one block per CU: the summary takes 128 KiB of LDS
+constexpr uint32_t kScanGrid = 256;  // one block per CU: the summary takes 128 KiB of LDS
+constexpr uint32_t kScanWaves = 4;   // waves per SIMD (launch bounds)
 constexpr int kCommitThreads = 256;
 constexpr uint32_t kRwWords = 1024;  // rare-bitmap words staged per scan chunk (64K nodes)
-#ifndef GOSSIP_SCAN_UNROLL
-#define GOSSIP_SCAN_UNROLL 2
-#endif
-constexpr int kScanUnroll = GOSSIP_SCAN_UNROLL;  // nodes per lane per scan step
+constexpr int kScanUnroll = 2;  // nodes per lane per scan step (1: equal, 4: slower)
 constexpr int kCommitUnroll = 4;     // dirty groups per wave per commit step
 
 // valid-node mask of bitmap word w (bits past N are zero in both bitmaps)
@@ -357,7 +345,7 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
 }
 
 template <int MODE, bool FAULTS>
-__global__ __launch_bounds__(kScanThreads, GOSSIP_SCAN_WAVES) void frontier_scan_kernel(FrontierBufs f, uint64_t* S,
+__global__ __launch_bounds__(kScanThreads, kScanWaves) void frontier_scan_kernel(FrontierBufs f, uint64_t* S,
                                                                       uint64_t N, uint32_t R, uint32_t k, uint32_t t,
                                                                       uint32_t key0, uint32_t key1, uint64_t per_block,
                                                                       const uint64_t* partial, uint32_t maj,

@@ -290,14 +290,44 @@ def sharded_round(engine, group=None, kinds: list | None = None, direct: bool | 
     return engine.round_commit(partial)
 
 
-def init_engine_comm(engine, group=None) -> None:
+def _all_ranks(ok: bool, group=None) -> bool:
+    """True iff `ok` holds on every rank (an all-reduce MIN: every rank learns the same answer)."""
+    dev = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(t.item())
+
+
+def init_engine_comm(engine, group=None) -> str | None:
     """Hands a shard engine its own RCCL communicator (gossip_comm_init_rank): rank 0
     makes the unique id, torch.distributed carries it; engine.step then runs every sharded round
-    inside the library (plan, collectives on the engine's stream, kernels)."""
+    inside the library (plan, collectives on the engine's stream, kernels).
+
+    Collective, and so is its outcome: every rank joins every step, also after a failure, and
+    every rank returns the same thing — None when every rank has its communicator, else the
+    reason (then the caller drives the rounds over torch.distributed on every rank).  Rank 0
+    broadcasts the id or None; each rank first loads RCCL itself (a rank that could not would
+    leave the others waiting inside ncclCommInitRank), and the init's success is agreed on by
+    an all-reduce MIN."""
     from .engine import comm_unique_id
-    box = [comm_unique_id() if dist.get_rank(group) == 0 else None]
+    rank0 = dist.get_rank(group) == 0
+    box, err = [None], None
+    try:  # rank 0: the id; every rank: RCCL loads and answers (a throwaway id elsewhere)
+        uid = comm_unique_id()
+        if rank0:
+            box[0] = uid
+    except Exception as exc:  # noqa: BLE001 - reported in the return value
+        err = f"RCCL unavailable on rank {dist.get_rank(group)}: {exc}"
     dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
-    engine.comm_init_rank(box[0])
+    if not _all_ranks(err is None and box[0] is not None, group):
+        return err or "RCCL unavailable on another rank"
+    try:
+        engine.comm_init_rank(box[0])
+    except Exception as exc:  # noqa: BLE001
+        err = f"gossip_comm_init_rank on rank {dist.get_rank(group)}: {exc}"
+    if not _all_ranks(err is None, group):
+        return err or "gossip_comm_init_rank failed on another rank"
+    return None
 
 
 def sharded_run(engine, max_rounds: int, group=None, kinds: list | None = None, direct: bool | None = None) -> list:

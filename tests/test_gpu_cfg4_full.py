@@ -53,6 +53,20 @@ def test_cfg4_single_engine_equals_oracle(single_engine_run):
     o.close()
 
 
+def test_cfg4_single_engine_equals_fixture(single_engine_run):
+    """The same run against the committed oracle fixture (tests/golden/cfg4_oracle.json, the file
+    bench.py checks every configs[3] line against): stats, per-rumor counts, final state digest."""
+    import hashlib
+    import json
+    res, full = single_engine_run
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "cfg4_oracle.json")) as f:
+        fx = json.load(f)
+    assert res.stats == fx["stats"]
+    assert res.infected.tolist() == fx["infected"]
+    words = np.ascontiguousarray(full[0], dtype="<u8")
+    assert hashlib.sha256(memoryview(words).cast("B")).hexdigest() == fx["state_sha256"]
+
+
 @pytest.mark.parametrize("plan", list(PLANS))
 def test_cfg4_G8_lockstep_equals_single_engine(single_engine_run, plan):
     res, full = single_engine_run

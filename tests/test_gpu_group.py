@@ -111,6 +111,51 @@ def test_cfg4_group_equals_one_engine(cfg4_one_engine, G):
             assert np.array_equal(e.read_shard(), full[:, e.lo:e.hi])
 
 
+def _rccl_devices(G):
+    import torch
+    if torch.cuda.device_count() < G:
+        pytest.skip(f"RCCL needs one device per shard: {G} shards, {torch.cuda.device_count()} device(s)")
+    return list(range(G))
+
+
+RCCL_PLANS = ["auto", "sparse", "classcoded", "exchange"]
+
+
+@pytest.mark.parametrize("plan", RCCL_PLANS)
+@pytest.mark.parametrize("G", [2, 4, 8])
+def test_rccl_group_equals_one_engine(plan, G):
+    """The RCCL transport (transport 1: ncclCommInitAll over distinct devices, collectives on the
+    engines' streams, the side-stream all-gather, grouped ncclSend / ncclRecv all-to-alls) against
+    one engine: every plan kind, per-round stats, per-rumor counts, final state."""
+    devs = _rccl_devices(G)
+    mode, k, R, N, seed = "pushpull", 2, 64, (1 << 20) + 77, 0x5EED0004
+    want, full = _one_engine(mode, k, R, N, seed)
+    params = dict(PLANS[plan], **({"xd_shards": 2} if plan in ("exchange", "auto") else {}))
+    with Group(N, R, mode, k, seed, flags=1, n_shards=G, devices=devs, transport=1, params=params) as g:
+        assert g.transport == 1
+        g.inject_random()
+        got = g.step(300)
+        assert got.stats == want.stats
+        assert np.array_equal(got.infected, want.infected)
+        for e in g.shards:
+            assert np.array_equal(e.read_shard(), full[:, e.lo:e.hi])
+
+
+@pytest.mark.parametrize("G", [2, 4])
+def test_rccl_group_antientropy(G):
+    devs = _rccl_devices(G)
+    N, K, k, seed = 1 << 16, 16, 1, 0x5EED0005
+    kw = dict(churn_fail=ct(0.01), churn_recover=ct(0.1))
+    want, rows = _one_engine("antientropy", k, K, N, seed, **kw)
+    with Group(N, K, "antientropy", k, seed, flags=1, n_shards=G, devices=devs, transport=1, **kw) as g:
+        assert g.transport == 1
+        g.inject_random()
+        got = g.step(400)
+        assert got.stats == want.stats
+        for e in g.shards:
+            assert np.array_equal(e.read_rows(), rows[e.lo:e.hi])
+
+
 def test_rccl_group_rejects_shared_device():
     from gossip_hip import GossipError
     with pytest.raises(GossipError):

@@ -7,7 +7,11 @@ boundaries with HIP shard engines equals a single-engine run bit for bit.
          all-gathers async with work.wait(), the engines bound to torch's stream;
   nccl — RCCL collectives on engine memory, in place, with the engines bound to
          torch's current stream (gossip_hip.sharded._bind_stream).  Needs two
-         devices (RCCL rejects two ranks on one GPU); skipped on a one-GPU box."""
+         devices (RCCL rejects two ranks on one GPU); skipped on a one-GPU box;
+  engine — every round inside the library (gossip_comm_unique_id /
+         gossip_comm_init_rank through gossip_hip.sharded.init_engine_comm, then
+         gossip_step: the engine's own RCCL communicator), the
+         path `bench.py --driver engine` measures.  Needs two devices likewise."""
 import os
 import socket
 import sys
@@ -36,10 +40,11 @@ def _worker(rank, world, port, case, q, backend="gloo"):
     from gossip_hip.sharded import sharded_run
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dev = rank if backend == "nccl" else 0
+    rccl = backend in ("nccl", "engine")
+    dev = rank if rccl else 0
     torch.cuda.set_device(dev)
     direct = True if backend == "gloo-dev" else None
-    if backend == "nccl":
+    if rccl:
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", dev))
     else:
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -47,7 +52,13 @@ def _worker(rank, world, port, case, q, backend="gloo"):
     kw = _ae_kw(mode)
     e = Engine(N, R, mode, k, seed, flags=1, device=dev, shard_rank=rank, shard_count=world, params=params, **kw)
     e.inject_random()
-    stats = sharded_run(e, 400, direct=direct)
+    if backend == "engine":
+        from gossip_hip.sharded import init_engine_comm
+        why = init_engine_comm(e)
+        assert why is None, why
+        stats = e.step(400).stats
+    else:
+        stats = sharded_run(e, 400, direct=direct)
     q.put((rank, e.lo, e.hi, stats, _state(e)))
     dist.destroy_process_group()
 
@@ -67,11 +78,11 @@ CASES = [("pushpull", 2, 64, 1 << 20, 0x5EED0004, None),
          ("antientropy", 1, 16, 1 << 18, 0x5EED0005, None)]
 
 
-@pytest.mark.parametrize("backend", ["gloo", "gloo-dev", "nccl"])
+@pytest.mark.parametrize("backend", ["gloo", "gloo-dev", "nccl", "engine"])
 @pytest.mark.parametrize("case", CASES, ids=["pushpull-1M", "push-ragged", "pushpull-exchange", "antientropy"])
 def test_two_processes_equal_one_engine(case, backend):
     import torch
-    if backend == "nccl" and torch.cuda.device_count() < 2:
+    if backend in ("nccl", "engine") and torch.cuda.device_count() < 2:
         pytest.skip("RCCL needs one device per rank")
     from gossip_hip import Engine
     mode, k, R, N, seed, _ = case

@@ -169,3 +169,43 @@ def test_cfg5_oracle_fixture_is_consistent():
     assert last["converged"] and last["full_nodes"] == last["alive_nodes"]
     assert all(c == last["alive_nodes"] for c in g["infected"][-1])  # every alive row holds the max vector
     assert len(g["rows_sha256"]) == 64 and all(len(v) == K for v in g["sample_rows"].values())
+
+
+def test_cfg4_oracle_fixture_is_consistent():
+    """tests/golden/cfg4_oracle.json (configs[3] on the OpenMP oracle, make_cfg4_golden.py): what the
+    full-size GPU test and bench.py's self-check compare against.  Per-rumor counts never fall and end
+    at N, every round's full count is the number of nodes holding every rumor (so at most the smallest
+    per-rumor count), the last round converged, the stats hash of the last round is the final hash."""
+    import json
+    import os
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "cfg4_oracle.json")
+    with open(path) as f:
+        g = json.load(f)
+    N, R = g["config"]["N"], g["config"]["R"]
+    assert (N, R, g["config"]["seed"], g["config"]["mode"], g["config"]["fanout"]) == \
+        (1 << 27, 64, hex(0x5EED0004), "pushpull", 2)
+    assert g["rounds"] == len(g["stats"]) == len(g["infected"]) == 15
+    assert [s["round"] for s in g["stats"]] == list(range(g["rounds"]))
+    for prev, cur in zip(g["infected"], g["infected"][1:]):
+        assert all(a <= b for a, b in zip(prev, cur))
+    assert all(c == N for c in g["infected"][-1])
+    assert all(s["full_nodes"] <= min(row) and s["alive_nodes"] == N for s, row in zip(g["stats"], g["infected"]))
+    assert [s["converged"] for s in g["stats"]] == [0] * 14 + [1]
+    assert g["stats"][-1]["state_hash"] == g["final_state_hash"]
+    assert len(g["state_sha256"]) == 64 and g["sample_words"][str(N - 1)] == (1 << 64) - 1
+
+
+def test_oracle_accepts_every_engine_param():
+    """The oracle exports the engine's ABI: every gossip_set_param name the engine knows (its path and
+    grid knobs) is accepted, so a host can apply one parameter set to both."""
+    import os
+    import re
+    src = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gossip-protocol_amd",
+                       "csrc", "engine.hip")
+    with open(src) as f:
+        names = sorted(set(re.findall(r'n == "(\w+)"', f.read())))
+    assert len(names) >= 10
+    e = op.OracleEngine(1000, 1, "push", 1, 1)
+    for name in names:
+        e.set_param(name, 0.5)
+    e.close()
