@@ -156,7 +156,8 @@ __global__ __launch_bounds__(kBlock) void round_flood_kernel(RoundArgs a) {
 // (:80-87); the neighbour's 2 s context (:77) expires after D lost attempts.
 // One lane per (value x, node u) walk: from position c, the sender is skipped
 // (no message); any other neighbour w costs a message, lost as a random-mode
-// edge (partition, or Philox({u, t, 4, c >> 2})[c & 3] < edge_loss).  A lost
+// edge (partition, or Philox({u, t, 4 | x << 16, c >> 2})[c & 3] < edge_loss: one draw per
+// message, i.e. per value, as each value is its own SyncRPC at main.go:81).  A lost
 // attempt ends the walk's round (the later neighbours wait); a delivered one
 // ORs x into S_{t+1}[w] (w's first sender: atomicMin over the lanes that
 // delivered x to w this round — snd stays kWalkNone while w lacks x) and moves
@@ -184,7 +185,7 @@ __global__ __launch_bounds__(kBlock) void round_flood_walks_kernel(RoundArgs a, 
         continue;
       }
       ++msgs;
-      const uint32_t lw = a.fa.loss ? lane_of(loss_draws(u, a.t, c >> 2, a.key0, a.key1), c & 3u) : 0u;
+      const uint32_t lw = a.fa.loss ? lane_of(loss_draws(u, a.t, c >> 2, a.key0, a.key1, x), c & 3u) : 0u;
       if (edge_lost(a.fa, rc, w, lw)) {
         at = at < 255u ? at + 1u : at;
         break;

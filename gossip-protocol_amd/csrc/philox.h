@@ -84,9 +84,11 @@ __host__ __device__ __forceinline__ Reach reach_of(uint32_t n, const Faults& f) 
   return Reach{(uint32_t)((q * f.N + f.parts - 1) / f.parts), (uint32_t)(((q + 1) * f.N + f.parts - 1) / f.parts)};
 }
 
-// the loss draws of edges 4q .. 4q+3 of node n in round t
-__host__ __device__ __forceinline__ u32x4 loss_draws(uint32_t n, uint32_t t, uint32_t q, uint32_t k0, uint32_t k1) {
-  return philox4x32_10(u32x4{n, t, 4u, q}, k0, k1);
+// the loss draws of edges 4q .. 4q+3 of node n in round t; FLOOD walks draw one per message:
+// value slot x in the tag word's upper half (x = 0: the random modes' draw), DESIGN.md §2.9
+__host__ __device__ __forceinline__ u32x4 loss_draws(uint32_t n, uint32_t t, uint32_t q, uint32_t k0, uint32_t k1,
+                                                     uint32_t x = 0) {
+  return philox4x32_10(u32x4{n, t, 4u | (x << 16), q}, k0, k1);
 }
 
 // edge n -> p lost?  rc = reach_of(n), lossw = lane j & 3 of loss_draws(n, t, j >> 2)

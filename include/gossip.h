@@ -165,7 +165,8 @@ int gossip_set_param(gossip_engine_t* eng, const char* name, double value);
 /* FLOOD peer source: directed adjacency Topology[u] = col[row_ptr[u]..row_ptr[u+1]),
  * global node ids, n == N.  Copied; never retained.  Plain FLOOD reads each row as a set;
  * an engine created with faults or stall_rounds keeps each row as listed (order and
- * repeats: the forwarding walk of main.go:72-87) and ends every walk. */
+ * repeats: the forwarding walk of main.go:72-87) and ends every walk (a
+ * known divergence: the reference's in-flight goroutine keeps the row it read at main.go:72). */
 int gossip_set_topology_csr(gossip_engine_t* eng, const uint32_t* row_ptr, const uint32_t* col,
                             uint64_t n, uint64_t n_edges);
 

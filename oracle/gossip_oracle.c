@@ -578,8 +578,19 @@ static int ae_round(oracle_sim_t* s, uint64_t* partial) {
  * w the value and moves on to c + 1 — unless the context has expired, when the walk stays on w
  * for good (it keeps retrying, and w can still learn x from it).  w's first sender of x is the
  * lowest u that delivered it in the round w learned it; w's walk of x starts the next round. */
-static int flood_lost(const oracle_sim_t* s, uint32_t u, uint32_t w, uint32_t j, const uint32_t key[2]) {
-  return edge_lost(&s->cfg, s->N, u, w, s->t, j, key);
+/* One SyncRPC per value (main.go:81): the message of value x from u at row position j is lost on a
+ * partition or when Philox({u, t, 4 | x << 16, j >> 2})[j & 3] < edge_loss (x = 0: the random
+ * modes' edge draw). */
+static int flood_lost(const oracle_sim_t* s, uint32_t u, uint32_t w, uint32_t j, uint32_t x, const uint32_t key[2]) {
+  const gossip_config_t* cfg = &s->cfg;
+  if (cfg->partitions > 1 &&
+      (uint64_t)u * cfg->partitions / s->N != (uint64_t)w * cfg->partitions / s->N) return 1;
+  if (cfg->edge_loss) {
+    uint32_t ctr[4] = {u, s->t, 4u | (x << 16), j >> 2}, d[4];
+    oracle_philox4x32_10(ctr, key, d);
+    if (d[j & 3] < cfg->edge_loss) return 1;
+  }
+  return 0;
 }
 
 static int holds(const oracle_sim_t* s, const uint64_t* S, uint64_t n, uint32_t x) {
@@ -605,7 +616,7 @@ static uint64_t flood_faults_round(oracle_sim_t* s, uint64_t* Sn) {
           continue;
         }
         ++msgs;
-        if (flood_lost(s, (uint32_t)u, w, c, key)) {
+        if (flood_lost(s, (uint32_t)u, w, c, x, key)) {
           if (a < 255) ++a;
           break;
         }
@@ -1256,7 +1267,8 @@ int oracle_set_param(oracle_sim_t* s, const char* name, double value) {
   }
   /* the engine's performance knobs (path choice, grids): no effect on the rounds' results */
   const char* known[] = {"alld_frac",  "filter_frac", "ahead",        "serve_grid",   "apply_grid", "push_waves",
-                         "ae_sparse",  "ae_cap",      "sparse_direct", "mid_frac",    "ae_dense_bin", "ae_dense_cap"};
+                         "ae_sparse",  "ae_cap",      "sparse_direct", "mid_frac",    "ae_dense_bin", "ae_dense_cap",
+                         "cls_frac"};
   for (size_t i = 0; i < sizeof known / sizeof known[0]; ++i)
     if (!strcmp(name, known[i])) return GOSSIP_OK;
   return GOSSIP_EINVAL;

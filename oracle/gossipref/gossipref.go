@@ -344,8 +344,19 @@ func contains(row []uint32, x uint32) (int, bool) {
 	return i, i < len(row) && row[i] == x
 }
 
-func (f *FloodSim) lost(u, w uint32, j uint64) bool {
-	return EdgeLost(f.Seed, f.N, f.Loss, f.Parts, u, w, f.T, uint32(j))
+// lost: the message of value x from u to w (position j of u's row) is lost — one SyncRPC per
+// value (main.go:81), so one loss draw per message: Philox({u, t, 4 | x<<16, j/4})[j%4].
+func (f *FloodSim) lost(u, w uint32, j uint64, x uint32) bool {
+	if f.Parts > 1 && (uint64(u)*uint64(f.Parts))/f.N != (uint64(w)*uint64(f.Parts))/f.N {
+		return true
+	}
+	if f.Loss != 0 {
+		d := Philox4x32_10([4]uint32{u, f.T, 4 | x<<16, uint32(j >> 2)}, Key(f.Seed))
+		if d[j&3] < f.Loss {
+			return true
+		}
+	}
+	return false
 }
 
 // Round: one synchronous FLOOD round.
@@ -399,7 +410,7 @@ func (f *FloodSim) Round() RoundStats {
 						continue
 					}
 					msgs++
-					if f.lost(uint32(u), w, uint64(c)) {
+					if f.lost(uint32(u), w, uint64(c), x) {
 						if a < 255 {
 							a++
 						}

@@ -110,22 +110,25 @@ def stats_of(S: np.ndarray, R: int):
     return full, [int(x) for x in inf]
 
 
-def loss_draw(seed: int, nodes, t: int, j: int) -> np.ndarray:
-    """Philox({n, t, 4, j>>2})[j&3]: the loss draw of edge j of node n in round t."""
+def loss_draw(seed: int, nodes, t: int, j: int, value: int = 0) -> np.ndarray:
+    """Philox({n, t, 4 | value << 16, j>>2})[j&3]: the loss draw of edge j of node n in round t
+    (DESIGN.md §2.8); FLOOD walks draw one per message, value = the value's slot (§2.9)."""
     n = np.asarray(nodes, dtype=np.uint32)
-    x = philox4x32_10(n, np.uint32(t), np.uint32(4), np.uint32(j >> 2), seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
+    x = philox4x32_10(n, np.uint32(t), np.uint32(4 | (value << 16)), np.uint32(j >> 2), seed & 0xFFFFFFFF,
+                      (seed >> 32) & 0xFFFFFFFF)
     return x[j & 3]
 
 
-def edge_lost(seed, N, loss, parts, n, p, t, j) -> np.ndarray:
-    """The edge n -> p (slot j of n, round t) is lost: partition or loss draw."""
+def edge_lost(seed, N, loss, parts, n, p, t, j, value: int = 0) -> np.ndarray:
+    """The edge n -> p (slot j of n, round t) is lost: partition or loss draw (DESIGN.md §2.8;
+    value: a FLOOD walk's message, one draw per value, §2.9)."""
     n = np.asarray(n, dtype=np.int64)
     p = np.asarray(p, dtype=np.int64)
     lost = np.zeros(n.shape, dtype=bool)
     if parts > 1:
         lost |= (n * parts) // N != (p * parts) // N
     if loss:
-        lost |= loss_draw(seed, n, t, j) < np.uint32(loss)
+        lost |= loss_draw(seed, n, t, j, value) < np.uint32(loss)
     return lost
 
 
@@ -197,14 +200,14 @@ class Sim:
     def _flood_faults_round(self, S, Sn):
         """FLOOD with faults (main.go:72-87): every walk of a value u held at the
         start of the round goes down u's row from its cursor.  Position c of u's row is lost in
-        round t like a random-mode edge (partition, or Philox({u, t, 4, c >> 2})[c & 3] <
-        edge_loss); the first sender is skipped without a message (:73)."""
+        round t like a random-mode edge (partition, or Philox({u, t, 4 | x << 16, c >> 2})[c & 3] <
+        edge_loss: one draw per message, each value being its own SyncRPC, main.go:81); the first
+        sender is skipped without a message (:73)."""
         D = self.D
         msgs = 0
         first = {}  # (w, x) -> lowest u that delivered x to w (w did not hold x)
         for u in range(self.N):
             row = self.rows[u]
-            lost_at = {}
             for x in range(self.R):
                 if not self._has(S, u, x):
                     continue
@@ -215,9 +218,7 @@ class Sim:
                         c += 1
                         continue
                     msgs += 1
-                    if c not in lost_at:
-                        lost_at[c] = bool(edge_lost(self.seed, self.N, self.loss, self.parts, [u], [w], self.t, c)[0])
-                    if lost_at[c]:
+                    if bool(edge_lost(self.seed, self.N, self.loss, self.parts, [u], [w], self.t, c, x)[0]):
                         a += 1
                         break
                     if not self._has(S, w, x):

@@ -79,3 +79,23 @@ def test_stall_mode_properties():
 
 def test_loss_threshold():
     assert loss_threshold(0.0) == 0 and loss_threshold(1.0) == 2**32 - 1 and loss_threshold(0.5) == 2**31
+
+
+def test_flood_new_topology_ends_walks():
+    """a topology message ends every walk, so a value already held is not sent
+    again over the new rows; a value injected after it starts a walk on them.  (main.go:72 reads
+    the row once per goroutine, so in the reference an in-flight walk would finish on the old
+    row: a documented divergence.)"""
+    N = 6
+    e = op.OracleEngine(N, 2, "flood", 0, 1, flags=1, stall_rounds=1)
+    e.set_topology([[1], [], [], [], [], []])  # 0 -> 1 only
+    e.inject(0, 0)
+    e.step(10)
+    assert e.read(1) == [0] and e.read(2) == []
+    e.set_topology([[2, 3], [4], [], [], [], []])
+    res = e.step(10)
+    assert res.stats[-1]["messages"] == 0 and e.read(2) == [] and e.read(4) == []  # walks ended
+    e.inject(0, 1)  # a new value walks the new rows: 0 -> 2, 3
+    e.step(10)
+    assert e.read(2) == [1] and e.read(3) == [1] and e.read(4) == []
+    e.close()

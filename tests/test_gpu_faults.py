@@ -100,7 +100,14 @@ def test_random_faults_stall_golden_every_path(golden, idx, path):
     e.close()
 
 
-@pytest.mark.parametrize("idx", range(6))
+def _n_flood_faults():
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "golden.json")) as f:
+        return len(json.load(f)["flood_faults"])
+
+
+@pytest.mark.parametrize("idx", range(_n_flood_faults()))
 def test_flood_faults_golden_gpu(golden, idx):
     """FLOOD with per-edge retries and the deadline stall (round_flood_faults_kernel)."""
     from conftest import inject_case
@@ -176,3 +183,26 @@ def test_stall_sharded_lockstep(plan):
     for e in engines:
         assert np.array_equal(e.read_shard(), full[:, e.lo:e.hi])
         e.close()
+
+
+def test_flood_walks_topology_change_mid_run_gpu():
+    """A topology message mid-run ends every walk (a known divergence from
+    main.go:72, whose goroutine keeps the row it read): the GPU equals the oracle round by round,
+    before and after the change, with losses and the deadline stall."""
+    N, R = 30, 3
+    row_a = [[(u + 1) % N, (u + 7) % N] for u in range(N)]
+    row_b = [[(u + 3) % N, (u + 11) % N, (u + 1) % N] for u in range(N)]
+    kw = dict(edge_loss=loss_threshold(0.3), stall_rounds=2)
+    runs = []
+    for x in (Engine(N, R, "flood", 0, 5, flags=1, **kw), op.OracleEngine(N, R, "flood", 0, 5, flags=1, **kw)):
+        x.set_topology(row_a)
+        for r in range(R):
+            x.inject(r * 9, r)
+        a = x.step(3)
+        x.set_topology(row_b)
+        x.inject(4, 0)
+        b = x.step(60)
+        runs.append((a.stats, b.stats, x.read_shard()))
+        x.close()
+    assert runs[0][0] == runs[1][0] and runs[0][1] == runs[1][1]
+    assert np.array_equal(runs[0][2], runs[1][2])

@@ -14,7 +14,7 @@ if os.environ.get("GOSSIP_LIB"):
 N = int(os.environ.get("EXP_N", 1 << 24))
 # EXP_PARAMS="name=value,...": gossip_set_param knobs (e.g. fuse_emit=0)
 PARAMS = {kv.split("=")[0]: float(kv.split("=")[1]) for kv in os.environ.get("EXP_PARAMS", "").split(",") if kv}
-e = Engine(N, 64, "pushpull", 2, 0x5EED0003, flags=FLAG_TIMING, params=PARAMS)
+e = Engine(N, 64, "pushpull", 2, int(os.environ.get("EXP_SEED", "0x5EED0003"), 0), flags=FLAG_TIMING, params=PARAMS)
 for i in range(int(os.environ.get("EXP_STEPS", 4))):
     if i == 1:
         e.reset_timing()

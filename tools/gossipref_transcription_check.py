@@ -47,6 +47,14 @@ def edge_lost(seed, N, loss, parts, n, p, t, j):  # gossipref.EdgeLost
     return False
 
 
+def msg_lost(seed, N, loss, parts, u, w, t, j, x):  # gossipref.FloodSim.lost
+    if parts > 1 and (u * parts) // N != (w * parts) // N:
+        return True
+    if loss != 0 and philox([u, t, 4 | (x << 16), j >> 2], key(seed))[j & 3] < loss:
+        return True
+    return False
+
+
 def random_case(c, max_rounds=256):  # gossipref.Sim (+ SetFaults)
     N, R, k, seed = c["N"], c["R"], c["k"], c["seed"]
     loss, parts, stall = c.get("edge_loss", 0), c.get("partitions", 0), c.get("stall_rounds", 0)
@@ -178,7 +186,7 @@ def flood_case(c):  # gossipref.FloodSim
                             cc += 1
                             continue
                         msgs += 1
-                        if edge_lost(seed, N, loss, parts, u, w, t, cc):
+                        if msg_lost(seed, N, loss, parts, u, w, t, cc, x):
                             a = min(a + 1, 255)
                             break
                         if not holds(S, w, x):
