@@ -57,16 +57,9 @@ struct BinGeom {
   uint32_t push_waves;   // push-pull apply: waves [0, push_waves) walk the pushes, the rest the responses
   uint32_t aos;          // push records also packed {value, id} (BinBufs::prec; one shard, big regions)
   uint32_t split;        // one shard: record ids as two u16 arrays (BinBufs::dst / src) instead of ids
-  uint32_t cls;          // per launch (aos only): class-split round (kRoundCls)
+  uint32_t tmap;         // persistent serve / apply tile order: 0 each XCD a contiguous tile range, 1 the
+                         // whole chip on consecutive tiles (gossip_set_param "tile_map")
 };
-
-// Dense-round options (launch_binned_round's opts): bits 0, 1 the edge filter; kRoundCls the
-// class-split layout of a big-region round: only the pushes of mixed senders (0 < S_t[n] <
-// full) are packed, compactly (BinBufs::coff); a full sender's push carries the full mask, so
-// serve marks its peer in a per-node bitmap (BinBufs::fpush) that apply ORs in; an empty
-// sender's record is a pull request only.  Exact for any state; the host picks it for rounds
-// with few mixed senders.
-constexpr uint32_t kRoundCls = 4u;
 
 // big: regions of up to 2 * kMaxSenders senders and 2 * kRecPerRegion records (one shard
 // past kMaxTilesD tiles: the emit's 16-bit packed tile counters, binned.hip V = 4)
@@ -82,9 +75,6 @@ struct BinBufs {
   uint64_t* resp;   // [nt_s][rp]   pull response S_t[p] & ~S_t[n]
   uint16_t* off;    // [nt_s][nt_d + 1] run starts inside each sender region
   uint16_t* offT;   // [nt_d + 1][nt_s]
-  uint16_t* coff;   // aos: [nt_s][nt_d + 1] class-split rounds: run starts of the mixed pushes in prec
-  uint16_t* coffT;  // aos: [nt_d + 1][nt_s]
-  uint32_t* fpush;  // aos: [nt_d][kTileD / 32] class-split rounds: node receives a full sender's push
   uint64_t* nzb;    // occupancy bitmaps of S_{t+1} written by K3 (frontier.h), or null
   uint64_t* fullb;
 };
@@ -98,9 +88,8 @@ void bin_carve(const BinGeom& g, void* base, BinBufs* b);
 // nzb/fullb): bit 0 drops pulls from empty peers, bit 1 pushes into full
 // peers — exact, it only removes edges that move nothing.
 hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, uint64_t* partial, uint32_t R,
-                               uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t opts,
-                               const Faults& fa, uint32_t flags, const RoundSync& rs, hipStream_t st,
-                               uint32_t push_waves = 0);
+                               uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t filt,
+                               const Faults& fa, uint32_t flags, const RoundSync& rs, hipStream_t st);
 
 // Dense round of a sharded engine (G > 1) after the state all-gather
 // (DESIGN.md §5): push pass P = every sender of the image, records for the

@@ -209,51 +209,6 @@ __device__ __forceinline__ uint32_t region_offsets_packed(uint32_t* cur, uint32_
   return total;
 }
 
-// Class-split rounds (kRoundCls), after the mixed records of a region were placed first in
-// their runs: cur (packed u16 fill pointers) - off_row (the run starts) = mixed records per
-// tile; writes their exclusive prefix to coff_row[0, nt] (the compact packed stream's run
-// starts).  Same thread partition as region_offsets_packed, so each thread reads back the
-// off_row entries it wrote itself.  Every thread calls it; it ends with a barrier.
-__device__ __forceinline__ void mixed_offsets(const uint32_t* cur, uint32_t nt, const uint16_t* off_row,
-                                              uint16_t* coff_row, uint32_t* wsum, uint32_t* wpre) {
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t nw = (nt + 1) >> 1;
-  const uint32_t per = (nw + kEmitThreads - 1) / kEmitThreads;
-  const uint32_t lo = min(tid * per, nw), hi = min(lo + per, nw);
-  auto mcount = [&](uint32_t w, uint32_t h) -> uint32_t {
-    const uint32_t d = 2 * w + h;
-    return d < nt ? ((cur[w] >> (16 * h)) & 0xFFFFu) - off_row[d] : 0u;
-  };
-  uint32_t mine = 0;
-  for (uint32_t w = lo; w < hi; ++w) mine += mcount(w, 0) + mcount(w, 1);
-  uint32_t inc = mine;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(inc, o, 64);
-    if (lane >= (uint32_t)o) inc += y;
-  }
-  if (lane == 63) wsum[wave] = inc;
-  __syncthreads();
-  if (tid == 0) {
-    uint32_t a = 0;
-    for (int w = 0; w < kEmitThreads / 64; ++w) {
-      wpre[w] = a;
-      a += wsum[w];
-    }
-    wpre[kEmitThreads / 64] = a;
-  }
-  __syncthreads();
-  uint32_t run = wpre[wave] + inc - mine;
-  for (uint32_t w = lo; w < hi; ++w) {
-    const uint32_t m0 = mcount(w, 0), m1 = mcount(w, 1);
-    coff_row[2 * w] = (uint16_t)run;
-    if (2 * w + 1 < nt) coff_row[2 * w + 1] = (uint16_t)(run + m0);
-    run += m0 + m1;
-  }
-  if (tid == 0) coff_row[nt] = (uint16_t)wpre[kEmitThreads / 64];
-  __syncthreads();
-}
-
 // KREG > 0: the k (<= KREG) peers of each sender stay in registers between passes.
 // FAULTS: edge loss / partitions active; off, none of that code exists.
 // V = 0: one shard.  V = 1, 2: one pass of a sharded dense round (EmitRange):
@@ -484,31 +439,19 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
 #pragma unroll
     for (uint32_t q = 0; q < kQ; ++q) mine[q] = ((const uint64_t*)st_ids)[tid + q * kEmitThreads];
     __syncthreads();  // every sender's peers are read before any record takes the room
-    // class-split rounds: the mixed senders' records (both directions) first in every run,
-    // so the run's mixed records are its prefix; then the others
-    auto place = [&](uint32_t sel) {  // sel 0: every record, 1: mixed only, 2: the others
 #pragma unroll
-      for (uint32_t q = 0; q < kQ; ++q) {
-        const uint32_t i = tid + q * kEmitThreads;
+    for (uint32_t q = 0; q < kQ; ++q) {
+      const uint32_t i = tid + q * kEmitThreads;
 #pragma unroll
-        for (uint32_t j = 0; j < 2; ++j) {
-          const uint32_t dd = (uint32_t)(mine[q] >> (54 + 2 * j)) & 3u;
-          if (!dd || (sel == 1 && dd != 3u) || (sel == 2 && dd == 3u)) continue;
-          const uint32_t p = (uint32_t)(mine[q] >> (27 * j)) & ((1u << 27) - 1u);
-          uint32_t tl, pl;
-          tile_of(p, &tl, &pl);
-          const uint32_t pos = place_tile(tl);
-          st_ids[pos] = pl | (i << kTileDLog) | dir_flags(dd);
-        }
+      for (uint32_t j = 0; j < 2; ++j) {
+        const uint32_t dd = (uint32_t)(mine[q] >> (54 + 2 * j)) & 3u;
+        if (!dd) continue;
+        const uint32_t p = (uint32_t)(mine[q] >> (27 * j)) & ((1u << 27) - 1u);
+        uint32_t tl, pl;
+        tile_of(p, &tl, &pl);
+        const uint32_t pos = place_tile(tl);
+        st_ids[pos] = pl | (i << kTileDLog) | dir_flags(dd);
       }
-    };
-    if (g.cls) {
-      place(1);
-      __syncthreads();
-      mixed_offsets(cur, g.nt_d, off_row, b.coff + (size_t)s * (g.nt_d + 1), wsum, wpre);
-      place(2);
-    } else {
-      place(0);
     }
   } else {
     for (uint32_t q = 0; q < kQ; ++q) {
@@ -575,26 +518,11 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
     }
     __syncthreads();
     uint32_t* gprec = b.prec + (size_t)s * g.rp * 3;
-    if (g.cls) {
-      // class-split: each tile's mixed records (the prefix of its run) packed compactly at
-      // coff_row's run start; the others carry no value (an empty sender pushes nothing, a full
-      // one the full mask: serve marks its peer in BinBufs::fpush)
-      const uint16_t* coff_row = b.coff + (size_t)s * (g.nt_d + 1);
-      for (uint32_t d = tid; d < g.nt_d; d += kEmitThreads) {
-        const uint32_t e0 = off_row[d], c0 = coff_row[d], m = (uint32_t)coff_row[d + 1] - c0;
-        for (uint32_t i = 0; i < m; ++i) {
-          const uint32_t id = id_of_pair(gdst[e0 + i], gsrc[e0 + i]);
-          const uint64_t x = sv[(id >> kTileDLog) & kIdNMask];
-          prec_st(&gprec[3 * (c0 + i)], (uint32_t)x, (uint32_t)(x >> 32), id);
-        }
-      }
-    } else {
 #pragma unroll 4
-      for (uint32_t e = tid; e < total; e += kEmitThreads) {
-        const uint32_t id = split ? id_of_pair(gdst[e], gsrc[e]) : gids[e];
-        const uint64_t x = sv[(id >> kTileDLog) & kIdNMask];  // (big regions always pack: g.aos)
-        prec_st(&gprec[3 * e], (uint32_t)x, (uint32_t)(x >> 32), id);
-      }
+    for (uint32_t e = tid; e < total; e += kEmitThreads) {
+      const uint32_t id = split ? id_of_pair(gdst[e], gsrc[e]) : gids[e];
+      const uint64_t x = sv[(id >> kTileDLog) & kIdNMask];  // (big regions always pack: g.aos)
+      prec_st(&gprec[3 * e], (uint32_t)x, (uint32_t)(x >> 32), id);
     }
   } else
   for (uint32_t e = tid; e < total; e += kEmitThreads) {
@@ -843,8 +771,7 @@ __device__ __forceinline__ void push_walk(const BinGeom& g, const BinBufs& b, ui
   const uint64_t* __restrict__ gvals = b.vals;
   const uint32_t* __restrict__ gprec = b.prec;
   constexpr bool aos = LAYOUT == 2, SPLIT = LAYOUT >= 1;
-  // class-split rounds: only the mixed senders' pushes, packed compactly (coff)
-  const uint16_t* rowb = (aos && g.cls ? b.coffT : b.offT) + (size_t)X * g.nt_s;
+  const uint16_t* rowb = b.offT + (size_t)X * g.nt_s;
   for_each_run_record<kUnroll>(g, rowb, rowb + g.nt_s, wmask, wlist, [&](const int32_t* rec) {
     uint32_t id[kUnroll];
     uint64_t v[kUnroll];
@@ -909,13 +836,11 @@ __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, cons
   __shared__ unsigned long long img[kTileD];
   __shared__ uint64_t wmask[(kTileThreads / 64) * kUnrollServe];
   __shared__ int32_t wlist[(kTileThreads / 64) * 64];
-  __shared__ uint32_t fbit[SPLIT ? kTileD / 32 : 1];  // class-split rounds: node gets a full sender's push
-  const bool cls = SPLIT && g.cls;
   // persistent: virtual block v = blockIdx.x, +gridDim.x, ... serves tile
   // tr.at(xcd_remap(v, tr.n)) (the XCD of v is that of blockIdx.x, as with one
   // block per tile); the next tile's image loads into registers during a walk
   const uint32_t nv = tr.n;
-  auto tile_of = [&](uint32_t v) { return tr.at(xcd_remap(v, nv)); };
+  auto tile_of = [&](uint32_t v) { return tr.at(g.tmap ? v : xcd_remap(v, nv)); };
   uint4 x[kTileQ];
   if (blockIdx.x < nv) tile_regs_load(x, S, (uint64_t)tile_of(blockIdx.x) << kTileDLog, g.N);
   for (uint32_t v = blockIdx.x; v < nv; v += gridDim.x) {
@@ -923,8 +848,6 @@ __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, cons
   __syncthreads();  // the previous walk is done with img
 #pragma unroll
   for (uint32_t q = 0; q < kTileQ; ++q) ((uint4*)img)[q * kTileThreads + threadIdx.x] = x[q];
-  if (cls)
-    for (uint32_t i = threadIdx.x; i < kTileD / 32; i += kTileThreads) fbit[i] = 0;
   __syncthreads();
   if (v + gridDim.x < nv) tile_regs_load(x, S, (uint64_t)tile_of(v + gridDim.x) << kTileDLog, g.N);
   const uint32_t* gids = b.ids;
@@ -944,22 +867,10 @@ __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, cons
       // a fully informed sender needs nothing; otherwise the whole S_t[p] goes
       // back (bits n already holds are harmless to OR), so no value is read
       // dense rounds: every response is written (K3 tells stale slots by kIdVF)
-      if (rec[u] < 0) continue;
-      if (id[u] & VF) {
-        // class-split: a full sender's push (no pull, a value) makes its peer full
-        if (cls && !(id[u] & kIdVZ)) {
-          const uint32_t p = id[u] & (kTileD - 1);
-          atomicOr(&fbit[p >> 5], 1u << (p & 31u));
-        }
-        continue;
-      }
+      if (rec[u] < 0 || (id[u] & VF)) continue;
       gresp[rec[u]] = (uint64_t)img[id[u] & (kTileD - 1)];
     }
   });
-  if (cls) {
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < kTileD / 32; i += kTileThreads) b.fpush[(size_t)T * (kTileD / 32) + i] = fbit[i];
-  }
   }
 }
 
@@ -991,7 +902,7 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
   // place stays safe: only this block reads or writes S[X] of its tiles.
   const uint32_t nv = g.nt_d;
   for (uint32_t v = blockIdx.x; v < nv; v += gridDim.x) {
-  const uint32_t X = xcd_remap(v, nv);
+  const uint32_t X = g.tmap ? v : xcd_remap(v, nv);
   const uint64_t node0 = (uint64_t)X << kTileDLog;
   __syncthreads();  // the previous epilogue is done with acc and cnt
   {
@@ -1001,17 +912,6 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
     for (uint32_t q = 0; q < kTileQ; ++q) ((uint4*)acc)[q * kTileThreads + tid] = xr[q];
   }
   if (tid < 64) cnt[tid] = 0;
-  if (LAYOUT == 2 && g.cls) {  // class-split: the nodes a full sender pushed to are full (bin_serve)
-    __syncthreads();
-    const uint64_t fm = full_mask1(R);
-    for (uint32_t i = tid; i < kTileD / 32; i += kTileThreads) {
-      uint32_t w = b.fpush[(size_t)X * (kTileD / 32) + i];
-      while (w) {
-        acc[i * 32 + (uint32_t)__ffs(w) - 1u] = fm;
-        w &= w - 1u;
-      }
-    }
-  }
   __syncthreads();
   const uint32_t wave = tid >> 6;
   const bool split = kApplySplit && mode == 3;
@@ -1102,9 +1002,8 @@ bool bin_path_ok(uint64_t N, uint32_t k, uint32_t W, uint32_t G) {
 size_t bin_bytes(const BinGeom& g) {
   const size_t recs = (size_t)g.nt_s * g.rp;
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-  const size_t offs = al((size_t)g.nt_s * (g.nt_d + 1) * 2);
   return (g.split ? 2 * al(recs * 2) : al(recs * 4)) + (g.aos ? al(recs * 12) : al(recs * 8)) + al(recs * 8) +
-         2 * offs + (g.aos ? 2 * offs + al((size_t)g.nt_d * kTileD / 8) : 0) + 256;
+         2 * al((size_t)g.nt_s * (g.nt_d + 1) * 2) + 256;
 }
 
 void bin_carve(const BinGeom& g, void* base, BinBufs* b) {
@@ -1130,28 +1029,12 @@ void bin_carve(const BinGeom& g, void* base, BinBufs* b) {
   b->off = (uint16_t*)p;
   p += al((size_t)g.nt_s * (g.nt_d + 1) * 2);
   b->offT = (uint16_t*)p;
-  p += al((size_t)g.nt_s * (g.nt_d + 1) * 2);
-  b->coff = b->coffT = nullptr;
-  b->fpush = nullptr;
-  if (g.aos) {  // class-split rounds (kRoundCls)
-    b->coff = (uint16_t*)p;
-    p += al((size_t)g.nt_s * (g.nt_d + 1) * 2);
-    b->coffT = (uint16_t*)p;
-    p += al((size_t)g.nt_s * (g.nt_d + 1) * 2);
-    b->fpush = (uint32_t*)p;
-  }
 }
 
-hipError_t launch_binned_round(const BinGeom& g0, const BinBufs& b, uint64_t* S, uint64_t* partial, uint32_t R,
-                               uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t opts,
-                               const Faults& fa, uint32_t flags, const RoundSync& rs, hipStream_t st,
-                               uint32_t push_waves) {
-  BinGeom g = g0;
-  uint32_t filt = opts & 3u;
+hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, uint64_t* partial, uint32_t R,
+                               uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t filt,
+                               const Faults& fa, uint32_t flags, const RoundSync& rs, hipStream_t st) {
   if (!b.nzb || !b.fullb) filt = 0;  // the bitmaps exist only with the frontier buffers
-  // class-split layout: big regions (packed pushes), push-pull, no faults (the big emit's PK pass)
-  g.cls = (opts & kRoundCls) && g.aos && mode == 3 && !fa.any() && g.k <= 2 ? 1u : 0u;
-  if (push_waves) g.push_waves = push_waves;
   const uint32_t eg = g.nt_s < kEmitGrid ? g.nt_s : kEmitGrid;  // persistent: one block per CU
 #define GOSSIP_EMIT(KR, F, VV) \
   bin_emit_kernel<KR, F, VV><<<eg, kEmitThreads, 0, st>>>(g, S, b, R, t, key0, key1, mode, filt, fa, EmitRange{})
@@ -1175,7 +1058,6 @@ hipError_t launch_binned_round(const BinGeom& g0, const BinBufs& b, uint64_t* S,
 #undef GOSSIP_EMIT_V
 #undef GOSSIP_EMIT
   launch_transpose_u16(b.off, b.offT, g.nt_s, g.nt_d + 1, partial, rs.plen, st);
-  if (g.cls) launch_transpose_u16(b.coff, b.coffT, g.nt_s, g.nt_d + 1, nullptr, 0u, st);
   if ((mode == 2 || mode == 3) && g.split)
     bin_serve_kernel<kIdVF, true><<<serve_grid(g.nt_d, g.serve_grid), kTileThreads, 0, st>>>(g, S, b, R,
                                                                                           IdxRange::all(g.nt_d));
@@ -1743,8 +1625,6 @@ void xd_carve_recv(const XdGeom& g, uint64_t cap_r, void* base, XdBufs* b) {
   b->rb.off = (uint16_t*)take(offs * 2);
   b->rb.offT = (uint16_t*)take(offs * 2);
   b->rb.nzb = b->rb.fullb = nullptr;
-  b->rb.coff = b->rb.coffT = nullptr;
-  b->rb.fpush = nullptr;
 }
 
 hipError_t launch_xd_requests(const XdGeom& g, const XdBufs& b, const uint64_t* S, uint32_t R, uint32_t t,

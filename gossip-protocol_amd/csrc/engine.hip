@@ -148,7 +148,6 @@ struct gossip_engine {
   double alld_frac = 1.0 / 64;    // sparse rounds with k * rare >= alld_frac * N commit every group's D (bench sweep)
   bool sparse_direct = true;      // ... and with an empty majority take the pushes into empty peers in S (kSparseDirect)
   double mid_frac = 0.5;          // sparse rounds test peers in the mid-level summary once this share hits the LDS one
-  double cls_frac = 0.7;          // big-region dense rounds take the class-split layout below this mixed share
   // pipelined rounds (binned engines): the host picks each round's path from the
   // totals it has read, predicted forward over the rounds still in flight, and
   // stays up to `ahead` rounds in front
@@ -505,22 +504,6 @@ uint32_t dense_filter(const gossip_engine* e, const Est& x, double frac) {
   return (pull && empty > frac ? 1u : 0u) | (push && full > frac ? 2u : 0u);
 }
 
-// A dense round's options (launch_binned_round): the edge filter, and for big-region rounds
-// the class-split layout (kRoundCls) when fewer than cls_frac of the senders are mixed, with
-// the apply's waves split between the push walk (mixed senders' pushes, fragmented runs, ~3x
-// the cost per record) and the reply walk (every pull, sequential) by that work.
-double filter_frac_of(const gossip_engine* e);
-uint32_t dense_opts(const gossip_engine* e, const Est& x) {
-  uint32_t opts = dense_filter(e, x, filter_frac_of(e));
-  const double N = (double)e->N, empty = 1.0 - x.nz / N, full = x.full / N, mixed = std::max(0.0, 1.0 - empty - full);
-  if (e->bg.aos && e->mode == GOSSIP_MODE_PUSHPULL && mixed < e->cls_frac) {
-    const double push = 3.0 * mixed, pull = mixed + empty + 0.3 * full;
-    const int pw = (int)std::lround(16.0 * push / std::max(push + pull, 1e-9));
-    opts |= kRoundCls | ((uint32_t)std::min(12, std::max(4, pw)) << 8);
-  }
-  return opts;
-}
-
 // the one-shard dense filter's threshold: gossip_set_param's, else 0.3 while the occupancy
 // bitmaps (N/8 bytes each) fit an XCD's 4 MiB L2; past that every probe is a 64-B fetch from
 // the MALL or HBM and the probes cost more than the edges they drop (2^27 nodes: emit
@@ -556,7 +539,7 @@ int round_timer_collect(gossip_engine* e, uint32_t slot, int64_t limit) {
 
 // One pipelined round: its kernels (bracketed by the slot's events when timing),
 // then the snapshot of the totals into ring slot `slot` (rs).
-int launch_round_path(gossip_engine* e, uint32_t t, bool sparse, uint32_t maj, bool all_d, uint32_t opts,
+int launch_round_path(gossip_engine* e, uint32_t t, bool sparse, uint32_t maj, bool all_d, uint32_t filt,
                       const RoundSync& rs, int slot) {
   const bool timed = e->timing && slot >= 0;
   if (timed) {
@@ -574,8 +557,8 @@ int launch_round_path(gossip_engine* e, uint32_t t, bool sparse, uint32_t maj, b
                                     !all_d ? kSparseFlags : (maj == 0 && e->sparse_direct ? kSparseDirect : kSparseAllD),
                                     e->fa, e->cfg.flags, rs, e->stream));
   else
-    HIP_OK(e, launch_binned_round(e->bg, e->bb, e->S, e->partial_d, e->R, t, e->key0, e->key1, e->mode,
-                                  opts & 0xFFu, e->fa, e->cfg.flags, rs, e->stream, opts >> 8));
+    HIP_OK(e, launch_binned_round(e->bg, e->bb, e->S, e->partial_d, e->R, t, e->key0, e->key1, e->mode, filt,
+                                  e->fa, e->cfg.flags, rs, e->stream));
   if (timed) {
     HIP_OK(e, hipEventRecord(e->evr[slot][1], e->stream));
     e->evr_round[slot] = t;
@@ -644,7 +627,7 @@ int step_planned(gossip_engine* e, uint32_t max_rounds, gossip_round_stats_t* st
       const uint32_t slot = launched % kRing;
       const RoundSync rs = ring_sync(e, slot);
       want[slot] = rs.seq;
-      if (int rc = launch_round_path(e, t0 + launched, sparse, maj, all_d, dense_opts(e, x), rs,
+      if (int rc = launch_round_path(e, t0 + launched, sparse, maj, all_d, dense_filter(e, x, filter_frac_of(e)), rs,
                                      (int)slot))
         return rc;
       ++launched;
@@ -801,7 +784,7 @@ int compute_round(gossip_engine* e, const uint64_t* gathered) {
     const Est x = est_of(e, tot.data());
     const bool sparse = choose_sparse(e, x, &maj, &all_d);
     if ((rc = timer_begin(e, 0))) return rc;
-    if ((rc = launch_round_path(e, e->t, sparse, maj, all_d, dense_opts(e, x), ring_sync(e, 0),
+    if ((rc = launch_round_path(e, e->t, sparse, maj, all_d, dense_filter(e, x, filter_frac_of(e)), ring_sync(e, 0),
                                 -1)))
       return rc;
     return timer_end(e, 0);  // stats are fused into the round kernels
@@ -1251,8 +1234,8 @@ int gossip_set_param(gossip_engine_t* e, const char* name, double v) {
     e->alld_frac = v;
   } else if (n == "sparse_direct") {
     e->sparse_direct = v != 0;
-  } else if (n == "cls_frac") {
-    e->cls_frac = v;
+  } else if (n == "tile_map") {
+    e->bg.tmap = v != 0 ? 1u : 0u;
   } else if (n == "mid_frac") {
     e->mid_frac = v;
   } else if (n == "filter_frac") {

@@ -67,20 +67,17 @@ def test_cfg4_single_engine_equals_fixture(single_engine_run):
     assert hashlib.sha256(memoryview(words).cast("B")).hexdigest() == fx["state_sha256"]
 
 
-# one engine, dense rounds in the class-split layout (binned.h kRoundCls: only mixed senders'
-# pushes packed, full senders' pushes as a bitmap marked by serve) on every dense round, on none,
-# or on every round of an all-dense run
-CLS_PATHS = {"auto_cls_always": {"cls_frac": 2.0}, "auto_cls_never": {"cls_frac": 0.0},
-             "dense_cls": {"sparse_frac": -1, "cls_frac": 2.0}, "dense_plain": {"sparse_frac": -1, "cls_frac": 0.0}}
+# one engine on other round paths against the same fixture: every round dense; every round sparse
+ONE_PATHS = {"dense": {"sparse_frac": -1}, "sparse": {"sparse_frac": 1.0}}
 
 
-@pytest.mark.parametrize("path", list(CLS_PATHS))
-def test_cfg4_dense_layouts_equal_fixture(path):
+@pytest.mark.parametrize("path", list(ONE_PATHS))
+def test_cfg4_round_paths_equal_fixture(path):
     import hashlib
     import json
     with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "cfg4_oracle.json")) as f:
         fx = json.load(f)
-    e = Engine(N, R, "pushpull", K, SEED, flags=1, params=CLS_PATHS[path])
+    e = Engine(N, R, "pushpull", K, SEED, flags=1, params=ONE_PATHS[path])
     e.inject_random()
     res = e.step(64)
     assert res.stats == fx["stats"]
@@ -88,25 +85,6 @@ def test_cfg4_dense_layouts_equal_fixture(path):
     words = np.ascontiguousarray(e.read_shard()[0], dtype="<u8")
     assert hashlib.sha256(memoryview(words).cast("B")).hexdigest() == fx["state_sha256"]
     e.close()
-
-
-@pytest.mark.parametrize("case", [("pushpull", 1, 5, 0x77), ("pushpull", 2, 64, 0x5EED0003)])
-def test_big_region_cls_equal_oracle(case):
-    """Past 4096 tiles (big regions) at a ragged size: every dense round class-split, k = 1 and 2,
-    a 5-bit full mask; against the OpenMP oracle."""
-    mode, k, r, seed = case
-    n = (1 << 26) + 4099
-    o = op.OracleEngine(n, r, mode, k, seed, flags=1, threads=THREADS)
-    o.inject_random()
-    ro = o.step(200)
-    e = Engine(n, r, mode, k, seed, flags=1, params={"sparse_frac": -1, "cls_frac": 2.0})
-    e.inject_random()
-    res = e.step(200)
-    assert res.stats == ro.stats
-    assert np.array_equal(res.infected, ro.infected)
-    assert np.array_equal(e.read_shard(), o.read_shard())
-    e.close()
-    o.close()
 
 
 @pytest.mark.parametrize("plan", list(PLANS))

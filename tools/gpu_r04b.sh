@@ -6,6 +6,8 @@ O=gpurun_out/${1:-r04_b}
 mkdir -p $O
 export TMPDIR=/tmp
 ok() { local rc=$1; if [ "$rc" -ne 0 ]; then echo "STOP: step exited $rc"; exit "$rc"; fi; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_faults.py -v --timeout 120 --timeout-method thread -x > $O/pytest_faults.txt 2>&1; ok $?
+tail -1 $O/pytest_faults.txt
 timeout -k 10 600 python -u -m pytest tests/test_gpu_cfg4_full.py -k "fixture or cls" -v --timeout 300 --timeout-method thread -x > $O/pytest_cls.txt 2>&1; ok $?
 tail -3 $O/pytest_cls.txt
 for c in 0 0.7 2; do
