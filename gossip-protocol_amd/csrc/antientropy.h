@@ -37,6 +37,10 @@ struct AeArgs {
   uint32_t btl, bnt, brs, bnreg;
   uint32_t spb;      // blocks per segment in the gather / apply / fix kernels
   uint32_t dcap;     // binned dense rounds: in-edges sorted per LDS pass (0 = the kernel's capacity)
+  // pipelined sparse rounds (engine step_ae): a word the previous round's launch_ae_gate wrote;
+  // 0 = that round converged, overflowed its edge list or did not run, so this round's sparse
+  // kernels return at once.  Null: always run.
+  const uint32_t* gate;
 };
 
 // binned sparse-scan geometry for N nodes, k exchanges per node
@@ -64,6 +68,9 @@ hipError_t launch_ae_sparse(const AeArgs& a, hipStream_t st);
 // pass also does the churn (no launch_ae_churn before it)
 hipError_t launch_ae_sparse_binned(const AeArgs& a, hipStream_t st);
 hipError_t launch_ae_sparse_stats(const AeArgs& a, hipStream_t st);
+// after a pipelined sparse round (a.partial / a.aux its totals): *gout = the round ran (a.gate
+// open or null), did not overflow its edge list (aux[1] <= segcap) and did not converge
+hipError_t launch_ae_gate(const AeArgs& a, uint32_t* gout, hipStream_t st);
 // binned dense round: geometry of its 2^14-node tiles (the sparse scan's
 // sender regions), whether the kernels' LDS tables cover it, and the round itself: the
 // emit (churn fused, records into a.brec, run starts into a.boff with a.btl / a.bnt of

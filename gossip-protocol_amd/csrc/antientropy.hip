@@ -43,6 +43,11 @@ constexpr int kAeWaves = kAeBlock / 64;
 // fallback dense-round kernels: no minimum waves per SIMD (forcing 3-6 spilled or was no
 // faster: DESIGN.md §3.7)
 
+// pipelined sparse rounds: the previous round closed the gate (converged, overflowed, or gated off)
+__device__ __forceinline__ bool ae_gated_off(const AeArgs& a) {
+  return a.gate && *(volatile const uint32_t*)a.gate == 0u;
+}
+
 __device__ __forceinline__ bool churned(uint8_t alive, uint32_t n, uint32_t t, uint32_t k0, uint32_t k1,
                                         uint32_t fail, uint32_t rec) {
   const uint32_t x = philox4x32_10(u32x4{n, t, 1u, 0u}, k0, k1).x;
@@ -398,6 +403,7 @@ __global__ __launch_bounds__(kAeBinThreads, (NT > kAeBinTiles ? 4 : kAeEmitWaves
   __shared__ __align__(16) uint32_t st[kAeBinRec];  // read back as uint4
   __shared__ uint32_t wsum[kAeBinThreads / 64];
   __shared__ uint32_t wpre[kAeBinThreads / 64 + 1];
+  if (ae_gated_off(a)) return;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t rs = 1u << a.brs, rp = rs * a.k, nt = a.bnt;
   const uint32_t tmask = (1u << a.btl) - 1u;
@@ -500,6 +506,7 @@ __global__ __launch_bounds__(kAeBinThreads) void ae_bin_scan_kernel(AeArgs a) {
   __shared__ uint64_t wa[kAeBinTileWords], ws[kAeBinTileWords];
   __shared__ uint32_t scnt;
   __shared__ uint64_t red[kAeBinThreads / 64];
+  if (ae_gated_off(a)) return;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t T = blockIdx.x, nt = a.bnt;
   const uint32_t tw = 1u << (a.btl - 6);  // words per tile
@@ -1058,6 +1065,7 @@ __device__ __forceinline__ size_t segment_base(const AeArgs& a) { return (size_t
 // snapshot the S_t rows of both ends (before any in-place write)
 template <uint32_t L>
 __global__ __launch_bounds__(kAeBlock) void ae_sparse_gather_kernel(AeArgs a) {
+  if (ae_gated_off(a)) return;
   constexpr uint32_t epb = kAeBlock / L;  // edges per block step
   const uint32_t c = threadIdx.x % L;
   const uint32_t m = segment_edges(a);
@@ -1075,6 +1083,7 @@ __global__ __launch_bounds__(kAeBlock) void ae_sparse_gather_kernel(AeArgs a) {
 // merge in place: both ends take the max of the two snapshots
 template <uint32_t L>
 __global__ __launch_bounds__(kAeBlock) void ae_sparse_apply_kernel(AeArgs a) {
+  if (ae_gated_off(a)) return;
   constexpr uint32_t epb = kAeBlock / L;
   const uint32_t c = threadIdx.x % L;
   const uint32_t m = segment_edges(a);
@@ -1096,6 +1105,7 @@ __global__ __launch_bounds__(kAeBlock) void ae_sparse_fix_kernel(AeArgs a) {
   constexpr uint32_t epb = kAeBlock / L;
   constexpr uint64_t gmask = L >= 64 ? ~0ull : ((1ull << L) - 1ull);
   __shared__ uint64_t red[kAeWaves];
+  if (ae_gated_off(a)) return;
   const uint32_t lane = threadIdx.x & 63, c = lane % L, lead = lane - c;
   const uint32_t m = segment_edges(a);
   const uint32_t tgt = c < a.K ? a.target[c] : 0u;
@@ -1129,6 +1139,7 @@ __global__ __launch_bounds__(kAeBlock) void ae_sparse_fix_kernel(AeArgs a) {
 __global__ __launch_bounds__(kAeBlock) void ae_sparse_stats_kernel(AeArgs a) {
   __shared__ uint32_t cnt[64], tgt[64];
   __shared__ uint64_t red[kAeWaves];
+  if (ae_gated_off(a)) return;
   if (threadIdx.x < 64) {
     cnt[threadIdx.x] = 0;
     tgt[threadIdx.x] = threadIdx.x < a.K ? a.target[threadIdx.x] : 0u;
@@ -1315,6 +1326,17 @@ hipError_t launch_ae_dense_binned(const AeArgs& a, hipStream_t st) {
     AE_DENSE_L(3)
   }
 #undef AE_DENSE_L
+  return hipGetLastError();
+}
+
+__global__ void ae_gate_kernel(AeArgs a, uint32_t* gout) {
+  if (threadIdx.x != 0) return;
+  const bool ran = !ae_gated_off(a);
+  *gout = ran && a.aux[1] <= a.segcap && a.partial[0] != a.partial[1] ? 1u : 0u;
+}
+
+hipError_t launch_ae_gate(const AeArgs& a, uint32_t* gout, hipStream_t st) {
+  ae_gate_kernel<<<1, 64, 0, st>>>(a, gout);
   return hipGetLastError();
 }
 

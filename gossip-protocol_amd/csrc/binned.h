@@ -57,8 +57,6 @@ struct BinGeom {
   uint32_t push_waves;   // push-pull apply: waves [0, push_waves) walk the pushes, the rest the responses
   uint32_t aos;          // push records also packed {value, id} (BinBufs::prec; one shard, big regions)
   uint32_t split;        // one shard: record ids as two u16 arrays (BinBufs::dst / src) instead of ids
-  uint32_t tmap;         // persistent serve / apply tile order: 0 each XCD a contiguous tile range, 1 the
-                         // whole chip on consecutive tiles (gossip_set_param "tile_map")
 };
 
 // big: regions of up to 2 * kMaxSenders senders and 2 * kRecPerRegion records (one shard

@@ -840,7 +840,7 @@ __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, cons
   // tr.at(xcd_remap(v, tr.n)) (the XCD of v is that of blockIdx.x, as with one
   // block per tile); the next tile's image loads into registers during a walk
   const uint32_t nv = tr.n;
-  auto tile_of = [&](uint32_t v) { return tr.at(g.tmap ? v : xcd_remap(v, nv)); };
+  auto tile_of = [&](uint32_t v) { return tr.at(xcd_remap(v, nv)); };
   uint4 x[kTileQ];
   if (blockIdx.x < nv) tile_regs_load(x, S, (uint64_t)tile_of(blockIdx.x) << kTileDLog, g.N);
   for (uint32_t v = blockIdx.x; v < nv; v += gridDim.x) {
@@ -902,7 +902,7 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
   // place stays safe: only this block reads or writes S[X] of its tiles.
   const uint32_t nv = g.nt_d;
   for (uint32_t v = blockIdx.x; v < nv; v += gridDim.x) {
-  const uint32_t X = g.tmap ? v : xcd_remap(v, nv);
+  const uint32_t X = xcd_remap(v, nv);
   const uint64_t node0 = (uint64_t)X << kTileDLog;
   __syncthreads();  // the previous epilogue is done with acc and cnt
   {

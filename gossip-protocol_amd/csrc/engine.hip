@@ -54,6 +54,10 @@ struct gossip_engine {
   // drain it first (copies), so a buffer handed to them needs no stream sync.  A host that runs
   // its own collectives through the per-kind calls always gets the publishing sync.
   bool driven = false;
+  // gossip_set_param "ordered_collectives": the host's collectives run on streams ordered after
+  // the engine's own (torch.distributed bound to the stream the engine launches on, as
+  // gossip_hip.sharded binds it), so a buffer handed out needs no publishing sync either
+  bool ordered = false;
 
   uint64_t N = 0, Nl = 0, lo = 0, hi = 0, nown = 0;
   uint32_t R = 0, W = 0, k = 0, mode = 0, G = 1, rank = 0;
@@ -111,6 +115,12 @@ struct gossip_engine {
   bool ae_sb_valid = false;      // the stale bits of alive, ae_hash and ae_stale describe V
   bool ae_sparse_last = false;   // the last round ran in place (V not rotated)
   uint64_t ae_sparse_rounds = 0, ae_overflows = 0;
+  // pipelined sparse rounds (step_ae): up to ae_ahead enqueued at once, each gated on device by its
+  // predecessor; per round a slot of totals + aux and a gate word
+  uint32_t ae_ahead = 8;
+  bool ae_dense_next = false;    // the next round runs dense (a pipelined sparse round overflowed)
+  uint64_t *ae_slot_d = nullptr, *ae_slot_h = nullptr;
+  uint32_t* ae_gate_d = nullptr;
   // sharded ANTIENTROPY (G > 1): V/Vn = own rows [Nl][K], aex_img = every
   // shard's {alive, stale} word pairs (the all-gather image, ae_sharded.h AexArgs::img)
   bool aex = false;
@@ -148,6 +158,7 @@ struct gossip_engine {
   double alld_frac = 1.0 / 64;    // sparse rounds with k * rare >= alld_frac * N commit every group's D (bench sweep)
   bool sparse_direct = true;      // ... and with an empty majority take the pushes into empty peers in S (kSparseDirect)
   double mid_frac = 0.5;          // sparse rounds test peers in the mid-level summary once this share hits the LDS one
+  double ns_frac = 0.9;           // ... and skip the LDS summary (frontier_scan_ns_kernel) once this share would hit it
   // pipelined rounds (binned engines): the host picks each round's path from the
   // totals it has read, predicted forward over the rounds still in flight, and
   // stays up to `ahead` rounds in front
@@ -267,6 +278,9 @@ void free_all(gossip_engine* e) {
     if (b) (void)hipFree(b);
   if (e->partial_h) (void)hipHostFree(e->partial_h);
   if (e->ae_aux_h) (void)hipHostFree(e->ae_aux_h);
+  if (e->ae_slot_d) (void)hipFree(e->ae_slot_d);
+  if (e->ae_gate_d) (void)hipFree(e->ae_gate_d);
+  if (e->ae_slot_h) (void)hipHostFree(e->ae_slot_h);
   if (e->ring_h) (void)hipHostFree(e->ring_h);
   for (auto& p : e->ev)
     for (auto& x : p)
@@ -504,6 +518,15 @@ uint32_t dense_filter(const gossip_engine* e, const Est& x, double frac) {
   return (pull && empty > frac ? 1u : 0u) | (push && full > frac ? 2u : 0u);
 }
 
+// a sparse round scanned without the LDS summary (more waves per CU): past 2^25 nodes (the
+// mid-level summary exists), once the LDS summary would answer "maybe rare" for at least ns_frac
+// of the peers, 1 - (1 - r)^g for a rare fraction r (predicted), so it filters almost nothing
+bool use_ns(const gossip_engine* e, const Est& x, uint32_t maj) {
+  if (!e->frontier || !e->fb.summ2 || e->fa.any() || e->k > 4) return false;
+  const double r = std::min(1.0, std::max(0.0, (maj ? (double)e->N - x.full : x.nz) / (double)e->N));
+  return 1.0 - std::pow(1.0 - r, (double)(1u << e->fb.glog)) >= e->ns_frac;
+}
+
 // the one-shard dense filter's threshold: gossip_set_param's, else 0.3 while the occupancy
 // bitmaps (N/8 bytes each) fit an XCD's 4 MiB L2; past that every probe is a 64-B fetch from
 // the MALL or HBM and the probes cost more than the edges they drop (2^27 nodes: emit
@@ -539,7 +562,7 @@ int round_timer_collect(gossip_engine* e, uint32_t slot, int64_t limit) {
 
 // One pipelined round: its kernels (bracketed by the slot's events when timing),
 // then the snapshot of the totals into ring slot `slot` (rs).
-int launch_round_path(gossip_engine* e, uint32_t t, bool sparse, uint32_t maj, bool all_d, uint32_t filt,
+int launch_round_path(gossip_engine* e, uint32_t t, bool sparse, uint32_t maj, bool all_d, uint32_t filt, bool ns,
                       const RoundSync& rs, int slot) {
   const bool timed = e->timing && slot >= 0;
   if (timed) {
@@ -555,7 +578,7 @@ int launch_round_path(gossip_engine* e, uint32_t t, bool sparse, uint32_t maj, b
   if (sparse)
     HIP_OK(e, launch_frontier_round(fb, e->S, e->N, e->partial_d, e->R, e->k, t, e->key0, e->key1, e->mode, maj,
                                     !all_d ? kSparseFlags : (maj == 0 && e->sparse_direct ? kSparseDirect : kSparseAllD),
-                                    e->fa, e->cfg.flags, rs, e->stream));
+                                    e->fa, e->cfg.flags, rs, e->stream, ns));
   else
     HIP_OK(e, launch_binned_round(e->bg, e->bb, e->S, e->partial_d, e->R, t, e->key0, e->key1, e->mode, filt,
                                   e->fa, e->cfg.flags, rs, e->stream));
@@ -627,7 +650,8 @@ int step_planned(gossip_engine* e, uint32_t max_rounds, gossip_round_stats_t* st
       const uint32_t slot = launched % kRing;
       const RoundSync rs = ring_sync(e, slot);
       want[slot] = rs.seq;
-      if (int rc = launch_round_path(e, t0 + launched, sparse, maj, all_d, dense_filter(e, x, filter_frac_of(e)), rs,
+      if (int rc = launch_round_path(e, t0 + launched, sparse, maj, all_d, dense_filter(e, x, filter_frac_of(e)),
+                                     sparse && use_ns(e, x, maj), rs,
                                      (int)slot))
         return rc;
       ++launched;
@@ -676,7 +700,7 @@ int ae_read_back(gossip_engine* e) {
 }
 
 bool ae_plan_sparse(const gossip_engine* e) {
-  if (!e->ae_sb_valid || e->ae_force == 0) return false;
+  if (!e->ae_sb_valid || e->ae_force == 0 || e->ae_dense_next) return false;
   if (e->ae_force == 1) return true;
   // exchanges with a stale end ~ 2k x (alive stale after churn): the alive stale
   // nodes that survive plus the stale dead ones that revive (x1.5 margin)
@@ -690,6 +714,7 @@ bool ae_plan_sparse(const gossip_engine* e) {
 int ae_round(gossip_engine* e) {
   int rc;
   bool sparse = ae_plan_sparse(e);
+  e->ae_dense_next = false;
   e->ae_sparse_last = false;
   if (sparse) {
     if (++e->ae_epoch == 0) {  // claims hold epochs: restart them after a wrap
@@ -758,6 +783,100 @@ int ae_round(gossip_engine* e) {
   return GOSSIP_OK;
 }
 
+// gossip_step of a one-engine ANTIENTROPY engine.  Dense rounds, and sparse
+// rounds without the binned scan, run one at a time (ae_round: plan, kernels, totals read back).
+// A run of sparse rounds is pipelined: up to ae_ahead rounds are enqueued at once, each with its
+// own slot of totals and a gate word the previous round's launch_ae_gate writes (it ran, its edge
+// list did not overflow, it did not converge), so the sparse kernels of a round past convergence
+// or after an overflow return at once; the host reads every slot after one sync.  An overflowed
+// round left V, the bitmaps and the claims untouched: it is rerun dense (ae_dense_next), as
+// ae_round does.  The rounds and their results are those of the unpipelined loop.
+int step_ae(gossip_engine* e, uint32_t max_rounds, gossip_round_stats_t* stats, uint64_t* infected,
+            uint32_t* rounds_done) {
+  const size_t pl = part_len(e), sw = pl + 2;  // a slot: the totals, then aux[0..1]
+  if (!e->ae_slot_d) {
+    HIP_OK(e, hipMalloc((void**)&e->ae_slot_d, kRing * sw * 8));
+    HIP_OK(e, hipMalloc((void**)&e->ae_gate_d, kRing * 4));
+    HIP_OK(e, hipHostMalloc((void**)&e->ae_slot_h, kRing * sw * 8, hipHostMallocDefault));
+  }
+  std::vector<uint64_t> part(pl);
+  uint32_t r = 0;
+  if (rounds_done) *rounds_done = 0;
+  auto commit = [&](uint64_t* tot, bool* conv) -> int {  // one round's totals to the caller
+    gossip_round_stats_t st;
+    if (int rc = gossip_round_commit(e, tot, &st)) return rc;
+    if (stats) stats[r] = st;
+    if (infected) std::memcpy(infected + (size_t)r * e->R, tot + 4, (size_t)e->R * 8);
+    ++r;
+    if (rounds_done) *rounds_done = r;
+    *conv = st.converged != 0;
+    return GOSSIP_OK;
+  };
+  while (r < max_rounds) {
+    bool conv = false;
+    if (e->ae_ahead < 2 || !e->ae_bin || !ae_plan_sparse(e)) {  // one round, as the generic loop runs it
+      if (int rc = gossip_round_compute(e, part.data())) return rc;
+      if (int rc = commit(part.data(), &conv)) return rc;
+      if (conv) break;
+      continue;
+    }
+    const uint32_t A = std::min<uint32_t>(std::min<uint32_t>(e->ae_ahead, kRing), max_rounds - r);
+    uint64_t *ab = e->alive, *abn = e->alive_n;
+    for (uint32_t i = 0; i < A; ++i) {
+      if (++e->ae_epoch == 0) {  // claims hold epochs: restart them after a wrap
+        HIP_OK(e, hipMemsetAsync(e->ae_claim, 0, (size_t)e->N * 4, e->stream));
+        e->ae_epoch = 1;
+      }
+      AeArgs a = make_ae_args(e);
+      a.ab = ab;
+      a.abn = abn;
+      a.t = e->t + i;
+      a.partial = e->ae_slot_d + i * sw;
+      a.aux = a.partial + pl;
+      a.gate = i ? e->ae_gate_d + (i - 1) : nullptr;
+      HIP_OK(e, hipMemsetAsync(a.partial, 0, sw * 8, e->stream));
+      if (e->timing) HIP_OK(e, hipEventRecord(e->evr[i][0], e->stream));
+      HIP_OK(e, launch_ae_sparse_binned(a, e->stream));  // churn fused into its first pass
+      HIP_OK(e, launch_ae_sparse_stats(a, e->stream));
+      HIP_OK(e, launch_ae_gate(a, e->ae_gate_d + i, e->stream));
+      if (e->timing) HIP_OK(e, hipEventRecord(e->evr[i][1], e->stream));
+      std::swap(ab, abn);
+    }
+    HIP_OK(e, hipMemcpyAsync(e->ae_slot_h, e->ae_slot_d, A * sw * 8, hipMemcpyDeviceToHost, e->stream));
+    HIP_OK(e, hipStreamSynchronize(e->stream));
+    for (uint32_t i = 0; i < A; ++i) {  // round i ran: round i - 1 neither converged nor overflowed
+      const uint64_t* tot = e->ae_slot_h + i * sw;
+      const uint64_t* aux = tot + pl;
+      if (aux[1] > e->ae_segcap) {  // overflow: the rounds after it did not run
+        ++e->ae_overflows;
+        e->ae_dense_next = true;
+        break;
+      }
+      if (e->timing) {  // the whole sparse round (emit .. stats) in timer 2
+        float ms = 0.f;
+        HIP_OK(e, hipEventElapsedTime(&ms, e->evr[i][0], e->evr[i][1]));
+        e->time_ms[2] += ms;
+        e->launches[2] += 1;
+      }
+      // ae_round's bookkeeping of a sparse round, then gossip_round_compute's
+      e->ae_hash += tot[3];
+      e->ae_stale = aux[0];
+      e->ae_full = tot[0];
+      e->ae_alive = tot[1];
+      e->ae_sb_valid = true;
+      e->ae_sparse_last = true;
+      ++e->ae_sparse_rounds;
+      std::memcpy(part.data(), tot, pl * 8);
+      part[3] = (e->cfg.flags & GOSSIP_FLAG_HASH) ? e->ae_hash : 0;
+      e->last_sparse = false;
+      if (int rc = commit(part.data(), &conv)) return rc;
+      if (conv || r >= max_rounds) break;
+    }
+    if (conv) break;
+  }
+  return GOSSIP_OK;
+}
+
 // compute S_{t+1} of the owned shard from the gathered image + partial stats (device)
 int compute_round(gossip_engine* e, const uint64_t* gathered) {
   const size_t bytes = (size_t)e->W * e->Nl * 8;
@@ -784,7 +903,8 @@ int compute_round(gossip_engine* e, const uint64_t* gathered) {
     const Est x = est_of(e, tot.data());
     const bool sparse = choose_sparse(e, x, &maj, &all_d);
     if ((rc = timer_begin(e, 0))) return rc;
-    if ((rc = launch_round_path(e, e->t, sparse, maj, all_d, dense_filter(e, x, filter_frac_of(e)), ring_sync(e, 0),
+    if ((rc = launch_round_path(e, e->t, sparse, maj, all_d, dense_filter(e, x, filter_frac_of(e)),
+                                sparse && use_ns(e, x, maj), ring_sync(e, 0),
                                 -1)))
       return rc;
     return timer_end(e, 0);  // stats are fused into the round kernels
@@ -1234,8 +1354,13 @@ int gossip_set_param(gossip_engine_t* e, const char* name, double v) {
     e->alld_frac = v;
   } else if (n == "sparse_direct") {
     e->sparse_direct = v != 0;
-  } else if (n == "tile_map") {
-    e->bg.tmap = v != 0 ? 1u : 0u;
+  } else if (n == "ae_ahead") {
+    if (v < 1 || v > kRing) return e->fail(GOSSIP_EINVAL, "ae_ahead: 1 .. %u", kRing);
+    e->ae_ahead = (uint32_t)v;
+  } else if (n == "ordered_collectives") {
+    e->ordered = v != 0;
+  } else if (n == "ns_frac") {
+    e->ns_frac = v;
   } else if (n == "mid_frac") {
     e->mid_frac = v;
   } else if (n == "filter_frac") {
@@ -1450,7 +1575,7 @@ int gossip_exchange_buffers(gossip_engine_t* e, void** send, void** recv, uint64
   uint64_t *s = nullptr, *img = nullptr;
   if (int rc = prepare_send(e, &s, &img)) return rc;
   // the caller's collective runs on another stream: publish the slice first
-  if (!e->driven) HIP_OK(e, hipStreamSynchronize(e->stream));
+  if (!e->driven && !e->ordered) HIP_OK(e, hipStreamSynchronize(e->stream));
   if (send) *send = s;
   if (recv) *recv = img;
   if (send_bytes) *send_bytes = e->aex ? e->Nl / 4 : (uint64_t)e->W * e->Nl * 8;
@@ -1769,7 +1894,7 @@ int gossip_xd_classes(gossip_engine_t* e, void** send, void** image, uint64_t* b
   const uint64_t nwo = (e->nown + 63) / 64;  // (a short last shard: its tail words stay zero)
   HIP_OK(e, hipMemcpyAsync(own, e->lf.nzb, nwo * 8, hipMemcpyDeviceToDevice, e->stream));
   HIP_OK(e, hipMemcpyAsync(own + nwl, e->lf.fullb, nwo * 8, hipMemcpyDeviceToDevice, e->stream));
-  if (!e->driven) HIP_OK(e, hipStreamSynchronize(e->stream));
+  if (!e->driven && !e->ordered) HIP_OK(e, hipStreamSynchronize(e->stream));
   e->xd_cls_ok = true;
   *send = own;
   *image = e->xd_cls;
@@ -1835,7 +1960,7 @@ int gossip_xd_serve(gossip_engine_t* e, void** replies) {
   if (int rc = timer_begin(e, 0)) return rc;
   HIP_OK(e, launch_xd_serve(e->xg, e->xb, e->S, e->xd_nin, e->R, e->stream));
   if (int rc = timer_end(e, 0)) return rc;
-  if (!e->driven) HIP_OK(e, hipStreamSynchronize(e->stream));
+  if (!e->driven && !e->ordered) HIP_OK(e, hipStreamSynchronize(e->stream));
   if (int rc = timer_collect(e, false)) return rc;
   *replies = e->xb.rep_out;
   return GOSSIP_OK;
@@ -1955,7 +2080,7 @@ int gossip_ae_serve(gossip_engine_t* e, void** send) {
   if (int rc = aex_check(e)) return rc;
   if (!e->aex_in) return e->fail(GOSSIP_ESTATE, "gossip_ae_request_recv first");
   HIP_OK(e, launch_aex_serve(make_aex_args(e), e->aex_in, e->aex_nin, e->aex_resp_out, e->stream));
-  if (!e->driven) HIP_OK(e, hipStreamSynchronize(e->stream));
+  if (!e->driven && !e->ordered) HIP_OK(e, hipStreamSynchronize(e->stream));
   *send = e->aex_resp_out;
   return GOSSIP_OK;
 }
@@ -2051,6 +2176,7 @@ int gossip_step(gossip_engine_t* e, uint32_t max_rounds, gossip_round_stats_t* s
   if (e->mode == GOSSIP_MODE_FLOOD && !e->has_topo) return e->fail(GOSSIP_ESTATE, "FLOOD needs a topology");
   if (int rc = set_dev(e)) return rc;
   if (e->binned) return step_planned(e, max_rounds, stats, infected, rounds_done);
+  if (e->mode == GOSSIP_MODE_ANTIENTROPY && !e->aex) return step_ae(e, max_rounds, stats, infected, rounds_done);
   std::vector<uint64_t> part(part_len(e));
   uint32_t r = 0;
   while (r < max_rounds) {

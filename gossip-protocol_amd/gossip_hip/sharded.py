@@ -240,6 +240,10 @@ def _bind_stream(engine, comm: _Comm):
     gossip_set_stream binds as such."""
     if comm.direct and comm.on_device:
         engine.set_stream(torch.cuda.current_stream().cuda_stream)
+        # torch's collectives wait for this stream: no publishing sync in the per-kind calls
+        if not getattr(engine, "_ordered", False):
+            engine.set_param("ordered_collectives", 1)
+            engine._ordered = True
 
 
 def _ae_round(engine, comm: _Comm) -> np.ndarray:

@@ -156,6 +156,11 @@ int gossip_set_stream(gossip_engine_t* eng, void* hip_stream);
  *                  past it reruns the round with the atomicMax passes)
  *   "xd_shards"    sharded random modes: dense rounds run as exchange rounds (kind 3) when
  *                  G >= this (default 6; 0 = never, always the state all-gather)
+ *   "ae_ahead"     ANTIENTROPY, one engine: sparse rounds enqueued at once, each gated on the
+ *                  device by the previous one (1..8, default 8; 1 = one round per host read)
+ *   "ordered_collectives"  1: the host runs its collectives on streams ordered after the
+ *                  engine's (gossip_set_stream to the collectives' launch stream), so the
+ *                  per-kind calls hand out buffers without a publishing stream sync (default 0)
  *   "cc_frac"      sharded random modes: dense rounds on the state image exchange it
  *                  class-coded (kind 4) while the mixed nodes (neither empty nor full) are
  *                  at most this fraction of N (default 0.75; 0 never, 1 always)

@@ -11,6 +11,8 @@ Paths (all must agree with the oracle and with each other):
   overflow — sparse forced with a 64-edge list (ae_cap): rounds whose list overflows are rerun dense
   *_direct — FLAG_AE_DIRECT_SCAN: the sparse scan probes the peers' bitmap words directly
              instead of binning the exchanges by the peer's tile
+  Runs of sparse rounds are pipelined (engine step_ae: ae_ahead rounds enqueued at once, each gated
+  on device by its predecessor); *_ahead1 runs them one at a time, *_ahead3 three at a time.
 """
 import os
 
@@ -31,7 +33,9 @@ PATHS = {"auto": (0, {}), "dense": (0, {"ae_sparse": 0}), "sparse": (0, {"ae_spa
          "overflow": (0, {"ae_sparse": 1, "ae_cap": 64}),
          # sparse rounds with the direct scan (random bitmap probes) instead of the binned one
          "sparse_direct": (FLAG_AE_DIRECT_SCAN, {"ae_sparse": 1}),
-         "auto_direct": (FLAG_AE_DIRECT_SCAN, {})}
+         "auto_direct": (FLAG_AE_DIRECT_SCAN, {}),
+         "auto_ahead1": (0, {"ae_ahead": 1}), "sparse_ahead3": (0, {"ae_sparse": 1, "ae_ahead": 3}),
+         "overflow_ahead3": (0, {"ae_sparse": 1, "ae_cap": 64, "ae_ahead": 3})}
 
 
 def _engine(path, *args, flags=0, **kw):
