@@ -505,17 +505,10 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
     }
     __syncthreads();  // every staged id is out
     uint64_t* sv = (uint64_t*)st_ids;  // 2 * kRecPerRegion u32 = kMaxS u64
-    if (PKC) {  // v[] was let go after the count pass (its registers held the peers): reread
+    // (V = 5 keeps v[] live through the count pass rather than rereading S here: 5.86 vs
+    // 5.98 ms per 2^27 dense round, profiles/r04_e/summary.txt)
 #pragma unroll
-      for (uint32_t q = 0; q < kQ; ++q) {
-        const uint32_t i = tid + q * kEmitThreads;
-        const uint64_t x = S[snd0 + base + min(i, nsend - 1)];
-        sv[i] = i < nsend ? x : 0ull;
-      }
-    } else {
-#pragma unroll
-      for (uint32_t q = 0; q < kQ; ++q) sv[tid + q * kEmitThreads] = v[q];
-    }
+    for (uint32_t q = 0; q < kQ; ++q) sv[tid + q * kEmitThreads] = v[q];
     __syncthreads();
     uint32_t* gprec = b.prec + (size_t)s * g.rp * 3;
 #pragma unroll 4

@@ -158,7 +158,6 @@ struct gossip_engine {
   double alld_frac = 1.0 / 64;    // sparse rounds with k * rare >= alld_frac * N commit every group's D (bench sweep)
   bool sparse_direct = true;      // ... and with an empty majority take the pushes into empty peers in S (kSparseDirect)
   double mid_frac = 0.5;          // sparse rounds test peers in the mid-level summary once this share hits the LDS one
-  double ns_frac = 0.9;           // ... and skip the LDS summary (frontier_scan_ns_kernel) once this share would hit it
   // pipelined rounds (binned engines): the host picks each round's path from the
   // totals it has read, predicted forward over the rounds still in flight, and
   // stays up to `ahead` rounds in front
@@ -518,15 +517,6 @@ uint32_t dense_filter(const gossip_engine* e, const Est& x, double frac) {
   return (pull && empty > frac ? 1u : 0u) | (push && full > frac ? 2u : 0u);
 }
 
-// a sparse round scanned without the LDS summary (more waves per CU): past 2^25 nodes (the
-// mid-level summary exists), once the LDS summary would answer "maybe rare" for at least ns_frac
-// of the peers, 1 - (1 - r)^g for a rare fraction r (predicted), so it filters almost nothing
-bool use_ns(const gossip_engine* e, const Est& x, uint32_t maj) {
-  if (!e->frontier || !e->fb.summ2 || e->fa.any() || e->k > 4) return false;
-  const double r = std::min(1.0, std::max(0.0, (maj ? (double)e->N - x.full : x.nz) / (double)e->N));
-  return 1.0 - std::pow(1.0 - r, (double)(1u << e->fb.glog)) >= e->ns_frac;
-}
-
 // the one-shard dense filter's threshold: gossip_set_param's, else 0.3 while the occupancy
 // bitmaps (N/8 bytes each) fit an XCD's 4 MiB L2; past that every probe is a 64-B fetch from
 // the MALL or HBM and the probes cost more than the edges they drop (2^27 nodes: emit
@@ -562,7 +552,7 @@ int round_timer_collect(gossip_engine* e, uint32_t slot, int64_t limit) {
 
 // One pipelined round: its kernels (bracketed by the slot's events when timing),
 // then the snapshot of the totals into ring slot `slot` (rs).
-int launch_round_path(gossip_engine* e, uint32_t t, bool sparse, uint32_t maj, bool all_d, uint32_t filt, bool ns,
+int launch_round_path(gossip_engine* e, uint32_t t, bool sparse, uint32_t maj, bool all_d, uint32_t filt,
                       const RoundSync& rs, int slot) {
   const bool timed = e->timing && slot >= 0;
   if (timed) {
@@ -578,7 +568,7 @@ int launch_round_path(gossip_engine* e, uint32_t t, bool sparse, uint32_t maj, b
   if (sparse)
     HIP_OK(e, launch_frontier_round(fb, e->S, e->N, e->partial_d, e->R, e->k, t, e->key0, e->key1, e->mode, maj,
                                     !all_d ? kSparseFlags : (maj == 0 && e->sparse_direct ? kSparseDirect : kSparseAllD),
-                                    e->fa, e->cfg.flags, rs, e->stream, ns));
+                                    e->fa, e->cfg.flags, rs, e->stream));
   else
     HIP_OK(e, launch_binned_round(e->bg, e->bb, e->S, e->partial_d, e->R, t, e->key0, e->key1, e->mode, filt,
                                   e->fa, e->cfg.flags, rs, e->stream));
@@ -651,8 +641,7 @@ int step_planned(gossip_engine* e, uint32_t max_rounds, gossip_round_stats_t* st
       const RoundSync rs = ring_sync(e, slot);
       want[slot] = rs.seq;
       if (int rc = launch_round_path(e, t0 + launched, sparse, maj, all_d, dense_filter(e, x, filter_frac_of(e)),
-                                     sparse && use_ns(e, x, maj), rs,
-                                     (int)slot))
+                                     rs, (int)slot))
         return rc;
       ++launched;
     }
@@ -904,8 +893,7 @@ int compute_round(gossip_engine* e, const uint64_t* gathered) {
     const bool sparse = choose_sparse(e, x, &maj, &all_d);
     if ((rc = timer_begin(e, 0))) return rc;
     if ((rc = launch_round_path(e, e->t, sparse, maj, all_d, dense_filter(e, x, filter_frac_of(e)),
-                                sparse && use_ns(e, x, maj), ring_sync(e, 0),
-                                -1)))
+                                ring_sync(e, 0), -1)))
       return rc;
     return timer_end(e, 0);  // stats are fused into the round kernels
   } else if (e->sbin) {  // sharded dense round: binned pipeline over the gathered image
@@ -1359,8 +1347,6 @@ int gossip_set_param(gossip_engine_t* e, const char* name, double v) {
     e->ae_ahead = (uint32_t)v;
   } else if (n == "ordered_collectives") {
     e->ordered = v != 0;
-  } else if (n == "ns_frac") {
-    e->ns_frac = v;
   } else if (n == "mid_frac") {
     e->mid_frac = v;
   } else if (n == "filter_frac") {

@@ -91,8 +91,6 @@ hipError_t launch_frontier_inject(const FrontierBufs& f, uint64_t* S, uint64_t N
 hipError_t launch_frontier_round(const FrontierBufs& f, uint64_t* S, uint64_t N, uint64_t* partial, uint32_t R,
                                  uint32_t k, uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t maj,
                                  uint32_t dmode, const Faults& fa, uint32_t flags, const RoundSync& rs,
-                                 hipStream_t st, bool ns = false);
-// ns: the scan without the LDS summary (more waves per CU; frontier.hip frontier_scan_ns_kernel),
-// for rounds whose LDS summary would be saturated; needs the mid-level summary (N > 2^25), no faults.
+                                 hipStream_t st);
 
 }  // namespace gossip

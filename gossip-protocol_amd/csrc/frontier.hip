@@ -155,11 +155,7 @@ __global__ __launch_bounds__(256) void frontier_summary_kernel(FrontierBufs f, u
 // A summary hit is confirmed in the exact rare bitmap before S_t[p] is read
 // (the bitmap is L2-resident; S is not).  Pull deltas belong to the node's own
 // lane and are plain stores to P; push deltas are atomic ORs into D.
-// T threads per block.  NS (no LDS summary; past 2^25 nodes, rounds whose LDS summary would be
-// saturated): every live edge of an acting node goes straight to the mid-level summary, and with
-// no 128 KiB of LDS per block three blocks share a CU: the scan waits on dependent probes, so
-// more waves in flight is what pays.
-template <int MAJ, int MODE, bool FAULTS, int T = kScanThreads, bool NS = false>  // FAULTS: edge loss / partitions active (§2.8)
+template <int MAJ, int MODE, bool FAULTS>  // FAULTS: edge loss / partitions active (§2.8)
 // direct (kSparseDirect, MAJ 0): pushes into majority peers go to Sw (= S) instead of D.
 __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const FrontierBufs& f,
                                           const uint64_t* __restrict__ S, uint64_t* Sw, uint64_t N, uint32_t R,
@@ -168,28 +164,27 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
   const uint32_t* summ = (const uint32_t*)summ4;
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t n4 = (f.summ_words + 3) / 4;
-  if (!NS)
-    for (uint32_t i = tid; i < n4; i += T) summ4[i] = ((const uint4*)f.summ)[i];
+  for (uint32_t i = tid; i < n4; i += kScanThreads) summ4[i] = ((const uint4*)f.summ)[i];
 
   constexpr bool kPush = (MODE & 1) != 0, kPull = (MODE & 2) != 0;
   const uint64_t fm = full_mask1(R), maj = MAJ ? fm : 0ull, nm1 = N - 1;
   const uint32_t glog = f.glog;
-  auto summ_bit = [&](uint32_t p) -> bool { return NS || ((summ[p >> (glog + 5)] >> ((p >> glog) & 31u)) & 1u); };
+  auto summ_bit = [&](uint32_t p) -> bool { return (summ[p >> (glog + 5)] >> ((p >> glog) & 31u)) & 1u; };
   // node ids are < 2^32 (gossip_create checks N), so all index math is 32-bit
   const uint32_t b0 = blockIdx.x * (uint32_t)per_block, b1 = (uint32_t)min<uint64_t>((uint64_t)b0 + per_block, N);
   for (uint32_t c0 = b0; c0 < b1; c0 += kRwWords * 64) {
     const uint32_t c1 = min(c0 + kRwWords * 64, b1);
     __syncthreads();  // previous chunk done with rws
-    for (uint32_t i = tid; i < ((c1 - c0 + 63) >> 6); i += T) rws[i] = rare_word<MAJ>(f, (c0 >> 6) + i, N);
+    for (uint32_t i = tid; i < ((c1 - c0 + 63) >> 6); i += kScanThreads) rws[i] = rare_word<MAJ>(f, (c0 >> 6) + i, N);
     __syncthreads();
-    for (uint32_t base = c0; base < c1; base += T * kScanUnroll) {
+    for (uint32_t base = c0; base < c1; base += kScanThreads * kScanUnroll) {
       uint64_t x[kScanUnroll], vp[kScanUnroll][4];
       uint32_t pp[kScanUnroll][4], hit[kScanUnroll], live[kScanUnroll];
       bool act[kScanUnroll], rn[kScanUnroll];
       // 1. draws and LDS summary tests (no global memory); live = edges not lost (§2.8)
 #pragma unroll
       for (int u = 0; u < kScanUnroll; ++u) {
-        const uint32_t n = base + u * T + tid;
+        const uint32_t n = base + u * kScanThreads + tid;
         const bool valid = n < c1;
         rn[u] = valid && ((rws[(n - c0) >> 6] >> lane) & 1ull);
         // a majority node only acts through a rare peer; push from an empty node and
@@ -256,7 +251,7 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
       // 3. S_t of the rare ends only (a majority node's value is known)
 #pragma unroll
       for (int u = 0; u < kScanUnroll; ++u) {
-        const uint32_t n = base + u * T + tid;
+        const uint32_t n = base + u * kScanThreads + tid;
         x[u] = rn[u] ? scan_ld(&S[n]) : maj;
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) vp[u][j] = ((hit[u] >> j) & 1u) ? scan_ld(&S[pp[u][j]]) : maj;
@@ -301,7 +296,7 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
 #pragma unroll
         for (int u = 0; u < kScanUnroll; ++u) {
           if (!act[u]) continue;
-          const uint32_t n = base + u * T + tid;
+          const uint32_t n = base + u * kScanThreads + tid;
           uint64_t acc = 0;
           u32x4 r4{0, 0, 0, 0}, lw{0, 0, 0, 0};
           const Reach rc = FAULTS ? reach_of(n, fa) : Reach{0u, 0xFFFFFFFFu};  // n's partition block (§2.8)
@@ -337,7 +332,7 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
       // pushes into it are atomic ORs too), so the commit reads no P for it.
 #pragma unroll
       for (int u = 0; u < kScanUnroll; ++u) {
-        const uint32_t n = base + u * T + tid;
+        const uint32_t n = base + u * kScanThreads + tid;
         const bool dmaj = MAJ == 0 && direct && !rn[u];
         if (dmaj && accs[u]) atomicOr((unsigned long long*)&Sw[n], (unsigned long long)accs[u]);
         const uint64_t pz = __ballot(!dmaj && accs[u] != 0);
@@ -364,27 +359,6 @@ __global__ __launch_bounds__(kScanThreads, kScanWaves) void frontier_scan_kernel
   else
     scan_body<0, MODE, FAULTS>(summ4, rws, f, S, S, N, R, k, t, key0, key1, per_block, mark_d != 0, direct != 0,
                                mid, fa);
-}
-
-// The NS scan (scan_body NS): no LDS summary, 512-thread blocks, three per CU.  No faults (the
-// host picks it only without); the mid-level summary must exist (N > 2^25).
-constexpr int kScanNsThreads = 512;
-constexpr uint32_t kScanNsGrid = 768;
-template <int MODE>
-__global__ __launch_bounds__(kScanNsThreads, 6) void frontier_scan_ns_kernel(FrontierBufs f, uint64_t* S, uint64_t N,
-                                                                           uint32_t R, uint32_t k, uint32_t t,
-                                                                           uint32_t key0, uint32_t key1,
-                                                                           uint64_t per_block, const uint64_t* partial,
-                                                                           uint32_t maj, uint32_t mark_d,
-                                                                           uint32_t direct, Faults fa) {
-  __shared__ uint64_t rws[kRwWords];
-  if (rare_count(partial, N, R, maj) == 0) return;  // converged (or nothing injected): nothing moves
-  if (maj)
-    scan_body<1, MODE, false, kScanNsThreads, true>(nullptr, rws, f, S, S, N, R, k, t, key0, key1, per_block,
-                                                    mark_d != 0, false, true, fa);
-  else
-    scan_body<0, MODE, false, kScanNsThreads, true>(nullptr, rws, f, S, S, N, R, k, t, key0, key1, per_block,
-                                                    mark_d != 0, direct != 0, true, fa);
 }
 
 // Stats of one 64-node group whose words went from old to nw (old == 0 in a
@@ -647,10 +621,9 @@ hipError_t launch_frontier_inject(const FrontierBufs& f, uint64_t* S, uint64_t N
 hipError_t launch_frontier_round(const FrontierBufs& f, uint64_t* S, uint64_t N, uint64_t* partial, uint32_t R,
                                  uint32_t k, uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t maj,
                                  uint32_t dmode, const Faults& fa, uint32_t flags, const RoundSync& rs,
-                                 hipStream_t st, bool ns) {
+                                 hipStream_t st) {
   if (N == 0) return hipSuccess;  // a shard without nodes
   if (maj != 0 && dmode == kSparseDirect) dmode = kSparseAllD;  // (a full peer takes no push)
-  if (ns && (fa.any() || !f.summ2 || k > 4)) ns = false;
   frontier_summary_kernel<<<(f.summ_words + 255) / 256 + (f.summ2_words + 255) / 256, 256, 0, st>>>(f, N, partial, R,
                                                                                                    maj);
   const uint64_t chunks = (N + kScanThreads - 1) / kScanThreads;
@@ -661,21 +634,6 @@ hipError_t launch_frontier_round(const FrontierBufs& f, uint64_t* S, uint64_t N,
   frontier_scan_kernel<MODE, FAULTS><<<grid, kScanThreads, 0, st>>>(f, S, N, R, k, t, key0, key1, per, partial, \
                                                                     maj, dmode != kSparseAllD, dmode == kSparseDirect, fa)
   const bool faults = fa.any();
-  if (ns) {
-    const uint64_t nch = (N + kScanNsThreads - 1) / kScanNsThreads;
-    const uint32_t ng = (uint32_t)(nch < kScanNsGrid ? nch : kScanNsGrid);
-    const uint64_t nper = ((N + ng - 1) / ng + kScanNsThreads - 1) / kScanNsThreads * kScanNsThreads;
-#define GOSSIP_SCAN_NS(MODE)                                                                                    \
-  frontier_scan_ns_kernel<MODE><<<ng, kScanNsThreads, 0, st>>>(f, S, N, R, k, t, key0, key1, nper, partial, maj, \
-                                                               dmode != kSparseAllD, dmode == kSparseDirect, fa)
-    switch (mode) {
-      case 1: GOSSIP_SCAN_NS(1); break;
-      case 2: GOSSIP_SCAN_NS(2); break;
-      case 3: GOSSIP_SCAN_NS(3); break;
-      default: return hipErrorInvalidValue;
-    }
-#undef GOSSIP_SCAN_NS
-  } else
   switch (mode) {
     case 1: if (faults) GOSSIP_SCAN(1, true); else GOSSIP_SCAN(1, false); break;
     case 2: if (faults) GOSSIP_SCAN(2, true); else GOSSIP_SCAN(2, false); break;

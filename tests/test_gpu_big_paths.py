@@ -25,10 +25,7 @@ THREADS = min(16, os.cpu_count() or 1)
 PATHS = {"auto": {}, "sparse_flags": {"sparse_frac": 1.0, "alld_frac": 1e30},
          "sparse_alld": {"sparse_frac": 1.0, "alld_frac": 0, "sparse_direct": 0},
          "sparse_direct": {"sparse_frac": 1.0, "alld_frac": 0, "sparse_direct": 1},
-         "sparse_mid": {"sparse_frac": 1.0, "mid_frac": 0},
-         # every sparse round scanned without the LDS summary (frontier_scan_ns_kernel; not with faults)
-         "sparse_ns": {"sparse_frac": 1.0, "ns_frac": 0},
-         "sparse_ns_direct": {"sparse_frac": 1.0, "ns_frac": 0, "alld_frac": 0, "sparse_direct": 1}}
+         "sparse_mid": {"sparse_frac": 1.0, "mid_frac": 0}}
 CASES = {"pushpull-k2-R64": ("pushpull", 2, 64, 0x5EED0003, 0), "push-k3-R5": ("push", 3, 5, 77, 0),
          "pull-k1-R7-loss": ("pull", 1, 7, 9, 1 << 30), "pull-k2-R3": ("pull", 2, 3, 0x51, 0)}
 

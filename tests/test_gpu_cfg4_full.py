@@ -68,8 +68,7 @@ def test_cfg4_single_engine_equals_fixture(single_engine_run):
 
 
 # one engine on other round paths against the same fixture: every round dense; every round sparse
-ONE_PATHS = {"dense": {"sparse_frac": -1}, "sparse": {"sparse_frac": 1.0},
-             "sparse_ns": {"ns_frac": 0}, "sparse_ns_never": {"ns_frac": 2}}
+ONE_PATHS = {"dense": {"sparse_frac": -1}, "sparse": {"sparse_frac": 1.0}}
 
 
 @pytest.mark.parametrize("path", list(ONE_PATHS))
