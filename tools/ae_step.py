@@ -10,6 +10,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "gossip-protocol_amd"))
 import torch  # noqa: E402,F401  (the HIP runtime, as bench.py has it)
 from gossip_hip import FLAG_TIMING, Engine, loss_threshold  # noqa: E402
+from gossip_hip import engine as _eng  # noqa: E402
+
+if os.environ.get("GOSSIP_LIB"):  # a variant build (tools/build_variants.sh)
+    _eng.load_library(os.environ["GOSSIP_LIB"])
 
 N, K, k, seed = 1 << int(os.environ.get("AE_LG", 26)), 16, 1, 0x5EED0005
 timing = os.environ.get("AE_TIMING", "1") != "0"
@@ -29,6 +33,6 @@ wall = (time.perf_counter() - t0) / runs
 d, dn = e.kernel_time(0)
 s, sn = e.kernel_time(2)
 st, _ = e.kernel_time(1)
-print(f"ae_ahead={os.environ.get('AE_AHEAD', 8)} timing={int(timing)}: {r.rounds} rounds, wall {wall * 1e3:.1f} ms per run, "
+print(f"{os.environ.get('GOSSIP_LIB', 'default')} ae_ahead={os.environ.get('AE_AHEAD', 8)} timing={int(timing)}: {r.rounds} rounds, wall {wall * 1e3:.1f} ms per run, "
       f"dense {dn // runs} x {d / max(dn, 1):.3f} ms, sparse {sn // runs} x {s / max(sn, 1):.3f} ms, "
       f"device {(d + s + st) / runs:.1f} ms per run, {N * r.rounds / wall:.3e} node-updates/s")
