@@ -5,8 +5,8 @@
 //
 // Reference: (*NodeState).Gossip, main.go:65-89 — here each exchange of the round
 // model is one SyncRPC-shaped request/reply between the two ends'
-// owners.  Every shard receives every shard's alive bits (its churn: a per-node Philox
-// draw, tag 1) and stale bits (row != target) each round, one 16-B word pair per 64 nodes:
+// owners.  Every shard receives every shard's alive bits (its churn: ae_churn_word, a
+// per-node Philox draw) and stale bits (row != target) each round, one 16-B word pair per 64 nodes:
 // an exchange between two rows equal to the target moves nothing, so only exchanges with
 // a stale end travel.
 #include "ae_sharded.h"
@@ -44,7 +44,8 @@ __global__ __launch_bounds__(kAxBlock) void aex_churn_kernel(AexArgs a) {
     bool al = false;
     if (ch * 64 + lane < a.nown) {
       const bool was = (a.img[2 * w] >> lane) & 1ull;
-      const uint32_t x = philox4x32_10(u32x4{(uint32_t)n, a.t, 1u, 0u}, a.key0, a.key1).x;
+      const u32x4 x0 = ae_first_draw((uint32_t)n, a.t, a.k, a.key0, a.key1);
+      const uint32_t x = ae_churn_word(x0, (uint32_t)n, a.t, a.k, a.key0, a.key1);
       al = was ? !(x < a.fail) : (x < a.rec);
     }
     const uint64_t b = __ballot(al);

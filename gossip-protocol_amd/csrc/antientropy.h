@@ -5,6 +5,10 @@
 
 namespace gossip {
 
+// AeArgs::flags bit (internal, above the ABI's GOSSIP_FLAG_*): the stale bits of S_t in ab are
+// exact, so the binned dense round may skip the exchanges that cannot move a row
+constexpr uint32_t kAeSbValid = 1u << 30;
+
 struct AeArgs {
   uint32_t* V;             // S_t rows [N][K] (sparse rounds update them in place)
   uint32_t* Vn;            // dense rounds: S_{t+1} rows

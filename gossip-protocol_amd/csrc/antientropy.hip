@@ -1,7 +1,7 @@
 // antientropy.hip — version-vector anti-entropy with churn (configs[4]).
 //
 // Each node holds K uint32 versions (AoS rows V[n*K + c], so a peer's whole
-// vector is one contiguous K*4-byte row).  Round t: churn by Philox tag 1,
+// vector is one contiguous K*4-byte row).  Round t: churn (ae_churn_word),
 // then every alive node n exchanges with its Philox peers p_j(n,t) that are
 // alive too: both take the elementwise max of the two S_t rows.  The
 // reference's only failure handling is retry-until-acked (main.go:77-87);
@@ -48,9 +48,8 @@ __device__ __forceinline__ bool ae_gated_off(const AeArgs& a) {
   return a.gate && *(volatile const uint32_t*)a.gate == 0u;
 }
 
-__device__ __forceinline__ bool churned(uint8_t alive, uint32_t n, uint32_t t, uint32_t k0, uint32_t k1,
-                                        uint32_t fail, uint32_t rec) {
-  const uint32_t x = philox4x32_10(u32x4{n, t, 1u, 0u}, k0, k1).x;
+// alive after round t's churn, from the churn word (ae_churn_word)
+__device__ __forceinline__ bool churned(bool alive, uint32_t x, uint32_t fail, uint32_t rec) {
   return alive ? !(x < fail) : (x < rec);
 }
 
@@ -133,7 +132,11 @@ __global__ __launch_bounds__(kAeBlock) void ae_churn_kernel(AeArgs a) {
   for (uint64_t ch = wave_id(); ch < chunks; ch += wave_count()) {
     const uint64_t n = ch * 64 + lane;
     bool al = false;
-    if (n < a.N) al = churned((a.ab[2 * ch] >> lane) & 1ull, (uint32_t)n, a.t, a.key0, a.key1, a.fail, a.rec);
+    if (n < a.N) {
+      const u32x4 x0 = ae_first_draw((uint32_t)n, a.t, a.k, a.key0, a.key1);
+      al = churned((a.ab[2 * ch] >> lane) & 1ull, ae_churn_word(x0, (uint32_t)n, a.t, a.k, a.key0, a.key1), a.fail,
+                   a.rec);
+    }
     const uint64_t b = __ballot(al);
     if (lane == 0) a.abn[2 * ch] = b;
     if (lane == 1) a.abn[2 * ch + 1] = a.ab[2 * ch + 1];
@@ -423,16 +426,20 @@ __global__ __launch_bounds__(kAeBinThreads, (NT > kAeBinTiles ? 4 : kAeEmitWaves
       const uint64_t ch = n >> 6;
       const bool in = n < a.N;
       const uint64_t aw = in ? a.ab[2 * ch] : 0ull, sw = in ? a.ab[2 * ch + 1] : 0ull;
-      const bool al = in && churned((aw >> lane) & 1ull, (uint32_t)n, a.t, a.key0, a.key1, a.fail, a.rec);
+      // one cipher for the churn and the first peers (k <= 3)
+      u32x4 x = ae_first_draw((uint32_t)n, a.t, a.k, a.key0, a.key1);
+      const bool al =
+          in && churned((aw >> lane) & 1ull, ae_churn_word(x, (uint32_t)n, a.t, a.k, a.key0, a.key1), a.fail, a.rec);
       const uint64_t nb = __ballot(al);
       if (in && lane == 0) a.abn[2 * ch] = nb;
       if (in && lane == 1) a.abn[2 * ch + 1] = sw;  // stale bits of S_t carried
       if (!al) continue;
       live |= 1u << q;
       stl |= (uint32_t)((sw >> lane) & 1ull) << q;
-      u32x4 x{0, 0, 0, 0};
       for (uint32_t j = 0; j < a.k; ++j) {
-        const uint32_t p = peer_j(a, (uint32_t)n, j, x);
+        // (x already holds the draw of j < 4 when k <= 3)
+        const uint32_t p =
+            j == 0 && a.k <= 3 ? peer_from_word(x.x, a.N - 1, (uint32_t)n) : peer_j(a, (uint32_t)n, j, x);
         if (K1) pr[q] = p;
         atomicAdd(&cur[p >> a.btl], 1u);
       }
@@ -665,7 +672,24 @@ struct AeSortSh {
   uint32_t* srt;   // [cap] sender | (node & 63) << 26, sorted by node
   const uint32_t* rt;  // run table or nullptr
   uint32_t *wsum, *wpre, *rng;  // [NW], [NW + 1], [3]: range end, range base, total
+  // stale filter (kAeSbValid: the stale bits of S_t in a.ab are exact): an in-edge matters only into a
+  // stale node, and one from an up-to-date sender (row == target, the componentwise maximum of
+  // every row) makes the node's S_{t+1} row the target whatever else it gets, so it is marked in
+  // tgtb and never sorted; only stale-sender in-edges into stale nodes are gathered
+  bool filt;
+  uint64_t* stile;        // [kAeDTile / 64] stale bits of the tile's nodes (S_t), when filt
+  uint32_t* tgtb;         // [kAeDTile / 32] node took an in-edge from an up-to-date sender, when filt
 };
+
+// the record is sorted (gathered) at all; marks tgtb for an up-to-date sender's in-edge
+__device__ __forceinline__ bool ae_sort_keep(const AeArgs& a, const AeSortSh& sh, uint32_t rec, uint32_t pl,
+                                             bool mark) {
+  if (!sh.filt) return true;
+  if (!((sh.stile[pl >> 6] >> (pl & 63u)) & 1ull)) return false;  // the node is up to date: nothing to take
+  if ((rec >> (a.btl + a.brs)) & 1u) return true;           // a stale sender: its row is gathered
+  if (mark) atomicOr(&sh.tgtb[pl >> 5], 1u << (pl & 31u));
+  return false;
+}
 
 __device__ __forceinline__ uint32_t ae_pget(const AeSortSh& sh, uint32_t i) {
   return i >= kAeDTile ? sh.rng[2] : (sh.pos2[i >> 1] >> ((i & 1u) << 4)) & 0xFFFFu;
@@ -677,10 +701,15 @@ __device__ void ae_sort_count(const AeArgs& a, const AeSortSh& sh, uint32_t T) {
   constexpr uint32_t nth = NW * 64;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (uint32_t i = tid; i < kAeDTile / 2; i += nth) sh.pos2[i] = 0;
+  if (sh.filt) {
+    for (uint32_t i = tid; i < kAeDTile / 32; i += nth) sh.tgtb[i] = 0;
+    const uint64_t w0 = ((uint64_t)T << kAeDTileLog) >> 6, nw = (a.N + 63) >> 6;
+    for (uint32_t i = tid; i < kAeDTile / 64; i += nth) sh.stile[i] = w0 + i < nw ? a.ab[2 * (w0 + i) + 1] : 0ull;
+  }
   __syncthreads();
   ae_tile_records<NW>(a, sh.rt, T, [&](uint32_t rec, uint32_t) {
       const uint32_t pl = rec & (kAeDTile - 1u);
-      atomicAdd(&sh.pos2[pl >> 1], 1u << ((pl & 1u) << 4));
+      if (ae_sort_keep(a, sh, rec, pl, true)) atomicAdd(&sh.pos2[pl >> 1], 1u << ((pl & 1u) << 4));
     });
   __syncthreads();
   constexpr uint32_t qw = (kAeDTile / 2 + nth - 1) / nth;  // words per thread
@@ -742,7 +771,7 @@ __device__ uint32_t ae_sort_range(const AeArgs& a, const AeSortSh& sh, uint32_t 
   if (ae_pget(sh, hi) != base) {
     ae_tile_records<NW>(a, sh.rt, T, [&](uint32_t rec, uint32_t reg) {
       const uint32_t pl = rec & (kAeDTile - 1u);
-      if (pl >= lo && pl < hi) {
+      if (pl >= lo && pl < hi && ae_sort_keep(a, sh, rec, pl, false)) {
         const uint32_t b = (pl & 1u) << 4;
         const uint32_t s = (((atomicAdd(&sh.pos2[pl >> 1], 1u << b) >> b) & 0xFFFFu) - base) & 0xFFFFu;
         if (s < cap) sh.srt[s] = ((reg << a.brs) + ((rec >> kAeDTileLog) & nmask)) | ((pl & 63u) << 26);
@@ -772,6 +801,8 @@ __global__ __launch_bounds__(kAeDThreads) void ae_dense_apply_kernel(AeArgs a) {
   __shared__ uint32_t scr[kW][64 * L];  // per wave: in-edge max-merges of its chunk, [node][component]
   __shared__ uint32_t wsum[kW], wpre[kW + 1], rng[3], cnt[64];
   __shared__ uint64_t red[kW];
+  __shared__ uint64_t stile[kAeDTile / 64];
+  __shared__ uint32_t tgtb[kAeDTile / 32];
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, sub = lane / L, c = lane % L;
   const uint32_t T = ae_tile_of(a.bnt);
   const uint64_t t0 = (uint64_t)T << kAeDTileLog;
@@ -783,7 +814,8 @@ __global__ __launch_bounds__(kAeDThreads) void ae_dense_apply_kernel(AeArgs a) {
     rt[r] = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
   }
   if (tid < 64) cnt[tid] = 0;
-  const AeSortSh sh{pos2, srt, rt, wsum, wpre, rng};
+  const bool filt = (a.flags & kAeSbValid) != 0;
+  const AeSortSh sh{pos2, srt, rt, wsum, wpre, rng, filt, stile, tgtb};
   ae_sort_count<kW>(a, sh, T);
   auto pget = [&](uint32_t i) { return ae_pget(sh, i); };
   const uint32_t tgt = c < a.K ? a.target[c] : 0u;
@@ -805,6 +837,9 @@ __global__ __launch_bounds__(kAeDThreads) void ae_dense_apply_kernel(AeArgs a) {
       const uint32_t c0 = ch << 6;
       const uint32_t e0 = ((c0 == lo ? base : pget(c0 - 1)) - base) & 0xFFFFu;
       const uint32_t ne = ((pget(c0 + 63) - base) & 0xFFFFu) - e0;  // the chunk's in-edges (wave-uniform)
+      // stale filter (as in ae_dense_apply_q_kernel)
+      const bool need = aln && (!filt || ((stile[ch] >> lane) & 1ull));
+      const bool totgt = filt && need && ((tgtb[(c0 >> 5) + (lane >> 5)] >> (lane & 31u)) & 1u);
 #pragma unroll
       for (uint32_t i = 0; i < L; ++i) sc[i * 64 + lane] = 0u;
       // every gather of the chunk is issued before any is used: own rows, the peers'
@@ -829,7 +864,7 @@ __global__ __launch_bounds__(kAeDThreads) void ae_dense_apply_kernel(AeArgs a) {
         for (uint32_t i = 0; i < L; ++i) {
           const uint32_t src = i * per + sub;
           const uint32_t pp = (uint32_t)__shfl((int)pj[j], (int)src, 64);
-          const bool go = __shfl((int)aln, (int)src, 64) && c < a.K;
+          const bool go = __shfl((int)(need && !totgt), (int)src, 64) && c < a.K;
           vp[j][i] = go ? V[(uint64_t)pp * a.K + c] : 0u;
         }
       }
@@ -866,6 +901,7 @@ __global__ __launch_bounds__(kAeDThreads) void ae_dense_apply_kernel(AeArgs a) {
 #pragma unroll
       for (uint32_t i = 0; i < L; ++i) {
         acc[i] = max(acc[i], sc[i * 64 + lane]);
+        if (__shfl((int)totgt, (int)(i * per + sub), 64) && c < a.K) acc[i] = tgt;
         const uint64_t node = nb + i * per + sub;
         const bool valid = node < a.N && c < a.K;
         if (valid) Vn[node * a.K + c] = acc[i];
@@ -916,6 +952,8 @@ __global__ __launch_bounds__(kAeQThreads) void ae_dense_apply_q_kernel(AeArgs a)
   __shared__ __align__(16) uint32_t scr[kW][64 * 16];
   __shared__ uint32_t wsum[kW], wpre[kW + 1], rng[3], cnt[64];
   __shared__ uint64_t red[kW];
+  __shared__ uint64_t stile[kAeDTile / 64];
+  __shared__ uint32_t tgtb[kAeDTile / 32];
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane >> 2, q = lane & 3;
   const uint32_t T = ae_tile_of(a.bnt);
   const uint64_t t0 = (uint64_t)T << kAeDTileLog;
@@ -923,7 +961,8 @@ __global__ __launch_bounds__(kAeQThreads) void ae_dense_apply_q_kernel(AeArgs a)
   const uint32_t* __restrict__ V = a.V;
   uint32_t* __restrict__ Vn = a.Vn;
   if (tid < 64) cnt[tid] = 0;
-  const AeSortSh sh{pos2, srt, nullptr, wsum, wpre, rng};
+  const bool filt = (a.flags & kAeSbValid) != 0;
+  const AeSortSh sh{pos2, srt, nullptr, wsum, wpre, rng, filt, stile, tgtb};
   ae_sort_count<kW>(a, sh, T);
   const uint4 tg = reinterpret_cast<const uint4*>(a.target)[q];
   const bool hashing = (a.flags & 1u) != 0;
@@ -944,6 +983,12 @@ __global__ __launch_bounds__(kAeQThreads) void ae_dense_apply_q_kernel(AeArgs a)
       const uint32_t c0 = ch << 6;
       const uint32_t e0 = ((c0 == lo ? base : ae_pget(sh, c0 - 1)) - base) & 0xFFFFu;
       const uint32_t ne = ((ae_pget(sh, c0 + 63) - base) & 0xFFFFu) - e0;  // the chunk's in-edges
+      // stale filter: an up-to-date node keeps its row (it is the target) and gathers nothing; a
+      // stale one takes the target outright from an alive up-to-date sender (tgtb).  (The peers'
+      // rows are gathered before their bits are known, so an up-to-date peer saves no traffic and
+      // is not probed for: its row is the target, and the max takes it.)
+      const bool need = aln && (!filt || ((stile[ch] >> lane) & 1ull));
+      const bool totgt = filt && need && ((tgtb[(c0 >> 5) + (lane >> 5)] >> (lane & 31u)) & 1u);
 #pragma unroll
       for (uint32_t g = 0; g < 4; ++g) reinterpret_cast<uint4*>(sc)[g * 64 + lane] = uint4{0, 0, 0, 0};
       // own rows, the peers' rows (alive bits awaited after), the first in-edge groups
@@ -967,13 +1012,11 @@ __global__ __launch_bounds__(kAeQThreads) void ae_dense_apply_q_kernel(AeArgs a)
         for (uint32_t g = 0; g < 4; ++g) {
           const uint32_t src = g * 16 + r;
           const uint32_t pp = (uint32_t)__shfl((int)pj[j], (int)src, 64);
-          const bool go = __shfl((int)aln, (int)src, 64);
+          const bool go = __shfl((int)(need && !totgt), (int)src, 64);
           vp[j][g] = go ? *row(pp) : uint4{0, 0, 0, 0};
         }
-      {
 #pragma unroll
-        for (uint32_t j = 0; j < KJ; ++j) exj[j] = aln && alive_bit(a.abn, pj[j]);
-      }
+      for (uint32_t j = 0; j < KJ; ++j) exj[j] = aln && alive_bit(a.abn, pj[j]);
       auto in_group = [&](uint32_t f0) {
         uint4 vi[kBQ];
         uint32_t ti[kBQ];
@@ -1011,6 +1054,7 @@ __global__ __launch_bounds__(kAeQThreads) void ae_dense_apply_q_kernel(AeArgs a)
       for (uint32_t g = 0; g < 4; ++g) {
         const uint32_t nr = g * 16 + r;
         o[g] = max4(o[g], reinterpret_cast<const uint4*>(sc)[nr * 4 + q]);
+        if (__shfl((int)totgt, (int)nr, 64)) o[g] = tg;
         const uint64_t node = nb + nr;
         const bool valid = node < a.N;
         if (valid) *reinterpret_cast<uint4*>(Vn + node * 16 + q * 4) = o[g];

@@ -711,10 +711,23 @@ __device__ __forceinline__ void for_each_run_record(const BinGeom& g, const uint
   uint64_t* wm = wmask_all + wave * U;
   int32_t* wl = wlist_all + wave * 64;
   const uint64_t below = (1ull << lane) - 1ull, upto = (2ull << lane) - 1ull;  // lane 63: 2 << 63 wraps to all ones
-  for (uint32_t s0 = (wave - w0) * 64; s0 < g.nt_s; s0 += nwaves * 64) {
+  // the next 64 runs' bounds load while this group's records are walked (one round trip less
+  // per group)
+  const uint32_t step = nwaves * 64;
+  uint32_t nbe = 0, nen = 0;
+  if ((wave - w0) * 64 < g.nt_s) {
+    const uint32_t sc = min((wave - w0) * 64 + lane, g.nt_s - 1);
+    nbe = rowb[sc];
+    nen = rowe[sc];
+  }
+  for (uint32_t s0 = (wave - w0) * 64; s0 < g.nt_s; s0 += step) {
     const uint32_t s = s0 + lane;
-    const uint32_t sc = min(s, g.nt_s - 1);
-    const uint32_t be0 = rowb[sc], en0 = rowe[sc];
+    const uint32_t be0 = nbe, en0 = nen;
+    if (s0 + step < g.nt_s) {
+      const uint32_t sc = min(s + step, g.nt_s - 1);
+      nbe = rowb[sc];
+      nen = rowe[sc];
+    }
     const uint32_t be = s < g.nt_s ? be0 : 0u, en = s < g.nt_s ? en0 : 0u;
     const uint32_t len = en - be;
     uint32_t inc = len;

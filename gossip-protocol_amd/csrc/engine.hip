@@ -106,6 +106,7 @@ struct gossip_engine {
   // ae_dbin = the engine's geometry fits, ae_dbin_on = gossip_set_param "ae_dense_bin"
   bool ae_dbin = false, ae_dbin_on = true;
   uint32_t ae_dcap = 0;  // gossip_set_param "ae_dense_cap" (tests: ranges, overflow fallback)
+  bool ae_dfilt = true;  // "ae_dense_filter": binned dense rounds skip exchanges that move no row (kAeSbValid)
   AeBinGeom ae_dg{};
   uint16_t* ae_dboff = nullptr;
   uint64_t ae_dense_fallbacks = 0;
@@ -739,6 +740,9 @@ int ae_round(gossip_engine* e) {
       d.bnt = e->ae_dg.nt;
       d.boff = e->ae_dboff;
       d.dcap = e->ae_dcap;
+      // stale filter (param ae_dense_filter) once a tenth of the nodes is up to date: before that it
+      // skips nothing and its checks cost
+      if (e->ae_sb_valid && e->ae_dfilt && (double)e->ae_stale < 0.9 * (double)e->N) d.flags |= kAeSbValid;
       if ((rc = timer_begin(e, 0))) return rc;
       HIP_OK(e, launch_ae_dense_binned(d, e->stream));
       if ((rc = timer_end(e, 0))) return rc;
@@ -1378,6 +1382,8 @@ int gossip_set_param(gossip_engine_t* e, const char* name, double v) {
   } else if (n == "ae_dense_bin") {
     if (v != 0 && v != 1) return e->fail(GOSSIP_EINVAL, "ae_dense_bin must be 0 or 1");
     e->ae_dbin_on = v != 0;
+  } else if (n == "ae_dense_filter") {
+    e->ae_dfilt = v != 0;
   } else if (n == "ae_dense_cap") {
     if (v < 0 || v > 65535) return e->fail(GOSSIP_EINVAL, "ae_dense_cap must be in [0, 65535] (0 = default)");
     e->ae_dcap = (uint32_t)v;

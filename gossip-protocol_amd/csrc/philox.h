@@ -97,6 +97,18 @@ __host__ __device__ __forceinline__ bool edge_lost(const Faults& f, const Reach&
 }
 
 // Rumor origins: stream tag 2.
+// ANTIENTROPY churn word of node n in round t: with fanout k <= 3 the last
+// word of the node's first peer draw x0 = Philox({n, t, 0, 0}) (peers use words 0 .. k-1), so
+// one cipher per node serves both; else Philox({n, t, 1, 0}).x (x0 unused)
+__host__ __device__ __forceinline__ uint32_t ae_churn_word(const u32x4& x0, uint32_t n, uint32_t t, uint32_t k,
+                                                           uint32_t k0, uint32_t k1) {
+  return k <= 3 ? x0.w : philox4x32_10(u32x4{n, t, 1u, 0u}, k0, k1).x;
+}
+// the first peer draw, computed only where ae_churn_word reads it
+__host__ __device__ __forceinline__ u32x4 ae_first_draw(uint32_t n, uint32_t t, uint32_t k, uint32_t k0, uint32_t k1) {
+  return k <= 3 ? philox4x32_10(u32x4{n, t, 0u, 0u}, k0, k1) : u32x4{0u, 0u, 0u, 0u};
+}
+
 __host__ __device__ __forceinline__ uint32_t origin_of(uint32_t r, uint64_t N, uint32_t k0, uint32_t k1) {
   const u32x4 x = philox4x32_10(u32x4{r, 0u, 2u, 0u}, k0, k1);
   return (uint32_t)(((uint64_t)x.x * N) >> 32);

@@ -90,7 +90,8 @@ struct oracle_sim {
   uint64_t *cc_bits, *cc_send, *cc_vals, cc_stride;
 };
 
-static inline int churned(int alive, uint32_t n, uint32_t t, const uint32_t key[2], uint32_t fail, uint32_t rec);
+static inline int churned(int alive, uint32_t n, uint32_t t, uint32_t k, const uint32_t key[2], uint32_t fail,
+                          uint32_t rec);
 static inline int alive_bit(const oracle_sim_t* s, uint64_t n);
 static void aex_own_fill_alive(oracle_sim_t* s);
 
@@ -439,7 +440,7 @@ int oracle_exchange_buffers(oracle_sim_t* s, void** send, void** recv, uint64_t*
       uint64_t* own = s->aex_img + (size_t)s->rank * s->Nl / 32;
       for (uint64_t i = 0; i < s->nown; ++i) {
         const uint64_t bit = 1ull << (i & 63), n = s->lo + i;
-        const int al = churned((own[2 * (i >> 6)] & bit) != 0, (uint32_t)n, s->t, key, s->cfg.churn_fail,
+        const int al = churned((own[2 * (i >> 6)] & bit) != 0, (uint32_t)n, s->t, s->k, key, s->cfg.churn_fail,
                                s->cfg.churn_recover);
         own[2 * (i >> 6)] = al ? own[2 * (i >> 6)] | bit : own[2 * (i >> 6)] & ~bit;
       }
@@ -479,11 +480,15 @@ static int in_sorted(const uint32_t* a, uint32_t len, uint32_t x) {
 
 /* One round S_t -> S_{t+1} for the owned nodes (Gossip, main.go:65-89, as a
  * synchronous round).  g = gathered exchange image (S_t or F_t). */
-/* Churn (Philox tag 1): the alive flag of node n after round t's churn. */
-static inline int churned(int alive, uint32_t n, uint32_t t, const uint32_t key[2], uint32_t fail, uint32_t rec) {
-  uint32_t ctr[4] = {n, t, 1u, 0u}, x[4];
+/* Churn: the alive flag of node n after round t's churn.  The draw is the last
+ * word of the node's first peer draw Philox({n, t, 0, 0}) for fanout k <= 3 (its words 0 .. k-1
+ * are the peers), else Philox({n, t, 1, 0})[0]. */
+static inline int churned(int alive, uint32_t n, uint32_t t, uint32_t k, const uint32_t key[2], uint32_t fail,
+                          uint32_t rec) {
+  uint32_t ctr[4] = {n, t, k <= 3 ? 0u : 1u, 0u}, x[4];
   oracle_philox4x32_10(ctr, key, x);
-  return alive ? !(x[0] < fail) : (x[0] < rec);
+  const uint32_t w = k <= 3 ? x[3] : x[0];
+  return alive ? !(w < fail) : (w < rec);
 }
 
 /* max-merge into a row word another thread may also be merging into (OpenMP rounds); max is
@@ -508,7 +513,7 @@ static int ae_round(oracle_sim_t* s, uint64_t* partial) {
   const uint32_t fail = s->cfg.churn_fail, rec = s->cfg.churn_recover;
   const int nt = s->threads, shared = nt > 1;
 #pragma omp parallel for num_threads(nt) if (nt > 1) schedule(static)
-  for (uint64_t n = 0; n < N; ++n) s->alive_n[n] = (uint8_t)churned(s->alive[n], (uint32_t)n, t, key, fail, rec);
+  for (uint64_t n = 0; n < N; ++n) s->alive_n[n] = (uint8_t)churned(s->alive[n], (uint32_t)n, t, k, key, fail, rec);
 #pragma omp parallel for num_threads(nt) if (nt > 1) schedule(static)
   for (uint64_t n = 0; n < N; ++n) memcpy(s->Vn + n * K, s->V + n * K, (size_t)K * 4);
   uint64_t msgs = 0;
@@ -1268,7 +1273,7 @@ int oracle_set_param(oracle_sim_t* s, const char* name, double value) {
   /* the engine's performance knobs (path choice, grids): no effect on the rounds' results */
   const char* known[] = {"alld_frac",  "filter_frac", "ahead",        "serve_grid",   "apply_grid", "push_waves",
                          "ae_sparse",  "ae_cap",      "sparse_direct", "mid_frac",    "ae_dense_bin", "ae_dense_cap",
-                         "ae_ahead",   "ordered_collectives"};
+                         "ae_ahead",   "ordered_collectives", "ae_dense_filter"};
   for (size_t i = 0; i < sizeof known / sizeof known[0]; ++i)
     if (!strcmp(name, known[i])) return GOSSIP_OK;
   return GOSSIP_EINVAL;

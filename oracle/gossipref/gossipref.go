@@ -17,7 +17,7 @@
 //   FloodSim (faults) flood_faults_round   one walk per (node, value) down Topology[node] in the message's order,
 //                                          head-of-line blocked by a lost attempt, stuck for good once StallRounds
 //                                          lost attempts expired the neighbour's context (main.go:72-87)
-//   AESim.Round     ae_round               gossip_oracle.c:355 (version-vector max-merge, Philox churn tag 1)
+//   AESim.Round     ae_round               gossip_oracle.c:355 (version-vector max-merge, Philox churn)
 //
 // Status in this image: no Go toolchain exists here or on the GPU box, so this
 // package has not been compiled or run ("go test" in this directory checks it
@@ -544,18 +544,22 @@ func (a *AESim) Inject(n uint64, c uint32) {
 	}
 }
 
-// Round: churn (Philox tag 1), then every exchange (n, p_j(n, t)) with both
+// Round: churn (the spare word of the first peer draw, Philox({n, t, 0, 0})[3], while
+// Fanout <= 3; else Philox({n, t, 1, 0})[0]), then every exchange (n, p_j(n, t)) with both
 // ends alive merges both S_t rows into both S_{t+1} rows.
 func (a *AESim) Round() RoundStats {
 	key := Key(a.Seed)
 	N, K := a.N, uint64(a.K)
 	alive := make([]bool, N)
 	for n := uint64(0); n < N; n++ {
-		x := Philox4x32_10([4]uint32{uint32(n), a.T, 1, 0}, key)
+		w := Philox4x32_10([4]uint32{uint32(n), a.T, 0, 0}, key)[3]
+		if a.Fanout > 3 {
+			w = Philox4x32_10([4]uint32{uint32(n), a.T, 1, 0}, key)[0]
+		}
 		if a.Alive[n] {
-			alive[n] = !(x[0] < a.Fail)
+			alive[n] = !(w < a.Fail)
 		} else {
-			alive[n] = x[0] < a.Rec
+			alive[n] = w < a.Rec
 		}
 	}
 	next := append([]uint32(nil), a.V...)

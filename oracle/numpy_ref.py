@@ -299,8 +299,9 @@ class Sim:
 class AntiEntropySim:
     """Version-vector anti-entropy with churn, unsharded, vectorised.
 
-    V[n, c] uint32; alive[n] bool.  Round t: churn by Philox tag 1 (x0 < fail
-    kills an alive node, x0 < recover revives a dead one), then over every edge
+    V[n, c] uint32; alive[n] bool.  Round t: churn by the word x = Philox({n, t, 0, 0})[3] for
+    fanout k <= 3 (the first peer draw's spare word), else Philox({n, t, 1, 0})[0] (x < fail
+    kills an alive node, x < recover revives a dead one), then over every edge
     (n, p_j(n, t)) with both ends alive, both ends take the elementwise max of
     the two S_t vectors.  Stats: alive count, alive nodes equal to the global
     max vector (constant between injections), per-component counts, hash.
@@ -328,7 +329,10 @@ class AntiEntropySim:
         N = self.N
         k0, k1 = self.seed & 0xFFFFFFFF, (self.seed >> 32) & 0xFFFFFFFF
         n = np.arange(N, dtype=np.uint32)
-        x0 = philox4x32_10(n, np.uint32(self.t), np.uint32(1), np.uint32(0), k0, k1)[0]
+        if self.k <= 3:
+            x0 = philox4x32_10(n, np.uint32(self.t), np.uint32(0), np.uint32(0), k0, k1)[3]
+        else:
+            x0 = philox4x32_10(n, np.uint32(self.t), np.uint32(1), np.uint32(0), k0, k1)[0]
         alive = np.where(self.alive, ~(x0 < np.uint32(self.fail)), x0 < np.uint32(self.rec))
         P = peers(self.seed, N, self.t, self.k).astype(np.int64)
         V = self.V

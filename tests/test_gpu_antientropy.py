@@ -3,7 +3,9 @@ bit-exact per round: stats, per-component counts, hash, and the rows and alive f
 
 Paths (all must agree with the oracle and with each other):
   auto     — dense rounds until the stale nodes are few, then sparse in-place rounds
-  dense    — ae_sparse = 0: every round dense (binned in-edge gathers, stats fused)
+  dense    — ae_sparse = 0: every round dense (binned in-edge gathers, stats fused; once the stale
+             bits are exact, exchanges that cannot move a row are skipped: the stale filter)
+  dense_nofilter — ae_dense_filter = 0: binned dense rounds gather every exchange's rows
   dense_atomic — ae_dense_bin = 0: dense rounds as pull pass + atomicMax push pass + stats pass
   dense_ranges — ae_dense_cap = 256: each tile's in-edges sorted in many LDS passes
   dense_fallback — ae_dense_cap = 16: every binned dense round overflows and is rerun atomically
@@ -28,6 +30,7 @@ THREADS = min(16, os.cpu_count() or 1)
 # (flags, gossip_set_param knobs) per path
 PATHS = {"auto": (0, {}), "dense": (0, {"ae_sparse": 0}), "sparse": (0, {"ae_sparse": 1}),
          "dense_atomic": (0, {"ae_sparse": 0, "ae_dense_bin": 0}),
+         "dense_nofilter": (0, {"ae_sparse": 0, "ae_dense_filter": 0}),
          "dense_ranges": (0, {"ae_sparse": 0, "ae_dense_cap": 256}),
          "dense_fallback": (0, {"ae_sparse": 0, "ae_dense_cap": 16}),
          "overflow": (0, {"ae_sparse": 1, "ae_cap": 64}),

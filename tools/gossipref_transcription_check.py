@@ -238,7 +238,8 @@ def ae_case(c):  # gossipref.AESim
     out = []
     for t in range(300):
         a2 = [(not x < fail) if al[n] else (x < rec) for n, x in
-              ((n, philox([n, t, 1, 0], key(seed))[0]) for n in range(N))]
+              ((n, philox([n, t, 0, 0], key(seed))[3] if k <= 3 else philox([n, t, 1, 0], key(seed))[0])
+               for n in range(N))]
         nx, msgs = V[:], 0
         for n in range(N):
             if not a2[n]:
