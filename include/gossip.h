@@ -154,7 +154,9 @@ int gossip_set_stream(gossip_engine_t* eng, void* hip_stream);
  *   "ae_dense_cap" ANTIENTROPY: in-edges per LDS pass of a binned dense round (0 = default
  *                  18432; smaller values split tiles into more passes, and a 64-node chunk
  *                  past it reruns the round with the atomicMax passes)
- *   "xd_shards"    sharded random modes: dense rounds run as exchange rounds (kind 3) when
+ *   "ae_dense_filter"  ANTIENTROPY: 1 binned dense rounds skip the exchanges that cannot move a
+ *                  row once fewer than 90 % of the nodes are stale (default), 0 gather them all
+ *   "xd_shards"   sharded random modes: dense rounds run as exchange rounds (kind 3) when
  *                  G >= this (default 6; 0 = never, always the state all-gather)
  *   "ae_ahead"     ANTIENTROPY, one engine: sparse rounds enqueued at once, each gated on the
  *                  device by the previous one (1..8, default 8; 1 = one round per host read)
