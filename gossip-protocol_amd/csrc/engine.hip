@@ -112,7 +112,7 @@ struct gossip_engine {
   uint64_t ae_dense_fallbacks = 0;
   uint64_t ae_cap = 0, ae_hash = 0, ae_stale = 0, ae_alive = 0, ae_full = 0;
   uint32_t ae_epoch = 0;
-  int ae_force = -1;             // GOSSIP_AE_SPARSE: -1 auto, 0 never, 1 whenever the bitmap is valid
+  int ae_force = -1;             // param "ae_sparse": -1 auto, 0 never, 1 whenever the bitmap is valid
   bool ae_sb_valid = false;      // the stale bits of alive, ae_hash and ae_stale describe V
   bool ae_sparse_last = false;   // the last round ran in place (V not rotated)
   uint64_t ae_sparse_rounds = 0, ae_overflows = 0;
