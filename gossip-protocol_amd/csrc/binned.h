@@ -24,6 +24,9 @@ constexpr uint32_t kMaxTilesD = 4096;     // tiles with sender values staged in 
 // Sharded dense rounds (sb_*): the pull pass stages no sender values, so its
 // tile counters cover the whole image (N <= kSbMaxTiles * kTileD = 2^27).
 constexpr uint32_t kSbMaxTiles = 8192;
+// one-shard rounds take the big regions (make_bin_geom(big)) past this many destination tiles
+// (2^24 nodes): the big emit costs more per sender, the walks gain more from longer runs
+constexpr uint32_t kBigFromTiles = 1024;
 
 // One emit pass of a sharded dense round: senders [snd0, snd0 + nsnd) (global
 // ids), edges whose peer lies in [dst0, dst0 + dstn), directions in dmask

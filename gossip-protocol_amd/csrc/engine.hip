@@ -1225,8 +1225,10 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
   bind_slices(e);
   if (e->mode != GOSSIP_MODE_FLOOD && e->mode != GOSSIP_MODE_ANTIENTROPY && !(cfg->flags & GOSSIP_FLAG_DIRECT) &&
       bin_path_ok(e->N, e->k, e->W, G)) {
-    // past kMaxTilesD tiles the emit regions double (longer runs per tile, binned.hip V = 4, 5)
-    e->bg = make_bin_geom(e->N, e->k, (e->N + kTileD - 1) / kTileD > kMaxTilesD);
+    // past kBigFromTiles tiles the emit regions double (longer runs per tile, binned.hip V = 4, 5):
+    // per dense round 2^25 nodes 1135 -> 1094 us, 2^26 2981 -> 2582 us; 2^24 slower (521 -> 583 us:
+    // its runs of 16 records gain less than the big emit costs), profiles/r04_s
+    e->bg = make_bin_geom(e->N, e->k, (e->N + kTileD - 1) / kTileD > kBigFromTiles);
     const size_t bytes = bin_bytes(e->bg);
     if (hipMalloc(&e->bin_mem, bytes) != hipSuccess) {
       e->err = "hipMalloc of " + std::to_string(bytes) + " bytes (bins) failed";
