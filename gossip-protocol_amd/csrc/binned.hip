@@ -37,7 +37,6 @@ constexpr uint32_t kEmitGrid = 256;  // one persistent emit block per CU (128 / 
 constexpr int kTileThreads = 1024;
 constexpr uint32_t kServeGrid = 256;  // persistent serve: one block per CU (the tile image takes 128 KiB of LDS)
 constexpr uint32_t kApplyGrid = 256;  // persistent apply, likewise
-constexpr int kUnroll = 16;  // records in flight per lane in the exchange rounds' run walkers (32 spills in K3)
 constexpr int kUnrollSeq = 8;  // records in flight per lane in the sequential response walker
 // push-pull apply: waves [0, push_waves) walk the pushes, the rest the responses
 // (BinGeom::push_waves, this default up to 2^25 nodes)
@@ -696,79 +695,13 @@ __device__ __forceinline__ void wave_sync() {
 // each load instruction reads consecutive records of a run).  The owner of a
 // record comes from a per-wave LDS bitmap of run starts in the window and a
 // list of the window's runs: rank = (run starts at or before it) - 1, one
-// popcount and one LDS read per record, no search.  fn(rec) receives the
+// popcount and one LDS read per record, no search.  load(rec) receives the
 // global record index s * rp + pos, or -1 past the end.
 // LDS per wave: wmask[U] u64, wlist[64] i32.  The walk is shared by the waves
 // [w0, w0 + nwaves) of the block (nwaves = 0: every wave).
-template <int U, typename F>
-__device__ __forceinline__ void for_each_run_record(const BinGeom& g, const uint16_t* rowb, const uint16_t* rowe,
-                                                    uint64_t* wmask_all, int32_t* wlist_all, F&& fn,
-                                                    uint32_t w0 = 0, uint32_t nwaves = 0) {
-  constexpr uint32_t kWin = 64 * U;
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (nwaves == 0) nwaves = blockDim.x >> 6;
-  uint64_t* wm = wmask_all + wave * U;
-  int32_t* wl = wlist_all + wave * 64;
-  const uint64_t below = (1ull << lane) - 1ull, upto = (2ull << lane) - 1ull;  // lane 63: 2 << 63 wraps to all ones
-  // the next 64 runs' bounds load while this group's records are walked (one round trip less
-  // per group)
-  const uint32_t step = nwaves * 64;
-  uint32_t nbe = 0, nen = 0;
-  if ((wave - w0) * 64 < g.nt_s) {
-    const uint32_t sc = min((wave - w0) * 64 + lane, g.nt_s - 1);
-    nbe = rowb[sc];
-    nen = rowe[sc];
-  }
-  for (uint32_t s0 = (wave - w0) * 64; s0 < g.nt_s; s0 += step) {
-    const uint32_t s = s0 + lane;
-    const uint32_t be0 = nbe, en0 = nen;
-    if (s0 + step < g.nt_s) {
-      const uint32_t sc = min(s + step, g.nt_s - 1);
-      nbe = rowb[sc];
-      nen = rowe[sc];
-    }
-    const uint32_t be = s < g.nt_s ? be0 : 0u, en = s < g.nt_s ? en0 : 0u;
-    const uint32_t len = en - be;
-    uint32_t inc = len;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(inc, o, 64);
-      if (lane >= (uint32_t)o) inc += y;
-    }
-    const uint32_t exc = inc - len;
-    const uint32_t total = __shfl(inc, 63, 64);
-    const int32_t basep = (int32_t)(s * g.rp + be - exc);  // record = basep(owner) + f (< 2^31)
-    for (uint32_t f0 = 0; f0 < total; f0 += kWin) {
-      if (lane < (uint32_t)U) wm[lane] = 0;
-      wave_sync();
-      // runs meeting this window, in order; a run begun in an earlier window marks position 0
-      const bool in = len != 0 && exc < f0 + kWin && exc + len > f0;
-      const uint64_t inm = __ballot(in);
-      if (in) {
-        const uint32_t pos = exc > f0 ? exc - f0 : 0u;
-        atomicOr((unsigned long long*)&wm[pos >> 6], 1ull << (pos & 63u));
-        wl[__popcll(inm & below)] = basep;
-      }
-      wave_sync();
-      int32_t rec[U];
-      uint32_t pre = 0;
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint64_t w = wm[u];
-        const uint32_t rank = pre + (uint32_t)__popcll(w & upto) - 1u;
-        pre += (uint32_t)__popcll(w);
-        const uint32_t f = f0 + u * 64 + lane;
-        rec[u] = f < total ? wl[rank & 63u] + (int32_t)f : -1;
-      }
-      wave_sync();  // the next window rewrites wm/wl
-      fn(rec);
-    }
-  }
-}
-
-// for_each_run_record, software-pipelined: load(rec) issues a window's loads into a Buf, and
-// proc(buf) consumes the previous window's, so one window's memory latency overlaps the
-// other's LDS work (a wave's loads retire in order: proc waits only for the older window)
+// Software-pipelined: load(rec) issues a window's loads into a Buf and proc(buf) consumes the
+// previous window's, so one window's memory latency overlaps the other's LDS work (a wave's
+// loads retire in order: proc waits only for the older window).
 template <int U, typename Buf, typename LD, typename PR>
 __device__ __forceinline__ void for_each_run_record_pipe(const BinGeom& g, const uint16_t* rowb, const uint16_t* rowe,
                                                          uint64_t* wmask_all, int32_t* wlist_all, LD&& load,
@@ -1557,7 +1490,7 @@ __global__ __launch_bounds__(kTileThreads) void xd_apply_kernel(XdGeom g, XdBufs
   __shared__ uint64_t red_hash[kTileThreads / 64];
   __shared__ uint32_t red_full[kTileThreads / 64];
   __shared__ uint32_t red_nz[kTileThreads / 64];
-  __shared__ uint64_t wmask[(kTileThreads / 64) * kUnroll];
+  __shared__ uint64_t wmask[(kTileThreads / 64) * kUnrollPipe];
   __shared__ int32_t wlist[(kTileThreads / 64) * 64];
   __shared__ uint32_t pl[kXdPref];  // the tile's sender regions: owner-run prefix rows (G + 1 each)
   __shared__ uint32_t po[kXdPref];  // and the runs' send positions (G each, stride G + 1)
