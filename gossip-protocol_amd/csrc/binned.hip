@@ -219,19 +219,22 @@ __device__ __forceinline__ uint32_t region_offsets_packed(uint32_t* cur, uint32_
 // this block has just streamed, so the reads hit L2.  V = 4: as V = 3 with regions
 // twice as large (up to 16384 senders, 32768 records; 16-bit tile counters packed in
 // pairs make the room), so the runs stay twice as long at N > 2^26; no next-region
-// prefetch (its registers).
+// prefetch (its registers).  V = 6, 7: the big regions of V = 4 for the sharded passes of
+// V = 1 (push, values written beside the u32 ids) and V = 2 (pull, no values); V = 8, 9: the
+// same with V = 5's peers kept between the passes (no faults, k <= 2).
 template <int KREG, bool FAULTS, int V>
 __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const uint64_t* __restrict__ S, BinBufs b,
                                                                   uint32_t R, uint32_t t, uint32_t key0,
                                                                   uint32_t key1, uint32_t mode, uint32_t filt,
                                                                   Faults fa, EmitRange er) {
-  constexpr bool SHARD = V == 1 || V == 2;
+  constexpr bool SHARD = V == 1 || V == 2 || V >= 6;
   constexpr bool STAGE = V == 0 || V == 1;  // sender values staged in LDS
-  constexpr bool BIG = V == 4 || V == 5;     // packed 16-bit tile counters, double regions
+  constexpr bool BIG = V >= 4;               // packed 16-bit tile counters, double regions
   // V = 5: BIG without faults, k <= 2 (the launch checks): the count pass keeps each sender's
   // peers and edge directions in the LDS staging room ({p0, p1, dirs} in a u64: p < 2^27), so
   // the placement pass draws no Philox again (one cipher per sender instead of two)
-  constexpr bool PKC = V == 5;
+  constexpr bool PKC = V == 5 || V == 8 || V == 9;
+  constexpr bool NOVALS = V == 7 || V == 9;  // the sharded pull pass writes no sender values
   constexpr uint32_t kMaxT = V >= 2 ? kSbMaxTiles : kMaxTilesD;
   constexpr uint32_t kMaxS = BIG ? 2 * kMaxSenders : kMaxSenders;
   __shared__ uint32_t cur[BIG ? kMaxT / 2 : kMaxT];
@@ -379,8 +382,8 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
           if (j >= g.k) break;
           const uint32_t p = peer_from_word(lane_of(x, j), nm1, n);
           uint32_t tl, pl;
-          tile_of(p, &tl, &pl);  // (one shard: always inside)
-          const uint32_t dd = peer_filter(d, p, filt, b.nzb, b.fullb);
+          const bool in = tile_of(p, &tl, &pl);  // (one shard: always inside)
+          const uint32_t dd = in ? peer_filter(d, p, filt, b.nzb, b.fullb) : 0u;
           if (!dd) continue;
           count_tile(tl);
           pk |= ((uint64_t)p << (27 * j)) | ((uint64_t)dd << (54 + 2 * j));
@@ -482,8 +485,8 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
   uint64_t* gvals = b.vals + (size_t)s * g.rp;
   uint16_t* gdst = b.dst + (size_t)s * g.rp;
   uint16_t* gsrc = b.src + (size_t)s * g.rp;
-  // the one-shard emits (BinGeom::split); V = 1, 2: sharded passes
-  constexpr bool split = V == 0 || V >= 3;
+  // the one-shard emits (BinGeom::split); V = 1, 2, 6, 7: sharded passes (u32 ids)
+  constexpr bool split = !SHARD;
   if constexpr (BIG) {
     // ids out first, then the region's sender values take the staging room and each
     // push is written packed {value, id} (BinGeom::aos), its value read from LDS: the
@@ -501,19 +504,27 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
         gids[e] = id;
       }
     }
-    __syncthreads();  // every staged id is out
-    uint64_t* sv = (uint64_t*)st_ids;  // 2 * kRecPerRegion u32 = kMaxS u64
-    // (V = 5 keeps v[] live through the count pass rather than rereading S here: 5.86 vs
-    // 5.98 ms per 2^27 dense round, profiles/r04_e/summary.txt)
+    if constexpr (!NOVALS) {
+      __syncthreads();  // every staged id is out
+      uint64_t* sv = (uint64_t*)st_ids;  // 2 * kRecPerRegion u32 = kMaxS u64
+      // (V = 5 keeps v[] live through the count pass rather than rereading S here: 5.86 vs
+      // 5.98 ms per 2^27 dense round, profiles/r04_e/summary.txt)
 #pragma unroll
-    for (uint32_t q = 0; q < kQ; ++q) sv[tid + q * kEmitThreads] = v[q];
-    __syncthreads();
-    uint32_t* gprec = b.prec + (size_t)s * g.rp * 3;
+      for (uint32_t q = 0; q < kQ; ++q) sv[tid + q * kEmitThreads] = v[q];
+      __syncthreads();
+      if constexpr (SHARD) {  // V = 6, 8: every value slot beside its u32 id (no holes)
 #pragma unroll 4
-    for (uint32_t e = tid; e < total; e += kEmitThreads) {
-      const uint32_t id = split ? id_of_pair(gdst[e], gsrc[e]) : gids[e];
-      const uint64_t x = sv[(id >> kTileDLog) & kIdNMask];  // (big regions always pack: g.aos)
-      prec_st(&gprec[3 * e], (uint32_t)x, (uint32_t)(x >> 32), id);
+        for (uint32_t e = tid; e < total; e += kEmitThreads)
+          rec_st(&gvals[e], sv[(gids[e] >> kTileDLog) & kIdNMask]);
+      } else {
+        uint32_t* gprec = b.prec + (size_t)s * g.rp * 3;
+#pragma unroll 4
+        for (uint32_t e = tid; e < total; e += kEmitThreads) {
+          const uint32_t id = split ? id_of_pair(gdst[e], gsrc[e]) : gids[e];
+          const uint64_t x = sv[(id >> kTileDLog) & kIdNMask];  // (one-shard big regions always pack: g.aos)
+          prec_st(&gprec[3 * e], (uint32_t)x, (uint32_t)(x >> 32), id);
+        }
+      }
     }
   } else
   for (uint32_t e = tid; e < total; e += kEmitThreads) {
@@ -1116,8 +1127,11 @@ SbGeom make_sb_geom(uint64_t N, uint32_t k, uint64_t lo, uint64_t nown) {
   SbGeom g{};
   g.lo = lo;
   g.nown = nown;
-  // region sizes as on one shard (make_bin_geom); peers are drawn over the global id space
-  g.p = g.q = make_bin_geom(N, k);
+  // region sizes as on one shard (make_bin_geom), big past 4096 image tiles: at 2^27 nodes runs
+  // of ~2 records become ~4 (dense round per rank 4.93 -> 4.14 ms at 2 x 2^26, 2.87 -> 2.56 ms at
+  // 4 x 2^25); with 2^26 or 2^25 image nodes the big emit costs more than that saves (4 x 2^24:
+  // 1.18 -> 1.23 ms; profiles/r04_ad).  Peers are drawn over the global id space.
+  g.p = g.q = make_bin_geom(N, k, (N + kTileD - 1) / kTileD > kMaxTilesD);
   g.p.split = g.q.split = 0u;
   g.p.aos = g.q.aos = 0u;  // (the sharded passes keep u32 ids + values)
   g.p.nt_s = (uint32_t)((N + g.p.ts - 1) / g.p.ts);      // every sender
@@ -1161,7 +1175,15 @@ void sb_emit(const BinGeom& gg, const BinBufs& bb, const uint64_t* image, uint32
   } else {                                                                \
     if (fa.any()) GOSSIP_EMIT(0, true, VV); else GOSSIP_EMIT(0, false, VV); \
   }
-  if (vals) {
+  if (gg.ts > kMaxSenders || gg.rp > kRecPerRegion) {  // big regions (make_sb_geom): V = 6-9
+    if (fa.any()) {
+      if (vals) GOSSIP_EMIT(0, true, 6); else GOSSIP_EMIT(0, true, 7);
+    } else if (gg.k <= 2) {
+      if (vals) GOSSIP_EMIT(0, false, 8); else GOSSIP_EMIT(0, false, 9);
+    } else {
+      if (vals) GOSSIP_EMIT(0, false, 6); else GOSSIP_EMIT(0, false, 7);
+    }
+  } else if (vals) {
     GOSSIP_EMIT_V(1)
   } else {
     GOSSIP_EMIT_V(2)

@@ -107,6 +107,29 @@ def test_lockstep_dense_past_4096_tiles():
             e.close()
 
 
+@pytest.mark.parametrize("k,faults", [(3, {}), (2, dict(edge_loss=1 << 29, partitions=3))], ids=["k3", "k2-faults"])
+def test_lockstep_dense_past_4096_tiles_big_regions(k, faults):
+    """Past 4096 image tiles the sharded dense round's passes take 16384-sender regions
+    (make_sb_geom; binned.hip emit V = 6, 7 with redrawn peers for k > 2 or faults; k <= 2
+    without faults keeps them, V = 8, 9: test_lockstep_dense_past_4096_tiles).  Two ragged shards
+    on the state all-gather, every round dense, against one engine."""
+    N, R, G = (1 << 26) + 12345, 64, 2
+    ref = Engine(N, R, "pushpull", k, 0x5EED0007, flags=1, **faults)
+    ref.inject_random()
+    want = ref.step(6)
+    full = ref.read_shard()
+    ref.close()
+    engines = [Engine(N, R, "pushpull", k, 0x5EED0007, flags=1, shard_rank=r, shard_count=G,
+                      params={"sparse_frac": -1, "xd_shards": 0, "cc_frac": 0}, **faults) for r in range(G)]
+    for e in engines:
+        e.inject_random()
+    got, kinds = run_lockstep(engines, 6)
+    assert got == want.stats and set(kinds) == {0}
+    for e in engines:
+        assert np.array_equal(e.read_shard(), full[:, e.lo:e.hi])
+        e.close()
+
+
 @pytest.mark.parametrize("plan", [({"xd_shards": 2, "sparse_frac": -1}, 3),
                                   ({"xd_shards": 0, "sparse_frac": -1, "cc_frac": 1}, 4)], ids=["exchange", "classcoded"])
 @pytest.mark.parametrize("faults", [dict(edge_loss=1 << 29, partitions=3), dict(edge_loss=1 << 29, stall_rounds=2),
