@@ -837,7 +837,9 @@ __device__ __forceinline__ void push_walk(const BinGeom& g, const BinBufs& b, ui
       const uint32_t id = SPLIT && !aos ? id_of_dst(bf.id[u]) : bf.id[u];
       const uint64_t v = bf.rec[u] < 0 || (id & VZ) ? 0ull : bf.v[u];
       const uint32_t p = id & (kTileD - 1);
-      if (v && (v & ~acc[p])) atomicOr(&acc[p], (unsigned long long)v);
+      // no read-before-OR: the LDS read's latency stalled the wave (0.7 % of the 2^27 dense round,
+      // profiles/r04_ag)
+      if (v) atomicOr(&acc[p], (unsigned long long)v);
     }
   }, 0u, nwaves);
 }
@@ -988,7 +990,7 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
           // a full sender's slot was never written this round (K2 skips it)
           if (p0 + u * qnt + qtid >= total || (id[u] & kIdVF)) continue;
           const uint32_t node = nb + ((id[u] >> kTileDLog) & kIdNMask);
-          if (r[u] & ~acc[node]) atomicOr(&acc[node], (unsigned long long)r[u]);
+          if (r[u]) atomicOr(&acc[node], (unsigned long long)r[u]);
         }
       }
     }
@@ -1570,7 +1572,7 @@ __global__ __launch_bounds__(kTileThreads) void xd_apply_kernel(XdGeom g, XdBufs
           for (int u = 0; u < kUnrollXd; ++u) {
             if (f0 + u * qnt + qtid >= total) continue;
             const uint32_t node = nb + nl[u];
-            if (rv[u] & ~acc[node]) atomicOr(&acc[node], (unsigned long long)rv[u]);
+            if (rv[u]) atomicOr(&acc[node], (unsigned long long)rv[u]);
           }
         }
       }
