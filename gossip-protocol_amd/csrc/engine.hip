@@ -208,6 +208,7 @@ struct gossip_engine {
   uint64_t* cc_vals = nullptr;  // [G][stride] the shards' mixed words
   uint64_t cc_vals_cap = 0, cc_stride = 0;
   uint64_t* sx_host = nullptr;  // pinned: [G + 2] counts / list bases
+  uint64_t* pub_d = nullptr;    // device values for device-side collectives (gossip_*_dev): [G] counts, [1] count, partials
 
   hipEvent_t ev[kTimers][2] = {};
   double time_ms[kTimers] = {};
@@ -269,6 +270,7 @@ void free_all(gossip_engine* e) {
   for (void* b : sx)
     if (b) (void)hipFree(b);
   if (e->sx_host) (void)hipHostFree(e->sx_host);
+  if (e->pub_d) (void)hipFree(e->pub_d);
   if (e->ae_aux_alias) e->ae_aux = e->ae_aux_h = nullptr;  // inside partial_d / partial_h
   void* ae[] = {e->V, e->Vn, e->target, e->alive, e->alive_n, e->ae_aux, e->ae_claim, e->ae_eid, e->ae_erow, e->ae_segn, e->ae_pmask,
                 e->ae_brec, e->ae_boff, e->ae_dboff, e->aex_img, e->aex_cnt, e->aex_boff, e->aex_bcnt, e->aex_req, e->aex_loc,
@@ -1591,6 +1593,31 @@ int gossip_dense_prepare(gossip_engine_t* e) {
   return GOSSIP_OK;
 }
 
+namespace {
+// --- device values for device-side collectives (the gossip_*_dev calls) ---
+// pub_d: [0, G) per-rank counts, [G] one count, [G + 2, G + 2 + part_len) partials.
+int pub_alloc(gossip_engine* e) {
+  if (e->pub_d) return GOSSIP_OK;
+  HIP_OK(e, hipMalloc((void**)&e->pub_d, (e->G + 2 + part_len(e)) * 8));
+  return GOSSIP_OK;
+}
+uint64_t* pub_counts(gossip_engine* e) { return e->pub_d; }
+uint64_t* pub_count(gossip_engine* e) { return e->pub_d + e->G; }
+uint64_t* pub_partial(gossip_engine* e) { return e->pub_d + e->G + 2; }
+// the own partials with the node count in slot 1 (what copy_partial_out hands the host)
+int pub_partial_out(gossip_engine* e) {
+  HIP_OK(e, launch_publish(e->partial_d, nullptr, pub_partial(e), (uint32_t)part_len(e), 1, e->nown, e->stream));
+  return GOSSIP_OK;
+}
+// A published value is ready for work enqueued later on the engine's stream; a caller whose
+// collectives run elsewhere gets it after a sync.  Timing (probe) mode syncs and folds the timers.
+int pub_ready(gossip_engine* e, bool collect, bool count = true) {
+  if (e->timing || (!e->driven && !e->ordered)) HIP_OK(e, hipStreamSynchronize(e->stream));
+  if (e->timing && collect) return timer_collect(e, count);
+  return GOSSIP_OK;
+}
+}  // namespace
+
 int gossip_round_compute(gossip_engine_t* e, uint64_t* partial) {
   if (!e || !partial) return GOSSIP_EINVAL;
   if (e->aex) return e->fail(GOSSIP_ESTATE, "sharded ANTIENTROPY rounds run through the gossip_ae_* calls");
@@ -1604,6 +1631,21 @@ int gossip_round_compute(gossip_engine_t* e, uint64_t* partial) {
   if (e->mode != GOSSIP_MODE_ANTIENTROPY) partial[1] = e->nown;
   else partial[3] = (e->cfg.flags & GOSSIP_FLAG_HASH) ? e->ae_hash : 0;
   e->last_sparse = false;
+  return GOSSIP_OK;
+}
+
+int gossip_round_compute_dev(gossip_engine_t* e, const uint64_t** partial) {
+  if (!e || !partial) return GOSSIP_EINVAL;
+  if (e->aex || e->mode == GOSSIP_MODE_ANTIENTROPY)
+    return e->fail(GOSSIP_ENOTSUP, "ANTIENTROPY partials are finished on the host: gossip_round_compute");
+  if (e->mode == GOSSIP_MODE_FLOOD && !e->has_topo) return e->fail(GOSSIP_ESTATE, "FLOOD needs a topology");
+  if (int rc = set_dev(e)) return rc;
+  if (int rc = pub_alloc(e)) return rc;
+  if (int rc = compute_round(e, current_image(e))) return rc;
+  if (int rc = pub_partial_out(e)) return rc;
+  if (int rc = pub_ready(e, true)) return rc;
+  e->last_sparse = false;
+  *partial = pub_partial(e);
   return GOSSIP_OK;
 }
 
@@ -1723,11 +1765,25 @@ int gossip_sparse_rare(gossip_engine_t* e, void** send, uint64_t* count) {
   if (int rc = sx_check(e, true)) return rc;
   if (int rc = sx_prepare(e)) return rc;
   HIP_OK(e, sx_compact(e->sg, e->sb, e->lf, e->S, e->sx_maj, e->stream));
-  const uint64_t nwl = (e->nown + 63) / 64;
+  const uint64_t nwl = (e->nown + 63) / 64;  // (the count: the word after the per-word bases)
   e->sx_host[0] = 0;
   HIP_OK(e, hipMemcpyAsync(e->sx_host, e->sb.wpos + nwl, 4, hipMemcpyDeviceToHost, e->stream));
   HIP_OK(e, hipStreamSynchronize(e->stream));
   *count = e->sx_host[0] & 0xFFFFFFFFull;
+  *send = e->sb.rare_send;
+  return GOSSIP_OK;
+}
+
+int gossip_sparse_rare_dev(gossip_engine_t* e, void** send, const uint64_t** count) {
+  if (!send || !count) return GOSSIP_EINVAL;
+  if (int rc = sx_check(e, true)) return rc;
+  if (int rc = pub_alloc(e)) return rc;
+  if (int rc = sx_prepare(e)) return rc;
+  HIP_OK(e, sx_compact(e->sg, e->sb, e->lf, e->S, e->sx_maj, e->stream));
+  const uint64_t nwl = (e->nown + 63) / 64;
+  HIP_OK(e, launch_publish(nullptr, e->sb.wpos + nwl, pub_count(e), 1, -1, 0, e->stream));
+  if (int rc = pub_ready(e, false)) return rc;
+  *count = pub_count(e);
   *send = e->sb.rare_send;
   return GOSSIP_OK;
 }
@@ -1742,9 +1798,9 @@ int gossip_sparse_rare_recv(gossip_engine_t* e, uint64_t stride, void** recv) {
   return GOSSIP_OK;
 }
 
-int gossip_sparse_scan(gossip_engine_t* e, const uint64_t* counts, void** send, uint64_t* send_counts) {
-  if (!counts || !send || !send_counts) return GOSSIP_EINVAL;
-  if (int rc = sx_check(e, true)) return rc;
+namespace {
+// the rare lists' bases, the index and the scan (the per-owner counts land in sb.msg_cnt)
+int sparse_scan_enqueue(gossip_engine* e, const uint64_t* counts) {
   if (!e->rare_recv) return e->fail(GOSSIP_ESTATE, "gossip_sparse_rare_recv first");
   uint64_t* cb = e->sx_host;
   cb[0] = 0;
@@ -1758,12 +1814,33 @@ int gossip_sparse_scan(gossip_engine_t* e, const uint64_t* counts, void** send, 
   HIP_OK(e, sx_index(e->sg, e->sb, e->rare_recv, e->sx_stride, rare, e->stream, e->sx_mid));
   HIP_OK(e, sx_scan(e->sg, e->sb, e->lf, e->S, e->rare_recv, e->sx_stride, rare, e->t, e->key0, e->key1, e->mode,
                     e->sx_maj, e->sx_alld, e->fa, e->stream, e->sx_mid));
-  if (int rc = timer_end(e, 0)) return rc;
+  return timer_end(e, 0);
+}
+}  // namespace
+
+int gossip_sparse_scan(gossip_engine_t* e, const uint64_t* counts, void** send, uint64_t* send_counts) {
+  if (!counts || !send || !send_counts) return GOSSIP_EINVAL;
+  if (int rc = sx_check(e, true)) return rc;
+  if (int rc = sparse_scan_enqueue(e, counts)) return rc;
   // (the copy below lands in cb's pinned buffer after the copy that read it: same stream)
   HIP_OK(e, hipMemcpyAsync(e->sx_host, e->sb.msg_cnt, (e->G + 1) * 4, hipMemcpyDeviceToHost, e->stream));
   HIP_OK(e, hipStreamSynchronize(e->stream));
   const uint32_t* c = (const uint32_t*)e->sx_host;
   for (uint32_t q = 0; q < e->G; ++q) send_counts[q] = c[q];
+  *send = e->sb.msg_out;
+  return GOSSIP_OK;
+}
+
+int gossip_sparse_scan_dev(gossip_engine_t* e, const uint64_t* counts, void** send, const uint64_t** send_counts) {
+  if (!counts || !send || !send_counts) return GOSSIP_EINVAL;
+  if (int rc = sx_check(e, true)) return rc;
+  if (int rc = pub_alloc(e)) return rc;
+  // (the bases' host-to-device copy reads sx_host: the caller's next host read of a device value
+  // syncs the stream before sx_host is written again)
+  if (int rc = sparse_scan_enqueue(e, counts)) return rc;
+  HIP_OK(e, launch_publish(nullptr, e->sb.msg_cnt, pub_counts(e), e->G, -1, 0, e->stream));
+  if (int rc = pub_ready(e, false)) return rc;
+  *send_counts = pub_counts(e);
   *send = e->sb.msg_out;
   return GOSSIP_OK;
 }
@@ -1776,19 +1853,38 @@ int gossip_sparse_msg_recv(gossip_engine_t* e, uint64_t items, void** recv) {
   return GOSSIP_OK;
 }
 
-int gossip_sparse_commit(gossip_engine_t* e, uint64_t items, uint64_t* partial) {
-  if (!partial) return GOSSIP_EINVAL;
-  if (int rc = sx_check(e, true)) return rc;
+namespace {
+int sparse_commit_enqueue(gossip_engine* e, uint64_t items) {
   if (items > e->msg_recv_cap) return e->fail(GOSSIP_EINVAL, "more messages than the receive buffer holds");
   if (int rc = timer_begin(e, 1)) return rc;
   HIP_OK(e, sx_apply(e->lf, e->msg_recv, items, e->sx_alld, e->stream));
   HIP_OK(e, launch_frontier_commit(e->lf, e->S, e->nown, e->partial_d, e->R, e->sx_alld ? kSparseAllD : kSparseFlags,
                                    e->cfg.flags, e->stream));
-  if (int rc = timer_end(e, 1)) return rc;
+  return timer_end(e, 1);
+}
+}  // namespace
+
+int gossip_sparse_commit(gossip_engine_t* e, uint64_t items, uint64_t* partial) {
+  if (!partial) return GOSSIP_EINVAL;
+  if (int rc = sx_check(e, true)) return rc;
+  if (int rc = sparse_commit_enqueue(e, items)) return rc;
   if (int rc = copy_partial_out(e, partial)) return rc;
   if (int rc = timer_collect(e)) return rc;
   e->sx_planned = false;
   e->last_sparse = true;
+  return GOSSIP_OK;
+}
+
+int gossip_sparse_commit_dev(gossip_engine_t* e, uint64_t items, const uint64_t** partial) {
+  if (!partial) return GOSSIP_EINVAL;
+  if (int rc = sx_check(e, true)) return rc;
+  if (int rc = pub_alloc(e)) return rc;
+  if (int rc = sparse_commit_enqueue(e, items)) return rc;
+  if (int rc = pub_partial_out(e)) return rc;
+  if (int rc = pub_ready(e, true)) return rc;
+  e->sx_planned = false;
+  e->last_sparse = true;
+  *partial = pub_partial(e);
   return GOSSIP_OK;
 }
 
@@ -1896,9 +1992,8 @@ int gossip_xd_classes(gossip_engine_t* e, void** send, void** image, uint64_t* b
   return GOSSIP_OK;
 }
 
-int gossip_xd_requests(gossip_engine_t* e, void** ids, void** vals, uint64_t* send_counts) {
-  if (!ids || !vals || !send_counts) return GOSSIP_EINVAL;
-  if (int rc = xd_check(e)) return rc;
+namespace {
+int xd_requests_enqueue(gossip_engine* e) {
   // a filtering round reads the gathered bitmaps: without gossip_xd_classes it runs unfiltered
   // (the filter only drops edges that move nothing, so either way the round is the same)
   const XdFilter xf{e->xd_cls, (uint32_t)((e->Nl + 63) / 64), e->xd_cls_ok ? e->xd_filt : 0u, e->xd_keep};
@@ -1913,11 +2008,31 @@ int gossip_xd_requests(gossip_engine_t* e, void** ids, void** vals, uint64_t* se
   HIP_OK(e, hipMemsetAsync(e->partial_d, 0, part_len(e) * 8, e->stream));
   if (int rc = timer_begin(e, 0)) return rc;
   HIP_OK(e, launch_xd_requests(e->xg, e->xb, e->S, e->R, e->t, e->key0, e->key1, e->mode, e->fa, xf, e->stream));
-  if (int rc = timer_end(e, 0)) return rc;
+  return timer_end(e, 0);
+}
+}  // namespace
+
+int gossip_xd_requests(gossip_engine_t* e, void** ids, void** vals, uint64_t* send_counts) {
+  if (!ids || !vals || !send_counts) return GOSSIP_EINVAL;
+  if (int rc = xd_check(e)) return rc;
+  if (int rc = xd_requests_enqueue(e)) return rc;
   HIP_OK(e, hipMemcpyAsync(e->xd_cnt_h, e->xb.ocnt, e->G * 4, hipMemcpyDeviceToHost, e->stream));
   HIP_OK(e, hipStreamSynchronize(e->stream));
   if (int rc = timer_collect(e, false)) return rc;
   for (uint32_t q = 0; q < e->G; ++q) send_counts[q] = e->xd_cnt_h[q];
+  *ids = e->xb.sid;
+  *vals = e->xb.sval;
+  return GOSSIP_OK;
+}
+
+int gossip_xd_requests_dev(gossip_engine_t* e, void** ids, void** vals, const uint64_t** send_counts) {
+  if (!ids || !vals || !send_counts) return GOSSIP_EINVAL;
+  if (int rc = xd_check(e)) return rc;
+  if (int rc = pub_alloc(e)) return rc;
+  if (int rc = xd_requests_enqueue(e)) return rc;
+  HIP_OK(e, launch_publish(nullptr, e->xb.ocnt, pub_counts(e), e->G, -1, 0, e->stream));
+  if (int rc = pub_ready(e, true, false)) return rc;
+  *send_counts = pub_counts(e);
   *ids = e->xb.sid;
   *vals = e->xb.sval;
   return GOSSIP_OK;
@@ -1968,19 +2083,40 @@ int gossip_xd_response_recv(gossip_engine_t* e, void** replies) {
   return GOSSIP_OK;
 }
 
-int gossip_xd_finish(gossip_engine_t* e, uint64_t* partial) {
-  if (!partial) return GOSSIP_EINVAL;
-  if (int rc = xd_check(e)) return rc;
+namespace {
+int xd_finish_enqueue(gossip_engine* e) {
   if (!e->xd_smem || !e->xd_rmem) return e->fail(GOSSIP_ESTATE, "gossip_xd_finish before the exchange");
   if (int rc = timer_begin(e, 0)) return rc;
   HIP_OK(e, launch_xd_apply(e->xg, e->xb, e->S, e->Snext, e->xd_nin, e->partial_d, e->R, e->mode, e->cfg.flags,
                             e->lf.nzb, e->lf.fullb, e->stream));
-  if (int rc = timer_end(e, 0)) return rc;
-  if (int rc = copy_partial_out(e, partial)) return rc;
-  if (int rc = timer_collect(e)) return rc;
+  return timer_end(e, 0);
+}
+void xd_finished(gossip_engine* e) {
   e->sx_valid = true;  // totals of the own nodes and exact bitmaps of S_{t+1}, fused into the apply
   e->xd_planned = e->xd_cls_ok = false;
   e->last_sparse = false;
+}
+}  // namespace
+
+int gossip_xd_finish(gossip_engine_t* e, uint64_t* partial) {
+  if (!partial) return GOSSIP_EINVAL;
+  if (int rc = xd_check(e)) return rc;
+  if (int rc = xd_finish_enqueue(e)) return rc;
+  if (int rc = copy_partial_out(e, partial)) return rc;
+  if (int rc = timer_collect(e)) return rc;
+  xd_finished(e);
+  return GOSSIP_OK;
+}
+
+int gossip_xd_finish_dev(gossip_engine_t* e, const uint64_t** partial) {
+  if (!partial) return GOSSIP_EINVAL;
+  if (int rc = xd_check(e)) return rc;
+  if (int rc = pub_alloc(e)) return rc;
+  if (int rc = xd_finish_enqueue(e)) return rc;
+  if (int rc = pub_partial_out(e)) return rc;
+  if (int rc = pub_ready(e, true)) return rc;
+  xd_finished(e);
+  *partial = pub_partial(e);
   return GOSSIP_OK;
 }
 

@@ -52,5 +52,9 @@ hipError_t launch_inject(uint64_t* S, uint64_t Nl, uint64_t lo, uint64_t hi, uin
 hipError_t launch_hash(const uint64_t* S, uint64_t Nl, uint64_t nown, uint32_t W, uint64_t N, uint64_t lo,
                        uint64_t* out, hipStream_t st);
 hipError_t launch_philox(const uint32_t* ctr, uint32_t k0, uint32_t k1, uint32_t* out, uint32_t n, hipStream_t st);
+// Small values a sharded round hands to a device-side collective (counts, partials):
+// out[i] = in64[i] or in32[i] (widened) for i < n, then out[slot] = value when slot >= 0.
+hipError_t launch_publish(const uint64_t* in64, const uint32_t* in32, uint64_t* out, uint32_t n, int32_t slot,
+                          uint64_t value, hipStream_t st);
 
 }  // namespace gossip

@@ -393,6 +393,19 @@ hipError_t launch_stall_update(uint8_t* stall, uint64_t N, uint32_t k, uint32_t 
   return hipGetLastError();
 }
 
+__global__ void publish_kernel(const uint64_t* __restrict__ in64, const uint32_t* __restrict__ in32,
+                               uint64_t* __restrict__ out, uint32_t n, int32_t slot, uint64_t value) {
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) out[i] = in64 ? in64[i] : (uint64_t)in32[i];
+  __syncthreads();
+  if (slot >= 0 && threadIdx.x == 0) out[slot] = value;
+}
+
+hipError_t launch_publish(const uint64_t* in64, const uint32_t* in32, uint64_t* out, uint32_t n, int32_t slot,
+                          uint64_t value, hipStream_t st) {
+  publish_kernel<<<1, 256, 0, st>>>(in64, in32, out, n, slot, value);
+  return hipGetLastError();
+}
+
 hipError_t launch_stats(const RoundArgs& a, hipStream_t st) {
   stats_kernel<<<grid_for(a.nown, 2048), kBlock, a.W * 64 * sizeof(uint32_t), st>>>(a);
   return hipGetLastError();

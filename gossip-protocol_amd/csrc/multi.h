@@ -68,11 +68,25 @@ class Transport {
   virtual int all_reduce_sum_u64(const std::vector<std::vector<uint64_t>>& mine, std::vector<uint64_t>* sum) = 0;
   virtual int all_reduce_max_u32(const std::vector<std::vector<uint32_t>>& mine, std::vector<uint32_t>* mx) = 0;
 
+  // Device-resident values (the engines' gossip_*_dev outputs, uint64, ready on their streams):
+  // the collective reads engine memory and one host read returns its result.  The defaults
+  // read the values to the host and run the host forms above.
+  // one[i]: engine i's value -> all[r] = rank r's
+  virtual int all_gather_dev(const std::vector<const uint64_t*>& one, std::vector<uint64_t>* all);
+  // cnt[i]: G values (items engine i sends to rank q) -> sendc[i] (those, on the host), recvc[i]
+  virtual int all_to_all_counts_dev(const std::vector<const uint64_t*>& cnt, std::vector<std::vector<uint64_t>>* sendc,
+                                    std::vector<std::vector<uint64_t>>* recvc);
+  // part[i]: n values of engine i -> their sum over every rank
+  virtual int all_reduce_sum_dev(const std::vector<const uint64_t*>& part, size_t n, std::vector<uint64_t>* sum);
+
  protected:
   int fail(int rc, const std::string& msg) {
     err_ = msg;
     return rc;
   }
+  // out[i] = the n values at p[i] (engine i's memory), after its stream has produced them
+  int read_dev(const std::vector<const uint64_t*>& p, size_t n, std::vector<std::vector<uint64_t>>* out);
+  virtual const std::vector<gossip_engine_t*>& engines() const = 0;
   std::string err_;
 };
 

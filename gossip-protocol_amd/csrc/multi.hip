@@ -82,6 +82,41 @@ Rccl& rccl() {
     if (e_ != hipSuccess) return fail(GOSSIP_EHIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
   } while (0)
 
+}  // namespace
+
+int Transport::read_dev(const std::vector<const uint64_t*>& p, size_t n, std::vector<std::vector<uint64_t>>* out) {
+  const std::vector<gossip_engine_t*>& eng = engines();
+  out->assign(eng.size(), std::vector<uint64_t>(n, 0));
+  for (size_t i = 0; i < eng.size(); ++i) {
+    HIPT_OK(hipSetDevice(engine_device(eng[i])));
+    HIPT_OK(hipMemcpyAsync((*out)[i].data(), p[i], n * 8, hipMemcpyDeviceToHost, engine_stream(eng[i])));
+    HIPT_OK(hipStreamSynchronize(engine_stream(eng[i])));
+  }
+  return GOSSIP_OK;
+}
+
+int Transport::all_gather_dev(const std::vector<const uint64_t*>& one, std::vector<uint64_t>* all) {
+  std::vector<std::vector<uint64_t>> v;
+  if (int rc = read_dev(one, 1, &v)) return rc;
+  std::vector<uint64_t> mine(v.size());
+  for (size_t i = 0; i < v.size(); ++i) mine[i] = v[i][0];
+  return all_gather_u64(mine, all);
+}
+
+int Transport::all_to_all_counts_dev(const std::vector<const uint64_t*>& cnt, std::vector<std::vector<uint64_t>>* sendc,
+                                     std::vector<std::vector<uint64_t>>* recvc) {
+  if (int rc = read_dev(cnt, engine_shards(engines()[0]), sendc)) return rc;
+  return all_to_all_counts(*sendc, recvc);
+}
+
+int Transport::all_reduce_sum_dev(const std::vector<const uint64_t*>& part, size_t n, std::vector<uint64_t>* sum) {
+  std::vector<std::vector<uint64_t>> v;
+  if (int rc = read_dev(part, n, &v)) return rc;
+  return all_reduce_sum_u64(v, sum);
+}
+
+namespace {
+
 std::vector<uint64_t> prefix(const std::vector<uint64_t>& c) {
   std::vector<uint64_t> o(c.size() + 1, 0);
   for (size_t q = 0; q < c.size(); ++q) o[q + 1] = o[q] + c[q];
@@ -105,8 +140,10 @@ class RcclTransport final : public Transport {
       if (scratch_.size() > i && scratch_[i]) (void)hipFree(scratch_[i]);
       (void)R.CommDestroy(comm_[i]);
     }
+    if (host_) (void)hipHostFree(host_);
   }
   int32_t kind() const override { return 1; }
+  const std::vector<gossip_engine_t*>& engines() const override { return eng_; }
 
   int all_gather_start(const std::vector<void*>& recv, const std::vector<const void*>& send, size_t bytes) override {
     if (bytes == 0) return GOSSIP_OK;
@@ -269,7 +306,80 @@ class RcclTransport final : public Transport {
     return sync_all();
   }
 
+  // the device-value forms: RCCL reads engine memory, one pinned host read per local engine
+  int all_gather_dev(const std::vector<const uint64_t*>& one, std::vector<uint64_t>* all) override {
+    if (int rc = scratch(G_ * 8)) return rc;
+    if (int rc = pinned(G_ * 8)) return rc;
+    RCCL_OK(R.GroupStart());
+    for (size_t i = 0; i < eng_.size(); ++i) {
+      HIPT_OK(hipSetDevice(engine_device(eng_[i])));
+      RCCL_OK(R.AllGather(one[i], scratch_[i], 1, ncclUint64, comm_[i], engine_stream(eng_[i])));
+    }
+    RCCL_OK(R.GroupEnd());
+    HIPT_OK(hipSetDevice(engine_device(eng_[0])));
+    HIPT_OK(hipMemcpyAsync(host_, scratch_[0], G_ * 8, hipMemcpyDeviceToHost, engine_stream(eng_[0])));
+    HIPT_OK(hipStreamSynchronize(engine_stream(eng_[0])));
+    all->assign(host_, host_ + G_);
+    return GOSSIP_OK;
+  }
+
+  int all_to_all_counts_dev(const std::vector<const uint64_t*>& cnt, std::vector<std::vector<uint64_t>>* sendc,
+                            std::vector<std::vector<uint64_t>>* recvc) override {
+    if (int rc = scratch(G_ * 8)) return rc;
+    if (int rc = pinned(eng_.size() * 2 * G_ * 8)) return rc;
+    RCCL_OK(R.GroupStart());  // one value to and from every rank, the own one included
+    for (size_t i = 0; i < eng_.size(); ++i) {
+      HIPT_OK(hipSetDevice(engine_device(eng_[i])));
+      for (uint32_t q = 0; q < G_; ++q) {
+        RCCL_OK(R.Send(cnt[i] + q, 1, ncclUint64, (int)q, comm_[i], engine_stream(eng_[i])));
+        RCCL_OK(R.Recv((uint64_t*)scratch_[i] + q, 1, ncclUint64, (int)q, comm_[i], engine_stream(eng_[i])));
+      }
+    }
+    RCCL_OK(R.GroupEnd());
+    for (size_t i = 0; i < eng_.size(); ++i) {
+      HIPT_OK(hipSetDevice(engine_device(eng_[i])));
+      uint64_t* h = host_ + i * 2 * G_;
+      HIPT_OK(hipMemcpyAsync(h, cnt[i], G_ * 8, hipMemcpyDeviceToHost, engine_stream(eng_[i])));
+      HIPT_OK(hipMemcpyAsync(h + G_, scratch_[i], G_ * 8, hipMemcpyDeviceToHost, engine_stream(eng_[i])));
+    }
+    if (int rc = sync_all()) return rc;
+    sendc->assign(eng_.size(), {});
+    recvc->assign(eng_.size(), {});
+    for (size_t i = 0; i < eng_.size(); ++i) {
+      const uint64_t* h = host_ + i * 2 * G_;
+      (*sendc)[i].assign(h, h + G_);
+      (*recvc)[i].assign(h + G_, h + 2 * G_);
+    }
+    return GOSSIP_OK;
+  }
+
+  int all_reduce_sum_dev(const std::vector<const uint64_t*>& part, size_t n, std::vector<uint64_t>* sum) override {
+    if (int rc = scratch(n * 8)) return rc;
+    if (int rc = pinned(n * 8)) return rc;
+    RCCL_OK(R.GroupStart());  // out of place: the engines keep their own partials
+    for (size_t i = 0; i < eng_.size(); ++i) {
+      HIPT_OK(hipSetDevice(engine_device(eng_[i])));
+      RCCL_OK(R.AllReduce(part[i], scratch_[i], n, ncclUint64, ncclSum, comm_[i], engine_stream(eng_[i])));
+    }
+    RCCL_OK(R.GroupEnd());
+    HIPT_OK(hipSetDevice(engine_device(eng_[0])));
+    HIPT_OK(hipMemcpyAsync(host_, scratch_[0], n * 8, hipMemcpyDeviceToHost, engine_stream(eng_[0])));
+    HIPT_OK(hipStreamSynchronize(engine_stream(eng_[0])));
+    sum->assign(host_, host_ + n);
+    return GOSSIP_OK;
+  }
+
  private:
+  int pinned(size_t bytes) {  // pinned host room for the device-value reads
+    if (bytes <= host_bytes_) return GOSSIP_OK;
+    if (host_) HIPT_OK(hipHostFree(host_));
+    host_ = nullptr;
+    host_bytes_ = 0;
+    const size_t want = std::max<size_t>(bytes, 4096);
+    HIPT_OK(hipHostMalloc((void**)&host_, want, hipHostMallocDefault));
+    host_bytes_ = want;
+    return GOSSIP_OK;
+  }
   int scratch(size_t bytes) {  // a small device buffer per engine for the host-side values
     if (bytes <= scratch_bytes_) return GOSSIP_OK;
     scratch_.resize(eng_.size(), nullptr);
@@ -296,6 +406,8 @@ class RcclTransport final : public Transport {
   uint32_t G_;
   std::vector<void*> scratch_;
   size_t scratch_bytes_ = 0;
+  uint64_t* host_ = nullptr;
+  size_t host_bytes_ = 0;
   std::vector<hipStream_t> side_;
   std::vector<hipEvent_t> ev_in_, ev_out_;
   bool pending_ = false;
@@ -310,6 +422,7 @@ class CopyTransport final : public Transport {
     for (gossip_engine_t* e : local) by_rank_[engine_rank(e)] = e;
   }
   int32_t kind() const override { return 2; }
+  const std::vector<gossip_engine_t*>& engines() const override { return eng_; }
 
   int all_gather(const std::vector<void*>& recv, const std::vector<const void*>& send, size_t bytes) override {
     if (bytes == 0) return GOSSIP_OK;
@@ -446,7 +559,10 @@ struct Driver {
     return GOSSIP_OK;
   }
 
-  int dense(std::vector<std::vector<uint64_t>>* part, bool cc) {
+  // Rounds of the random modes hand their counts and partials over as device values
+  // (gossip_*_dev): each exchange of them ends in one host read, so a dense round waits on the
+  // host once, an exchange round twice, a sparse round three times.
+  int dense(std::vector<const uint64_t*>* pd, bool cc) {
     std::vector<void*> recv(n());
     std::vector<const void*> send(n());
     if (cc) {  // class-coded state all-gather
@@ -481,22 +597,23 @@ struct Driver {
       for (size_t i = 0; i < n(); ++i) ENG(i, gossip_dense_prepare(L[i]));
       TR(tr->join());
     }
-    for (size_t i = 0; i < n(); ++i) ENG(i, gossip_round_compute(L[i], (*part)[i].data()));
+    for (size_t i = 0; i < n(); ++i) ENG(i, gossip_round_compute_dev(L[i], &(*pd)[i]));
     return GOSSIP_OK;
   }
 
-  int sparse(std::vector<std::vector<uint64_t>>* part) {
+  int sparse(std::vector<const uint64_t*>* pd) {
     std::vector<void*> rare(n()), rrecv(n()), out(n()), in(n());
-    std::vector<uint64_t> cnt(n());
-    for (size_t i = 0; i < n(); ++i) ENG(i, gossip_sparse_rare(L[i], &rare[i], &cnt[i]));
+    std::vector<const uint64_t*> cnt(n());
+    for (size_t i = 0; i < n(); ++i) ENG(i, gossip_sparse_rare_dev(L[i], &rare[i], &cnt[i]));
     std::vector<uint64_t> counts;
-    TR(tr->all_gather_u64(cnt, &counts));
+    TR(tr->all_gather_dev(cnt, &counts));
     const uint64_t stride = *std::max_element(counts.begin(), counts.end());
     for (size_t i = 0; i < n(); ++i) ENG(i, gossip_sparse_rare_recv(L[i], stride, &rrecv[i]));
     if (stride) TR(tr->all_gather(rrecv, std::vector<const void*>(rare.begin(), rare.end()), stride * 16));
-    std::vector<std::vector<uint64_t>> oc(n(), std::vector<uint64_t>(G)), ic;
-    for (size_t i = 0; i < n(); ++i) ENG(i, gossip_sparse_scan(L[i], counts.data(), &out[i], oc[i].data()));
-    TR(tr->all_to_all_counts(oc, &ic));
+    std::vector<std::vector<uint64_t>> oc, ic;
+    std::vector<const uint64_t*> sc(n());
+    for (size_t i = 0; i < n(); ++i) ENG(i, gossip_sparse_scan_dev(L[i], counts.data(), &out[i], &sc[i]));
+    TR(tr->all_to_all_counts_dev(sc, &oc, &ic));
     std::vector<std::vector<uint64_t>> ob(n()), ib(n());
     std::vector<uint64_t> nin(n());
     for (size_t i = 0; i < n(); ++i) {
@@ -508,18 +625,19 @@ struct Driver {
       }
     }
     TR(tr->all_to_all_v(in, ib, std::vector<const void*>(out.begin(), out.end()), ob));
-    for (size_t i = 0; i < n(); ++i) ENG(i, gossip_sparse_commit(L[i], nin[i], (*part)[i].data()));
+    for (size_t i = 0; i < n(); ++i) ENG(i, gossip_sparse_commit_dev(L[i], nin[i], &(*pd)[i]));
     return GOSSIP_OK;
   }
 
-  int exchange(std::vector<std::vector<uint64_t>>* part) {
+  int exchange(std::vector<const uint64_t*>* pd) {
     std::vector<void*> cls(n()), img(n()), ids(n()), vals(n()), rid(n()), rval(n()), rep(n()), back(n());
     std::vector<uint64_t> nb(n());
     for (size_t i = 0; i < n(); ++i) ENG(i, gossip_xd_classes(L[i], &cls[i], &img[i], &nb[i]));
     if (nb[0]) TR(tr->all_gather(img, std::vector<const void*>(cls.begin(), cls.end()), nb[0]));
-    std::vector<std::vector<uint64_t>> oc(n(), std::vector<uint64_t>(G)), ic;
-    for (size_t i = 0; i < n(); ++i) ENG(i, gossip_xd_requests(L[i], &ids[i], &vals[i], oc[i].data()));
-    TR(tr->all_to_all_counts(oc, &ic));
+    std::vector<std::vector<uint64_t>> oc, ic;
+    std::vector<const uint64_t*> sc(n());
+    for (size_t i = 0; i < n(); ++i) ENG(i, gossip_xd_requests_dev(L[i], &ids[i], &vals[i], &sc[i]));
+    TR(tr->all_to_all_counts_dev(sc, &oc, &ic));
     std::vector<uint64_t> nin(n());
     std::vector<std::vector<uint64_t>> o4(n()), i4(n()), o8(n()), i8(n());
     for (size_t i = 0; i < n(); ++i) {
@@ -541,7 +659,7 @@ struct Driver {
     }
     // the replies go back: what engine i received from q returns to q
     TR(tr->all_to_all_v(back, o8, std::vector<const void*>(rep.begin(), rep.end()), i8));
-    for (size_t i = 0; i < n(); ++i) ENG(i, gossip_xd_finish(L[i], (*part)[i].data()));
+    for (size_t i = 0; i < n(); ++i) ENG(i, gossip_xd_finish_dev(L[i], &(*pd)[i]));
     return GOSSIP_OK;
   }
 
@@ -579,17 +697,23 @@ struct Driver {
   int round(gossip_round_stats_t* st, std::vector<uint64_t>* total) {
     int32_t kind = 0;
     if (int rc = plan(&kind)) return rc;
-    std::vector<std::vector<uint64_t>> part(n(), std::vector<uint64_t>(gossip_partial_len(L[0])));
+    const size_t plen = gossip_partial_len(L[0]);
+    std::vector<std::vector<uint64_t>> part;  // ANTIENTROPY: partials finished on the host
+    std::vector<const uint64_t*> pd(n(), nullptr);  // the others: device values
     int rc;
     switch (kind) {
-      case 1: rc = sparse(&part); break;
-      case 2: rc = antientropy(&part); break;
-      case 3: rc = exchange(&part); break;
-      case 4: rc = dense(&part, true); break;
-      default: rc = dense(&part, false); break;
+      case 1: rc = sparse(&pd); break;
+      case 2:
+        part.assign(n(), std::vector<uint64_t>(plen));
+        rc = antientropy(&part);
+        break;
+      case 3: rc = exchange(&pd); break;
+      case 4: rc = dense(&pd, true); break;
+      default: rc = dense(&pd, false); break;
     }
     if (rc) return rc;
-    TR(tr->all_reduce_sum_u64(part, total));
+    if (kind == 2) TR(tr->all_reduce_sum_u64(part, total));
+    else TR(tr->all_reduce_sum_dev(pd, plen, total));
     for (size_t i = 0; i < n(); ++i) {
       gossip_round_stats_t s;
       ENG(i, gossip_round_commit(L[i], total->data(), &s));

@@ -98,6 +98,13 @@ SIGNATURES = [
     ("xd_serve", C.c_int, [P, C.POINTER(P)]),
     ("xd_response_recv", C.c_int, [P, C.POINTER(P)]),
     ("xd_finish", C.c_int, [P, U64P]),
+    # device-resident round values (ABI v9): the value stays in engine memory (a uint64 pointer)
+    ("round_compute_dev", C.c_int, [P, C.POINTER(P)]),
+    ("sparse_rare_dev", C.c_int, [P, C.POINTER(P), C.POINTER(P)]),
+    ("sparse_scan_dev", C.c_int, [P, U64P, C.POINTER(P), C.POINTER(P)]),
+    ("sparse_commit_dev", C.c_int, [P, C.c_uint64, C.POINTER(P)]),
+    ("xd_requests_dev", C.c_int, [P, C.POINTER(P), C.POINTER(P), C.POINTER(P)]),
+    ("xd_finish_dev", C.c_int, [P, C.POINTER(P)]),
     ("cc_send", C.c_int, [P, C.POINTER(P), U64P, C.POINTER(P), U64P]),
     ("cc_recv", C.c_int, [P, C.c_uint64, C.POINTER(P), C.POINTER(P)]),
     ("cc_expand", C.c_int, [P, U64P]),

@@ -385,6 +385,42 @@ class AbiEngine:
         self._check(self._fn("sparse_commit")(self._h, items, out.ctypes.data_as(_abi.U64P)))
         return out
 
+    # -- device-resident round values (ABI v9, include/gossip.h gossip_*_dev): device pointers to
+    # uint64 values that a device-side collective consumes without a host read of its own --
+    def round_compute_dev(self) -> int:
+        p = C.c_void_p()
+        self._check(self._fn("round_compute_dev")(self._h, C.byref(p)))
+        return p.value
+
+    def sparse_rare_dev(self):
+        """(rare list pointer, pointer to the count)."""
+        ptr, cnt = C.c_void_p(), C.c_void_p()
+        self._check(self._fn("sparse_rare_dev")(self._h, C.byref(ptr), C.byref(cnt)))
+        return ptr.value, cnt.value
+
+    def sparse_scan_dev(self, counts):
+        """(messages pointer, pointer to the G items-per-owner counts)."""
+        c = np.ascontiguousarray(counts, dtype=np.uint64)
+        ptr, cnt = C.c_void_p(), C.c_void_p()
+        self._check(self._fn("sparse_scan_dev")(self._h, c.ctypes.data_as(_abi.U64P), C.byref(ptr), C.byref(cnt)))
+        return ptr.value, cnt.value
+
+    def sparse_commit_dev(self, items: int) -> int:
+        p = C.c_void_p()
+        self._check(self._fn("sparse_commit_dev")(self._h, C.c_uint64(items), C.byref(p)))
+        return p.value
+
+    def xd_requests_dev(self):
+        """(ids pointer, values pointer, pointer to the G items-per-owner counts)."""
+        ids, vals, cnt = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        self._check(self._fn("xd_requests_dev")(self._h, C.byref(ids), C.byref(vals), C.byref(cnt)))
+        return ids.value, vals.value, cnt.value
+
+    def xd_finish_dev(self) -> int:
+        p = C.c_void_p()
+        self._check(self._fn("xd_finish_dev")(self._h, C.byref(p)))
+        return p.value
+
 
 class Engine(AbiEngine):
     """The HIP engine (libgossip_hip.so) on one gfx950 device."""

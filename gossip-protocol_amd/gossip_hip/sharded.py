@@ -134,6 +134,32 @@ class _Comm:
         dist.all_to_all_single(out, self.small(values), group=self.group)
         return [int(x) for x in out.cpu()]
 
+    # device-resident values (engine.*_dev, RCCL): the collective reads engine memory on the
+    # engine's (= torch's current) stream and one host read of its result is the round's only
+    # sync for that exchange
+    def dev_all_gather_one(self, ptr: int) -> list:
+        out = torch.empty(self.world, dtype=torch.int64, device="cuda")
+        dist.all_gather_into_tensor(out, _as_tensor(ptr, 8, True), group=self.group)
+        return [int(x) for x in out.cpu()]
+
+    def dev_all_to_all_counts(self, ptr: int):
+        """(sent counts, received counts) from the G counts at ptr."""
+        send = _as_tensor(ptr, self.world * 8, True)
+        recv = torch.empty_like(send)
+        dist.all_to_all_single(recv, send, group=self.group)
+        both = [int(x) for x in torch.cat([send, recv]).cpu()]
+        return both[:self.world], both[self.world:]
+
+    def dev_all_reduce_sum(self, ptr: int, n: int) -> np.ndarray:
+        t = _as_tensor(ptr, n * 8, True).clone()  # (the engine keeps its own partials)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        return t.cpu().numpy().view(np.uint64)
+
+
+def _dev_values(engine, comm: "_Comm") -> bool:
+    """Device-side counts and partials (RCCL on device engines with the ABI v9 calls)."""
+    return comm.direct and engine.on_device and comm.world > 1 and engine.supports("round_compute_dev")
+
 
 def _plan(engine, comm: _Comm) -> int:
     if not engine.supports("sharded_plan"):
@@ -160,27 +186,40 @@ def _dense_round(engine, comm: _Comm) -> np.ndarray:
         engine.dense_prepare()
         if work is not None:
             work.wait()
+    if _dev_values(engine, comm):
+        return comm.dev_all_reduce_sum(engine.round_compute_dev(), engine.partial_len())
     return engine.round_compute()
 
 
 def _sparse_round(engine, comm: _Comm) -> np.ndarray:
     w = comm.world
-    send_p, count = engine.sparse_rare()
-    counts = comm.all_gather_small(count)
+    dev = _dev_values(engine, comm)
+    if dev:
+        send_p, count_p = engine.sparse_rare_dev()
+        counts = comm.dev_all_gather_one(count_p)
+    else:
+        send_p, count = engine.sparse_rare()
+        counts = comm.all_gather_small(count)
     stride = max(counts)
     recv_p = engine.sparse_rare_recv(stride)
     if stride:
         comm.all_gather(_as_tensor(recv_p, stride * 16 * w, engine.on_device),
                         _as_tensor(send_p, stride * 16, engine.on_device))
-    out_p, out_counts = engine.sparse_scan(counts)
-    out_counts = [int(c) for c in out_counts]
-    in_counts = comm.all_to_all_small(out_counts)
+    if dev:
+        out_p, counts_p = engine.sparse_scan_dev(counts)
+        out_counts, in_counts = comm.dev_all_to_all_counts(counts_p)
+    else:
+        out_p, out_counts = engine.sparse_scan(counts)
+        out_counts = [int(c) for c in out_counts]
+        in_counts = comm.all_to_all_small(out_counts)
     n_in = sum(in_counts)
     in_p = engine.sparse_msg_recv(n_in)
     # every rank joins the collective, also one with nothing to send or receive (G > 2)
     comm.all_to_all(_as_tensor(in_p, n_in * 16, engine.on_device),
                     _as_tensor(out_p, sum(out_counts) * 16, engine.on_device),
                     [c * ITEM_WORDS for c in in_counts], [c * ITEM_WORDS for c in out_counts])
+    if dev:
+        return comm.dev_all_reduce_sum(engine.sparse_commit_dev(n_in), engine.partial_len())
     return engine.sparse_commit(n_in)
 
 
@@ -188,8 +227,13 @@ def _xd_round(engine, comm: _Comm) -> np.ndarray:
     cls_p, img_p, nb = engine.xd_classes()
     if nb and comm.world > 1:  # every shard's class bitmaps (in place): the edge filter of this round
         comm.all_gather(_as_tensor(img_p, nb * comm.world, engine.on_device), _as_tensor(cls_p, nb, engine.on_device))
-    ids_p, vals_p, counts = engine.xd_requests()
-    in_counts = comm.all_to_all_small(counts) if comm.world > 1 else counts
+    dv = _dev_values(engine, comm)
+    if dv:
+        ids_p, vals_p, counts_p = engine.xd_requests_dev()
+        counts, in_counts = comm.dev_all_to_all_counts(counts_p)
+    else:
+        ids_p, vals_p, counts = engine.xd_requests()
+        in_counts = comm.all_to_all_small(counts) if comm.world > 1 else counts
     n_in, n_out = sum(in_counts), sum(counts)
     rid_p, rval_p = engine.xd_request_recv(n_in)
     dev = engine.on_device
@@ -206,6 +250,8 @@ def _xd_round(engine, comm: _Comm) -> np.ndarray:
         comm.all_to_all(_as_tensor(back_p, n_out * 8, dev), _as_tensor(rep_p, n_in * 8, dev), counts, in_counts)
     else:
         _as_tensor(back_p, n_out * 8, dev).copy_(_as_tensor(rep_p, n_in * 8, dev))
+    if dv:
+        return comm.dev_all_reduce_sum(engine.xd_finish_dev(), engine.partial_len())
     return engine.xd_finish()
 
 
@@ -229,6 +275,8 @@ def _cc_round(engine, comm: _Comm) -> np.ndarray:
     elif count:
         _as_tensor(rvals_p, count * 8, dev).copy_(_as_tensor(vals_p, count * 8, dev))
     engine.cc_expand(counts)
+    if _dev_values(engine, comm):
+        return comm.dev_all_reduce_sum(engine.round_compute_dev(), engine.partial_len())
     return engine.round_compute()
 
 
@@ -289,7 +337,8 @@ def sharded_round(engine, group=None, kinds: list | None = None, direct: bool | 
         partial = _sparse_round(engine, comm)
     else:
         partial = _dense_round(engine, comm)
-    if comm.world > 1:
+    # the device-value path returns the global sum already (one all-reduce on engine memory)
+    if comm.world > 1 and not (kind != 2 and _dev_values(engine, comm)):
         partial = comm.all_reduce_sum(partial)
     return engine.round_commit(partial)
 

@@ -41,7 +41,7 @@ import (
 )
 
 // ABIVersion is the gossip.h version this binding is written against.
-const ABIVersion = 8
+const ABIVersion = 9
 
 // Mode is a dissemination rule (DESIGN.md §2).
 type Mode uint32
@@ -738,6 +738,57 @@ func (e *Engine) XDResponseRecv() (uintptr, error) {
 func (e *Engine) XDFinish() ([]uint64, error) {
 	out := make([]uint64, e.PartialLen())
 	return out, e.locked(func() C.int { return C.gossip_xd_finish(e.h, u64p(out)) })
+}
+
+// Device-resident round values (ABI v9, gossip_*_dev): the same calls with their counts and partials
+// left in engine memory (uint64 device pointers) for a device-side collective on the engine's stream.
+
+// RoundComputeDev: the partials of a dense round (PartialLen values on the device).
+func (e *Engine) RoundComputeDev() (partial uintptr, err error) {
+	var p *C.uint64_t
+	err = e.locked(func() C.int { return C.gossip_round_compute_dev(e.h, &p) })
+	return uintptr(unsafe.Pointer(p)), err
+}
+
+// SparseRareDev: the own rare list and a device pointer to its count.
+func (e *Engine) SparseRareDev() (send, count uintptr, err error) {
+	var s unsafe.Pointer
+	var c *C.uint64_t
+	err = e.locked(func() C.int { return C.gossip_sparse_rare_dev(e.h, &s, &c) })
+	return uintptr(s), uintptr(unsafe.Pointer(c)), err
+}
+
+// SparseScanDev: the pushes for other shards and a device pointer to the G per-owner counts.
+func (e *Engine) SparseScanDev(counts []uint64) (send, sendCounts uintptr, err error) {
+	if len(counts) != int(e.cfg.ShardCount) {
+		return 0, 0, fmt.Errorf("gossipgpu: SparseScanDev wants %d counts", e.cfg.ShardCount)
+	}
+	var s unsafe.Pointer
+	var c *C.uint64_t
+	err = e.locked(func() C.int { return C.gossip_sparse_scan_dev(e.h, u64p(counts), &s, &c) })
+	return uintptr(s), uintptr(unsafe.Pointer(c)), err
+}
+
+// SparseCommitDev ends a sparse round; the partials stay on the device.
+func (e *Engine) SparseCommitDev(items uint64) (partial uintptr, err error) {
+	var p *C.uint64_t
+	err = e.locked(func() C.int { return C.gossip_sparse_commit_dev(e.h, C.uint64_t(items), &p) })
+	return uintptr(unsafe.Pointer(p)), err
+}
+
+// XDRequestsDev: the items of an exchange round and a device pointer to the G per-owner counts.
+func (e *Engine) XDRequestsDev() (ids, vals, counts uintptr, err error) {
+	var i, v unsafe.Pointer
+	var c *C.uint64_t
+	err = e.locked(func() C.int { return C.gossip_xd_requests_dev(e.h, &i, &v, &c) })
+	return uintptr(i), uintptr(v), uintptr(unsafe.Pointer(c)), err
+}
+
+// XDFinishDev merges the replies; the partials stay on the device.
+func (e *Engine) XDFinishDev() (partial uintptr, err error) {
+	var p *C.uint64_t
+	err = e.locked(func() C.int { return C.gossip_xd_finish_dev(e.h, &p) })
+	return uintptr(unsafe.Pointer(p)), err
 }
 
 // CCSend: the own occupancy bitmaps of a class-coded dense round (plan kind 4; [nz][full], bitsBytes

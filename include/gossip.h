@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define GOSSIP_ABI_VERSION 8u
+#define GOSSIP_ABI_VERSION 9u
 
 /* Dissemination modes. */
 enum gossip_mode {
@@ -341,6 +341,29 @@ int gossip_xd_request_recv(gossip_engine_t* eng, uint64_t items, void** ids, voi
 int gossip_xd_serve(gossip_engine_t* eng, void** replies);
 int gossip_xd_response_recv(gossip_engine_t* eng, void** replies);
 int gossip_xd_finish(gossip_engine_t* eng, uint64_t* partial);
+
+/* --- device-resident round values (ABI v9) ------------------------------
+ * The calls above that hand the host a count vector or the partial vector read it back and
+ * synchronize the engine's stream.  Their _dev forms enqueue the same work and leave the
+ * values in engine memory (uint64; counts widened), so the caller's device-side collective
+ * (RCCL on the engine's stream, or a torch collective on the stream gossip_set_stream bound)
+ * consumes them and one host read of its result ends the exchange:
+ *   gossip_round_compute_dev -> partial_len values (node count in [1], as gossip_round_compute);
+ *                               random and FLOOD modes (ANTIENTROPY partials finish on the host)
+ *   gossip_sparse_rare_dev   -> 1 value, the own rare count
+ *   gossip_sparse_scan_dev   -> G values, the items for each owner
+ *   gossip_sparse_commit_dev -> partial_len values
+ *   gossip_xd_requests_dev   -> G values, the items for each owner
+ *   gossip_xd_finish_dev     -> partial_len values
+ * The pointer stays valid, and its values unchanged, until the next _dev call on the engine.
+ * Without a driver or ordered collectives ("ordered_collectives"), and in timing mode, the
+ * call synchronizes the stream before returning (the value is then final for any stream). */
+int gossip_round_compute_dev(gossip_engine_t* eng, const uint64_t** partial);
+int gossip_sparse_rare_dev(gossip_engine_t* eng, void** send, const uint64_t** count);
+int gossip_sparse_scan_dev(gossip_engine_t* eng, const uint64_t* counts, void** send, const uint64_t** send_counts);
+int gossip_sparse_commit_dev(gossip_engine_t* eng, uint64_t items, const uint64_t** partial);
+int gossip_xd_requests_dev(gossip_engine_t* eng, void** ids, void** vals, const uint64_t** send_counts);
+int gossip_xd_finish_dev(gossip_engine_t* eng, const uint64_t** partial);
 
 /* --- class-coded state all-gather (random modes, W == 1, G > 1) --------
  * A dense round on the state image whose all-gather sends, per shard, its two occupancy

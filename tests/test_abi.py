@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert eng_mod.load_library().gossip_abi_version() == 8
+    assert eng_mod.load_library().gossip_abi_version() == 9
 
 
 def test_library_reads_no_environment():
