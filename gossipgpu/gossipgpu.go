@@ -1,5 +1,5 @@
 // Package gossipgpu binds the MI355X gossip-round engine (libgossip_hip.so, the C ABI of
-// include/gossip.h, ABI v8) for Go hosts such as 0xSherlokMo/gossip-protocol's main.go.
+// include/gossip.h, ABI v9) for Go hosts such as 0xSherlokMo/gossip-protocol's main.go.
 //
 // The reference floods each value once to its topology neighbours with blocking SyncRPCs
 // ((*NodeState).Gossip, main.go:65-89), one process per node.  Here one Engine holds every
