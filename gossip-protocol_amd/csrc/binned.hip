@@ -700,66 +700,95 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Visits every record of the runs (s, T) for s in [0, nt_s): a wave takes 64
-// consecutive runs at a time (lane = run) and scans their lengths; the
+// Visits every record of the runs (s, T) for s in [0, nt_s): a wave takes 64 * RPL
+// consecutive runs at a time (RPL consecutive runs per lane) and scans their lengths; the
 // concatenated records are then walked in windows of 64*U, lane-strided (so
 // each load instruction reads consecutive records of a run).  The owner of a
 // record comes from a per-wave LDS bitmap of run starts in the window and a
 // list of the window's runs: rank = (run starts at or before it) - 1, one
 // popcount and one LDS read per record, no search.  load(rec) receives the
 // global record index s * rp + pos, or -1 past the end.
-// LDS per wave: wmask[U] u64, wlist[64] i32.  The walk is shared by the waves
+// LDS per wave: wmask[U] u64, wlist[64 * RPL] i32.  The walk is shared by the waves
 // [w0, w0 + nwaves) of the block (nwaves = 0: every wave).
 // Software-pipelined: load(rec) issues a window's loads into a Buf and proc(buf) consumes the
 // previous window's, so one window's memory latency overlaps the other's LDS work (a wave's
 // loads retire in order: proc waits only for the older window).
-template <int U, typename Buf, typename LD, typename PR>
+template <int U, typename Buf, int RPL = 1, typename LD, typename PR>
 __device__ __forceinline__ void for_each_run_record_pipe(const BinGeom& g, const uint16_t* rowb, const uint16_t* rowe,
                                                          uint64_t* wmask_all, int32_t* wlist_all, LD&& load,
                                                          PR&& proc, uint32_t w0 = 0, uint32_t nwaves = 0) {
-  constexpr uint32_t kWin = 64 * U;
+  // RPL runs per lane (consecutive): a wave takes 64 * RPL runs at a time
+  constexpr uint32_t kWin = 64 * U, kRuns = 64 * RPL;
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (nwaves == 0) nwaves = blockDim.x >> 6;
   uint64_t* wm = wmask_all + wave * U;
-  int32_t* wl = wlist_all + wave * 64;
+  int32_t* wl = wlist_all + wave * kRuns;
   const uint64_t below = (1ull << lane) - 1ull, upto = (2ull << lane) - 1ull;
-  const uint32_t step = nwaves * 64;
-  uint32_t nbe = 0, nen = 0;
-  if ((wave - w0) * 64 < g.nt_s) {
-    const uint32_t sc = min((wave - w0) * 64 + lane, g.nt_s - 1);
-    nbe = rowb[sc];
-    nen = rowe[sc];
+  const uint32_t step = nwaves * kRuns;
+  uint32_t nbe[RPL], nen[RPL];
+#pragma unroll
+  for (int r = 0; r < RPL; ++r) nbe[r] = nen[r] = 0;
+  if ((wave - w0) * kRuns < g.nt_s) {
+#pragma unroll
+    for (int r = 0; r < RPL; ++r) {
+      const uint32_t sc = min((wave - w0) * kRuns + lane * RPL + r, g.nt_s - 1);
+      nbe[r] = rowb[sc];
+      nen[r] = rowe[sc];
+    }
   }
   Buf pend;
   bool have = false;
-  for (uint32_t s0 = (wave - w0) * 64; s0 < g.nt_s; s0 += step) {
-    const uint32_t s = s0 + lane;
-    const uint32_t be0 = nbe, en0 = nen;
-    if (s0 + step < g.nt_s) {
-      const uint32_t sc = min(s + step, g.nt_s - 1);
-      nbe = rowb[sc];
-      nen = rowe[sc];
+  for (uint32_t s0 = (wave - w0) * kRuns; s0 < g.nt_s; s0 += step) {
+    uint32_t len[RPL], exc[RPL];
+    int32_t basep[RPL];
+    uint32_t lsum = 0;
+#pragma unroll
+    for (int r = 0; r < RPL; ++r) {
+      const uint32_t s = s0 + lane * RPL + r;
+      const uint32_t be = s < g.nt_s ? nbe[r] : 0u, en = s < g.nt_s ? nen[r] : 0u;
+      len[r] = en - be;
+      exc[r] = lsum;  // (the lane's own part: the wave's prefix is added below)
+      basep[r] = (int32_t)(s * g.rp + be);
+      lsum += len[r];
     }
-    const uint32_t be = s < g.nt_s ? be0 : 0u, en = s < g.nt_s ? en0 : 0u;
-    const uint32_t len = en - be;
-    uint32_t inc = len;
+    if (s0 + step < g.nt_s) {
+#pragma unroll
+      for (int r = 0; r < RPL; ++r) {
+        const uint32_t sc = min(s0 + step + lane * RPL + r, g.nt_s - 1);
+        nbe[r] = rowb[sc];
+        nen[r] = rowe[sc];
+      }
+    }
+    uint32_t inc = lsum;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t y = __shfl_up(inc, o, 64);
       if (lane >= (uint32_t)o) inc += y;
     }
-    const uint32_t exc = inc - len;
     const uint32_t total = __shfl(inc, 63, 64);
-    const int32_t basep = (int32_t)(s * g.rp + be - exc);
+#pragma unroll
+    for (int r = 0; r < RPL; ++r) {
+      exc[r] += inc - lsum;
+      basep[r] -= (int32_t)exc[r];
+    }
     for (uint32_t f0 = 0; f0 < total; f0 += kWin) {
       if (lane < (uint32_t)U) wm[lane] = 0;
       wave_sync();
-      const bool in = len != 0 && exc < f0 + kWin && exc + len > f0;
-      const uint64_t inm = __ballot(in);
-      if (in) {
-        const uint32_t pos = exc > f0 ? exc - f0 : 0u;
-        atomicOr((unsigned long long*)&wm[pos >> 6], 1ull << (pos & 63u));
-        wl[__popcll(inm & below)] = basep;
+      bool in[RPL];
+      uint32_t before = 0;
+#pragma unroll
+      for (int r = 0; r < RPL; ++r) {
+        in[r] = len[r] != 0 && exc[r] < f0 + kWin && exc[r] + len[r] > f0;
+        before += (uint32_t)__popcll(__ballot(in[r]) & below);
+      }
+#pragma unroll
+      for (int r = 0; r < RPL; ++r) {
+        if (in[r]) {
+          const uint32_t pos = exc[r] > f0 ? exc[r] - f0 : 0u;
+          atomicOr((unsigned long long*)&wm[pos >> 6], 1ull << (pos & 63u));
+          wl[before] = basep[r];
+          ++before;
+        }
       }
       wave_sync();
       int32_t rec[U];
@@ -770,7 +799,7 @@ __device__ __forceinline__ void for_each_run_record_pipe(const BinGeom& g, const
         const uint32_t rank = pre + (uint32_t)__popcll(w & upto) - 1u;
         pre += (uint32_t)__popcll(w);
         const uint32_t f = f0 + u * 64 + lane;
-        rec[u] = f < total ? wl[rank & 63u] + (int32_t)f : -1;
+        rec[u] = f < total ? wl[rank & (kRuns - 1u)] + (int32_t)f : -1;
       }
       wave_sync();  // the next window rewrites wm/wl
       Buf nb = load(rec);
@@ -794,6 +823,11 @@ struct IdBuf {
   uint32_t id[U];
 };
 constexpr int kUnrollPipe = 4;  // records per lane and window in the pipelined walks (8: 2^27 dense round 5737 vs 5686 us)
+// Serve's walk: windows of 8 records per lane over groups of 128 runs (2 per lane): more loads in
+// flight per wave than 4 over 64 (its buffers are ids only).  2^27 dense round 5601-5613 -> 5558-5576
+// us, 2^24 equal; 8 over 256 runs, 16 over 128 and apply's push walk over 128 runs: slower
+// (profiles/r04_ak/).
+constexpr int kServeU = 8, kServeRPL = 2, kPushRPL = 1;
 
 // The pushes aimed at tile X (its runs in every sender region) ORed into acc,
 // by the waves [0, nwaves) (0: all).  VZ: the record id's no-push flag.
@@ -807,7 +841,7 @@ __device__ __forceinline__ void push_walk(const BinGeom& g, const BinBufs& b, ui
   constexpr bool aos = LAYOUT == 2, SPLIT = LAYOUT >= 1;
   const uint16_t* rowb = b.offT + (size_t)X * g.nt_s;
   constexpr int U = kUnrollPipe;
-  for_each_run_record_pipe<U, PushBuf<U>>(g, rowb, rowb + g.nt_s, wmask, wlist, [&](const int32_t* rec) {
+  for_each_run_record_pipe<U, PushBuf<U>, kPushRPL>(g, rowb, rowb + g.nt_s, wmask, wlist, [&](const int32_t* rec) {
     PushBuf<U> bf;
 #pragma unroll
     for (int u = 0; u < U; ++u) bf.rec[u] = rec[u];
@@ -873,8 +907,8 @@ template <uint32_t VF, bool SPLIT = false>
 __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, const uint64_t* __restrict__ S, BinBufs b,
                                                                   uint32_t R, IdxRange tr) {
   __shared__ unsigned long long img[kTileD];
-  __shared__ uint64_t wmask[(kTileThreads / 64) * kUnrollPipe];
-  __shared__ int32_t wlist[(kTileThreads / 64) * 64];
+  __shared__ uint64_t wmask[(kTileThreads / 64) * kServeU];
+  __shared__ int32_t wlist[(kTileThreads / 64) * 64 * kServeRPL];
   // persistent: virtual block v = blockIdx.x, +gridDim.x, ... serves tile
   // tr.at(xcd_remap(v, tr.n)) (the XCD of v is that of blockIdx.x, as with one
   // block per tile); the next tile's image loads into registers during a walk
@@ -892,8 +926,8 @@ __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, cons
   const uint32_t* gids = b.ids;
   uint64_t* __restrict__ gresp = b.resp;
   const uint16_t* rowb = b.offT + (size_t)T * g.nt_s;
-  constexpr int U = kUnrollPipe;
-  for_each_run_record_pipe<U, IdBuf<U>>(g, rowb, rowb + g.nt_s, wmask, wlist, [&](const int32_t* rec) {
+  constexpr int U = kServeU;
+  for_each_run_record_pipe<U, IdBuf<U>, kServeRPL>(g, rowb, rowb + g.nt_s, wmask, wlist, [&](const int32_t* rec) {
     IdBuf<U> bf;
 #pragma unroll
     for (int u = 0; u < U; ++u) bf.rec[u] = rec[u];
@@ -936,7 +970,7 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
   __shared__ uint32_t red_full[kTileThreads / 64];
   __shared__ uint32_t red_nz[kTileThreads / 64];
   __shared__ uint64_t wmask[(kTileThreads / 64) * kUnrollPipe];
-  __shared__ int32_t wlist[(kTileThreads / 64) * 64];
+  __shared__ int32_t wlist[(kTileThreads / 64) * 64 * kPushRPL];
   const uint32_t tid = threadIdx.x;
   // persistent (grid apply_grid(nt_d)): virtual block v = blockIdx.x,
   // +gridDim.x, ... applies tile xcd_remap(v, nt_d) (same XCD as blockIdx.x);
@@ -1515,7 +1549,7 @@ __global__ __launch_bounds__(kTileThreads) void xd_apply_kernel(XdGeom g, XdBufs
   __shared__ uint32_t red_full[kTileThreads / 64];
   __shared__ uint32_t red_nz[kTileThreads / 64];
   __shared__ uint64_t wmask[(kTileThreads / 64) * kUnrollPipe];
-  __shared__ int32_t wlist[(kTileThreads / 64) * 64];
+  __shared__ int32_t wlist[(kTileThreads / 64) * 64 * kPushRPL];
   __shared__ uint32_t pl[kXdPref];  // the tile's sender regions: owner-run prefix rows (G + 1 each)
   __shared__ uint32_t po[kXdPref];  // and the runs' send positions (G each, stride G + 1)
   const uint32_t tid = threadIdx.x, G = g.G;
