@@ -825,7 +825,7 @@ struct IdBuf {
 constexpr int kUnrollPipe = 4;  // records per lane and window in the pipelined walks (8: 2^27 dense round 5737 vs 5686 us)
 // Serve's walk: windows of 8 records per lane over groups of 128 runs (2 per lane): more loads in
 // flight per wave than 4 over 64 (its buffers are ids only).  2^27 dense round 5601-5613 -> 5558-5576
-// us, 2^24 equal; 8 over 256 runs, 16 over 128 and apply's push walk over 128 runs: slower
+// us, 2^24 equal; 8 over 256 runs, 16 over 128, and apply's push walk over 128 runs or with 6 / 8 records per lane: slower
 // (profiles/r04_ak/).
 constexpr int kServeU = 8, kServeRPL = 2, kPushRPL = 1;
 
