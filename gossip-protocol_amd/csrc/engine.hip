@@ -1500,7 +1500,7 @@ int gossip_reset(gossip_engine_t* e) {
   e->sx_valid = e->gtot_valid = e->last_sparse = false;
   // a dense_prepare or sparse plan of the old state must not leak into the next round
   e->sb_pre = e->ev_pre_pending = e->sx_planned = e->xd_planned = e->cc_planned = false;
-  if (e->frontier) {  // all-zero state: zero totals, empty bitmaps (D, P and dirty flags are zero between rounds)
+  if (e->frontier) {  // all-zero state: zero totals, empty bitmaps (D and its dirty flags are zero between rounds)
     const size_t nwb = (e->N + 63) / 64 * 8;
     HIP_OK(e, hipMemsetAsync(e->fb.nzb, 0, nwb, e->stream));
     HIP_OK(e, hipMemsetAsync(e->fb.fullb, 0, nwb, e->stream));

@@ -22,10 +22,10 @@ struct FrontierBufs {
   uint64_t* nzb;      // [ceil(N/64)] bit n: S[n] != 0
   uint64_t* fullb;    // [ceil(N/64)] bit n: S[n] == full mask
   uint32_t* summ;     // [summ_words] bit b: some rare node in [b*g, (b+1)*g)
-  uint64_t* D;        // [N] pending push deltas (atomic OR), zero outside a sparse round
-  uint64_t* P;        // [N] pending pull deltas (plain store by the node's own lane), zero outside
-  uint8_t* dirtyD;    // [ceil(N/64)] group g has a push delta (not kept in all_d rounds)
-  uint8_t* dirtyP;    // [ceil(N/64)] group g has a pull delta
+  // [N] pending deltas, zero outside a sparse round: pushes and (round 4) the node's own pull
+  // deltas alike, atomic ORs (one array: the commit reads and clears one word per node, not two)
+  uint64_t* D;
+  uint8_t* dirtyD;    // [ceil(N/64)] group g has a delta (not kept in all_d rounds)
   uint32_t glog;      // g = 1 << glog nodes per summary bit
   uint32_t summ_words;
   // Mid-level summary (one shard, 2^25 < N <= 2^30: the exact bitmaps no longer fit an XCD's

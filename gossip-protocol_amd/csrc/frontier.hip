@@ -35,14 +35,10 @@ namespace gossip {
 namespace {
 
 constexpr int kScanThreads = 1024;
-// (non-temporal hints on the scan's S gathers and P stores: equal)
+// (non-temporal hints on the scan's S gathers: equal)
 template <typename T>
 __device__ __forceinline__ T scan_ld(const T* p) {
   return *p;
-}
-template <typename T>
-__device__ __forceinline__ void scan_st(T* p, T v) {
-  *p = v;
 }
 constexpr uint32_t kScanGrid = 256;  // one block per CU: the summary takes 128 KiB of LDS
 constexpr uint32_t kScanWaves = 4;   // waves per SIMD (launch bounds)
@@ -326,19 +322,21 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
           accs[u] = acc & ~x[u];
         }
       }
-      // pull deltas: whole 8-word chunks (P is zero where there is no delta), so
-      // no store is a partial 64-B chunk.  Direct rounds: a majority (empty) node's
-      // pull goes straight into its S word, which nobody reads this round (the
-      // pushes into it are atomic ORs too), so the commit reads no P for it.
+      // pull deltas: ORed into D beside the pushes (a separate array written with whole
+      // 8-word chunks cost the commit a second read and clear per node: sparse rounds
+      // -2 % at 2^24, profiles/r04_an/).  Direct rounds: a majority (empty) node's pull
+      // goes straight into its S word, which nobody reads this round (the pushes into it
+      // are atomic ORs too), so the commit reads no delta for it.
 #pragma unroll
       for (int u = 0; u < kScanUnroll; ++u) {
         const uint32_t n = base + u * kScanThreads + tid;
-        const bool dmaj = MAJ == 0 && direct && !rn[u];
-        if (dmaj && accs[u]) atomicOr((unsigned long long*)&Sw[n], (unsigned long long)accs[u]);
-        const uint64_t pz = __ballot(!dmaj && accs[u] != 0);
-        if (!pz) continue;
-        if (n < c1 && ((pz >> (lane & ~7u)) & 0xFFull)) scan_st(&f.P[n], dmaj ? (uint64_t)0 : accs[u]);
-        if (!dmaj && accs[u]) f.dirtyP[n >> 6] = 1;
+        if (!accs[u]) continue;
+        if (MAJ == 0 && direct && !rn[u]) {
+          atomicOr((unsigned long long*)&Sw[n], (unsigned long long)accs[u]);
+          continue;
+        }
+        atomicOr((unsigned long long*)&f.D[n], (unsigned long long)accs[u]);
+        if (mark_d) f.dirtyD[n >> 6] = 1;
       }
     }
   }
@@ -432,11 +430,11 @@ __global__ __launch_bounds__(kCommitThreads) void frontier_rebuild_kernel(Fronti
 }
 
 // K2: a wave takes 64 groups, finds the dirty ones by one coalesced load of
-// their flags, and commits kCommitUnroll of them per step: S |= D | P in
-// place, D, P and the flags back to zero, bitmaps and stats deltas.  dmode
-// kSparseAllD: every group's D is read (the scan kept no push flags);
-// kSparseDirect: every group is visited (majority nodes took pushes in S), D / P
-// read where flagged, and the totals are absolute (partial zeroed before).
+// their flags, and commits kCommitUnroll of them per step: S |= D in place,
+// D and the flags back to zero, bitmaps and stats deltas.  dmode
+// kSparseAllD: every group's D is read (the scan kept no flags);
+// kSparseDirect: every group is visited (majority nodes took their deltas in S),
+// D read where flagged, and the totals are absolute (partial zeroed before).
 __global__ __launch_bounds__(kCommitThreads) void frontier_commit_kernel(FrontierBufs f, uint64_t* __restrict__ S,
                                                                           uint64_t N, uint64_t* __restrict__ partial,
                                                                           uint32_t R, uint32_t flags, uint32_t dmode) {
@@ -453,11 +451,10 @@ __global__ __launch_bounds__(kCommitThreads) void frontier_commit_kernel(Frontie
        c += (uint64_t)gridDim.x * (kCommitThreads / 64)) {
     const uint64_t gl = (c << 6) + lane;
     const bool gv = gl < ngroups;
-    const uint8_t fd = gv ? (all_d ? 1 : f.dirtyD[gl]) : 0, fp = gv ? f.dirtyP[gl] : 0;
+    const uint8_t fd = gv ? (all_d ? 1 : f.dirtyD[gl]) : 0;
     if (fd && !all_d) f.dirtyD[gl] = 0;
-    if (fp) f.dirtyP[gl] = 0;
-    const uint64_t mD = __ballot(fd != 0), mP = __ballot(fp != 0);
-    uint64_t mask = abs_t ? __ballot(gv) : (mD | mP);
+    const uint64_t mD = __ballot(fd != 0);
+    uint64_t mask = abs_t ? __ballot(gv) : mD;
     while (mask) {
       uint32_t gi[kCommitUnroll];
       uint32_t cntg = 0;
@@ -469,14 +466,13 @@ __global__ __launch_bounds__(kCommitThreads) void frontier_commit_kernel(Frontie
           ++cntg;
         }
       }
-      uint64_t d[kCommitUnroll], pv[kCommitUnroll], old[kCommitUnroll];
+      uint64_t d[kCommitUnroll], old[kCommitUnroll];
 #pragma unroll
       for (int u = 0; u < kCommitUnroll; ++u) {
         const uint64_t n = (((c << 6) + (gi[u] & 63u)) << 6) + lane;
         const bool valid = gi[u] < 64 && n < N;
-        const bool hd = gi[u] < 64 && ((mD >> gi[u]) & 1ull), hp = gi[u] < 64 && ((mP >> gi[u]) & 1ull);
+        const bool hd = gi[u] < 64 && ((mD >> gi[u]) & 1ull);
         d[u] = valid && hd ? f.D[n] : 0ull;
-        pv[u] = valid && hp ? f.P[n] : 0ull;
         old[u] = valid ? S[n] : 0ull;
       }
 #pragma unroll
@@ -485,13 +481,12 @@ __global__ __launch_bounds__(kCommitThreads) void frontier_commit_kernel(Frontie
         const uint64_t g = (c << 6) + gi[u];
         const uint64_t n = (g << 6) + lane;
         const bool valid = n < N;
-        const uint64_t nw = old[u] | d[u] | pv[u];
+        const uint64_t nw = old[u] | d[u];
         // write whole 8-word (64 B) chunks: a partial chunk costs the HBM a read-modify-write
         const uint32_t sh = lane & ~7u;
-        const uint64_t chg = __ballot(valid && nw != old[u]), dz = __ballot(d[u] != 0), pz = __ballot(pv[u] != 0);
+        const uint64_t chg = __ballot(valid && nw != old[u]), dz = __ballot(d[u] != 0);
         if (valid && ((chg >> sh) & 0xFFull)) S[n] = nw;
         if (valid && ((dz >> sh) & 0xFFull)) f.D[n] = 0;
-        if (valid && ((pz >> sh) & 0xFFull)) f.P[n] = 0;
         gs.add(f, g, n, valid, abs_t ? 0ull : old[u], nw, fm, do_hash, lane);
       }
     }
@@ -558,7 +553,7 @@ size_t frontier_bytes(uint64_t N) {
   const size_t nwords = (N + 63) / 64;
   const uint32_t glog = frontier_glog(N);
   const size_t sw = ((((N + (1ull << glog) - 1) >> glog) + 127) / 128) * 4;  // u32 words, uint4-padded
-  return 2 * al256(nwords * 8) + al256(sw * 4) + 2 * al256(N * 8) + 2 * al256(nwords) +
+  return 2 * al256(nwords * 8) + al256(sw * 4) + al256(N * 8) + al256(nwords) +
          al256((size_t)frontier_summ2_words(N) * 4);
 }
 
@@ -575,11 +570,7 @@ void frontier_carve(uint64_t N, void* base, FrontierBufs* f) {
   p += al256((size_t)f->summ_words * 4);
   f->D = (uint64_t*)p;
   p += al256(N * 8);
-  f->P = (uint64_t*)p;
-  p += al256(N * 8);
   f->dirtyD = (uint8_t*)p;
-  p += al256(nwords);
-  f->dirtyP = (uint8_t*)p;
   p += al256(nwords);
   f->g2log = frontier_g2log(N);
   f->summ2_words = frontier_summ2_words(N);

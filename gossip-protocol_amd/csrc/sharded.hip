@@ -335,14 +335,13 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, uint32_t*
           accs[u] = acc & ~x[u];
         }
       }
-      // pull deltas: whole 8-word chunks (P is zero where there is no delta)
+      // pull deltas: ORed into D beside the pushes (frontier.hip: one delta array)
 #pragma unroll
       for (int u = 0; u < kScanUnroll; ++u) {
         const uint32_t i = base + u * kScanThreads + tid;
-        const uint64_t pz = __ballot(accs[u] != 0);
-        if (!pz) continue;
-        if (i < c1 && ((pz >> (lane & ~7u)) & 0xFFull)) a.lf.P[i] = accs[u];
-        if (accs[u]) a.lf.dirtyP[i >> 6] = 1;
+        if (!accs[u]) continue;
+        atomicOr((unsigned long long*)&a.lf.D[i], (unsigned long long)accs[u]);
+        if (a.mark_d) a.lf.dirtyD[i >> 6] = 1;
       }
     }
   }
