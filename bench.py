@@ -215,6 +215,45 @@ def single_gpu_roofline(eng, nodes: int, workload: str) -> dict:
     return rl
 
 
+def sharded_roofline(eng, driver: str, trace, alg_round: int, world: int, backend: str) -> dict:
+    """N > 1: the dense round's fraction of the HBM roofline on WHOLE-round time per rank (plan,
+    collectives over the links, kernels, host reads), from hipEvents around each round of the
+    timed steps on the stream the collectives are ordered on (torch driver: torch.cuda.Event
+    pairs in gossip_hip.sharded.sharded_run; engine driver: gossip_round_wall).  The device work
+    alone (engine timer 0, collectives excluded) is reported beside it, with the link bytes this
+    rank sent per round (the collectives' sizes)."""
+    dense_ms = dense_n = dense_link = sparse_ms = sparse_n = sparse_link = 0.0
+    if driver == "engine":
+        dense_ms, dense_n, dense_link = eng.round_wall(0)
+        sparse_ms, sparse_n, sparse_link = eng.round_wall(1)
+    elif trace:
+        for r in trace:
+            ms = r["events"][0].elapsed_time(r["events"][1]) if "events" in r else 0.0
+            if r["kind"] == 1:
+                sparse_ms, sparse_n, sparse_link = sparse_ms + ms, sparse_n + 1, sparse_link + r["link_bytes"]
+            else:
+                dense_ms, dense_n, dense_link = dense_ms + ms, dense_n + 1, dense_link + r["link_bytes"]
+    round_s = dense_ms / 1e3 / max(dense_n, 1)
+    dev_ms, dev_n = eng.kernel_time(0)
+    dev_s = dev_ms / 1e3 / max(dev_n, 1)
+    achieved = alg_round / round_s / 1e9 if round_s > 0 else 0.0
+    dev_achieved = alg_round / dev_s / 1e9 if dev_s > 0 else 0.0
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": None, "bytes_per_node_round": alg_round // max(eng.hi - eng.lo, 1),
+            "alg_bytes_per_launch": alg_round, "avg_launch_us": round_s * 1e6,
+            "round_wall_us": round_s * 1e6, "dense_rounds_timed": int(dense_n),
+            "link_bytes_per_round": dense_link / max(dense_n, 1),
+            "sparse_round_wall_us": sparse_ms * 1e3 / max(sparse_n, 1), "sparse_rounds_timed": int(sparse_n),
+            "link_bytes_per_sparse_round": sparse_link / max(sparse_n, 1),
+            "device_only": {"avg_round_us": dev_s * 1e6, "rounds": int(dev_n), "frac": dev_achieved / HBM_PEAK_GBS,
+                            "what": "engine timer 0: the hot kernels' device time per round, collectives excluded"},
+            "kernel": ("sharded dense rounds, each timed whole per rank: plan, collectives (state all-gather, "
+                       "class-coded all-gather or exchange all-to-alls), kernels and host reads, from hipEvents on "
+                       "the stream the collectives are ordered on; alg bytes = 64 B x own nodes"
+                       + (" (gloo rehearsal: collectives staged through the host, not a link measurement)"
+                          if backend == "gloo" else ""))}
+
+
 def secondary_run(device: int, steps: int, warmup: int) -> dict:
     """configs[2] on the same GPU (2^24 nodes: the state fits the 256 MiB Infinity Cache), same step."""
     from gossip_hip import FLAG_TIMING, Engine
@@ -349,12 +388,14 @@ def main():
     if world > 1 and driver == "torch":
         use_torch_driver()
 
+    trace = None  # torch driver, timed steps: per round {"kind", "link_bytes", "events"}
+
     def one_step():
         eng.reset()
         eng.inject_random()
         if driver == "engine":  # one GPU, or every rank in gossip_step over the engine's RCCL comm
             return eng.step(64, with_infected=False).stats
-        return sharded_run(eng, 64)
+        return sharded_run(eng, 64, trace=trace)
 
     fx = load_fixture(n_total, seed)
 
@@ -370,17 +411,27 @@ def main():
         torch.cuda.synchronize()
 
     warm_check = None
+    engine_driver_verified = None  # N > 1, --driver engine: did the library-driven run match the fixture?
     for i in range(args.warmup):
         st = one_step()
         if i == 0 and fx is not None:  # before the timed steps: a wrong result is caught, not timed
             warm_check = verify(st)
+            if world > 1 and driver == "engine":
+                engine_driver_verified = warm_check is None
             if warm_check and world > 1 and driver == "engine":
                 driver_note = (f"the engine-driven run differed from the oracle fixture ({warm_check}): the "
                                "rounds are driven over torch.distributed instead")
                 print(f"warning: {driver_note}", file=sys.stderr)
+                if args.driver == "engine":  # asked for explicitly: a wrong library result fails the run
+                    print("error: --driver engine gave a wrong result", file=sys.stderr)
+                    if world > 1:
+                        dist.destroy_process_group()
+                    sys.exit(3)
                 driver = "torch"
                 use_torch_driver()
     eng.reset_timing()
+    if world > 1 and driver == "torch":
+        trace = []
     barrier()
     t0 = time.perf_counter()
     rounds, last = [], None
@@ -406,17 +457,7 @@ def main():
     if world == 1:
         rl = single_gpu_roofline(eng, n_total, workload)
     else:
-        alg_round = bpn * nown  # algorithmic bytes of one round over this rank's nodes
-        round_ms, round_launches = eng.kernel_time(0)
-        dense_s = round_ms / 1e3 / max(round_launches, 1)
-        achieved = alg_round / dense_s / 1e9
-        rl = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-              "frac": achieved / HBM_PEAK_GBS, "traffic": None, "bytes_per_node_round": bpn,
-              "alg_bytes_per_launch": alg_round, "avg_launch_us": dense_s * 1e6, "rounds_timed": round_launches,
-              "kernel": ("sharded rounds, hipEvent-timed device work of the hot kernels per round (timer 0): "
-                         "dense = exchange round (count + emit, bin + serve + unpermute, apply; G >= 6) or the "
-                         "binned push / pull passes + serve + apply after the state all-gather (G < 6), "
-                         "sparse = rare index + sharded scan (DESIGN.md §5); collectives not included")}
+        rl = sharded_roofline(eng, driver, trace, bpn * nown, world, args.backend)
     eng.close()
 
     if rank == 0:
@@ -439,6 +480,7 @@ def main():
                        **({"driver": driver} if world > 1 else {}),
                        **({"driver_note": driver_note} if driver_note else {})},
             "verified": verified,
+            **({"engine_driver_verified": engine_driver_verified} if engine_driver_verified is not None else {}),
             "verification": (f"per-round stats ({', '.join(STAT_KEYS)}) and the final state hash of the last "
                              f"timed step{' (all ranks, hash summed over the shards)' if world > 1 else ''} equal "
                              f"the OpenMP oracle's run of the same workload ({os.path.relpath(FIXTURE, ROOT)})"

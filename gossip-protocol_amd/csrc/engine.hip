@@ -15,7 +15,7 @@
 #include <string>
 #include <vector>
 
-#include "../../include/gossip.h"
+#include "../../include/gossip_shard.h"
 #include "ae_sharded.h"
 #include "antientropy.h"
 #include "binned.h"
@@ -58,6 +58,14 @@ struct gossip_engine {
   // the engine's own (torch.distributed bound to the stream the engine launches on, as
   // gossip_hip.sharded binds it), so a buffer handed out needs no publishing sync either
   bool ordered = false;
+  // gossip_set_param "rccl_dev_collectives": the RCCL transport's device-value collectives
+  // (counts and partials read by RCCL from engine memory).  Off by default until they have run
+  // on a box with two or more GPUs; off, RCCL takes the base forms (read_dev + host collectives).
+  bool rccl_dev = false;
+  // gossip_round_wall: whole library-driven sharded rounds by class (dense / sparse / ANTIENTROPY)
+  double wall_ms[3] = {};
+  uint64_t wall_n[3] = {}, wall_link[3] = {};
+  hipEvent_t wall_ev[2] = {};
 
   uint64_t N = 0, Nl = 0, lo = 0, hi = 0, nown = 0;
   uint32_t R = 0, W = 0, k = 0, mode = 0, G = 1, rank = 0;
@@ -203,7 +211,11 @@ struct gossip_engine {
   uint8_t* xd_keep = nullptr;    // [nown] per sender: the edges that survive the filter (count pass -> emit)
   // class-coded state exchange for dense image rounds (sharded.h cc_*), plan kind 4
   bool cc_planned = false;
-  double cc_frac = 0.75;  // gossip_set_param "cc_frac": at most this global fraction of mixed nodes
+  double cc_frac = 0.75;
+  // gossip_set_param "link_gbps": sharded random-mode rounds pick sparse / dense by a per-rank
+  // cost model with a link term (shard_round_costs); 0 = the fixed sparse_frac thresholds
+  double link_gbps = 76.0;
+  double plan_cost[2] = {};  // the last plan's modelled sparse / dense ms (tools/shard_probe.py)  // gossip_set_param "cc_frac": at most this global fraction of mixed nodes
   uint64_t* cc_bits = nullptr;  // [G][cc_slot_words] every shard's bitmaps + prefix (all-gather in place)
   uint64_t* cc_vals = nullptr;  // [G][stride] the shards' mixed words
   uint64_t cc_vals_cap = 0, cc_stride = 0;
@@ -288,6 +300,8 @@ void free_all(gossip_engine* e) {
     for (auto& x : p)
       if (x) (void)hipEventDestroy(x);
   for (auto& x : e->ev_pre)
+    if (x) (void)hipEventDestroy(x);
+  for (auto& x : e->wall_ev)
     if (x) (void)hipEventDestroy(x);
   for (auto& p : e->evr)
     for (auto& x : p)
@@ -498,6 +512,42 @@ double sparse_frac_of(const gossip_engine* e) {
   // before exchange rounds: 1/25 (a round with ~5 % rare nodes is cheaper as a class-filtered
   // exchange round, profiles/r02_xdfilt/); before state all-gathers: 1/4
   return e->xd && e->xd_shards && e->G >= e->xd_shards ? 0.04 : 0.25;
+}
+
+// Per-rank cost model of one sharded round of the random modes, in ms: device time from the
+// measured rates plus link time = the bytes the rank sends over its links /
+// (link_gbps x the G - 1 links it uses, at most 7).  Only steers the plan (every kind computes
+// the same bits).  Device rates: a sparse round's Philox floor 2.3 ps per own node (round 0 at
+// 2^27 on one GPU: 311 us) plus 0.3 ns per edge with a rare end (rounds 6-7 at 2^27: 0.15-0.42
+// ns); a dense round on the state image 7.3 ps per image node + 47 ps per own node (N = 2 / 4
+// ranks x 2^26 / 2^25: 4.14 / 2.56 ms, profiles/r04_ad/); an exchange round 67 ps per own node
+// (G = 8 x 2^24: 1.13 ms, profiles/r02_xd/).  Link bytes per rank: sparse = the rare-list
+// all-gather (16 B per rare node of the shard to each other shard) + the off-shard pushes
+// (16 B items, ~k per rare node); state all-gather = 8 B per own node to each other shard
+// (class-coded: its bitmaps + prefixes, 20 B per 64 nodes, + 8 B per mixed node); exchange =
+// 40 (G - 1) / G B per own node (12-B items out, 8-B replies back, k = 2).
+struct ShardCosts {
+  double sparse, dense;
+  bool dense_xd, dense_cc;
+};
+ShardCosts shard_round_costs(const gossip_engine* e, const Est& x) {
+  // (Nl, not the own count: every rank must reach the same plan, also with ragged shards)
+  const double N = (double)e->N, G = (double)e->G, Nl = (double)e->Nl, k = (double)e->k;
+  const double rare = std::min(x.nz, N - x.full), rare_own = rare / G;
+  const double bw = e->link_gbps * 1e6 * std::min(G - 1.0, 7.0);  // bytes per ms
+  ShardCosts c{};
+  c.sparse = 2.3e-9 * Nl + 3e-7 * 2.0 * k * rare_own +
+             (16.0 * rare_own * (G - 1.0) + 16.0 * k * rare_own * (G - 1.0) / G) / bw;
+  c.dense_xd = e->xd && e->xd_shards && e->G >= e->xd_shards;
+  const double mixed = std::max(0.0, x.nz - x.full);
+  c.dense_cc = !c.dense_xd && e->cc_frac > 0 && mixed / N <= e->cc_frac;
+  if (c.dense_xd) {
+    c.dense = 6.7e-8 * Nl + 40.0 * (G - 1.0) / G * Nl / bw;
+  } else {
+    const double slice = c.dense_cc ? 20.0 / 64.0 * Nl + 8.0 * mixed / G : 8.0 * Nl;
+    c.dense = 7.3e-9 * N + 4.7e-8 * Nl + slice * (G - 1.0) / bw;
+  }
+  return c;
 }
 
 // sparse when the smaller rare class is at most sparse_frac * N; maj = which
@@ -785,7 +835,10 @@ int ae_round(gossip_engine* e) {
 // list did not overflow, it did not converge), so the sparse kernels of a round past convergence
 // or after an overflow return at once; the host reads every slot after one sync.  An overflowed
 // round left V, the bitmaps and the claims untouched: it is rerun dense (ae_dense_next), as
-// ae_round does.  The rounds and their results are those of the unpipelined loop.
+// ae_round does.  Every round's stats and state equal the unpipelined loop's; its path choice
+// need not: the plan (ae_plan_sparse) is made once per batch, so a round the unpipelined loop
+// would have planned dense (churn reviving stale nodes) may run sparse here, overflow and be
+// rerun dense.  That moves ae_sparse_rounds, ae_overflows and timer 2, never a result bit.
 int step_ae(gossip_engine* e, uint32_t max_rounds, gossip_round_stats_t* stats, uint64_t* infected,
             uint32_t* rounds_done) {
   const size_t pl = part_len(e), sw = pl + 2;  // a slot: the totals, then aux[0..1]
@@ -1355,6 +1408,11 @@ int gossip_set_param(gossip_engine_t* e, const char* name, double v) {
     e->ae_ahead = (uint32_t)v;
   } else if (n == "ordered_collectives") {
     e->ordered = v != 0;
+  } else if (n == "link_gbps") {
+    if (v < 0) return e->fail(GOSSIP_EINVAL, "link_gbps must be >= 0 (0 = fixed sparse_frac thresholds)");
+    e->link_gbps = v;
+  } else if (n == "rccl_dev_collectives") {
+    e->rccl_dev = v != 0;
   } else if (n == "mid_frac") {
     e->mid_frac = v;
   } else if (n == "filter_frac") {
@@ -1740,6 +1798,12 @@ int gossip_sharded_plan(gossip_engine_t* e, const uint64_t* total, int32_t* kind
   uint32_t maj = 0;
   bool all_d = false;
   e->sx_planned = choose_sparse(e, est_of(e, e->gtot.data()), &maj, &all_d);
+  if (!e->sparse_frac_set && e->link_gbps > 0) {  // the link-aware cost model decides instead
+    const ShardCosts c = shard_round_costs(e, est_of(e, e->gtot.data()));
+    e->sx_planned = c.sparse < c.dense;
+    e->plan_cost[0] = c.sparse;
+    e->plan_cost[1] = c.dense;
+  }
   e->sx_maj = maj;
   e->sx_alld = all_d;
   {  // the mid-level summary of the global rare bitmap (choose_sparse's rule, sharded summary)
@@ -2461,6 +2525,19 @@ int gossip_reset_timing(gossip_engine_t* e) {
     e->launches[w] = 0;
   }
   for (auto& r : e->evr_round) r = -1;  // (pending per-round events are dropped with the totals)
+  for (int c = 0; c < 3; ++c) {
+    e->wall_ms[c] = 0;
+    e->wall_n[c] = e->wall_link[c] = 0;
+  }
+  return GOSSIP_OK;
+}
+
+int gossip_round_wall(const gossip_engine_t* e, uint32_t cls, double* total_ms, uint64_t* rounds,
+                      uint64_t* link_bytes) {
+  if (!e || cls > 2) return GOSSIP_EINVAL;
+  if (total_ms) *total_ms = e->wall_ms[cls];
+  if (rounds) *rounds = e->wall_n[cls];
+  if (link_bytes) *link_bytes = e->wall_link[cls];
   return GOSSIP_OK;
 }
 
@@ -2558,6 +2635,31 @@ hipStream_t engine_stream(gossip_engine_t* e) { return e->stream; }
 int engine_device(const gossip_engine_t* e) { return e->device; }
 uint32_t engine_rank(const gossip_engine_t* e) { return e->rank; }
 uint32_t engine_shards(const gossip_engine_t* e) { return e->G; }
+bool engine_rccl_dev(const gossip_engine_t* e) { return e->rccl_dev; }
+
+// whole library-driven rounds (gossip_round_wall): an event on the engine's stream before the
+// plan, another after the commit (whose totals the host has read: the stream is drained)
+int engine_wall_begin(gossip_engine_t* e) {
+  if (!e->timing) return GOSSIP_OK;
+  if (!e->wall_ev[0]) {
+    HIP_OK(e, hipEventCreate(&e->wall_ev[0]));
+    HIP_OK(e, hipEventCreate(&e->wall_ev[1]));
+  }
+  HIP_OK(e, hipEventRecord(e->wall_ev[0], e->stream));
+  return GOSSIP_OK;
+}
+
+int engine_wall_end(gossip_engine_t* e, uint32_t cls, uint64_t link_bytes) {
+  e->wall_n[cls] += 1;
+  e->wall_link[cls] += link_bytes;
+  if (!e->timing || !e->wall_ev[0]) return GOSSIP_OK;
+  HIP_OK(e, hipEventRecord(e->wall_ev[1], e->stream));
+  HIP_OK(e, hipEventSynchronize(e->wall_ev[1]));
+  float ms = 0.f;
+  HIP_OK(e, hipEventElapsedTime(&ms, e->wall_ev[0], e->wall_ev[1]));
+  e->wall_ms[cls] += ms;
+  return GOSSIP_OK;
+}
 uint32_t engine_rumors(const gossip_engine_t* e) { return e->R; }
 uint32_t engine_mode(const gossip_engine_t* e) { return e->mode; }
 }  // namespace gossip

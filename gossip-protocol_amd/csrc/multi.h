@@ -12,7 +12,7 @@
 #include <string>
 #include <vector>
 
-#include "../../include/gossip.h"
+#include "../../include/gossip_shard.h"
 
 namespace gossip {
 
@@ -21,6 +21,9 @@ hipStream_t engine_stream(gossip_engine_t* e);
 int engine_device(const gossip_engine_t* e);
 uint32_t engine_rank(const gossip_engine_t* e);
 uint32_t engine_shards(const gossip_engine_t* e);
+bool engine_rccl_dev(const gossip_engine_t* e);  // gossip_set_param 'rccl_dev_collectives'
+int engine_wall_begin(gossip_engine_t* e);  // gossip_round_wall: a library-driven round starts
+int engine_wall_end(gossip_engine_t* e, uint32_t cls, uint64_t link_bytes);  // ... and ended
 uint32_t engine_rumors(const gossip_engine_t* e);
 uint32_t engine_mode(const gossip_engine_t* e);
 

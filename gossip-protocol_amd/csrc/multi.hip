@@ -306,8 +306,12 @@ class RcclTransport final : public Transport {
     return sync_all();
   }
 
-  // the device-value forms: RCCL reads engine memory, one pinned host read per local engine
+  // the device-value forms: RCCL reads engine memory, one pinned host read per local engine.
+  // Unverified on distinct GPUs, so they are opt-in (gossip_set_param "rccl_dev_collectives" on
+  // the first local engine); by default the base forms run (read_dev, then the host collectives).
+  bool dev_on() const { return engine_rccl_dev(eng_[0]); }
   int all_gather_dev(const std::vector<const uint64_t*>& one, std::vector<uint64_t>* all) override {
+    if (!dev_on()) return Transport::all_gather_dev(one, all);
     if (int rc = scratch(G_ * 8)) return rc;
     if (int rc = pinned(G_ * 8)) return rc;
     RCCL_OK(R.GroupStart());
@@ -325,6 +329,7 @@ class RcclTransport final : public Transport {
 
   int all_to_all_counts_dev(const std::vector<const uint64_t*>& cnt, std::vector<std::vector<uint64_t>>* sendc,
                             std::vector<std::vector<uint64_t>>* recvc) override {
+    if (!dev_on()) return Transport::all_to_all_counts_dev(cnt, sendc, recvc);
     if (int rc = scratch(G_ * 8)) return rc;
     if (int rc = pinned(eng_.size() * 2 * G_ * 8)) return rc;
     RCCL_OK(R.GroupStart());  // one value to and from every rank, the own one included
@@ -354,6 +359,7 @@ class RcclTransport final : public Transport {
   }
 
   int all_reduce_sum_dev(const std::vector<const uint64_t*>& part, size_t n, std::vector<uint64_t>* sum) override {
+    if (!dev_on()) return Transport::all_reduce_sum_dev(part, n, sum);
     if (int rc = scratch(n * 8)) return rc;
     if (int rc = pinned(n * 8)) return rc;
     RCCL_OK(R.GroupStart());  // out of place: the engines keep their own partials
@@ -507,8 +513,23 @@ struct Driver {
   Transport* tr;
   std::string* err;
   uint32_t G;
+  std::vector<uint64_t> lb;  // this round's bytes each local shard put on its links (gossip_round_wall)
 
   size_t n() const { return L.size(); }
+  // link-byte model of the collectives (what leaves the shard's GPU): an all-gather sends its
+  // slice to G - 1 shards, an all-to-all what is addressed to other shards, a ring all-reduce
+  // 2 (G - 1) / G of the vector
+  void lb_all_gather(uint64_t bytes) {
+    for (auto& x : lb) x += bytes * (G - 1);
+  }
+  void lb_all_to_all(const std::vector<std::vector<uint64_t>>& sendb) {
+    for (size_t i = 0; i < n(); ++i)
+      for (uint32_t q = 0; q < G; ++q)
+        if (q != engine_rank(L[i])) lb[i] += sendb[i][q];
+  }
+  void lb_all_reduce(uint64_t bytes) {
+    for (auto& x : lb) x += 2 * (G - 1) * bytes / G;
+  }
 
   int eng_fail(size_t i, int rc) {
     *err = std::string("shard ") + std::to_string(engine_rank(L[i])) + ": " + gossip_last_error(L[i]);
@@ -571,11 +592,13 @@ struct Driver {
       for (size_t i = 0; i < n(); ++i) ENG(i, gossip_cc_send(L[i], &bits[i], &nb[i], &vals[i], &cnt[i]));
       std::vector<uint64_t> counts;
       TR(tr->all_gather_u64(cnt, &counts));
+      lb_all_gather(8);
       const uint64_t stride = *std::max_element(counts.begin(), counts.end());
       for (size_t i = 0; i < n(); ++i) {
         ENG(i, gossip_cc_recv(L[i], stride, &recv[i], &rvals[i]));
         send[i] = bits[i];
       }
+      lb_all_gather(nb[0] + stride * 8);
       // the bitmaps, then the mixed words, in flight while the own-slice part of the round runs
       TR(tr->all_gather_start(recv, send, nb[0]));
       if (stride) {  // (the same side stream: joined together below)
@@ -594,6 +617,7 @@ struct Driver {
       }
       // the state image in flight while the own-slice part of the round runs
       TR(tr->all_gather_start(recv, send, nb[0]));
+      lb_all_gather(nb[0]);
       for (size_t i = 0; i < n(); ++i) ENG(i, gossip_dense_prepare(L[i]));
       TR(tr->join());
     }
@@ -610,6 +634,7 @@ struct Driver {
     const uint64_t stride = *std::max_element(counts.begin(), counts.end());
     for (size_t i = 0; i < n(); ++i) ENG(i, gossip_sparse_rare_recv(L[i], stride, &rrecv[i]));
     if (stride) TR(tr->all_gather(rrecv, std::vector<const void*>(rare.begin(), rare.end()), stride * 16));
+    lb_all_gather(8 + stride * 16);
     std::vector<std::vector<uint64_t>> oc, ic;
     std::vector<const uint64_t*> sc(n());
     for (size_t i = 0; i < n(); ++i) ENG(i, gossip_sparse_scan_dev(L[i], counts.data(), &out[i], &sc[i]));
@@ -625,6 +650,8 @@ struct Driver {
       }
     }
     TR(tr->all_to_all_v(in, ib, std::vector<const void*>(out.begin(), out.end()), ob));
+    lb_all_gather(8);  // (the counts)
+    lb_all_to_all(ob);
     for (size_t i = 0; i < n(); ++i) ENG(i, gossip_sparse_commit_dev(L[i], nin[i], &(*pd)[i]));
     return GOSSIP_OK;
   }
@@ -634,6 +661,7 @@ struct Driver {
     std::vector<uint64_t> nb(n());
     for (size_t i = 0; i < n(); ++i) ENG(i, gossip_xd_classes(L[i], &cls[i], &img[i], &nb[i]));
     if (nb[0]) TR(tr->all_gather(img, std::vector<const void*>(cls.begin(), cls.end()), nb[0]));
+    lb_all_gather(nb[0]);
     std::vector<std::vector<uint64_t>> oc, ic;
     std::vector<const uint64_t*> sc(n());
     for (size_t i = 0; i < n(); ++i) ENG(i, gossip_xd_requests_dev(L[i], &ids[i], &vals[i], &sc[i]));
@@ -659,6 +687,10 @@ struct Driver {
     }
     // the replies go back: what engine i received from q returns to q
     TR(tr->all_to_all_v(back, o8, std::vector<const void*>(rep.begin(), rep.end()), i8));
+    lb_all_gather(8);  // (the counts)
+    lb_all_to_all(o4);
+    lb_all_to_all(o8);
+    lb_all_to_all(i8);  // the replies go back
     for (size_t i = 0; i < n(); ++i) ENG(i, gossip_xd_finish_dev(L[i], &(*pd)[i]));
     return GOSSIP_OK;
   }
@@ -669,6 +701,7 @@ struct Driver {
     std::vector<uint64_t> nb(n());
     for (size_t i = 0; i < n(); ++i) ENG(i, gossip_exchange_buffers(L[i], &s[i], &recv[i], &nb[i]));
     TR(tr->all_gather(recv, std::vector<const void*>(s.begin(), s.end()), nb[0]));
+    lb_all_gather(nb[0] + 8);
     std::vector<std::vector<uint64_t>> oc(n(), std::vector<uint64_t>(G)), ic;
     for (size_t i = 0; i < n(); ++i) ENG(i, gossip_ae_requests(L[i], &req[i], oc[i].data()));
     TR(tr->all_to_all_counts(oc, &ic));
@@ -690,11 +723,15 @@ struct Driver {
       ENG(i, gossip_ae_response_recv(L[i], &back[i]));
     }
     TR(tr->all_to_all_v(back, op, std::vector<const void*>(resp.begin(), resp.end()), ip));
+    lb_all_to_all(oq);
+    lb_all_to_all(ip);  // the responses go back
     for (size_t i = 0; i < n(); ++i) ENG(i, gossip_ae_finish(L[i], (*part)[i].data()));
     return GOSSIP_OK;
   }
 
   int round(gossip_round_stats_t* st, std::vector<uint64_t>* total) {
+    lb.assign(n(), 0);
+    for (size_t i = 0; i < n(); ++i) ENG(i, engine_wall_begin(L[i]));
     int32_t kind = 0;
     if (int rc = plan(&kind)) return rc;
     const size_t plen = gossip_partial_len(L[0]);
@@ -714,11 +751,14 @@ struct Driver {
     if (rc) return rc;
     if (kind == 2) TR(tr->all_reduce_sum_u64(part, total));
     else TR(tr->all_reduce_sum_dev(pd, plen, total));
+    lb_all_reduce(plen * 8);
     for (size_t i = 0; i < n(); ++i) {
       gossip_round_stats_t s;
       ENG(i, gossip_round_commit(L[i], total->data(), &s));
       if (i == 0) *st = s;
     }
+    const uint32_t cls = kind == 1 ? 1u : kind == 2 ? 2u : 0u;
+    for (size_t i = 0; i < n(); ++i) ENG(i, engine_wall_end(L[i], cls, lb[i]));
     return GOSSIP_OK;
   }
 #undef ENG

@@ -119,6 +119,7 @@ SIGNATURES = [
     ("philox_device", C.c_int, [P, U32P, U32P, U32P, C.c_uint32]),
     ("kernel_time", C.c_int, [P, C.c_uint32, C.POINTER(C.c_double), U64P]),
     ("reset_timing", C.c_int, [P]),
+    ("round_wall", C.c_int, [P, C.c_uint32, C.POINTER(C.c_double), U64P, U64P]),
     # multi-GPU driven by the engine
     ("comm_unique_id", C.c_int, [C.c_char_p]),
     ("comm_init_rank", C.c_int, [P, C.c_char_p]),

@@ -458,6 +458,13 @@ class Engine(AbiEngine):
     def reset_timing(self):
         self._check(self._fn("reset_timing")(self._h))
 
+    def round_wall(self, cls: int):
+        """Library-driven sharded rounds of class cls (0 dense, 1 sparse, 2 ANTIENTROPY):
+        (whole-round ms incl. collectives, rounds, link bytes this shard sent); gossip_round_wall."""
+        ms, n, lb = C.c_double(), C.c_uint64(), C.c_uint64()
+        self._check(self._fn("round_wall")(self._h, C.c_uint32(cls), C.byref(ms), C.byref(n), C.byref(lb)))
+        return ms.value, n.value, lb.value
+
     def philox_device(self, ctr: np.ndarray, key) -> np.ndarray:
         ctr = np.ascontiguousarray(ctr, dtype=np.uint32).reshape(-1, 4)
         key = np.ascontiguousarray(key, dtype=np.uint32)

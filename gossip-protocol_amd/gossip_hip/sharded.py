@@ -73,6 +73,11 @@ class _Comm:
     def __init__(self, engine, group, direct: bool | None = None):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        # bytes this rank put on its links this round (the model of gossip_round_wall): an
+        # all-gather sends the slice to world - 1 ranks, an all-to-all what goes to other ranks,
+        # a ring all-reduce 2 (world - 1) / world of the vector
+        self.link = 0
         self.on_device = engine.on_device
         self.direct = engine.on_device and self.world > 1 and _device_collectives(group)
         if direct is not None:  # tests: the collectives on engine memory as RCCL would run them
@@ -82,7 +87,18 @@ class _Comm:
         if self.on_device:
             torch.cuda.synchronize()
 
+    def _lb_gather(self, send: torch.Tensor):
+        self.link += send.numel() * send.element_size() * (self.world - 1)
+
+    def _lb_a2a(self, send: torch.Tensor, send_splits):
+        el = send.element_size()
+        self.link += sum(int(c) * el for q, c in enumerate(send_splits) if q != self.rank)
+
+    def _lb_reduce(self, t: torch.Tensor):
+        self.link += 2 * (self.world - 1) * t.numel() * t.element_size() // max(self.world, 1)
+
     def all_gather(self, recv: torch.Tensor, send: torch.Tensor):
+        self._lb_gather(send)
         if self.direct:
             dist.all_gather_into_tensor(recv, send, group=self.group)
             return
@@ -95,11 +111,13 @@ class _Comm:
         """Device collectives: returns the pending work (the caller's stream waits on wait());
         staged collectives complete before returning None."""
         if self.direct:
+            self._lb_gather(send)
             return dist.all_gather_into_tensor(recv, send, group=self.group, async_op=True)
         self.all_gather(recv, send)
         return None
 
     def all_to_all(self, recv: torch.Tensor, send: torch.Tensor, recv_splits, send_splits):
+        self._lb_a2a(send, send_splits)
         if self.direct:
             dist.all_to_all_single(recv, send, output_split_sizes=recv_splits, input_split_sizes=send_splits,
                                    group=self.group)
@@ -116,20 +134,24 @@ class _Comm:
 
     def all_reduce_max(self, values: np.ndarray) -> np.ndarray:
         t = self.small(np.asarray(values, dtype=np.int64))
+        self._lb_reduce(t)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         return t.cpu().numpy()
 
     def all_reduce_sum(self, partial: np.ndarray) -> np.ndarray:
         t = self.small(partial.view(np.int64))
+        self._lb_reduce(t)
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
         return t.cpu().numpy().view(np.uint64)
 
     def all_gather_small(self, value: int) -> list:
+        self.link += 8 * (self.world - 1)
         out = self.small(np.zeros(self.world))
         dist.all_gather_into_tensor(out, self.small([value]), group=self.group)
         return [int(x) for x in out.cpu()]
 
     def all_to_all_small(self, values) -> list:
+        self.link += 8 * (self.world - 1)
         out = self.small(np.zeros(self.world))
         dist.all_to_all_single(out, self.small(values), group=self.group)
         return [int(x) for x in out.cpu()]
@@ -138,6 +160,7 @@ class _Comm:
     # engine's (= torch's current) stream and one host read of its result is the round's only
     # sync for that exchange
     def dev_all_gather_one(self, ptr: int) -> list:
+        self.link += 8 * (self.world - 1)
         out = torch.empty(self.world, dtype=torch.int64, device="cuda")
         dist.all_gather_into_tensor(out, _as_tensor(ptr, 8, True), group=self.group)
         return [int(x) for x in out.cpu()]
@@ -145,6 +168,7 @@ class _Comm:
     def dev_all_to_all_counts(self, ptr: int):
         """(sent counts, received counts) from the G counts at ptr."""
         send = _as_tensor(ptr, self.world * 8, True)
+        self.link += 8 * (self.world - 1)
         recv = torch.empty_like(send)
         dist.all_to_all_single(recv, send, group=self.group)
         both = [int(x) for x in torch.cat([send, recv]).cpu()]
@@ -152,6 +176,7 @@ class _Comm:
 
     def dev_all_reduce_sum(self, ptr: int, n: int) -> np.ndarray:
         t = _as_tensor(ptr, n * 8, True).clone()  # (the engine keeps its own partials)
+        self._lb_reduce(t)
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
         return t.cpu().numpy().view(np.uint64)
 
@@ -280,18 +305,21 @@ def _cc_round(engine, comm: _Comm) -> np.ndarray:
     return engine.round_compute()
 
 
-def _bind_stream(engine, comm: _Comm):
+def _bind_stream(engine, comm: _Comm) -> bool:
     """Device collectives are enqueued on torch's current stream (the RCCL stream waits for
     it, and work.wait() / a synchronous collective make it wait in turn): the engine must
     launch on that same stream, or its kernels could read the image before the all-gather
     wrote it.  torch's default stream is the null stream (cuda_stream 0), which
-    gossip_set_stream binds as such."""
+    gossip_set_stream binds as such.  Returns True when it also set ordered_collectives (torch's
+    collectives wait for this stream, so the per-kind calls skip their publishing sync); the
+    caller clears it when the round ends (sharded_round), so the flag never outlives the round
+    that bound the stream (a later host driver, staged collectives or another stream get the
+    sync back)."""
     if comm.direct and comm.on_device:
         engine.set_stream(torch.cuda.current_stream().cuda_stream)
-        # torch's collectives wait for this stream: no publishing sync in the per-kind calls
-        if not getattr(engine, "_ordered", False):
-            engine.set_param("ordered_collectives", 1)
-            engine._ordered = True
+        engine.set_param("ordered_collectives", 1)
+        return True
+    return False
 
 
 def _ae_round(engine, comm: _Comm) -> np.ndarray:
@@ -317,30 +345,39 @@ def _ae_round(engine, comm: _Comm) -> np.ndarray:
     return engine.ae_finish()
 
 
-def sharded_round(engine, group=None, kinds: list | None = None, direct: bool | None = None) -> dict:
+def sharded_round(engine, group=None, kinds: list | None = None, direct: bool | None = None,
+                  trace: list | None = None) -> dict:
     """Runs one round of a sharded engine; every rank must call it.  With RCCL the engine is
     bound to the caller's current torch stream, so every kernel is ordered after the
     collectives that feed it.  kinds: the round's plan kind is appended to it.  direct (tests):
-    force the in-place collective path that RCCL takes, also for host engines over gloo."""
+    force the in-place collective path that RCCL takes, also for host engines over gloo.
+    trace: gets {"kind", "link_bytes"} of the round (the bytes this rank sent over its links)."""
     comm = _Comm(engine, group, direct)
-    _bind_stream(engine, comm)
-    kind = _plan(engine, comm)
-    if kinds is not None:
-        kinds.append(kind)
-    if kind == 2:
-        partial = _ae_round(engine, comm)
-    elif kind == 3:
-        partial = _xd_round(engine, comm)
-    elif kind == 4:
-        partial = _cc_round(engine, comm)
-    elif kind == 1:
-        partial = _sparse_round(engine, comm)
-    else:
-        partial = _dense_round(engine, comm)
-    # the device-value path returns the global sum already (one all-reduce on engine memory)
-    if comm.world > 1 and not (kind != 2 and _dev_values(engine, comm)):
-        partial = comm.all_reduce_sum(partial)
-    return engine.round_commit(partial)
+    ordered = _bind_stream(engine, comm)
+    try:
+        kind = _plan(engine, comm)
+        if kinds is not None:
+            kinds.append(kind)
+        if kind == 2:
+            partial = _ae_round(engine, comm)
+        elif kind == 3:
+            partial = _xd_round(engine, comm)
+        elif kind == 4:
+            partial = _cc_round(engine, comm)
+        elif kind == 1:
+            partial = _sparse_round(engine, comm)
+        else:
+            partial = _dense_round(engine, comm)
+        # the device-value path returns the global sum already (one all-reduce on engine memory)
+        if comm.world > 1 and not (kind != 2 and _dev_values(engine, comm)):
+            partial = comm.all_reduce_sum(partial)
+        st = engine.round_commit(partial)
+        if trace is not None:
+            trace.append({"kind": kind, "link_bytes": comm.link})
+        return st
+    finally:
+        if ordered:  # scoped to this round (ADVICE r04: the flag must not outlive the binding)
+            engine.set_param("ordered_collectives", 0)
 
 
 def _all_ranks(ok: bool, group=None) -> bool:
@@ -383,13 +420,25 @@ def init_engine_comm(engine, group=None) -> str | None:
     return None
 
 
-def sharded_run(engine, max_rounds: int, group=None, kinds: list | None = None, direct: bool | None = None) -> list:
-    """Rounds until converged (same stop rule as gossip_step); kinds collects the plan kinds."""
-    if engine.on_device and torch.cuda.is_available():
+def sharded_run(engine, max_rounds: int, group=None, kinds: list | None = None, direct: bool | None = None,
+                trace: list | None = None) -> list:
+    """Rounds until converged (same stop rule as gossip_step); kinds collects the plan kinds.
+    trace: one entry per round, {"kind", "link_bytes"} and, on a device engine, "events" = a
+    timing torch.cuda.Event pair on the current stream around the whole round (plan,
+    collectives, kernels, host reads: the RCCL collectives are ordered on that stream)."""
+    on_dev = engine.on_device and torch.cuda.is_available()
+    if on_dev:
         engine.set_stream(torch.cuda.current_stream().cuda_stream)
     out = []
     for _ in range(max_rounds):
-        st = sharded_round(engine, group, kinds, direct)
+        ev = None
+        if trace is not None and on_dev:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+        st = sharded_round(engine, group, kinds, direct, trace)
+        if ev is not None:
+            ev[1].record()
+            trace[-1]["events"] = ev
         out.append(st)
         if st["converged"] or (engine.cfg.mode == 0 and st["messages"] == 0):
             break

@@ -87,6 +87,7 @@ struct oracle_sim {
    * word), the own mixed words, every shard's at q * cc_stride */
   int cc_planned;
   double cc_frac;
+  double link_gbps; /* engine.hip link_gbps: the link-aware plan (0 = the fixed thresholds) */
   uint64_t *cc_bits, *cc_send, *cc_vals, cc_stride;
 };
 
@@ -253,6 +254,7 @@ int oracle_create(const gossip_config_t* cfg, int threads, oracle_sim_t** out) {
   s->sparse_frac = 0.25;
   s->xd_shards = 6;
   s->cc_frac = 0.75;
+  s->link_gbps = 76.0;
   s->xd_filter_frac = 0.6; /* engine.hip xd_filter_frac */
   s->flood_edges = s->mode == GOSSIP_MODE_FLOOD && faulty;
   if (s->flood_edges) {
@@ -880,6 +882,25 @@ int oracle_sharded_plan(oracle_sim_t* s, const uint64_t* total, int32_t* kind) {
   /* the engine's default threshold (engine.hip sparse_frac_of): 1/25 before exchange rounds */
   const double frac = s->sparse_frac_set ? s->sparse_frac : s->xd_shards && s->G >= s->xd_shards ? 0.04 : 0.25;
   s->planned = (notfull < nz ? notfull : nz) <= frac * (double)s->N;
+  if (!s->sparse_frac_set && s->link_gbps > 0) { /* the engine's link-aware cost model (shard_round_costs) */
+    const double N = (double)s->N, G = (double)s->G, Nl = (double)s->Nl, k = (double)s->k;
+    const double full_n = (double)s->gtot[0];
+    const double rare = nz < N - full_n ? nz : N - full_n, rare_own = rare / G;
+    const double bw = s->link_gbps * 1e6 * (G - 1.0 < 7.0 ? G - 1.0 : 7.0);
+    const double c_sparse = 2.3e-9 * Nl + 3e-7 * 2.0 * k * rare_own +
+                            (16.0 * rare_own * (G - 1.0) + 16.0 * k * rare_own * (G - 1.0) / G) / bw;
+    const int dense_xd = s->xd_shards && s->G >= s->xd_shards;
+    const double mixed_n = nz - full_n > 0.0 ? nz - full_n : 0.0;
+    const int dense_cc = !dense_xd && s->cc_frac > 0 && mixed_n / N <= s->cc_frac;
+    double c_dense;
+    if (dense_xd) {
+      c_dense = 6.7e-8 * Nl + 40.0 * (G - 1.0) / G * Nl / bw;
+    } else {
+      const double slice = dense_cc ? 20.0 / 64.0 * Nl + 8.0 * mixed_n / G : 8.0 * Nl;
+      c_dense = 7.3e-9 * N + 4.7e-8 * Nl + slice * (G - 1.0) / bw;
+    }
+    s->planned = c_sparse < c_dense;
+  }
   s->xd_planned = !s->planned && s->xd_shards && s->G >= s->xd_shards;
   /* the engine's dense_filter of the global totals (engine.hip): pulls from empty peers once more
    * than xd_filter_frac of the nodes are empty, pushes into full peers likewise */
@@ -1245,7 +1266,8 @@ int oracle_cc_expand(oracle_sim_t* s, const uint64_t* counts) {
   return GOSSIP_OK;
 }
 
-/* gossip_set_param: the engine's tuning knobs.  Only sparse_frac matters here (it picks the
+/* gossip_set_param: the engine's tuning knobs.  sparse_frac, link_gbps, cc_frac, xd_shards and
+ * xd_filter_frac matter here (they pick the
  * sharded round protocol, which the gloo tests exercise); the rest steer engine kernel
  * choices that this restatement does not have, and are accepted as no-ops. */
 int oracle_set_param(oracle_sim_t* s, const char* name, double value) {
@@ -1253,6 +1275,11 @@ int oracle_set_param(oracle_sim_t* s, const char* name, double value) {
   if (!strcmp(name, "sparse_frac")) {
     s->sparse_frac = value;
     s->sparse_frac_set = 1;
+    return GOSSIP_OK;
+  }
+  if (!strcmp(name, "link_gbps")) {
+    if (value < 0) return GOSSIP_EINVAL;
+    s->link_gbps = value;
     return GOSSIP_OK;
   }
   if (!strcmp(name, "cc_frac")) {
@@ -1273,7 +1300,7 @@ int oracle_set_param(oracle_sim_t* s, const char* name, double value) {
   /* the engine's performance knobs (path choice, grids): no effect on the rounds' results */
   const char* known[] = {"alld_frac",  "filter_frac", "ahead",        "serve_grid",   "apply_grid", "push_waves",
                          "ae_sparse",  "ae_cap",      "sparse_direct", "mid_frac",    "ae_dense_bin", "ae_dense_cap",
-                         "ae_ahead",   "ordered_collectives", "ae_dense_filter"};
+                         "ae_ahead",   "ordered_collectives", "ae_dense_filter", "rccl_dev_collectives"};
   for (size_t i = 0; i < sizeof known / sizeof known[0]; ++i)
     if (!strcmp(name, known[i])) return GOSSIP_OK;
   return GOSSIP_EINVAL;

@@ -23,7 +23,7 @@
 #define GOSSIP_ORACLE_H_
 
 #include <stdint.h>
-#include "../include/gossip.h"
+#include "../include/gossip_shard.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -53,7 +53,7 @@ uint64_t oracle_partial_len(const oracle_sim_t* s);
 int oracle_exchange_buffers(oracle_sim_t* s, void** send, void** recv, uint64_t* send_bytes);
 int oracle_round_compute(oracle_sim_t* s, uint64_t* partial);
 int oracle_round_commit(oracle_sim_t* s, const uint64_t* total, gossip_round_stats_t* stats);
-/* sparse sharded rounds: the protocol of include/gossip.h (gossip_sharded_plan ...) */
+/* sparse sharded rounds: the protocol of include/gossip_shard.h (gossip_sharded_plan ...) */
 int oracle_sharded_plan(oracle_sim_t* s, const uint64_t* total, int32_t* kind);
 int oracle_local_totals(oracle_sim_t* s, uint64_t* partial);
 int oracle_sparse_rare(oracle_sim_t* s, void** send, uint64_t* count);

@@ -12,10 +12,25 @@ from gossip_hip import engine as eng_mod
 from gossip_hip import _abi
 
 
-def header_functions():
-    src = open(os.path.join(ROOT, "include", "gossip.h")).read()
+def header_functions(names=("gossip.h", "gossip_shard.h")):
+    src = "".join(open(os.path.join(ROOT, "include", h)).read() for h in names)
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(gossip_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_headers_split_the_contract_from_the_shard_protocol():
+    """gossip.h is the drop-in contract (create, topology, inject, step, read, comm init, groups,
+    timing); the per-kind steps of a host-driven sharded round live in gossip_shard.h only."""
+    core, shard = set(header_functions(("gossip.h",))), set(header_functions(("gossip_shard.h",)))
+    assert not core & shard
+    for f in ("gossip_create", "gossip_set_topology_csr", "gossip_inject", "gossip_step", "gossip_read_bitset",
+              "gossip_comm_init_rank", "gossip_group_step"):
+        assert f in core, f
+    for f in core | shard:
+        protocol = re.match(r"gossip_(xd|cc|sparse|ae)_", f) or f.endswith("_dev") or f in (
+            "gossip_exchange_buffers", "gossip_round_compute", "gossip_round_commit", "gossip_sharded_plan",
+            "gossip_dense_prepare", "gossip_local_totals", "gossip_partial_len")
+        assert bool(protocol) == (f in shard), f
 
 
 def test_library_exports_every_declared_symbol():

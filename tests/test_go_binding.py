@@ -8,11 +8,13 @@ import re
 from conftest import ROOT
 
 HEADER = os.path.join(ROOT, "include", "gossip.h")
+SHARD_HEADER = os.path.join(ROOT, "include", "gossip_shard.h")
 BINDING = os.path.join(ROOT, "gossipgpu", "gossipgpu.go")
+SHARD_BINDING = os.path.join(ROOT, "gossipgpu", "gossipgpu_shard.go")
 
 
-def _header():
-    return re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+def _header(path=HEADER):
+    return re.sub(r"/\*.*?\*/", "", open(path).read(), flags=re.S)
 
 
 def _struct_fields(src, name):
@@ -21,11 +23,15 @@ def _struct_fields(src, name):
 
 
 def test_binding_calls_exactly_the_header_functions():
-    hdr = set(re.findall(r"\b(gossip_[a-z_0-9]+)\s*\(", _header()))
-    go = open(BINDING).read()
-    called = set(re.findall(r"\bC\.(gossip_[a-z_0-9]+)\s*\(", go))
-    assert called <= hdr, called - hdr
-    assert called == hdr, hdr - called  # every entry point has a Go method
+    """gossipgpu.go binds gossip.h (the drop-in contract), gossipgpu_shard.go binds gossip_shard.h
+    (the per-kind steps of a host-driven sharded round), each exactly."""
+    for header, binding in ((HEADER, BINDING), (SHARD_HEADER, SHARD_BINDING)):
+        hdr = set(re.findall(r"\b(gossip_[a-z_0-9]+)\s*\(", _header(header)))
+        go = open(binding).read()
+        called = set(re.findall(r"\bC\.(gossip_[a-z_0-9]+)\s*\(", go))
+        assert called <= hdr, (binding, called - hdr)
+        assert called == hdr, (binding, hdr - called)  # every entry point has a Go method
+    assert '#include "gossip_shard.h"' in open(SHARD_BINDING).read()
 
 
 def test_binding_constants_exist():
@@ -33,6 +39,9 @@ def test_binding_constants_exist():
     go = open(BINDING).read()
     for const in set(re.findall(r"\bC\.(GOSSIP_[A-Z_0-9]+)", go)):
         assert re.search(r"\b" + const + r"\b", hdr), const
+    shard = _header(SHARD_HEADER)
+    for const in set(re.findall(r"\bC\.(GOSSIP_[A-Z_0-9]+)", open(SHARD_BINDING).read())):
+        assert re.search(r"\b" + const + r"\b", hdr + shard), const
     assert "const ABIVersion = " + re.search(r"GOSSIP_ABI_VERSION (\d+)u", hdr).group(1) in go
 
 

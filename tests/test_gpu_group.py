@@ -121,16 +121,19 @@ def _rccl_devices(G):
 RCCL_PLANS = ["auto", "sparse", "classcoded", "exchange"]
 
 
+@pytest.mark.parametrize("dev", [0, 1])
 @pytest.mark.parametrize("plan", RCCL_PLANS)
 @pytest.mark.parametrize("G", [2, 4, 8])
-def test_rccl_group_equals_one_engine(plan, G):
+def test_rccl_group_equals_one_engine(plan, G, dev):
     """The RCCL transport (transport 1: ncclCommInitAll over distinct devices, collectives on the
     engines' streams, the side-stream all-gather, grouped ncclSend / ncclRecv all-to-alls) against
-    one engine: every plan kind, per-round stats, per-rumor counts, final state."""
+    one engine: every plan kind, per-round stats, per-rumor counts, final state.  dev 1 turns on
+    the opt-in device-value collectives (param rccl_dev_collectives; off by default)."""
     devs = _rccl_devices(G)
     mode, k, R, N, seed = "pushpull", 2, 64, (1 << 20) + 77, 0x5EED0004
     want, full = _one_engine(mode, k, R, N, seed)
     params = dict(PLANS[plan], **({"xd_shards": 2} if plan in ("exchange", "auto") else {}))
+    params["rccl_dev_collectives"] = dev
     with Group(N, R, mode, k, seed, flags=1, n_shards=G, devices=devs, transport=1, params=params) as g:
         assert g.transport == 1
         g.inject_random()

@@ -119,8 +119,10 @@ def test_two_ranks_equal_one(case, plan, world=2, direct=None):
             assert set(kinds) == {0}  # FLOOD and W > 1: the plain state all-gather only
         elif plan in PLAN_KINDS:
             assert set(kinds) == PLAN_KINDS[plan]
-        elif plan == "auto":
+        elif plan == "auto" and N >= 1000:
             assert 4 in kinds and 1 in kinds  # sparse rounds and class-coded dense rounds at G < xd_shards
+        elif plan == "auto":  # a few nodes: the link-aware cost model may keep every round dense
+            assert set(kinds) <= {0, 1, 4}
 
 
 @pytest.mark.parametrize("plan", ["auto", "sparse", "dense", "exchange", "classcoded"])
