@@ -60,6 +60,9 @@ struct BinGeom {
   uint32_t push_waves;   // push-pull apply: waves [0, push_waves) walk the pushes, the rest the responses
   uint32_t aos;          // push records also packed {value, id} (BinBufs::prec; one shard, big regions)
   uint32_t split;        // one shard: record ids as two u16 arrays (BinBufs::dst / src) instead of ids
+  uint32_t lr;           // host only (one shard, split): serve reads its ids in long runs (BinBufs::dst2)
+  uint32_t lr_nb;        // tiles per block of the ids' regrouping (bin_dst_group_kernel)
+  uint32_t lr_ng;        // region groups (kLrG regions each)
 };
 
 // big: regions of up to 2 * kMaxSenders senders and 2 * kRecPerRegion records (one shard
@@ -78,6 +81,11 @@ struct BinBufs {
   uint16_t* offT;   // [nt_d + 1][nt_s]
   uint64_t* nzb;    // occupancy bitmaps of S_{t+1} written by K3 (frontier.h), or null
   uint64_t* fullb;
+  // lr: dst regrouped per group of kLrG regions (binned.hip bin_dst_group_kernel): tile T's runs of
+  // group g concatenated in region order at dst2[base2[T * lr_ng + g]] (the group's span of the
+  // record index space holds its segments)
+  uint16_t* dst2;   // [nt_s][rp]
+  uint32_t* base2;  // [nt_d][lr_ng]
 };
 
 size_t bin_bytes(const BinGeom& g);

@@ -23,6 +23,8 @@
 //
 // OR is commutative and idempotent and every read is of S_t, so the record
 // order inside a run (decided by LDS atomics) never changes a result bit.
+#include <type_traits>
+
 #include "binned.h"
 #include "philox.h"
 #include "round.h"
@@ -802,7 +804,16 @@ __device__ __forceinline__ void for_each_run_record_pipe(const BinGeom& g, const
         rec[u] = f < total ? wl[rank & (kRuns - 1u)] + (int32_t)f : -1;
       }
       wave_sync();  // the next window rewrites wm/wl
-      Buf nb = load(rec);
+      Buf nb;
+      if constexpr (std::is_invocable_v<LD&, const int32_t*, const int32_t*, uint32_t>) {
+        // (serve's long-run ids: the record's index f in the group's concatenation, and the group)
+        int32_t fx[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) fx[u] = rec[u] >= 0 ? (int32_t)(f0 + u * 64 + lane) : -1;
+        nb = load(rec, fx, s0);
+      } else {
+        nb = load(rec);
+      }
       if (have) proc(pend);
       pend = nb;
       have = true;
@@ -828,6 +839,7 @@ constexpr int kUnrollPipe = 4;  // records per lane and window in the pipelined 
 // us, 2^24 equal; 8 over 256 runs, 16 over 128, and apply's push walk over 128 runs or with 6 / 8 records per lane: slower
 // (profiles/r04_ak/).
 constexpr int kServeU = 8, kServeRPL = 2, kPushRPL = 1;
+constexpr uint32_t kLrG = 64 * kServeRPL;  // regions per group of serve's long-run ids (BinGeom::lr)
 
 // The pushes aimed at tile X (its runs in every sender region) ORed into acc,
 // by the waves [0, nwaves) (0: all).  VZ: the record id's no-push flag.
@@ -903,7 +915,10 @@ __device__ __forceinline__ void tile_regs_load(uint4 (&x)[Q], const uint64_t* __
 // every record aimed at T from a sender that is not yet fully informed gets
 // its pull response S_t[p] written next to it when nonzero (every one, in dense rounds).
 // VF: the record id's no-pull flag (kIdVF; exchange rounds' binned items: kXbVF).
-template <uint32_t VF, bool SPLIT = false>
+// LR (one shard, split ids): the ids come from dst2, regrouped by bin_dst_group_kernel so that a
+// wave group's records (kLrG consecutive regions' runs for tile T, in region order) are one
+// contiguous stretch: dst2[base2[T][g] + f] for the record at index f of group g's walk.
+template <uint32_t VF, bool SPLIT = false, bool LR = false>
 __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, const uint64_t* __restrict__ S, BinBufs b,
                                                                   uint32_t R, IdxRange tr) {
   __shared__ unsigned long long img[kTileD];
@@ -927,28 +942,157 @@ __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, cons
   uint64_t* __restrict__ gresp = b.resp;
   const uint16_t* rowb = b.offT + (size_t)T * g.nt_s;
   constexpr int U = kServeU;
-  for_each_run_record_pipe<U, IdBuf<U>, kServeRPL>(g, rowb, rowb + g.nt_s, wmask, wlist, [&](const int32_t* rec) {
-    IdBuf<U> bf;
-#pragma unroll
-    for (int u = 0; u < U; ++u) bf.rec[u] = rec[u];
-    if constexpr (SPLIT) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) bf.id[u] = (uint32_t)*(&b.dst[rec[u] >= 0 ? rec[u] : 0]);
-    } else {
-#pragma unroll
-      for (int u = 0; u < U; ++u) bf.id[u] = *(&gids[rec[u] >= 0 ? rec[u] : 0]);
-    }
-    return bf;
-  }, [&](const IdBuf<U>& bf) {
+  auto proc = [&](const IdBuf<U>& bf) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t id = SPLIT ? id_of_dst(bf.id[u]) : bf.id[u];
       if (bf.rec[u] < 0 || (id & VF)) continue;
       gresp[bf.rec[u]] = (uint64_t)img[id & (kTileD - 1)];
     }
-  });
+  };
+  if constexpr (LR) {
+    // wave w walks the groups w, w + 16, ... of the tile: their dst2 bases, one per lane
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t gw = wave + (kTileThreads / 64) * lane;
+    const uint32_t my2 = gw < g.lr_ng ? b.base2[(size_t)T * g.lr_ng + gw] : 0u;
+    for_each_run_record_pipe<U, IdBuf<U>, kServeRPL>(g, rowb, rowb + g.nt_s, wmask, wlist,
+        [&](const int32_t* rec, const int32_t* fx, uint32_t s0) {
+      const uint32_t g2 = __shfl(my2, (int)((s0 / kLrG - wave) / (kTileThreads / 64)), 64);
+      IdBuf<U> bf;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        bf.rec[u] = rec[u];
+        bf.id[u] = (uint32_t)*(&b.dst2[fx[u] >= 0 ? g2 + (uint32_t)fx[u] : 0u]);
+      }
+      return bf;
+    }, proc);
+  } else {
+    for_each_run_record_pipe<U, IdBuf<U>, kServeRPL>(g, rowb, rowb + g.nt_s, wmask, wlist, [&](const int32_t* rec) {
+      IdBuf<U> bf;
+#pragma unroll
+      for (int u = 0; u < U; ++u) bf.rec[u] = rec[u];
+      if constexpr (SPLIT) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) bf.id[u] = (uint32_t)*(&b.dst[rec[u] >= 0 ? rec[u] : 0]);
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u) bf.id[u] = *(&gids[rec[u] >= 0 ? rec[u] : 0]);
+      }
+      return bf;
+    }, proc);
+  }
   }
 }
+
+// --- serve's ids in long runs (BinGeom::lr) ------------------------------
+// At 2^27 nodes a (region, tile) run holds ~4 records, so serve's id walk reads one 8-B piece
+// per run, each from another line (the lines are shared by neighbouring tiles' runs, which other
+// blocks walk at other times): ~0.75 ms of the 2 ms serve (profiles/r04_n/).  This pass regroups
+// the ids once per round, per group of kLrG regions (= serve's runs per wave group) and block of
+// lr_nb tiles: tile T's runs of the group, concatenated in region order, become one stretch of
+// dst2 at base2[T][g].  A block reads its group's pieces (each region's ids for the lr_nb tiles:
+// one contiguous piece), sorts them by tile in LDS and writes each tile's stretch contiguously.
+// The segments of a group's blocks tile the group's own span of the record index space (its
+// regions' record counts add up to it), so dst2 has the size of dst.
+constexpr uint32_t kLrMaxNB = 64;
+constexpr uint32_t kLrCap = 36864;  // ids staged per block; a larger segment takes the direct path
+constexpr int kLrThreads = 1024;
+static_assert(kLrG == 64 * kServeRPL, "a regrouped stretch is one wave group of serve's walk");
+
+__global__ __launch_bounds__(kLrThreads) void bin_dst_group_kernel(BinGeom g, BinBufs b) {
+  __shared__ uint16_t offs[kLrG][kLrMaxNB + 1];  // each region's run starts for the block's tiles
+  __shared__ uint32_t pre[kLrG][kLrMaxNB];       // a run's start inside its tile's stretch
+  __shared__ uint32_t tstart[kLrMaxNB + 1];      // each tile's stretch inside the segment; [ntl] = size
+  __shared__ uint16_t stage[kLrCap];
+  __shared__ uint32_t scr[kLrThreads / 64 + 1];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t nbk = (g.nt_d + g.lr_nb - 1) / g.lr_nb;
+  const uint32_t gi = blockIdx.x / nbk, bk = blockIdx.x % nbk;
+  const uint32_t r0 = gi * kLrG, nr = min(kLrG, g.nt_s - r0);
+  const uint32_t T0 = bk * g.lr_nb, ntl = min(g.lr_nb, g.nt_d - T0);
+  for (uint32_t i = tid; i < nr * (ntl + 1); i += kLrThreads) {
+    const uint32_t ri = i / (ntl + 1), ti = i % (ntl + 1);
+    offs[ri][ti] = b.off[(size_t)(r0 + ri) * (g.nt_d + 1) + T0 + ti];
+  }
+  __syncthreads();
+  if (tid < ntl) {  // tile tid: its runs in region order
+    uint32_t run = 0;
+    for (uint32_t ri = 0; ri < nr; ++ri) {
+      pre[ri][tid] = run;
+      run += (uint32_t)offs[ri][tid + 1] - offs[ri][tid];
+    }
+    tstart[tid] = run;  // (the total, scanned below)
+  }
+  // the segment starts after every record of the group's regions in the tiles before T0
+  uint32_t seg0;
+  block_exscan<kLrThreads>(tid < nr ? (uint32_t)offs[tid][0] : 0u, scr, &seg0);  // (syncs)
+  if (tid < 64) {  // tile stretches: exclusive scan of the totals (ntl <= 64 = one wave)
+    const uint32_t c = lane < ntl ? tstart[lane] : 0u;
+    uint32_t inc = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o, 64);
+      if (lane >= (uint32_t)o) inc += y;
+    }
+    if (lane < ntl) tstart[lane] = inc - c;
+    if (lane == 63) tstart[ntl] = inc;
+  }
+  __syncthreads();
+  const uint32_t total = tstart[ntl];
+  const size_t segstart = (size_t)r0 * g.rp + seg0;
+  if (tid < ntl) b.base2[(size_t)(T0 + tid) * g.lr_ng + gi] = (uint32_t)(segstart + tstart[tid]);
+  const bool staged = total <= kLrCap;  // else (never at random peers' sizes) straight to dst2
+  // lane = tile (sub-run (ri, T0 + lane)): its ids go to one place in the tile's stretch; a wave
+  // takes 2 regions at a time and issues every load of both before any is stored (one memory
+  // round trip per 2 regions; the lanes of a load instruction read within the two pieces)
+  constexpr uint32_t kL = 8;
+  for (uint32_t ri0 = 2 * wave; ri0 < nr; ri0 += 2 * (kLrThreads / 64)) {
+    uint32_t a[2], len[2], dpos[2];
+    const uint16_t* src[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t ri = min(ri0 + h, nr - 1);
+      const bool on = lane < ntl && ri0 + h < nr;
+      a[h] = on ? offs[ri][lane] : 0u;
+      len[h] = on ? (uint32_t)offs[ri][lane + 1] - a[h] : 0u;
+      dpos[h] = on ? tstart[lane] + pre[ri][lane] : 0u;
+      src[h] = b.dst + (size_t)(r0 + ri) * g.rp;
+    }
+    uint32_t most = max(len[0], len[1]);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) most = max(most, (uint32_t)__shfl_xor((int)most, o, 64));
+    for (uint32_t i0 = 0; i0 < most; i0 += kL) {
+      uint16_t v[2][kL];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (uint32_t i = 0; i < kL; ++i) v[h][i] = i0 + i < len[h] ? src[h][a[h] + i0 + i] : (uint16_t)0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (uint32_t i = 0; i < kL; ++i) {
+          if (i0 + i >= len[h]) break;
+          if (staged) stage[dpos[h] + i0 + i] = v[h][i];
+          else b.dst2[segstart + dpos[h] + i0 + i] = v[h][i];
+        }
+    }
+  }
+  if (!staged) return;
+  __syncthreads();
+  // the segment out: 8-B stores where the destination is 8-B aligned, 2-B stores at its ends
+  const uint32_t head = (uint32_t)((4 - (segstart & 3)) & 3);
+  uint16_t* out = b.dst2 + segstart;
+  if (tid < min(head, total)) out[tid] = stage[tid];
+  const uint32_t nw = total > head ? (total - head) / 4 : 0u;
+  uint64_t* out8 = (uint64_t*)(out + head);
+  for (uint32_t w = tid; w < nw; w += kLrThreads) {
+    const uint32_t q = head + 4 * w;
+    out8[w] = (uint64_t)stage[q] | ((uint64_t)stage[q + 1] << 16) | ((uint64_t)stage[q + 2] << 32) |
+              ((uint64_t)stage[q + 3] << 48);
+  }
+  for (uint32_t i = head + 4 * nw + tid; i < total; i += kLrThreads) out[i] = stage[i];
+}
+
 
 uint32_t serve_grid(uint32_t tiles, uint32_t cap = kServeGrid) { return cap == 0 || tiles < cap ? tiles : cap; }
 
@@ -1065,6 +1209,13 @@ BinGeom make_bin_geom(uint64_t N, uint32_t k, bool big) {
   // arrays' 16-B + 32-B pieces of a run
   g.aos = big ? 1u : 0u;  // (packed pushes at 2^24: 570 vs 520 us per dense round)
   g.split = 1u;  // (sharded geometries clear it: their passes keep u32 ids)
+  // serve's long-run ids (host: BinGeom::lr, off by default): groups of kLrG regions, blocks of lr_nb
+  // tiles (a power of two <= kLrMaxNB) holding ~32768 ids on average, well inside kLrCap
+  g.lr = 0u;
+  g.lr_ng = (g.nt_s + kLrG - 1) / kLrG;
+  const double per_tile = (double)kLrG * g.rp / (double)g.nt_d;  // ids per (group, tile), on average
+  g.lr_nb = 1u;
+  while (g.lr_nb < kLrMaxNB && per_tile * (2 * g.lr_nb) <= 32768.0) g.lr_nb *= 2;
   return g;
 }
 
@@ -1079,7 +1230,8 @@ size_t bin_bytes(const BinGeom& g) {
   const size_t recs = (size_t)g.nt_s * g.rp;
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   return (g.split ? 2 * al(recs * 2) : al(recs * 4)) + (g.aos ? al(recs * 12) : al(recs * 8)) + al(recs * 8) +
-         2 * al((size_t)g.nt_s * (g.nt_d + 1) * 2) + 256;
+         2 * al((size_t)g.nt_s * (g.nt_d + 1) * 2) + 256 +
+         (g.split ? al(recs * 2) + al((size_t)g.nt_d * g.lr_ng * 4) : 0);  // dst2, base2 (BinGeom::lr)
 }
 
 void bin_carve(const BinGeom& g, void* base, BinBufs* b) {
@@ -1105,6 +1257,15 @@ void bin_carve(const BinGeom& g, void* base, BinBufs* b) {
   b->off = (uint16_t*)p;
   p += al((size_t)g.nt_s * (g.nt_d + 1) * 2);
   b->offT = (uint16_t*)p;
+  p += al((size_t)g.nt_s * (g.nt_d + 1) * 2);
+  b->dst2 = nullptr;
+  b->base2 = nullptr;
+  if (g.split) {
+    p += 256;
+    b->dst2 = (uint16_t*)p;
+    p += al(recs * 2);
+    b->base2 = (uint32_t*)p;
+  }
 }
 
 hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, uint64_t* partial, uint32_t R,
@@ -1134,7 +1295,11 @@ hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, 
 #undef GOSSIP_EMIT_V
 #undef GOSSIP_EMIT
   launch_transpose_u16(b.off, b.offT, g.nt_s, g.nt_d + 1, partial, rs.plen, st);
-  if ((mode == 2 || mode == 3) && g.split)
+  if ((mode == 2 || mode == 3) && g.split && g.lr && b.dst2) {  // serve's ids regrouped into long runs
+    bin_dst_group_kernel<<<g.lr_ng * ((g.nt_d + g.lr_nb - 1) / g.lr_nb), kLrThreads, 0, st>>>(g, b);
+    bin_serve_kernel<kIdVF, true, true><<<serve_grid(g.nt_d, g.serve_grid), kTileThreads, 0, st>>>(
+        g, S, b, R, IdxRange::all(g.nt_d));
+  } else if ((mode == 2 || mode == 3) && g.split)
     bin_serve_kernel<kIdVF, true><<<serve_grid(g.nt_d, g.serve_grid), kTileThreads, 0, st>>>(g, S, b, R,
                                                                                           IdxRange::all(g.nt_d));
   else if (mode == 2 || mode == 3)

@@ -517,9 +517,10 @@ double sparse_frac_of(const gossip_engine* e) {
 // Per-rank cost model of one sharded round of the random modes, in ms: device time from the
 // measured rates plus link time = the bytes the rank sends over its links /
 // (link_gbps x the G - 1 links it uses, at most 7).  Only steers the plan (every kind computes
-// the same bits).  Device rates: a sparse round's Philox floor 2.3 ps per own node (round 0 at
-// 2^27 on one GPU: 311 us) plus 0.3 ns per edge with a rare end (rounds 6-7 at 2^27: 0.15-0.42
-// ns); a dense round on the state image 7.3 ps per image node + 47 ps per own node (N = 2 / 4
+// the same bits).  Device rates: a sparse round costs 2.3 ps per own node (the Philox floor; round
+// 0 at 2^27 on one GPU: 311 us) plus up to 70 ps per own node as the rare share r grows, x (1 -
+// e^(-r / 0.05)) (the summaries saturate: G = 2 x 2^26 at r = 3.7 / 19 / 25 %: 2.41 / 5.0 / 4.83 ms,
+// profiles/r05_shard/probe_G2_fixed.txt); a dense round on the state image 7.3 ps per image node + 47 ps per own node (N = 2 / 4
 // ranks x 2^26 / 2^25: 4.14 / 2.56 ms, profiles/r04_ad/); an exchange round 67 ps per own node
 // (G = 8 x 2^24: 1.13 ms, profiles/r02_xd/).  Link bytes per rank: sparse = the rare-list
 // all-gather (16 B per rare node of the shard to each other shard) + the off-shard pushes
@@ -536,7 +537,7 @@ ShardCosts shard_round_costs(const gossip_engine* e, const Est& x) {
   const double rare = std::min(x.nz, N - x.full), rare_own = rare / G;
   const double bw = e->link_gbps * 1e6 * std::min(G - 1.0, 7.0);  // bytes per ms
   ShardCosts c{};
-  c.sparse = 2.3e-9 * Nl + 3e-7 * 2.0 * k * rare_own +
+  c.sparse = Nl * (2.3e-9 + 7.0e-8 * (1.0 - std::exp(-rare / N / 0.05))) +
              (16.0 * rare_own * (G - 1.0) + 16.0 * k * rare_own * (G - 1.0) / G) / bw;
   c.dense_xd = e->xd && e->xd_shards && e->G >= e->xd_shards;
   const double mixed = std::max(0.0, x.nz - x.full);
@@ -1408,6 +1409,9 @@ int gossip_set_param(gossip_engine_t* e, const char* name, double v) {
     e->ae_ahead = (uint32_t)v;
   } else if (n == "ordered_collectives") {
     e->ordered = v != 0;
+  } else if (n == "serve_lr") {
+    if (v != 0 && v != 1) return e->fail(GOSSIP_EINVAL, "serve_lr must be 0 or 1");
+    e->bg.lr = v != 0 ? 1u : 0u;
   } else if (n == "link_gbps") {
     if (v < 0) return e->fail(GOSSIP_EINVAL, "link_gbps must be >= 0 (0 = fixed sparse_frac thresholds)");
     e->link_gbps = v;

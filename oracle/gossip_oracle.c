@@ -12,6 +12,7 @@
  */
 #include "gossip_oracle.h"
 
+#include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -579,8 +580,8 @@ static int ae_round(oracle_sim_t* s, uint64_t* partial) {
  * blocks in SyncRPC on each neighbour until it is acked (:80-87); a neighbour's 2 s context
  * (:77) expires after stall_rounds = D lost attempts (D = 0: never).  Round t, every walk of a
  * value x held by u goes on from its position c: the sender is skipped (no message); any other
- * neighbour w costs one message, which is lost like a random-mode edge (partition, or
- * Philox({u, t, 4, c >> 2})[c & 3] < edge_loss; the same for every value at (u, c, t)).  A lost
+ * neighbour w costs one message, which is lost like a random-mode edge (partition, or its own
+ * loss draw: each value is one SyncRPC, so the draw is per (u, c, t, value), flood_lost below).  A lost
  * attempt ends the walk's round (head-of-line: the later neighbours wait); a delivered one gives
  * w the value and moves on to c + 1 — unless the context has expired, when the walk stays on w
  * for good (it keeps retrying, and w can still learn x from it).  w's first sender of x is the
@@ -887,7 +888,7 @@ int oracle_sharded_plan(oracle_sim_t* s, const uint64_t* total, int32_t* kind) {
     const double full_n = (double)s->gtot[0];
     const double rare = nz < N - full_n ? nz : N - full_n, rare_own = rare / G;
     const double bw = s->link_gbps * 1e6 * (G - 1.0 < 7.0 ? G - 1.0 : 7.0);
-    const double c_sparse = 2.3e-9 * Nl + 3e-7 * 2.0 * k * rare_own +
+    const double c_sparse = Nl * (2.3e-9 + 7.0e-8 * (1.0 - exp(-rare / N / 0.05))) +
                             (16.0 * rare_own * (G - 1.0) + 16.0 * k * rare_own * (G - 1.0) / G) / bw;
     const int dense_xd = s->xd_shards && s->G >= s->xd_shards;
     const double mixed_n = nz - full_n > 0.0 ? nz - full_n : 0.0;
@@ -1300,7 +1301,7 @@ int oracle_set_param(oracle_sim_t* s, const char* name, double value) {
   /* the engine's performance knobs (path choice, grids): no effect on the rounds' results */
   const char* known[] = {"alld_frac",  "filter_frac", "ahead",        "serve_grid",   "apply_grid", "push_waves",
                          "ae_sparse",  "ae_cap",      "sparse_direct", "mid_frac",    "ae_dense_bin", "ae_dense_cap",
-                         "ae_ahead",   "ordered_collectives", "ae_dense_filter", "rccl_dev_collectives"};
+                         "ae_ahead",   "ordered_collectives", "ae_dense_filter", "rccl_dev_collectives", "serve_lr"};
   for (size_t i = 0; i < sizeof known / sizeof known[0]; ++i)
     if (!strcmp(name, known[i])) return GOSSIP_OK;
   return GOSSIP_EINVAL;

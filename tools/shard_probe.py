@@ -53,6 +53,10 @@ class Timed:
                 self.gathered = (G - 1) * r[2]
             elif name == "xd_requests":  # items in (12 B) and replies in (8 B), ~ the items it sends off-rank
                 self.gathered += 20 * (sum(r[2]) - r[2][self._rank])
+            elif name == "sparse_rare":  # its rare list to every other rank (16-B items); by symmetry ~ what it receives
+                self.gathered = (G - 1) * 16 * r[1]
+            elif name == "sparse_scan":  # pushes for other shards (16-B items)
+                self.gathered += 16 * (sum(int(c) for c in r[1]) - int(r[1][self._rank]))
             return r
         return g
 
@@ -97,3 +101,11 @@ for rep in range(2):
                   flush=True)
         print(f"G={G} rounds={len(rounds)} sum per-rank {sum(r[2] for r in rounds):.2f} ms  "
               f"gathered per rank {sum(r[5] for r in rounds) / 2**20:.1f} MiB", flush=True)
+        # the planner's link term (engine.hip shard_round_costs): the bytes a rank receives (= what it
+        # sends, by symmetry) over link_gbps x min(G - 1, 7) links, added to the device time
+        bw = PARAMS.get("link_gbps", 76.0) or 76.0
+        link_ms = sum(r[5] for r in rounds) / (bw * 1e6 * min(G - 1, 7))
+        print(f"G={G} plan link_gbps={PARAMS.get('link_gbps', 76.0)}: modelled per-rank wall "
+              f"{sum(r[2] for r in rounds) + link_ms:.2f} ms = device {sum(r[2] for r in rounds):.2f} + "
+              f"link {link_ms:.2f} (at {bw:g} GB/s per link); kinds "
+              f"{''.join('DSAXC'[r[1]] for r in rounds)}", flush=True)
