@@ -166,6 +166,13 @@ int gossip_set_stream(gossip_engine_t* eng, void* hip_stream);
  *   "cc_frac"      sharded random modes: dense rounds on the state image exchange it
  *                  class-coded (kind 4) while the mixed nodes (neither empty nor full) are
  *                  at most this fraction of N (default 0.75; 0 never, 1 always)
+ *   "link_gbps"    sharded random modes: a round is sparse or dense by a per-rank cost model
+ *                  of device time plus link bytes over this many GB/s per xGMI link (default
+ *                  76; 0 = the fixed sparse_frac thresholds)
+ *   "rccl_dev_collectives"  1: the RCCL transport's collectives read the round's counts and
+ *                  partials from engine memory (gossip_*_dev); default 0: one host read first
+ *   "serve_lr"     one shard, dense rounds: 1 regroups serve's record ids into long runs
+ *                  first (default 0)
  * Unknown names return GOSSIP_EINVAL. */
 int gossip_set_param(gossip_engine_t* eng, const char* name, double value);
 
