@@ -86,6 +86,9 @@ struct BinBufs {
   // record index space holds its segments)
   uint16_t* dst2;   // [nt_s][rp]
   uint32_t* base2;  // [nt_d][lr_ng]
+  // one shard: the persistent serve's / apply's tile queues, 8 counters each (one per XCD), zeroed
+  // by the round's transpose kernel (binned.hip TileQueue); null: the static tile order
+  uint32_t* dyn;
 };
 
 size_t bin_bytes(const BinGeom& g);

@@ -104,6 +104,26 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {
   return (b & 7u) * (n >> 3) + (b >> 3);
 }
 
+// Dynamic tile order of the persistent serve / apply (BinBufs::dyn, one shard, nv a multiple of 8):
+// a block on XCD x (blockIdx.x % 8, as xcd_remap assumes) takes the next tile of x's contiguous
+// range (xcd_remap's order) from x's counter, then steals from the other XCDs' ranges once x's is
+// dry, so the kernel ends when the last tile does, not when the slowest block's static share does.
+// Every tile is taken exactly once whichever XCD runs a block (speed only).
+struct TileQueue {
+  uint32_t* c;  // 8 counters, zeroed by the round's transpose kernel
+  uint32_t nv;
+  __device__ uint32_t claim() const {  // (one thread) the next tile, or nv
+    const uint32_t per = nv >> 3, x0 = blockIdx.x & 7u;
+    for (uint32_t h = 0; h < 8; ++h) {
+      const uint32_t x = (x0 + h) & 7u;
+      if (__atomic_load_n(&c[x], __ATOMIC_RELAXED) >= per) continue;  // dry: no atomic
+      const uint32_t i = atomicAdd(&c[x], 1u);
+      if (i < per) return x * per + i;
+    }
+    return nv;
+  }
+};
+
 // Which directions an edge n -> p carries (bit 0 push, bit 1 pull; 0: no
 // record).  From the sender alone: a push needs S_t[n] != 0, a pull is
 // pointless once n holds every rumor.  filt bit 0 also drops pull-only edges
@@ -560,10 +580,13 @@ constexpr uint32_t kTrT = 64, kTrRows = 4;
 __global__ __launch_bounds__(kTrT * kTrRows) void transpose_u16_kernel(const uint16_t* __restrict__ in,
                                                                        uint16_t* __restrict__ out, uint32_t rows,
                                                                        uint32_t cols, uint64_t* __restrict__ partial,
-                                                                       uint32_t plen) {
-  // the dense round's stats are absolute: clear the totals before K3 adds to them
-  if (blockIdx.x == 0 && blockIdx.y == 0)
+                                                                       uint32_t plen, uint32_t* __restrict__ dyn) {
+  // the dense round's stats are absolute: clear the totals before K3 adds to them; and the
+  // serve / apply tile queues (16 counters)
+  if (blockIdx.x == 0 && blockIdx.y == 0) {
     for (uint32_t i = threadIdx.y * kTrT + threadIdx.x; i < plen; i += kTrT * kTrRows) partial[i] = 0;
+    if (dyn && threadIdx.y == 0 && threadIdx.x < 16) dyn[threadIdx.x] = 0;
+  }
   __shared__ uint32_t tile[kTrT][kTrT + 1];
   constexpr uint32_t kPer = kTrT / kTrRows;
   const uint32_t c0 = blockIdx.x * kTrT, r0 = blockIdx.y * kTrT, tx = threadIdx.x, ty = threadIdx.y;
@@ -585,9 +608,9 @@ __global__ __launch_bounds__(kTrT * kTrRows) void transpose_u16_kernel(const uin
 
 // launch of transpose_u16_kernel over a [rows][cols] table
 void launch_transpose_u16(const uint16_t* in, uint16_t* out, uint32_t rows, uint32_t cols, uint64_t* partial,
-                          uint32_t plen, hipStream_t st) {
+                          uint32_t plen, hipStream_t st, uint32_t* dyn = nullptr) {
   const dim3 tg((cols + kTrT - 1) / kTrT, (rows + kTrT - 1) / kTrT);
-  transpose_u16_kernel<<<tg, dim3(kTrT, kTrRows), 0, st>>>(in, out, rows, cols, partial, plen);
+  transpose_u16_kernel<<<tg, dim3(kTrT, kTrRows), 0, st>>>(in, out, rows, cols, partial, plen, dyn);
 }
 
 
@@ -928,16 +951,28 @@ __global__ __launch_bounds__(kTileThreads) void bin_serve_kernel(BinGeom g, cons
   // tr.at(xcd_remap(v, tr.n)) (the XCD of v is that of blockIdx.x, as with one
   // block per tile); the next tile's image loads into registers during a walk
   const uint32_t nv = tr.n;
-  auto tile_of = [&](uint32_t v) { return tr.at(xcd_remap(v, nv)); };
+  // b.dyn: tiles from the per-XCD queues (TileQueue; the whole range only), claimed one ahead
+  const bool dyn = b.dyn && tr.lo == 0 && tr.skip0 == tr.skip1 && nv >= 8 && (nv & 7u) == 0;
+  const TileQueue tq{b.dyn, nv};
+  __shared__ uint32_t s_claim;
+  auto tile_of = [&](uint32_t v) { return tr.at(dyn ? v : xcd_remap(v, nv)); };
   uint4 x[kTileQ];
-  if (blockIdx.x < nv) tile_regs_load(x, S, (uint64_t)tile_of(blockIdx.x) << kTileDLog, g.N);
-  for (uint32_t v = blockIdx.x; v < nv; v += gridDim.x) {
+  uint32_t v0 = blockIdx.x;
+  if (dyn) {
+    if (threadIdx.x == 0) s_claim = tq.claim();
+    __syncthreads();
+    v0 = s_claim;
+  }
+  if (v0 < nv) tile_regs_load(x, S, (uint64_t)tile_of(v0) << kTileDLog, g.N);
+  for (uint32_t v = v0, vn; v < nv; v = vn) {
   const uint32_t T = tile_of(v);
-  __syncthreads();  // the previous walk is done with img
+  __syncthreads();  // the previous walk is done with img (and every thread has read s_claim)
 #pragma unroll
   for (uint32_t q = 0; q < kTileQ; ++q) ((uint4*)img)[q * kTileThreads + threadIdx.x] = x[q];
+  if (dyn && threadIdx.x == 0) s_claim = tq.claim();
   __syncthreads();
-  if (v + gridDim.x < nv) tile_regs_load(x, S, (uint64_t)tile_of(v + gridDim.x) << kTileDLog, g.N);
+  vn = dyn ? s_claim : v + gridDim.x;
+  if (vn < nv) tile_regs_load(x, S, (uint64_t)tile_of(vn) << kTileDLog, g.N);
   const uint32_t* gids = b.ids;
   uint64_t* __restrict__ gresp = b.resp;
   const uint16_t* rowb = b.offT + (size_t)T * g.nt_s;
@@ -1121,10 +1156,20 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
   // the next tile's S_t loads into registers during the current tile's work.  In
   // place stays safe: only this block reads or writes S[X] of its tiles.
   const uint32_t nv = g.nt_d;
-  for (uint32_t v = blockIdx.x; v < nv; v += gridDim.x) {
-  const uint32_t X = xcd_remap(v, nv);
+  // b.dyn (one shard): tiles from the per-XCD queues (TileQueue), else the static order
+  const bool dyn = b.dyn && nv >= 8 && (nv & 7u) == 0;
+  const TileQueue tq{b.dyn ? b.dyn + 8 : nullptr, nv};
+  __shared__ uint32_t s_claim;
+  for (uint32_t v = blockIdx.x;;) {
+  __syncthreads();  // the previous epilogue is done with acc, cnt and s_claim
+  if (dyn) {
+    if (tid == 0) s_claim = tq.claim();
+    __syncthreads();
+    v = s_claim;
+  }
+  if (v >= nv) break;
+  const uint32_t X = dyn ? v : xcd_remap(v, nv);
   const uint64_t node0 = (uint64_t)X << kTileDLog;
-  __syncthreads();  // the previous epilogue is done with acc and cnt
   {
     uint4 xr[kTileQ];
     tile_regs_load(xr, S, node0, Nn);
@@ -1175,6 +1220,7 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
   }
   __syncthreads();
   tile_epilogue(acc, node0, Nn, hid0, Snext, partial, R, flags, cnt, red_hash, red_full, red_nz, b.nzb, b.fullb);
+  if (!dyn) v += gridDim.x;
   }
 }
 
@@ -1231,7 +1277,8 @@ size_t bin_bytes(const BinGeom& g) {
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   return (g.split ? 2 * al(recs * 2) : al(recs * 4)) + (g.aos ? al(recs * 12) : al(recs * 8)) + al(recs * 8) +
          2 * al((size_t)g.nt_s * (g.nt_d + 1) * 2) + 256 +
-         (g.split ? al(recs * 2) + al((size_t)g.nt_d * g.lr_ng * 4) : 0);  // dst2, base2 (BinGeom::lr)
+         (g.split ? al(recs * 2) + al((size_t)g.nt_d * g.lr_ng * 4) : 0) +  // dst2, base2 (BinGeom::lr)
+         256;  // the tile queues (dyn)
 }
 
 void bin_carve(const BinGeom& g, void* base, BinBufs* b) {
@@ -1265,7 +1312,11 @@ void bin_carve(const BinGeom& g, void* base, BinBufs* b) {
     b->dst2 = (uint16_t*)p;
     p += al(recs * 2);
     b->base2 = (uint32_t*)p;
+    p += al((size_t)g.nt_d * g.lr_ng * 4);
+  } else {
+    p += 256;
   }
+  b->dyn = (uint32_t*)p;  // 16 u32 (sharded passes clear it: their order stays static)
 }
 
 hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, uint64_t* partial, uint32_t R,
@@ -1294,7 +1345,7 @@ hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, 
   }
 #undef GOSSIP_EMIT_V
 #undef GOSSIP_EMIT
-  launch_transpose_u16(b.off, b.offT, g.nt_s, g.nt_d + 1, partial, rs.plen, st);
+  launch_transpose_u16(b.off, b.offT, g.nt_s, g.nt_d + 1, partial, rs.plen, st, b.dyn);
   if ((mode == 2 || mode == 3) && g.split && g.lr && b.dst2) {  // serve's ids regrouped into long runs
     bin_dst_group_kernel<<<g.lr_ng * ((g.nt_d + g.lr_nb - 1) / g.lr_nb), kLrThreads, 0, st>>>(g, b);
     bin_serve_kernel<kIdVF, true, true><<<serve_grid(g.nt_d, g.serve_grid), kTileThreads, 0, st>>>(
@@ -1348,6 +1399,7 @@ void sb_carve(const SbGeom& g, void* base, SbBufs* b) {
   bin_carve(g.p, base, &b->p);
   bin_carve(g.q, (char*)base + bin_bytes(g.p), &b->q);
   b->p.nzb = b->p.fullb = b->q.nzb = b->q.fullb = nullptr;
+  b->p.dyn = b->q.dyn = nullptr;
 }
 
 namespace {
@@ -1877,6 +1929,9 @@ void xd_carve_recv(const XdGeom& g, uint64_t cap_r, void* base, XdBufs* b) {
   b->rb.off = (uint16_t*)take(offs * 2);
   b->rb.offT = (uint16_t*)take(offs * 2);
   b->rb.nzb = b->rb.fullb = nullptr;
+  b->rb.dst2 = nullptr;  // (no long-run ids, static tile order)
+  b->rb.base2 = nullptr;
+  b->rb.dyn = nullptr;
 }
 
 hipError_t launch_xd_requests(const XdGeom& g, const XdBufs& b, const uint64_t* S, uint32_t R, uint32_t t,

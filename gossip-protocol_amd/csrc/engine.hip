@@ -153,6 +153,7 @@ struct gossip_engine {
   bool binned = false;
   BinGeom bg{};
   BinBufs bb{};
+  uint32_t* bb_dyn = nullptr;  // the tile queues (gossip_set_param "tile_queues" 0 clears bb.dyn)
   void* bin_mem = nullptr;
   // frontier (sparse-round) path, on top of the binned one
   bool frontier = false;
@@ -1291,6 +1292,11 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
       return bail(GOSSIP_ENOMEM);
     }
     bin_carve(e->bg, e->bin_mem, &e->bb);
+    // the serve / apply tile queues pay where a persistent block has many tiles: 2^27 nodes (32
+    // per block) 5578 -> 5497 us per dense round; at 2^24 (4 per block) 510 -> 525 us
+    // (profiles/r05_tq/); param tile_queues overrides
+    e->bb_dyn = e->bb.dyn;
+    if (e->bg.nt_d < 4096) e->bb.dyn = nullptr;
     e->binned = true;
     if (!(cfg->flags & GOSSIP_FLAG_DENSE)) {
       const size_t fbytes = frontier_bytes(e->N);
@@ -1409,6 +1415,9 @@ int gossip_set_param(gossip_engine_t* e, const char* name, double v) {
     e->ae_ahead = (uint32_t)v;
   } else if (n == "ordered_collectives") {
     e->ordered = v != 0;
+  } else if (n == "tile_queues") {
+    if (v != 0 && v != 1) return e->fail(GOSSIP_EINVAL, "tile_queues must be 0 or 1");
+    e->bb.dyn = v != 0 ? e->bb_dyn : nullptr;
   } else if (n == "serve_lr") {
     if (v != 0 && v != 1) return e->fail(GOSSIP_EINVAL, "serve_lr must be 0 or 1");
     e->bg.lr = v != 0 ? 1u : 0u;

@@ -173,6 +173,8 @@ int gossip_set_stream(gossip_engine_t* eng, void* hip_stream);
  *                  partials from engine memory (gossip_*_dev); default 0: one host read first
  *   "serve_lr"     one shard, dense rounds: 1 regroups serve's record ids into long runs
  *                  first (default 0)
+ *   "tile_queues"  one shard, dense rounds: 1 = serve and apply take tiles from per-XCD
+ *                  queues (default from 4096 tiles = 2^26 nodes), 0 = the static order
  * Unknown names return GOSSIP_EINVAL. */
 int gossip_set_param(gossip_engine_t* eng, const char* name, double value);
 
