@@ -310,11 +310,21 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
     }
   };
   if (!BIG && blockIdx.x < nr) load_values(region(blockIdx.x), v);
-  for (uint32_t r = blockIdx.x; r < nr; r += gridDim.x) {
+  // one shard, big regions, b.dyn: regions from one queue (b.dyn[16], zeroed by the round's transpose
+  // for the next round), so the launch ends with its last region, not its slowest block's share
+  const bool dynq = BIG && !SHARD && b.dyn != nullptr;
+  __shared__ uint32_t s_claim;
+  for (uint32_t r = blockIdx.x;;) {
+  __syncthreads();  // the previous region's write-out has read cur/st_ids/sval (and s_claim is read)
+  if (dynq) {
+    if (tid == 0) s_claim = atomicAdd(&b.dyn[16], 1u);
+    __syncthreads();
+    r = s_claim;
+  }
+  if (r >= nr) break;
   const uint32_t s = region(r);
   const uint64_t base = (uint64_t)s << g.ts_log;
   const uint32_t nsend = (uint32_t)min<uint64_t>(g.ts, nsnd - base);
-  __syncthreads();  // the previous region's write-out has read cur/st_ids/sval
 
   for (uint32_t d = tid; d < (BIG ? (g.nt_d + 1) >> 1 : g.nt_d); d += kEmitThreads) cur[d] = 0;
   if (BIG) load_values(s, v);
@@ -569,6 +579,7 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
 #pragma unroll
     for (uint32_t q = 0; q < kQ; ++q) v[q] = vn[q];
   }
+  if (!dynq) r += gridDim.x;
   }
 }
 
@@ -585,7 +596,7 @@ __global__ __launch_bounds__(kTrT * kTrRows) void transpose_u16_kernel(const uin
   // serve / apply tile queues (16 counters)
   if (blockIdx.x == 0 && blockIdx.y == 0) {
     for (uint32_t i = threadIdx.y * kTrT + threadIdx.x; i < plen; i += kTrT * kTrRows) partial[i] = 0;
-    if (dyn && threadIdx.y == 0 && threadIdx.x < 16) dyn[threadIdx.x] = 0;
+    if (dyn && threadIdx.y == 0 && threadIdx.x < 17) dyn[threadIdx.x] = 0;  // (dyn[16]: the next emit's)
   }
   __shared__ uint32_t tile[kTrT][kTrT + 1];
   constexpr uint32_t kPer = kTrT / kTrRows;

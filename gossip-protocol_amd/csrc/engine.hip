@@ -1296,6 +1296,10 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
     // per block) 5578 -> 5497 us per dense round; at 2^24 (4 per block) 510 -> 525 us
     // (profiles/r05_tq/); param tile_queues overrides
     e->bb_dyn = e->bb.dyn;
+    if (hipMemset(e->bb_dyn, 0, 17 * 4) != hipSuccess) {  // (the first emit's queue; later rounds' transposes)
+      e->err = "hipMemset of the tile queues failed";
+      return bail(GOSSIP_EHIP);
+    }
     if (e->bg.nt_d < 4096) e->bb.dyn = nullptr;
     e->binned = true;
     if (!(cfg->flags & GOSSIP_FLAG_DENSE)) {
