@@ -45,6 +45,16 @@ struct AeArgs {
   // 0 = that round converged, overflowed its edge list or did not run, so this round's sparse
   // kernels return at once.  Null: always run.
   const uint32_t* gate;
+  // pipelined sparse rounds, the emit's part (round 5): gate_out = this round's gate word, which the
+  // emit computes from the previous round of the batch (gate_prev null: the batch's first round;
+  // else *gate_prev open, its edge list did not overflow (its aux[1] <= segcap) and it did not
+  // converge (its partial[0] != [1]), prev_partial being that round's slot of totals) and block 0
+  // stores; zero / nzero: this round's slot, cleared by the emit's block 0 before any kernel adds
+  uint32_t* gate_out;
+  const uint32_t* gate_prev;
+  const uint64_t* prev_partial;
+  uint64_t* zero;
+  uint32_t pl, nzero;
 };
 
 // binned sparse-scan geometry for N nodes, k exchanges per node
@@ -72,9 +82,6 @@ hipError_t launch_ae_sparse(const AeArgs& a, hipStream_t st);
 // pass also does the churn (no launch_ae_churn before it)
 hipError_t launch_ae_sparse_binned(const AeArgs& a, hipStream_t st);
 hipError_t launch_ae_sparse_stats(const AeArgs& a, hipStream_t st);
-// after a pipelined sparse round (a.partial / a.aux its totals): *gout = the round ran (a.gate
-// open or null), did not overflow its edge list (aux[1] <= segcap) and did not converge
-hipError_t launch_ae_gate(const AeArgs& a, uint32_t* gout, hipStream_t st);
 // binned dense round: geometry of its 2^14-node tiles (the sparse scan's
 // sender regions), whether the kernels' LDS tables cover it, and the round itself: the
 // emit (churn fused, records into a.brec, run starts into a.boff with a.btl / a.bnt of

@@ -74,23 +74,33 @@ __device__ __forceinline__ uint64_t hash_term(uint32_t v, uint32_t c, uint64_t n
   return v ? mix64((uint64_t)v + ((uint64_t)c * N + n) * kGold64) : 0ull;
 }
 
+// inject_random's rows, and their componentwise max folded into target (zeroed before) in the same
+// pass: a thread keeps one quad q of components (the grid stride is a multiple of (K + 3) / 4), so
+// its running max is per component; one LDS max per block, one global atomicMax per component.
+// K % 4 == 0: the quad is one 16-B store (the rows are 16-B aligned: 4K bytes each).
 __global__ __launch_bounds__(kAeBlock) void ae_init_kernel(uint32_t* V, uint64_t N, uint32_t K, uint32_t k0,
-                                                           uint32_t k1) {
-  const uint32_t c4 = (K + 3) / 4;
-  for (uint64_t i = (uint64_t)blockIdx.x * kAeBlock + threadIdx.x; i < N * c4; i += (uint64_t)gridDim.x * kAeBlock) {
-    const uint32_t n = (uint32_t)(i / c4), q = (uint32_t)(i % c4);
-    const u32x4 x = philox4x32_10(u32x4{n, q, 3u, 0u}, k0, k1);
-    for (uint32_t r = 0; r < 4 && 4 * q + r < K; ++r) V[(uint64_t)n * K + 4 * q + r] = lane_of(x, r) & 0xFFFFu;
-  }
-}
-
-__global__ __launch_bounds__(kAeBlock) void ae_target_kernel(const uint32_t* V, uint64_t N, uint32_t K,
-                                                             uint32_t* target) {
+                                                           uint32_t k1, uint32_t* target) {
   __shared__ uint32_t m[64];
   if (threadIdx.x < 64) m[threadIdx.x] = 0;
   __syncthreads();
-  for (uint64_t i = (uint64_t)blockIdx.x * kAeBlock + threadIdx.x; i < N * K; i += (uint64_t)gridDim.x * kAeBlock)
-    atomicMax(&m[i % K], V[i]);
+  const uint32_t c4 = (K + 3) / 4;
+  uint32_t mx[4] = {0, 0, 0, 0}, q0 = ~0u;
+  for (uint64_t i = (uint64_t)blockIdx.x * kAeBlock + threadIdx.x; i < N * c4; i += (uint64_t)gridDim.x * kAeBlock) {
+    const uint32_t n = (uint32_t)(i / c4), q = (uint32_t)(i % c4);
+    q0 = q;
+    const u32x4 x = philox4x32_10(u32x4{n, q, 3u, 0u}, k0, k1);
+    const uint32_t v[4] = {x.x & 0xFFFFu, x.y & 0xFFFFu, x.z & 0xFFFFu, x.w & 0xFFFFu};
+    if ((K & 3u) == 0) {
+      *reinterpret_cast<uint4*>(V + (uint64_t)n * K + 4 * q) = uint4{v[0], v[1], v[2], v[3]};
+    } else {
+      for (uint32_t r = 0; r < 4 && 4 * q + r < K; ++r) V[(uint64_t)n * K + 4 * q + r] = v[r];
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < 4; ++r) mx[r] = max(mx[r], v[r]);
+  }
+  if (q0 != ~0u)
+    for (uint32_t r = 0; r < 4 && 4 * q0 + r < K; ++r)
+      if (mx[r]) atomicMax(&m[4 * q0 + r], mx[r]);
   __syncthreads();
   if (threadIdx.x < K && m[threadIdx.x]) atomicMax(&target[threadIdx.x], m[threadIdx.x]);
 }
@@ -406,7 +416,20 @@ __global__ __launch_bounds__(kAeBinThreads, (NT > kAeBinTiles ? 4 : kAeEmitWaves
   __shared__ __align__(16) uint32_t st[kAeBinRec];  // read back as uint4
   __shared__ uint32_t wsum[kAeBinThreads / 64];
   __shared__ uint32_t wpre[kAeBinThreads / 64 + 1];
-  if (ae_gated_off(a)) return;
+  if (a.gate_out) {  // pipelined sparse round: this round's gate from the previous one (AeArgs)
+    bool run = true;
+    if (a.gate_prev) {
+      const uint64_t* pa = a.prev_partial + a.pl;  // its aux words
+      run = *(volatile const uint32_t*)a.gate_prev != 0u && pa[1] <= a.segcap &&
+            a.prev_partial[0] != a.prev_partial[1];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) *a.gate_out = run ? 1u : 0u;
+    if (!run) return;
+  } else if (ae_gated_off(a)) {
+    return;
+  }
+  if (a.zero && blockIdx.x == 0)
+    for (uint32_t i = threadIdx.x; i < a.nzero; i += kAeBinThreads) a.zero[i] = 0;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t rs = 1u << a.brs, rp = rs * a.k, nt = a.bnt;
   const uint32_t tmask = (1u << a.btl) - 1u;
@@ -1249,10 +1272,10 @@ uint32_t ae_lanes(uint32_t K) {
 
 hipError_t launch_ae_init(uint32_t* V, uint32_t* target, uint64_t N, uint32_t K, uint32_t k0, uint32_t k1,
                           hipStream_t st) {
-  ae_init_kernel<<<ae_grid(N * ((K + 3) / 4), kAeBlock, 65536), kAeBlock, 0, st>>>(V, N, K, k0, k1);
   hipError_t e = hipMemsetAsync(target, 0, K * 4, st);
   if (e != hipSuccess) return e;
-  ae_target_kernel<<<ae_grid(N * K, kAeBlock, 4096), kAeBlock, 0, st>>>(V, N, K, target);
+  // (the grid stride must be a multiple of (K + 3) / 4: kAeBlock is)
+  ae_init_kernel<<<ae_grid(N * ((K + 3) / 4), kAeBlock, 65536), kAeBlock, 0, st>>>(V, N, K, k0, k1, target);
   return hipGetLastError();
 }
 
@@ -1373,16 +1396,6 @@ hipError_t launch_ae_dense_binned(const AeArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-__global__ void ae_gate_kernel(AeArgs a, uint32_t* gout) {
-  if (threadIdx.x != 0) return;
-  const bool ran = !ae_gated_off(a);
-  *gout = ran && a.aux[1] <= a.segcap && a.partial[0] != a.partial[1] ? 1u : 0u;
-}
-
-hipError_t launch_ae_gate(const AeArgs& a, uint32_t* gout, hipStream_t st) {
-  ae_gate_kernel<<<1, 64, 0, st>>>(a, gout);
-  return hipGetLastError();
-}
 
 hipError_t launch_ae_sparse_stats(const AeArgs& a, hipStream_t st) {
   // few blocks: each adds its totals with three same-address atomics

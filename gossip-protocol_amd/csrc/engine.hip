@@ -833,8 +833,8 @@ int ae_round(gossip_engine* e) {
 // gossip_step of a one-engine ANTIENTROPY engine.  Dense rounds, and sparse
 // rounds without the binned scan, run one at a time (ae_round: plan, kernels, totals read back).
 // A run of sparse rounds is pipelined: up to ae_ahead rounds are enqueued at once, each with its
-// own slot of totals and a gate word the previous round's launch_ae_gate writes (it ran, its edge
-// list did not overflow, it did not converge), so the sparse kernels of a round past convergence
+// own slot of totals and a gate word its emit writes from the previous round's slot (that round ran,
+// its edge list did not overflow, it did not converge), so the sparse kernels of a round past convergence
 // or after an overflow return at once; the host reads every slot after one sync.  An overflowed
 // round left V, the bitmaps and the claims untouched: it is rerun dense (ae_dense_next), as
 // ae_round does.  Every round's stats and state equal the unpipelined loop's; its path choice
@@ -883,12 +883,18 @@ int step_ae(gossip_engine* e, uint32_t max_rounds, gossip_round_stats_t* stats, 
       a.t = e->t + i;
       a.partial = e->ae_slot_d + i * sw;
       a.aux = a.partial + pl;
-      a.gate = i ? e->ae_gate_d + (i - 1) : nullptr;
-      HIP_OK(e, hipMemsetAsync(a.partial, 0, sw * 8, e->stream));
+      // the emit opens or closes this round's gate from the previous round's slot and clears this
+      // round's slot (no memset, no gate kernel per round: ~15 us each, profiles/r05_ae/)
+      a.gate = e->ae_gate_d + i;
+      a.gate_out = e->ae_gate_d + i;
+      a.gate_prev = i ? e->ae_gate_d + (i - 1) : nullptr;
+      a.prev_partial = i ? e->ae_slot_d + (i - 1) * sw : nullptr;
+      a.pl = (uint32_t)pl;
+      a.zero = a.partial;
+      a.nzero = (uint32_t)sw;
       if (e->timing) HIP_OK(e, hipEventRecord(e->evr[i][0], e->stream));
       HIP_OK(e, launch_ae_sparse_binned(a, e->stream));  // churn fused into its first pass
       HIP_OK(e, launch_ae_sparse_stats(a, e->stream));
-      HIP_OK(e, launch_ae_gate(a, e->ae_gate_d + i, e->stream));
       if (e->timing) HIP_OK(e, hipEventRecord(e->evr[i][1], e->stream));
       std::swap(ab, abn);
     }
