@@ -37,7 +37,11 @@ struct FrontierBufs {
   // one-shard rounds decide on the device, from the exact rare count of S_t: summ2 is built and
   // used when 1 - (1 - r)^g >= mid_frac (the LDS summary is that saturated)
   float mid_frac;
-  uint64_t id0;       // global id of node 0 of these arrays (a shard's first node; 0 on one GPU): the hash uses global ids
+  // round 5: the scan's edges with a possibly rare end go through a per-wave LDS queue and are
+  // resolved 128 at a time (one chain of round trips per 128 edges, not per wave batch); 0: the
+  // per-batch resolution (param scan_queue)
+  uint32_t scan_q;
+  uint64_t id0;      // global id of node 0 of these arrays (a shard's first node; 0 on one GPU): the hash uses global ids
 };
 
 uint32_t frontier_glog(uint64_t N);

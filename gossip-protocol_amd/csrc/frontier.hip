@@ -43,7 +43,7 @@ __device__ __forceinline__ T scan_ld(const T* p) {
 constexpr uint32_t kScanGrid = 256;  // one block per CU: the summary takes 128 KiB of LDS
 constexpr uint32_t kScanWaves = 4;   // waves per SIMD (launch bounds)
 constexpr int kCommitThreads = 256;
-constexpr uint32_t kRwWords = 1024;  // rare-bitmap words staged per scan chunk (64K nodes)
+constexpr uint32_t kRwWords = 512;   // rare-bitmap words staged per scan chunk (32K nodes; LDS room for the queues)
 constexpr int kScanUnroll = 2;  // nodes per lane per scan step (1: equal, 4: slower)
 constexpr int kCommitUnroll = 4;     // dirty groups per wave per commit step
 
@@ -342,6 +342,175 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, const Fro
   }
 }
 
+// Queued scan (round 5, FrontierBufs::scan_q, k <= 4).  In the rounds between the light and the
+// heavy ones most waves of 128 nodes hold a few edges with a possibly rare end, and resolving
+// them where they are drawn costs every such batch the whole chain of round trips (summary
+// probes, S_t gathers, atomics) for a handful of lanes: with 16 waves per CU (the LDS summary
+// allows one block) those rounds were latency-bound at 2-3x their Philox floor.  Here a wave
+// appends each such edge to its own LDS queue and resolves the queue 128 edges at a time: one
+// chain per 128 edges, two edges per lane, every load of the chain issued before any is used.
+//
+// A queued edge: x = node - block base (< 2^24) | rare(n) << 24 | summary hit(p) << 25, y = p.
+// Both ends' deltas are relative to S_t, so splitting a node's pulls over queue entries (one
+// OR per edge instead of one per node) changes no bit.
+constexpr uint32_t kQFlush = 128;             // edges resolved per flush (2 per lane)
+constexpr uint32_t kQCap = kQFlush + 64;      // a flush starts as soon as kQFlush are queued
+
+template <int MAJ, int MODE>
+__device__ __forceinline__ void scan_flush(const uint2* qw, uint32_t nf, const FrontierBufs& f,
+                                           const uint64_t* __restrict__ S, uint64_t* Sw, uint32_t b0, uint64_t maj,
+                                           bool mark_d, bool direct, bool mid, uint32_t lane) {
+  constexpr bool kPush = (MODE & 1) != 0, kPull = (MODE & 2) != 0;
+  constexpr int kE = kQFlush / 64;
+  uint32_t n[kE], p[kE];
+  bool rn[kE], hit[kE];
+#pragma unroll
+  for (int e = 0; e < kE; ++e) {
+    const uint32_t i = lane + 64u * e;
+    const uint2 q = i < nf ? qw[i] : uint2{0u, 0u};
+    n[e] = b0 + (q.x & 0xFFFFFFu);
+    rn[e] = (q.x >> 24) & 1u;
+    hit[e] = (q.x >> 25) & 1u;
+    p[e] = q.y;
+  }
+  if (f.glog && mid) {
+    uint32_t sw[kE];
+#pragma unroll
+    for (int e = 0; e < kE; ++e) sw[e] = hit[e] ? f.summ2[p[e] >> (f.g2log + 5)] : 0u;
+#pragma unroll
+    for (int e = 0; e < kE; ++e) hit[e] = hit[e] && ((sw[e] >> ((p[e] >> f.g2log) & 31u)) & 1u);
+  }
+  if (f.glog) {
+    uint64_t rw[kE];
+#pragma unroll
+    for (int e = 0; e < kE; ++e) rw[e] = hit[e] ? (MAJ ? f.fullb[p[e] >> 6] : f.nzb[p[e] >> 6]) : 0ull;
+#pragma unroll
+    for (int e = 0; e < kE; ++e) {
+      const bool bit = (rw[e] >> (p[e] & 63u)) & 1ull;
+      if (bit == (MAJ != 0)) hit[e] = false;
+    }
+  }
+  uint64_t x[kE], vp[kE];
+#pragma unroll
+  for (int e = 0; e < kE; ++e) {
+    x[e] = rn[e] ? scan_ld(&S[n[e]]) : maj;
+    vp[e] = hit[e] ? scan_ld(&S[p[e]]) : maj;
+  }
+  uint64_t dpush[kE], dpull[kE];
+#pragma unroll
+  for (int e = 0; e < kE; ++e) {
+    const bool any = rn[e] || hit[e];  // both ends majority (or an empty slot): nothing moves
+    dpush[e] = kPush && any ? x[e] & ~vp[e] : 0ull;
+    dpull[e] = kPull && any ? vp[e] & ~x[e] : 0ull;
+  }
+#pragma unroll
+  for (int e = 0; e < kE; ++e) {
+    if (dpush[e]) {
+      if (MAJ == 0 && direct && !hit[e]) {  // an empty peer: nobody reads its S_t
+        atomicOr((unsigned long long*)&Sw[p[e]], (unsigned long long)dpush[e]);
+      } else {
+        atomicOr((unsigned long long*)&f.D[p[e]], (unsigned long long)dpush[e]);
+        if (mark_d) f.dirtyD[p[e] >> 6] = 1;
+      }
+    }
+    if (dpull[e]) {
+      if (MAJ == 0 && direct && !rn[e]) {
+        atomicOr((unsigned long long*)&Sw[n[e]], (unsigned long long)dpull[e]);
+      } else {
+        atomicOr((unsigned long long*)&f.D[n[e]], (unsigned long long)dpull[e]);
+        if (mark_d) f.dirtyD[n[e] >> 6] = 1;
+      }
+    }
+  }
+}
+
+template <int MAJ, int MODE, bool FAULTS>
+__device__ __forceinline__ void scan_body_q(uint4* summ4, uint64_t* rws, uint2* qs, const FrontierBufs& f,
+                                            const uint64_t* __restrict__ S, uint64_t* Sw, uint64_t N, uint32_t R,
+                                            uint32_t k, uint32_t t, uint32_t key0, uint32_t key1, uint64_t per_block,
+                                            bool mark_d, bool direct, bool mid, const Faults& fa) {
+  const uint32_t* summ = (const uint32_t*)summ4;
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  uint2* qw = qs + (tid >> 6) * kQCap;  // this wave's queue
+  const uint32_t n4 = (f.summ_words + 3) / 4;
+  for (uint32_t i = tid; i < n4; i += kScanThreads) summ4[i] = ((const uint4*)f.summ)[i];
+
+  constexpr bool kPush = (MODE & 1) != 0, kPull = (MODE & 2) != 0;
+  const uint64_t maj = MAJ ? full_mask1(R) : 0ull;
+  const uint32_t nm1 = (uint32_t)(N - 1), glog = f.glog;
+  auto summ_bit = [&](uint32_t p) -> bool { return (summ[p >> (glog + 5)] >> ((p >> glog) & 31u)) & 1u; };
+  const uint32_t b0 = blockIdx.x * (uint32_t)per_block, b1 = (uint32_t)min<uint64_t>((uint64_t)b0 + per_block, N);
+  uint32_t qn = 0;  // entries in this wave's queue (wave-uniform)
+  for (uint32_t c0 = b0; c0 < b1; c0 += kRwWords * 64) {
+    const uint32_t c1 = min(c0 + kRwWords * 64, b1);
+    __syncthreads();  // previous chunk done with rws
+    for (uint32_t i = tid; i < ((c1 - c0 + 63) >> 6); i += kScanThreads) rws[i] = rare_word<MAJ>(f, (c0 >> 6) + i, N);
+    __syncthreads();
+    for (uint32_t base = c0; base < c1; base += kScanThreads * kScanUnroll) {
+      uint32_t pp[kScanUnroll][4], cand[kScanUnroll];
+      bool rn[kScanUnroll];
+      bool any = false;
+#pragma unroll
+      for (int u = 0; u < kScanUnroll; ++u) {
+        const uint32_t n = base + u * kScanThreads + tid;
+        const bool valid = n < c1;
+        rn[u] = valid && ((rws[(n - c0) >> 6] >> lane) & 1ull);
+        const bool act = valid && (rn[u] || !((!kPull && MAJ == 0) || (!kPush && MAJ == 1)));
+        cand[u] = 0;  // bit j: edge j is live and has a rare or possibly rare end
+        if (act) {
+          const u32x4 r4 = philox4x32_10(u32x4{n, t, 0u, 0u}, key0, key1);
+          u32x4 lw{0, 0, 0, 0};
+          Reach rc{0u, 0xFFFFFFFFu};
+          if (FAULTS) {
+            if (fa.loss) lw = loss_draws(n, t, 0u, key0, key1);
+            rc = reach_of(n, fa);
+          }
+#pragma unroll
+          for (uint32_t j = 0; j < 4; ++j) {
+            if (j >= k) break;
+            pp[u][j] = peer_from_word(lane_of(r4, j), nm1, n);
+            const bool lost = FAULTS && edge_lost(fa, rc, pp[u][j], lane_of(lw, j));
+            if (!lost && (rn[u] || summ_bit(pp[u][j]))) cand[u] |= 1u << j;
+          }
+        }
+        any = any || cand[u] != 0u;
+      }
+      if (!__ballot(any)) continue;  // most waves of the light rounds
+#pragma unroll
+      for (int u = 0; u < kScanUnroll; ++u) {
+        const uint32_t n = base + u * kScanThreads + tid;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+          if (j >= k) break;
+          const bool c = (cand[u] >> j) & 1u;
+          const uint64_t m = __ballot(c);
+          if (!m) continue;
+          if (c) {
+            const uint32_t pos =
+                qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            const bool h = !rn[u] || summ_bit(pp[u][j]);  // a rare node's edges are all queued
+            qw[pos] = uint2{(n - b0) | (uint32_t)rn[u] << 24 | (uint32_t)h << 25, pp[u][j]};
+          }
+          qn += (uint32_t)__popcll(m);
+          if (qn >= kQFlush) {
+            __builtin_amdgcn_wave_barrier();
+            scan_flush<MAJ, MODE>(qw, kQFlush, f, S, Sw, b0, maj, mark_d, direct, mid, lane);
+            qn -= kQFlush;  // (< 64 left: move them to the front)
+            const uint2 rest = lane < qn ? qw[kQFlush + lane] : uint2{0u, 0u};
+            __builtin_amdgcn_wave_barrier();
+            if (lane < qn) qw[lane] = rest;
+            __builtin_amdgcn_wave_barrier();
+          }
+        }
+      }
+    }
+  }
+  if (qn) {
+    __builtin_amdgcn_wave_barrier();
+    scan_flush<MAJ, MODE>(qw, qn, f, S, Sw, b0, maj, mark_d, direct, mid, lane);
+  }
+}
+
 template <int MODE, bool FAULTS>
 __global__ __launch_bounds__(kScanThreads, kScanWaves) void frontier_scan_kernel(FrontierBufs f, uint64_t* S,
                                                                       uint64_t N, uint32_t R, uint32_t k, uint32_t t,
@@ -350,8 +519,18 @@ __global__ __launch_bounds__(kScanThreads, kScanWaves) void frontier_scan_kernel
                                                                       uint32_t mark_d, uint32_t direct, Faults fa) {
   __shared__ uint4 summ4[kSummBits / 128];
   __shared__ uint64_t rws[kRwWords];
+  __shared__ uint2 qs[(kScanThreads / 64) * kQCap];  // 24 KiB: 128 + 4 + 24 KiB of the CU's 160
   if (rare_count(partial, N, R, maj) == 0) return;  // converged (or nothing injected): nothing moves
   const bool mid = use_mid(f, partial, N, R, maj);  // (the summary kernel built summ2 this round)
+  if (f.scan_q && k <= 4) {
+    if (maj)
+      scan_body_q<1, MODE, FAULTS>(summ4, rws, qs, f, S, S, N, R, k, t, key0, key1, per_block, mark_d != 0, false, mid,
+                                   fa);
+    else
+      scan_body_q<0, MODE, FAULTS>(summ4, rws, qs, f, S, S, N, R, k, t, key0, key1, per_block, mark_d != 0,
+                                   direct != 0, mid, fa);
+    return;
+  }
   if (maj)
     scan_body<1, MODE, FAULTS>(summ4, rws, f, S, S, N, R, k, t, key0, key1, per_block, mark_d != 0, false, mid, fa);
   else
@@ -575,6 +754,7 @@ void frontier_carve(uint64_t N, void* base, FrontierBufs* f) {
   f->g2log = frontier_g2log(N);
   f->summ2_words = frontier_summ2_words(N);
   f->summ2 = f->summ2_words ? (uint32_t*)p : nullptr;
+  f->scan_q = 1;
 }
 
 hipError_t launch_frontier_summary(const FrontierBufs& f, uint64_t N, uint32_t maj, hipStream_t st) {

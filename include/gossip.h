@@ -140,6 +140,8 @@ int gossip_set_stream(gossip_engine_t* eng, void* hip_stream);
  *   "mid_frac"     past 2^25 nodes sparse rounds test a peer in the L2-resident mid-level
  *                  summary once this share of peers would hit the LDS summary (default 0.5;
  *                  decided per round on the device from the exact rare count)
+ *   "scan_queue"   sparse rounds resolve the edges with a possibly rare end from a per-wave
+ *                  queue, 128 at a time (default 1; 0: where they are drawn)
  *   "filter_frac"  dense rounds drop edges by the peer's class above this empty/full fraction
  *                  (default 0.3 up to 2^25 nodes; past that off: the probes miss the L2)
  *   "xd_filter_frac"  exchange dense rounds likewise (default 0.6; >= 1 never)

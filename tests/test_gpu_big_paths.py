@@ -27,6 +27,8 @@ PATHS = {"auto": {}, "sparse_flags": {"sparse_frac": 1.0, "alld_frac": 1e30},
          "sparse_alld": {"sparse_frac": 1.0, "alld_frac": 0, "sparse_direct": 0},
          "sparse_direct": {"sparse_frac": 1.0, "alld_frac": 0, "sparse_direct": 1},
          "sparse_mid": {"sparse_frac": 1.0, "mid_frac": 0},
+         # edges resolved where they are drawn (no per-wave queue; the default before round 5)
+         "sparse_noq": {"sparse_frac": 1.0, "scan_queue": 0},
          # every round dense with serve's ids regrouped into long runs (param serve_lr, opt-in: the
          # A/B of profiles/r05_lr2/ measured it slower at 2^27, kept under test)
          "dense_serve_lr": {"sparse_frac": -1.0, "serve_lr": 1}}

@@ -22,6 +22,7 @@ for spec in sys.argv[1:]:
         r = e.step(64, with_infected=False)
     ms, n = e.kernel_time(0)
     d, nd = e.kernel_time(3)
+    sp, ns = e.kernel_time(4)
     print(f"[{spec}] {ms / steps:.3f} ms/step, rounds {r.rounds}, dense rounds/step {nd / steps:.1f}, "
-          f"dense {d * 1e3 / max(nd, 1):.1f} us", flush=True)
+          f"dense {d * 1e3 / max(nd, 1):.1f} us, sparse {sp / steps:.3f} ms/step in {ns / steps:.1f} rounds", flush=True)
     e.close()
