@@ -1439,7 +1439,7 @@ int gossip_set_param(gossip_engine_t* e, const char* name, double v) {
   } else if (n == "mid_frac") {
     e->mid_frac = v;
   } else if (n == "scan_queue") {
-    e->fb.scan_q = v != 0 ? 1u : 0u;
+    e->fb.scan_q = e->lf.scan_q = v != 0 ? 1u : 0u;
   } else if (n == "filter_frac") {
     e->filter_frac = v;
     e->filter_frac_set = true;

@@ -540,9 +540,23 @@ __global__ __launch_bounds__(kScanThreads, kScanWaves) void frontier_scan_kernel
 
 // Stats of one 64-node group whose words went from old to nw (old == 0 in a
 // rebuild), and its two bitmap words (wave-exclusive plain stores).
+// Per-rumor counts are summed bit-sliced per lane (slice b = weight 2^b, up to 31 groups) and
+// transposed once per slice when the slices fill up: 5 transposes per 31 groups instead of one
+// per group (the transpose was most of a commit's VALU work).
 struct GroupStats {
   uint64_t hash = 0;
   uint32_t full = 0, nz = 0, c_lane = 0;
+  uint64_t sl[5] = {0, 0, 0, 0, 0};
+  uint32_t sn = 0;  // words added to sl since the last fold (wave-uniform)
+
+  __device__ __forceinline__ void fold(uint32_t lane) {
+#pragma unroll
+    for (uint32_t b = 0; b < 5; ++b) {
+      if (__ballot(sl[b] != 0)) c_lane += (uint32_t)__popcll(transpose64(sl[b], lane)) << b;
+      sl[b] = 0;
+    }
+    sn = 0;
+  }
 
   __device__ __forceinline__ void add(const FrontierBufs& f, uint64_t g, uint64_t n, bool valid, uint64_t old,
                                       uint64_t nw, uint64_t fm, bool do_hash, uint32_t lane) {
@@ -558,13 +572,23 @@ struct GroupStats {
       hash += mix64(nw + (f.id0 + n) * kGold64);
       if (old) hash -= mix64(old + (f.id0 + n) * kGold64);
     }
-    if (__ballot(nb != 0)) c_lane += (uint32_t)__popcll(transpose64(nb, lane));
+    if (__ballot(nb != 0)) {
+      uint64_t c = nb;  // ripple-carry add into the slices
+#pragma unroll
+      for (uint32_t b = 0; b < 5; ++b) {
+        const uint64_t t = sl[b] & c;
+        sl[b] ^= c;
+        c = t;
+      }
+      if (++sn == 31) fold(lane);
+    }
   }
 
   // block-level fold into the running totals
   __device__ __forceinline__ void flush(uint64_t* __restrict__ partial, uint32_t R, uint32_t* cnt,
                                         uint64_t (*red)[kCommitThreads / 64]) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (sn) fold(lane);
     if (lane < R && c_lane) atomicAdd(&cnt[lane], c_lane);
     const uint64_t h = wave_sum64(hash);
     if (lane == 0) {
@@ -645,12 +669,16 @@ __global__ __launch_bounds__(kCommitThreads) void frontier_commit_kernel(Frontie
           ++cntg;
         }
       }
-      uint64_t d[kCommitUnroll], old[kCommitUnroll];
+      uint64_t d[kCommitUnroll], old[kCommitUnroll], rw[kCommitUnroll];
+      // direct rounds: D holds deltas of S_t's rare (nonzero) nodes only (every delta into a
+      // majority node went to S), so D is read only where S_t's bitmap word has the node
+#pragma unroll
+      for (int u = 0; u < kCommitUnroll; ++u) rw[u] = abs_t && gi[u] < 64 ? f.nzb[(c << 6) + gi[u]] : ~0ull;
 #pragma unroll
       for (int u = 0; u < kCommitUnroll; ++u) {
         const uint64_t n = (((c << 6) + (gi[u] & 63u)) << 6) + lane;
         const bool valid = gi[u] < 64 && n < N;
-        const bool hd = gi[u] < 64 && ((mD >> gi[u]) & 1ull);
+        const bool hd = gi[u] < 64 && ((mD >> gi[u]) & 1ull) && ((rw[u] >> lane) & 1ull);
         d[u] = valid && hd ? f.D[n] : 0ull;
         old[u] = valid ? S[n] : 0ull;
       }

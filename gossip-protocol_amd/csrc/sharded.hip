@@ -18,7 +18,7 @@ namespace {
 
 constexpr int kScanThreads = 1024;
 constexpr uint32_t kScanGrid = 256;  // one block per CU: the summary takes 128 KiB of LDS
-constexpr uint32_t kRwWords = 1024;  // own rare-bitmap words staged per chunk (64K nodes)
+constexpr uint32_t kRwWords = 512;   // own rare-bitmap words staged per chunk (32K nodes; LDS room for the queues)
 constexpr int kScanUnroll = 2;
 constexpr uint32_t kMsgShift = 40;   // message node word: owner << 40 | node at the owner
 // up to this many rare nodes (all shards), the index skips the per-word ranks and the
@@ -347,13 +347,182 @@ __device__ __forceinline__ void scan_body(uint4* summ4, uint64_t* rws, uint32_t*
   }
 }
 
+// Queued scan (frontier.hip scan_body_q; FrontierBufs::scan_q, k <= 4): the edges with a possibly
+// rare end wait in a per-wave LDS queue and are resolved 128 at a time, two per lane, every
+// load of the chain issued before any is used.  A queued edge: x = own index - block base
+// (< 2^24) | rare(n) << 24 | summary hit(p) << 25, y = p (global id).
+constexpr uint32_t kQFlush = 128;
+constexpr uint32_t kQCap = kQFlush + 64;
+
+template <int MAJ, int MODE, bool FAULTS>
+__device__ __forceinline__ void scan_body_q(uint4* summ4, uint64_t* rws, uint2* qs, uint32_t* lcnt,
+                                            const ScanArgs& a) {
+  const uint32_t* summ = (const uint32_t*)summ4;
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  uint2* qw = qs + (tid >> 6) * kQCap;  // this wave's queue
+  const uint32_t n4 = (a.gsumm_words + 3) / 4;
+  for (uint32_t i = tid; i < n4; i += kScanThreads) summ4[i] = ((const uint4*)a.gsumm)[i];
+
+  constexpr bool kPush = (MODE & 1) != 0, kPull = (MODE & 2) != 0;
+  const uint64_t maj = MAJ ? full_mask1(a.R) : 0ull, nm1 = a.N - 1;
+  const uint32_t glog = a.gglog, lo = (uint32_t)a.lo, nown = (uint32_t)a.nown, k = a.k;
+  auto summ_bit = [&](uint32_t p) -> bool { return (summ[p >> (glog + 5)] >> ((p >> glog) & 31u)) & 1u; };
+  const uint64_t below = (1ull << lane) - 1ull;
+  auto push_to = [&](uint32_t p, uint64_t d) {  // every lane of the wave together (scan_body)
+    const bool local = d && (p - lo < nown);
+    if (local) {
+      atomicOr((unsigned long long*)&a.lf.D[p - lo], (unsigned long long)d);
+      if (a.mark_d) a.lf.dirtyD[(p - lo) >> 6] = 1;
+    }
+    const bool remote = d && !local;
+    const uint64_t m = __ballot(remote);
+    if (!m) return;
+    const uint32_t first = (uint32_t)__builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane == first) base = atomicAdd(lcnt, (uint32_t)__popcll(m));
+    base = __shfl(base, first, 64);
+    if (remote) {
+      const uint32_t q = (uint32_t)(p / a.Nl);
+      a.msg[blockIdx.x * a.seg_cap + base + (uint32_t)__popcll(m & below)] =
+          SxItem{((uint64_t)q << kMsgShift) | (p - (uint64_t)q * a.Nl), d};
+    }
+  };
+  const uint32_t b0 = blockIdx.x * (uint32_t)a.per_block;
+  const uint32_t b1 = (uint32_t)min<uint64_t>((uint64_t)b0 + a.per_block, a.nown);
+  constexpr int kE = kQFlush / 64;
+  auto flush = [&](uint32_t nf) {
+    uint32_t i[kE], p[kE];
+    bool rn[kE], hit[kE];
+#pragma unroll
+    for (int e = 0; e < kE; ++e) {
+      const uint32_t s = lane + 64u * e;
+      const uint2 q = s < nf ? qw[s] : uint2{0u, 0u};
+      i[e] = b0 + (q.x & 0xFFFFFFu);
+      rn[e] = (q.x >> 24) & 1u;
+      hit[e] = (q.x >> 25) & 1u;
+      p[e] = q.y;
+    }
+    if (a.gsumm2) {
+      uint32_t sw[kE];
+#pragma unroll
+      for (int e = 0; e < kE; ++e) sw[e] = hit[e] ? a.gsumm2[p[e] >> (a.g2log + 5)] : 0u;
+#pragma unroll
+      for (int e = 0; e < kE; ++e) hit[e] = hit[e] && ((sw[e] >> ((p[e] >> a.g2log) & 31u)) & 1u);
+    }
+    uint64_t rw[kE];
+#pragma unroll
+    for (int e = 0; e < kE; ++e) rw[e] = hit[e] ? a.grb[p[e] >> 6] : 0ull;
+#pragma unroll
+    for (int e = 0; e < kE; ++e) hit[e] = hit[e] && ((rw[e] >> (p[e] & 63u)) & 1ull);
+    uint32_t pre[kE];
+#pragma unroll
+    for (int e = 0; e < kE; ++e) pre[e] = hit[e] && (p[e] - lo >= nown) && a.gpre ? a.gpre[p[e] >> 6] : 0u;
+    uint64_t x[kE], vp[kE];
+#pragma unroll
+    for (int e = 0; e < kE; ++e) {
+      x[e] = rn[e] ? a.S[i[e]] : maj;
+      if (!hit[e]) vp[e] = maj;
+      else if (p[e] - lo < nown) vp[e] = a.S[p[e] - lo];
+      else vp[e] = rare_value(a, p[e], rw[e], pre[e]);
+    }
+    uint64_t dpush[kE], dpull[kE];
+#pragma unroll
+    for (int e = 0; e < kE; ++e) {
+      const bool any = rn[e] || hit[e];  // both ends majority (or an empty slot): nothing moves
+      dpush[e] = kPush && any ? x[e] & ~vp[e] : 0ull;
+      dpull[e] = kPull && any ? vp[e] & ~x[e] : 0ull;
+    }
+#pragma unroll
+    for (int e = 0; e < kE; ++e) {
+      push_to(p[e], dpush[e]);
+      if (dpull[e]) {
+        atomicOr((unsigned long long*)&a.lf.D[i[e]], (unsigned long long)dpull[e]);
+        if (a.mark_d) a.lf.dirtyD[i[e] >> 6] = 1;
+      }
+    }
+  };
+  uint32_t qn = 0;  // entries in this wave's queue (wave-uniform)
+  for (uint32_t c0 = b0; c0 < b1; c0 += kRwWords * 64) {
+    const uint32_t c1 = min(c0 + kRwWords * 64, b1);
+    __syncthreads();  // previous chunk done with rws
+    for (uint32_t i = tid; i < ((c1 - c0 + 63) >> 6); i += kScanThreads)
+      rws[i] = own_rare(a.lf, (c0 >> 6) + i, a.nown, MAJ);
+    __syncthreads();
+    for (uint32_t base = c0; base < c1; base += kScanThreads * kScanUnroll) {
+      uint32_t pp[kScanUnroll][4], cand[kScanUnroll];
+      bool rn[kScanUnroll];
+      bool any = false;
+#pragma unroll
+      for (int u = 0; u < kScanUnroll; ++u) {
+        const uint32_t i = base + u * kScanThreads + tid;
+        const bool valid = i < c1;
+        const uint32_t n = lo + i;
+        rn[u] = valid && ((rws[(i - c0) >> 6] >> lane) & 1ull);
+        const bool act = valid && (rn[u] || !((!kPull && MAJ == 0) || (!kPush && MAJ == 1)));
+        cand[u] = 0;  // bit j: edge j is live and has a rare or possibly rare end
+        if (act) {
+          const u32x4 r4 = philox4x32_10(u32x4{n, a.t, 0u, 0u}, a.key0, a.key1);
+          const u32x4 lw = FAULTS && a.fa.loss ? loss_draws(n, a.t, 0u, a.key0, a.key1) : u32x4{0, 0, 0, 0};
+          const Reach rc = FAULTS ? reach_of(n, a.fa) : Reach{0u, 0xFFFFFFFFu};  // n's partition block (§2.8)
+#pragma unroll
+          for (uint32_t j = 0; j < 4; ++j) {
+            if (j >= k) break;
+            pp[u][j] = peer_from_word(lane_of(r4, j), nm1, n);
+            const bool lost = FAULTS && edge_lost(a.fa, rc, pp[u][j], lane_of(lw, j));
+            if (!lost && (rn[u] || summ_bit(pp[u][j]))) cand[u] |= 1u << j;
+          }
+        }
+        any = any || cand[u] != 0u;
+      }
+      if (!__ballot(any)) continue;
+#pragma unroll
+      for (int u = 0; u < kScanUnroll; ++u) {
+        const uint32_t i = base + u * kScanThreads + tid;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+          if (j >= k) break;
+          const bool c = (cand[u] >> j) & 1u;
+          const uint64_t m = __ballot(c);
+          if (!m) continue;
+          if (c) {
+            const uint32_t pos =
+                qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            const bool h = !rn[u] || summ_bit(pp[u][j]);  // a rare node's edges are all queued
+            qw[pos] = uint2{(i - b0) | (uint32_t)rn[u] << 24 | (uint32_t)h << 25, pp[u][j]};
+          }
+          qn += (uint32_t)__popcll(m);
+          if (qn >= kQFlush) {
+            __builtin_amdgcn_wave_barrier();
+            flush(kQFlush);
+            qn -= kQFlush;  // (< 64 left: move them to the front)
+            const uint2 rest = lane < qn ? qw[kQFlush + lane] : uint2{0u, 0u};
+            __builtin_amdgcn_wave_barrier();
+            if (lane < qn) qw[lane] = rest;
+            __builtin_amdgcn_wave_barrier();
+          }
+        }
+      }
+    }
+  }
+  if (qn) {
+    __builtin_amdgcn_wave_barrier();
+    flush(qn);
+  }
+}
+
 template <int MODE, bool FAULTS>
 __global__ __launch_bounds__(kScanThreads) void sx_scan_kernel(ScanArgs a, uint32_t maj) {
   __shared__ uint4 summ4[kSummBits / 128];
   __shared__ uint64_t rws[kRwWords];
+  __shared__ uint2 qs[(kScanThreads / 64) * kQCap];  // 24 KiB
   __shared__ uint32_t lcnt;
   if (threadIdx.x == 0) lcnt = 0;  // (scan_body syncs before the first use)
-  if (maj)
+  if (a.lf.scan_q && a.k <= 4) {
+    if (maj)
+      scan_body_q<1, MODE, FAULTS>(summ4, rws, qs, &lcnt, a);
+    else
+      scan_body_q<0, MODE, FAULTS>(summ4, rws, qs, &lcnt, a);
+  } else if (maj)
     scan_body<1, MODE, FAULTS>(summ4, rws, &lcnt, a);
   else
     scan_body<0, MODE, FAULTS>(summ4, rws, &lcnt, a);
