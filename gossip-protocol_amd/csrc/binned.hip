@@ -633,7 +633,7 @@ __device__ __forceinline__ void tile_epilogue(const unsigned long long* acc, uin
                                               uint64_t* __restrict__ Snext, uint64_t* __restrict__ partial,
                                               uint32_t R, uint32_t flags, uint32_t* cnt, uint64_t* red_hash,
                                               uint32_t* red_full, uint32_t* red_nz, uint64_t* __restrict__ nzb,
-                                              uint64_t* __restrict__ fullb) {
+                                              uint64_t* __restrict__ fullb, uint64_t* btot) {
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint64_t fm = full_mask1(R);
   const bool do_hash = (flags & 1u) != 0;
@@ -721,9 +721,30 @@ __device__ __forceinline__ void tile_epilogue(const unsigned long long* acc, uin
       f += red_full[w];
       z += red_nz[w];
     }
-    if (f) atomicAdd((unsigned long long*)&partial[0], (unsigned long long)f);
-    if (h) atomicAdd((unsigned long long*)&partial[3], (unsigned long long)h);
-    if (z) atomicAdd((unsigned long long*)&partial[4 + R], (unsigned long long)z);  // nonzero nodes
+    if (btot) {  // a persistent block: its tiles' totals stay in LDS until block_totals_flush
+      btot[0] += f;
+      btot[1] += h;
+      btot[2] += z;
+    } else {
+      if (f) atomicAdd((unsigned long long*)&partial[0], (unsigned long long)f);
+      if (h) atomicAdd((unsigned long long*)&partial[3], (unsigned long long)h);
+      if (z) atomicAdd((unsigned long long*)&partial[4 + R], (unsigned long long)z);  // nonzero nodes
+    }
+  }
+  if (!btot && tid < R && cnt[tid]) atomicAdd((unsigned long long*)&partial[4 + tid], (unsigned long long)cnt[tid]);
+}
+
+// A persistent apply block's totals (tile_epilogue with btot), once, after its last tile: ~67
+// same-address atomics per block instead of per tile (8192 tiles at 2^27).  All-dense rounds
+// 510 -> 502 us at 2^24, equal at 2^27 (profiles/r05_bt/).
+__device__ __forceinline__ void block_totals_flush(uint64_t* __restrict__ partial, uint32_t R, const uint32_t* cnt,
+                                                   const uint64_t* btot) {
+  const uint32_t tid = threadIdx.x;
+  __syncthreads();
+  if (tid == 0) {
+    if (btot[0]) atomicAdd((unsigned long long*)&partial[0], (unsigned long long)btot[0]);
+    if (btot[1]) atomicAdd((unsigned long long*)&partial[3], (unsigned long long)btot[1]);
+    if (btot[2]) atomicAdd((unsigned long long*)&partial[4 + R], (unsigned long long)btot[2]);
   }
   if (tid < R && cnt[tid]) atomicAdd((unsigned long long*)&partial[4 + tid], (unsigned long long)cnt[tid]);
 }
@@ -1171,6 +1192,9 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
   const bool dyn = b.dyn && nv >= 8 && (nv & 7u) == 0;
   const TileQueue tq{b.dyn ? b.dyn + 8 : nullptr, nv};
   __shared__ uint32_t s_claim;
+  __shared__ uint64_t btot[3];  // the block's totals over its tiles (cnt too: not reset per tile)
+  if (tid < 64) cnt[tid] = 0;
+  if (tid < 3) btot[tid] = 0;
   for (uint32_t v = blockIdx.x;;) {
   __syncthreads();  // the previous epilogue is done with acc, cnt and s_claim
   if (dyn) {
@@ -1187,7 +1211,6 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
 #pragma unroll
     for (uint32_t q = 0; q < kTileQ; ++q) ((uint4*)acc)[q * kTileThreads + tid] = xr[q];
   }
-  if (tid < 64) cnt[tid] = 0;
   __syncthreads();
   const uint32_t wave = tid >> 6;
   const bool split = kApplySplit && mode == 3;
@@ -1230,9 +1253,11 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
     }
   }
   __syncthreads();
-  tile_epilogue(acc, node0, Nn, hid0, Snext, partial, R, flags, cnt, red_hash, red_full, red_nz, b.nzb, b.fullb);
+  tile_epilogue(acc, node0, Nn, hid0, Snext, partial, R, flags, cnt, red_hash, red_full, red_nz, b.nzb, b.fullb,
+                btot);
   if (!dyn) v += gridDim.x;
   }
+  block_totals_flush(partial, R, cnt, btot);
 }
 
 // Apply grid: one persistent block per CU (BinGeom::apply_grid = 0: one block per tile).
@@ -1788,6 +1813,9 @@ __global__ __launch_bounds__(kTileThreads) void xd_apply_kernel(XdGeom g, XdBufs
   const bool do_push = (mode == 1 || mode == 3) && (!split || wave < nwav / 2);
   const bool do_pull = (mode == 2 || mode == 3) && (!split || wave >= nwav / 2);
   const uint32_t qt0 = split ? kTileThreads / 2 : 0u, qnt = split ? kTileThreads / 2 : kTileThreads;
+  __shared__ uint64_t btot[3];  // the block's totals over its tiles (cnt too: not reset per tile)
+  if (tid < 64) cnt[tid] = 0;
+  if (tid < 3) btot[tid] = 0;
   for (uint32_t v = blockIdx.x; v < nv; v += gridDim.x) {
     const uint32_t X = xcd_remap(v, nv);
     const uint64_t node0 = (uint64_t)X << kTileDLog;
@@ -1804,7 +1832,6 @@ __global__ __launch_bounds__(kTileThreads) void xd_apply_kernel(XdGeom g, XdBufs
       pl[i] = rlofs[(size_t)s * (G + 1) + o];
       po[i] = o < G ? b.roff[(size_t)s * G + o] : 0u;
     }
-    if (tid < 64) cnt[tid] = 0;
     __syncthreads();
     if (do_push) push_walk<kXbVZ, 0>(g.r, b.rb, X, acc, wmask, wlist, split ? nwav / 2 : 0u);
     if (do_pull) {  // replies, in send order: region s's items are G runs (one per owner)
@@ -1840,8 +1867,10 @@ __global__ __launch_bounds__(kTileThreads) void xd_apply_kernel(XdGeom g, XdBufs
       }
     }
     __syncthreads();
-    tile_epilogue(acc, node0, g.nown, g.lo, Snext, partial, R, flags, cnt, red_hash, red_full, red_nz, nzb, fullb);
+    tile_epilogue(acc, node0, g.nown, g.lo, Snext, partial, R, flags, cnt, red_hash, red_full, red_nz, nzb, fullb,
+                  btot);
   }
+  block_totals_flush(partial, R, cnt, btot);
 }
 
 }  // namespace

@@ -42,10 +42,15 @@ __device__ __forceinline__ T scan_ld(const T* p) {
 }
 constexpr uint32_t kScanGrid = 256;  // one block per CU: the summary takes 128 KiB of LDS
 constexpr uint32_t kScanWaves = 4;   // waves per SIMD (launch bounds)
-constexpr int kCommitThreads = 256;
+// commit / rebuild blocks of 1024 threads, at most kCommitMaxBlocks of them: each block ends in
+// ~67 same-address atomics on the totals, which cost more than the waves gain past ~512 blocks
+// (2^24 sparse rounds 132 -> 125 us against 256-thread blocks up to 4096; profiles/r05_cc2/)
+constexpr int kCommitThreads = 1024;
+constexpr uint32_t kCommitMaxBlocks = 512;
 constexpr uint32_t kRwWords = 512;   // rare-bitmap words staged per scan chunk (32K nodes; LDS room for the queues)
 constexpr int kScanUnroll = 2;  // nodes per lane per scan step (1: equal, 4: slower)
 constexpr int kCommitUnroll = 4;     // dirty groups per wave per commit step
+constexpr uint32_t kCommitChunkLog = 6;  // 64 groups per wave chunk (16 / 32: slower, profiles/r05_cc/)
 
 // valid-node mask of bitmap word w (bits past N are zero in both bitmaps)
 __device__ __forceinline__ uint64_t word_valid(uint64_t w, uint64_t N) {
@@ -650,10 +655,10 @@ __global__ __launch_bounds__(kCommitThreads) void frontier_commit_kernel(Frontie
   const uint64_t fm = full_mask1(R), ngroups = (N + 63) >> 6;
   const bool do_hash = (flags & 1u) != 0;
   GroupStats gs;
-  for (uint64_t c = (uint64_t)blockIdx.x * (kCommitThreads / 64) + wave; (c << 6) < ngroups;
+  for (uint64_t c = (uint64_t)blockIdx.x * (kCommitThreads / 64) + wave; (c << kCommitChunkLog) < ngroups;
        c += (uint64_t)gridDim.x * (kCommitThreads / 64)) {
-    const uint64_t gl = (c << 6) + lane;
-    const bool gv = gl < ngroups;
+    const uint64_t gl = (c << kCommitChunkLog) + lane;
+    const bool gv = lane < (1u << kCommitChunkLog) && gl < ngroups;
     const uint8_t fd = gv ? (all_d ? 1 : f.dirtyD[gl]) : 0;
     if (fd && !all_d) f.dirtyD[gl] = 0;
     const uint64_t mD = __ballot(fd != 0);
@@ -673,10 +678,10 @@ __global__ __launch_bounds__(kCommitThreads) void frontier_commit_kernel(Frontie
       // direct rounds: D holds deltas of S_t's rare (nonzero) nodes only (every delta into a
       // majority node went to S), so D is read only where S_t's bitmap word has the node
 #pragma unroll
-      for (int u = 0; u < kCommitUnroll; ++u) rw[u] = abs_t && gi[u] < 64 ? f.nzb[(c << 6) + gi[u]] : ~0ull;
+      for (int u = 0; u < kCommitUnroll; ++u) rw[u] = abs_t && gi[u] < 64 ? f.nzb[(c << kCommitChunkLog) + gi[u]] : ~0ull;
 #pragma unroll
       for (int u = 0; u < kCommitUnroll; ++u) {
-        const uint64_t n = (((c << 6) + (gi[u] & 63u)) << 6) + lane;
+        const uint64_t n = (((c << kCommitChunkLog) + (gi[u] & 63u)) << 6) + lane;
         const bool valid = gi[u] < 64 && n < N;
         const bool hd = gi[u] < 64 && ((mD >> gi[u]) & 1ull) && ((rw[u] >> lane) & 1ull);
         d[u] = valid && hd ? f.D[n] : 0ull;
@@ -685,7 +690,7 @@ __global__ __launch_bounds__(kCommitThreads) void frontier_commit_kernel(Frontie
 #pragma unroll
       for (int u = 0; u < kCommitUnroll; ++u) {
         if ((uint32_t)u >= cntg) break;
-        const uint64_t g = (c << 6) + gi[u];
+        const uint64_t g = (c << kCommitChunkLog) + gi[u];
         const uint64_t n = (g << 6) + lane;
         const bool valid = n < N;
         const uint64_t nw = old[u] | d[u];
@@ -730,7 +735,7 @@ __global__ void frontier_inject_kernel(FrontierBufs f, uint64_t* S, uint64_t N, 
 uint32_t commit_grid(uint64_t N) {
   const uint64_t groups = (N + 63) >> 6, per = kCommitThreads / 64;
   const uint64_t blocks = (groups + per - 1) / per;
-  return (uint32_t)(blocks < 2048 ? blocks : 2048);
+  return (uint32_t)(blocks < kCommitMaxBlocks ? blocks : kCommitMaxBlocks);
 }
 
 }  // namespace
@@ -795,9 +800,10 @@ hipError_t launch_frontier_summary(const FrontierBufs& f, uint64_t N, uint32_t m
 hipError_t launch_frontier_commit(const FrontierBufs& f, uint64_t* S, uint64_t N, uint64_t* partial, uint32_t R,
                                   uint32_t dmode, uint32_t flags, hipStream_t st) {
   if (N == 0) return hipSuccess;  // a shard without nodes
-  const uint64_t wchunks = (((N + 63) >> 6) + 63) >> 6;  // 64-group chunks, one per wave
+  const uint64_t wchunks = (((N + 63) >> 6) + (1u << kCommitChunkLog) - 1) >> kCommitChunkLog;  // one per wave
   const uint64_t cblocks = (wchunks + kCommitThreads / 64 - 1) / (kCommitThreads / 64);
-  frontier_commit_kernel<<<(uint32_t)(cblocks < 4096 ? cblocks : 4096), kCommitThreads, 0, st>>>(f, S, N, partial,
+  frontier_commit_kernel<<<(uint32_t)(cblocks < kCommitMaxBlocks ? cblocks : kCommitMaxBlocks), kCommitThreads, 0,
+                           st>>>(f, S, N, partial,
                                                                                                  R, flags, dmode);
   return hipGetLastError();
 }
