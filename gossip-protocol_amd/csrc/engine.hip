@@ -165,7 +165,7 @@ struct gossip_engine {
   double filter_frac = 0.3;       // dense rounds filter edges by the peer's class above this empty / full fraction
   bool filter_frac_set = false;   // else off past 2^25 nodes (filter_frac_of)
   double xd_filter_frac = 0.6;    // exchange rounds likewise (their probe hits a G-shard class image: G = 8 sweep)
-  double alld_frac = 1.0 / 64;    // sparse rounds with k * rare >= alld_frac * N commit every group's D (bench sweep)
+  double alld_frac = 1.0 / 128;   // sparse rounds with k * rare >= alld_frac * N commit every group's D (sweep: profiles/r05_ad/)
   bool sparse_direct = true;      // ... and with an empty majority take the pushes into empty peers in S (kSparseDirect)
   double mid_frac = 0.5;          // sparse rounds test peers in the mid-level summary once this share hits the LDS one
   // pipelined rounds (binned engines): the host picks each round's path from the

@@ -134,7 +134,7 @@ int gossip_set_stream(gossip_engine_t* eng, void* hip_stream);
  *   "sparse_frac"  random modes: a round runs sparse when the rare class is at most
  *                  this fraction of N (default 1/16; sharded 1/4, or 1/25 when the dense
  *                  rounds are exchange rounds; < 0 never, >= 1 always)
- *   "alld_frac"    sparse rounds commit every group's D once k x rare >= this x N
+ *   "alld_frac"    sparse rounds commit every group's D once k x rare >= this x N (default 1/128)
  *   "sparse_direct"  such rounds with an empty majority OR the pushes into empty peers
  *                  straight into the state and recompute the totals (default 1; 0: into D)
  *   "mid_frac"     past 2^25 nodes sparse rounds test a peer in the L2-resident mid-level
