@@ -103,6 +103,9 @@ struct gossip_engine {
   // one memset per round move both)
   uint64_t *ae_aux = nullptr, *ae_aux_h = nullptr;
   bool ae_aux_alias = false;
+  // one-engine ANTIENTROPY: gossip_reset's zeroing of V is pending (set_dev does it before any other
+  // call; gossip_inject_random, which writes every row, drops it: a 4 GiB memset at configs[4])
+  bool ae_v_zero = false;
   uint32_t *ae_eid = nullptr, *ae_erow = nullptr, *ae_claim = nullptr, *ae_segn = nullptr;
   void* ae_pmask = nullptr;  // dense rounds: [N][k] push masks
   uint32_t ae_nseg = 1, ae_spc = 1, ae_segcap = 1;
@@ -254,6 +257,10 @@ namespace {
 
 int set_dev(gossip_engine* e) {
   HIP_OK(e, hipSetDevice(e->device));
+  if (e->ae_v_zero) {
+    e->ae_v_zero = false;
+    HIP_OK(e, hipMemsetAsync(e->V, 0, e->N * e->R * 4, e->stream));
+  }
   return GOSSIP_OK;
 }
 
@@ -760,15 +767,23 @@ int ae_round(gossip_engine* e) {
   bool sparse = ae_plan_sparse(e);
   e->ae_dense_next = false;
   e->ae_sparse_last = false;
+  // partial and the aux words after it start at zero: cleared by the binned emit's block 0 (the
+  // round's first kernel; no memset and no host gap, profiles/r05_ae3/), else by a memset
+  const uint32_t nz = (uint32_t)(part_len(e) + 2);
+  const bool dbin = e->ae_dbin && e->ae_dbin_on;
+  if (sparse ? !e->ae_bin : !dbin) HIP_OK(e, hipMemsetAsync(e->partial_d, 0, (size_t)nz * 8, e->stream));
   if (sparse) {
     if (++e->ae_epoch == 0) {  // claims hold epochs: restart them after a wrap
       HIP_OK(e, hipMemsetAsync(e->ae_claim, 0, (size_t)e->N * 4, e->stream));
       e->ae_epoch = 1;
     }
-    const AeArgs a = make_ae_args(e);  // (partial and aux cleared by compute_round)
+    AeArgs a = make_ae_args(e);
     if ((rc = timer_begin(e, 2))) return rc;
     if (e->ae_bin) {
+      a.zero = e->partial_d;
+      a.nzero = nz;
       HIP_OK(e, launch_ae_sparse_binned(a, e->stream));  // churn fused into its first pass
+      a.zero = nullptr;
     } else {
       HIP_OK(e, launch_ae_churn(a, e->stream));
       HIP_OK(e, launch_ae_sparse(a, e->stream));
@@ -787,9 +802,11 @@ int ae_round(gossip_engine* e) {
   }
   if (!sparse) {
     const AeArgs a = make_ae_args(e);
-    bool binned = e->ae_dbin && e->ae_dbin_on;
+    bool binned = dbin;
     if (binned) {  // in-edge gathers, stats fused (no timer-1 part)
       AeArgs d = a;
+      d.zero = e->partial_d;
+      d.nzero = nz;
       d.btl = e->ae_dg.tl;
       d.bnt = e->ae_dg.nt;
       d.boff = e->ae_dboff;
@@ -936,9 +953,8 @@ int step_ae(gossip_engine* e, uint32_t max_rounds, gossip_round_stats_t* stats, 
 // compute S_{t+1} of the owned shard from the gathered image + partial stats (device)
 int compute_round(gossip_engine* e, const uint64_t* gathered) {
   const size_t bytes = (size_t)e->W * e->Nl * 8;
-  // (one-engine ANTIENTROPY: the aux words after partial_d too)
-  if (!e->binned) HIP_OK(e, hipMemsetAsync(e->partial_d, 0, (part_len(e) + (e->ae_aux_alias ? 2 : 0)) * 8, e->stream));
-  if (e->mode == GOSSIP_MODE_ANTIENTROPY) return ae_round(e);
+  if (e->mode == GOSSIP_MODE_ANTIENTROPY) return ae_round(e);  // (clears partial and aux itself)
+  if (!e->binned) HIP_OK(e, hipMemsetAsync(e->partial_d, 0, part_len(e) * 8, e->stream));
   RoundArgs a = make_args(e, gathered);
   int rc;
   if (e->mode == GOSSIP_MODE_FLOOD) {
@@ -1555,7 +1571,7 @@ int gossip_reset(gossip_engine_t* e) {
     e->aex_churned = ~0ull;
     e->aex_target_ok = e->aex_patch_ok = e->aex_inc_ok = false;
   } else if (e->mode == GOSSIP_MODE_ANTIENTROPY) {
-    HIP_OK(e, hipMemsetAsync(e->V, 0, e->N * e->R * 4, e->stream));
+    e->ae_v_zero = true;  // V: zeroed by the next call's set_dev, unless inject_random overwrites it
     HIP_OK(e, hipMemsetAsync(e->target, 0, 256, e->stream));
     HIP_OK(e, launch_ae_fill_alive(e->alive, e->N, e->stream));
     e->ae_sb_valid = false;
@@ -1623,6 +1639,7 @@ int gossip_inject(gossip_engine_t* e, uint64_t node, uint32_t rumor) {
 
 int gossip_inject_random(gossip_engine_t* e) {
   if (!e) return GOSSIP_EINVAL;
+  if (e->mode == GOSSIP_MODE_ANTIENTROPY && !e->aex) e->ae_v_zero = false;  // ae_init writes every row
   if (int rc = set_dev(e)) return rc;
   if (e->aex) {
     HIP_OK(e, launch_aex_init(e->V, e->lo, e->nown, e->R, e->key0, e->key1, e->stream));
@@ -1707,8 +1724,10 @@ int gossip_round_compute(gossip_engine_t* e, uint64_t* partial) {
   if (e->mode == GOSSIP_MODE_FLOOD && !e->has_topo) return e->fail(GOSSIP_ESTATE, "FLOOD needs a topology");
   if (int rc = set_dev(e)) return rc;
   if (int rc = compute_round(e, current_image(e))) return rc;
-  HIP_OK(e, hipMemcpyAsync(e->partial_h, e->partial_d, part_len(e) * 8, hipMemcpyDeviceToHost, e->stream));
-  HIP_OK(e, hipStreamSynchronize(e->stream));
+  if (e->mode != GOSSIP_MODE_ANTIENTROPY) {  // (ae_round read partial and aux back already)
+    HIP_OK(e, hipMemcpyAsync(e->partial_h, e->partial_d, part_len(e) * 8, hipMemcpyDeviceToHost, e->stream));
+    HIP_OK(e, hipStreamSynchronize(e->stream));
+  }
   if (int rc = timer_collect(e)) return rc;
   std::memcpy(partial, e->partial_h, part_len(e) * 8);
   if (e->mode != GOSSIP_MODE_ANTIENTROPY) partial[1] = e->nown;
