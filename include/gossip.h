@@ -140,6 +140,9 @@ int gossip_set_stream(gossip_engine_t* eng, void* hip_stream);
  *   "mid_frac"     past 2^25 nodes sparse rounds test a peer in the L2-resident mid-level
  *                  summary once this share of peers would hit the LDS summary (default 0.5;
  *                  decided per round on the device from the exact rare count)
+ *   "place_tries"  a binned engine with a record slab of 512 MiB or more times a zero-state trial
+ *                  round on up to this many fresh allocations of the slab before its first round
+ *                  and keeps the fastest (default 8; 1: the first allocation)
  *   "scan_queue"   sparse rounds resolve the edges with a possibly rare end from a per-wave
  *                  queue, 128 at a time (default 1; 0: where they are drawn)
  *   "filter_frac"  dense rounds drop edges by the peer's class above this empty/full fraction
@@ -278,7 +281,9 @@ int gossip_philox_device(gossip_engine_t* eng, const uint32_t* ctr4, const uint3
  * 1 = the separate stats kernel (direct path only; fused in the binned path),
  * 2 = ANTIENTROPY sparse rounds' kernels (their stats pass counts under 1; dense rounds under 0),
  * 3 = dense rounds of a binned engine: emit + transpose + serve + apply of each round,
- * 4 = sparse (frontier) rounds of a binned engine: summary + scan + commit of each round. */
+ * 4 = sparse (frontier) rounds of a binned engine: summary + scan + commit of each round,
+ * 5 = placement trial rounds of a binned engine's record slab (param place_tries; before its
+ *     first round). */
 int gossip_kernel_time(const gossip_engine_t* eng, uint32_t which, double* total_ms, uint64_t* launches);
 int gossip_reset_timing(gossip_engine_t* eng);
 /* G > 1 rounds driven by the library (gossip_step / gossip_group_step): per class of round,
