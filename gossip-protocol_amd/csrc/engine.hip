@@ -164,6 +164,7 @@ struct gossip_engine {
   // and the fastest is kept (param place_tries; 1: the first allocation)
   uint32_t place_tries = 8;
   bool placed = false;
+  bool ae_placed = false;  // one-engine ANTIENTROPY: rows and records placed (ae_place)
   // frontier (sparse-round) path, on top of the binned one
   bool frontier = false;
   FrontierBufs fb{};
@@ -466,8 +467,6 @@ AeArgs make_ae_args(gossip_engine* e) {
   return a;
 }
 
-// Binned engines: make partial_d hold the exact totals of S (and the bitmaps
-// exact) when an untracked write (plain inject) left them stale.
 // A binned engine's record slab carved at `slab`, for a trial round (no bitmaps written).
 BinBufs trial_bufs(const gossip_engine* e, void* slab) {
   BinBufs b{};
@@ -556,6 +555,8 @@ int place_bins(gossip_engine* e) {
   return rc;
 }
 
+// Binned engines: make partial_d hold the exact totals of S (and the bitmaps
+// exact) when an untracked write (plain inject) left them stale.
 int prepare_planned(gossip_engine* e) {
   if (int rc = place_bins(e)) return rc;
   if (!e->frontier || e->fr_valid) return GOSSIP_OK;
@@ -857,9 +858,92 @@ bool ae_plan_sparse(const gossip_engine* e) {
   return pred <= 0.7 * (double)e->ae_cap;  // the largest segment, not the mean, must fit
 }
 
+// One-engine ANTIENTROPY, before its first dense round: the same placement choice as place_bins
+// for the rows (V, Vn) and the records (brec), which the dense apply gathers from.  Each candidate
+// gets a copy of the rows; its trial is a dense round of the current state into its own Vn with
+// scratch totals (the real round rewrites everything the trial wrote).
+int ae_place(gossip_engine* e) {
+  e->ae_placed = true;
+  const size_t vb = (size_t)e->N * e->R * 4;
+  if (e->place_tries <= 1 || !(e->ae_dbin && e->ae_dbin_on) || vb < (512ull << 20)) return GOSSIP_OK;
+  const size_t pl = part_len(e), rb = (size_t)e->ae_bg.nreg * ((size_t)e->k << e->ae_bg.rs) * 4;
+  uint64_t* part = nullptr;
+  HIP_OK(e, hipMalloc((void**)&part, (pl + 8) * 8));
+  struct Cand {
+    uint32_t *V, *Vn, *brec;
+  };
+  std::vector<Cand> cand{{e->V, e->Vn, e->ae_brec}};
+  std::vector<float> tms;
+  hipEvent_t ev[2];
+  HIP_OK(e, hipEventCreate(&ev[0]));
+  HIP_OK(e, hipEventCreate(&ev[1]));
+  int rc = GOSSIP_OK;
+  for (uint32_t i = 0; i < e->place_tries && rc == GOSSIP_OK; ++i) {
+    if (i > 0) {
+      Cand c{nullptr, nullptr, nullptr};
+      if (hipMalloc((void**)&c.V, vb) != hipSuccess || hipMalloc((void**)&c.Vn, vb) != hipSuccess ||
+          hipMalloc((void**)&c.brec, rb) != hipSuccess) {
+        (void)hipGetLastError();  // no room for another trial: keep the best so far
+        if (c.V) (void)hipFree(c.V);
+        if (c.Vn) (void)hipFree(c.Vn);
+        break;
+      }
+      cand.push_back(c);
+      if (hipMemcpyAsync(c.V, e->V, vb, hipMemcpyDeviceToDevice, e->stream) != hipSuccess) rc = GOSSIP_EHIP;
+    }
+    AeArgs d = make_ae_args(e);
+    d.V = cand.back().V;
+    d.Vn = cand.back().Vn;
+    d.brec = cand.back().brec;
+    d.partial = part;
+    d.aux = part + pl;
+    d.zero = part;
+    d.nzero = (uint32_t)(pl + 2);
+    d.btl = e->ae_dg.tl;
+    d.bnt = e->ae_dg.nt;
+    d.boff = e->ae_dboff;
+    d.dcap = e->ae_dcap;
+    float ms = 0.f;
+    for (int r = 0; r < 2 && rc == GOSSIP_OK; ++r) {
+      if (r == 1 && hipEventRecord(ev[0], e->stream) != hipSuccess) rc = GOSSIP_EHIP;
+      if (rc == GOSSIP_OK && launch_ae_dense_binned(d, e->stream) != hipSuccess) rc = GOSSIP_EHIP;
+    }
+    if (rc == GOSSIP_OK && (hipEventRecord(ev[1], e->stream) != hipSuccess ||
+                            hipEventSynchronize(ev[1]) != hipSuccess ||
+                            hipEventElapsedTime(&ms, ev[0], ev[1]) != hipSuccess))
+      rc = GOSSIP_EHIP;
+#ifdef GOSSIP_EXP_PLACE_LOG
+    std::fprintf(stderr, "ae_place: candidate %u trial %.1f us\n", i, ms * 1e3);
+#endif
+    tms.push_back(ms);
+    e->time_ms[5] += 2.0 * ms;
+    e->launches[5] += 2;
+  }
+  (void)hipEventDestroy(ev[0]);
+  (void)hipEventDestroy(ev[1]);
+  (void)hipFree(part);
+  size_t best = 0;
+  for (size_t i = 1; i < tms.size(); ++i)
+    if (tms[i] < tms[best]) best = i;
+  if (rc != GOSSIP_OK) best = 0;
+  HIP_OK(e, hipStreamSynchronize(e->stream));
+  for (size_t i = 0; i < cand.size(); ++i) {
+    if (i == best) continue;
+    (void)hipFree(cand[i].V);
+    (void)hipFree(cand[i].Vn);
+    (void)hipFree(cand[i].brec);
+  }
+  e->V = cand[best].V;  // (a candidate's V holds a copy of the rows)
+  e->Vn = cand[best].Vn;
+  e->ae_brec = cand[best].brec;
+  if (rc != GOSSIP_OK) return e->fail(rc, "ANTIENTROPY placement trial failed");
+  return GOSSIP_OK;
+}
+
 int ae_round(gossip_engine* e) {
   int rc;
   bool sparse = ae_plan_sparse(e);
+  if (!sparse && !e->ae_placed && (rc = ae_place(e))) return rc;
   e->ae_dense_next = false;
   e->ae_sparse_last = false;
   // partial and the aux words after it start at zero: cleared by the binned emit's block 0 (the
