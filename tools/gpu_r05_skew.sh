@@ -1,5 +1,6 @@
 #!/bin/bash
-# Skew between the record slab's arrays (experiment builds exp/libsk*.so), each process with the
+# Skew between the record slab's arrays (experiment builds exp/libsk*.so of a GOSSIP_EXP_SKEW macro in
+# bin_carve, removed after this A/B: no skew helped), each process with the
 # placement calibration on: dense round at 2^27 (tools/place_probe4.py), 3 processes per variant.
 set -u
 O=gpurun_out/${1:-r05_skew}
