@@ -165,6 +165,7 @@ struct gossip_engine {
   uint32_t place_tries = 8;
   bool placed = false;
   bool ae_placed = false;  // one-engine ANTIENTROPY: rows and records placed (ae_place)
+  bool sb_placed = false;  // sharded: the state all-gather rounds' slab placed (place_sb)
   // frontier (sparse-round) path, on top of the binned one
   bool frontier = false;
   FrontierBufs fb{};
@@ -467,52 +468,33 @@ AeArgs make_ae_args(gossip_engine* e) {
   return a;
 }
 
-// A binned engine's record slab carved at `slab`, for a trial round (no bitmaps written).
-BinBufs trial_bufs(const gossip_engine* e, void* slab) {
-  BinBufs b{};
-  bin_carve(e->bg, slab, &b);
-  b.nzb = b.fullb = nullptr;
-  if (!e->bb.dyn) b.dyn = nullptr;
-  return b;
-}
-
-// Device time (ms) of one dense round over the slab at `slab`, on a zero state (the unused second
-// image: binned rounds run in place on S) with scratch totals; the average of two after a warm-up.
-int place_trial(gossip_engine* e, void* slab, uint64_t* part, float* ms) {
-  const BinBufs b = trial_bufs(e, slab);
-  if (b.dyn) HIP_OK(e, hipMemsetAsync(b.dyn, 0, 17 * 4, e->stream));
-  const RoundSync rs{nullptr, (uint32_t)part_len(e), 0u};
+// Device time (ms) per launch of `run` on the engine's stream: the average of two after a warm-up.
+template <class Run>
+int timed_trial(gossip_engine* e, Run run, float* ms) {
   hipEvent_t ev[2];
   HIP_OK(e, hipEventCreate(&ev[0]));
   HIP_OK(e, hipEventCreate(&ev[1]));
-  int rc = GOSSIP_OK;
-  for (int i = 0; i < 3 && rc == GOSSIP_OK; ++i) {
-    if (i == 1 && hipEventRecord(ev[0], e->stream) != hipSuccess) rc = GOSSIP_EHIP;
-    if (rc == GOSSIP_OK && launch_binned_round(e->bg, b, e->img[1], part, e->R, 0u, e->key0, e->key1, e->mode, 0u,
-                                               Faults{}, 0u, rs, e->stream) != hipSuccess)
-      rc = GOSSIP_EHIP;
+  bool ok = true;
+  for (int i = 0; i < 3 && ok; ++i) {
+    if (i == 1) ok = hipEventRecord(ev[0], e->stream) == hipSuccess;
+    if (ok) ok = run() == hipSuccess;
   }
-  if (rc == GOSSIP_OK && (hipEventRecord(ev[1], e->stream) != hipSuccess ||
-                          hipEventSynchronize(ev[1]) != hipSuccess || hipEventElapsedTime(ms, ev[0], ev[1]) != hipSuccess))
-    rc = GOSSIP_EHIP;
+  ok = ok && hipEventRecord(ev[1], e->stream) == hipSuccess && hipEventSynchronize(ev[1]) == hipSuccess &&
+       hipEventElapsedTime(ms, ev[0], ev[1]) == hipSuccess;
   *ms *= 0.5f;
   (void)hipEventDestroy(ev[0]);
   (void)hipEventDestroy(ev[1]);
-  if (rc != GOSSIP_OK) return e->fail(rc, "placement trial round failed");
-  return GOSSIP_OK;
+  return ok ? GOSSIP_OK : e->fail(GOSSIP_EHIP, "placement trial round failed");
 }
 
-// Before the first round of a binned engine with a slab of 512 MiB or more: time a trial round on
-// up to place_tries allocations of the record slab (the ones tried are held while the next is
-// made, so each is a fresh placement) and keep the fastest.  Timer 5: the trial rounds.
-int place_bins(gossip_engine* e) {
-  if (e->placed) return GOSSIP_OK;
-  e->placed = true;
-  const size_t bytes = bin_bytes(e->bg);
-  if (!e->binned || e->place_tries <= 1 || bytes < (512ull << 20) || !e->img[1]) return GOSSIP_OK;
-  uint64_t* part = nullptr;
-  HIP_OK(e, hipMalloc((void**)&part, (part_len(e) + 8) * 8));
-  std::vector<void*> cand{e->bin_mem};
+// Placement of a slab: `trial(slab, &ms)` times a round over the slab at `slab`;
+// up to place_tries fresh allocations of `bytes` are tried (each held while the next is made, so
+// each is a fresh placement) and the fastest is kept in *mem (the others are freed).  Timer 5 gets
+// the trial rounds.  Returns whether *mem moved.
+template <class Trial>
+int place_slab(gossip_engine* e, void** mem, size_t bytes, Trial trial, bool* moved, const char* what) {
+  *moved = false;
+  std::vector<void*> cand{*mem};
   std::vector<float> tms;
   int rc = GOSSIP_OK;
   for (uint32_t i = 0; i < e->place_tries && rc == GOSSIP_OK; ++i) {
@@ -525,23 +507,51 @@ int place_bins(gossip_engine* e) {
       cand.push_back(p);
     }
     float ms = 0.f;
-    rc = place_trial(e, cand.back(), part, &ms);
+    rc = trial(cand.back(), &ms);
 #ifdef GOSSIP_EXP_PLACE_LOG
-    std::fprintf(stderr, "place_bins: candidate %u slab %p trial %.1f us\n", i, cand.back(), ms * 1e3);
+    std::fprintf(stderr, "%s: candidate %u slab %p trial %.1f us\n", what, i, cand.back(), ms * 1e3);
 #endif
+    (void)what;
     tms.push_back(ms);
     e->time_ms[5] += 3.0 * ms;
     e->launches[5] += 3;
   }
-  (void)hipFree(part);
   size_t best = 0;
   for (size_t i = 1; i < tms.size(); ++i)
     if (tms[i] < tms[best]) best = i;
+  if (rc != GOSSIP_OK) best = 0;
   for (size_t i = 0; i < cand.size(); ++i)
     if (i != best) (void)hipFree(cand[i]);
-  if (rc != GOSSIP_OK) best = 0;
-  if (cand[best] != e->bin_mem) {
-    e->bin_mem = cand[best];
+  *moved = cand[best] != *mem;
+  *mem = cand[best];
+  return rc;
+}
+
+// Before the first round of a binned engine with a record slab of 512 MiB or more: its placement
+// (place_slab), each trial a dense round on a zero state (the second image, unused by the in-place
+// binned rounds) with scratch totals and no bitmaps.
+int place_bins(gossip_engine* e) {
+  if (e->placed) return GOSSIP_OK;
+  e->placed = true;
+  const size_t bytes = bin_bytes(e->bg);
+  if (!e->binned || e->place_tries <= 1 || bytes < (512ull << 20) || !e->img[1]) return GOSSIP_OK;
+  uint64_t* part = nullptr;
+  HIP_OK(e, hipMalloc((void**)&part, (part_len(e) + 8) * 8));
+  const RoundSync rs{nullptr, (uint32_t)part_len(e), 0u};
+  bool moved = false;
+  const int rc = place_slab(e, &e->bin_mem, bytes, [&](void* slab, float* ms) {
+    BinBufs b{};
+    bin_carve(e->bg, slab, &b);
+    b.nzb = b.fullb = nullptr;
+    if (!e->bb.dyn) b.dyn = nullptr;
+    if (b.dyn) HIP_OK(e, hipMemsetAsync(b.dyn, 0, 17 * 4, e->stream));
+    return timed_trial(e, [&] {
+      return launch_binned_round(e->bg, b, e->img[1], part, e->R, 0u, e->key0, e->key1, e->mode, 0u, Faults{}, 0u,
+                                 rs, e->stream);
+    }, ms);
+  }, &moved, "place_bins");
+  (void)hipFree(part);
+  if (moved) {
     BinBufs nb{};
     bin_carve(e->bg, e->bin_mem, &nb);
     nb.nzb = e->bb.nzb;
@@ -552,6 +562,38 @@ int place_bins(gossip_engine* e) {
     nb.dst2 = e->bb.dst2 ? nb.dst2 : nullptr;
     e->bb = nb;
   }
+  return rc;
+}
+
+// A sharded engine's dense-round slab (the state all-gather rounds' push and pull passes, sb_*)
+// the same way, before its first such round: each trial a round over the current image into a
+// scratch slice with scratch totals and no bitmaps (image read only).
+int place_sb(gossip_engine* e) {
+  if (e->sb_placed) return GOSSIP_OK;
+  e->sb_placed = true;
+  const size_t bytes = sb_bytes(e->sbg);
+  if (!e->sbin || e->place_tries <= 1 || bytes < (512ull << 20)) return GOSSIP_OK;
+  uint64_t *part = nullptr, *snext = nullptr;
+  HIP_OK(e, hipMalloc((void**)&part, (part_len(e) + 8) * 8));
+  if (hipMalloc((void**)&snext, std::max<uint64_t>(e->nown, 1) * 8) != hipSuccess) {
+    (void)hipFree(part);
+    return e->fail(GOSSIP_ENOMEM, "placement scratch allocation failed");
+  }
+  bool moved = false;
+  const uint64_t* image = current_image(e);
+  const int rc = place_slab(e, &e->sb_mem, bytes, [&](void* slab, float* ms) {
+    SbBufs b{};
+    sb_carve(e->sbg, slab, &b);
+    return timed_trial(e, [&] {
+      if (hipError_t x = hipMemsetAsync(part, 0, part_len(e) * 8, e->stream)) return x;
+      return launch_sb_round(e->sbg, b, image, snext, part, e->R, e->t, e->key0, e->key1, e->mode, Faults{}, 0u,
+                             nullptr, nullptr, e->stream);
+    }, ms);
+  }, &moved, "place_sb");
+  (void)hipStreamSynchronize(e->stream);
+  (void)hipFree(part);
+  (void)hipFree(snext);
+  if (moved) sb_carve(e->sbg, e->sb_mem, &e->sbb);
   return rc;
 }
 
@@ -1159,6 +1201,7 @@ int compute_round(gossip_engine* e, const uint64_t* gathered) {
       return rc;
     return timer_end(e, 0);  // stats are fused into the round kernels
   } else if (e->sbin) {  // sharded dense round: binned pipeline over the gathered image
+    if ((rc = place_sb(e))) return rc;  // (a no-op once gossip_dense_prepare has placed the slab)
     if ((rc = timer_begin(e, 0))) return rc;
     if (e->sb_pre)  // the own-slice part was enqueued by gossip_dense_prepare
       HIP_OK(e, launch_sb_post(e->sbg, e->sbb, gathered, e->Snext, e->partial_d, e->R, e->t, e->key0, e->key1,
@@ -1864,6 +1907,7 @@ int gossip_dense_prepare(gossip_engine_t* e) {
   if (!e) return GOSSIP_EINVAL;
   if (!e->sbin || e->sb_pre) return GOSSIP_OK;
   if (int rc = set_dev(e)) return rc;
+  if (int rc = place_sb(e)) return rc;  // before the first pass writes into the slab
   if (e->timing) HIP_OK(e, hipEventRecord(e->ev_pre[0], e->stream));
   HIP_OK(e, launch_sb_pre(e->sbg, e->sbb, current_image(e), e->R, e->t, e->key0, e->key1, e->mode, e->fa,
                           e->stream));
