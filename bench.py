@@ -39,6 +39,7 @@ RUMORS = 64
 FANOUT = 2
 MODE = "pushpull"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+ENGINE_PARAMS = {}  # gossip_set_param knobs of every engine the bench makes (--place-tries)
 # configs[3] on the OpenMP C oracle (tests/golden/make_cfg4_golden.py): every run of that workload
 # is checked against it, at every GPU count, before and after the timed steps
 FIXTURE = os.path.join(ROOT, "tests", "golden", "cfg4_oracle.json")
@@ -161,7 +162,7 @@ def dense_only(n_nodes: int, seed: int, device: int, steps: int = 2):
     from gossip_hip import FLAG_DENSE, FLAG_TIMING, Engine
     # ahead 1: no round enqueued past convergence inside the timed region
     e = Engine(n_nodes, RUMORS, MODE, FANOUT, seed, flags=FLAG_TIMING | FLAG_DENSE, device=device,
-               params={"ahead": 1})
+               params={**ENGINE_PARAMS, "ahead": 1})
     e.reset(); e.inject_random(); e.step(64, with_infected=False)
     e.reset_timing()
     for _ in range(steps):
@@ -258,7 +259,7 @@ def secondary_run(device: int, steps: int, warmup: int) -> dict:
     """configs[2] on the same GPU (2^24 nodes: the state fits the 256 MiB Infinity Cache), same step."""
     from gossip_hip import FLAG_TIMING, Engine
     n = NODES_SECONDARY
-    e = Engine(n, RUMORS, MODE, FANOUT, SEED_SECONDARY, flags=FLAG_TIMING, device=device)
+    e = Engine(n, RUMORS, MODE, FANOUT, SEED_SECONDARY, flags=FLAG_TIMING, device=device, params=dict(ENGINE_PARAMS))
 
     def one():
         e.reset(); e.inject_random()
@@ -292,7 +293,7 @@ def antientropy_run(device: int, steps: int, warmup: int) -> dict:
     SURVEY.md §8(d)'s 4K(2 + 2k) = 256 B per node-round."""
     from gossip_hip import FLAG_TIMING, Engine, loss_threshold
     n, K, k, seed = 1 << 26, 16, 1, 0x5EED0005
-    e = Engine(n, K, "antientropy", k, seed, flags=FLAG_TIMING, device=device,
+    e = Engine(n, K, "antientropy", k, seed, flags=FLAG_TIMING, device=device, params=dict(ENGINE_PARAMS),
                churn_fail=loss_threshold(0.01), churn_recover=loss_threshold(0.1))
 
     def one():
@@ -337,6 +338,9 @@ def main():
     ap.add_argument("--no-dense-only", action="store_true", help="skip the all-dense comparison run (profiling)")
     ap.add_argument("--no-secondary", action="store_true", help="skip the configs[2] line (profiling)")
     ap.add_argument("--no-antientropy", action="store_true", help="skip the configs[4] line (profiling)")
+    ap.add_argument("--place-tries", type=int, default=0,
+                    help="engine param place_tries (0: the engine's default; 1: no placement trial rounds, "
+                         "for PMC passes that should count only the workload's rounds)")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="collectives for N > 1: nccl (= RCCL, the measured path) or gloo (a rehearsal of the "
                          "multi-rank code on a box with fewer GPUs than ranks: ranks share devices; --driver torch)")
@@ -346,6 +350,8 @@ def main():
                          "(gossip_comm_init_rank + gossip_step, DESIGN.md §5.5; not yet run on distinct GPUs, so "
                          "opt-in: a run that differs from the oracle fixture falls back to torch)")
     args = ap.parse_args()
+    if args.place_tries:
+        ENGINE_PARAMS["place_tries"] = args.place_tries
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -370,7 +376,7 @@ def main():
     else:
         seed = SEED_TOTAL if n_total >= NODES_TOTAL or world > 1 else SEED_SECONDARY
     eng = Engine(n_total, RUMORS, MODE, FANOUT, seed, flags=FLAG_TIMING, device=local,
-                 shard_rank=rank, shard_count=world)
+                 shard_rank=rank, shard_count=world, params=dict(ENGINE_PARAMS))
     driver = (args.driver or "torch") if world > 1 else "engine"
     driver_note = None
     if world > 1 and driver == "engine" and args.backend == "gloo":

@@ -27,7 +27,7 @@ python tools/rounds.py $(find $O/prof24 -name '*kernel_trace.csv' | head -1) > $
 tail -16 $O/rounds_2p24.txt
 if [ "${SKIP_PMC:-0}" != "1" ]; then
   for n in 27 24; do
-    B="python bench.py --nodes $((1 << n)) --steps 2 --warmup 1 $P"
+    B="python bench.py --nodes $((1 << n)) --steps 2 --warmup 1 --place-tries 1 $P"
     timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc$n -o fetch -- $B > $O/pmc_fetch$n.out 2>&1; ok $?
     timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/pmc$n -o write -- $B > $O/pmc_write$n.out 2>&1; ok $?
     python tools/pmc_dense.py $O/pmc$n "pushpull k=2 R=64, 2^$n nodes over 1 GPU" $O/pmc_dense_2p$n.json; ok $?
