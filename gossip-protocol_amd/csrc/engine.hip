@@ -901,9 +901,9 @@ bool ae_plan_sparse(const gossip_engine* e) {
 }
 
 // One-engine ANTIENTROPY, before its first dense round: the same placement choice as place_bins
-// for the rows (V, Vn) and the records (brec), which the dense apply gathers from.  Each candidate
-// gets a copy of the rows; its trial is a dense round of the current state into its own Vn with
-// scratch totals (the real round rewrites everything the trial wrote).
+// for the rows (V, Vn), which the dense apply gathers from, over 1.5 x place_tries candidates.
+// Each candidate gets a copy of the rows; its trial is a dense round of the current state into its
+// own Vn with scratch totals (the real round rewrites everything the trial wrote).
 int ae_place(gossip_engine* e) {
   e->ae_placed = true;
   const size_t vb = (size_t)e->N * e->R * 4;
@@ -920,18 +920,21 @@ int ae_place(gossip_engine* e) {
   HIP_OK(e, hipEventCreate(&ev[0]));
   HIP_OK(e, hipEventCreate(&ev[1]));
   int rc = GOSSIP_OK;
-  for (uint32_t i = 0; i < e->place_tries && rc == GOSSIP_OK; ++i) {
+  const uint32_t tries = e->place_tries * 3 / 2;  // a fast placement of the rows is rarer (~1 in 8)
+  for (uint32_t i = 0; i < tries && rc == GOSSIP_OK; ++i) {
     if (i > 0) {
-      Cand c{nullptr, nullptr, nullptr};
-      if (hipMalloc((void**)&c.V, vb) != hipSuccess || hipMalloc((void**)&c.Vn, vb) != hipSuccess ||
-          hipMalloc((void**)&c.brec, rb) != hipSuccess) {
+      // the rows carry the mode, the records do not (profiles/r05_pl/r05_aem/): only the rows move
+      Cand c{nullptr, nullptr, cand[0].brec};
+      if ((!c.V && hipMalloc((void**)&c.V, vb) != hipSuccess) || (!c.Vn && hipMalloc((void**)&c.Vn, vb) != hipSuccess) ||
+          (!c.brec && hipMalloc((void**)&c.brec, rb) != hipSuccess)) {
         (void)hipGetLastError();  // no room for another trial: keep the best so far
         if (c.V) (void)hipFree(c.V);
         if (c.Vn) (void)hipFree(c.Vn);
         break;
       }
       cand.push_back(c);
-      if (hipMemcpyAsync(c.V, e->V, vb, hipMemcpyDeviceToDevice, e->stream) != hipSuccess) rc = GOSSIP_EHIP;
+      if (c.V != e->V && hipMemcpyAsync(c.V, e->V, vb, hipMemcpyDeviceToDevice, e->stream) != hipSuccess)
+        rc = GOSSIP_EHIP;
     }
     AeArgs d = make_ae_args(e);
     d.V = cand.back().V;
@@ -971,9 +974,10 @@ int ae_place(gossip_engine* e) {
   HIP_OK(e, hipStreamSynchronize(e->stream));
   for (size_t i = 0; i < cand.size(); ++i) {
     if (i == best) continue;
-    (void)hipFree(cand[i].V);
-    (void)hipFree(cand[i].Vn);
-    (void)hipFree(cand[i].brec);
+    const Cand& b = cand[best];
+    if (cand[i].V != b.V) (void)hipFree(cand[i].V);
+    if (cand[i].Vn != b.Vn) (void)hipFree(cand[i].Vn);
+    if (cand[i].brec != b.brec) (void)hipFree(cand[i].brec);
   }
   e->V = cand[best].V;  // (a candidate's V holds a copy of the rows)
   e->Vn = cand[best].Vn;
