@@ -8,7 +8,7 @@ import torch
 
 import oracle_py as op
 from conftest import inject_case
-from gossip_hip import FLAG_DENSE, FLAG_DIRECT, Cluster, Engine, grid_topology
+from gossip_hip import FLAG_DENSE, FLAG_DIRECT, FLAG_TIMING, Cluster, Engine, grid_topology
 from gossip_hip.engine import GossipError
 
 pytestmark = pytest.mark.gpu
@@ -136,6 +136,22 @@ def test_cfg3_pushpull_16M_r64(path):
     assert res.converged
     inf = res.infected.astype(np.int64)
     assert (np.diff(inf, axis=0) >= 0).all() and (inf[-1] == 1 << 24).all()
+
+
+def test_placement_trials_move_time_not_bits():
+    """Before its first round a configs[2] engine times trial rounds on fresh allocations of its
+    record slab (param place_tries): 8 candidates x 3 rounds in timer 5 by default,
+    none with place_tries 1; the rounds equal the oracle's either way."""
+    cfg = (1 << 24, 64, "pushpull", 2, 0x5EED0003)
+    ro, oshard = _oracle_run(cfg, "random", 256, THREADS)
+    for params, trials in (({}, 24), ({"place_tries": 1}, 0)):
+        e = Engine(*cfg, flags=1 | FLAG_TIMING, params=params)
+        inject_case(e, "random")
+        r = e.step(256)
+        assert r.stats == ro.stats and np.array_equal(r.infected, ro.infected)
+        assert np.array_equal(e.read_shard(), oshard)
+        assert e.kernel_time(5)[1] == trials
+        e.close()
 
 
 @pytest.mark.parametrize("path", PATHS, indirect=True)

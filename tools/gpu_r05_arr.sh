@@ -1,5 +1,6 @@
 #!/bin/bash
-# Which array of the record slab carries the dense round's placement mode: experiment builds whose
+# Which array of the record slab carries the dense round's placement mode: experiment builds (a
+# GOSSIP_EXP_ARR macro in place_bins, removed after this measurement) whose
 # trial rounds take only the masked arrays from each candidate (3 dst+src, 4 prec, 8 resp,
 # 16 off+offT, 31 all), 8 candidates each, logged (tools/place_probe4.py).
 set -u
