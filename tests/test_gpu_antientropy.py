@@ -93,6 +93,31 @@ def test_antientropy_sparse_tail_1M():
     assert res.converged and res.rounds > 40
 
 
+def test_reset_zeroes_rows_lazily():
+    """gossip_reset leaves the zeroing of the rows pending until a call needs it, and
+    inject_random (which writes every row) drops it: a read after a reset sees
+    zeros, and runs after reset + inject_random, with or without a read in between, equal the
+    oracle's.  2^23 rows of K = 16 are 512 MiB, so the rows' placement trials (ae_place) run too."""
+    N, K, k, seed = 1 << 23, 16, 1, 0x5EED0005
+    kw = dict(flags=1, churn_fail=ct(0.01), churn_recover=ct(0.1))
+    e = _engine("auto", N, K, "antientropy", k, seed, **kw)
+    o = op.OracleEngine(N, K, "antientropy", k, seed, threads=THREADS, **kw)
+    for x in (e, o):
+        x.inject_random()
+    _compare(e, o, N, K, 3, (0, N - 1))
+    e.reset()
+    assert not e.read_rows().any()           # the pending zeroing ran before the read
+    for x in (e, o):
+        x.reset()
+        x.inject_random()
+    _compare(e, o, N, K, 4, (0, 5, N - 1))
+    for x in (e, o):                          # reset straight into a random write: no zeroing at all
+        x.reset()
+        x.inject_random()
+    res = _compare(e, o, N, K, 400, (1, N // 2, N - 1))
+    assert res.converged
+
+
 def test_dense_bin_params():
     """The binned dense round's knobs are validated; K > 16 engines keep the atomic passes."""
     e = Engine(4096, 16, "antientropy", 1, 0x5EED0005, flags=1, params={"ae_dense_bin": 1, "ae_dense_cap": 0})
