@@ -1667,6 +1667,12 @@ int gossip_set_param(gossip_engine_t* e, const char* name, double v) {
     e->ae_ahead = (uint32_t)v;
   } else if (n == "ordered_collectives") {
     e->ordered = v != 0;
+  } else if (n == "timing") {  // pause / resume the hipEvent timers of a GOSSIP_FLAG_TIMING engine
+    if (v != 0 && v != 1) return e->fail(GOSSIP_EINVAL, "timing must be 0 or 1");
+    if (v != 0 && !(e->cfg.flags & GOSSIP_FLAG_TIMING))
+      return e->fail(GOSSIP_ESTATE, "timing needs an engine created with GOSSIP_FLAG_TIMING");
+    if (int rc = timer_collect(e)) return rc;  // (no event of a timed round left pending)
+    e->timing = v != 0;
   } else if (n == "place_tries") {
     if (v < 1 || v > 16) return e->fail(GOSSIP_EINVAL, "place_tries must be in [1, 16]");
     e->place_tries = (uint32_t)v;

@@ -140,6 +140,8 @@ int gossip_set_stream(gossip_engine_t* eng, void* hip_stream);
  *   "mid_frac"     past 2^25 nodes sparse rounds test a peer in the L2-resident mid-level
  *                  summary once this share of peers would hit the LDS summary (default 0.5;
  *                  decided per round on the device from the exact rare count)
+ *   "timing"       0 pauses, 1 resumes the timers of an engine created with GOSSIP_FLAG_TIMING
+ *                  (their hipEvents between rounds cost a few µs each)
  *   "place_tries"  a binned engine with a record slab of 512 MiB or more times a zero-state trial
  *                  round on up to this many fresh allocations of the slab before its first round
  *                  and keeps the fastest (default 8; 1: the first allocation)
