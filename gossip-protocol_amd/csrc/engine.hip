@@ -161,8 +161,9 @@ struct gossip_engine {
   // placement of the record slab (place_bins): the dense round's time depends on where the slab
   // lands (4.98-5.48 ms at 2^27 across fresh allocations in one process, profiles/r05_pl/r05_pl4/,
   // r05_pl6/); before the first round place_tries allocations are timed on a zero-state trial round
-  // and the fastest is kept (param place_tries; 1: the first allocation)
-  uint32_t place_tries = 8;
+  // and the fastest is kept (param place_tries; 1: the first allocation; 16 vs 8 at 2^27:
+  // 5.09 / 5.10 / 5.08 against 5.21 / 5.09 / 5.09 ms, profiles/r05_pl/r05_pl9/)
+  uint32_t place_tries = 12;
   bool placed = false;
   bool ae_placed = false;  // one-engine ANTIENTROPY: rows and records placed (ae_place)
   bool sb_placed = false;  // sharded: the state all-gather rounds' slab placed (place_sb)

@@ -144,7 +144,7 @@ int gossip_set_stream(gossip_engine_t* eng, void* hip_stream);
  *                  (their hipEvents between rounds cost a few µs each)
  *   "place_tries"  a binned engine with a record slab of 512 MiB or more times a zero-state trial
  *                  round on up to this many fresh allocations of the slab before its first round
- *                  and keeps the fastest (default 8; 1: the first allocation)
+ *                  and keeps the fastest (default 12; 1: the first allocation)
  *   "scan_queue"   sparse rounds resolve the edges with a possibly rare end from a per-wave
  *                  queue, 128 at a time (default 1; 0: where they are drawn)
  *   "filter_frac"  dense rounds drop edges by the peer's class above this empty/full fraction

@@ -140,11 +140,11 @@ def test_cfg3_pushpull_16M_r64(path):
 
 def test_placement_trials_move_time_not_bits():
     """Before its first round a configs[2] engine times trial rounds on fresh allocations of its
-    record slab (param place_tries): 8 candidates x 3 rounds in timer 5 by default,
+    record slab (param place_tries): 12 candidates x 3 rounds in timer 5 by default,
     none with place_tries 1; the rounds equal the oracle's either way."""
     cfg = (1 << 24, 64, "pushpull", 2, 0x5EED0003)
     ro, oshard = _oracle_run(cfg, "random", 256, THREADS)
-    for params, trials in (({}, 24), ({"place_tries": 1}, 0)):
+    for params, trials in (({}, 36), ({"place_tries": 1}, 0)):
         e = Engine(*cfg, flags=1 | FLAG_TIMING, params=params)
         inject_case(e, "random")
         r = e.step(256)

@@ -1,4 +1,4 @@
-"""Placement calibration check: one 2^27 engine per process with param place_tries = PROBE_TRIES
+"""Placement calibration check: one 2^27 (PROBE_N) engine per process with param place_tries = PROBE_TRIES
 (1: the first allocation of the record slab; n: the fastest of n zero-state trial rounds; unset:
 the default),
 its dense-round time on the bench workload (timer 3) and its trial rounds (timer 5).  Not product code."""
@@ -14,7 +14,8 @@ if os.environ.get("GOSSIP_LIB"):  # a library variant (tools/build_variants.sh)
     _eng.load_library(os.environ["GOSSIP_LIB"])
 
 tries = os.environ.get("PROBE_TRIES")  # unset: the engine's default
-e = Engine(1 << 27, 64, "pushpull", 2, 0x5EED0004, flags=FLAG_TIMING,
+N = int(os.environ.get("PROBE_N", 1 << 27))
+e = Engine(N, 64, "pushpull", 2, 0x5EED0004 if N == 1 << 27 else 0x5EED0003, flags=FLAG_TIMING,
            params={"place_tries": int(tries)} if tries else {})
 out = []
 trial = None
