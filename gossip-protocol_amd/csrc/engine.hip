@@ -902,7 +902,7 @@ bool ae_plan_sparse(const gossip_engine* e) {
 }
 
 // One-engine ANTIENTROPY, before its first dense round: the same placement choice as place_bins
-// for the rows (V, Vn), which the dense apply gathers from, over 1.5 x place_tries candidates.
+// for the rows (V, Vn), which the dense apply gathers from, over place_tries candidates.
 // Each candidate gets a copy of the rows; its trial is a dense round of the current state into its
 // own Vn with scratch totals (the real round rewrites everything the trial wrote).
 int ae_place(gossip_engine* e) {
@@ -921,7 +921,7 @@ int ae_place(gossip_engine* e) {
   HIP_OK(e, hipEventCreate(&ev[0]));
   HIP_OK(e, hipEventCreate(&ev[1]));
   int rc = GOSSIP_OK;
-  const uint32_t tries = e->place_tries * 3 / 2;  // a fast placement of the rows is rarer (~1 in 8)
+  const uint32_t tries = e->place_tries;  // 12 by default: a fast placement of the rows is ~1 in 8
   for (uint32_t i = 0; i < tries && rc == GOSSIP_OK; ++i) {
     if (i > 0) {
       // the rows carry the mode, the records do not (profiles/r05_pl/r05_aem/): only the rows move
