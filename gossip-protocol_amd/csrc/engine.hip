@@ -678,6 +678,8 @@ struct ShardCosts {
   double sparse, dense;
   bool dense_xd, dense_cc;
 };
+uint32_t dense_filter(const gossip_engine* e, const Est& x, double frac);
+
 ShardCosts shard_round_costs(const gossip_engine* e, const Est& x) {
   // (Nl, not the own count: every rank must reach the same plan, also with ragged shards)
   const double N = (double)e->N, G = (double)e->G, Nl = (double)e->Nl, k = (double)e->k;
@@ -690,7 +692,15 @@ ShardCosts shard_round_costs(const gossip_engine* e, const Est& x) {
   const double mixed = std::max(0.0, x.nz - x.full);
   c.dense_cc = !c.dense_xd && e->cc_frac > 0 && mixed / N <= e->cc_frac;
   if (c.dense_xd) {
-    c.dense = 6.7e-8 * Nl + 40.0 * (G - 1.0) / G * Nl / bw;
+    // items per own sender edge that survive the class filter (gossip_xd_classes, dense_filter of
+    // these totals): a pull-only edge (empty sender) into an empty peer and a push-only one (full
+    // sender) into a full peer are never sent.  Device time fitted on the G = 8 probe (unfiltered
+    // 1.15 ms, filtered at 34 % kept 0.93 ms per 2^24-node rank, profiles/r05_probes/); round 4's
+    // model priced every round unfiltered and planned the two filtered rounds sparse (1.6-1.7 ms)
+    const uint32_t filt = e->k <= 8 ? dense_filter(e, x, e->xd_filter_frac) : 0u;
+    const double ef = 1.0 - x.nz / N, ff = x.full / N, mf = std::max(0.0, 1.0 - ef - ff);
+    const double kept = mf + ef * ((filt & 1u) ? 1.0 - ef : 1.0) + ff * ((filt & 2u) ? 1.0 - ff : 1.0);
+    c.dense = Nl * (4.85e-8 + 2.0e-8 * kept) + 40.0 * (G - 1.0) / G * Nl * kept / bw;
   } else {
     const double slice = c.dense_cc ? 20.0 / 64.0 * Nl + 8.0 * mixed / G : 8.0 * Nl;
     c.dense = 7.3e-9 * N + 4.7e-8 * Nl + slice * (G - 1.0) / bw;

@@ -894,8 +894,17 @@ int oracle_sharded_plan(oracle_sim_t* s, const uint64_t* total, int32_t* kind) {
     const double mixed_n = nz - full_n > 0.0 ? nz - full_n : 0.0;
     const int dense_cc = !dense_xd && s->cc_frac > 0 && mixed_n / N <= s->cc_frac;
     double c_dense;
-    if (dense_xd) {
-      c_dense = 6.7e-8 * Nl + 40.0 * (G - 1.0) / G * Nl / bw;
+    if (dense_xd) { /* the items that survive the class filter (the engine's dense_filter below) */
+      unsigned filt = 0;
+      if (s->k <= 8) {
+        const double empty = 1.0 - nz / N, full = full_n / N;
+        const int can_pull = s->mode != GOSSIP_MODE_PUSH, can_push = s->mode != GOSSIP_MODE_PULL;
+        filt = (can_pull && empty > s->xd_filter_frac ? 1u : 0u) | (can_push && full > s->xd_filter_frac ? 2u : 0u);
+      }
+      const double ef = 1.0 - nz / N, ff = full_n / N;
+      const double mf = 1.0 - ef - ff > 0.0 ? 1.0 - ef - ff : 0.0;
+      const double kept = mf + ef * ((filt & 1u) ? 1.0 - ef : 1.0) + ff * ((filt & 2u) ? 1.0 - ff : 1.0);
+      c_dense = Nl * (4.85e-8 + 2.0e-8 * kept) + 40.0 * (G - 1.0) / G * Nl * kept / bw;
     } else {
       const double slice = dense_cc ? 20.0 / 64.0 * Nl + 8.0 * mixed_n / G : 8.0 * Nl;
       c_dense = 7.3e-9 * N + 4.7e-8 * Nl + slice * (G - 1.0) / bw;
