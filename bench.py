@@ -440,6 +440,7 @@ def main():
                     sys.exit(3)
                 driver = "torch"
                 use_torch_driver()
+    placement = eng.kernel_time(5)  # the record slab's placement trial rounds, in warm-up
     eng.reset_timing()
     if world > 1 and driver == "torch":
         trace = []
@@ -467,6 +468,9 @@ def main():
     workload = workload_name(args.nodes_per_gpu if per_gpu else n_total, world, per_gpu)
     if world == 1:
         rl = single_gpu_roofline(eng, n_total, workload)
+        rl["placement_trials"] = {"rounds": placement[1], "ms": placement[0],
+                                  "note": "dense trial rounds on fresh allocations of the record slab before the "
+                                          "first round (param place_tries), in the warm-up: not in the timed steps"}
     else:
         rl = sharded_roofline(eng, driver, trace, bpn * nown, world, args.backend)
     eng.close()
