@@ -216,7 +216,19 @@ def single_gpu_roofline(eng, nodes: int, workload: str) -> dict:
     return rl
 
 
-def sharded_roofline(eng, driver: str, trace, alg_round: int, world: int, backend: str) -> dict:
+def plan_model(eng, steps: int) -> dict:
+    """N > 1: the planner's own price of the timed steps (gossip_plan_model) beside
+    the measured line: its plan (one letter per round), the modelled per-rank wall per step (device
+    time from the rates measured on one GPU + link bytes over link_gbps per xGMI link) and its link
+    part.  A real N-GPU line then shows at once whether the link rate the model assumes holds."""
+    ms, link, n, plan = eng.plan_model()
+    return {"plan": plan, "model_wall_ms": ms / max(steps, 1), "model_link_ms": link / max(steps, 1),
+            "model_device_ms": (ms - link) / max(steps, 1), "rounds_modelled": int(n // max(steps, 1)),
+            "link_gbps": ENGINE_PARAMS.get("link_gbps", 76.0),
+            "what": "per step and rank: S sparse, X exchange, C class-coded, D state all-gather dense rounds"}
+
+
+def sharded_roofline(eng, driver: str, trace, alg_round: int, world: int, backend: str, steps: int = 1) -> dict:
     """N > 1: the dense round's fraction of the HBM roofline on WHOLE-round time per rank (plan,
     collectives over the links, kernels, host reads), from hipEvents around each round of the
     timed steps on the stream the collectives are ordered on (torch driver: torch.cuda.Event
@@ -248,6 +260,7 @@ def sharded_roofline(eng, driver: str, trace, alg_round: int, world: int, backen
             "link_bytes_per_sparse_round": sparse_link / max(sparse_n, 1),
             "device_only": {"avg_round_us": dev_s * 1e6, "rounds": int(dev_n), "frac": dev_achieved / HBM_PEAK_GBS,
                             "what": "engine timer 0: the hot kernels' device time per round, collectives excluded"},
+            "plan_model": plan_model(eng, steps),
             "kernel": ("sharded dense rounds, each timed whole per rank: plan, collectives (state all-gather, "
                        "class-coded all-gather or exchange all-to-alls), kernels and host reads, from hipEvents on "
                        "the stream the collectives are ordered on; alg bytes = 64 B x own nodes"
@@ -472,7 +485,7 @@ def main():
                                   "note": "dense trial rounds on fresh allocations of the record slab before the "
                                           "first round (param place_tries), in the warm-up: not in the timed steps"}
     else:
-        rl = sharded_roofline(eng, driver, trace, bpn * nown, world, args.backend)
+        rl = sharded_roofline(eng, driver, trace, bpn * nown, world, args.backend, args.steps)
     eng.close()
 
     if rank == 0:

@@ -85,8 +85,17 @@ __global__ __launch_bounds__(kAeBlock) void ae_init_kernel(uint32_t* V, uint64_t
   __syncthreads();
   const uint32_t c4 = (K + 3) / 4;
   uint32_t mx[4] = {0, 0, 0, 0}, q0 = ~0u;
+  // a thread's running maxima belong to its quad q0: flushed whenever the quad changes (the grid
+  // stride is not always a multiple of c4, e.g. K = 9..12 past ~5.6M nodes)
+  auto flush = [&]() {
+    for (uint32_t r = 0; r < 4 && 4 * q0 + r < K; ++r)
+      if (mx[r]) atomicMax(&m[4 * q0 + r], mx[r]);
+#pragma unroll
+    for (uint32_t r = 0; r < 4; ++r) mx[r] = 0;
+  };
   for (uint64_t i = (uint64_t)blockIdx.x * kAeBlock + threadIdx.x; i < N * c4; i += (uint64_t)gridDim.x * kAeBlock) {
     const uint32_t n = (uint32_t)(i / c4), q = (uint32_t)(i % c4);
+    if (q != q0 && q0 != ~0u) flush();
     q0 = q;
     const u32x4 x = philox4x32_10(u32x4{n, q, 3u, 0u}, k0, k1);
     const uint32_t v[4] = {x.x & 0xFFFFu, x.y & 0xFFFFu, x.z & 0xFFFFu, x.w & 0xFFFFu};
@@ -98,9 +107,7 @@ __global__ __launch_bounds__(kAeBlock) void ae_init_kernel(uint32_t* V, uint64_t
 #pragma unroll
     for (uint32_t r = 0; r < 4; ++r) mx[r] = max(mx[r], v[r]);
   }
-  if (q0 != ~0u)
-    for (uint32_t r = 0; r < 4 && 4 * q0 + r < K; ++r)
-      if (mx[r]) atomicMax(&m[4 * q0 + r], mx[r]);
+  if (q0 != ~0u) flush();
   __syncthreads();
   if (threadIdx.x < K && m[threadIdx.x]) atomicMax(&target[threadIdx.x], m[threadIdx.x]);
 }
@@ -1274,7 +1281,7 @@ hipError_t launch_ae_init(uint32_t* V, uint32_t* target, uint64_t N, uint32_t K,
                           hipStream_t st) {
   hipError_t e = hipMemsetAsync(target, 0, K * 4, st);
   if (e != hipSuccess) return e;
-  // (the grid stride must be a multiple of (K + 3) / 4: kAeBlock is)
+  // (the kernel flushes a thread's maxima whenever its quad changes: any grid stride is exact)
   ae_init_kernel<<<ae_grid(N * ((K + 3) / 4), kAeBlock, 65536), kAeBlock, 0, st>>>(V, N, K, k0, k1, target);
   return hipGetLastError();
 }

@@ -29,6 +29,18 @@
 #include "multi.h"
 #include "philox.h"
 
+// 1: one-shard dense rounds past 2^26 nodes bin 32768-sender regions (binned.hip
+// bin_emit_huge_kernel); 0 (default): 16384 — an A/B build knob (tools/build_variants.sh):
+// the huge emit re-reads each record's sender value from S at random, DESIGN.md §3.7
+#ifndef GOSSIP_HUGE_REGIONS
+#define GOSSIP_HUGE_REGIONS 0
+#endif
+// 1 (default): the one-GPU planner may run a sparse-class round as a dense round whose emit drops
+// the pull-only edges into empty mid-level-summary groups (summ_dense); 0: never (A/B build knob)
+#ifndef GOSSIP_SUMM_DENSE
+#define GOSSIP_SUMM_DENSE 0
+#endif
+
 using namespace gossip;
 
 namespace {
@@ -228,6 +240,9 @@ struct gossip_engine {
   // gossip_set_param "link_gbps": sharded random-mode rounds pick sparse / dense by a per-rank
   // cost model with a link term (shard_round_costs); 0 = the fixed sparse_frac thresholds
   double link_gbps = 76.0;
+  std::string model_plan;                // gossip_plan_model: this run's plan kinds, one letter per round
+  double model_ms = 0, model_link_ms = 0;  // the modelled per-rank ms of the planned rounds since reset_timing
+  uint64_t model_rounds = 0;
   double plan_cost[2] = {};  // the last plan's modelled sparse / dense ms (tools/shard_probe.py)  // gossip_set_param "cc_frac": at most this global fraction of mixed nodes
   uint64_t* cc_bits = nullptr;  // [G][cc_slot_words] every shard's bitmaps + prefix (all-gather in place)
   uint64_t* cc_vals = nullptr;  // [G][stride] the shards' mixed words
@@ -560,7 +575,6 @@ int place_bins(gossip_engine* e) {
     HIP_OK(e, hipMemset(nb.dyn, 0, 17 * 4));
     e->bb_dyn = nb.dyn;
     if (!e->bb.dyn) nb.dyn = nullptr;
-    nb.dst2 = e->bb.dst2 ? nb.dst2 : nullptr;
     e->bb = nb;
   }
   return rc;
@@ -675,7 +689,8 @@ double sparse_frac_of(const gossip_engine* e) {
 // (class-coded: its bitmaps + prefixes, 20 B per 64 nodes, + 8 B per mixed node); exchange =
 // 40 (G - 1) / G B per own node (12-B items out, 8-B replies back, k = 2).
 struct ShardCosts {
-  double sparse, dense;
+  double sparse, dense;            // modelled ms per rank: device + link
+  double sparse_link, dense_link;  // their link parts
   bool dense_xd, dense_cc;
 };
 uint32_t dense_filter(const gossip_engine* e, const Est& x, double frac);
@@ -686,8 +701,8 @@ ShardCosts shard_round_costs(const gossip_engine* e, const Est& x) {
   const double rare = std::min(x.nz, N - x.full), rare_own = rare / G;
   const double bw = e->link_gbps * 1e6 * std::min(G - 1.0, 7.0);  // bytes per ms
   ShardCosts c{};
-  c.sparse = Nl * (2.3e-9 + 7.0e-8 * (1.0 - std::exp(-rare / N / 0.05))) +
-             (16.0 * rare_own * (G - 1.0) + 16.0 * k * rare_own * (G - 1.0) / G) / bw;
+  c.sparse_link = (16.0 * rare_own * (G - 1.0) + 16.0 * k * rare_own * (G - 1.0) / G) / bw;
+  c.sparse = Nl * (2.3e-9 + 7.0e-8 * (1.0 - std::exp(-rare / N / 0.05))) + c.sparse_link;
   c.dense_xd = e->xd && e->xd_shards && e->G >= e->xd_shards;
   const double mixed = std::max(0.0, x.nz - x.full);
   c.dense_cc = !c.dense_xd && e->cc_frac > 0 && mixed / N <= e->cc_frac;
@@ -700,10 +715,12 @@ ShardCosts shard_round_costs(const gossip_engine* e, const Est& x) {
     const uint32_t filt = e->k <= 8 ? dense_filter(e, x, e->xd_filter_frac) : 0u;
     const double ef = 1.0 - x.nz / N, ff = x.full / N, mf = std::max(0.0, 1.0 - ef - ff);
     const double kept = mf + ef * ((filt & 1u) ? 1.0 - ef : 1.0) + ff * ((filt & 2u) ? 1.0 - ff : 1.0);
-    c.dense = Nl * (4.85e-8 + 2.0e-8 * kept) + 40.0 * (G - 1.0) / G * Nl * kept / bw;
+    c.dense_link = 40.0 * (G - 1.0) / G * Nl * kept / bw;
+    c.dense = Nl * (4.85e-8 + 2.0e-8 * kept) + c.dense_link;
   } else {
     const double slice = c.dense_cc ? 20.0 / 64.0 * Nl + 8.0 * mixed / G : 8.0 * Nl;
-    c.dense = 7.3e-9 * N + 4.7e-8 * Nl + slice * (G - 1.0) / bw;
+    c.dense_link = slice * (G - 1.0) / bw;
+    c.dense = 7.3e-9 * N + 4.7e-8 * Nl + c.dense_link;
   }
   return c;
 }
@@ -735,6 +752,20 @@ uint32_t dense_filter(const gossip_engine* e, const Est& x, double frac) {
 double filter_frac_of(const gossip_engine* e) {
   if (e->filter_frac_set) return e->filter_frac;
   return e->N <= (1ull << 25) ? e->filter_frac : 2.0;
+}
+
+// One shard past 2^25 nodes, empty majority: between the light sparse rounds and the dense ones,
+// a sparse round's scan probes the summaries for every edge and fetches the exact bitmap for the
+// quarter that hit (2^27 nodes, 3.7 % nonzero: 3.4 ms), while a dense round whose emit drops the
+// pull-only edges into empty 8-node groups (binned.hip peer_filter with summ2, an L2-resident
+// probe) moves ~30 % of the records.  Chosen when the nonzero share is in [kSummDenseLo, sparse
+// threshold] (profiles/r06_*); a forced path (sparse_frac set) keeps its rounds.
+constexpr double kSummDenseLo = 0.005;
+bool summ_dense(const gossip_engine* e, const Est& x, uint32_t maj) {
+  if (!GOSSIP_SUMM_DENSE || maj != 0 || !e->binned || !e->frontier || !e->fb.summ2 || e->sparse_frac_set ||
+      e->N <= (1ull << 25))
+    return false;
+  return x.nz >= kSummDenseLo * (double)e->N;
 }
 
 RoundSync ring_sync(gossip_engine* e, uint32_t slot) {
@@ -780,9 +811,16 @@ int launch_round_path(gossip_engine* e, uint32_t t, bool sparse, uint32_t maj, b
     HIP_OK(e, launch_frontier_round(fb, e->S, e->N, e->partial_d, e->R, e->k, t, e->key0, e->key1, e->mode, maj,
                                     !all_d ? kSparseFlags : (maj == 0 && e->sparse_direct ? kSparseDirect : kSparseAllD),
                                     e->fa, e->cfg.flags, rs, e->stream));
-  else
-    HIP_OK(e, launch_binned_round(e->bg, e->bb, e->S, e->partial_d, e->R, t, e->key0, e->key1, e->mode, filt,
-                                  e->fa, e->cfg.flags, rs, e->stream));
+  else {
+    BinBufs bb = e->bb;
+    if ((filt & 1u) && fb.summ2 && e->N > (1ull << 25)) {  // pull-only edges tested in the mid-level summary
+      HIP_OK(e, launch_frontier_summ2(fb, e->N, 0u, e->stream));
+      bb.summ2 = fb.summ2;
+      bb.g2log = fb.g2log;
+    }
+    HIP_OK(e, launch_binned_round(e->bg, bb, e->S, e->partial_d, e->R, t, e->key0, e->key1, e->mode, filt, e->fa,
+                                  e->cfg.flags, rs, e->stream));
+  }
   if (timed) {
     HIP_OK(e, hipEventRecord(e->evr[slot][1], e->stream));
     e->evr_round[slot] = t;
@@ -847,13 +885,16 @@ int step_planned(gossip_engine* e, uint32_t max_rounds, gossip_round_stats_t* st
       for (uint32_t i = done; i < launched; ++i) x = predict(e, x);
       uint32_t maj = 0;
       bool all_d = false;
-      const bool sparse = choose_sparse(e, x, &maj, &all_d);
+      bool sparse = choose_sparse(e, x, &maj, &all_d);
+      uint32_t filt = dense_filter(e, x, filter_frac_of(e));
+      if (sparse && summ_dense(e, x, maj)) {  // a dense round that skips the edges into empty groups
+        sparse = false;
+        filt |= 1u;
+      }
       const uint32_t slot = launched % kRing;
       const RoundSync rs = ring_sync(e, slot);
       want[slot] = rs.seq;
-      if (int rc = launch_round_path(e, t0 + launched, sparse, maj, all_d, dense_filter(e, x, filter_frac_of(e)),
-                                     rs, (int)slot))
-        return rc;
+      if (int rc = launch_round_path(e, t0 + launched, sparse, maj, all_d, filt, rs, (int)slot)) return rc;
       ++launched;
     }
     if (done == launched) break;
@@ -1209,9 +1250,14 @@ int compute_round(gossip_engine* e, const uint64_t* gathered) {
     uint32_t maj = 0;
     bool all_d = false;
     const Est x = est_of(e, tot.data());
-    const bool sparse = choose_sparse(e, x, &maj, &all_d);
+    bool sparse = choose_sparse(e, x, &maj, &all_d);
+    uint32_t filt = dense_filter(e, x, filter_frac_of(e));
+    if (sparse && summ_dense(e, x, maj)) {  // (as step_planned)
+      sparse = false;
+      filt |= 1u;
+    }
     if ((rc = timer_begin(e, 0))) return rc;
-    if ((rc = launch_round_path(e, e->t, sparse, maj, all_d, dense_filter(e, x, filter_frac_of(e)),
+    if ((rc = launch_round_path(e, e->t, sparse, maj, all_d, filt,
                                 ring_sync(e, 0), -1)))
       return rc;
     return timer_end(e, 0);  // stats are fused into the round kernels
@@ -1544,7 +1590,9 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
     // past kBigFromTiles tiles the emit regions double (longer runs per tile, binned.hip V = 4, 5):
     // per dense round 2^25 nodes 1135 -> 1094 us, 2^26 2981 -> 2582 us; 2^24 slower (521 -> 583 us:
     // its runs of 16 records gain less than the big emit costs), profiles/r04_s
-    e->bg = make_bin_geom(e->N, e->k, (e->N + kTileD - 1) / kTileD > kBigFromTiles);
+    // past kMaxTilesD tiles (2^26 nodes) with k <= 2: 32768-sender regions (binned.hip
+    // bin_emit_huge_kernel; runs of ~8 records at 2^27 instead of ~4)
+    e->bg = make_bin_geom(e->N, e->k, (e->N + kTileD - 1) / kTileD > kBigFromTiles, GOSSIP_HUGE_REGIONS != 0);
     const size_t bytes = bin_bytes(e->bg);
     if (hipMalloc(&e->bin_mem, bytes) != hipSuccess) {
       e->err = "hipMalloc of " + std::to_string(bytes) + " bytes (bins) failed";
@@ -1687,12 +1735,6 @@ int gossip_set_param(gossip_engine_t* e, const char* name, double v) {
   } else if (n == "place_tries") {
     if (v < 1 || v > 16) return e->fail(GOSSIP_EINVAL, "place_tries must be in [1, 16]");
     e->place_tries = (uint32_t)v;
-  } else if (n == "tile_queues") {
-    if (v != 0 && v != 1) return e->fail(GOSSIP_EINVAL, "tile_queues must be 0 or 1");
-    e->bb.dyn = v != 0 ? e->bb_dyn : nullptr;
-  } else if (n == "serve_lr") {
-    if (v != 0 && v != 1) return e->fail(GOSSIP_EINVAL, "serve_lr must be 0 or 1");
-    e->bg.lr = v != 0 ? 1u : 0u;
   } else if (n == "link_gbps") {
     if (v < 0) return e->fail(GOSSIP_EINVAL, "link_gbps must be >= 0 (0 = fixed sparse_frac thresholds)");
     e->link_gbps = v;
@@ -1710,15 +1752,6 @@ int gossip_set_param(gossip_engine_t* e, const char* name, double v) {
   } else if (n == "ahead") {
     if (v < 1 || v > kRing - 1) return e->fail(GOSSIP_EINVAL, "ahead must be in [1, %u]", kRing - 1);
     e->ahead = (uint32_t)v;
-  } else if (n == "serve_grid") {
-    if (v < 0 || v > 65536) return e->fail(GOSSIP_EINVAL, "serve_grid must be in [0, 65536]");
-    e->bg.serve_grid = (uint32_t)v;
-  } else if (n == "apply_grid") {
-    if (v < 0 || v > 65536) return e->fail(GOSSIP_EINVAL, "apply_grid must be in [0, 65536]");
-    e->bg.apply_grid = e->sbg.p.apply_grid = (uint32_t)v;
-  } else if (n == "push_waves") {
-    if (v < 1 || v > 15) return e->fail(GOSSIP_EINVAL, "push_waves must be in [1, 15]");
-    e->bg.push_waves = e->sbg.p.push_waves = e->sbg.q.push_waves = (uint32_t)v;
   } else if (n == "cc_frac") {
     if (v < 0 || v > 1) return e->fail(GOSSIP_EINVAL, "cc_frac must be in [0, 1] (0 = never)");
     e->cc_frac = v;
@@ -1914,6 +1947,9 @@ int gossip_exchange_buffers(gossip_engine_t* e, void** send, void** recv, uint64
   if (!e) return GOSSIP_EINVAL;
   if (e->mode == GOSSIP_MODE_FLOOD && !e->has_topo) return e->fail(GOSSIP_ESTATE, "FLOOD needs a topology");
   if (int rc = set_dev(e)) return rc;
+  // the state all-gather rounds' slab is placed before the first collective starts: trials
+  // timed while the all-gather runs would read a half-written image under link traffic
+  if (int rc = place_sb(e)) return rc;
   uint64_t *s = nullptr, *img = nullptr;
   if (int rc = prepare_send(e, &s, &img)) return rc;
   // the caller's collective runs on another stream: publish the slice first
@@ -1928,7 +1964,7 @@ int gossip_dense_prepare(gossip_engine_t* e) {
   if (!e) return GOSSIP_EINVAL;
   if (!e->sbin || e->sb_pre) return GOSSIP_OK;
   if (int rc = set_dev(e)) return rc;
-  if (int rc = place_sb(e)) return rc;  // before the first pass writes into the slab
+  if (int rc = place_sb(e)) return rc;  // (placed already by gossip_exchange_buffers / gossip_cc_send)
   if (e->timing) HIP_OK(e, hipEventRecord(e->ev_pre[0], e->stream));
   HIP_OK(e, launch_sb_pre(e->sbg, e->sbb, current_image(e), e->R, e->t, e->key0, e->key1, e->mode, e->fa,
                           e->stream));
@@ -2089,12 +2125,12 @@ int gossip_sharded_plan(gossip_engine_t* e, const uint64_t* total, int32_t* kind
   uint32_t maj = 0;
   bool all_d = false;
   e->sx_planned = choose_sparse(e, est_of(e, e->gtot.data()), &maj, &all_d);
-  if (!e->sparse_frac_set && e->link_gbps > 0) {  // the link-aware cost model decides instead
-    const ShardCosts c = shard_round_costs(e, est_of(e, e->gtot.data()));
+  // (link_gbps 0: priced at the default rate, for gossip_plan_model only)
+  const ShardCosts c = shard_round_costs(e, est_of(e, e->gtot.data()));
+  if (!e->sparse_frac_set && e->link_gbps > 0)  // the link-aware cost model decides instead
     e->sx_planned = c.sparse < c.dense;
-    e->plan_cost[0] = c.sparse;
-    e->plan_cost[1] = c.dense;
-  }
+  e->plan_cost[0] = c.sparse;
+  e->plan_cost[1] = c.dense;
   e->sx_maj = maj;
   e->sx_alld = all_d;
   {  // the mid-level summary of the global rare bitmap (choose_sparse's rule, sharded summary)
@@ -2112,6 +2148,13 @@ int gossip_sharded_plan(gossip_engine_t* e, const uint64_t* total, int32_t* kind
   const double mixed = ((double)e->gtot[4 + e->R] - (double)e->gtot[0]) / (double)e->N;
   e->cc_planned = !e->sx_planned && !e->xd_planned && e->cc_frac > 0 && mixed <= e->cc_frac;
   *kind = e->sx_planned ? 1 : e->xd_planned ? 3 : e->cc_planned ? 4 : 0;
+  // the model's price of the round as planned (gossip_plan_model): the plan of the current run
+  // (restarted at round 0) and the modelled ms since gossip_reset_timing
+  if (e->t == 0) e->model_plan.clear();
+  e->model_plan.push_back("DSAXC"[*kind]);
+  e->model_ms += e->sx_planned ? c.sparse : c.dense;
+  e->model_link_ms += e->sx_planned ? c.sparse_link : c.dense_link;
+  e->model_rounds += 1;
   return GOSSIP_OK;
 }
 
@@ -2256,6 +2299,7 @@ int cc_check(gossip_engine* e) {
 int gossip_cc_send(gossip_engine_t* e, void** bits, uint64_t* bits_bytes, void** vals, uint64_t* count) {
   if (!bits || !bits_bytes || !vals || !count) return GOSSIP_EINVAL;
   if (int rc = cc_check(e)) return rc;
+  if (int rc = place_sb(e)) return rc;  // (as in gossip_exchange_buffers: before the collectives)
   const uint64_t nwl = (e->Nl + 63) / 64, slot = cc_slot_words(e->Nl);
   if (!e->cc_bits) {
     HIP_OK(e, hipMalloc((void**)&e->cc_bits, (size_t)e->G * slot * 8));
@@ -2819,6 +2863,22 @@ int gossip_reset_timing(gossip_engine_t* e) {
   for (int c = 0; c < 3; ++c) {
     e->wall_ms[c] = 0;
     e->wall_n[c] = e->wall_link[c] = 0;
+  }
+  e->model_ms = e->model_link_ms = 0;
+  e->model_rounds = 0;
+  return GOSSIP_OK;
+}
+
+int gossip_plan_model(const gossip_engine_t* e, double* model_ms, double* link_ms, uint64_t* rounds, char* plan,
+                      uint32_t cap) {
+  if (!e || !model_ms || !link_ms || !rounds) return GOSSIP_EINVAL;
+  *model_ms = e->model_ms;
+  *link_ms = e->model_link_ms;
+  *rounds = e->model_rounds;
+  if (plan && cap) {
+    const size_t n = std::min<size_t>(e->model_plan.size(), cap - 1);
+    std::memcpy(plan, e->model_plan.data(), n);
+    plan[n] = 0;
   }
   return GOSSIP_OK;
 }

@@ -17,6 +17,8 @@ FLAG_DENSE = 1 << 3
 FLAG_SHARD_DIRECT = 1 << 4
 FLAG_AE_DIRECT_SCAN = 1 << 5
 
+ABI_VERSION = 10  # include/gossip.h GOSSIP_ABI_VERSION (v10: gossip_round_wall)
+
 STATUS = {0: "OK", -1: "EINVAL", -2: "EHIP", -3: "ENOMEM", -4: "ESTATE", -5: "ENODEV", -6: "ENOTSUP", -7: "ERCCL"}
 UNIQUE_ID_BYTES = 128
 TRANSPORT_AUTO, TRANSPORT_RCCL, TRANSPORT_COPY = 0, 1, 2
@@ -120,6 +122,7 @@ SIGNATURES = [
     ("kernel_time", C.c_int, [P, C.c_uint32, C.POINTER(C.c_double), U64P]),
     ("reset_timing", C.c_int, [P]),
     ("round_wall", C.c_int, [P, C.c_uint32, C.POINTER(C.c_double), U64P, U64P]),
+    ("plan_model", C.c_int, [P, C.POINTER(C.c_double), C.POINTER(C.c_double), U64P, C.c_char_p, C.c_uint32]),
     # multi-GPU driven by the engine
     ("comm_unique_id", C.c_int, [C.c_char_p]),
     ("comm_init_rank", C.c_int, [P, C.c_char_p]),

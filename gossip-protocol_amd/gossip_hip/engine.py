@@ -40,7 +40,18 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         if not os.path.exists(path):
             raise FileNotFoundError(f"{path} missing: build it with `make -C gossip-protocol_amd` "
                                     "(the engine has no CPU fallback)")
-        _LIB = _abi.bind(C.CDLL(path), "gossip_")
+        lib = C.CDLL(path)
+        # the version first: a library of another ABI fails here with a clear message, not on the
+        # first entry point it lacks
+        ver = getattr(lib, "gossip_abi_version", None)
+        if ver is None:
+            raise RuntimeError(f"{path} exports no gossip_abi_version: not a gossip engine library")
+        ver.restype = C.c_uint32
+        ver.argtypes = []
+        if ver() != _abi.ABI_VERSION:
+            raise RuntimeError(f"{path} has ABI v{ver()}, this binding is written for v{_abi.ABI_VERSION}: "
+                               "rebuild it with `make -C gossip-protocol_amd`")
+        _LIB = _abi.bind(lib, "gossip_")
     return _LIB
 
 
@@ -464,6 +475,14 @@ class Engine(AbiEngine):
         ms, n, lb = C.c_double(), C.c_uint64(), C.c_uint64()
         self._check(self._fn("round_wall")(self._h, C.c_uint32(cls), C.byref(ms), C.byref(n), C.byref(lb)))
         return ms.value, n.value, lb.value
+
+    def plan_model(self):
+        """The planner's model of the sharded rounds it planned (gossip_plan_model): (modelled per-rank
+        ms since reset_timing, its link part, rounds covered, the current run's plan string)."""
+        ms, link, n = C.c_double(), C.c_double(), C.c_uint64()
+        buf = C.create_string_buffer(256)
+        self._check(self._fn("plan_model")(self._h, C.byref(ms), C.byref(link), C.byref(n), buf, C.c_uint32(256)))
+        return ms.value, link.value, n.value, buf.value.decode()
 
     def philox_device(self, ctr: np.ndarray, key) -> np.ndarray:
         ctr = np.ascontiguousarray(ctr, dtype=np.uint32).reshape(-1, 4)

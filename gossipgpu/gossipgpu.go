@@ -1,5 +1,5 @@
 // Package gossipgpu binds the MI355X gossip-round engine (libgossip_hip.so, the C ABI of
-// include/gossip.h, ABI v9) for Go hosts such as 0xSherlokMo/gossip-protocol's main.go.
+// include/gossip.h, ABI v10) for Go hosts such as 0xSherlokMo/gossip-protocol's main.go.
 //
 // The reference floods each value once to its topology neighbours with blocking SyncRPCs
 // ((*NodeState).Gossip, main.go:65-89), one process per node.  Here one Engine holds every
@@ -33,6 +33,7 @@ package gossipgpu
 import "C"
 
 import (
+	"bytes"
 	"fmt"
 	"sort"
 	"strconv"
@@ -41,7 +42,7 @@ import (
 )
 
 // ABIVersion is the gossip.h version this binding is written against.
-const ABIVersion = 9
+const ABIVersion = 10
 
 // Mode is a dissemination rule (DESIGN.md §2).
 type Mode uint32
@@ -527,6 +528,20 @@ func (e *Engine) RoundWall(cls uint32) (float64, uint64, uint64, error) {
 		return 0, 0, 0, e.fail(rc)
 	}
 	return float64(ms), uint64(n), uint64(lb), nil
+}
+
+// PlanModel returns the planner's model of the sharded rounds it planned (gossip_plan_model):
+// modelled per-rank ms and their link part since ResetTiming, the rounds covered, and the current
+// run's plan string (S sparse, X exchange, C class-coded, D state all-gather).
+func (e *Engine) PlanModel() (float64, float64, uint64, string, error) {
+	var ms, link C.double
+	var n C.uint64_t
+	buf := make([]byte, 256)
+	if rc := C.gossip_plan_model(e.h, &ms, &link, &n, (*C.char)(unsafe.Pointer(&buf[0])), C.uint32_t(len(buf))); rc != 0 {
+		return 0, 0, 0, "", e.fail(rc)
+	}
+	plan := string(buf[:bytes.IndexByte(buf, 0)])
+	return float64(ms), float64(link), uint64(n), plan, nil
 }
 
 // PhiloxDevice runs Philox4x32-10 on the device for known-answer tests (ctr: 4 words per counter).

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define GOSSIP_ABI_VERSION 9u
+#define GOSSIP_ABI_VERSION 10u
 
 /* Dissemination modes. */
 enum gossip_mode {
@@ -129,60 +129,52 @@ const char* gossip_last_error(const gossip_engine_t* eng);
  * previous stream first. */
 int gossip_set_stream(gossip_engine_t* eng, void* hip_stream);
 
-/* Tuning and path-selection knobs, for tests and benchmarks (the library reads no
- * environment variables).  Every value only moves time, never a result bit:
- *   "sparse_frac"  random modes: a round runs sparse when the rare class is at most
- *                  this fraction of N (default 1/16; sharded 1/4, or 1/25 when the dense
- *                  rounds are exchange rounds; < 0 never, >= 1 always)
- *   "alld_frac"    sparse rounds commit every group's D once k x rare >= this x N (default 1/128)
- *   "sparse_direct"  such rounds with an empty majority OR the pushes into empty peers
- *                  straight into the state and recompute the totals (default 1; 0: into D)
- *   "mid_frac"     past 2^25 nodes sparse rounds test a peer in the L2-resident mid-level
- *                  summary once this share of peers would hit the LDS summary (default 0.5;
- *                  decided per round on the device from the exact rare count)
+/* Knobs (the library reads no environment variables).  Every value only moves time, never a
+ * result bit.  Unknown names return GOSSIP_EINVAL.
+ * Operational:
  *   "timing"       0 pauses, 1 resumes the timers of an engine created with GOSSIP_FLAG_TIMING
  *                  (their hipEvents between rounds cost a few µs each)
  *   "place_tries"  a binned engine with a record slab of 512 MiB or more times a zero-state trial
- *                  round on up to this many fresh allocations of the slab before its first round
- *                  and keeps the fastest (default 12; 1: the first allocation)
- *   "scan_queue"   sparse rounds resolve the edges with a possibly rare end from a per-wave
- *                  queue, 128 at a time (default 1; 0: where they are drawn)
- *   "filter_frac"  dense rounds drop edges by the peer's class above this empty/full fraction
- *                  (default 0.3 up to 2^25 nodes; past that off: the probes miss the L2)
- *   "xd_filter_frac"  exchange dense rounds likewise (default 0.6; >= 1 never)
+ *                  round on up to this many allocations of the slab before its first round and keeps
+ *                  the fastest (default 12; 1: the first allocation).  At most two slabs are held at
+ *                  once (the best so far and the candidate)
  *   "ahead"        rounds enqueued ahead of the stats read back (1..7, default 2)
- *   "apply_grid"   persistent blocks of the dense apply pass (0 = one block per tile)
- *   "serve_grid"   persistent blocks of the one-shard dense serve pass (0 = one block per tile)
- *   "push_waves"   waves of the dense apply pass walking the pushes (of 16; the rest walk the replies)
- *   "ae_sparse"    ANTIENTROPY: -1 plan sparse rounds (default), 0 never, 1 whenever valid
- *   "ae_cap"       ANTIENTROPY: edge-list capacity of sparse rounds (reallocates the list)
- *   "ae_dense_bin" ANTIENTROPY: 1 dense rounds as binned in-edge gathers (default, N <= 2^26),
- *                  0 pull pass + atomicMax push pass + stats pass
- *   "ae_dense_cap" ANTIENTROPY: in-edges per LDS pass of a binned dense round (0 = default
- *                  18432; smaller values split tiles into more passes, and a 64-node chunk
- *                  past it reruns the round with the atomicMax passes)
- *   "ae_dense_filter"  ANTIENTROPY: 1 binned dense rounds skip the exchanges that cannot move a
- *                  row once fewer than 90 % of the nodes are stale (default), 0 gather them all
- *   "xd_shards"   sharded random modes: dense rounds run as exchange rounds (kind 3) when
- *                  G >= this (default 6; 0 = never, always the state all-gather)
  *   "ae_ahead"     ANTIENTROPY, one engine: sparse rounds enqueued at once, each gated on the
  *                  device by the previous one (1..8, default 8; 1 = one round per host read)
  *   "ordered_collectives"  1: the host runs its collectives on streams ordered after the
  *                  engine's (gossip_set_stream to the collectives' launch stream), so the
  *                  per-kind calls hand out buffers without a publishing stream sync (default 0)
- *   "cc_frac"      sharded random modes: dense rounds on the state image exchange it
- *                  class-coded (kind 4) while the mixed nodes (neither empty nor full) are
- *                  at most this fraction of N (default 0.75; 0 never, 1 always)
  *   "link_gbps"    sharded random modes: a round is sparse or dense by a per-rank cost model
  *                  of device time plus link bytes over this many GB/s per xGMI link (default
- *                  76; 0 = the fixed sparse_frac thresholds)
+ *                  76; 0 = the fixed sparse_frac thresholds); gossip_plan_model reports it
  *   "rccl_dev_collectives"  1: the RCCL transport's collectives read the round's counts and
  *                  partials from engine memory (gossip_*_dev); default 0: one host read first
- *   "serve_lr"     one shard, dense rounds: 1 regroups serve's record ids into long runs
- *                  first (default 0)
- *   "tile_queues"  one shard, dense rounds: 1 = serve and apply take tiles from per-XCD
- *                  queues (default from 4096 tiles = 2^26 nodes), 0 = the static order
- * Unknown names return GOSSIP_EINVAL. */
+ * Path selection, for the parity tests' A/B paths (each forces a kernel path the planner would
+ * otherwise choose by cost; tests/test_abi.py pins this list):
+ *   "sparse_frac"  random modes: a round runs sparse when the rare class is at most this fraction
+ *                  of N (default 1/16; sharded 1/4, or 1/25 before exchange rounds; < 0 never,
+ *                  >= 1 always; overrides link_gbps)
+ *   "alld_frac"    sparse rounds commit every group's D once k x rare >= this x N (default 1/128)
+ *   "sparse_direct"  such rounds with an empty majority OR the pushes into empty peers straight
+ *                  into the state (default 1; 0: into D)
+ *   "mid_frac"     past 2^25 nodes sparse rounds test a peer in the mid-level summary once this
+ *                  share of peers would hit the LDS summary (default 0.5)
+ *   "scan_queue"   sparse rounds resolve the edges with a possibly rare end from a per-wave queue
+ *                  (default 1; 0: where they are drawn)
+ *   "filter_frac"  dense rounds drop edges by the peer's class above this empty/full fraction
+ *                  (default 0.3 up to 2^25 nodes; past that off: the probes miss the L2)
+ *   "xd_filter_frac"  exchange dense rounds likewise (default 0.6; >= 1 never)
+ *   "xd_shards"    sharded random modes: dense rounds run as exchange rounds when G >= this
+ *                  (default 6; 0 = never)
+ *   "cc_frac"      sharded random modes: dense rounds on the state image exchange it class-coded
+ *                  while the mixed nodes are at most this fraction of N (default 0.75; 0 never)
+ *   "ae_sparse"    ANTIENTROPY: -1 plan sparse rounds (default), 0 never, 1 whenever valid
+ *   "ae_cap"       ANTIENTROPY: edge-list capacity of sparse rounds (reallocates the list)
+ *   "ae_dense_bin" ANTIENTROPY: 1 dense rounds as binned in-edge gathers (default, N <= 2^26),
+ *                  0 pull pass + atomicMax push pass + stats pass
+ *   "ae_dense_cap" ANTIENTROPY: in-edges per LDS pass of a binned dense round (0 = 18432)
+ *   "ae_dense_filter"  ANTIENTROPY: 1 binned dense rounds skip the exchanges that cannot move a
+ *                  row once fewer than 90 % of the nodes are stale (default), 0 gather them all */
 int gossip_set_param(gossip_engine_t* eng, const char* name, double value);
 
 /* FLOOD peer source: directed adjacency Topology[u] = col[row_ptr[u]..row_ptr[u+1]),
@@ -297,6 +289,14 @@ int gossip_reset_timing(gossip_engine_t* eng);
  * gossip_reset_timing. */
 int gossip_round_wall(const gossip_engine_t* eng, uint32_t cls, double* total_ms, uint64_t* rounds,
                       uint64_t* link_bytes);
+/* G > 1 random modes (either driver: the library's or a host's own collectives): the planner's
+ * model of the rounds it planned (ABI v10) — the modelled per-rank ms (device time
+ * from the measured rates plus link bytes over link_gbps x min(G - 1, 7) xGMI links) and its link
+ * part, summed since gossip_reset_timing, the rounds they cover, and the current run's plan (one
+ * letter per round since round 0: S sparse, X exchange, C class-coded, D state all-gather) in
+ * plan[0 .. cap), NUL-terminated.  A measured N-GPU run can be set against it round for round. */
+int gossip_plan_model(const gossip_engine_t* eng, double* model_ms, double* link_ms, uint64_t* rounds, char* plan,
+                      uint32_t cap);
 
 #ifdef __cplusplus
 }

@@ -1,5 +1,5 @@
 /*
- * gossip_shard.h — the per-kind steps of a sharded round (libgossip_hip.so, ABI v9).
+ * gossip_shard.h — the per-kind steps of a sharded round (libgossip_hip.so, ABI v10).
  *
  * A host that drives N GPUs through gossip_step (gossip.h: the engine owns its RCCL
  * communicators) never needs this header.  It is for a host that runs the

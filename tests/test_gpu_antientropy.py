@@ -126,3 +126,16 @@ def test_dense_bin_params():
             e.set_param(name, bad)
     e.set_param("ae_dense_bin", 0)
     e.set_param("ae_dense_cap", 64)
+
+
+def test_init_target_K12_past_grid_stride():
+    """K = 12 (3 quads per row) past ~5.6M nodes: ae_init_kernel's grid stride (2^24 threads) is no
+    multiple of 3, so a thread's quad changes between iterations and its running maxima must be
+    flushed per quad.  The target and the first rounds equal the oracle's."""
+    N, K, k, seed = (1 << 23) + 77, 12, 1, 0x5EED000C
+    kw = dict(flags=1, churn_fail=ct(0.01), churn_recover=ct(0.1))
+    e = _engine("auto", N, K, "antientropy", k, seed, **kw)
+    o = op.OracleEngine(N, K, "antientropy", k, seed, threads=THREADS, **kw)
+    for x in (e, o):
+        x.inject_random()
+    _compare(e, o, N, K, 4, (0, 1, N // 3, N - 1))

@@ -3,8 +3,8 @@
 Past 2^25 nodes the occupancy bitmaps outgrow an XCD's L2, so sparse rounds test a peer in an
 L2-resident mid-level summary before its exact bitmap word (FrontierBufs::summ2,
 csrc/frontier.hip); and every heavy sparse round with an empty majority ORs the pushes into
-empty peers straight into the state (kSparseDirect).  serve's long-run ids (param serve_lr, every round
-dense) are here too.  Each path must equal the oracle bit for
+empty peers straight into the state (kSparseDirect).  Every round on the dense pipeline (big
+regions, packed pushes) is here too.  Each path must equal the oracle bit for
 bit: per-round stats, per-rumor counts and the final state.  Ragged N (not a multiple of 64 or
 of the summary groups).  Reference: (*NodeState).Gossip, main.go:65-89, as rounds.
 """
@@ -29,9 +29,8 @@ PATHS = {"auto": {}, "sparse_flags": {"sparse_frac": 1.0, "alld_frac": 1e30},
          "sparse_mid": {"sparse_frac": 1.0, "mid_frac": 0},
          # edges resolved where they are drawn (no per-wave queue; the default before round 5)
          "sparse_noq": {"sparse_frac": 1.0, "scan_queue": 0},
-         # every round dense with serve's ids regrouped into long runs (param serve_lr, opt-in: the
-         # A/B of profiles/r05_lr2/ measured it slower at 2^27, kept under test)
-         "dense_serve_lr": {"sparse_frac": -1.0, "serve_lr": 1}}
+         # every round on the dense pipeline (16384-sender regions, packed pushes)
+         "dense": {"sparse_frac": -1.0}}
 CASES = {"pushpull-k2-R64": ("pushpull", 2, 64, 0x5EED0003, 0), "push-k3-R5": ("push", 3, 5, 77, 0),
          "pull-k1-R7-loss": ("pull", 1, 7, 9, 1 << 30), "pull-k2-R3": ("pull", 2, 3, 0x51, 0)}
 

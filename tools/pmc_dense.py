@@ -14,7 +14,7 @@ import json
 import os
 import sys
 
-DENSE = ("bin_emit_kernel", "transpose_u16_kernel", "bin_serve_kernel", "bin_apply_kernel", "bin_dst_group_kernel")
+DENSE = ("bin_emit_kernel", "bin_emit_huge_kernel", "transpose_u16_kernel", "bin_serve_kernel", "bin_apply_kernel")
 
 
 def kname(s):

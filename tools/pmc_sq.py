@@ -12,7 +12,7 @@ import json
 import os
 import sys
 
-KEEP = ("bin_emit_kernel", "transpose_u16_kernel", "bin_serve_kernel", "bin_apply_kernel", "bin_dst_group_kernel",
+KEEP = ("bin_emit_kernel", "bin_emit_huge_kernel", "transpose_u16_kernel", "bin_serve_kernel", "bin_apply_kernel",
         "frontier_scan_kernel", "frontier_commit_kernel")
 
 

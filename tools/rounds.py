@@ -8,7 +8,7 @@ import csv
 import sys
 
 path = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof/run_kernel_trace.csv"
-SHORT = {"bin_count_kernel": "count", "bin_emit_kernel": "emit", "transpose_u16_kernel": "u16", "transpose_u32_kernel": "u32", "bin_serve_kernel": "serve",
+SHORT = {"bin_count_kernel": "count", "bin_emit_kernel": "emit", "bin_emit_huge_kernel": "emit", "transpose_u16_kernel": "u16", "transpose_u32_kernel": "u32", "bin_serve_kernel": "serve",
          "bin_apply_kernel": "apply", "frontier_summary_kernel": "summ", "frontier_scan_kernel": "scan", "frontier_scan_ns_kernel": "scan_ns",
          "frontier_rebuild_kernel": "rebuild", "frontier_commit_kernel": "commit", "frontier_inject_kernel": "inject", "round_snapshot_kernel": "snap",
          "bs_emit_kernel": "bs_emit", "bs_test_kernel": "bs_test"}
