@@ -60,14 +60,11 @@ struct BinGeom {
   uint32_t push_waves;   // push-pull apply: waves [0, push_waves) walk the pushes, the rest the responses
   uint32_t aos;          // push records also packed {value, id} (BinBufs::prec; one shard, big regions)
   uint32_t split;        // one shard: record ids as two u16 arrays (BinBufs::dst / src) instead of ids
-  uint32_t huge;         // one shard past kMaxTilesD tiles, k <= 2: 32768-sender regions (binned.hip
-                         // bin_emit_huge_kernel; offsets mod 2^16, exact totals in BinBufs::rtot)
 };
 
 // big: regions of up to 2 * kMaxSenders senders and 2 * kRecPerRegion records (one shard
 // past kMaxTilesD tiles: the emit's 16-bit packed tile counters, binned.hip V = 4)
-// huge: 32768-sender regions where they apply (one shard past kMaxTilesD tiles, k <= 2), else big
-BinGeom make_bin_geom(uint64_t N, uint32_t k, bool big = false, bool huge = false);
+BinGeom make_bin_geom(uint64_t N, uint32_t k, bool big = false);
 bool bin_path_ok(uint64_t N, uint32_t k, uint32_t W, uint32_t G);
 
 struct BinBufs {
@@ -84,12 +81,6 @@ struct BinBufs {
   // one shard: the persistent serve's / apply's tile queues, 8 counters each (one per XCD), zeroed
   // by the round's transpose kernel (binned.hip TileQueue); null: the static tile order
   uint32_t* dyn;
-  uint32_t* rtot;   // [nt_s] records per sender region (huge regions: off holds them mod 2^16)
-  // filt bit 0 past 2^25 nodes (big / huge emits): the peer's group bit in the mid-level summary
-  // of the nonzero nodes (FrontierBufs::summ2, 2^g2log nodes per bit) instead of its exact bit;
-  // null: the exact bitmap nzb
-  const uint32_t* summ2;
-  uint32_t g2log;
 };
 
 size_t bin_bytes(const BinGeom& g);

@@ -72,12 +72,11 @@ __device__ __forceinline__ void prec_ld(const uint32_t* p, uint32_t& a, uint32_t
   c = v.z;
 }
 
-// record id word: p_local [0,14) | n_local [14,29) | flags.  K1 rewrites every
+// record id word: p_local [0,14) | n_local [14,28) | flags.  K1 rewrites every
 // id each round, so a flag never outlives its round.
-// (n_local takes 15 bits in the huge regions' 32768-sender ids, bin_emit_huge_kernel)
-constexpr uint32_t kIdVZ = 1u << 30;  // no push on this record (sender empty, or the peer already full)
-constexpr uint32_t kIdVF = 1u << 31;  // no pull (sender full, or the peer empty)
-constexpr uint32_t kIdNMask = (1u << 15) - 1u;
+constexpr uint32_t kIdVZ = 1u << 28;  // no push on this record (sender empty, or the peer already full)
+constexpr uint32_t kIdVF = 1u << 29;  // no pull (sender full, or the peer empty)
+constexpr uint32_t kIdNMask = (1u << 14) - 1u;
 
 // Split record ids (BinGeom::split, one shard): the id word becomes two u16 arrays, so serve
 // and the push walk read 2 B (dst) instead of 4 and the reply walk 2 B (src): 12 B per node
@@ -136,19 +135,10 @@ __device__ __forceinline__ uint32_t sender_dirs(uint32_t mode, uint64_t v, uint6
   return push | (pull << 1);
 }
 
-// summ2 (one shard past 2^25 nodes: BinBufs::summ2, built for this round from the nonzero
-// bitmap): pull-only edges are dropped when the peer's whole 2^g2log-node group is empty — a
-// conservative test (an edge into an empty peer of a nonempty group stays; it moves nothing) whose
-// probes hit the 2 MiB L2-resident summary instead of the 16 MiB exact bitmap
 __device__ __forceinline__ uint32_t peer_filter(uint32_t d, uint32_t p, uint32_t filt, const uint64_t* nzb,
-                                                const uint64_t* fullb, const uint32_t* summ2 = nullptr,
-                                                uint32_t g2log = 0) {
+                                                const uint64_t* fullb) {
   // only one-way edges are probed: a two-way record stays anyway
-  if ((filt & 1u) && d == 2u) {
-    const bool nz = summ2 ? (summ2[p >> (g2log + 5)] >> ((p >> g2log) & 31u)) & 1u
-                          : (nzb[p >> 6] >> (p & 63u)) & 1ull;
-    if (!nz) d = 0u;
-  }
+  if ((filt & 1u) && d == 2u && !((nzb[p >> 6] >> (p & 63u)) & 1ull)) d = 0u;
   if ((filt & 2u) && d == 1u && ((fullb[p >> 6] >> (p & 63u)) & 1ull)) d = 0u;
   return d;
 }
@@ -425,7 +415,7 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
           const uint32_t p = peer_from_word(lane_of(x, j), nm1, n);
           uint32_t tl, pl;
           const bool in = tile_of(p, &tl, &pl);  // (one shard: always inside)
-          const uint32_t dd = in ? peer_filter(d, p, filt, b.nzb, b.fullb, b.summ2, b.g2log) : 0u;
+          const uint32_t dd = in ? peer_filter(d, p, filt, b.nzb, b.fullb) : 0u;
           if (!dd) continue;
           count_tile(tl);
           pk |= ((uint64_t)p << (27 * j)) | ((uint64_t)dd << (54 + 2 * j));
@@ -451,7 +441,7 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
         if (FAULTS && edge_lost(fa, rc, p, lane_of(lw, j & 3u))) continue;
         uint32_t tl, pl;
         if (!tile_of(p, &tl, &pl)) continue;
-        if (peer_filter(d, p, filt, b.nzb, b.fullb, b.summ2, b.g2log)) count_tile(tl);
+        if (peer_filter(d, p, filt, b.nzb, b.fullb)) count_tile(tl);
       }
     }
   }
@@ -514,7 +504,7 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
         if (FAULTS && edge_lost(fa, rc, p, lane_of(lw, j & 3u))) continue;
         uint32_t tl, pl;
         if (!tile_of(p, &tl, &pl)) continue;
-        const uint32_t d = peer_filter(d0, p, filt, b.nzb, b.fullb, b.summ2, b.g2log);
+        const uint32_t d = peer_filter(d0, p, filt, b.nzb, b.fullb);
         if (!d) continue;
         const uint32_t pos = place_tile(tl);
         st_ids[pos] = pl | (i << kTileDLog) | dir_flags(d);
@@ -590,214 +580,6 @@ __global__ __launch_bounds__(kEmitThreads) void bin_emit_kernel(BinGeom g, const
     for (uint32_t q = 0; q < kQ; ++q) v[q] = vn[q];
   }
   if (!dynq) r += gridDim.x;
-  }
-}
-
-// --- huge regions (one shard past kMaxTilesD tiles, k <= 2; BinGeom::huge) ---------------------
-// The run length of a (region, tile) pair is 2 R T / N records for R-sender regions and T-node tiles:
-// ~4 at 2^27 nodes with the 16384-sender regions of V = 4 / 5, so serve and apply walk 8-48-B pieces
-// (DESIGN.md §8.1).  Here a region is 32768 senders (65536 records at k = 2, runs of ~8): their
-// peers and edge directions stay in registers ({p0, p1, dirs} per sender, 32 senders per lane), the
-// count pass sorts the whole region's tile counts (16-bit, two per LDS word), and the records are
-// then staged and written in passes over ranges of destination tiles, each pass's records at most
-// kHugeCap (a pass that would overflow the staging room writes its records straight to their slots).
-// Offsets stay u16: a region's positions and run lengths are taken mod 2^16 (no run reaches 2^16
-// records, and every record position is below 2^16); the region's exact total goes to rtot.
-// Sender values for the packed pushes are re-read from S (the region's 256 KiB slice: L2 / MALL).
-constexpr uint32_t kHugeSenders = 32768;
-constexpr uint32_t kHugeQ = kHugeSenders / kEmitThreads;  // senders per lane
-constexpr uint32_t kHugePasses = 2;                       // tile ranges per region
-constexpr uint32_t kHugeCap = 36608;  // staged records per pass (LDS: 143 KiB + 16 KiB of counters)
-constexpr uint32_t kHugeChunk = 2;    // sender values loaded ahead, per lane
-constexpr uint32_t kHugeOut = 8;      // records per lane and step of the write-out
-static_assert(kHugeQ % kHugeChunk == 0, "huge emit: whole chunks of senders per lane");
-
-// region_offsets_packed for 65536-record regions: the 16-bit halves hold positions mod 2^16 (masked,
-// so a half never carries into its neighbour), off_row likewise; bnd[h] = the exact number of
-// records before tile h * span (h < passes), bnd[passes] = the total.
-__device__ __forceinline__ uint32_t region_offsets_huge(uint32_t* cur, uint32_t nt, uint16_t* off_row, uint32_t* wsum,
-                                                        uint32_t* wpre, uint32_t* bnd, uint32_t span) {
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t nw = (nt + 1) >> 1;
-  const uint32_t per = (nw + kEmitThreads - 1) / kEmitThreads;
-  const uint32_t lo = min(tid * per, nw), hi = min(lo + per, nw);
-  uint32_t mine = 0;
-  for (uint32_t w = lo; w < hi; ++w) mine += (cur[w] & 0xFFFFu) + (cur[w] >> 16);
-  uint32_t inc = mine;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(inc, o, 64);
-    if (lane >= (uint32_t)o) inc += y;
-  }
-  if (lane == 63) wsum[wave] = inc;
-  __syncthreads();
-  if (tid == 0) {
-    uint32_t a = 0;
-    for (int w = 0; w < kEmitThreads / 64; ++w) {
-      wpre[w] = a;
-      a += wsum[w];
-    }
-    wpre[kEmitThreads / 64] = a;
-  }
-  __syncthreads();
-  uint32_t run = wpre[wave] + inc - mine;
-  const uint32_t hspan = span >> 1;  // (span is even: a boundary tile starts a word)
-  for (uint32_t w = lo; w < hi; ++w) {
-    if (w % hspan == 0 && w / hspan < kHugePasses) bnd[w / hspan] = run;
-    const uint32_t c0 = cur[w] & 0xFFFFu, c1 = cur[w] >> 16;
-    const uint32_t r0 = run, r1 = run + c0;
-    cur[w] = (r0 & 0xFFFFu) | (r1 << 16);
-    off_row[2 * w] = (uint16_t)r0;
-    if (2 * w + 1 < nt) off_row[2 * w + 1] = (uint16_t)r1;
-    run = r1 + c1;
-  }
-  const uint32_t total = wpre[kEmitThreads / 64];
-  if (tid == 0) {
-    off_row[nt] = (uint16_t)total;
-    for (uint32_t h = 0; h <= kHugePasses; ++h)  // boundaries past the last word
-      if (h == kHugePasses || h * hspan >= nw) bnd[h] = total;
-  }
-  __syncthreads();
-  return total;
-}
-
-template <bool FAULTS>
-__global__ __launch_bounds__(kEmitThreads) void bin_emit_huge_kernel(BinGeom g, const uint64_t* __restrict__ S,
-                                                                       BinBufs b, uint32_t R, uint32_t t,
-                                                                       uint32_t key0, uint32_t key1, uint32_t mode,
-                                                                       uint32_t filt, Faults fa) {
-  __shared__ uint32_t cur[kSbMaxTiles / 2];
-  __shared__ __align__(16) uint32_t st[kHugeCap];
-  __shared__ uint32_t wsum[kEmitThreads / 64];
-  __shared__ uint32_t wpre[kEmitThreads / 64 + 1];
-  __shared__ uint32_t bnd[kHugePasses + 1];
-  __shared__ uint32_t s_claim;
-  const uint64_t nm1 = g.N - 1, fm = full_mask1(R);
-  const uint32_t span = ((g.nt_d + kHugePasses - 1) / kHugePasses + 1) & ~1u;
-  constexpr uint32_t kP27 = (1u << 27) - 1u;
-  const bool dynq = b.dyn != nullptr;  // regions from one queue (b.dyn[16], zeroed by the round's transpose)
-  for (uint32_t r = blockIdx.x;;) {
-    __syncthreads();  // the previous region's write-out has read st (and s_claim is read)
-    if (dynq) {
-      if (threadIdx.x == 0) s_claim = atomicAdd(&b.dyn[16], 1u);
-      __syncthreads();
-      r = s_claim;
-    }
-    if (r >= g.nt_s) break;
-    // an opaque copy of the lane index per region: values derived from it (32 sender indices per
-    // lane) are recomputed in each region, not hoisted out of the region loop and spilled
-    uint32_t tid;
-    __asm__ volatile("" : "=v"(tid) : "0"(threadIdx.x));
-    const uint64_t base = (uint64_t)r << g.ts_log;
-    const uint32_t nsend = (uint32_t)min<uint64_t>(g.ts, g.N - base);
-    for (uint32_t d = tid; d < (g.nt_d + 1) >> 1; d += kEmitThreads) cur[d] = 0;
-    __syncthreads();
-    // count pass: one Philox per sender, peers and directions kept in registers
-    uint64_t pk[kHugeQ];
-    uint64_t v[kHugeChunk];
-#pragma unroll
-    for (uint32_t c = 0; c < kHugeChunk; ++c) v[c] = S[base + min(tid + c * kEmitThreads, nsend - 1)];
-#pragma unroll
-    for (uint32_t q0 = 0; q0 < kHugeQ; q0 += kHugeChunk) {
-      uint64_t vn[kHugeChunk];
-      if (q0 + kHugeChunk < kHugeQ) {
-#pragma unroll
-        for (uint32_t c = 0; c < kHugeChunk; ++c)
-          vn[c] = S[base + min(tid + (q0 + kHugeChunk + c) * kEmitThreads, nsend - 1)];
-      }
-#pragma unroll
-      for (uint32_t c = 0; c < kHugeChunk; ++c) {
-        const uint32_t q = q0 + c, i = tid + q * kEmitThreads;
-        uint64_t x64 = 0;
-        const uint32_t d = i < nsend ? sender_dirs(mode, v[c], fm) : 0u;
-        if (d) {
-          const uint32_t n = (uint32_t)(base + i);
-          const u32x4 x = philox4x32_10(u32x4{n, t, 0u, 0u}, key0, key1);
-          const u32x4 lw = FAULTS && fa.loss ? loss_draws(n, t, 0u, key0, key1) : u32x4{0, 0, 0, 0};
-          const Reach rc = FAULTS ? reach_of(n, fa) : Reach{0u, 0xFFFFFFFFu};
-#pragma unroll
-          for (uint32_t j = 0; j < 2; ++j) {
-            if (j >= g.k) break;
-            const uint32_t p = peer_from_word(lane_of(x, j), nm1, n);
-            if (FAULTS && edge_lost(fa, rc, p, lane_of(lw, j))) continue;
-            const uint32_t dd = peer_filter(d, p, filt, b.nzb, b.fullb, b.summ2, b.g2log);
-            if (!dd) continue;
-            const uint32_t tl = p >> kTileDLog;
-            atomicAdd(&cur[tl >> 1], 1u << ((tl & 1u) << 4));
-            x64 |= ((uint64_t)p << (27 * j)) | ((uint64_t)dd << (54 + 2 * j));
-          }
-        }
-        pk[q] = x64;
-        __builtin_amdgcn_sched_barrier(0);  // one sender's cipher at a time (interleaved ciphers spill)
-      }
-      if (q0 + kHugeChunk < kHugeQ) {
-#pragma unroll
-        for (uint32_t c = 0; c < kHugeChunk; ++c) v[c] = vn[c];
-      }
-    }
-    __syncthreads();
-    uint16_t* off_row = b.off + (size_t)r * (g.nt_d + 1);
-    const uint32_t total = region_offsets_huge(cur, g.nt_d, off_row, wsum, wpre, bnd, span);
-    if (tid == 0) b.rtot[r] = total;
-    uint16_t* gdst = b.dst + (size_t)r * g.rp;
-    uint16_t* gsrc = b.src + (size_t)r * g.rp;
-    uint32_t* gprec = b.prec + (size_t)r * g.rp * 3;
-    // an overflowing pass stages its ids in the region's reply slots instead (unused until serve)
-    uint32_t* gscr = (uint32_t*)(b.resp + (size_t)r * g.rp);
-    auto put = [&](uint32_t e, uint32_t id, uint64_t x) {  // record e of the region, x = S_t[its sender]
-      rec_st(&gdst[e], dst_of(id));
-      rec_st(&gsrc[e], src_of(id));
-      prec_st(&gprec[3 * e], (uint32_t)x, (uint32_t)(x >> 32), id);
-    };
-    for (uint32_t h = 0; h < kHugePasses; ++h) {
-      const uint32_t ta = h * span, tb = min(ta + span, g.nt_d);
-      const uint32_t pbase = bnd[h], pcnt = bnd[h + 1] - bnd[h];
-      const bool direct = pcnt > kHugeCap;  // (never at random peers' sizes: ~N(32768, 128))
-      if (h) __syncthreads();  // the previous pass's write-out has read st
-      // opaque per pass: the edges' fields are derived again in each pass, not hoisted out of the
-      // pass loop for both passes at once (that spilled ~250 VGPRs)
-#pragma unroll
-      for (uint32_t q = 0; q < kHugeQ; ++q) __asm__ volatile("" : "+v"(pk[q]));
-#pragma unroll
-      for (uint32_t q = 0; q < kHugeQ; ++q) {
-        const uint32_t i = tid + q * kEmitThreads;
-#pragma unroll
-        for (uint32_t j = 0; j < 2; ++j) {
-          const uint32_t dd = (uint32_t)(pk[q] >> (54 + 2 * j)) & 3u;
-          const uint32_t p = (uint32_t)(pk[q] >> (27 * j)) & kP27;
-          const uint32_t tl = p >> kTileDLog;
-          if (!dd || tl < ta || tl >= tb) continue;
-          const uint32_t sh = (tl & 1u) << 4;
-          const uint32_t pos = (atomicAdd(&cur[tl >> 1], 1u << sh) >> sh) & 0xFFFFu;  // < 2^16: exact
-          const uint32_t id = (p & (kTileD - 1)) | (i << kTileDLog) | dir_flags(dd);
-          if (!direct) st[pos - pbase] = id;
-          else gscr[pos] = id;
-        }
-        __builtin_amdgcn_sched_barrier(0);  // (all 64 slot atomics in flight at once spill)
-      }
-      __syncthreads();
-      if (direct) __threadfence_block();  // (the ids just stored to gscr by other waves of the block)
-      // write-out, kHugeOut records per lane at a time: every id and sender value is loaded before
-      // any record is stored (one dependent S gather per record at a time left the emit latency-bound:
-      // 3.3 ms per 2^27 round, profiles/r06_a)
-      for (uint32_t e0 = 0; e0 < pcnt; e0 += kHugeOut * kEmitThreads) {
-        uint32_t id[kHugeOut];
-        uint64_t x[kHugeOut];
-#pragma unroll
-        for (uint32_t u = 0; u < kHugeOut; ++u) {
-          const uint32_t e = e0 + u * kEmitThreads + tid;
-          id[u] = e < pcnt ? (direct ? gscr[pbase + e] : st[e]) : 0u;
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < kHugeOut; ++u) x[u] = S[base + ((id[u] >> kTileDLog) & kIdNMask)];
-#pragma unroll
-        for (uint32_t u = 0; u < kHugeOut; ++u) {
-          const uint32_t e = e0 + u * kEmitThreads + tid;
-          if (e < pcnt) put(pbase + e, id[u], x[u]);
-        }
-      }
-    }
-    if (!dynq) r += gridDim.x;
   }
 }
 
@@ -1021,7 +803,7 @@ __device__ __forceinline__ void for_each_run_record_pipe(const BinGeom& g, const
     for (int r = 0; r < RPL; ++r) {
       const uint32_t s = s0 + lane * RPL + r;
       const uint32_t be = s < g.nt_s ? nbe[r] : 0u, en = s < g.nt_s ? nen[r] : 0u;
-      len[r] = (en - be) & 0xFFFFu;  // (huge regions: offsets mod 2^16, a run is < 2^16 records)
+      len[r] = en - be;
       exc[r] = lsum;  // (the lane's own part: the wave's prefix is added below)
       basep[r] = (int32_t)(s * g.rp + be);
       lsum += len[r];
@@ -1302,17 +1084,12 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
   if (do_pull) {  // responses owed to this tile's own senders
     const uint32_t* __restrict__ qids = bq.ids;
     const uint64_t* __restrict__ gresp = bq.resp;
-    // huge regions (32768 senders = two tiles): the tile's senders are one half of region X / 2, and
-    // its records are walked whole, keeping the half's (the other tile of the region reads the same
-    // records at about the same time on the same XCD: xcd_remap / TileQueue hand out neighbours)
-    const bool huge = gq.huge != 0;
-    const uint32_t per = huge ? 1u : kTileD >> gq.ts_log;
-    const uint32_t s0 = huge ? X >> 1 : X * per, s1 = min(s0 + per, gq.nt_s);
-    const uint32_t half = huge ? (X & 1u) : 0u;
+    const uint32_t per = kTileD >> gq.ts_log;
+    const uint32_t s0 = X * per, s1 = min(s0 + per, gq.nt_s);
     for (uint32_t s = s0; s < s1; ++s) {
-      const uint32_t total = huge ? bq.rtot[s] : bq.off[(size_t)s * (gq.nt_d + 1) + gq.nt_d];
+      const uint32_t total = bq.off[(size_t)s * (gq.nt_d + 1) + gq.nt_d];
       const size_t reg = (size_t)s * gq.rp;
-      const uint32_t nb = huge ? 0u : (s - s0) << gq.ts_log;
+      const uint32_t nb = (s - s0) << gq.ts_log;
       const uint32_t qtid = tid - qt0;
       for (uint32_t p0 = 0; p0 < total; p0 += qnt * kUnrollSeq) {
         uint64_t r[kUnrollSeq];
@@ -1329,9 +1106,7 @@ __global__ __launch_bounds__(kTileThreads) void bin_apply_kernel(BinGeom g, BinB
         for (int u = 0; u < kUnrollSeq; ++u) {
           // a full sender's slot was never written this round (K2 skips it)
           if (p0 + u * qnt + qtid >= total || (id[u] & kIdVF)) continue;
-          const uint32_t nl = (id[u] >> kTileDLog) & kIdNMask;
-          if (huge && (nl >> kTileDLog) != half) continue;  // the region's other tile
-          const uint32_t node = nb + (huge ? nl & (kTileD - 1) : nl);
+          const uint32_t node = nb + ((id[u] >> kTileDLog) & kIdNMask);
           if (r[u]) atomicOr(&acc[node], (unsigned long long)r[u]);
         }
       }
@@ -1353,24 +1128,10 @@ uint32_t apply_grid(const BinGeom& g) {
 
 }  // namespace
 
-BinGeom make_bin_geom(uint64_t N, uint32_t k, bool big, bool huge) {
+BinGeom make_bin_geom(uint64_t N, uint32_t k, bool big) {
   BinGeom g{};
   g.N = N;
   g.k = k;
-  if (huge && k <= 2 && (N + kTileD - 1) / kTileD > kMaxTilesD && (N + kTileD - 1) / kTileD <= kSbMaxTiles) {
-    g.huge = 1u;
-    g.ts = kHugeSenders;
-    g.ts_log = 15;
-    g.rp = kHugeSenders * k;
-    g.nt_s = (uint32_t)((N + g.ts - 1) / g.ts);
-    g.nt_d = (uint32_t)((N + kTileD - 1) / kTileD);
-    g.apply_grid = kApplyGrid;
-    g.serve_grid = kServeGrid;
-    g.push_waves = kPushWavesBig;
-    g.aos = 1u;
-    g.split = 1u;
-    return g;
-  }
   uint32_t ts = big ? 2 * kMaxSenders : kMaxSenders, lg = big ? 14 : 13;
   while (ts * k > (big ? 2 * kRecPerRegion : kRecPerRegion)) {
     ts >>= 1;
@@ -1405,8 +1166,7 @@ size_t bin_bytes(const BinGeom& g) {
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   return (g.split ? 2 * al(recs * 2) : al(recs * 4)) + (g.aos ? al(recs * 12) : al(recs * 8)) + al(recs * 8) +
          2 * al((size_t)g.nt_s * (g.nt_d + 1) * 2) + 256 +
-         256 +  // the tile queues (dyn)
-         al((size_t)g.nt_s * 4);  // rtot
+         256;  // the tile queues (dyn)
 }
 
 void bin_carve(const BinGeom& g, void* base, BinBufs* b) {
@@ -1435,10 +1195,7 @@ void bin_carve(const BinGeom& g, void* base, BinBufs* b) {
   p += al((size_t)g.nt_s * (g.nt_d + 1) * 2);
   p += 256;
   b->dyn = (uint32_t*)p;  // 16 u32 (sharded passes clear it: their order stays static)
-  p += 256;
-  b->rtot = (uint32_t*)p;  // [nt_s] exact record counts (written by the huge emit)
-  b->summ2 = nullptr;  // (the engine points it at the frontier's mid-level summary per round)
-  b->g2log = 0;
+
 }
 
 hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, uint64_t* partial, uint32_t R,
@@ -1454,12 +1211,7 @@ hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, 
   } else {                                                                \
     if (fa.any()) GOSSIP_EMIT(0, true, VV); else GOSSIP_EMIT(0, false, VV); \
   }
-  if (g.huge) {  // 32768-sender regions (make_bin_geom(huge))
-    if (fa.any())
-      bin_emit_huge_kernel<true><<<eg, kEmitThreads, 0, st>>>(g, S, b, R, t, key0, key1, mode, filt, fa);
-    else
-      bin_emit_huge_kernel<false><<<eg, kEmitThreads, 0, st>>>(g, S, b, R, t, key0, key1, mode, filt, fa);
-  } else if (g.ts > kMaxSenders || g.rp > kRecPerRegion) {  // make_bin_geom(big): V = 4, 5
+  if (g.ts > kMaxSenders || g.rp > kRecPerRegion) {  // make_bin_geom(big): V = 4, 5
     // 16 senders per lane keep no room for their peers in registers (KREG = 2 spills 78
     // VGPRs): V = 5 keeps them in LDS between the passes, V = 4 draws them again
     if (fa.any()) GOSSIP_EMIT(0, true, 4);
@@ -2057,7 +1809,6 @@ void xd_carve_recv(const XdGeom& g, uint64_t cap_r, void* base, XdBufs* b) {
   b->rb.offT = (uint16_t*)take(offs * 2);
   b->rb.nzb = b->rb.fullb = nullptr;
   b->rb.dyn = nullptr;
-  b->rb.rtot = nullptr;
 }
 
 hipError_t launch_xd_requests(const XdGeom& g, const XdBufs& b, const uint64_t* S, uint32_t R, uint32_t t,

@@ -29,18 +29,6 @@
 #include "multi.h"
 #include "philox.h"
 
-// 1: one-shard dense rounds past 2^26 nodes bin 32768-sender regions (binned.hip
-// bin_emit_huge_kernel); 0 (default): 16384 — an A/B build knob (tools/build_variants.sh):
-// the huge emit re-reads each record's sender value from S at random, DESIGN.md §3.7
-#ifndef GOSSIP_HUGE_REGIONS
-#define GOSSIP_HUGE_REGIONS 0
-#endif
-// 1 (default): the one-GPU planner may run a sparse-class round as a dense round whose emit drops
-// the pull-only edges into empty mid-level-summary groups (summ_dense); 0: never (A/B build knob)
-#ifndef GOSSIP_SUMM_DENSE
-#define GOSSIP_SUMM_DENSE 0
-#endif
-
 using namespace gossip;
 
 namespace {
@@ -754,20 +742,6 @@ double filter_frac_of(const gossip_engine* e) {
   return e->N <= (1ull << 25) ? e->filter_frac : 2.0;
 }
 
-// One shard past 2^25 nodes, empty majority: between the light sparse rounds and the dense ones,
-// a sparse round's scan probes the summaries for every edge and fetches the exact bitmap for the
-// quarter that hit (2^27 nodes, 3.7 % nonzero: 3.4 ms), while a dense round whose emit drops the
-// pull-only edges into empty 8-node groups (binned.hip peer_filter with summ2, an L2-resident
-// probe) moves ~30 % of the records.  Chosen when the nonzero share is in [kSummDenseLo, sparse
-// threshold] (profiles/r06_*); a forced path (sparse_frac set) keeps its rounds.
-constexpr double kSummDenseLo = 0.005;
-bool summ_dense(const gossip_engine* e, const Est& x, uint32_t maj) {
-  if (!GOSSIP_SUMM_DENSE || maj != 0 || !e->binned || !e->frontier || !e->fb.summ2 || e->sparse_frac_set ||
-      e->N <= (1ull << 25))
-    return false;
-  return x.nz >= kSummDenseLo * (double)e->N;
-}
-
 RoundSync ring_sync(gossip_engine* e, uint32_t slot) {
   RoundSync rs;
   rs.ring = e->ring_d + (size_t)slot * (part_len(e) + 1);
@@ -811,16 +785,9 @@ int launch_round_path(gossip_engine* e, uint32_t t, bool sparse, uint32_t maj, b
     HIP_OK(e, launch_frontier_round(fb, e->S, e->N, e->partial_d, e->R, e->k, t, e->key0, e->key1, e->mode, maj,
                                     !all_d ? kSparseFlags : (maj == 0 && e->sparse_direct ? kSparseDirect : kSparseAllD),
                                     e->fa, e->cfg.flags, rs, e->stream));
-  else {
-    BinBufs bb = e->bb;
-    if ((filt & 1u) && fb.summ2 && e->N > (1ull << 25)) {  // pull-only edges tested in the mid-level summary
-      HIP_OK(e, launch_frontier_summ2(fb, e->N, 0u, e->stream));
-      bb.summ2 = fb.summ2;
-      bb.g2log = fb.g2log;
-    }
-    HIP_OK(e, launch_binned_round(e->bg, bb, e->S, e->partial_d, e->R, t, e->key0, e->key1, e->mode, filt, e->fa,
-                                  e->cfg.flags, rs, e->stream));
-  }
+  else
+    HIP_OK(e, launch_binned_round(e->bg, e->bb, e->S, e->partial_d, e->R, t, e->key0, e->key1, e->mode, filt,
+                                  e->fa, e->cfg.flags, rs, e->stream));
   if (timed) {
     HIP_OK(e, hipEventRecord(e->evr[slot][1], e->stream));
     e->evr_round[slot] = t;
@@ -885,12 +852,8 @@ int step_planned(gossip_engine* e, uint32_t max_rounds, gossip_round_stats_t* st
       for (uint32_t i = done; i < launched; ++i) x = predict(e, x);
       uint32_t maj = 0;
       bool all_d = false;
-      bool sparse = choose_sparse(e, x, &maj, &all_d);
-      uint32_t filt = dense_filter(e, x, filter_frac_of(e));
-      if (sparse && summ_dense(e, x, maj)) {  // a dense round that skips the edges into empty groups
-        sparse = false;
-        filt |= 1u;
-      }
+      const bool sparse = choose_sparse(e, x, &maj, &all_d);
+      const uint32_t filt = dense_filter(e, x, filter_frac_of(e));
       const uint32_t slot = launched % kRing;
       const RoundSync rs = ring_sync(e, slot);
       want[slot] = rs.seq;
@@ -1250,12 +1213,8 @@ int compute_round(gossip_engine* e, const uint64_t* gathered) {
     uint32_t maj = 0;
     bool all_d = false;
     const Est x = est_of(e, tot.data());
-    bool sparse = choose_sparse(e, x, &maj, &all_d);
-    uint32_t filt = dense_filter(e, x, filter_frac_of(e));
-    if (sparse && summ_dense(e, x, maj)) {  // (as step_planned)
-      sparse = false;
-      filt |= 1u;
-    }
+    const bool sparse = choose_sparse(e, x, &maj, &all_d);
+    const uint32_t filt = dense_filter(e, x, filter_frac_of(e));
     if ((rc = timer_begin(e, 0))) return rc;
     if ((rc = launch_round_path(e, e->t, sparse, maj, all_d, filt,
                                 ring_sync(e, 0), -1)))
@@ -1590,9 +1549,7 @@ int gossip_create(const gossip_config_t* cfg, gossip_engine_t** out) {
     // past kBigFromTiles tiles the emit regions double (longer runs per tile, binned.hip V = 4, 5):
     // per dense round 2^25 nodes 1135 -> 1094 us, 2^26 2981 -> 2582 us; 2^24 slower (521 -> 583 us:
     // its runs of 16 records gain less than the big emit costs), profiles/r04_s
-    // past kMaxTilesD tiles (2^26 nodes) with k <= 2: 32768-sender regions (binned.hip
-    // bin_emit_huge_kernel; runs of ~8 records at 2^27 instead of ~4)
-    e->bg = make_bin_geom(e->N, e->k, (e->N + kTileD - 1) / kTileD > kBigFromTiles, GOSSIP_HUGE_REGIONS != 0);
+    e->bg = make_bin_geom(e->N, e->k, (e->N + kTileD - 1) / kTileD > kBigFromTiles);
     const size_t bytes = bin_bytes(e->bg);
     if (hipMalloc(&e->bin_mem, bytes) != hipSuccess) {
       e->err = "hipMalloc of " + std::to_string(bytes) + " bytes (bins) failed";

@@ -56,10 +56,6 @@ void frontier_carve(uint64_t N, void* base, FrontierBufs* f);
 // summary f.summ2 when f has one.  No early exit.
 hipError_t launch_frontier_summary(const FrontierBufs& f, uint64_t N, uint32_t maj, hipStream_t st);
 
-// The mid-level summary alone (f.summ2, when f has one): what a dense round's summary filter probes
-// (binned.h BinBufs::summ2)
-hipError_t launch_frontier_summ2(const FrontierBufs& f, uint64_t N, uint32_t maj, hipStream_t st);
-
 // how a sparse round's push deltas reach its commit (launch_frontier_round)
 constexpr uint32_t kSparseFlags = 0, kSparseAllD = 1, kSparseDirect = 2;
 

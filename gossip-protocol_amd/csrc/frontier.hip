@@ -790,22 +790,6 @@ void frontier_carve(uint64_t N, void* base, FrontierBufs* f) {
   f->scan_q = 1;
 }
 
-namespace {
-__global__ __launch_bounds__(256) void frontier_summ2_kernel(FrontierBufs f, uint64_t N, uint32_t maj) {
-  const uint32_t s = blockIdx.x * 256 + threadIdx.x;
-  if (maj)
-    summ2_body<1>(f, s, N);
-  else
-    summ2_body<0>(f, s, N);
-}
-}  // namespace
-
-hipError_t launch_frontier_summ2(const FrontierBufs& f, uint64_t N, uint32_t maj, hipStream_t st) {
-  if (N == 0 || !f.summ2) return hipSuccess;
-  frontier_summ2_kernel<<<(f.summ2_words + 255) / 256, 256, 0, st>>>(f, N, maj);
-  return hipGetLastError();
-}
-
 hipError_t launch_frontier_summary(const FrontierBufs& f, uint64_t N, uint32_t maj, hipStream_t st) {
   if (N == 0) return hipSuccess;  // a shard without nodes
   const uint32_t s2 = f.summ2 ? f.summ2_words : 0u;  // the mid-level summary too when f has one

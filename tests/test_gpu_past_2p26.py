@@ -1,11 +1,12 @@
-"""GPU, the one-shard dense rounds past 2^26 nodes with 32768-sender regions against the OpenMP oracle.
+"""GPU, the one-shard round paths past 2^26 nodes (more than 4096 destination tiles) against the
+OpenMP oracle.
 
-Past 4096 destination tiles (N > 2^26) with fanout <= 2 the dense emit bins 32768-sender regions
-(binned.hip bin_emit_huge_kernel): the peers stay in registers, the records are written in two
-passes over halves of the tiles, the run offsets are kept mod 2^16 with exact totals per region,
-and the apply's reply walk takes its half of a region's records (a tile is half a region).  Every
-path must equal the oracle bit for bit: per-round stats, per-rumor counts and the final state.
-N = 2^26 + 4099: 4097 tiles, a ragged last region (4099 senders) and a ragged last tile.
+Past 4096 tiles the sender values no longer fit the emit's LDS beside the tile counters, so the
+dense emit bins 16384-sender regions with 16-bit packed tile counters and writes each push packed
+with its id (binned.hip V = 5; V = 4 with faults), and serve / apply run their per-XCD tile queues.
+N = 2^26 + 4099: 4097 tiles, a ragged last region and a ragged last tile.  Every path must equal the
+oracle bit for bit: per-round stats, per-rumor counts and the final state.  (Round 6 ran the same
+cases on the 32768-sender layout it measured and dropped, profiles/r06_huge/.)
 Reference: (*NodeState).Gossip, main.go:65-89, as rounds.
 """
 import os
@@ -22,7 +23,8 @@ N = (1 << 26) + 4099
 THREADS = min(16, os.cpu_count() or 1)
 ROUNDS = 40
 # auto: as planned (sparse and dense rounds); dense: every round on the dense pipeline; dense_filter:
-# every round dense with the edge filter (empty / full peers' one-way edges dropped in the emit)
+# every round dense with the edge filter (empty / full peers' one-way edges dropped in the emit;
+# past 2^25 nodes off by default, forced here)
 PATHS = {"auto": {}, "dense": {"sparse_frac": -1.0},
          "dense_filter": {"sparse_frac": -1.0, "filter_frac": 0.3}}
 CASES = {"pushpull-k2-R64": ("pushpull", 2, 64, 0x5EED0003, 0, 0),
@@ -50,7 +52,7 @@ def oracle_runs():
 
 @pytest.mark.parametrize("case", list(CASES))
 @pytest.mark.parametrize("path", list(PATHS))
-def test_huge_regions_equal_oracle(oracle_runs, case, path):
+def test_past_4096_tiles_equal_oracle(oracle_runs, case, path):
     mode, k, r, seed, loss, parts = CASES[case]
     ro, full = oracle_runs(case)
     e = Engine(N, r, mode, k, seed, flags=1, edge_loss=loss, partitions=parts, params=PATHS[path])
