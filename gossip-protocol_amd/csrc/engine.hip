@@ -492,42 +492,51 @@ int timed_trial(gossip_engine* e, Run run, float* ms) {
 }
 
 // Placement of a slab: `trial(slab, &ms)` times a round over the slab at `slab`;
-// up to place_tries fresh allocations of `bytes` are tried (each held while the next is made, so
-// each is a fresh placement) and the fastest is kept in *mem (the others are freed).  Timer 5 gets
-// the trial rounds.  Returns whether *mem moved.
+// up to place_tries allocations of `bytes` are tried and the fastest is kept in *mem.  At most two
+// slabs are held beside the kept one: the best so far, the last loser (held while the next
+// candidate is allocated, so that candidate cannot reuse its pages) and the new candidate
+// (round 5 held every candidate: 75 GB at 2^27).  Timer 5 gets the trial rounds.  Returns whether
+// *mem moved.
 template <class Trial>
 int place_slab(gossip_engine* e, void** mem, size_t bytes, Trial trial, bool* moved, const char* what) {
   *moved = false;
-  std::vector<void*> cand{*mem};
-  std::vector<float> tms;
-  int rc = GOSSIP_OK;
-  for (uint32_t i = 0; i < e->place_tries && rc == GOSSIP_OK; ++i) {
-    if (i > 0) {
-      void* p = nullptr;
-      if (hipMalloc(&p, bytes) != hipSuccess) {
-        (void)hipGetLastError();  // no room for another trial: keep the best so far
-        break;
-      }
-      cand.push_back(p);
-    }
-    float ms = 0.f;
-    rc = trial(cand.back(), &ms);
-#ifdef GOSSIP_EXP_PLACE_LOG
-    std::fprintf(stderr, "%s: candidate %u slab %p trial %.1f us\n", what, i, cand.back(), ms * 1e3);
-#endif
-    (void)what;
-    tms.push_back(ms);
+  void* best = *mem;
+  void* held = nullptr;
+  float best_ms = 0.f;
+  int rc = trial(best, &best_ms);
+  auto account = [&](float ms) {
     e->time_ms[5] += 3.0 * ms;
     e->launches[5] += 3;
+  };
+  account(best_ms);
+#ifdef GOSSIP_EXP_PLACE_LOG
+  std::fprintf(stderr, "%s: candidate 0 slab %p trial %.1f us\n", what, best, best_ms * 1e3);
+#endif
+  for (uint32_t i = 1; i < e->place_tries && rc == GOSSIP_OK; ++i) {
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) {
+      (void)hipGetLastError();  // no room for another trial: keep the best so far
+      break;
+    }
+    float ms = 0.f;
+    rc = trial(p, &ms);
+    account(ms);
+#ifdef GOSSIP_EXP_PLACE_LOG
+    std::fprintf(stderr, "%s: candidate %u slab %p trial %.1f us\n", what, i, p, ms * 1e3);
+#endif
+    void* loser = p;
+    if (rc == GOSSIP_OK && ms < best_ms) {
+      loser = best;
+      best = p;
+      best_ms = ms;
+    }
+    if (held) (void)hipFree(held);  // (its trial has completed: timed_trial synchronizes)
+    held = loser;
   }
-  size_t best = 0;
-  for (size_t i = 1; i < tms.size(); ++i)
-    if (tms[i] < tms[best]) best = i;
-  if (rc != GOSSIP_OK) best = 0;
-  for (size_t i = 0; i < cand.size(); ++i)
-    if (i != best) (void)hipFree(cand[i]);
-  *moved = cand[best] != *mem;
-  *mem = cand[best];
+  (void)what;
+  if (held) (void)hipFree(held);
+  *moved = best != *mem;
+  *mem = best;
   return rc;
 }
 
@@ -923,38 +932,41 @@ int ae_place(gossip_engine* e) {
   e->ae_placed = true;
   const size_t vb = (size_t)e->N * e->R * 4;
   if (e->place_tries <= 1 || !(e->ae_dbin && e->ae_dbin_on) || vb < (512ull << 20)) return GOSSIP_OK;
-  const size_t pl = part_len(e), rb = (size_t)e->ae_bg.nreg * ((size_t)e->k << e->ae_bg.rs) * 4;
+  const size_t pl = part_len(e);
   uint64_t* part = nullptr;
   HIP_OK(e, hipMalloc((void**)&part, (pl + 8) * 8));
   struct Cand {
-    uint32_t *V, *Vn, *brec;
+    uint32_t *V, *Vn;
   };
-  std::vector<Cand> cand{{e->V, e->Vn, e->ae_brec}};
-  std::vector<float> tms;
+  // (as place_slab: the kept rows, the best candidate so far, the last loser held while the next
+  // candidate is allocated, and that candidate: at most two sets of rows beside the kept ones)
+  Cand best{e->V, e->Vn}, held{nullptr, nullptr};
+  float best_ms = 0.f;
   hipEvent_t ev[2];
   HIP_OK(e, hipEventCreate(&ev[0]));
   HIP_OK(e, hipEventCreate(&ev[1]));
   int rc = GOSSIP_OK;
+  auto release = [](Cand& c) {
+    if (c.V) (void)hipFree(c.V);
+    if (c.Vn) (void)hipFree(c.Vn);
+    c = Cand{nullptr, nullptr};
+  };
   const uint32_t tries = e->place_tries;  // 12 by default: a fast placement of the rows is ~1 in 8
   for (uint32_t i = 0; i < tries && rc == GOSSIP_OK; ++i) {
+    Cand c = best;
     if (i > 0) {
       // the rows carry the mode, the records do not (profiles/r05_pl/r05_aem/): only the rows move
-      Cand c{nullptr, nullptr, cand[0].brec};
-      if ((!c.V && hipMalloc((void**)&c.V, vb) != hipSuccess) || (!c.Vn && hipMalloc((void**)&c.Vn, vb) != hipSuccess) ||
-          (!c.brec && hipMalloc((void**)&c.brec, rb) != hipSuccess)) {
+      c = Cand{nullptr, nullptr};
+      if (hipMalloc((void**)&c.V, vb) != hipSuccess || hipMalloc((void**)&c.Vn, vb) != hipSuccess) {
         (void)hipGetLastError();  // no room for another trial: keep the best so far
-        if (c.V) (void)hipFree(c.V);
-        if (c.Vn) (void)hipFree(c.Vn);
+        release(c);
         break;
       }
-      cand.push_back(c);
-      if (c.V != e->V && hipMemcpyAsync(c.V, e->V, vb, hipMemcpyDeviceToDevice, e->stream) != hipSuccess)
-        rc = GOSSIP_EHIP;
+      if (hipMemcpyAsync(c.V, best.V, vb, hipMemcpyDeviceToDevice, e->stream) != hipSuccess) rc = GOSSIP_EHIP;
     }
     AeArgs d = make_ae_args(e);
-    d.V = cand.back().V;
-    d.Vn = cand.back().Vn;
-    d.brec = cand.back().brec;
+    d.V = c.V;
+    d.Vn = c.Vn;
     d.partial = part;
     d.aux = part + pl;
     d.zero = part;
@@ -975,28 +987,29 @@ int ae_place(gossip_engine* e) {
 #ifdef GOSSIP_EXP_PLACE_LOG
     std::fprintf(stderr, "ae_place: candidate %u trial %.1f us\n", i, ms * 1e3);
 #endif
-    tms.push_back(ms);
     e->time_ms[5] += 2.0 * ms;
     e->launches[5] += 2;
+    if (i == 0) {
+      best_ms = ms;
+      continue;
+    }
+    Cand loser = c;
+    if (rc == GOSSIP_OK && ms < best_ms) {
+      loser = best;
+      best = c;
+      best_ms = ms;
+    }
+    if (held.V) (void)hipStreamSynchronize(e->stream);  // (no trial is still reading the rows freed next)
+    release(held);
+    held = loser;
   }
   (void)hipEventDestroy(ev[0]);
   (void)hipEventDestroy(ev[1]);
   (void)hipFree(part);
-  size_t best = 0;
-  for (size_t i = 1; i < tms.size(); ++i)
-    if (tms[i] < tms[best]) best = i;
-  if (rc != GOSSIP_OK) best = 0;
   HIP_OK(e, hipStreamSynchronize(e->stream));
-  for (size_t i = 0; i < cand.size(); ++i) {
-    if (i == best) continue;
-    const Cand& b = cand[best];
-    if (cand[i].V != b.V) (void)hipFree(cand[i].V);
-    if (cand[i].Vn != b.Vn) (void)hipFree(cand[i].Vn);
-    if (cand[i].brec != b.brec) (void)hipFree(cand[i].brec);
-  }
-  e->V = cand[best].V;  // (a candidate's V holds a copy of the rows)
-  e->Vn = cand[best].Vn;
-  e->ae_brec = cand[best].brec;
+  release(held);
+  e->V = best.V;  // (a candidate's V holds a copy of the rows)
+  e->Vn = best.Vn;
   if (rc != GOSSIP_OK) return e->fail(rc, "ANTIENTROPY placement trial failed");
   return GOSSIP_OK;
 }

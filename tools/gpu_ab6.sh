@@ -10,6 +10,10 @@
 #   PMC    1: HBM bytes and L2 request counters of each variant's dense rounds (one pass per counter
 #          group, tools/pmc_dense.py + tools/pmc_sq.py), with placement trials off (place_tries 1)
 #   LIST   1: rocprofv3 --list-avail into $OUT/counters.txt
+#   PROBES "G log2N,...": tools/shard_probe.py per-rank device time (PROBE_LIB: a variant)
+#   REH    1: gloo rehearsals of bench.py --gpus 2 and 4 on the one GPU (the N > 1 line's fields)
+#   SEQ    "N:engines,...": placement over engines made one after another (tools/place_seq.py)
+#   SKIP_AB 1: stop before the per-variant A/B
 #   PLACE  1: TLB / L2 / DRAM-credit counters of every placement candidate's trial rounds at 2^27
 #          (tools/place_probe4.py under rocprofv3 --pmc, one pass per group; tools/place_pmc.py), with
 #          the library PLACE_LIB (default: the in-tree one)
@@ -41,6 +45,31 @@ if [ "${TESTS:-none}" != none ]; then
     -p no:cacheprovider > $O/pytest_gpu.txt 2>&1
   rc=$?; tail -4 $O/pytest_gpu.txt; ok $rc pytest
 fi
+if [ -n "${SEQ:-}" ]; then  # placement over engines made one after another: "N:engines,..." (tools/place_seq.py)
+  IFS=, read -ra SS <<< "$SEQ"
+  for q in "${SS[@]}"; do
+    PROBE_N=${q%%:*} PROBE_ENGINES=${q##*:} timeout -k 10 600 python -u tools/place_seq.py > $O/place_seq_${q%%:*}.txt 2>&1
+    ok $? "place_seq $q"
+    cat $O/place_seq_${q%%:*}.txt
+  done
+fi
+if [ -n "${PROBES:-}" ]; then  # per-rank device time of sharded rounds: "G log2N" pairs, comma-separated
+  IFS=, read -ra PS <<< "$PROBES"
+  for g in "${PS[@]}"; do
+    set -- $g
+    GOSSIP_LIB=${PROBE_LIB:-} timeout -k 10 300 python tools/shard_probe.py $1 $2 > $O/probe_G$1.txt 2>&1; ok $? "probe $g"
+    tail -2 $O/probe_G$1.txt
+  done
+fi
+if [ "${REH:-0}" = 1 ]; then  # gloo rehearsals of the N > 1 bench line on one GPU (not a measurement)
+  for G in 2 4; do
+    timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node $G --master-addr 127.0.0.1 \
+      --master-port $((29515 + G)) bench.py --gpus $G --steps 2 --warmup 1 --backend gloo \
+      > $O/bench_rehearsal_gloo_G$G.json 2> $O/rehearsal_G$G.err; ok $? "rehearsal G=$G"
+    cat $O/bench_rehearsal_gloo_G$G.json
+  done
+fi
+if [ "${SKIP_AB:-0}" = 1 ]; then echo done; exit 0; fi
 for n in ${SIZES:-134217728}; do
   for X in ${VARS:-default}; do
     L=exp/lib$X.so; [ "$X" = default ] && L=""
