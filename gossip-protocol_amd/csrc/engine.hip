@@ -12,6 +12,7 @@
 #include <cstring>
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <string>
 #include <vector>
 
@@ -514,15 +515,22 @@ int place_slab(gossip_engine* e, void** mem, size_t bytes, Trial trial, bool* mo
 #endif
   for (uint32_t i = 1; i < e->place_tries && rc == GOSSIP_OK; ++i) {
     void* p = nullptr;
+#ifdef GOSSIP_EXP_PLACE_LOG
+    const auto t0 = std::chrono::steady_clock::now();
+#endif
     if (hipMalloc(&p, bytes) != hipSuccess) {
       (void)hipGetLastError();  // no room for another trial: keep the best so far
       break;
     }
+#ifdef GOSSIP_EXP_PLACE_LOG
+    const auto t1 = std::chrono::steady_clock::now();
+#endif
     float ms = 0.f;
     rc = trial(p, &ms);
     account(ms);
 #ifdef GOSSIP_EXP_PLACE_LOG
-    std::fprintf(stderr, "%s: candidate %u slab %p trial %.1f us\n", what, i, p, ms * 1e3);
+    std::fprintf(stderr, "%s: candidate %u slab %p trial %.1f us, hipMalloc %.1f ms\n", what, i, p, ms * 1e3,
+                 std::chrono::duration<double, std::milli>(t1 - t0).count());
 #endif
     void* loser = p;
     if (rc == GOSSIP_OK && ms < best_ms) {
@@ -530,7 +538,14 @@ int place_slab(gossip_engine* e, void** mem, size_t bytes, Trial trial, bool* mo
       best = p;
       best_ms = ms;
     }
+#ifdef GOSSIP_EXP_PLACE_LOG
+    const auto t2 = std::chrono::steady_clock::now();
+#endif
     if (held) (void)hipFree(held);  // (its trial has completed: timed_trial synchronizes)
+#ifdef GOSSIP_EXP_PLACE_LOG
+    std::fprintf(stderr, "%s: hipFree %.1f ms\n", what,
+                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t2).count());
+#endif
     held = loser;
   }
   (void)what;

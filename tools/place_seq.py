@@ -37,7 +37,7 @@ for i in range(int(os.environ.get("PROBE_ENGINES", 4))):
             while not stop.is_set():
                 low[0] = min(low[0], torch.cuda.mem_get_info()[0])
                 time.sleep(0.002)
-        th = threading.Thread(target=sample) if s == 0 else None
+        th = threading.Thread(target=sample) if s == 0 and not os.environ.get("PROBE_NOSAMPLE") else None
         if th:
             th.start()
         t0 = time.perf_counter()
