@@ -180,6 +180,9 @@ struct gossip_engine {
   double xd_filter_frac = 0.6;    // exchange rounds likewise (their probe hits a G-shard class image: G = 8 sweep)
   double alld_frac = 1.0 / 128;   // sparse rounds with k * rare >= alld_frac * N commit every group's D (sweep: profiles/r05_ad/)
   bool sparse_direct = true;      // ... and with an empty majority take the pushes into empty peers in S (kSparseDirect)
+  // sparse rounds take the binned scan (frontier.hip K1a / K1b) once this share of peers would hit
+  // the LDS summary (param bin_scan_frac)
+  double bscan_frac = 0.6;
   double mid_frac = 0.5;          // sparse rounds test peers in the mid-level summary once this share hits the LDS one
   // pipelined rounds (binned engines): the host picks each round's path from the
   // totals it has read, predicted forward over the rounds still in flight, and
@@ -748,6 +751,19 @@ bool choose_sparse(const gossip_engine* e, const Est& x, uint32_t* maj, bool* al
   return rare <= sparse_frac_of(e) * (double)e->N;
 }
 
+// the binned sparse scan: once the LDS summary (g nodes per bit) would have a bit set under
+// 1 - (1 - r)^g >= bscan_frac of the peers it filters too little, and binning every edge by peer
+// tile costs less than probing the mid-level summary and the exact bitmap per edge (DESIGN.md
+// §3.3).  Its records and run table live in the dense round's record slab.
+bool bscan_round(const gossip_engine* e, const Est& x, uint32_t maj) {
+  if (!e->binned || !e->frontier || !bs_path_ok(e->N, e->k) || e->bscan_frac > 1.0) return false;
+  const size_t recs = (size_t)e->bg.nt_s * e->bg.rp;
+  if (bs_rec_bytes(e->N, e->k) > recs * 8 || bs_tab_bytes(e->N) > recs * 8) return false;
+  const double N = (double)e->N, rare = maj ? N - x.full : x.nz;
+  const double g = (double)(1u << e->fb.glog);
+  return 1.0 - std::pow(1.0 - std::min(std::max(rare / N, 0.0), 1.0), g) >= e->bscan_frac;
+}
+
 // dense rounds: probe the peer's class in emit when many edges would move
 // nothing (pulls from empty peers early in a run, pushes into full peers late)
 uint32_t dense_filter(const gossip_engine* e, const Est& x, double frac) {
@@ -793,7 +809,7 @@ int round_timer_collect(gossip_engine* e, uint32_t slot, int64_t limit) {
 // One pipelined round: its kernels (bracketed by the slot's events when timing),
 // then the snapshot of the totals into ring slot `slot` (rs).
 int launch_round_path(gossip_engine* e, uint32_t t, bool sparse, uint32_t maj, bool all_d, uint32_t filt,
-                      const RoundSync& rs, int slot) {
+                      const RoundSync& rs, int slot, bool bscan) {
   const bool timed = e->timing && slot >= 0;
   if (timed) {
     if (int rc = round_timer_collect(e, (uint32_t)slot, INT64_MAX)) return rc;
@@ -805,6 +821,12 @@ int launch_round_path(gossip_engine* e, uint32_t t, bool sparse, uint32_t maj, b
   // at 61 % -920 us; profiles/r03_mid).  The kernels decide from the exact rare count.
   FrontierBufs fb = e->fb;
   fb.mid_frac = (float)e->mid_frac;
+  if (sparse && bscan) {  // (the slab pointers change when placement re-carves it)
+    fb.brec = (uint32_t*)e->bb.resp;
+    fb.btab = (uint16_t*)(e->bb.prec ? (void*)e->bb.prec : (void*)e->bb.vals);
+    fb.btiles = bs_tiles(e->N);
+    fb.bregions = bs_regions(e->N);
+  }
   if (sparse)
     HIP_OK(e, launch_frontier_round(fb, e->S, e->N, e->partial_d, e->R, e->k, t, e->key0, e->key1, e->mode, maj,
                                     !all_d ? kSparseFlags : (maj == 0 && e->sparse_direct ? kSparseDirect : kSparseAllD),
@@ -881,7 +903,9 @@ int step_planned(gossip_engine* e, uint32_t max_rounds, gossip_round_stats_t* st
       const uint32_t slot = launched % kRing;
       const RoundSync rs = ring_sync(e, slot);
       want[slot] = rs.seq;
-      if (int rc = launch_round_path(e, t0 + launched, sparse, maj, all_d, filt, rs, (int)slot)) return rc;
+      if (int rc = launch_round_path(e, t0 + launched, sparse, maj, all_d, filt, rs, (int)slot,
+                                     sparse && bscan_round(e, x, maj)))
+        return rc;
       ++launched;
     }
     if (done == launched) break;
@@ -1245,7 +1269,7 @@ int compute_round(gossip_engine* e, const uint64_t* gathered) {
     const uint32_t filt = dense_filter(e, x, filter_frac_of(e));
     if ((rc = timer_begin(e, 0))) return rc;
     if ((rc = launch_round_path(e, e->t, sparse, maj, all_d, filt,
-                                ring_sync(e, 0), -1)))
+                                ring_sync(e, 0), -1, sparse && bscan_round(e, x, maj))))
       return rc;
     return timer_end(e, 0);  // stats are fused into the round kernels
   } else if (e->sbin) {  // sharded dense round: binned pipeline over the gathered image
@@ -1725,6 +1749,8 @@ int gossip_set_param(gossip_engine_t* e, const char* name, double v) {
     e->link_gbps = v;
   } else if (n == "rccl_dev_collectives") {
     e->rccl_dev = v != 0;
+  } else if (n == "bin_scan_frac") {
+    e->bscan_frac = v;
   } else if (n == "mid_frac") {
     e->mid_frac = v;
   } else if (n == "scan_queue") {

@@ -41,6 +41,12 @@ struct FrontierBufs {
   // resolved 128 at a time (one chain of round trips per 128 edges, not per wave batch); 0: the
   // per-batch resolution (param scan_queue)
   uint32_t scan_q;
+  // round 6, binned sparse scan (frontier.hip K1a / K1b): set per round by the engine when the
+  // round takes it (null: the LDS-summary scan).  brec: [bregions][k * 4096] u32 records,
+  // btab: [bregions][btiles + 1] u16 run starts; both carved from the dense round's record slab.
+  uint32_t* brec;
+  uint16_t* btab;
+  uint32_t btiles, bregions;
   uint64_t id0;      // global id of node 0 of these arrays (a shard's first node; 0 on one GPU): the hash uses global ids
 };
 
@@ -49,6 +55,13 @@ uint32_t frontier_glog(uint64_t N);
 uint32_t frontier_g2log(uint64_t N);
 uint32_t frontier_summ2_words(uint64_t N);
 size_t frontier_bytes(uint64_t N);
+// the binned sparse scan's geometry: tiles of 2^19 peers, regions of 4096 senders; ok for
+// k <= 4 and N <= 2^29; bytes of its record array and of its run-start table
+bool bs_path_ok(uint64_t N, uint32_t k);
+uint32_t bs_tiles(uint64_t N);
+uint32_t bs_regions(uint64_t N);
+size_t bs_rec_bytes(uint64_t N, uint32_t k);
+size_t bs_tab_bytes(uint64_t N);
 void frontier_carve(uint64_t N, void* base, FrontierBufs* f);
 
 // Coarse summary (f.summ, 1 bit per 2^f.glog nodes) of the rare set of an

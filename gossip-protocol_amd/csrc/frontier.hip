@@ -26,6 +26,8 @@
 // dense round bit for bit.  K2 in rebuild mode computes absolute stats and
 // both bitmaps from S (after inject/reset or a direct-path round).
 #include "frontier.h"
+
+#include <algorithm>
 #include "philox.h"
 #include "round.h"
 #include "wave.h"
@@ -516,6 +518,305 @@ __device__ __forceinline__ void scan_body_q(uint4* summ4, uint64_t* rws, uint2* 
   }
 }
 
+// Binned sparse scan (round 6, FrontierBufs::brec).  In the heaviest sparse rounds at 2^27
+// (1-4 % rare nodes) the LDS summary (128 nodes per bit) is saturated and every edge of a
+// majority node costs a random probe of the mid-level summary in the L2 and a quarter of them
+// one of the exact bitmap in the MALL: ~3.5 * 10^8 random requests, which bound the scan at
+// ~2.9 ms whatever the occupancy (an LDS-free scan at 8 waves per SIMD measured the same,
+// DESIGN.md §3.7).  Here the peer test moves into LDS the way the dense round moves its
+// gathers: K1a draws every node's peers and bins its live edges by peer tile (2^19 nodes) into
+// 4-B records {p - tile base | rare(n) << 19 | n - region base << 20}, one contiguous
+// tile-sorted run list per 4096-node region plus a u16 run-start table; K1b loads one tile's
+// exact rare bitmap (64 KiB) into LDS, walks that tile's run of every region of its chunk and
+// resolves the edges with a rare end through the per-wave queue of the queued scan (S_t gathers
+// and atomics).  Traffic: 8 B per node written and read (k = 2) instead of the probes.
+constexpr uint32_t kBsRegLog = 12;                 // 4096 senders per region (n - region base: 12 bits)
+constexpr uint32_t kBsTileLog = 19;                // 2^19 peers per tile (p - tile base: 19 bits; 64 KiB bitmap)
+constexpr uint32_t kBsTileWords = 1u << (kBsTileLog - 6);
+constexpr int kBsEmitThreads = 1024;               // 4 senders per thread and region
+constexpr int kBsTestThreads = 1024;
+constexpr uint32_t kBsEmitGrid = 512;              // persistent emit blocks (2 per CU: 68 KiB of LDS each)
+constexpr uint32_t kBsMaxTiles = kBsEmitThreads;   // one tile counter per emit thread: N <= 2^29
+constexpr uint32_t kBsTestBlocks = 1024;           // K1b blocks: tiles x region chunks
+#ifndef GOSSIP_BS_UNROLL
+#define GOSSIP_BS_UNROLL 4
+#endif
+constexpr int kBsUnroll = GOSSIP_BS_UNROLL;        // K1b record windows in flight per wave
+
+template <int MAJ, int MODE, bool FAULTS, int KM>  // KM: peers per node held in registers (>= k)
+__device__ __forceinline__ void bs_emit_body(uint32_t* cnt, uint32_t* stg, const FrontierBufs& f, uint64_t N,
+                                             uint32_t k, uint32_t t, uint32_t key0, uint32_t key1, const Faults& fa) {
+  constexpr bool kPush = (MODE & 1) != 0, kPull = (MODE & 2) != 0;
+  constexpr int kU = (1 << kBsRegLog) / kBsEmitThreads;
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t nm1 = (uint32_t)(N - 1), ntiles = f.btiles, nreg = f.bregions, rcap = k << kBsRegLog;
+  for (uint32_t i = tid; i < ntiles; i += kBsEmitThreads) cnt[i] = 0;
+  for (uint32_t r = blockIdx.x; r < nreg; r += gridDim.x) {
+    const uint32_t n0 = r << kBsRegLog;
+    __syncthreads();  // cnt zeroed (first region) / stg drained (the previous one)
+    uint32_t pp[kU][KM], rk[kU][KM], live[kU];
+    bool rn[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const uint32_t n = n0 + u * kBsEmitThreads + tid;
+      const bool valid = n < N;
+      const uint32_t w0 = __builtin_amdgcn_readfirstlane((n0 + u * kBsEmitThreads + (tid & ~63u)) >> 6);
+      rn[u] = valid && ((rare_word<MAJ>(f, w0, N) >> lane) & 1ull);
+      const bool act = valid && (rn[u] || !((!kPull && MAJ == 0) || (!kPush && MAJ == 1)));
+      live[u] = 0;
+      if (act) {
+        const u32x4 r4 = philox4x32_10(u32x4{n, t, 0u, 0u}, key0, key1);
+        u32x4 lw{0, 0, 0, 0};
+        Reach rc{0u, 0xFFFFFFFFu};
+        if (FAULTS) {
+          if (fa.loss) lw = loss_draws(n, t, 0u, key0, key1);
+          rc = reach_of(n, fa);
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < KM; ++j) {
+          if (j >= k) break;
+          pp[u][j] = peer_from_word(lane_of(r4, j), nm1, n);
+          const bool lost = FAULTS && edge_lost(fa, rc, pp[u][j], lane_of(lw, j));
+          if (!lost) {
+            live[u] |= 1u << j;
+            rk[u][j] = atomicAdd(&cnt[pp[u][j] >> kBsTileLog], 1u);  // rank inside the tile's run
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // run starts: exclusive scan over the tiles (one counter per thread), the table row, and
+    // cnt back to zero for the next region once every edge has read its start
+    uint32_t total = 0;
+    const uint32_t c = tid < ntiles ? cnt[tid] : 0u;
+    const uint32_t st0 = block_exscan<kBsEmitThreads>(c, stg, &total);  // (stg as scratch: not yet in use)
+    uint16_t* row = f.btab + (size_t)r * (ntiles + 1);
+    if (tid < ntiles) {
+      row[tid] = (uint16_t)st0;
+      cnt[tid] = st0;
+    }
+    if (tid == 0) row[ntiles] = (uint16_t)total;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const uint32_t nl = u * kBsEmitThreads + tid;
+#pragma unroll
+      for (uint32_t j = 0; j < KM; ++j)
+        if ((live[u] >> j) & 1u) {
+          const uint32_t p = pp[u][j];
+          stg[cnt[p >> kBsTileLog] + rk[u][j]] =
+              (p & ((1u << kBsTileLog) - 1u)) | (uint32_t)rn[u] << kBsTileLog | nl << (kBsTileLog + 1);
+        }
+    }
+    __syncthreads();
+    uint32_t* out = f.brec + (size_t)r * rcap;
+    for (uint32_t i = tid; i < total; i += kBsEmitThreads) out[i] = stg[i];
+    for (uint32_t i = tid; i < ntiles; i += kBsEmitThreads) cnt[i] = 0;
+  }
+}
+
+// (k <= 2 without faults: 8 waves per SIMD, two blocks per CU overlap one region's Philox with
+// another's stores; the other instances would spill at 64 VGPRs)
+template <int MODE, bool FAULTS, int KM>
+__global__ __launch_bounds__(kBsEmitThreads, (KM == 2 && !FAULTS) ? 8 : 4) void frontier_bs_emit_kernel(FrontierBufs f, uint64_t N, uint32_t R,
+                                                                         uint32_t k, uint32_t t, uint32_t key0,
+                                                                         uint32_t key1, const uint64_t* partial,
+                                                                         uint32_t maj, Faults fa) {
+  __shared__ uint32_t cnt[kBsMaxTiles];
+  __shared__ uint32_t stg[4u << kBsRegLog];
+  if (rare_count(partial, N, R, maj) == 0) return;
+  if (maj)
+    bs_emit_body<1, MODE, FAULTS, KM>(cnt, stg, f, N, k, t, key0, key1, fa);
+  else
+    bs_emit_body<0, MODE, FAULTS, KM>(cnt, stg, f, N, k, t, key0, key1, fa);
+}
+
+// a queued edge of K1b: x = n | rare(n) << 31, y = p | rare(p) << 31 (N <= 2^31: bs_path_ok)
+template <int MAJ, int MODE>
+__device__ __forceinline__ void bs_flush(const uint2* qw, uint32_t nf, const FrontierBufs& f,
+                                         const uint64_t* __restrict__ S, uint64_t* Sw, uint64_t maj, bool mark_d,
+                                         bool direct, uint32_t lane) {
+  constexpr bool kPush = (MODE & 1) != 0, kPull = (MODE & 2) != 0;
+  constexpr int kE = kQFlush / 64;
+  uint32_t n[kE], p[kE];
+  bool rn[kE], hit[kE];
+#pragma unroll
+  for (int e = 0; e < kE; ++e) {
+    const uint32_t i = lane + 64u * e;
+    const uint2 q = i < nf ? qw[i] : uint2{0u, 0u};
+    n[e] = q.x & 0x7FFFFFFFu;
+    rn[e] = q.x >> 31;
+    p[e] = q.y & 0x7FFFFFFFu;
+    hit[e] = q.y >> 31;
+  }
+  uint64_t x[kE], vp[kE];
+#pragma unroll
+  for (int e = 0; e < kE; ++e) {
+    x[e] = rn[e] ? scan_ld(&S[n[e]]) : maj;
+    vp[e] = hit[e] ? scan_ld(&S[p[e]]) : maj;
+  }
+#pragma unroll
+  for (int e = 0; e < kE; ++e) {
+    const bool any = rn[e] || hit[e];  // (an empty slot: neither)
+    const uint64_t dpush = kPush && any ? x[e] & ~vp[e] : 0ull;
+    const uint64_t dpull = kPull && any ? vp[e] & ~x[e] : 0ull;
+    if (dpush) {
+      if (MAJ == 0 && direct && !hit[e]) {
+        atomicOr((unsigned long long*)&Sw[p[e]], (unsigned long long)dpush);
+      } else {
+        atomicOr((unsigned long long*)&f.D[p[e]], (unsigned long long)dpush);
+        if (mark_d) f.dirtyD[p[e] >> 6] = 1;
+      }
+    }
+    if (dpull) {
+      if (MAJ == 0 && direct && !rn[e]) {
+        atomicOr((unsigned long long*)&Sw[n[e]], (unsigned long long)dpull);
+      } else {
+        atomicOr((unsigned long long*)&f.D[n[e]], (unsigned long long)dpull);
+        if (mark_d) f.dirtyD[n[e] >> 6] = 1;
+      }
+    }
+  }
+}
+
+// K1b: block = (peer tile T, region chunk).  A wave takes 64 regions at a time (lane = region),
+// compacts their nonempty runs of tile T and walks the concatenation lane-strided, 64 records
+// per window: the run of record i0 + lane is found from the wave-uniform run starts by
+// readlane (a window spans ~3 of the ~32-record runs).
+template <int MAJ, int MODE>
+__device__ __forceinline__ void bs_test_body(uint64_t* bm, uint2* qs, uint64_t* wbs, uint32_t* rtab, const FrontierBufs& f,
+                                             const uint64_t* __restrict__ S, uint64_t* Sw, uint64_t N, uint32_t R,
+                                             uint32_t k, bool mark_d, bool direct) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t ntiles = f.btiles, nreg = f.bregions, rcap = k << kBsRegLog;
+  const uint32_t T = blockIdx.x % ntiles, chunk = blockIdx.x / ntiles, nch = gridDim.x / ntiles;
+  const uint32_t per = (nreg + nch - 1) / nch, r0 = chunk * per, r1 = min(r0 + per, nreg);
+  const uint64_t maj = MAJ ? full_mask1(R) : 0ull, nwords = (N + 63) >> 6, w0 = (uint64_t)T * kBsTileWords;
+  for (uint32_t i = tid; i < kBsTileWords; i += kBsTestThreads)
+    bm[i] = w0 + i < nwords ? rare_word<MAJ>(f, w0 + i, N) : 0ull;
+  __syncthreads();
+  uint2* qw = qs + wave * kQCap;
+  uint64_t* wb = wbs + wave * 16;
+  uint32_t* rbase = rtab + wave * 128;
+  uint32_t* rreg = rbase + 64;
+  uint32_t qn = 0;
+  const uint32_t pbase = T << kBsTileLog;
+  for (uint32_t rb = r0 + wave * 64; rb < r1; rb += (kBsTestThreads / 64) * 64) {
+    const uint32_t r = rb + lane;
+    uint32_t s = 0, len = 0;
+    if (r < r1) {
+      const uint16_t* row = f.btab + (size_t)r * (ntiles + 1);
+      s = row[T];
+      len = (uint32_t)row[T + 1] - s;
+    }
+    // compact the nonempty runs to the low lanes (their order kept), then exclusive starts E
+    const uint64_t ne = __ballot(len != 0);
+    const uint32_t m = (uint32_t)__popcll(ne);
+    const uint32_t dstl = __builtin_amdgcn_mbcnt_hi((uint32_t)(ne >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ne, 0u));
+    // ds_permute writes by destination lane: nonempty lanes to slots [0, m) in order, the
+    // empty ones behind them (a permutation: no two lanes share a slot)
+    const uint32_t dst = len ? dstl : m + (lane - dstl);
+    const uint32_t cr = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst * 4), (int)r);
+    const uint32_t cs = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst * 4), (int)s);
+    const uint32_t cl = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst * 4), (int)len);
+    const uint32_t rl = lane < m ? cl : 0u;
+    uint32_t inc = rl;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o, 64);
+      if (lane >= (uint32_t)o) inc += y;
+    }
+    const uint32_t E = inc - rl;                                  // start of compacted run `lane`
+    const uint32_t total = __shfl(inc, 63, 64);
+    // per compacted run: its record-index base (region offset + run start - E, mod 2^32) and region
+    if (lane < m) {
+      rbase[lane] = cr * rcap + cs - E;
+      rreg[lane] = cr;
+    }
+    // windows of 1024 records: the run starts inside a window as a 16-word bitmap; in step s
+    // (records w + 64 s + lane) every lane reads word s, so a record's run is the count of
+    // starts before the window + the starts in words < s + popcount(word s up to its lane) - 1:
+    // no search and no dependence between steps
+    for (uint32_t w = 0; w < total; w += 1024) {
+      if (lane < 16) wb[lane] = 0ull;
+      __builtin_amdgcn_wave_barrier();
+      if (lane < m && E >= w && E < w + 1024) atomicOr((unsigned long long*)&wb[(E - w) >> 6], 1ull << ((E - w) & 63u));
+      __builtin_amdgcn_wave_barrier();
+      const uint64_t myw = lane < 16 ? wb[lane] : 0ull;
+      uint32_t cu = (uint32_t)__popcll(myw);
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        const uint32_t y = __shfl_up(cu, o, 64);
+        if (lane >= (uint32_t)o) cu += y;
+      }
+      cu -= (uint32_t)__popcll(myw);  // starts in the words before this lane's
+      const uint32_t before = (uint32_t)__popcll(__ballot(lane < m && E < w));
+      const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+      const uint32_t nsteps = min(16u, (total - w + 63) >> 6);
+      for (uint32_t s0 = 0; s0 < nsteps; s0 += kBsUnroll) {
+      uint32_t rec[kBsUnroll], rrs[kBsUnroll];
+#pragma unroll
+      for (int u = 0; u < kBsUnroll; ++u) {
+        const uint32_t st = min(s0 + u, 15u), i = w + 64u * (s0 + u) + lane;
+        const uint64_t word = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(myw >> 32), (int)st) << 32) |
+                              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)myw, (int)st);
+        const uint32_t cus = (uint32_t)__builtin_amdgcn_readlane((int)cu, (int)st);
+        const bool valid = s0 + u < nsteps && i < total;
+        const uint32_t run = valid ? before + cus + (uint32_t)__popcll(word & upto) - 1u : 0u;
+        rrs[u] = rreg[run];
+        rec[u] = valid ? f.brec[rbase[run] + i] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < kBsUnroll; ++u) {
+        const uint32_t pl = rec[u] & ((1u << kBsTileLog) - 1u);
+        const bool valid = s0 + u < nsteps && w + 64u * (s0 + u) + lane < total;
+        const bool rnb = valid && ((rec[u] >> kBsTileLog) & 1u);
+        const bool hit = valid && ((bm[pl >> 6] >> (pl & 63u)) & 1ull);
+        const bool c = rnb || hit;
+        const uint64_t mk = __ballot(c);
+        if (!mk) continue;
+        if (c) {
+          const uint32_t pos =
+              qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+          const uint32_t n = (rrs[u] << kBsRegLog) + (rec[u] >> (kBsTileLog + 1));
+          qw[pos] = uint2{n | (uint32_t)rnb << 31, (pbase + pl) | (uint32_t)hit << 31};
+        }
+        qn += (uint32_t)__popcll(mk);
+        if (qn >= kQFlush) {
+          __builtin_amdgcn_wave_barrier();
+          bs_flush<MAJ, MODE>(qw, kQFlush, f, S, Sw, maj, mark_d, direct, lane);
+          qn -= kQFlush;
+          const uint2 rest = lane < qn ? qw[kQFlush + lane] : uint2{0u, 0u};
+          __builtin_amdgcn_wave_barrier();
+          if (lane < qn) qw[lane] = rest;
+          __builtin_amdgcn_wave_barrier();
+        }
+      }
+      }
+    }
+  }
+  if (qn) {
+    __builtin_amdgcn_wave_barrier();
+    bs_flush<MAJ, MODE>(qw, qn, f, S, Sw, maj, mark_d, direct, lane);
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kBsTestThreads) void frontier_bs_test_kernel(FrontierBufs f, uint64_t* S, uint64_t N,
+                                                                         uint32_t R, uint32_t k,
+                                                                         const uint64_t* partial, uint32_t maj,
+                                                                         uint32_t mark_d, uint32_t direct) {
+  __shared__ uint64_t bm[kBsTileWords];
+  __shared__ uint2 qs[(kBsTestThreads / 64) * kQCap];
+  __shared__ uint64_t wbs[(kBsTestThreads / 64) * 16];
+  __shared__ uint32_t rtab[(kBsTestThreads / 64) * 128];
+  if (rare_count(partial, N, R, maj) == 0) return;
+  if (maj)
+    bs_test_body<1, MODE>(bm, qs, wbs, rtab, f, S, S, N, R, k, mark_d != 0, false);
+  else
+    bs_test_body<0, MODE>(bm, qs, wbs, rtab, f, S, S, N, R, k, mark_d != 0, direct != 0);
+}
+
 template <int MODE, bool FAULTS>
 __global__ __launch_bounds__(kScanThreads, kScanWaves) void frontier_scan_kernel(FrontierBufs f, uint64_t* S,
                                                                       uint64_t N, uint32_t R, uint32_t k, uint32_t t,
@@ -761,6 +1062,12 @@ uint32_t frontier_summ2_words(uint64_t N) {
   return (uint32_t)((((N + (1ull << frontier_g2log(N)) - 1) >> frontier_g2log(N)) + 31) / 32);
 }
 
+bool bs_path_ok(uint64_t N, uint32_t k) { return N > 0 && k >= 1 && k <= 4 && N <= ((uint64_t)kBsMaxTiles << kBsTileLog); }
+uint32_t bs_tiles(uint64_t N) { return (uint32_t)((N + (1ull << kBsTileLog) - 1) >> kBsTileLog); }
+uint32_t bs_regions(uint64_t N) { return (uint32_t)((N + (1ull << kBsRegLog) - 1) >> kBsRegLog); }
+size_t bs_rec_bytes(uint64_t N, uint32_t k) { return (size_t)bs_regions(N) * ((size_t)k << kBsRegLog) * 4; }
+size_t bs_tab_bytes(uint64_t N) { return (size_t)bs_regions(N) * (bs_tiles(N) + 1) * 2; }
+
 size_t frontier_bytes(uint64_t N) {
   const size_t nwords = (N + 63) / 64;
   const uint32_t glog = frontier_glog(N);
@@ -829,6 +1136,27 @@ hipError_t launch_frontier_round(const FrontierBufs& f, uint64_t* S, uint64_t N,
                                  hipStream_t st) {
   if (N == 0) return hipSuccess;  // a shard without nodes
   if (maj != 0 && dmode == kSparseDirect) dmode = kSparseAllD;  // (a full peer takes no push)
+  const bool faults = fa.any();
+  if (f.brec && f.btab && bs_path_ok(N, k)) {  // the binned sparse scan (K1a + K1b)
+    const uint32_t nch = std::max(1u, std::min(f.bregions, kBsTestBlocks / f.btiles));
+    const uint32_t egrid = std::min(f.bregions, kBsEmitGrid);
+#define GOSSIP_BS(MODE, FAULTS)                                                                                 \
+  if (k <= 2)                                                                                                    \
+    frontier_bs_emit_kernel<MODE, FAULTS, 2><<<egrid, kBsEmitThreads, 0, st>>>(f, N, R, k, t, key0, key1, partial, maj, \
+                                                                              fa);                              \
+  else                                                                                                          \
+    frontier_bs_emit_kernel<MODE, FAULTS, 4><<<egrid, kBsEmitThreads, 0, st>>>(f, N, R, k, t, key0, key1, partial, maj, \
+                                                                              fa);                              \
+  frontier_bs_test_kernel<MODE><<<f.btiles * nch, kBsTestThreads, 0, st>>>(f, S, N, R, k, partial, maj,          \
+                                                                          dmode != kSparseAllD, dmode == kSparseDirect)
+    switch (mode) {
+      case 1: if (faults) { GOSSIP_BS(1, true); } else { GOSSIP_BS(1, false); } break;
+      case 2: if (faults) { GOSSIP_BS(2, true); } else { GOSSIP_BS(2, false); } break;
+      case 3: if (faults) { GOSSIP_BS(3, true); } else { GOSSIP_BS(3, false); } break;
+      default: return hipErrorInvalidValue;
+    }
+#undef GOSSIP_BS
+  } else {
   frontier_summary_kernel<<<(f.summ_words + 255) / 256 + (f.summ2_words + 255) / 256, 256, 0, st>>>(f, N, partial, R,
                                                                                                    maj);
   const uint64_t chunks = (N + kScanThreads - 1) / kScanThreads;
@@ -838,7 +1166,6 @@ hipError_t launch_frontier_round(const FrontierBufs& f, uint64_t* S, uint64_t N,
 #define GOSSIP_SCAN(MODE, FAULTS)                                                                           \
   frontier_scan_kernel<MODE, FAULTS><<<grid, kScanThreads, 0, st>>>(f, S, N, R, k, t, key0, key1, per, partial, \
                                                                     maj, dmode != kSparseAllD, dmode == kSparseDirect, fa)
-  const bool faults = fa.any();
   switch (mode) {
     case 1: if (faults) GOSSIP_SCAN(1, true); else GOSSIP_SCAN(1, false); break;
     case 2: if (faults) GOSSIP_SCAN(2, true); else GOSSIP_SCAN(2, false); break;
@@ -846,6 +1173,7 @@ hipError_t launch_frontier_round(const FrontierBufs& f, uint64_t* S, uint64_t N,
     default: return hipErrorInvalidValue;
   }
 #undef GOSSIP_SCAN
+  }
   // absolute totals: after the scan (it reads the rare count), before the commit adds to them
   if (dmode == kSparseDirect) {
     const hipError_t me = hipMemsetAsync(partial, 0, (size_t)rs.plen * 8, st);

@@ -159,6 +159,9 @@ int gossip_set_stream(gossip_engine_t* eng, void* hip_stream);
  *                  into the state (default 1; 0: into D)
  *   "mid_frac"     past 2^25 nodes sparse rounds test a peer in the mid-level summary once this
  *                  share of peers would hit the LDS summary (default 0.5)
+ *   "bin_scan_frac"  sparse rounds bin their edges by peer tile and test the peers from an LDS
+ *                  copy of the rare bitmap once this share of peers would hit the LDS summary
+ *                  (default 0.6; 0: every sparse round of an engine with the dense pipeline; > 1 never)
  *   "scan_queue"   sparse rounds resolve the edges with a possibly rare end from a per-wave queue
  *                  (default 1; 0: where they are drawn)
  *   "filter_frac"  dense rounds drop edges by the peer's class above this empty/full fraction

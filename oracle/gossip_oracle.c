@@ -1308,10 +1308,9 @@ int oracle_set_param(oracle_sim_t* s, const char* name, double value) {
     return GOSSIP_OK;
   }
   /* the engine's performance knobs (path choice, grids): no effect on the rounds' results */
-  const char* known[] = {"alld_frac",  "filter_frac", "ahead",        "serve_grid",   "apply_grid", "push_waves",
-                         "ae_sparse",  "ae_cap",      "sparse_direct", "mid_frac",    "ae_dense_bin", "ae_dense_cap",
-                         "ae_ahead",   "ordered_collectives", "ae_dense_filter", "rccl_dev_collectives", "serve_lr", "tile_queues",
-                         "scan_queue", "place_tries", "timing"};
+  const char* known[] = {"alld_frac",  "filter_frac", "ahead",        "ae_sparse",  "ae_cap",      "sparse_direct",
+                         "mid_frac",   "bin_scan_frac", "ae_dense_bin", "ae_dense_cap", "ae_ahead", "ordered_collectives",
+                         "ae_dense_filter", "rccl_dev_collectives", "scan_queue", "place_tries", "timing"};
   for (size_t i = 0; i < sizeof known / sizeof known[0]; ++i)
     if (!strcmp(name, known[i])) return GOSSIP_OK;
   return GOSSIP_EINVAL;

@@ -104,13 +104,13 @@ def _header_knobs():
 
 
 def test_knob_list_is_pinned():
-    """gossip_set_param accepts exactly the knobs gossip.h documents: 7 operational ones and 14 that
+    """gossip_set_param accepts exactly the knobs gossip.h documents: 7 operational ones and 15 that
     force the parity tests' A/B paths (round 6 removed serve_lr, serve_grid, apply_grid, push_waves
-    and tile_queues)."""
+    and tile_queues, and added bin_scan_frac)."""
     ops, tests = _header_knobs()
     assert ops == {"timing", "place_tries", "ahead", "ae_ahead", "ordered_collectives", "link_gbps",
                    "rccl_dev_collectives"}
-    assert tests == {"sparse_frac", "alld_frac", "sparse_direct", "mid_frac", "scan_queue", "filter_frac",
+    assert tests == {"sparse_frac", "alld_frac", "sparse_direct", "mid_frac", "bin_scan_frac", "scan_queue", "filter_frac",
                      "xd_filter_frac", "xd_shards", "cc_frac", "ae_sparse", "ae_cap", "ae_dense_bin", "ae_dense_cap",
                      "ae_dense_filter"}
     src = open(os.path.join(ROOT, "gossip-protocol_amd", "csrc", "engine.hip")).read()

@@ -29,6 +29,10 @@ PATHS = {"auto": {}, "sparse_flags": {"sparse_frac": 1.0, "alld_frac": 1e30},
          "sparse_mid": {"sparse_frac": 1.0, "mid_frac": 0},
          # edges resolved where they are drawn (no per-wave queue; the default before round 5)
          "sparse_noq": {"sparse_frac": 1.0, "scan_queue": 0},
+         # every round on the binned scan (round 6), with the heavy rounds' direct commits and
+         # with dirty flags throughout
+         "sparse_bscan": {"sparse_frac": 1.0, "bin_scan_frac": 0},
+         "sparse_bscan_flags": {"sparse_frac": 1.0, "bin_scan_frac": 0, "alld_frac": 1e30},
          # every round on the dense pipeline (16384-sender regions, packed pushes)
          "dense": {"sparse_frac": -1.0}}
 CASES = {"pushpull-k2-R64": ("pushpull", 2, 64, 0x5EED0003, 0), "push-k3-R5": ("push", 3, 5, 77, 0),

@@ -38,17 +38,21 @@ def test_device_philox_kat(golden):
 #   sparse_direct — every round sparse; with an empty majority the pushes into empty peers go
 #            straight into S and the commit recomputes the totals (the heavy-round default)
 #   sparse_noq — every round sparse, edges resolved where drawn (scan_queue 0: no per-wave queue)
+#   sparse_bscan — every round sparse on the binned scan (edges binned by peer tile, peers tested
+#            against an LDS copy of the rare bitmap; bin_scan_frac 0)
 #   dense_filter — every round dense, emit dropping edges by the peer's class (occupancy bitmaps)
 #   direct — the random-access kernels
-PATHS = ["auto", "dense", "dense_filter", "sparse", "sparse_alld", "sparse_direct", "sparse_noq", "direct"]
+PATHS = ["auto", "dense", "dense_filter", "sparse", "sparse_alld", "sparse_direct", "sparse_noq", "sparse_bscan",
+         "direct"]
 _PATH_FLAGS = {"auto": 0, "dense": FLAG_DENSE, "dense_filter": 0, "sparse": 0, "sparse_alld": 0, "sparse_direct": 0,
-               "sparse_noq": 0, "direct": FLAG_DIRECT}
+               "sparse_noq": 0, "sparse_bscan": 0, "direct": FLAG_DIRECT}
 # gossip_set_param knobs; alld_frac: 0 = every sparse round commits every group's D, huge = none does
 _PATH_PARAMS = {"dense_filter": {"sparse_frac": -1, "filter_frac": 0},
                 "sparse": {"sparse_frac": 1.0, "alld_frac": 1e30},
                 "sparse_alld": {"sparse_frac": 1.0, "alld_frac": 0, "sparse_direct": 0},
                 "sparse_direct": {"sparse_frac": 1.0, "alld_frac": 0, "sparse_direct": 1},
-                "sparse_noq": {"sparse_frac": 1.0, "scan_queue": 0}}
+                "sparse_noq": {"sparse_frac": 1.0, "scan_queue": 0},
+                "sparse_bscan": {"sparse_frac": 1.0, "bin_scan_frac": 0}}
 
 
 @pytest.fixture

@@ -3,7 +3,8 @@
 # history at 233a6c4).  Every step runs under its own time limit and the first failure ends the run.
 #   OUT    output directory under gpurun_out/ (default ab6)
 #   TESTS  pytest targets run first ("none": skip)
-#   VARS   library variants: default (the in-tree library) or X = exp/libX.so (tools/build_variants.sh)
+#   VARS   library variants: default (the in-tree library) or X = exp/libX.so (tools/build_variants.sh),
+#          or p:name=value[,name=value] = the in-tree library with those gossip_set_param knobs
 #   SIZES  node counts of the dense-round A/B (tools/exp_bench.py, every round as planned)
 #   STEPS  bench steps per variant and size (default 4; the first is untimed)
 #   KPROF  1: per-kernel rocprofv3 --stats of each variant and size (default 1)
@@ -73,6 +74,9 @@ if [ "${SKIP_AB:-0}" = 1 ]; then echo done; exit 0; fi
 for n in ${SIZES:-134217728}; do
   for X in ${VARS:-default}; do
     L=exp/lib$X.so; [ "$X" = default ] && L=""
+    XP=""
+    if [ "${X#p:}" != "$X" ]; then XP=${X#p:}; L=""; X=$(echo "$XP" | tr '=,' '__'); fi
+    export EXP_PARAMS=$XP
     D=$O/$X.$n
     GOSSIP_LIB=$L EXP_N=$n EXP_STEPS=${STEPS:-4} timeout -k 10 300 python -u tools/exp_bench.py > $D.txt 2>&1
     ok $? "bench $X $n"
@@ -90,7 +94,7 @@ for n in ${SIZES:-134217728}; do
       for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum" \
                  "TCC_HIT_sum TCC_MISS_sum TA_TA_BUSY_sum TD_TD_BUSY_sum"; do
         i=$((i+1))
-        GOSSIP_LIB=$L EXP_N=$n EXP_STEPS=2 EXP_PARAMS=place_tries=1 timeout -s KILL 120 rocprofv3 --pmc $grp \
+        GOSSIP_LIB=$L EXP_N=$n EXP_STEPS=2 EXP_PARAMS=place_tries=1${XP:+,$XP} timeout -s KILL 120 rocprofv3 --pmc $grp \
           --kernel-trace --output-format csv -d $D.pmc/p$i -o p -- python tools/exp_bench.py > $D.pmc.p$i.txt 2>&1
         ok $? "pmc pass $i $X $n"
       done

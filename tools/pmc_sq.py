@@ -13,7 +13,7 @@ import os
 import sys
 
 KEEP = ("bin_emit_kernel", "bin_emit_huge_kernel", "transpose_u16_kernel", "bin_serve_kernel", "bin_apply_kernel",
-        "frontier_scan_kernel", "frontier_commit_kernel")
+        "frontier_scan_kernel", "frontier_commit_kernel", "frontier_bs_emit_kernel", "frontier_bs_test_kernel")
 
 
 def kname(s):

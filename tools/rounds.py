@@ -11,8 +11,8 @@ path = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof/run_kernel_trace.c
 SHORT = {"bin_count_kernel": "count", "bin_emit_kernel": "emit", "bin_emit_huge_kernel": "emit", "transpose_u16_kernel": "u16", "transpose_u32_kernel": "u32", "bin_serve_kernel": "serve",
          "bin_apply_kernel": "apply", "frontier_summary_kernel": "summ", "frontier_scan_kernel": "scan", "frontier_scan_ns_kernel": "scan_ns",
          "frontier_rebuild_kernel": "rebuild", "frontier_commit_kernel": "commit", "frontier_inject_kernel": "inject", "round_snapshot_kernel": "snap",
-         "bs_emit_kernel": "bs_emit", "bs_test_kernel": "bs_test"}
-STARTS = ("summ", "emit", "rebuild")
+         "frontier_bs_emit_kernel": "bs_emit", "frontier_bs_test_kernel": "bs_test"}
+STARTS = ("summ", "emit", "rebuild", "bs_emit")
 
 
 def short(name):
@@ -44,6 +44,6 @@ tot = 0
 for r in rounds[cut:]:
     t = sum(d for _, _, d in r)
     tot += t
-    kind = "sparse" if any(n in ("scan", "scan_ns") for _, n, _ in r) else "dense "
+    kind = "sparse" if any(n in ("scan", "scan_ns", "bs_test") for _, n, _ in r) else "dense "
     print(kind, " ".join(f"{n}:{d:6.1f}" for _, n, d in r), f" round {t:6.1f} us")
 print(f"rounds {len(rounds) - cut}, kernel time {tot / 1000:.2f} ms")
