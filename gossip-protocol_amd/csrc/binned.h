@@ -84,6 +84,8 @@ struct BinBufs {
 };
 
 size_t bin_bytes(const BinGeom& g);
+// [rows][cols] u16 table -> [cols][rows] (64 x 64 LDS tiles)
+void bin_transpose_u16(const uint16_t* in, uint16_t* out, uint32_t rows, uint32_t cols, hipStream_t st);
 void bin_carve(const BinGeom& g, void* base, BinBufs* b);
 
 // One dense round, in place on S.  The totals in partial are cleared and

@@ -1128,6 +1128,11 @@ uint32_t apply_grid(const BinGeom& g) {
 
 }  // namespace
 
+// [rows][cols] u16 table -> [cols][rows] (the binned sparse scan's run table, frontier.hip)
+void bin_transpose_u16(const uint16_t* in, uint16_t* out, uint32_t rows, uint32_t cols, hipStream_t st) {
+  launch_transpose_u16(in, out, rows, cols, nullptr, 0u, st);
+}
+
 BinGeom make_bin_geom(uint64_t N, uint32_t k, bool big) {
   BinGeom g{};
   g.N = N;

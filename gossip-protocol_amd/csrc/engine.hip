@@ -759,6 +759,11 @@ bool bscan_round(const gossip_engine* e, const Est& x, uint32_t maj) {
   if (!e->binned || !e->frontier || !bs_path_ok(e->N, e->k) || e->bscan_frac > 1.0) return false;
   const size_t recs = (size_t)e->bg.nt_s * e->bg.rp;
   if (bs_rec_bytes(e->N, e->k) > recs * 8 || bs_tab_bytes(e->N) > recs * 8) return false;
+  if (e->bscan_frac <= 0.0) return true;
+  // by default only where the LDS summary is coarse (g >= 64 nodes per bit: past 2^25 nodes, where
+  // the mid-level summary exists); at 2^24 the one heavy sparse round it took ran 590 us and the
+  // step's sparse rounds 1.10 -> 1.44 ms (K1b has too few regions per tile to fill its waves)
+  if (!e->fb.summ2) return false;
   const double N = (double)e->N, rare = maj ? N - x.full : x.nz;
   const double g = (double)(1u << e->fb.glog);
   return 1.0 - std::pow(1.0 - std::min(std::max(rare / N, 0.0), 1.0), g) >= e->bscan_frac;
@@ -826,6 +831,7 @@ int launch_round_path(gossip_engine* e, uint32_t t, bool sparse, uint32_t maj, b
     fb.btab = (uint16_t*)(e->bb.prec ? (void*)e->bb.prec : (void*)e->bb.vals);
     fb.btiles = bs_tiles(e->N);
     fb.bregions = bs_regions(e->N);
+    fb.btabT = fb.btab + bs_tab_bytes(e->N) / 4;  // (the second half of bs_tab_bytes)
   }
   if (sparse)
     HIP_OK(e, launch_frontier_round(fb, e->S, e->N, e->partial_d, e->R, e->k, t, e->key0, e->key1, e->mode, maj,

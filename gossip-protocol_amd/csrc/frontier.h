@@ -43,9 +43,10 @@ struct FrontierBufs {
   uint32_t scan_q;
   // round 6, binned sparse scan (frontier.hip K1a / K1b): set per round by the engine when the
   // round takes it (null: the LDS-summary scan).  brec: [bregions][k * 4096] u32 records,
-  // btab: [bregions][btiles + 1] u16 run starts; both carved from the dense round's record slab.
+  // btab: [bregions][btiles + 1] u16 run starts (+ btabT); all carved from the dense round's record slab.
   uint32_t* brec;
   uint16_t* btab;
+  uint16_t* btabT;   // [btiles + 1][bregions]: btab transposed (K1b reads a tile's column contiguously)
   uint32_t btiles, bregions;
   uint64_t id0;      // global id of node 0 of these arrays (a shard's first node; 0 on one GPU): the hash uses global ids
 };

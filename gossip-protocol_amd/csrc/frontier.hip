@@ -26,6 +26,7 @@
 // dense round bit for bit.  K2 in rebuild mode computes absolute stats and
 // both bitmaps from S (after inject/reset or a direct-path round).
 #include "frontier.h"
+#include "binned.h"
 
 #include <algorithm>
 #include "philox.h"
@@ -531,7 +532,13 @@ __device__ __forceinline__ void scan_body_q(uint4* summ4, uint64_t* rws, uint2* 
 // resolves the edges with a rare end through the per-wave queue of the queued scan (S_t gathers
 // and atomics).  Traffic: 8 B per node written and read (k = 2) instead of the probes.
 constexpr uint32_t kBsRegLog = 12;                 // 4096 senders per region (n - region base: 12 bits)
-constexpr uint32_t kBsTileLog = 19;                // 2^19 peers per tile (p - tile base: 19 bits; 64 KiB bitmap)
+#ifndef GOSSIP_BS_TILE_LOG
+#define GOSSIP_BS_TILE_LOG 19
+#endif
+#ifndef GOSSIP_BS_TEST_WAVES
+#define GOSSIP_BS_TEST_WAVES 4
+#endif
+constexpr uint32_t kBsTileLog = GOSSIP_BS_TILE_LOG;  // 2^19 peers per tile (p - tile base: 19 bits; 64 KiB bitmap)
 constexpr uint32_t kBsTileWords = 1u << (kBsTileLog - 6);
 constexpr int kBsEmitThreads = 1024;               // 4 senders per thread and region
 constexpr int kBsTestThreads = 1024;
@@ -689,7 +696,16 @@ __device__ __forceinline__ void bs_test_body(uint64_t* bm, uint2* qs, uint64_t* 
                                              uint32_t k, bool mark_d, bool direct) {
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t ntiles = f.btiles, nreg = f.bregions, rcap = k << kBsRegLog;
-  const uint32_t T = blockIdx.x % ntiles, chunk = blockIdx.x / ntiles, nch = gridDim.x / ntiles;
+  // XCD-aware: blocks b, b + 8, ... share an XCD (and its L2); give them adjacent tiles of one
+  // region chunk, so that the runs of neighbouring tiles (adjacent in each region's list) share
+  // their boundary lines in that L2 instead of fetching them twice
+  const uint32_t nch = gridDim.x / ntiles;
+  uint32_t T = blockIdx.x % ntiles, chunk = blockIdx.x / ntiles;
+  if (ntiles % 8 == 0) {
+    const uint32_t per_x = ntiles / 8, j = blockIdx.x / 8;
+    T = (blockIdx.x % 8) * per_x + j % per_x;
+    chunk = j / per_x;
+  }
   const uint32_t per = (nreg + nch - 1) / nch, r0 = chunk * per, r1 = min(r0 + per, nreg);
   const uint64_t maj = MAJ ? full_mask1(R) : 0ull, nwords = (N + 63) >> 6, w0 = (uint64_t)T * kBsTileWords;
   for (uint32_t i = tid; i < kBsTileWords; i += kBsTestThreads)
@@ -704,10 +720,9 @@ __device__ __forceinline__ void bs_test_body(uint64_t* bm, uint2* qs, uint64_t* 
   for (uint32_t rb = r0 + wave * 64; rb < r1; rb += (kBsTestThreads / 64) * 64) {
     const uint32_t r = rb + lane;
     uint32_t s = 0, len = 0;
-    if (r < r1) {
-      const uint16_t* row = f.btab + (size_t)r * (ntiles + 1);
-      s = row[T];
-      len = (uint32_t)row[T + 1] - s;
+    if (r < r1) {  // (the transposed table: a wave reads two runs of 64 consecutive u16)
+      s = f.btabT[(size_t)T * nreg + r];
+      len = (uint32_t)f.btabT[(size_t)(T + 1) * nreg + r] - s;
     }
     // compact the nonempty runs to the low lanes (their order kept), then exclusive starts E
     const uint64_t ne = __ballot(len != 0);
@@ -802,7 +817,7 @@ __device__ __forceinline__ void bs_test_body(uint64_t* bm, uint2* qs, uint64_t* 
 }
 
 template <int MODE>
-__global__ __launch_bounds__(kBsTestThreads) void frontier_bs_test_kernel(FrontierBufs f, uint64_t* S, uint64_t N,
+__global__ __launch_bounds__(kBsTestThreads, GOSSIP_BS_TEST_WAVES) void frontier_bs_test_kernel(FrontierBufs f, uint64_t* S, uint64_t N,
                                                                          uint32_t R, uint32_t k,
                                                                          const uint64_t* partial, uint32_t maj,
                                                                          uint32_t mark_d, uint32_t direct) {
@@ -1066,7 +1081,7 @@ bool bs_path_ok(uint64_t N, uint32_t k) { return N > 0 && k >= 1 && k <= 4 && N 
 uint32_t bs_tiles(uint64_t N) { return (uint32_t)((N + (1ull << kBsTileLog) - 1) >> kBsTileLog); }
 uint32_t bs_regions(uint64_t N) { return (uint32_t)((N + (1ull << kBsRegLog) - 1) >> kBsRegLog); }
 size_t bs_rec_bytes(uint64_t N, uint32_t k) { return (size_t)bs_regions(N) * ((size_t)k << kBsRegLog) * 4; }
-size_t bs_tab_bytes(uint64_t N) { return (size_t)bs_regions(N) * (bs_tiles(N) + 1) * 2; }
+size_t bs_tab_bytes(uint64_t N) { return 2 * (((size_t)bs_regions(N) * (bs_tiles(N) + 1) * 2 + 255) & ~(size_t)255); }
 
 size_t frontier_bytes(uint64_t N) {
   const size_t nwords = (N + 63) / 64;
@@ -1147,6 +1162,7 @@ hipError_t launch_frontier_round(const FrontierBufs& f, uint64_t* S, uint64_t N,
   else                                                                                                          \
     frontier_bs_emit_kernel<MODE, FAULTS, 4><<<egrid, kBsEmitThreads, 0, st>>>(f, N, R, k, t, key0, key1, partial, maj, \
                                                                               fa);                              \
+  bin_transpose_u16(f.btab, f.btabT, f.bregions, f.btiles + 1, st);                                            \
   frontier_bs_test_kernel<MODE><<<f.btiles * nch, kBsTestThreads, 0, st>>>(f, S, N, R, k, partial, maj,          \
                                                                           dmode != kSparseAllD, dmode == kSparseDirect)
     switch (mode) {

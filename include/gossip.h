@@ -161,7 +161,8 @@ int gossip_set_stream(gossip_engine_t* eng, void* hip_stream);
  *                  share of peers would hit the LDS summary (default 0.5)
  *   "bin_scan_frac"  sparse rounds bin their edges by peer tile and test the peers from an LDS
  *                  copy of the rare bitmap once this share of peers would hit the LDS summary
- *                  (default 0.6; 0: every sparse round of an engine with the dense pipeline; > 1 never)
+ *                  (default 0.6, past 2^25 nodes; 0: every sparse round of an engine with the dense
+ *                  pipeline, at any size; > 1 never)
  *   "scan_queue"   sparse rounds resolve the edges with a possibly rare end from a per-wave queue
  *                  (default 1; 0: where they are drawn)
  *   "filter_frac"  dense rounds drop edges by the peer's class above this empty/full fraction
