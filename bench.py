@@ -22,6 +22,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -393,8 +394,12 @@ def main():
         seed = args.seed
     else:
         seed = SEED_TOTAL if n_total >= NODES_TOTAL or world > 1 else SEED_SECONDARY
+    mem_free0 = torch.cuda.mem_get_info()[0] if world == 1 else None
+    t_create = time.perf_counter()
     eng = Engine(n_total, RUMORS, MODE, FANOUT, seed, flags=FLAG_TIMING, device=local,
                  shard_rank=rank, shard_count=world, params=dict(ENGINE_PARAMS))
+    create_ms = (time.perf_counter() - t_create) * 1e3
+    mem_free1 = torch.cuda.mem_get_info()[0] if world == 1 else None
     driver = (args.driver or "torch") if world > 1 else "engine"
     driver_note = None
     if world > 1 and driver == "engine" and args.backend == "gloo":
@@ -436,8 +441,25 @@ def main():
 
     warm_check = None
     engine_driver_verified = None  # N > 1, --driver engine: did the library-driven run match the fixture?
+    first_step = None  # one GPU: wall time and least free device memory of the first step (its placement trials)
     for i in range(args.warmup):
-        st = one_step()
+        if i == 0 and world == 1:
+            low, stop = [mem_free1], threading.Event()
+
+            def sample():
+                while not stop.is_set():
+                    low[0] = min(low[0], torch.cuda.mem_get_info()[0])
+                    time.sleep(0.002)
+            th = threading.Thread(target=sample)
+            th.start()
+            t_first = time.perf_counter()
+            st = one_step()
+            first_ms = (time.perf_counter() - t_first) * 1e3
+            stop.set()
+            th.join()
+            first_step = (first_ms, mem_free1 - low[0])
+        else:
+            st = one_step()
         if i == 0 and fx is not None:  # before the timed steps: a wrong result is caught, not timed
             warm_check = verify(st)
             if world > 1 and driver == "engine":
@@ -484,6 +506,14 @@ def main():
         rl["placement_trials"] = {"rounds": placement[1], "ms": placement[0],
                                   "note": "dense trial rounds on fresh allocations of the record slab before the "
                                           "first round (param place_tries), in the warm-up: not in the timed steps"}
+        if first_step is not None:
+            rl["engine_setup"] = {
+                "create_ms": round(create_ms, 1), "device_bytes_after_create": int(mem_free0 - mem_free1),
+                "first_step_ms": round(first_step[0], 1), "timed_step_ms": round(dt / max(args.steps, 1) * 1e3, 2),
+                "peak_extra_device_bytes_first_step": int(first_step[1]),
+                "note": "gossip_create wall time and the device memory it took; the first step's wall time and the "
+                        "most device memory it held beyond that (torch.cuda.mem_get_info sampled every 2 ms): the "
+                        "placement trials hold at most two candidate record slabs (DESIGN.md §3.7)"}
     else:
         rl = sharded_roofline(eng, driver, trace, bpn * nown, world, args.backend, args.steps)
     eng.close()

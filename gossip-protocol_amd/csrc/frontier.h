@@ -16,7 +16,10 @@
 
 namespace gossip {
 
-constexpr uint32_t kSummBits = 1u << 20;  // LDS summary: at most 2^20 bits (128 KiB; 2^19 / 2^18 slower, §3.7)
+#ifndef GOSSIP_SUMM_LOG
+#define GOSSIP_SUMM_LOG 20
+#endif
+constexpr uint32_t kSummBits = 1u << GOSSIP_SUMM_LOG;  // LDS summary: at most 2^20 bits (128 KiB; 2^19 / 2^18 slower, §3.7)
 
 struct FrontierBufs {
   uint64_t* nzb;      // [ceil(N/64)] bit n: S[n] != 0

@@ -43,8 +43,11 @@ template <typename T>
 __device__ __forceinline__ T scan_ld(const T* p) {
   return *p;
 }
-constexpr uint32_t kScanGrid = 256;  // one block per CU: the summary takes 128 KiB of LDS
-constexpr uint32_t kScanWaves = 4;   // waves per SIMD (launch bounds)
+#ifndef GOSSIP_SCAN_BPC
+#define GOSSIP_SCAN_BPC 1
+#endif
+constexpr uint32_t kScanGrid = 256 * GOSSIP_SCAN_BPC;  // one block per CU: the summary takes 128 KiB of LDS
+constexpr uint32_t kScanWaves = 4 * GOSSIP_SCAN_BPC;   // waves per SIMD (launch bounds)
 // commit / rebuild blocks of 1024 threads, at most kCommitMaxBlocks of them: each block ends in
 // ~67 same-address atomics on the totals, which cost more than the waves gain past ~512 blocks
 // (2^24 sparse rounds 132 -> 125 us against 256-thread blocks up to 4096; profiles/r05_cc2/)
