@@ -1,7 +1,8 @@
 #!/bin/bash
 # SQ / TCP / TCC / TA counters per kernel (launch averages, tools/pmc_sq.py) of tools/exp_bench.py on
 # the bench workload, one rocprofv3 --pmc pass per counter group.  OUT: directory under gpurun_out/;
-# EXP_N / EXP_SEED / EXP_PARAMS as exp_bench.py.
+# EXP_N / EXP_SEED / EXP_PARAMS as exp_bench.py; PMC_CMD: another program to profile (default the bench
+# workload through tools/exp_bench.py), PMC_NODES: the node count per-node figures divide by.
 set -u
 O=gpurun_out/${OUT:-pmck}
 mkdir -p $O
@@ -13,7 +14,7 @@ for grp in "SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_L
            "TCC_HIT_sum TCC_MISS_sum TA_TA_BUSY_sum TD_TD_BUSY_sum"; do
   i=$((i+1))
   EXP_STEPS=2 timeout -s KILL 150 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d $O/p$i -o p \
-    -- python tools/exp_bench.py > $O/p$i.txt 2>&1
+    -- ${PMC_CMD:-python tools/exp_bench.py} > $O/p$i.txt 2>&1
   rc=$?; if [ $rc -ne 0 ]; then echo "STOP: pass $i exited $rc"; tail -3 $O/p$i.txt; exit $rc; fi
 done
-PMC_NODES=${EXP_N:-16777216} python tools/pmc_sq.py $O $O/pmc_k.json > /dev/null && echo pmc ok
+PMC_NODES=${PMC_NODES:-${EXP_N:-16777216}} python tools/pmc_sq.py $O $O/pmc_k.json > /dev/null && echo pmc ok

@@ -13,7 +13,8 @@ import os
 import sys
 
 KEEP = ("bin_emit_kernel", "bin_emit_huge_kernel", "transpose_u16_kernel", "bin_serve_kernel", "bin_apply_kernel",
-        "frontier_scan_kernel", "frontier_commit_kernel", "frontier_bs_emit_kernel", "frontier_bs_test_kernel")
+        "frontier_scan_kernel", "frontier_commit_kernel", "frontier_bs_emit_kernel", "frontier_bs_test_kernel",
+        "xd_count_kernel", "xd_emit_kernel", "xd_bin_kernel", "xd_unperm_kernel", "xd_apply_kernel", "sx_scan_kernel")
 
 
 def kname(s):
