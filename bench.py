@@ -22,7 +22,6 @@ import argparse
 import json
 import os
 import sys
-import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -444,20 +443,11 @@ def main():
     first_step = None  # one GPU: wall time and least free device memory of the first step (its placement trials)
     for i in range(args.warmup):
         if i == 0 and world == 1:
-            low, stop = [mem_free1], threading.Event()
-
-            def sample():
-                while not stop.is_set():
-                    low[0] = min(low[0], torch.cuda.mem_get_info()[0])
-                    time.sleep(0.002)
-            th = threading.Thread(target=sample)
-            th.start()
+            # (no memory sampling here: a thread polling hipMemGetInfo during the trials made this
+            # step 3.9 s instead of ~0.24 s; tools/place_seq.py measures the peak separately)
             t_first = time.perf_counter()
             st = one_step()
-            first_ms = (time.perf_counter() - t_first) * 1e3
-            stop.set()
-            th.join()
-            first_step = (first_ms, mem_free1 - low[0])
+            first_step = ((time.perf_counter() - t_first) * 1e3, mem_free1 - torch.cuda.mem_get_info()[0])
         else:
             st = one_step()
         if i == 0 and fx is not None:  # before the timed steps: a wrong result is caught, not timed
@@ -510,10 +500,10 @@ def main():
             rl["engine_setup"] = {
                 "create_ms": round(create_ms, 1), "device_bytes_after_create": int(mem_free0 - mem_free1),
                 "first_step_ms": round(first_step[0], 1), "timed_step_ms": round(dt / max(args.steps, 1) * 1e3, 2),
-                "peak_extra_device_bytes_first_step": int(first_step[1]),
-                "note": "gossip_create wall time and the device memory it took; the first step's wall time and the "
-                        "most device memory it held beyond that (torch.cuda.mem_get_info sampled every 2 ms): the "
-                        "placement trials hold at most two candidate record slabs (DESIGN.md §3.7)"}
+                "extra_device_bytes_after_first_step": int(first_step[1]),
+                "note": "gossip_create wall time and the device memory it took; the first step's wall time (it runs "
+                        "the placement trials, which hold at most two candidate record slabs beside the kept one: "
+                        "DESIGN.md §3.7, peak measured by tools/place_seq.py) and what it left allocated"}
     else:
         rl = sharded_roofline(eng, driver, trace, bpn * nown, world, args.backend, args.steps)
     eng.close()
