@@ -15,7 +15,8 @@ from gossip_hip import engine as _eng  # noqa: E402
 
 if os.environ.get("GOSSIP_LIB"):
     _eng.load_library(os.environ["GOSSIP_LIB"])
-N = 1 << int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 27
+# argv[1]: log2 of the node count, or the node count itself when > 64 (odd sizes)
+N = (1 << int(sys.argv[1]) if int(sys.argv[1]) <= 64 else int(sys.argv[1])) if len(sys.argv) > 1 else 1 << 27
 SEED = int(sys.argv[2], 0) if len(sys.argv) > 2 else 0x5EED0004
 PARAMS = {a.split("=")[0]: float(a.split("=")[1]) for a in sys.argv[3].split()} if len(sys.argv) > 3 else {}
 e = Engine(N, 64, "pushpull", 2, SEED, flags=1, params=PARAMS)
