@@ -92,10 +92,13 @@ void bin_carve(const BinGeom& g, void* base, BinBufs* b);
 // recomputed (layout as stats_kernel's plus [4+R] = nonzero nodes); a
 // one-block kernel hands them to the host through rs.  filt (needs exact
 // nzb/fullb): bit 0 drops pulls from empty peers, bit 1 pushes into full
-// peers — exact, it only removes edges that move nothing.
+// peers — exact, it only removes edges that move nothing.  parts (placement trials): bit 0 emit +
+// transpose, bit 1 serve, bit 2 apply; a round is all three.
+constexpr uint32_t kBinAll = 7u;
 hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, uint64_t* partial, uint32_t R,
                                uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t filt,
-                               const Faults& fa, uint32_t flags, const RoundSync& rs, hipStream_t st);
+                               const Faults& fa, uint32_t flags, const RoundSync& rs, hipStream_t st,
+                               uint32_t parts = kBinAll);
 
 // Dense round of a sharded engine (G > 1) after the state all-gather
 // (DESIGN.md §5): push pass P = every sender of the image, records for the

@@ -1203,10 +1203,11 @@ void bin_carve(const BinGeom& g, void* base, BinBufs* b) {
 
 }
 
-hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, uint64_t* partial, uint32_t R,
-                               uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t filt,
-                               const Faults& fa, uint32_t flags, const RoundSync& rs, hipStream_t st) {
-  if (!b.nzb || !b.fullb) filt = 0;  // the bitmaps exist only with the frontier buffers
+namespace {
+// K1 + the run-offset transpose of a one-shard dense round
+void launch_bin_emit(const BinGeom& g, const BinBufs& b, uint64_t* S, uint64_t* partial, uint32_t R, uint32_t t,
+                     uint32_t key0, uint32_t key1, uint32_t mode, uint32_t filt, const Faults& fa,
+                     const RoundSync& rs, hipStream_t st) {
   const uint32_t eg = g.nt_s < kEmitGrid ? g.nt_s : kEmitGrid;  // persistent: one block per CU
 #define GOSSIP_EMIT(KR, F, VV) \
   bin_emit_kernel<KR, F, VV><<<eg, kEmitThreads, 0, st>>>(g, S, b, R, t, key0, key1, mode, filt, fa, EmitRange{})
@@ -1230,14 +1231,25 @@ hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, 
 #undef GOSSIP_EMIT_V
 #undef GOSSIP_EMIT
   launch_transpose_u16(b.off, b.offT, g.nt_s, g.nt_d + 1, partial, rs.plen, st, b.dyn);
-  if ((mode == 2 || mode == 3) && g.split)
+}
+}  // namespace
+
+hipError_t launch_binned_round(const BinGeom& g, const BinBufs& b, uint64_t* S, uint64_t* partial, uint32_t R,
+                               uint32_t t, uint32_t key0, uint32_t key1, uint32_t mode, uint32_t filt,
+                               const Faults& fa, uint32_t flags, const RoundSync& rs, hipStream_t st,
+                               uint32_t parts) {
+  if (!b.nzb || !b.fullb) filt = 0;  // the bitmaps exist only with the frontier buffers
+  if (parts & 1u) launch_bin_emit(g, b, S, partial, R, t, key0, key1, mode, filt, fa, rs, st);
+  const bool pull = mode == 2 || mode == 3;
+  if ((parts & 2u) && pull && g.split)
     bin_serve_kernel<kIdVF, true><<<serve_grid(g.nt_d, g.serve_grid), kTileThreads, 0, st>>>(g, S, b, R,
                                                                                           IdxRange::all(g.nt_d));
-  else if (mode == 2 || mode == 3)
+  else if ((parts & 2u) && pull)
     bin_serve_kernel<kIdVF, false><<<serve_grid(g.nt_d, g.serve_grid), kTileThreads, 0, st>>>(g, S, b, R,
                                                                                            IdxRange::all(g.nt_d));
   // in place: K3 of tile X reads and writes only S[X] (push values and pull
   // responses come from the record buffers), and K1/K2 have finished reading S_t
+  if (!(parts & 4u)) return hipGetLastError();
   if (g.aos)
     bin_apply_kernel<2><<<apply_grid(g), kTileThreads, 0, st>>>(g, b, g, b, S, S, g.N, 0, partial, R, mode, flags);
   else if (g.split)
