@@ -41,60 +41,6 @@ thread_local std::string g_create_error;
 constexpr int kTimers = 6;
 constexpr uint32_t kRing = 8;
 
-// Record slab built with the virtual-memory API (placement): physical handles of
-// `chunk` bytes (0: one handle for the whole slab) mapped into one reserved range, in order or,
-// with `shuffle`, at VA slots permuted by a fixed LCG, so the slab's physical pages are chosen
-// per chunk rather than by hipMalloc.
-struct VmmSlab {
-  void* va = nullptr;
-  size_t size = 0, chunk = 0;
-  std::vector<hipMemGenericAllocationHandle_t> h;
-};
-
-[[maybe_unused]] void vmm_free(VmmSlab* s) {
-  if (!s->va) return;
-  (void)hipDeviceSynchronize();
-  (void)hipMemUnmap(s->va, s->size);
-  for (auto x : s->h) (void)hipMemRelease(x);
-  (void)hipMemAddressFree(s->va, s->size);
-  *s = VmmSlab{};
-}
-
-[[maybe_unused]] hipError_t vmm_alloc(VmmSlab* s, size_t bytes, size_t chunk, bool shuffle, int dev) {
-  hipMemAllocationProp prop{};
-  prop.type = hipMemAllocationTypePinned;
-  prop.location.type = hipMemLocationTypeDevice;
-  prop.location.id = dev;
-  size_t gran = 0;
-  if (hipError_t x = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended)) return x;
-  if (gran == 0) gran = 2u << 20;
-  chunk = chunk ? (chunk + gran - 1) / gran * gran : 0;
-  const size_t unit = chunk ? chunk : gran;
-  s->size = (bytes + unit - 1) / unit * unit;
-  s->chunk = chunk ? chunk : s->size;
-  if (hipError_t x = hipMemAddressReserve(&s->va, s->size, gran, nullptr, 0)) return x;
-  const size_t n = s->size / s->chunk;
-  std::vector<size_t> slot(n);
-  for (size_t i = 0; i < n; ++i) slot[i] = i;
-  if (shuffle) {
-    uint64_t z = 0x9E3779B97F4A7C15ull;
-    for (size_t i = n; i > 1; --i) {
-      z = z * 6364136223846793005ull + 1442695040888963407ull;
-      std::swap(slot[i - 1], slot[(z >> 33) % i]);
-    }
-  }
-  for (size_t i = 0; i < n; ++i) {
-    hipMemGenericAllocationHandle_t h{};
-    if (hipError_t x = hipMemCreate(&h, s->chunk, &prop, 0)) return x;
-    s->h.push_back(h);
-    if (hipError_t x = hipMemMap((char*)s->va + slot[i] * s->chunk, s->chunk, 0, h, 0)) return x;
-  }
-  hipMemAccessDesc ad{};
-  ad.location = prop.location;
-  ad.flags = hipMemAccessFlagsProtReadWrite;
-  return hipMemSetAccess(s->va, s->size, &ad, 1);
-}
-
 }  // namespace
 
 struct gossip_engine {
@@ -213,7 +159,6 @@ struct gossip_engine {
   BinBufs bb{};
   uint32_t* bb_dyn = nullptr;  // the tile queues (gossip_set_param "tile_queues" 0 clears bb.dyn)
   void* bin_mem = nullptr;
-  VmmSlab bin_vmm;  // the slab when built with the VMM API (then bin_mem == bin_vmm.va)
   // placement of the record slab (place_bins): the dense round's time depends on where the slab
   // lands (4.98-5.48 ms at 2^27 across fresh allocations in one process, profiles/r05_pl/r05_pl4/,
   // r05_pl6/); before the first round place_tries allocations are timed on a zero-state trial round
@@ -353,8 +298,7 @@ void free_all(gossip_engine* e) {
   void* fe[] = {e->stall_d, e->fw.att};
   for (void* b : fe)
     if (b) (void)hipFree(b);
-  if (e->bin_vmm.va) vmm_free(&e->bin_vmm);
-  else if (e->bin_mem) (void)hipFree(e->bin_mem);
+  if (e->bin_mem) (void)hipFree(e->bin_mem);
   if (e->fr_mem) (void)hipFree(e->fr_mem);
   void* sx[] = {e->lf_mem, e->sx_mem, e->rare_recv, e->msg_recv, e->sb_mem, e->xd_smem, e->xd_rmem,
                 e->cc_bits, e->cc_vals, e->xd_cls, e->xd_keep};
@@ -632,24 +576,6 @@ int place_bins(gossip_engine* e) {
     e->bb = nb;
     return GOSSIP_OK;
   };
-#ifdef GOSSIP_SLAB_VMM
-  // experiment build (tools/build_variants.sh): the slab from the VMM API instead of the trials;
-  // GOSSIP_SLAB_VMM 1 = one handle, 2 = GOSSIP_SLAB_CHUNK_MB chunks in order, 3 = shuffled
-  if (e->binned && bytes >= (512ull << 20)) {
-#ifndef GOSSIP_SLAB_CHUNK_MB
-#define GOSSIP_SLAB_CHUNK_MB 2
-#endif
-    const size_t chunk = GOSSIP_SLAB_VMM == 1 ? 0 : ((size_t)GOSSIP_SLAB_CHUNK_MB << 20);
-    HIP_OK(e, hipDeviceSynchronize());
-    if (hipError_t x = vmm_alloc(&e->bin_vmm, bytes, chunk, GOSSIP_SLAB_VMM == 3, e->device)) {
-      vmm_free(&e->bin_vmm);
-      return e->fail(GOSSIP_EHIP, "VMM slab: %s", hipGetErrorString(x));
-    }
-    HIP_OK(e, hipFree(e->bin_mem));
-    e->bin_mem = e->bin_vmm.va;
-    return recarve();
-  }
-#endif
   if (!e->binned || e->place_tries <= 1 || bytes < (512ull << 20) || !e->img[1]) return GOSSIP_OK;
   uint64_t* part = nullptr;
   HIP_OK(e, hipMalloc((void**)&part, (part_len(e) + 8) * 8));
@@ -665,12 +591,10 @@ int place_bins(gossip_engine* e) {
       return launch_binned_round(e->bg, b, e->img[1], part, e->R, 0u, e->key0, e->key1, e->mode, 0u, Faults{}, 0u,
                                  rs, e->stream, parts);
     };
-#ifdef GOSSIP_PLACE_FULL_ROUND  // (A/B build: every trial a whole dense round, rounds 5-6)
-    return timed_trial(e, [&] { return part_round(kBinAll); }, ms);
-#else
     // The slab's mode is serve's (the trial round follows bin_serve at r = 0.93-0.99 across
     // candidates): one emit fills the candidate's records, then serve alone is
-    // timed (its tile queues cleared before each launch)
+    // timed (its tile queues cleared before each launch).  Whole trial rounds chose equally fast
+    // slabs at twice the cost (first step at 2^27 230 vs 127 ms, profiles/r06_vmm/place_serve)
     HIP_OK(e, part_round(1u));
     return timed_trial(e, [&] {
       if (b.dyn) {
@@ -678,7 +602,6 @@ int place_bins(gossip_engine* e) {
       }
       return part_round(2u);
     }, ms);
-#endif
   }, &moved, "place_bins");
   (void)hipFree(part);
   if (moved) {

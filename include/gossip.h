@@ -134,10 +134,10 @@ int gossip_set_stream(gossip_engine_t* eng, void* hip_stream);
  * Operational:
  *   "timing"       0 pauses, 1 resumes the timers of an engine created with GOSSIP_FLAG_TIMING
  *                  (their hipEvents between rounds cost a few µs each)
- *   "place_tries"  a binned engine with a record slab of 512 MiB or more times a zero-state trial
- *                  round on up to this many allocations of the slab before its first round and keeps
- *                  the fastest (default 12; 1: the first allocation).  At most two slabs are held at
- *                  once (the best so far and the candidate)
+ *   "place_tries"  a binned engine with a record slab of 512 MiB or more times the serve pass of a
+ *                  zero-state trial round on up to this many allocations of the slab before its first
+ *                  round and keeps the fastest (default 12; 1: the first allocation).  At most two
+ *                  slabs are held at once beside the kept one
  *   "ahead"        rounds enqueued ahead of the stats read back (1..7, default 2)
  *   "ae_ahead"     ANTIENTROPY, one engine: sparse rounds enqueued at once, each gated on the
  *                  device by the previous one (1..8, default 8; 1 = one round per host read)
