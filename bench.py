@@ -493,9 +493,10 @@ def main():
     workload = workload_name(args.nodes_per_gpu if per_gpu else n_total, world, per_gpu)
     if world == 1:
         rl = single_gpu_roofline(eng, n_total, workload)
-        rl["placement_trials"] = {"rounds": placement[1], "ms": placement[0],
-                                  "note": "dense trial rounds on fresh allocations of the record slab before the "
-                                          "first round (param place_tries), in the warm-up: not in the timed steps"}
+        rl["placement_trials"] = {"launches": placement[1], "ms": placement[0],
+                                  "note": "serve launches timed on fresh allocations of the record slab (one emit "
+                                          "each, not counted) before the first round (param place_tries, DESIGN.md "
+                                          "\u00a73.7), in the warm-up: not in the timed steps"}
         if first_step is not None:
             rl["engine_setup"] = {
                 "create_ms": round(create_ms, 1), "device_bytes_after_create": int(mem_free0 - mem_free1),
