@@ -225,7 +225,8 @@ def plan_model(eng, steps: int) -> dict:
     return {"plan": plan, "model_wall_ms": ms / max(steps, 1), "model_link_ms": link / max(steps, 1),
             "model_device_ms": (ms - link) / max(steps, 1), "rounds_modelled": int(n // max(steps, 1)),
             "link_gbps": ENGINE_PARAMS.get("link_gbps", 76.0),
-            "what": "per step and rank: S sparse, X exchange, C class-coded, D state all-gather dense rounds"}
+            "what": "per step and rank: S sparse, X exchange, C class-coded, D state all-gather dense rounds, "
+                    "R replicated after the state all-gather, r replicated on the whole image (no collective)"}
 
 
 def sharded_roofline(eng, driver: str, trace, alg_round: int, world: int, backend: str, steps: int = 1) -> dict:

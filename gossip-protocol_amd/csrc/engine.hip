@@ -229,6 +229,16 @@ struct gossip_engine {
   // class-coded state exchange for dense image rounds (sharded.h cc_*), plan kind 4
   bool cc_planned = false;
   double cc_frac = 0.75;
+  // replicated dense rounds (plan kinds 5 / 6): every rank runs the one-GPU binned
+  // round over the whole state image in place, so the next dense round needs no collective
+  // before it (kind 6) — where the links cost more than the extra device time (G = 2 at 2^27)
+  int replicate = -1;           // gossip_set_param "replicate": -1 by the cost model, 0 never, 1 every dense round
+  bool rep_planned = false;     // this round is replicated
+  bool rep_img_ok = false;      // the image holds S_t of every node (the last round was replicated)
+  BinGeom rbg{};
+  BinBufs rbb{};
+  void* rep_mem = nullptr;      // the one-GPU record slab over all N nodes, at the first replicated round
+  uint64_t* rep_part = nullptr; // that round's whole-image totals (scratch: the ranks report own-slice totals)
   // gossip_set_param "link_gbps": sharded random-mode rounds pick sparse / dense by a per-rank
   // cost model with a link term (shard_round_costs); 0 = the fixed sparse_frac thresholds
   double link_gbps = 76.0;
@@ -299,6 +309,8 @@ void free_all(gossip_engine* e) {
   for (void* b : fe)
     if (b) (void)hipFree(b);
   if (e->bin_mem) (void)hipFree(e->bin_mem);
+  if (e->rep_mem) (void)hipFree(e->rep_mem);
+  if (e->rep_part) (void)hipFree(e->rep_part);
   if (e->fr_mem) (void)hipFree(e->fr_mem);
   void* sx[] = {e->lf_mem, e->sx_mem, e->rare_recv, e->msg_recv, e->sb_mem, e->xd_smem, e->xd_rmem,
                 e->cc_bits, e->cc_vals, e->xd_cls, e->xd_keep};
@@ -723,6 +735,11 @@ struct ShardCosts {
   double sparse, dense;            // modelled ms per rank: device + link
   double sparse_link, dense_link;  // their link parts
   bool dense_xd, dense_cc;
+  // a replicated dense round (kinds 5 / 6): device time of the one-GPU round over
+  // all N nodes (5.1 ms at 2^27 on MI355X: 3.8e-8 ms per node) plus the own-slice totals, and the
+  // state all-gather when the image is not whole yet (kind 5)
+  double rep, rep_link;
+  bool rep_ok;
 };
 uint32_t dense_filter(const gossip_engine* e, const Est& x, double frac);
 
@@ -753,6 +770,9 @@ ShardCosts shard_round_costs(const gossip_engine* e, const Est& x) {
     c.dense_link = slice * (G - 1.0) / bw;
     c.dense = 7.3e-9 * N + 4.7e-8 * Nl + c.dense_link;
   }
+  c.rep_ok = e->replicate != 0 && e->sx && bin_path_ok(e->N, e->k, 1, 1);
+  c.rep_link = e->rep_img_ok ? 0.0 : 8.0 * Nl * (G - 1.0) / bw;
+  c.rep = 3.8e-8 * N + 1.5e-9 * Nl + c.rep_link;
   return c;
 }
 
@@ -1265,6 +1285,36 @@ int step_ae(gossip_engine* e, uint32_t max_rounds, gossip_round_stats_t* stats, 
 }
 
 // compute S_{t+1} of the owned shard from the gathered image + partial stats (device)
+// A replicated dense round (plan kinds 5 / 6): the one-GPU binned round over the
+// whole image of S_t (gathered by the driver for kind 5, left by the previous replicated round for
+// kind 6) in place, so every rank holds S_{t+1} of every node; the rank reports the totals of its
+// own slice (and rebuilds its own bitmaps) like any other sharded round, so the driver's
+// all-reduce stays as it is.  Bits as the sharded kinds: the same draws and edges (§2).
+int rep_compute(gossip_engine* e) {
+  if (!e->rep_mem) {  // (no placement trials: the slab serves a handful of rounds per run)
+    e->rbg = make_bin_geom(e->N, e->k, (e->N + kTileD - 1) / kTileD > kBigFromTiles);
+    const size_t bytes = bin_bytes(e->rbg);
+    if (hipMalloc(&e->rep_mem, bytes) != hipSuccess) {
+      e->rep_mem = nullptr;
+      return e->fail(GOSSIP_ENOMEM, "hipMalloc of %zu bytes (replicated-round records) failed", bytes);
+    }
+    bin_carve(e->rbg, e->rep_mem, &e->rbb);
+    e->rbb.nzb = e->rbb.fullb = nullptr;  // (no edge filter: it needs bitmaps of the whole image)
+    HIP_OK(e, hipMemset(e->rbb.dyn, 0, 17 * 4));
+    if (e->rbg.nt_d < 4096) e->rbb.dyn = nullptr;  // (the tile queues pay past 4096 tiles, as on one GPU)
+  }
+  if (!e->rep_part) HIP_OK(e, hipMalloc((void**)&e->rep_part, (part_len(e) + 8) * 8));
+  int rc;
+  if ((rc = timer_begin(e, 0))) return rc;
+  const RoundSync rs{nullptr, (uint32_t)part_len(e), 0u};
+  HIP_OK(e, launch_binned_round(e->rbg, e->rbb, current_image(e), e->rep_part, e->R, e->t, e->key0, e->key1, e->mode,
+                                0u, e->fa, e->cfg.flags, rs, e->stream));
+  HIP_OK(e, hipMemsetAsync(e->partial_d, 0, part_len(e) * 8, e->stream));
+  HIP_OK(e, launch_frontier_rebuild(e->lf, e->S, e->nown, e->partial_d, e->R, e->cfg.flags, e->stream));
+  e->sx_valid = true;
+  return timer_end(e, 0);
+}
+
 int compute_round(gossip_engine* e, const uint64_t* gathered) {
   const size_t bytes = (size_t)e->W * e->Nl * 8;
   if (e->mode == GOSSIP_MODE_ANTIENTROPY) return ae_round(e);  // (clears partial and aux itself)
@@ -1294,6 +1344,8 @@ int compute_round(gossip_engine* e, const uint64_t* gathered) {
                                 ring_sync(e, 0), -1, sparse && bscan_round(e, x, maj))))
       return rc;
     return timer_end(e, 0);  // stats are fused into the round kernels
+  } else if (e->rep_planned) {  // replicated dense round: the one-GPU round over the whole image
+    return rep_compute(e);
   } else if (e->sbin) {  // sharded dense round: binned pipeline over the gathered image
     if ((rc = place_sb(e))) return rc;  // (a no-op once gossip_dense_prepare has placed the slab)
     if ((rc = timer_begin(e, 0))) return rc;
@@ -1785,6 +1837,8 @@ int gossip_set_param(gossip_engine_t* e, const char* name, double v) {
   } else if (n == "ahead") {
     if (v < 1 || v > kRing - 1) return e->fail(GOSSIP_EINVAL, "ahead must be in [1, %u]", kRing - 1);
     e->ahead = (uint32_t)v;
+  } else if (n == "replicate") {  // < 0: by the cost model, 0: never, > 0: every dense round
+    e->replicate = v < 0 ? -1 : v > 0 ? 1 : 0;
   } else if (n == "cc_frac") {
     if (v < 0 || v > 1) return e->fail(GOSSIP_EINVAL, "cc_frac must be in [0, 1] (0 = never)");
     e->cc_frac = v;
@@ -1911,6 +1965,7 @@ int gossip_reset(gossip_engine_t* e) {
   e->sx_valid = e->gtot_valid = e->last_sparse = false;
   // a dense_prepare or sparse plan of the old state must not leak into the next round
   e->sb_pre = e->ev_pre_pending = e->sx_planned = e->xd_planned = e->cc_planned = false;
+  e->rep_planned = e->rep_img_ok = false;
   if (e->frontier) {  // all-zero state: zero totals, empty bitmaps (D and its dirty flags are zero between rounds)
     const size_t nwb = (e->N + 63) / 64 * 8;
     HIP_OK(e, hipMemsetAsync(e->fb.nzb, 0, nwb, e->stream));
@@ -1945,7 +2000,7 @@ int gossip_inject(gossip_engine_t* e, uint64_t node, uint32_t rumor) {
   }
   HIP_OK(e, launch_inject(e->S, e->Nl, e->lo, e->hi, e->N, e->R, e->key0, e->key1, (int64_t)node, rumor, e->stream,
                           e->flood_edges ? &e->fw : nullptr));
-  e->fr_valid = e->sx_valid = e->gtot_valid = false;
+  e->fr_valid = e->sx_valid = e->gtot_valid = e->rep_img_ok = false;
   return GOSSIP_OK;
 }
 
@@ -1970,7 +2025,7 @@ int gossip_inject_random(gossip_engine_t* e) {
   }
   HIP_OK(e, launch_inject(e->S, e->Nl, e->lo, e->hi, e->N, e->R, e->key0, e->key1, -1, 0, e->stream,
                           e->flood_edges ? &e->fw : nullptr));
-  e->fr_valid = e->sx_valid = e->gtot_valid = false;
+  e->fr_valid = e->sx_valid = e->gtot_valid = e->rep_img_ok = false;
   return GOSSIP_OK;
 }
 
@@ -1995,7 +2050,7 @@ int gossip_exchange_buffers(gossip_engine_t* e, void** send, void** recv, uint64
 
 int gossip_dense_prepare(gossip_engine_t* e) {
   if (!e) return GOSSIP_EINVAL;
-  if (!e->sbin || e->sb_pre) return GOSSIP_OK;
+  if (!e->sbin || e->sb_pre || e->rep_planned) return GOSSIP_OK;
   if (int rc = set_dev(e)) return rc;
   if (int rc = place_sb(e)) return rc;  // (placed already by gossip_exchange_buffers / gossip_cc_send)
   if (e->timing) HIP_OK(e, hipEventRecord(e->ev_pre[0], e->stream));
@@ -2073,7 +2128,9 @@ int gossip_round_commit(gossip_engine_t* e, const uint64_t* total, gossip_round_
     if (int rc = set_dev(e)) return rc;
     HIP_OK(e, launch_stall_update(e->stall_d, e->N, e->k, e->t, e->key0, e->key1, e->fa, e->stream));
   }
-  if (!e->last_sparse) rotate(e);  // sparse sharded rounds update S in place
+  if (!e->last_sparse && !e->rep_planned) rotate(e);  // sparse and replicated rounds update S in place
+  e->rep_img_ok = e->rep_planned;  // a replicated round leaves S_{t+1} of every node in the image
+  e->rep_planned = false;
   if (e->aex) {  // V = S_{t+1}, Vn = S_t, aex_dirty = the rows where they differ
     e->aex_patch_ok = e->aex_round_done;
     e->aex_round_done = false;
@@ -2138,7 +2195,7 @@ int gossip_local_totals(gossip_engine_t* e, uint64_t* partial) {
 
 int gossip_sharded_plan(gossip_engine_t* e, const uint64_t* total, int32_t* kind) {
   if (!e || !kind) return GOSSIP_EINVAL;
-  e->sx_planned = e->xd_planned = e->cc_planned = false;
+  e->sx_planned = e->xd_planned = e->cc_planned = e->rep_planned = false;
   if (e->aex) {  // 2: an anti-entropy exchange round; -2: the global max vector is needed first
     *kind = e->aex_target_ok ? 2 : -2;
     return GOSSIP_OK;
@@ -2160,8 +2217,16 @@ int gossip_sharded_plan(gossip_engine_t* e, const uint64_t* total, int32_t* kind
   e->sx_planned = choose_sparse(e, est_of(e, e->gtot.data()), &maj, &all_d);
   // (link_gbps 0: priced at the default rate, for gossip_plan_model only)
   const ShardCosts c = shard_round_costs(e, est_of(e, e->gtot.data()));
-  if (!e->sparse_frac_set && e->link_gbps > 0)  // the link-aware cost model decides instead
-    e->sx_planned = c.sparse < c.dense;
+  const bool model = !e->sparse_frac_set && e->link_gbps > 0;
+  // replicated dense rounds: forced (param replicate 1), or by the model where one with a whole
+  // image already (device time only) costs less than the sharded dense round: entering costs the
+  // all-gather once (kind 5), every following dense round none (kind 6).  The model's per-node
+  // fits come from 2^24-2^27-node runs: below 2^22 nodes it replicates only when forced
+  const bool rep_auto = e->replicate < 0 && model && e->N >= (1ull << 22) && c.rep - c.rep_link < c.dense;
+  const bool rep_any = c.rep_ok && (e->replicate == 1 || rep_auto);
+  if (model)  // the link-aware cost model decides instead
+    e->sx_planned = c.sparse < (rep_any ? std::min(c.dense, c.rep) : c.dense);
+  e->rep_planned = !e->sx_planned && rep_any;
   e->plan_cost[0] = c.sparse;
   e->plan_cost[1] = c.dense;
   e->sx_maj = maj;
@@ -2171,7 +2236,7 @@ int gossip_sharded_plan(gossip_engine_t* e, const uint64_t* total, int32_t* kind
     const double r = std::min(1.0, std::min(x.nz, (double)e->N - x.full) / (double)e->N);
     e->sx_mid = e->sb.gsum.summ2 && 1.0 - std::pow(1.0 - r, (double)(1u << e->sb.gsum.glog)) >= e->mid_frac;
   }
-  e->xd_planned = !e->sx_planned && e->xd && e->xd_shards && e->G >= e->xd_shards;
+  e->xd_planned = !e->sx_planned && !e->rep_planned && e->xd && e->xd_shards && e->G >= e->xd_shards;
   // exchange rounds drop the one-way edges into empty / full peers when many nodes are (the
   // global totals are exact: no prediction), after an all-gather of the class bitmaps
   // (k <= 8: one keep byte per sender carries the count pass's probes to the emit pass)
@@ -2179,14 +2244,14 @@ int gossip_sharded_plan(gossip_engine_t* e, const uint64_t* total, int32_t* kind
   e->xd_cls_ok = false;
   // dense on the state image: class-coded when few nodes are mixed (neither empty nor full)
   const double mixed = ((double)e->gtot[4 + e->R] - (double)e->gtot[0]) / (double)e->N;
-  e->cc_planned = !e->sx_planned && !e->xd_planned && e->cc_frac > 0 && mixed <= e->cc_frac;
-  *kind = e->sx_planned ? 1 : e->xd_planned ? 3 : e->cc_planned ? 4 : 0;
+  e->cc_planned = !e->sx_planned && !e->xd_planned && !e->rep_planned && e->cc_frac > 0 && mixed <= e->cc_frac;
+  *kind = e->sx_planned ? 1 : e->rep_planned ? (e->rep_img_ok ? 6 : 5) : e->xd_planned ? 3 : e->cc_planned ? 4 : 0;
   // the model's price of the round as planned (gossip_plan_model): the plan of the current run
   // (restarted at round 0) and the modelled ms since gossip_reset_timing
   if (e->t == 0) e->model_plan.clear();
-  e->model_plan.push_back("DSAXC"[*kind]);
-  e->model_ms += e->sx_planned ? c.sparse : c.dense;
-  e->model_link_ms += e->sx_planned ? c.sparse_link : c.dense_link;
+  e->model_plan.push_back("DSAXCRr"[*kind]);
+  e->model_ms += e->sx_planned ? c.sparse : e->rep_planned ? c.rep : c.dense;
+  e->model_link_ms += e->sx_planned ? c.sparse_link : e->rep_planned ? c.rep_link : c.dense_link;
   e->model_rounds += 1;
   return GOSSIP_OK;
 }

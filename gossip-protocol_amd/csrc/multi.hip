@@ -746,7 +746,11 @@ struct Driver {
         break;
       case 3: rc = exchange(&pd); break;
       case 4: rc = dense(&pd, true); break;
-      default: rc = dense(&pd, false); break;
+      case 6:  // replicated, the image whole already: no collective before it
+        for (size_t i = 0; i < n(); ++i) ENG(i, gossip_round_compute_dev(L[i], &pd[i]));
+        rc = GOSSIP_OK;
+        break;
+      default: rc = dense(&pd, false); break;  // 0, 5 (the state all-gather, then the replicated round)
     }
     if (rc) return rc;
     if (kind == 2) TR(tr->all_reduce_sum_u64(part, total));

@@ -21,6 +21,11 @@ without a GPU):
   class-coded   (kind 4, DESIGN.md §5.1: dense rounds while few nodes are mixed) the
                 state all-gather as each shard's two occupancy bitmaps (empty / full)
                 plus the words of its mixed nodes, expanded into the image on arrival;
+  replicated    (kinds 5 / 6, DESIGN.md §5.7: dense rounds where the links cost more than the
+                extra device time, e.g. G = 2 at 2^27 nodes) every rank runs the whole round over
+                the whole image in place: kind 5 after the state all-gather (as a dense round),
+                kind 6 with no collective before it (the previous round left every node's
+                S_{t+1} in the image); then the all-reduce of the own-slice partials;
   ANTIENTROPY   ("Design B") all-gather of the alive and stale bits,
                 all-to-all of request items {p, n, V_t[n]} to p's owner and of its
                 replies V_t[p], all-reduce of the partials; the global max vector
@@ -280,6 +285,13 @@ def _xd_round(engine, comm: _Comm) -> np.ndarray:
     return engine.xd_finish()
 
 
+def _rep_round(engine, comm: _Comm) -> np.ndarray:
+    """Kind 6: the image already holds S_t of every node (the last round was replicated)."""
+    if _dev_values(engine, comm):
+        return comm.dev_all_reduce_sum(engine.round_compute_dev(), engine.partial_len())
+    return engine.round_compute()
+
+
 def _cc_round(engine, comm: _Comm) -> np.ndarray:
     bits_p, nbytes, vals_p, count = engine.cc_send()
     w, dev = comm.world, engine.on_device
@@ -366,7 +378,9 @@ def sharded_round(engine, group=None, kinds: list | None = None, direct: bool | 
             partial = _cc_round(engine, comm)
         elif kind == 1:
             partial = _sparse_round(engine, comm)
-        else:
+        elif kind == 6:
+            partial = _rep_round(engine, comm)
+        else:  # 0, and 5 (the state all-gather, then the replicated round)
             partial = _dense_round(engine, comm)
         # the device-value path returns the global sum already (one all-reduce on engine memory)
         if comm.world > 1 and not (kind != 2 and _dev_values(engine, comm)):
@@ -620,7 +634,7 @@ def lockstep_run(engines, max_rounds: int, items: list | None = None):
     """One process driving G shard engines (one per GPU, or several on one) through the
     same rounds as sharded_run, with device copies in place of the collectives.
     Returns (per-round stats, per-round kind: 0 dense / 1 sparse / 2 ANTIENTROPY / 3 exchange dense /
-    4 class-coded dense).  items (exchange rounds; host engines too): per round, each shard's
+    4 class-coded dense / 5, 6 replicated dense after / without the all-gather).  items (exchange rounds; host engines too): per round, each shard's
     item counts per owner."""
     stats, kinds = [], []
     for _ in range(max_rounds):
@@ -638,7 +652,8 @@ def lockstep_run(engines, max_rounds: int, items: list | None = None):
         if ks[0] == 3:
             parts = _lockstep_xd(engines, items)
         else:
-            parts = {1: _lockstep_sparse, 2: _lockstep_ae, 4: _lockstep_cc}.get(ks[0], _lockstep_dense)(engines)
+            parts = {1: _lockstep_sparse, 2: _lockstep_ae, 4: _lockstep_cc,
+                     6: lambda es: [e.round_compute() for e in es]}.get(ks[0], _lockstep_dense)(engines)
         tot = _lockstep_sum(parts)
         st = [e.round_commit(tot) for e in engines]
         assert all(s == st[0] for s in st)

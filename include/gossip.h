@@ -170,6 +170,10 @@ int gossip_set_stream(gossip_engine_t* eng, void* hip_stream);
  *   "xd_filter_frac"  exchange dense rounds likewise (default 0.6; >= 1 never)
  *   "xd_shards"    sharded random modes: dense rounds run as exchange rounds when G >= this
  *                  (default 6; 0 = never)
+ *   "replicate"    sharded random modes: a dense round runs replicated, every rank computing the
+ *                  whole image in place, so the next dense round needs no collective before it
+ *                  (plan kinds 5 / 6): < 0 where the link-aware model prices it
+ *                  cheaper, past 2^22 nodes (default -1), 0 never, > 0 every dense round
  *   "cc_frac"      sharded random modes: dense rounds on the state image exchange it class-coded
  *                  while the mixed nodes are at most this fraction of N (default 0.75; 0 never)
  *   "ae_sparse"    ANTIENTROPY: -1 plan sparse rounds (default), 0 never, 1 whenever valid

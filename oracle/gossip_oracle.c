@@ -88,6 +88,9 @@ struct oracle_sim {
    * word), the own mixed words, every shard's at q * cc_stride */
   int cc_planned;
   double cc_frac;
+  /* replicated dense rounds (engine.hip rep_compute, plan kinds 5 / 6): every shard
+   * computes the whole image's round, so the next dense round needs no all-gather */
+  int replicate, rep_planned, rep_img_ok;
   double link_gbps; /* engine.hip link_gbps: the link-aware plan (0 = the fixed thresholds) */
   uint64_t *cc_bits, *cc_send, *cc_vals, cc_stride;
 };
@@ -256,6 +259,7 @@ int oracle_create(const gossip_config_t* cfg, int threads, oracle_sim_t** out) {
   s->xd_shards = 6;
   s->cc_frac = 0.75;
   s->link_gbps = 76.0;
+  s->replicate = -1;
   s->xd_filter_frac = 0.6; /* engine.hip xd_filter_frac */
   s->flood_edges = s->mode == GOSSIP_MODE_FLOOD && faulty;
   if (s->flood_edges) {
@@ -378,6 +382,7 @@ int oracle_reset(oracle_sim_t* s) {
   }
   s->t = 0;
   s->gtot_valid = s->planned = s->last_sparse = 0;
+  s->rep_planned = s->rep_img_ok = 0;
   return GOSSIP_OK;
 }
 
@@ -397,6 +402,7 @@ int oracle_inject(oracle_sim_t* s, uint64_t node, uint32_t rumor) {
     return GOSSIP_OK;
   }
   s->gtot_valid = 0;
+  s->rep_img_ok = 0;
   if (node < s->lo || node >= s->hi) return GOSSIP_OK;
   uint64_t* w = &s->S[(size_t)(rumor >> 6) * s->Nl + (node - s->lo)];
   if (s->flood_edges && !(*w & (1ull << (rumor & 63)))) { /* a client's value: its walk starts next round */
@@ -670,9 +676,47 @@ static void stall_update(oracle_sim_t* s) {
   }
 }
 
+static void totals_of(const oracle_sim_t* s, const uint64_t* X, uint64_t* partial);
+
+/* Replicated dense round (plan kinds 5 / 6): S_{t+1} of every node from the whole image of S_t
+ * (s->recv: gathered for kind 5, left by the previous replicated round for kind 6), written back
+ * into the image; the own slice becomes Snext and the partial holds its totals, as in a sharded
+ * dense round.  Same draws, edges and faults as oracle_round_compute. */
+static int rep_round(oracle_sim_t* s, uint64_t* partial) {
+  const uint64_t N = s->N;
+  const uint32_t k = s->k, t = s->t;
+  const uint32_t key[2] = {(uint32_t)s->cfg.seed, (uint32_t)(s->cfg.seed >> 32)};
+  uint64_t* g = s->recv;
+  uint64_t* ni = (uint64_t*)malloc(N * 8);
+  if (!ni) return GOSSIP_ENOMEM;
+  memcpy(ni, g, N * 8);
+  const int do_pull = s->mode == GOSSIP_MODE_PULL || s->mode == GOSSIP_MODE_PUSHPULL;
+  const int do_push = s->mode == GOSSIP_MODE_PUSH || s->mode == GOSSIP_MODE_PUSHPULL;
+  for (uint64_t sn = 0; sn < N; ++sn) {
+    uint32_t n = (uint32_t)sn, x[4] = {0, 0, 0, 0};
+    for (uint32_t j = 0; j < k; ++j) {
+      if ((j & 3) == 0) {
+        uint32_t ctr[4] = {n, t, 0u, j >> 2};
+        oracle_philox4x32_10(ctr, key, x);
+      }
+      uint32_t p = peer_from_word(x[j & 3], N, n);
+      if (lost_edge(s, n, p, j, key)) continue;
+      if (do_pull) ni[n] |= g[p];
+      if (do_push) ni[p] |= g[n];
+    }
+  }
+  memcpy(g, ni, N * 8);
+  memset(s->Snext, 0, (size_t)s->Nl * 8);
+  memcpy(s->Snext, ni + s->lo, s->nown * 8);
+  free(ni);
+  totals_of(s, s->Snext, partial);
+  return GOSSIP_OK;
+}
+
 int oracle_round_compute(oracle_sim_t* s, uint64_t* partial) {
   if (!s || !partial) return GOSSIP_EINVAL;
   if (s->mode == GOSSIP_MODE_ANTIENTROPY) return ae_round(s, partial);
+  if (s->rep_planned) return rep_round(s, partial);
   const uint64_t* g = s->G > 1 ? s->recv : s->send;
   const uint64_t N = s->N, Nl = s->Nl, lo = s->lo, nown = s->nown;
   const uint32_t W = s->W, k = s->k, t = s->t;
@@ -808,6 +852,8 @@ int oracle_round_commit(oracle_sim_t* s, const uint64_t* total, gossip_round_sta
     tmp = s->S; s->S = s->Snext; s->Snext = tmp;
   }
   s->last_sparse = 0;
+  s->rep_img_ok = s->rep_planned; /* the image holds S_{t+1} of every node after a replicated round */
+  s->rep_planned = 0;
   if (s->streak) stall_update(s); /* (uses s->t: the round just computed) */
   memcpy(s->gtot, total, oracle_partial_len(s) * 8);
   s->gtot_valid = 1;
@@ -861,7 +907,7 @@ int oracle_local_totals(oracle_sim_t* s, uint64_t* partial) {
 
 int oracle_sharded_plan(oracle_sim_t* s, const uint64_t* total, int32_t* kind) {
   if (!s || !kind) return GOSSIP_EINVAL;
-  s->planned = s->xd_planned = s->cc_planned = 0;
+  s->planned = s->xd_planned = s->cc_planned = s->rep_planned = 0;
   if (s->aex) {
     *kind = s->aex_target_ok ? 2 : -2;
     return GOSSIP_OK;
@@ -883,6 +929,9 @@ int oracle_sharded_plan(oracle_sim_t* s, const uint64_t* total, int32_t* kind) {
   /* the engine's default threshold (engine.hip sparse_frac_of): 1/25 before exchange rounds */
   const double frac = s->sparse_frac_set ? s->sparse_frac : s->xd_shards && s->G >= s->xd_shards ? 0.04 : 0.25;
   s->planned = (notfull < nz ? notfull : nz) <= frac * (double)s->N;
+  /* the engine's replicated round (shard_round_costs' rep): the one-GPU round over all N nodes,
+   * plus the state all-gather while the image is not whole */
+  double c_rep = 0.0, c_dense = 0.0;
   if (!s->sparse_frac_set && s->link_gbps > 0) { /* the engine's link-aware cost model (shard_round_costs) */
     const double N = (double)s->N, G = (double)s->G, Nl = (double)s->Nl, k = (double)s->k;
     const double full_n = (double)s->gtot[0];
@@ -893,7 +942,6 @@ int oracle_sharded_plan(oracle_sim_t* s, const uint64_t* total, int32_t* kind) {
     const int dense_xd = s->xd_shards && s->G >= s->xd_shards;
     const double mixed_n = nz - full_n > 0.0 ? nz - full_n : 0.0;
     const int dense_cc = !dense_xd && s->cc_frac > 0 && mixed_n / N <= s->cc_frac;
-    double c_dense;
     if (dense_xd) { /* the items that survive the class filter (the engine's dense_filter below) */
       unsigned filt = 0;
       if (s->k <= 8) {
@@ -909,9 +957,15 @@ int oracle_sharded_plan(oracle_sim_t* s, const uint64_t* total, int32_t* kind) {
       const double slice = dense_cc ? 20.0 / 64.0 * Nl + 8.0 * mixed_n / G : 8.0 * Nl;
       c_dense = 7.3e-9 * N + 4.7e-8 * Nl + slice * (G - 1.0) / bw;
     }
-    s->planned = c_sparse < c_dense;
+    c_rep = 3.8e-8 * N + 1.5e-9 * Nl;
+    const double c_rep_all = c_rep + (s->rep_img_ok ? 0.0 : 8.0 * Nl * (G - 1.0) / bw);
+    const int rep_auto = s->replicate < 0 && s->N >= (1ull << 22) && c_rep < c_dense;
+    s->planned = c_sparse < ((s->replicate == 1 || rep_auto) && c_rep_all < c_dense ? c_rep_all : c_dense);
+    s->rep_planned = !s->planned && rep_auto;
   }
-  s->xd_planned = !s->planned && s->xd_shards && s->G >= s->xd_shards;
+  /* (the engine's rep_any: forced, or the model's choice above, past 2^22 nodes) */
+  if (s->replicate == 1) s->rep_planned = !s->planned;
+  s->xd_planned = !s->planned && !s->rep_planned && s->xd_shards && s->G >= s->xd_shards;
   /* the engine's dense_filter of the global totals (engine.hip): pulls from empty peers once more
    * than xd_filter_frac of the nodes are empty, pushes into full peers likewise */
   s->xd_filt = 0;
@@ -923,8 +977,8 @@ int oracle_sharded_plan(oracle_sim_t* s, const uint64_t* total, int32_t* kind) {
   }
   /* the engine's class-coded all-gather: at most cc_frac mixed (nonzero, not full) nodes */
   const double mixed = ((double)s->gtot[4 + s->R] - (double)s->gtot[0]) / (double)s->N;
-  s->cc_planned = !s->planned && !s->xd_planned && s->cc_frac > 0 && mixed <= s->cc_frac;
-  *kind = s->planned ? 1 : s->xd_planned ? 3 : s->cc_planned ? 4 : 0;
+  s->cc_planned = !s->planned && !s->xd_planned && !s->rep_planned && s->cc_frac > 0 && mixed <= s->cc_frac;
+  *kind = s->planned ? 1 : s->rep_planned ? (s->rep_img_ok ? 6 : 5) : s->xd_planned ? 3 : s->cc_planned ? 4 : 0;
   return GOSSIP_OK;
 }
 
@@ -1276,8 +1330,8 @@ int oracle_cc_expand(oracle_sim_t* s, const uint64_t* counts) {
   return GOSSIP_OK;
 }
 
-/* gossip_set_param: the engine's tuning knobs.  sparse_frac, link_gbps, cc_frac, xd_shards and
- * xd_filter_frac matter here (they pick the
+/* gossip_set_param: the engine's tuning knobs.  sparse_frac, link_gbps, cc_frac, xd_shards,
+ * xd_filter_frac and replicate matter here (they pick the
  * sharded round protocol, which the gloo tests exercise); the rest steer engine kernel
  * choices that this restatement does not have, and are accepted as no-ops. */
 int oracle_set_param(oracle_sim_t* s, const char* name, double value) {
@@ -1290,6 +1344,10 @@ int oracle_set_param(oracle_sim_t* s, const char* name, double value) {
   if (!strcmp(name, "link_gbps")) {
     if (value < 0) return GOSSIP_EINVAL;
     s->link_gbps = value;
+    return GOSSIP_OK;
+  }
+  if (!strcmp(name, "replicate")) { /* < 0: by the cost model, 0: never, > 0: every dense round */
+    s->replicate = value < 0 ? -1 : value > 0 ? 1 : 0;
     return GOSSIP_OK;
   }
   if (!strcmp(name, "cc_frac")) {

@@ -104,14 +104,14 @@ def _header_knobs():
 
 
 def test_knob_list_is_pinned():
-    """gossip_set_param accepts exactly the knobs gossip.h documents: 7 operational ones and 15 that
+    """gossip_set_param accepts exactly the knobs gossip.h documents: 7 operational ones and 16 that
     force the parity tests' A/B paths (round 6 removed serve_lr, serve_grid, apply_grid, push_waves
-    and tile_queues, and added bin_scan_frac)."""
+    and tile_queues, and added bin_scan_frac and replicate)."""
     ops, tests = _header_knobs()
     assert ops == {"timing", "place_tries", "ahead", "ae_ahead", "ordered_collectives", "link_gbps",
                    "rccl_dev_collectives"}
     assert tests == {"sparse_frac", "alld_frac", "sparse_direct", "mid_frac", "bin_scan_frac", "scan_queue", "filter_frac",
-                     "xd_filter_frac", "xd_shards", "cc_frac", "ae_sparse", "ae_cap", "ae_dense_bin", "ae_dense_cap",
+                     "xd_filter_frac", "xd_shards", "replicate", "cc_frac", "ae_sparse", "ae_cap", "ae_dense_bin", "ae_dense_cap",
                      "ae_dense_filter"}
     src = open(os.path.join(ROOT, "gossip-protocol_amd", "csrc", "engine.hip")).read()
     body = src[src.index("int gossip_set_param("):src.index("int gossip_set_topology_csr(")]

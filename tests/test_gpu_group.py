@@ -16,7 +16,8 @@ pytestmark = pytest.mark.gpu
 
 PLANS = {"auto": {}, "sparse": {"sparse_frac": 1.0}, "dense": {"sparse_frac": -1, "xd_shards": 0, "cc_frac": 0},
          "classcoded": {"sparse_frac": -1, "xd_shards": 0, "cc_frac": 1},
-         "exchange": {"sparse_frac": -1, "xd_shards": 2}, "auto_exchange": {"xd_shards": 2}}
+         "exchange": {"sparse_frac": -1, "xd_shards": 2}, "auto_exchange": {"xd_shards": 2},
+         "replicated": {"sparse_frac": -1, "replicate": 1}, "auto_replicated": {"replicate": 1}}
 CASES = [("pushpull", 2, 64, 1 << 20, 0x5EED0004, 4), ("push", 3, 1, 300001, 7, 3),
          ("pull", 1, 5, 100000, 11, 2), ("pushpull", 2, 5, 12, 3, 5)]
 IDS = ["pushpull-1M-G4", "push-ragged-G3", "pull-G2", "pushpull-N12-G5-empty"]

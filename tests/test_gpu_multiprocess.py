@@ -75,11 +75,14 @@ def _state(e):
 CASES = [("pushpull", 2, 64, 1 << 20, 0x5EED0004, None),
          ("push", 3, 1, 300001, 7, None),
          ("pushpull", 2, 64, (1 << 20) + 77, 0x5EED0004, {"xd_shards": 2}),  # dense rounds as exchange rounds
-         ("antientropy", 1, 16, 1 << 18, 0x5EED0005, None)]
+         ("antientropy", 1, 16, 1 << 18, 0x5EED0005, None),
+         # dense rounds replicated (kinds 5 / 6): all-gather once, then no collective
+         ("pushpull", 2, 64, (1 << 20) + 3, 0x5EED0004, {"replicate": 1})]
 
 
 @pytest.mark.parametrize("backend", ["gloo", "gloo-dev", "nccl", "engine"])
-@pytest.mark.parametrize("case", CASES, ids=["pushpull-1M", "push-ragged", "pushpull-exchange", "antientropy"])
+@pytest.mark.parametrize("case", CASES, ids=["pushpull-1M", "push-ragged", "pushpull-exchange", "antientropy",
+                                           "pushpull-replicated"])
 def test_two_processes_equal_one_engine(case, backend):
     import torch
     if backend in ("nccl", "engine") and torch.cuda.device_count() < 2:

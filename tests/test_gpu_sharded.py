@@ -31,7 +31,9 @@ PLANS = {"auto": (0, {}), "sparse": (0, {"sparse_frac": 1.0}), "sparse_alld": (0
          # dense sharded rounds on the direct kernels instead of the binned push/pull passes
          "dense_direct": (FLAG_SHARD_DIRECT, {"sparse_frac": -1, "xd_shards": 0, "cc_frac": 0}),
          "classcoded_direct": (FLAG_SHARD_DIRECT, {"sparse_frac": -1, "xd_shards": 0, "cc_frac": 1}),
-         "auto_direct": (FLAG_SHARD_DIRECT, {"xd_shards": 0})}
+         "auto_direct": (FLAG_SHARD_DIRECT, {"xd_shards": 0}),
+         # dense rounds replicated: every shard computes the whole image (kinds 5 / 6)
+         "replicated": (0, {"sparse_frac": -1, "replicate": 1}), "auto_replicated": (0, {"replicate": 1})}
 
 
 @pytest.mark.parametrize("plan", list(PLANS))
@@ -62,6 +64,56 @@ def test_lockstep_shards_equal_one_engine(case, plan):
         assert set(kinds) == {4}
     elif plan in ("auto", "auto_direct"):
         assert 4 in kinds  # G < xd_shards: dense rounds with few mixed nodes go class-coded
+    elif plan == "replicated":  # the image gathered once, then whole after every round
+        assert kinds[0] == 5 and set(kinds[1:]) <= {6}
+    elif plan == "auto_replicated":
+        assert 5 in kinds and set(kinds) <= {1, 5, 6}
+    for e in engines:
+        e.close()
+
+
+@pytest.mark.parametrize("G", [2, 3])
+def test_lockstep_model_replicates_past_2p22(G):
+    """Past 2^22 nodes at G = 2-3 the link-aware model prices a replicated dense round (the one-GPU
+    round over the whole image, no collective once the image is whole) below the state all-gather
+    round, and plans it by itself: kinds 5 then 6; the rounds still equal one engine."""
+    N, R, k, seed = (1 << 23) + 5, 64, 2, 0x5EED0004
+    ref = Engine(N, R, "pushpull", k, seed, flags=1)
+    ref.inject_random()
+    want = ref.step(200)
+    full = ref.read_shard()
+    ref.close()
+    engines = [Engine(N, R, "pushpull", k, seed, flags=1, shard_rank=r, shard_count=G) for r in range(G)]
+    for e in engines:
+        e.inject_random()
+    got, kinds = run_lockstep(engines, 200)
+    assert got == want.stats
+    for e in engines:
+        assert np.array_equal(e.read_shard(), full[:, e.lo:e.hi])
+    assert 5 in kinds and 6 in kinds, kinds
+    for e in engines:
+        e.close()
+
+
+def test_lockstep_replicated_faults_stall():
+    """Replicated rounds draw, lose and stall edges as every other path."""
+    from gossip_hip.engine import loss_threshold
+    N, R, k, seed, G = 30011, 64, 2, 0x5EED0004, 3
+    kw = dict(edge_loss=loss_threshold(0.1), partitions=3, stall_rounds=3)
+    ref = Engine(N, R, "pushpull", k, seed, flags=1, **kw)
+    ref.inject_random()
+    want = ref.step(300)
+    full = ref.read_shard()
+    ref.close()
+    engines = [Engine(N, R, "pushpull", k, seed, flags=1, shard_rank=r, shard_count=G, params={"replicate": 1, "sparse_frac": -1}, **kw)
+               for r in range(G)]
+    for e in engines:
+        e.inject_random()
+    got, kinds = run_lockstep(engines, 300)
+    assert got == want.stats
+    for e in engines:
+        assert np.array_equal(e.read_shard(), full[:, e.lo:e.hi])
+    assert kinds[0] == 5 and set(kinds[1:]) <= {6}
     for e in engines:
         e.close()
 

@@ -58,9 +58,14 @@ PLANS = {
     "exchange-unfiltered": {"sparse_frac": -1, "xd_shards": 2, "xd_filter_frac": 1.0},
     "auto-exchange": {"xd_shards": 2},
     "classcoded": {"sparse_frac": -1, "xd_shards": 0, "cc_frac": 1},
+    # replicated dense rounds (kinds 5 / 6): every rank computes the whole image;
+    # the first dense round after the all-gather, the ones after it with no collective
+    "replicated": {"sparse_frac": -1, "replicate": 1},
+    "auto-replicated": {"replicate": 1},
 }
 # the kinds every round of a plan must have (random modes)
-PLAN_KINDS = {"sparse": {1}, "dense": {0}, "exchange": {3}, "exchange-unfiltered": {3}, "classcoded": {4}}
+PLAN_KINDS = {"sparse": {1}, "dense": {0}, "exchange": {3}, "exchange-unfiltered": {3}, "classcoded": {4},
+              "replicated": {5, 6}}
 
 
 def _worker(rank, world, port, case, q, params=None, direct=None):
@@ -119,13 +124,18 @@ def test_two_ranks_equal_one(case, plan, world=2, direct=None):
             assert set(kinds) == {0}  # FLOOD and W > 1: the plain state all-gather only
         elif plan in PLAN_KINDS:
             assert set(kinds) == PLAN_KINDS[plan]
+            if plan == "replicated":  # the image is gathered once, then stays whole
+                assert kinds[0] == 5 and set(kinds[1:]) == {6}
+        elif plan == "auto-replicated":  # every dense round replicated; after a sparse one, gathered again
+            assert {1, 5} <= set(kinds) <= {1, 5, 6}
+            assert all(k == 5 for i, k in enumerate(kinds) if k in (5, 6) and (i == 0 or kinds[i - 1] == 1))
         elif plan == "auto" and N >= 1000:
             assert 4 in kinds and 1 in kinds  # sparse rounds and class-coded dense rounds at G < xd_shards
         elif plan == "auto":  # a few nodes: the link-aware cost model may keep every round dense
             assert set(kinds) <= {0, 1, 4}
 
 
-@pytest.mark.parametrize("plan", ["auto", "sparse", "dense", "exchange", "classcoded"])
+@pytest.mark.parametrize("plan", ["auto", "sparse", "dense", "exchange", "classcoded", "replicated", "auto-replicated"])
 @pytest.mark.parametrize("world", [3])  # ragged shards; world 2 of the same protocol runs on the GPU box
 def test_direct_collective_path_equals_one(plan, world):
     """The driver's RCCL branch (collectives in place on the engines' own buffers: all-gathers
