@@ -776,6 +776,21 @@ ShardCosts shard_round_costs(const gossip_engine* e, const Est& x) {
   return c;
 }
 
+// What replicating saves over the dense rounds after this one (kind 6 instead of a sharded dense
+// round each), as far as the mean-field predictor sees them: up to 8 rounds, until one that the
+// model would run sparse.  Only steers the plan.
+double rep_gain_ahead(const gossip_engine* e, Est x) {
+  double gain = 0.0;
+  for (int i = 0; i < 8; ++i) {
+    x = predict(e, x);
+    const ShardCosts c = shard_round_costs(e, x);
+    const double rep6 = c.rep - c.rep_link;
+    if (c.sparse < std::min(c.dense, rep6)) break;  // the dense phase ends
+    gain += std::max(0.0, c.dense - rep6);
+  }
+  return gain;
+}
+
 // sparse when the smaller rare class is at most sparse_frac * N; maj = which
 // class is rare; all_d once the rare ends' pushes (~k per rare node) reach
 // alld_frac * N (launch_frontier_round)
@@ -2218,11 +2233,14 @@ int gossip_sharded_plan(gossip_engine_t* e, const uint64_t* total, int32_t* kind
   // (link_gbps 0: priced at the default rate, for gossip_plan_model only)
   const ShardCosts c = shard_round_costs(e, est_of(e, e->gtot.data()));
   const bool model = !e->sparse_frac_set && e->link_gbps > 0;
-  // replicated dense rounds: forced (param replicate 1), or by the model where one with a whole
-  // image already (device time only) costs less than the sharded dense round: entering costs the
-  // all-gather once (kind 5), every following dense round none (kind 6).  The model's per-node
-  // fits come from 2^24-2^27-node runs: below 2^22 nodes it replicates only when forced
-  const bool rep_auto = e->replicate < 0 && model && e->N >= (1ull << 22) && c.rep - c.rep_link < c.dense;
+  // replicated dense rounds: forced (param replicate 1), or by the model: with a whole image
+  // (kind 6) while one costs less than the sharded dense round; entering (kind 5: the all-gather
+  // plus the whole round) where what it costs over the sharded round is won back over the dense
+  // rounds the mean-field predictor (§3.4) sees ahead.  The model's per-node fits come from
+  // 2^24-2^27-node runs: below 2^22 nodes it replicates only when forced
+  const double rep6 = c.rep - c.rep_link;
+  bool rep_auto = e->replicate < 0 && model && e->N >= (1ull << 22) && rep6 < c.dense;
+  if (rep_auto && !e->rep_img_ok) rep_auto = c.rep - c.dense < rep_gain_ahead(e, est_of(e, e->gtot.data()));
   const bool rep_any = c.rep_ok && (e->replicate == 1 || rep_auto);
   if (model)  // the link-aware cost model decides instead
     e->sx_planned = c.sparse < (rep_any ? std::min(c.dense, c.rep) : c.dense);

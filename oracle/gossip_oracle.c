@@ -905,6 +905,76 @@ int oracle_local_totals(oracle_sim_t* s, uint64_t* partial) {
   return GOSSIP_OK;
 }
 
+/* The engine's per-rank cost model of one sharded round (engine.hip shard_round_costs), in ms, at
+ * nz nonzero and full_n full nodes: the sparse round, the dense round of the kind the plan would
+ * pick (exchange / class-coded / state all-gather), the replicated round's device time and the
+ * state all-gather that enters it. */
+static void plan_costs(const oracle_sim_t* s, double nz, double full_n, double* c_sparse, double* c_dense,
+                       double* c_rep, double* c_gather) {
+  const double N = (double)s->N, G = (double)s->G, Nl = (double)s->Nl, k = (double)s->k;
+  const double rare = nz < N - full_n ? nz : N - full_n, rare_own = rare / G;
+  const double bw = s->link_gbps * 1e6 * (G - 1.0 < 7.0 ? G - 1.0 : 7.0);
+  *c_sparse = Nl * (2.3e-9 + 7.0e-8 * (1.0 - exp(-rare / N / 0.05))) +
+              (16.0 * rare_own * (G - 1.0) + 16.0 * k * rare_own * (G - 1.0) / G) / bw;
+  const int dense_xd = s->xd_shards && s->G >= s->xd_shards;
+  const double mixed_n = nz - full_n > 0.0 ? nz - full_n : 0.0;
+  const int dense_cc = !dense_xd && s->cc_frac > 0 && mixed_n / N <= s->cc_frac;
+  if (dense_xd) { /* the items that survive the class filter (the engine's dense_filter) */
+    unsigned filt = 0;
+    if (s->k <= 8) {
+      const double empty = 1.0 - nz / N, full = full_n / N;
+      const int can_pull = s->mode != GOSSIP_MODE_PUSH, can_push = s->mode != GOSSIP_MODE_PULL;
+      filt = (can_pull && empty > s->xd_filter_frac ? 1u : 0u) | (can_push && full > s->xd_filter_frac ? 2u : 0u);
+    }
+    const double ef = 1.0 - nz / N, ff = full_n / N;
+    const double mf = 1.0 - ef - ff > 0.0 ? 1.0 - ef - ff : 0.0;
+    const double kept = mf + ef * ((filt & 1u) ? 1.0 - ef : 1.0) + ff * ((filt & 2u) ? 1.0 - ff : 1.0);
+    *c_dense = Nl * (4.85e-8 + 2.0e-8 * kept) + 40.0 * (G - 1.0) / G * Nl * kept / bw;
+  } else {
+    const double slice = dense_cc ? 20.0 / 64.0 * Nl + 8.0 * mixed_n / G : 8.0 * Nl;
+    *c_dense = 7.3e-9 * N + 4.7e-8 * Nl + slice * (G - 1.0) / bw;
+  }
+  *c_rep = 3.8e-8 * N + 1.5e-9 * Nl;
+  *c_gather = 8.0 * Nl * (G - 1.0) / bw;
+}
+
+/* The engine's mean-field predictor (engine.hip predict): one round of every rumor's holder count
+ * inf[r]; returns the predicted nonzero and full node counts. */
+static void predict_round(const oracle_sim_t* s, double* inf, double* nz, double* full) {
+  const double keep = (1.0 - (double)s->cfg.edge_loss / 4294967296.0) *
+                      (s->cfg.partitions > 1 ? 1.0 / s->cfg.partitions : 1.0);
+  const double N = (double)s->N, k = (double)s->k * keep;
+  const int push = s->mode == GOSSIP_MODE_PUSH || s->mode == GOSSIP_MODE_PUSHPULL;
+  const int pull = s->mode == GOSSIP_MODE_PULL || s->mode == GOSSIP_MODE_PUSHPULL;
+  double all_miss = 1.0, all_hit = 1.0;
+  for (uint32_t r = 0; r < s->R; ++r) {
+    const double u = 1.0 - inf[r] / N;
+    double v = u;
+    if (pull) v *= pow(u, k);
+    if (push) v *= exp(-k * (1.0 - u));
+    inf[r] = (1.0 - v) * N;
+    all_miss *= v;
+    all_hit *= 1.0 - v;
+  }
+  *nz = N * (1.0 - all_miss);
+  *full = N * all_hit;
+}
+
+/* The engine's rep_gain_ahead: what replicating saves over the dense rounds after this one, up to
+ * 8 predicted rounds, until one the model would run sparse. */
+static double rep_gain_ahead(const oracle_sim_t* s) {
+  double inf[64], nz = 0, full = 0, gain = 0.0;
+  for (uint32_t r = 0; r < s->R && r < 64; ++r) inf[r] = (double)s->gtot[4 + r];
+  for (int i = 0; i < 8; ++i) {
+    predict_round(s, inf, &nz, &full);
+    double c_sparse, c_dense, c_rep, c_gather;
+    plan_costs(s, nz, full, &c_sparse, &c_dense, &c_rep, &c_gather);
+    if (c_sparse < (c_dense < c_rep ? c_dense : c_rep)) break;
+    gain += c_dense - c_rep > 0.0 ? c_dense - c_rep : 0.0;
+  }
+  return gain;
+}
+
 int oracle_sharded_plan(oracle_sim_t* s, const uint64_t* total, int32_t* kind) {
   if (!s || !kind) return GOSSIP_EINVAL;
   s->planned = s->xd_planned = s->cc_planned = s->rep_planned = 0;
@@ -931,35 +1001,15 @@ int oracle_sharded_plan(oracle_sim_t* s, const uint64_t* total, int32_t* kind) {
   s->planned = (notfull < nz ? notfull : nz) <= frac * (double)s->N;
   /* the engine's replicated round (shard_round_costs' rep): the one-GPU round over all N nodes,
    * plus the state all-gather while the image is not whole */
-  double c_rep = 0.0, c_dense = 0.0;
   if (!s->sparse_frac_set && s->link_gbps > 0) { /* the engine's link-aware cost model (shard_round_costs) */
-    const double N = (double)s->N, G = (double)s->G, Nl = (double)s->Nl, k = (double)s->k;
     const double full_n = (double)s->gtot[0];
-    const double rare = nz < N - full_n ? nz : N - full_n, rare_own = rare / G;
-    const double bw = s->link_gbps * 1e6 * (G - 1.0 < 7.0 ? G - 1.0 : 7.0);
-    const double c_sparse = Nl * (2.3e-9 + 7.0e-8 * (1.0 - exp(-rare / N / 0.05))) +
-                            (16.0 * rare_own * (G - 1.0) + 16.0 * k * rare_own * (G - 1.0) / G) / bw;
-    const int dense_xd = s->xd_shards && s->G >= s->xd_shards;
-    const double mixed_n = nz - full_n > 0.0 ? nz - full_n : 0.0;
-    const int dense_cc = !dense_xd && s->cc_frac > 0 && mixed_n / N <= s->cc_frac;
-    if (dense_xd) { /* the items that survive the class filter (the engine's dense_filter below) */
-      unsigned filt = 0;
-      if (s->k <= 8) {
-        const double empty = 1.0 - nz / N, full = full_n / N;
-        const int can_pull = s->mode != GOSSIP_MODE_PUSH, can_push = s->mode != GOSSIP_MODE_PULL;
-        filt = (can_pull && empty > s->xd_filter_frac ? 1u : 0u) | (can_push && full > s->xd_filter_frac ? 2u : 0u);
-      }
-      const double ef = 1.0 - nz / N, ff = full_n / N;
-      const double mf = 1.0 - ef - ff > 0.0 ? 1.0 - ef - ff : 0.0;
-      const double kept = mf + ef * ((filt & 1u) ? 1.0 - ef : 1.0) + ff * ((filt & 2u) ? 1.0 - ff : 1.0);
-      c_dense = Nl * (4.85e-8 + 2.0e-8 * kept) + 40.0 * (G - 1.0) / G * Nl * kept / bw;
-    } else {
-      const double slice = dense_cc ? 20.0 / 64.0 * Nl + 8.0 * mixed_n / G : 8.0 * Nl;
-      c_dense = 7.3e-9 * N + 4.7e-8 * Nl + slice * (G - 1.0) / bw;
-    }
-    c_rep = 3.8e-8 * N + 1.5e-9 * Nl;
-    const double c_rep_all = c_rep + (s->rep_img_ok ? 0.0 : 8.0 * Nl * (G - 1.0) / bw);
-    const int rep_auto = s->replicate < 0 && s->N >= (1ull << 22) && c_rep < c_dense;
+    double c_sparse, c_dense, c_rep, c_gather;
+    plan_costs(s, nz, full_n, &c_sparse, &c_dense, &c_rep, &c_gather);
+    const double c_rep_all = c_rep + (s->rep_img_ok ? 0.0 : c_gather);
+    /* the engine's rep_auto: with a whole image while cheaper than the sharded dense round; entering
+     * where the extra cost is won back over the dense rounds the mean-field predictor sees ahead */
+    int rep_auto = s->replicate < 0 && s->N >= (1ull << 22) && c_rep < c_dense;
+    if (rep_auto && !s->rep_img_ok) rep_auto = c_rep_all - c_dense < rep_gain_ahead(s);
     s->planned = c_sparse < ((s->replicate == 1 || rep_auto) && c_rep_all < c_dense ? c_rep_all : c_dense);
     s->rep_planned = !s->planned && rep_auto;
   }
