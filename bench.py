@@ -226,7 +226,8 @@ def plan_model(eng, steps: int) -> dict:
             "model_device_ms": (ms - link) / max(steps, 1), "rounds_modelled": int(n // max(steps, 1)),
             "link_gbps": ENGINE_PARAMS.get("link_gbps", 76.0),
             "what": "per step and rank: S sparse, X exchange, C class-coded, D state all-gather dense rounds, "
-                    "R replicated after the state all-gather, r replicated on the whole image (no collective)"}
+                    "R / Q replicated after the state / class-coded all-gather, r replicated on the whole image "
+                    "(no collective)"}
 
 
 def sharded_roofline(eng, driver: str, trace, alg_round: int, world: int, backend: str, steps: int = 1) -> dict:

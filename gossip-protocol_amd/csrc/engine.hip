@@ -771,7 +771,9 @@ ShardCosts shard_round_costs(const gossip_engine* e, const Est& x) {
     c.dense = 7.3e-9 * N + 4.7e-8 * Nl + c.dense_link;
   }
   c.rep_ok = e->replicate != 0 && e->sx && bin_path_ok(e->N, e->k, 1, 1);
-  c.rep_link = e->rep_img_ok ? 0.0 : 8.0 * Nl * (G - 1.0) / bw;
+  // entering gathers the image class-coded where the dense round would (kind 7), else whole (5)
+  const double cc_slice = 20.0 / 64.0 * Nl + 8.0 * mixed / G;
+  c.rep_link = e->rep_img_ok ? 0.0 : (c.dense_cc ? cc_slice : 8.0 * Nl) * (G - 1.0) / bw;
   c.rep = 3.8e-8 * N + 1.5e-9 * Nl + c.rep_link;
   return c;
 }
@@ -2262,12 +2264,15 @@ int gossip_sharded_plan(gossip_engine_t* e, const uint64_t* total, int32_t* kind
   e->xd_cls_ok = false;
   // dense on the state image: class-coded when few nodes are mixed (neither empty nor full)
   const double mixed = ((double)e->gtot[4 + e->R] - (double)e->gtot[0]) / (double)e->N;
-  e->cc_planned = !e->sx_planned && !e->xd_planned && !e->rep_planned && e->cc_frac > 0 && mixed <= e->cc_frac;
-  *kind = e->sx_planned ? 1 : e->rep_planned ? (e->rep_img_ok ? 6 : 5) : e->xd_planned ? 3 : e->cc_planned ? 4 : 0;
+  // entering replication over the class-coded all-gather (kind 7): the image expanded whole, then
+  // the replicated round
+  const bool rep_cc = e->rep_planned && !e->rep_img_ok && c.dense_cc;
+  e->cc_planned = (!e->sx_planned && !e->xd_planned && !e->rep_planned && e->cc_frac > 0 && mixed <= e->cc_frac) || rep_cc;
+  *kind = e->sx_planned ? 1 : e->rep_planned ? (e->rep_img_ok ? 6 : rep_cc ? 7 : 5) : e->xd_planned ? 3 : e->cc_planned ? 4 : 0;
   // the model's price of the round as planned (gossip_plan_model): the plan of the current run
   // (restarted at round 0) and the modelled ms since gossip_reset_timing
   if (e->t == 0) e->model_plan.clear();
-  e->model_plan.push_back("DSAXCRr"[*kind]);
+  e->model_plan.push_back("DSAXCRrQ"[*kind]);
   e->model_ms += e->sx_planned ? c.sparse : e->rep_planned ? c.rep : c.dense;
   e->model_link_ms += e->sx_planned ? c.sparse_link : e->rep_planned ? c.rep_link : c.dense_link;
   e->model_rounds += 1;

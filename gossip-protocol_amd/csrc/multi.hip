@@ -745,7 +745,8 @@ struct Driver {
         rc = antientropy(&part);
         break;
       case 3: rc = exchange(&pd); break;
-      case 4: rc = dense(&pd, true); break;
+      case 4:
+      case 7: rc = dense(&pd, true); break;  // (7: class-coded all-gather, then the replicated round)
       case 6:  // replicated, the image whole already: no collective before it
         for (size_t i = 0; i < n(); ++i) ENG(i, gossip_round_compute_dev(L[i], &pd[i]));
         rc = GOSSIP_OK;

@@ -24,8 +24,9 @@ without a GPU):
   replicated    (kinds 5 / 6, DESIGN.md §5.7: dense rounds where the links cost more than the
                 extra device time, e.g. G = 2 at 2^27 nodes) every rank runs the whole round over
                 the whole image in place: kind 5 after the state all-gather (as a dense round),
-                kind 6 with no collective before it (the previous round left every node's
-                S_{t+1} in the image); then the all-reduce of the own-slice partials;
+                kind 7 after the class-coded all-gather, kind 6 with no collective before it
+                (the previous round left every node's S_{t+1} in the image); then the
+                all-reduce of the own-slice partials;
   ANTIENTROPY   ("Design B") all-gather of the alive and stale bits,
                 all-to-all of request items {p, n, V_t[n]} to p's owner and of its
                 replies V_t[p], all-reduce of the partials; the global max vector
@@ -374,7 +375,7 @@ def sharded_round(engine, group=None, kinds: list | None = None, direct: bool | 
             partial = _ae_round(engine, comm)
         elif kind == 3:
             partial = _xd_round(engine, comm)
-        elif kind == 4:
+        elif kind in (4, 7):  # 7: the class-coded all-gather, then the replicated round
             partial = _cc_round(engine, comm)
         elif kind == 1:
             partial = _sparse_round(engine, comm)
@@ -634,7 +635,8 @@ def lockstep_run(engines, max_rounds: int, items: list | None = None):
     """One process driving G shard engines (one per GPU, or several on one) through the
     same rounds as sharded_run, with device copies in place of the collectives.
     Returns (per-round stats, per-round kind: 0 dense / 1 sparse / 2 ANTIENTROPY / 3 exchange dense /
-    4 class-coded dense / 5, 6 replicated dense after / without the all-gather).  items (exchange rounds; host engines too): per round, each shard's
+    4 class-coded dense / 5, 7, 6 replicated dense after the all-gather, after the class-coded one, or
+    without any).  items (exchange rounds; host engines too): per round, each shard's
     item counts per owner."""
     stats, kinds = [], []
     for _ in range(max_rounds):
@@ -652,7 +654,7 @@ def lockstep_run(engines, max_rounds: int, items: list | None = None):
         if ks[0] == 3:
             parts = _lockstep_xd(engines, items)
         else:
-            parts = {1: _lockstep_sparse, 2: _lockstep_ae, 4: _lockstep_cc,
+            parts = {1: _lockstep_sparse, 2: _lockstep_ae, 4: _lockstep_cc, 7: _lockstep_cc,
                      6: lambda es: [e.round_compute() for e in es]}.get(ks[0], _lockstep_dense)(engines)
         tot = _lockstep_sum(parts)
         st = [e.round_commit(tot) for e in engines]

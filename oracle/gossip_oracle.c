@@ -935,7 +935,8 @@ static void plan_costs(const oracle_sim_t* s, double nz, double full_n, double* 
     *c_dense = 7.3e-9 * N + 4.7e-8 * Nl + slice * (G - 1.0) / bw;
   }
   *c_rep = 3.8e-8 * N + 1.5e-9 * Nl;
-  *c_gather = 8.0 * Nl * (G - 1.0) / bw;
+  /* entering replication gathers the image class-coded where the dense round would (kind 7) */
+  *c_gather = (dense_cc ? 20.0 / 64.0 * Nl + 8.0 * mixed_n / G : 8.0 * Nl) * (G - 1.0) / bw;
 }
 
 /* The engine's mean-field predictor (engine.hip predict): one round of every rumor's holder count
@@ -1027,8 +1028,11 @@ int oracle_sharded_plan(oracle_sim_t* s, const uint64_t* total, int32_t* kind) {
   }
   /* the engine's class-coded all-gather: at most cc_frac mixed (nonzero, not full) nodes */
   const double mixed = ((double)s->gtot[4 + s->R] - (double)s->gtot[0]) / (double)s->N;
-  s->cc_planned = !s->planned && !s->xd_planned && !s->rep_planned && s->cc_frac > 0 && mixed <= s->cc_frac;
-  *kind = s->planned ? 1 : s->rep_planned ? (s->rep_img_ok ? 6 : 5) : s->xd_planned ? 3 : s->cc_planned ? 4 : 0;
+  /* the engine's kind 7: entering replication over the class-coded all-gather */
+  const int rep_cc = s->rep_planned && !s->rep_img_ok && !(s->xd_shards && s->G >= s->xd_shards) &&
+                     s->cc_frac > 0 && mixed <= s->cc_frac;
+  s->cc_planned = (!s->planned && !s->xd_planned && !s->rep_planned && s->cc_frac > 0 && mixed <= s->cc_frac) || rep_cc;
+  *kind = s->planned ? 1 : s->rep_planned ? (s->rep_img_ok ? 6 : rep_cc ? 7 : 5) : s->xd_planned ? 3 : s->cc_planned ? 4 : 0;
   return GOSSIP_OK;
 }
 

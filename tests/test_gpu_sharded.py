@@ -64,10 +64,10 @@ def test_lockstep_shards_equal_one_engine(case, plan):
         assert set(kinds) == {4}
     elif plan in ("auto", "auto_direct"):
         assert 4 in kinds  # G < xd_shards: dense rounds with few mixed nodes go class-coded
-    elif plan == "replicated":  # the image gathered once, then whole after every round
-        assert kinds[0] == 5 and set(kinds[1:]) <= {6}
+    elif plan == "replicated":  # the image gathered once (whole or class-coded), then whole after every round
+        assert kinds[0] in (5, 7) and set(kinds[1:]) <= {6}
     elif plan == "auto_replicated":
-        assert 5 in kinds and set(kinds) <= {1, 5, 6}
+        assert set(kinds) & {5, 7} and set(kinds) <= {1, 5, 6, 7}
     for e in engines:
         e.close()
 
@@ -76,7 +76,8 @@ def test_lockstep_shards_equal_one_engine(case, plan):
 def test_lockstep_model_replicates_past_2p22(G):
     """Past 2^22 nodes at G = 2-3 the link-aware model prices a replicated dense round (the one-GPU
     round over the whole image, no collective once the image is whole) below the state all-gather
-    round, and plans it by itself: kinds 5 then 6; the rounds still equal one engine."""
+    round, and plans it by itself: kind 5 or 7 (entered over the whole or the class-coded
+    all-gather), then 6; the rounds still equal one engine."""
     N, R, k, seed = (1 << 23) + 5, 64, 2, 0x5EED0004
     ref = Engine(N, R, "pushpull", k, seed, flags=1)
     ref.inject_random()
@@ -90,7 +91,7 @@ def test_lockstep_model_replicates_past_2p22(G):
     assert got == want.stats
     for e in engines:
         assert np.array_equal(e.read_shard(), full[:, e.lo:e.hi])
-    assert 5 in kinds and 6 in kinds, kinds
+    assert set(kinds) & {5, 7} and 6 in kinds, kinds
     for e in engines:
         e.close()
 
@@ -113,7 +114,7 @@ def test_lockstep_replicated_faults_stall():
     assert got == want.stats
     for e in engines:
         assert np.array_equal(e.read_shard(), full[:, e.lo:e.hi])
-    assert kinds[0] == 5 and set(kinds[1:]) <= {6}
+    assert kinds[0] in (5, 7) and set(kinds[1:]) <= {6}
     for e in engines:
         e.close()
 

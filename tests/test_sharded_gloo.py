@@ -64,8 +64,7 @@ PLANS = {
     "auto-replicated": {"replicate": 1},
 }
 # the kinds every round of a plan must have (random modes)
-PLAN_KINDS = {"sparse": {1}, "dense": {0}, "exchange": {3}, "exchange-unfiltered": {3}, "classcoded": {4},
-              "replicated": {5, 6}}
+PLAN_KINDS = {"sparse": {1}, "dense": {0}, "exchange": {3}, "exchange-unfiltered": {3}, "classcoded": {4}}
 
 
 def _worker(rank, world, port, case, q, params=None, direct=None):
@@ -124,11 +123,11 @@ def test_two_ranks_equal_one(case, plan, world=2, direct=None):
             assert set(kinds) == {0}  # FLOOD and W > 1: the plain state all-gather only
         elif plan in PLAN_KINDS:
             assert set(kinds) == PLAN_KINDS[plan]
-            if plan == "replicated":  # the image is gathered once, then stays whole
-                assert kinds[0] == 5 and set(kinds[1:]) == {6}
+        elif plan == "replicated":  # the image gathered once (whole or class-coded), then stays whole
+            assert kinds[0] in (5, 7) and set(kinds[1:]) == {6}
         elif plan == "auto-replicated":  # every dense round replicated; after a sparse one, gathered again
-            assert {1, 5} <= set(kinds) <= {1, 5, 6}
-            assert all(k == 5 for i, k in enumerate(kinds) if k in (5, 6) and (i == 0 or kinds[i - 1] == 1))
+            assert 1 in kinds and set(kinds) & {5, 7} and set(kinds) <= {1, 5, 6, 7}
+            assert all(k in (5, 7) for i, k in enumerate(kinds) if k in (5, 6, 7) and (i == 0 or kinds[i - 1] == 1))
         elif plan == "auto" and N >= 1000:
             assert 4 in kinds and 1 in kinds  # sparse rounds and class-coded dense rounds at G < xd_shards
         elif plan == "auto":  # a few nodes: the link-aware cost model may keep every round dense

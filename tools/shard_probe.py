@@ -108,4 +108,4 @@ for rep in range(2):
         print(f"G={G} plan link_gbps={PARAMS.get('link_gbps', 76.0)}: modelled per-rank wall "
               f"{sum(r[2] for r in rounds) + link_ms:.2f} ms = device {sum(r[2] for r in rounds):.2f} + "
               f"link {link_ms:.2f} (at {bw:g} GB/s per link); kinds "
-              f"{''.join('DSAXCRr'[r[1]] for r in rounds)}", flush=True)
+              f"{''.join('DSAXCRrQ'[r[1]] for r in rounds)}", flush=True)
