@@ -48,6 +48,9 @@ int gossip_round_commit(gossip_engine_t* eng, const uint64_t* total, gossip_roun
  *   kind  0: dense round -> the exchange_buffers / round_compute sequence;
  *   kind  3: exchange dense round (no state image; see the gossip_xd_* calls below);
  *   kind  4: dense round on a class-coded state all-gather (gossip_cc_* below);
+ *   kind  5 / 7: replicated dense round (param "replicate"): the steps of kind 0 /
+ *            kind 4, then gossip_round_compute runs the whole image's round on every rank;
+ *   kind  6: replicated dense round with the image already whole: gossip_round_compute only;
  *   kind  1: sparse round:
  *     gossip_sparse_rare(&send, &count)        own rare nodes, 16-B items {node, value}
  *     all-gather of count, stride = max count
