@@ -570,6 +570,31 @@ int place_slab(gossip_engine* e, void** mem, size_t bytes, Trial trial, bool* mo
   return rc;
 }
 
+// One placement candidate's trial (place_bins, rep_compute): one emit over the image `img` (read
+// only) fills the candidate's records, then serve alone is timed, its tile queues cleared before
+// each launch.  The slab's mode is serve's (the trial round follows bin_serve at r = 0.93-0.99
+// across candidates); whole trial rounds chose equally fast slabs at twice the
+// cost (first step at 2^27 230 vs 127 ms, profiles/r06_vmm/place_serve).
+int serve_trial(gossip_engine* e, const BinGeom& g, bool dyn, void* slab, uint64_t* img, uint64_t* part, float* ms) {
+  BinBufs b{};
+  bin_carve(g, slab, &b);
+  b.nzb = b.fullb = nullptr;
+  if (!dyn) b.dyn = nullptr;
+  if (b.dyn) HIP_OK(e, hipMemsetAsync(b.dyn, 0, 17 * 4, e->stream));
+  const RoundSync rs{nullptr, (uint32_t)part_len(e), 0u};
+  auto part_round = [&](uint32_t parts) {
+    return launch_binned_round(g, b, img, part, e->R, 0u, e->key0, e->key1, e->mode, 0u, Faults{}, 0u, rs,
+                               e->stream, parts);
+  };
+  HIP_OK(e, part_round(1u));
+  return timed_trial(e, [&] {
+    if (b.dyn) {
+      if (hipError_t x = hipMemsetAsync(b.dyn, 0, 16 * 4, e->stream)) return x;
+    }
+    return part_round(2u);
+  }, ms);
+}
+
 // Before the first round of a binned engine with a record slab of 512 MiB or more: its placement
 // (place_slab), each trial a dense round on a zero state (the second image, unused by the in-place
 // binned rounds) with scratch totals and no bitmaps.
@@ -591,29 +616,9 @@ int place_bins(gossip_engine* e) {
   if (!e->binned || e->place_tries <= 1 || bytes < (512ull << 20) || !e->img[1]) return GOSSIP_OK;
   uint64_t* part = nullptr;
   HIP_OK(e, hipMalloc((void**)&part, (part_len(e) + 8) * 8));
-  const RoundSync rs{nullptr, (uint32_t)part_len(e), 0u};
   bool moved = false;
   const int rc = place_slab(e, &e->bin_mem, bytes, [&](void* slab, float* ms) {
-    BinBufs b{};
-    bin_carve(e->bg, slab, &b);
-    b.nzb = b.fullb = nullptr;
-    if (!e->bb.dyn) b.dyn = nullptr;
-    if (b.dyn) HIP_OK(e, hipMemsetAsync(b.dyn, 0, 17 * 4, e->stream));
-    auto part_round = [&](uint32_t parts) {
-      return launch_binned_round(e->bg, b, e->img[1], part, e->R, 0u, e->key0, e->key1, e->mode, 0u, Faults{}, 0u,
-                                 rs, e->stream, parts);
-    };
-    // The slab's mode is serve's (the trial round follows bin_serve at r = 0.93-0.99 across
-    // candidates): one emit fills the candidate's records, then serve alone is
-    // timed (its tile queues cleared before each launch).  Whole trial rounds chose equally fast
-    // slabs at twice the cost (first step at 2^27 230 vs 127 ms, profiles/r06_vmm/place_serve)
-    HIP_OK(e, part_round(1u));
-    return timed_trial(e, [&] {
-      if (b.dyn) {
-        if (hipError_t x = hipMemsetAsync(b.dyn, 0, 16 * 4, e->stream)) return x;
-      }
-      return part_round(2u);
-    }, ms);
+    return serve_trial(e, e->bg, e->bb.dyn != nullptr, slab, e->img[1], part, ms);
   }, &moved, "place_bins");
   (void)hipFree(part);
   if (moved) {
@@ -1308,19 +1313,28 @@ int step_ae(gossip_engine* e, uint32_t max_rounds, gossip_round_stats_t* stats, 
 // own slice (and rebuilds its own bitmaps) like any other sharded round, so the driver's
 // all-reduce stays as it is.  Bits as the sharded kinds: the same draws and edges (§2).
 int rep_compute(gossip_engine* e) {
-  if (!e->rep_mem) {  // (no placement trials: the slab serves a handful of rounds per run)
+  if (!e->rep_part) HIP_OK(e, hipMalloc((void**)&e->rep_part, (part_len(e) + 8) * 8));
+  if (!e->rep_mem) {
     e->rbg = make_bin_geom(e->N, e->k, (e->N + kTileD - 1) / kTileD > kBigFromTiles);
     const size_t bytes = bin_bytes(e->rbg);
     if (hipMalloc(&e->rep_mem, bytes) != hipSuccess) {
       e->rep_mem = nullptr;
       return e->fail(GOSSIP_ENOMEM, "hipMalloc of %zu bytes (replicated-round records) failed", bytes);
     }
+    const bool dyn = e->rbg.nt_d >= 4096;  // (the tile queues pay past 4096 tiles, as on one GPU)
+    // placed as the one-GPU slab (place_bins): the trials read the image, write only records
+    if (e->place_tries > 1 && bytes >= (512ull << 20)) {
+      bool moved = false;
+      if (int rc = place_slab(e, &e->rep_mem, bytes, [&](void* slab, float* ms) {
+            return serve_trial(e, e->rbg, dyn, slab, current_image(e), e->rep_part, ms);
+          }, &moved, "place_rep"))
+        return rc;
+    }
     bin_carve(e->rbg, e->rep_mem, &e->rbb);
     e->rbb.nzb = e->rbb.fullb = nullptr;  // (no edge filter: it needs bitmaps of the whole image)
     HIP_OK(e, hipMemset(e->rbb.dyn, 0, 17 * 4));
-    if (e->rbg.nt_d < 4096) e->rbb.dyn = nullptr;  // (the tile queues pay past 4096 tiles, as on one GPU)
+    if (!dyn) e->rbb.dyn = nullptr;
   }
-  if (!e->rep_part) HIP_OK(e, hipMalloc((void**)&e->rep_part, (part_len(e) + 8) * 8));
   int rc;
   if ((rc = timer_begin(e, 0))) return rc;
   const RoundSync rs{nullptr, (uint32_t)part_len(e), 0u};

@@ -79,8 +79,10 @@ for rep in range(2):
             parts = sh._lockstep_sparse(tes)
         elif ks[0] == 3:
             parts = sh._lockstep_xd(tes)
-        elif ks[0] == 4:
+        elif ks[0] in (4, 7):  # (7: class-coded all-gather, then the replicated round)
             parts = sh._lockstep_cc(tes)
+        elif ks[0] == 6:  # replicated on the whole image: no exchange
+            parts = [te.round_compute() for te in tes]
         else:
             parts = sh._lockstep_dense(tes)
         tot = sh._lockstep_sum(parts)
@@ -96,7 +98,7 @@ for rep in range(2):
     if rep == 1:
         for t, k, ms, full, calls, gb in rounds:
             br = " ".join(f"{n}={v:.3f}" for n, v in calls.items())
-            kind = ['dense ', 'sparse', 'ae', 'xdense', 'ccoded'][k]
+            kind = ['dense ', 'sparse', 'ae', 'xdense', 'ccoded', 'rep-ag', 'rep   ', 'rep-cc'][k]
             print(f"G={G} round {t:2d} {kind} per-rank {ms:7.3f} ms  full={full}  gathered={gb / 2**20:.1f} MiB  [{br}]",
                   flush=True)
         print(f"G={G} rounds={len(rounds)} sum per-rank {sum(r[2] for r in rounds):.2f} ms  "
