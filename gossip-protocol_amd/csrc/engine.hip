@@ -2067,8 +2067,10 @@ int gossip_exchange_buffers(gossip_engine_t* e, void** send, void** recv, uint64
   if (e->mode == GOSSIP_MODE_FLOOD && !e->has_topo) return e->fail(GOSSIP_ESTATE, "FLOOD needs a topology");
   if (int rc = set_dev(e)) return rc;
   // the state all-gather rounds' slab is placed before the first collective starts: trials
-  // timed while the all-gather runs would read a half-written image under link traffic
-  if (int rc = place_sb(e)) return rc;
+  // timed while the all-gather runs would read a half-written image under link traffic (a
+  // replicated round does not use it)
+  if (!e->rep_planned)
+    if (int rc = place_sb(e)) return rc;
   uint64_t *s = nullptr, *img = nullptr;
   if (int rc = prepare_send(e, &s, &img)) return rc;
   // the caller's collective runs on another stream: publish the slice first
@@ -2434,7 +2436,8 @@ int cc_check(gossip_engine* e) {
 int gossip_cc_send(gossip_engine_t* e, void** bits, uint64_t* bits_bytes, void** vals, uint64_t* count) {
   if (!bits || !bits_bytes || !vals || !count) return GOSSIP_EINVAL;
   if (int rc = cc_check(e)) return rc;
-  if (int rc = place_sb(e)) return rc;  // (as in gossip_exchange_buffers: before the collectives)
+  if (!e->rep_planned)  // (as in gossip_exchange_buffers: before the collectives)
+    if (int rc = place_sb(e)) return rc;
   const uint64_t nwl = (e->Nl + 63) / 64, slot = cc_slot_words(e->Nl);
   if (!e->cc_bits) {
     HIP_OK(e, hipMalloc((void**)&e->cc_bits, (size_t)e->G * slot * 8));
