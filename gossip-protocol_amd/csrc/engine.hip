@@ -516,6 +516,13 @@ int timed_trial(gossip_engine* e, Run run, float* ms) {
 template <class Trial>
 int place_slab(gossip_engine* e, void** mem, size_t bytes, Trial trial, bool* moved, const char* what) {
   *moved = false;
+  // A wall-time budget: on some boxes and processes a fresh multi-GiB hipMalloc / hipFree takes
+  // 0.1 s to seconds instead of milliseconds (a 3.3 s first step at 2^27 where 130 ms is usual,
+  // with the trials' device time unchanged at 66 ms): past it no further candidate
+  // is tried and the best so far is kept.  (400 ms cut such a box's lottery to 2-5 candidates and
+  // left 2 of 4 engines in the 5.5-ms mode, profiles/r06_vmm/budget400)
+  constexpr double kPlaceBudgetMs = 2000.0;
+  const auto t_start = std::chrono::steady_clock::now();
   void* best = *mem;
   void* held = nullptr;
   float best_ms = 0.f;
@@ -529,6 +536,8 @@ int place_slab(gossip_engine* e, void** mem, size_t bytes, Trial trial, bool* mo
   std::fprintf(stderr, "%s: candidate 0 slab %p trial %.1f us\n", what, best, best_ms * 1e3);
 #endif
   for (uint32_t i = 1; i < e->place_tries && rc == GOSSIP_OK; ++i) {
+    if (std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count() > kPlaceBudgetMs)
+      break;
     void* p = nullptr;
 #ifdef GOSSIP_EXP_PLACE_LOG
     const auto t0 = std::chrono::steady_clock::now();
