@@ -1336,8 +1336,12 @@ int rep_compute(gossip_engine* e) {
       bool moved = false;
       if (int rc = place_slab(e, &e->rep_mem, bytes, [&](void* slab, float* ms) {
             return serve_trial(e, e->rbg, dyn, slab, current_image(e), e->rep_part, ms);
-          }, &moved, "place_rep"))
+          }, &moved, "place_rep")) {
+        (void)hipStreamSynchronize(e->stream);
+        (void)hipFree(e->rep_mem);  // (never carved: the next replicated round allocates again)
+        e->rep_mem = nullptr;
         return rc;
+      }
     }
     bin_carve(e->rbg, e->rep_mem, &e->rbb);
     e->rbb.nzb = e->rbb.fullb = nullptr;  // (no edge filter: it needs bitmaps of the whole image)
